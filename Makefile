@@ -1,0 +1,100 @@
+# Build for the MI355X-native framework (gfx950 / CDNA4).
+#
+# Parity with the reference makefile (/root/reference/makefile:1-15): the same targets `build`,
+# `clean`, `run`, `runOn2` and the same product `./final` (stdin -> stdout). The toolchain is
+# hipcc (device code, --offload-arch=gfx950) + g++ -fopenmp (host code, libgomp like PyTorch) +
+# MPICH (/opt/conda) + RCCL, instead of mpicxx + nvcc + libcudart_static.
+#
+#   make build        libmoc.so (Python package) + ./final (MPI CLI)
+#   make run          mpiexec -np 2 ./final < $(INPUT)
+#   make runOn2       mpiexec -np 2 -machinefile mf --map-by node ./final < $(INPUT)
+#   make test         CPU test-suite (pytest -m "not gpu")
+#   make asan         host-only ASan/UBSan build of ./final_asan (GPU code built without sanitizers)
+
+ROCM      ?= /opt/rocm
+MPI_HOME  ?= /opt/conda
+ARCH      ?= gfx950
+HIPCC     ?= $(ROCM)/bin/hipcc
+CXX       := g++
+NP        ?= 2
+INPUT     ?= tests/data/input1.txt
+JOBS      ?= 8
+
+BUILD     := build
+OBJ       := $(BUILD)/obj
+PKG_LIB   := mpi_openmp_cuda_amd/lib/libmoc.so
+MPILIB    := $(BUILD)/mpilib
+
+INC       := -Icsrc/include
+CXXFLAGS  := -O3 -std=c++17 -fPIC -fopenmp -Wall -Wextra -Wno-unused-parameter $(INC) -I$(ROCM)/include -D__HIP_PLATFORM_AMD__
+HIPFLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) $(INC) -Wno-unused-result
+MPIFLAGS  := -I$(MPI_HOME)/include
+LDROCM    := -L$(ROCM)/lib -lamdhip64 -Wl,-rpath,$(ROCM)/lib
+
+CORE_SRCS := $(wildcard csrc/src/*.cpp) $(wildcard csrc/src/runtime/*.cpp)
+HIP_SRCS  := $(wildcard csrc/src/hip/*.hip)
+COMM_SRCS := $(wildcard csrc/src/comm/*.cpp)
+CORE_OBJS := $(patsubst csrc/src/%.cpp,$(OBJ)/%.o,$(CORE_SRCS))
+HIP_OBJS  := $(patsubst csrc/src/%.hip,$(OBJ)/%.o,$(HIP_SRCS))
+COMM_OBJS := $(patsubst csrc/src/%.cpp,$(OBJ)/%.o,$(COMM_SRCS))
+HEADERS   := $(shell find csrc/include -name '*.h' -o -name '*.hpp')
+
+.PHONY: all build lib clean run runOn2 test asan
+
+all: build
+build: lib final
+
+lib: $(PKG_LIB)
+
+$(OBJ)/%.o: csrc/src/%.cpp $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) $(if $(findstring /comm/,$@),$(MPIFLAGS)) -c $< -o $@
+
+$(OBJ)/%.o: csrc/src/%.hip $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(PKG_LIB): $(CORE_OBJS) $(HIP_OBJS)
+	@mkdir -p $(dir $@)
+	$(CXX) -shared -fopenmp -o $@ $^ $(LDROCM)
+
+# MPICH's conda wrapper names a compiler that is not installed, so link libmpi directly through a
+# private directory (keeps /opt/conda/lib — and its older libstdc++ — off the binary's search path).
+$(MPILIB)/libmpi.so:
+	@mkdir -p $(MPILIB)
+	ln -sf $(MPI_HOME)/lib/libmpi.so.12 $(MPILIB)/libmpi.so.12
+	ln -sf $(MPI_HOME)/lib/libmpi.so.12 $(MPILIB)/libmpi.so
+	ln -sf $(MPI_HOME)/lib/libgfortran.so.4 $(MPILIB)/libgfortran.so.4
+	ln -sf $(MPI_HOME)/lib/libquadmath.so.0 $(MPILIB)/libquadmath.so.0
+
+$(OBJ)/apps/final.o: csrc/apps/final.cpp $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) $(MPIFLAGS) -c $< -o $@
+
+final: $(OBJ)/apps/final.o $(COMM_OBJS) $(CORE_OBJS) $(HIP_OBJS) $(MPILIB)/libmpi.so
+	$(CXX) -fopenmp -o $@ $(OBJ)/apps/final.o $(COMM_OBJS) $(CORE_OBJS) $(HIP_OBJS) \
+	    -L$(MPILIB) -lmpi -Wl,-rpath-link,$(MPI_HOME)/lib -Wl,-rpath,'$$ORIGIN/$(MPILIB)' $(LDROCM) -lrccl
+
+# Host-side sanitizers only (GPU ASan is not available on the target pool).
+asan: $(MPILIB)/libmpi.so
+	@mkdir -p $(BUILD)/asan
+	for f in $(CORE_SRCS) $(COMM_SRCS) csrc/apps/final.cpp; do \
+	  $(CXX) -O1 -g -std=c++17 -fopenmp -fsanitize=address,undefined -fno-omit-frame-pointer $(INC) \
+	    -I$(ROCM)/include -D__HIP_PLATFORM_AMD__ $(MPIFLAGS) -c $$f -o $(BUILD)/asan/$$(echo $$f | tr / _).o || exit 1; \
+	done
+	$(HIPCC) -O1 -g -std=c++17 --offload-arch=$(ARCH) $(INC) -Xarch_host -fsanitize=address \
+	    -c $(HIP_SRCS) -o $(BUILD)/asan/kernels.o
+	$(CXX) -fopenmp -fsanitize=address,undefined -o final_asan $(BUILD)/asan/*.o \
+	    -L$(MPILIB) -lmpi -Wl,-rpath-link,$(MPI_HOME)/lib -Wl,-rpath,'$$ORIGIN/$(MPILIB)' $(LDROCM) -lrccl
+
+clean:
+	rm -rf $(BUILD) final final_asan $(PKG_LIB)
+
+run: build
+	$(MPI_HOME)/bin/mpiexec -np $(NP) ./final < $(INPUT)
+
+runOn2: build
+	$(MPI_HOME)/bin/mpiexec -np 2 -machinefile mf --map-by node ./final < $(INPUT)
+
+test:
+	python -m pytest tests/ -x -q -m "not gpu"

@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""Headline benchmark: elements/s of the full distributed search on input6-shaped data.
+
+Metric (BASELINE.json): "wall-clock (s) + elements/sec on input6.txt array at 1/2/4/8 MI355X", on
+synthetic arrays of the input6.txt shape (W = 4 3 2 10, |Seq1| = 26, |Seq2| in 6..11; no datasets are
+available offline, so records are drawn at random; data="synthetic").
+
+One timed step = one complete job over the global batch, exactly the work `./final` does between parsing
+and printing (reference flow main.c:149-197):
+  1. root broadcasts the problem header (weights + Seq1) over the process group (RCCL on GPUs),
+  2. every rank uploads it to its engine (LUT + Seq1 -> device),
+  3. every rank moves its contiguous slice of the records from node-shared host memory to its GPU
+     (pinned DMA over its own PCIe link), runs the gfx950 search kernels, and DMAs the (score, n, k)
+     results back into the node-shared result array the root prints from,
+  4. an all-reduce of the per-rank record counts closes the job (the reference's MPI_Gather point).
+Weak scaling: --records-per-gpu is fixed per rank, the global batch grows with N.
+
+Run: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under torch.distributed.run.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "wall-clock (s) + elements/sec on input6.txt array at 1/2/4/8 MI355X"
+
+
+def parse_args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--records-per-gpu", type=int, default=1 << 25)
+    ap.add_argument("--shape", default="input6")
+    ap.add_argument("--shm", type=int, default=1, help="1: node-shared /dev/shm arrays; 0: private pinned")
+    ap.add_argument("--verify", type=int, default=20000, help="records per rank checked against the CPU engine")
+    ap.add_argument("--seed", type=int, default=1234)
+    return ap.parse_args()
+
+
+class HostArrays:
+    """Per-rank slice of the node-shared input/result arrays (/dev/shm files, or private memory)."""
+
+    def __init__(self, tag, rank, lengths, use_shm):
+        n = lengths.shape[0]
+        total = int(lengths.sum())
+        self.paths = []
+        self.shm = False
+        nbytes = 8 * (n + 1) + 12 * n + total
+        if use_shm and os.path.isdir("/dev/shm"):
+            st = os.statvfs("/dev/shm")
+            # leave room for every local rank's slice (up to 8) plus headroom
+            if st.f_bavail * st.f_frsize > 10 * nbytes:
+                self.shm = True
+        if self.shm:
+            def mk(name, dtype, count):
+                p = f"/dev/shm/moc_bench_{tag}_{rank}_{name}"
+                self.paths.append(p)
+                return np.memmap(p, dtype=dtype, mode="w+", shape=(max(count, 1),))[:count]
+        else:
+            def mk(name, dtype, count):
+                return np.empty(count, dtype=dtype)
+        self.offsets = mk("offsets", np.int64, n + 1)
+        self.offsets[0] = 0
+        np.cumsum(lengths, out=self.offsets[1:])
+        self.codes = mk("codes", np.uint8, total)
+        self.results = mk("results", np.int32, 3 * n)
+
+    def cleanup(self):
+        for p in self.paths:
+            try:
+                os.unlink(p)
+            except OSError:
+                pass
+
+
+def main():
+    args = parse_args()
+    import torch
+    import torch.distributed as dist
+
+    from mpi_openmp_cuda_amd import HipSearchEngine, Problem, search_cpu
+    from mpi_openmp_cuda_amd._lib import Pinned
+    from mpi_openmp_cuda_amd.ops.align import as_triples
+    from mpi_openmp_cuda_amd.utils.synthetic import SHAPES, fill_codes
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    distributed = world > 1
+    if distributed:
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if distributed:
+            dist.barrier(device_ids=[local_rank])
+        torch.cuda.synchronize(dev)
+
+    shape = SHAPES[args.shape]
+    # ---- problem header (root) and this rank's synthetic slice (untimed setup = the parsed input)
+    rng = np.random.default_rng(args.seed)
+    seq1 = rng.integers(1, 27, size=shape.L1, dtype=np.uint8)
+    weights = np.array(shape.weights, dtype=np.int32)
+    header = torch.from_numpy(np.concatenate([weights, seq1.astype(np.int32)])).to(dev)
+    R = args.records_per_gpu
+    rrng = np.random.default_rng(args.seed + 1 + rank)
+    lengths = rrng.integers(shape.l2_min, shape.l2_max + 1, size=R, dtype=np.int64)
+    tag = os.environ.get("MASTER_PORT", str(os.getpid()))
+    host = HostArrays(tag, rank, lengths, bool(args.shm))
+    fill_codes(host.codes, args.seed + 101 + rank)
+    del lengths
+    pin = Pinned(host.codes, host.offsets, host.results)
+
+    eng = HipSearchEngine(device=local_rank)
+    done = torch.zeros(1, dtype=torch.int64, device=dev)
+    hdr_host = np.empty(4 + shape.L1, dtype=np.int32)
+
+    def step():
+        if distributed:
+            dist.broadcast(header, src=0)
+        hdr_host[:] = header.cpu().numpy()
+        eng.set_problem(hdr_host[:4], hdr_host[4:].astype(np.uint8))
+        eng.solve(host.codes, host.offsets, out=host.results.view(np.dtype([("score", "<i4"), ("n", "<i4"),
+                                                                            ("k", "<i4")])))
+        done.fill_(R)
+        if distributed:
+            dist.all_reduce(done)
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if distributed:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    st = eng.stats()
+
+    # ---- verification (untimed): sample of this rank's results vs the CPU engine
+    nv = min(args.verify, R)
+    ok = 1
+    if nv > 0:
+        sub = Problem(shape.weights, seq1, host.codes[:int(host.offsets[nv])], host.offsets[:nv + 1].copy())
+        ref = as_triples(search_cpu(sub))
+        ok = int(np.array_equal(host.results[:3 * nv].reshape(-1, 3), ref))
+    okt = torch.tensor([ok], dtype=torch.int32, device=dev)
+    if distributed:
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+
+    total_records = R * world
+    total_elems = int(host.offsets[-1]) * world  # per-rank chars ~ equal (same length distribution)
+    if distributed:
+        te = torch.tensor([int(host.offsets[-1])], dtype=torch.int64, device=dev)
+        dist.all_reduce(te)
+        total_elems = int(te.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    value = total_elems * args.steps / elapsed
+    cells_per_rec = float(np.mean([(shape.L1 - l + 1) * l for l in range(shape.l2_min, shape.l2_max + 1)]))
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "elements/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "wall_clock_s": round(elapsed, 6),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic",
+            "config": {
+                "model": f"{args.shape}-shaped alignment search (W={list(shape.weights)}, |Seq1|={shape.L1}, "
+                         f"|Seq2|={shape.l2_min}..{shape.l2_max})",
+                "global_batch": total_records,
+                "seq_len": shape.L1,
+                "parallelism": f"dp{world}",
+            },
+            "records_per_s": round(total_records * args.steps / elapsed, 1),
+            "cells_per_s_est": round(total_records * cells_per_rec * args.steps / elapsed, 1),
+            "rank0_kernel_ms_per_step": round(st["kernel_ms"], 4),
+            "rank0_h2d_bytes_per_step": int(st["h2d_bytes"]),
+            "rank0_d2h_bytes_per_step": int(st["d2h_bytes"]),
+            "host_arrays": "shm" if host.shm else "private",
+            "verified": bool(okt.item()),
+        }
+        print(json.dumps(out), flush=True)
+    pin.release()
+    if distributed:
+        dist.barrier(device_ids=[local_rank])
+        dist.destroy_process_group()
+    host.cleanup()
+
+
+if __name__ == "__main__":
+    main()

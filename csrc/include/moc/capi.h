@@ -1,0 +1,64 @@
+/* Flat C ABI of libmoc.so — consumed by the Python package through ctypes (no pybind/torch build
+ * dependency, so the same shared object serves the CLI, the tests and the torch-facing ops).
+ * Every function returns 0 on success or -1 on error (message: moc_last_error()). */
+#ifndef MOC_CAPI_H_
+#define MOC_CAPI_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct moc_result {
+  int32_t score, n, k;
+} moc_result;
+
+const char* moc_last_error(void);
+int moc_abi_version(void);
+int moc_set_log_level(const char* level);
+
+/* ---- problem / io ---- */
+void* moc_parse(const char* data, size_t len, int strict_limits);
+void moc_problem_free(void* p);
+int moc_problem_info(void* p, int32_t* weights4, int64_t* L1, int64_t* n, int64_t* total_chars);
+const uint8_t* moc_problem_seq1(void* p);
+const uint8_t* moc_problem_codes(void* p);
+const int64_t* moc_problem_offsets(void* p);
+/* Formats rows into buf (cap bytes); returns bytes written or -1 (needs ~96 B per row). */
+int64_t moc_format_results(const moc_result* r, int64_t n, int64_t first_index, char* buf, int64_t cap);
+
+/* ---- score table ---- */
+int moc_score_table(const int32_t* weights4, int32_t* lut1024, uint8_t* cls1024);
+
+/* ---- CPU engine (OpenMP) ---- */
+int moc_cpu_solve(const int32_t* weights4, const uint8_t* seq1, int64_t L1, const uint8_t* codes,
+                  const int64_t* offsets, int64_t n, int semantics, int threads, moc_result* out);
+int moc_brute_force(const int32_t* weights4, const uint8_t* seq1, int64_t L1, const uint8_t* codes,
+                    const int64_t* offsets, int64_t n, int semantics, moc_result* out);
+
+/* ---- partition ---- */
+int moc_partition(const int64_t* lengths, int64_t n, int64_t L1, int parts, double cell_w, double byte_w,
+                  double record_w, int64_t* bounds_out /* parts+1 */);
+
+/* ---- HIP engine ---- */
+int moc_device_count(void);
+/* Page-locks [p, p+bytes) for direct DMA (hipHostRegister on the enclosing page range). */
+int moc_host_register(void* p, size_t bytes);
+int moc_host_unregister(void* p);
+int moc_device_info_json(int device, char* buf, int64_t cap);
+void* moc_engine_create(int device, int64_t chunk_records, int64_t chunk_bytes, int pin_host);
+void moc_engine_destroy(void* e);
+int moc_engine_set_problem(void* e, const int32_t* weights4, const uint8_t* seq1, int64_t L1, int semantics);
+int moc_engine_solve(void* e, const uint8_t* codes, const int64_t* offsets, int64_t n, moc_result* out);
+int moc_engine_solve_device(void* e, const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets,
+                            int64_t n, moc_result* d_out, void* stream);
+/* stats: kernel_ms, total_ms, h2d_bytes, d2h_bytes, chunks, cells, records */
+int moc_engine_stats(void* e, double* out7);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

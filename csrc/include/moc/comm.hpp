@@ -1,0 +1,96 @@
+// Distributed layer of the native CLI: MPI bootstrap + host collectives, RCCL device collectives,
+// and the node-shared input window.
+//
+// Reference collectives: MPI_Bcast x4 (main.c:149-152, incl. the 16-int weights
+// over-read, bug B3), MPI_Scatter of fixed 2000-byte records (main.c:174) and MPI_Gather x3
+// (main.c:195-197), all blocking, host-memory, rooted at 0, and with no device binding (B14).
+//
+// Here:
+//   * MpiContext   — MPI_Init_thread, world + node-local communicators, local rank -> device.
+//   * host helpers — exact-count broadcasts, 64-bit-safe Scatterv/Gatherv of bytes.
+//   * SharedWindow — MPI_Win_allocate_shared over the node communicator: the root parses the input
+//                    into it once and every rank DMAs its own slice over its own PCIe link.
+//   * RcclComm     — ncclCommInitRank with the unique id broadcast over MPI; device broadcast and
+//                    grouped variable-size send/recv (the scatter/gather of records over xGMI).
+#pragma once
+
+#include <mpi.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "moc/common.hpp"
+
+namespace moc {
+
+class MpiContext {
+ public:
+  MpiContext(int* argc, char*** argv);
+  ~MpiContext();
+  MpiContext(const MpiContext&) = delete;
+  MpiContext& operator=(const MpiContext&) = delete;
+
+  int rank = 0, size = 1;
+  int local_rank = 0, local_size = 1;
+  int node_count = 1;
+  MPI_Comm world = MPI_COMM_WORLD;
+  MPI_Comm node = MPI_COMM_NULL;  // ranks sharing this node's memory
+  bool single_node() const { return node_count == 1; }
+  std::string hostname;
+
+  [[noreturn]] void abort(int code, const std::string& msg) const;
+};
+
+void mpi_check(int rc, const char* what);
+
+// Broadcast of arbitrary byte counts (>2 GiB safe) from root.
+void bcast_bytes(void* buf, int64_t bytes, int root, MPI_Comm comm);
+// Root sends counts[r] bytes at displs[r] of sendbuf to rank r (64-bit safe, any sizes).
+void scatterv_bytes(const void* sendbuf, const std::vector<int64_t>& counts, const std::vector<int64_t>& displs,
+                    void* recvbuf, int root, MPI_Comm comm);
+// Inverse of scatterv_bytes.
+void gatherv_bytes(const void* sendbuf, int64_t count, void* recvbuf, const std::vector<int64_t>& counts,
+                   const std::vector<int64_t>& displs, int root, MPI_Comm comm);
+
+class SharedWindow {
+ public:
+  // Collective over ctx.node; only the node's local rank 0 allocates `bytes` (others pass 0).
+  SharedWindow(const MpiContext& ctx, int64_t bytes);
+  ~SharedWindow();
+  char* base() const { return base_; }
+  int64_t bytes() const { return bytes_; }
+  void fence() const;  // MPI_Win_sync + node barrier: makes the owner's writes visible
+
+ private:
+  MPI_Win win_ = MPI_WIN_NULL;
+  MPI_Comm comm_ = MPI_COMM_NULL;
+  char* base_ = nullptr;
+  int64_t bytes_ = 0;
+};
+
+class RcclComm {
+ public:
+  RcclComm(const MpiContext& ctx, int device);
+  ~RcclComm();
+  RcclComm(const RcclComm&) = delete;
+  RcclComm& operator=(const RcclComm&) = delete;
+
+  void bcast(void* dbuf, int64_t bytes, int root, hipStream_t s);
+  // Root: sends slices [displs[r], displs[r]+counts[r]) of d_send to every rank r != root.
+  // Others: receive counts[rank] bytes into d_recv. One ncclGroup, variable sizes.
+  void scatterv(const void* d_send, const std::vector<int64_t>& counts, const std::vector<int64_t>& displs,
+                void* d_recv, int root, hipStream_t s);
+  // Inverse: every rank != root sends its slice to root, which receives it at displs[r].
+  void gatherv(const void* d_send, int64_t count, void* d_recv, const std::vector<int64_t>& counts,
+               const std::vector<int64_t>& displs, int root, hipStream_t s);
+  void check_async() const;  // ncclCommGetAsyncError -> throw
+  ncclComm_t comm() const { return comm_; }
+
+ private:
+  const MpiContext& ctx_;
+  ncclComm_t comm_ = nullptr;
+};
+
+}  // namespace moc

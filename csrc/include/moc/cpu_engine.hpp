@@ -1,0 +1,51 @@
+// CPU (OpenMP) search engine — the "GPU kernel stubbed" backend of BASELINE.json config 1, and the
+// C++ test oracle for the HIP kernels.
+//
+// Reference semantics (cudaFunctions.cu:63-176, race-free reading):
+//   score(o, 0)  = sum_i T[s2_i][s1_{i+o}]                                  (no hyphen)
+//   score(o, k)  = sum_{i<k} T[s2_i][s1_{i+o}] + sum_{i>=k} T[s2_i][s1_{i+o+1}],  k = 1..L2-1
+//   offsets o in [0, L1-L2) (exclusive, :116), ties -> first in offset-major / mutant-minor order
+//   (strict `max <` at :161); L2 == L1 -> (0,0) only (:74-106); L2 > L1 -> (INT_MIN, 0, 0).
+// Closed form used here: with P_d(k) = sum_{i<k} T[s2_i][s1_{i+d}] and Tot_d = P_d(L2),
+//   score(o, k>=1) = P_o(k) - P_{o+1}(k) + Tot_{o+1}  -> O(L1*L2) instead of O(L1*L2^2).
+#pragma once
+
+#include <cstdint>
+
+#include "moc/common.hpp"
+#include "moc/problem.hpp"
+#include "moc/score_table.hpp"
+
+namespace moc {
+
+// Lexicographic "better than" for candidates: higher score, then smaller offset, then smaller k
+// (k == 0 is the un-mutated sequence and comes first inside an offset, as in the reference loop).
+inline bool better(const Result& a, const Result& b) {
+  if (a.score != b.score) return a.score > b.score;
+  if (a.n != b.n) return a.n < b.n;
+  return a.k < b.k;
+}
+
+// Best candidate for one record restricted to offsets [o_begin, o_end) of the full candidate set.
+// Returns {kNoCandidateScore, -1, -1} when the range holds no candidate.
+Result solve_offsets(const ScoreTable& t, const uint8_t* s1, int64_t L1, const uint8_t* s2, int64_t L2,
+                     int64_t o_begin, int64_t o_end, Semantics sem);
+
+// Number of offsets in the candidate set of a record (reference: L1-L2, spec: L1-L2+1; 1 if equal).
+int64_t candidate_offsets(int64_t L1, int64_t L2, Semantics sem);
+
+// Full search for one record.
+Result solve_record(const ScoreTable& t, const uint8_t* s1, int64_t L1, const uint8_t* s2, int64_t L2,
+                    Semantics sem);
+
+// Batch search (OpenMP). Records [0, batch.size()) -> out[0..N). Parallel over records when there are
+// many, over offset ranges of each record when there are few (the "context-parallel" split, §5.7).
+void solve_batch_cpu(const ScoreTable& t, const uint8_t* s1, int64_t L1, const RecordBatch& batch, Result* out,
+                     Semantics sem, int num_threads = 0);
+
+// Literal O(L1*L2^2) emulation of calc_result's loops (cudaFunctions.cu:74-172), race-free.
+// Test oracle only.
+Result brute_force_record(const ScoreTable& t, const uint8_t* s1, int64_t L1, const uint8_t* s2, int64_t L2,
+                          Semantics sem);
+
+}  // namespace moc

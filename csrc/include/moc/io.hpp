@@ -1,0 +1,40 @@
+// Input parser and result writer (root rank only — PDF p.5: one process reads and writes).
+//
+// Reference: fscanf-based reading (main.c:76-108) with an OpenMP loop that calls fscanf on the
+// shared stdin from many threads (bug B2: nondeterministic record order) and unbounded %s reads
+// (bug B12). Output: printf per row (main.c:199-211).
+//
+// Here: the whole stream is read in bulk, the header is tokenised sequentially, and the record area
+// is tokenised + upper-cased + encoded by a two-pass OpenMP scan (count, prefix-sum, fill), so the
+// order is always input order and the thread count only changes speed.
+#pragma once
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "moc/common.hpp"
+#include "moc/problem.hpp"
+
+namespace moc {
+
+struct ParseOptions {
+  bool strict_limits = false;  // enforce PDF limits: |Seq1| <= 3000, |Seq2| <= 2000
+  int64_t max_l1 = 0;          // 0 = unlimited
+  int64_t max_l2 = 0;          // 0 = unlimited
+};
+
+// Reads the whole stream into memory (bulk fread; no per-token stdio).
+std::vector<char> read_stream(FILE* f);
+
+// Parses "W1 W2 W3 W4 / Seq1 / N / Seq2 x N" (PDF p.5-6). Whitespace of any kind (incl. CRLF)
+// separates tokens, exactly like fscanf %d/%s. Throws moc::Error with a precise message.
+Problem parse_problem(const char* data, size_t len, const ParseOptions& opt = {});
+
+// Formats "#i: score: S, n: N, k: K\n" rows (main.c:204) for results[0..n), numbering from
+// first_index, in parallel, then writes them with one fwrite.
+void write_results(FILE* f, const Result* results, int64_t n, int64_t first_index = 0);
+std::string format_results(const Result* results, int64_t n, int64_t first_index = 0);
+
+}  // namespace moc

@@ -1,0 +1,50 @@
+// Problem model: weights + Seq1 + a CSR batch of Seq2 records, all letters already encoded 1..26.
+//
+// Reference equivalent: weights int[4] (main.c:55), seq1 = malloc(3000) (main.c:66) and the
+// fixed-stride seq2_all[N*2000] buffer (main.c:93). A fixed 2000-byte stride wastes >99% of the
+// scatter bytes on input6 and overflows on a 2000-letter record (bug B12), so records are packed
+// CSR here: codes[] concatenated, offsets[N+1].
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include "moc/common.hpp"
+
+namespace moc {
+
+struct RecordBatch {
+  std::vector<uint8_t> codes;    // concatenated letter codes (1..26)
+  std::vector<int64_t> offsets;  // size N+1, offsets[0] == 0
+
+  RecordBatch() : offsets(1, 0) {}
+  int64_t size() const { return static_cast<int64_t>(offsets.size()) - 1; }
+  int64_t length(int64_t i) const { return offsets[i + 1] - offsets[i]; }
+  const uint8_t* record(int64_t i) const { return codes.data() + offsets[i]; }
+  int64_t total_chars() const { return offsets.back(); }
+  int64_t max_length() const;
+  void push_back(const uint8_t* c, int64_t n);
+  // Contiguous slice [b, e) re-based to offset 0.
+  RecordBatch slice(int64_t b, int64_t e) const;
+};
+
+struct Problem {
+  Weights weights;
+  std::vector<uint8_t> seq1;  // letter codes
+  RecordBatch seq2;
+
+  int64_t L1() const { return static_cast<int64_t>(seq1.size()); }
+};
+
+// Number of candidate cells the O(L1*L2) search touches for one record: (L1-L2+1)*L2, 0 if L2 > L1.
+inline int64_t record_cells(int64_t L1, int64_t L2) { return L2 <= L1 ? (L1 - L2 + 1) * L2 : 0; }
+
+// Throws moc::Error when the int32 score arithmetic (shared by the CPU and device engines, as in the
+// reference's int counters, cudaFunctions.cu:103,161) could overflow for this problem.
+void validate_score_range(const Weights& w, int64_t max_len2);
+
+// Encodes an ASCII string (letters only, any case) into codes; throws on a non-letter.
+std::vector<uint8_t> encode_sequence(const char* s, int64_t n);
+std::string decode_sequence(const uint8_t* codes, int64_t n);
+
+}  // namespace moc

@@ -1,0 +1,45 @@
+// Fused pair-score lookup table.
+//
+// The reference builds two 27x27 char membership matrices (build_mat, main.c:14-44, groups at
+// main.c:59-60), uploads them plus the weights into __constant__ memory (cudaFunctions.cu:9-13,35-61)
+// and, per character pair, walks an if/else chain ($ -> % -> # -> ' ', cudaFunctions.cu:132-153)
+// followed by a 4-bin atomic histogram and a weight dot product.
+//
+// Here the whole chain collapses into ONE int32 table T[a][b] = +W1 / -W2 / -W3 / -W4 (fully
+// initialised — fixes bug B1, main.c:24), so the device inner loop is a single LDS gather + add.
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "moc/common.hpp"
+
+namespace moc {
+
+enum PairClass : uint8_t { kDollar = 0, kPercent = 1, kHash = 2, kSpace = 3 };
+
+// First-type ("%") groups: PDF p.1-2, main.c:59 (9 groups; the reference pads with two "").
+const std::vector<std::string>& first_type_groups();
+// Second-type ("#") groups: PDF p.2, main.c:60 (11 groups).
+const std::vector<std::string>& second_type_groups();
+
+struct ScoreTable {
+  Weights weights;
+  // cls[a*32+b]: PairClass of (Seq2 letter a, Seq1 letter b), codes 1..26; row/col 0 and 27..31 = kSpace.
+  std::array<uint8_t, kLutStride * kLutStride> cls{};
+  // lut[a*32+b]: signed score contribution of that pair.
+  std::array<int32_t, kLutStride * kLutStride> lut{};
+
+  static ScoreTable build(const Weights& w);
+
+  int32_t score(int a, int b) const { return lut[a * kLutStride + b]; }
+  PairClass pair_class(int a, int b) const { return static_cast<PairClass>(cls[a * kLutStride + b]); }
+
+  int32_t max_abs() const;  // max |T| — used to pick safe device key widths
+  // The reference's display character for a pair class ('$', '%', '#', ' ').
+  static char class_char(PairClass c);
+};
+
+}  // namespace moc

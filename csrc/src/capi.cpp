@@ -1,0 +1,211 @@
+// C ABI implementation (see moc/capi.h).
+#include "moc/capi.h"
+
+#include <cstring>
+#include <exception>
+#include <string>
+
+#include "moc/cpu_engine.hpp"
+#include "moc/hip_engine.hpp"
+#include "moc/io.hpp"
+#include "moc/partition.hpp"
+#include "moc/problem.hpp"
+#include "moc/runtime/device.hpp"
+#include "moc/runtime/hip_check.hpp"
+#include "moc/runtime/log.hpp"
+#include "moc/score_table.hpp"
+
+static_assert(sizeof(moc_result) == sizeof(moc::Result), "ABI result layout");
+
+namespace {
+thread_local std::string g_err;
+
+template <class F>
+int guard(F&& f) {
+  try {
+    f();
+    return 0;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+  } catch (...) {
+    g_err = "unknown error";
+  }
+  return -1;
+}
+
+moc::Weights weights_of(const int32_t* w4) {
+  moc::Weights w;
+  for (int i = 0; i < 4; ++i) w.w[i] = w4[i];
+  return w;
+}
+
+moc::RecordBatch view_batch(const uint8_t* codes, const int64_t* offsets, int64_t n) {
+  moc::RecordBatch b;
+  const int64_t base = offsets[0];
+  b.codes.assign(codes + base, codes + offsets[n]);
+  b.offsets.resize(static_cast<size_t>(n) + 1);
+  for (int64_t i = 0; i <= n; ++i) b.offsets[i] = offsets[i] - base;
+  return b;
+}
+}  // namespace
+
+extern "C" {
+
+const char* moc_last_error(void) { return g_err.c_str(); }
+int moc_abi_version(void) { return 1; }
+int moc_set_log_level(const char* level) {
+  return guard([&] { moc::log_set_level(std::string(level)); });
+}
+
+void* moc_parse(const char* data, size_t len, int strict_limits) {
+  moc::Problem* p = nullptr;
+  int rc = guard([&] {
+    moc::ParseOptions opt;
+    opt.strict_limits = strict_limits != 0;
+    p = new moc::Problem(moc::parse_problem(data, len, opt));
+  });
+  return rc == 0 ? p : nullptr;
+}
+
+void moc_problem_free(void* p) { delete static_cast<moc::Problem*>(p); }
+
+int moc_problem_info(void* p, int32_t* weights4, int64_t* L1, int64_t* n, int64_t* total_chars) {
+  return guard([&] {
+    auto* pr = static_cast<moc::Problem*>(p);
+    for (int i = 0; i < 4; ++i) weights4[i] = pr->weights.w[i];
+    *L1 = pr->L1();
+    *n = pr->seq2.size();
+    *total_chars = pr->seq2.total_chars();
+  });
+}
+const uint8_t* moc_problem_seq1(void* p) { return static_cast<moc::Problem*>(p)->seq1.data(); }
+const uint8_t* moc_problem_codes(void* p) { return static_cast<moc::Problem*>(p)->seq2.codes.data(); }
+const int64_t* moc_problem_offsets(void* p) { return static_cast<moc::Problem*>(p)->seq2.offsets.data(); }
+
+int64_t moc_format_results(const moc_result* r, int64_t n, int64_t first_index, char* buf, int64_t cap) {
+  int64_t written = -1;
+  guard([&] {
+    std::string s = moc::format_results(reinterpret_cast<const moc::Result*>(r), n, first_index);
+    if (static_cast<int64_t>(s.size()) > cap) throw moc::Error("format buffer too small");
+    std::memcpy(buf, s.data(), s.size());
+    written = static_cast<int64_t>(s.size());
+  });
+  return written;
+}
+
+int moc_score_table(const int32_t* weights4, int32_t* lut1024, uint8_t* cls1024) {
+  return guard([&] {
+    moc::ScoreTable t = moc::ScoreTable::build(weights_of(weights4));
+    if (lut1024) std::memcpy(lut1024, t.lut.data(), sizeof(int32_t) * t.lut.size());
+    if (cls1024) std::memcpy(cls1024, t.cls.data(), t.cls.size());
+  });
+}
+
+int moc_cpu_solve(const int32_t* weights4, const uint8_t* seq1, int64_t L1, const uint8_t* codes,
+                  const int64_t* offsets, int64_t n, int semantics, int threads, moc_result* out) {
+  return guard([&] {
+    moc::Weights w = weights_of(weights4);
+    moc::RecordBatch b = view_batch(codes, offsets, n);
+    moc::validate_score_range(w, std::max<int64_t>(b.max_length(), 1));
+    moc::ScoreTable t = moc::ScoreTable::build(w);
+    moc::solve_batch_cpu(t, seq1, L1, b, reinterpret_cast<moc::Result*>(out), static_cast<moc::Semantics>(semantics),
+                         threads);
+  });
+}
+
+int moc_brute_force(const int32_t* weights4, const uint8_t* seq1, int64_t L1, const uint8_t* codes,
+                    const int64_t* offsets, int64_t n, int semantics, moc_result* out) {
+  return guard([&] {
+    moc::ScoreTable t = moc::ScoreTable::build(weights_of(weights4));
+    for (int64_t i = 0; i < n; ++i) {
+      moc::Result r = moc::brute_force_record(t, seq1, L1, codes + offsets[i], offsets[i + 1] - offsets[i],
+                                              static_cast<moc::Semantics>(semantics));
+      std::memcpy(out + i, &r, sizeof r);
+    }
+  });
+}
+
+int moc_partition(const int64_t* lengths, int64_t n, int64_t L1, int parts, double cell_w, double byte_w,
+                  double record_w, int64_t* bounds_out) {
+  return guard([&] {
+    moc::CostModel m{cell_w, byte_w, record_w};
+    auto b = moc::partition_by_cost(lengths, n, L1, parts, m);
+    std::memcpy(bounds_out, b.data(), sizeof(int64_t) * b.size());
+  });
+}
+
+int moc_device_count(void) { return moc::device_count(); }
+
+int moc_host_register(void* p, size_t bytes) {
+  return guard([&] {
+    const uintptr_t page = 4096;
+    uintptr_t b = reinterpret_cast<uintptr_t>(p) & ~(page - 1);
+    uintptr_t e = (reinterpret_cast<uintptr_t>(p) + bytes + page - 1) & ~(page - 1);
+    MOC_HIP_CHECK(hipHostRegister(reinterpret_cast<void*>(b), e - b, hipHostRegisterDefault));
+  });
+}
+
+int moc_host_unregister(void* p) {
+  return guard([&] {
+    MOC_HIP_CHECK(hipHostUnregister(reinterpret_cast<void*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t{4095})));
+  });
+}
+
+int moc_device_info_json(int device, char* buf, int64_t cap) {
+  return guard([&] {
+    std::string s = moc::device_info(device).json();
+    if (static_cast<int64_t>(s.size()) + 1 > cap) throw moc::Error("buffer too small");
+    std::memcpy(buf, s.c_str(), s.size() + 1);
+  });
+}
+
+void* moc_engine_create(int device, int64_t chunk_records, int64_t chunk_bytes, int pin_host) {
+  moc::HipEngine* e = nullptr;
+  int rc = guard([&] {
+    moc::EngineOptions o;
+    o.device = device;
+    if (chunk_records > 0) o.chunk_records = chunk_records;
+    if (chunk_bytes > 0) o.chunk_bytes = chunk_bytes;
+    o.pin_host = pin_host != 0;
+    e = new moc::HipEngine(o);
+  });
+  return rc == 0 ? e : nullptr;
+}
+
+void moc_engine_destroy(void* e) { delete static_cast<moc::HipEngine*>(e); }
+
+int moc_engine_set_problem(void* e, const int32_t* weights4, const uint8_t* seq1, int64_t L1, int semantics) {
+  return guard([&] {
+    static_cast<moc::HipEngine*>(e)->set_problem(weights_of(weights4), seq1, L1, static_cast<moc::Semantics>(semantics));
+  });
+}
+
+int moc_engine_solve(void* e, const uint8_t* codes, const int64_t* offsets, int64_t n, moc_result* out) {
+  return guard([&] {
+    static_cast<moc::HipEngine*>(e)->solve(codes, offsets, n, reinterpret_cast<moc::Result*>(out));
+  });
+}
+
+int moc_engine_solve_device(void* e, const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets,
+                            int64_t n, moc_result* d_out, void* stream) {
+  return guard([&] {
+    static_cast<moc::HipEngine*>(e)->solve_device(d_codes, d_offsets, h_offsets, n,
+                                                  reinterpret_cast<moc::Result*>(d_out),
+                                                  static_cast<hipStream_t>(stream));
+  });
+}
+
+int moc_engine_stats(void* e, double* out7) {
+  return guard([&] {
+    const auto& s = static_cast<moc::HipEngine*>(e)->stats();
+    out7[0] = s.kernel_ms;
+    out7[1] = s.total_ms;
+    out7[2] = static_cast<double>(s.h2d_bytes);
+    out7[3] = static_cast<double>(s.d2h_bytes);
+    out7[4] = static_cast<double>(s.chunks);
+    out7[5] = static_cast<double>(s.cells);
+    out7[6] = static_cast<double>(s.records);
+  });
+}
+
+}  // extern "C"

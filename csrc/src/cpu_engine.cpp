@@ -1,0 +1,133 @@
+#include "moc/cpu_engine.hpp"
+
+#include <omp.h>
+
+#include <algorithm>
+#include <vector>
+
+namespace moc {
+
+int64_t candidate_offsets(int64_t L1, int64_t L2, Semantics sem) {
+  if (L2 > L1 || L2 <= 0) return 0;
+  if (L2 == L1) return 1;
+  return sem == Semantics::Spec ? L1 - L2 + 1 : L1 - L2;
+}
+
+namespace {
+
+// prefix[k] = P_d(k) for k = 0..L2 (diagonal d: Seq2[i] faces Seq1[i+d]).
+inline void diag_prefix(const ScoreTable& t, const uint8_t* s1, const uint8_t* s2, int64_t L2, int64_t d,
+                        int32_t* prefix) {
+  int32_t acc = 0;
+  prefix[0] = 0;
+  const uint8_t* a = s1 + d;
+  for (int64_t i = 0; i < L2; ++i) {
+    acc += t.lut[s2[i] * kLutStride + a[i]];
+    prefix[i + 1] = acc;
+  }
+}
+
+inline void consider(Result& best, int32_t score, int64_t o, int64_t k) {
+  Result c{score, static_cast<int32_t>(o), static_cast<int32_t>(k)};
+  if (best.n < 0 || better(c, best)) best = c;
+}
+
+}  // namespace
+
+Result solve_offsets(const ScoreTable& t, const uint8_t* s1, int64_t L1, const uint8_t* s2, int64_t L2,
+                     int64_t o_begin, int64_t o_end, Semantics sem) {
+  Result best{kNoCandidateScore, -1, -1};
+  const int64_t n_off = candidate_offsets(L1, L2, sem);
+  o_end = std::min(o_end, n_off);
+  if (o_begin >= o_end) return best;
+  if (L2 == L1) {  // equal lengths: un-shifted, un-mutated only (cudaFunctions.cu:74-106)
+    int32_t s = 0;
+    for (int64_t i = 0; i < L2; ++i) s += t.lut[s2[i] * kLutStride + s1[i]];
+    consider(best, s, 0, 0);
+    return best;
+  }
+  const int64_t last_mut_off = L1 - L2;  // offsets with a hyphen need o + L2 + 1 <= L1
+  std::vector<int32_t> cur(L2 + 1), nxt(L2 + 1);
+  diag_prefix(t, s1, s2, L2, o_begin, cur.data());
+  for (int64_t o = o_begin; o < o_end; ++o) {
+    consider(best, cur[L2], o, 0);
+    if (o < last_mut_off) {
+      diag_prefix(t, s1, s2, L2, o + 1, nxt.data());
+      const int32_t tot_next = nxt[L2];
+      for (int64_t k = 1; k < L2; ++k) consider(best, cur[k] - nxt[k] + tot_next, o, k);
+      std::swap(cur, nxt);
+    }
+  }
+  return best;
+}
+
+Result solve_record(const ScoreTable& t, const uint8_t* s1, int64_t L1, const uint8_t* s2, int64_t L2,
+                    Semantics sem) {
+  Result r = solve_offsets(t, s1, L1, s2, L2, 0, L1 + 1, sem);
+  return r.n < 0 ? no_candidate() : r;
+}
+
+void solve_batch_cpu(const ScoreTable& t, const uint8_t* s1, int64_t L1, const RecordBatch& batch, Result* out,
+                     Semantics sem, int num_threads) {
+  const int64_t n = batch.size();
+  const int nt = num_threads > 0 ? num_threads : omp_get_max_threads();
+  if (n >= 4 * nt || nt == 1) {
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nt)
+    for (int64_t i = 0; i < n; ++i) out[i] = solve_record(t, s1, L1, batch.record(i), batch.length(i), sem);
+    return;
+  }
+  // Few records: split each record's offset range across threads and merge (max is order-free).
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t L2 = batch.length(i);
+    const int64_t n_off = candidate_offsets(L1, L2, sem);
+    if (n_off <= 1) {
+      out[i] = solve_record(t, s1, L1, batch.record(i), L2, sem);
+      continue;
+    }
+    std::vector<Result> part(nt, Result{kNoCandidateScore, -1, -1});
+#pragma omp parallel num_threads(nt)
+    {
+      const int tid = omp_get_thread_num();
+      const int64_t b = n_off * tid / nt, e = n_off * (tid + 1) / nt;
+      part[tid] = solve_offsets(t, s1, L1, batch.record(i), L2, b, e, sem);
+    }
+    Result best{kNoCandidateScore, -1, -1};
+    for (const auto& p : part)
+      if (p.n >= 0 && (best.n < 0 || better(p, best))) best = p;
+    out[i] = best.n < 0 ? no_candidate() : best;
+  }
+}
+
+Result brute_force_record(const ScoreTable& t, const uint8_t* s1, int64_t L1, const uint8_t* s2, int64_t L2,
+                          Semantics sem) {
+  if (L2 > L1) return no_candidate();
+  if (L2 == L1) {
+    int32_t s = 0;
+    for (int64_t i = 0; i < L2; ++i) s += t.lut[s2[i] * kLutStride + s1[i]];
+    return Result{s, 0, 0};
+  }
+  Result best{kNoCandidateScore, 0, 0};
+  bool have = false;
+  for (int64_t o = 0; o < L1 - L2; ++o) {
+    for (int64_t m = 0; m < L2; ++m) {
+      int32_t s = 0;
+      for (int64_t i = 0; i < L2; ++i) {
+        const int64_t j = (i < m || m == 0) ? i + o : i + o + 1;
+        s += t.lut[s2[i] * kLutStride + s1[j]];
+      }
+      if (!have || best.score < s) {
+        best = Result{s, static_cast<int32_t>(o), static_cast<int32_t>(m)};
+        have = true;
+      }
+    }
+  }
+  if (sem == Semantics::Spec) {
+    int32_t s = 0;
+    const int64_t o = L1 - L2;
+    for (int64_t i = 0; i < L2; ++i) s += t.lut[s2[i] * kLutStride + s1[i + o]];
+    if (!have || best.score < s) best = Result{s, static_cast<int32_t>(o), 0};
+  }
+  return best;
+}
+
+}  // namespace moc

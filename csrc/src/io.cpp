@@ -1,0 +1,247 @@
+#include "moc/io.hpp"
+
+#include <omp.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstdlib>
+#include <cstring>
+
+namespace moc {
+
+namespace {
+
+inline bool is_space(unsigned char c) { return c == ' ' || c == '\n' || c == '\r' || c == '\t' || c == '\v' || c == '\f'; }
+
+struct Cursor {
+  const char* p;
+  const char* end;
+  // Returns the next whitespace-delimited token [b, e) or false at end of input.
+  bool next(const char*& b, const char*& e) {
+    while (p < end && is_space(static_cast<unsigned char>(*p))) ++p;
+    if (p >= end) return false;
+    b = p;
+    while (p < end && !is_space(static_cast<unsigned char>(*p))) ++p;
+    e = p;
+    return true;
+  }
+};
+
+int64_t parse_int(const char* b, const char* e, const char* what) {
+  std::string tok(b, e);
+  char* stop = nullptr;
+  errno = 0;
+  long long v = std::strtoll(tok.c_str(), &stop, 10);
+  if (errno != 0 || stop != tok.c_str() + tok.size())
+    throw Error(std::string("expected an integer for ") + what + ", got '" + tok + "'");
+  return v;
+}
+
+}  // namespace
+
+std::vector<char> read_stream(FILE* f) {
+  std::vector<char> buf;
+  size_t cap = 1 << 20, len = 0;
+  buf.resize(cap);
+  while (true) {
+    size_t got = std::fread(buf.data() + len, 1, cap - len, f);
+    len += got;
+    if (len < cap) {
+      if (std::ferror(f)) throw Error("error while reading input stream");
+      break;
+    }
+    cap *= 2;
+    buf.resize(cap);
+  }
+  buf.resize(len);
+  return buf;
+}
+
+Problem parse_problem(const char* data, size_t len, const ParseOptions& opt) {
+  Problem prob;
+  Cursor cur{data, data + len};
+  const char *b, *e;
+  static const char* wname[4] = {"W1", "W2", "W3", "W4"};
+  for (int i = 0; i < 4; ++i) {
+    if (!cur.next(b, e)) throw Error(std::string("unexpected end of input while reading ") + wname[i]);
+    int64_t v = parse_int(b, e, wname[i]);
+    if (v < 0 || v > INT32_MAX) throw Error(std::string(wname[i]) + " out of range");
+    prob.weights.w[i] = static_cast<int32_t>(v);
+  }
+  if (!cur.next(b, e)) throw Error("unexpected end of input while reading Seq1");
+  prob.seq1 = encode_sequence(b, e - b);
+  if (!cur.next(b, e)) throw Error("unexpected end of input while reading the number of sequences");
+  const int64_t n = parse_int(b, e, "number_of_sequences");
+  if (n < 0) throw Error("number_of_sequences must be >= 0");
+
+  const int64_t l1_cap = opt.strict_limits ? kSpecMaxSeq1 : opt.max_l1;
+  const int64_t l2_cap = opt.strict_limits ? kSpecMaxSeq2 : opt.max_l2;
+  if (l1_cap > 0 && prob.L1() > l1_cap)
+    throw Error("Seq1 has " + std::to_string(prob.L1()) + " letters, limit is " + std::to_string(l1_cap));
+
+  // ---- parallel two-pass tokenisation of the record area -------------------------------------
+  const char* area = cur.p;
+  const size_t area_len = static_cast<size_t>(cur.end - cur.p);
+  int nthreads = omp_get_max_threads();
+  if (area_len < (size_t{1} << 16)) nthreads = 1;
+  nthreads = std::max(1, nthreads);
+
+  // Chunk starts moved forward to a token start: a token belongs to the chunk holding its first byte.
+  std::vector<size_t> start(nthreads + 1);
+  for (int t = 0; t <= nthreads; ++t) start[t] = area_len * static_cast<size_t>(t) / nthreads;
+  for (int t = 1; t < nthreads; ++t) {
+    size_t s = start[t];
+    while (s < area_len && s > 0 && !is_space(static_cast<unsigned char>(area[s - 1]))) ++s;
+    start[t] = std::max(s, start[t - 1]);
+  }
+  start[nthreads] = area_len;
+
+  std::vector<int64_t> tok_count(nthreads + 1, 0), char_count(nthreads + 1, 0);
+  std::vector<int64_t> bad_pos(nthreads, -1);
+#pragma omp parallel num_threads(nthreads)
+  {
+    const int t = omp_get_thread_num();
+    Cursor c{area + start[t], area + start[t + 1]};
+    const char *tb = nullptr, *te = nullptr;
+    int64_t nt = 0, nc = 0;
+    // A token may run past the chunk end; Cursor stops at the chunk end only for the *start*.
+    c.end = area + area_len;
+    while (true) {
+      // skip spaces but never start a token at/after our chunk end
+      while (c.p < area + start[t + 1] && is_space(static_cast<unsigned char>(*c.p))) ++c.p;
+      if (c.p >= area + start[t + 1]) break;
+      c.next(tb, te);
+      ++nt;
+      nc += te - tb;
+    }
+    tok_count[t + 1] = nt;
+    char_count[t + 1] = nc;
+  }
+  for (int t = 0; t < nthreads; ++t) {
+    tok_count[t + 1] += tok_count[t];
+    char_count[t + 1] += char_count[t];
+  }
+  const int64_t total_tokens = tok_count[nthreads];
+  if (total_tokens < n)
+    throw Error("expected " + std::to_string(n) + " Seq2 records, found only " + std::to_string(total_tokens));
+
+  // Only the first n tokens are records (extra trailing tokens are ignored, like the reference).
+  int64_t n_chars = 0;
+  {
+    // characters of the first n tokens: find the thread holding token n-1 and count precisely
+    n_chars = char_count[nthreads];
+    if (total_tokens > n) {
+      n_chars = 0;
+      Cursor c{area, area + area_len};
+      // rare path (extra tokens): sequential recount of the first n token lengths
+      for (int64_t i = 0; i < n; ++i) {
+        c.next(b, e);
+        n_chars += e - b;
+      }
+    }
+  }
+  prob.seq2.codes.resize(static_cast<size_t>(n_chars));
+  prob.seq2.offsets.assign(static_cast<size_t>(n) + 1, 0);
+  uint8_t* codes = prob.seq2.codes.data();
+  int64_t* offs = prob.seq2.offsets.data();
+
+#pragma omp parallel num_threads(nthreads)
+  {
+    const int t = omp_get_thread_num();
+    int64_t tok = tok_count[t];
+    int64_t pos = char_count[t];
+    Cursor c{area + start[t], area + area_len};
+    const char *tb = nullptr, *te = nullptr;
+    while (tok < n) {
+      while (c.p < area + start[t + 1] && is_space(static_cast<unsigned char>(*c.p))) ++c.p;
+      if (c.p >= area + start[t + 1]) break;
+      c.next(tb, te);
+      for (const char* q = tb; q < te; ++q) {
+        int code = letter_code(static_cast<unsigned char>(*q));
+        if (code == 0 && bad_pos[t] < 0) bad_pos[t] = tok;
+        codes[pos++] = static_cast<uint8_t>(code);
+      }
+      offs[tok + 1] = pos;
+      ++tok;
+    }
+  }
+  for (int t = 0; t < nthreads; ++t)
+    if (bad_pos[t] >= 0) throw Error("Seq2 record #" + std::to_string(bad_pos[t]) + " contains a non-letter character");
+
+  if (l2_cap > 0) {
+    for (int64_t i = 0; i < n; ++i)
+      if (prob.seq2.length(i) > l2_cap)
+        throw Error("Seq2 record #" + std::to_string(i) + " has " + std::to_string(prob.seq2.length(i)) +
+                    " letters, limit is " + std::to_string(l2_cap));
+  }
+  validate_score_range(prob.weights, std::max<int64_t>(prob.seq2.max_length(), 1));
+  return prob;
+}
+
+// ---- writer -------------------------------------------------------------------------------------
+
+namespace {
+inline char* put_int(char* p, int64_t v) {
+  char tmp[24];
+  int n = 0;
+  bool neg = v < 0;
+  uint64_t u = neg ? static_cast<uint64_t>(-(v + 1)) + 1 : static_cast<uint64_t>(v);
+  do {
+    tmp[n++] = static_cast<char>('0' + u % 10);
+    u /= 10;
+  } while (u);
+  if (neg) *p++ = '-';
+  while (n) *p++ = tmp[--n];
+  return p;
+}
+inline char* put_str(char* p, const char* s) {
+  while (*s) *p++ = *s++;
+  return p;
+}
+inline char* format_row(char* p, int64_t idx, const Result& r) {
+  *p++ = '#';
+  p = put_int(p, idx);
+  p = put_str(p, ": score: ");
+  p = put_int(p, r.score);
+  p = put_str(p, ", n: ");
+  p = put_int(p, r.n);
+  p = put_str(p, ", k: ");
+  p = put_int(p, r.k);
+  *p++ = '\n';
+  return p;
+}
+constexpr int kMaxRow = 96;
+}  // namespace
+
+std::string format_results(const Result* results, int64_t n, int64_t first_index) {
+  int nthreads = n > 65536 ? omp_get_max_threads() : 1;
+  std::vector<std::string> parts(nthreads);
+#pragma omp parallel num_threads(nthreads)
+  {
+    const int t = omp_get_thread_num();
+    const int64_t b = n * t / nthreads, e = n * (t + 1) / nthreads;
+    std::string& s = parts[t];
+    s.resize(static_cast<size_t>(e - b) * kMaxRow);
+    char* p = s.data();
+    for (int64_t i = b; i < e; ++i) p = format_row(p, first_index + i, results[i]);
+    s.resize(static_cast<size_t>(p - s.data()));
+  }
+  size_t total = 0;
+  for (auto& s : parts) total += s.size();
+  std::string out;
+  out.reserve(total);
+  for (auto& s : parts) out += s;
+  return out;
+}
+
+void write_results(FILE* f, const Result* results, int64_t n, int64_t first_index) {
+  const int64_t kBlock = int64_t{1} << 22;  // bound the formatting buffer for huge N
+  for (int64_t b = 0; b < n; b += kBlock) {
+    const int64_t e = std::min(n, b + kBlock);
+    std::string s = format_results(results + b, e - b, first_index + b);
+    std::fwrite(s.data(), 1, s.size(), f);
+  }
+  std::fflush(f);
+}
+
+}  // namespace moc

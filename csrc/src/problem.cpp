@@ -1,0 +1,58 @@
+#include "moc/problem.hpp"
+
+#include <algorithm>
+#include <cstdlib>
+#include <string>
+
+namespace moc {
+
+int64_t RecordBatch::max_length() const {
+  int64_t m = 0;
+  for (int64_t i = 0; i < size(); ++i) m = std::max(m, length(i));
+  return m;
+}
+
+void RecordBatch::push_back(const uint8_t* c, int64_t n) {
+  codes.insert(codes.end(), c, c + n);
+  offsets.push_back(offsets.back() + n);
+}
+
+RecordBatch RecordBatch::slice(int64_t b, int64_t e) const {
+  RecordBatch out;
+  if (e <= b) return out;
+  const int64_t base = offsets[b];
+  out.codes.assign(codes.begin() + base, codes.begin() + offsets[e]);
+  out.offsets.resize(e - b + 1);
+  for (int64_t i = b; i <= e; ++i) out.offsets[i - b] = offsets[i] - base;
+  return out;
+}
+
+void validate_score_range(const Weights& w, int64_t max_len2) {
+  int64_t m = 0;
+  for (int i = 0; i < 4; ++i) {
+    if (w.w[i] < 0) throw Error("weights must be non-negative (PDF p.2), got " + std::to_string(w.w[i]));
+    m = std::max<int64_t>(m, w.w[i]);
+  }
+  // Device keys hold 2*max|T|*L2 in int32 with headroom; the CPU engine matches bit-for-bit.
+  if (m * std::max<int64_t>(max_len2, 1) >= (int64_t{1} << 29))
+    throw Error("max weight * max Seq2 length = " + std::to_string(m * max_len2) +
+                " exceeds the int32 score range supported (< 2^29)");
+}
+
+std::vector<uint8_t> encode_sequence(const char* s, int64_t n) {
+  std::vector<uint8_t> out(n);
+  for (int64_t i = 0; i < n; ++i) {
+    int c = letter_code(static_cast<unsigned char>(s[i]));
+    if (c == 0) throw Error(std::string("non-letter character '") + s[i] + "' in sequence");
+    out[i] = static_cast<uint8_t>(c);
+  }
+  return out;
+}
+
+std::string decode_sequence(const uint8_t* codes, int64_t n) {
+  std::string s(n, '?');
+  for (int64_t i = 0; i < n; ++i) s[i] = code_letter(codes[i]);
+  return s;
+}
+
+}  // namespace moc

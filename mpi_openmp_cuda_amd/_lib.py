@@ -1,0 +1,118 @@
+"""ctypes binding of the native core ``lib/libmoc.so`` (C ABI: csrc/include/moc/capi.h).
+
+The shared object is built in-tree by ``make lib`` (or ``__graft_entry__.build()``); it holds the
+parser, score table, OpenMP CPU engine, partitioner and the HIP engine + gfx950 kernels. There is no
+silent Python fallback for the GPU path: if the library is missing, importing an op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_size_t, c_uint8, c_void_p
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libmoc.so")
+
+RESULT_DTYPE = np.dtype([("score", "<i4"), ("n", "<i4"), ("k", "<i4")])
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    """An error reported by the native core (message from moc_last_error)."""
+
+
+def _decl(lib):
+    P = POINTER
+    sig = {
+        "moc_last_error": (c_char_p, []),
+        "moc_abi_version": (c_int, []),
+        "moc_set_log_level": (c_int, [c_char_p]),
+        "moc_parse": (c_void_p, [c_char_p, c_size_t, c_int]),
+        "moc_problem_free": (None, [c_void_p]),
+        "moc_problem_info": (c_int, [c_void_p, P(c_int32), P(c_int64), P(c_int64), P(c_int64)]),
+        "moc_problem_seq1": (c_void_p, [c_void_p]),
+        "moc_problem_codes": (c_void_p, [c_void_p]),
+        "moc_problem_offsets": (c_void_p, [c_void_p]),
+        "moc_format_results": (c_int64, [c_void_p, c_int64, c_int64, c_void_p, c_int64]),
+        "moc_score_table": (c_int, [P(c_int32), c_void_p, c_void_p]),
+        "moc_cpu_solve": (c_int, [P(c_int32), c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p]),
+        "moc_brute_force": (c_int, [P(c_int32), c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
+        "moc_partition": (c_int, [c_void_p, c_int64, c_int64, c_int, c_double, c_double, c_double, c_void_p]),
+        "moc_device_count": (c_int, []),
+        "moc_host_register": (c_int, [c_void_p, c_size_t]),
+        "moc_host_unregister": (c_int, [c_void_p]),
+        "moc_device_info_json": (c_int, [c_int, c_char_p, c_int64]),
+        "moc_engine_create": (c_void_p, [c_int, c_int64, c_int64, c_int]),
+        "moc_engine_destroy": (None, [c_void_p]),
+        "moc_engine_set_problem": (c_int, [c_void_p, P(c_int32), c_void_p, c_int64, c_int]),
+        "moc_engine_solve": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
+        "moc_engine_solve_device": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+        "moc_engine_stats": (c_int, [c_void_p, P(c_double)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+
+
+def lib():
+    """Returns the loaded native library, raising a clear error if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeError(
+                f"native library not built: {LIB_PATH} is missing — run `make lib` "
+                "(or `python -c 'import __graft_entry__ as g; g.build()'`) first")
+        l = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        _decl(l)
+        _lib = l
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        raise NativeError(lib().moc_last_error().decode(errors="replace"))
+    return rc
+
+
+def ptr(a):
+    """Raw pointer of a contiguous numpy array (or None)."""
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "array must be C-contiguous"
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def weights_arg(weights):
+    w = (c_int32 * 4)(*[int(x) for x in weights])
+    return w
+
+
+class Pinned:
+    """Context manager / handle that page-locks numpy arrays for direct DMA (hipHostRegister)."""
+
+    def __init__(self, *arrays):
+        self._ptrs = []
+        for a in arrays:
+            if a is None or a.nbytes == 0:
+                continue
+            check(lib().moc_host_register(ctypes.c_void_p(a.ctypes.data), a.nbytes))
+            self._ptrs.append(a.ctypes.data)
+
+    def release(self):
+        for p in self._ptrs:
+            lib().moc_host_unregister(ctypes.c_void_p(p))
+        self._ptrs = []
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.release()
+
+
+def loaded_path():
+    return LIB_PATH if _lib is not None else None

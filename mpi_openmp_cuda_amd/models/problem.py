@@ -1,0 +1,112 @@
+"""Problem container: weights + Seq1 + a CSR batch of Seq2 records (letters encoded 1..26).
+
+Reference: int weights[4] (main.c:55), seq1 = malloc(3000) (main.c:66) and the fixed 2000-byte-stride
+seq2_all buffer (main.c:93). Here records are packed CSR (codes + int64 offsets), the layout every
+native engine, transport and kernel consumes.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Iterable, Sequence
+
+import numpy as np
+
+from .. import _lib
+from .scoring import Weights, decode, encode
+
+
+@dataclass
+class Problem:
+    weights: Weights
+    seq1: np.ndarray  # uint8 codes
+    codes: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint8))  # uint8 codes, concatenated
+    offsets: np.ndarray = field(default_factory=lambda: np.zeros(1, np.int64))  # int64, n+1
+
+    def __post_init__(self):
+        self.weights = Weights.of(self.weights)
+        self.seq1 = np.ascontiguousarray(self.seq1, dtype=np.uint8)
+        self.codes = np.ascontiguousarray(self.codes, dtype=np.uint8)
+        self.offsets = np.ascontiguousarray(self.offsets, dtype=np.int64)
+
+    # ------------------------------------------------------------------ construction
+    @classmethod
+    def from_strings(cls, weights: Sequence[int], seq1: str, seq2: Iterable[str]) -> "Problem":
+        recs = [encode(s) for s in seq2]
+        lengths = np.array([len(r) for r in recs], dtype=np.int64)
+        offsets = np.zeros(len(recs) + 1, dtype=np.int64)
+        np.cumsum(lengths, out=offsets[1:])
+        codes = np.concatenate(recs) if recs else np.zeros(0, np.uint8)
+        return cls(Weights.of(weights), encode(seq1), codes, offsets)
+
+    @classmethod
+    def parse(cls, text, strict_limits: bool = False) -> "Problem":
+        """Parses the reference stdin format with the native OpenMP parser (csrc/src/io.cpp)."""
+        if isinstance(text, str):
+            text = text.encode()
+        L = _lib.lib()
+        h = L.moc_parse(text, len(text), 1 if strict_limits else 0)
+        if not h:
+            raise ValueError(L.moc_last_error().decode())
+        try:
+            w = (ctypes.c_int32 * 4)()
+            l1, n, tot = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+            _lib.check(L.moc_problem_info(h, w, ctypes.byref(l1), ctypes.byref(n), ctypes.byref(tot)))
+
+            def grab(p, count, dtype):
+                if count == 0:
+                    return np.zeros(0, dtype)
+                buf = (ctypes.c_char * (count * np.dtype(dtype).itemsize)).from_address(p)
+                return np.frombuffer(buf, dtype=dtype).copy()
+
+            seq1 = grab(L.moc_problem_seq1(h), l1.value, np.uint8)
+            codes = grab(L.moc_problem_codes(h), tot.value, np.uint8)
+            offsets = grab(L.moc_problem_offsets(h), n.value + 1, np.int64)
+            return cls(Weights.of(list(w)), seq1, codes, offsets)
+        finally:
+            L.moc_problem_free(h)
+
+    @classmethod
+    def read(cls, path, strict_limits: bool = False) -> "Problem":
+        with open(path, "rb") as f:
+            return cls.parse(f.read(), strict_limits)
+
+    # ------------------------------------------------------------------ views
+    @property
+    def n(self) -> int:
+        return int(self.offsets.shape[0] - 1)
+
+    @property
+    def L1(self) -> int:
+        return int(self.seq1.shape[0])
+
+    @property
+    def lengths(self) -> np.ndarray:
+        return np.diff(self.offsets)
+
+    @property
+    def total_chars(self) -> int:
+        return int(self.offsets[-1] - self.offsets[0])
+
+    def record(self, i: int) -> str:
+        return decode(self.codes[self.offsets[i]:self.offsets[i + 1]])
+
+    def seq1_str(self) -> str:
+        return decode(self.seq1)
+
+    def cells(self) -> int:
+        """Candidate cells of the O(L1*L2) search: sum over records of (L1-L2+1)*L2 (0 if L2 > L1)."""
+        L2 = self.lengths
+        c = np.where(L2 <= self.L1, (self.L1 - L2 + 1) * L2, 0)
+        return int(c.sum())
+
+    def slice(self, b: int, e: int) -> "Problem":
+        offs = self.offsets[b:e + 1]
+        return Problem(self.weights, self.seq1, self.codes[offs[0]:offs[-1]], offs - offs[0])
+
+    def to_text(self) -> str:
+        """Serialises back to the reference stdin format (PDF p.5-6)."""
+        w = self.weights.as_list()
+        lines = [" ".join(map(str, w)), self.seq1_str(), str(self.n)]
+        lines += [self.record(i) for i in range(self.n)]
+        return "\n".join(lines) + "\n"

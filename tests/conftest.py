@@ -1,0 +1,66 @@
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DATA = os.path.join(ROOT, "tests", "data")
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+MPIEXEC = os.environ.get("MOC_MPIEXEC", "/opt/conda/bin/mpiexec")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) GPU")
+    config.addinivalue_line("markers", "slow: long-running test")
+
+
+_built = {"done": False}
+
+
+def ensure_built():
+    """Builds libmoc.so and ./final in-tree once per session if they are missing or stale."""
+    if _built["done"]:
+        return
+    subprocess.run(["make", "-C", ROOT, f"-j{min(16, os.cpu_count() or 8)}", "build"], check=True,
+                   stdout=subprocess.DEVNULL)
+    _built["done"] = True
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _native_build():
+    ensure_built()
+
+
+def input_path(i):
+    return os.path.join(DATA, f"input{i}.txt")
+
+
+def expected(i):
+    with open(os.path.join(DATA, "expected", f"input{i}.out")) as f:
+        return f.read()
+
+
+def gpu_available():
+    try:
+        import torch
+
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+def run_final(args, stdin_path=None, stdin_bytes=None, np_=1, env=None, timeout=120):
+    """Runs ./final under mpiexec (MPICH). Returns CompletedProcess."""
+    e = dict(os.environ)
+    e.setdefault("OMP_NUM_THREADS", "2")
+    if env:
+        e.update(env)
+    cmd = [MPIEXEC, "-np", str(np_), os.path.join(ROOT, "final")] + list(args)
+    data = stdin_bytes
+    if stdin_path is not None:
+        with open(stdin_path, "rb") as f:
+            data = f.read()
+    return subprocess.run(cmd, input=data, capture_output=True, timeout=timeout, env=e)

@@ -1,0 +1,78 @@
+"""CLI behaviour: determinism, semantics flag, error handling, fault injection (no hangs: every run is
+bounded by a timeout), input edge cases through ./final."""
+import subprocess
+
+import pytest
+
+from conftest import expected, input_path, run_final
+
+
+@pytest.mark.parametrize("threads", ["1", "3", "8"])
+def test_deterministic_over_threads(threads):
+    # reference bug B2: parallel fscanf permutes rows with > 1 OpenMP thread
+    r = run_final(["--backend=cpu"], stdin_path=input_path(1), np_=2, env={"OMP_NUM_THREADS": threads})
+    assert r.stdout.decode() == expected(1)
+
+
+def test_help_and_unknown_flag():
+    r = run_final(["--help"], stdin_bytes=b"")
+    assert r.returncode == 0 and b"usage" in r.stdout
+    r = run_final(["--bogus=1"], stdin_bytes=b"")
+    assert r.returncode == 2 and b"unknown flag" in r.stderr
+
+
+def test_env_flag_override():
+    r = run_final([], stdin_path=input_path(6), np_=2, env={"MOC_BACKEND": "cpu", "MOC_TRANSPORT": "mpi"})
+    assert r.returncode == 0 and r.stdout.decode() == expected(6)
+
+
+def test_spec_semantics_flag():
+    text = b"10 2 3 4\nABCDEFGH\n1\nFGH\n"
+    ref = run_final(["--backend=cpu"], stdin_bytes=text)
+    spec = run_final(["--backend=cpu", "--semantics=spec"], stdin_bytes=text)
+    assert ref.stdout == b"#0: score: 16, n: 4, k: 1\n"
+    assert spec.stdout == b"#0: score: 30, n: 5, k: 0\n"
+
+
+def test_parse_error_exit_code():
+    r = run_final(["--backend=cpu"], stdin_bytes=b"1 2 3 4\nAB1\n1\nA\n", np_=3)
+    assert r.returncode == 1
+    assert b"non-letter" in r.stderr and r.stdout == b""
+
+
+def test_edge_records_through_cli():
+    text = b"1 1 1 1\nABCD\n4\nABCD\nABCDE\nA\nDCBA\n"
+    r = run_final(["--backend=cpu"], stdin_bytes=text, np_=3)
+    lines = r.stdout.decode().splitlines()
+    assert lines[0] == "#0: score: 4, n: 0, k: 0"
+    assert lines[1] == "#1: score: -2147483648, n: 0, k: 0"
+    assert len(lines) == 4
+
+
+def test_zero_records():
+    r = run_final(["--backend=cpu"], stdin_bytes=b"1 1 1 1\nABCD\n0\n", np_=2)
+    assert r.returncode == 0 and r.stdout == b""
+
+
+@pytest.mark.parametrize("phase", ["parse", "bcast", "distribute", "compute", "gather"])
+@pytest.mark.parametrize("rank", [0, 1])
+def test_fault_injection_aborts_cleanly(phase, rank):
+    # reference bug B11: exit(1) on one rank without MPI_Abort leaves the peers blocked forever
+    if phase == "parse" and rank == 1:
+        pytest.skip("only the root parses")
+    try:
+        r = run_final(["--backend=cpu", f"--inject-fault={phase}:{rank}"], stdin_path=input_path(3), np_=2,
+                      timeout=60)
+    except subprocess.TimeoutExpired:
+        pytest.fail("fault did not abort the job (hang)")
+    assert r.returncode != 0
+    assert b"injected fault" in r.stderr or phase == "parse"
+
+
+def test_timing_json():
+    import json
+
+    r = run_final(["--backend=cpu", "--timing"], stdin_path=input_path(4), np_=2)
+    line = [l for l in r.stderr.decode().splitlines() if l.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["records"] == 30 and d["ranks"] == 2 and "compute_ms" in d["timing"]

@@ -1,0 +1,128 @@
+"""GPU (MI355X / gfx950) tests: HIP engine == CPU engine == goldens. Numerics oracle: the CPU engine,
+itself pinned to the brute-force replay of the reference loops (test_oracles.py)."""
+import numpy as np
+import pytest
+
+from conftest import expected, gpu_available, input_path, run_final
+
+pytestmark = pytest.mark.gpu
+
+if not gpu_available():  # pragma: no cover - collected on CPU hosts only with -m gpu
+    pytest.skip("no GPU", allow_module_level=True)
+
+import torch  # noqa: E402
+
+from mpi_openmp_cuda_amd import (HipSearchEngine, Problem, Semantics, brute_force_native, format_results,  # noqa: E402
+                                 make_synthetic, search_cpu)
+from mpi_openmp_cuda_amd.ops.align import align_search_device, as_triples, device_info  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def engine():
+    e = HipSearchEngine(device=0)
+    yield e
+    e.close()
+
+
+def check(engine, prob, sem=Semantics.REFERENCE):
+    engine.set_problem(prob.weights, prob.seq1, sem)
+    got = as_triples(engine.solve(prob.codes, prob.offsets))
+    ref = as_triples(search_cpu(prob, sem))
+    bad = np.nonzero((got != ref).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first #{bad[:5]}: got {got[bad[:5]]} ref {ref[bad[:5]]}"
+    return got
+
+
+def test_device_is_gfx950():
+    info = device_info(0)
+    assert info["arch"].startswith("gfx950"), info
+    assert info["wave"] == 64
+
+
+@pytest.mark.parametrize("i", [1, 2, 3, 4, 5, 6])
+def test_goldens(engine, i):
+    prob = Problem.read(input_path(i))
+    engine.set_problem(prob.weights, prob.seq1)
+    assert format_results(engine.solve(prob.codes, prob.offsets)) == expected(i)
+
+
+@pytest.mark.parametrize("shape,n", [("input6", 5000), ("input1", 700), ("input3", 40), ("input4", 300),
+                                     ("limits", 24)])
+@pytest.mark.parametrize("sem", [Semantics.REFERENCE, Semantics.SPEC])
+def test_random_shapes(engine, shape, n, sem):
+    check(engine, make_synthetic(shape, n, seed=n), sem)
+
+
+def test_mixed_packed_and_tiles(engine):
+    # one batch mixing packed records (offset range <= 64), tile records, equal length and L2 > L1
+    rng = np.random.default_rng(7)
+    s1 = "".join(chr(65 + x) for x in rng.integers(0, 26, 300))
+    recs = [s1, s1 + "A", s1[:250], s1[5:299], "A", "AB", s1[::3]]
+    recs += ["".join(chr(65 + x) for x in rng.integers(0, 26, rng.integers(1, 300))) for _ in range(200)]
+    prob = Problem.from_strings([5, 1, 2, 3], s1, recs)
+    for sem in (Semantics.REFERENCE, Semantics.SPEC):
+        check(engine, prob, sem)
+    got = as_triples(engine.solve(prob.codes, prob.offsets))
+    assert tuple(got[1]) == (-2**31, 0, 0)
+
+
+def test_small_brute_force(engine):
+    rng = np.random.default_rng(3)
+    for _ in range(20):
+        L1 = int(rng.integers(1, 90))
+        recs = ["".join(chr(65 + x) for x in rng.integers(0, 26, rng.integers(1, L1 + 3))) for _ in range(30)]
+        s1 = "".join(chr(65 + x) for x in rng.integers(0, 26, L1))
+        prob = Problem.from_strings(rng.integers(0, 12, 4), s1, recs)
+        engine.set_problem(prob.weights, prob.seq1)
+        got = as_triples(engine.solve(prob.codes, prob.offsets))
+        assert np.array_equal(got, as_triples(brute_force_native(prob)))
+
+
+def test_wide_keys(engine):
+    # large weights force the 64-bit hot-loop key path
+    prob = make_synthetic("limits", 12, seed=5)
+    prob.weights = type(prob.weights)(200000, 100, 300, 2)
+    check(engine, prob)
+
+
+def test_chunked_pipeline():
+    prob = make_synthetic("input6", 200_000, seed=11)
+    eng = HipSearchEngine(device=0, chunk_records=30_000, chunk_bytes=1 << 18)
+    check(eng, prob)
+    st = eng.stats()
+    assert st["chunks"] >= 7 and st["records"] == prob.n
+    eng.close()
+
+
+def test_device_resident_torch(engine):
+    prob = make_synthetic("input4", 64, seed=2)
+    engine.set_problem(prob.weights, prob.seq1)
+    dev = torch.device("cuda:0")
+    codes_t = torch.from_numpy(prob.codes).to(dev)
+    offs_t = torch.from_numpy(prob.offsets).to(dev)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        out = align_search_device(engine, codes_t, offs_t, prob.offsets, stream=s)
+    s.synchronize()
+    assert np.array_equal(out.cpu().numpy(), as_triples(search_cpu(prob)))
+
+
+@pytest.mark.parametrize("i", [3, 6])
+def test_final_cli_hip(i):
+    r = run_final(["--backend=hip"], stdin_path=input_path(i), np_=1)
+    assert r.returncode == 0, r.stderr.decode()
+    assert r.stdout.decode() == expected(i)
+
+
+@pytest.mark.parametrize("transport", ["shm", "mpi"])
+def test_final_cli_two_ranks_one_gpu(transport):
+    # two ranks share the single test GPU (RCCL needs distinct GPUs; shm/mpi transports do not)
+    r = run_final(["--backend=hip", f"--transport={transport}", "--device=0"], stdin_path=input_path(4), np_=2)
+    assert r.returncode == 0, r.stderr.decode()
+    assert r.stdout.decode() == expected(4)
+
+
+def test_final_cli_rccl_single_rank():
+    r = run_final(["--backend=hip", "--transport=rccl"], stdin_path=input_path(3), np_=1)
+    assert r.returncode == 0, r.stderr.decode()
+    assert r.stdout.decode() == expected(3)

@@ -1,0 +1,92 @@
+"""Score table, parser and formatter units (SURVEY.md §4.3 'unit')."""
+import numpy as np
+import pytest
+
+from mpi_openmp_cuda_amd import PairClass, Problem, format_results
+from mpi_openmp_cuda_amd.models.scoring import (FIRST_TYPE_GROUPS, SECOND_TYPE_GROUPS, alignment_string, class_table,
+                                                pair_class, score_table)
+from mpi_openmp_cuda_amd.ops.align import native_score_table
+from mpi_openmp_cuda_amd.utils.io import format_results_py
+
+
+def test_groups_match_spec():
+    assert len(FIRST_TYPE_GROUPS) == 9 and len(SECOND_TYPE_GROUPS) == 11
+    assert set(FIRST_TYPE_GROUPS) == {"NDEQ", "MILV", "FYW", "NEQK", "QHRK", "HY", "STA", "NHQK", "MILF"}
+
+
+@pytest.mark.parametrize("w", [(10, 2, 3, 4), (4, 3, 2, 10), (100, 2, 3, 4), (0, 0, 0, 0)])
+def test_native_table_matches_python(w):
+    assert np.array_equal(native_score_table(w), score_table(w))
+
+
+def test_table_symmetric_and_fully_initialised():
+    t = class_table()
+    assert np.array_equal(t, t.T)
+    assert set(np.unique(t)) <= {0, 1, 2, 3}
+    for a in range(1, 27):
+        assert t[a, a] == PairClass.DOLLAR
+    # padding rows/cols are "space" (bug B1: the reference left 416/729 entries uninitialised)
+    assert (t[0, :] == PairClass.SPACE).all() and (t[:, 27:] == PairClass.SPACE).all()
+
+
+def test_pdf_alignment_example():
+    # PDF p.2-3: APQRSBATAV vs ASQRSEAVSL, W = 10 2 3 4 -> 5*10 - 2*2 - 2*3 - 1*4 = 36
+    line = alignment_string("APQRSBATAV", "ASQRSEAVSL", 0, 0)
+    assert line == "$#$$$ $#%%"
+    assert pair_class("A", "S") == PairClass.PERCENT  # STA
+    assert pair_class("P", "S") == PairClass.HASH  # STPA
+
+
+def test_parser_crlf_lowercase_whitespace():
+    text = b"10 2 3 4\r\napqrsbatav\r\n  2\r\n asqreavsl \r\n\tHELLO\r\n"
+    p = Problem.parse(text)
+    assert p.weights.as_list() == [10, 2, 3, 4]
+    assert p.seq1_str() == "APQRSBATAV"
+    assert p.n == 2 and p.record(0) == "ASQREAVSL" and p.record(1) == "HELLO"
+
+
+def test_parser_large_parallel_path():
+    # > 64 KiB record area -> the two-pass OpenMP tokeniser; order must be input order
+    rng = np.random.default_rng(0)
+    recs = ["".join(chr(65 + x) for x in rng.integers(0, 26, rng.integers(1, 40))) for _ in range(5000)]
+    text = "1 2 3 4\nABCDEFGHIJKLMNOPQRSTUVWXYZ\n%d\n" % len(recs) + "\n".join(recs) + "\n"
+    p = Problem.parse(text)
+    assert p.n == len(recs)
+    assert all(p.record(i) == recs[i] for i in range(0, len(recs), 97))
+    assert p.record(len(recs) - 1) == recs[-1]
+
+
+@pytest.mark.parametrize("text,msg", [
+    (b"1 2 3\n", "W4"),
+    (b"1 2 3 4\nABC\n3\nAB\nCD\n", "expected 3"),
+    (b"1 2 3 4\nAB1C\n1\nAB\n", "non-letter"),
+    (b"1 2 3 4\nABC\n1\nA-B\n", "non-letter"),
+    (b"1 -2 3 4\nABC\n1\nAB\n", "out of range"),
+    (b"1 2 3 4\nABC\nx\n", "integer"),
+])
+def test_parser_errors(text, msg):
+    with pytest.raises(ValueError, match=msg):
+        Problem.parse(text)
+
+
+def test_strict_limits():
+    long1 = "A" * 3001
+    with pytest.raises(ValueError, match="limit"):
+        Problem.parse(f"1 1 1 1\n{long1}\n1\nA\n", strict_limits=True)
+    assert Problem.parse(f"1 1 1 1\n{long1}\n1\nA\n").L1 == 3001
+
+
+def test_extra_tokens_ignored():
+    p = Problem.parse(b"1 2 3 4\nABCD\n1\nAB\nEXTRA\n")
+    assert p.n == 1 and p.record(0) == "AB"
+
+
+def test_formatter_matches_python():
+    r = np.array([[1, 2, 3], [-2**31, 0, 0], [2**31 - 1, 2999, 1999]], dtype=np.int32)
+    assert format_results(r, first_index=7) == format_results_py(r, first_index=7)
+
+
+def test_roundtrip_text():
+    p = Problem.from_strings([4, 3, 2, 10], "ABCDEFGHIJKLMNOPQRSTUVWXYZ", ["ABCDEF", "MNOPQRSTXXX"])
+    q = Problem.parse(p.to_text())
+    assert np.array_equal(p.codes, q.codes) and np.array_equal(p.offsets, q.offsets)
