@@ -46,6 +46,10 @@ int moc_partition(const int64_t* lengths, int64_t n, int64_t L1, int parts, doub
 int moc_device_count(void);
 /* Page-locks [p, p+bytes) for direct DMA (hipHostRegister on the enclosing page range). */
 int moc_host_register(void* p, size_t bytes);
+/* Runs the DPP/shuffle self-test kernel; fills 192 ints (layout: align_kernels.hip dpp_probe_kernel). */
+int moc_dpp_probe(int32_t* out192);
+/* Transfer calibration: GB/s for kind 0 H2D, 1 D2H, 2 both, 3 zero-copy read, 4 zero-copy write, 5 D2D. */
+double moc_transfer_probe(int kind, size_t bytes, int iters);
 int moc_host_unregister(void* p);
 int moc_device_info_json(int device, char* buf, int64_t cap);
 void* moc_engine_create(int device, int64_t chunk_records, int64_t chunk_bytes, int pin_host);

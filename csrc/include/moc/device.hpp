@@ -60,6 +60,7 @@ struct Plan {
   const int32_t* long_recs = nullptr;  // device: records handled by the tile kernel
   int64_t n_long = 0;
   unsigned long long* keys = nullptr;  // device scratch, n_long entries (tile-kernel partial maxima)
+  int* debug = nullptr;                // optional per-lane dump of one tile (debug builds/tools only)
 };
 
 // Lanes a record needs in the packed kernel (offsets 0..L1-L2 incl. the helper diagonal).
@@ -68,6 +69,12 @@ inline int64_t lanes_needed(int64_t L1, int64_t L2) { return L2 <= L1 ? L1 - L2 
 // Launches packed + tile + finalize kernels for one batch on `stream`; results -> out[0..n).
 void launch_search(const ProblemView& pv, const BatchView& bv, const Plan& plan, Result* out,
                    hipStream_t stream);
+
+// One-wave self-test of the DPP / shuffle primitives (192 ints, see align_kernels.hip).
+void launch_dpp_probe(int* d_out, hipStream_t stream);
+
+// Transfer calibration in GB/s (kinds: transfer_probe.hip). Allocates/frees its own buffers.
+double transfer_probe(int kind, size_t bytes, int iters);
 
 }  // namespace dev
 }  // namespace moc

@@ -136,6 +136,23 @@ int moc_partition(const int64_t* lengths, int64_t n, int64_t L1, int parts, doub
 
 int moc_device_count(void) { return moc::device_count(); }
 
+int moc_dpp_probe(int32_t* out192) {
+  return guard([&] {
+    int* d = nullptr;
+    MOC_HIP_CHECK(hipMalloc(&d, 192 * sizeof(int)));
+    moc::dev::launch_dpp_probe(d, nullptr);
+    MOC_HIP_CHECK(hipGetLastError());
+    MOC_HIP_CHECK(hipMemcpy(out192, d, 192 * sizeof(int), hipMemcpyDeviceToHost));
+    MOC_HIP_CHECK(hipFree(d));
+  });
+}
+
+double moc_transfer_probe(int kind, size_t bytes, int iters) {
+  double gbs = -1;
+  guard([&] { gbs = moc::dev::transfer_probe(kind, bytes, iters); });
+  return gbs;
+}
+
 int moc_host_register(void* p, size_t bytes) {
   return guard([&] {
     const uintptr_t page = 4096;

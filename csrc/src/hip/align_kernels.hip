@@ -21,8 +21,14 @@ namespace {
 constexpr int kLutInts = kLutStride * kLutStride;  // 1024
 constexpr int kDppWaveShl1 = 0x130;                // lane i <- lane i+1 (lane 63: bound)
 
+// The result goes through an empty asm so the backend's DPP combiner cannot fold the move into the
+// consuming VALU op: on gfx950 / ROCm 7.2 the folded `v_subrev_u32_dpp vD, vP, vP wave_shl:1` computed
+// P(lane+1) - P(lane) instead of P(lane) - P(lane+1) (measured with tools/debug_tiles.py: every
+// tile-kernel candidate came out with the sign of d flipped). One extra v_mov_dpp per cell.
 __device__ __forceinline__ int wave_shl1(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, kDppWaveShl1, 0xf, 0xf, true);
+  int r = __builtin_amdgcn_update_dpp(0, v, kDppWaveShl1, 0xf, 0xf, true);
+  asm volatile("" : "+v"(r));
+  return r;
 }
 // Same shift, but lane 63 receives `fill` instead of 0.
 __device__ __forceinline__ int wave_shl1_fill(int v, int fill) {
@@ -200,7 +206,7 @@ __global__ __launch_bounds__(256) void packed_search_kernel(ProblemView pv, Batc
 template <bool Wide, bool Seq1Lds>
 __global__ __launch_bounds__(256) void tile_search_kernel(ProblemView pv, BatchView bv, const Tile* __restrict__ tiles,
                                                           int64_t n_tiles, const int32_t* __restrict__ long_recs,
-                                                          unsigned long long* __restrict__ keys) {
+                                                          unsigned long long* __restrict__ keys, int* debug) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   int* lut = reinterpret_cast<int*>(smem);
   uint8_t* s1l = smem + kLutInts * sizeof(int);
@@ -245,6 +251,20 @@ __global__ __launch_bounds__(256) void tile_search_kernel(ProblemView pv, BatchV
   const int Pn = wave_shl1(P);
   const bool own = lane < kTileOffsets && o <= L1 - L2;
   unsigned long long key = lane_candidate<Wide>(own, o, L1, L2, pv.semantics, P, Pn, best, shift, mask);
+  if (debug && wave == debug[0]) {
+    debug[64 + lane * 4 + 0] = P;
+    debug[64 + lane * 4 + 1] = static_cast<int>(best);
+    debug[64 + lane * 4 + 2] = Pn;
+    debug[64 + lane * 4 + 3] = x;
+    if (lane == 0) {
+      debug[1] = L2;
+      debug[2] = o0;
+      debug[3] = r;
+      for (int i = 0; i < 8 && i < L2; ++i) debug[8 + i] = rec[i];
+      debug[16] = static_cast<int>(key >> 32);
+      debug[17] = static_cast<int>(key);
+    }
+  }
   key = wave_max_u64(key);
   if (lane == 0 && key != 0ull) atomicMax(keys + li, key);
 }
@@ -257,6 +277,21 @@ __global__ void finalize_long_kernel(BatchView bv, const int32_t* __restrict__ l
   const int r = long_recs[i];
   const int L2 = static_cast<int>(bv.offsets[r + 1] - bv.offsets[r]);
   out[r] = decode_key(keys[i], L2);
+}
+
+// Self-test of the cross-lane primitives the search kernels rely on (one wave):
+//   out[0..63]   = wave_shl1(lane)           expected lane+1, lane 63 -> 0
+//   out[64..127] = wave_shl1_fill(lane, 777) expected lane+1, lane 63 -> 777
+//   out[128..191]= wave_max_i32(lane*7 % 61)  expected 60 everywhere
+__global__ void dpp_probe_kernel(int* out) {
+  const int lane = threadIdx.x & 63;
+  out[lane] = wave_shl1(lane);
+  out[64 + lane] = wave_shl1_fill(lane, 777);
+  out[128 + lane] = wave_max_i32((lane * 7) % 61);
+}
+
+void launch_dpp_probe(int* d_out, hipStream_t stream) {
+  hipLaunchKernelGGL(dpp_probe_kernel, dim3(1), dim3(64), 0, stream, d_out);
 }
 
 // =====================================================================================================
@@ -282,10 +317,10 @@ void launch_all(const ProblemView& pv, const BatchView& bv, const Plan& plan, Re
     const int64_t blocks = (plan.n_tiles * 64 + kBlock - 1) / kBlock;
     if (s1_in_lds)
       hipLaunchKernelGGL((tile_search_kernel<Wide, true>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock),
-                         lds_lut + lds_s1, stream, pv, bv, plan.tiles, plan.n_tiles, plan.long_recs, plan.keys);
+                         lds_lut + lds_s1, stream, pv, bv, plan.tiles, plan.n_tiles, plan.long_recs, plan.keys, plan.debug);
     else
       hipLaunchKernelGGL((tile_search_kernel<Wide, false>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock),
-                         lds_lut, stream, pv, bv, plan.tiles, plan.n_tiles, plan.long_recs, plan.keys);
+                         lds_lut, stream, pv, bv, plan.tiles, plan.n_tiles, plan.long_recs, plan.keys, plan.debug);
     const int64_t fb = (plan.n_long + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(finalize_long_kernel, dim3(static_cast<unsigned>(fb)), dim3(kBlock), 0, stream, bv,
                        plan.long_recs, plan.keys, plan.n_long, out);

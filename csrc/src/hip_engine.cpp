@@ -1,6 +1,8 @@
 #include "moc/hip_engine.hpp"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "moc/problem.hpp"
@@ -25,7 +27,8 @@ namespace {
 class PinGuard {
  public:
   PinGuard(const void* p, size_t bytes) {
-    if (!p || bytes == 0) return;
+    // Small buffers may share pages with unrelated allocations: leave them pageable (HIP stages them).
+    if (!p || bytes < (size_t{64} << 20)) return;
     hipPointerAttribute_t attr;
     if (hipPointerGetAttributes(&attr, p) == hipSuccess && attr.type != hipMemoryTypeUnregistered) return;
     (void)hipGetLastError();
@@ -269,8 +272,28 @@ void HipEngine::solve(const uint8_t* codes, const int64_t* offsets, int64_t n, R
     plan.long_recs = reinterpret_cast<const int32_t*>(static_cast<char*>(s.d_plan) + lay.long_off);
     plan.keys = reinterpret_cast<unsigned long long*>(static_cast<char*>(s.d_plan) + lay.keys_off);
     dev::BatchView bv{static_cast<const uint8_t*>(s.d_codes), static_cast<const int64_t*>(s.d_offsets), cn};
+    int* d_dbg = nullptr;
+    const char* dbg_env = std::getenv("MOC_DEBUG_TILE");
+    if (dbg_env) {
+      MOC_HIP_CHECK(hipMalloc(&d_dbg, 4096));
+      std::vector<int> init(1024, 0);
+      init[0] = std::atoi(dbg_env);
+      MOC_HIP_CHECK(hipMemcpy(d_dbg, init.data(), 4096, hipMemcpyHostToDevice));
+      plan.debug = d_dbg;
+    }
     MOC_HIP_CHECK(hipEventRecord(s.ev_k0, s_compute_));
     dev::launch_search(problem_view(hp.max_l2), bv, plan, static_cast<Result*>(s.d_out), s_compute_);
+    if (d_dbg) {
+      std::vector<int> h(1024);
+      MOC_HIP_CHECK(hipStreamSynchronize(s_compute_));
+      MOC_HIP_CHECK(hipMemcpy(h.data(), d_dbg, 4096, hipMemcpyDeviceToHost));
+      std::fprintf(stderr, "DBG tile=%d L2=%d o0=%d r=%d codes=%d,%d,%d,%d,%d,%d,%d,%d key0=%08x%08x\n", h[0], h[1], h[2],
+                   h[3], h[8], h[9], h[10], h[11], h[12], h[13], h[14], h[15], h[16], h[17]);
+      for (int l = 0; l < 64; ++l)
+        std::fprintf(stderr, "DBG lane %d P=%d best=%d Pn=%d x=%d\n", l, h[64 + 4 * l], h[65 + 4 * l], h[66 + 4 * l],
+                     h[67 + 4 * l]);
+      (void)hipFree(d_dbg);
+    }
     MOC_HIP_CHECK(hipGetLastError());
     MOC_HIP_CHECK(hipEventRecord(s.ev_k1, s_compute_));
     // ---- return stream: D2H straight into the caller's result array

@@ -44,6 +44,8 @@ def _decl(lib):
         "moc_device_count": (c_int, []),
         "moc_host_register": (c_int, [c_void_p, c_size_t]),
         "moc_host_unregister": (c_int, [c_void_p]),
+        "moc_dpp_probe": (c_int, [c_void_p]),
+        "moc_transfer_probe": (c_double, [c_int, c_size_t, c_int]),
         "moc_device_info_json": (c_int, [c_int, c_char_p, c_int64]),
         "moc_engine_create": (c_void_p, [c_int, c_int64, c_int64, c_int]),
         "moc_engine_destroy": (None, [c_void_p]),

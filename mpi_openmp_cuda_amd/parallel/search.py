@@ -1,0 +1,159 @@
+"""Distributed search over a torch.distributed process group (Python twin of csrc/apps/final.cpp).
+
+Reference flow (main.c:110-197): root reads, Bcast x4, Scatter fixed-stride records, per-rank GPU work,
+Gather x3, root prints. Here:
+  * header (weights, |Seq1|, N, semantics) + Seq1: exact-count broadcasts through the process group
+    (RCCL on GPU ranks, gloo on CPU ranks);
+  * cost-balanced contiguous bounds (parallel/partition.py), valid for any world size;
+  * transport "shm": the root writes the CSR batch once into a node-shared /dev/shm window; every rank
+    DMAs its own slice to its GPU and writes its results back in place — no payload collectives at all
+    (single node);
+  * transport "p2p": root sends every rank its slice (lengths + letters) with point-to-point
+    send/recv over the process group (RCCL over xGMI / network on GPUs) and receives the results back.
+"""
+from __future__ import annotations
+
+import os
+import uuid
+from typing import Optional
+
+import numpy as np
+
+from .. import _lib
+from ..models.problem import Problem
+from ..models.scoring import Semantics
+from ..ops.align import HipSearchEngine, device_count, empty_results, search_cpu
+from ..utils.timer import PhaseTimer
+from . import dist as D
+from .partition import CPU_COST, GPU_COST, partition
+
+
+class NodeWindow:
+    """A /dev/shm file mapped by every rank of the node: offsets[N+1] | results[N] | codes[T]."""
+
+    def __init__(self, name: str, n: int, total: int, create: bool):
+        self.path = f"/dev/shm/{name}"
+        self.n, self.total = n, total
+        self.off_bytes = 8 * (n + 1)
+        self.res_bytes = (12 * n + 7) & ~7
+        size = max(self.off_bytes + self.res_bytes + total, 8)
+        mode = "w+" if create else "r+"
+        self._mm = np.memmap(self.path, dtype=np.uint8, mode=mode, shape=(size,))
+        self.offsets = self._mm[:self.off_bytes].view(np.int64)
+        self.results = self._mm[self.off_bytes:self.off_bytes + 12 * n].view(_lib.RESULT_DTYPE)
+        self.codes = self._mm[self.off_bytes + self.res_bytes:self.off_bytes + self.res_bytes + total]
+
+    def close(self, unlink: bool):
+        self._mm._mmap.close() if getattr(self._mm, "_mmap", None) is not None else None
+        if unlink:
+            try:
+                os.unlink(self.path)
+            except OSError:
+                pass
+
+
+class DistributedSearch:
+    def __init__(self, ctx: D.DistContext, backend: str = "auto", transport: str = "auto", threads: int = 0,
+                 device: Optional[int] = None):
+        self.ctx = ctx
+        if backend == "auto":
+            backend = "hip" if device_count() > 0 else "cpu"
+        self.backend = backend
+        if transport == "auto":
+            transport = "shm" if ctx.single_node else "p2p"
+        if transport == "shm" and not ctx.single_node:
+            raise ValueError("transport=shm needs every rank on one node")
+        self.transport = transport
+        self.threads = threads
+        self.engine = HipSearchEngine(ctx.local_rank if device is None else device) if backend == "hip" else None
+        self.timer = PhaseTimer()
+
+    def _compute(self, prob: Problem, sem: Semantics, codes, offsets, out):
+        if self.engine is not None:
+            self.engine.solve(codes, offsets, out=out)
+        else:
+            sub = Problem(prob.weights, prob.seq1, codes[offsets[0]:offsets[-1]], offsets - offsets[0])
+            out[:] = search_cpu(sub, sem, self.threads)
+
+    def run(self, problem: Optional[Problem], semantics=Semantics.REFERENCE) -> Optional[np.ndarray]:
+        ctx, T = self.ctx, self.timer
+        sem = Semantics.parse(semantics)
+        with T.phase("bcast"):
+            if ctx.is_root:
+                hdr = np.array(problem.weights.as_list() + [problem.L1, problem.n, problem.total_chars, int(sem)],
+                               np.int64)
+            else:
+                hdr = None
+            hdr = D.bcast_array(ctx, hdr, 8, np.int64)
+            w, L1, n, total, sem = list(hdr[:4]), int(hdr[4]), int(hdr[5]), int(hdr[6]), Semantics(int(hdr[7]))
+            seq1 = D.bcast_array(ctx, problem.seq1 if ctx.is_root else None, L1, np.uint8)
+            prob = Problem(w, seq1)
+            if self.engine is not None:
+                self.engine.set_problem(w, seq1, sem)
+            bounds = partition(problem.lengths, L1, ctx.world, GPU_COST if self.backend == "hip" else CPU_COST) \
+                if ctx.is_root else None
+            bounds = D.bcast_array(ctx, bounds, ctx.world + 1, np.int64)
+        b, e = int(bounds[ctx.rank]), int(bounds[ctx.rank + 1])
+        if self.transport == "shm":
+            return self._run_shm(problem, prob, sem, n, total, b, e)
+        return self._run_p2p(problem, prob, sem, n, bounds, b, e)
+
+    def _run_shm(self, problem, prob, sem, n, total, b, e):
+        ctx, T = self.ctx, self.timer
+        with T.phase("distribute"):
+            name_arr = None
+            if ctx.is_root:  # fixed 20-byte name: "moc_win_" + 12 hex digits
+                name_arr = np.frombuffer(f"moc_win_{uuid.uuid4().hex[:12]}".encode(), np.uint8)
+            name = bytes(D.bcast_array(ctx, name_arr, 20, np.uint8)).decode()
+            win = None
+            if ctx.is_root:
+                win = NodeWindow(name, n, total, create=True)
+                win.offsets[:] = problem.offsets
+                win.codes[:] = problem.codes
+                win._mm.flush()
+            D.barrier(ctx)
+            if not ctx.is_root:
+                win = NodeWindow(name, n, total, create=False)
+        with T.phase("compute"):
+            if e > b:
+                self._compute(prob, sem, win.codes, win.offsets[b:e + 1], win.results[b:e])
+        with T.phase("gather"):
+            D.barrier(ctx)
+            out = np.array(win.results) if ctx.is_root else None
+            D.barrier(ctx)
+            win.close(unlink=ctx.is_root)
+        return out
+
+    def _run_p2p(self, problem, prob, sem, n, bounds, b, e):
+        ctx, T = self.ctx, self.timer
+        with T.phase("distribute"):
+            if ctx.is_root:
+                lengths = problem.lengths
+                for r in range(1, ctx.world):
+                    rb, re = int(bounds[r]), int(bounds[r + 1])
+                    if re > rb:
+                        D.send_array(ctx, lengths[rb:re], r)
+                        D.send_array(ctx, problem.codes[problem.offsets[rb]:problem.offsets[re]], r)
+                my_offsets = problem.offsets[b:e + 1] - problem.offsets[b]
+                my_codes = problem.codes[problem.offsets[b]:problem.offsets[e]]
+            else:
+                my_len = D.recv_array(ctx, e - b, np.int64, 0)
+                my_offsets = np.zeros(e - b + 1, np.int64)
+                np.cumsum(my_len, out=my_offsets[1:])
+                my_codes = D.recv_array(ctx, int(my_offsets[-1]), np.uint8, 0)
+        with T.phase("compute"):
+            mine = empty_results(e - b)
+            if e > b:
+                self._compute(prob, sem, my_codes, my_offsets, mine)
+        with T.phase("gather"):
+            if ctx.is_root:
+                out = empty_results(n)
+                out[b:e] = mine
+                for r in range(1, ctx.world):
+                    rb, re = int(bounds[r]), int(bounds[r + 1])
+                    if re > rb:
+                        out[rb:re] = D.recv_array(ctx, 3 * (re - rb), np.int32, r).view(_lib.RESULT_DTYPE)
+                return out
+            if e > b:
+                D.send_array(ctx, mine.view(np.int32), 0)
+            return None

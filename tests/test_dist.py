@@ -1,0 +1,43 @@
+"""Multi-process torch.distributed path on CPU (gloo, world_size 2-3): the Python twin of ./final
+(parallel/search.py) must reproduce the goldens with both transports, for any world size."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT, expected, input_path
+
+_port = [29700]
+
+
+def torchrun(nproc, args, timeout=180):
+    _port[0] += 1
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={_port[0]}", "-m", "mpi_openmp_cuda_amd"] + args
+    return subprocess.run(cmd, capture_output=True, timeout=timeout, env=env, cwd="/tmp")
+
+
+@pytest.mark.parametrize("transport", ["shm", "p2p"])
+@pytest.mark.parametrize("i,nproc", [(3, 2), (6, 3), (2, 2)])
+def test_gloo_goldens(transport, i, nproc):
+    r = torchrun(nproc, ["--backend=cpu", "--dist-backend=gloo", f"--transport={transport}",
+                         f"--input={input_path(i)}"])
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    assert r.stdout.decode() == expected(i)
+
+
+def test_single_process_cli_stdin():
+    with open(input_path(1), "rb") as f:
+        r = subprocess.run([sys.executable, "-m", "mpi_openmp_cuda_amd", "--backend=cpu"], stdin=f,
+                           capture_output=True, env=dict(os.environ, PYTHONPATH=ROOT), cwd="/tmp", timeout=120)
+    assert r.returncode == 0 and r.stdout.decode() == expected(1)
+
+
+def test_input_error_all_ranks_exit():
+    bad = os.path.join("/tmp", "moc_bad_input.txt")
+    with open(bad, "w") as f:
+        f.write("1 2 3 4\nAB1\n1\nA\n")
+    r = torchrun(2, ["--backend=cpu", "--dist-backend=gloo", f"--input={bad}"], timeout=120)
+    assert r.returncode != 0 and b"non-letter" in r.stderr

@@ -33,6 +33,17 @@ def check(engine, prob, sem=Semantics.REFERENCE):
     return got
 
 
+def test_dpp_primitives():
+    # the kernels rely on DPP wave_shl:1 = "lane i reads lane i+1", lane 63 bound (0 or fill value)
+    from mpi_openmp_cuda_amd import _lib
+
+    out = np.zeros(192, np.int32)
+    _lib.check(_lib.lib().moc_dpp_probe(_lib.ptr(out)))
+    assert out[:63].tolist() == list(range(1, 64)) and out[63] == 0
+    assert out[64:127].tolist() == list(range(1, 64)) and out[127] == 777
+    assert (out[128:] == 60).all()
+
+
 def test_device_is_gfx950():
     info = device_info(0)
     assert info["arch"].startswith("gfx950"), info

@@ -1,0 +1,13 @@
+"""Prints host<->device transfer ceilings (GB/s) measured by the native probe (transfer_probe.hip)."""
+import json
+import sys
+
+sys.path.insert(0, ".")
+from mpi_openmp_cuda_amd import _lib  # noqa: E402
+
+names = ["h2d_memcpy", "d2h_memcpy", "h2d+d2h_concurrent", "zero_copy_read", "zero_copy_write", "d2d_memcpy"]
+res = {}
+for mb in (16, 256):
+    for kind, name in enumerate(names):
+        res[f"{name}_{mb}MB"] = round(_lib.lib().moc_transfer_probe(kind, mb << 20, 10 if mb == 16 else 4), 2)
+print(json.dumps(res, indent=1))
