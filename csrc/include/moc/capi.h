@@ -52,14 +52,21 @@ int moc_dpp_probe(int32_t* out192);
 double moc_transfer_probe(int kind, size_t bytes, int iters);
 int moc_host_unregister(void* p);
 int moc_device_info_json(int device, char* buf, int64_t cap);
-void* moc_engine_create(int device, int64_t chunk_records, int64_t chunk_bytes, int pin_host);
+void* moc_engine_create(int device, int64_t chunk_records, int64_t chunk_bytes, int allow_direct);
 void moc_engine_destroy(void* e);
 int moc_engine_set_problem(void* e, const int32_t* weights4, const uint8_t* seq1, int64_t L1, int semantics);
 int moc_engine_solve(void* e, const uint8_t* codes, const int64_t* offsets, int64_t n, moc_result* out);
+/* fmt: 0 = R12 (moc_result), 1 = R8 {i32,u16,u16}, 2 = R4 {i16,u8,u8}; lengths8 / min_l2 / max_l2 optional
+ * (NULL / -1). Pinned host buffers + short records -> zero-copy streaming kernel. */
+int moc_engine_solve_ex(void* e, const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths8, int64_t n,
+                        void* out, int fmt, int64_t min_l2, int64_t max_l2);
+int moc_engine_auto_format(void* e, int64_t max_l2);
+int moc_engine_pin(void* e, const void* p, size_t bytes);
+int moc_expand_results(const void* in, int fmt, int64_t n, moc_result* out);
 int moc_engine_solve_device(void* e, const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets,
                             int64_t n, moc_result* d_out, void* stream);
-/* stats: kernel_ms, total_ms, h2d_bytes, d2h_bytes, chunks, cells, records */
-int moc_engine_stats(void* e, double* out7);
+/* stats: kernel_ms, total_ms, h2d_bytes, d2h_bytes, chunks, cells, records, direct, format */
+int moc_engine_stats(void* e, double* out9);
 
 #ifdef __cplusplus
 }

@@ -7,9 +7,12 @@
 // Here: one launch per *batch*. Parallelism is over offsets (diagonals): every lane owns one offset
 // `o` and streams over the Seq2 positions, keeping its running diagonal prefix sum P_o in a register;
 // the neighbour diagonal's P_{o+1} comes from lane+1 through a DPP wave shift, so a cell costs one LDS
-// LUT gather plus a handful of VALU ops and no atomics/barriers (design: SURVEY.md §7.3).
-//   * packed kernel: records whose offset range fits in a wave (L1-L2+1 <= 64 lanes) are packed
-//     several per wave in fixed-width lane slots (the input6-shaped regime);
+// gather plus a handful of VALU ops, and no atomics or barriers (design: SURVEY.md §7.3).
+//   * short kernel: records whose offset range fits in a wave (L1-L2+1 <= 64 lanes) are packed
+//     several per wave in fixed-width lane slots (the input6-shaped regime). Persistent blocks pull
+//     tiles of ~1K records, stage their letters in LDS with 16-byte loads — straight from pinned host
+//     memory when the batch lives there (zero-copy streaming: PCIe is the bound, so no staging copy) —
+//     and score against a per-block LDS profile S[c][j] = T[c][Seq1[j]].
 //   * tile kernel: longer offset ranges are cut into 63-offset tiles (lane 63 is the helper diagonal)
 //     listed by the host planner; partial maxima merge through one 64-bit atomicMax per wave on an
 //     order-free packed key (score, -(o*L2+k)) — deterministic tie-break, no races (fixes B9).
@@ -22,6 +25,25 @@
 #include "moc/common.hpp"
 
 namespace moc {
+
+// Result wire formats (device -> host). R12 is moc::Result; R8/R4 are chosen automatically when the
+// problem's bounds fit, to cut the D2H bytes per record by 1.5x / 3x.
+enum class ResultFormat : int32_t { R12 = 0, R8 = 1, R4 = 2 };
+struct R8 {
+  int32_t score;
+  uint16_t n, k;
+};
+struct R4 {
+  int16_t score;  // INT16_MIN encodes "no candidate" (INT_MIN)
+  uint8_t n, k;
+};
+static_assert(sizeof(R8) == 8 && sizeof(R4) == 4, "packed result formats");
+inline int result_bytes(ResultFormat f) { return f == ResultFormat::R12 ? 12 : f == ResultFormat::R8 ? 8 : 4; }
+// Smallest format able to hold every result of a problem with these bounds.
+ResultFormat pick_result_format(int64_t L1, int64_t max_l2, int32_t max_abs_weight);
+// Expands packed results to moc::Result (host side).
+void expand_results(const void* in, ResultFormat f, int64_t n, Result* out);
+
 namespace dev {
 
 constexpr int kWave = 64;
@@ -51,24 +73,45 @@ struct Tile {
   int32_t o0;
 };
 
-// Host-built launch plan for one batch (see planner in hip_engine.cpp).
+// Host-built plan for the tile kernel of one batch.
 struct Plan {
-  int32_t slot = 0;           // lanes per record in the packed kernel (0 = no packed records)
-  int32_t rec_per_wave = 0;   // floor(64 / slot)
-  int64_t n_tiles = 0;        // tile-kernel work items
-  const Tile* tiles = nullptr;      // device: (long-record index, first offset) per tile
+  int64_t n_tiles = 0;                 // tile-kernel work items
+  const Tile* tiles = nullptr;         // device: (long-record index, first offset) per tile
   const int32_t* long_recs = nullptr;  // device: records handled by the tile kernel
   int64_t n_long = 0;
   unsigned long long* keys = nullptr;  // device scratch, n_long entries (tile-kernel partial maxima)
-  int* debug = nullptr;                // optional per-lane dump of one tile (debug builds/tools only)
 };
 
-// Lanes a record needs in the packed kernel (offsets 0..L1-L2 incl. the helper diagonal).
+// Arguments of the short-record kernel. All pointers must be device-accessible: device memory, or
+// pinned host memory (hipHostMalloc / hipHostRegister) for zero-copy streaming.
+struct ShortArgs {
+  const uint8_t* codes = nullptr;     // base pointer: record i starts at codes + offsets[i]
+  const int64_t* offsets = nullptr;   // n+1 absolute offsets
+  const uint8_t* lengths8 = nullptr;  // optional narrow lengths (saves 7 B/record of reads)
+  int64_t n = 0;
+  void* out = nullptr;                // results, format `fmt`, record i at index i
+  int32_t fmt = 0;                    // ResultFormat
+  int32_t slot = 0;                   // lanes per record (max lanes_needed over the batch, <= 64)
+  int32_t rpw = 0;                    // records per wave = 64 / slot
+  int32_t tile_records = 0;           // records per block tile
+  int32_t codes_cap = 0;              // LDS bytes for one tile's letters (>= tile_records*max_l2+32)
+  int32_t max_l2 = 0;
+  unsigned* counter = nullptr;        // device work counter, zeroed before each launch
+};
+
+// Lanes a record needs in the short kernel (offsets 0..L1-L2 incl. the helper diagonal).
 inline int64_t lanes_needed(int64_t L1, int64_t L2) { return L2 <= L1 ? L1 - L2 + 1 : 1; }
 
-// Launches packed + tile + finalize kernels for one batch on `stream`; results -> out[0..n).
-void launch_search(const ProblemView& pv, const BatchView& bv, const Plan& plan, Result* out,
-                   hipStream_t stream);
+// Configures tile size / LDS budget for the short kernel; returns false when the batch cannot run in
+// it (a record needs more than 64 lanes). Fills slot/rpw/tile_records/codes_cap.
+bool configure_short(int64_t L1, int64_t min_l2, int64_t max_l2, ShortArgs& a);
+
+// Short-record kernel (all records with lanes_needed <= a.slot are processed; others are skipped).
+void launch_short(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStream_t stream);
+
+// Tile kernel + finalize for the long records listed in `plan`; results -> out (format fmt).
+void launch_tiles(const ProblemView& pv, const BatchView& bv, const Plan& plan, void* out, int fmt,
+                  hipStream_t stream);
 
 // One-wave self-test of the DPP / shuffle primitives (192 ints, see align_kernels.hip).
 void launch_dpp_probe(int* d_out, hipStream_t stream);

@@ -1,16 +1,21 @@
-// Per-rank GPU engine: problem upload, launch planning, and the chunked host<->device pipeline.
+// Per-rank GPU engine: problem upload, launch planning, and host<->device data movement.
 //
 // Reference: send_divided_Seq2_To_Cuda (cudaFunctions.cu:178-242) — cudaMalloc per call and per
 // record (leaking all but the last dev_count_signs), a blocking H2D of the whole fixed-stride chunk,
 // one launch + cudaDeviceSynchronize per record, three blocking D2H copies, and the problem state in
 // __constant__ symbols uploaded by four separate calls (cudaFunctions.cu:35-61).
 //
-// Here: pooled device buffers (grown, never freed per call), the problem (LUT + Seq1) uploaded once,
-// and a double-buffered 3-stream pipeline per chunk of records:
-//     copy stream:    H2D codes/offsets/plan of chunk c+1
-//     compute stream: packed + tile kernels of chunk c
-//     return stream:  D2H results of chunk c-1 straight into the caller's (pinned) result array
-// ordered by events only — no device-wide synchronisation inside the loop.
+// Here two data paths, chosen per call:
+//   * direct (zero-copy streaming): when the batch lives in pinned host memory (hipHostMalloc /
+//     hipHostRegister — e.g. the node-shared input window) and every record fits the short kernel, ONE
+//     persistent kernel reads the letters straight over PCIe into LDS and writes packed results straight
+//     back. Measured on MI355X: kernel reads of pinned host memory run at the hipMemcpy rate
+//     (~56-57 GB/s, tools/probe_transfers.py), so staging copies would only add a second pass.
+//   * staged pipeline: pooled device buffers (grown, never freed per call) and a double-buffered
+//     3-stream chunk pipeline — copy stream H2D chunk c+1 | compute stream kernels of chunk c | return
+//     stream D2H of chunk c-1 — ordered by events only. Used for pageable memory and for batches with
+//     long records (tile kernel + host-planned tile lists).
+// Results are written in the smallest wire format that fits the problem (R4/R8/R12, moc/device.hpp).
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -26,16 +31,25 @@
 namespace moc {
 
 struct EngineOptions {
-  int device = -1;                     // -1: keep the current device
-  int64_t chunk_records = 1 << 21;     // max records per pipeline chunk
-  int64_t chunk_bytes = 64ll << 20;    // max letter bytes per pipeline chunk
-  bool pin_host = true;                // hipHostRegister caller buffers for direct DMA
+  int device = -1;                   // -1: keep the current device
+  int64_t chunk_records = 1 << 21;   // staged pipeline: max records per chunk
+  int64_t chunk_bytes = 64ll << 20;  // staged pipeline: max letter bytes per chunk
+  bool allow_direct = true;          // use zero-copy streaming when the host buffers are pinned
 };
 
 struct EngineStats {
-  double kernel_ms = 0;  // sum of compute-stream time (events), last solve
+  double kernel_ms = 0;  // device time of the search kernels (events), last solve
   double total_ms = 0;   // wall time of the last solve call
   int64_t h2d_bytes = 0, d2h_bytes = 0, chunks = 0, cells = 0, records = 0;
+  int32_t direct = 0;    // 1 if the last solve used the zero-copy streaming path
+  int32_t format = 0;    // ResultFormat of the last solve
+};
+
+// Optional metadata about a batch (e.g. known from parsing / generation) that lets the engine skip its
+// own scan over the lengths.
+struct BatchHints {
+  int64_t min_l2 = -1;
+  int64_t max_l2 = -1;
 };
 
 class HipEngine {
@@ -49,34 +63,48 @@ class HipEngine {
   // Same, with Seq1 already on this device (e.g. delivered by an RCCL broadcast).
   void set_problem_device(const Weights& w, const uint8_t* d_seq1, int64_t L1, Semantics sem);
 
-  // Host CSR in -> host results out (the pipeline). `offsets` are absolute (n+1 entries).
+  // Host batch in -> host results out as moc::Result. `codes` is the base pointer (record i starts at
+  // codes + offsets[i]); `offsets` has n+1 absolute entries.
   void solve(const uint8_t* codes, const int64_t* offsets, int64_t n, Result* out);
+  // General form: optional uint8 lengths (max L2 <= 255), results in `fmt`.
+  void solve_ex(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths8, int64_t n, void* out,
+                ResultFormat fmt, const BatchHints& hints = {});
+  // Smallest result format for this problem given the batch's longest record.
+  ResultFormat auto_format(int64_t max_l2) const;
 
   // Device-resident batch: d_codes/d_offsets/d_out on this device; h_offsets is a host copy of the
   // offsets used for planning. Work is queued on `stream` (0 = engine compute stream); no sync.
   void solve_device(const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets, int64_t n,
                     Result* d_out, hipStream_t stream);
 
+  // Page-locks a host range for the lifetime of the engine (or until unpin); enables the direct path.
+  void pin(const void* p, size_t bytes);
+  void unpin_all();
+
   const EngineStats& stats() const { return stats_; }
   int device() const { return device_; }
   hipStream_t compute_stream() const { return s_compute_; }
   int64_t L1() const { return L1_; }
+  int num_cus() const { return num_cus_; }
 
  private:
   struct Slot;  // one double-buffer half
-  struct HostPlan {
-    int32_t slot = 0, rpw = 0;
+  struct ChunkPlan {
+    int64_t min_short = 0, max_l2 = 0, n_short = 0, cells = 0;
     std::vector<dev::Tile> tiles;
     std::vector<int32_t> long_recs;
-    int64_t max_l2 = 0, cells = 0;
   };
-  void plan_chunk(const int64_t* offsets, int64_t n, HostPlan& hp) const;
+  void plan_chunk(const int64_t* offsets, int64_t n, ChunkPlan& cp) const;
   dev::ProblemView problem_view(int64_t max_l2) const;
   void ensure(void*& ptr, size_t& cap, size_t bytes);
   void ensure_host(void*& ptr, size_t& cap, size_t bytes);
+  bool direct_pointers(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths8, int64_t n, void* out,
+                       int fb, dev::ShortArgs& a) const;
+  void run_staged(const uint8_t* codes, const int64_t* offsets, int64_t n, void* out, ResultFormat fmt);
 
   EngineOptions opt_;
   int device_ = 0;
+  int num_cus_ = 256;
   hipStream_t s_copy_ = nullptr, s_compute_ = nullptr, s_return_ = nullptr;
   // problem
   ScoreTable table_{};
@@ -86,12 +114,15 @@ class HipEngine {
   Semantics sem_ = Semantics::Reference;
   bool have_problem_ = false;
   std::vector<std::unique_ptr<Slot>> slots_;
+  unsigned* d_counter_ = nullptr;  // direct-path work counter
+  hipEvent_t ev_a_ = nullptr, ev_b_ = nullptr;
   // scratch for solve_device
   void* d_plan_ = nullptr;
   size_t d_plan_cap_ = 0;
   void* h_plan_ = nullptr;
   size_t h_plan_cap_ = 0;
   hipEvent_t ev_plan_ = nullptr;
+  std::vector<void*> pinned_;
   EngineStats stats_;
 };
 

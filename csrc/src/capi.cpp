@@ -6,6 +6,7 @@
 #include <string>
 
 #include "moc/cpu_engine.hpp"
+#include "moc/device.hpp"
 #include "moc/hip_engine.hpp"
 #include "moc/io.hpp"
 #include "moc/partition.hpp"
@@ -158,7 +159,7 @@ int moc_host_register(void* p, size_t bytes) {
     const uintptr_t page = 4096;
     uintptr_t b = reinterpret_cast<uintptr_t>(p) & ~(page - 1);
     uintptr_t e = (reinterpret_cast<uintptr_t>(p) + bytes + page - 1) & ~(page - 1);
-    MOC_HIP_CHECK(hipHostRegister(reinterpret_cast<void*>(b), e - b, hipHostRegisterDefault));
+    MOC_HIP_CHECK(hipHostRegister(reinterpret_cast<void*>(b), e - b, hipHostRegisterMapped));
   });
 }
 
@@ -176,14 +177,14 @@ int moc_device_info_json(int device, char* buf, int64_t cap) {
   });
 }
 
-void* moc_engine_create(int device, int64_t chunk_records, int64_t chunk_bytes, int pin_host) {
+void* moc_engine_create(int device, int64_t chunk_records, int64_t chunk_bytes, int allow_direct) {
   moc::HipEngine* e = nullptr;
   int rc = guard([&] {
     moc::EngineOptions o;
     o.device = device;
     if (chunk_records > 0) o.chunk_records = chunk_records;
     if (chunk_bytes > 0) o.chunk_bytes = chunk_bytes;
-    o.pin_host = pin_host != 0;
+    o.allow_direct = allow_direct != 0;
     e = new moc::HipEngine(o);
   });
   return rc == 0 ? e : nullptr;
@@ -203,6 +204,24 @@ int moc_engine_solve(void* e, const uint8_t* codes, const int64_t* offsets, int6
   });
 }
 
+int moc_engine_solve_ex(void* e, const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths8, int64_t n,
+                        void* out, int fmt, int64_t min_l2, int64_t max_l2) {
+  return guard([&] {
+    moc::BatchHints h;
+    h.min_l2 = min_l2;
+    h.max_l2 = max_l2;
+    static_cast<moc::HipEngine*>(e)->solve_ex(codes, offsets, lengths8, n, out, static_cast<moc::ResultFormat>(fmt), h);
+  });
+}
+
+int moc_engine_auto_format(void* e, int64_t max_l2) {
+  return static_cast<int>(static_cast<moc::HipEngine*>(e)->auto_format(max_l2));
+}
+
+int moc_engine_pin(void* e, const void* p, size_t bytes) {
+  return guard([&] { static_cast<moc::HipEngine*>(e)->pin(p, bytes); });
+}
+
 int moc_engine_solve_device(void* e, const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets,
                             int64_t n, moc_result* d_out, void* stream) {
   return guard([&] {
@@ -212,16 +231,24 @@ int moc_engine_solve_device(void* e, const uint8_t* d_codes, const int64_t* d_of
   });
 }
 
-int moc_engine_stats(void* e, double* out7) {
+int moc_engine_stats(void* e, double* out9) {
   return guard([&] {
     const auto& s = static_cast<moc::HipEngine*>(e)->stats();
-    out7[0] = s.kernel_ms;
-    out7[1] = s.total_ms;
-    out7[2] = static_cast<double>(s.h2d_bytes);
-    out7[3] = static_cast<double>(s.d2h_bytes);
-    out7[4] = static_cast<double>(s.chunks);
-    out7[5] = static_cast<double>(s.cells);
-    out7[6] = static_cast<double>(s.records);
+    out9[0] = s.kernel_ms;
+    out9[1] = s.total_ms;
+    out9[2] = static_cast<double>(s.h2d_bytes);
+    out9[3] = static_cast<double>(s.d2h_bytes);
+    out9[4] = static_cast<double>(s.chunks);
+    out9[5] = static_cast<double>(s.cells);
+    out9[6] = static_cast<double>(s.records);
+    out9[7] = static_cast<double>(s.direct);
+    out9[8] = static_cast<double>(s.format);
+  });
+}
+
+int moc_expand_results(const void* in, int fmt, int64_t n, moc_result* out) {
+  return guard([&] {
+    moc::expand_results(in, static_cast<moc::ResultFormat>(fmt), n, reinterpret_cast<moc::Result*>(out));
   });
 }
 

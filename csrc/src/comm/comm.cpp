@@ -168,7 +168,15 @@ RcclComm::RcclComm(const MpiContext& ctx, int device) : ctx_(ctx) {
   ncclUniqueId id;
   if (ctx.rank == 0) MOC_NCCL_CHECK(ncclGetUniqueId(&id));
   MOC_MPI_CHECK(MPI_Bcast(&id, sizeof id, MPI_BYTE, 0, ctx.world));
-  MOC_NCCL_CHECK(ncclCommInitRank(&comm_, ctx.size, id, ctx.rank));
+  // RCCL prints a version banner on stdout during init; stdout carries results only (main.c:204).
+  std::fflush(stdout);
+  const int saved = dup(1);
+  dup2(2, 1);
+  const ncclResult_t rc = ncclCommInitRank(&comm_, ctx.size, id, ctx.rank);
+  std::fflush(stdout);
+  dup2(saved, 1);
+  close(saved);
+  MOC_NCCL_CHECK(rc);
 }
 
 RcclComm::~RcclComm() {

@@ -1,0 +1,163 @@
+// Device helpers shared by the gfx950 search kernels (wave64 cross-lane ops, candidate keys, result
+// formats). Included only by .hip translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "moc/device.hpp"
+
+namespace moc {
+namespace dev {
+namespace kc {
+
+constexpr int kLutInts = kLutStride * kLutStride;  // 1024
+constexpr int kDppWaveShl1 = 0x130;                // lane i <- lane i+1 (lane 63: bound)
+
+// The result goes through an empty asm so the backend's DPP combiner cannot fold the move into the
+// consuming VALU op: on gfx950 / ROCm 7.2 the folded `v_subrev_u32_dpp vD, vP, vP wave_shl:1` computed
+// P(lane+1) - P(lane) instead of P(lane) - P(lane+1) (found with tools/debug_tiles.py: every
+// tile-kernel candidate came out with the sign of d flipped). One extra v_mov_dpp per cell.
+__device__ __forceinline__ int wave_shl1(int v) {
+  int r = __builtin_amdgcn_update_dpp(0, v, kDppWaveShl1, 0xf, 0xf, true);
+  asm volatile("" : "+v"(r));
+  return r;
+}
+// Same shift, but lane 63 receives `fill` instead of 0.
+__device__ __forceinline__ int wave_shl1_fill(int v, int fill) {
+  int r = __builtin_amdgcn_update_dpp(fill, v, kDppWaveShl1, 0xf, 0xf, false);
+  asm volatile("" : "+v"(r));
+  return r;
+}
+
+// ---- hot-loop keys: (d = P_o(k) - P_{o+1}(k), k) with "larger d, then smaller k" ordering ----------
+template <bool Wide>
+struct HotKey;
+
+template <>
+struct HotKey<false> {  // int32: d in the high bits, (mask - k) in the low `shift` bits
+  using T = int32_t;
+  static __device__ __forceinline__ T min() { return INT32_MIN; }
+  static __device__ __forceinline__ T make(int d, int k, int shift, int mask) {
+    return static_cast<int32_t>((static_cast<uint32_t>(d) << shift) | static_cast<uint32_t>(mask - k));
+  }
+  static __device__ __forceinline__ int d(T key, int shift) { return key >> shift; }
+  static __device__ __forceinline__ int k(T key, int mask) { return mask - (key & mask); }
+};
+
+template <>
+struct HotKey<true> {  // int64: d in the high word, (0xffffffff - k) in the low word
+  using T = int64_t;
+  static __device__ __forceinline__ T min() { return INT64_MIN; }
+  static __device__ __forceinline__ T make(int d, int k, int, int) {
+    return static_cast<int64_t>(d) * 4294967296ll + static_cast<int64_t>(0xffffffffu - static_cast<uint32_t>(k));
+  }
+  static __device__ __forceinline__ int d(T key, int) { return static_cast<int>(key >> 32); }
+  static __device__ __forceinline__ int k(T key, int) {
+    return static_cast<int>(0xffffffffu - static_cast<uint32_t>(key & 0xffffffffll));
+  }
+};
+
+// ---- final 64-bit candidate keys: score high, ~(o*L2 + k) low -> max = best with reference tie-break
+__device__ __forceinline__ unsigned long long final_key(int score, uint32_t idx) {
+  return (static_cast<unsigned long long>(static_cast<uint32_t>(score) ^ 0x80000000u) << 32) |
+         static_cast<unsigned long long>(0xffffffffu - idx);
+}
+
+__device__ __forceinline__ Result decode_key(unsigned long long key, int L2) {
+  if (key == 0ull) return Result{INT32_MIN, 0, 0};
+  const int score = static_cast<int>(static_cast<uint32_t>(key >> 32) ^ 0x80000000u);
+  const uint32_t idx = 0xffffffffu - static_cast<uint32_t>(key);
+  return Result{score, static_cast<int>(idx / static_cast<uint32_t>(L2)),
+                static_cast<int>(idx % static_cast<uint32_t>(L2))};
+}
+
+__device__ __forceinline__ unsigned long long max_u64(unsigned long long a, unsigned long long b) {
+  return a > b ? a : b;
+}
+
+__device__ __forceinline__ unsigned long long shfl_down_u64(unsigned long long v, int d) {
+  const int lo = __shfl_down(static_cast<int>(v), d, 64);
+  const int hi = __shfl_down(static_cast<int>(v >> 32), d, 64);
+  return (static_cast<unsigned long long>(static_cast<uint32_t>(hi)) << 32) | static_cast<uint32_t>(lo);
+}
+
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const int lo = __shfl_xor(static_cast<int>(v), d, 64);
+    const int hi = __shfl_xor(static_cast<int>(v >> 32), d, 64);
+    v = max_u64(v, (static_cast<unsigned long long>(static_cast<uint32_t>(hi)) << 32) | static_cast<uint32_t>(lo));
+  }
+  return v;
+}
+
+__device__ __forceinline__ int wave_max_i32(int v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v = max(v, __shfl_xor(v, d, 64));
+  return v;
+}
+
+// Inclusive prefix sum over the 64 lanes of a wave.
+__device__ __forceinline__ int wave_inclusive_sum(int v, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int t = __shfl_up(v, d, 64);
+    if (lane >= d) v += t;
+  }
+  return v;
+}
+
+// Lane's best candidate key for offset `o` after the sweep.
+//   P = Tot_o, Pn = Tot_{o+1}, best = best hot key over k = 1..steps.
+// Hot-loop steps past L2 only repeat k = L2 with d = Tot_o - Tot_{o+1}, whose score equals the
+// un-mutated candidate's with a larger index, so they can never win (no masking needed in the loop).
+template <bool Wide>
+__device__ __forceinline__ unsigned long long lane_candidate(bool own, int o, int L1, int L2, int sem, int P, int Pn,
+                                                             typename HotKey<Wide>::T best, int shift, int mask) {
+  using K = HotKey<Wide>;
+  unsigned long long key = 0;
+  if (!own) return key;
+  const int last = L1 - L2;  // un-mutated at o == last: spec only (or the equal-length case)
+  const bool v0 = (o < last) || (o == last && (sem == static_cast<int>(Semantics::Spec) || L2 == L1));
+  if (v0) key = final_key(P, static_cast<uint32_t>(o) * static_cast<uint32_t>(L2));
+  if (o < last && L2 >= 2 && best != K::min()) {
+    const int s1 = K::d(best, shift) + Pn;
+    const int k = K::k(best, mask);
+    key = max_u64(key, final_key(s1, static_cast<uint32_t>(o) * static_cast<uint32_t>(L2) + static_cast<uint32_t>(k)));
+  }
+  return key;
+}
+
+// ---- result formats -------------------------------------------------------------------------------
+__device__ __forceinline__ void store_result(void* out, int64_t r, int fmt, const Result& v) {
+  if (fmt == static_cast<int>(ResultFormat::R4)) {
+    R4 x;
+    x.score = static_cast<int16_t>(v.score == INT32_MIN ? INT16_MIN : v.score);
+    x.n = static_cast<uint8_t>(v.n);
+    x.k = static_cast<uint8_t>(v.k);
+    static_cast<R4*>(out)[r] = x;
+  } else if (fmt == static_cast<int>(ResultFormat::R8)) {
+    R8 x;
+    x.score = v.score;
+    x.n = static_cast<uint16_t>(v.n);
+    x.k = static_cast<uint16_t>(v.k);
+    static_cast<R8*>(out)[r] = x;
+  } else {
+    static_cast<Result*>(out)[r] = v;
+  }
+}
+
+__device__ __forceinline__ void stage_lut(int* lut, const int32_t* g) {
+  for (int t = threadIdx.x; t < kLutInts; t += blockDim.x) lut[t] = g[t];
+}
+__device__ __forceinline__ void stage_bytes(uint8_t* dst, const uint8_t* src, int n) {
+  // 4-byte copy; both buffers are padded so rounding n up to a multiple of 4 stays in bounds
+  const int n4 = (n + 3) >> 2;
+  const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
+  uint32_t* d = reinterpret_cast<uint32_t*>(dst);
+  for (int t = threadIdx.x; t < n4; t += blockDim.x) d[t] = s[t];
+}
+
+}  // namespace kc
+}  // namespace dev
+}  // namespace moc

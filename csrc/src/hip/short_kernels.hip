@@ -1,0 +1,231 @@
+// Short-record search kernel (records with L1 - L2 + 1 <= 64 offsets; the input6-shaped regime).
+//
+// Persistent blocks of 4 waves pull tiles of `tile_records` consecutive records from a device work
+// counter. Per tile the block:
+//   1. reads the tile's lengths (narrow uint8 lengths when available, else offsets) and block-scans
+//      them into LDS-local offsets;
+//   2. copies the tile's letters into LDS with 16-byte loads — from device memory, or straight from
+//      pinned host memory (zero-copy streaming: the batch crosses PCIe exactly once and no staging
+//      buffers/copies are needed);
+//   3. scores every record: each wave holds 64/slot records in fixed lane slots, lane = offset o,
+//      P += S[c][o+i] from the per-block LDS profile S[c][j] = T[c][Seq1[j]] (row 0 = padding = 0, so
+//      lanes past their record's end add 0 and need no masking), P_{o+1} via DPP wave_shl:1,
+//      best = max over k of pack(P_o(k) - P_{o+1}(k), k);
+//   4. reduces each slot with a segmented suffix max of 64-bit keys and writes the tile's results
+//      (R4/R8/R12) back with coalesced dword stores.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "kernel_common.hpp"
+
+namespace moc {
+namespace dev {
+
+using namespace kc;
+
+namespace {
+constexpr int kBlock = 256;
+constexpr int kMaxTile = 1024;            // records per block tile (4 per thread in the scan)
+constexpr int kShortLdsBudget = 60 * 1024;  // stay under the 64 KiB default dynamic-LDS limit
+
+struct ShortLayout {
+  int row = 0;          // profile row length (entries), Profile mode
+  int table_bytes = 0;  // profile or LUT
+  int s1_bytes = 0;     // LUT mode: Seq1 copy
+  int loff_off = 0, codes_off = 0, res_off = 0, total = 0;
+  bool profile = false;
+};
+
+inline int align16(int x) { return (x + 15) & ~15; }
+
+ShortLayout short_layout(int L1, int tile_records, int codes_cap, int fmt_bytes, bool profile) {
+  ShortLayout l;
+  l.profile = profile;
+  if (profile) {
+    l.row = (L1 + kWave + 3) & ~3;
+    l.table_bytes = align16(kAlphabet * l.row * 4);
+  } else {
+    l.table_bytes = kLutInts * 4;
+    l.s1_bytes = align16(L1 + kWave + 4);
+  }
+  l.loff_off = l.table_bytes + l.s1_bytes;
+  l.codes_off = l.loff_off + align16((tile_records + 1) * 4 + 32);
+  l.res_off = l.codes_off + align16(codes_cap);
+  l.total = l.res_off + align16(tile_records * fmt_bytes);
+  return l;
+}
+}  // namespace
+
+template <bool Wide, bool Profile>
+__global__ __launch_bounds__(kBlock) void short_search_kernel(ProblemView pv, ShortArgs a, ShortLayout lay) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  int* table = reinterpret_cast<int*>(smem);
+  uint8_t* s1l = smem + lay.table_bytes;
+  int* loff = reinterpret_cast<int*>(smem + lay.loff_off);
+  int* misc = loff + a.tile_records + 1;  // 8 ints of slack: [0] tile id, [4..7] per-wave scan totals
+  uint8_t* codes_l = smem + lay.codes_off;
+  uint8_t* res_l = smem + lay.res_off;
+  const int L1 = pv.L1;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+  // ---- per-block problem tables (built once, reused for every tile this block pulls)
+  if (Profile) {
+    const int row = lay.row;
+    for (int e = tid; e < kAlphabet * row; e += kBlock) {
+      const int c = e / row, j = e - c * row;
+      table[e] = (c >= 1 && j < L1) ? pv.lut[c * kLutStride + pv.seq1[j]] : 0;
+    }
+  } else {
+    for (int e = tid; e < kLutInts; e += kBlock) {
+      const int c = e >> 5;
+      table[e] = c >= 1 ? pv.lut[e] : 0;  // row 0 = padding -> contributes 0
+    }
+    stage_bytes(s1l, pv.seq1, L1 + kWave);
+  }
+
+  using K = HotKey<Wide>;
+  const int slot = a.slot, rpw = a.rpw;
+  const int sl = lane / slot;
+  const int o = lane - sl * slot;
+  const int shift = pv.key_shift, mask = (1 << pv.key_shift) - 1;
+  const int fb = a.fmt == static_cast<int>(ResultFormat::R4) ? 4 : a.fmt == static_cast<int>(ResultFormat::R8) ? 8 : 12;
+  const int64_t n_tiles = (a.n + a.tile_records - 1) / a.tile_records;
+
+  for (;;) {
+    __syncthreads();  // previous tile fully consumed (and tables built on the first pass)
+    if (tid == 0) misc[0] = static_cast<int>(atomicAdd(a.counter, 1u));
+    __syncthreads();
+    const int64_t t = misc[0];
+    if (t >= n_tiles) break;  // block-uniform exit; every wave reaches it
+    const int64_t rb = t * a.tile_records;
+    const int m = static_cast<int>(min(static_cast<int64_t>(a.tile_records), a.n - rb));
+    const int64_t start = a.offsets[rb];
+    const int64_t end = a.offsets[rb + m];
+
+    // ---- 1. lengths -> block exclusive scan -> loff[0..m]
+    int len4[4];
+    int sum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = tid * 4 + q;
+      int L = 0;
+      if (r < m) L = a.lengths8 ? static_cast<int>(a.lengths8[rb + r]) : static_cast<int>(a.offsets[rb + r + 1] - a.offsets[rb + r]);
+      len4[q] = L;
+      sum += L;
+    }
+    const int incl = wave_inclusive_sum(sum, lane);
+    if (lane == 63) misc[4 + wave] = incl;
+    __syncthreads();
+    int excl = incl - sum;
+    for (int w = 0; w < wave; ++w) excl += misc[4 + w];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = tid * 4 + q;
+      if (r < m) loff[r] = excl;
+      excl += len4[q];
+    }
+    if (tid == kBlock - 1) loff[m] = excl;  // the last thread's running sum is the tile total
+
+    // ---- 2. letters -> LDS (16-byte loads; never crosses a page the tile does not touch)
+    const uintptr_t p0 = reinterpret_cast<uintptr_t>(a.codes + start);
+    const uintptr_t a0 = p0 & ~uintptr_t{15};
+    const int shift_b = static_cast<int>(p0 - a0);
+    const int nvec = static_cast<int>((reinterpret_cast<uintptr_t>(a.codes + end) + 15 - a0) >> 4);
+    for (int v = tid; v < nvec; v += kBlock)
+      reinterpret_cast<uint4*>(codes_l)[v] = reinterpret_cast<const uint4*>(a0)[v];
+    __syncthreads();
+
+    // ---- 3. score: each wave takes groups of rpw records
+    for (int g = wave; g * rpw < m; g += 4) {
+      const int rl = g * rpw + sl;
+      const bool in = sl < rpw && rl < m;
+      int L2 = 0, roff = 0;
+      if (in) {
+        roff = loff[rl];
+        L2 = loff[rl + 1] - roff;
+      }
+      const int need = L2 <= L1 ? L1 - L2 + 1 : 1;
+      const bool mine = in && need <= slot;
+      const bool on = mine && L2 <= L1 && o < need;
+      const int steps = wave_max_i32(on ? L2 : 0);
+      const uint8_t* rec = codes_l + shift_b + roff;
+      int P = 0;
+      typename K::T best = K::min();
+      for (int i = 0; i < steps; ++i) {
+        const int c = (on && i < L2) ? rec[i] : 0;
+        int v;
+        if (Profile)
+          v = table[c * lay.row + o + i];
+        else
+          v = table[(c << 5) | s1l[o + i]];
+        P += v;
+        const int Pn = wave_shl1(P);
+        const typename K::T key = K::make(P - Pn, i + 1, shift, mask);
+        best = key > best ? key : best;
+      }
+      const int Pn = wave_shl1(P);
+      unsigned long long key = lane_candidate<Wide>(on, o, L1, L2, pv.semantics, P, Pn, best, shift, mask);
+      for (int d = 1; d < slot; d <<= 1) {  // segmented suffix max within the slot
+        const unsigned long long other = shfl_down_u64(key, d);
+        if (o + d < slot) key = max_u64(key, other);
+      }
+      if (mine && o == 0) store_result(res_l, rl, a.fmt, decode_key(key, L2 > 0 ? L2 : 1));
+    }
+    __syncthreads();
+
+    // ---- 4. results -> out (coalesced dwords; long records are overwritten later by the tile kernel)
+    uint32_t* dst = reinterpret_cast<uint32_t*>(static_cast<char*>(a.out) + rb * fb);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(res_l);
+    const int nd = m * fb / 4;
+    for (int q = tid; q < nd; q += kBlock) dst[q] = src[q];
+  }
+}
+
+bool configure_short(int64_t L1, int64_t min_l2, int64_t max_l2, ShortArgs& a) {
+  if (lanes_needed(L1, min_l2) > kWave) return false;
+  a.slot = static_cast<int32_t>(std::max<int64_t>(1, lanes_needed(L1, min_l2)));
+  a.rpw = kWave / a.slot;
+  const int64_t l2cap = std::max<int64_t>(1, std::min(max_l2, L1 + 1));
+  const int fb = result_bytes(static_cast<ResultFormat>(a.fmt));
+  const bool profile = kAlphabet * ((L1 + kWave + 3) & ~3) * 4 <= 24 * 1024;
+  for (int tr = kMaxTile; tr >= 1; tr /= 2) {
+    // worst-case letters of a tile: records longer than L1 are never scored but still staged
+    const int64_t cap = static_cast<int64_t>(tr) * std::max(max_l2, int64_t{1}) + 48;
+    if (cap > kShortLdsBudget) continue;
+    ShortLayout l = short_layout(static_cast<int>(L1), tr, static_cast<int>(cap), fb, profile);
+    if (l.total <= kShortLdsBudget) {
+      a.tile_records = tr;
+      a.codes_cap = static_cast<int32_t>(cap);
+      a.max_l2 = static_cast<int32_t>(l2cap);
+      return true;
+    }
+  }
+  return false;
+}
+
+void launch_short(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStream_t stream) {
+  if (a.n <= 0) return;
+  const int fb = result_bytes(static_cast<ResultFormat>(a.fmt));
+  const bool profile = kAlphabet * ((pv.L1 + kWave + 3) & ~3) * 4 <= 24 * 1024;
+  const ShortLayout lay = short_layout(pv.L1, a.tile_records, a.codes_cap, fb, profile);
+  const int64_t n_tiles = (a.n + a.tile_records - 1) / a.tile_records;
+  const int per_cu = std::max(1, std::min(8, 160 * 1024 / std::max(lay.total, 1)));
+  const int64_t blocks = std::min<int64_t>(n_tiles, static_cast<int64_t>(num_cus) * per_cu);
+  (void)hipMemsetAsync(a.counter, 0, sizeof(unsigned), stream);
+  const dim3 grid(static_cast<unsigned>(std::max<int64_t>(blocks, 1))), block(kBlock);
+  if (pv.key_shift > 0) {
+    if (profile)
+      hipLaunchKernelGGL((short_search_kernel<false, true>), grid, block, lay.total, stream, pv, a, lay);
+    else
+      hipLaunchKernelGGL((short_search_kernel<false, false>), grid, block, lay.total, stream, pv, a, lay);
+  } else {
+    if (profile)
+      hipLaunchKernelGGL((short_search_kernel<true, true>), grid, block, lay.total, stream, pv, a, lay);
+    else
+      hipLaunchKernelGGL((short_search_kernel<true, false>), grid, block, lay.total, stream, pv, a, lay);
+  }
+}
+
+}  // namespace dev
+}  // namespace moc

@@ -1,5 +1,7 @@
 #include "moc/hip_engine.hpp"
 
+#include <omp.h>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -14,47 +16,65 @@ namespace moc {
 
 int32_t choose_key_shift(int32_t max_abs_weight, int64_t max_l2) {
   int shift = 1;
-  while ((int64_t{1} << shift) < max_l2) ++shift;  // mask = 2^shift - 1 >= L2 - 1
+  while ((int64_t{1} << shift) < max_l2 + 1) ++shift;  // mask = 2^shift - 1 >= every k used (<= L2)
   const int64_t dmax = 2 * static_cast<int64_t>(std::max(max_abs_weight, 1)) * std::max<int64_t>(max_l2, 1);
   if (shift > 24 || (dmax << shift) >= (int64_t{1} << 31)) return 0;  // 64-bit hot keys
   return shift;
 }
 
-// ------------------------------------------------------------------------------------------------
-// Host-memory pinning for direct DMA: registers the page range of a caller buffer for the duration
-// of one solve() (skipped when the memory is already pinned, e.g. hipHostMalloc or registered).
-namespace {
-class PinGuard {
- public:
-  PinGuard(const void* p, size_t bytes) {
-    // Small buffers may share pages with unrelated allocations: leave them pageable (HIP stages them).
-    if (!p || bytes < (size_t{64} << 20)) return;
-    hipPointerAttribute_t attr;
-    if (hipPointerGetAttributes(&attr, p) == hipSuccess && attr.type != hipMemoryTypeUnregistered) return;
-    (void)hipGetLastError();
-    const uintptr_t page = 4096;
-    uintptr_t b = reinterpret_cast<uintptr_t>(p) & ~(page - 1);
-    uintptr_t e = (reinterpret_cast<uintptr_t>(p) + bytes + page - 1) & ~(page - 1);
-    hipError_t err = hipHostRegister(reinterpret_cast<void*>(b), e - b, hipHostRegisterDefault);
-    if (err == hipSuccess) {
-      base_ = reinterpret_cast<void*>(b);
+ResultFormat pick_result_format(int64_t L1, int64_t max_l2, int32_t max_abs_weight) {
+  const int64_t smax = static_cast<int64_t>(std::max(max_abs_weight, 1)) * std::max<int64_t>(max_l2, 1);
+  if (L1 <= 255 && max_l2 <= 255 && smax < 32767) return ResultFormat::R4;
+  if (L1 <= 65535 && max_l2 <= 65535) return ResultFormat::R8;
+  return ResultFormat::R12;
+}
+
+void expand_results(const void* in, ResultFormat f, int64_t n, Result* out) {
+  if (f == ResultFormat::R12) {
+    if (in != out) std::memmove(out, in, sizeof(Result) * static_cast<size_t>(n));
+    return;
+  }
+#pragma omp parallel for schedule(static) if (n > 65536)
+  for (int64_t i = 0; i < n; ++i) {
+    if (f == ResultFormat::R8) {
+      const R8 x = static_cast<const R8*>(in)[i];
+      out[i] = Result{x.score, x.n, x.k};
     } else {
-      (void)hipGetLastError();  // fall back to pageable DMA (slower, still correct)
-      MOC_LOG_DEBUG("hipHostRegister(%zu bytes) failed: %s", static_cast<size_t>(e - b), hipGetErrorString(err));
+      const R4 x = static_cast<const R4*>(in)[i];
+      out[i] = Result{x.score == INT16_MIN ? INT32_MIN : x.score, x.n, x.k};
     }
   }
-  ~PinGuard() {
-    if (base_) (void)hipHostUnregister(base_);
-  }
-  PinGuard(const PinGuard&) = delete;
-  PinGuard& operator=(const PinGuard&) = delete;
+}
 
- private:
-  void* base_ = nullptr;
-};
+namespace {
+// True when [p, p+bytes) is page-locked host memory (hipHostMalloc or hipHostRegister); *dev gets the
+// device-side address of p.
+bool pinned_range(const void* p, size_t bytes, const void** dev) {
+  if (!p) return false;
+  hipPointerAttribute_t a, b;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  if (a.type != hipMemoryTypeHost) return false;
+  if (bytes > 1) {
+    if (hipPointerGetAttributes(&b, static_cast<const char*>(p) + bytes - 1) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    if (b.type != hipMemoryTypeHost) return false;
+  }
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, const_cast<void*>(p), 0) != hipSuccess || !d) {
+    (void)hipGetLastError();
+    return false;
+  }
+  *dev = d;
+  return true;
+}
 }  // namespace
 
-// One half of the double buffer: device buffers + pinned plan staging + events.
+// One half of the double buffer of the staged pipeline.
 struct HipEngine::Slot {
   void* d_codes = nullptr;
   size_t d_codes_cap = 0;
@@ -66,6 +86,7 @@ struct HipEngine::Slot {
   size_t d_plan_cap = 0;
   void* h_plan = nullptr;  // pinned staging for tiles | long_recs
   size_t h_plan_cap = 0;
+  unsigned* d_counter = nullptr;
   hipEvent_t ev_h2d = nullptr, ev_k0 = nullptr, ev_k1 = nullptr, ev_done = nullptr;
   bool busy = false;
 };
@@ -73,6 +94,9 @@ struct HipEngine::Slot {
 HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
   if (opt_.device >= 0) MOC_HIP_CHECK(hipSetDevice(opt_.device));
   MOC_HIP_CHECK(hipGetDevice(&device_));
+  hipDeviceProp_t prop;
+  MOC_HIP_CHECK(hipGetDeviceProperties(&prop, device_));
+  num_cus_ = prop.multiProcessorCount;
   MOC_HIP_CHECK(hipStreamCreateWithFlags(&s_copy_, hipStreamNonBlocking));
   MOC_HIP_CHECK(hipStreamCreateWithFlags(&s_compute_, hipStreamNonBlocking));
   MOC_HIP_CHECK(hipStreamCreateWithFlags(&s_return_, hipStreamNonBlocking));
@@ -82,8 +106,12 @@ HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
     MOC_HIP_CHECK(hipEventCreate(&s->ev_k0));
     MOC_HIP_CHECK(hipEventCreate(&s->ev_k1));
     MOC_HIP_CHECK(hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming));
+    MOC_HIP_CHECK(hipMalloc(&s->d_counter, sizeof(unsigned)));
     slots_.push_back(std::move(s));
   }
+  MOC_HIP_CHECK(hipMalloc(&d_counter_, sizeof(unsigned)));
+  MOC_HIP_CHECK(hipEventCreate(&ev_a_));
+  MOC_HIP_CHECK(hipEventCreate(&ev_b_));
   MOC_HIP_CHECK(hipEventCreateWithFlags(&ev_plan_, hipEventDisableTiming));
 }
 
@@ -95,20 +123,41 @@ HipEngine::~HipEngine() {
     (void)hipFree(s->d_offsets);
     (void)hipFree(s->d_out);
     (void)hipFree(s->d_plan);
+    (void)hipFree(s->d_counter);
     (void)hipHostFree(s->h_plan);
     (void)hipEventDestroy(s->ev_h2d);
     (void)hipEventDestroy(s->ev_k0);
     (void)hipEventDestroy(s->ev_k1);
     (void)hipEventDestroy(s->ev_done);
   }
+  unpin_all();
+  (void)hipFree(d_counter_);
   (void)hipFree(d_plan_);
   (void)hipHostFree(h_plan_);
   (void)hipEventDestroy(ev_plan_);
+  (void)hipEventDestroy(ev_a_);
+  (void)hipEventDestroy(ev_b_);
   (void)hipFree(d_lut_);
   (void)hipFree(d_seq1_);
   (void)hipStreamDestroy(s_copy_);
   (void)hipStreamDestroy(s_compute_);
   (void)hipStreamDestroy(s_return_);
+}
+
+void HipEngine::pin(const void* p, size_t bytes) {
+  if (!p || bytes == 0) return;
+  const void* d = nullptr;
+  if (pinned_range(p, bytes, &d)) return;  // already pinned
+  const uintptr_t page = 4096;
+  uintptr_t b = reinterpret_cast<uintptr_t>(p) & ~(page - 1);
+  uintptr_t e = (reinterpret_cast<uintptr_t>(p) + bytes + page - 1) & ~(page - 1);
+  MOC_HIP_CHECK(hipHostRegister(reinterpret_cast<void*>(b), e - b, hipHostRegisterMapped));
+  pinned_.push_back(reinterpret_cast<void*>(b));
+}
+
+void HipEngine::unpin_all() {
+  for (void* p : pinned_) (void)hipHostUnregister(p);
+  pinned_.clear();
 }
 
 void HipEngine::ensure(void*& ptr, size_t& cap, size_t bytes) {
@@ -133,17 +182,18 @@ void HipEngine::ensure_host(void*& ptr, size_t& cap, size_t bytes) {
 void HipEngine::set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, Semantics sem) {
   MOC_HIP_CHECK(hipSetDevice(device_));
   if (L1 > (int64_t{1} << 30)) throw Error("Seq1 too long for the device engine");
-  MOC_HIP_CHECK(hipDeviceSynchronize());  // previous problem's launches may still read the buffers
   table_ = ScoreTable::build(w);
   L1_ = L1;
   sem_ = sem;
   if (!d_lut_) MOC_HIP_CHECK(hipMalloc(&d_lut_, sizeof(int32_t) * kLutStride * kLutStride));
-  MOC_HIP_CHECK(hipFree(d_seq1_));
-  d_seq1_ = nullptr;
   const size_t s1bytes = static_cast<size_t>(L1) + dev::kSeq1Pad;
-  MOC_HIP_CHECK(hipMalloc(&d_seq1_, s1bytes));
   std::vector<uint8_t> padded(s1bytes, 0);
   if (L1) std::memcpy(padded.data(), seq1, static_cast<size_t>(L1));
+  // Kernels of a previous problem may still be queued on our streams: order the uploads behind them
+  // on the compute stream (no device-wide synchronisation).
+  MOC_HIP_CHECK(hipStreamSynchronize(s_compute_));
+  MOC_HIP_CHECK(hipFree(d_seq1_));
+  MOC_HIP_CHECK(hipMalloc(&d_seq1_, s1bytes));
   MOC_HIP_CHECK(hipMemcpy(d_lut_, table_.lut.data(), sizeof(int32_t) * table_.lut.size(), hipMemcpyHostToDevice));
   MOC_HIP_CHECK(hipMemcpy(d_seq1_, padded.data(), s1bytes, hipMemcpyHostToDevice));
   have_problem_ = true;
@@ -161,39 +211,67 @@ dev::ProblemView HipEngine::problem_view(int64_t max_l2) const {
   pv.seq1 = d_seq1_;
   pv.L1 = static_cast<int32_t>(L1_);
   pv.semantics = static_cast<int32_t>(sem_);
-  pv.key_shift = choose_key_shift(table_.max_abs(), max_l2);
+  pv.key_shift = choose_key_shift(table_.max_abs(), std::min<int64_t>(std::max<int64_t>(max_l2, 1), L1_ + 1));
   return pv;
 }
 
-void HipEngine::plan_chunk(const int64_t* offsets, int64_t n, HostPlan& hp) const {
-  hp.slot = 0;
-  hp.tiles.clear();
-  hp.long_recs.clear();
-  hp.max_l2 = 0;
-  hp.cells = 0;
-  int64_t slot = 0;
-  for (int64_t i = 0; i < n; ++i) {
-    const int64_t L2 = offsets[i + 1] - offsets[i];
-    hp.max_l2 = std::max(hp.max_l2, L2);
-    hp.cells += record_cells(L1_, L2);
-    const int64_t need = dev::lanes_needed(L1_, L2);
-    if (need <= dev::kWave) {
-      slot = std::max(slot, need);
-    } else {
-      const int32_t li = static_cast<int32_t>(hp.long_recs.size());
-      hp.long_recs.push_back(static_cast<int32_t>(i));
-      for (int64_t o0 = 0; o0 < need; o0 += dev::kTileOffsets)
-        hp.tiles.push_back(dev::Tile{li, static_cast<int32_t>(o0)});
+ResultFormat HipEngine::auto_format(int64_t max_l2) const {
+  return pick_result_format(L1_, max_l2, table_.max_abs());
+}
+
+// Splits a chunk's records into the short-kernel set (<= 64 lanes) and the long list (tile kernel).
+// OpenMP: per-thread partial lists are concatenated in thread order, so long_recs stays sorted.
+void HipEngine::plan_chunk(const int64_t* offsets, int64_t n, ChunkPlan& cp) const {
+  cp.tiles.clear();
+  cp.long_recs.clear();
+  const int64_t short_min_len = std::max<int64_t>(L1_ - (dev::kWave - 1), 0);  // lanes_needed <= 64
+  const int nt = n > (1 << 16) ? omp_get_max_threads() : 1;
+  std::vector<std::vector<int32_t>> part(nt);
+  std::vector<int64_t> mins(nt, INT64_MAX), maxs(nt, 0), nshort(nt, 0), cells(nt, 0);
+#pragma omp parallel num_threads(nt)
+  {
+    const int t = omp_get_thread_num();
+    const int64_t b = n * t / nt, e = n * (t + 1) / nt;
+    int64_t mn = INT64_MAX, mx = 0, ns = 0, cl = 0;
+    for (int64_t i = b; i < e; ++i) {
+      const int64_t L2 = offsets[i + 1] - offsets[i];
+      mx = std::max(mx, L2);
+      cl += record_cells(L1_, L2);
+      if (L2 >= short_min_len) {
+        mn = std::min(mn, L2);
+        ++ns;
+      } else {
+        part[t].push_back(static_cast<int32_t>(i));
+      }
     }
+    mins[t] = mn;
+    maxs[t] = mx;
+    nshort[t] = ns;
+    cells[t] = cl;
   }
-  hp.slot = static_cast<int32_t>(slot);
-  hp.rpw = slot > 0 ? static_cast<int32_t>(dev::kWave / slot) : 0;
-  if (hp.max_l2 * L1_ >= (int64_t{1} << 32))
+  cp.min_short = INT64_MAX;
+  cp.max_l2 = 0;
+  cp.n_short = 0;
+  cp.cells = 0;
+  for (int t = 0; t < nt; ++t) {
+    cp.min_short = std::min(cp.min_short, mins[t]);
+    cp.max_l2 = std::max(cp.max_l2, maxs[t]);
+    cp.n_short += nshort[t];
+    cp.cells += cells[t];
+    cp.long_recs.insert(cp.long_recs.end(), part[t].begin(), part[t].end());
+  }
+  for (size_t li = 0; li < cp.long_recs.size(); ++li) {
+    const int64_t L2 = offsets[cp.long_recs[li] + 1] - offsets[cp.long_recs[li]];
+    const int64_t need = dev::lanes_needed(L1_, L2);
+    for (int64_t o0 = 0; o0 < need; o0 += dev::kTileOffsets)
+      cp.tiles.push_back(dev::Tile{static_cast<int32_t>(li), static_cast<int32_t>(o0)});
+  }
+  if (cp.max_l2 * std::max<int64_t>(L1_, 1) >= (int64_t{1} << 32))
     throw Error("L1 * max L2 exceeds the 32-bit candidate index of the device engine");
 }
 
 namespace {
-// Layout of one chunk's plan in a single buffer: tiles | long_recs | keys(8-aligned).
+// Layout of one chunk's tile plan in a single buffer: tiles | long_recs | keys(8-aligned).
 struct PlanLayout {
   size_t tiles_off = 0, long_off = 0, keys_off = 0, upload_bytes = 0, total = 0;
   PlanLayout(size_t n_tiles, size_t n_long) {
@@ -203,23 +281,120 @@ struct PlanLayout {
     total = keys_off + n_long * sizeof(unsigned long long);
   }
 };
+
+struct LenStats {
+  int64_t mn = INT64_MAX, mx = 0;
+};
+LenStats scan_lengths(const int64_t* offsets, const uint8_t* lengths8, int64_t n) {
+  const int nt = n > (1 << 16) ? omp_get_max_threads() : 1;
+  std::vector<int64_t> mins(nt, INT64_MAX), maxs(nt, 0);
+#pragma omp parallel num_threads(nt)
+  {
+    const int t = omp_get_thread_num();
+    const int64_t b = n * t / nt, e = n * (t + 1) / nt;
+    int64_t mn = INT64_MAX, mx = 0;
+    if (lengths8) {
+      for (int64_t i = b; i < e; ++i) {
+        const int64_t L = lengths8[i];
+        mn = std::min(mn, L);
+        mx = std::max(mx, L);
+      }
+    } else {
+      for (int64_t i = b; i < e; ++i) {
+        const int64_t L = offsets[i + 1] - offsets[i];
+        mn = std::min(mn, L);
+        mx = std::max(mx, L);
+      }
+    }
+    mins[t] = mn;
+    maxs[t] = mx;
+  }
+  LenStats s;
+  for (int t = 0; t < nt; ++t) {
+    s.mn = std::min(s.mn, mins[t]);
+    s.mx = std::max(s.mx, maxs[t]);
+  }
+  return s;
+}
 }  // namespace
 
+bool HipEngine::direct_pointers(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths8, int64_t n,
+                                void* out, int fb, dev::ShortArgs& a) const {
+  const void *dc = nullptr, *doff = nullptr, *dlen = nullptr, *dout = nullptr;
+  const int64_t c0 = offsets[0], c1 = offsets[n];
+  if (c1 > c0 && !pinned_range(codes + c0, static_cast<size_t>(c1 - c0), &dc)) return false;
+  if (!pinned_range(offsets, sizeof(int64_t) * static_cast<size_t>(n + 1), &doff)) return false;
+  if (lengths8 && !pinned_range(lengths8, static_cast<size_t>(n), &dlen)) return false;
+  if (!pinned_range(out, static_cast<size_t>(fb) * static_cast<size_t>(n), &dout)) return false;
+  // device view of the codes base pointer (record i at base + offsets[i])
+  a.codes = c1 > c0 ? static_cast<const uint8_t*>(dc) - c0 : nullptr;
+  a.offsets = static_cast<const int64_t*>(doff);
+  a.lengths8 = static_cast<const uint8_t*>(dlen);
+  a.out = const_cast<void*>(dout);
+  return c1 > c0;
+}
+
 void HipEngine::solve(const uint8_t* codes, const int64_t* offsets, int64_t n, Result* out) {
+  solve_ex(codes, offsets, nullptr, n, out, ResultFormat::R12);
+}
+
+void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths8, int64_t n, void* out,
+                         ResultFormat fmt, const BatchHints& hints) {
   if (!have_problem_) throw Error("HipEngine::solve before set_problem");
   MOC_HIP_CHECK(hipSetDevice(device_));
   Stopwatch wall;
   wall.start();
   stats_ = EngineStats{};
+  stats_.format = static_cast<int32_t>(fmt);
+  stats_.records = n;
   if (n <= 0) return;
-  const int64_t total_chars = offsets[n] - offsets[0];
-  std::unique_ptr<PinGuard> pin_codes, pin_offs, pin_out;
-  if (opt_.pin_host) {
-    pin_codes = std::make_unique<PinGuard>(codes + offsets[0], static_cast<size_t>(total_chars));
-    pin_offs = std::make_unique<PinGuard>(offsets, sizeof(int64_t) * static_cast<size_t>(n + 1));
-    pin_out = std::make_unique<PinGuard>(out, sizeof(Result) * static_cast<size_t>(n));
+  const int fb = result_bytes(fmt);
+
+  // ---- batch bounds (hints, or one parallel pass over the lengths)
+  LenStats ls;
+  if (hints.min_l2 >= 0 && hints.max_l2 >= 0) {
+    ls.mn = hints.min_l2;
+    ls.mx = hints.max_l2;
+  } else {
+    ls = scan_lengths(offsets, lengths8, n);
   }
-  HostPlan hp;
+  if (lengths8 && ls.mx > 255) lengths8 = nullptr;
+  if (fmt == ResultFormat::R4 && (L1_ > 255 || ls.mx > 255 || table_.max_abs() * ls.mx >= 32767))
+    throw Error("result format R4 cannot hold this batch");
+  if (fmt == ResultFormat::R8 && (L1_ > 65535 || ls.mx > 65535)) throw Error("result format R8 cannot hold this batch");
+
+  // ---- direct zero-copy streaming path
+  dev::ShortArgs a;
+  a.n = n;
+  a.fmt = static_cast<int32_t>(fmt);
+  a.counter = d_counter_;
+  if (opt_.allow_direct && dev::configure_short(L1_, ls.mn, ls.mx, a) &&
+      direct_pointers(codes, offsets, lengths8, n, out, fb, a)) {
+    const dev::ProblemView pv = problem_view(ls.mx);
+    MOC_HIP_CHECK(hipEventRecord(ev_a_, s_compute_));
+    dev::launch_short(pv, a, num_cus_, s_compute_);
+    MOC_HIP_CHECK(hipGetLastError());
+    MOC_HIP_CHECK(hipEventRecord(ev_b_, s_compute_));
+    MOC_HIP_CHECK(hipEventSynchronize(ev_b_));
+    float ms = 0;
+    MOC_HIP_CHECK(hipEventElapsedTime(&ms, ev_a_, ev_b_));
+    stats_.kernel_ms = ms;
+    stats_.direct = 1;
+    stats_.chunks = 1;
+    stats_.h2d_bytes = (offsets[n] - offsets[0]) + (a.lengths8 ? n : 8 * n);
+    stats_.d2h_bytes = static_cast<int64_t>(fb) * n;
+    wall.stop();
+    stats_.total_ms = wall.total_ms();
+    return;
+  }
+  run_staged(codes, offsets, n, out, fmt);
+  wall.stop();
+  stats_.total_ms = wall.total_ms();
+}
+
+void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t n, void* out, ResultFormat fmt) {
+  const int fb = result_bytes(fmt);
+  ChunkPlan cp;
   double kernel_ms = 0;
   auto retire = [&](Slot& s) {
     if (!s.busy) return;
@@ -241,18 +416,33 @@ void HipEngine::solve(const uint8_t* codes, const int64_t* offsets, int64_t n, R
     const int64_t cn = re - rb;
     Slot& s = *slots_[chunk % 2];
     retire(s);
-    plan_chunk(offsets + rb, cn, hp);
-    stats_.cells += hp.cells;
-    const PlanLayout lay(hp.tiles.size(), hp.long_recs.size());
+    plan_chunk(offsets + rb, cn, cp);
+    stats_.cells += cp.cells;
+    // records that the short kernel cannot hold (LDS budget) go to the tile kernel too
+    dev::ShortArgs a;
+    a.fmt = static_cast<int32_t>(fmt);
+    bool short_ok = cp.n_short > 0 && dev::configure_short(L1_, cp.min_short, cp.max_l2, a);
+    if (cp.n_short > 0 && !short_ok) {
+      cp.long_recs.clear();
+      cp.tiles.clear();
+      for (int64_t i = 0; i < cn; ++i) cp.long_recs.push_back(static_cast<int32_t>(i));
+      for (size_t li = 0; li < cp.long_recs.size(); ++li) {
+        const int64_t L2 = offsets[rb + li + 1] - offsets[rb + li];
+        const int64_t need = dev::lanes_needed(L1_, L2);
+        for (int64_t o0 = 0; o0 < need; o0 += dev::kTileOffsets)
+          cp.tiles.push_back(dev::Tile{static_cast<int32_t>(li), static_cast<int32_t>(o0)});
+      }
+    }
+    const PlanLayout lay(cp.tiles.size(), cp.long_recs.size());
     const size_t cbytes = static_cast<size_t>(offsets[re] - offsets[rb]);
-    ensure(s.d_codes, s.d_codes_cap, std::max<size_t>(cbytes, 4));
+    ensure(s.d_codes, s.d_codes_cap, std::max<size_t>(cbytes, 16) + 32);
     ensure(s.d_offsets, s.d_offsets_cap, sizeof(int64_t) * static_cast<size_t>(cn + 1));
-    ensure(s.d_out, s.d_out_cap, sizeof(Result) * static_cast<size_t>(cn));
+    ensure(s.d_out, s.d_out_cap, static_cast<size_t>(fb) * static_cast<size_t>(cn));
     if (lay.total) {
       ensure(s.d_plan, s.d_plan_cap, lay.total);
-      ensure_host(s.h_plan, s.h_plan_cap, lay.upload_bytes);
-      std::memcpy(static_cast<char*>(s.h_plan) + lay.tiles_off, hp.tiles.data(), hp.tiles.size() * sizeof(dev::Tile));
-      std::memcpy(static_cast<char*>(s.h_plan) + lay.long_off, hp.long_recs.data(), hp.long_recs.size() * sizeof(int32_t));
+      ensure_host(s.h_plan, s.h_plan_cap, std::max<size_t>(lay.upload_bytes, 8));
+      std::memcpy(static_cast<char*>(s.h_plan) + lay.tiles_off, cp.tiles.data(), cp.tiles.size() * sizeof(dev::Tile));
+      std::memcpy(static_cast<char*>(s.h_plan) + lay.long_off, cp.long_recs.data(), cp.long_recs.size() * sizeof(int32_t));
     }
     // ---- copy stream: H2D
     if (cbytes) MOC_HIP_CHECK(hipMemcpyAsync(s.d_codes, codes + offsets[rb], cbytes, hipMemcpyHostToDevice, s_copy_));
@@ -263,53 +453,43 @@ void HipEngine::solve(const uint8_t* codes, const int64_t* offsets, int64_t n, R
     stats_.h2d_bytes += static_cast<int64_t>(cbytes + sizeof(int64_t) * (cn + 1) + lay.upload_bytes);
     // ---- compute stream
     MOC_HIP_CHECK(hipStreamWaitEvent(s_compute_, s.ev_h2d, 0));
-    dev::Plan plan;
-    plan.slot = hp.slot;
-    plan.rec_per_wave = hp.rpw;
-    plan.n_tiles = static_cast<int64_t>(hp.tiles.size());
-    plan.n_long = static_cast<int64_t>(hp.long_recs.size());
-    plan.tiles = reinterpret_cast<const dev::Tile*>(static_cast<char*>(s.d_plan) + lay.tiles_off);
-    plan.long_recs = reinterpret_cast<const int32_t*>(static_cast<char*>(s.d_plan) + lay.long_off);
-    plan.keys = reinterpret_cast<unsigned long long*>(static_cast<char*>(s.d_plan) + lay.keys_off);
-    dev::BatchView bv{static_cast<const uint8_t*>(s.d_codes), static_cast<const int64_t*>(s.d_offsets), cn};
-    int* d_dbg = nullptr;
-    const char* dbg_env = std::getenv("MOC_DEBUG_TILE");
-    if (dbg_env) {
-      MOC_HIP_CHECK(hipMalloc(&d_dbg, 4096));
-      std::vector<int> init(1024, 0);
-      init[0] = std::atoi(dbg_env);
-      MOC_HIP_CHECK(hipMemcpy(d_dbg, init.data(), 4096, hipMemcpyHostToDevice));
-      plan.debug = d_dbg;
-    }
     MOC_HIP_CHECK(hipEventRecord(s.ev_k0, s_compute_));
-    dev::launch_search(problem_view(hp.max_l2), bv, plan, static_cast<Result*>(s.d_out), s_compute_);
-    if (d_dbg) {
-      std::vector<int> h(1024);
-      MOC_HIP_CHECK(hipStreamSynchronize(s_compute_));
-      MOC_HIP_CHECK(hipMemcpy(h.data(), d_dbg, 4096, hipMemcpyDeviceToHost));
-      std::fprintf(stderr, "DBG tile=%d L2=%d o0=%d r=%d codes=%d,%d,%d,%d,%d,%d,%d,%d key0=%08x%08x\n", h[0], h[1], h[2],
-                   h[3], h[8], h[9], h[10], h[11], h[12], h[13], h[14], h[15], h[16], h[17]);
-      for (int l = 0; l < 64; ++l)
-        std::fprintf(stderr, "DBG lane %d P=%d best=%d Pn=%d x=%d\n", l, h[64 + 4 * l], h[65 + 4 * l], h[66 + 4 * l],
-                     h[67 + 4 * l]);
-      (void)hipFree(d_dbg);
+    const dev::ProblemView pv = problem_view(cp.max_l2);
+    const uint8_t* dcodes = static_cast<const uint8_t*>(s.d_codes);
+    const int64_t* doffs = static_cast<const int64_t*>(s.d_offsets);
+    if (short_ok) {
+      a.codes = dcodes - offsets[rb];  // base: record i at base + offsets[i] (absolute offsets)
+      a.offsets = doffs;
+      a.lengths8 = nullptr;
+      a.n = cn;
+      a.out = s.d_out;
+      a.counter = s.d_counter;
+      dev::launch_short(pv, a, num_cus_, s_compute_);
+    }
+    if (!cp.tiles.empty()) {
+      dev::Plan plan;
+      plan.n_tiles = static_cast<int64_t>(cp.tiles.size());
+      plan.n_long = static_cast<int64_t>(cp.long_recs.size());
+      plan.tiles = reinterpret_cast<const dev::Tile*>(static_cast<char*>(s.d_plan) + lay.tiles_off);
+      plan.long_recs = reinterpret_cast<const int32_t*>(static_cast<char*>(s.d_plan) + lay.long_off);
+      plan.keys = reinterpret_cast<unsigned long long*>(static_cast<char*>(s.d_plan) + lay.keys_off);
+      dev::BatchView bv{dcodes, doffs, cn};
+      dev::launch_tiles(pv, bv, plan, s.d_out, static_cast<int>(fmt), s_compute_);
     }
     MOC_HIP_CHECK(hipGetLastError());
     MOC_HIP_CHECK(hipEventRecord(s.ev_k1, s_compute_));
     // ---- return stream: D2H straight into the caller's result array
     MOC_HIP_CHECK(hipStreamWaitEvent(s_return_, s.ev_k1, 0));
-    MOC_HIP_CHECK(hipMemcpyAsync(out + rb, s.d_out, sizeof(Result) * cn, hipMemcpyDeviceToHost, s_return_));
+    MOC_HIP_CHECK(hipMemcpyAsync(static_cast<char*>(out) + rb * fb, s.d_out, static_cast<size_t>(fb) * cn,
+                                 hipMemcpyDeviceToHost, s_return_));
     MOC_HIP_CHECK(hipEventRecord(s.ev_done, s_return_));
-    stats_.d2h_bytes += static_cast<int64_t>(sizeof(Result) * cn);
+    stats_.d2h_bytes += static_cast<int64_t>(fb) * cn;
     s.busy = true;
     rb = re;
   }
   for (auto& s : slots_) retire(*s);
-  wall.stop();
   stats_.kernel_ms = kernel_ms;
-  stats_.total_ms = wall.total_ms();
   stats_.chunks = chunk;
-  stats_.records = n;
 }
 
 void HipEngine::solve_device(const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets, int64_t n,
@@ -318,30 +498,53 @@ void HipEngine::solve_device(const uint8_t* d_codes, const int64_t* d_offsets, c
   MOC_HIP_CHECK(hipSetDevice(device_));
   if (n <= 0) return;
   if (!stream) stream = s_compute_;
-  HostPlan hp;
-  plan_chunk(h_offsets, n, hp);
-  const PlanLayout lay(hp.tiles.size(), hp.long_recs.size());
+  ChunkPlan cp;
+  plan_chunk(h_offsets, n, cp);
+  dev::ShortArgs a;
+  a.fmt = static_cast<int32_t>(ResultFormat::R12);
+  bool short_ok = cp.n_short > 0 && dev::configure_short(L1_, cp.min_short, cp.max_l2, a);
+  if (cp.n_short > 0 && !short_ok) {  // everything through the tile kernel
+    cp.long_recs.clear();
+    cp.tiles.clear();
+    for (int64_t i = 0; i < n; ++i) cp.long_recs.push_back(static_cast<int32_t>(i));
+    for (size_t li = 0; li < cp.long_recs.size(); ++li) {
+      const int64_t need = dev::lanes_needed(L1_, h_offsets[li + 1] - h_offsets[li]);
+      for (int64_t o0 = 0; o0 < need; o0 += dev::kTileOffsets)
+        cp.tiles.push_back(dev::Tile{static_cast<int32_t>(li), static_cast<int32_t>(o0)});
+    }
+  }
+  const PlanLayout lay(cp.tiles.size(), cp.long_recs.size());
   MOC_HIP_CHECK(hipEventSynchronize(ev_plan_));  // previous call's plan buffers are free again
   if (lay.total) {
     ensure(d_plan_, d_plan_cap_, lay.total);
-    ensure_host(h_plan_, h_plan_cap_, lay.upload_bytes);
-    std::memcpy(static_cast<char*>(h_plan_) + lay.tiles_off, hp.tiles.data(), hp.tiles.size() * sizeof(dev::Tile));
-    std::memcpy(static_cast<char*>(h_plan_) + lay.long_off, hp.long_recs.data(), hp.long_recs.size() * sizeof(int32_t));
+    ensure_host(h_plan_, h_plan_cap_, std::max<size_t>(lay.upload_bytes, 8));
+    std::memcpy(static_cast<char*>(h_plan_) + lay.tiles_off, cp.tiles.data(), cp.tiles.size() * sizeof(dev::Tile));
+    std::memcpy(static_cast<char*>(h_plan_) + lay.long_off, cp.long_recs.data(), cp.long_recs.size() * sizeof(int32_t));
     MOC_HIP_CHECK(hipMemcpyAsync(d_plan_, h_plan_, lay.upload_bytes, hipMemcpyHostToDevice, stream));
   }
-  dev::Plan plan;
-  plan.slot = hp.slot;
-  plan.rec_per_wave = hp.rpw;
-  plan.n_tiles = static_cast<int64_t>(hp.tiles.size());
-  plan.n_long = static_cast<int64_t>(hp.long_recs.size());
-  plan.tiles = reinterpret_cast<const dev::Tile*>(static_cast<char*>(d_plan_) + lay.tiles_off);
-  plan.long_recs = reinterpret_cast<const int32_t*>(static_cast<char*>(d_plan_) + lay.long_off);
-  plan.keys = reinterpret_cast<unsigned long long*>(static_cast<char*>(d_plan_) + lay.keys_off);
-  dev::BatchView bv{d_codes + h_offsets[0], d_offsets, n};
-  dev::launch_search(problem_view(hp.max_l2), bv, plan, d_out, stream);
+  const dev::ProblemView pv = problem_view(cp.max_l2);
+  if (short_ok) {
+    a.codes = d_codes;
+    a.offsets = d_offsets;
+    a.n = n;
+    a.out = d_out;
+    a.counter = d_counter_;
+    dev::launch_short(pv, a, num_cus_, stream);
+  }
+  if (!cp.tiles.empty()) {
+    dev::Plan plan;
+    plan.n_tiles = static_cast<int64_t>(cp.tiles.size());
+    plan.n_long = static_cast<int64_t>(cp.long_recs.size());
+    plan.tiles = reinterpret_cast<const dev::Tile*>(static_cast<char*>(d_plan_) + lay.tiles_off);
+    plan.long_recs = reinterpret_cast<const int32_t*>(static_cast<char*>(d_plan_) + lay.long_off);
+    plan.keys = reinterpret_cast<unsigned long long*>(static_cast<char*>(d_plan_) + lay.keys_off);
+    dev::BatchView bv{d_codes + h_offsets[0], d_offsets, n};
+    dev::launch_tiles(pv, bv, plan, d_out, static_cast<int>(ResultFormat::R12), stream);
+  }
   MOC_HIP_CHECK(hipGetLastError());
   MOC_HIP_CHECK(hipEventRecord(ev_plan_, stream));
-  stats_.cells = hp.cells;
+  stats_ = EngineStats{};
+  stats_.cells = cp.cells;
   stats_.records = n;
 }
 

@@ -16,6 +16,11 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libmoc.so")
 
 RESULT_DTYPE = np.dtype([("score", "<i4"), ("n", "<i4"), ("k", "<i4")])
+# Packed result wire formats (moc/device.hpp ResultFormat): index = format id.
+R8_DTYPE = np.dtype([("score", "<i4"), ("n", "<u2"), ("k", "<u2")])
+R4_DTYPE = np.dtype([("score", "<i2"), ("n", "u1"), ("k", "u1")])
+FORMAT_DTYPES = [RESULT_DTYPE, R8_DTYPE, R4_DTYPE]
+FORMAT_NAMES = ["r12", "r8", "r4"]
 
 _lib = None
 
@@ -51,6 +56,11 @@ def _decl(lib):
         "moc_engine_destroy": (None, [c_void_p]),
         "moc_engine_set_problem": (c_int, [c_void_p, P(c_int32), c_void_p, c_int64, c_int]),
         "moc_engine_solve": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
+        "moc_engine_solve_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_int64,
+                                        c_int64]),
+        "moc_engine_auto_format": (c_int, [c_void_p, c_int64]),
+        "moc_engine_pin": (c_int, [c_void_p, c_void_p, c_size_t]),
+        "moc_expand_results": (c_int, [c_void_p, c_int, c_int64, c_void_p]),
         "moc_engine_solve_device": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
         "moc_engine_stats": (c_int, [c_void_p, P(c_double)]),
     }

@@ -25,8 +25,16 @@ def empty_results(n: int) -> np.ndarray:
 
 
 def as_triples(results: np.ndarray) -> np.ndarray:
-    """Structured results -> (n, 3) int32 view [score, n, k]."""
-    return results.view(np.int32).reshape(-1, 3)
+    """Results in any wire format (R12/R8/R4 structured, or (n,3) ints) -> (n, 3) int32 [score, n, k]."""
+    r = np.asarray(results)
+    if r.dtype == RESULT_DTYPE:
+        return r.view(np.int32).reshape(-1, 3)
+    if r.dtype.names:
+        score = r["score"].astype(np.int32)
+        if r.dtype == _lib.R4_DTYPE:
+            score[r["score"] == np.iinfo(np.int16).min] = np.iinfo(np.int32).min
+        return np.stack([score, r["n"].astype(np.int32), r["k"].astype(np.int32)], axis=1)
+    return np.asarray(r, dtype=np.int32).reshape(-1, 3)
 
 
 # ---------------------------------------------------------------------------------------------- CPU
@@ -67,16 +75,26 @@ def device_info(device: int = 0) -> dict:
     return json.loads(buf.value.decode())
 
 
+def _format_id(fmt) -> int:
+    if isinstance(fmt, (int, np.integer)):
+        return int(fmt)
+    return _lib.FORMAT_NAMES.index(str(fmt).lower())
+
+
 class HipSearchEngine:
-    """Per-rank gfx950 engine: problem upload, host planning, chunked H2D/compute/D2H pipeline."""
+    """Per-rank gfx950 engine: problem upload, planning, and host<->device data movement.
+
+    ``solve`` picks the zero-copy streaming path automatically when every host buffer is pinned
+    (``pin`` / ``_lib.Pinned`` / hipHostMalloc) and all records fit the short kernel; otherwise it runs
+    the staged double-buffered chunk pipeline (csrc/src/hip_engine.cpp)."""
 
     def __init__(self, device: Optional[int] = None, chunk_records: int = 0, chunk_bytes: int = 0,
-                 pin_host: bool = True):
+                 allow_direct: bool = True):
         L = _lib.lib()
         if L.moc_device_count() <= 0:
             raise _lib.NativeError("HipSearchEngine needs a visible HIP device (none found)")
         self._h = L.moc_engine_create(-1 if device is None else int(device), int(chunk_records), int(chunk_bytes),
-                                      1 if pin_host else 0)
+                                      1 if allow_direct else 0)
         if not self._h:
             raise _lib.NativeError(L.moc_last_error().decode())
         self.problem_L1 = None
@@ -99,14 +117,36 @@ class HipSearchEngine:
             int(Semantics.parse(semantics))))
         self.problem_L1 = int(seq1.shape[0])
 
-    def solve(self, codes: np.ndarray, offsets: np.ndarray, out: Optional[np.ndarray] = None) -> np.ndarray:
-        """Host CSR -> host results (pinned DMA, double-buffered chunks). ``codes[offsets[i]:offsets[i+1]]``
-        is record i; ``offsets`` may be a slice of a larger absolute offset array."""
+    def pin(self, *arrays):
+        """Page-locks host arrays for the engine's lifetime (enables the zero-copy path)."""
+        for a in arrays:
+            if a is not None and a.nbytes:
+                _lib.check(_lib.lib().moc_engine_pin(self._h, ctypes.c_void_p(a.ctypes.data), a.nbytes))
+
+    def auto_format(self, max_l2: int) -> str:
+        return _lib.FORMAT_NAMES[_lib.lib().moc_engine_auto_format(self._h, int(max_l2))]
+
+    def solve(self, codes: np.ndarray, offsets: np.ndarray, out: Optional[np.ndarray] = None,
+              lengths: Optional[np.ndarray] = None, fmt="r12", l2_range=None) -> np.ndarray:
+        """Host CSR -> host results. ``codes[offsets[i]:offsets[i+1]]`` is record i (``offsets`` may be a
+        slice of a larger absolute offset array). ``fmt``: r12 | r8 | r4 | auto (smallest that fits);
+        ``lengths``: optional uint8 record lengths; ``l2_range``: optional known (min, max) length."""
         offsets = np.ascontiguousarray(offsets, dtype=np.int64)
         n = offsets.shape[0] - 1
+        if l2_range is None and (fmt == "auto"):
+            L2 = np.diff(offsets) if n else np.zeros(1, np.int64)
+            l2_range = (int(L2.min()) if n else 0, int(L2.max()) if n else 0)
+        if fmt == "auto":
+            fmt = self.auto_format(l2_range[1])
+        fid = _format_id(fmt)
         if out is None:
-            out = empty_results(n)
-        _lib.check(_lib.lib().moc_engine_solve(self._h, _lib.ptr(codes), _lib.ptr(offsets), n, _lib.ptr(out)))
+            out = np.empty(n, dtype=_lib.FORMAT_DTYPES[fid])
+        assert out.dtype.itemsize == _lib.FORMAT_DTYPES[fid].itemsize and out.size >= n
+        if lengths is not None:
+            assert lengths.dtype == np.uint8 and lengths.shape[0] >= n
+        lo, hi = l2_range if l2_range is not None else (-1, -1)
+        _lib.check(_lib.lib().moc_engine_solve_ex(self._h, _lib.ptr(codes), _lib.ptr(offsets), _lib.ptr(lengths), n,
+                                                  _lib.ptr(out), fid, int(lo), int(hi)))
         return out
 
     def solve_device(self, codes_t, offsets_t, h_offsets: np.ndarray, out_t, stream=None):
@@ -127,10 +167,12 @@ class HipSearchEngine:
         return out_t
 
     def stats(self) -> dict:
-        v = (ctypes.c_double * 7)()
+        v = (ctypes.c_double * 9)()
         _lib.check(_lib.lib().moc_engine_stats(self._h, v))
-        keys = ["kernel_ms", "total_ms", "h2d_bytes", "d2h_bytes", "chunks", "cells", "records"]
-        return dict(zip(keys, list(v)))
+        keys = ["kernel_ms", "total_ms", "h2d_bytes", "d2h_bytes", "chunks", "cells", "records", "direct", "format"]
+        d = dict(zip(keys, list(v)))
+        d["format"] = _lib.FORMAT_NAMES[int(d["format"])]
+        return d
 
 
 def search_hip(problem: Problem, semantics=Semantics.REFERENCE, device: Optional[int] = None,

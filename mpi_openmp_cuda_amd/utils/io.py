@@ -10,9 +10,11 @@ from .. import _lib
 
 def format_results(results: np.ndarray, first_index: int = 0) -> str:
     """Native parallel formatter (csrc/src/io.cpp). ``results`` is a RESULT_DTYPE array or (n, 3) ints."""
+    from ..ops.align import as_triples
+
     r = np.ascontiguousarray(results)
     if r.dtype != _lib.RESULT_DTYPE:
-        r = np.ascontiguousarray(np.asarray(r, dtype=np.int32).reshape(-1, 3)).view(_lib.RESULT_DTYPE).reshape(-1)
+        r = np.ascontiguousarray(as_triples(r)).view(_lib.RESULT_DTYPE).reshape(-1)
     n = r.shape[0]
     cap = 96 * n + 16
     buf = np.empty(cap, np.uint8)

@@ -105,6 +105,42 @@ def test_chunked_pipeline():
     eng.close()
 
 
+@pytest.mark.parametrize("fmt", ["r12", "r8", "r4"])
+@pytest.mark.parametrize("use_lengths", [False, True])
+def test_zero_copy_direct(fmt, use_lengths):
+    # pinned host buffers + short records -> one streaming kernel reading/writing host memory
+    prob = make_synthetic("input6", 300_001, seed=21)
+    eng = HipSearchEngine(device=0)
+    eng.set_problem(prob.weights, prob.seq1)
+    from mpi_openmp_cuda_amd import _lib
+
+    out = np.zeros(prob.n, dtype=_lib.FORMAT_DTYPES[_lib.FORMAT_NAMES.index(fmt)])
+    lengths = np.diff(prob.offsets).astype(np.uint8) if use_lengths else None
+    eng.pin(prob.codes, prob.offsets, out, lengths)
+    eng.solve(prob.codes, prob.offsets, out=out, lengths=lengths, fmt=fmt)
+    assert eng.stats()["direct"] == 1
+    assert np.array_equal(as_triples(out), as_triples(search_cpu(prob)))
+    eng.close()
+
+
+@pytest.mark.parametrize("fmt", ["r8", "r4", "auto"])
+def test_staged_formats(engine, fmt):
+    prob = make_synthetic("input1", 5000, seed=4)
+    engine.set_problem(prob.weights, prob.seq1)
+    got = engine.solve(prob.codes, prob.offsets, fmt=fmt)
+    assert engine.stats()["direct"] == 0
+    assert np.array_equal(as_triples(got), as_triples(search_cpu(prob)))
+
+
+def test_short_config_fallback(engine):
+    # records far longer than Seq1 blow the short kernel's LDS tile budget -> everything via tiles
+    rng = np.random.default_rng(9)
+    s1 = "".join(chr(65 + x) for x in rng.integers(0, 26, 30))
+    recs = ["".join(chr(65 + x) for x in rng.integers(0, 26, n)) for n in (70000, 20, 29, 30, 31, 5)]
+    prob = Problem.from_strings([3, 1, 2, 1], s1, recs)
+    check(engine, prob)
+
+
 def test_device_resident_torch(engine):
     prob = make_synthetic("input4", 64, seed=2)
     engine.set_problem(prob.weights, prob.seq1)
