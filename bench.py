@@ -41,6 +41,7 @@ def parse_args():
     ap.add_argument("--shm", type=int, default=1, help="1: node-shared /dev/shm arrays; 0: private pinned")
     ap.add_argument("--verify", type=int, default=20000, help="records per rank checked against the CPU engine")
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, default) | gloo (multi-rank rehearsal)")
     return ap.parse_args()
 
 
@@ -97,15 +98,24 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    gpu = local_rank % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     distributed = world > 1
+    nccl = args.dist_backend == "nccl"
+    cdev = dev if nccl else torch.device("cpu")  # where collective tensors live
     if distributed:
-        dist.init_process_group("nccl", device_id=dev)
+        if nccl:
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     def barrier():
         if distributed:
-            dist.barrier(device_ids=[local_rank])
+            if nccl:
+                dist.barrier(device_ids=[gpu])
+            else:
+                dist.barrier()
         torch.cuda.synchronize(dev)
 
     shape = SHAPES[args.shape]
@@ -113,7 +123,7 @@ def main():
     rng = np.random.default_rng(args.seed)
     seq1 = rng.integers(1, 27, size=shape.L1, dtype=np.uint8)
     weights = np.array(shape.weights, dtype=np.int32)
-    header = torch.from_numpy(np.concatenate([weights, seq1.astype(np.int32)])).to(dev)
+    header = torch.from_numpy(np.concatenate([weights, seq1.astype(np.int32)])).to(cdev)
     R = args.records_per_gpu
     rrng = np.random.default_rng(args.seed + 1 + rank)
     lengths = rrng.integers(shape.l2_min, shape.l2_max + 1, size=R, dtype=np.int64)
@@ -121,7 +131,7 @@ def main():
     host = HostArrays(tag, rank, lengths, bool(args.shm))
     fill_codes(host.codes, args.seed + 101 + rank)
     del lengths
-    eng = HipSearchEngine(device=local_rank)
+    eng = HipSearchEngine(device=gpu)
     eng.set_problem(weights, seq1)
     fmt = eng.auto_format(shape.l2_max)
     from mpi_openmp_cuda_amd import _lib
@@ -134,7 +144,7 @@ def main():
     else:
         host.results = np.empty(R, dtype=rdt)
     pin = Pinned(host.codes, host.offsets, host.lengths, host.results)
-    done = torch.zeros(1, dtype=torch.int64, device=dev)
+    done = torch.zeros(1, dtype=torch.int64, device=cdev)
     hdr_host = np.empty(4 + shape.L1, dtype=np.int32)
 
     def step():
@@ -156,7 +166,7 @@ def main():
         step()
     barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
     if distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
@@ -169,14 +179,14 @@ def main():
         sub = Problem(shape.weights, seq1, host.codes[:int(host.offsets[nv])], host.offsets[:nv + 1].copy())
         ref = as_triples(search_cpu(sub))
         ok = int(np.array_equal(as_triples(host.results[:nv]), ref))
-    okt = torch.tensor([ok], dtype=torch.int32, device=dev)
+    okt = torch.tensor([ok], dtype=torch.int32, device=cdev)
     if distributed:
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
 
     total_records = R * world
     total_elems = int(host.offsets[-1]) * world  # per-rank chars ~ equal (same length distribution)
     if distributed:
-        te = torch.tensor([int(host.offsets[-1])], dtype=torch.int64, device=dev)
+        te = torch.tensor([int(host.offsets[-1])], dtype=torch.int64, device=cdev)
         dist.all_reduce(te)
         total_elems = int(te.item())
     ms_per_step = elapsed / args.steps * 1e3
@@ -217,7 +227,7 @@ def main():
         print(json.dumps(out), flush=True)
     pin.release()
     if distributed:
-        dist.barrier(device_ids=[local_rank])
+        barrier()
         dist.destroy_process_group()
     host.cleanup()
 
