@@ -65,8 +65,8 @@ int moc_engine_pin(void* e, const void* p, size_t bytes);
 int moc_expand_results(const void* in, int fmt, int64_t n, moc_result* out);
 int moc_engine_solve_device(void* e, const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets,
                             int64_t n, moc_result* d_out, void* stream);
-/* stats: kernel_ms, total_ms, h2d_bytes, d2h_bytes, chunks, cells, records, direct, format */
-int moc_engine_stats(void* e, double* out9);
+/* stats: kernel_ms, total_ms, h2d_bytes, d2h_bytes, chunks, cells, records, direct, format, kernels */
+int moc_engine_stats(void* e, double* out10);
 
 #ifdef __cplusplus
 }

@@ -106,6 +106,11 @@ inline int64_t lanes_needed(int64_t L1, int64_t L2) { return L2 <= L1 ? L1 - L2 
 // it (a record needs more than 64 lanes). Fills slot/rpw/tile_records/codes_cap.
 bool configure_short(int64_t L1, int64_t min_l2, int64_t max_l2, ShortArgs& a);
 
+// Inter-record SIMD kernel (one lane per record, packed int16; swipe_kernels.hip) for tiny problems:
+// returns false unless every record fits (|Seq1| <= 200, |Seq2| <= 32, int16-exact weights).
+bool configure_swipe(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs_weight, ShortArgs& a);
+void launch_swipe(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStream_t stream);
+
 // Short-record kernel (all records with lanes_needed <= a.slot are processed; others are skipped).
 void launch_short(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStream_t stream);
 

@@ -43,6 +43,7 @@ struct EngineStats {
   int64_t h2d_bytes = 0, d2h_bytes = 0, chunks = 0, cells = 0, records = 0;
   int32_t direct = 0;    // 1 if the last solve used the zero-copy streaming path
   int32_t format = 0;    // ResultFormat of the last solve
+  int32_t kernels = 0;   // bitmask of kernels used: 1 swipe (lane/record), 2 short (lane/offset), 4 tiles
 };
 
 // Optional metadata about a batch (e.g. known from parsing / generation) that lets the engine skip its

@@ -231,18 +231,19 @@ int moc_engine_solve_device(void* e, const uint8_t* d_codes, const int64_t* d_of
   });
 }
 
-int moc_engine_stats(void* e, double* out9) {
+int moc_engine_stats(void* e, double* out10) {
   return guard([&] {
     const auto& s = static_cast<moc::HipEngine*>(e)->stats();
-    out9[0] = s.kernel_ms;
-    out9[1] = s.total_ms;
-    out9[2] = static_cast<double>(s.h2d_bytes);
-    out9[3] = static_cast<double>(s.d2h_bytes);
-    out9[4] = static_cast<double>(s.chunks);
-    out9[5] = static_cast<double>(s.cells);
-    out9[6] = static_cast<double>(s.records);
-    out9[7] = static_cast<double>(s.direct);
-    out9[8] = static_cast<double>(s.format);
+    out10[0] = s.kernel_ms;
+    out10[1] = s.total_ms;
+    out10[2] = static_cast<double>(s.h2d_bytes);
+    out10[3] = static_cast<double>(s.d2h_bytes);
+    out10[4] = static_cast<double>(s.chunks);
+    out10[5] = static_cast<double>(s.cells);
+    out10[6] = static_cast<double>(s.records);
+    out10[7] = static_cast<double>(s.direct);
+    out10[8] = static_cast<double>(s.format);
+    out10[9] = static_cast<double>(s.kernels);
   });
 }
 

@@ -1,0 +1,320 @@
+// Inter-record SIMD kernel for tiny problems (input6-shaped: |Seq1| <= ~100, |Seq2| <= 32, small W).
+//
+// One LANE = one whole record (vs. one lane per offset in short_kernels.hip): every lane keeps all its
+// offsets' running diagonal sums P_o in registers as packed int16 pairs, so
+//   * no cross-lane traffic at all in the hot loop (no DPP, no segmented reductions per record),
+//   * two cells per VALU op (v_pk_add_u16 / v_pk_sub_u16 / v_pk_mad_u16 / v_pk_max_i16),
+//   * the profile row segment S[c][i .. i+NOFF) a lane needs at step i is read with NOFF/8 aligned
+//     ds_read_b128: the block keeps 8 copies of the int16 profile, copy s shifted left by s columns, so
+//     step i reads copy (i mod 8) at column i - (i mod 8) (a multiple of 8 -> 16-byte aligned).
+// Per step and per pair of offsets (2m, 2m+1):
+//     P2[m]  += (S[c][i+2m], S[c][i+2m+1])                         v_pk_add_u16
+//     D2      = P2[m] - (P_{2m+1}, P_{2m+2})                        v_alignbit + v_pk_sub_u16
+//     B2[m]   = max(B2[m], D2 * 2^ks + (mask - (i+1)))             v_pk_mad_u16 + v_pk_max_i16
+// i.e. ~2.5 VALU ops per cell. Records stream through the same persistent, LDS-tiled block loop as the
+// short kernel (zero-copy from pinned host memory when the batch lives there).
+// Exactness: int16 arithmetic is exact because the host only selects this kernel when
+// 2*max|W|*max|Seq2|*2^ks + mask < 2^15 (no key can wrap) — see configure_swipe.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "kernel_common.hpp"
+
+namespace moc {
+namespace dev {
+
+using namespace kc;
+
+namespace {
+constexpr int kBlock = 256;
+constexpr int kMaxTile = 1024;
+constexpr int kLdsBudget = 60 * 1024;
+
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ s16x2 as_s16x2(uint32_t v) { return __builtin_bit_cast(s16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+struct SwipeLayout {
+  int row = 0;          // profile row length (int16 entries), multiple of 8
+  int copy_elems = 0;   // 27 * row
+  int prof_bytes = 0;
+  int loff_off = 0, codes_off = 0, res_off = 0, total = 0;
+};
+
+inline int al16(int x) { return (x + 15) & ~15; }
+
+SwipeLayout swipe_layout(int L1, int noff, int l2w, int tile_records, int codes_cap, int fb) {
+  SwipeLayout l;
+  l.row = (std::max(L1, 4 * l2w) + noff + 8 + 7) & ~7;
+  l.copy_elems = kAlphabet * l.row;
+  l.prof_bytes = al16(8 * l.copy_elems * 2);
+  l.loff_off = l.prof_bytes;
+  l.codes_off = l.loff_off + al16((tile_records + 1) * 4 + 32);
+  l.res_off = l.codes_off + al16(codes_cap);
+  l.total = l.res_off + al16(tile_records * fb);
+  return l;
+}
+
+inline int kbits_for(int l2w) {  // bits for k in the int16 keys: k <= 4*l2w
+  int b = 1;
+  while ((1 << b) <= 4 * l2w) ++b;
+  return b;
+}
+}  // namespace
+
+template <int NOFF, int L2W>
+__global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, ShortArgs a, SwipeLayout lay) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  short* prof = reinterpret_cast<short*>(smem);
+  int* loff = reinterpret_cast<int*>(smem + lay.loff_off);
+  int* misc = loff + a.tile_records + 1;
+  uint8_t* codes_l = smem + lay.codes_off;
+  uint8_t* res_l = smem + lay.res_off;
+  const int L1 = pv.L1;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int KB = (4 * L2W < 8) ? 3 : (4 * L2W < 16) ? 4 : (4 * L2W < 32) ? 5 : (4 * L2W < 64) ? 6 : 7;
+  constexpr int KMASK = (1 << KB) - 1;
+  constexpr int NP = NOFF / 2;  // packed accumulators
+
+  // ---- 8 shifted int16 profile copies: prof[s][c][j] = S[c][j + s] (row 0 and j >= L1: 0)
+  {
+    const int row = lay.row, ce = lay.copy_elems;
+    for (int e = tid; e < 8 * ce; e += kBlock) {
+      const int s = e / ce, rem = e - s * ce, c = rem / row, j = rem - c * row + s;
+      prof[e] = static_cast<short>((c >= 1 && j < L1) ? pv.lut[c * kLutStride + pv.seq1[j]] : 0);
+    }
+  }
+  const int fb = a.fmt == static_cast<int>(ResultFormat::R4) ? 4 : a.fmt == static_cast<int>(ResultFormat::R8) ? 8 : 12;
+  const int64_t n_tiles = (a.n + a.tile_records - 1) / a.tile_records;
+  const int sem = pv.semantics;
+
+  for (;;) {
+    __syncthreads();
+    if (tid == 0) misc[0] = static_cast<int>(atomicAdd(a.counter, 1u));
+    __syncthreads();
+    const int64_t t = misc[0];
+    if (t >= n_tiles) break;
+    const int64_t rb = t * a.tile_records;
+    const int m = static_cast<int>(min(static_cast<int64_t>(a.tile_records), a.n - rb));
+    const int64_t start = a.offsets[rb];
+    const int64_t end = a.offsets[rb + m];
+
+    // ---- lengths -> block exclusive scan -> loff[0..m]
+    int len4[4];
+    int sum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = tid * 4 + q;
+      int L = 0;
+      if (r < m) L = a.lengths8 ? static_cast<int>(a.lengths8[rb + r]) : static_cast<int>(a.offsets[rb + r + 1] - a.offsets[rb + r]);
+      len4[q] = L;
+      sum += L;
+    }
+    const int incl = wave_inclusive_sum(sum, lane);
+    if (lane == 63) misc[4 + wave] = incl;
+    __syncthreads();
+    int excl = incl - sum;
+    for (int w = 0; w < wave; ++w) excl += misc[4 + w];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = tid * 4 + q;
+      if (r < m) loff[r] = excl;
+      excl += len4[q];
+    }
+    if (tid == kBlock - 1) loff[m] = excl;
+
+    // ---- letters -> LDS (16-byte loads)
+    const uintptr_t p0 = reinterpret_cast<uintptr_t>(a.codes + start);
+    const uintptr_t a0 = p0 & ~uintptr_t{15};
+    const int shift_b = static_cast<int>(p0 - a0);
+    const int nvec = static_cast<int>((reinterpret_cast<uintptr_t>(a.codes + end) + 15 - a0) >> 4);
+    for (int v = tid; v < nvec; v += kBlock)
+      reinterpret_cast<uint4*>(codes_l)[v] = reinterpret_cast<const uint4*>(a0)[v];
+    __syncthreads();
+
+    // ---- one record per lane
+    for (int g = wave; g * 64 < m; g += 4) {
+      const int rl = g * 64 + lane;
+      const bool in = rl < m;
+      int L2 = 0, rs = 0;
+      if (in) {
+        rs = shift_b + loff[rl];
+        L2 = loff[rl + 1] - loff[rl];
+      }
+      const int need = L2 <= L1 ? L1 - L2 + 1 : 1;
+      const bool mine = in && need <= NOFF;  // others belong to the tile kernel (mixed batches)
+      const bool on = mine && L2 <= L1;
+      // record letters -> L2W aligned words (bytes past the record end zeroed: they add row 0 = 0)
+      uint32_t wd[L2W];
+      {
+        const uint32_t* l32 = reinterpret_cast<const uint32_t*>(codes_l);
+        const int wb = rs >> 2, sh = (rs & 3) * 8;
+        uint32_t prev = on ? l32[wb] : 0u;
+#pragma unroll
+        for (int k = 0; k < L2W; ++k) {
+          const uint32_t nxt = on ? l32[wb + k + 1] : 0u;
+          uint32_t w = sh ? ((prev >> sh) | (nxt << (32 - sh))) : prev;
+          const int left = L2 - 4 * k;  // bytes of the record in this word
+          w = left >= 4 ? w : (left <= 0 ? 0u : (w & ((1u << (8 * left)) - 1u)));
+          wd[k] = on ? w : 0u;
+          prev = nxt;
+        }
+      }
+      const int steps = wave_max_i32(on ? L2 : 0);
+
+      uint32_t P2[NP], B2[NP];
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        P2[q] = 0u;
+        B2[q] = 0x80008000u;  // (INT16_MIN, INT16_MIN)
+      }
+#pragma unroll
+      for (int i0 = 0; i0 < 4 * L2W; i0 += 8) {
+        if (i0 >= steps) break;  // wave-uniform
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const int i = i0 + s;
+          const int c = (wd[i >> 2] >> (8 * (i & 3))) & 0xff;
+          const uint4* rowp = reinterpret_cast<const uint4*>(prof + s * lay.copy_elems + c * lay.row + i0);
+          uint32_t v[NP];
+#pragma unroll
+          for (int q = 0; q < NOFF / 8; ++q) {
+            const uint4 x = rowp[q];
+            v[4 * q + 0] = x.x;
+            v[4 * q + 1] = x.y;
+            v[4 * q + 2] = x.z;
+            v[4 * q + 3] = x.w;
+          }
+#pragma unroll
+          for (int q = 0; q < NP; ++q) P2[q] = as_u32(as_s16x2(P2[q]) + as_s16x2(v[q]));
+          const short kc = static_cast<short>(KMASK - (i + 1));
+          const s16x2 kadd = {kc, kc};
+          const s16x2 kmul = {static_cast<short>(1 << KB), static_cast<short>(1 << KB)};
+#pragma unroll
+          for (int q = 0; q < NP; ++q) {
+            const uint32_t nxt = q + 1 < NP ? P2[q + 1] : 0u;
+            const uint32_t Q = __builtin_amdgcn_alignbit(nxt, P2[q], 16);  // (P_{2q+1}, P_{2q+2})
+            const s16x2 D = as_s16x2(P2[q]) - as_s16x2(Q);
+            const s16x2 K = D * kmul + kadd;
+            B2[q] = as_u32(__builtin_elementwise_max(as_s16x2(B2[q]), K));
+          }
+        }
+      }
+
+      // ---- per-lane selection over the record's offsets: 32-bit keys (score+2^15 | ~(o<<KB | k))
+      const int last = L1 - L2;
+      uint32_t best = 0;
+#pragma unroll
+      for (int o = 0; o < NOFF; ++o) {
+        const int Po = static_cast<short>(o & 1 ? (P2[o >> 1] >> 16) : (P2[o >> 1] & 0xffff));
+        const int o1 = o + 1;
+        const int Pn = o1 < NOFF ? static_cast<short>(o1 & 1 ? (P2[o1 >> 1] >> 16) : (P2[o1 >> 1] & 0xffff)) : 0;
+        const int bk = static_cast<short>(o & 1 ? (B2[o >> 1] >> 16) : (B2[o >> 1] & 0xffff));
+        const bool own = on && o < need;
+        const bool v0 = own && (o < last || (o == last && (sem == static_cast<int>(Semantics::Spec) || L2 == L1)));
+        const uint32_t idx0 = static_cast<uint32_t>(o) << KB;
+        const uint32_t k0 = v0 ? ((static_cast<uint32_t>(Po + 32768) << 16) | (0xffffu - idx0)) : 0u;
+        const bool v1 = own && o < last && L2 >= 2 && bk != -32768;
+        const int d = bk >> KB;
+        const int kk = KMASK - (bk & KMASK);
+        const uint32_t k1 = v1 ? ((static_cast<uint32_t>(d + Pn + 32768) << 16) | (0xffffu - (idx0 | kk))) : 0u;
+        best = max(best, max(k0, k1));
+      }
+      if (mine) {
+        Result res;
+        if (best == 0u) {
+          res = Result{INT32_MIN, 0, 0};
+        } else {
+          const uint32_t idx = 0xffffu - (best & 0xffffu);
+          res = Result{static_cast<int>(best >> 16) - 32768, static_cast<int>(idx >> KB), static_cast<int>(idx & KMASK)};
+        }
+        store_result(res_l, rl, a.fmt, res);
+      }
+    }
+    __syncthreads();
+    uint32_t* dst = reinterpret_cast<uint32_t*>(static_cast<char*>(a.out) + rb * fb);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(res_l);
+    const int nd = m * fb / 4;
+    for (int q = tid; q < nd; q += kBlock) dst[q] = src[q];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------
+namespace {
+struct SwipeChoice {
+  int noff = 0, l2w = 0;
+};
+
+SwipeChoice swipe_choice(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs_weight) {
+  SwipeChoice c;
+  const int64_t need = lanes_needed(L1, std::min(min_l2, L1));
+  if (need > 64 || max_l2 > 32 || L1 > 200) return c;
+  const int l2w = max_l2 <= 16 ? 4 : 8;
+  const int noff = static_cast<int>(((std::max<int64_t>(need, 2) + 7) / 8) * 8);
+  const int kb = kbits_for(l2w);
+  const int64_t dmax = 2 * static_cast<int64_t>(std::max(max_abs_weight, 1)) * std::max<int64_t>(max_l2, 1);
+  if ((dmax << kb) + (1 << kb) >= 32767) return c;                              // hot keys fit int16
+  if (static_cast<int64_t>(std::max(max_abs_weight, 1)) * max_l2 * 2 >= 32767) return c;  // sums fit int16
+  c.noff = noff;
+  c.l2w = l2w;
+  return c;
+}
+}  // namespace
+
+bool configure_swipe(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs_weight, ShortArgs& a) {
+  const SwipeChoice ch = swipe_choice(L1, min_l2, max_l2, max_abs_weight);
+  if (!ch.noff) return false;
+  const int fb = result_bytes(static_cast<ResultFormat>(a.fmt));
+  for (int tr = kMaxTile; tr >= 64; tr /= 2) {
+    const int cap = tr * static_cast<int>(std::max<int64_t>(max_l2, 1)) + 64;
+    SwipeLayout l = swipe_layout(static_cast<int>(L1), ch.noff, ch.l2w, tr, cap, fb);
+    if (l.total <= kLdsBudget) {
+      a.tile_records = tr;
+      a.codes_cap = cap;
+      a.max_l2 = static_cast<int32_t>(max_l2);
+      a.slot = ch.noff;  // informational
+      a.rpw = ch.l2w;    // informational
+      return true;
+    }
+  }
+  return false;
+}
+
+void launch_swipe(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStream_t stream) {
+  if (a.n <= 0) return;
+  const int noff = a.slot, l2w = a.rpw;
+  const int fb = result_bytes(static_cast<ResultFormat>(a.fmt));
+  const SwipeLayout lay = swipe_layout(pv.L1, noff, l2w, a.tile_records, a.codes_cap, fb);
+  const int64_t n_tiles = (a.n + a.tile_records - 1) / a.tile_records;
+  const int per_cu = std::max(1, std::min(8, 160 * 1024 / std::max(lay.total, 1)));
+  const int64_t blocks = std::min<int64_t>(n_tiles, static_cast<int64_t>(num_cus) * per_cu);
+  (void)hipMemsetAsync(a.counter, 0, sizeof(unsigned), stream);
+  const dim3 grid(static_cast<unsigned>(std::max<int64_t>(blocks, 1))), block(kBlock);
+#define MOC_SWIPE_CASE(NO, LW)                                                                              \
+  if (noff == NO && l2w == LW) {                                                                          \
+    hipLaunchKernelGGL((swipe_search_kernel<NO, LW>), grid, block, lay.total, stream, pv, a, lay);        \
+    return;                                                                                               \
+  }
+  MOC_SWIPE_CASE(8, 4)
+  MOC_SWIPE_CASE(16, 4)
+  MOC_SWIPE_CASE(24, 4)
+  MOC_SWIPE_CASE(32, 4)
+  MOC_SWIPE_CASE(40, 4)
+  MOC_SWIPE_CASE(48, 4)
+  MOC_SWIPE_CASE(56, 4)
+  MOC_SWIPE_CASE(64, 4)
+  MOC_SWIPE_CASE(8, 8)
+  MOC_SWIPE_CASE(16, 8)
+  MOC_SWIPE_CASE(24, 8)
+  MOC_SWIPE_CASE(32, 8)
+  MOC_SWIPE_CASE(40, 8)
+  MOC_SWIPE_CASE(48, 8)
+  MOC_SWIPE_CASE(56, 8)
+  MOC_SWIPE_CASE(64, 8)
+#undef MOC_SWIPE_CASE
+}
+
+}  // namespace dev
+}  // namespace moc

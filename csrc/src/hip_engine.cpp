@@ -368,11 +368,16 @@ void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uin
   a.n = n;
   a.fmt = static_cast<int32_t>(fmt);
   a.counter = d_counter_;
-  if (opt_.allow_direct && dev::configure_short(L1_, ls.mn, ls.mx, a) &&
+  const bool swipe = dev::configure_swipe(L1_, ls.mn, ls.mx, table_.max_abs(), a);
+  if (opt_.allow_direct && (swipe || dev::configure_short(L1_, ls.mn, ls.mx, a)) &&
       direct_pointers(codes, offsets, lengths8, n, out, fb, a)) {
     const dev::ProblemView pv = problem_view(ls.mx);
     MOC_HIP_CHECK(hipEventRecord(ev_a_, s_compute_));
-    dev::launch_short(pv, a, num_cus_, s_compute_);
+    if (swipe)
+      dev::launch_swipe(pv, a, num_cus_, s_compute_);
+    else
+      dev::launch_short(pv, a, num_cus_, s_compute_);
+    stats_.kernels = swipe ? 1 : 2;
     MOC_HIP_CHECK(hipGetLastError());
     MOC_HIP_CHECK(hipEventRecord(ev_b_, s_compute_));
     MOC_HIP_CHECK(hipEventSynchronize(ev_b_));
@@ -421,7 +426,9 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
     // records that the short kernel cannot hold (LDS budget) go to the tile kernel too
     dev::ShortArgs a;
     a.fmt = static_cast<int32_t>(fmt);
-    bool short_ok = cp.n_short > 0 && dev::configure_short(L1_, cp.min_short, cp.max_l2, a);
+    const bool swipe = cp.n_short > 0 && cp.long_recs.empty() &&
+                       dev::configure_swipe(L1_, cp.min_short, cp.max_l2, table_.max_abs(), a);
+    bool short_ok = swipe || (cp.n_short > 0 && dev::configure_short(L1_, cp.min_short, cp.max_l2, a));
     if (cp.n_short > 0 && !short_ok) {
       cp.long_recs.clear();
       cp.tiles.clear();
@@ -464,7 +471,11 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
       a.n = cn;
       a.out = s.d_out;
       a.counter = s.d_counter;
-      dev::launch_short(pv, a, num_cus_, s_compute_);
+      if (swipe)
+        dev::launch_swipe(pv, a, num_cus_, s_compute_);
+      else
+        dev::launch_short(pv, a, num_cus_, s_compute_);
+      stats_.kernels |= swipe ? 1 : 2;
     }
     if (!cp.tiles.empty()) {
       dev::Plan plan;
@@ -475,6 +486,7 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
       plan.keys = reinterpret_cast<unsigned long long*>(static_cast<char*>(s.d_plan) + lay.keys_off);
       dev::BatchView bv{dcodes, doffs, cn};
       dev::launch_tiles(pv, bv, plan, s.d_out, static_cast<int>(fmt), s_compute_);
+      stats_.kernels |= 4;
     }
     MOC_HIP_CHECK(hipGetLastError());
     MOC_HIP_CHECK(hipEventRecord(s.ev_k1, s_compute_));
@@ -502,7 +514,9 @@ void HipEngine::solve_device(const uint8_t* d_codes, const int64_t* d_offsets, c
   plan_chunk(h_offsets, n, cp);
   dev::ShortArgs a;
   a.fmt = static_cast<int32_t>(ResultFormat::R12);
-  bool short_ok = cp.n_short > 0 && dev::configure_short(L1_, cp.min_short, cp.max_l2, a);
+  const bool swipe = cp.n_short > 0 && cp.long_recs.empty() &&
+                     dev::configure_swipe(L1_, cp.min_short, cp.max_l2, table_.max_abs(), a);
+  bool short_ok = swipe || (cp.n_short > 0 && dev::configure_short(L1_, cp.min_short, cp.max_l2, a));
   if (cp.n_short > 0 && !short_ok) {  // everything through the tile kernel
     cp.long_recs.clear();
     cp.tiles.clear();
@@ -529,7 +543,10 @@ void HipEngine::solve_device(const uint8_t* d_codes, const int64_t* d_offsets, c
     a.n = n;
     a.out = d_out;
     a.counter = d_counter_;
-    dev::launch_short(pv, a, num_cus_, stream);
+    if (swipe)
+      dev::launch_swipe(pv, a, num_cus_, stream);
+    else
+      dev::launch_short(pv, a, num_cus_, stream);
   }
   if (!cp.tiles.empty()) {
     dev::Plan plan;
@@ -546,6 +563,7 @@ void HipEngine::solve_device(const uint8_t* d_codes, const int64_t* d_offsets, c
   stats_ = EngineStats{};
   stats_.cells = cp.cells;
   stats_.records = n;
+  stats_.kernels = (short_ok ? (swipe ? 1 : 2) : 0) | (cp.tiles.empty() ? 0 : 4);
 }
 
 }  // namespace moc

@@ -132,6 +132,40 @@ def test_staged_formats(engine, fmt):
     assert np.array_equal(as_triples(got), as_triples(search_cpu(prob)))
 
 
+@pytest.mark.parametrize("L1,lo,hi,w", [(26, 6, 11, (4, 3, 2, 10)), (12, 1, 14, (3, 1, 1, 2)),
+                                        (40, 20, 32, (5, 2, 3, 4)), (60, 10, 16, (2, 2, 1, 3)),
+                                        (100, 40, 32, (1, 1, 1, 1)), (9, 9, 9, (7, 1, 2, 3))])
+@pytest.mark.parametrize("sem", [Semantics.REFERENCE, Semantics.SPEC])
+def test_swipe_kernel_shapes(engine, L1, lo, hi, w, sem):
+    # lane-per-record packed-int16 kernel across offset widths (NOFF 8..64) and record widths (<=16, <=32)
+    rng = np.random.default_rng(L1 * 100 + lo)
+    s1 = "".join(chr(65 + x) for x in rng.integers(0, 26, L1))
+    lens = rng.integers(max(1, min(lo, hi)), max(lo, hi) + 1, 3000)
+    recs = ["".join(chr(65 + x) for x in rng.integers(0, 26, n)) for n in lens]
+    prob = Problem.from_strings(w, s1, recs)
+    engine.set_problem(prob.weights, prob.seq1, sem)
+    got = engine.solve(prob.codes, prob.offsets, fmt="auto")
+    kinds = engine.stats()["kernels"]
+    assert np.array_equal(as_triples(got), as_triples(search_cpu(prob, sem))), kinds
+    if L1 - min(lo, hi) + 1 <= 64:
+        assert kinds == ["swipe"], kinds
+
+
+def test_kernel_selection(engine):
+    p6 = make_synthetic("input6", 2000, seed=1)
+    engine.set_problem(p6.weights, p6.seq1)
+    engine.solve(p6.codes, p6.offsets)
+    assert engine.stats()["kernels"] == ["swipe"]
+    p1 = make_synthetic("input1", 2000, seed=1)  # W1 = 100 overflows the int16 keys -> lane/offset kernel
+    engine.set_problem(p1.weights, p1.seq1)
+    engine.solve(p1.codes, p1.offsets)
+    assert engine.stats()["kernels"] == ["short"]
+    p4 = make_synthetic("input4", 50, seed=1)
+    engine.set_problem(p4.weights, p4.seq1)
+    engine.solve(p4.codes, p4.offsets)
+    assert engine.stats()["kernels"] == ["tiles"]
+
+
 def test_short_config_fallback(engine):
     # records far longer than Seq1 blow the short kernel's LDS tile budget -> everything via tiles
     rng = np.random.default_rng(9)
