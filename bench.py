@@ -42,13 +42,18 @@ def parse_args():
     ap.add_argument("--verify", type=int, default=20000, help="records per rank checked against the CPU engine")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, default) | gloo (multi-rank rehearsal)")
+    ap.add_argument("--numa", type=int, default=1, help="bind each rank to its GPU's NUMA node")
+    ap.add_argument("--packed", type=int, default=1, help="letters as 5-bit packed CSR (1) or one byte each (0)")
     return ap.parse_args()
 
 
 class HostArrays:
     """Per-rank slice of the node-shared input/result arrays (/dev/shm files, or private memory)."""
 
-    def __init__(self, tag, rank, lengths, use_shm):
+    def __init__(self, tag, rank, lengths, use_shm, packed, seed):
+        from mpi_openmp_cuda_amd.models.problem import pack5, packed5_bytes
+        from mpi_openmp_cuda_amd.utils.synthetic import fill_codes
+
         n = lengths.shape[0]
         total = int(lengths.sum())
         self.paths = []
@@ -72,7 +77,18 @@ class HostArrays:
         np.cumsum(lengths, out=self.offsets[1:])
         self.lengths = mk("lengths", np.uint8, n)  # narrow lengths (the parser's by-product)
         self.lengths[:] = lengths
-        self.codes = mk("codes", np.uint8, total)
+        # letters: the parser's packed CSR (5 bits per letter) or one byte per letter
+        letters = np.empty(total, dtype=np.uint8)
+        fill_codes(letters, seed)
+        self.packed = bool(packed)
+        if self.packed:
+            self.codes = mk("codes5", np.uint8, packed5_bytes(total))
+            pack5(letters, out=self.codes)
+        else:
+            self.codes = mk("codes", np.uint8, total)
+            self.codes[:] = letters
+        self.check_letters = letters[:min(total, 1 << 22)].copy()  # kept for the untimed verification
+        del letters
         self.results = None  # allocated once the result wire format is known
 
     def cleanup(self):
@@ -91,7 +107,7 @@ def main():
     from mpi_openmp_cuda_amd import HipSearchEngine, Problem, search_cpu
     from mpi_openmp_cuda_amd._lib import Pinned
     from mpi_openmp_cuda_amd.ops.align import as_triples
-    from mpi_openmp_cuda_amd.utils.synthetic import SHAPES, fill_codes
+    from mpi_openmp_cuda_amd.utils.synthetic import SHAPES
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -118,6 +134,10 @@ def main():
                 dist.barrier()
         torch.cuda.synchronize(dev)
 
+    from mpi_openmp_cuda_amd import _lib
+
+    # host buffers the GPU streams over PCIe go on the NUMA node of its root complex
+    numa = _lib.lib().moc_bind_numa(gpu) if args.numa else -1
     shape = SHAPES[args.shape]
     # ---- problem header (root) and this rank's synthetic slice (untimed setup = the parsed input)
     rng = np.random.default_rng(args.seed)
@@ -128,14 +148,11 @@ def main():
     rrng = np.random.default_rng(args.seed + 1 + rank)
     lengths = rrng.integers(shape.l2_min, shape.l2_max + 1, size=R, dtype=np.int64)
     tag = os.environ.get("MASTER_PORT", str(os.getpid()))
-    host = HostArrays(tag, rank, lengths, bool(args.shm))
-    fill_codes(host.codes, args.seed + 101 + rank)
+    host = HostArrays(tag, rank, lengths, bool(args.shm), args.packed, args.seed + 101 + rank)
     del lengths
     eng = HipSearchEngine(device=gpu)
     eng.set_problem(weights, seq1)
     fmt = eng.auto_format(shape.l2_max)
-    from mpi_openmp_cuda_amd import _lib
-
     rdt = _lib.FORMAT_DTYPES[_lib.FORMAT_NAMES.index(fmt)]
     if host.shm:
         p = f"/dev/shm/moc_bench_{tag}_{rank}_results"
@@ -153,7 +170,7 @@ def main():
         hdr_host[:] = header.cpu().numpy()
         eng.set_problem(hdr_host[:4], hdr_host[4:].astype(np.uint8))
         eng.solve(host.codes, host.offsets, out=host.results, lengths=host.lengths, fmt=fmt,
-                  l2_range=(shape.l2_min, shape.l2_max))
+                  l2_range=(shape.l2_min, shape.l2_max), packed5=host.packed)
         done.fill_(R)
         if distributed:
             dist.all_reduce(done)
@@ -174,9 +191,11 @@ def main():
 
     # ---- verification (untimed): sample of this rank's results vs the CPU engine
     nv = min(args.verify, R)
+    while nv > 0 and int(host.offsets[nv]) > host.check_letters.shape[0]:
+        nv //= 2
     ok = 1
     if nv > 0:
-        sub = Problem(shape.weights, seq1, host.codes[:int(host.offsets[nv])], host.offsets[:nv + 1].copy())
+        sub = Problem(shape.weights, seq1, host.check_letters[:int(host.offsets[nv])], host.offsets[:nv + 1].copy())
         ref = as_triples(search_cpu(sub))
         ok = int(np.array_equal(as_triples(host.results[:nv]), ref))
     okt = torch.tensor([ok], dtype=torch.int32, device=cdev)
@@ -221,6 +240,9 @@ def main():
             "rank0_d2h_bytes_per_step": int(st["d2h_bytes"]),
             "host_arrays": "shm" if host.shm else "private",
             "result_format": fmt,
+            "letters": "packed5" if host.packed else "bytes",
+            "rank0_numa_node": numa,
+            "rank0_kernels": st["kernels"],
             "zero_copy": bool(st["direct"]),
             "verified": bool(okt.item()),
         }

@@ -29,6 +29,11 @@ const int64_t* moc_problem_offsets(void* p);
 /* Formats rows into buf (cap bytes); returns bytes written or -1 (needs ~96 B per row). */
 int64_t moc_format_results(const moc_result* r, int64_t n, int64_t first_index, char* buf, int64_t cap);
 
+/* ---- 5-bit packed letter codes (moc/problem.hpp) ---- */
+int64_t moc_packed5_bytes(int64_t n_chars);
+int moc_pack5(const uint8_t* codes, int64_t n, uint8_t* out);
+int moc_unpack5(const uint8_t* packed, int64_t begin, int64_t n, uint8_t* out);
+
 /* ---- score table ---- */
 int moc_score_table(const int32_t* weights4, int32_t* lut1024, uint8_t* cls1024);
 
@@ -46,6 +51,9 @@ int moc_partition(const int64_t* lengths, int64_t n, int64_t L1, int parts, doub
 int moc_device_count(void);
 /* Page-locks [p, p+bytes) for direct DMA (hipHostRegister on the enclosing page range). */
 int moc_host_register(void* p, size_t bytes);
+/* Binds CPUs + future host allocations of this process to the device's NUMA node; returns node or -1. */
+int moc_bind_numa(int device);
+int moc_device_numa_node(int device);
 /* Runs the DPP/shuffle self-test kernel; fills 192 ints (layout: align_kernels.hip dpp_probe_kernel). */
 int moc_dpp_probe(int32_t* out192);
 /* Transfer calibration: GB/s for kind 0 H2D, 1 D2H, 2 both, 3 zero-copy read, 4 zero-copy write, 5 D2D. */
@@ -59,7 +67,7 @@ int moc_engine_solve(void* e, const uint8_t* codes, const int64_t* offsets, int6
 /* fmt: 0 = R12 (moc_result), 1 = R8 {i32,u16,u16}, 2 = R4 {i16,u8,u8}; lengths8 / min_l2 / max_l2 optional
  * (NULL / -1). Pinned host buffers + short records -> zero-copy streaming kernel. */
 int moc_engine_solve_ex(void* e, const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths8, int64_t n,
-                        void* out, int fmt, int64_t min_l2, int64_t max_l2);
+                        void* out, int fmt, int64_t min_l2, int64_t max_l2, int packed5);
 int moc_engine_auto_format(void* e, int64_t max_l2);
 int moc_engine_pin(void* e, const void* p, size_t bytes);
 int moc_expand_results(const void* in, int fmt, int64_t n, moc_result* out);

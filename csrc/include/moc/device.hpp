@@ -96,8 +96,12 @@ struct ShortArgs {
   int32_t tile_records = 0;           // records per block tile
   int32_t codes_cap = 0;              // LDS bytes for one tile's letters (>= tile_records*max_l2+32)
   int32_t max_l2 = 0;
+  int32_t packed5 = 0;                // 1: `codes` is a 5-bit packed stream (char j at bit 5j); swipe only
   unsigned* counter = nullptr;        // device work counter, zeroed before each launch
 };
+
+// Unpacks n chars of a 5-bit packed stream (device memory) starting at bit `bit0` into byte codes.
+void launch_unpack5(const uint8_t* packed, int64_t bit0, int64_t n, uint8_t* out, hipStream_t stream);
 
 // Lanes a record needs in the short kernel (offsets 0..L1-L2 incl. the helper diagonal).
 inline int64_t lanes_needed(int64_t L1, int64_t L2) { return L2 <= L1 ? L1 - L2 + 1 : 1; }

@@ -67,9 +67,10 @@ class HipEngine {
   // Host batch in -> host results out as moc::Result. `codes` is the base pointer (record i starts at
   // codes + offsets[i]); `offsets` has n+1 absolute entries.
   void solve(const uint8_t* codes, const int64_t* offsets, int64_t n, Result* out);
-  // General form: optional uint8 lengths (max L2 <= 255), results in `fmt`.
+  // General form: optional uint8 lengths (max L2 <= 255), results in `fmt`. With `packed5`, `codes` is
+  // a 5-bit packed stream (moc::pack5; char j at bit 5j) instead of one byte per letter.
   void solve_ex(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths8, int64_t n, void* out,
-                ResultFormat fmt, const BatchHints& hints = {});
+                ResultFormat fmt, const BatchHints& hints = {}, bool packed5 = false);
   // Smallest result format for this problem given the batch's longest record.
   ResultFormat auto_format(int64_t max_l2) const;
 
@@ -100,8 +101,9 @@ class HipEngine {
   void ensure(void*& ptr, size_t& cap, size_t bytes);
   void ensure_host(void*& ptr, size_t& cap, size_t bytes);
   bool direct_pointers(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths8, int64_t n, void* out,
-                       int fb, dev::ShortArgs& a) const;
-  void run_staged(const uint8_t* codes, const int64_t* offsets, int64_t n, void* out, ResultFormat fmt);
+                       int fb, bool packed5, dev::ShortArgs& a) const;
+  void run_staged(const uint8_t* codes, const int64_t* offsets, int64_t n, void* out, ResultFormat fmt,
+                  bool packed5);
 
   EngineOptions opt_;
   int device_ = 0;

@@ -26,4 +26,11 @@ DeviceInfo device_info(int id);
 // Picks local_rank % count (or `requested` when >= 0), calls hipSetDevice, returns the id.
 int select_device(int local_rank, int requested = -1);
 
+// NUMA node the device's PCIe function hangs off (sysfs), or -1 when unknown.
+int device_numa_node(int device);
+// Binds the calling process's CPUs (sched_setaffinity) and its future page allocations
+// (set_mempolicy MPOL_PREFERRED) to the device's NUMA node, so host buffers that the GPU streams
+// over PCIe live next to its root complex. Returns the node, or -1 if nothing was changed.
+int bind_numa_to_device(int device);
+
 }  // namespace moc

@@ -94,6 +94,14 @@ int64_t moc_format_results(const moc_result* r, int64_t n, int64_t first_index, 
   return written;
 }
 
+int64_t moc_packed5_bytes(int64_t n_chars) { return moc::packed5_bytes(n_chars); }
+int moc_pack5(const uint8_t* codes, int64_t n, uint8_t* out) {
+  return guard([&] { moc::pack5(codes, n, out); });
+}
+int moc_unpack5(const uint8_t* packed, int64_t begin, int64_t n, uint8_t* out) {
+  return guard([&] { moc::unpack5(packed, begin, n, out); });
+}
+
 int moc_score_table(const int32_t* weights4, int32_t* lut1024, uint8_t* cls1024) {
   return guard([&] {
     moc::ScoreTable t = moc::ScoreTable::build(weights_of(weights4));
@@ -154,6 +162,9 @@ double moc_transfer_probe(int kind, size_t bytes, int iters) {
   return gbs;
 }
 
+int moc_bind_numa(int device) { return moc::bind_numa_to_device(device); }
+int moc_device_numa_node(int device) { return moc::device_numa_node(device); }
+
 int moc_host_register(void* p, size_t bytes) {
   return guard([&] {
     const uintptr_t page = 4096;
@@ -205,12 +216,13 @@ int moc_engine_solve(void* e, const uint8_t* codes, const int64_t* offsets, int6
 }
 
 int moc_engine_solve_ex(void* e, const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths8, int64_t n,
-                        void* out, int fmt, int64_t min_l2, int64_t max_l2) {
+                        void* out, int fmt, int64_t min_l2, int64_t max_l2, int packed5) {
   return guard([&] {
     moc::BatchHints h;
     h.min_l2 = min_l2;
     h.max_l2 = max_l2;
-    static_cast<moc::HipEngine*>(e)->solve_ex(codes, offsets, lengths8, n, out, static_cast<moc::ResultFormat>(fmt), h);
+    static_cast<moc::HipEngine*>(e)->solve_ex(codes, offsets, lengths8, n, out, static_cast<moc::ResultFormat>(fmt), h,
+                                              packed5 != 0);
   });
 }
 

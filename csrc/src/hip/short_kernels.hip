@@ -182,6 +182,23 @@ __global__ __launch_bounds__(kBlock) void short_search_kernel(ProblemView pv, Sh
   }
 }
 
+// 5-bit packed stream -> byte codes (staged pipeline path for packed batches).
+__global__ void unpack5_kernel(const uint8_t* __restrict__ packed, int64_t bit0, int64_t n, uint8_t* __restrict__ out) {
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t bit = bit0 + 5 * i;
+    const uint32_t lo = packed[bit >> 3], hi = packed[(bit >> 3) + 1];
+    out[i] = static_cast<uint8_t>(((lo | (hi << 8)) >> (bit & 7)) & 31u);
+  }
+}
+
+void launch_unpack5(const uint8_t* packed, int64_t bit0, int64_t n, uint8_t* out, hipStream_t stream) {
+  if (n <= 0) return;
+  const int64_t blocks = std::min<int64_t>((n + kBlock - 1) / kBlock, 4096);
+  hipLaunchKernelGGL(unpack5_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, stream, packed, bit0, n,
+                     out);
+}
+
 bool configure_short(int64_t L1, int64_t min_l2, int64_t max_l2, ShortArgs& a) {
   if (lanes_needed(L1, min_l2) > kWave) return false;
   a.slot = static_cast<int32_t>(std::max<int64_t>(1, lanes_needed(L1, min_l2)));

@@ -64,8 +64,9 @@ inline int kbits_for(int l2w) {  // bits for k in the int16 keys: k <= 4*l2w
 }
 }  // namespace
 
-template <int NOFF, int L2W>
+template <int NOFF, int L2W, bool P5>
 __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, ShortArgs a, SwipeLayout lay) {
+  constexpr int NW = P5 ? (20 * L2W + 31) / 32 : L2W;  // record words held per lane
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   short* prof = reinterpret_cast<short*>(smem);
   int* loff = reinterpret_cast<int*>(smem + lay.loff_off);
@@ -125,11 +126,14 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
     }
     if (tid == kBlock - 1) loff[m] = excl;
 
-    // ---- letters -> LDS (16-byte loads)
-    const uintptr_t p0 = reinterpret_cast<uintptr_t>(a.codes + start);
+    // ---- letters -> LDS (16-byte loads). Byte codes: char j at byte j. Packed: char j at bit 5j.
+    //      shift_b = position (bytes, or bits when P5) of the tile's first char inside the LDS copy.
+    const int64_t b_first = P5 ? (5 * start) >> 3 : start;
+    const int64_t b_end = P5 ? (5 * end + 7) >> 3 : end;
+    const uintptr_t p0 = reinterpret_cast<uintptr_t>(a.codes + b_first);
     const uintptr_t a0 = p0 & ~uintptr_t{15};
-    const int shift_b = static_cast<int>(p0 - a0);
-    const int nvec = static_cast<int>((reinterpret_cast<uintptr_t>(a.codes + end) + 15 - a0) >> 4);
+    const int shift_b = P5 ? static_cast<int>(8 * (p0 - a0) + ((5 * start) & 7)) : static_cast<int>(p0 - a0);
+    const int nvec = static_cast<int>((reinterpret_cast<uintptr_t>(a.codes + b_end) + 15 - a0) >> 4);
     for (int v = tid; v < nvec; v += kBlock)
       reinterpret_cast<uint4*>(codes_l)[v] = reinterpret_cast<const uint4*>(a0)[v];
     __syncthreads();
@@ -140,24 +144,26 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
       const bool in = rl < m;
       int L2 = 0, rs = 0;
       if (in) {
-        rs = shift_b + loff[rl];
+        rs = P5 ? shift_b + 5 * loff[rl] : shift_b + loff[rl];  // bit (P5) or byte position in LDS
         L2 = loff[rl + 1] - loff[rl];
       }
       const int need = L2 <= L1 ? L1 - L2 + 1 : 1;
       const bool mine = in && need <= NOFF;  // others belong to the tile kernel (mixed batches)
       const bool on = mine && L2 <= L1;
-      // record letters -> L2W aligned words (bytes past the record end zeroed: they add row 0 = 0)
-      uint32_t wd[L2W];
+      // record letters -> NW aligned words (bits past the record end zeroed: they add row 0 = 0)
+      uint32_t wd[NW];
       {
         const uint32_t* l32 = reinterpret_cast<const uint32_t*>(codes_l);
-        const int wb = rs >> 2, sh = (rs & 3) * 8;
+        const int wb = P5 ? rs >> 5 : rs >> 2;
+        const int sh = P5 ? (rs & 31) : (rs & 3) * 8;
+        const int rbits = (P5 ? 5 : 8) * L2;
         uint32_t prev = on ? l32[wb] : 0u;
 #pragma unroll
-        for (int k = 0; k < L2W; ++k) {
+        for (int k = 0; k < NW; ++k) {
           const uint32_t nxt = on ? l32[wb + k + 1] : 0u;
           uint32_t w = sh ? ((prev >> sh) | (nxt << (32 - sh))) : prev;
-          const int left = L2 - 4 * k;  // bytes of the record in this word
-          w = left >= 4 ? w : (left <= 0 ? 0u : (w & ((1u << (8 * left)) - 1u)));
+          const int left = rbits - 32 * k;  // record bits in this word
+          w = left >= 32 ? w : (left <= 0 ? 0u : (w & ((1u << left) - 1u)));
           wd[k] = on ? w : 0u;
           prev = nxt;
         }
@@ -176,7 +182,13 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
           const int i = i0 + s;
-          const int c = (wd[i >> 2] >> (8 * (i & 3))) & 0xff;
+          int c;
+          if (P5) {  // compile-time bit position 5i
+            const int bit = 5 * i, w = bit >> 5, sh = bit & 31;
+            c = sh <= 27 ? (wd[w] >> sh) & 31 : ((wd[w] >> sh) | (wd[w + 1 < NW ? w + 1 : w] << (32 - sh))) & 31;
+          } else {
+            c = (wd[i >> 2] >> (8 * (i & 3))) & 0xff;
+          }
           const uint4* rowp = reinterpret_cast<const uint4*>(prof + s * lay.copy_elems + c * lay.row + i0);
           uint32_t v[NP];
 #pragma unroll
@@ -294,7 +306,10 @@ void launch_swipe(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStr
   const dim3 grid(static_cast<unsigned>(std::max<int64_t>(blocks, 1))), block(kBlock);
 #define MOC_SWIPE_CASE(NO, LW)                                                                              \
   if (noff == NO && l2w == LW) {                                                                          \
-    hipLaunchKernelGGL((swipe_search_kernel<NO, LW>), grid, block, lay.total, stream, pv, a, lay);        \
+    if (a.packed5)                                                                                        \
+      hipLaunchKernelGGL((swipe_search_kernel<NO, LW, true>), grid, block, lay.total, stream, pv, a, lay); \
+    else                                                                                                  \
+      hipLaunchKernelGGL((swipe_search_kernel<NO, LW, false>), grid, block, lay.total, stream, pv, a, lay); \
     return;                                                                                               \
   }
   MOC_SWIPE_CASE(8, 4)

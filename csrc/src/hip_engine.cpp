@@ -80,6 +80,8 @@ struct HipEngine::Slot {
   size_t d_codes_cap = 0;
   void* d_offsets = nullptr;
   size_t d_offsets_cap = 0;
+  void* d_packed = nullptr;  // 5-bit packed letters of the chunk (packed batches)
+  size_t d_packed_cap = 0;
   void* d_out = nullptr;
   size_t d_out_cap = 0;
   void* d_plan = nullptr;  // tiles | long_recs | keys
@@ -121,6 +123,7 @@ HipEngine::~HipEngine() {
   for (auto& s : slots_) {
     (void)hipFree(s->d_codes);
     (void)hipFree(s->d_offsets);
+    (void)hipFree(s->d_packed);
     (void)hipFree(s->d_out);
     (void)hipFree(s->d_plan);
     (void)hipFree(s->d_counter);
@@ -319,15 +322,17 @@ LenStats scan_lengths(const int64_t* offsets, const uint8_t* lengths8, int64_t n
 }  // namespace
 
 bool HipEngine::direct_pointers(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths8, int64_t n,
-                                void* out, int fb, dev::ShortArgs& a) const {
+                                void* out, int fb, bool packed5, dev::ShortArgs& a) const {
   const void *dc = nullptr, *doff = nullptr, *dlen = nullptr, *dout = nullptr;
   const int64_t c0 = offsets[0], c1 = offsets[n];
-  if (c1 > c0 && !pinned_range(codes + c0, static_cast<size_t>(c1 - c0), &dc)) return false;
+  // byte range of the letters: [b0, b1)
+  const int64_t b0 = packed5 ? (5 * c0) >> 3 : c0, b1 = packed5 ? ((5 * c1 + 7) >> 3) + 1 : c1;
+  if (c1 > c0 && !pinned_range(codes + b0, static_cast<size_t>(b1 - b0), &dc)) return false;
   if (!pinned_range(offsets, sizeof(int64_t) * static_cast<size_t>(n + 1), &doff)) return false;
   if (lengths8 && !pinned_range(lengths8, static_cast<size_t>(n), &dlen)) return false;
   if (!pinned_range(out, static_cast<size_t>(fb) * static_cast<size_t>(n), &dout)) return false;
-  // device view of the codes base pointer (record i at base + offsets[i])
-  a.codes = c1 > c0 ? static_cast<const uint8_t*>(dc) - c0 : nullptr;
+  // device view of the codes base pointer (record i at base + offsets[i], or at bit 5*offsets[i])
+  a.codes = c1 > c0 ? static_cast<const uint8_t*>(dc) - b0 : nullptr;
   a.offsets = static_cast<const int64_t*>(doff);
   a.lengths8 = static_cast<const uint8_t*>(dlen);
   a.out = const_cast<void*>(dout);
@@ -339,7 +344,7 @@ void HipEngine::solve(const uint8_t* codes, const int64_t* offsets, int64_t n, R
 }
 
 void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths8, int64_t n, void* out,
-                         ResultFormat fmt, const BatchHints& hints) {
+                         ResultFormat fmt, const BatchHints& hints, bool packed5) {
   if (!have_problem_) throw Error("HipEngine::solve before set_problem");
   MOC_HIP_CHECK(hipSetDevice(device_));
   Stopwatch wall;
@@ -368,9 +373,11 @@ void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uin
   a.n = n;
   a.fmt = static_cast<int32_t>(fmt);
   a.counter = d_counter_;
+  a.packed5 = packed5 ? 1 : 0;
   const bool swipe = dev::configure_swipe(L1_, ls.mn, ls.mx, table_.max_abs(), a);
-  if (opt_.allow_direct && (swipe || dev::configure_short(L1_, ls.mn, ls.mx, a)) &&
-      direct_pointers(codes, offsets, lengths8, n, out, fb, a)) {
+  // packed letters stream straight into the swipe kernel only; other kernels read unpacked bytes
+  if (opt_.allow_direct && (swipe || (!packed5 && dev::configure_short(L1_, ls.mn, ls.mx, a))) &&
+      direct_pointers(codes, offsets, lengths8, n, out, fb, packed5, a)) {
     const dev::ProblemView pv = problem_view(ls.mx);
     MOC_HIP_CHECK(hipEventRecord(ev_a_, s_compute_));
     if (swipe)
@@ -386,18 +393,20 @@ void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uin
     stats_.kernel_ms = ms;
     stats_.direct = 1;
     stats_.chunks = 1;
-    stats_.h2d_bytes = (offsets[n] - offsets[0]) + (a.lengths8 ? n : 8 * n);
+    const int64_t letters = offsets[n] - offsets[0];
+    stats_.h2d_bytes = (packed5 ? (5 * letters + 7) / 8 : letters) + (a.lengths8 ? n : 8 * n);
     stats_.d2h_bytes = static_cast<int64_t>(fb) * n;
     wall.stop();
     stats_.total_ms = wall.total_ms();
     return;
   }
-  run_staged(codes, offsets, n, out, fmt);
+  run_staged(codes, offsets, n, out, fmt, packed5);
   wall.stop();
   stats_.total_ms = wall.total_ms();
 }
 
-void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t n, void* out, ResultFormat fmt) {
+void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t n, void* out, ResultFormat fmt,
+                           bool packed5) {
   const int fb = result_bytes(fmt);
   ChunkPlan cp;
   double kernel_ms = 0;
@@ -443,6 +452,10 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
     const PlanLayout lay(cp.tiles.size(), cp.long_recs.size());
     const size_t cbytes = static_cast<size_t>(offsets[re] - offsets[rb]);
     ensure(s.d_codes, s.d_codes_cap, std::max<size_t>(cbytes, 16) + 32);
+    // packed chunk: bytes [pb0, pb1) of the 5-bit stream, char offsets[rb] at bit pbit within it
+    const int64_t pb0 = (5 * offsets[rb]) >> 3, pb1 = ((5 * offsets[re] + 7) >> 3) + 1;
+    const int64_t pbit = 5 * offsets[rb] - 8 * pb0;
+    if (packed5) ensure(s.d_packed, s.d_packed_cap, static_cast<size_t>(pb1 - pb0) + 16);
     ensure(s.d_offsets, s.d_offsets_cap, sizeof(int64_t) * static_cast<size_t>(cn + 1));
     ensure(s.d_out, s.d_out_cap, static_cast<size_t>(fb) * static_cast<size_t>(cn));
     if (lay.total) {
@@ -452,14 +465,24 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
       std::memcpy(static_cast<char*>(s.h_plan) + lay.long_off, cp.long_recs.data(), cp.long_recs.size() * sizeof(int32_t));
     }
     // ---- copy stream: H2D
-    if (cbytes) MOC_HIP_CHECK(hipMemcpyAsync(s.d_codes, codes + offsets[rb], cbytes, hipMemcpyHostToDevice, s_copy_));
+    size_t letter_bytes = cbytes;
+    if (packed5) {
+      letter_bytes = static_cast<size_t>(pb1 - pb0);
+      if (cbytes)
+        MOC_HIP_CHECK(hipMemcpyAsync(s.d_packed, codes + pb0, letter_bytes, hipMemcpyHostToDevice, s_copy_));
+    } else if (cbytes) {
+      MOC_HIP_CHECK(hipMemcpyAsync(s.d_codes, codes + offsets[rb], cbytes, hipMemcpyHostToDevice, s_copy_));
+    }
     MOC_HIP_CHECK(hipMemcpyAsync(s.d_offsets, offsets + rb, sizeof(int64_t) * (cn + 1), hipMemcpyHostToDevice, s_copy_));
     if (lay.upload_bytes)
       MOC_HIP_CHECK(hipMemcpyAsync(s.d_plan, s.h_plan, lay.upload_bytes, hipMemcpyHostToDevice, s_copy_));
     MOC_HIP_CHECK(hipEventRecord(s.ev_h2d, s_copy_));
-    stats_.h2d_bytes += static_cast<int64_t>(cbytes + sizeof(int64_t) * (cn + 1) + lay.upload_bytes);
+    stats_.h2d_bytes += static_cast<int64_t>(letter_bytes + sizeof(int64_t) * (cn + 1) + lay.upload_bytes);
     // ---- compute stream
     MOC_HIP_CHECK(hipStreamWaitEvent(s_compute_, s.ev_h2d, 0));
+    if (packed5)
+      dev::launch_unpack5(static_cast<const uint8_t*>(s.d_packed), pbit, static_cast<int64_t>(cbytes),
+                          static_cast<uint8_t*>(s.d_codes), s_compute_);
     MOC_HIP_CHECK(hipEventRecord(s.ev_k0, s_compute_));
     const dev::ProblemView pv = problem_view(cp.max_l2);
     const uint8_t* dcodes = static_cast<const uint8_t*>(s.d_codes);

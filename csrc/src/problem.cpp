@@ -39,6 +39,30 @@ void validate_score_range(const Weights& w, int64_t max_len2) {
                 " exceeds the int32 score range supported (< 2^29)");
 }
 
+void pack5(const uint8_t* codes, int64_t n, uint8_t* out) {
+  const int64_t groups = (n + 7) / 8;  // 8 chars -> 5 bytes, independent per group
+#pragma omp parallel for schedule(static) if (groups > 65536)
+  for (int64_t g = 0; g < groups; ++g) {
+    uint64_t v = 0;
+    const int64_t b = g * 8;
+    const int m = static_cast<int>(std::min<int64_t>(8, n - b));
+    for (int j = 0; j < m; ++j) v |= static_cast<uint64_t>(codes[b + j] & 31u) << (5 * j);
+    uint8_t* o = out + g * 5;
+    for (int j = 0; j < 5; ++j) o[j] = static_cast<uint8_t>(v >> (8 * j));
+  }
+  const int64_t used = groups * 5, total = packed5_bytes(n);
+  for (int64_t i = used; i < total; ++i) out[i] = 0;
+}
+
+void unpack5(const uint8_t* packed, int64_t begin, int64_t n, uint8_t* out) {
+#pragma omp parallel for schedule(static) if (n > (1 << 20))
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t bit = 5 * (begin + i);
+    const uint32_t lo = packed[bit >> 3], hi = packed[(bit >> 3) + 1];
+    out[i] = static_cast<uint8_t>(((lo | (hi << 8)) >> (bit & 7)) & 31u);
+  }
+}
+
 std::vector<uint8_t> encode_sequence(const char* s, int64_t n) {
   std::vector<uint8_t> out(n);
   for (int64_t i = 0; i < n; ++i) {

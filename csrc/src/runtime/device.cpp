@@ -1,7 +1,12 @@
 #include "moc/runtime/device.hpp"
 
 #include <hip/hip_runtime_api.h>
+#include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
+#include <cctype>
+#include <fstream>
 #include <sstream>
 
 #include "moc/runtime/hip_check.hpp"
@@ -38,6 +43,50 @@ std::string DeviceInfo::json() const {
      << ", \"wave\": " << wave_size << ", \"mem_gb\": " << (global_mem / 1e9) << ", \"lds_per_block\": " << lds_per_block
      << "}";
   return os.str();
+}
+
+int device_numa_node(int device) {
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof bus, device) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  std::string id(bus);
+  for (auto& c : id) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
+  std::ifstream f("/sys/bus/pci/devices/" + id + "/numa_node");
+  int node = -1;
+  if (!(f >> node)) return -1;
+  return node;
+}
+
+int bind_numa_to_device(int device) {
+  const int node = device_numa_node(device);
+  if (node < 0) return -1;
+  std::ifstream f("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist");
+  std::string list;
+  if (!(f >> list)) return -1;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  int ncpu = 0;
+  std::stringstream ss(list);
+  std::string part;
+  while (std::getline(ss, part, ',')) {
+    const auto dash = part.find('-');
+    const int a = std::stoi(part.substr(0, dash));
+    const int b = dash == std::string::npos ? a : std::stoi(part.substr(dash + 1));
+    for (int c = a; c <= b && c < CPU_SETSIZE; ++c) {
+      CPU_SET(c, &set);
+      ++ncpu;
+    }
+  }
+  if (ncpu == 0) return -1;
+  if (sched_setaffinity(0, sizeof set, &set) != 0) return -1;
+  unsigned long mask[16] = {0};
+  if (node >= static_cast<int>(sizeof(mask) * 8)) return node;
+  mask[node / (8 * sizeof(unsigned long))] |= 1ul << (node % (8 * sizeof(unsigned long)));
+  constexpr int kMpolPreferred = 1;
+  syscall(SYS_set_mempolicy, kMpolPreferred, mask, sizeof(mask) * 8);  // best effort
+  return node;
 }
 
 int select_device(int local_rank, int requested) {

@@ -43,12 +43,17 @@ def _decl(lib):
         "moc_problem_offsets": (c_void_p, [c_void_p]),
         "moc_format_results": (c_int64, [c_void_p, c_int64, c_int64, c_void_p, c_int64]),
         "moc_score_table": (c_int, [P(c_int32), c_void_p, c_void_p]),
+        "moc_packed5_bytes": (c_int64, [c_int64]),
+        "moc_pack5": (c_int, [c_void_p, c_int64, c_void_p]),
+        "moc_unpack5": (c_int, [c_void_p, c_int64, c_int64, c_void_p]),
         "moc_cpu_solve": (c_int, [P(c_int32), c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p]),
         "moc_brute_force": (c_int, [P(c_int32), c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
         "moc_partition": (c_int, [c_void_p, c_int64, c_int64, c_int, c_double, c_double, c_double, c_void_p]),
         "moc_device_count": (c_int, []),
         "moc_host_register": (c_int, [c_void_p, c_size_t]),
         "moc_host_unregister": (c_int, [c_void_p]),
+        "moc_bind_numa": (c_int, [c_int]),
+        "moc_device_numa_node": (c_int, [c_int]),
         "moc_dpp_probe": (c_int, [c_void_p]),
         "moc_transfer_probe": (c_double, [c_int, c_size_t, c_int]),
         "moc_device_info_json": (c_int, [c_int, c_char_p, c_int64]),
@@ -57,7 +62,7 @@ def _decl(lib):
         "moc_engine_set_problem": (c_int, [c_void_p, P(c_int32), c_void_p, c_int64, c_int]),
         "moc_engine_solve": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
         "moc_engine_solve_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_int64,
-                                        c_int64]),
+                                        c_int64, c_int]),
         "moc_engine_auto_format": (c_int, [c_void_p, c_int64]),
         "moc_engine_pin": (c_int, [c_void_p, c_void_p, c_size_t]),
         "moc_expand_results": (c_int, [c_void_p, c_int, c_int64, c_void_p]),

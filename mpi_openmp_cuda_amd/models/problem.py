@@ -16,6 +16,31 @@ from .. import _lib
 from .scoring import Weights, decode, encode
 
 
+def packed5_bytes(n_chars: int) -> int:
+    """Bytes of a 5-bit packed letter stream (incl. 16 bytes of read slack)."""
+    return int(_lib.lib().moc_packed5_bytes(int(n_chars)))
+
+
+def pack5(codes: np.ndarray, out: np.ndarray = None) -> np.ndarray:
+    """Byte letter codes (1..26) -> 5-bit packed stream (char j at bits [5j, 5j+5)); native + OpenMP.
+
+    26 letters need only 5 bits, so every transfer of a packed batch (PCIe, xGMI, MPI) moves 37.5% fewer
+    bytes; the gfx950 streaming kernel decodes the fields in registers."""
+    codes = np.ascontiguousarray(codes, dtype=np.uint8)
+    nb = packed5_bytes(codes.shape[0])
+    if out is None:
+        out = np.empty(nb, dtype=np.uint8)
+    assert out.dtype == np.uint8 and out.shape[0] >= nb
+    _lib.check(_lib.lib().moc_pack5(_lib.ptr(codes), codes.shape[0], _lib.ptr(out)))
+    return out
+
+
+def unpack5(packed: np.ndarray, begin: int, n: int) -> np.ndarray:
+    out = np.empty(n, dtype=np.uint8)
+    _lib.check(_lib.lib().moc_unpack5(_lib.ptr(np.ascontiguousarray(packed)), int(begin), int(n), _lib.ptr(out)))
+    return out
+
+
 @dataclass
 class Problem:
     weights: Weights

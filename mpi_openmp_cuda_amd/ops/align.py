@@ -127,10 +127,11 @@ class HipSearchEngine:
         return _lib.FORMAT_NAMES[_lib.lib().moc_engine_auto_format(self._h, int(max_l2))]
 
     def solve(self, codes: np.ndarray, offsets: np.ndarray, out: Optional[np.ndarray] = None,
-              lengths: Optional[np.ndarray] = None, fmt="r12", l2_range=None) -> np.ndarray:
+              lengths: Optional[np.ndarray] = None, fmt="r12", l2_range=None, packed5: bool = False) -> np.ndarray:
         """Host CSR -> host results. ``codes[offsets[i]:offsets[i+1]]`` is record i (``offsets`` may be a
         slice of a larger absolute offset array). ``fmt``: r12 | r8 | r4 | auto (smallest that fits);
-        ``lengths``: optional uint8 record lengths; ``l2_range``: optional known (min, max) length."""
+        ``lengths``: optional uint8 record lengths; ``l2_range``: optional known (min, max) length;
+        ``packed5``: ``codes`` is a 5-bit packed stream (models.problem.pack5) instead of bytes."""
         offsets = np.ascontiguousarray(offsets, dtype=np.int64)
         n = offsets.shape[0] - 1
         if l2_range is None and (fmt == "auto"):
@@ -146,7 +147,7 @@ class HipSearchEngine:
             assert lengths.dtype == np.uint8 and lengths.shape[0] >= n
         lo, hi = l2_range if l2_range is not None else (-1, -1)
         _lib.check(_lib.lib().moc_engine_solve_ex(self._h, _lib.ptr(codes), _lib.ptr(offsets), _lib.ptr(lengths), n,
-                                                  _lib.ptr(out), fid, int(lo), int(hi)))
+                                                  _lib.ptr(out), fid, int(lo), int(hi), 1 if packed5 else 0))
         return out
 
     def solve_device(self, codes_t, offsets_t, h_offsets: np.ndarray, out_t, stream=None):

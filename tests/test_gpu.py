@@ -123,6 +123,28 @@ def test_zero_copy_direct(fmt, use_lengths):
     eng.close()
 
 
+@pytest.mark.parametrize("shape,n", [("input6", 250_003), ("input1", 3000), ("input4", 200), ("input3", 20)])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_packed5_letters(shape, n, pinned):
+    # 5-bit packed letters: streamed straight into the swipe kernel (pinned, tiny problems) or unpacked
+    # on the device by the staged pipeline (everything else)
+    from mpi_openmp_cuda_amd.models.problem import pack5
+
+    prob = make_synthetic(shape, n, seed=n)
+    packed = pack5(prob.codes)
+    eng = HipSearchEngine(device=0, chunk_records=max(n // 3, 1))
+    eng.set_problem(prob.weights, prob.seq1)
+    out = np.zeros(prob.n, dtype=np.dtype([("score", "<i4"), ("n", "<i4"), ("k", "<i4")]))
+    if pinned:
+        eng.pin(packed, prob.offsets, out)
+    eng.solve(packed, prob.offsets, out=out, packed5=True)
+    st = eng.stats()
+    assert np.array_equal(as_triples(out), as_triples(search_cpu(prob))), st
+    if pinned and shape == "input6":
+        assert st["direct"] == 1 and st["kernels"] == ["swipe"]
+    eng.close()
+
+
 @pytest.mark.parametrize("fmt", ["r8", "r4", "auto"])
 def test_staged_formats(engine, fmt):
     prob = make_synthetic("input1", 5000, seed=4)

@@ -86,6 +86,22 @@ def test_formatter_matches_python():
     assert format_results(r, first_index=7) == format_results_py(r, first_index=7)
 
 
+@pytest.mark.parametrize("n", [0, 1, 7, 8, 9, 1000, 300_001])
+def test_pack5_roundtrip(n):
+    from mpi_openmp_cuda_amd.models.problem import pack5, packed5_bytes, unpack5
+
+    rng = np.random.default_rng(n)
+    codes = rng.integers(1, 27, n, dtype=np.uint8)
+    p = pack5(codes)
+    assert p.shape[0] == packed5_bytes(n) == (5 * n + 7) // 8 + 16
+    assert np.array_equal(unpack5(p, 0, n), codes)
+    if n > 10:
+        assert np.array_equal(unpack5(p, 3, n - 5), codes[3:n - 2])
+    # bit layout: char j at bits [5j, 5j+5) of the little-endian stream
+    if n >= 2:
+        assert (int(p[0]) & 31) == codes[0] and ((int(p[0]) >> 5) | ((int(p[1]) & 3) << 3)) == codes[1]
+
+
 def test_roundtrip_text():
     p = Problem.from_strings([4, 3, 2, 10], "ABCDEFGHIJKLMNOPQRSTUVWXYZ", ["ABCDEF", "MNOPQRSTXXX"])
     q = Problem.parse(p.to_text())
