@@ -9,7 +9,9 @@
 #   make run          mpiexec -np 2 ./final < $(INPUT)
 #   make runOn2       mpiexec -np 2 -machinefile mf --map-by node ./final < $(INPUT)
 #   make test         CPU test-suite (pytest -m "not gpu")
-#   make asan         host-only ASan/UBSan build of ./final_asan (GPU code built without sanitizers)
+#   make asan         ASan/UBSan build of the g++ host code -> ./final_asan (the thin hipcc launcher
+#                     objects and all device code are built without sanitizers: no GPU ASan on the pool)
+#   make tsan         ThreadSanitizer build of the host code -> ./final_tsan (OpenMP paths, CPU backend)
 
 ROCM      ?= /opt/rocm
 MPI_HOME  ?= /opt/conda
@@ -29,7 +31,7 @@ INC       := -Icsrc/include
 CXXFLAGS  := -O3 -std=c++17 -fPIC -fopenmp -Wall -Wextra -Wno-unused-parameter $(INC) -I$(ROCM)/include -D__HIP_PLATFORM_AMD__
 HIPFLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) $(INC) -Wno-unused-result
 MPIFLAGS  := -I$(MPI_HOME)/include
-LDROCM    := -L$(ROCM)/lib -lamdhip64 -Wl,-rpath,$(ROCM)/lib
+LDROCM    := -L$(ROCM)/lib -lamdhip64 -lrocprofiler-sdk-roctx -Wl,-rpath,$(ROCM)/lib
 
 CORE_SRCS := $(wildcard csrc/src/*.cpp) $(wildcard csrc/src/runtime/*.cpp)
 HIP_SRCS  := $(wildcard csrc/src/hip/*.hip)
@@ -39,7 +41,7 @@ HIP_OBJS  := $(patsubst csrc/src/%.hip,$(OBJ)/%.o,$(HIP_SRCS))
 COMM_OBJS := $(patsubst csrc/src/%.cpp,$(OBJ)/%.o,$(COMM_SRCS))
 HEADERS   := $(shell find csrc/include -name '*.h' -o -name '*.hpp')
 
-.PHONY: all build lib clean run runOn2 test asan
+.PHONY: all build lib clean run runOn2 test asan tsan
 
 all: build
 build: lib final
@@ -82,13 +84,33 @@ asan: $(MPILIB)/libmpi.so
 	  $(CXX) -O1 -g -std=c++17 -fopenmp -fsanitize=address,undefined -fno-omit-frame-pointer $(INC) \
 	    -I$(ROCM)/include -D__HIP_PLATFORM_AMD__ $(MPIFLAGS) -c $$f -o $(BUILD)/asan/$$(echo $$f | tr / _).o || exit 1; \
 	done
-	$(HIPCC) -O1 -g -std=c++17 --offload-arch=$(ARCH) $(INC) -Xarch_host -fsanitize=address \
-	    -c $(HIP_SRCS) -o $(BUILD)/asan/kernels.o
+	for f in $(HIP_SRCS); do \
+	  $(HIPCC) -O1 -g -fPIC -std=c++17 --offload-arch=$(ARCH) $(INC) \
+	    -c $$f -o $(BUILD)/asan/$$(basename $$f .hip).hip.o || exit 1; \
+	done
 	$(CXX) -fopenmp -fsanitize=address,undefined -o final_asan $(BUILD)/asan/*.o \
 	    -L$(MPILIB) -lmpi -Wl,-rpath-link,$(MPI_HOME)/lib -Wl,-rpath,'$$ORIGIN/$(MPILIB)' $(LDROCM) -lrccl
 
+# ThreadSanitizer build of the host paths (OpenMP parser / CPU engine / formatter) — CPU backend only.
+# Built with ROCm's clang + LLVM libomp so the Archer OMPT tool (libarcher) can tell TSan about OpenMP
+# barriers/tasks; libgomp is not TSan-aware and every parallel-region join reads as a race.
+#   make tsan && OMP_TOOL_LIBRARIES=$(ROCM)/lib/llvm/lib/libarcher.so mpiexec -np 2 ./final_tsan --backend=cpu < in
+TSAN_CXX  := $(ROCM)/lib/llvm/bin/clang++
+tsan: $(MPILIB)/libmpi.so
+	@mkdir -p $(BUILD)/tsan
+	for f in $(CORE_SRCS) $(COMM_SRCS) csrc/apps/final.cpp; do \
+	  $(TSAN_CXX) -O1 -g -std=c++17 -fopenmp -fsanitize=thread $(INC) \
+	    -I$(ROCM)/include -D__HIP_PLATFORM_AMD__ $(MPIFLAGS) -c $$f -o $(BUILD)/tsan/$$(echo $$f | tr / _).o || exit 1; \
+	done
+	for f in $(HIP_SRCS); do \
+	  $(HIPCC) -O1 -g -fPIC -std=c++17 --offload-arch=$(ARCH) $(INC) -c $$f -o $(BUILD)/tsan/$$(basename $$f .hip).hip.o || exit 1; \
+	done
+	$(TSAN_CXX) -fopenmp -fsanitize=thread -o final_tsan $(BUILD)/tsan/*.o \
+	    -L$(MPILIB) -lmpi -Wl,-rpath-link,$(MPI_HOME)/lib -Wl,-rpath,'$$ORIGIN/$(MPILIB)' \
+	    -L$(ROCM)/lib/llvm/lib -Wl,-rpath,$(ROCM)/lib/llvm/lib $(LDROCM) -lrccl
+
 clean:
-	rm -rf $(BUILD) final final_asan $(PKG_LIB)
+	rm -rf $(BUILD) final final_asan final_tsan $(PKG_LIB)
 
 run: build
 	$(MPI_HOME)/bin/mpiexec -np $(NP) ./final < $(INPUT)

@@ -2,13 +2,18 @@
 //     mpiexec -np N ./final < inputX.txt   ->   "#i: score: S, n: N, k: K" per Seq2, input order.
 //
 // Flow (reference call stacks E2/E3), re-designed:
-//   1. MPI bootstrap; rank -> GPU by node-local rank (reference: every rank on GPU 0, B14).
-//   2. Root reads + parses stdin in bulk (OpenMP tokeniser; reference: racy parallel fscanf, B2).
+//   1. MPI bootstrap; rank -> GPU by node-local rank or --device-map (reference: all ranks on GPU 0, B14).
+//   2. Root reads + parses the input: in bulk (OpenMP tokeniser; reference: racy parallel fscanf, B2), or
+//      in bounded batches (--batch-records, parse of batch b+1 overlapped with the search of batch b).
 //   3. Exact-count header/Seq1 broadcast (reference: 16 ints into int[4], B3).
-//   4. Cost-balanced contiguous partition, valid for any -np (reference: B4/B5/B6).
+//   4. Decomposition (--partition):
+//        cost/even — contiguous record ranges, cost-balanced by default, valid for any -np (B4/B5/B6);
+//        offsets   — context parallel: every rank searches a share of EVERY record's
+//                    offset range; one MAX all-reduce of packed 64-bit keys combines them (the Reduce the
+//                    reference never had). For few huge records, or fewer records than GPUs.
 //   5. Distribution by transport:
-//        shm  — root parses once into an MPI shared window; each rank DMAs its own slice over its own
-//               PCIe link and writes results back in place (single node; no payload copies at all);
+//        shm  — root parses once into an MPI shared window; each rank reads its slice over its own PCIe
+//               link (zero-copy when the window is pinned) and writes results back in place;
 //        rccl — root uploads, RCCL grouped send/recv scatters slices over xGMI, results gathered back;
 //        mpi  — host Scatterv/Gatherv (CPU backend, or GPU ranks without a shared window).
 //   6. Every rank runs its engine (HIP kernels, or the OpenMP CPU engine), root prints in order.
@@ -19,7 +24,9 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <future>
 #include <memory>
+#include <sstream>
 #include <string>
 #include <vector>
 
@@ -34,6 +41,7 @@
 #include "moc/runtime/hip_check.hpp"
 #include "moc/runtime/log.hpp"
 #include "moc/runtime/timer.hpp"
+#include "moc/runtime/trace.hpp"
 #include "moc/score_table.hpp"
 
 using namespace moc;
@@ -45,27 +53,42 @@ const char* kUsage =
     "  --backend=auto|hip|cpu      compute engine (auto: hip when a GPU is visible)\n"
     "  --transport=auto|shm|rccl|mpi   record distribution (auto: shm on one node, else rccl/mpi)\n"
     "  --semantics=reference|spec  candidate set (spec adds the un-mutated final offset, bug B8)\n"
-    "  --partition=cost|even       rank decomposition\n"
+    "  --partition=cost|even|offsets   rank decomposition (offsets: split every record's offset range)\n"
+    "  --batch-records=B           streaming mode: parse/search/print B records at a time (0 = all at once)\n"
+    "  --batch-chars=C             streaming mode: also cap a batch at C letters\n"
+    "  --skip-records=S            start at record #S (resume a partially printed run)\n"
+    "  --input=PATH                read PATH instead of stdin\n"
     "  --timing                    per-phase JSON on stderr (root)\n"
     "  --strict-limits             enforce |Seq1|<=3000, |Seq2|<=2000 (PDF p.5-6)\n"
+    "  --max-l1=L --max-l2=L       explicit length limits (0 = unlimited)\n"
     "  --device=K                  force device K (default: node-local rank %% devices)\n"
+    "  --device-map=a,b,...        node-local rank i -> device map[i %% len]\n"
+    "  --pin-window=0|1            page-lock the shm window so GPU ranks stream it zero-copy (default 1)\n"
     "  --chunk-records=R --chunk-bytes=B   pipeline chunk sizes\n"
     "  --threads=T                 OpenMP threads (default: OMP_NUM_THREADS / all)\n"
     "  --log-level=error|warn|info|debug\n"
     "  --inject-fault=PHASE[:RANK] test hook: fail at parse|bcast|distribute|compute|gather\n"
     "every flag can also be given as environment variable MOC_<FLAG> (e.g. MOC_BACKEND=cpu)\n";
 
-const std::vector<std::string> kKnown = {"backend", "transport", "semantics", "partition", "timing",
-                                         "strict-limits", "device", "chunk-records", "chunk-bytes", "threads",
-                                         "log-level", "inject-fault", "help"};
+const std::vector<std::string> kKnown = {
+    "backend", "transport", "semantics", "partition", "batch-records", "batch-chars", "skip-records", "input",
+    "timing", "strict-limits", "max-l1", "max-l2", "device", "device-map", "pin-window", "chunk-records",
+    "chunk-bytes", "threads", "log-level", "inject-fault", "help"};
 
 struct Header {
   int32_t w[4];
   int32_t semantics;
-  int32_t status;  // 0 ok, else parse error on root
+  int32_t status;  // 0 ok, else input error on root
   int64_t L1;
+  int64_t n_total;      // number_of_sequences
+  int64_t first_index;  // --skip-records actually applied
+};
+
+struct BatchHeader {
   int64_t n;
   int64_t total_chars;
+  int32_t status;  // 0 ok, else input error on root
+  int32_t pad;
 };
 
 struct FaultHook {
@@ -82,6 +105,25 @@ std::string to_lower(std::string s) {
   return s;
 }
 
+std::vector<int> parse_int_list(const std::string& s) {
+  std::vector<int> v;
+  std::stringstream ss(s);
+  std::string tok;
+  while (std::getline(ss, tok, ','))
+    if (!tok.empty()) v.push_back(std::stoi(tok));
+  return v;
+}
+
+// Drops the first s records of a batch (bulk mode + --skip-records).
+void drop_front(RecordBatch& b, int64_t s) {
+  s = std::min<int64_t>(s, b.size());
+  if (s <= 0) return;
+  const int64_t c0 = b.offsets[s];
+  b.codes.erase(b.codes.begin(), b.codes.begin() + c0);
+  b.offsets.erase(b.offsets.begin(), b.offsets.begin() + s);
+  for (auto& o : b.offsets) o -= c0;
+}
+
 // Runs the selected engine on one contiguous slice (host buffers).
 struct RankEngine {
   bool gpu = false;
@@ -90,6 +132,7 @@ struct RankEngine {
   std::vector<uint8_t> seq1;
   Semantics sem = Semantics::Reference;
   int threads = 0;
+  double kernel_ms = 0;  // accumulated device time of the search kernels
 
   void set_problem(const Weights& w, const std::vector<uint8_t>& s1, Semantics s) {
     sem = s;
@@ -97,311 +140,560 @@ struct RankEngine {
     table = ScoreTable::build(w);
     if (gpu) hip->set_problem(w, s1.data(), static_cast<int64_t>(s1.size()), s);
   }
-  void solve(const uint8_t* codes, const int64_t* offsets, int64_t n, Result* out) {
-    if (n <= 0) return;
-    if (gpu) {
-      hip->solve(codes, offsets, n, out);
-      return;
-    }
+  static RecordBatch copy_slice(const uint8_t* codes, const int64_t* offsets, int64_t n) {
     RecordBatch b;
     b.codes.assign(codes + offsets[0], codes + offsets[n]);
     b.offsets.resize(static_cast<size_t>(n) + 1);
     for (int64_t i = 0; i <= n; ++i) b.offsets[i] = offsets[i] - offsets[0];
-    solve_batch_cpu(table, seq1.data(), static_cast<int64_t>(seq1.size()), b, out, sem, threads);
+    return b;
+  }
+  void solve(const uint8_t* codes, const int64_t* offsets, int64_t n, Result* out) {
+    if (n <= 0) return;
+    if (gpu) {
+      hip->solve(codes, offsets, n, out);
+      kernel_ms += hip->stats().kernel_ms;
+      return;
+    }
+    solve_batch_cpu(table, seq1.data(), static_cast<int64_t>(seq1.size()), copy_slice(codes, offsets, n), out, sem,
+                    threads);
+  }
+  // Context-parallel share `part` of `parts` of every record -> packed keys.
+  void solve_keys(const uint8_t* codes, const int64_t* offsets, int64_t n, int part, int parts, uint64_t* keys) {
+    if (n <= 0) return;
+    if (gpu) {
+      hip->search_keys(codes, offsets, n, part, parts, keys);
+      kernel_ms += hip->stats().kernel_ms;
+      return;
+    }
+    solve_keys_cpu(table, seq1.data(), static_cast<int64_t>(seq1.size()), copy_slice(codes, offsets, n), part, parts,
+                   keys, sem, threads);
   }
 };
 
-int run(MpiContext& ctx, int argc, char** argv) {
-  Flags flags(argc, argv);
-  if (flags.get_bool("help", false)) {
-    if (ctx.rank == kRoot) std::fputs(kUsage, stdout);
-    return 0;
-  }
-  auto unknown = flags.unknown(kKnown);
-  if (!unknown.empty()) {
-    if (ctx.rank == kRoot) std::fprintf(stderr, "unknown flag --%s\n%s", unknown[0].c_str(), kUsage);
-    return 2;
-  }
-  log_set_level(flags.get("log-level", "warn"));
-  const int threads = static_cast<int>(flags.get_int("threads", 0));
-  if (threads > 0) omp_set_num_threads(threads);
-  FaultHook fault;
-  {
-    std::string f = flags.get("inject-fault", "");
-    auto colon = f.find(':');
-    fault.phase = f.substr(0, colon);
-    if (colon != std::string::npos) fault.rank = std::stoi(f.substr(colon + 1));
-  }
-  const bool timing = flags.get_bool("timing", false);
-  const std::string sem_s = to_lower(flags.get("semantics", "reference"));
-  if (sem_s != "reference" && sem_s != "spec") throw Error("--semantics must be reference|spec");
-  const Semantics sem = sem_s == "spec" ? Semantics::Spec : Semantics::Reference;
+class Job {
+ public:
+  Job(MpiContext& ctx, const Flags& flags) : ctx_(ctx), flags_(flags) {}
+  int run();
 
-  // ---- 1. engine / device selection (per rank), transport agreement (collective)
-  std::string backend = to_lower(flags.get("backend", "auto"));
+ private:
+  void setup_engine();
+  void run_batch(RecordBatch* rb, int64_t n, int64_t total_chars, int64_t first_index);
+  void batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds, bool cp);
+  void batch_mpi(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds, bool cp);
+  void batch_rccl(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds, bool cp);
+  void print(const Result* r, int64_t n, int64_t first_index);  // first_index relative to the batch
+  void report(const Header& h);
+
+  MpiContext& ctx_;
+  const Flags& flags_;
+  FaultHook fault_;
+  RankEngine eng_;
+  int device_ = -1;
+  bool all_gpu_ = false;
+  std::string transport_, partition_;
+  bool pin_window_ = true;
+  std::unique_ptr<RcclComm> nccl_;
+  PhaseTimer pt_;
+  Stopwatch total_;
+  double compute_ms_ = 0;
+  int64_t cells_ = 0, chars_ = 0, records_ = 0, batches_ = 0;
+  int64_t first_index_ = 0;      // global index of the current batch's first record
+  std::vector<Result> results_;  // root: results of the current batch (mpi/rccl transports)
+};
+
+void Job::setup_engine() {
+  const int threads = static_cast<int>(flags_.get_int("threads", 0));
+  if (threads > 0) omp_set_num_threads(threads);
+  const std::string backend = to_lower(flags_.get("backend", "auto"));
+  if (backend != "auto" && backend != "hip" && backend != "cpu") throw Error("--backend must be auto|hip|cpu");
   const int ndev = (backend == "cpu") ? 0 : device_count();
   if (backend == "hip" && ndev == 0) throw Error("--backend=hip but no HIP device is visible");
-  RankEngine eng;
-  eng.threads = threads;
-  eng.gpu = ndev > 0;
-  int device = -1;
-  if (eng.gpu) {
-    device = select_device(ctx.local_rank, static_cast<int>(flags.get_int("device", -1)));
+  eng_.threads = threads;
+  eng_.gpu = ndev > 0;
+  if (eng_.gpu) {
+    int requested = static_cast<int>(flags_.get_int("device", -1));
+    const std::vector<int> map = parse_int_list(flags_.get("device-map", ""));
+    if (requested < 0 && !map.empty()) requested = map[static_cast<size_t>(ctx_.local_rank) % map.size()];
+    device_ = select_device(ctx_.local_rank, requested);
     EngineOptions eo;
-    eo.device = device;
-    eo.chunk_records = flags.get_int("chunk-records", eo.chunk_records);
-    eo.chunk_bytes = flags.get_int("chunk-bytes", eo.chunk_bytes);
-    eng.hip = std::make_unique<HipEngine>(eo);
+    eo.device = device_;
+    eo.chunk_records = flags_.get_int("chunk-records", eo.chunk_records);
+    eo.chunk_bytes = flags_.get_int("chunk-bytes", eo.chunk_bytes);
+    eng_.hip = std::make_unique<HipEngine>(eo);
   }
-  int all_gpu = eng.gpu ? 1 : 0;
-  MPI_Allreduce(MPI_IN_PLACE, &all_gpu, 1, MPI_INT, MPI_MIN, ctx.world);
-  std::string transport = to_lower(flags.get("transport", "auto"));
-  if (transport == "auto") transport = ctx.single_node() ? "shm" : (all_gpu ? "rccl" : "mpi");
-  if (transport == "shm" && !ctx.single_node()) throw Error("--transport=shm needs all ranks on one node");
-  if (transport == "rccl" && !all_gpu) throw Error("--transport=rccl needs a GPU on every rank");
-  if (transport != "shm" && transport != "rccl" && transport != "mpi") throw Error("unknown --transport " + transport);
-  MOC_LOG_INFO("rank %d/%d host %s local %d/%d engine=%s device=%d transport=%s", ctx.rank, ctx.size,
-               ctx.hostname.c_str(), ctx.local_rank, ctx.local_size, eng.gpu ? "hip" : "cpu", device,
-               transport.c_str());
+  int all_gpu = eng_.gpu ? 1 : 0;
+  MPI_Allreduce(MPI_IN_PLACE, &all_gpu, 1, MPI_INT, MPI_MIN, ctx_.world);
+  all_gpu_ = all_gpu != 0;
+  transport_ = to_lower(flags_.get("transport", "auto"));
+  if (transport_ == "auto") transport_ = ctx_.single_node() ? "shm" : (all_gpu_ ? "rccl" : "mpi");
+  if (transport_ == "shm" && !ctx_.single_node()) throw Error("--transport=shm needs all ranks on one node");
+  if (transport_ == "rccl" && !all_gpu_) throw Error("--transport=rccl needs a GPU on every rank");
+  if (transport_ != "shm" && transport_ != "rccl" && transport_ != "mpi")
+    throw Error("unknown --transport " + transport_);
+  partition_ = to_lower(flags_.get("partition", "cost"));
+  if (partition_ != "cost" && partition_ != "even" && partition_ != "offsets")
+    throw Error("--partition must be cost|even|offsets");
+  pin_window_ = flags_.get_bool("pin-window", true);
+  if (transport_ == "rccl") nccl_ = std::make_unique<RcclComm>(ctx_, device_);
+  MOC_LOG_INFO("rank %d/%d host %s local %d/%d engine=%s device=%d transport=%s partition=%s", ctx_.rank, ctx_.size,
+               ctx_.hostname.c_str(), ctx_.local_rank, ctx_.local_size, eng_.gpu ? "hip" : "cpu", device_,
+               transport_.c_str(), partition_.c_str());
+}
 
-  PhaseTimer pt;
-  Stopwatch total;
-  total.start();
+void Job::print(const Result* r, int64_t n, int64_t first_index) {
+  if (ctx_.rank != kRoot) return;
+  pt_.begin("print");
+  write_results(stdout, r, n, first_index_ + first_index);
+  pt_.end();
+}
 
-  // ---- 2. root reads + parses
-  Problem prob;
+// One batch of records: decomposition + distribution + search + combine + print.
+// rb: the batch (root only; offsets rebased to 0), n / total_chars known on every rank.
+void Job::run_batch(RecordBatch* rb, int64_t n, int64_t total_chars, int64_t first_index) {
+  ++batches_;
+  first_index_ = first_index;
+  records_ += n;
+  chars_ += total_chars;
+  const int p = ctx_.size;
+  const bool cp = partition_ == "offsets";
+  std::vector<int64_t> bounds(static_cast<size_t>(p) + 1, 0);
+  if (ctx_.rank == kRoot) {
+    const int64_t L1 = static_cast<int64_t>(eng_.seq1.size());
+    std::vector<int64_t> len(static_cast<size_t>(n));
+    for (int64_t i = 0; i < n; ++i) {
+      len[i] = rb->length(i);
+      cells_ += record_cells(L1, len[i]);
+    }
+    if (!cp) {
+      CostModel cm = all_gpu_ ? CostModel{1.0, 200.0, 2400.0} : CostModel{1.0, 4.0, 64.0};
+      bounds = partition_ == "even" ? partition_even(n, p) : partition_by_cost(len.data(), n, L1, p, cm);
+    }
+  }
+  if (!cp) bcast_bytes(bounds.data(), sizeof(int64_t) * (p + 1), kRoot, ctx_.world);
+  if (transport_ == "shm")
+    batch_shm(rb, n, total_chars, bounds, cp);
+  else if (transport_ == "mpi")
+    batch_mpi(rb, n, total_chars, bounds, cp);
+  else
+    batch_rccl(rb, n, total_chars, bounds, cp);
+}
+
+void Job::batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds, bool cp) {
+  // layout: offsets[(N+1)] | results[N] (or keys[N] in cp mode) | codes[total]   (8-byte aligned sections)
+  const int64_t off_bytes = 8 * (n + 1);
+  const int64_t res_bytes = ((12 * n) + 7) & ~int64_t{7};
+  pt_.begin("distribute");
+  auto win = std::make_unique<SharedWindow>(ctx_, off_bytes + res_bytes + total_chars);
+  int64_t* w_offs = reinterpret_cast<int64_t*>(win->base());
+  Result* w_res = reinterpret_cast<Result*>(win->base() + off_bytes);
+  uint8_t* w_codes = reinterpret_cast<uint8_t*>(win->base() + off_bytes + res_bytes);
+  if (ctx_.rank == kRoot) {
+    const int64_t* src_off = rb->offsets.data();
+    const uint8_t* src_codes = rb->codes.data();
+    const int nt = total_chars > (1 << 20) ? omp_get_max_threads() : 1;
+#pragma omp parallel num_threads(nt)
+    {
+      const int t = omp_get_thread_num();
+      const int64_t cb = total_chars * t / nt, ce = total_chars * (t + 1) / nt;
+      std::memcpy(w_codes + cb, src_codes + cb, static_cast<size_t>(ce - cb));
+      const int64_t ob = (n + 1) * t / nt, oe = (n + 1) * (t + 1) / nt;
+      std::memcpy(w_offs + ob, src_off + ob, static_cast<size_t>(oe - ob) * 8);
+    }
+    *rb = RecordBatch{};  // the window is now the only copy
+  }
+  fault_.at("distribute", ctx_.rank);
+  win->fence();
+  pt_.end();
+  pt_.begin("compute");
+  fault_.at("compute", ctx_.rank);
+  Stopwatch sw;
+  sw.start();
+  if (cp) {
+    std::vector<uint64_t> keys(static_cast<size_t>(n), 0);
+    eng_.solve_keys(w_codes, w_offs, n, ctx_.rank, ctx_.size, keys.data());
+    sw.stop();
+    pt_.end();
+    pt_.begin("gather");
+    fault_.at("gather", ctx_.rank);
+    allreduce_max_u64(keys.data(), n, ctx_.world);
+    if (ctx_.rank == kRoot)
+      for (int64_t i = 0; i < n; ++i) w_res[i] = decode_key(keys[i], w_offs[i + 1] - w_offs[i]);
+    pt_.end();
+  } else {
+    const int64_t my_b = bounds[ctx_.rank], my_n = bounds[ctx_.rank + 1] - my_b;
+    // GPU ranks: page-lock the window so the engine streams its slice zero-copy (one kernel reading the
+    // letters over PCIe and writing the results in place) instead of staging through device buffers.
+    bool pinned = false;
+    if (eng_.gpu && pin_window_ && my_n > 0) {
+      try {
+        eng_.hip->pin(win->base(), static_cast<size_t>(win->bytes()));
+        pinned = true;
+      } catch (const std::exception& e) {
+        MOC_LOG_WARN("could not page-lock the shared window (%s); using the staged pipeline", e.what());
+      }
+    }
+    eng_.solve(w_codes, w_offs + my_b, my_n, w_res + my_b);
+    if (pinned) eng_.hip->unpin_all();
+    sw.stop();
+    pt_.end();
+    pt_.begin("gather");
+    fault_.at("gather", ctx_.rank);
+    win->fence();
+    pt_.end();
+  }
+  compute_ms_ += sw.total_ms();
+  print(w_res, n, 0);
+}
+
+void Job::batch_mpi(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds, bool cp) {
+  const int p = ctx_.size;
+  pt_.begin("distribute");
+  fault_.at("distribute", ctx_.rank);
+  if (cp) {  // every rank needs every record
+    RecordBatch all;
+    if (ctx_.rank == kRoot) all = std::move(*rb);
+    all.offsets.resize(static_cast<size_t>(n) + 1);
+    all.codes.resize(static_cast<size_t>(total_chars));
+    bcast_bytes(all.offsets.data(), 8 * (n + 1), kRoot, ctx_.world);
+    bcast_bytes(all.codes.data(), total_chars, kRoot, ctx_.world);
+    pt_.end();
+    pt_.begin("compute");
+    fault_.at("compute", ctx_.rank);
+    Stopwatch sw;
+    sw.start();
+    std::vector<uint64_t> keys(static_cast<size_t>(n), 0);
+    eng_.solve_keys(all.codes.data(), all.offsets.data(), n, ctx_.rank, ctx_.size, keys.data());
+    sw.stop();
+    compute_ms_ += sw.total_ms();
+    pt_.end();
+    pt_.begin("gather");
+    fault_.at("gather", ctx_.rank);
+    allreduce_max_u64(keys.data(), n, ctx_.world);
+    pt_.end();
+    if (ctx_.rank == kRoot) {
+      results_.resize(static_cast<size_t>(n));
+      for (int64_t i = 0; i < n; ++i) results_[i] = decode_key(keys[i], all.length(i));
+    }
+    print(results_.data(), n, 0);
+    return;
+  }
+  const int64_t my_b = bounds[ctx_.rank], my_n = bounds[ctx_.rank + 1] - my_b;
+  std::vector<int64_t> lcount(p), ldispl(p), ccount(p), cdispl(p);
+  for (int r = 0; r < p; ++r) {
+    lcount[r] = 8 * (bounds[r + 1] - bounds[r]);
+    ldispl[r] = 8 * bounds[r];
+  }
+  std::vector<int64_t> lengths;
+  if (ctx_.rank == kRoot) {
+    lengths.resize(static_cast<size_t>(n));
+    for (int64_t i = 0; i < n; ++i) lengths[i] = rb->length(i);
+    for (int r = 0; r < p; ++r) {
+      ccount[r] = rb->offsets[bounds[r + 1]] - rb->offsets[bounds[r]];
+      cdispl[r] = rb->offsets[bounds[r]];
+    }
+  }
+  bcast_bytes(ccount.data(), 8 * p, kRoot, ctx_.world);
+  std::vector<int64_t> my_len(static_cast<size_t>(my_n));
+  scatterv_bytes(lengths.data(), lcount, ldispl, my_len.data(), kRoot, ctx_.world);
+  std::vector<uint8_t> my_codes(static_cast<size_t>(ccount[ctx_.rank]));
+  scatterv_bytes(ctx_.rank == kRoot ? rb->codes.data() : nullptr, ccount, cdispl, my_codes.data(), kRoot, ctx_.world);
+  std::vector<int64_t> my_off(static_cast<size_t>(my_n) + 1, 0);
+  for (int64_t i = 0; i < my_n; ++i) my_off[i + 1] = my_off[i] + my_len[i];
+  pt_.end();
+  pt_.begin("compute");
+  fault_.at("compute", ctx_.rank);
+  std::vector<Result> mine(static_cast<size_t>(my_n));
+  Stopwatch sw;
+  sw.start();
+  eng_.solve(my_codes.data(), my_off.data(), my_n, mine.data());
+  sw.stop();
+  compute_ms_ += sw.total_ms();
+  pt_.end();
+  pt_.begin("gather");
+  fault_.at("gather", ctx_.rank);
+  std::vector<int64_t> rcount(p), rdispl(p);
+  for (int r = 0; r < p; ++r) {
+    rcount[r] = 12 * (bounds[r + 1] - bounds[r]);
+    rdispl[r] = 12 * bounds[r];
+  }
+  if (ctx_.rank == kRoot) results_.resize(static_cast<size_t>(n));
+  gatherv_bytes(mine.data(), 12 * my_n, results_.data(), rcount, rdispl, kRoot, ctx_.world);
+  pt_.end();
+  print(results_.data(), n, 0);
+}
+
+// Device buffers of one rccl batch (freed on scope exit, also when unwinding).
+struct DeviceBufs {
+  std::vector<void*> ptrs;
+  template <typename T>
+  T* alloc(int64_t bytes) {
+    void* p = nullptr;
+    MOC_HIP_CHECK(hipMalloc(&p, static_cast<size_t>(std::max<int64_t>(bytes, 16))));
+    ptrs.push_back(p);
+    return static_cast<T*>(p);
+  }
+  ~DeviceBufs() {
+    for (void* p : ptrs) (void)hipFree(p);
+  }
+};
+
+void Job::batch_rccl(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds, bool cp) {
+  RcclComm& nccl = *nccl_;
+  hipStream_t s = eng_.hip->compute_stream();
+  const int p = ctx_.size;
+  DeviceBufs bufs;
+  pt_.begin("distribute");
+  fault_.at("distribute", ctx_.rank);
+  if (cp) {
+    // root uploads the batch once; RCCL broadcasts it to every device over xGMI; each GPU searches its
+    // share of every record's offset tiles; ncclAllReduce(MAX, uint64) combines the packed keys.
+    uint8_t* d_codes = bufs.alloc<uint8_t>(total_chars);
+    int64_t* d_offs = bufs.alloc<int64_t>(8 * (n + 1));
+    std::vector<int64_t> h_offs(static_cast<size_t>(n) + 1);
+    if (ctx_.rank == kRoot) {
+      h_offs = rb->offsets;
+      MOC_HIP_CHECK(hipMemcpyAsync(d_codes, rb->codes.data(), total_chars, hipMemcpyHostToDevice, s));
+      MOC_HIP_CHECK(hipMemcpyAsync(d_offs, rb->offsets.data(), 8 * (n + 1), hipMemcpyHostToDevice, s));
+    }
+    nccl.bcast(d_codes, total_chars, kRoot, s);
+    nccl.bcast(d_offs, 8 * (n + 1), kRoot, s);
+    bcast_bytes(h_offs.data(), 8 * (n + 1), kRoot, ctx_.world);  // host copy for tile planning
+    MOC_HIP_CHECK(hipStreamSynchronize(s));
+    nccl.check_async();
+    pt_.end();
+    pt_.begin("compute");
+    fault_.at("compute", ctx_.rank);
+    Stopwatch sw;
+    sw.start();
+    auto* d_keys = bufs.alloc<unsigned long long>(8 * n);
+    eng_.hip->search_keys_device(d_codes, d_offs, h_offs.data(), n, ctx_.rank, ctx_.size, d_keys, s);
+    MOC_HIP_CHECK(hipStreamSynchronize(s));
+    sw.stop();
+    compute_ms_ += sw.total_ms();
+    pt_.end();
+    pt_.begin("gather");
+    fault_.at("gather", ctx_.rank);
+    nccl.allreduce_max_u64(d_keys, n, s);
+    if (ctx_.rank == kRoot) {
+      auto* d_res = bufs.alloc<Result>(12 * n);
+      eng_.hip->finalize_keys_device(d_offs, n, d_keys, d_res, ResultFormat::R12, s);
+      results_.resize(static_cast<size_t>(n));
+      MOC_HIP_CHECK(hipMemcpyAsync(results_.data(), d_res, 12 * n, hipMemcpyDeviceToHost, s));
+    }
+    MOC_HIP_CHECK(hipStreamSynchronize(s));
+    nccl.check_async();
+    pt_.end();
+    print(results_.data(), n, 0);
+    return;
+  }
+  const int64_t my_b = bounds[ctx_.rank], my_n = bounds[ctx_.rank + 1] - my_b;
+  // counts in bytes for codes and (absolute) offsets; each rank receives n_r+1 offsets
+  std::vector<int64_t> ccount(p), cdispl(p), ocount(p), odispl(p);
+  if (ctx_.rank == kRoot) {
+    for (int r = 0; r < p; ++r) {
+      ccount[r] = rb->offsets[bounds[r + 1]] - rb->offsets[bounds[r]];
+      cdispl[r] = rb->offsets[bounds[r]];
+    }
+  }
+  bcast_bytes(ccount.data(), 8 * p, kRoot, ctx_.world);
+  bcast_bytes(cdispl.data(), 8 * p, kRoot, ctx_.world);
+  for (int r = 0; r < p; ++r) {
+    ocount[r] = 8 * (bounds[r + 1] - bounds[r] + 1);
+    odispl[r] = 8 * bounds[r];
+  }
+  uint8_t* d_all_codes = nullptr;
+  int64_t* d_all_offs = nullptr;
+  Result* d_all_out = nullptr;
+  if (ctx_.rank == kRoot) {
+    d_all_codes = bufs.alloc<uint8_t>(total_chars);
+    d_all_offs = bufs.alloc<int64_t>(8 * (n + 1));
+    d_all_out = bufs.alloc<Result>(12 * n);
+    MOC_HIP_CHECK(hipMemcpyAsync(d_all_codes, rb->codes.data(), total_chars, hipMemcpyHostToDevice, s));
+    MOC_HIP_CHECK(hipMemcpyAsync(d_all_offs, rb->offsets.data(), 8 * (n + 1), hipMemcpyHostToDevice, s));
+  }
+  uint8_t* d_codes = bufs.alloc<uint8_t>(ccount[ctx_.rank]);
+  int64_t* d_offs = bufs.alloc<int64_t>(8 * (my_n + 1));
+  Result* d_out = bufs.alloc<Result>(12 * my_n);
+  nccl.scatterv(d_all_codes, ccount, cdispl, d_codes, kRoot, s);
+  nccl.scatterv(d_all_offs, ocount, odispl, d_offs, kRoot, s);
+  std::vector<int64_t> h_offs(static_cast<size_t>(my_n) + 1);
+  MOC_HIP_CHECK(hipMemcpyAsync(h_offs.data(), d_offs, 8 * (my_n + 1), hipMemcpyDeviceToHost, s));
+  MOC_HIP_CHECK(hipStreamSynchronize(s));
+  nccl.check_async();
+  pt_.end();
+  pt_.begin("compute");
+  fault_.at("compute", ctx_.rank);
+  Stopwatch sw;
+  sw.start();
+  // d_codes holds this rank's letters starting at absolute offset h_offs[0]
+  if (my_n > 0) eng_.hip->solve_device(d_codes - h_offs[0], d_offs, h_offs.data(), my_n, d_out, s);
+  MOC_HIP_CHECK(hipStreamSynchronize(s));
+  sw.stop();
+  compute_ms_ += sw.total_ms();
+  pt_.end();
+  pt_.begin("gather");
+  fault_.at("gather", ctx_.rank);
+  std::vector<int64_t> rcount(p), rdispl(p);
+  for (int r = 0; r < p; ++r) {
+    rcount[r] = 12 * (bounds[r + 1] - bounds[r]);
+    rdispl[r] = 12 * bounds[r];
+  }
+  nccl.gatherv(d_out, 12 * my_n, d_all_out, rcount, rdispl, kRoot, s);
+  if (ctx_.rank == kRoot) {
+    results_.resize(static_cast<size_t>(n));
+    MOC_HIP_CHECK(hipMemcpyAsync(results_.data(), d_all_out, 12 * n, hipMemcpyDeviceToHost, s));
+  }
+  MOC_HIP_CHECK(hipStreamSynchronize(s));
+  nccl.check_async();
+  pt_.end();
+  print(results_.data(), n, 0);
+}
+
+void Job::report(const Header& h) {
+  double mx[2] = {compute_ms_, eng_.kernel_ms};
+  MPI_Reduce(ctx_.rank == kRoot ? MPI_IN_PLACE : mx, mx, 2, MPI_DOUBLE, MPI_MAX, kRoot, ctx_.world);
+  if (ctx_.rank != kRoot || !flags_.get_bool("timing", false)) return;
+  const double wall_s = total_.total_ms() / 1e3;
+  std::fprintf(stderr,
+               "{\"timing\": %s, \"ranks\": %d, \"nodes\": %d, \"engine\": \"%s\", \"transport\": \"%s\", "
+               "\"partition\": \"%s\", \"batches\": %lld, \"first_index\": %lld, \"records\": %lld, "
+               "\"elements\": %lld, \"cells\": %lld, \"max_rank_compute_ms\": %.3f, \"max_rank_kernel_ms\": %.3f, "
+               "\"wall_s\": %.6f, \"elements_per_s\": %.1f, \"cells_per_s\": %.1f}\n",
+               pt_.json().c_str(), ctx_.size, ctx_.node_count, eng_.gpu ? "hip" : "cpu", transport_.c_str(),
+               partition_.c_str(), static_cast<long long>(batches_), static_cast<long long>(h.first_index),
+               static_cast<long long>(records_), static_cast<long long>(chars_), static_cast<long long>(cells_),
+               mx[0], mx[1], wall_s, wall_s > 0 ? chars_ / wall_s : 0.0, wall_s > 0 ? cells_ / wall_s : 0.0);
+}
+
+int Job::run() {
+  log_set_level(flags_.get("log-level", "warn"));
+  {
+    std::string f = flags_.get("inject-fault", "");
+    auto colon = f.find(':');
+    fault_.phase = f.substr(0, colon);
+    if (colon != std::string::npos) fault_.rank = std::stoi(f.substr(colon + 1));
+  }
+  const std::string sem_s = to_lower(flags_.get("semantics", "reference"));
+  if (sem_s != "reference" && sem_s != "spec") throw Error("--semantics must be reference|spec");
+  const Semantics sem = sem_s == "spec" ? Semantics::Spec : Semantics::Reference;
+  const int64_t batch_records = flags_.get_int("batch-records", 0);
+  const int64_t batch_chars = flags_.get_int("batch-chars", 0);
+  const int64_t skip = flags_.get_int("skip-records", 0);
+  if (batch_records < 0 || batch_chars < 0 || skip < 0) throw Error("--batch-records/--batch-chars/--skip-records >= 0");
+  const bool streaming = batch_records > 0 || batch_chars > 0;
+  ParseOptions po;
+  po.strict_limits = flags_.get_bool("strict-limits", false);
+  po.max_l1 = flags_.get_int("max-l1", 0);
+  po.max_l2 = flags_.get_int("max-l2", 0);
+
+  setup_engine();
+  total_.start();
+
+  // ---- root opens the input; parses it whole (bulk) or just its header (streaming)
   Header h{};
-  std::string parse_error;
-  if (ctx.rank == kRoot) {
-    pt.begin("parse");
+  std::string error;
+  FILE* in = stdin;
+  std::unique_ptr<StreamReader> reader;
+  RecordBatch bulk;
+  std::vector<uint8_t> seq1;
+  if (ctx_.rank == kRoot) {
+    pt_.begin("parse");
     try {
-      fault.at("parse", ctx.rank);
-      std::vector<char> text = read_stream(stdin);
-      ParseOptions po;
-      po.strict_limits = flags.get_bool("strict-limits", false);
-      prob = parse_problem(text.data(), text.size(), po);
+      fault_.at("parse", ctx_.rank);
+      const std::string path = flags_.get("input", "");
+      if (!path.empty() && !(in = std::fopen(path.c_str(), "rb"))) throw Error("cannot open --input " + path);
+      Weights w{};
+      if (streaming) {
+        reader = std::make_unique<StreamReader>(in, po);
+        w = reader->weights();
+        seq1 = reader->seq1();
+        h.n_total = reader->count();
+        h.first_index = reader->skip(skip);
+      } else {
+        std::vector<char> text = read_stream(in);
+        Problem prob = parse_problem(text.data(), text.size(), po);
+        w = prob.weights;
+        seq1 = std::move(prob.seq1);
+        bulk = std::move(prob.seq2);
+        h.n_total = bulk.size();
+        h.first_index = std::min<int64_t>(skip, h.n_total);
+        drop_front(bulk, h.first_index);
+      }
+      for (int i = 0; i < 4; ++i) h.w[i] = w.w[i];
     } catch (const std::exception& e) {
-      parse_error = e.what();
+      error = e.what();
       h.status = 1;
     }
-    pt.end();
-    for (int i = 0; i < 4; ++i) h.w[i] = prob.weights.w[i];
+    pt_.end();
     h.semantics = static_cast<int32_t>(sem);
-    h.L1 = prob.L1();
-    h.n = prob.seq2.size();
-    h.total_chars = prob.seq2.total_chars();
+    h.L1 = static_cast<int64_t>(seq1.size());
   }
 
-  // ---- 3. header + Seq1 broadcast (exact counts)
-  pt.begin("bcast");
-  fault.at("bcast", ctx.rank);
-  bcast_bytes(&h, sizeof h, kRoot, ctx.world);
+  // ---- header + Seq1 broadcast (exact counts)
+  pt_.begin("bcast");
+  fault_.at("bcast", ctx_.rank);
+  bcast_bytes(&h, sizeof h, kRoot, ctx_.world);
   if (h.status != 0) {
-    if (ctx.rank == kRoot) std::fprintf(stderr, "input error: %s\n", parse_error.c_str());
+    if (ctx_.rank == kRoot) std::fprintf(stderr, "input error: %s\n", error.c_str());
+    if (in != stdin && in) std::fclose(in);
     return 1;
   }
-  for (int i = 0; i < 4; ++i) prob.weights.w[i] = h.w[i];
-  prob.seq1.resize(static_cast<size_t>(h.L1));
-  bcast_bytes(prob.seq1.data(), h.L1, kRoot, ctx.world);
-  eng.set_problem(prob.weights, prob.seq1, sem);
-  pt.end();
+  Weights w{};
+  for (int i = 0; i < 4; ++i) w.w[i] = h.w[i];
+  seq1.resize(static_cast<size_t>(h.L1));
+  bcast_bytes(seq1.data(), h.L1, kRoot, ctx_.world);
+  eng_.set_problem(w, seq1, sem);
+  pt_.end();
 
-  // ---- 4. partition (root computes, everybody gets the bounds)
-  const int p = ctx.size;
-  std::vector<int64_t> bounds(static_cast<size_t>(p) + 1, 0);
-  if (ctx.rank == kRoot) {
-    std::vector<int64_t> len(static_cast<size_t>(h.n));
-    for (int64_t i = 0; i < h.n; ++i) len[i] = prob.seq2.length(i);
-    const std::string mode = to_lower(flags.get("partition", "cost"));
-    CostModel cm = all_gpu ? CostModel{1.0, 200.0, 2400.0} : CostModel{1.0, 4.0, 64.0};
-    bounds = mode == "even" ? partition_even(h.n, p) : partition_by_cost(len.data(), h.n, h.L1, p, cm);
-  }
-  bcast_bytes(bounds.data(), sizeof(int64_t) * (p + 1), kRoot, ctx.world);
-  const int64_t my_b = bounds[ctx.rank], my_n = bounds[ctx.rank + 1] - my_b;
-
-  // ---- 5/6. distribute + compute (+ gather)
-  std::vector<Result> results;  // root: all N (mpi/rccl transports)
-  const Result* print_from = nullptr;
-  std::unique_ptr<SharedWindow> win;
-  double compute_ms = 0;
-
-  if (transport == "shm") {
-    // layout: offsets[(N+1)] | results[N] | codes[total]   (8-byte aligned sections)
-    const int64_t off_bytes = 8 * (h.n + 1);
-    const int64_t res_bytes = ((12 * h.n) + 7) & ~int64_t{7};
-    pt.begin("distribute");
-    win = std::make_unique<SharedWindow>(ctx, off_bytes + res_bytes + h.total_chars);
-    int64_t* w_offs = reinterpret_cast<int64_t*>(win->base());
-    Result* w_res = reinterpret_cast<Result*>(win->base() + off_bytes);
-    uint8_t* w_codes = reinterpret_cast<uint8_t*>(win->base() + off_bytes + res_bytes);
-    if (ctx.rank == kRoot) {
-      const int64_t* src_off = prob.seq2.offsets.data();
-      const uint8_t* src_codes = prob.seq2.codes.data();
-#pragma omp parallel
-      {
-        const int t = omp_get_thread_num(), nt = omp_get_num_threads();
-        const int64_t cb = h.total_chars * t / nt, ce = h.total_chars * (t + 1) / nt;
-        std::memcpy(w_codes + cb, src_codes + cb, static_cast<size_t>(ce - cb));
-        const int64_t ob = (h.n + 1) * t / nt, oe = (h.n + 1) * (t + 1) / nt;
-        std::memcpy(w_offs + ob, src_off + ob, static_cast<size_t>(oe - ob) * 8);
+  int rc = 0;
+  if (!streaming) {
+    int64_t sizes[2] = {bulk.size(), bulk.total_chars()};
+    bcast_bytes(sizes, sizeof sizes, kRoot, ctx_.world);
+    run_batch(ctx_.rank == kRoot ? &bulk : nullptr, sizes[0], sizes[1], h.first_index);
+  } else {
+    // root: parse of batch b+1 runs on a helper thread while batch b is searched and printed
+    const int64_t max_rec = batch_records > 0 ? batch_records : INT64_MAX;
+    const int64_t max_chr = batch_chars > 0 ? batch_chars : INT64_MAX;
+    auto parse_next = [&reader, max_rec, max_chr]() {
+      auto b = std::make_unique<RecordBatch>();
+      reader->next_batch(max_rec, *b, max_chr);
+      return b;
+    };
+    std::future<std::unique_ptr<RecordBatch>> next;
+    if (ctx_.rank == kRoot) next = std::async(std::launch::async, parse_next);
+    int64_t first = h.first_index;
+    while (true) {
+      BatchHeader bh{};
+      std::unique_ptr<RecordBatch> cur;
+      if (ctx_.rank == kRoot) {
+        pt_.begin("parse");
+        try {
+          cur = next.get();
+          bh.n = cur->size();
+          bh.total_chars = cur->total_chars();
+          if (bh.n > 0) next = std::async(std::launch::async, parse_next);
+        } catch (const std::exception& e) {
+          error = e.what();
+          bh.status = 1;
+        }
+        pt_.end();
       }
-      prob.seq2 = RecordBatch{};  // the window is now the only copy
-    }
-    fault.at("distribute", ctx.rank);
-    win->fence();
-    pt.end();
-    pt.begin("compute");
-    fault.at("compute", ctx.rank);
-    Stopwatch sw;
-    sw.start();
-    eng.solve(w_codes, w_offs + my_b, my_n, w_res + my_b);
-    sw.stop();
-    compute_ms = sw.total_ms();
-    pt.end();
-    pt.begin("gather");
-    fault.at("gather", ctx.rank);
-    win->fence();
-    pt.end();
-    print_from = w_res;
-  } else if (transport == "mpi") {
-    pt.begin("distribute");
-    fault.at("distribute", ctx.rank);
-    std::vector<int64_t> lcount(p), ldispl(p), ccount(p), cdispl(p);
-    for (int r = 0; r < p; ++r) {
-      lcount[r] = 8 * (bounds[r + 1] - bounds[r]);
-      ldispl[r] = 8 * bounds[r];
-    }
-    std::vector<int64_t> lengths;
-    if (ctx.rank == kRoot) {
-      lengths.resize(static_cast<size_t>(h.n));
-      for (int64_t i = 0; i < h.n; ++i) lengths[i] = prob.seq2.length(i);
-      for (int r = 0; r < p; ++r) {
-        ccount[r] = prob.seq2.offsets[bounds[r + 1]] - prob.seq2.offsets[bounds[r]];
-        cdispl[r] = prob.seq2.offsets[bounds[r]];
+      bcast_bytes(&bh, sizeof bh, kRoot, ctx_.world);
+      if (bh.status != 0) {
+        if (ctx_.rank == kRoot) std::fprintf(stderr, "input error: %s\n", error.c_str());
+        rc = 1;
+        break;
       }
-    }
-    bcast_bytes(ccount.data(), 8 * p, kRoot, ctx.world);
-    std::vector<int64_t> my_len(static_cast<size_t>(my_n));
-    scatterv_bytes(lengths.data(), lcount, ldispl, my_len.data(), kRoot, ctx.world);
-    std::vector<uint8_t> my_codes(static_cast<size_t>(ccount[ctx.rank]));
-    scatterv_bytes(prob.seq2.codes.data(), ccount, cdispl, my_codes.data(), kRoot, ctx.world);
-    std::vector<int64_t> my_off(static_cast<size_t>(my_n) + 1, 0);
-    for (int64_t i = 0; i < my_n; ++i) my_off[i + 1] = my_off[i] + my_len[i];
-    pt.end();
-    pt.begin("compute");
-    fault.at("compute", ctx.rank);
-    std::vector<Result> mine(static_cast<size_t>(my_n));
-    Stopwatch sw;
-    sw.start();
-    eng.solve(my_codes.data(), my_off.data(), my_n, mine.data());
-    sw.stop();
-    compute_ms = sw.total_ms();
-    pt.end();
-    pt.begin("gather");
-    fault.at("gather", ctx.rank);
-    std::vector<int64_t> rcount(p), rdispl(p);
-    for (int r = 0; r < p; ++r) {
-      rcount[r] = 12 * (bounds[r + 1] - bounds[r]);
-      rdispl[r] = 12 * bounds[r];
-    }
-    if (ctx.rank == kRoot) results.resize(static_cast<size_t>(h.n));
-    gatherv_bytes(mine.data(), 12 * my_n, results.data(), rcount, rdispl, kRoot, ctx.world);
-    pt.end();
-    print_from = results.data();
-  } else {  // rccl
-    RcclComm nccl(ctx, device);
-    hipStream_t s = eng.hip->compute_stream();
-    pt.begin("distribute");
-    fault.at("distribute", ctx.rank);
-    // counts in bytes for codes and (absolute) offsets; each rank receives n_r+1 offsets
-    std::vector<int64_t> ccount(p), cdispl(p), ocount(p), odispl(p);
-    if (ctx.rank == kRoot) {
-      for (int r = 0; r < p; ++r) {
-        ccount[r] = prob.seq2.offsets[bounds[r + 1]] - prob.seq2.offsets[bounds[r]];
-        cdispl[r] = prob.seq2.offsets[bounds[r]];
-      }
-    }
-    bcast_bytes(ccount.data(), 8 * p, kRoot, ctx.world);
-    bcast_bytes(cdispl.data(), 8 * p, kRoot, ctx.world);
-    for (int r = 0; r < p; ++r) {
-      ocount[r] = 8 * (bounds[r + 1] - bounds[r] + 1);
-      odispl[r] = 8 * bounds[r];
-    }
-    uint8_t *d_all_codes = nullptr, *d_codes = nullptr;
-    int64_t *d_all_offs = nullptr, *d_offs = nullptr;
-    Result *d_out = nullptr, *d_all_out = nullptr;
-    if (ctx.rank == kRoot) {
-      MOC_HIP_CHECK(hipMalloc(&d_all_codes, std::max<int64_t>(h.total_chars, 1)));
-      MOC_HIP_CHECK(hipMalloc(&d_all_offs, 8 * (h.n + 1)));
-      MOC_HIP_CHECK(hipMalloc(&d_all_out, std::max<int64_t>(12 * h.n, 4)));
-      MOC_HIP_CHECK(hipMemcpyAsync(d_all_codes, prob.seq2.codes.data(), h.total_chars, hipMemcpyHostToDevice, s));
-      MOC_HIP_CHECK(hipMemcpyAsync(d_all_offs, prob.seq2.offsets.data(), 8 * (h.n + 1), hipMemcpyHostToDevice, s));
-    }
-    MOC_HIP_CHECK(hipMalloc(&d_codes, std::max<int64_t>(ccount[ctx.rank], 1)));
-    MOC_HIP_CHECK(hipMalloc(&d_offs, 8 * (my_n + 1)));
-    MOC_HIP_CHECK(hipMalloc(&d_out, std::max<int64_t>(12 * my_n, 4)));
-    nccl.scatterv(d_all_codes, ccount, cdispl, d_codes, kRoot, s);
-    nccl.scatterv(d_all_offs, ocount, odispl, d_offs, kRoot, s);
-    std::vector<int64_t> h_offs(static_cast<size_t>(my_n) + 1);
-    MOC_HIP_CHECK(hipMemcpyAsync(h_offs.data(), d_offs, 8 * (my_n + 1), hipMemcpyDeviceToHost, s));
-    MOC_HIP_CHECK(hipStreamSynchronize(s));
-    nccl.check_async();
-    pt.end();
-    pt.begin("compute");
-    fault.at("compute", ctx.rank);
-    Stopwatch sw;
-    sw.start();
-    // d_codes holds this rank's letters starting at absolute offset h_offs[0]
-    if (my_n > 0) eng.hip->solve_device(d_codes - h_offs[0], d_offs, h_offs.data(), my_n, d_out, s);
-    MOC_HIP_CHECK(hipStreamSynchronize(s));
-    sw.stop();
-    compute_ms = sw.total_ms();
-    pt.end();
-    pt.begin("gather");
-    fault.at("gather", ctx.rank);
-    std::vector<int64_t> rcount(p), rdispl(p);
-    for (int r = 0; r < p; ++r) {
-      rcount[r] = 12 * (bounds[r + 1] - bounds[r]);
-      rdispl[r] = 12 * bounds[r];
-    }
-    nccl.gatherv(d_out, 12 * my_n, d_all_out, rcount, rdispl, kRoot, s);
-    if (ctx.rank == kRoot) {
-      results.resize(static_cast<size_t>(h.n));
-      MOC_HIP_CHECK(hipMemcpyAsync(results.data(), d_all_out, 12 * h.n, hipMemcpyDeviceToHost, s));
-    }
-    MOC_HIP_CHECK(hipStreamSynchronize(s));
-    nccl.check_async();
-    pt.end();
-    (void)hipFree(d_all_codes);
-    (void)hipFree(d_all_offs);
-    (void)hipFree(d_all_out);
-    (void)hipFree(d_codes);
-    (void)hipFree(d_offs);
-    (void)hipFree(d_out);
-    print_from = results.data();
-  }
-
-  // ---- print (root) + timing
-  double max_compute = compute_ms;
-  MPI_Reduce(ctx.rank == kRoot ? MPI_IN_PLACE : &max_compute, &max_compute, 1, MPI_DOUBLE, MPI_MAX, kRoot, ctx.world);
-  if (ctx.rank == kRoot) {
-    pt.begin("print");
-    write_results(stdout, print_from, h.n, 0);
-    pt.end();
-    total.stop();
-    if (timing) {
-      const double wall_s = total.total_ms() / 1e3;
-      std::fprintf(stderr,
-                   "{\"timing\": %s, \"ranks\": %d, \"nodes\": %d, \"engine\": \"%s\", \"transport\": \"%s\", "
-                   "\"records\": %lld, \"elements\": %lld, \"max_rank_compute_ms\": %.3f, \"wall_s\": %.6f, "
-                   "\"elements_per_s\": %.1f}\n",
-                   pt.json().c_str(), ctx.size, ctx.node_count, eng.gpu ? "hip" : "cpu", transport.c_str(),
-                   static_cast<long long>(h.n), static_cast<long long>(h.total_chars), max_compute, wall_s,
-                   wall_s > 0 ? h.total_chars / wall_s : 0.0);
+      if (bh.n == 0) break;
+      run_batch(cur.get(), bh.n, bh.total_chars, first);
+      first += bh.n;
     }
   }
-  MPI_Barrier(ctx.world);
-  return 0;
+  if (in != stdin && in) std::fclose(in);
+  total_.stop();
+  report(h);
+  MPI_Barrier(ctx_.world);
+  return rc;
 }
 
 }  // namespace
@@ -410,7 +702,18 @@ int main(int argc, char** argv) {
   MpiContext ctx(&argc, &argv);
   int rc = 0;
   try {
-    rc = run(ctx, argc, argv);
+    Flags flags(argc, argv);
+    if (flags.get_bool("help", false)) {
+      if (ctx.rank == kRoot) std::fputs(kUsage, stdout);
+      return 0;
+    }
+    auto unknown = flags.unknown(kKnown);
+    if (!unknown.empty()) {
+      if (ctx.rank == kRoot) std::fprintf(stderr, "unknown flag --%s\n%s", unknown[0].c_str(), kUsage);
+      return 2;
+    }
+    Job job(ctx, flags);
+    rc = job.run();
   } catch (const std::exception& e) {
     ctx.abort(3, e.what());
   }

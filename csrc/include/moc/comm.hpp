@@ -54,6 +54,9 @@ void scatterv_bytes(const void* sendbuf, const std::vector<int64_t>& counts, con
 void gatherv_bytes(const void* sendbuf, int64_t count, void* recvbuf, const std::vector<int64_t>& counts,
                    const std::vector<int64_t>& displs, int root, MPI_Comm comm);
 
+// In-place element-wise MAX over all ranks of n uint64 values (context-parallel key combine, §5.7).
+void allreduce_max_u64(uint64_t* buf, int64_t n, MPI_Comm comm);
+
 class SharedWindow {
  public:
   // Collective over ctx.node; only the node's local rank 0 allocates `bytes` (others pass 0).
@@ -85,6 +88,8 @@ class RcclComm {
   // Inverse: every rank != root sends its slice to root, which receives it at displs[r].
   void gatherv(const void* d_send, int64_t count, void* d_recv, const std::vector<int64_t>& counts,
                const std::vector<int64_t>& displs, int root, hipStream_t s);
+  // In-place element-wise MAX of n uint64 device values over all ranks (packed candidate keys).
+  void allreduce_max_u64(void* dbuf, int64_t n, hipStream_t s);
   void check_async() const;  // ncclCommGetAsyncError -> throw
   ncclComm_t comm() const { return comm_; }
 

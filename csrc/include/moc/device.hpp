@@ -119,8 +119,13 @@ void launch_swipe(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStr
 void launch_short(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStream_t stream);
 
 // Tile kernel + finalize for the long records listed in `plan`; results -> out (format fmt).
+// plan.long_recs == nullptr means the identity list (record li of the batch).
 void launch_tiles(const ProblemView& pv, const BatchView& bv, const Plan& plan, void* out, int fmt,
                   hipStream_t stream);
+// The two halves separately (context-parallel mode: keys are max-reduced across ranks in between).
+// launch_tile_keys zeroes plan.keys[0..n_long) and max-accumulates the plan's tiles into them.
+void launch_tile_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream);
+void launch_finalize_keys(const BatchView& bv, const Plan& plan, void* out, int fmt, hipStream_t stream);
 
 // One-wave self-test of the DPP / shuffle primitives (192 ints, see align_kernels.hip).
 void launch_dpp_probe(int* d_out, hipStream_t stream);

@@ -79,6 +79,17 @@ class HipEngine {
   void solve_device(const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets, int64_t n,
                     Result* d_out, hipStream_t stream);
 
+  // Context-parallel search: this engine evaluates part `part` of `parts` of the batch's
+  // global list of 63-offset tiles and writes one packed 64-bit key per record (moc::encode_key; 0 =
+  // no candidate in this part). A MAX all-reduce of the keys over the parts + finalize_keys gives the
+  // full answer; this splits single huge records across GPUs.
+  void search_keys_device(const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets, int64_t n,
+                          int part, int parts, unsigned long long* d_keys, hipStream_t stream);
+  void finalize_keys_device(const int64_t* d_offsets, int64_t n, const unsigned long long* d_keys, void* d_out,
+                            ResultFormat fmt, hipStream_t stream);
+  // Host-memory form of search_keys_device (uploads the batch, returns host keys; synchronous).
+  void search_keys(const uint8_t* codes, const int64_t* offsets, int64_t n, int part, int parts, uint64_t* keys);
+
   // Page-locks a host range for the lifetime of the engine (or until unpin); enables the direct path.
   void pin(const void* p, size_t bytes);
   void unpin_all();

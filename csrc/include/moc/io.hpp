@@ -32,6 +32,34 @@ std::vector<char> read_stream(FILE* f);
 // separates tokens, exactly like fscanf %d/%s. Throws moc::Error with a precise message.
 Problem parse_problem(const char* data, size_t len, const ParseOptions& opt = {});
 
+// Incremental reader for the streaming mode (`final --batch-records=B`): parses the
+// header up front, then hands out the records in bounded batches, so host memory is O(batch) instead of
+// O(input). Same token rules and error messages as parse_problem. skip() consumes records without
+// encoding them (`--skip-records`, resuming a partially printed run).
+class StreamReader {
+ public:
+  explicit StreamReader(FILE* f, const ParseOptions& opt = {}, size_t block_bytes = size_t{8} << 20);
+  const Weights& weights() const { return weights_; }
+  const std::vector<uint8_t>& seq1() const { return seq1_; }
+  int64_t count() const { return count_; }         // number_of_sequences from the header
+  int64_t next_index() const { return next_; }     // index of the next record to be read
+  int64_t skip(int64_t records);                   // returns the number actually skipped
+  // Parses up to max_records (and, after the first record, at most max_chars letters) of the following
+  // records into `out` (offsets rebased to 0). Returns the number of records (0 once all are read).
+  int64_t next_batch(int64_t max_records, RecordBatch& out, int64_t max_chars = INT64_MAX);
+
+ private:
+  bool token(const char*& b, const char*& e);  // next token, refilling the buffer as needed
+  FILE* f_;
+  ParseOptions opt_;
+  std::vector<char> buf_;
+  size_t pos_ = 0, len_ = 0;
+  bool eof_ = false;
+  Weights weights_{};
+  std::vector<uint8_t> seq1_;
+  int64_t count_ = 0, next_ = 0, l2_cap_ = 0;
+};
+
 // Formats "#i: score: S, n: N, k: K\n" rows (main.c:204) for results[0..n), numbering from
 // first_index, in parallel, then writes them with one fwrite.
 void write_results(FILE* f, const Result* results, int64_t n, int64_t first_index = 0);

@@ -45,18 +45,12 @@ class Stopwatch {
   bool running_ = false;
 };
 
-// Ordered named phases, emitted as one JSON object (the --timing output).
+// Ordered named phases, emitted as one JSON object (the --timing output). Each phase is also a roctx
+// range (runtime/trace.hpp), so profiler timelines carry the same phase names.
 class PhaseTimer {
  public:
-  void begin(const std::string& name) {
-    cur_ = name;
-    sw_.reset();
-    sw_.start();
-  }
-  void end() {
-    sw_.stop();
-    add(cur_, sw_.total_ms());
-  }
+  void begin(const std::string& name);  // closes the open phase, if any
+  void end();
   void add(const std::string& name, double ms) {
     for (auto& p : phases_)
       if (p.first == name) {
@@ -75,6 +69,7 @@ class PhaseTimer {
 
  private:
   std::string cur_;
+  bool open_ = false;
   Stopwatch sw_;
   std::vector<std::pair<std::string, double>> phases_;
 };

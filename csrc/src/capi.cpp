@@ -122,6 +122,27 @@ int moc_cpu_solve(const int32_t* weights4, const uint8_t* seq1, int64_t L1, cons
   });
 }
 
+int moc_cpu_solve_keys(const int32_t* weights4, const uint8_t* seq1, int64_t L1, const uint8_t* codes,
+                       const int64_t* offsets, int64_t n, int semantics, int part, int parts, int threads,
+                       uint64_t* keys) {
+  return guard([&] {
+    moc::Weights w = weights_of(weights4);
+    moc::RecordBatch b = view_batch(codes, offsets, n);
+    moc::validate_score_range(w, std::max<int64_t>(b.max_length(), 1));
+    moc::ScoreTable t = moc::ScoreTable::build(w);
+    moc::solve_keys_cpu(t, seq1, L1, b, part, parts, keys, static_cast<moc::Semantics>(semantics), threads);
+  });
+}
+
+int moc_decode_keys(const uint64_t* keys, const int64_t* offsets, int64_t n, moc_result* out) {
+  return guard([&] {
+    for (int64_t i = 0; i < n; ++i) {
+      moc::Result r = moc::decode_key(keys[i], offsets[i + 1] - offsets[i]);
+      std::memcpy(out + i, &r, sizeof r);
+    }
+  });
+}
+
 int moc_brute_force(const int32_t* weights4, const uint8_t* seq1, int64_t L1, const uint8_t* codes,
                     const int64_t* offsets, int64_t n, int semantics, moc_result* out) {
   return guard([&] {
@@ -240,6 +261,30 @@ int moc_engine_solve_device(void* e, const uint8_t* d_codes, const int64_t* d_of
     static_cast<moc::HipEngine*>(e)->solve_device(d_codes, d_offsets, h_offsets, n,
                                                   reinterpret_cast<moc::Result*>(d_out),
                                                   static_cast<hipStream_t>(stream));
+  });
+}
+
+int moc_engine_search_keys(void* e, const uint8_t* codes, const int64_t* offsets, int64_t n, int part, int parts,
+                           uint64_t* keys) {
+  return guard([&] { static_cast<moc::HipEngine*>(e)->search_keys(codes, offsets, n, part, parts, keys); });
+}
+
+int moc_engine_search_keys_device(void* e, const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets,
+                                  int64_t n, int part, int parts, uint64_t* d_keys, void* stream) {
+  return guard([&] {
+    static_cast<moc::HipEngine*>(e)->search_keys_device(d_codes, d_offsets, h_offsets, n, part, parts,
+                                                        reinterpret_cast<unsigned long long*>(d_keys),
+                                                        static_cast<hipStream_t>(stream));
+  });
+}
+
+int moc_engine_finalize_keys_device(void* e, const int64_t* d_offsets, int64_t n, const uint64_t* d_keys, void* d_out,
+                                    int fmt, void* stream) {
+  return guard([&] {
+    static_cast<moc::HipEngine*>(e)->finalize_keys_device(d_offsets, n,
+                                                          reinterpret_cast<const unsigned long long*>(d_keys), d_out,
+                                                          static_cast<moc::ResultFormat>(fmt),
+                                                          static_cast<hipStream_t>(stream));
   });
 }
 

@@ -65,6 +65,14 @@ void bcast_bytes(void* buf, int64_t bytes, int root, MPI_Comm comm) {
   }
 }
 
+void allreduce_max_u64(uint64_t* buf, int64_t n, MPI_Comm comm) {
+  const int64_t step = kMpiChunk / 8;
+  for (int64_t off = 0; off < n; off += step) {
+    const int c = static_cast<int>(std::min(step, n - off));
+    MOC_MPI_CHECK(MPI_Allreduce(MPI_IN_PLACE, buf + off, c, MPI_UINT64_T, MPI_MAX, comm));
+  }
+}
+
 namespace {
 // Point-to-point transfer of a byte range in < 2^31 pieces (posted as non-blocking requests).
 void post_send(std::vector<MPI_Request>& reqs, const char* p, int64_t bytes, int peer, int tag, MPI_Comm comm) {
@@ -191,6 +199,11 @@ void RcclComm::check_async() const {
   ncclResult_t st = ncclSuccess;
   MOC_NCCL_CHECK(ncclCommGetAsyncError(comm_, &st));
   if (st != ncclSuccess) throw Error(std::string("RCCL async error: ") + ncclGetErrorString(st));
+}
+
+void RcclComm::allreduce_max_u64(void* dbuf, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  MOC_NCCL_CHECK(ncclAllReduce(dbuf, dbuf, static_cast<size_t>(n), ncclUint64, ncclMax, comm_, s));
 }
 
 void RcclComm::bcast(void* dbuf, int64_t bytes, int root, hipStream_t s) {

@@ -98,6 +98,41 @@ void solve_batch_cpu(const ScoreTable& t, const uint8_t* s1, int64_t L1, const R
   }
 }
 
+void solve_keys_cpu(const ScoreTable& t, const uint8_t* s1, int64_t L1, const RecordBatch& batch, int part,
+                    int parts, uint64_t* keys, Semantics sem, int num_threads) {
+  if (parts < 1 || part < 0 || part >= parts) throw Error("solve_keys_cpu: bad part");
+  const int64_t n = batch.size();
+  const int nt = num_threads > 0 ? num_threads : omp_get_max_threads();
+  auto range = [&](int64_t i, int64_t& b, int64_t& e) {
+    const int64_t c = candidate_offsets(L1, batch.length(i), sem);
+    b = c * part / parts;
+    e = c * (part + 1) / parts;
+  };
+  if (n >= 4 * nt || nt == 1) {
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nt)
+    for (int64_t i = 0; i < n; ++i) {
+      int64_t b, e;
+      range(i, b, e);
+      const int64_t L2 = batch.length(i);
+      keys[i] = encode_key(solve_offsets(t, s1, L1, batch.record(i), L2, b, e, sem), L2);
+    }
+    return;
+  }
+  for (int64_t i = 0; i < n; ++i) {  // few records: threads split this part's range further
+    int64_t b, e;
+    range(i, b, e);
+    const int64_t L2 = batch.length(i);
+    std::vector<uint64_t> k(nt, 0);
+#pragma omp parallel num_threads(nt)
+    {
+      const int tid = omp_get_thread_num();
+      const int64_t tb = b + (e - b) * tid / nt, te = b + (e - b) * (tid + 1) / nt;
+      k[tid] = encode_key(solve_offsets(t, s1, L1, batch.record(i), L2, tb, te, sem), L2);
+    }
+    keys[i] = *std::max_element(k.begin(), k.end());
+  }
+}
+
 Result brute_force_record(const ScoreTable& t, const uint8_t* s1, int64_t L1, const uint8_t* s2, int64_t L2,
                           Semantics sem) {
   if (L2 > L1) return no_candidate();

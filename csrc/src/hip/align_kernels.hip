@@ -42,7 +42,7 @@ __global__ __launch_bounds__(256) void tile_search_kernel(ProblemView pv, BatchV
   const Tile tile = tiles[wave];
   const int li = __builtin_amdgcn_readfirstlane(tile.li);
   const int o0 = __builtin_amdgcn_readfirstlane(tile.o0);
-  const int r = __builtin_amdgcn_readfirstlane(long_recs[li]);
+  const int r = long_recs ? __builtin_amdgcn_readfirstlane(long_recs[li]) : li;  // null: identity (CP plans)
   const int64_t base = bv.offsets[r] - bv.offsets[0];
   const int L2 = __builtin_amdgcn_readfirstlane(static_cast<int>(bv.offsets[r + 1] - bv.offsets[r]));
   const uint8_t* rec = bv.codes + base;
@@ -77,7 +77,7 @@ __global__ void finalize_long_kernel(BatchView bv, const int32_t* __restrict__ l
                                      const unsigned long long* __restrict__ keys, int64_t n_long, void* out, int fmt) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= n_long) return;
-  const int r = long_recs[i];
+  const int r = long_recs ? long_recs[i] : static_cast<int>(i);
   const int L2 = static_cast<int>(bv.offsets[r + 1] - bv.offsets[r]);
   store_result(out, r, fmt, decode_key(keys[i], L2 > 0 ? L2 : 1));
 }
@@ -102,12 +102,10 @@ constexpr int kBlock = 256;
 constexpr int kMaxSeq1Lds = 56 * 1024;  // Seq1 staged in LDS up to this size (keeps dyn. LDS < 64 KiB)
 
 template <bool Wide>
-void launch_tiles_t(const ProblemView& pv, const BatchView& bv, const Plan& plan, void* out, int fmt,
-                    hipStream_t stream) {
+void launch_search_t(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream) {
   const size_t lds_lut = kLutInts * sizeof(int);
   const size_t lds_s1 = static_cast<size_t>(pv.L1 + kSeq1Pad + 3) & ~size_t{3};
   const bool s1_in_lds = pv.L1 + kSeq1Pad <= kMaxSeq1Lds;
-  (void)hipMemsetAsync(plan.keys, 0, sizeof(unsigned long long) * plan.n_long, stream);
   const int64_t blocks = (plan.n_tiles * 64 + kBlock - 1) / kBlock;
   if (s1_in_lds)
     hipLaunchKernelGGL((tile_search_kernel<Wide, true>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock),
@@ -115,19 +113,34 @@ void launch_tiles_t(const ProblemView& pv, const BatchView& bv, const Plan& plan
   else
     hipLaunchKernelGGL((tile_search_kernel<Wide, false>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock), lds_lut,
                        stream, pv, bv, plan.tiles, plan.n_tiles, plan.long_recs, plan.keys);
+}
+
+void launch_finalize(const BatchView& bv, const Plan& plan, void* out, int fmt, hipStream_t stream) {
+  if (plan.n_long <= 0) return;
   const int64_t fb = (plan.n_long + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(finalize_long_kernel, dim3(static_cast<unsigned>(fb)), dim3(kBlock), 0, stream, bv,
                      plan.long_recs, plan.keys, plan.n_long, out, fmt);
 }
 }  // namespace
 
+void launch_tile_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream) {
+  if (plan.n_long > 0) (void)hipMemsetAsync(plan.keys, 0, sizeof(unsigned long long) * plan.n_long, stream);
+  if (plan.n_tiles <= 0) return;
+  if (pv.key_shift > 0)
+    launch_search_t<false>(pv, bv, plan, stream);
+  else
+    launch_search_t<true>(pv, bv, plan, stream);
+}
+
+void launch_finalize_keys(const BatchView& bv, const Plan& plan, void* out, int fmt, hipStream_t stream) {
+  launch_finalize(bv, plan, out, fmt, stream);
+}
+
 void launch_tiles(const ProblemView& pv, const BatchView& bv, const Plan& plan, void* out, int fmt,
                   hipStream_t stream) {
   if (plan.n_tiles <= 0) return;
-  if (pv.key_shift > 0)
-    launch_tiles_t<false>(pv, bv, plan, out, fmt, stream);
-  else
-    launch_tiles_t<true>(pv, bv, plan, out, fmt, stream);
+  launch_tile_keys(pv, bv, plan, stream);
+  launch_finalize(bv, plan, out, fmt, stream);
 }
 
 }  // namespace dev

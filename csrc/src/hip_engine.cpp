@@ -11,6 +11,7 @@
 #include "moc/runtime/hip_check.hpp"
 #include "moc/runtime/log.hpp"
 #include "moc/runtime/timer.hpp"
+#include "moc/runtime/trace.hpp"
 
 namespace moc {
 
@@ -347,6 +348,7 @@ void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uin
                          ResultFormat fmt, const BatchHints& hints, bool packed5) {
   if (!have_problem_) throw Error("HipEngine::solve before set_problem");
   MOC_HIP_CHECK(hipSetDevice(device_));
+  TraceRange tr("moc.solve");
   Stopwatch wall;
   wall.start();
   stats_ = EngineStats{};
@@ -430,6 +432,7 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
     const int64_t cn = re - rb;
     Slot& s = *slots_[chunk % 2];
     retire(s);
+    TraceRange tr_chunk("moc.chunk");
     plan_chunk(offsets + rb, cn, cp);
     stats_.cells += cp.cells;
     // records that the short kernel cannot hold (LDS budget) go to the tile kernel too
@@ -533,6 +536,7 @@ void HipEngine::solve_device(const uint8_t* d_codes, const int64_t* d_offsets, c
   MOC_HIP_CHECK(hipSetDevice(device_));
   if (n <= 0) return;
   if (!stream) stream = s_compute_;
+  TraceRange tr("moc.solve_device");
   ChunkPlan cp;
   plan_chunk(h_offsets, n, cp);
   dev::ShortArgs a;
@@ -587,6 +591,104 @@ void HipEngine::solve_device(const uint8_t* d_codes, const int64_t* d_offsets, c
   stats_.cells = cp.cells;
   stats_.records = n;
   stats_.kernels = (short_ok ? (swipe ? 1 : 2) : 0) | (cp.tiles.empty() ? 0 : 4);
+}
+
+}  // namespace moc
+
+namespace moc {
+
+void HipEngine::search_keys_device(const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets,
+                                   int64_t n, int part, int parts, unsigned long long* d_keys, hipStream_t stream) {
+  if (!have_problem_) throw Error("HipEngine::search_keys before set_problem");
+  if (parts < 1 || part < 0 || part >= parts) throw Error("search_keys: bad part");
+  MOC_HIP_CHECK(hipSetDevice(device_));
+  if (n <= 0) return;
+  if (!stream) stream = s_compute_;
+  TraceRange tr("moc.search_keys");
+  // global tile list over all records (record-major); this part takes a contiguous share of it
+  int64_t total = 0, max_l2 = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t L2 = h_offsets[i + 1] - h_offsets[i];
+    max_l2 = std::max(max_l2, L2);
+    total += (dev::lanes_needed(L1_, L2) + dev::kTileOffsets - 1) / dev::kTileOffsets;
+  }
+  if (max_l2 * std::max<int64_t>(L1_, 1) >= (int64_t{1} << 32))
+    throw Error("L1 * max L2 exceeds the 32-bit candidate index of the device engine");
+  const int64_t g0 = total * part / parts, g1 = total * (part + 1) / parts;
+  std::vector<dev::Tile> tiles;
+  tiles.reserve(static_cast<size_t>(g1 - g0));
+  int64_t g = 0;
+  for (int64_t i = 0; i < n && g < g1; ++i) {
+    const int64_t need = dev::lanes_needed(L1_, h_offsets[i + 1] - h_offsets[i]);
+    const int64_t nt = (need + dev::kTileOffsets - 1) / dev::kTileOffsets;
+    for (int64_t t = std::max<int64_t>(g0 - g, 0); t < nt && g + t < g1; ++t)
+      tiles.push_back(dev::Tile{static_cast<int32_t>(i), static_cast<int32_t>(t * dev::kTileOffsets)});
+    g += nt;
+  }
+  MOC_HIP_CHECK(hipEventSynchronize(ev_plan_));  // previous call's plan buffers are free again
+  const size_t bytes = std::max<size_t>(tiles.size() * sizeof(dev::Tile), 8);
+  ensure(d_plan_, d_plan_cap_, bytes);
+  ensure_host(h_plan_, h_plan_cap_, bytes);
+  if (!tiles.empty()) {
+    std::memcpy(h_plan_, tiles.data(), tiles.size() * sizeof(dev::Tile));
+    MOC_HIP_CHECK(hipMemcpyAsync(d_plan_, h_plan_, tiles.size() * sizeof(dev::Tile), hipMemcpyHostToDevice, stream));
+  }
+  dev::Plan plan;
+  plan.n_tiles = static_cast<int64_t>(tiles.size());
+  plan.tiles = static_cast<const dev::Tile*>(d_plan_);
+  plan.long_recs = nullptr;
+  plan.n_long = n;
+  plan.keys = d_keys;
+  dev::BatchView bv{d_codes + h_offsets[0], d_offsets, n};
+  dev::launch_tile_keys(problem_view(max_l2), bv, plan, stream);
+  MOC_HIP_CHECK(hipGetLastError());
+  MOC_HIP_CHECK(hipEventRecord(ev_plan_, stream));
+  stats_ = EngineStats{};
+  stats_.records = n;
+  stats_.kernels = plan.n_tiles ? 4 : 0;
+}
+
+void HipEngine::finalize_keys_device(const int64_t* d_offsets, int64_t n, const unsigned long long* d_keys,
+                                     void* d_out, ResultFormat fmt, hipStream_t stream) {
+  MOC_HIP_CHECK(hipSetDevice(device_));
+  if (n <= 0) return;
+  if (!stream) stream = s_compute_;
+  dev::Plan plan;
+  plan.long_recs = nullptr;
+  plan.n_long = n;
+  plan.keys = const_cast<unsigned long long*>(d_keys);
+  dev::BatchView bv{nullptr, d_offsets, n};
+  dev::launch_finalize_keys(bv, plan, d_out, static_cast<int>(fmt), stream);
+  MOC_HIP_CHECK(hipGetLastError());
+}
+
+void HipEngine::search_keys(const uint8_t* codes, const int64_t* offsets, int64_t n, int part, int parts,
+                            uint64_t* keys) {
+  MOC_HIP_CHECK(hipSetDevice(device_));
+  if (n <= 0) return;
+  Stopwatch wall;
+  wall.start();
+  Slot& s = *slots_[0];
+  const size_t cbytes = static_cast<size_t>(offsets[n] - offsets[0]);
+  ensure(s.d_codes, s.d_codes_cap, std::max<size_t>(cbytes, 16) + 32);
+  ensure(s.d_offsets, s.d_offsets_cap, sizeof(int64_t) * static_cast<size_t>(n + 1));
+  ensure(s.d_out, s.d_out_cap, sizeof(uint64_t) * static_cast<size_t>(n));
+  if (cbytes)
+    MOC_HIP_CHECK(hipMemcpyAsync(s.d_codes, codes + offsets[0], cbytes, hipMemcpyHostToDevice, s_compute_));
+  MOC_HIP_CHECK(hipMemcpyAsync(s.d_offsets, offsets, sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, s_compute_));
+  MOC_HIP_CHECK(hipEventRecord(ev_a_, s_compute_));
+  search_keys_device(static_cast<const uint8_t*>(s.d_codes) - offsets[0], static_cast<const int64_t*>(s.d_offsets),
+                     offsets, n, part, parts, static_cast<unsigned long long*>(s.d_out), s_compute_);
+  MOC_HIP_CHECK(hipEventRecord(ev_b_, s_compute_));
+  MOC_HIP_CHECK(hipMemcpyAsync(keys, s.d_out, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, s_compute_));
+  MOC_HIP_CHECK(hipStreamSynchronize(s_compute_));
+  float ms = 0;
+  MOC_HIP_CHECK(hipEventElapsedTime(&ms, ev_a_, ev_b_));
+  stats_.kernel_ms = ms;
+  stats_.h2d_bytes = static_cast<int64_t>(cbytes + sizeof(int64_t) * (n + 1));
+  stats_.d2h_bytes = static_cast<int64_t>(sizeof(uint64_t) * n);
+  wall.stop();
+  stats_.total_ms = wall.total_ms();
 }
 
 }  // namespace moc

@@ -178,6 +178,110 @@ Problem parse_problem(const char* data, size_t len, const ParseOptions& opt) {
   return prob;
 }
 
+// ---- streaming reader ---------------------------------------------------------------------------
+
+StreamReader::StreamReader(FILE* f, const ParseOptions& opt, size_t block_bytes) : f_(f), opt_(opt) {
+  buf_.resize(std::max<size_t>(block_bytes, 4096));
+  const char *b, *e;
+  static const char* wname[4] = {"W1", "W2", "W3", "W4"};
+  for (int i = 0; i < 4; ++i) {
+    if (!token(b, e)) throw Error(std::string("unexpected end of input while reading ") + wname[i]);
+    int64_t v = parse_int(b, e, wname[i]);
+    if (v < 0 || v > INT32_MAX) throw Error(std::string(wname[i]) + " out of range");
+    weights_.w[i] = static_cast<int32_t>(v);
+  }
+  if (!token(b, e)) throw Error("unexpected end of input while reading Seq1");
+  seq1_ = encode_sequence(b, e - b);
+  if (!token(b, e)) throw Error("unexpected end of input while reading the number of sequences");
+  count_ = parse_int(b, e, "number_of_sequences");
+  if (count_ < 0) throw Error("number_of_sequences must be >= 0");
+  const int64_t l1_cap = opt_.strict_limits ? kSpecMaxSeq1 : opt_.max_l1;
+  l2_cap_ = opt_.strict_limits ? kSpecMaxSeq2 : opt_.max_l2;
+  if (l1_cap > 0 && static_cast<int64_t>(seq1_.size()) > l1_cap)
+    throw Error("Seq1 has " + std::to_string(seq1_.size()) + " letters, limit is " + std::to_string(l1_cap));
+}
+
+bool StreamReader::token(const char*& b, const char*& e) {
+  // skip whitespace
+  while (true) {
+    while (pos_ < len_ && is_space(static_cast<unsigned char>(buf_[pos_]))) ++pos_;
+    if (pos_ < len_) break;
+    if (eof_) return false;
+    pos_ = len_ = 0;
+    len_ = std::fread(buf_.data(), 1, buf_.size(), f_);
+    if (len_ < buf_.size()) {
+      if (std::ferror(f_)) throw Error("error while reading input stream");
+      eof_ = true;
+    }
+  }
+  // token [pos_, q); extend the buffer while it runs into the end of the loaded data
+  size_t q = pos_;
+  while (true) {
+    while (q < len_ && !is_space(static_cast<unsigned char>(buf_[q]))) ++q;
+    if (q < len_ || eof_) break;
+    // move the partial token to the front (grow if it fills the buffer) and read more
+    const size_t keep = len_ - pos_;
+    if (pos_ > 0) std::memmove(buf_.data(), buf_.data() + pos_, keep);
+    if (keep == buf_.size()) buf_.resize(buf_.size() * 2);
+    q = keep;
+    pos_ = 0;
+    const size_t got = std::fread(buf_.data() + keep, 1, buf_.size() - keep, f_);
+    len_ = keep + got;
+    if (len_ < buf_.size()) {
+      if (std::ferror(f_)) throw Error("error while reading input stream");
+      eof_ = true;
+    }
+  }
+  b = buf_.data() + pos_;
+  e = buf_.data() + q;
+  pos_ = q;
+  return true;
+}
+
+int64_t StreamReader::skip(int64_t records) {
+  const char *b, *e;
+  int64_t done = 0;
+  while (done < records && next_ < count_) {
+    if (!token(b, e))
+      throw Error("expected " + std::to_string(count_) + " Seq2 records, found only " + std::to_string(next_));
+    ++next_;
+    ++done;
+  }
+  return done;
+}
+
+int64_t StreamReader::next_batch(int64_t max_records, RecordBatch& out, int64_t max_chars) {
+  out.codes.clear();
+  out.offsets.assign(1, 0);
+  const char *b, *e;
+  int64_t got = 0, max_len = 0;
+  while (got < max_records && next_ < count_) {
+    if (got > 0 && static_cast<int64_t>(out.codes.size()) >= max_chars) break;
+    if (!token(b, e))
+      throw Error("expected " + std::to_string(count_) + " Seq2 records, found only " + std::to_string(next_));
+    const int64_t L = e - b;
+    if (l2_cap_ > 0 && L > l2_cap_)
+      throw Error("Seq2 record #" + std::to_string(next_) + " has " + std::to_string(L) + " letters, limit is " +
+                  std::to_string(l2_cap_));
+    const size_t at = out.codes.size();
+    out.codes.resize(at + static_cast<size_t>(L));
+    uint8_t* dst = out.codes.data() + at;
+    int bad = 0;
+    for (int64_t j = 0; j < L; ++j) {
+      const int c = letter_code(static_cast<unsigned char>(b[j]));
+      bad |= (c == 0);
+      dst[j] = static_cast<uint8_t>(c);
+    }
+    if (bad) throw Error("Seq2 record #" + std::to_string(next_) + " contains a non-letter character");
+    out.offsets.push_back(static_cast<int64_t>(out.codes.size()));
+    max_len = std::max(max_len, L);
+    ++next_;
+    ++got;
+  }
+  if (got) validate_score_range(weights_, std::max<int64_t>(max_len, 1));
+  return got;
+}
+
 // ---- writer -------------------------------------------------------------------------------------
 
 namespace {

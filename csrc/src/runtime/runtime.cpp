@@ -1,4 +1,6 @@
-// Host runtime utilities: flags, logging, phase timer JSON.
+// Host runtime utilities: flags, logging, phase timer JSON, roctx ranges.
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -8,6 +10,7 @@
 #include "moc/runtime/flags.hpp"
 #include "moc/runtime/log.hpp"
 #include "moc/runtime/timer.hpp"
+#include "moc/runtime/trace.hpp"
 
 namespace moc {
 
@@ -126,7 +129,45 @@ void logf(LogLevel lvl, const char* fmt, ...) {
     std::fprintf(stderr, "[moc %s] %s\n", names[static_cast<int>(lvl)], msg);
 }
 
+// ---------------------------------------------------------------- trace
+bool trace_enabled() {
+  static const bool on = [] {
+    const char* v = std::getenv("MOC_TRACE");
+    return !(v && (std::strcmp(v, "0") == 0 || std::strcmp(v, "off") == 0));
+  }();
+  return on;
+}
+void trace_push(const char* name) {
+  if (trace_enabled()) roctxRangePushA(name);
+}
+void trace_pop() {
+  if (trace_enabled()) roctxRangePop();
+}
+void trace_mark(const char* name) {
+  if (trace_enabled()) roctxMarkA(name);
+}
+void trace_name_thread(const char* name) {
+  if (trace_enabled()) roctxNameOsThread(name);
+}
+
 // ---------------------------------------------------------------- timer
+void PhaseTimer::begin(const std::string& name) {
+  if (open_) end();
+  cur_ = name;
+  sw_.reset();
+  sw_.start();
+  trace_push(cur_.c_str());
+  open_ = true;
+}
+
+void PhaseTimer::end() {
+  if (!open_) return;
+  sw_.stop();
+  trace_pop();
+  open_ = false;
+  add(cur_, sw_.total_ms());
+}
+
 std::string PhaseTimer::json(const std::vector<std::pair<std::string, double>>& extra) const {
   std::ostringstream os;
   os.precision(6);

@@ -7,8 +7,8 @@ window. See README.md and SURVEY.md.
 """
 from .models.problem import Problem
 from .models.scoring import PairClass, Semantics, Weights
-from .ops.align import (HipSearchEngine, align_search, align_search_device, brute_force_native, device_count,
-                        search_cpu, search_hip)
+from .ops.align import (HipSearchEngine, align_search, align_search_device, brute_force_native, decode_keys,
+                        device_count, search_cpu, search_hip, search_keys_cpu)
 from .utils.io import format_results, write_results
 from .utils.synthetic import make_synthetic
 
@@ -16,5 +16,5 @@ __version__ = "0.1.0"
 __all__ = [
     "Problem", "PairClass", "Semantics", "Weights", "HipSearchEngine", "align_search", "align_search_device",
     "brute_force_native", "device_count", "search_cpu", "search_hip", "format_results", "write_results",
-    "make_synthetic",
+    "make_synthetic", "search_keys_cpu", "decode_keys",
 ]

@@ -47,6 +47,9 @@ def _decl(lib):
         "moc_pack5": (c_int, [c_void_p, c_int64, c_void_p]),
         "moc_unpack5": (c_int, [c_void_p, c_int64, c_int64, c_void_p]),
         "moc_cpu_solve": (c_int, [P(c_int32), c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p]),
+        "moc_cpu_solve_keys": (c_int, [P(c_int32), c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_int, c_int,
+                                       c_int, c_void_p]),
+        "moc_decode_keys": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
         "moc_brute_force": (c_int, [P(c_int32), c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
         "moc_partition": (c_int, [c_void_p, c_int64, c_int64, c_int, c_double, c_double, c_double, c_void_p]),
         "moc_device_count": (c_int, []),
@@ -68,6 +71,10 @@ def _decl(lib):
         "moc_expand_results": (c_int, [c_void_p, c_int, c_int64, c_void_p]),
         "moc_engine_solve_device": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
         "moc_engine_stats": (c_int, [c_void_p, P(c_double)]),
+        "moc_engine_search_keys": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p]),
+        "moc_engine_search_keys_device": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int,
+                                                  c_void_p, c_void_p]),
+        "moc_engine_finalize_keys_device": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_void_p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -48,6 +48,37 @@ def search_cpu(problem: Problem, semantics=Semantics.REFERENCE, threads: int = 0
     return out
 
 
+def search_keys_cpu(problem: Problem, part: int, parts: int, semantics=Semantics.REFERENCE,
+                    threads: int = 0) -> np.ndarray:
+    """Context-parallel partial search: part ``part`` of ``parts`` of every record's offset
+    range -> packed uint64 keys (0 = no candidate in this part). ``np.maximum`` over all parts, then
+    :func:`decode_keys`, equals :func:`search_cpu`."""
+    keys = np.zeros(problem.n, np.uint64)
+    _lib.check(_lib.lib().moc_cpu_solve_keys(
+        _lib.weights_arg(problem.weights.as_list()), _lib.ptr(problem.seq1), problem.L1,
+        _lib.ptr(problem.codes), _lib.ptr(problem.offsets), problem.n, int(Semantics.parse(semantics)),
+        int(part), int(parts), int(threads), _lib.ptr(keys)))
+    return keys
+
+
+def decode_keys(keys: np.ndarray, offsets: np.ndarray) -> np.ndarray:
+    """Packed keys ((score^2^31)<<32 | ~(n*L2+k)) -> structured (score, n, k) results."""
+    keys = np.ascontiguousarray(keys, dtype=np.uint64)
+    offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+    out = empty_results(keys.shape[0])
+    _lib.check(_lib.lib().moc_decode_keys(_lib.ptr(keys), _lib.ptr(offsets), keys.shape[0], _lib.ptr(out)))
+    return out
+
+
+def keys_to_ordered_int64(keys: np.ndarray) -> np.ndarray:
+    """uint64 keys -> int64 with the same order (flip the top bit), for signed MAX all-reduces."""
+    return (np.ascontiguousarray(keys, dtype=np.uint64) ^ np.uint64(1 << 63)).view(np.int64)
+
+
+def ordered_int64_to_keys(v: np.ndarray) -> np.ndarray:
+    return np.ascontiguousarray(v, dtype=np.int64).view(np.uint64) ^ np.uint64(1 << 63)
+
+
 def brute_force_native(problem: Problem, semantics=Semantics.REFERENCE) -> np.ndarray:
     """Literal O(L1*L2^2) replay of the reference loops, in C++ (test oracle)."""
     out = empty_results(problem.n)
@@ -165,6 +196,45 @@ class HipSearchEngine:
         _lib.check(_lib.lib().moc_engine_solve_device(
             self._h, ctypes.c_void_p(codes_t.data_ptr()), ctypes.c_void_p(offsets_t.data_ptr()), _lib.ptr(h_offsets),
             n, ctypes.c_void_p(out_t.data_ptr()), ctypes.c_void_p(stream.cuda_stream)))
+        return out_t
+
+    def search_keys(self, codes: np.ndarray, offsets: np.ndarray, part: int, parts: int) -> np.ndarray:
+        """Context-parallel partial search on the GPU: this engine's share (part of parts) of the batch's
+        63-offset tiles -> packed uint64 keys per record (see :func:`search_keys_cpu`)."""
+        codes = np.ascontiguousarray(codes, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        n = offsets.shape[0] - 1
+        keys = np.zeros(n, np.uint64)
+        _lib.check(_lib.lib().moc_engine_search_keys(self._h, _lib.ptr(codes), _lib.ptr(offsets), n, int(part),
+                                                     int(parts), _lib.ptr(keys)))
+        return keys
+
+    def search_keys_device(self, codes_t, offsets_t, h_offsets: np.ndarray, part: int, parts: int, keys_t,
+                           stream=None):
+        """Device-resident form: keys_t is an int64 tensor [n] receiving the uint64 key bits."""
+        import torch
+
+        h_offsets = np.ascontiguousarray(h_offsets, dtype=np.int64)
+        n = h_offsets.shape[0] - 1
+        assert keys_t.dtype == torch.int64 and keys_t.numel() == n
+        if stream is None:
+            stream = torch.cuda.current_stream(codes_t.device)
+        _lib.check(_lib.lib().moc_engine_search_keys_device(
+            self._h, ctypes.c_void_p(codes_t.data_ptr()), ctypes.c_void_p(offsets_t.data_ptr()), _lib.ptr(h_offsets),
+            n, int(part), int(parts), ctypes.c_void_p(keys_t.data_ptr()), ctypes.c_void_p(stream.cuda_stream)))
+        return keys_t
+
+    def finalize_keys_device(self, offsets_t, keys_t, out_t, stream=None):
+        """Device keys -> int32 [n, 3] results (score, n, k)."""
+        import torch
+
+        n = keys_t.numel()
+        assert out_t.dtype == torch.int32 and out_t.shape == (n, 3)
+        if stream is None:
+            stream = torch.cuda.current_stream(keys_t.device)
+        _lib.check(_lib.lib().moc_engine_finalize_keys_device(
+            self._h, ctypes.c_void_p(offsets_t.data_ptr()), n, ctypes.c_void_p(keys_t.data_ptr()),
+            ctypes.c_void_p(out_t.data_ptr()), 0, ctypes.c_void_p(stream.cuda_stream)))
         return out_t
 
     def stats(self) -> dict:

@@ -76,3 +76,75 @@ def test_timing_json():
     line = [l for l in r.stderr.decode().splitlines() if l.startswith("{")][-1]
     d = json.loads(line)
     assert d["records"] == 30 and d["ranks"] == 2 and "compute_ms" in d["timing"]
+
+
+# ---- decomposition / streaming / resume
+
+@pytest.mark.parametrize("i", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("transport", ["shm", "mpi"])
+@pytest.mark.parametrize("np_", [1, 3])
+def test_offsets_partition(i, transport, np_):
+    # context parallel: every rank searches a share of every record's offsets, MAX-all-reduce of keys
+    r = run_final(["--backend=cpu", "--partition=offsets", f"--transport={transport}"], stdin_path=input_path(i),
+                  np_=np_)
+    assert r.returncode == 0, r.stderr.decode()
+    assert r.stdout.decode() == expected(i)
+
+
+@pytest.mark.parametrize("batch", ["--batch-records=1", "--batch-records=4", "--batch-chars=30"])
+@pytest.mark.parametrize("partition", ["cost", "offsets"])
+def test_streaming_batches(batch, partition):
+    for i in (1, 3, 6):
+        r = run_final(["--backend=cpu", batch, f"--partition={partition}"], stdin_path=input_path(i), np_=2)
+        assert r.returncode == 0, r.stderr.decode()
+        assert r.stdout.decode() == expected(i)
+
+
+@pytest.mark.parametrize("extra", [[], ["--batch-records=3"]])
+def test_skip_records_resume(extra):
+    exp = expected(1).splitlines(keepends=True)
+    r = run_final(["--backend=cpu", "--skip-records=4"] + extra, stdin_path=input_path(1), np_=2)
+    assert r.returncode == 0 and r.stdout.decode() == "".join(exp[4:])
+    r = run_final(["--backend=cpu", "--skip-records=99"] + extra, stdin_path=input_path(1), np_=2)
+    assert r.returncode == 0 and r.stdout == b""
+
+
+def test_input_flag_large_file(tmp_path):
+    # MPICH's hydra cannot forward a large stdin here ("reading stdin too slowly"); --input reads the file
+    from mpi_openmp_cuda_amd import format_results, make_synthetic, search_cpu
+
+    prob = make_synthetic("input6", 60000, seed=4)
+    path = tmp_path / "in.txt"
+    path.write_text(prob.to_text())
+    want = format_results(search_cpu(prob))
+    for extra in ([], ["--batch-records=7000"], ["--partition=offsets"]):
+        r = run_final(["--backend=cpu", f"--input={path}"] + extra, stdin_bytes=b"", np_=3)
+        assert r.returncode == 0, r.stderr.decode()
+        assert r.stdout.decode() == want
+
+
+def test_streaming_parse_error_mid_stream():
+    text = b"1 2 3 4\nABCDEFG\n5\nABC\nABD\nAB1\nAC\nAD\n"
+    r = run_final(["--backend=cpu", "--batch-records=2"], stdin_bytes=text, np_=2)
+    assert r.returncode == 1 and b"non-letter" in r.stderr
+    # the batch before the bad record was already printed (a resume restarts at --skip-records=2)
+    assert [l.split(":")[0] for l in r.stdout.decode().splitlines()] == ["#0", "#1"]
+
+
+def test_length_limit_flags():
+    text = b"1 1 1 1\nABCDEFG\n2\nABC\nABCDE\n"
+    r = run_final(["--backend=cpu", "--max-l2=4"], stdin_bytes=text)
+    assert r.returncode == 1 and b"limit is 4" in r.stderr
+    r = run_final(["--backend=cpu", "--max-l1=6"], stdin_bytes=text)
+    assert r.returncode == 1 and b"limit is 6" in r.stderr
+    r = run_final(["--backend=cpu", "--max-l2=5", "--batch-records=1"], stdin_bytes=text)
+    assert r.returncode == 0 and len(r.stdout.splitlines()) == 2
+
+
+def test_timing_json_has_throughput():
+    import json
+
+    r = run_final(["--backend=cpu", "--timing", "--batch-records=3"], stdin_path=input_path(1), np_=2)
+    t = json.loads(r.stderr.decode().strip().splitlines()[-1])
+    assert t["records"] == 10 and t["batches"] == 4 and t["cells"] > 0 and t["cells_per_s"] > 0
+    assert set(t["timing"]) >= {"parse_ms", "bcast_ms", "distribute_ms", "compute_ms", "gather_ms", "print_ms"}

@@ -229,3 +229,71 @@ def test_final_cli_rccl_single_rank():
     r = run_final(["--backend=hip", "--transport=rccl"], stdin_path=input_path(3), np_=1)
     assert r.returncode == 0, r.stderr.decode()
     assert r.stdout.decode() == expected(3)
+
+
+@pytest.mark.parametrize("shape,n", [("input3", 8), ("input4", 60), ("input1", 200), ("input6", 3000)])
+@pytest.mark.parametrize("parts", [1, 2, 5])
+def test_context_parallel_keys(engine, shape, n, parts):
+    # GPU partial searches (shares of the global tile list) combine by MAX into the full search
+    from mpi_openmp_cuda_amd import decode_keys, search_keys_cpu
+
+    prob = make_synthetic(shape, n, seed=n + parts)
+    for sem in (Semantics.REFERENCE, Semantics.SPEC):
+        engine.set_problem(prob.weights, prob.seq1, sem)
+        keys = np.zeros(prob.n, np.uint64)
+        for part in range(parts):
+            keys = np.maximum(keys, engine.search_keys(prob.codes, prob.offsets, part, parts))
+        ref = as_triples(search_cpu(prob, sem))
+        assert np.array_equal(as_triples(decode_keys(keys, prob.offsets)), ref)
+        # each GPU share is a lower bound of the CPU full-range key (same encoding on both sides)
+        full = search_keys_cpu(prob, 0, 1, sem)
+        assert np.array_equal(keys, full)
+
+
+def test_context_parallel_device_finalize(engine):
+    prob = make_synthetic("input3", 6, seed=3)
+    engine.set_problem(prob.weights, prob.seq1)
+    dev = torch.device("cuda:0")
+    codes_t = torch.from_numpy(prob.codes).to(dev)
+    offs_t = torch.from_numpy(prob.offsets).to(dev)
+    keys = torch.zeros(prob.n, dtype=torch.int64, device=dev)
+    parts = []
+    for part in range(3):
+        k = torch.empty_like(keys)
+        engine.search_keys_device(codes_t, offs_t, prob.offsets, part, 3, k)
+        parts.append(k)
+    torch.cuda.synchronize()
+    # uint64 max == signed max after flipping the top bit
+    flip = torch.tensor(-2**63, dtype=torch.int64, device=dev)
+    best = torch.stack([p ^ flip for p in parts]).max(dim=0).values ^ flip
+    out = torch.empty(prob.n, 3, dtype=torch.int32, device=dev)
+    engine.finalize_keys_device(offs_t, best, out)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), as_triples(search_cpu(prob)))
+
+
+@pytest.mark.parametrize("args", [["--partition=offsets", "--transport=shm"], ["--partition=offsets", "--transport=rccl"],
+                                  ["--partition=offsets", "--transport=mpi"], ["--batch-records=3"],
+                                  ["--batch-records=2", "--transport=rccl"], ["--pin-window=0"]])
+def test_final_cli_hip_modes(args):
+    for i in (1, 3, 4, 6):
+        r = run_final(["--backend=hip"] + args, stdin_path=input_path(i), np_=1)
+        assert r.returncode == 0, r.stderr.decode()
+        assert r.stdout.decode() == expected(i), args
+
+
+def test_final_cli_hip_two_ranks_offsets():
+    r = run_final(["--backend=hip", "--transport=shm", "--partition=offsets", "--device=0"], stdin_path=input_path(3),
+                  np_=2)
+    assert r.returncode == 0, r.stderr.decode()
+    assert r.stdout.decode() == expected(3)
+
+
+def test_final_cli_zero_copy_window(tmp_path):
+    # GPU ranks page-lock the shm window and stream their slice zero-copy; output == CPU
+    prob = make_synthetic("input6", 100_000, seed=8)
+    path = tmp_path / "in6.txt"
+    path.write_text(prob.to_text())
+    r = run_final(["--backend=hip", "--transport=shm", f"--input={path}", "--timing"], stdin_bytes=b"", np_=1)
+    assert r.returncode == 0, r.stderr.decode()
+    assert r.stdout.decode() == format_results(search_cpu(prob))
