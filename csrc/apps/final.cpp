@@ -221,9 +221,10 @@ void Job::setup_engine() {
     eo.chunk_bytes = flags_.get_int("chunk-bytes", eo.chunk_bytes);
     eng_.hip = std::make_unique<HipEngine>(eo);
   }
-  int all_gpu = eng_.gpu ? 1 : 0;
-  MPI_Allreduce(MPI_IN_PLACE, &all_gpu, 1, MPI_INT, MPI_MIN, ctx_.world);
-  all_gpu_ = all_gpu != 0;
+  int gpu_minmax[2] = {eng_.gpu ? 1 : 0, eng_.gpu ? 0 : -1};  // {min gpu, -max gpu}
+  MPI_Allreduce(MPI_IN_PLACE, gpu_minmax, 2, MPI_INT, MPI_MIN, ctx_.world);
+  all_gpu_ = gpu_minmax[0] != 0;
+  const bool any_gpu = gpu_minmax[1] != 0;
   transport_ = to_lower(flags_.get("transport", "auto"));
   if (transport_ == "auto") transport_ = ctx_.single_node() ? "shm" : (all_gpu_ ? "rccl" : "mpi");
   if (transport_ == "shm" && !ctx_.single_node()) throw Error("--transport=shm needs all ranks on one node");
@@ -233,6 +234,10 @@ void Job::setup_engine() {
   partition_ = to_lower(flags_.get("partition", "cost"));
   if (partition_ != "cost" && partition_ != "even" && partition_ != "offsets")
     throw Error("--partition must be cost|even|offsets");
+  // GPU ranks split by shares of the tile list, CPU ranks by shares of each record's offsets: the two
+  // decompositions do not tile each other, so the context-parallel mode needs one engine kind
+  if (partition_ == "offsets" && any_gpu && !all_gpu_)
+    throw Error("--partition=offsets needs the same backend on every rank (use --backend=hip or --backend=cpu)");
   pin_window_ = flags_.get_bool("pin-window", true);
   if (transport_ == "rccl") nccl_ = std::make_unique<RcclComm>(ctx_, device_);
   MOC_LOG_INFO("rank %d/%d host %s local %d/%d engine=%s device=%d transport=%s partition=%s", ctx_.rank, ctx_.size,

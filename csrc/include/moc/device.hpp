@@ -67,19 +67,26 @@ struct BatchView {
   int64_t n;
 };
 
-// One tile-kernel work item: index into Plan::long_recs and the tile's first offset.
-struct Tile {
+// Tile-kernel work decomposition. The long records' offset ranges are cut into wave tiles of
+// kTileOffsets * U offsets (U sub-tiles of 63 owned offsets + 1 helper lane, processed together so the
+// sub-tiles share each step's Seq2 letter and overlap their dependency chains). The tiles of all long
+// records form one record-major list; every wave runs a contiguous, cost-balanced slice of it, from
+// starts[w] to starts[w+1] (exclusive), given as (long-record index, tile index within the record).
+struct WaveStart {
   int32_t li;
-  int32_t o0;
+  int32_t t;
 };
+
+inline int64_t tiles_of(int64_t need, int u) { return (need + kTileOffsets * u - 1) / (kTileOffsets * u); }
 
 // Host-built plan for the tile kernel of one batch.
 struct Plan {
-  int64_t n_tiles = 0;                 // tile-kernel work items
-  const Tile* tiles = nullptr;         // device: (long-record index, first offset) per tile
-  const int32_t* long_recs = nullptr;  // device: records handled by the tile kernel
+  int64_t n_waves = 0;                 // tile-kernel waves
+  const WaveStart* starts = nullptr;   // device, n_waves + 1 entries
+  const int32_t* long_recs = nullptr;  // device: records handled by the tile kernel (null = identity)
   int64_t n_long = 0;
   unsigned long long* keys = nullptr;  // device scratch, n_long entries (tile-kernel partial maxima)
+  int32_t u = 2;                       // sub-tiles per wave tile (1, 2 or 4)
 };
 
 // Arguments of the short-record kernel. All pointers must be device-accessible: device memory, or

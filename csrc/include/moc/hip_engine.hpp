@@ -104,10 +104,12 @@ class HipEngine {
   struct Slot;  // one double-buffer half
   struct ChunkPlan {
     int64_t min_short = 0, max_l2 = 0, n_short = 0, cells = 0;
-    std::vector<dev::Tile> tiles;
     std::vector<int32_t> long_recs;
   };
   void plan_chunk(const int64_t* offsets, int64_t n, ChunkPlan& cp) const;
+  std::vector<dev::WaveStart> plan_waves(const int64_t* offsets, const int32_t* long_recs, int64_t n_long, int part,
+                                         int parts, int& u_out) const;
+  dev::Plan device_plan(void* d_plan, size_t n_starts, bool has_long_recs, int64_t n_long, int u) const;
   dev::ProblemView problem_view(int64_t max_l2) const;
   void ensure(void*& ptr, size_t& cap, size_t bytes);
   void ensure_host(void*& ptr, size_t& cap, size_t bytes);
@@ -119,6 +121,8 @@ class HipEngine {
   EngineOptions opt_;
   int device_ = 0;
   int num_cus_ = 256;
+  int tile_u_ = 0;              // tile-kernel sub-tiles per wave tile (0 = per batch; MOC_TILE_U = 1|2|4)
+  int tile_waves_per_cu_ = 32;  // tile-kernel waves per CU (MOC_TILE_WAVES_PER_CU)
   hipStream_t s_copy_ = nullptr, s_compute_ = nullptr, s_return_ = nullptr;
   // problem
   ScoreTable table_{};

@@ -21,9 +21,9 @@ namespace dev {
 
 using namespace kc;
 
-template <bool Wide, bool Seq1Lds>
-__global__ __launch_bounds__(256) void tile_search_kernel(ProblemView pv, BatchView bv, const Tile* __restrict__ tiles,
-                                                          int64_t n_tiles, const int32_t* __restrict__ long_recs,
+template <bool Wide, bool Seq1Lds, int U>
+__global__ __launch_bounds__(256) void tile_search_kernel(ProblemView pv, BatchView bv, const WaveStart* __restrict__ starts,
+                                                          int64_t n_waves, const int32_t* __restrict__ long_recs,
                                                           unsigned long long* __restrict__ keys) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   int* lut = reinterpret_cast<int*>(smem);
@@ -32,45 +32,91 @@ __global__ __launch_bounds__(256) void tile_search_kernel(ProblemView pv, BatchV
   stage_lut(lut, pv.lut);
   if (Seq1Lds) stage_bytes(s1l, pv.seq1, L1 + kSeq1Pad);
   __syncthreads();
+  const int64_t w = static_cast<int64_t>(blockIdx.x) * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (w >= n_waves) return;  // wave-uniform; no barrier follows
   const uint8_t* s1 = Seq1Lds ? s1l : pv.seq1;
+  const int s1_last = L1 + kSeq1Pad - 1;
 
   using K = HotKey<Wide>;
   const int lane = threadIdx.x & 63;
-  const int64_t wave = __builtin_amdgcn_readfirstlane(
-      static_cast<int>((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6));
-  if (wave >= n_tiles) return;  // wave-uniform exit (no barrier follows)
-  const Tile tile = tiles[wave];
-  const int li = __builtin_amdgcn_readfirstlane(tile.li);
-  const int o0 = __builtin_amdgcn_readfirstlane(tile.o0);
-  const int r = long_recs ? __builtin_amdgcn_readfirstlane(long_recs[li]) : li;  // null: identity (CP plans)
-  const int64_t base = bv.offsets[r] - bv.offsets[0];
-  const int L2 = __builtin_amdgcn_readfirstlane(static_cast<int>(bv.offsets[r + 1] - bv.offsets[r]));
-  const uint8_t* rec = bv.codes + base;
-  const int o = o0 + lane;
   const int shift = pv.key_shift, mask = (1 << pv.key_shift) - 1;
+  constexpr int kSpan = kTileOffsets * U;  // offsets per wave tile
 
-  int x = s1[min(o, L1 + kSeq1Pad - 1)];
-  int P = 0;
-  typename K::T best = K::min();
-  const int feed0 = o0 + 64;  // lane 63's next letter index
-  const int steps = L2 <= L1 ? L2 : 0;
-  for (int i = 0; i < steps; ++i) {
-    const int c = __builtin_amdgcn_readfirstlane(static_cast<int>(rec[i]));
-    P += lut[(c << 5) | x];
-    const int Pn = wave_shl1(P);
-    if (i + 1 < L2) {
-      const typename K::T key = K::make(P - Pn, i + 1, shift, mask);
-      best = key > best ? key : best;
+  const WaveStart ws = starts[w], we = starts[w + 1];
+  int li = __builtin_amdgcn_readfirstlane(ws.li), t = __builtin_amdgcn_readfirstlane(ws.t);
+  const int end_li = __builtin_amdgcn_readfirstlane(we.li), end_t = __builtin_amdgcn_readfirstlane(we.t);
+  while (li < end_li || (li == end_li && t < end_t)) {  // wave-uniform
+    // ---- one record: its letters stay in registers across the run's tiles of it
+    const int r = long_recs ? __builtin_amdgcn_readfirstlane(long_recs[li]) : li;  // null: identity (CP plans)
+    const uint8_t* rec = bv.codes + (bv.offsets[r] - bv.offsets[0]);
+    const int L2 = __builtin_amdgcn_readfirstlane(static_cast<int>(bv.offsets[r + 1] - bv.offsets[r]));
+    const int steps = L2 <= L1 ? L2 : 0;
+    const int need = L2 <= L1 ? L1 - L2 + 1 : 1;
+    const int ntiles = (need + kSpan - 1) / kSpan;
+    const int t_stop = li == end_li ? min(end_t, ntiles) : ntiles;
+    const int cv_first = lane < steps ? static_cast<int>(rec[lane]) : 0;
+    unsigned long long acc = 0;
+    for (; t < t_stop; ++t) {
+      const int o0 = t * kSpan;
+      MOC_DCHECK(o0 >= 0 && o0 <= L1);
+      // sub-tile u: lanes 0..62 own offsets o0 + 63u + lane, lane 63 is its helper diagonal
+      int x[U], P[U];
+      typename K::T best[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        x[u] = s1[min(o0 + kTileOffsets * u + lane, s1_last)];
+        P[u] = 0;
+        best[u] = K::min();
+      }
+      // Seq2 letters and the helper lanes' Seq1 feeds arrive 64 steps at a time as one coalesced load
+      // per wave (lane j holds step j's value; the next chunk's letters are in flight meanwhile); each
+      // step pulls its values out with v_readlane, so only the LDS LUT reads sit on its critical path.
+      auto step = [&](int cv, const int (&fv)[U], int j, int k, bool key) {
+        const int c = __builtin_amdgcn_readlane(cv, j);
+        const int* row = lut + (c << 5);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          P[u] += row[x[u]];
+          if (key) {
+            const int Pn = wave_shl1(P[u]);
+            const typename K::T kk = K::make(P[u] - Pn, k, shift, mask);
+            best[u] = kk > best[u] ? kk : best[u];
+            x[u] = wave_shl1_fill(x[u], __builtin_amdgcn_readlane(fv[u], j));
+          }
+        }
+      };
+      int cv = cv_first;
+      int i0 = 0;
+      for (; i0 + 64 < steps; i0 += 64) {  // full chunks (the record's last letter lies beyond)
+        const int cv_next = i0 + 64 + lane < steps ? static_cast<int>(rec[i0 + 64 + lane]) : 0;
+        int fv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) fv[u] = s1[min(o0 + kTileOffsets * u + 64 + i0 + lane, s1_last)];
+#pragma unroll 8
+        for (int j = 0; j < 64; ++j) step(cv, fv, j, i0 + j + 1, true);
+        cv = cv_next;
+      }
+      if (steps > 0) {  // last chunk: 1..64 steps; no hyphen after the final letter
+        const int m = steps - i0;
+        int fv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) fv[u] = s1[min(o0 + kTileOffsets * u + 64 + i0 + lane, s1_last)];
+        for (int j = 0; j < m - 1; ++j) step(cv, fv, j, i0 + j + 1, true);
+        step(cv, fv, m - 1, 0, false);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int o = o0 + kTileOffsets * u + lane;
+        const int Pn = wave_shl1(P[u]);
+        const bool own = lane < kTileOffsets && L2 <= L1 && o <= L1 - L2;
+        acc = max_u64(acc, lane_candidate<Wide>(own, o, L1, L2, pv.semantics, P[u], Pn, best[u], shift, mask));
+      }
     }
-    const int fidx = min(feed0 + i, L1 + kSeq1Pad - 1);
-    const int feed = __builtin_amdgcn_readfirstlane(static_cast<int>(s1[fidx]));
-    x = wave_shl1_fill(x, feed);
+    const unsigned long long k = wave_max_u64(acc);
+    if (lane == 0 && k != 0ull) atomicMax(keys + li, k);
+    ++li;
+    t = 0;
   }
-  const int Pn = wave_shl1(P);
-  const bool own = lane < kTileOffsets && L2 <= L1 && o <= L1 - L2;
-  unsigned long long key = lane_candidate<Wide>(own, o, L1, L2, pv.semantics, P, Pn, best, shift, mask);
-  key = wave_max_u64(key);
-  if (lane == 0 && key != 0ull) atomicMax(keys + li, key);
 }
 
 __global__ void finalize_long_kernel(BatchView bv, const int32_t* __restrict__ long_recs,
@@ -101,18 +147,27 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kMaxSeq1Lds = 56 * 1024;  // Seq1 staged in LDS up to this size (keeps dyn. LDS < 64 KiB)
 
-template <bool Wide>
+template <bool Wide, int U>
 void launch_search_t(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream) {
   const size_t lds_lut = kLutInts * sizeof(int);
   const size_t lds_s1 = static_cast<size_t>(pv.L1 + kSeq1Pad + 3) & ~size_t{3};
   const bool s1_in_lds = pv.L1 + kSeq1Pad <= kMaxSeq1Lds;
-  const int64_t blocks = (plan.n_tiles * 64 + kBlock - 1) / kBlock;
+  const int64_t blocks = (plan.n_waves * 64 + kBlock - 1) / kBlock;
   if (s1_in_lds)
-    hipLaunchKernelGGL((tile_search_kernel<Wide, true>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock),
-                       lds_lut + lds_s1, stream, pv, bv, plan.tiles, plan.n_tiles, plan.long_recs, plan.keys);
+    hipLaunchKernelGGL((tile_search_kernel<Wide, true, U>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock),
+                       lds_lut + lds_s1, stream, pv, bv, plan.starts, plan.n_waves, plan.long_recs, plan.keys);
   else
-    hipLaunchKernelGGL((tile_search_kernel<Wide, false>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock), lds_lut,
-                       stream, pv, bv, plan.tiles, plan.n_tiles, plan.long_recs, plan.keys);
+    hipLaunchKernelGGL((tile_search_kernel<Wide, false, U>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock),
+                       lds_lut, stream, pv, bv, plan.starts, plan.n_waves, plan.long_recs, plan.keys);
+}
+
+template <bool Wide>
+void launch_search_u(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream) {
+  switch (plan.u) {
+    case 1: launch_search_t<Wide, 1>(pv, bv, plan, stream); break;
+    case 4: launch_search_t<Wide, 4>(pv, bv, plan, stream); break;
+    default: launch_search_t<Wide, 2>(pv, bv, plan, stream); break;
+  }
 }
 
 void launch_finalize(const BatchView& bv, const Plan& plan, void* out, int fmt, hipStream_t stream) {
@@ -125,11 +180,11 @@ void launch_finalize(const BatchView& bv, const Plan& plan, void* out, int fmt, 
 
 void launch_tile_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream) {
   if (plan.n_long > 0) (void)hipMemsetAsync(plan.keys, 0, sizeof(unsigned long long) * plan.n_long, stream);
-  if (plan.n_tiles <= 0) return;
+  if (plan.n_waves <= 0) return;
   if (pv.key_shift > 0)
-    launch_search_t<false>(pv, bv, plan, stream);
+    launch_search_u<false>(pv, bv, plan, stream);
   else
-    launch_search_t<true>(pv, bv, plan, stream);
+    launch_search_u<true>(pv, bv, plan, stream);
 }
 
 void launch_finalize_keys(const BatchView& bv, const Plan& plan, void* out, int fmt, hipStream_t stream) {
@@ -138,7 +193,7 @@ void launch_finalize_keys(const BatchView& bv, const Plan& plan, void* out, int 
 
 void launch_tiles(const ProblemView& pv, const BatchView& bv, const Plan& plan, void* out, int fmt,
                   hipStream_t stream) {
-  if (plan.n_tiles <= 0) return;
+  if (plan.n_long <= 0) return;
   launch_tile_keys(pv, bv, plan, stream);
   launch_finalize(bv, plan, out, fmt, stream);
 }

@@ -6,6 +6,20 @@
 
 #include "moc/device.hpp"
 
+// Device-side bounds checks: compiled in with -DMOC_DEBUG_KERNELS (make debug-kernels),
+// they print the failing condition and let the kernel continue — a report, never a GPU fault.
+#ifdef MOC_DEBUG_KERNELS
+#define MOC_DCHECK(cond)                                                                                     \
+  do {                                                                                                       \
+    if (!(cond)) printf("MOC_DCHECK %s:%d block %d thread %d: %s\n", __FILE__, __LINE__, (int)blockIdx.x,    \
+                        (int)threadIdx.x, #cond);                                                            \
+  } while (0)
+#else
+#define MOC_DCHECK(cond) \
+  do {                   \
+  } while (0)
+#endif
+
 namespace moc {
 namespace dev {
 namespace kc {

@@ -100,6 +100,14 @@ HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
   hipDeviceProp_t prop;
   MOC_HIP_CHECK(hipGetDeviceProperties(&prop, device_));
   num_cus_ = prop.multiProcessorCount;
+  if (const char* u = std::getenv("MOC_TILE_U")) {  // tuning override of the per-batch choice
+    const int v = std::atoi(u);
+    if (v == 1 || v == 2 || v == 4) tile_u_ = v;
+  }
+  if (const char* w = std::getenv("MOC_TILE_WAVES_PER_CU")) {
+    const int v = std::atoi(w);
+    if (v >= 1 && v <= 32) tile_waves_per_cu_ = v;
+  }
   MOC_HIP_CHECK(hipStreamCreateWithFlags(&s_copy_, hipStreamNonBlocking));
   MOC_HIP_CHECK(hipStreamCreateWithFlags(&s_compute_, hipStreamNonBlocking));
   MOC_HIP_CHECK(hipStreamCreateWithFlags(&s_return_, hipStreamNonBlocking));
@@ -226,7 +234,6 @@ ResultFormat HipEngine::auto_format(int64_t max_l2) const {
 // Splits a chunk's records into the short-kernel set (<= 64 lanes) and the long list (tile kernel).
 // OpenMP: per-thread partial lists are concatenated in thread order, so long_recs stays sorted.
 void HipEngine::plan_chunk(const int64_t* offsets, int64_t n, ChunkPlan& cp) const {
-  cp.tiles.clear();
   cp.long_recs.clear();
   const int64_t short_min_len = std::max<int64_t>(L1_ - (dev::kWave - 1), 0);  // lanes_needed <= 64
   const int nt = n > (1 << 16) ? omp_get_max_threads() : 1;
@@ -264,28 +271,88 @@ void HipEngine::plan_chunk(const int64_t* offsets, int64_t n, ChunkPlan& cp) con
     cp.cells += cells[t];
     cp.long_recs.insert(cp.long_recs.end(), part[t].begin(), part[t].end());
   }
-  for (size_t li = 0; li < cp.long_recs.size(); ++li) {
-    const int64_t L2 = offsets[cp.long_recs[li] + 1] - offsets[cp.long_recs[li]];
-    const int64_t need = dev::lanes_needed(L1_, L2);
-    for (int64_t o0 = 0; o0 < need; o0 += dev::kTileOffsets)
-      cp.tiles.push_back(dev::Tile{static_cast<int32_t>(li), static_cast<int32_t>(o0)});
-  }
   if (cp.max_l2 * std::max<int64_t>(L1_, 1) >= (int64_t{1} << 32))
     throw Error("L1 * max L2 exceeds the 32-bit candidate index of the device engine");
 }
 
 namespace {
-// Layout of one chunk's tile plan in a single buffer: tiles | long_recs | keys(8-aligned).
+// Layout of one chunk's tile plan in a single buffer: wave starts | long_recs | keys (8-aligned).
 struct PlanLayout {
-  size_t tiles_off = 0, long_off = 0, keys_off = 0, upload_bytes = 0, total = 0;
-  PlanLayout(size_t n_tiles, size_t n_long) {
-    long_off = n_tiles * sizeof(dev::Tile);
+  size_t starts_off = 0, long_off = 0, keys_off = 0, upload_bytes = 0, total = 0;
+  PlanLayout(size_t n_starts, size_t n_long) {
+    long_off = n_starts * sizeof(dev::WaveStart);
     keys_off = (long_off + n_long * sizeof(int32_t) + 7) & ~size_t{7};
     upload_bytes = long_off + n_long * sizeof(int32_t);
     total = keys_off + n_long * sizeof(unsigned long long);
   }
 };
 
+// Per-tile fixed cost in step units (record/tile setup, the wave reduction), for load balancing.
+constexpr int64_t kTileOverheadSteps = 24;
+}  // namespace
+
+// Device view of an uploaded plan buffer (starts | long_recs | keys). Identity record lists upload no
+// long_recs (PlanLayout built with n_long = 0): their keys follow the starts.
+dev::Plan HipEngine::device_plan(void* d_plan, size_t n_starts, bool has_long_recs, int64_t n_long,
+                                 int u) const {
+  const PlanLayout lay(n_starts, has_long_recs ? static_cast<size_t>(n_long) : 0);
+  char* base = static_cast<char*>(d_plan);
+  dev::Plan plan;
+  plan.u = u;
+  plan.n_waves = static_cast<int64_t>(n_starts) - 1;
+  plan.starts = reinterpret_cast<const dev::WaveStart*>(base + lay.starts_off);
+  plan.long_recs = has_long_recs ? reinterpret_cast<const int32_t*>(base + lay.long_off) : nullptr;
+  plan.n_long = n_long;
+  plan.keys = reinterpret_cast<unsigned long long*>(base + lay.keys_off);
+  return plan;
+}
+
+// Cost-balanced contiguous wave runs over the record-major tile list of the long records (record li =
+// offsets-relative index long_recs[li], or li when long_recs is null), restricted to part `part` of
+// `parts` of the total cost (context-parallel shares). Returns n_waves + 1 starts (empty: no work).
+std::vector<dev::WaveStart> HipEngine::plan_waves(const int64_t* offsets, const int32_t* long_recs, int64_t n_long,
+                                                  int part, int parts, int& u_out) const {
+  std::vector<dev::WaveStart> starts;
+  if (n_long <= 0) return starts;
+  int64_t sum_l2 = 0;
+  for (int64_t li = 0; li < n_long; ++li) {
+    const int64_t r = long_recs ? long_recs[li] : li;
+    sum_l2 += offsets[r + 1] - offsets[r];
+  }
+  // sub-tiles per wave tile: 4 amortises the per-tile setup over short records, 2 keeps more waves busy
+  // on long ones (measured: profiles/tile_variants.log)
+  const int u = tile_u_ > 0 ? tile_u_ : (sum_l2 < 96 * n_long ? 4 : 2);
+  u_out = u;
+  std::vector<int64_t> pre(static_cast<size_t>(n_long) + 1, 0), tcost(static_cast<size_t>(n_long));
+  std::vector<int32_t> ntiles(static_cast<size_t>(n_long));
+  int64_t total_tiles = 0;
+  for (int64_t li = 0; li < n_long; ++li) {
+    const int64_t r = long_recs ? long_recs[li] : li;
+    const int64_t L2 = offsets[r + 1] - offsets[r];
+    const int64_t nt = dev::tiles_of(dev::lanes_needed(L1_, L2), u);
+    ntiles[li] = static_cast<int32_t>(nt);
+    tcost[li] = (L2 <= L1_ ? L2 : 0) + kTileOverheadSteps;
+    pre[li + 1] = pre[li] + nt * tcost[li];
+    total_tiles += nt;
+  }
+  const int64_t C = pre[n_long];
+  const int64_t lo = C * part / parts, hi = C * (part + 1) / parts;
+  // position of cost threshold X in (li, t): first tile whose start cost is >= X
+  auto locate = [&](int64_t X) {
+    if (X >= C) return dev::WaveStart{static_cast<int32_t>(n_long), 0};
+    const int64_t li = std::upper_bound(pre.begin(), pre.end(), X) - pre.begin() - 1;
+    const int64_t t = (X - pre[li] + tcost[li] - 1) / tcost[li];
+    if (t >= ntiles[li]) return dev::WaveStart{static_cast<int32_t>(li + 1), 0};
+    return dev::WaveStart{static_cast<int32_t>(li), static_cast<int32_t>(t)};
+  };
+  const int64_t part_tiles = std::max<int64_t>(1, total_tiles * (hi - lo) / std::max<int64_t>(C, 1));
+  const int64_t n_waves = std::min<int64_t>(part_tiles, static_cast<int64_t>(num_cus_) * tile_waves_per_cu_);
+  starts.resize(static_cast<size_t>(n_waves) + 1);
+  for (int64_t w = 0; w <= n_waves; ++w) starts[w] = locate(lo + (hi - lo) * w / n_waves);
+  return starts;
+}
+
+namespace {
 struct LenStats {
   int64_t mn = INT64_MAX, mx = 0;
 };
@@ -441,18 +508,14 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
     const bool swipe = cp.n_short > 0 && cp.long_recs.empty() &&
                        dev::configure_swipe(L1_, cp.min_short, cp.max_l2, table_.max_abs(), a);
     bool short_ok = swipe || (cp.n_short > 0 && dev::configure_short(L1_, cp.min_short, cp.max_l2, a));
-    if (cp.n_short > 0 && !short_ok) {
-      cp.long_recs.clear();
-      cp.tiles.clear();
-      for (int64_t i = 0; i < cn; ++i) cp.long_recs.push_back(static_cast<int32_t>(i));
-      for (size_t li = 0; li < cp.long_recs.size(); ++li) {
-        const int64_t L2 = offsets[rb + li + 1] - offsets[rb + li];
-        const int64_t need = dev::lanes_needed(L1_, L2);
-        for (int64_t o0 = 0; o0 < need; o0 += dev::kTileOffsets)
-          cp.tiles.push_back(dev::Tile{static_cast<int32_t>(li), static_cast<int32_t>(o0)});
-      }
-    }
-    const PlanLayout lay(cp.tiles.size(), cp.long_recs.size());
+    // everything through the tile kernel (identity record list) when the short kernel cannot hold it
+    const bool all_tiles = cp.n_short > 0 && !short_ok;
+    const int32_t* lrecs = all_tiles ? nullptr : cp.long_recs.data();
+    const int64_t n_long = all_tiles ? cn : static_cast<int64_t>(cp.long_recs.size());
+    int tile_u = 0;
+    const std::vector<dev::WaveStart> starts = plan_waves(offsets + rb, lrecs, n_long, 0, 1, tile_u);
+    const PlanLayout lay(starts.size(), lrecs ? static_cast<size_t>(n_long) : 0);
+    const size_t keys_extra = lrecs ? 0 : sizeof(unsigned long long) * static_cast<size_t>(n_long);
     const size_t cbytes = static_cast<size_t>(offsets[re] - offsets[rb]);
     ensure(s.d_codes, s.d_codes_cap, std::max<size_t>(cbytes, 16) + 32);
     // packed chunk: bytes [pb0, pb1) of the 5-bit stream, char offsets[rb] at bit pbit within it
@@ -461,11 +524,12 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
     if (packed5) ensure(s.d_packed, s.d_packed_cap, static_cast<size_t>(pb1 - pb0) + 16);
     ensure(s.d_offsets, s.d_offsets_cap, sizeof(int64_t) * static_cast<size_t>(cn + 1));
     ensure(s.d_out, s.d_out_cap, static_cast<size_t>(fb) * static_cast<size_t>(cn));
-    if (lay.total) {
-      ensure(s.d_plan, s.d_plan_cap, lay.total);
+    if (!starts.empty()) {
+      ensure(s.d_plan, s.d_plan_cap, lay.total + keys_extra);
       ensure_host(s.h_plan, s.h_plan_cap, std::max<size_t>(lay.upload_bytes, 8));
-      std::memcpy(static_cast<char*>(s.h_plan) + lay.tiles_off, cp.tiles.data(), cp.tiles.size() * sizeof(dev::Tile));
-      std::memcpy(static_cast<char*>(s.h_plan) + lay.long_off, cp.long_recs.data(), cp.long_recs.size() * sizeof(int32_t));
+      std::memcpy(static_cast<char*>(s.h_plan) + lay.starts_off, starts.data(), starts.size() * sizeof(dev::WaveStart));
+      if (lrecs)
+        std::memcpy(static_cast<char*>(s.h_plan) + lay.long_off, lrecs, static_cast<size_t>(n_long) * sizeof(int32_t));
     }
     // ---- copy stream: H2D
     size_t letter_bytes = cbytes;
@@ -477,7 +541,7 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
       MOC_HIP_CHECK(hipMemcpyAsync(s.d_codes, codes + offsets[rb], cbytes, hipMemcpyHostToDevice, s_copy_));
     }
     MOC_HIP_CHECK(hipMemcpyAsync(s.d_offsets, offsets + rb, sizeof(int64_t) * (cn + 1), hipMemcpyHostToDevice, s_copy_));
-    if (lay.upload_bytes)
+    if (!starts.empty())
       MOC_HIP_CHECK(hipMemcpyAsync(s.d_plan, s.h_plan, lay.upload_bytes, hipMemcpyHostToDevice, s_copy_));
     MOC_HIP_CHECK(hipEventRecord(s.ev_h2d, s_copy_));
     stats_.h2d_bytes += static_cast<int64_t>(letter_bytes + sizeof(int64_t) * (cn + 1) + lay.upload_bytes);
@@ -503,13 +567,8 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
         dev::launch_short(pv, a, num_cus_, s_compute_);
       stats_.kernels |= swipe ? 1 : 2;
     }
-    if (!cp.tiles.empty()) {
-      dev::Plan plan;
-      plan.n_tiles = static_cast<int64_t>(cp.tiles.size());
-      plan.n_long = static_cast<int64_t>(cp.long_recs.size());
-      plan.tiles = reinterpret_cast<const dev::Tile*>(static_cast<char*>(s.d_plan) + lay.tiles_off);
-      plan.long_recs = reinterpret_cast<const int32_t*>(static_cast<char*>(s.d_plan) + lay.long_off);
-      plan.keys = reinterpret_cast<unsigned long long*>(static_cast<char*>(s.d_plan) + lay.keys_off);
+    if (!starts.empty()) {
+      dev::Plan plan = device_plan(s.d_plan, starts.size(), lrecs != nullptr, n_long, tile_u);
       dev::BatchView bv{dcodes, doffs, cn};
       dev::launch_tiles(pv, bv, plan, s.d_out, static_cast<int>(fmt), s_compute_);
       stats_.kernels |= 4;
@@ -544,23 +603,20 @@ void HipEngine::solve_device(const uint8_t* d_codes, const int64_t* d_offsets, c
   const bool swipe = cp.n_short > 0 && cp.long_recs.empty() &&
                      dev::configure_swipe(L1_, cp.min_short, cp.max_l2, table_.max_abs(), a);
   bool short_ok = swipe || (cp.n_short > 0 && dev::configure_short(L1_, cp.min_short, cp.max_l2, a));
-  if (cp.n_short > 0 && !short_ok) {  // everything through the tile kernel
-    cp.long_recs.clear();
-    cp.tiles.clear();
-    for (int64_t i = 0; i < n; ++i) cp.long_recs.push_back(static_cast<int32_t>(i));
-    for (size_t li = 0; li < cp.long_recs.size(); ++li) {
-      const int64_t need = dev::lanes_needed(L1_, h_offsets[li + 1] - h_offsets[li]);
-      for (int64_t o0 = 0; o0 < need; o0 += dev::kTileOffsets)
-        cp.tiles.push_back(dev::Tile{static_cast<int32_t>(li), static_cast<int32_t>(o0)});
-    }
-  }
-  const PlanLayout lay(cp.tiles.size(), cp.long_recs.size());
+  const bool all_tiles = cp.n_short > 0 && !short_ok;  // everything through the tile kernel
+  const int32_t* lrecs = all_tiles ? nullptr : cp.long_recs.data();
+  const int64_t n_long = all_tiles ? n : static_cast<int64_t>(cp.long_recs.size());
+  int tile_u = 0;
+  const std::vector<dev::WaveStart> starts = plan_waves(h_offsets, lrecs, n_long, 0, 1, tile_u);
+  const PlanLayout lay(starts.size(), lrecs ? static_cast<size_t>(n_long) : 0);
+  const size_t keys_extra = lrecs ? 0 : sizeof(unsigned long long) * static_cast<size_t>(n_long);
   MOC_HIP_CHECK(hipEventSynchronize(ev_plan_));  // previous call's plan buffers are free again
-  if (lay.total) {
-    ensure(d_plan_, d_plan_cap_, lay.total);
+  if (!starts.empty()) {
+    ensure(d_plan_, d_plan_cap_, lay.total + keys_extra);
     ensure_host(h_plan_, h_plan_cap_, std::max<size_t>(lay.upload_bytes, 8));
-    std::memcpy(static_cast<char*>(h_plan_) + lay.tiles_off, cp.tiles.data(), cp.tiles.size() * sizeof(dev::Tile));
-    std::memcpy(static_cast<char*>(h_plan_) + lay.long_off, cp.long_recs.data(), cp.long_recs.size() * sizeof(int32_t));
+    std::memcpy(static_cast<char*>(h_plan_) + lay.starts_off, starts.data(), starts.size() * sizeof(dev::WaveStart));
+    if (lrecs)
+      std::memcpy(static_cast<char*>(h_plan_) + lay.long_off, lrecs, static_cast<size_t>(n_long) * sizeof(int32_t));
     MOC_HIP_CHECK(hipMemcpyAsync(d_plan_, h_plan_, lay.upload_bytes, hipMemcpyHostToDevice, stream));
   }
   const dev::ProblemView pv = problem_view(cp.max_l2);
@@ -575,13 +631,8 @@ void HipEngine::solve_device(const uint8_t* d_codes, const int64_t* d_offsets, c
     else
       dev::launch_short(pv, a, num_cus_, stream);
   }
-  if (!cp.tiles.empty()) {
-    dev::Plan plan;
-    plan.n_tiles = static_cast<int64_t>(cp.tiles.size());
-    plan.n_long = static_cast<int64_t>(cp.long_recs.size());
-    plan.tiles = reinterpret_cast<const dev::Tile*>(static_cast<char*>(d_plan_) + lay.tiles_off);
-    plan.long_recs = reinterpret_cast<const int32_t*>(static_cast<char*>(d_plan_) + lay.long_off);
-    plan.keys = reinterpret_cast<unsigned long long*>(static_cast<char*>(d_plan_) + lay.keys_off);
+  if (!starts.empty()) {
+    dev::Plan plan = device_plan(d_plan_, starts.size(), lrecs != nullptr, n_long, tile_u);
     dev::BatchView bv{d_codes + h_offsets[0], d_offsets, n};
     dev::launch_tiles(pv, bv, plan, d_out, static_cast<int>(ResultFormat::R12), stream);
   }
@@ -590,7 +641,7 @@ void HipEngine::solve_device(const uint8_t* d_codes, const int64_t* d_offsets, c
   stats_ = EngineStats{};
   stats_.cells = cp.cells;
   stats_.records = n;
-  stats_.kernels = (short_ok ? (swipe ? 1 : 2) : 0) | (cp.tiles.empty() ? 0 : 4);
+  stats_.kernels = (short_ok ? (swipe ? 1 : 2) : 0) | (starts.empty() ? 0 : 4);
 }
 
 }  // namespace moc
@@ -605,37 +656,26 @@ void HipEngine::search_keys_device(const uint8_t* d_codes, const int64_t* d_offs
   if (n <= 0) return;
   if (!stream) stream = s_compute_;
   TraceRange tr("moc.search_keys");
-  // global tile list over all records (record-major); this part takes a contiguous share of it
-  int64_t total = 0, max_l2 = 0;
-  for (int64_t i = 0; i < n; ++i) {
-    const int64_t L2 = h_offsets[i + 1] - h_offsets[i];
-    max_l2 = std::max(max_l2, L2);
-    total += (dev::lanes_needed(L1_, L2) + dev::kTileOffsets - 1) / dev::kTileOffsets;
-  }
+  int64_t max_l2 = 0;
+  for (int64_t i = 0; i < n; ++i) max_l2 = std::max(max_l2, h_offsets[i + 1] - h_offsets[i]);
   if (max_l2 * std::max<int64_t>(L1_, 1) >= (int64_t{1} << 32))
     throw Error("L1 * max L2 exceeds the 32-bit candidate index of the device engine");
-  const int64_t g0 = total * part / parts, g1 = total * (part + 1) / parts;
-  std::vector<dev::Tile> tiles;
-  tiles.reserve(static_cast<size_t>(g1 - g0));
-  int64_t g = 0;
-  for (int64_t i = 0; i < n && g < g1; ++i) {
-    const int64_t need = dev::lanes_needed(L1_, h_offsets[i + 1] - h_offsets[i]);
-    const int64_t nt = (need + dev::kTileOffsets - 1) / dev::kTileOffsets;
-    for (int64_t t = std::max<int64_t>(g0 - g, 0); t < nt && g + t < g1; ++t)
-      tiles.push_back(dev::Tile{static_cast<int32_t>(i), static_cast<int32_t>(t * dev::kTileOffsets)});
-    g += nt;
-  }
+  // the record-major tile list of all records; this part takes a contiguous, cost-balanced share of it
+  int tile_u = 0;
+  const std::vector<dev::WaveStart> starts = plan_waves(h_offsets, nullptr, n, part, parts, tile_u);
   MOC_HIP_CHECK(hipEventSynchronize(ev_plan_));  // previous call's plan buffers are free again
-  const size_t bytes = std::max<size_t>(tiles.size() * sizeof(dev::Tile), 8);
+  const size_t bytes = std::max<size_t>(starts.size() * sizeof(dev::WaveStart), 8);
   ensure(d_plan_, d_plan_cap_, bytes);
   ensure_host(h_plan_, h_plan_cap_, bytes);
-  if (!tiles.empty()) {
-    std::memcpy(h_plan_, tiles.data(), tiles.size() * sizeof(dev::Tile));
-    MOC_HIP_CHECK(hipMemcpyAsync(d_plan_, h_plan_, tiles.size() * sizeof(dev::Tile), hipMemcpyHostToDevice, stream));
+  if (!starts.empty()) {
+    std::memcpy(h_plan_, starts.data(), starts.size() * sizeof(dev::WaveStart));
+    MOC_HIP_CHECK(hipMemcpyAsync(d_plan_, h_plan_, starts.size() * sizeof(dev::WaveStart), hipMemcpyHostToDevice,
+                                 stream));
   }
   dev::Plan plan;
-  plan.n_tiles = static_cast<int64_t>(tiles.size());
-  plan.tiles = static_cast<const dev::Tile*>(d_plan_);
+  plan.u = tile_u;
+  plan.n_waves = starts.empty() ? 0 : static_cast<int64_t>(starts.size()) - 1;
+  plan.starts = static_cast<const dev::WaveStart*>(d_plan_);
   plan.long_recs = nullptr;
   plan.n_long = n;
   plan.keys = d_keys;
@@ -645,7 +685,7 @@ void HipEngine::search_keys_device(const uint8_t* d_codes, const int64_t* d_offs
   MOC_HIP_CHECK(hipEventRecord(ev_plan_, stream));
   stats_ = EngineStats{};
   stats_.records = n;
-  stats_.kernels = plan.n_tiles ? 4 : 0;
+  stats_.kernels = plan.n_waves ? 4 : 0;
 }
 
 void HipEngine::finalize_keys_device(const int64_t* d_offsets, int64_t n, const unsigned long long* d_keys,

@@ -13,7 +13,9 @@ from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_size_
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libmoc.so")
+# MOC_LIB_PATH selects an alternative build of the same library (A/B kernel experiments, the
+# `make debug-kernels` build); the default is the in-tree build.
+LIB_PATH = os.environ.get("MOC_LIB_PATH") or os.path.join(_HERE, "lib", "libmoc.so")
 
 RESULT_DTYPE = np.dtype([("score", "<i4"), ("n", "<i4"), ("k", "<i4")])
 # Packed result wire formats (moc/device.hpp ResultFormat): index = format id.
