@@ -41,7 +41,7 @@ HIP_OBJS  := $(patsubst csrc/src/%.hip,$(OBJ)/%.o,$(HIP_SRCS))
 COMM_OBJS := $(patsubst csrc/src/%.cpp,$(OBJ)/%.o,$(COMM_SRCS))
 HEADERS   := $(shell find csrc/include -name '*.h' -o -name '*.hpp')
 
-.PHONY: all build lib clean run runOn2 test asan tsan
+.PHONY: all build lib clean run runOn2 test asan tsan debug-kernels
 
 all: build
 build: lib final
@@ -108,6 +108,15 @@ tsan: $(MPILIB)/libmpi.so
 	$(TSAN_CXX) -fopenmp -fsanitize=thread -o final_tsan $(BUILD)/tsan/*.o \
 	    -L$(MPILIB) -lmpi -Wl,-rpath-link,$(MPI_HOME)/lib -Wl,-rpath,'$$ORIGIN/$(MPILIB)' \
 	    -L$(ROCM)/lib/llvm/lib -Wl,-rpath,$(ROCM)/lib/llvm/lib $(LDROCM) -lrccl
+
+# Device-side bounds checks (MOC_DCHECK: printf, never a fault) in every kernel -> build/debug/libmoc.so;
+# select it with MOC_LIB_PATH=$$PWD/build/debug/libmoc.so.
+debug-kernels:
+	@mkdir -p $(BUILD)/debug
+	for f in $(HIP_SRCS); do \
+	  $(HIPCC) $(HIPFLAGS) -DMOC_DEBUG_KERNELS -c $$f -o $(BUILD)/debug/$$(basename $$f .hip).hip.o || exit 1; \
+	done
+	$(CXX) -shared -fopenmp -o $(BUILD)/debug/libmoc.so $(CORE_OBJS) $(BUILD)/debug/*.hip.o $(LDROCM)
 
 clean:
 	rm -rf $(BUILD) final final_asan final_tsan $(PKG_LIB)

@@ -44,14 +44,16 @@ def parse_args():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, default) | gloo (multi-rank rehearsal)")
     ap.add_argument("--numa", type=int, default=1, help="bind each rank to its GPU's NUMA node")
     ap.add_argument("--packed", type=int, default=1, help="letters as 5-bit packed CSR (1) or one byte each (0)")
+    ap.add_argument("--narrow", type=int, default=1,
+                    help="1: narrowest wire formats that fit (4-bit lengths, R2 results); 0: uint8 lengths, R4")
     return ap.parse_args()
 
 
 class HostArrays:
     """Per-rank slice of the node-shared input/result arrays (/dev/shm files, or private memory)."""
 
-    def __init__(self, tag, rank, lengths, use_shm, packed, seed):
-        from mpi_openmp_cuda_amd.models.problem import pack5, packed5_bytes
+    def __init__(self, tag, rank, lengths, use_shm, packed, seed, len_base):
+        from mpi_openmp_cuda_amd.models.problem import pack5, pack_lengths4, packed5_bytes
         from mpi_openmp_cuda_amd.utils.synthetic import fill_codes
 
         n = lengths.shape[0]
@@ -75,8 +77,14 @@ class HostArrays:
         self.offsets = mk("offsets", np.int64, n + 1)
         self.offsets[0] = 0
         np.cumsum(lengths, out=self.offsets[1:])
-        self.lengths = mk("lengths", np.uint8, n)  # narrow lengths (the parser's by-product)
-        self.lengths[:] = lengths
+        # narrow lengths (the parser's by-product): 4 bits above the batch's minimum when the range allows
+        self.len_bits = 4 if len_base is not None else 8
+        if self.len_bits == 4:
+            self.lengths = mk("lengths4", np.uint8, (n + 1) // 2)
+            pack_lengths4(lengths, len_base, out=self.lengths)
+        else:
+            self.lengths = mk("lengths", np.uint8, n)
+            self.lengths[:] = lengths
         # letters: the parser's packed CSR (5 bits per letter) or one byte per letter
         letters = np.empty(total, dtype=np.uint8)
         fill_codes(letters, seed)
@@ -148,11 +156,13 @@ def main():
     rrng = np.random.default_rng(args.seed + 1 + rank)
     lengths = rrng.integers(shape.l2_min, shape.l2_max + 1, size=R, dtype=np.int64)
     tag = os.environ.get("MASTER_PORT", str(os.getpid()))
-    host = HostArrays(tag, rank, lengths, bool(args.shm), args.packed, args.seed + 101 + rank)
+    narrow4 = bool(args.narrow) and shape.l2_max - shape.l2_min <= 15
+    host = HostArrays(tag, rank, lengths, bool(args.shm), args.packed, args.seed + 101 + rank,
+                      shape.l2_min if narrow4 else None)
     del lengths
     eng = HipSearchEngine(device=gpu)
     eng.set_problem(weights, seq1)
-    fmt = eng.auto_format(shape.l2_max)
+    fmt = eng.auto_format(shape.l2_max, shape.l2_min if args.narrow else 0)
     rdt = _lib.FORMAT_DTYPES[_lib.FORMAT_NAMES.index(fmt)]
     if host.shm:
         p = f"/dev/shm/moc_bench_{tag}_{rank}_results"
@@ -170,7 +180,8 @@ def main():
         hdr_host[:] = header.cpu().numpy()
         eng.set_problem(hdr_host[:4], hdr_host[4:].astype(np.uint8))
         eng.solve(host.codes, host.offsets, out=host.results, lengths=host.lengths, fmt=fmt,
-                  l2_range=(shape.l2_min, shape.l2_max), packed5=host.packed)
+                  l2_range=(shape.l2_min, shape.l2_max), packed5=host.packed, lengths_bits=host.len_bits,
+                  lengths_base=shape.l2_min)
         done.fill_(R)
         if distributed:
             dist.all_reduce(done)
@@ -179,8 +190,12 @@ def main():
         step()
     barrier()
     t0 = time.perf_counter()
+    kms, tms = [], []
     for _ in range(args.steps):
         step()
+        st = eng.stats()
+        kms.append(st["kernel_ms"])
+        tms.append(st["total_ms"])
     barrier()
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
@@ -197,7 +212,8 @@ def main():
     if nv > 0:
         sub = Problem(shape.weights, seq1, host.check_letters[:int(host.offsets[nv])], host.offsets[:nv + 1].copy())
         ref = as_triples(search_cpu(sub))
-        ok = int(np.array_equal(as_triples(host.results[:nv]), ref))
+        r2 = eng.r2_params(shape.l2_min, shape.l2_max) if fmt == "r2" else None
+        ok = int(np.array_equal(as_triples(host.results[:nv], r2=r2), ref))
     okt = torch.tensor([ok], dtype=torch.int32, device=cdev)
     if distributed:
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
@@ -235,11 +251,14 @@ def main():
             },
             "records_per_s": round(total_records * args.steps / elapsed, 1),
             "cells_per_s_est": round(total_records * cells_per_rec * args.steps / elapsed, 1),
-            "rank0_kernel_ms_per_step": round(st["kernel_ms"], 4),
+            "rank0_kernel_ms_per_step": round(float(np.median(kms)), 4),
+            "rank0_kernel_ms_min_max": [round(min(kms), 4), round(max(kms), 4)],
+            "rank0_solve_ms_median": round(float(np.median(tms)), 4),
             "rank0_h2d_bytes_per_step": int(st["h2d_bytes"]),
             "rank0_d2h_bytes_per_step": int(st["d2h_bytes"]),
             "host_arrays": "shm" if host.shm else "private",
             "result_format": fmt,
+            "lengths_bits": host.len_bits,
             "letters": "packed5" if host.packed else "bytes",
             "rank0_numa_node": numa,
             "rank0_kernels": st["kernels"],

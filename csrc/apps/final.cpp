@@ -221,7 +221,7 @@ void Job::setup_engine() {
     eo.chunk_bytes = flags_.get_int("chunk-bytes", eo.chunk_bytes);
     eng_.hip = std::make_unique<HipEngine>(eo);
   }
-  int gpu_minmax[2] = {eng_.gpu ? 1 : 0, eng_.gpu ? 0 : -1};  // {min gpu, -max gpu}
+  int gpu_minmax[2] = {eng_.gpu ? 1 : 0, eng_.gpu ? -1 : 0};  // MIN -> {min gpu, -max gpu}
   MPI_Allreduce(MPI_IN_PLACE, gpu_minmax, 2, MPI_INT, MPI_MIN, ctx_.world);
   all_gpu_ = gpu_minmax[0] != 0;
   const bool any_gpu = gpu_minmax[1] != 0;

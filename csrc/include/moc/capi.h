@@ -64,19 +64,26 @@ int moc_device_numa_node(int device);
 int moc_dpp_probe(int32_t* out192);
 /* Transfer calibration: GB/s for kind 0 H2D, 1 D2H, 2 both, 3 zero-copy read, 4 zero-copy write, 5 D2D. */
 double moc_transfer_probe(int kind, size_t bytes, int iters);
+/* out6: type, hostPointer, devicePointer, hipHostGetDevicePointer, hipMemGetAddressRange base, size */
+int moc_pointer_info(const void* p, size_t bytes, uint64_t* out6);
+/* 1 when every byte of [p, p+bytes) is page-locked through this library's registry */
+int moc_pinned_covers(const void* p, size_t bytes);
 int moc_host_unregister(void* p);
 int moc_device_info_json(int device, char* buf, int64_t cap);
 void* moc_engine_create(int device, int64_t chunk_records, int64_t chunk_bytes, int allow_direct);
 void moc_engine_destroy(void* e);
 int moc_engine_set_problem(void* e, const int32_t* weights4, const uint8_t* seq1, int64_t L1, int semantics);
 int moc_engine_solve(void* e, const uint8_t* codes, const int64_t* offsets, int64_t n, moc_result* out);
-/* fmt: 0 = R12 (moc_result), 1 = R8 {i32,u16,u16}, 2 = R4 {i16,u8,u8}; lengths8 / min_l2 / max_l2 optional
- * (NULL / -1). Pinned host buffers + short records -> zero-copy streaming kernel. */
-int moc_engine_solve_ex(void* e, const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths8, int64_t n,
-                        void* out, int fmt, int64_t min_l2, int64_t max_l2, int packed5);
-int moc_engine_auto_format(void* e, int64_t max_l2);
+/* fmt: 0 = R12 (moc_result), 1 = R8 {i32,u16,u16}, 2 = R4 {i16,u8,u8}, 3 = R2 (u16 mixed-radix code,
+ * moc_engine_r2_params); lengths (len_bits 8, or 4 = two per byte, value + len_base) / min_l2 / max_l2
+ * optional (NULL / -1). Pinned host buffers + short records -> zero-copy streaming kernel. */
+int moc_engine_solve_ex(void* e, const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths, int len_bits,
+                        int len_base, int64_t n, void* out, int fmt, int64_t min_l2, int64_t max_l2, int packed5);
+int moc_engine_auto_format(void* e, int64_t max_l2, int64_t min_l2);
+/* R2 parameters {smin, kw, j} for records with lengths in [min_l2, max_l2] */
+int moc_engine_r2_params(void* e, int64_t min_l2, int64_t max_l2, int32_t* out3);
 int moc_engine_pin(void* e, const void* p, size_t bytes);
-int moc_expand_results(const void* in, int fmt, int64_t n, moc_result* out);
+
 int moc_engine_solve_device(void* e, const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets,
                             int64_t n, moc_result* d_out, void* stream);
 int moc_engine_search_keys(void* e, const uint8_t* codes, const int64_t* offsets, int64_t n, int part, int parts,

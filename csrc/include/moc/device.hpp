@@ -26,9 +26,9 @@
 
 namespace moc {
 
-// Result wire formats (device -> host). R12 is moc::Result; R8/R4 are chosen automatically when the
-// problem's bounds fit, to cut the D2H bytes per record by 1.5x / 3x.
-enum class ResultFormat : int32_t { R12 = 0, R8 = 1, R4 = 2 };
+// Result wire formats (device -> host). R12 is moc::Result; R8/R4/R2 are chosen automatically when the
+// problem's bounds fit, to cut the D2H bytes per record by 1.5x / 3x / 6x.
+enum class ResultFormat : int32_t { R12 = 0, R8 = 1, R4 = 2, R2 = 3 };
 struct R8 {
   int32_t score;
   uint16_t n, k;
@@ -38,11 +38,24 @@ struct R4 {
   uint8_t n, k;
 };
 static_assert(sizeof(R8) == 8 && sizeof(R4) == 4, "packed result formats");
-inline int result_bytes(ResultFormat f) { return f == ResultFormat::R12 ? 12 : f == ResultFormat::R8 ? 8 : 4; }
-// Smallest format able to hold every result of a problem with these bounds.
+// R2: one uint16 per record, code = (score - smin) * j + n * kw + k (mixed radix), 0xFFFF = no
+// candidate. Valid for a batch whose lengths lie in the [min_l2, max_l2] the parameters were made for.
+struct R2Params {
+  int32_t smin = 0;  // lowest possible score
+  int32_t kw = 0;    // radix of k (>= max_l2)
+  int32_t j = 0;     // radix of the score code (> every n * kw + k)
+};
+constexpr uint16_t kR2None = 0xFFFF;
+inline int result_bytes(ResultFormat f) {
+  return f == ResultFormat::R12 ? 12 : f == ResultFormat::R8 ? 8 : f == ResultFormat::R4 ? 4 : 2;
+}
+// R2 parameters for a problem (L1, pair-score range [min_t, max_t]) and a record-length range; false
+// when the codes would not fit 16 bits.
+bool r2_params(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t min_t, int32_t max_t, R2Params& p);
+// Smallest of R12/R8/R4 able to hold every result of a problem with these bounds.
 ResultFormat pick_result_format(int64_t L1, int64_t max_l2, int32_t max_abs_weight);
-// Expands packed results to moc::Result (host side).
-void expand_results(const void* in, ResultFormat f, int64_t n, Result* out);
+// Expands packed results to moc::Result (host side); `r2` is required for R2.
+void expand_results(const void* in, ResultFormat f, int64_t n, Result* out, const R2Params* r2 = nullptr);
 
 namespace dev {
 
@@ -57,6 +70,7 @@ struct ProblemView {
   int32_t L1;
   int32_t semantics;    // moc::Semantics
   int32_t key_shift;    // bits reserved for k in the int32 hot-loop key (0 -> 64-bit keys)
+  R2Params r2;          // parameters of the R2 result format (when used)
 };
 
 // One batch of records on the device. Offsets are absolute (int64) and rebased by offsets[0], so
@@ -87,6 +101,7 @@ struct Plan {
   int64_t n_long = 0;
   unsigned long long* keys = nullptr;  // device scratch, n_long entries (tile-kernel partial maxima)
   int32_t u = 2;                       // sub-tiles per wave tile (1, 2 or 4)
+  R2Params r2;                         // finalize: parameters of the R2 result format
 };
 
 // Arguments of the short-record kernel. All pointers must be device-accessible: device memory, or
@@ -95,6 +110,8 @@ struct ShortArgs {
   const uint8_t* codes = nullptr;     // base pointer: record i starts at codes + offsets[i]
   const int64_t* offsets = nullptr;   // n+1 absolute offsets
   const uint8_t* lengths8 = nullptr;  // optional narrow lengths (saves 7 B/record of reads)
+  const uint8_t* lengths4 = nullptr;  // optional nibble lengths: record i = len_base + nibble i (low first)
+  int32_t len_base = 0;
   int64_t n = 0;
   void* out = nullptr;                // results, format `fmt`, record i at index i
   int32_t fmt = 0;                    // ResultFormat
@@ -105,6 +122,7 @@ struct ShortArgs {
   int32_t max_l2 = 0;
   int32_t packed5 = 0;                // 1: `codes` is a 5-bit packed stream (char j at bit 5j); swipe only
   unsigned* counter = nullptr;        // device work counter, zeroed before each launch
+  int64_t dbg_codes_end = -1;         // debug builds: end of the readable letter bytes (from `codes`)
 };
 
 // Unpacks n chars of a 5-bit packed stream (device memory) starting at bit `bit0` into byte codes.

@@ -44,6 +44,7 @@ struct EngineStats {
   int32_t direct = 0;    // 1 if the last solve used the zero-copy streaming path
   int32_t format = 0;    // ResultFormat of the last solve
   int32_t kernels = 0;   // bitmask of kernels used: 1 swipe (lane/record), 2 short (lane/offset), 4 tiles
+  R2Params r2;           // parameters of the R2 results of the last solve (when fmt == R2)
 };
 
 // Optional metadata about a batch (e.g. known from parsing / generation) that lets the engine skip its
@@ -67,12 +68,17 @@ class HipEngine {
   // Host batch in -> host results out as moc::Result. `codes` is the base pointer (record i starts at
   // codes + offsets[i]); `offsets` has n+1 absolute entries.
   void solve(const uint8_t* codes, const int64_t* offsets, int64_t n, Result* out);
-  // General form: optional uint8 lengths (max L2 <= 255), results in `fmt`. With `packed5`, `codes` is
-  // a 5-bit packed stream (moc::pack5; char j at bit 5j) instead of one byte per letter.
-  void solve_ex(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths8, int64_t n, void* out,
-                ResultFormat fmt, const BatchHints& hints = {}, bool packed5 = false);
-  // Smallest result format for this problem given the batch's longest record.
-  ResultFormat auto_format(int64_t max_l2) const;
+  // General form: optional narrow lengths — len_bits 8 (uint8, max L2 <= 255) or 4 (two per byte, low
+  // nibble first, record i = len_base + nibble) — results in `fmt`. With `packed5`, `codes` is a 5-bit
+  // packed stream (moc::pack5; char j at bit 5j) instead of one byte per letter. R2 results are encoded
+  // for the hints' [min_l2, max_l2] (or the batch's own range): stats().r2 holds the parameters.
+  void solve_ex(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths, int64_t n, void* out,
+                ResultFormat fmt, const BatchHints& hints = {}, bool packed5 = false, int len_bits = 8,
+                int len_base = 0);
+  // Smallest result format for this problem given the batch's length range (min_l2 <= 0: unknown,
+  // R2 not considered).
+  ResultFormat auto_format(int64_t max_l2, int64_t min_l2 = 0) const;
+  R2Params r2_params_for(int64_t min_l2, int64_t max_l2) const;
 
   // Device-resident batch: d_codes/d_offsets/d_out on this device; h_offsets is a host copy of the
   // offsets used for planning. Work is queued on `stream` (0 = engine compute stream); no sync.
@@ -113,8 +119,8 @@ class HipEngine {
   dev::ProblemView problem_view(int64_t max_l2) const;
   void ensure(void*& ptr, size_t& cap, size_t bytes);
   void ensure_host(void*& ptr, size_t& cap, size_t bytes);
-  bool direct_pointers(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths8, int64_t n, void* out,
-                       int fb, bool packed5, dev::ShortArgs& a) const;
+  bool direct_pointers(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths, int len_bits,
+                       int len_base, int64_t n, void* out, int fb, bool packed5, dev::ShortArgs& a) const;
   void run_staged(const uint8_t* codes, const int64_t* offsets, int64_t n, void* out, ResultFormat fmt,
                   bool packed5);
 
@@ -126,6 +132,8 @@ class HipEngine {
   hipStream_t s_copy_ = nullptr, s_compute_ = nullptr, s_return_ = nullptr;
   // problem
   ScoreTable table_{};
+  int32_t min_t_ = 0, max_t_ = 0;  // pair-score range over letters (R2 parameters)
+  R2Params r2_{};                  // R2 parameters of the current solve
   int32_t* d_lut_ = nullptr;
   uint8_t* d_seq1_ = nullptr;
   int64_t L1_ = 0;

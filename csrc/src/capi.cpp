@@ -3,7 +3,10 @@
 
 #include <cstring>
 #include <exception>
+#include <map>
+#include <mutex>
 #include <string>
+#include <vector>
 
 #include "moc/cpu_engine.hpp"
 #include "moc/device.hpp"
@@ -14,6 +17,7 @@
 #include "moc/runtime/device.hpp"
 #include "moc/runtime/hip_check.hpp"
 #include "moc/runtime/log.hpp"
+#include "moc/runtime/pinned.hpp"
 #include "moc/score_table.hpp"
 
 static_assert(sizeof(moc_result) == sizeof(moc::Result), "ABI result layout");
@@ -39,6 +43,10 @@ moc::Weights weights_of(const int32_t* w4) {
   for (int i = 0; i < 4; ++i) w.w[i] = w4[i];
   return w;
 }
+
+// moc_host_register calls -> the registrations each made (released together by moc_host_unregister)
+std::mutex g_host_regs_mu;
+std::map<void*, std::vector<void*>> g_host_regs;
 
 moc::RecordBatch view_batch(const uint8_t* codes, const int64_t* offsets, int64_t n) {
   moc::RecordBatch b;
@@ -188,16 +196,56 @@ int moc_device_numa_node(int device) { return moc::device_numa_node(device); }
 
 int moc_host_register(void* p, size_t bytes) {
   return guard([&] {
-    const uintptr_t page = 4096;
-    uintptr_t b = reinterpret_cast<uintptr_t>(p) & ~(page - 1);
-    uintptr_t e = (reinterpret_cast<uintptr_t>(p) + bytes + page - 1) & ~(page - 1);
-    MOC_HIP_CHECK(hipHostRegister(reinterpret_cast<void*>(b), e - b, hipHostRegisterMapped));
+    std::vector<void*> made = moc::pinned::register_range(p, bytes);
+    std::lock_guard<std::mutex> lock(g_host_regs_mu);
+    auto& v = g_host_regs[p];
+    v.insert(v.end(), made.begin(), made.end());
   });
 }
 
+/* Diagnostics: device address of a pinned host range (0 when the range is not page-locked as one
+ * registration), and the runtime's view of the pointer (type, host and device pointers). */
+int moc_pointer_info(const void* p, size_t bytes, uint64_t* out4) {
+  return guard([&] {
+    out4[0] = out4[1] = out4[2] = out4[3] = out4[4] = out4[5] = 0;
+    {
+      hipDeviceptr_t base = nullptr;
+      size_t size = 0;
+      if (hipMemGetAddressRange(&base, &size, reinterpret_cast<hipDeviceptr_t>(const_cast<void*>(p))) == hipSuccess) {
+        out4[4] = reinterpret_cast<uint64_t>(base);
+        out4[5] = size;
+      } else {
+        (void)hipGetLastError();
+      }
+    }
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+      (void)hipGetLastError();
+      return;
+    }
+    out4[0] = static_cast<uint64_t>(a.type);
+    out4[1] = reinterpret_cast<uint64_t>(a.hostPointer);
+    out4[2] = reinterpret_cast<uint64_t>(a.devicePointer);
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, const_cast<void*>(p), 0) == hipSuccess) out4[3] = reinterpret_cast<uint64_t>(d);
+    else (void)hipGetLastError();
+    (void)bytes;
+  });
+}
+
+int moc_pinned_covers(const void* p, size_t bytes) { return moc::pinned::covers(p, bytes) ? 1 : 0; }
+
 int moc_host_unregister(void* p) {
   return guard([&] {
-    MOC_HIP_CHECK(hipHostUnregister(reinterpret_cast<void*>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t{4095})));
+    std::vector<void*> bases;
+    {
+      std::lock_guard<std::mutex> lock(g_host_regs_mu);
+      auto it = g_host_regs.find(p);
+      if (it == g_host_regs.end()) return;
+      bases = std::move(it->second);
+      g_host_regs.erase(it);
+    }
+    moc::pinned::unregister(bases);
   });
 }
 
@@ -236,19 +284,28 @@ int moc_engine_solve(void* e, const uint8_t* codes, const int64_t* offsets, int6
   });
 }
 
-int moc_engine_solve_ex(void* e, const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths8, int64_t n,
-                        void* out, int fmt, int64_t min_l2, int64_t max_l2, int packed5) {
+int moc_engine_solve_ex(void* e, const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths, int len_bits,
+                        int len_base, int64_t n, void* out, int fmt, int64_t min_l2, int64_t max_l2, int packed5) {
   return guard([&] {
     moc::BatchHints h;
     h.min_l2 = min_l2;
     h.max_l2 = max_l2;
-    static_cast<moc::HipEngine*>(e)->solve_ex(codes, offsets, lengths8, n, out, static_cast<moc::ResultFormat>(fmt), h,
-                                              packed5 != 0);
+    static_cast<moc::HipEngine*>(e)->solve_ex(codes, offsets, lengths, n, out, static_cast<moc::ResultFormat>(fmt), h,
+                                              packed5 != 0, len_bits, len_base);
   });
 }
 
-int moc_engine_auto_format(void* e, int64_t max_l2) {
-  return static_cast<int>(static_cast<moc::HipEngine*>(e)->auto_format(max_l2));
+int moc_engine_auto_format(void* e, int64_t max_l2, int64_t min_l2) {
+  return static_cast<int>(static_cast<moc::HipEngine*>(e)->auto_format(max_l2, min_l2));
+}
+
+int moc_engine_r2_params(void* e, int64_t min_l2, int64_t max_l2, int32_t* out3) {
+  return guard([&] {
+    const moc::R2Params p = static_cast<moc::HipEngine*>(e)->r2_params_for(min_l2, max_l2);
+    out3[0] = p.smin;
+    out3[1] = p.kw;
+    out3[2] = p.j;
+  });
 }
 
 int moc_engine_pin(void* e, const void* p, size_t bytes) {
@@ -288,9 +345,13 @@ int moc_engine_finalize_keys_device(void* e, const int64_t* d_offsets, int64_t n
   });
 }
 
-int moc_engine_stats(void* e, double* out10) {
+int moc_engine_stats(void* e, double* out13) {
   return guard([&] {
+    double* out10 = out13;
     const auto& s = static_cast<moc::HipEngine*>(e)->stats();
+    out13[10] = s.r2.smin;
+    out13[11] = s.r2.kw;
+    out13[12] = s.r2.j;
     out10[0] = s.kernel_ms;
     out10[1] = s.total_ms;
     out10[2] = static_cast<double>(s.h2d_bytes);
@@ -304,9 +365,16 @@ int moc_engine_stats(void* e, double* out10) {
   });
 }
 
-int moc_expand_results(const void* in, int fmt, int64_t n, moc_result* out) {
+int moc_expand_results(const void* in, int fmt, int64_t n, const int32_t* r2_3, moc_result* out) {
   return guard([&] {
-    moc::expand_results(in, static_cast<moc::ResultFormat>(fmt), n, reinterpret_cast<moc::Result*>(out));
+    moc::R2Params p;
+    if (r2_3) {
+      p.smin = r2_3[0];
+      p.kw = r2_3[1];
+      p.j = r2_3[2];
+    }
+    moc::expand_results(in, static_cast<moc::ResultFormat>(fmt), n, reinterpret_cast<moc::Result*>(out),
+                        r2_3 ? &p : nullptr);
   });
 }
 

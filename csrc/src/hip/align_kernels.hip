@@ -119,13 +119,13 @@ __global__ __launch_bounds__(256) void tile_search_kernel(ProblemView pv, BatchV
   }
 }
 
-__global__ void finalize_long_kernel(BatchView bv, const int32_t* __restrict__ long_recs,
+__global__ void finalize_long_kernel(R2Params r2, BatchView bv, const int32_t* __restrict__ long_recs,
                                      const unsigned long long* __restrict__ keys, int64_t n_long, void* out, int fmt) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= n_long) return;
   const int r = long_recs ? long_recs[i] : static_cast<int>(i);
   const int L2 = static_cast<int>(bv.offsets[r + 1] - bv.offsets[r]);
-  store_result(out, r, fmt, decode_key(keys[i], L2 > 0 ? L2 : 1));
+  store_result(out, r, fmt, decode_key(keys[i], L2 > 0 ? L2 : 1), r2);
 }
 
 // Self-test of the cross-lane primitives the search kernels rely on (one wave):
@@ -173,7 +173,7 @@ void launch_search_u(const ProblemView& pv, const BatchView& bv, const Plan& pla
 void launch_finalize(const BatchView& bv, const Plan& plan, void* out, int fmt, hipStream_t stream) {
   if (plan.n_long <= 0) return;
   const int64_t fb = (plan.n_long + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(finalize_long_kernel, dim3(static_cast<unsigned>(fb)), dim3(kBlock), 0, stream, bv,
+  hipLaunchKernelGGL(finalize_long_kernel, dim3(static_cast<unsigned>(fb)), dim3(kBlock), 0, stream, plan.r2, bv,
                      plan.long_recs, plan.keys, plan.n_long, out, fmt);
 }
 }  // namespace

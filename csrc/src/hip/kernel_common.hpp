@@ -143,8 +143,11 @@ __device__ __forceinline__ unsigned long long lane_candidate(bool own, int o, in
 }
 
 // ---- result formats -------------------------------------------------------------------------------
-__device__ __forceinline__ void store_result(void* out, int64_t r, int fmt, const Result& v) {
-  if (fmt == static_cast<int>(ResultFormat::R4)) {
+__device__ __forceinline__ void store_result(void* out, int64_t r, int fmt, const Result& v, const R2Params& p) {
+  if (fmt == static_cast<int>(ResultFormat::R2)) {
+    static_cast<uint16_t*>(out)[r] =
+        v.score == INT32_MIN ? kR2None : static_cast<uint16_t>((v.score - p.smin) * p.j + v.n * p.kw + v.k);
+  } else if (fmt == static_cast<int>(ResultFormat::R4)) {
     R4 x;
     x.score = static_cast<int16_t>(v.score == INT32_MIN ? INT16_MIN : v.score);
     x.n = static_cast<uint8_t>(v.n);
@@ -159,6 +162,29 @@ __device__ __forceinline__ void store_result(void* out, int64_t r, int fmt, cons
   } else {
     static_cast<Result*>(out)[r] = v;
   }
+}
+
+__device__ __forceinline__ int fmt_bytes(int fmt) {
+  return fmt == static_cast<int>(ResultFormat::R12) ? 12
+         : fmt == static_cast<int>(ResultFormat::R8) ? 8
+         : fmt == static_cast<int>(ResultFormat::R4) ? 4
+                                                      : 2;
+}
+
+// Length of record `idx` of the batch from the narrowest available source.
+__device__ __forceinline__ int record_length(const ShortArgs& a, int64_t idx) {
+  if (a.lengths4) return a.len_base + ((a.lengths4[idx >> 1] >> (4 * (idx & 1))) & 15);
+  if (a.lengths8) return a.lengths8[idx];
+  return static_cast<int>(a.offsets[idx + 1] - a.offsets[idx]);
+}
+
+// Copies a block's staged results (LDS) to the output: dwords, plus a trailing halfword for R2 tiles
+// of odd length. `dst` is 4-byte aligned (tiles start at multiples of 64 records).
+__device__ __forceinline__ void copy_results(void* dst, const uint8_t* src, int bytes, int tid, int nthreads) {
+  const int nd = bytes >> 2;
+  for (int q = tid; q < nd; q += nthreads) static_cast<uint32_t*>(dst)[q] = reinterpret_cast<const uint32_t*>(src)[q];
+  if ((bytes & 2) && tid == 0)
+    static_cast<uint16_t*>(dst)[2 * nd] = reinterpret_cast<const uint16_t*>(src)[2 * nd];
 }
 
 __device__ __forceinline__ void stage_lut(int* lut, const int32_t* g) {

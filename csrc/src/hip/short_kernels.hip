@@ -89,7 +89,7 @@ __global__ __launch_bounds__(kBlock) void short_search_kernel(ProblemView pv, Sh
   const int sl = lane / slot;
   const int o = lane - sl * slot;
   const int shift = pv.key_shift, mask = (1 << pv.key_shift) - 1;
-  const int fb = a.fmt == static_cast<int>(ResultFormat::R4) ? 4 : a.fmt == static_cast<int>(ResultFormat::R8) ? 8 : 12;
+  const int fb = fmt_bytes(a.fmt);
   const int64_t n_tiles = (a.n + a.tile_records - 1) / a.tile_records;
 
   for (;;) {
@@ -110,7 +110,7 @@ __global__ __launch_bounds__(kBlock) void short_search_kernel(ProblemView pv, Sh
     for (int q = 0; q < 4; ++q) {
       const int r = tid * 4 + q;
       int L = 0;
-      if (r < m) L = a.lengths8 ? static_cast<int>(a.lengths8[rb + r]) : static_cast<int>(a.offsets[rb + r + 1] - a.offsets[rb + r]);
+      if (r < m) L = record_length(a, rb + r);
       len4[q] = L;
       sum += L;
     }
@@ -170,15 +170,12 @@ __global__ __launch_bounds__(kBlock) void short_search_kernel(ProblemView pv, Sh
         const unsigned long long other = shfl_down_u64(key, d);
         if (o + d < slot) key = max_u64(key, other);
       }
-      if (mine && o == 0) store_result(res_l, rl, a.fmt, decode_key(key, L2 > 0 ? L2 : 1));
+      if (mine && o == 0) store_result(res_l, rl, a.fmt, decode_key(key, L2 > 0 ? L2 : 1), pv.r2);
     }
     __syncthreads();
 
     // ---- 4. results -> out (coalesced dwords; long records are overwritten later by the tile kernel)
-    uint32_t* dst = reinterpret_cast<uint32_t*>(static_cast<char*>(a.out) + rb * fb);
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(res_l);
-    const int nd = m * fb / 4;
-    for (int q = tid; q < nd; q += kBlock) dst[q] = src[q];
+    copy_results(static_cast<char*>(a.out) + rb * fb, res_l, m * fb, tid, kBlock);
   }
 }
 

@@ -87,7 +87,7 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
       prof[e] = static_cast<short>((c >= 1 && j < L1) ? pv.lut[c * kLutStride + pv.seq1[j]] : 0);
     }
   }
-  const int fb = a.fmt == static_cast<int>(ResultFormat::R4) ? 4 : a.fmt == static_cast<int>(ResultFormat::R8) ? 8 : 12;
+  const int fb = fmt_bytes(a.fmt);
   const int64_t n_tiles = (a.n + a.tile_records - 1) / a.tile_records;
   const int sem = pv.semantics;
 
@@ -109,7 +109,7 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
     for (int q = 0; q < 4; ++q) {
       const int r = tid * 4 + q;
       int L = 0;
-      if (r < m) L = a.lengths8 ? static_cast<int>(a.lengths8[rb + r]) : static_cast<int>(a.offsets[rb + r + 1] - a.offsets[rb + r]);
+      if (r < m) L = record_length(a, rb + r);
       len4[q] = L;
       sum += L;
     }
@@ -124,7 +124,10 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
       if (r < m) loff[r] = excl;
       excl += len4[q];
     }
-    if (tid == kBlock - 1) loff[m] = excl;
+    if (tid == kBlock - 1) {
+      loff[m] = excl;
+      MOC_DCHECK(excl == end - start);  // lengths agree with offsets
+    }
 
     // ---- letters -> LDS (16-byte loads). Byte codes: char j at byte j. Packed: char j at bit 5j.
     //      shift_b = position (bytes, or bits when P5) of the tile's first char inside the LDS copy.
@@ -134,6 +137,12 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
     const uintptr_t a0 = p0 & ~uintptr_t{15};
     const int shift_b = P5 ? static_cast<int>(8 * (p0 - a0) + ((5 * start) & 7)) : static_cast<int>(p0 - a0);
     const int nvec = static_cast<int>((reinterpret_cast<uintptr_t>(a.codes + b_end) + 15 - a0) >> 4);
+    if (tid == 0) {
+      MOC_DCHECK(a.dbg_codes_end < 0 || a0 + 16 * static_cast<uintptr_t>(nvec) <=
+                                            reinterpret_cast<uintptr_t>(a.codes) + a.dbg_codes_end);
+      MOC_DCHECK(end >= start && m > 0 && m <= a.tile_records);
+      MOC_DCHECK((P5 ? (5 * (end - start) + 7) / 8 + 32 : end - start + 32) <= a.codes_cap);
+    }
     for (int v = tid; v < nvec; v += kBlock)
       reinterpret_cast<uint4*>(codes_l)[v] = reinterpret_cast<const uint4*>(a0)[v];
     __syncthreads();
@@ -242,14 +251,11 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
           const uint32_t idx = 0xffffu - (best & 0xffffu);
           res = Result{static_cast<int>(best >> 16) - 32768, static_cast<int>(idx >> KB), static_cast<int>(idx & KMASK)};
         }
-        store_result(res_l, rl, a.fmt, res);
+        store_result(res_l, rl, a.fmt, res, pv.r2);
       }
     }
     __syncthreads();
-    uint32_t* dst = reinterpret_cast<uint32_t*>(static_cast<char*>(a.out) + rb * fb);
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(res_l);
-    const int nd = m * fb / 4;
-    for (int q = tid; q < nd; q += kBlock) dst[q] = src[q];
+    copy_results(static_cast<char*>(a.out) + rb * fb, res_l, m * fb, tid, kBlock);
   }
 }
 

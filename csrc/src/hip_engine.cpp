@@ -10,6 +10,7 @@
 #include "moc/problem.hpp"
 #include "moc/runtime/hip_check.hpp"
 #include "moc/runtime/log.hpp"
+#include "moc/runtime/pinned.hpp"
 #include "moc/runtime/timer.hpp"
 #include "moc/runtime/trace.hpp"
 
@@ -30,14 +31,37 @@ ResultFormat pick_result_format(int64_t L1, int64_t max_l2, int32_t max_abs_weig
   return ResultFormat::R12;
 }
 
-void expand_results(const void* in, ResultFormat f, int64_t n, Result* out) {
+bool r2_params(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t min_t, int32_t max_t, R2Params& p) {
+  min_l2 = std::max<int64_t>(min_l2, 1);
+  max_l2 = std::max(max_l2, min_l2);
+  const int64_t smin = std::min(static_cast<int64_t>(min_t) * min_l2, static_cast<int64_t>(min_t) * max_l2);
+  const int64_t smax = std::max(static_cast<int64_t>(max_t) * min_l2, static_cast<int64_t>(max_t) * max_l2);
+  const int64_t kw = max_l2;
+  const int64_t j = std::max<int64_t>(L1 - min_l2 + 1, 1) * kw;  // > (L1 - min_l2) * kw + (kw - 1) >= n*kw + k
+  if ((smax - smin + 1) * j > kR2None) return false;            // 0xFFFF stays free for "no candidate"
+  p.smin = static_cast<int32_t>(smin);
+  p.kw = static_cast<int32_t>(kw);
+  p.j = static_cast<int32_t>(j);
+  return true;
+}
+
+void expand_results(const void* in, ResultFormat f, int64_t n, Result* out, const R2Params* r2) {
   if (f == ResultFormat::R12) {
     if (in != out) std::memmove(out, in, sizeof(Result) * static_cast<size_t>(n));
     return;
   }
+  if (f == ResultFormat::R2 && (!r2 || r2->j <= 0 || r2->kw <= 0)) throw Error("expand_results: R2 needs its parameters");
 #pragma omp parallel for schedule(static) if (n > 65536)
   for (int64_t i = 0; i < n; ++i) {
-    if (f == ResultFormat::R8) {
+    if (f == ResultFormat::R2) {
+      const uint16_t c = static_cast<const uint16_t*>(in)[i];
+      if (c == kR2None) {
+        out[i] = Result{INT32_MIN, 0, 0};
+      } else {
+        const int32_t idx = c % r2->j;
+        out[i] = Result{c / r2->j + r2->smin, idx / r2->kw, idx % r2->kw};
+      }
+    } else if (f == ResultFormat::R8) {
       const R8 x = static_cast<const R8*>(in)[i];
       out[i] = Result{x.score, x.n, x.k};
     } else {
@@ -48,28 +72,11 @@ void expand_results(const void* in, ResultFormat f, int64_t n, Result* out) {
 }
 
 namespace {
-// True when [p, p+bytes) is page-locked host memory (hipHostMalloc or hipHostRegister); *dev gets the
-// device-side address of p.
+// True when every byte of [p, p+bytes) is page-locked through the registry (moc/runtime/pinned.hpp);
+// *dev gets the device-side address of p.
 bool pinned_range(const void* p, size_t bytes, const void** dev) {
-  if (!p) return false;
-  hipPointerAttribute_t a, b;
-  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
-  if (a.type != hipMemoryTypeHost) return false;
-  if (bytes > 1) {
-    if (hipPointerGetAttributes(&b, static_cast<const char*>(p) + bytes - 1) != hipSuccess) {
-      (void)hipGetLastError();
-      return false;
-    }
-    if (b.type != hipMemoryTypeHost) return false;
-  }
-  void* d = nullptr;
-  if (hipHostGetDevicePointer(&d, const_cast<void*>(p), 0) != hipSuccess || !d) {
-    (void)hipGetLastError();
-    return false;
-  }
+  const void* d = pinned::device_address(p, bytes);
+  if (!d) return false;
   *dev = d;
   return true;
 }
@@ -157,18 +164,12 @@ HipEngine::~HipEngine() {
 }
 
 void HipEngine::pin(const void* p, size_t bytes) {
-  if (!p || bytes == 0) return;
-  const void* d = nullptr;
-  if (pinned_range(p, bytes, &d)) return;  // already pinned
-  const uintptr_t page = 4096;
-  uintptr_t b = reinterpret_cast<uintptr_t>(p) & ~(page - 1);
-  uintptr_t e = (reinterpret_cast<uintptr_t>(p) + bytes + page - 1) & ~(page - 1);
-  MOC_HIP_CHECK(hipHostRegister(reinterpret_cast<void*>(b), e - b, hipHostRegisterMapped));
-  pinned_.push_back(reinterpret_cast<void*>(b));
+  const std::vector<void*> made = pinned::register_range(p, bytes);  // only pages not yet locked
+  pinned_.insert(pinned_.end(), made.begin(), made.end());
 }
 
 void HipEngine::unpin_all() {
-  for (void* p : pinned_) (void)hipHostUnregister(p);
+  pinned::unregister(pinned_);
   pinned_.clear();
 }
 
@@ -195,6 +196,13 @@ void HipEngine::set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, S
   MOC_HIP_CHECK(hipSetDevice(device_));
   if (L1 > (int64_t{1} << 30)) throw Error("Seq1 too long for the device engine");
   table_ = ScoreTable::build(w);
+  min_t_ = INT32_MAX;
+  max_t_ = INT32_MIN;
+  for (int x = 1; x < kAlphabet; ++x)
+    for (int y = 1; y < kAlphabet; ++y) {
+      min_t_ = std::min(min_t_, table_.lut[x * kLutStride + y]);
+      max_t_ = std::max(max_t_, table_.lut[x * kLutStride + y]);
+    }
   L1_ = L1;
   sem_ = sem;
   if (!d_lut_) MOC_HIP_CHECK(hipMalloc(&d_lut_, sizeof(int32_t) * kLutStride * kLutStride));
@@ -224,11 +232,20 @@ dev::ProblemView HipEngine::problem_view(int64_t max_l2) const {
   pv.L1 = static_cast<int32_t>(L1_);
   pv.semantics = static_cast<int32_t>(sem_);
   pv.key_shift = choose_key_shift(table_.max_abs(), std::min<int64_t>(std::max<int64_t>(max_l2, 1), L1_ + 1));
+  pv.r2 = r2_;
   return pv;
 }
 
-ResultFormat HipEngine::auto_format(int64_t max_l2) const {
+ResultFormat HipEngine::auto_format(int64_t max_l2, int64_t min_l2) const {
+  R2Params p;
+  if (min_l2 > 0 && r2_params(L1_, min_l2, max_l2, min_t_, max_t_, p)) return ResultFormat::R2;
   return pick_result_format(L1_, max_l2, table_.max_abs());
+}
+
+R2Params HipEngine::r2_params_for(int64_t min_l2, int64_t max_l2) const {
+  R2Params p;
+  if (!r2_params(L1_, min_l2, max_l2, min_t_, max_t_, p)) throw Error("R2 cannot hold records of these lengths");
+  return p;
 }
 
 // Splits a chunk's records into the short-kernel set (<= 64 lanes) and the long list (tile kernel).
@@ -304,6 +321,7 @@ dev::Plan HipEngine::device_plan(void* d_plan, size_t n_starts, bool has_long_re
   plan.long_recs = has_long_recs ? reinterpret_cast<const int32_t*>(base + lay.long_off) : nullptr;
   plan.n_long = n_long;
   plan.keys = reinterpret_cast<unsigned long long*>(base + lay.keys_off);
+  plan.r2 = r2_;
   return plan;
 }
 
@@ -389,20 +407,25 @@ LenStats scan_lengths(const int64_t* offsets, const uint8_t* lengths8, int64_t n
 }
 }  // namespace
 
-bool HipEngine::direct_pointers(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths8, int64_t n,
-                                void* out, int fb, bool packed5, dev::ShortArgs& a) const {
+bool HipEngine::direct_pointers(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths, int len_bits,
+                                int len_base, int64_t n, void* out, int fb, bool packed5, dev::ShortArgs& a) const {
   const void *dc = nullptr, *doff = nullptr, *dlen = nullptr, *dout = nullptr;
   const int64_t c0 = offsets[0], c1 = offsets[n];
   // byte range of the letters: [b0, b1)
   const int64_t b0 = packed5 ? (5 * c0) >> 3 : c0, b1 = packed5 ? ((5 * c1 + 7) >> 3) + 1 : c1;
-  if (c1 > c0 && !pinned_range(codes + b0, static_cast<size_t>(b1 - b0), &dc)) return false;
+  // the kernels stage letters with 16-byte loads: up to 15 bytes past the range end must be mapped too
+  if (c1 > c0 && !pinned_range(codes + b0, static_cast<size_t>(b1 - b0) + 16, &dc)) return false;
   if (!pinned_range(offsets, sizeof(int64_t) * static_cast<size_t>(n + 1), &doff)) return false;
-  if (lengths8 && !pinned_range(lengths8, static_cast<size_t>(n), &dlen)) return false;
+  const size_t len_bytes = len_bits == 4 ? static_cast<size_t>((n + 1) / 2) : static_cast<size_t>(n);
+  if (lengths && !pinned_range(lengths, len_bytes, &dlen)) return false;
   if (!pinned_range(out, static_cast<size_t>(fb) * static_cast<size_t>(n), &dout)) return false;
   // device view of the codes base pointer (record i at base + offsets[i], or at bit 5*offsets[i])
   a.codes = c1 > c0 ? static_cast<const uint8_t*>(dc) - b0 : nullptr;
+  a.dbg_codes_end = b1;
   a.offsets = static_cast<const int64_t*>(doff);
-  a.lengths8 = static_cast<const uint8_t*>(dlen);
+  a.lengths8 = len_bits == 8 ? static_cast<const uint8_t*>(dlen) : nullptr;
+  a.lengths4 = len_bits == 4 ? static_cast<const uint8_t*>(dlen) : nullptr;
+  a.len_base = len_base;
   a.out = const_cast<void*>(dout);
   return c1 > c0;
 }
@@ -411,8 +434,9 @@ void HipEngine::solve(const uint8_t* codes, const int64_t* offsets, int64_t n, R
   solve_ex(codes, offsets, nullptr, n, out, ResultFormat::R12);
 }
 
-void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths8, int64_t n, void* out,
-                         ResultFormat fmt, const BatchHints& hints, bool packed5) {
+void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths, int64_t n, void* out,
+                         ResultFormat fmt, const BatchHints& hints, bool packed5, int len_bits, int len_base) {
+  if (lengths && len_bits != 8 && len_bits != 4) throw Error("lengths must be 8- or 4-bit");
   if (!have_problem_) throw Error("HipEngine::solve before set_problem");
   MOC_HIP_CHECK(hipSetDevice(device_));
   TraceRange tr("moc.solve");
@@ -430,12 +454,18 @@ void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uin
     ls.mn = hints.min_l2;
     ls.mx = hints.max_l2;
   } else {
-    ls = scan_lengths(offsets, lengths8, n);
+    ls = scan_lengths(offsets, len_bits == 8 ? lengths : nullptr, n);
   }
-  if (lengths8 && ls.mx > 255) lengths8 = nullptr;
+  if (len_bits == 8 && lengths && ls.mx > 255) lengths = nullptr;
+  if (len_bits == 4 && lengths && (ls.mn < len_base || ls.mx > len_base + 15))
+    throw Error("nibble lengths cannot hold this batch's lengths");
   if (fmt == ResultFormat::R4 && (L1_ > 255 || ls.mx > 255 || table_.max_abs() * ls.mx >= 32767))
     throw Error("result format R4 cannot hold this batch");
   if (fmt == ResultFormat::R8 && (L1_ > 65535 || ls.mx > 65535)) throw Error("result format R8 cannot hold this batch");
+  r2_ = R2Params{};
+  if (fmt == ResultFormat::R2 && !r2_params(L1_, ls.mn, ls.mx, min_t_, max_t_, r2_))
+    throw Error("result format R2 cannot hold this batch");
+  stats_.r2 = r2_;
 
   // ---- direct zero-copy streaming path
   dev::ShortArgs a;
@@ -446,7 +476,7 @@ void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uin
   const bool swipe = dev::configure_swipe(L1_, ls.mn, ls.mx, table_.max_abs(), a);
   // packed letters stream straight into the swipe kernel only; other kernels read unpacked bytes
   if (opt_.allow_direct && (swipe || (!packed5 && dev::configure_short(L1_, ls.mn, ls.mx, a))) &&
-      direct_pointers(codes, offsets, lengths8, n, out, fb, packed5, a)) {
+      direct_pointers(codes, offsets, lengths, len_bits, len_base, n, out, fb, packed5, a)) {
     const dev::ProblemView pv = problem_view(ls.mx);
     MOC_HIP_CHECK(hipEventRecord(ev_a_, s_compute_));
     if (swipe)
@@ -463,7 +493,7 @@ void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uin
     stats_.direct = 1;
     stats_.chunks = 1;
     const int64_t letters = offsets[n] - offsets[0];
-    stats_.h2d_bytes = (packed5 ? (5 * letters + 7) / 8 : letters) + (a.lengths8 ? n : 8 * n);
+    stats_.h2d_bytes = (packed5 ? (5 * letters + 7) / 8 : letters) + (a.lengths4 ? (n + 1) / 2 : a.lengths8 ? n : 8 * n);
     stats_.d2h_bytes = static_cast<int64_t>(fb) * n;
     wall.stop();
     stats_.total_ms = wall.total_ms();
@@ -558,6 +588,7 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
       a.codes = dcodes - offsets[rb];  // base: record i at base + offsets[i] (absolute offsets)
       a.offsets = doffs;
       a.lengths8 = nullptr;
+      a.lengths4 = nullptr;
       a.n = cn;
       a.out = s.d_out;
       a.counter = s.d_counter;

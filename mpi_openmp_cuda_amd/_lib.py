@@ -21,8 +21,11 @@ RESULT_DTYPE = np.dtype([("score", "<i4"), ("n", "<i4"), ("k", "<i4")])
 # Packed result wire formats (moc/device.hpp ResultFormat): index = format id.
 R8_DTYPE = np.dtype([("score", "<i4"), ("n", "<u2"), ("k", "<u2")])
 R4_DTYPE = np.dtype([("score", "<i2"), ("n", "u1"), ("k", "u1")])
-FORMAT_DTYPES = [RESULT_DTYPE, R8_DTYPE, R4_DTYPE]
-FORMAT_NAMES = ["r12", "r8", "r4"]
+# R2: one uint16 per record, (score - smin) * j + n * kw + k, 0xFFFF = no candidate; decoding needs the
+# (smin, kw, j) parameters the engine reports (HipSearchEngine.r2_params / stats()["r2"]).
+R2_DTYPE = np.dtype("<u2")
+FORMAT_DTYPES = [RESULT_DTYPE, R8_DTYPE, R4_DTYPE, R2_DTYPE]
+FORMAT_NAMES = ["r12", "r8", "r4", "r2"]
 
 _lib = None
 
@@ -57,6 +60,8 @@ def _decl(lib):
         "moc_device_count": (c_int, []),
         "moc_host_register": (c_int, [c_void_p, c_size_t]),
         "moc_host_unregister": (c_int, [c_void_p]),
+        "moc_pointer_info": (c_int, [c_void_p, c_size_t, c_void_p]),
+        "moc_pinned_covers": (c_int, [c_void_p, c_size_t]),
         "moc_bind_numa": (c_int, [c_int]),
         "moc_device_numa_node": (c_int, [c_int]),
         "moc_dpp_probe": (c_int, [c_void_p]),
@@ -66,11 +71,12 @@ def _decl(lib):
         "moc_engine_destroy": (None, [c_void_p]),
         "moc_engine_set_problem": (c_int, [c_void_p, P(c_int32), c_void_p, c_int64, c_int]),
         "moc_engine_solve": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
-        "moc_engine_solve_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_int64,
-                                        c_int64, c_int]),
-        "moc_engine_auto_format": (c_int, [c_void_p, c_int64]),
+        "moc_engine_solve_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int64, c_void_p, c_int,
+                                        c_int64, c_int64, c_int]),
+        "moc_engine_auto_format": (c_int, [c_void_p, c_int64, c_int64]),
+        "moc_engine_r2_params": (c_int, [c_void_p, c_int64, c_int64, c_void_p]),
         "moc_engine_pin": (c_int, [c_void_p, c_void_p, c_size_t]),
-        "moc_expand_results": (c_int, [c_void_p, c_int, c_int64, c_void_p]),
+        "moc_expand_results": (c_int, [c_void_p, c_int, c_int64, c_void_p, c_void_p]),
         "moc_engine_solve_device": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
         "moc_engine_stats": (c_int, [c_void_p, P(c_double)]),
         "moc_engine_search_keys": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p]),

@@ -35,6 +35,22 @@ def pack5(codes: np.ndarray, out: np.ndarray = None) -> np.ndarray:
     return out
 
 
+def pack_lengths4(lengths: np.ndarray, base: int, out: np.ndarray = None) -> np.ndarray:
+    """Record lengths in [base, base + 15] -> 4 bits each, two per byte (record i in the low nibble of
+    byte i // 2 when i is even, the high nibble when odd) — the streaming kernels' narrowest length form."""
+    v = np.asarray(lengths).astype(np.int64) - int(base)
+    if v.size and (v.min() < 0 or v.max() > 15):
+        raise ValueError("lengths do not fit 4 bits above the base")
+    n = v.shape[0]
+    if out is None:
+        out = np.empty((n + 1) // 2, dtype=np.uint8)
+    lo = v[0::2].astype(np.uint8)
+    hi = np.zeros_like(lo)
+    hi[: n // 2] = v[1::2].astype(np.uint8)
+    np.bitwise_or(lo, np.left_shift(hi, 4), out=out[: (n + 1) // 2])
+    return out
+
+
 def unpack5(packed: np.ndarray, begin: int, n: int) -> np.ndarray:
     out = np.empty(n, dtype=np.uint8)
     _lib.check(_lib.lib().moc_unpack5(_lib.ptr(np.ascontiguousarray(packed)), int(begin), int(n), _lib.ptr(out)))

@@ -24,9 +24,19 @@ def empty_results(n: int) -> np.ndarray:
     return np.zeros(n, dtype=RESULT_DTYPE)
 
 
-def as_triples(results: np.ndarray) -> np.ndarray:
-    """Results in any wire format (R12/R8/R4 structured, or (n,3) ints) -> (n, 3) int32 [score, n, k]."""
+def as_triples(results: np.ndarray, r2=None) -> np.ndarray:
+    """Results in any wire format (R12/R8/R4 structured, R2 codes with their (smin, kw, j) parameters, or
+    (n,3) ints) -> (n, 3) int32 [score, n, k]."""
     r = np.asarray(results)
+    if r.dtype == _lib.R2_DTYPE:
+        if r2 is None:
+            raise ValueError("R2 results need their (smin, kw, j) parameters")
+        smin, kw, j = (int(v) for v in r2)
+        c = r.astype(np.int64)
+        idx = c % j
+        out = np.stack([c // j + smin, idx // kw, idx % kw], axis=1).astype(np.int32)
+        out[c == 0xFFFF] = (np.iinfo(np.int32).min, 0, 0)
+        return out
     if r.dtype == RESULT_DTYPE:
         return r.view(np.int32).reshape(-1, 3)
     if r.dtype.names:
@@ -154,31 +164,43 @@ class HipSearchEngine:
             if a is not None and a.nbytes:
                 _lib.check(_lib.lib().moc_engine_pin(self._h, ctypes.c_void_p(a.ctypes.data), a.nbytes))
 
-    def auto_format(self, max_l2: int) -> str:
-        return _lib.FORMAT_NAMES[_lib.lib().moc_engine_auto_format(self._h, int(max_l2))]
+    def auto_format(self, max_l2: int, min_l2: int = 0) -> str:
+        """Smallest result format for records of lengths [min_l2, max_l2] (min_l2 = 0: unknown -> no R2)."""
+        return _lib.FORMAT_NAMES[_lib.lib().moc_engine_auto_format(self._h, int(max_l2), int(min_l2))]
+
+    def r2_params(self, min_l2: int, max_l2: int) -> tuple:
+        """(smin, kw, j) of the R2 format for records of lengths [min_l2, max_l2]."""
+        v = np.zeros(3, np.int32)
+        _lib.check(_lib.lib().moc_engine_r2_params(self._h, int(min_l2), int(max_l2), _lib.ptr(v)))
+        return tuple(int(x) for x in v)
 
     def solve(self, codes: np.ndarray, offsets: np.ndarray, out: Optional[np.ndarray] = None,
-              lengths: Optional[np.ndarray] = None, fmt="r12", l2_range=None, packed5: bool = False) -> np.ndarray:
+              lengths: Optional[np.ndarray] = None, fmt="r12", l2_range=None, packed5: bool = False,
+              lengths_bits: int = 8, lengths_base: int = 0) -> np.ndarray:
         """Host CSR -> host results. ``codes[offsets[i]:offsets[i+1]]`` is record i (``offsets`` may be a
-        slice of a larger absolute offset array). ``fmt``: r12 | r8 | r4 | auto (smallest that fits);
-        ``lengths``: optional uint8 record lengths; ``l2_range``: optional known (min, max) length;
-        ``packed5``: ``codes`` is a 5-bit packed stream (models.problem.pack5) instead of bytes."""
+        slice of a larger absolute offset array). ``fmt``: r12 | r8 | r4 | r2 | auto (smallest that fits);
+        ``lengths``: optional narrow record lengths, uint8 (``lengths_bits`` 8) or two per byte
+        (``lengths_bits`` 4, low nibble first, length = ``lengths_base`` + nibble; see pack_lengths4);
+        ``l2_range``: optional known (min, max) length (R2 results are encoded for it: decode with
+        ``r2_params(*l2_range)`` or ``stats()["r2"]``); ``packed5``: ``codes`` is a 5-bit packed stream
+        (models.problem.pack5) instead of bytes."""
         offsets = np.ascontiguousarray(offsets, dtype=np.int64)
         n = offsets.shape[0] - 1
         if l2_range is None and (fmt == "auto"):
             L2 = np.diff(offsets) if n else np.zeros(1, np.int64)
             l2_range = (int(L2.min()) if n else 0, int(L2.max()) if n else 0)
         if fmt == "auto":
-            fmt = self.auto_format(l2_range[1])
+            fmt = self.auto_format(l2_range[1], l2_range[0])
         fid = _format_id(fmt)
         if out is None:
             out = np.empty(n, dtype=_lib.FORMAT_DTYPES[fid])
         assert out.dtype.itemsize == _lib.FORMAT_DTYPES[fid].itemsize and out.size >= n
         if lengths is not None:
-            assert lengths.dtype == np.uint8 and lengths.shape[0] >= n
+            assert lengths.dtype == np.uint8 and lengths.shape[0] >= (n if lengths_bits == 8 else (n + 1) // 2)
         lo, hi = l2_range if l2_range is not None else (-1, -1)
-        _lib.check(_lib.lib().moc_engine_solve_ex(self._h, _lib.ptr(codes), _lib.ptr(offsets), _lib.ptr(lengths), n,
-                                                  _lib.ptr(out), fid, int(lo), int(hi), 1 if packed5 else 0))
+        _lib.check(_lib.lib().moc_engine_solve_ex(self._h, _lib.ptr(codes), _lib.ptr(offsets), _lib.ptr(lengths),
+                                                  int(lengths_bits), int(lengths_base), n, _lib.ptr(out), fid, int(lo),
+                                                  int(hi), 1 if packed5 else 0))
         return out
 
     def solve_device(self, codes_t, offsets_t, h_offsets: np.ndarray, out_t, stream=None):
@@ -238,11 +260,12 @@ class HipSearchEngine:
         return out_t
 
     def stats(self) -> dict:
-        v = (ctypes.c_double * 10)()
+        v = (ctypes.c_double * 13)()
         _lib.check(_lib.lib().moc_engine_stats(self._h, v))
         keys = ["kernel_ms", "total_ms", "h2d_bytes", "d2h_bytes", "chunks", "cells", "records", "direct", "format",
                 "kernels"]
-        d = dict(zip(keys, list(v)))
+        d = dict(zip(keys, list(v)[:10]))
+        d["r2"] = tuple(int(x) for x in list(v)[10:13])
         d["format"] = _lib.FORMAT_NAMES[int(d["format"])]
         d["kernels"] = [k for b, k in ((1, "swipe"), (2, "short"), (4, "tiles")) if int(d["kernels"]) & b]
         return d

@@ -151,7 +151,7 @@ def test_staged_formats(engine, fmt):
     engine.set_problem(prob.weights, prob.seq1)
     got = engine.solve(prob.codes, prob.offsets, fmt=fmt)
     assert engine.stats()["direct"] == 0
-    assert np.array_equal(as_triples(got), as_triples(search_cpu(prob)))
+    assert np.array_equal(as_triples(got, r2=engine.stats()["r2"]), as_triples(search_cpu(prob)))
 
 
 @pytest.mark.parametrize("L1,lo,hi,w", [(26, 6, 11, (4, 3, 2, 10)), (12, 1, 14, (3, 1, 1, 2)),
@@ -168,7 +168,7 @@ def test_swipe_kernel_shapes(engine, L1, lo, hi, w, sem):
     engine.set_problem(prob.weights, prob.seq1, sem)
     got = engine.solve(prob.codes, prob.offsets, fmt="auto")
     kinds = engine.stats()["kernels"]
-    assert np.array_equal(as_triples(got), as_triples(search_cpu(prob, sem))), kinds
+    assert np.array_equal(as_triples(got, r2=engine.stats()["r2"]), as_triples(search_cpu(prob, sem))), kinds
     if L1 - min(lo, hi) + 1 <= 64:
         assert kinds == ["swipe"], kinds
 
@@ -297,3 +297,71 @@ def test_final_cli_zero_copy_window(tmp_path):
     r = run_final(["--backend=hip", "--transport=shm", f"--input={path}", "--timing"], stdin_bytes=b"", np_=1)
     assert r.returncode == 0, r.stderr.decode()
     assert r.stdout.decode() == format_results(search_cpu(prob))
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+@pytest.mark.parametrize("packed", [False, True])
+@pytest.mark.parametrize("shape,n", [("input6", 200_003), ("input1", 3001)])
+def test_r2_results_and_nibble_lengths(pinned, packed, shape, n):
+    # 2-byte results + 4-bit lengths: the narrowest wire formats of the streaming path
+    from mpi_openmp_cuda_amd import _lib
+    from mpi_openmp_cuda_amd.models.problem import pack5, pack_lengths4
+    from mpi_openmp_cuda_amd.utils.synthetic import SHAPES
+
+    sh = SHAPES[shape]
+    prob = make_synthetic(shape, n, seed=n)
+    eng = HipSearchEngine(device=0)
+    eng.set_problem(prob.weights, prob.seq1)
+    fmt = eng.auto_format(sh.l2_max, sh.l2_min)
+    if shape == "input6":
+        assert fmt == "r2"
+    if fmt != "r2":
+        pytest.skip(f"{shape}: R2 does not fit ({fmt})")
+    codes = pack5(prob.codes) if packed else prob.codes
+    lengths = pack_lengths4(np.diff(prob.offsets), sh.l2_min)
+    out = np.zeros(prob.n, dtype=_lib.R2_DTYPE)
+    if pinned:
+        eng.pin(codes, prob.offsets, out, lengths)
+    eng.solve(codes, prob.offsets, out=out, lengths=lengths, lengths_bits=4, lengths_base=sh.l2_min, fmt="r2",
+              l2_range=(sh.l2_min, sh.l2_max), packed5=packed)
+    st = eng.stats()
+    assert st["r2"] == eng.r2_params(sh.l2_min, sh.l2_max)
+    assert np.array_equal(as_triples(out, r2=st["r2"]), as_triples(search_cpu(prob))), st
+    if pinned and shape == "input6":
+        assert st["direct"] == 1
+    eng.close()
+
+
+@pytest.mark.parametrize("L1,lo,hi,kernel", [(90, 3, 11, "tiles"), (40, 33, 38, "short")])
+def test_r2_tiles_and_short_kernels(engine, L1, lo, hi, kernel):
+    # R2 through the tile kernel's finalize and the lane/offset kernel (staged path)
+    rng = np.random.default_rng(5)
+    s1 = "".join(chr(65 + x) for x in rng.integers(0, 26, L1))
+    recs = ["".join(chr(65 + x) for x in rng.integers(0, 26, rng.integers(lo, hi + 1))) for _ in range(501)]
+    prob = Problem.from_strings([2, 1, 1, 1], s1, recs)
+    engine.set_problem(prob.weights, prob.seq1)
+    L2 = np.diff(prob.offsets)
+    rng2 = (int(L2.min()), int(L2.max()))
+    assert engine.auto_format(rng2[1], rng2[0]) == "r2"
+    got = engine.solve(prob.codes, prob.offsets, fmt="r2", l2_range=rng2)
+    assert engine.stats()["kernels"] == [kernel]
+    assert np.array_equal(as_triples(got, r2=engine.stats()["r2"]), as_triples(search_cpu(prob)))
+
+
+def test_pinned_registry_neighbours():
+    # arrays sharing pages: every page is locked exactly once, coverage is exact, release is clean
+    from mpi_openmp_cuda_amd import _lib
+
+    L = _lib.lib()
+    bufs = [np.zeros(3000 + 1000 * i, np.uint8) for i in range(6)]  # small heap arrays: shared pages
+    e1, e2 = HipSearchEngine(device=0), HipSearchEngine(device=0)
+    e1.pin(bufs[0], bufs[2], bufs[4])
+    for i, b in enumerate(bufs):
+        if i % 2 == 0:
+            assert L.moc_pinned_covers(_lib.ptr(b), b.nbytes) == 1
+    e2.pin(*bufs)  # overlaps e1's pages: only the missing pages get registered
+    assert all(L.moc_pinned_covers(_lib.ptr(b), b.nbytes) == 1 for b in bufs)
+    e2.close()
+    assert all(L.moc_pinned_covers(_lib.ptr(bufs[i]), bufs[i].nbytes) == 1 for i in (0, 2, 4))
+    e1.close()
+    assert not any(L.moc_pinned_covers(_lib.ptr(b), b.nbytes) for b in bufs)

@@ -106,3 +106,36 @@ def test_roundtrip_text():
     p = Problem.from_strings([4, 3, 2, 10], "ABCDEFGHIJKLMNOPQRSTUVWXYZ", ["ABCDEF", "MNOPQRSTXXX"])
     q = Problem.parse(p.to_text())
     assert np.array_equal(p.codes, q.codes) and np.array_equal(p.offsets, q.offsets)
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 7, 1000])
+def test_pack_lengths4(n):
+    from mpi_openmp_cuda_amd.models.problem import pack_lengths4
+
+    rng = np.random.default_rng(n)
+    L = rng.integers(6, 22, n)
+    p = pack_lengths4(L, 6)
+    assert p.shape[0] == (n + 1) // 2
+    got = np.empty(n, np.int64)
+    got[0::2] = (p & 15)[: (n + 1) // 2] + 6
+    got[1::2] = (p >> 4)[: n // 2] + 6
+    assert np.array_equal(got, L)
+    with pytest.raises(ValueError):
+        pack_lengths4(np.array([5, 30]), 6)
+
+
+def test_r2_decode_python_and_native():
+    # R2 code = (score - smin) * j + n * kw + k, 0xFFFF = none; python and native decoders agree
+    from mpi_openmp_cuda_amd import _lib
+    from mpi_openmp_cuda_amd.ops.align import as_triples
+
+    smin, kw, j = -110, 11, 231
+    trip = np.array([[-110, 0, 0], [44, 20, 10], [3, 7, 2], [-2**31, 0, 0]], np.int32)
+    codes = np.array([(s - smin) * j + n * kw + k if s != -2**31 else 0xFFFF for s, n, k in trip], np.uint16)
+    assert np.array_equal(as_triples(codes, r2=(smin, kw, j)), trip)
+    out = np.empty(len(codes), _lib.RESULT_DTYPE)
+    prm = np.array([smin, kw, j], np.int32)
+    _lib.check(_lib.lib().moc_expand_results(_lib.ptr(codes), 3, len(codes), _lib.ptr(prm), _lib.ptr(out)))
+    assert np.array_equal(as_triples(out), trip)
+    with pytest.raises(ValueError):
+        as_triples(codes)
