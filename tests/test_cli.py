@@ -148,3 +148,26 @@ def test_timing_json_has_throughput():
     t = json.loads(r.stderr.decode().strip().splitlines()[-1])
     assert t["records"] == 10 and t["batches"] == 4 and t["cells"] > 0 and t["cells_per_s"] > 0
     assert set(t["timing"]) >= {"parse_ms", "bcast_ms", "distribute_ms", "compute_ms", "gather_ms", "print_ms"}
+
+
+def test_cmake_build_matches(tmp_path):
+    # the CMake build produces a working ./final and libmoc.so
+    import shutil
+
+    if not shutil.which("cmake") or not shutil.which("ninja"):
+        pytest.skip("cmake/ninja not available")
+    import os
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    bdir = tmp_path / "cm"
+    r = subprocess.run(["cmake", "-S", root, "-B", str(bdir), "-G", "Ninja"], capture_output=True, timeout=300)
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    r = subprocess.run(["cmake", "--build", str(bdir), "-j", "8", "--target", "final"], capture_output=True,
+                       timeout=900)
+    assert r.returncode == 0, r.stdout.decode()[-2000:]
+    from conftest import MPIEXEC
+
+    with open(input_path(4), "rb") as f:
+        out = subprocess.run([MPIEXEC, "-np", "2", str(bdir / "final"), "--backend=cpu"], input=f.read(),
+                             capture_output=True, timeout=120)
+    assert out.returncode == 0 and out.stdout.decode() == expected(4)
