@@ -25,6 +25,8 @@ def main(argv=None) -> int:
     ap.add_argument("--input", default="-", help="input file (default: stdin)")
     ap.add_argument("--backend", default="auto", choices=["auto", "hip", "cpu"])
     ap.add_argument("--transport", default="auto", choices=["auto", "shm", "p2p"])
+    ap.add_argument("--partition", default="records", choices=["records", "offsets"],
+                    help="records: cost-balanced record ranges; offsets: context parallel (split every record)")
     ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"])
     ap.add_argument("--semantics", default="reference", choices=["reference", "spec"])
     ap.add_argument("--threads", type=int, default=0)
@@ -53,7 +55,8 @@ def main(argv=None) -> int:
             print(f"input error: {err}", file=sys.stderr)
         D.finalize(ctx)
         return 1
-    search = DistributedSearch(ctx, backend="hip" if use_gpu else "cpu", transport=a.transport, threads=a.threads)
+    search = DistributedSearch(ctx, backend="hip" if use_gpu else "cpu", transport=a.transport, threads=a.threads,
+                               partition=a.partition)
     results = search.run(problem, Semantics.parse(a.semantics))
     if ctx.is_root:
         write_results(results)

@@ -137,3 +137,16 @@ def allreduce_max(ctx: DistContext, x: float) -> float:
     t = torch.tensor([x], dtype=torch.float64, device=ctx.device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def allreduce_max_int64(ctx: DistContext, arr: np.ndarray) -> np.ndarray:
+    """Element-wise MAX of an int64 array over all ranks (RCCL on GPU ranks, gloo on CPU)."""
+    import torch
+    import torch.distributed as dist
+
+    arr = np.ascontiguousarray(arr, dtype=np.int64)
+    if not ctx.distributed or arr.size == 0:
+        return arr
+    t = torch.from_numpy(arr.copy()).to(ctx.device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.cpu().numpy()

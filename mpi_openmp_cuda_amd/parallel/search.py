@@ -10,6 +10,9 @@ Gather x3, root prints. Here:
     (single node);
   * transport "p2p": root sends every rank its slice (lengths + letters) with point-to-point
     send/recv over the process group (RCCL over xGMI / network on GPUs) and receives the results back.
+  * partition "offsets" (context parallel): every rank sees every record and searches its
+    share of each record's offsets; the packed 64-bit candidate keys are combined with ONE MAX all-reduce
+    (the Reduce the reference never had) and the root decodes them.
 """
 from __future__ import annotations
 
@@ -22,7 +25,8 @@ import numpy as np
 from .. import _lib
 from ..models.problem import Problem
 from ..models.scoring import Semantics
-from ..ops.align import HipSearchEngine, device_count, empty_results, search_cpu
+from ..ops.align import (HipSearchEngine, decode_keys, device_count, empty_results, keys_to_ordered_int64,
+                        ordered_int64_to_keys, search_cpu, search_keys_cpu)
 from ..utils.timer import PhaseTimer
 from . import dist as D
 from .partition import CPU_COST, GPU_COST, partition
@@ -54,8 +58,11 @@ class NodeWindow:
 
 class DistributedSearch:
     def __init__(self, ctx: D.DistContext, backend: str = "auto", transport: str = "auto", threads: int = 0,
-                 device: Optional[int] = None):
+                 device: Optional[int] = None, partition: str = "records"):
         self.ctx = ctx
+        if partition not in ("records", "offsets"):
+            raise ValueError("partition must be records|offsets")
+        self.partition = partition
         if backend == "auto":
             backend = "hip" if device_count() > 0 else "cpu"
         self.backend = backend
@@ -67,6 +74,11 @@ class DistributedSearch:
         self.threads = threads
         self.engine = HipSearchEngine(ctx.local_rank if device is None else device) if backend == "hip" else None
         self.timer = PhaseTimer()
+        if partition == "offsets" and ctx.distributed:
+            # GPU ranks split tile lists, CPU ranks offset ranges: one engine kind for the whole group
+            kinds = D.allreduce_max_int64(ctx, np.array([1 if self.engine else 0, 0 if self.engine else 1]))
+            if kinds[0] and kinds[1]:
+                raise ValueError("partition=offsets needs the same backend on every rank")
 
     def _compute(self, prob: Problem, sem: Semantics, codes, offsets, out):
         if self.engine is not None:
@@ -94,6 +106,8 @@ class DistributedSearch:
                 if ctx.is_root else None
             bounds = D.bcast_array(ctx, bounds, ctx.world + 1, np.int64)
         b, e = int(bounds[ctx.rank]), int(bounds[ctx.rank + 1])
+        if self.partition == "offsets":
+            return self._run_offsets(problem, prob, sem, n, total)
         if self.transport == "shm":
             return self._run_shm(problem, prob, sem, n, total, b, e)
         return self._run_p2p(problem, prob, sem, n, bounds, b, e)
@@ -157,3 +171,41 @@ class DistributedSearch:
             if e > b:
                 D.send_array(ctx, mine.view(np.int32), 0)
             return None
+
+    def _keys(self, prob: Problem, sem: Semantics, codes, offsets) -> np.ndarray:
+        if self.engine is not None:
+            return self.engine.search_keys(codes, offsets, self.ctx.rank, self.ctx.world)
+        sub = Problem(prob.weights, prob.seq1, codes[offsets[0]:offsets[-1]], offsets - offsets[0])
+        return search_keys_cpu(sub, self.ctx.rank, self.ctx.world, sem, self.threads)
+
+    def _run_offsets(self, problem, prob, sem, n, total):
+        ctx, T = self.ctx, self.timer
+        with T.phase("distribute"):  # every rank needs every record
+            if self.transport == "shm":
+                name_arr = None
+                if ctx.is_root:
+                    name_arr = np.frombuffer(f"moc_win_{uuid.uuid4().hex[:12]}".encode(), np.uint8)
+                name = bytes(D.bcast_array(ctx, name_arr, 20, np.uint8)).decode()
+                win = None
+                if ctx.is_root:
+                    win = NodeWindow(name, n, total, create=True)
+                    win.offsets[:] = problem.offsets
+                    win.codes[:] = problem.codes
+                    win._mm.flush()
+                D.barrier(ctx)
+                if not ctx.is_root:
+                    win = NodeWindow(name, n, total, create=False)
+                codes, offsets = win.codes, win.offsets
+            else:
+                win = None
+                offsets = D.bcast_array(ctx, problem.offsets if ctx.is_root else None, n + 1, np.int64)
+                codes = D.bcast_array(ctx, problem.codes if ctx.is_root else None, total, np.uint8)
+        with T.phase("compute"):
+            keys = self._keys(prob, sem, np.asarray(codes), np.asarray(offsets)) if n else np.zeros(0, np.uint64)
+        with T.phase("gather"):
+            best = ordered_int64_to_keys(D.allreduce_max_int64(ctx, keys_to_ordered_int64(keys)))
+            out = decode_keys(best, np.asarray(offsets)) if ctx.is_root else None
+            if win is not None:
+                D.barrier(ctx)
+                win.close(unlink=ctx.is_root)
+        return out

@@ -28,6 +28,16 @@ def test_gloo_goldens(transport, i, nproc):
     assert r.stdout.decode() == expected(i)
 
 
+@pytest.mark.parametrize("transport", ["shm", "p2p"])
+@pytest.mark.parametrize("i,nproc", [(3, 2), (2, 3), (4, 2)])
+def test_gloo_context_parallel(transport, i, nproc):
+    # --partition=offsets: every rank searches a share of every record; MAX all-reduce of packed keys
+    r = torchrun(nproc, ["--backend=cpu", "--dist-backend=gloo", f"--transport={transport}", "--partition=offsets",
+                         f"--input={input_path(i)}"])
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    assert r.stdout.decode() == expected(i)
+
+
 def test_single_process_cli_stdin():
     with open(input_path(1), "rb") as f:
         r = subprocess.run([sys.executable, "-m", "mpi_openmp_cuda_amd", "--backend=cpu"], stdin=f,
