@@ -41,7 +41,7 @@ HIP_OBJS  := $(patsubst csrc/src/%.hip,$(OBJ)/%.o,$(HIP_SRCS))
 COMM_OBJS := $(patsubst csrc/src/%.cpp,$(OBJ)/%.o,$(COMM_SRCS))
 HEADERS   := $(shell find csrc/include -name '*.h' -o -name '*.hpp')
 
-.PHONY: all build lib clean run runOn2 test asan tsan debug-kernels
+.PHONY: all build lib clean run runOn2 test unit asan tsan debug-kernels
 
 all: build
 build: lib final
@@ -127,5 +127,12 @@ run: build
 runOn2: build
 	$(MPI_HOME)/bin/mpiexec -np 2 -machinefile mf --map-by node ./final < $(INPUT)
 
-test:
+test: unit
 	python -m pytest tests/ -x -q -m "not gpu"
+
+# native unit tests of the host core (no GPU, no MPI)
+$(BUILD)/test_core: csrc/tests/test_core.cpp $(CORE_OBJS) $(HIP_OBJS) $(HEADERS)
+	$(CXX) $(CXXFLAGS) -o $@ csrc/tests/test_core.cpp $(CORE_OBJS) $(HIP_OBJS) $(LDROCM)
+
+unit: $(BUILD)/test_core
+	$(BUILD)/test_core

@@ -1,0 +1,209 @@
+// Native unit tests of the host core (SURVEY.md §4.3 "unit (C++)"): score table vs the spec groups,
+// parser and streaming reader edge cases, partitioner, packed-key ordering, 5-bit packing, CPU engine vs
+// the brute-force replay of the reference loops. No GPU, no MPI. Run: `make unit` or `ctest`.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "moc/cpu_engine.hpp"
+#include "moc/io.hpp"
+#include "moc/partition.hpp"
+#include "moc/problem.hpp"
+#include "moc/score_table.hpp"
+
+using namespace moc;
+
+namespace {
+int g_failed = 0, g_checks = 0;
+
+#define CHECK(cond)                                                              \
+  do {                                                                           \
+    ++g_checks;                                                                  \
+    if (!(cond)) {                                                               \
+      ++g_failed;                                                                \
+      std::fprintf(stderr, "%s:%d: CHECK failed: %s\n", __FILE__, __LINE__, #cond); \
+    }                                                                            \
+  } while (0)
+
+template <typename F>
+bool throws(F f, const char* needle) {
+  try {
+    f();
+  } catch (const Error& e) {
+    return std::strstr(e.what(), needle) != nullptr;
+  }
+  return false;
+}
+
+bool in_any_group(const std::vector<std::string>& groups, char a, char b) {
+  for (const auto& g : groups)
+    if (g.find(a) != std::string::npos && g.find(b) != std::string::npos) return true;
+  return false;
+}
+
+void test_score_table() {
+  const Weights w{{10, 2, 3, 4}};
+  const ScoreTable t = ScoreTable::build(w);
+  for (char a = 'A'; a <= 'Z'; ++a)
+    for (char b = 'A'; b <= 'Z'; ++b) {
+      const int x = a - 'A' + 1, y = b - 'A' + 1;
+      PairClass want = kSpace;
+      if (a == b) want = kDollar;
+      else if (in_any_group(first_type_groups(), a, b)) want = kPercent;
+      else if (in_any_group(second_type_groups(), a, b)) want = kHash;
+      CHECK(t.pair_class(x, y) == want);
+      CHECK(t.pair_class(x, y) == t.pair_class(y, x));
+      const int32_t s = t.lut[x * kLutStride + y];
+      CHECK(s == (want == kDollar ? 10 : want == kPercent ? -2 : want == kHash ? -3 : -4));
+    }
+  CHECK(t.max_abs() == 10);
+}
+
+void test_parser() {
+  const std::string text = "10 2 3 4\r\napqrsbatav\r\n  2\r\n asqreavsl \r\n\tHELLO\r\nEXTRA\n";
+  Problem p = parse_problem(text.data(), text.size());
+  CHECK(p.weights.w[0] == 10 && p.weights.w[3] == 4);
+  CHECK(p.L1() == 10 && p.seq2.size() == 2);
+  CHECK(p.seq2.length(0) == 9 && p.seq2.length(1) == 5);
+  CHECK(p.seq2.record(1)[0] == letter_code('H'));
+  CHECK(throws([] { parse_problem("1 2 3", 5); }, "W4"));
+  CHECK(throws([] { std::string s = "1 2 3 4\nAB1C\n1\nAB\n"; parse_problem(s.data(), s.size()); }, "non-letter"));
+  CHECK(throws([] { std::string s = "1 2 3 4\nABC\n3\nAB\nCD\n"; parse_problem(s.data(), s.size()); }, "expected 3"));
+  CHECK(throws([] { std::string s = "1 -2 3 4\nABC\n1\nAB\n"; parse_problem(s.data(), s.size()); }, "out of range"));
+  ParseOptions lim;
+  lim.max_l2 = 3;
+  CHECK(throws([&] { std::string s = "1 2 3 4\nABCDE\n1\nABCD\n"; parse_problem(s.data(), s.size(), lim); },
+               "limit is 3"));
+  std::string empty = "1 1 1 1\nABCD\n0\n";
+  CHECK(parse_problem(empty.data(), empty.size()).seq2.size() == 0);
+}
+
+void test_stream_reader() {
+  // records spanning refills of a tiny buffer, batches, skip, limits
+  std::string text = "4 3 2 10\nABCDEFGHIJKLMNOPQRSTUVWXYZ\n7\n";
+  std::vector<std::string> recs = {"ABCDEF", "xyz", "QRSTUVWXYZAB", "M", "LONGERRECORDABCDEFGHIJ", "AA", "ZZZ"};
+  for (auto& r : recs) text += r + "\n";
+  FILE* f = fmemopen(text.data(), text.size(), "rb");
+  StreamReader rd(f, {}, 4096);
+  CHECK(rd.count() == 7 && rd.seq1().size() == 26 && rd.weights().w[3] == 10);
+  CHECK(rd.skip(1) == 1 && rd.next_index() == 1);
+  RecordBatch b;
+  CHECK(rd.next_batch(2, b) == 2);
+  CHECK(b.size() == 2 && b.length(0) == 3 && b.length(1) == 12 && b.record(0)[0] == letter_code('X'));
+  CHECK(rd.next_batch(100, b, 10) == 2);  // letter cap: stops after the batch reaches 10 letters
+  CHECK(b.length(0) == 1 && b.length(1) == 22);
+  CHECK(rd.next_batch(100, b) == 2);
+  CHECK(rd.next_batch(100, b) == 0);
+  std::fclose(f);
+  std::string bad = "1 1 1 1\nABC\n3\nAB\nA1\nC\n";
+  FILE* g = fmemopen(bad.data(), bad.size(), "rb");
+  StreamReader rb(g);
+  RecordBatch x;
+  CHECK(rb.next_batch(1, x) == 1);
+  CHECK(throws([&] { rb.next_batch(5, x); }, "record #1"));
+  std::fclose(g);
+}
+
+void test_partition() {
+  std::vector<int64_t> len = {10, 20, 5, 7, 1000, 3, 3, 3};
+  for (int p : {1, 2, 3, 8, 13}) {
+    auto b = partition_by_cost(len.data(), static_cast<int64_t>(len.size()), 1200, p);
+    CHECK(static_cast<int>(b.size()) == p + 1 && b.front() == 0 && b.back() == static_cast<int64_t>(len.size()));
+    for (int r = 0; r < p; ++r) CHECK(b[r] <= b[r + 1]);
+    auto e = partition_even(static_cast<int64_t>(len.size()), p);
+    CHECK(e.back() == static_cast<int64_t>(len.size()));
+  }
+  auto z = partition_by_cost(nullptr, 0, 10, 4);
+  CHECK(z.size() == 5 && z.back() == 0);
+}
+
+void test_keys() {
+  // higher score wins; then the smaller offset; then the smaller k (k = 0 first)
+  const int64_t L2 = 7;
+  const uint64_t a = encode_key(Result{5, 2, 3}, L2), b = encode_key(Result{5, 2, 4}, L2),
+                 c = encode_key(Result{5, 1, 6}, L2), d = encode_key(Result{6, 9, 6}, L2),
+                 e = encode_key(Result{-100, 0, 0}, L2);
+  CHECK(a > b && c > a && d > c && e < a && e > 0);
+  CHECK(encode_key(no_candidate(), L2) == 0);
+  for (const Result& r : {Result{5, 2, 3}, Result{-7, 0, 0}, Result{123456, 999, 6}}) {
+    const Result q = decode_key(encode_key(r, L2), L2);
+    CHECK(q.score == r.score && q.n == r.n && q.k == r.k);
+  }
+  const Result none = decode_key(0, L2);
+  CHECK(none.score == kNoCandidateScore && none.n == 0 && none.k == 0);
+}
+
+void test_pack5() {
+  std::mt19937 rng(1);
+  for (int64_t n : {0, 1, 7, 8, 9, 1000, 70000}) {
+    std::vector<uint8_t> c(static_cast<size_t>(n));
+    for (auto& x : c) x = static_cast<uint8_t>(1 + rng() % 26);
+    std::vector<uint8_t> p(static_cast<size_t>(packed5_bytes(n)));
+    pack5(c.data(), n, p.data());
+    std::vector<uint8_t> u(static_cast<size_t>(n));
+    unpack5(p.data(), 0, n, u.data());
+    CHECK(u == c);
+  }
+}
+
+void test_engine_vs_brute_force() {
+  std::mt19937 rng(7);
+  for (int trial = 0; trial < 60; ++trial) {
+    const int64_t L1 = 1 + rng() % 40;
+    Weights w{{static_cast<int32_t>(rng() % 12), static_cast<int32_t>(rng() % 12), static_cast<int32_t>(rng() % 12),
+               static_cast<int32_t>(rng() % 12)}};
+    const ScoreTable t = ScoreTable::build(w);
+    std::vector<uint8_t> s1(static_cast<size_t>(L1));
+    for (auto& x : s1) x = static_cast<uint8_t>(1 + rng() % 26);
+    RecordBatch batch;
+    for (int r = 0; r < 12; ++r) {
+      const int64_t L2 = 1 + rng() % (L1 + 2);
+      std::vector<uint8_t> s2(static_cast<size_t>(L2));
+      for (auto& x : s2) x = static_cast<uint8_t>(1 + rng() % 26);
+      batch.push_back(s2.data(), L2);
+    }
+    for (Semantics sem : {Semantics::Reference, Semantics::Spec}) {
+      std::vector<Result> out(static_cast<size_t>(batch.size()));
+      solve_batch_cpu(t, s1.data(), L1, batch, out.data(), sem, 2);
+      for (int64_t i = 0; i < batch.size(); ++i) {
+        const Result bf = brute_force_record(t, s1.data(), L1, batch.record(i), batch.length(i), sem);
+        CHECK(out[i].score == bf.score && out[i].n == bf.n && out[i].k == bf.k);
+      }
+      // context-parallel shares combine to the same answers
+      std::vector<uint64_t> keys(static_cast<size_t>(batch.size()), 0), part(keys.size());
+      for (int p = 0; p < 3; ++p) {
+        solve_keys_cpu(t, s1.data(), L1, batch, p, 3, part.data(), sem, 2);
+        for (size_t i = 0; i < keys.size(); ++i) keys[i] = std::max(keys[i], part[i]);
+      }
+      for (int64_t i = 0; i < batch.size(); ++i) {
+        const Result r = decode_key(keys[i], batch.length(i));
+        CHECK(r.score == out[i].score && r.n == out[i].n && r.k == out[i].k);
+      }
+    }
+  }
+}
+
+void test_formatter() {
+  const Result r[3] = {{1, 2, 3}, {kNoCandidateScore, 0, 0}, {-5, 10, 0}};
+  CHECK(format_results(r, 3, 7) == "#7: score: 1, n: 2, k: 3\n#8: score: -2147483648, n: 0, k: 0\n"
+                                   "#9: score: -5, n: 10, k: 0\n");
+}
+}  // namespace
+
+int main() {
+  const std::vector<std::pair<const char*, std::function<void()>>> tests = {
+      {"score_table", test_score_table}, {"parser", test_parser},     {"stream_reader", test_stream_reader},
+      {"partition", test_partition},     {"keys", test_keys},         {"pack5", test_pack5},
+      {"engine_vs_brute_force", test_engine_vs_brute_force},          {"formatter", test_formatter}};
+  for (const auto& t : tests) {
+    const int before = g_failed;
+    t.second();
+    std::printf("%-24s %s\n", t.first, g_failed == before ? "ok" : "FAILED");
+  }
+  std::printf("%d checks, %d failed\n", g_checks, g_failed);
+  return g_failed ? 1 : 0;
+}
