@@ -30,6 +30,7 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kMaxTile = 1024;
 constexpr int kLdsBudget = 60 * 1024;
+constexpr int kMaxV = 4;  // 16-byte letter vectors per thread per tile (register prefetch)
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
@@ -91,30 +92,82 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
   const int64_t n_tiles = (a.n + a.tile_records - 1) / a.tile_records;
   const int sem = pv.semantics;
 
-  for (;;) {
-    __syncthreads();
-    if (tid == 0) misc[0] = static_cast<int>(atomicAdd(a.counter, 1u));
-    __syncthreads();
-    const int64_t t = misc[0];
-    if (t >= n_tiles) break;
-    const int64_t rb = t * a.tile_records;
-    const int m = static_cast<int>(min(static_cast<int64_t>(a.tile_records), a.n - rb));
-    const int64_t start = a.offsets[rb];
-    const int64_t end = a.offsets[rb + m];
-
-    // ---- lengths -> block exclusive scan -> loff[0..m]
+  // ---- tile fetch: the next tile's lengths and letters are loaded into registers while the current
+  //      tile is being scored, so the PCIe / HBM read latency hides behind the compute (the streaming
+  //      path is bound by host-link bytes: keep the link busy all the time).
+  struct Fetch {
+    int64_t t, rb, start, end;
+    int m;
     int len4[4];
-    int sum = 0;
+    uintptr_t a0;
+    int nvec;
+    uint4 v[kMaxV];
+  };
+  auto fetch = [&](int64_t t, Fetch& f) {
+    f.t = t;
+    f.rb = f.start = f.end = 0;
+    f.m = f.nvec = 0;
+    f.a0 = 0;
+#pragma unroll
+    for (int k = 0; k < kMaxV; ++k) f.v[k] = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) f.len4[q] = 0;
+    if (t >= n_tiles) return;
+    f.rb = t * a.tile_records;
+    f.m = static_cast<int>(min(static_cast<int64_t>(a.tile_records), a.n - f.rb));
+    f.start = a.offsets[f.rb];
+    f.end = a.offsets[f.rb + f.m];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = tid * 4 + q;
-      int L = 0;
-      if (r < m) L = record_length(a, rb + r);
-      len4[q] = L;
-      sum += L;
+      f.len4[q] = r < f.m ? record_length(a, f.rb + r) : 0;
     }
+    const int64_t b_first = P5 ? (5 * f.start) >> 3 : f.start;
+    const int64_t b_end = P5 ? (5 * f.end + 7) >> 3 : f.end;
+    f.a0 = reinterpret_cast<uintptr_t>(a.codes + b_first) & ~uintptr_t{15};
+    f.nvec = static_cast<int>((reinterpret_cast<uintptr_t>(a.codes + b_end) + 15 - f.a0) >> 4);
+    MOC_DCHECK(f.nvec <= kMaxV * kBlock);
+#pragma unroll
+    for (int k = 0; k < kMaxV; ++k) {
+      const int v = tid + k * kBlock;
+      if (v < f.nvec) f.v[k] = reinterpret_cast<const uint4*>(f.a0)[v];
+    }
+  };
+  auto grab = [&]() -> int64_t {
+    if (tid == 0) misc[0] = static_cast<int>(atomicAdd(a.counter, 1u));
+    __syncthreads();
+    const int64_t t = misc[0];
+    __syncthreads();  // misc[0] is reused by the next grab
+    return t;
+  };
+
+  Fetch cur, nxt;
+  fetch(grab(), cur);
+  for (;;) {
+    if (cur.t >= n_tiles) break;
+    const int64_t rb = cur.rb, start = cur.start, end = cur.end;
+    const int m = cur.m;
+    __syncthreads();  // the previous tile's LDS (loff, letters, results) is free again
+
+    // ---- lengths -> block exclusive scan -> loff[0..m]
+    int sum = cur.len4[0] + cur.len4[1] + cur.len4[2] + cur.len4[3];
     const int incl = wave_inclusive_sum(sum, lane);
     if (lane == 63) misc[4 + wave] = incl;
+    // ---- letters -> LDS. Byte codes: char j at byte j. Packed: char j at bit 5j.
+    //      shift_b = position (bytes, or bits when P5) of the tile's first char inside the LDS copy.
+#pragma unroll
+    for (int k = 0; k < kMaxV; ++k) {
+      const int v = tid + k * kBlock;
+      if (v < cur.nvec) reinterpret_cast<uint4*>(codes_l)[v] = cur.v[k];
+    }
+    const uintptr_t p0 = reinterpret_cast<uintptr_t>(a.codes + (P5 ? (5 * start) >> 3 : start));
+    const int shift_b = P5 ? static_cast<int>(8 * (p0 - cur.a0) + ((5 * start) & 7)) : static_cast<int>(p0 - cur.a0);
+    if (tid == 0) {
+      MOC_DCHECK(a.dbg_codes_end < 0 || cur.a0 + 16 * static_cast<uintptr_t>(cur.nvec) <=
+                                            reinterpret_cast<uintptr_t>(a.codes) + a.dbg_codes_end);
+      MOC_DCHECK(end >= start && m > 0 && m <= a.tile_records);
+      MOC_DCHECK((P5 ? (5 * (end - start) + 7) / 8 + 32 : end - start + 32) <= a.codes_cap);
+    }
     __syncthreads();
     int excl = incl - sum;
     for (int w = 0; w < wave; ++w) excl += misc[4 + w];
@@ -122,30 +175,14 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
     for (int q = 0; q < 4; ++q) {
       const int r = tid * 4 + q;
       if (r < m) loff[r] = excl;
-      excl += len4[q];
+      excl += cur.len4[q];
     }
     if (tid == kBlock - 1) {
       loff[m] = excl;
       MOC_DCHECK(excl == end - start);  // lengths agree with offsets
     }
-
-    // ---- letters -> LDS (16-byte loads). Byte codes: char j at byte j. Packed: char j at bit 5j.
-    //      shift_b = position (bytes, or bits when P5) of the tile's first char inside the LDS copy.
-    const int64_t b_first = P5 ? (5 * start) >> 3 : start;
-    const int64_t b_end = P5 ? (5 * end + 7) >> 3 : end;
-    const uintptr_t p0 = reinterpret_cast<uintptr_t>(a.codes + b_first);
-    const uintptr_t a0 = p0 & ~uintptr_t{15};
-    const int shift_b = P5 ? static_cast<int>(8 * (p0 - a0) + ((5 * start) & 7)) : static_cast<int>(p0 - a0);
-    const int nvec = static_cast<int>((reinterpret_cast<uintptr_t>(a.codes + b_end) + 15 - a0) >> 4);
-    if (tid == 0) {
-      MOC_DCHECK(a.dbg_codes_end < 0 || a0 + 16 * static_cast<uintptr_t>(nvec) <=
-                                            reinterpret_cast<uintptr_t>(a.codes) + a.dbg_codes_end);
-      MOC_DCHECK(end >= start && m > 0 && m <= a.tile_records);
-      MOC_DCHECK((P5 ? (5 * (end - start) + 7) / 8 + 32 : end - start + 32) <= a.codes_cap);
-    }
-    for (int v = tid; v < nvec; v += kBlock)
-      reinterpret_cast<uint4*>(codes_l)[v] = reinterpret_cast<const uint4*>(a0)[v];
-    __syncthreads();
+    // next tile: its loads are in flight while this one is scored
+    fetch(grab(), nxt);  // grab() synchronises: loff / letters are complete
 
     // ---- one record per lane
     for (int g = wave; g * 64 < m; g += 4) {
@@ -256,6 +293,7 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
     }
     __syncthreads();
     copy_results(static_cast<char*>(a.out) + rb * fb, res_l, m * fb, tid, kBlock);
+    cur = nxt;
   }
 }
 
@@ -287,6 +325,7 @@ bool configure_swipe(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs
   const int fb = result_bytes(static_cast<ResultFormat>(a.fmt));
   for (int tr = kMaxTile; tr >= 64; tr /= 2) {
     const int cap = tr * static_cast<int>(std::max<int64_t>(max_l2, 1)) + 64;
+    if (cap + 32 > kMaxV * kBlock * 16) continue;  // a tile's letters must fit the register prefetch
     SwipeLayout l = swipe_layout(static_cast<int>(L1), ch.noff, ch.l2w, tr, cap, fb);
     if (l.total <= kLdsBudget) {
       a.tile_records = tr;
