@@ -50,7 +50,8 @@ namespace {
 
 const char* kUsage =
     "usage: mpiexec -np N ./final [options] < input.txt\n"
-    "  --backend=auto|hip|cpu      compute engine (auto: hip when a GPU is visible)\n"
+    "  --backend=auto|hip|cpu      compute engine (auto: hip when a GPU is visible and the job has\n"
+    "                              >= --gpu-min-cells cells per rank, default 3e8; else the OpenMP engine)\n"
     "  --transport=auto|shm|rccl|mpi   record distribution (auto: shm on one node, else rccl/mpi)\n"
     "  --semantics=reference|spec  candidate set (spec adds the un-mutated final offset, bug B8)\n"
     "  --partition=cost|even|offsets   rank decomposition (offsets: split every record's offset range)\n"
@@ -71,7 +72,7 @@ const char* kUsage =
     "every flag can also be given as environment variable MOC_<FLAG> (e.g. MOC_BACKEND=cpu)\n";
 
 const std::vector<std::string> kKnown = {
-    "backend", "transport", "semantics", "partition", "batch-records", "batch-chars", "skip-records", "input",
+    "backend", "gpu-min-cells", "transport", "semantics", "partition", "batch-records", "batch-chars", "skip-records", "input",
     "timing", "strict-limits", "max-l1", "max-l2", "device", "device-map", "pin-window", "chunk-records",
     "chunk-bytes", "threads", "log-level", "inject-fault", "help"};
 
@@ -82,6 +83,7 @@ struct Header {
   int64_t L1;
   int64_t n_total;      // number_of_sequences
   int64_t first_index;  // --skip-records actually applied
+  int64_t cells;        // search cells of the job (-1: unknown, streaming)
 };
 
 struct BatchHeader {
@@ -176,7 +178,7 @@ class Job {
   int run();
 
  private:
-  void setup_engine();
+  void setup_engine(int64_t cells);
   void run_batch(RecordBatch* rb, int64_t n, int64_t total_chars, int64_t first_index);
   void batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds, bool cp);
   void batch_mpi(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds, bool cp);
@@ -201,11 +203,14 @@ class Job {
   std::vector<Result> results_;  // root: results of the current batch (mpi/rccl transports)
 };
 
-void Job::setup_engine() {
+void Job::setup_engine(int64_t cells) {
   const int threads = static_cast<int>(flags_.get_int("threads", 0));
-  if (threads > 0) omp_set_num_threads(threads);
-  const std::string backend = to_lower(flags_.get("backend", "auto"));
+  std::string backend = to_lower(flags_.get("backend", "auto"));
   if (backend != "auto" && backend != "hip" && backend != "cpu") throw Error("--backend must be auto|hip|cpu");
+  // auto: a job too small to pay for bringing up the GPU runtime (hundreds of ms) runs on the OpenMP
+  // engine; `cells` < 0 means unknown (streaming) and counts as large
+  const int64_t min_cells = flags_.get_int("gpu-min-cells", int64_t{300} * 1000 * 1000);
+  if (backend == "auto" && cells >= 0 && cells < min_cells * ctx_.size) backend = "cpu";
   const int ndev = (backend == "cpu") ? 0 : device_count();
   if (backend == "hip" && ndev == 0) throw Error("--backend=hip but no HIP device is visible");
   eng_.threads = threads;
@@ -591,7 +596,8 @@ int Job::run() {
   po.max_l1 = flags_.get_int("max-l1", 0);
   po.max_l2 = flags_.get_int("max-l2", 0);
 
-  setup_engine();
+  const int threads = static_cast<int>(flags_.get_int("threads", 0));
+  if (threads > 0) omp_set_num_threads(threads);
   total_.start();
 
   // ---- root opens the input; parses it whole (bulk) or just its header (streaming)
@@ -614,6 +620,7 @@ int Job::run() {
         seq1 = reader->seq1();
         h.n_total = reader->count();
         h.first_index = reader->skip(skip);
+        h.cells = -1;
       } else {
         std::vector<char> text = read_stream(in);
         Problem prob = parse_problem(text.data(), text.size(), po);
@@ -623,6 +630,8 @@ int Job::run() {
         h.n_total = bulk.size();
         h.first_index = std::min<int64_t>(skip, h.n_total);
         drop_front(bulk, h.first_index);
+        h.cells = 0;
+        for (int64_t i = 0; i < bulk.size(); ++i) h.cells += record_cells(static_cast<int64_t>(seq1.size()), bulk.length(i));
       }
       for (int i = 0; i < 4; ++i) h.w[i] = w.w[i];
     } catch (const std::exception& e) {
@@ -647,6 +656,9 @@ int Job::run() {
   for (int i = 0; i < 4; ++i) w.w[i] = h.w[i];
   seq1.resize(static_cast<size_t>(h.L1));
   bcast_bytes(seq1.data(), h.L1, kRoot, ctx_.world);
+  pt_.end();
+  pt_.begin("setup");
+  setup_engine(h.cells);  // collective: engine kind, transport, RCCL communicator
   eng_.set_problem(w, seq1, sem);
   pt_.end();
 

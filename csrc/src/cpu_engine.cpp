@@ -76,26 +76,36 @@ void solve_batch_cpu(const ScoreTable& t, const uint8_t* s1, int64_t L1, const R
     for (int64_t i = 0; i < n; ++i) out[i] = solve_record(t, s1, L1, batch.record(i), batch.length(i), sem);
     return;
   }
-  // Few records: split each record's offset range across threads and merge (max is order-free).
+  // Few records: split every record's offset range into chunks and run all (record, chunk) items in ONE
+  // parallel loop (one fork/join for the batch, dynamic balance), then merge per record — max is
+  // order-free, so the result does not depend on the thread count.
+  struct Item {
+    int64_t rec, ob, oe;
+  };
+  std::vector<Item> items;
   for (int64_t i = 0; i < n; ++i) {
-    const int64_t L2 = batch.length(i);
-    const int64_t n_off = candidate_offsets(L1, L2, sem);
+    const int64_t n_off = candidate_offsets(L1, batch.length(i), sem);
+    const int64_t chunk = std::max<int64_t>(16, (n_off + 4 * nt - 1) / (4 * nt));
     if (n_off <= 1) {
-      out[i] = solve_record(t, s1, L1, batch.record(i), L2, sem);
+      items.push_back(Item{i, 0, L1 + 1});
       continue;
     }
-    std::vector<Result> part(nt, Result{kNoCandidateScore, -1, -1});
-#pragma omp parallel num_threads(nt)
-    {
-      const int tid = omp_get_thread_num();
-      const int64_t b = n_off * tid / nt, e = n_off * (tid + 1) / nt;
-      part[tid] = solve_offsets(t, s1, L1, batch.record(i), L2, b, e, sem);
-    }
-    Result best{kNoCandidateScore, -1, -1};
-    for (const auto& p : part)
-      if (p.n >= 0 && (best.n < 0 || better(p, best))) best = p;
-    out[i] = best.n < 0 ? no_candidate() : best;
+    for (int64_t ob = 0; ob < n_off; ob += chunk) items.push_back(Item{i, ob, std::min(n_off, ob + chunk)});
   }
+  std::vector<Result> part(items.size());
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nt)
+  for (int64_t j = 0; j < static_cast<int64_t>(items.size()); ++j) {
+    const Item& it = items[j];
+    part[j] = solve_offsets(t, s1, L1, batch.record(it.rec), batch.length(it.rec), it.ob, it.oe, sem);
+  }
+  for (int64_t i = 0; i < n; ++i) out[i] = Result{kNoCandidateScore, -1, -1};
+  for (size_t j = 0; j < items.size(); ++j) {
+    Result& b = out[items[j].rec];
+    const Result& p = part[j];
+    if (p.n >= 0 && (b.n < 0 || better(p, b))) b = p;
+  }
+  for (int64_t i = 0; i < n; ++i)
+    if (out[i].n < 0) out[i] = no_candidate();
 }
 
 void solve_keys_cpu(const ScoreTable& t, const uint8_t* s1, int64_t L1, const RecordBatch& batch, int part,
@@ -118,19 +128,26 @@ void solve_keys_cpu(const ScoreTable& t, const uint8_t* s1, int64_t L1, const Re
     }
     return;
   }
-  for (int64_t i = 0; i < n; ++i) {  // few records: threads split this part's range further
+  // few records: this part's range of every record in chunks, one parallel loop for the batch
+  struct Item {
+    int64_t rec, ob, oe;
+  };
+  std::vector<Item> items;
+  for (int64_t i = 0; i < n; ++i) {
     int64_t b, e;
     range(i, b, e);
-    const int64_t L2 = batch.length(i);
-    std::vector<uint64_t> k(nt, 0);
-#pragma omp parallel num_threads(nt)
-    {
-      const int tid = omp_get_thread_num();
-      const int64_t tb = b + (e - b) * tid / nt, te = b + (e - b) * (tid + 1) / nt;
-      k[tid] = encode_key(solve_offsets(t, s1, L1, batch.record(i), L2, tb, te, sem), L2);
-    }
-    keys[i] = *std::max_element(k.begin(), k.end());
+    const int64_t chunk = std::max<int64_t>(16, (e - b + 4 * nt - 1) / (4 * nt));
+    for (int64_t ob = b; ob < e; ob += chunk) items.push_back(Item{i, ob, std::min(e, ob + chunk)});
   }
+  std::vector<uint64_t> pk(items.size());
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nt)
+  for (int64_t j = 0; j < static_cast<int64_t>(items.size()); ++j) {
+    const Item& it = items[j];
+    const int64_t L2 = batch.length(it.rec);
+    pk[j] = encode_key(solve_offsets(t, s1, L1, batch.record(it.rec), L2, it.ob, it.oe, sem), L2);
+  }
+  for (int64_t i = 0; i < n; ++i) keys[i] = 0;
+  for (size_t j = 0; j < items.size(); ++j) keys[items[j].rec] = std::max(keys[items[j].rec], pk[j]);
 }
 
 Result brute_force_record(const ScoreTable& t, const uint8_t* s1, int64_t L1, const uint8_t* s2, int64_t L2,
