@@ -31,20 +31,27 @@ INC       := -Icsrc/include
 CXXFLAGS  := -O3 -std=c++17 -fPIC -fopenmp -Wall -Wextra -Wno-unused-parameter $(INC) -I$(ROCM)/include -D__HIP_PLATFORM_AMD__
 HIPFLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) $(INC) -Wno-unused-result
 MPIFLAGS  := -I$(MPI_HOME)/include
-LDROCM    := -L$(ROCM)/lib -lamdhip64 -lrocprofiler-sdk-roctx -Wl,-rpath,$(ROCM)/lib
+LDROCM    := -L$(ROCM)/lib -lamdhip64 -Wl,-rpath,$(ROCM)/lib
+GPU_PLUGIN := mpi_openmp_cuda_amd/lib/libmoc_final_gpu.so
 
-CORE_SRCS := $(wildcard csrc/src/*.cpp) $(wildcard csrc/src/runtime/*.cpp)
+# host core without any ROCm dependency (parser, CPU engine, partitioner, runtime utilities)
+CPU_SRCS  := csrc/src/cpu_engine.cpp csrc/src/io.cpp csrc/src/partition.cpp csrc/src/problem.cpp \
+             csrc/src/score_table.cpp csrc/src/runtime/runtime.cpp
+# host code of the GPU engine (HIP runtime API) and the C ABI of libmoc.so
+GPU_SRCS  := csrc/src/hip_engine.cpp csrc/src/capi.cpp csrc/src/runtime/device.cpp csrc/src/runtime/pinned.cpp
+CORE_SRCS := $(CPU_SRCS) $(GPU_SRCS)
 HIP_SRCS  := $(wildcard csrc/src/hip/*.hip)
-COMM_SRCS := $(wildcard csrc/src/comm/*.cpp)
+CPU_OBJS  := $(patsubst csrc/src/%.cpp,$(OBJ)/%.o,$(CPU_SRCS))
 CORE_OBJS := $(patsubst csrc/src/%.cpp,$(OBJ)/%.o,$(CORE_SRCS))
 HIP_OBJS  := $(patsubst csrc/src/%.hip,$(OBJ)/%.o,$(HIP_SRCS))
-COMM_OBJS := $(patsubst csrc/src/%.cpp,$(OBJ)/%.o,$(COMM_SRCS))
+COMM_OBJS := $(OBJ)/comm/comm.o
+RCCL_OBJS := $(OBJ)/comm/rccl_comm.o
 HEADERS   := $(shell find csrc/include -name '*.h' -o -name '*.hpp')
 
 .PHONY: all build lib clean run runOn2 test unit asan tsan debug-kernels
 
 all: build
-build: lib final
+build: lib final $(GPU_PLUGIN)
 
 lib: $(PKG_LIB)
 
@@ -58,7 +65,7 @@ $(OBJ)/%.o: csrc/src/%.hip $(HEADERS)
 
 $(PKG_LIB): $(CORE_OBJS) $(HIP_OBJS)
 	@mkdir -p $(dir $@)
-	$(CXX) -shared -fopenmp -o $@ $^ $(LDROCM)
+	$(CXX) -shared -fopenmp -o $@ $^ $(LDROCM) -ldl
 
 # MPICH's conda wrapper names a compiler that is not installed, so link libmpi directly through a
 # private directory (keeps /opt/conda/lib — and its older libstdc++ — off the binary's search path).
@@ -69,27 +76,31 @@ $(MPILIB)/libmpi.so:
 	ln -sf $(MPI_HOME)/lib/libgfortran.so.4 $(MPILIB)/libgfortran.so.4
 	ln -sf $(MPI_HOME)/lib/libquadmath.so.0 $(MPILIB)/libquadmath.so.0
 
-$(OBJ)/apps/final.o: csrc/apps/final.cpp $(HEADERS)
+$(OBJ)/apps/%.o: csrc/apps/%.cpp $(HEADERS)
 	@mkdir -p $(dir $@)
 	$(CXX) $(CXXFLAGS) $(MPIFLAGS) -c $< -o $@
 
-final: $(OBJ)/apps/final.o $(COMM_OBJS) $(CORE_OBJS) $(HIP_OBJS) $(MPILIB)/libmpi.so
-	$(CXX) -fopenmp -o $@ $(OBJ)/apps/final.o $(COMM_OBJS) $(CORE_OBJS) $(HIP_OBJS) \
-	    -L$(MPILIB) -lmpi -Wl,-rpath-link,$(MPI_HOME)/lib -Wl,-rpath,'$$ORIGIN/$(MPILIB)' $(LDROCM) -lrccl
+# ./final links MPI and the CPU core only; the GPU side is a plugin it dlopens when a rank uses a GPU
+final: $(OBJ)/apps/final.o $(COMM_OBJS) $(CPU_OBJS) $(MPILIB)/libmpi.so
+	$(CXX) -fopenmp -o $@ $(OBJ)/apps/final.o $(COMM_OBJS) $(CPU_OBJS) \
+	    -L$(MPILIB) -lmpi -Wl,-rpath-link,$(MPI_HOME)/lib -Wl,-rpath,'$$ORIGIN/$(MPILIB)' -ldl
 
-# Host-side sanitizers only (GPU ASan is not available on the target pool).
+$(GPU_PLUGIN): $(OBJ)/apps/final_gpu.o $(RCCL_OBJS) $(COMM_OBJS) $(PKG_LIB) $(MPILIB)/libmpi.so
+	$(CXX) -shared -fopenmp -o $@ $(OBJ)/apps/final_gpu.o $(RCCL_OBJS) $(COMM_OBJS) \
+	    -L$(dir $(PKG_LIB)) -lmoc -Wl,-rpath,'$$ORIGIN' -L$(MPILIB) -lmpi -Wl,-rpath-link,$(MPI_HOME)/lib \
+	    -Wl,-rpath,'$$ORIGIN/../../$(MPILIB)' $(LDROCM) -lrccl
+
+# Host-side sanitizers (GPU ASan is not available on the target pool). ./final links no ROCm code, so
+# the sanitized binaries cover everything the CPU backend runs; a GPU rank would dlopen the plugin.
+SAN_SRCS := $(CPU_SRCS) csrc/src/comm/comm.cpp csrc/apps/final.cpp
 asan: $(MPILIB)/libmpi.so
-	@mkdir -p $(BUILD)/asan
-	for f in $(CORE_SRCS) $(COMM_SRCS) csrc/apps/final.cpp; do \
+	@rm -rf $(BUILD)/asan && mkdir -p $(BUILD)/asan
+	for f in $(SAN_SRCS); do \
 	  $(CXX) -O1 -g -std=c++17 -fopenmp -fsanitize=address,undefined -fno-omit-frame-pointer $(INC) \
 	    -I$(ROCM)/include -D__HIP_PLATFORM_AMD__ $(MPIFLAGS) -c $$f -o $(BUILD)/asan/$$(echo $$f | tr / _).o || exit 1; \
 	done
-	for f in $(HIP_SRCS); do \
-	  $(HIPCC) -O1 -g -fPIC -std=c++17 --offload-arch=$(ARCH) $(INC) \
-	    -c $$f -o $(BUILD)/asan/$$(basename $$f .hip).hip.o || exit 1; \
-	done
 	$(CXX) -fopenmp -fsanitize=address,undefined -o final_asan $(BUILD)/asan/*.o \
-	    -L$(MPILIB) -lmpi -Wl,-rpath-link,$(MPI_HOME)/lib -Wl,-rpath,'$$ORIGIN/$(MPILIB)' $(LDROCM) -lrccl
+	    -L$(MPILIB) -lmpi -Wl,-rpath-link,$(MPI_HOME)/lib -Wl,-rpath,'$$ORIGIN/$(MPILIB)' -ldl
 
 # ThreadSanitizer build of the host paths (OpenMP parser / CPU engine / formatter) — CPU backend only.
 # Built with ROCm's clang + LLVM libomp so the Archer OMPT tool (libarcher) can tell TSan about OpenMP
@@ -97,17 +108,14 @@ asan: $(MPILIB)/libmpi.so
 #   make tsan && OMP_TOOL_LIBRARIES=$(ROCM)/lib/llvm/lib/libarcher.so mpiexec -np 2 ./final_tsan --backend=cpu < in
 TSAN_CXX  := $(ROCM)/lib/llvm/bin/clang++
 tsan: $(MPILIB)/libmpi.so
-	@mkdir -p $(BUILD)/tsan
-	for f in $(CORE_SRCS) $(COMM_SRCS) csrc/apps/final.cpp; do \
+	@rm -rf $(BUILD)/tsan && mkdir -p $(BUILD)/tsan
+	for f in $(SAN_SRCS); do \
 	  $(TSAN_CXX) -O1 -g -std=c++17 -fopenmp -fsanitize=thread $(INC) \
 	    -I$(ROCM)/include -D__HIP_PLATFORM_AMD__ $(MPIFLAGS) -c $$f -o $(BUILD)/tsan/$$(echo $$f | tr / _).o || exit 1; \
 	done
-	for f in $(HIP_SRCS); do \
-	  $(HIPCC) -O1 -g -fPIC -std=c++17 --offload-arch=$(ARCH) $(INC) -c $$f -o $(BUILD)/tsan/$$(basename $$f .hip).hip.o || exit 1; \
-	done
 	$(TSAN_CXX) -fopenmp -fsanitize=thread -o final_tsan $(BUILD)/tsan/*.o \
 	    -L$(MPILIB) -lmpi -Wl,-rpath-link,$(MPI_HOME)/lib -Wl,-rpath,'$$ORIGIN/$(MPILIB)' \
-	    -L$(ROCM)/lib/llvm/lib -Wl,-rpath,$(ROCM)/lib/llvm/lib $(LDROCM) -lrccl
+	    -L$(ROCM)/lib/llvm/lib -Wl,-rpath,$(ROCM)/lib/llvm/lib -ldl
 
 # Device-side bounds checks (MOC_DCHECK: printf, never a fault) in every kernel -> build/debug/libmoc.so;
 # select it with MOC_LIB_PATH=$$PWD/build/debug/libmoc.so.
@@ -116,10 +124,10 @@ debug-kernels:
 	for f in $(HIP_SRCS); do \
 	  $(HIPCC) $(HIPFLAGS) -DMOC_DEBUG_KERNELS -c $$f -o $(BUILD)/debug/$$(basename $$f .hip).hip.o || exit 1; \
 	done
-	$(CXX) -shared -fopenmp -o $(BUILD)/debug/libmoc.so $(CORE_OBJS) $(BUILD)/debug/*.hip.o $(LDROCM)
+	$(CXX) -shared -fopenmp -o $(BUILD)/debug/libmoc.so $(CORE_OBJS) $(BUILD)/debug/*.hip.o $(LDROCM) -ldl
 
 clean:
-	rm -rf $(BUILD) final final_asan final_tsan $(PKG_LIB)
+	rm -rf $(BUILD) final final_asan final_tsan $(PKG_LIB) $(GPU_PLUGIN)
 
 run: build
 	$(MPI_HOME)/bin/mpiexec -np $(NP) ./final < $(INPUT)
@@ -131,8 +139,8 @@ test: unit
 	python -m pytest tests/ -x -q -m "not gpu"
 
 # native unit tests of the host core (no GPU, no MPI)
-$(BUILD)/test_core: csrc/tests/test_core.cpp $(CORE_OBJS) $(HIP_OBJS) $(HEADERS)
-	$(CXX) $(CXXFLAGS) -o $@ csrc/tests/test_core.cpp $(CORE_OBJS) $(HIP_OBJS) $(LDROCM)
+$(BUILD)/test_core: csrc/tests/test_core.cpp $(CPU_OBJS) $(HEADERS)
+	$(CXX) $(CXXFLAGS) -o $@ csrc/tests/test_core.cpp $(CPU_OBJS) -ldl
 
 unit: $(BUILD)/test_core
 	$(BUILD)/test_core

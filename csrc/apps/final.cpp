@@ -18,8 +18,9 @@
 //        mpi  — host Scatterv/Gatherv (CPU backend, or GPU ranks without a shared window).
 //   6. Every rank runs its engine (HIP kernels, or the OpenMP CPU engine), root prints in order.
 // Any error on any rank -> message + MPI_Abort (reference: exit(1) without abort, peers hang, B11).
-#include <hip/hip_runtime_api.h>
+#include <dlfcn.h>
 #include <omp.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -32,13 +33,11 @@
 
 #include "moc/comm.hpp"
 #include "moc/cpu_engine.hpp"
-#include "moc/hip_engine.hpp"
+#include "moc/gpu_rank.hpp"
 #include "moc/io.hpp"
 #include "moc/partition.hpp"
 #include "moc/problem.hpp"
-#include "moc/runtime/device.hpp"
 #include "moc/runtime/flags.hpp"
-#include "moc/runtime/hip_check.hpp"
 #include "moc/runtime/log.hpp"
 #include "moc/runtime/timer.hpp"
 #include "moc/runtime/trace.hpp"
@@ -126,10 +125,54 @@ void drop_front(RecordBatch& b, int64_t s) {
   for (auto& o : b.offsets) o -= c0;
 }
 
+// The GPU plugin (moc/gpu_rank.hpp): mpi_openmp_cuda_amd/lib/libmoc_final_gpu.so next to this binary,
+// or $MOC_GPU_PLUGIN. Loaded once, on the first question about GPUs; never for CPU-backend runs.
+struct GpuPlugin {
+  GpuDeviceCountFn device_count = nullptr;
+  GpuRankCreateFn create = nullptr;
+  std::string error;
+};
+
+const GpuPlugin& gpu_plugin() {
+  static const GpuPlugin p = [] {
+    GpuPlugin g;
+    std::string path;
+    if (const char* env = std::getenv("MOC_GPU_PLUGIN")) {
+      path = env;
+    } else {
+      char exe[4096];
+      const ssize_t len = readlink("/proc/self/exe", exe, sizeof exe - 1);
+      std::string dir = ".";
+      if (len > 0) {
+        exe[len] = 0;
+        dir = std::string(exe);
+        dir = dir.substr(0, dir.rfind('/'));
+      }
+      path = dir + "/mpi_openmp_cuda_amd/lib/libmoc_final_gpu.so";
+    }
+    void* h = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+      const char* e = dlerror();
+      g.error = e ? e : ("cannot load " + path);
+      return g;
+    }
+    g.device_count = reinterpret_cast<GpuDeviceCountFn>(dlsym(h, kGpuDeviceCountSym));
+    g.create = reinterpret_cast<GpuRankCreateFn>(dlsym(h, kGpuRankCreateSym));
+    if (!g.device_count || !g.create) g.error = "GPU plugin " + path + " lacks its entry points";
+    return g;
+  }();
+  return p;
+}
+
+int gpu_device_count() {
+  const GpuPlugin& g = gpu_plugin();
+  return g.device_count && g.create ? g.device_count() : 0;
+}
+
 // Runs the selected engine on one contiguous slice (host buffers).
 struct RankEngine {
   bool gpu = false;
-  std::unique_ptr<HipEngine> hip;
+  std::unique_ptr<GpuRank> hip;
   ScoreTable table{};
   std::vector<uint8_t> seq1;
   Semantics sem = Semantics::Reference;
@@ -153,7 +196,7 @@ struct RankEngine {
     if (n <= 0) return;
     if (gpu) {
       hip->solve(codes, offsets, n, out);
-      kernel_ms += hip->stats().kernel_ms;
+      kernel_ms += hip->last_kernel_ms();
       return;
     }
     solve_batch_cpu(table, seq1.data(), static_cast<int64_t>(seq1.size()), copy_slice(codes, offsets, n), out, sem,
@@ -164,7 +207,7 @@ struct RankEngine {
     if (n <= 0) return;
     if (gpu) {
       hip->search_keys(codes, offsets, n, part, parts, keys);
-      kernel_ms += hip->stats().kernel_ms;
+      kernel_ms += hip->last_kernel_ms();
       return;
     }
     solve_keys_cpu(table, seq1.data(), static_cast<int64_t>(seq1.size()), copy_slice(codes, offsets, n), part, parts,
@@ -194,7 +237,6 @@ class Job {
   bool all_gpu_ = false;
   std::string transport_, partition_;
   bool pin_window_ = true;
-  std::unique_ptr<RcclComm> nccl_;
   PhaseTimer pt_;
   Stopwatch total_;
   double compute_ms_ = 0;
@@ -211,20 +253,21 @@ void Job::setup_engine(int64_t cells) {
   // engine; `cells` < 0 means unknown (streaming) and counts as large
   const int64_t min_cells = flags_.get_int("gpu-min-cells", int64_t{300} * 1000 * 1000);
   if (backend == "auto" && cells >= 0 && cells < min_cells * ctx_.size) backend = "cpu";
-  const int ndev = (backend == "cpu") ? 0 : device_count();
-  if (backend == "hip" && ndev == 0) throw Error("--backend=hip but no HIP device is visible");
+  const int ndev = (backend == "cpu") ? 0 : gpu_device_count();
+  if (backend == "hip" && ndev == 0)
+    throw Error("--backend=hip but no HIP device is visible" +
+                (gpu_plugin().error.empty() ? std::string() : " (" + gpu_plugin().error + ")"));
   eng_.threads = threads;
   eng_.gpu = ndev > 0;
   if (eng_.gpu) {
-    int requested = static_cast<int>(flags_.get_int("device", -1));
-    const std::vector<int> map = parse_int_list(flags_.get("device-map", ""));
-    if (requested < 0 && !map.empty()) requested = map[static_cast<size_t>(ctx_.local_rank) % map.size()];
-    device_ = select_device(ctx_.local_rank, requested);
-    EngineOptions eo;
-    eo.device = device_;
-    eo.chunk_records = flags_.get_int("chunk-records", eo.chunk_records);
-    eo.chunk_bytes = flags_.get_int("chunk-bytes", eo.chunk_bytes);
-    eng_.hip = std::make_unique<HipEngine>(eo);
+    GpuRankOptions go;
+    go.device = static_cast<int>(flags_.get_int("device", -1));
+    go.device_map = parse_int_list(flags_.get("device-map", ""));
+    go.chunk_records = flags_.get_int("chunk-records", 0);
+    go.chunk_bytes = flags_.get_int("chunk-bytes", 0);
+    go.log_level = flags_.get("log-level", "warn");
+    eng_.hip.reset(gpu_plugin().create(ctx_, go));
+    device_ = eng_.hip->device();
   }
   int gpu_minmax[2] = {eng_.gpu ? 1 : 0, eng_.gpu ? -1 : 0};  // MIN -> {min gpu, -max gpu}
   MPI_Allreduce(MPI_IN_PLACE, gpu_minmax, 2, MPI_INT, MPI_MIN, ctx_.world);
@@ -244,7 +287,7 @@ void Job::setup_engine(int64_t cells) {
   if (partition_ == "offsets" && any_gpu && !all_gpu_)
     throw Error("--partition=offsets needs the same backend on every rank (use --backend=hip or --backend=cpu)");
   pin_window_ = flags_.get_bool("pin-window", true);
-  if (transport_ == "rccl") nccl_ = std::make_unique<RcclComm>(ctx_, device_);
+  if (transport_ == "rccl") eng_.hip->init_rccl();
   MOC_LOG_INFO("rank %d/%d host %s local %d/%d engine=%s device=%d transport=%s partition=%s", ctx_.rank, ctx_.size,
                ctx_.hostname.c_str(), ctx_.local_rank, ctx_.local_size, eng_.gpu ? "hip" : "cpu", device_,
                transport_.c_str(), partition_.c_str());
@@ -432,130 +475,15 @@ void Job::batch_mpi(RecordBatch* rb, int64_t n, int64_t total_chars, const std::
   print(results_.data(), n, 0);
 }
 
-// Device buffers of one rccl batch (freed on scope exit, also when unwinding).
-struct DeviceBufs {
-  std::vector<void*> ptrs;
-  template <typename T>
-  T* alloc(int64_t bytes) {
-    void* p = nullptr;
-    MOC_HIP_CHECK(hipMalloc(&p, static_cast<size_t>(std::max<int64_t>(bytes, 16))));
-    ptrs.push_back(p);
-    return static_cast<T*>(p);
-  }
-  ~DeviceBufs() {
-    for (void* p : ptrs) (void)hipFree(p);
-  }
-};
-
 void Job::batch_rccl(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds, bool cp) {
-  RcclComm& nccl = *nccl_;
-  hipStream_t s = eng_.hip->compute_stream();
-  const int p = ctx_.size;
-  DeviceBufs bufs;
-  pt_.begin("distribute");
-  fault_.at("distribute", ctx_.rank);
-  if (cp) {
-    // root uploads the batch once; RCCL broadcasts it to every device over xGMI; each GPU searches its
-    // share of every record's offset tiles; ncclAllReduce(MAX, uint64) combines the packed keys.
-    uint8_t* d_codes = bufs.alloc<uint8_t>(total_chars);
-    int64_t* d_offs = bufs.alloc<int64_t>(8 * (n + 1));
-    std::vector<int64_t> h_offs(static_cast<size_t>(n) + 1);
-    if (ctx_.rank == kRoot) {
-      h_offs = rb->offsets;
-      MOC_HIP_CHECK(hipMemcpyAsync(d_codes, rb->codes.data(), total_chars, hipMemcpyHostToDevice, s));
-      MOC_HIP_CHECK(hipMemcpyAsync(d_offs, rb->offsets.data(), 8 * (n + 1), hipMemcpyHostToDevice, s));
-    }
-    nccl.bcast(d_codes, total_chars, kRoot, s);
-    nccl.bcast(d_offs, 8 * (n + 1), kRoot, s);
-    bcast_bytes(h_offs.data(), 8 * (n + 1), kRoot, ctx_.world);  // host copy for tile planning
-    MOC_HIP_CHECK(hipStreamSynchronize(s));
-    nccl.check_async();
-    pt_.end();
-    pt_.begin("compute");
-    fault_.at("compute", ctx_.rank);
-    Stopwatch sw;
-    sw.start();
-    auto* d_keys = bufs.alloc<unsigned long long>(8 * n);
-    eng_.hip->search_keys_device(d_codes, d_offs, h_offs.data(), n, ctx_.rank, ctx_.size, d_keys, s);
-    MOC_HIP_CHECK(hipStreamSynchronize(s));
-    sw.stop();
-    compute_ms_ += sw.total_ms();
-    pt_.end();
-    pt_.begin("gather");
-    fault_.at("gather", ctx_.rank);
-    nccl.allreduce_max_u64(d_keys, n, s);
-    if (ctx_.rank == kRoot) {
-      auto* d_res = bufs.alloc<Result>(12 * n);
-      eng_.hip->finalize_keys_device(d_offs, n, d_keys, d_res, ResultFormat::R12, s);
-      results_.resize(static_cast<size_t>(n));
-      MOC_HIP_CHECK(hipMemcpyAsync(results_.data(), d_res, 12 * n, hipMemcpyDeviceToHost, s));
-    }
-    MOC_HIP_CHECK(hipStreamSynchronize(s));
-    nccl.check_async();
-    pt_.end();
-    print(results_.data(), n, 0);
-    return;
-  }
-  const int64_t my_b = bounds[ctx_.rank], my_n = bounds[ctx_.rank + 1] - my_b;
-  // counts in bytes for codes and (absolute) offsets; each rank receives n_r+1 offsets
-  std::vector<int64_t> ccount(p), cdispl(p), ocount(p), odispl(p);
-  if (ctx_.rank == kRoot) {
-    for (int r = 0; r < p; ++r) {
-      ccount[r] = rb->offsets[bounds[r + 1]] - rb->offsets[bounds[r]];
-      cdispl[r] = rb->offsets[bounds[r]];
-    }
-  }
-  bcast_bytes(ccount.data(), 8 * p, kRoot, ctx_.world);
-  bcast_bytes(cdispl.data(), 8 * p, kRoot, ctx_.world);
-  for (int r = 0; r < p; ++r) {
-    ocount[r] = 8 * (bounds[r + 1] - bounds[r] + 1);
-    odispl[r] = 8 * bounds[r];
-  }
-  uint8_t* d_all_codes = nullptr;
-  int64_t* d_all_offs = nullptr;
-  Result* d_all_out = nullptr;
-  if (ctx_.rank == kRoot) {
-    d_all_codes = bufs.alloc<uint8_t>(total_chars);
-    d_all_offs = bufs.alloc<int64_t>(8 * (n + 1));
-    d_all_out = bufs.alloc<Result>(12 * n);
-    MOC_HIP_CHECK(hipMemcpyAsync(d_all_codes, rb->codes.data(), total_chars, hipMemcpyHostToDevice, s));
-    MOC_HIP_CHECK(hipMemcpyAsync(d_all_offs, rb->offsets.data(), 8 * (n + 1), hipMemcpyHostToDevice, s));
-  }
-  uint8_t* d_codes = bufs.alloc<uint8_t>(ccount[ctx_.rank]);
-  int64_t* d_offs = bufs.alloc<int64_t>(8 * (my_n + 1));
-  Result* d_out = bufs.alloc<Result>(12 * my_n);
-  nccl.scatterv(d_all_codes, ccount, cdispl, d_codes, kRoot, s);
-  nccl.scatterv(d_all_offs, ocount, odispl, d_offs, kRoot, s);
-  std::vector<int64_t> h_offs(static_cast<size_t>(my_n) + 1);
-  MOC_HIP_CHECK(hipMemcpyAsync(h_offs.data(), d_offs, 8 * (my_n + 1), hipMemcpyDeviceToHost, s));
-  MOC_HIP_CHECK(hipStreamSynchronize(s));
-  nccl.check_async();
-  pt_.end();
-  pt_.begin("compute");
-  fault_.at("compute", ctx_.rank);
-  Stopwatch sw;
-  sw.start();
-  // d_codes holds this rank's letters starting at absolute offset h_offs[0]
-  if (my_n > 0) eng_.hip->solve_device(d_codes - h_offs[0], d_offs, h_offs.data(), my_n, d_out, s);
-  MOC_HIP_CHECK(hipStreamSynchronize(s));
-  sw.stop();
-  compute_ms_ += sw.total_ms();
-  pt_.end();
-  pt_.begin("gather");
-  fault_.at("gather", ctx_.rank);
-  std::vector<int64_t> rcount(p), rdispl(p);
-  for (int r = 0; r < p; ++r) {
-    rcount[r] = 12 * (bounds[r + 1] - bounds[r]);
-    rdispl[r] = 12 * bounds[r];
-  }
-  nccl.gatherv(d_out, 12 * my_n, d_all_out, rcount, rdispl, kRoot, s);
-  if (ctx_.rank == kRoot) {
-    results_.resize(static_cast<size_t>(n));
-    MOC_HIP_CHECK(hipMemcpyAsync(results_.data(), d_all_out, 12 * n, hipMemcpyDeviceToHost, s));
-  }
-  MOC_HIP_CHECK(hipStreamSynchronize(s));
-  nccl.check_async();
-  pt_.end();
+  PhaseHooks hooks;
+  hooks.begin = [this](const char* phase) {
+    pt_.begin(phase);
+    fault_.at(phase, ctx_.rank);
+  };
+  hooks.end = [this] { pt_.end(); };
+  if (ctx_.rank == kRoot) results_.resize(static_cast<size_t>(n));
+  compute_ms_ += eng_.hip->rccl_batch(rb, n, total_chars, bounds, cp, results_.data(), hooks);
   print(results_.data(), n, 0);
 }
 

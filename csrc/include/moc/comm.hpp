@@ -10,12 +10,10 @@
 //   * host helpers — exact-count broadcasts, 64-bit-safe Scatterv/Gatherv of bytes.
 //   * SharedWindow — MPI_Win_allocate_shared over the node communicator: the root parses the input
 //                    into it once and every rank DMAs its own slice over its own PCIe link.
-//   * RcclComm     — ncclCommInitRank with the unique id broadcast over MPI; device broadcast and
-//                    grouped variable-size send/recv (the scatter/gather of records over xGMI).
+// RcclComm (moc/rccl_comm.hpp) adds the RCCL device collectives on top of an MpiContext.
 #pragma once
 
 #include <mpi.h>
-#include <rccl/rccl.h>
 
 #include <cstdint>
 #include <string>
@@ -73,29 +71,5 @@ class SharedWindow {
   int64_t bytes_ = 0;
 };
 
-class RcclComm {
- public:
-  RcclComm(const MpiContext& ctx, int device);
-  ~RcclComm();
-  RcclComm(const RcclComm&) = delete;
-  RcclComm& operator=(const RcclComm&) = delete;
-
-  void bcast(void* dbuf, int64_t bytes, int root, hipStream_t s);
-  // Root: sends slices [displs[r], displs[r]+counts[r]) of d_send to every rank r != root.
-  // Others: receive counts[rank] bytes into d_recv. One ncclGroup, variable sizes.
-  void scatterv(const void* d_send, const std::vector<int64_t>& counts, const std::vector<int64_t>& displs,
-                void* d_recv, int root, hipStream_t s);
-  // Inverse: every rank != root sends its slice to root, which receives it at displs[r].
-  void gatherv(const void* d_send, int64_t count, void* d_recv, const std::vector<int64_t>& counts,
-               const std::vector<int64_t>& displs, int root, hipStream_t s);
-  // In-place element-wise MAX of n uint64 device values over all ranks (packed candidate keys).
-  void allreduce_max_u64(void* dbuf, int64_t n, hipStream_t s);
-  void check_async() const;  // ncclCommGetAsyncError -> throw
-  ncclComm_t comm() const { return comm_; }
-
- private:
-  const MpiContext& ctx_;
-  ncclComm_t comm_ = nullptr;
-};
 
 }  // namespace moc

@@ -1,0 +1,63 @@
+// GPU side of the `final` CLI, built as a plugin (mpi_openmp_cuda_amd/lib/libmoc_final_gpu.so) and
+// loaded with dlopen only when a rank runs the HIP backend. `final` itself links no ROCm library, so
+//   * CPU-backend runs (BASELINE.json config 1, small jobs under --backend=auto) start as fast as a plain
+//     MPI program and work on hosts without ROCm,
+//   * GPU runs pay for the HIP/RCCL runtimes only when they use them.
+// The reference links the CUDA runtime statically into every rank (makefile:4).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "moc/comm.hpp"
+#include "moc/common.hpp"
+#include "moc/problem.hpp"
+
+namespace moc {
+
+struct GpuRankOptions {
+  int device = -1;              // explicit device, or -1: node-local rank (or device_map)
+  std::vector<int> device_map;  // node-local rank i -> device_map[i % size]
+  int64_t chunk_records = 0;    // 0: engine defaults
+  int64_t chunk_bytes = 0;
+  std::string log_level = "warn";
+};
+
+// Phase hooks of the caller's timer / fault injection (the rccl batch runs its own phases).
+struct PhaseHooks {
+  std::function<void(const char*)> begin;  // starts a phase (and fires the fault hook for it)
+  std::function<void()> end;
+};
+
+class GpuRank {
+ public:
+  virtual ~GpuRank() = default;
+  virtual int device() const = 0;
+  virtual void set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, Semantics sem) = 0;
+  // Host batch -> host results (record i at codes + offsets[i]); zero-copy when the buffers are pinned.
+  virtual void solve(const uint8_t* codes, const int64_t* offsets, int64_t n, Result* out) = 0;
+  // Context-parallel share `part` of `parts` of every record -> packed 64-bit keys (host).
+  virtual void search_keys(const uint8_t* codes, const int64_t* offsets, int64_t n, int part, int parts,
+                           uint64_t* keys) = 0;
+  virtual double last_kernel_ms() const = 0;
+  virtual void pin(const void* p, size_t bytes) = 0;
+  virtual void unpin_all() = 0;
+  // Creates the RCCL communicator (collective over ctx.world: every rank must call it).
+  virtual void init_rccl() = 0;
+  // One batch over RCCL (transport=rccl): root uploads, slices scatter over xGMI (or, with `cp`, the
+  // batch is broadcast and packed keys are MAX-all-reduced), results gather to the root's `out`.
+  // `rb` is read on the root only; returns this rank's compute milliseconds.
+  virtual double rccl_batch(const RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds,
+                            bool cp, Result* out, const PhaseHooks& hooks) = 0;
+};
+
+// Plugin entry points (extern "C", resolved with dlsym).
+using GpuDeviceCountFn = int (*)();
+using GpuRankCreateFn = GpuRank* (*)(const MpiContext& ctx, const GpuRankOptions& opt);
+constexpr const char* kGpuDeviceCountSym = "moc_final_gpu_device_count";
+constexpr const char* kGpuRankCreateSym = "moc_final_gpu_create";
+
+}  // namespace moc

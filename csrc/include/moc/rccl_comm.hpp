@@ -1,0 +1,41 @@
+// RCCL communicator for GPU ranks: ncclCommInitRank with the unique id broadcast over MPI; device
+// broadcast, grouped variable-size send/recv (the scatter/gather of records over xGMI) and the MAX
+// all-reduce of packed candidate keys (context-parallel mode). Reference collectives: SURVEY.md §2.3.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "moc/comm.hpp"
+
+namespace moc {
+
+class RcclComm {
+ public:
+  RcclComm(const MpiContext& ctx, int device);
+  ~RcclComm();
+  RcclComm(const RcclComm&) = delete;
+  RcclComm& operator=(const RcclComm&) = delete;
+
+  void bcast(void* dbuf, int64_t bytes, int root, hipStream_t s);
+  // Root: sends slices [displs[r], displs[r]+counts[r]) of d_send to every rank r != root.
+  // Others: receive counts[rank] bytes into d_recv. One ncclGroup, variable sizes.
+  void scatterv(const void* d_send, const std::vector<int64_t>& counts, const std::vector<int64_t>& displs,
+                void* d_recv, int root, hipStream_t s);
+  // Inverse: every rank != root sends its slice to root, which receives it at displs[r].
+  void gatherv(const void* d_send, int64_t count, void* d_recv, const std::vector<int64_t>& counts,
+               const std::vector<int64_t>& displs, int root, hipStream_t s);
+  // In-place element-wise MAX of n uint64 device values over all ranks (packed candidate keys).
+  void allreduce_max_u64(void* dbuf, int64_t n, hipStream_t s);
+  void check_async() const;  // ncclCommGetAsyncError -> throw
+  ncclComm_t comm() const { return comm_; }
+
+ private:
+  const MpiContext& ctx_;
+  ncclComm_t comm_ = nullptr;
+};
+
+}  // namespace moc

@@ -2,7 +2,8 @@
 // has no tracing at all (no NVTX, no timers, main.c / cudaFunctions.cu). The ranges cost one call into
 // librocprofiler-sdk-roctx (a no-op unless a profiler is attached) and show up in
 //   rocprofv3 --marker-trace --kernel-trace -- ./final ...
-// next to the kernels. MOC_TRACE=0 turns them off entirely.
+// next to the kernels. The roctx library is loaded on first use when a rocprofiler tool is present
+// (MOC_TRACE=1 forces it, MOC_TRACE=0 turns the ranges off entirely).
 #pragma once
 
 namespace moc {

@@ -1,5 +1,5 @@
 // Host runtime utilities: flags, logging, phase timer JSON, roctx ranges.
-#include <rocprofiler-sdk-roctx/roctx.h>
+#include <dlfcn.h>
 
 #include <cstdio>
 #include <cstdlib>
@@ -130,24 +130,51 @@ void logf(LogLevel lvl, const char* fmt, ...) {
 }
 
 // ---------------------------------------------------------------- trace
-bool trace_enabled() {
-  static const bool on = [] {
+// roctx is resolved at the first range (dlopen of librocprofiler-sdk-roctx), so CPU-only runs of the
+// host core never map any ROCm library. Entry points of the roctx C API (roctx.h).
+namespace {
+struct Roctx {
+  int (*push)(const char*) = nullptr;
+  int (*pop)() = nullptr;
+  void (*mark)(const char*) = nullptr;
+  int (*name_thread)(const char*) = nullptr;
+};
+const Roctx& roctx() {
+  static const Roctx r = [] {
+    Roctx x;
     const char* v = std::getenv("MOC_TRACE");
-    return !(v && (std::strcmp(v, "0") == 0 || std::strcmp(v, "off") == 0));
+    if (v && (std::strcmp(v, "0") == 0 || std::strcmp(v, "off") == 0)) return x;
+    // default: only when a rocprofiler tool (rocprofv3) or the SDK is already in the process — ranges
+    // are no-ops otherwise, and loading the library would cost every CPU-only run its start-up time
+    const bool forced = v && (std::strcmp(v, "1") == 0 || std::strcmp(v, "on") == 0);
+    const bool profiler = dlopen("librocprofiler-sdk-tool.so.1", RTLD_NOLOAD | RTLD_LAZY) ||
+                          dlopen("librocprofiler-sdk.so.1", RTLD_NOLOAD | RTLD_LAZY);
+    if (!forced && !profiler) return x;
+    void* h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) return x;
+    x.push = reinterpret_cast<int (*)(const char*)>(dlsym(h, "roctxRangePushA"));
+    x.pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));
+    x.mark = reinterpret_cast<void (*)(const char*)>(dlsym(h, "roctxMarkA"));
+    x.name_thread = reinterpret_cast<int (*)(const char*)>(dlsym(h, "roctxNameOsThread"));
+    return x;
   }();
-  return on;
+  return r;
 }
+}  // namespace
+
+bool trace_enabled() { return roctx().push != nullptr; }
 void trace_push(const char* name) {
-  if (trace_enabled()) roctxRangePushA(name);
+  if (roctx().push) roctx().push(name);
 }
 void trace_pop() {
-  if (trace_enabled()) roctxRangePop();
+  if (roctx().pop) roctx().pop();
 }
 void trace_mark(const char* name) {
-  if (trace_enabled()) roctxMarkA(name);
+  if (roctx().mark) roctx().mark(name);
 }
 void trace_name_thread(const char* name) {
-  if (trace_enabled()) roctxNameOsThread(name);
+  if (roctx().name_thread) roctx().name_thread(name);
 }
 
 // ---------------------------------------------------------------- timer
