@@ -524,7 +524,9 @@ int Job::run() {
   po.max_l1 = flags_.get_int("max-l1", 0);
   po.max_l2 = flags_.get_int("max-l2", 0);
 
-  const int threads = static_cast<int>(flags_.get_int("threads", 0));
+  // OpenMP threads: --threads, else OMP_NUM_THREADS, else the node's cores shared by its ranks
+  int threads = static_cast<int>(flags_.get_int("threads", 0));
+  if (threads <= 0 && !std::getenv("OMP_NUM_THREADS")) threads = std::max(1, omp_get_num_procs() / ctx_.local_size);
   if (threads > 0) omp_set_num_threads(threads);
   total_.start();
 
