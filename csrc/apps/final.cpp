@@ -552,7 +552,7 @@ int Job::run() {
         h.first_index = reader->skip(skip);
         h.cells = -1;
       } else {
-        std::vector<char> text = read_stream(in);
+        uvector<char> text = read_stream(in);
         Problem prob = parse_problem(text.data(), text.size(), po);
         w = prob.weights;
         seq1 = std::move(prob.seq1);

@@ -92,7 +92,7 @@ double GpuRankImpl::rccl_batch(const RecordBatch* rb, int64_t n, int64_t total_c
     int64_t* d_offs = bufs.alloc<int64_t>(8 * (n + 1));
     std::vector<int64_t> h_offs(static_cast<size_t>(n) + 1);
     if (ctx_.rank == kRoot) {
-      h_offs = rb->offsets;
+      h_offs.assign(rb->offsets.begin(), rb->offsets.end());
       MOC_HIP_CHECK(hipMemcpyAsync(d_codes, rb->codes.data(), total_chars, hipMemcpyHostToDevice, s));
       MOC_HIP_CHECK(hipMemcpyAsync(d_offs, rb->offsets.data(), 8 * (n + 1), hipMemcpyHostToDevice, s));
     }

@@ -26,7 +26,7 @@ struct ParseOptions {
 };
 
 // Reads the whole stream into memory (bulk fread; no per-token stdio).
-std::vector<char> read_stream(FILE* f);
+uvector<char> read_stream(FILE* f);
 
 // Parses "W1 W2 W3 W4 / Seq1 / N / Seq2 x N" (PDF p.5-6). Whitespace of any kind (incl. CRLF)
 // separates tokens, exactly like fscanf %d/%s. Throws moc::Error with a precise message.

@@ -7,15 +7,39 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <vector>
 
 #include "moc/common.hpp"
 
 namespace moc {
 
+// Allocator whose resize() leaves new elements default-initialised (not zeroed): batch buffers are
+// written in full right after they are sized, so zero-filling hundreds of MB first is pure waste.
+template <typename T>
+struct DefaultInitAllocator : std::allocator<T> {
+  template <typename U>
+  struct rebind {
+    using other = DefaultInitAllocator<U>;
+  };
+  DefaultInitAllocator() = default;
+  template <typename U>
+  DefaultInitAllocator(const DefaultInitAllocator<U>&) noexcept {}
+  template <typename U>
+  void construct(U* p) noexcept {
+    ::new (static_cast<void*>(p)) U;
+  }
+  template <typename U, typename... Args>
+  void construct(U* p, Args&&... args) {
+    ::new (static_cast<void*>(p)) U(std::forward<Args>(args)...);
+  }
+};
+template <typename T>
+using uvector = std::vector<T, DefaultInitAllocator<T>>;
+
 struct RecordBatch {
-  std::vector<uint8_t> codes;    // concatenated letter codes (1..26)
-  std::vector<int64_t> offsets;  // size N+1, offsets[0] == 0
+  uvector<uint8_t> codes;    // concatenated letter codes (1..26)
+  uvector<int64_t> offsets;  // size N+1, offsets[0] == 0
 
   RecordBatch() : offsets(1, 0) {}
   int64_t size() const { return static_cast<int64_t>(offsets.size()) - 1; }

@@ -1,6 +1,7 @@
 #include "moc/io.hpp"
 
 #include <omp.h>
+#include <sys/stat.h>
 
 #include <algorithm>
 #include <cerrno>
@@ -11,7 +12,18 @@ namespace moc {
 
 namespace {
 
-inline bool is_space(unsigned char c) { return c == ' ' || c == '\n' || c == '\r' || c == '\t' || c == '\v' || c == '\f'; }
+// fscanf's separators: ' ' and \t \n \v \f \r (0x09..0x0d)
+inline bool is_space(unsigned char c) { return c == ' ' || static_cast<unsigned char>(c - 9) <= 4; }
+
+// letter -> code (1..26, either case), 0 for anything else
+struct CodeTable {
+  uint8_t v[256];
+  CodeTable() {
+    for (int c = 0; c < 256; ++c) v[c] = static_cast<uint8_t>(letter_code(static_cast<unsigned char>(c)));
+  }
+  uint8_t operator[](unsigned char c) const { return v[c]; }
+};
+const CodeTable kCodeOf;
 
 struct Cursor {
   const char* p;
@@ -39,12 +51,27 @@ int64_t parse_int(const char* b, const char* e, const char* what) {
 
 }  // namespace
 
-std::vector<char> read_stream(FILE* f) {
-  std::vector<char> buf;
-  size_t cap = 1 << 20, len = 0;
+uvector<char> read_stream(FILE* f) {
+  uvector<char> buf;
+  size_t len = 0;
+  struct stat st;
+  if (fstat(fileno(f), &st) == 0 && S_ISREG(st.st_mode) && st.st_size > 0) {
+    // regular file: one allocation of the remaining size (+1 to detect growth), one read
+    const long pos = std::ftell(f);
+    const size_t want = static_cast<size_t>(st.st_size) - static_cast<size_t>(pos > 0 ? pos : 0) + 1;
+    buf.resize(want);
+    len = std::fread(buf.data(), 1, want, f);
+    if (len < want) {
+      if (std::ferror(f)) throw Error("error while reading input stream");
+      buf.resize(len);
+      return buf;
+    }
+  }
+  // pipe / terminal (or a file that grew): read in growing blocks; new memory is not zero-filled
+  size_t cap = std::max<size_t>(buf.size(), size_t{1} << 20);
   buf.resize(cap);
   while (true) {
-    size_t got = std::fread(buf.data() + len, 1, cap - len, f);
+    const size_t got = std::fread(buf.data() + len, 1, cap - len, f);
     len += got;
     if (len < cap) {
       if (std::ferror(f)) throw Error("error while reading input stream");
@@ -85,34 +112,45 @@ Problem parse_problem(const char* data, size_t len, const ParseOptions& opt) {
   int nthreads = omp_get_max_threads();
   if (area_len < (size_t{1} << 16)) nthreads = 1;
   nthreads = std::max(1, nthreads);
+  const unsigned char* ua = reinterpret_cast<const unsigned char*>(area);
 
-  // Chunk starts moved forward to a token start: a token belongs to the chunk holding its first byte.
+  // Chunk boundaries moved forward past any token they cut, so every token lies inside one chunk.
   std::vector<size_t> start(nthreads + 1);
   for (int t = 0; t <= nthreads; ++t) start[t] = area_len * static_cast<size_t>(t) / nthreads;
   for (int t = 1; t < nthreads; ++t) {
-    size_t s = start[t];
-    while (s < area_len && s > 0 && !is_space(static_cast<unsigned char>(area[s - 1]))) ++s;
-    start[t] = std::max(s, start[t - 1]);
+    size_t s0 = start[t];
+    while (s0 < area_len && s0 > 0 && !is_space(ua[s0 - 1])) ++s0;
+    start[t] = std::max(s0, start[t - 1]);
   }
   start[nthreads] = area_len;
 
+  // pass 1 (branch-free, vectorisable): tokens = space->letter transitions, letters = non-space bytes
   std::vector<int64_t> tok_count(nthreads + 1, 0), char_count(nthreads + 1, 0);
-  std::vector<int64_t> bad_pos(nthreads, -1);
+  std::vector<int64_t> bad_tok(nthreads, -1);
 #pragma omp parallel num_threads(nthreads)
   {
     const int t = omp_get_thread_num();
-    Cursor c{area + start[t], area + start[t + 1]};
-    const char *tb = nullptr, *te = nullptr;
+    const size_t b = start[t], e = start[t + 1];
     int64_t nt = 0, nc = 0;
-    // A token may run past the chunk end; Cursor stops at the chunk end only for the *start*.
-    c.end = area + area_len;
-    while (true) {
-      // skip spaces but never start a token at/after our chunk end
-      while (c.p < area + start[t + 1] && is_space(static_cast<unsigned char>(*c.p))) ++c.p;
-      if (c.p >= area + start[t + 1]) break;
-      c.next(tb, te);
-      ++nt;
-      nc += te - tb;
+    if (b < e) {  // a chunk starts at a token start or at whitespace
+      const int64_t first = is_space(ua[b]) ? 0 : 1;
+      nt = first;
+      nc = first;
+      // independent iterations (the previous byte is re-read, not carried): vectorises; 8-bit lanes
+      // summed per 255-byte block so the counters cannot overflow
+      for (size_t blk = b + 1; blk < e; blk += 255) {
+        const size_t be = std::min(e, blk + 255);
+        unsigned t_cnt = 0, c_cnt = 0;
+        for (size_t i = blk; i < be; ++i) {
+          const unsigned char c = ua[i], p = ua[i - 1];
+          const unsigned lt = (c != ' ') & (static_cast<unsigned char>(c - 9) > 4);  // c is a token byte
+          const unsigned ps = (p == ' ') | (static_cast<unsigned char>(p - 9) <= 4);  // p is whitespace
+          t_cnt += lt & ps;
+          c_cnt += lt;
+        }
+        nt += t_cnt;
+        nc += c_cnt;
+      }
     }
     tok_count[t + 1] = nt;
     char_count[t + 1] = nc;
@@ -126,55 +164,66 @@ Problem parse_problem(const char* data, size_t len, const ParseOptions& opt) {
     throw Error("expected " + std::to_string(n) + " Seq2 records, found only " + std::to_string(total_tokens));
 
   // Only the first n tokens are records (extra trailing tokens are ignored, like the reference).
-  int64_t n_chars = 0;
-  {
-    // characters of the first n tokens: find the thread holding token n-1 and count precisely
-    n_chars = char_count[nthreads];
-    if (total_tokens > n) {
-      n_chars = 0;
-      Cursor c{area, area + area_len};
-      // rare path (extra tokens): sequential recount of the first n token lengths
-      for (int64_t i = 0; i < n; ++i) {
-        c.next(b, e);
-        n_chars += e - b;
-      }
+  int64_t n_chars = char_count[nthreads];
+  if (total_tokens > n) {  // rare path: count the letters of the first n tokens exactly
+    n_chars = 0;
+    Cursor c{area, area + area_len};
+    for (int64_t i = 0; i < n; ++i) {
+      c.next(b, e);
+      n_chars += e - b;
     }
   }
-  prob.seq2.codes.resize(static_cast<size_t>(n_chars));
-  prob.seq2.offsets.assign(static_cast<size_t>(n) + 1, 0);
+  prob.seq2.codes.resize(static_cast<size_t>(n_chars));  // uninitialised: pass 2 writes every byte
+  prob.seq2.offsets.resize(static_cast<size_t>(n) + 1);
+  prob.seq2.offsets[0] = 0;
   uint8_t* codes = prob.seq2.codes.data();
   int64_t* offs = prob.seq2.offsets.data();
 
+  // pass 2: encode letters and record token ends (token by token; table lookups), tracking each
+  // thread's longest record and first offending record for the checks below
+  std::vector<int64_t> max_len(nthreads, 0), long_tok(nthreads, -1), long_len(nthreads, 0);
 #pragma omp parallel num_threads(nthreads)
   {
     const int t = omp_get_thread_num();
     int64_t tok = tok_count[t];
     int64_t pos = char_count[t];
-    Cursor c{area + start[t], area + area_len};
-    const char *tb = nullptr, *te = nullptr;
+    int64_t first_bad = -1, mx = 0, lt = -1, ll = 0;
+    size_t i = start[t];
+    const size_t e = start[t + 1];
     while (tok < n) {
-      while (c.p < area + start[t + 1] && is_space(static_cast<unsigned char>(*c.p))) ++c.p;
-      if (c.p >= area + start[t + 1]) break;
-      c.next(tb, te);
-      for (const char* q = tb; q < te; ++q) {
-        int code = letter_code(static_cast<unsigned char>(*q));
-        if (code == 0 && bad_pos[t] < 0) bad_pos[t] = tok;
-        codes[pos++] = static_cast<uint8_t>(code);
+      while (i < e && is_space(ua[i])) ++i;
+      if (i >= e) break;
+      const int64_t p0 = pos;
+      unsigned bad = 0;
+      while (i < e && !is_space(ua[i])) {
+        const uint8_t code = kCodeOf[ua[i++]];
+        bad |= (code == 0);
+        codes[pos++] = code;
       }
-      offs[tok + 1] = pos;
-      ++tok;
+      const int64_t L = pos - p0;
+      if (bad && first_bad < 0) first_bad = tok;
+      if (l2_cap > 0 && L > l2_cap && lt < 0) {
+        lt = tok;
+        ll = L;
+      }
+      mx = std::max(mx, L);
+      offs[++tok] = pos;
     }
+    bad_tok[t] = first_bad;
+    max_len[t] = mx;
+    long_tok[t] = lt;
+    long_len[t] = ll;
   }
-  for (int t = 0; t < nthreads; ++t)
-    if (bad_pos[t] >= 0) throw Error("Seq2 record #" + std::to_string(bad_pos[t]) + " contains a non-letter character");
-
-  if (l2_cap > 0) {
-    for (int64_t i = 0; i < n; ++i)
-      if (prob.seq2.length(i) > l2_cap)
-        throw Error("Seq2 record #" + std::to_string(i) + " has " + std::to_string(prob.seq2.length(i)) +
-                    " letters, limit is " + std::to_string(l2_cap));
+  int64_t longest = 0;
+  for (int t = 0; t < nthreads; ++t) {
+    if (bad_tok[t] >= 0 && bad_tok[t] < n)
+      throw Error("Seq2 record #" + std::to_string(bad_tok[t]) + " contains a non-letter character");
+    if (long_tok[t] >= 0 && long_tok[t] < n)
+      throw Error("Seq2 record #" + std::to_string(long_tok[t]) + " has " + std::to_string(long_len[t]) +
+                  " letters, limit is " + std::to_string(l2_cap));
+    longest = std::max(longest, max_len[t]);
   }
-  validate_score_range(prob.weights, std::max<int64_t>(prob.seq2.max_length(), 1));
+  validate_score_range(prob.weights, std::max<int64_t>(longest, 1));
   return prob;
 }
 
@@ -339,11 +388,25 @@ std::string format_results(const Result* results, int64_t n, int64_t first_index
 }
 
 void write_results(FILE* f, const Result* results, int64_t n, int64_t first_index) {
-  const int64_t kBlock = int64_t{1} << 22;  // bound the formatting buffer for huge N
+  // rows are formatted in parallel into per-thread buffers (never zero-filled, never concatenated)
+  // and written in order; blocks bound the buffer memory for huge N
+  const int64_t kBlock = int64_t{1} << 22;
+  const int nthreads = n > 65536 ? omp_get_max_threads() : 1;
+  std::vector<uvector<char>> parts(static_cast<size_t>(nthreads));
+  std::vector<size_t> used(static_cast<size_t>(nthreads));
   for (int64_t b = 0; b < n; b += kBlock) {
-    const int64_t e = std::min(n, b + kBlock);
-    std::string s = format_results(results + b, e - b, first_index + b);
-    std::fwrite(s.data(), 1, s.size(), f);
+    const int64_t e = std::min(n, b + kBlock), m = e - b;
+#pragma omp parallel num_threads(nthreads)
+    {
+      const int t = omp_get_thread_num();
+      const int64_t rb = b + m * t / nthreads, re = b + m * (t + 1) / nthreads;
+      uvector<char>& buf = parts[t];
+      buf.resize(static_cast<size_t>(re - rb) * kMaxRow);
+      char* p = buf.data();
+      for (int64_t i = rb; i < re; ++i) p = format_row(p, first_index + i, results[i]);
+      used[t] = static_cast<size_t>(p - buf.data());
+    }
+    for (int t = 0; t < nthreads; ++t) std::fwrite(parts[t].data(), 1, used[t], f);
   }
   std::fflush(f);
 }
