@@ -92,6 +92,12 @@ struct BatchHeader {
   int32_t pad;
 };
 
+// An input problem found after the header went out (deferred parsing into the shared window); raised on
+// every rank after a status broadcast, so all of them leave the job the same way (exit code 1).
+struct InputError : Error {
+  using Error::Error;
+};
+
 struct FaultHook {
   std::string phase;
   int rank = 0;
@@ -223,7 +229,8 @@ class Job {
  private:
   void setup_engine(int64_t cells);
   void run_batch(RecordBatch* rb, int64_t n, int64_t total_chars, int64_t first_index);
-  void batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds, bool cp);
+  void batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, bool cp);
+  std::vector<int64_t> make_bounds(const int64_t* offsets, int64_t n, bool cp);
   void batch_mpi(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds, bool cp);
   void batch_rccl(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds, bool cp);
   void print(const Result* r, int64_t n, int64_t first_index);  // first_index relative to the batch
@@ -242,6 +249,8 @@ class Job {
   double compute_ms_ = 0;
   int64_t cells_ = 0, chars_ = 0, records_ = 0, batches_ = 0;
   int64_t first_index_ = 0;      // global index of the current batch's first record
+  uvector<char> text_;                 // root: the input (kept for deferred parsing)
+  std::unique_ptr<BulkParser> parser_;  // root: pass 1 done, letters encoded straight into the window
   std::vector<Result> results_;  // root: results of the current batch (mpi/rccl transports)
 };
 
@@ -307,31 +316,42 @@ void Job::run_batch(RecordBatch* rb, int64_t n, int64_t total_chars, int64_t fir
   first_index_ = first_index;
   records_ += n;
   chars_ += total_chars;
-  const int p = ctx_.size;
   const bool cp = partition_ == "offsets";
+  if (transport_ == "shm") {  // the window is filled first; the bounds come from it
+    batch_shm(rb, n, total_chars, cp);
+    return;
+  }
+  const std::vector<int64_t> bounds = make_bounds(ctx_.rank == kRoot ? rb->offsets.data() : nullptr, n, cp);
+  if (transport_ == "mpi")
+    batch_mpi(rb, n, total_chars, bounds, cp);
+  else
+    batch_rccl(rb, n, total_chars, bounds, cp);
+}
+
+// Root: record lengths -> search cells (for --timing) and the cost-balanced rank bounds; broadcast.
+std::vector<int64_t> Job::make_bounds(const int64_t* offsets, int64_t n, bool cp) {
+  const int p = ctx_.size;
   std::vector<int64_t> bounds(static_cast<size_t>(p) + 1, 0);
   if (ctx_.rank == kRoot) {
     const int64_t L1 = static_cast<int64_t>(eng_.seq1.size());
     std::vector<int64_t> len(static_cast<size_t>(n));
+    int64_t cells = 0;
+#pragma omp parallel for reduction(+ : cells) schedule(static) if (n > 65536)
     for (int64_t i = 0; i < n; ++i) {
-      len[i] = rb->length(i);
-      cells_ += record_cells(L1, len[i]);
+      len[i] = offsets[i + 1] - offsets[i];
+      cells += record_cells(L1, len[i]);
     }
+    cells_ += cells;
     if (!cp) {
       CostModel cm = all_gpu_ ? CostModel{1.0, 200.0, 2400.0} : CostModel{1.0, 4.0, 64.0};
       bounds = partition_ == "even" ? partition_even(n, p) : partition_by_cost(len.data(), n, L1, p, cm);
     }
   }
   if (!cp) bcast_bytes(bounds.data(), sizeof(int64_t) * (p + 1), kRoot, ctx_.world);
-  if (transport_ == "shm")
-    batch_shm(rb, n, total_chars, bounds, cp);
-  else if (transport_ == "mpi")
-    batch_mpi(rb, n, total_chars, bounds, cp);
-  else
-    batch_rccl(rb, n, total_chars, bounds, cp);
+  return bounds;
 }
 
-void Job::batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds, bool cp) {
+void Job::batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, bool cp) {
   // layout: offsets[(N+1)] | results[N] (or keys[N] in cp mode) | codes[total]   (8-byte aligned sections)
   const int64_t off_bytes = 8 * (n + 1);
   const int64_t res_bytes = ((12 * n) + 7) & ~int64_t{7};
@@ -340,23 +360,42 @@ void Job::batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, const std::
   int64_t* w_offs = reinterpret_cast<int64_t*>(win->base());
   Result* w_res = reinterpret_cast<Result*>(win->base() + off_bytes);
   uint8_t* w_codes = reinterpret_cast<uint8_t*>(win->base() + off_bytes + res_bytes);
+  int32_t status = 0;
+  std::string error;
   if (ctx_.rank == kRoot) {
-    const int64_t* src_off = rb->offsets.data();
-    const uint8_t* src_codes = rb->codes.data();
-    const int nt = total_chars > (1 << 20) ? omp_get_max_threads() : 1;
+    if (parser_) {  // deferred pass 2: letters encoded straight into the window, no intermediate copy
+      try {
+        parser_->fill(w_codes, w_offs);
+      } catch (const std::exception& e) {
+        status = 1;
+        error = e.what();
+      }
+      parser_.reset();
+      text_ = uvector<char>();
+    } else {
+      const int64_t* src_off = rb->offsets.data();
+      const uint8_t* src_codes = rb->codes.data();
+      const int nt = total_chars > (1 << 20) ? omp_get_max_threads() : 1;
 #pragma omp parallel num_threads(nt)
-    {
-      const int t = omp_get_thread_num();
-      const int64_t cb = total_chars * t / nt, ce = total_chars * (t + 1) / nt;
-      std::memcpy(w_codes + cb, src_codes + cb, static_cast<size_t>(ce - cb));
-      const int64_t ob = (n + 1) * t / nt, oe = (n + 1) * (t + 1) / nt;
-      std::memcpy(w_offs + ob, src_off + ob, static_cast<size_t>(oe - ob) * 8);
+      {
+        const int t = omp_get_thread_num();
+        const int64_t cb = total_chars * t / nt, ce = total_chars * (t + 1) / nt;
+        std::memcpy(w_codes + cb, src_codes + cb, static_cast<size_t>(ce - cb));
+        const int64_t ob = (n + 1) * t / nt, oe = (n + 1) * (t + 1) / nt;
+        std::memcpy(w_offs + ob, src_off + ob, static_cast<size_t>(oe - ob) * 8);
+      }
+      *rb = RecordBatch{};  // the window is now the only copy
     }
-    *rb = RecordBatch{};  // the window is now the only copy
+  }
+  bcast_bytes(&status, sizeof status, kRoot, ctx_.world);
+  if (status != 0) {
+    win.reset();  // collective, on every rank, before leaving
+    throw InputError(error);
   }
   fault_.at("distribute", ctx_.rank);
   win->fence();
   pt_.end();
+  const std::vector<int64_t> bounds = make_bounds(ctx_.rank == kRoot ? w_offs : nullptr, n, cp);
   pt_.begin("compute");
   fault_.at("compute", ctx_.rank);
   Stopwatch sw;
@@ -552,16 +591,26 @@ int Job::run() {
         h.first_index = reader->skip(skip);
         h.cells = -1;
       } else {
-        uvector<char> text = read_stream(in);
-        Problem prob = parse_problem(text.data(), text.size(), po);
-        w = prob.weights;
-        seq1 = std::move(prob.seq1);
-        bulk = std::move(prob.seq2);
-        h.n_total = bulk.size();
+        text_ = read_stream(in);
+        auto parser = std::make_unique<BulkParser>(text_.data(), text_.size(), po);  // header + pass 1
+        w = parser->weights();
+        seq1 = parser->seq1();
+        h.n_total = parser->count();
         h.first_index = std::min<int64_t>(skip, h.n_total);
-        drop_front(bulk, h.first_index);
-        h.cells = 0;
-        for (int64_t i = 0; i < bulk.size(); ++i) h.cells += record_cells(static_cast<int64_t>(seq1.size()), bulk.length(i));
+        h.cells = parser->cells_estimate();
+        // shm transport (the single-node default) without a skip: pass 2 later writes straight into
+        // the node-shared window; otherwise encode now into a private batch
+        const std::string tr = to_lower(flags_.get("transport", "auto"));
+        const bool into_window = h.first_index == 0 && (tr == "shm" || (tr == "auto" && ctx_.single_node()));
+        if (into_window) {
+          parser_ = std::move(parser);
+        } else {
+          bulk.codes.resize(static_cast<size_t>(parser->total_chars()));
+          bulk.offsets.resize(static_cast<size_t>(parser->count()) + 1);
+          parser->fill(bulk.codes.data(), bulk.offsets.data());
+          text_ = uvector<char>();
+          drop_front(bulk, h.first_index);
+        }
       }
       for (int i = 0; i < 4; ++i) h.w[i] = w.w[i];
     } catch (const std::exception& e) {
@@ -595,8 +644,18 @@ int Job::run() {
   int rc = 0;
   if (!streaming) {
     int64_t sizes[2] = {bulk.size(), bulk.total_chars()};
+    if (parser_) {
+      sizes[0] = parser_->count();
+      sizes[1] = parser_->total_chars();
+    }
     bcast_bytes(sizes, sizeof sizes, kRoot, ctx_.world);
-    run_batch(ctx_.rank == kRoot ? &bulk : nullptr, sizes[0], sizes[1], h.first_index);
+    try {
+      run_batch(ctx_.rank == kRoot ? &bulk : nullptr, sizes[0], sizes[1], h.first_index);
+    } catch (const InputError& e) {
+      if (ctx_.rank == kRoot) std::fprintf(stderr, "input error: %s\n", e.what());
+      if (in != stdin && in) std::fclose(in);
+      return 1;
+    }
   } else {
     // root: parse of batch b+1 runs on a helper thread while batch b is searched and printed
     const int64_t max_rec = batch_records > 0 ? batch_records : INT64_MAX;

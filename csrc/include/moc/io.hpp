@@ -28,6 +28,32 @@ struct ParseOptions {
 // Reads the whole stream into memory (bulk fread; no per-token stdio).
 uvector<char> read_stream(FILE* f);
 
+// Two-phase parser of an in-memory input: the constructor reads the header and counts the records and
+// letters (parallel pass 1); fill() encodes them into caller-provided buffers (parallel pass 2) — e.g.
+// straight into a node-shared window, with no intermediate copy. `data` must outlive fill().
+class BulkParser {
+ public:
+  BulkParser(const char* data, size_t len, const ParseOptions& opt = {});
+  const Weights& weights() const { return weights_; }
+  const std::vector<uint8_t>& seq1() const { return seq1_; }
+  int64_t count() const { return n_; }
+  int64_t total_chars() const { return total_chars_; }
+  // codes[0..total_chars()), offsets[0..count()] (offsets[0] = 0); throws on non-letters / limits.
+  void fill(uint8_t* codes, int64_t* offsets) const;
+  // n * (L1 - avg + 1) * avg from the mean record length (before fill; for engine selection).
+  int64_t cells_estimate() const;
+
+ private:
+  Weights weights_{};
+  std::vector<uint8_t> seq1_;
+  int64_t n_ = 0, total_chars_ = 0, l2_cap_ = 0;
+  const char* area_ = nullptr;
+  size_t area_len_ = 0;
+  int nthreads_ = 1;
+  std::vector<size_t> start_;
+  std::vector<int64_t> tok_count_, char_count_;
+};
+
 // Parses "W1 W2 W3 W4 / Seq1 / N / Seq2 x N" (PDF p.5-6). Whitespace of any kind (incl. CRLF)
 // separates tokens, exactly like fscanf %d/%s. Throws moc::Error with a precise message.
 Problem parse_problem(const char* data, size_t len, const ParseOptions& opt = {});

@@ -2,6 +2,7 @@
 
 #include <omp.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cerrno>
@@ -84,8 +85,7 @@ uvector<char> read_stream(FILE* f) {
   return buf;
 }
 
-Problem parse_problem(const char* data, size_t len, const ParseOptions& opt) {
-  Problem prob;
+BulkParser::BulkParser(const char* data, size_t len, const ParseOptions& opt) {
   Cursor cur{data, data + len};
   const char *b, *e;
   static const char* wname[4] = {"W1", "W2", "W3", "W4"};
@@ -93,44 +93,43 @@ Problem parse_problem(const char* data, size_t len, const ParseOptions& opt) {
     if (!cur.next(b, e)) throw Error(std::string("unexpected end of input while reading ") + wname[i]);
     int64_t v = parse_int(b, e, wname[i]);
     if (v < 0 || v > INT32_MAX) throw Error(std::string(wname[i]) + " out of range");
-    prob.weights.w[i] = static_cast<int32_t>(v);
+    weights_.w[i] = static_cast<int32_t>(v);
   }
   if (!cur.next(b, e)) throw Error("unexpected end of input while reading Seq1");
-  prob.seq1 = encode_sequence(b, e - b);
+  seq1_ = encode_sequence(b, e - b);
   if (!cur.next(b, e)) throw Error("unexpected end of input while reading the number of sequences");
-  const int64_t n = parse_int(b, e, "number_of_sequences");
-  if (n < 0) throw Error("number_of_sequences must be >= 0");
+  n_ = parse_int(b, e, "number_of_sequences");
+  if (n_ < 0) throw Error("number_of_sequences must be >= 0");
 
   const int64_t l1_cap = opt.strict_limits ? kSpecMaxSeq1 : opt.max_l1;
-  const int64_t l2_cap = opt.strict_limits ? kSpecMaxSeq2 : opt.max_l2;
-  if (l1_cap > 0 && prob.L1() > l1_cap)
-    throw Error("Seq1 has " + std::to_string(prob.L1()) + " letters, limit is " + std::to_string(l1_cap));
+  l2_cap_ = opt.strict_limits ? kSpecMaxSeq2 : opt.max_l2;
+  if (l1_cap > 0 && static_cast<int64_t>(seq1_.size()) > l1_cap)
+    throw Error("Seq1 has " + std::to_string(seq1_.size()) + " letters, limit is " + std::to_string(l1_cap));
 
-  // ---- parallel two-pass tokenisation of the record area -------------------------------------
-  const char* area = cur.p;
-  const size_t area_len = static_cast<size_t>(cur.end - cur.p);
+  // ---- pass 1 over the record area (parallel) -------------------------------------------------
+  area_ = cur.p;
+  area_len_ = static_cast<size_t>(cur.end - cur.p);
   int nthreads = omp_get_max_threads();
-  if (area_len < (size_t{1} << 16)) nthreads = 1;
-  nthreads = std::max(1, nthreads);
-  const unsigned char* ua = reinterpret_cast<const unsigned char*>(area);
+  if (area_len_ < (size_t{1} << 16)) nthreads = 1;
+  nthreads_ = std::max(1, nthreads);
+  const unsigned char* ua = reinterpret_cast<const unsigned char*>(area_);
 
   // Chunk boundaries moved forward past any token they cut, so every token lies inside one chunk.
-  std::vector<size_t> start(nthreads + 1);
-  for (int t = 0; t <= nthreads; ++t) start[t] = area_len * static_cast<size_t>(t) / nthreads;
-  for (int t = 1; t < nthreads; ++t) {
-    size_t s0 = start[t];
-    while (s0 < area_len && s0 > 0 && !is_space(ua[s0 - 1])) ++s0;
-    start[t] = std::max(s0, start[t - 1]);
+  start_.assign(static_cast<size_t>(nthreads_) + 1, 0);
+  for (int t = 0; t <= nthreads_; ++t) start_[t] = area_len_ * static_cast<size_t>(t) / nthreads_;
+  for (int t = 1; t < nthreads_; ++t) {
+    size_t s0 = start_[t];
+    while (s0 < area_len_ && s0 > 0 && !is_space(ua[s0 - 1])) ++s0;
+    start_[t] = std::max(s0, start_[t - 1]);
   }
-  start[nthreads] = area_len;
-
+  start_[nthreads_] = area_len_;
   // pass 1 (branch-free, vectorisable): tokens = space->letter transitions, letters = non-space bytes
-  std::vector<int64_t> tok_count(nthreads + 1, 0), char_count(nthreads + 1, 0);
-  std::vector<int64_t> bad_tok(nthreads, -1);
-#pragma omp parallel num_threads(nthreads)
+  tok_count_.assign(static_cast<size_t>(nthreads_) + 1, 0);
+  char_count_.assign(static_cast<size_t>(nthreads_) + 1, 0);
+#pragma omp parallel num_threads(nthreads_)
   {
     const int t = omp_get_thread_num();
-    const size_t b = start[t], e = start[t + 1];
+    const size_t b = start_[t], e = start_[t + 1];
     int64_t nt = 0, nc = 0;
     if (b < e) {  // a chunk starts at a token start or at whitespace
       const int64_t first = is_space(ua[b]) ? 0 : 1;
@@ -152,44 +151,45 @@ Problem parse_problem(const char* data, size_t len, const ParseOptions& opt) {
         nc += c_cnt;
       }
     }
-    tok_count[t + 1] = nt;
-    char_count[t + 1] = nc;
+    tok_count_[t + 1] = nt;
+    char_count_[t + 1] = nc;
   }
-  for (int t = 0; t < nthreads; ++t) {
-    tok_count[t + 1] += tok_count[t];
-    char_count[t + 1] += char_count[t];
+  for (int t = 0; t < nthreads_; ++t) {
+    tok_count_[t + 1] += tok_count_[t];
+    char_count_[t + 1] += char_count_[t];
   }
-  const int64_t total_tokens = tok_count[nthreads];
-  if (total_tokens < n)
-    throw Error("expected " + std::to_string(n) + " Seq2 records, found only " + std::to_string(total_tokens));
+  const int64_t total_tokens = tok_count_[nthreads_];
+  if (total_tokens < n_)
+    throw Error("expected " + std::to_string(n_) + " Seq2 records, found only " + std::to_string(total_tokens));
 
   // Only the first n tokens are records (extra trailing tokens are ignored, like the reference).
-  int64_t n_chars = char_count[nthreads];
-  if (total_tokens > n) {  // rare path: count the letters of the first n tokens exactly
-    n_chars = 0;
-    Cursor c{area, area + area_len};
-    for (int64_t i = 0; i < n; ++i) {
+  total_chars_ = char_count_[nthreads_];
+  if (total_tokens > n_) {  // rare path: count the letters of the first n tokens exactly
+    total_chars_ = 0;
+    Cursor c{area_, area_ + area_len_};
+    for (int64_t i = 0; i < n_; ++i) {
       c.next(b, e);
-      n_chars += e - b;
+      total_chars_ += e - b;
     }
   }
-  prob.seq2.codes.resize(static_cast<size_t>(n_chars));  // uninitialised: pass 2 writes every byte
-  prob.seq2.offsets.resize(static_cast<size_t>(n) + 1);
-  prob.seq2.offsets[0] = 0;
-  uint8_t* codes = prob.seq2.codes.data();
-  int64_t* offs = prob.seq2.offsets.data();
+}
 
+void BulkParser::fill(uint8_t* codes, int64_t* offs) const {
   // pass 2: encode letters and record token ends (token by token; table lookups), tracking each
   // thread's longest record and first offending record for the checks below
-  std::vector<int64_t> max_len(nthreads, 0), long_tok(nthreads, -1), long_len(nthreads, 0);
-#pragma omp parallel num_threads(nthreads)
+  const int nthreads = nthreads_;
+  const int64_t n = n_, l2_cap = l2_cap_;
+  const unsigned char* ua = reinterpret_cast<const unsigned char*>(area_);
+  std::vector<int64_t> bad_tok(nthreads, -1), max_len(nthreads, 0), long_tok(nthreads, -1), long_len(nthreads, 0);
+  offs[0] = 0;
+#pragma omp parallel num_threads(nthreads_)
   {
     const int t = omp_get_thread_num();
-    int64_t tok = tok_count[t];
-    int64_t pos = char_count[t];
+    int64_t tok = tok_count_[t];
+    int64_t pos = char_count_[t];
     int64_t first_bad = -1, mx = 0, lt = -1, ll = 0;
-    size_t i = start[t];
-    const size_t e = start[t + 1];
+    size_t i = start_[t];
+    const size_t e = start_[t + 1];
     while (tok < n) {
       while (i < e && is_space(ua[i])) ++i;
       if (i >= e) break;
@@ -223,7 +223,24 @@ Problem parse_problem(const char* data, size_t len, const ParseOptions& opt) {
                   " letters, limit is " + std::to_string(l2_cap));
     longest = std::max(longest, max_len[t]);
   }
-  validate_score_range(prob.weights, std::max<int64_t>(longest, 1));
+  validate_score_range(weights_, std::max<int64_t>(longest, 1));
+}
+
+int64_t BulkParser::cells_estimate() const {
+  const int64_t L1 = static_cast<int64_t>(seq1_.size());
+  if (n_ <= 0) return 0;
+  const int64_t avg = std::max<int64_t>(1, total_chars_ / n_);
+  return avg <= L1 ? n_ * (L1 - avg + 1) * avg : 0;
+}
+
+Problem parse_problem(const char* data, size_t len, const ParseOptions& opt) {
+  BulkParser p(data, len, opt);
+  Problem prob;
+  prob.weights = p.weights();
+  prob.seq1 = p.seq1();
+  prob.seq2.codes.resize(static_cast<size_t>(p.total_chars()));  // uninitialised: fill writes every byte
+  prob.seq2.offsets.resize(static_cast<size_t>(p.count()) + 1);
+  p.fill(prob.seq2.codes.data(), prob.seq2.offsets.data());
   return prob;
 }
 
@@ -388,12 +405,20 @@ std::string format_results(const Result* results, int64_t n, int64_t first_index
 }
 
 void write_results(FILE* f, const Result* results, int64_t n, int64_t first_index) {
-  // rows are formatted in parallel into per-thread buffers (never zero-filled, never concatenated)
-  // and written in order; blocks bound the buffer memory for huge N
+  // Rows are formatted in parallel into per-thread buffers (never zero-filled, never concatenated).
+  // When the stream is a regular file, every thread writes its part at its own file offset (pwrite), so
+  // multi-GB outputs are written in parallel; otherwise (pipe, terminal) parts go out in order.
+  // Blocks bound the buffer memory for huge N.
   const int64_t kBlock = int64_t{1} << 22;
   const int nthreads = n > 65536 ? omp_get_max_threads() : 1;
+  std::fflush(f);
+  const int fd = fileno(f);
+  struct stat st;
+  off_t file_pos = -1;
+  if (nthreads > 1 && fstat(fd, &st) == 0 && S_ISREG(st.st_mode)) file_pos = lseek(fd, 0, SEEK_CUR);
   std::vector<uvector<char>> parts(static_cast<size_t>(nthreads));
-  std::vector<size_t> used(static_cast<size_t>(nthreads));
+  std::vector<size_t> used(static_cast<size_t>(nthreads) + 1);
+  bool write_error = false;
   for (int64_t b = 0; b < n; b += kBlock) {
     const int64_t e = std::min(n, b + kBlock), m = e - b;
 #pragma omp parallel num_threads(nthreads)
@@ -404,10 +429,34 @@ void write_results(FILE* f, const Result* results, int64_t n, int64_t first_inde
       buf.resize(static_cast<size_t>(re - rb) * kMaxRow);
       char* p = buf.data();
       for (int64_t i = rb; i < re; ++i) p = format_row(p, first_index + i, results[i]);
-      used[t] = static_cast<size_t>(p - buf.data());
+      used[t + 1] = static_cast<size_t>(p - buf.data());
+      if (file_pos >= 0) {
+#pragma omp barrier
+#pragma omp single
+        for (int q = 0; q < nthreads; ++q) used[q + 1] += used[q];  // used[t] = byte offset of part t
+        // (implicit barrier after single)
+        size_t done = 0;
+        const size_t len = used[t + 1] - used[t];
+        while (done < len) {
+          const ssize_t w = pwrite(fd, buf.data() + done, len - done, file_pos + static_cast<off_t>(used[t] + done));
+          if (w <= 0) {
+#pragma omp atomic write
+            write_error = true;
+            break;
+          }
+          done += static_cast<size_t>(w);
+        }
+      }
     }
-    for (int t = 0; t < nthreads; ++t) std::fwrite(parts[t].data(), 1, used[t], f);
+    if (file_pos >= 0) {
+      file_pos += static_cast<off_t>(used[nthreads]);
+    } else {
+      for (int t = 0; t < nthreads; ++t) std::fwrite(parts[t].data(), 1, used[t + 1], f);
+    }
+    used[0] = 0;
   }
+  if (file_pos >= 0 && lseek(fd, file_pos, SEEK_SET) < 0) write_error = true;
+  if (write_error) throw Error("error while writing the results");
   std::fflush(f);
 }
 

@@ -171,3 +171,17 @@ def test_cmake_build_matches(tmp_path):
         out = subprocess.run([MPIEXEC, "-np", "2", str(bdir / "final"), "--backend=cpu"], input=f.read(),
                              capture_output=True, timeout=120)
     assert out.returncode == 0 and out.stdout.decode() == expected(4)
+
+
+@pytest.mark.parametrize("transport", ["shm", "mpi"])
+@pytest.mark.parametrize("np_", [1, 3])
+def test_record_error_after_header(transport, np_):
+    # with the shm transport the records are encoded straight into the shared window after the header
+    # went out; a bad record must still end every rank with exit code 1 and the record's index
+    text = b"1 2 3 4\nABCDEFG\n4\nABC\nABD\nAB1\nAC\n"
+    r = run_final(["--backend=cpu", f"--transport={transport}"], stdin_bytes=text, np_=np_)
+    assert r.returncode == 1, r.stderr.decode()
+    assert b"record #2" in r.stderr and r.stdout == b""
+    ok = b"1 2 3 4\nABCDEFG\n3\nAB\nABCD\nAC\n"
+    r = run_final(["--backend=cpu", f"--transport={transport}", "--max-l2=2"], stdin_bytes=ok, np_=np_)
+    assert r.returncode == 1 and b"record #1 has 4 letters, limit is 2" in r.stderr

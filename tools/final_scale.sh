@@ -1,0 +1,15 @@
+# End-to-end ./final at scale on one GPU (BASELINE.json "wall-clock" with 10^9 letters): generate an
+# input6-shaped file, then time the whole job (read + parse + search + print to a file) and its phases.
+set -e
+mkdir -p gpurun_out
+F=/tmp/moc_big6.txt
+timeout -k 10 300 python3 tools/gen_synthetic.py --shape input6 --records ${RECORDS:-134217728} --out $F
+for mode in "" "--batch-records=16777216"; do
+  s=$(date +%s%N)
+  timeout -k 10 300 /opt/conda/bin/mpiexec -np 1 ./final --timing --input=$F $mode > /tmp/moc_big6.out \
+    2> gpurun_out/final_scale_timing.txt
+  e=$(date +%s%N)
+  echo "mode='$mode' wall_ms=$(( (e - s) / 1000000 )) out_bytes=$(stat -c %s /tmp/moc_big6.out) $(tail -1 gpurun_out/final_scale_timing.txt)"
+done
+head -c 300 /tmp/moc_big6.out
+rm -f $F /tmp/moc_big6.out
