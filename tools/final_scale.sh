@@ -4,7 +4,7 @@ set -e
 mkdir -p gpurun_out
 F=/tmp/moc_big6.txt
 timeout -k 10 300 python3 tools/gen_synthetic.py --shape input6 --records ${RECORDS:-134217728} --out $F
-for mode in "" "--batch-records=16777216"; do
+for mode in "" "--pin-window=0" "--batch-records=16777216"; do
   s=$(date +%s%N)
   timeout -k 10 300 /opt/conda/bin/mpiexec -np 1 ./final --timing --input=$F $mode > /tmp/moc_big6.out \
     2> gpurun_out/final_scale_timing.txt
