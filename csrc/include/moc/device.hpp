@@ -4,18 +4,23 @@
 // cudaDeviceSynchronize, launched with grid = ceil(rows*2000/1024) blocks of which at most two hold
 // work, with a serial (offset, mutant) loop inside every thread (cudaFunctions.cu:116-167).
 //
-// Here: one launch per *batch*. Parallelism is over offsets (diagonals): every lane owns one offset
-// `o` and streams over the Seq2 positions, keeping its running diagonal prefix sum P_o in a register;
-// the neighbour diagonal's P_{o+1} comes from lane+1 through a DPP wave shift, so a cell costs one LDS
-// gather plus a handful of VALU ops, and no atomics or barriers (design: SURVEY.md §7.3).
+// Here: one launch per *batch*, three kernels chosen per batch (design: SURVEY.md §7.3):
+//   * swipe kernel (swipe_kernels.hip): tiny problems (|Seq1| <= 200, |Seq2| <= 32, int16-exact
+//     weights): one LANE per record, all of its offsets' running sums in registers as packed int16
+//     pairs — two cells per VALU op, no cross-lane traffic; the headline (input6-shaped) path.
+//   For the others parallelism is over offsets (diagonals): every lane owns one offset `o` and streams
+//   over the Seq2 positions, keeping its running diagonal prefix sum P_o in a register; the neighbour
+//   diagonal's P_{o+1} comes from lane+1 through a DPP wave shift, so a cell costs one LDS gather plus a
+//   handful of VALU ops, and no atomics or barriers.
 //   * short kernel: records whose offset range fits in a wave (L1-L2+1 <= 64 lanes) are packed
 //     several per wave in fixed-width lane slots (the input6-shaped regime). Persistent blocks pull
 //     tiles of ~1K records, stage their letters in LDS with 16-byte loads — straight from pinned host
 //     memory when the batch lives there (zero-copy streaming: PCIe is the bound, so no staging copy) —
 //     and score against a per-block LDS profile S[c][j] = T[c][Seq1[j]].
-//   * tile kernel: longer offset ranges are cut into 63-offset tiles (lane 63 is the helper diagonal)
-//     listed by the host planner; partial maxima merge through one 64-bit atomicMax per wave on an
-//     order-free packed key (score, -(o*L2+k)) — deterministic tie-break, no races (fixes B9).
+//   * tile kernel: longer offset ranges are cut into wave tiles of U x 63 offsets (lane 63 of each
+//     sub-tile is its helper diagonal), walked by persistent waves in cost-balanced runs planned on the
+//     host; partial maxima merge through one 64-bit atomicMax per record run on an order-free packed
+//     key (score, -(o*L2+k)) — deterministic tie-break, no races (fixes B9).
 #pragma once
 
 #include <hip/hip_runtime_api.h>

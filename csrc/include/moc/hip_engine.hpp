@@ -86,7 +86,7 @@ class HipEngine {
                     Result* d_out, hipStream_t stream);
 
   // Context-parallel search: this engine evaluates part `part` of `parts` of the batch's
-  // global list of 63-offset tiles and writes one packed 64-bit key per record (moc::encode_key; 0 =
+  // global list of offset tiles and writes one packed 64-bit key per record (moc::encode_key; 0 =
   // no candidate in this part). A MAX all-reduce of the keys over the parts + finalize_keys gives the
   // full answer; this splits single huge records across GPUs.
   void search_keys_device(const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets, int64_t n,

@@ -1,12 +1,18 @@
-// Long-record search kernels (gfx950, wave64): one wave = (record, 63 consecutive offsets).
+// Long-record search kernels (gfx950, wave64). Work unit: a wave tile = (record, 63·U consecutive
+// offsets) as U sub-tiles of 63 owned offsets + 1 helper lane that advance together (they share each
+// Seq2 letter; their dependency chains interleave). Persistent waves walk cost-balanced contiguous runs
+// of the record-major tile list (host plan: moc::HipEngine::plan_waves), keeping a record's letters in
+// registers and its running best key across the run (one reduction + atomic per record run).
 //
 // Replaces calc_result (cudaFunctions.cu:63-176) for records whose offset range does not fit in one
 // wave (L1 - L2 + 1 > 64; input3/input4-shaped). See moc/device.hpp for the design summary and
 // csrc/include/moc/cpu_engine.hpp for the closed form
 //     score(o, 0) = Tot_o,   score(o, k>=1) = P_o(k) - P_{o+1}(k) + Tot_{o+1}.
 // Per lane (= one offset o) and per Seq2 position i:
-//     x   = Seq1[o+i]           (shifted in from lane+1 with DPP; lane 63 gets a wave-uniform LDS read)
-//     P  += LUT[Seq2[i]][x]     (one conflict-free ds_read_b32: <= 27 distinct consecutive dwords)
+//     x   = Seq1[o+i]           (shifted in from lane+1 with DPP; lane 63 gets the next Seq1 letter,
+//                                 64 of them fetched per load and pulled out with v_readlane)
+//     P  += LUT[Seq2[i]][x]     (one conflict-free ds_read_b32: <= 27 distinct consecutive dwords;
+//                                 Seq2[i] arrives 64 letters per load, broadcast with v_readlane)
 //     Pn  = P of lane+1         (DPP wave_shl:1 — the neighbouring diagonal, no LDS traffic)
 //     key = max(key, pack(P - Pn, k = i+1))   (ties -> smallest k, exactly the reference order)
 // Lane 63 only provides the helper diagonal; the wave's best candidate goes to the record's slot with

@@ -222,7 +222,7 @@ class HipSearchEngine:
 
     def search_keys(self, codes: np.ndarray, offsets: np.ndarray, part: int, parts: int) -> np.ndarray:
         """Context-parallel partial search on the GPU: this engine's share (part of parts) of the batch's
-        63-offset tiles -> packed uint64 keys per record (see :func:`search_keys_cpu`)."""
+        offset tiles -> packed uint64 keys per record (see :func:`search_keys_cpu`)."""
         codes = np.ascontiguousarray(codes, dtype=np.uint8)
         offsets = np.ascontiguousarray(offsets, dtype=np.int64)
         n = offsets.shape[0] - 1
