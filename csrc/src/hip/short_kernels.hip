@@ -152,18 +152,27 @@ __global__ __launch_bounds__(kBlock) void short_search_kernel(ProblemView pv, Sh
       const uint8_t* rec = codes_l + shift_b + roff;
       int P = 0;
       typename K::T best = K::min();
-      for (int i = 0; i < steps; ++i) {
+      // 8 steps per round: the letter and table reads of the round are issued together (independent
+      // LDS reads in flight), then the dependent prefix / neighbour / key chain consumes them
+      auto gather = [&](int i) {
         const int c = (on && i < L2) ? rec[i] : 0;
-        int v;
-        if (Profile)
-          v = table[c * lay.row + o + i];
-        else
-          v = table[(c << 5) | s1l[o + i]];
+        return Profile ? table[c * lay.row + o + i] : table[(c << 5) | s1l[o + i]];
+      };
+      auto step = [&](int v, int i) {
         P += v;
         const int Pn = wave_shl1(P);
         const typename K::T key = K::make(P - Pn, i + 1, shift, mask);
         best = key > best ? key : best;
+      };
+      int i = 0;
+      for (; i + 8 <= steps; i += 8) {
+        int v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = gather(i + j);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) step(v[j], i + j);
       }
+      for (; i < steps; ++i) step(gather(i), i);
       const int Pn = wave_shl1(P);
       unsigned long long key = lane_candidate<Wide>(on, o, L1, L2, pv.semantics, P, Pn, best, shift, mask);
       for (int d = 1; d < slot; d <<= 1) {  // segmented suffix max within the slot

@@ -48,7 +48,8 @@ inline int al16(int x) { return (x + 15) & ~15; }
 
 SwipeLayout swipe_layout(int L1, int noff, int l2w, int tile_records, int codes_cap, int fb) {
   SwipeLayout l;
-  l.row = (std::max(L1, 4 * l2w) + noff + 8 + 7) & ~7;
+  // a multiple of 64 int16 (8 chunks of 16 B) so the per-letter XOR swizzle of chunk indices stays in the row
+  l.row = (std::max(L1, 4 * l2w) + noff + 8 + 63) & ~63;
   l.copy_elems = kAlphabet * l.row;
   l.prof_bytes = al16(8 * l.copy_elems * 2);
   l.loff_off = l.prof_bytes;
@@ -80,11 +81,15 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
   constexpr int KMASK = (1 << KB) - 1;
   constexpr int NP = NOFF / 2;  // packed accumulators
 
-  // ---- 8 shifted int16 profile copies: prof[s][c][j] = S[c][j + s] (row 0 and j >= L1: 0)
+  // ---- 8 shifted int16 profile copies: prof[s][c][j] = S[c][j + s] (row 0 and j >= L1: 0).
+  //      Rows are 128-byte multiples, so the 16-byte chunk q of every row would start on the same LDS
+  //      bank; chunk q of row c is stored at chunk q ^ (c & 7) instead, spreading the 16 lanes of a
+  //      ds_read_b128 group (16 records reading 16 rows) over 8 bank quads — 8-way -> ~2-way conflicts.
   {
     const int row = lay.row, ce = lay.copy_elems;
     for (int e = tid; e < 8 * ce; e += kBlock) {
-      const int s = e / ce, rem = e - s * ce, c = rem / row, j = rem - c * row + s;
+      const int s = e / ce, rem = e - s * ce, c = rem / row, jj = rem - c * row;
+      const int j = ((((jj >> 3) ^ (c & 7)) << 3) | (jj & 7)) + s;  // element stored at jj holds column j
       prof[e] = static_cast<short>((c >= 1 && j < L1) ? pv.lut[c * kLutStride + pv.seq1[j]] : 0);
     }
   }
@@ -235,11 +240,12 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
           } else {
             c = (wd[i >> 2] >> (8 * (i & 3))) & 0xff;
           }
-          const uint4* rowp = reinterpret_cast<const uint4*>(prof + s * lay.copy_elems + c * lay.row + i0);
+          const uint4* rowp = reinterpret_cast<const uint4*>(prof + s * lay.copy_elems + c * lay.row);
+          const int sw = c & 7;
           uint32_t v[NP];
 #pragma unroll
           for (int q = 0; q < NOFF / 8; ++q) {
-            const uint4 x = rowp[q];
+            const uint4 x = rowp[((i0 >> 3) + q) ^ sw];
             v[4 * q + 0] = x.x;
             v[4 * q + 1] = x.y;
             v[4 * q + 2] = x.z;
