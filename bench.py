@@ -204,7 +204,11 @@ def main():
     elapsed = float(t.item())
     st = eng.stats()
 
-    # ---- verification (untimed): sample of this rank's results vs the CPU engine
+    # ---- verification (untimed): the result array is poisoned and one more step is run, so a step that
+    # skipped work (stale results from an earlier step) cannot pass; a sample is checked vs the CPU engine
+    host.results[:] = np.iinfo(host.results.dtype).max if host.results.dtype.kind == "u" else 0
+    step()
+    barrier()
     nv = min(args.verify, R)
     while nv > 0 and int(host.offsets[nv]) > host.check_letters.shape[0]:
         nv //= 2
@@ -214,6 +218,12 @@ def main():
         ref = as_triples(search_cpu(sub))
         r2 = eng.r2_params(shape.l2_min, shape.l2_max) if fmt == "r2" else None
         ok = int(np.array_equal(as_triples(host.results[:nv], r2=r2), ref))
+        # and the tail of the batch was written by the last step too (no sentinel left anywhere)
+        tail = host.results[R - min(R, 1 << 16):]
+        if host.results.dtype.kind == "u":
+            ok &= int(not (tail == np.iinfo(host.results.dtype).max).any())
+        else:
+            ok &= int(not (tail.view(np.uint8).reshape(tail.shape[0], -1) == 0).all(axis=1).any())
     okt = torch.tensor([ok], dtype=torch.int32, device=cdev)
     if distributed:
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)

@@ -35,6 +35,7 @@ struct EngineOptions {
   int64_t chunk_records = 1 << 21;   // staged pipeline: max records per chunk
   int64_t chunk_bytes = 64ll << 20;  // staged pipeline: max letter bytes per chunk
   bool allow_direct = true;          // use zero-copy streaming when the host buffers are pinned
+  bool use_graphs = true;            // replay the direct path's launches as a captured hipGraph
 };
 
 struct EngineStats {
@@ -121,6 +122,7 @@ class HipEngine {
   void ensure_host(void*& ptr, size_t& cap, size_t bytes);
   bool direct_pointers(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths, int len_bits,
                        int len_base, int64_t n, void* out, int fb, bool packed5, dev::ShortArgs& a) const;
+  void launch_direct(const dev::ProblemView& pv, const dev::ShortArgs& a, bool swipe);
   void run_staged(const uint8_t* codes, const int64_t* offsets, int64_t n, void* out, ResultFormat fmt,
                   bool packed5);
 
@@ -149,6 +151,13 @@ class HipEngine {
   size_t h_plan_cap_ = 0;
   hipEvent_t ev_plan_ = nullptr;
   std::vector<void*> pinned_;
+  struct DirectKey {
+    dev::ProblemView pv;
+    dev::ShortArgs a;
+    int32_t swipe;
+  };
+  DirectKey graph_key_{};
+  hipGraphExec_t graph_exec_ = nullptr;
   EngineStats stats_;
 };
 

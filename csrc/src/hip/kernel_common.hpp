@@ -171,6 +171,19 @@ __device__ __forceinline__ int fmt_bytes(int fmt) {
                                                       : 2;
 }
 
+// Persistent-kernel work counter {next tile, blocks done}: the last block to leave resets both to 0, so
+// the next launch needs no memset (and a captured hipGraph replays correctly). Call from every block
+// after it left its tile loop; stream order makes the reset visible to the next kernel.
+__device__ __forceinline__ void release_work_counter(unsigned* counter) {
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(counter + 1, 1u) == gridDim.x - 1) {
+      atomicExch(counter, 0u);
+      atomicExch(counter + 1, 0u);
+    }
+  }
+}
+
 // Length of record `idx` of the batch from the narrowest available source.
 __device__ __forceinline__ int record_length(const ShortArgs& a, int64_t idx) {
   if (a.lengths4) return a.len_base + ((a.lengths4[idx >> 1] >> (4 * (idx & 1))) & 15);

@@ -186,6 +186,7 @@ __global__ __launch_bounds__(kBlock) void short_search_kernel(ProblemView pv, Sh
     // ---- 4. results -> out (coalesced dwords; long records are overwritten later by the tile kernel)
     copy_results(static_cast<char*>(a.out) + rb * fb, res_l, m * fb, tid, kBlock);
   }
+  release_work_counter(a.counter);
 }
 
 // 5-bit packed stream -> byte codes (staged pipeline path for packed batches).
@@ -235,7 +236,6 @@ void launch_short(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStr
   const int64_t n_tiles = (a.n + a.tile_records - 1) / a.tile_records;
   const int per_cu = std::max(1, std::min(8, 160 * 1024 / std::max(lay.total, 1)));
   const int64_t blocks = std::min<int64_t>(n_tiles, static_cast<int64_t>(num_cus) * per_cu);
-  (void)hipMemsetAsync(a.counter, 0, sizeof(unsigned), stream);
   const dim3 grid(static_cast<unsigned>(std::max<int64_t>(blocks, 1))), block(kBlock);
   if (pv.key_shift > 0) {
     if (profile)

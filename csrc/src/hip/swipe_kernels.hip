@@ -301,6 +301,7 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
     copy_results(static_cast<char*>(a.out) + rb * fb, res_l, m * fb, tid, kBlock);
     cur = nxt;
   }
+  release_work_counter(a.counter);
 }
 
 // ------------------------------------------------------------------------------------------------------
@@ -353,7 +354,6 @@ void launch_swipe(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStr
   const int64_t n_tiles = (a.n + a.tile_records - 1) / a.tile_records;
   const int per_cu = std::max(1, std::min(8, 160 * 1024 / std::max(lay.total, 1)));
   const int64_t blocks = std::min<int64_t>(n_tiles, static_cast<int64_t>(num_cus) * per_cu);
-  (void)hipMemsetAsync(a.counter, 0, sizeof(unsigned), stream);
   const dim3 grid(static_cast<unsigned>(std::max<int64_t>(blocks, 1))), block(kBlock);
 #define MOC_SWIPE_CASE(NO, LW)                                                                              \
   if (noff == NO && l2w == LW) {                                                                          \

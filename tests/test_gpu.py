@@ -365,3 +365,28 @@ def test_pinned_registry_neighbours():
     assert all(L.moc_pinned_covers(_lib.ptr(bufs[i]), bufs[i].nbytes) == 1 for i in (0, 2, 4))
     e1.close()
     assert not any(L.moc_pinned_covers(_lib.ptr(b), b.nbytes) for b in bufs)
+
+
+def test_graph_replay_sees_new_data():
+    # repeated direct solves over the same pinned buffers replay a captured hipGraph; the replay must do
+    # the full work on the buffers' current contents (self-resetting work counter, no stale results)
+    prob = make_synthetic("input6", 100_003, seed=31)
+    other = make_synthetic("input6", 100_003, seed=32)
+    eng = HipSearchEngine(device=0)
+    eng.set_problem(prob.weights, prob.seq1)
+    codes = prob.codes.copy()
+    offsets = prob.offsets.copy()
+    out = np.zeros(prob.n, dtype=np.dtype([("score", "<i4"), ("n", "<i4"), ("k", "<i4")]))
+    eng.pin(codes, offsets, out)
+    for _ in range(3):
+        eng.solve(codes, offsets, out=out)
+        assert eng.stats()["direct"] == 1
+    assert np.array_equal(as_triples(out), as_triples(search_cpu(prob)))
+    # same buffers and lengths, new letters
+    m = min(codes.shape[0], other.codes.shape[0])
+    codes[:m] = other.codes[:m]
+    out[:] = 0
+    eng.solve(codes, offsets, out=out)
+    newp = Problem(prob.weights, prob.seq1, codes, offsets)
+    assert np.array_equal(as_triples(out), as_triples(search_cpu(newp)))
+    eng.close()
