@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "kernel_common.hpp"
 
@@ -330,7 +331,9 @@ bool configure_swipe(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs
   const SwipeChoice ch = swipe_choice(L1, min_l2, max_l2, max_abs_weight);
   if (!ch.noff) return false;
   const int fb = result_bytes(static_cast<ResultFormat>(a.fmt));
-  for (int tr = kMaxTile; tr >= 64; tr /= 2) {
+  int max_tile = kMaxTile;
+  if (const char* v = std::getenv("MOC_SWIPE_TILE")) max_tile = std::max(64, std::min(kMaxTile, std::atoi(v)));
+  for (int tr = max_tile; tr >= 64; tr /= 2) {
     const int cap = tr * static_cast<int>(std::max<int64_t>(max_l2, 1)) + 64;
     if (cap + 32 > kMaxV * kBlock * 16) continue;  // a tile's letters must fit the register prefetch
     SwipeLayout l = swipe_layout(static_cast<int>(L1), ch.noff, ch.l2w, tr, cap, fb);
