@@ -55,6 +55,8 @@ struct BatchHints {
   int64_t max_l2 = -1;
 };
 
+// One engine per (rank, device). Not thread-safe: calls on one engine must not overlap (the streams,
+// pooled buffers, work counter and cached graph are per engine); use one engine per thread instead.
 class HipEngine {
  public:
   explicit HipEngine(const EngineOptions& opt = {});

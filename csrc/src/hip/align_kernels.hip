@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include "kernel_common.hpp"
+#include "moc/runtime/hip_check.hpp"
 
 namespace moc {
 namespace dev {
@@ -185,7 +186,7 @@ void launch_finalize(const BatchView& bv, const Plan& plan, void* out, int fmt, 
 }  // namespace
 
 void launch_tile_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream) {
-  if (plan.n_long > 0) (void)hipMemsetAsync(plan.keys, 0, sizeof(unsigned long long) * plan.n_long, stream);
+  if (plan.n_long > 0) MOC_HIP_CHECK(hipMemsetAsync(plan.keys, 0, sizeof(unsigned long long) * plan.n_long, stream));
   if (plan.n_waves <= 0) return;
   if (pv.key_shift > 0)
     launch_search_u<false>(pv, bv, plan, stream);
