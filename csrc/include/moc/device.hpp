@@ -76,7 +76,18 @@ struct ProblemView {
   int32_t semantics;    // moc::Semantics
   int32_t key_shift;    // bits reserved for k in the int32 hot-loop key (0 -> 64-bit keys)
   R2Params r2;          // parameters of the R2 result format (when used)
+  // tile16 kernel (moc/score_table.hpp Profile16): packed (D, S) Seq1 profile, 26 rows of L1 uint16
+  // entries + overhang, padded to 16 bytes; null when the problem does not fit it (weights or LDS)
+  const uint16_t* prof16 = nullptr;
+  int32_t prof16_bytes = 0;
+  int32_t prof16_bias = 0;
 };
+
+// Entries after the tile16 profile's last row: reads of wave-tile lanes past the valid offsets reach
+// at most L1 + 63*U - 1 (U <= 4) into a row.
+constexpr int kProf16Overhang = 256;
+// LDS budget of one tile16 workgroup (the whole CU: a single workgroup may declare all 160 KiB).
+constexpr int kProf16MaxLds = 160 * 1024;
 
 // One batch of records on the device. Offsets are absolute (int64) and rebased by offsets[0], so
 // a chunk of a bigger CSR array can be transferred and launched without host-side rebasing.
@@ -157,6 +168,11 @@ void launch_tiles(const ProblemView& pv, const BatchView& bv, const Plan& plan, 
 // launch_tile_keys zeroes plan.keys[0..n_long) and max-accumulates the plan's tiles into them.
 void launch_tile_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream);
 void launch_finalize_keys(const BatchView& bv, const Plan& plan, void* out, int fmt, hipStream_t stream);
+// tile16 variant of launch_tile_keys (pv.prof16 must be set): packed-int16 sweep over the LDS profile,
+// then one wave per record recovers k on the winning diagonal and writes final keys.
+void launch_tile16_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream);
+// Waves per CU the tile16 kernel keeps resident (16-wave workgroups, as many as the LDS allows).
+int tile16_waves_per_cu(int prof16_bytes);
 
 // One-wave self-test of the DPP / shuffle primitives (192 ints, see align_kernels.hip).
 void launch_dpp_probe(int* d_out, hipStream_t stream);

@@ -112,6 +112,7 @@ HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
     const int v = std::atoi(u);
     if (v == 1 || v == 2 || v == 4) tile_u_ = v;
   }
+  if (const char* t16 = std::getenv("MOC_TILE16")) tile16_ = std::atoi(t16) != 0;
   if (const char* w = std::getenv("MOC_TILE_WAVES_PER_CU")) {
     const int v = std::atoi(w);
     if (v >= 1 && v <= 32) tile_waves_per_cu_ = v;
@@ -162,6 +163,7 @@ HipEngine::~HipEngine() {
   (void)hipEventDestroy(ev_b_);
   (void)hipFree(d_lut_);
   (void)hipFree(d_seq1_);
+  (void)hipFree(d_prof16_);
   (void)hipStreamDestroy(s_copy_);
   (void)hipStreamDestroy(s_compute_);
   (void)hipStreamDestroy(s_return_);
@@ -220,6 +222,20 @@ void HipEngine::set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, S
   MOC_HIP_CHECK(hipMalloc(&d_seq1_, s1bytes));
   MOC_HIP_CHECK(hipMemcpy(d_lut_, table_.lut.data(), sizeof(int32_t) * table_.lut.size(), hipMemcpyHostToDevice));
   MOC_HIP_CHECK(hipMemcpy(d_seq1_, padded.data(), s1bytes, hipMemcpyHostToDevice));
+  // tile16 long-record kernel: packed (D, S) Seq1 profile, staged whole into one CU's LDS
+  MOC_HIP_CHECK(hipFree(d_prof16_));
+  d_prof16_ = nullptr;
+  prof16_bytes_ = 0;
+  Profile16 prof;
+  const int64_t pbytes = ((2 * ((kAlphabet - 1) * L1 + dev::kProf16Overhang)) + 15) & ~int64_t{15};
+  if (tile16_ && L1 > 0 && pbytes <= dev::kProf16MaxLds &&
+      build_profile16(table_, padded.data(), L1, dev::kProf16Overhang, prof)) {
+    prof.entries.resize(static_cast<size_t>(pbytes / 2), 0);
+    MOC_HIP_CHECK(hipMalloc(&d_prof16_, static_cast<size_t>(pbytes)));
+    MOC_HIP_CHECK(hipMemcpy(d_prof16_, prof.entries.data(), static_cast<size_t>(pbytes), hipMemcpyHostToDevice));
+    prof16_bytes_ = static_cast<int32_t>(pbytes);
+    prof16_bias_ = prof.bias;
+  }
   have_problem_ = true;
 }
 
@@ -237,6 +253,9 @@ dev::ProblemView HipEngine::problem_view(int64_t max_l2) const {
   pv.semantics = static_cast<int32_t>(sem_);
   pv.key_shift = choose_key_shift(table_.max_abs(), std::min<int64_t>(std::max<int64_t>(max_l2, 1), L1_ + 1));
   pv.r2 = r2_;
+  pv.prof16 = d_prof16_;
+  pv.prof16_bytes = prof16_bytes_;
+  pv.prof16_bias = prof16_bias_;
   return pv;
 }
 
@@ -368,7 +387,8 @@ std::vector<dev::WaveStart> HipEngine::plan_waves(const int64_t* offsets, const 
     return dev::WaveStart{static_cast<int32_t>(li), static_cast<int32_t>(t)};
   };
   const int64_t part_tiles = std::max<int64_t>(1, total_tiles * (hi - lo) / std::max<int64_t>(C, 1));
-  const int64_t n_waves = std::min<int64_t>(part_tiles, static_cast<int64_t>(num_cus_) * tile_waves_per_cu_);
+  const int waves_per_cu = d_prof16_ ? dev::tile16_waves_per_cu(prof16_bytes_) : tile_waves_per_cu_;
+  const int64_t n_waves = std::min<int64_t>(part_tiles, static_cast<int64_t>(num_cus_) * waves_per_cu);
   starts.resize(static_cast<size_t>(n_waves) + 1);
   for (int64_t w = 0; w <= n_waves; ++w) starts[w] = locate(lo + (hi - lo) * w / n_waves);
   return starts;
@@ -642,7 +662,7 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
       dev::Plan plan = device_plan(s.d_plan, starts.size(), lrecs != nullptr, n_long, tile_u);
       dev::BatchView bv{dcodes, doffs, cn};
       dev::launch_tiles(pv, bv, plan, s.d_out, static_cast<int>(fmt), s_compute_);
-      stats_.kernels |= 4;
+      stats_.kernels |= d_prof16_ ? 8 : 4;
     }
     MOC_HIP_CHECK(hipGetLastError());
     MOC_HIP_CHECK(hipEventRecord(s.ev_k1, s_compute_));
@@ -712,7 +732,7 @@ void HipEngine::solve_device(const uint8_t* d_codes, const int64_t* d_offsets, c
   stats_ = EngineStats{};
   stats_.cells = cp.cells;
   stats_.records = n;
-  stats_.kernels = (short_ok ? (swipe ? 1 : 2) : 0) | (starts.empty() ? 0 : 4);
+  stats_.kernels = (short_ok ? (swipe ? 1 : 2) : 0) | (starts.empty() ? 0 : (d_prof16_ ? 8 : 4));
 }
 
 }  // namespace moc
@@ -756,7 +776,7 @@ void HipEngine::search_keys_device(const uint8_t* d_codes, const int64_t* d_offs
   MOC_HIP_CHECK(hipEventRecord(ev_plan_, stream));
   stats_ = EngineStats{};
   stats_.records = n;
-  stats_.kernels = plan.n_waves ? 4 : 0;
+  stats_.kernels = plan.n_waves ? (d_prof16_ ? 8 : 4) : 0;
 }
 
 void HipEngine::finalize_keys_device(const int64_t* d_offsets, int64_t n, const unsigned long long* d_keys,

@@ -187,6 +187,90 @@ void test_engine_vs_brute_force() {
   }
 }
 
+// Host replay of the tile16 kernel's arithmetic (tile16_kernels.hip): per offset, packed (D, S) uint16
+// halves with wrap-around, a per-half int16 running max, flushed into int32 every 64 steps; pass 1 keys
+// (score, ~(2o + mutated)); then the k of the winning offset re-found on its diagonal. Must equal the
+// CPU engine exactly, including ties.
+void test_profile16() {
+  std::mt19937 rng(11);
+  for (int trial = 0; trial < 40; ++trial) {
+    const int64_t L1 = 1 + rng() % 400;
+    const int32_t wmax = trial % 2 ? 100 : 12;
+    Weights w{{static_cast<int32_t>(rng() % wmax), static_cast<int32_t>(rng() % 27),
+               static_cast<int32_t>(rng() % 27), static_cast<int32_t>(rng() % 27)}};
+    const ScoreTable t = ScoreTable::build(w);
+    std::vector<uint8_t> s1(static_cast<size_t>(L1));
+    for (auto& x : s1) x = static_cast<uint8_t>(1 + rng() % (trial % 3 ? 26 : 3));  // few letters: many ties
+    Profile16 prof;
+    if (!build_profile16(t, s1.data(), L1, 256, prof)) {
+      CHECK(w.w[0] + std::max({w.w[1], w.w[2], w.w[3]}) > 127);
+      continue;
+    }
+    CHECK(prof.entries.size() == static_cast<size_t>(26 * L1 + 256));
+    auto entry = [&](int c, int64_t j) { return prof.entries[static_cast<size_t>((c - 1) * L1 + j)]; };
+    RecordBatch batch;
+    for (int r = 0; r < 6; ++r) {
+      const int64_t L2 = 1 + rng() % (L1 + 2);
+      std::vector<uint8_t> s2(static_cast<size_t>(L2));
+      for (auto& x : s2) x = static_cast<uint8_t>(1 + rng() % (trial % 3 ? 26 : 3));
+      batch.push_back(s2.data(), L2);
+    }
+    for (Semantics sem : {Semantics::Reference, Semantics::Spec}) {
+      std::vector<Result> out(static_cast<size_t>(batch.size()));
+      solve_batch_cpu(t, s1.data(), L1, batch, out.data(), sem, 1);
+      for (int64_t r = 0; r < batch.size(); ++r) {
+        const uint8_t* s2 = batch.record(r);
+        const int64_t L2 = batch.length(r);
+        uint64_t best_key = 0;
+        for (int64_t o = 0; L2 <= L1 && o <= L1 - L2; ++o) {
+          int32_t Dc = 0, Pc = 0, maxD = INT32_MIN;
+          for (int64_t i0 = 0; i0 < L2; i0 += 64) {
+            const int64_t m = std::min<int64_t>(64, L2 - i0);
+            uint16_t accD = 0, accS = 0;
+            int16_t bestD = INT16_MIN;
+            bool any = false;
+            for (int64_t j = 0; j < m; ++j) {
+              const uint16_t e = entry(s2[i0 + j], o + i0 + j);
+              accS = static_cast<uint16_t>(accS + (e & 0xff));
+              accD = static_cast<uint16_t>(accD + static_cast<uint16_t>(static_cast<int16_t>(static_cast<int8_t>(e >> 8))));
+              if (i0 + j + 1 < L2) {  // k = i+1 <= L2-1 is a candidate
+                bestD = std::max(bestD, static_cast<int16_t>(accD));
+                any = true;
+              }
+            }
+            if (any) maxD = std::max(maxD, Dc + bestD);
+            Dc += static_cast<int16_t>(accD);
+            Pc += static_cast<int16_t>(static_cast<uint16_t>(accS - prof.bias * m));
+          }
+          const int64_t last = L1 - L2;
+          const bool v0 = o < last || (o == last && (sem == Semantics::Spec || L2 == L1));
+          auto key1 = [](int32_t s, uint32_t idx) {
+            return (static_cast<uint64_t>(static_cast<uint32_t>(s) ^ 0x80000000u) << 32) | (0xffffffffu - idx);
+          };
+          if (v0) best_key = std::max(best_key, key1(Pc, static_cast<uint32_t>(2 * o)));
+          if (o < last && L2 >= 2) best_key = std::max(best_key, key1(maxD + Pc - Dc, static_cast<uint32_t>(2 * o + 1)));
+        }
+        Result got{kNoCandidateScore, 0, 0};
+        if (best_key) {
+          const int32_t score = static_cast<int32_t>(static_cast<uint32_t>(best_key >> 32) ^ 0x80000000u);
+          const uint32_t idx = 0xffffffffu - static_cast<uint32_t>(best_key);
+          got = Result{score, static_cast<int32_t>(idx >> 1), 0};
+          if (idx & 1) {  // pass 2: smallest k >= 1 on the winning diagonal
+            int32_t tot1 = 0, d = 0;
+            for (int64_t i = 0; i < L2; ++i) tot1 += t.score(s2[i], s1[got.n + 1 + i]);
+            got.k = -1;
+            for (int64_t i = 0; i + 1 < L2 && got.k < 0; ++i) {
+              d += t.score(s2[i], s1[got.n + i]) - t.score(s2[i], s1[got.n + i + 1]);
+              if (d + tot1 == score) got.k = static_cast<int32_t>(i + 1);
+            }
+          }
+        }
+        CHECK(got.score == out[r].score && got.n == out[r].n && got.k == out[r].k);
+      }
+    }
+  }
+}
+
 void test_formatter() {
   const Result r[3] = {{1, 2, 3}, {kNoCandidateScore, 0, 0}, {-5, 10, 0}};
   CHECK(format_results(r, 3, 7) == "#7: score: 1, n: 2, k: 3\n#8: score: -2147483648, n: 0, k: 0\n"
@@ -198,7 +282,8 @@ int main() {
   const std::vector<std::pair<const char*, std::function<void()>>> tests = {
       {"score_table", test_score_table}, {"parser", test_parser},     {"stream_reader", test_stream_reader},
       {"partition", test_partition},     {"keys", test_keys},         {"pack5", test_pack5},
-      {"engine_vs_brute_force", test_engine_vs_brute_force},          {"formatter", test_formatter}};
+      {"engine_vs_brute_force", test_engine_vs_brute_force},          {"formatter", test_formatter},
+      {"profile16", test_profile16}};
   for (const auto& t : tests) {
     const int before = g_failed;
     t.second();

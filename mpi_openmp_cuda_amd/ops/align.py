@@ -267,7 +267,7 @@ class HipSearchEngine:
         d = dict(zip(keys, list(v)[:10]))
         d["r2"] = tuple(int(x) for x in list(v)[10:13])
         d["format"] = _lib.FORMAT_NAMES[int(d["format"])]
-        d["kernels"] = [k for b, k in ((1, "swipe"), (2, "short"), (4, "tiles")) if int(d["kernels"]) & b]
+        d["kernels"] = [k for b, k in ((1, "swipe"), (2, "short"), (4, "tiles"), (8, "tile16")) if int(d["kernels"]) & b]
         return d
 
 

@@ -182,10 +182,35 @@ def test_kernel_selection(engine):
     engine.set_problem(p1.weights, p1.seq1)
     engine.solve(p1.codes, p1.offsets)
     assert engine.stats()["kernels"] == ["short"]
-    p4 = make_synthetic("input4", 50, seed=1)
+    p4 = make_synthetic("input4", 50, seed=1)  # long records: packed-int16 profile kernel
     engine.set_problem(p4.weights, p4.seq1)
     engine.solve(p4.codes, p4.offsets)
+    assert engine.stats()["kernels"] == ["tile16"]
+    engine.set_problem([120, 20, 1, 1], p4.seq1)  # T range 140 > 127: profile bytes overflow -> DPP tiles
+    engine.solve(p4.codes, p4.offsets)
     assert engine.stats()["kernels"] == ["tiles"]
+
+
+def _letters(rng, n, alphabet):
+    return "".join(chr(65 + x) for x in rng.integers(0, alphabet, n))
+
+
+@pytest.mark.parametrize("L1,weights,alphabet", [
+    (3000, [10, 2, 3, 4], 26),     # reference buffer limit
+    (3140, [100, 27, 5, 3], 3),    # largest Seq1 whose profile fits the LDS; T range 127; tie-heavy
+    (700, [1, 0, 0, 0], 2),        # scores tie everywhere: the k re-walk must pick the smallest
+    (200, [0, 0, 0, 0], 26),       # all zero
+])
+@pytest.mark.parametrize("sem", [Semantics.REFERENCE, Semantics.SPEC])
+def test_tile16_edges(engine, L1, weights, alphabet, sem):
+    rng = np.random.default_rng(L1 + alphabet)
+    s1 = _letters(rng, L1, alphabet)
+    lens = [1, 2, 63, 64, 65, 127, 128, 129, L1 - 64, L1 - 65, L1 - 1, L1, L1 + 1]
+    lens += list(rng.integers(1, min(L1, 2000), 40))
+    recs = [_letters(rng, n, alphabet) for n in lens] + [s1[3:L1 - 70], s1[::2]]
+    prob = Problem.from_strings(weights, s1, recs)
+    check(engine, prob, sem)
+    assert "tile16" in engine.stats()["kernels"]
 
 
 def test_short_config_fallback(engine):
@@ -332,7 +357,7 @@ def test_r2_results_and_nibble_lengths(pinned, packed, shape, n):
     eng.close()
 
 
-@pytest.mark.parametrize("L1,lo,hi,kernel", [(90, 3, 11, "tiles"), (40, 33, 38, "short")])
+@pytest.mark.parametrize("L1,lo,hi,kernel", [(90, 3, 11, "tile16"), (40, 33, 38, "short")])
 def test_r2_tiles_and_short_kernels(engine, L1, lo, hi, kernel):
     # R2 through the tile kernel's finalize and the lane/offset kernel (staged path)
     rng = np.random.default_rng(5)
