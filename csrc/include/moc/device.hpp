@@ -21,6 +21,11 @@
 //     sub-tile is its helper diagonal), walked by persistent waves in cost-balanced runs planned on the
 //     host; partial maxima merge through one 64-bit atomicMax per record run on an order-free packed
 //     key (score, -(o*L2+k)) — deterministic tie-break, no races (fixes B9).
+//   * tile16 kernel (tile16_kernels.hip): the same kind of plan, two offsets per lane: one ds_read_u16
+//     of an LDS-resident int8 difference profile feeds both, summed in the halves of one register
+//     (2 SDWA adds + 1 v_pk_max_i16 per two cells, no cross-lane moves); Tot_o from one anchor diagonal
+//     per tile + a suffix scan; the k of each record's winning offset recovered afterwards on that one
+//     diagonal. Used whenever the weights and Seq1 fit it (T range <= 127, L1 <= 3111).
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -76,16 +81,15 @@ struct ProblemView {
   int32_t semantics;    // moc::Semantics
   int32_t key_shift;    // bits reserved for k in the int32 hot-loop key (0 -> 64-bit keys)
   R2Params r2;          // parameters of the R2 result format (when used)
-  // tile16 kernel (moc/score_table.hpp Profile16): packed (D, S) Seq1 profile, 26 rows of L1 uint16
+  // tile16 kernel (moc/score_table.hpp Profile16): packed int8 pair D profile, 26 rows of L1 uint16
   // entries + overhang, padded to 16 bytes; null when the problem does not fit it (weights or LDS)
   const uint16_t* prof16 = nullptr;
   int32_t prof16_bytes = 0;
-  int32_t prof16_bias = 0;
 };
 
 // Entries after the tile16 profile's last row: reads of wave-tile lanes past the valid offsets reach
-// at most L1 + 63*U - 1 (U <= 4) into a row.
-constexpr int kProf16Overhang = 256;
+// at most L1 + 128*U - 2 (U <= 8) into a row.
+constexpr int kProf16Overhang = 1024;
 // LDS budget of one tile16 workgroup (the whole CU: a single workgroup may declare all 160 KiB).
 constexpr int kProf16MaxLds = 160 * 1024;
 
@@ -107,7 +111,9 @@ struct WaveStart {
   int32_t t;
 };
 
-inline int64_t tiles_of(int64_t need, int u) { return (need + kTileOffsets * u - 1) / (kTileOffsets * u); }
+// Offsets per wave tile: U sub-tiles of 63 (tile kernel) or 128 (tile16: two offsets per lane).
+inline int tile_span(bool tile16, int u) { return (tile16 ? 128 : kTileOffsets) * u; }
+inline int64_t tiles_of(int64_t need, int span) { return (need + span - 1) / span; }
 
 // Host-built plan for the tile kernel of one batch.
 struct Plan {
@@ -116,7 +122,7 @@ struct Plan {
   const int32_t* long_recs = nullptr;  // device: records handled by the tile kernel (null = identity)
   int64_t n_long = 0;
   unsigned long long* keys = nullptr;  // device scratch, n_long entries (tile-kernel partial maxima)
-  int32_t u = 2;                       // sub-tiles per wave tile (1, 2 or 4)
+  int32_t u = 2;                       // sub-tiles per wave tile (1, 2 or 4; tile16 also 8)
   R2Params r2;                         // finalize: parameters of the R2 result format
 };
 

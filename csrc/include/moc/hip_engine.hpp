@@ -141,7 +141,7 @@ class HipEngine {
   int32_t* d_lut_ = nullptr;
   uint8_t* d_seq1_ = nullptr;
   uint16_t* d_prof16_ = nullptr;  // tile16 profile (null: the problem does not fit it, or MOC_TILE16=0)
-  int32_t prof16_bytes_ = 0, prof16_bias_ = 0;
+  int32_t prof16_bytes_ = 0;
   bool tile16_ = true;            // MOC_TILE16 (A/B switch of the long-record kernel)
   int64_t L1_ = 0;
   Semantics sem_ = Semantics::Reference;

@@ -42,17 +42,16 @@ struct ScoreTable {
   static char class_char(PairClass c);
 };
 
-// Packed Seq1 profile of the tile16 kernel (csrc/src/hip/tile16_kernels.hip): for Seq2 letter c = 1..26
-// (row c-1) and Seq1 position j, one uint16 entry
-//     low byte  = S + bias           S = T[c][Seq1[j]]                    (unsigned, bias = -min S)
-//     high byte = D  (int8)          D = T[c][Seq1[j]] - T[c][Seq1[j+1]]  (Seq1[L1] = pad code 0)
-// so that one LDS read + one v_perm give the packed int16 pair (D, S) whose running sums are the
-// diagonal difference P_o(k) - P_{o+1}(k) and the diagonal total Tot_o. Rows are L1 entries long and
-// packed back to back; `overhang` zero entries follow the last row (reads of tiles past the valid
-// offsets). Returns false (out untouched) when some S or D does not fit its byte.
+// Packed Seq1 difference profile of the tile16 kernel (csrc/src/hip/tile16_kernels.hip). With
+//     D[c][j] = T[c][Seq1[j]] - T[c][Seq1[j+1]]   (Seq1[L1] = pad code 0; D[c][j >= L1] = 0)
+// the entry for Seq2 letter c = 1..26 (row c-1) and Seq1 position j is the uint16
+//     low byte = D[c][j] (int8),  high byte = D[c][j+1] (int8)
+// i.e. the step-i terms of the two adjacent diagonals o = j - i and o + 1 that one lane carries: one
+// LDS read feeds two cells, whose running sums are D_o(k) = P_o(k) - P_{o+1}(k). Rows are L1 entries
+// long and packed back to back; `overhang` zero entries follow the last row (reads of tiles past the
+// valid offsets). Returns false (out untouched) when some D does not fit a signed byte.
 struct Profile16 {
   std::vector<uint16_t> entries;
-  int32_t bias = 0;
   int64_t row = 0;  // entries per row (= L1)
 };
 bool build_profile16(const ScoreTable& t, const uint8_t* seq1, int64_t L1, int64_t overhang, Profile16& out);

@@ -1,33 +1,33 @@
-// Long-record search kernel, packed-int16 profile variant ("tile16"; gfx950, wave64).
+// Long-record search kernel, packed-int16 difference-profile variant ("tile16"; gfx950, wave64).
 //
-// Same work decomposition as tile_search_kernel (align_kernels.hip: persistent waves over cost-balanced
-// runs of 63*U-offset wave tiles, one lane per offset), but the per-cell work is cut from a LUT gather,
-// two DPP moves and five VALU ops to ONE LDS read and THREE VALU ops, by reading a precomputed Seq1
-// profile instead of shifting Seq1 letters across lanes:
-//
-//   profile entry (row c = Seq2 letter, column j = Seq1 position; moc::Profile16, 2 bytes)
-//       low byte  S + bias,  S = T[c][Seq1[j]]
-//       high byte D (int8),  D = T[c][Seq1[j]] - T[c][Seq1[j+1]]
-//   per lane (offset o) and Seq2 position i:
-//       e    = prof[c_i][o + i]           ds_read_u16 — lanes read consecutive halfwords: conflict-free;
-//                                         the address is lane base + a wave-uniform SGPR term, and the U
-//                                         sub-tiles of a wave tile sit at immediate offsets (+126 B)
-//       w    = (sext D << 16) | (S+bias)  v_perm_b32
-//       acc += w                          v_pk_add_u16: high half = D_o(i+1) = P_o(i+1) - P_{o+1}(i+1),
-//                                         low half = P_o(i+1) + bias*(i+1) (both mod 2^16)
-//       best = max(best, acc)             v_pk_max_i16: high half = running max of D over k = i+1
-//   every 64 steps the int16 halves are flushed into int32 (|partial sums| <= 64*127 < 2^15, exact).
-//
-// Per offset this yields Tot_o, Tot_{o+1} = Tot_o - D_o(L2) and max_k D_o(k) — the best score of the
-// offset, max(Tot_o [k = 0], max_k D_o(k) + Tot_{o+1}), but not WHICH k. So the sweep reduces keys
-// (score, ~(2o + mutated)) — same order as the reference (score, then smallest o, then k = 0 first) —
-// and a second kernel re-walks only the winning diagonal of each record (one wave, O(L2)) to find the
-// smallest k with that score and write the engine's final key (score, ~(o*L2 + k)). Host replay of the
-// arithmetic, ties included: csrc/tests/test_core.cpp test_profile16.
+// Work decomposition as tile_search_kernel (align_kernels.hip): persistent waves walk cost-balanced runs
+// of wave tiles planned on the host, one record's letters in registers across its tiles, one 64-bit
+// atomicMax per record run. The per-cell work is what changes. With the closed form
+//     score(o, 0) = Tot_o,   score(o, k >= 1) = D_o(k) + Tot_{o+1},   D_o(k) = P_o(k) - P_{o+1}(k)
+//     D_o(k) = sum_{i<k} Dt[c_i][o + i],   Dt[c][j] = T[c][Seq1[j]] - T[c][Seq1[j+1]]
+// the hot loop only needs the running sums of Dt along each diagonal and their running maximum. Dt
+// fits a signed byte for every realistic weight set (T range <= 127), so:
+//   * LDS holds Profile16 (moc/score_table.hpp): entry [c][j] = bytes (Dt[c][j], Dt[c][j+1]) — the
+//     step-i terms of the two adjacent diagonals o = j - i and o + 1. A LANE carries such a pair of
+//     offsets, as the two int16 halves of one register, so one conflict-free ds_read_u16 feeds two cells;
+//   * per step and lane:  acc.lo += sext(byte0); acc.hi += sext(byte1)   2 x v_add_u16_sdwa
+//                         best = max(best, acc)                          v_pk_max_i16
+//     i.e. 1.5 VALU + 0.5 LDS read per cell (the LUT-gather + DPP form of tile_search_kernel costs ~7);
+//     the letter's row offset arrives with one v_readlane per step for the whole wave tile, and the U
+//     sub-tiles (128 offsets each) sit at immediate LDS offsets;
+//   * every 64 steps the int16 halves are folded into int32 (|partial sums| <= 64*128 < 2^15: exact);
+//   * Tot_o is not summed per cell: per tile one anchor diagonal Tot_{oA} (oA = first offset past the
+//     tile or past the valid range) is summed by the wave from the int32 LUT, and
+//     Tot_o = Tot_{oA} + sum_{o <= o' < oA} D_{o'}(L2) comes from a wave suffix scan.
+// Per offset this gives the best score, but not which k: the sweep reduces keys (score, ~(2o + mutated))
+// — the reference order: score, then smallest o, then k = 0 first — and resolve16_kernel re-walks only
+// the winning diagonal of each record (one wave, O(L2)) to find the smallest k with that score and
+// write the engine's final key (score, ~(o*L2 + k)). Host replay of all of it, ties included:
+// csrc/tests/test_core.cpp test_profile16.
 //
 // Replaces calc_result (cudaFunctions.cu:63-176) for long records when the weights fit the profile
-// bytes (|T| range <= 127, i.e. W1 + max(W2,W3,W4) <= 127) and the profile fits one CU's LDS
-// (26*L1 + 256 halfwords <= 160 KiB: L1 <= 3140, covering the reference's 3000-letter buffers).
+// bytes (W1 + max(W2,W3,W4) <= 127) and the profile fits one CU's LDS (26*L1 + 1024 halfwords
+// <= 160 KiB: L1 <= 3111, covering the reference's 3000-letter Seq1 buffer, myProto.h:3).
 #include <hip/hip_runtime.h>
 
 #include "kernel_common.hpp"
@@ -39,32 +39,49 @@ namespace dev {
 using namespace kc;
 
 namespace {
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kBlock16 = 1024;  // 16 waves: the profile takes most of the CU's LDS, one workgroup holds it
 constexpr int kWavesPerBlock16 = kBlock16 / 64;
-constexpr uint32_t kPermDS = 0x08010c00u;  // bytes: [S+bias, 0x00, D, sign(D)]
+constexpr int kSub = 128;                    // offsets per sub-tile (2 per lane)
+constexpr uint32_t kBestInit = 0x80008000u;  // both halves INT16_MIN
 
-__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) {
-  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
+// acc.lo += sext(e.byte0), acc.hi += sext(e.byte1): 16-bit wrapping adds on sub-dword operands (SDWA)
+__device__ __forceinline__ void add_pair(uint32_t& acc, uint32_t e) {
+  asm("v_add_u16_sdwa %0, %0, sext(%1) dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:BYTE_0"
+      : "+v"(acc)
+      : "v"(e));
+  asm("v_add_u16_sdwa %0, %0, sext(%1) dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:BYTE_1"
+      : "+v"(acc)
+      : "v"(e));
 }
 __device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b) {
   return __builtin_bit_cast(uint32_t,
                             __builtin_elementwise_max(__builtin_bit_cast(s16x2, a), __builtin_bit_cast(s16x2, b)));
 }
-constexpr uint32_t kBestInit = 0x80008000u;  // both halves INT16_MIN
+__device__ __forceinline__ int lo16(uint32_t v) { return static_cast<int16_t>(v & 0xffffu); }
+__device__ __forceinline__ int hi16(uint32_t v) { return static_cast<int>(v) >> 16; }
 
-// Pass-1 key of an offset: (score, ~(2o + mutated)); the same packing as final_key.
-__device__ __forceinline__ unsigned long long pass1_candidate(bool own, int o, int L1, int L2, int sem, int P, int Dfin,
+// Pass-1 key of offset o: (score, ~(2o + mutated)); the same packing as final_key.
+__device__ __forceinline__ unsigned long long pass1_candidate(int o, int L1, int L2, int sem, int tot, int tot_next,
                                                               int maxD) {
   unsigned long long key = 0;
-  if (!own) return key;
   const int last = L1 - L2;
-  const bool v0 = (o < last) || (o == last && (sem == static_cast<int>(Semantics::Spec) || L2 == L1));
-  if (v0) key = final_key(P, 2u * static_cast<uint32_t>(o));
-  if (o < last && L2 >= 2) key = max_u64(key, final_key(maxD + P - Dfin, 2u * static_cast<uint32_t>(o) + 1u));
+  if (L2 > L1 || o > last) return key;
+  const bool v0 = (o < last) || (sem == static_cast<int>(Semantics::Spec) || L2 == L1);
+  if (v0) key = final_key(tot, 2u * static_cast<uint32_t>(o));
+  if (o < last && L2 >= 2) key = max_u64(key, final_key(maxD + tot_next, 2u * static_cast<uint32_t>(o) + 1u));
   return key;
+}
+
+// Inclusive suffix sum over the lanes of a wave (lane l gets sum of v over lanes l..63).
+__device__ __forceinline__ int wave_suffix_sum(int v, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int t = __shfl_down(v, d, 64);
+    if (lane + d < 64) v += t;
+  }
+  return v;
 }
 }  // namespace
 
@@ -85,9 +102,8 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
   if (w >= n_waves) return;  // wave-uniform; no barrier follows
   const int L1 = pv.L1;
   const int rowb = 2 * L1;  // bytes per profile row
-  const int bias = pv.prof16_bias;
   const int lane = threadIdx.x & 63;
-  constexpr int kSpan = kTileOffsets * U;
+  constexpr int kSpan = kSub * U;
 
   const WaveStart ws = starts[w], we = starts[w + 1];
   int li = __builtin_amdgcn_readfirstlane(ws.li), t = __builtin_amdgcn_readfirstlane(ws.t);
@@ -100,74 +116,85 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
     const int need = L2 <= L1 ? L1 - L2 + 1 : 1;
     const int ntiles = (need + kSpan - 1) / kSpan;
     const int t_stop = li == end_li ? min(end_t, ntiles) : ntiles;
-    const int cv_first = lane < steps ? static_cast<int>(rec[lane]) : 0;
+    // byte offset of (letter row, step) for this lane's step of the first chunk
+    auto row_off = [&](int i) {
+      const int c = i < steps ? static_cast<int>(rec[i]) : 1;
+      return max(c - 1, 0) * rowb + 2 * i;
+    };
+    const int so_first = row_off(lane);
     unsigned long long acc64 = 0;
-    for (; t < t_stop; ++t) {
+    for (; t < t_stop && L2 <= L1; ++t) {
       const int o0 = t * kSpan;
       MOC_DCHECK(o0 >= 0 && o0 <= L1);
-      // sub-tile u: lane owns offset o0 + 63u + lane (lane 63 duplicates the next sub-tile's lane 0)
-      const unsigned char* lbase = smem + 2 * (o0 + lane);
+      // sub-tile u: lane owns offsets o0 + 128u + 2*lane (low half) and + 1 (high half)
+      const unsigned char* lbase = smem + 2 * o0 + 4 * lane;
       uint32_t acc[U], best[U];
-      int Dc[U], Pc[U], maxD[U];
+      int DcA[U], DcB[U], mxA[U], mxB[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         acc[u] = 0;
         best[u] = kBestInit;
-        Dc[u] = 0;
-        Pc[u] = 0;
-        maxD[u] = INT32_MIN;
+        DcA[u] = DcB[u] = 0;
+        mxA[u] = mxB[u] = INT32_MIN;
       }
-      auto step = [&](int cv, int j, int i, bool key) {
-        const int c = __builtin_amdgcn_readlane(cv, j);
-        const int soff = __builtin_amdgcn_readfirstlane(max(c - 1, 0) * rowb + 2 * i);
+      auto step = [&](int so, int j, bool key) {
+        const int soff = __builtin_amdgcn_readlane(so, j);
         const unsigned char* p = lbase + soff;
-        MOC_DCHECK(2 * (o0 + lane) + soff + 2 * kTileOffsets * (U - 1) + 2 <= pv.prof16_bytes);
+        MOC_DCHECK(2 * o0 + 4 * lane + soff + 2 * kSub * (U - 1) + 2 <= pv.prof16_bytes);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          const uint32_t e = *reinterpret_cast<const uint16_t*>(p + 2 * kTileOffsets * u);
-          acc[u] = pk_add(acc[u], __builtin_amdgcn_perm(e, e, kPermDS));
+          const uint32_t e = *reinterpret_cast<const uint16_t*>(p + 2 * kSub * u);
+          add_pair(acc[u], e);
           if (key) best[u] = pk_max(best[u], acc[u]);
         }
       };
       // every 64-step chunk starts from zero halves and folds them into the int32 state at its end
-      auto flush = [&](int m, bool any_key) {
+      auto flush = [&](bool any_key) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          if (any_key) maxD[u] = max(maxD[u], Dc[u] + (static_cast<int>(best[u]) >> 16));
-          Dc[u] += static_cast<int>(acc[u]) >> 16;
-          Pc[u] += static_cast<int16_t>(static_cast<uint16_t>((acc[u] & 0xffffu) - static_cast<uint32_t>(bias * m)));
-        }
-      };
-      int cv = cv_first;
-      int i0 = 0;
-      for (; i0 + 64 < steps; i0 += 64) {  // full chunks (the record's last letter lies beyond)
-        const int cv_next = i0 + 64 + lane < steps ? static_cast<int>(rec[i0 + 64 + lane]) : 0;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
+          if (any_key) {
+            mxA[u] = max(mxA[u], DcA[u] + lo16(best[u]));
+            mxB[u] = max(mxB[u], DcB[u] + hi16(best[u]));
+          }
+          DcA[u] += lo16(acc[u]);
+          DcB[u] += hi16(acc[u]);
           acc[u] = 0;
           best[u] = kBestInit;
         }
+      };
+      int so = so_first;
+      int i0 = 0;
+      for (; i0 + 64 < steps; i0 += 64) {  // full chunks (the record's last letter lies beyond)
+        const int so_next = row_off(i0 + 64 + lane);
 #pragma unroll 16
-        for (int j = 0; j < 64; ++j) step(cv, j, i0 + j, true);
-        flush(64, true);
-        cv = cv_next;
+        for (int j = 0; j < 64; ++j) step(so, j, true);
+        flush(true);
+        so = so_next;
       }
       if (steps > 0) {  // last chunk: 1..64 steps; no hyphen after the final letter
         const int m = steps - i0;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          acc[u] = 0;
-          best[u] = kBestInit;
-        }
-        for (int j = 0; j < m - 1; ++j) step(cv, j, i0 + j, true);
-        step(cv, m - 1, i0 + m - 1, false);
-        flush(m, m > 1);
+        for (int j = 0; j < m - 1; ++j) step(so, j, true);
+        step(so, m - 1, false);
+        flush(m > 1);
       }
+      // ---- Tot per offset: anchor diagonal oA, then suffix sums of the D totals (valid offsets only)
+      const int oA = min(o0 + kSpan, need);
+      int anchor = 0;
+      for (int i = lane; i < steps; i += 64) anchor += pv.lut[rec[i] * kLutStride + pv.seq1[oA + i]];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int o = o0 + kTileOffsets * u + lane;
-        const bool own = lane < kTileOffsets && L2 <= L1 && o <= L1 - L2;
-        acc64 = max_u64(acc64, pass1_candidate(own, o, L1, L2, pv.semantics, Pc[u], Dc[u], maxD[u]));
+      for (int d = 32; d >= 1; d >>= 1) anchor += __shfl_xor(anchor, d, 64);
+      int carry = anchor;  // Tot at the end of the sub-tile being processed
+#pragma unroll
+      for (int u = U - 1; u >= 0; --u) {
+        const int oa = o0 + kSub * u + 2 * lane;
+        const int ca = oa < oA ? DcA[u] : 0, cb = oa + 1 < oA ? DcB[u] : 0;
+        const int pair = ca + cb;
+        const int excl = wave_suffix_sum(pair, lane) - pair;
+        const int totB = carry + excl + cb;  // Tot_{oa+1}
+        const int totA = totB + ca;          // Tot_{oa}
+        carry = __shfl(totA, 0, 64);
+        acc64 = max_u64(acc64, pass1_candidate(oa, L1, L2, pv.semantics, totA, totB, mxA[u]));
+        acc64 = max_u64(acc64, pass1_candidate(oa + 1, L1, L2, pv.semantics, totB, totB - cb, mxB[u]));
       }
     }
     const unsigned long long k = wave_max_u64(acc64);
@@ -255,8 +282,9 @@ void launch_tile16_keys(const ProblemView& pv, const BatchView& bv, const Plan& 
   if (plan.n_waves <= 0) return;
   switch (plan.u) {
     case 1: launch16_t<1>(pv, bv, plan, stream); break;
-    case 4: launch16_t<4>(pv, bv, plan, stream); break;
-    default: launch16_t<2>(pv, bv, plan, stream); break;
+    case 2: launch16_t<2>(pv, bv, plan, stream); break;
+    case 8: launch16_t<8>(pv, bv, plan, stream); break;
+    default: launch16_t<4>(pv, bv, plan, stream); break;
   }
   const int64_t rb = (plan.n_long + 3) / 4;
   hipLaunchKernelGGL(resolve16_kernel, dim3(static_cast<unsigned>(rb)), dim3(256), 0, stream, pv, bv, plan.long_recs,

@@ -110,7 +110,7 @@ HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
   if (const char* g = std::getenv("MOC_GRAPHS")) opt_.use_graphs = std::atoi(g) != 0;
   if (const char* u = std::getenv("MOC_TILE_U")) {  // tuning override of the per-batch choice
     const int v = std::atoi(u);
-    if (v == 1 || v == 2 || v == 4) tile_u_ = v;
+    if (v == 1 || v == 2 || v == 4 || (v == 8 && tile16_)) tile_u_ = v;
   }
   if (const char* t16 = std::getenv("MOC_TILE16")) tile16_ = std::atoi(t16) != 0;
   if (const char* w = std::getenv("MOC_TILE_WAVES_PER_CU")) {
@@ -234,7 +234,6 @@ void HipEngine::set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, S
     MOC_HIP_CHECK(hipMalloc(&d_prof16_, static_cast<size_t>(pbytes)));
     MOC_HIP_CHECK(hipMemcpy(d_prof16_, prof.entries.data(), static_cast<size_t>(pbytes), hipMemcpyHostToDevice));
     prof16_bytes_ = static_cast<int32_t>(pbytes);
-    prof16_bias_ = prof.bias;
   }
   have_problem_ = true;
 }
@@ -255,7 +254,6 @@ dev::ProblemView HipEngine::problem_view(int64_t max_l2) const {
   pv.r2 = r2_;
   pv.prof16 = d_prof16_;
   pv.prof16_bytes = prof16_bytes_;
-  pv.prof16_bias = prof16_bias_;
   return pv;
 }
 
@@ -362,6 +360,7 @@ std::vector<dev::WaveStart> HipEngine::plan_waves(const int64_t* offsets, const 
   }
   // sub-tiles per wave tile: 4 amortises the per-tile setup over short records, 2 keeps more waves busy
   // on long ones (measured: profiles/tile_variants.log)
+  // (measured, both kernels: profiles/tile_variants.log, profiles/tile16_variants.log)
   const int u = tile_u_ > 0 ? tile_u_ : (sum_l2 < 96 * n_long ? 4 : 2);
   u_out = u;
   std::vector<int64_t> pre(static_cast<size_t>(n_long) + 1, 0), tcost(static_cast<size_t>(n_long));
@@ -370,7 +369,7 @@ std::vector<dev::WaveStart> HipEngine::plan_waves(const int64_t* offsets, const 
   for (int64_t li = 0; li < n_long; ++li) {
     const int64_t r = long_recs ? long_recs[li] : li;
     const int64_t L2 = offsets[r + 1] - offsets[r];
-    const int64_t nt = dev::tiles_of(dev::lanes_needed(L1_, L2), u);
+    const int64_t nt = dev::tiles_of(dev::lanes_needed(L1_, L2), dev::tile_span(d_prof16_ != nullptr, u));
     ntiles[li] = static_cast<int32_t>(nt);
     tcost[li] = (L2 <= L1_ ? L2 : 0) + kTileOverheadSteps;
     pre[li + 1] = pre[li] + nt * tcost[li];

@@ -68,29 +68,23 @@ int32_t ScoreTable::max_abs() const {
 
 bool build_profile16(const ScoreTable& t, const uint8_t* seq1, int64_t L1, int64_t overhang, Profile16& out) {
   if (L1 <= 0 || overhang < 0) return false;
-  int32_t smin = INT32_MAX, smax = INT32_MIN, dmin = INT32_MAX, dmax = INT32_MIN;
+  int32_t dmin = INT32_MAX, dmax = INT32_MIN;
   for (int c = 1; c < kAlphabet; ++c)
-    for (int x = 0; x < kAlphabet; ++x) {  // x = 0: the pad code after Seq1
-      const int32_t s = t.score(c, x);
-      smin = std::min(smin, s);
-      smax = std::max(smax, s);
+    for (int x = 0; x < kAlphabet; ++x)  // 0: the pad code after Seq1
       for (int y = 0; y < kAlphabet; ++y) {
-        const int32_t d = s - t.score(c, y);
+        const int32_t d = t.score(c, x) - t.score(c, y);
         dmin = std::min(dmin, d);
         dmax = std::max(dmax, d);
       }
-    }
-  if (static_cast<int64_t>(smax) - smin > 255 || dmin < -128 || dmax > 127) return false;
-  out.bias = -smin;
+  if (dmin < -128 || dmax > 127) return false;
   out.row = L1;
   out.entries.assign(static_cast<size_t>((kAlphabet - 1) * L1 + overhang), 0);
+  std::vector<int32_t> d(static_cast<size_t>(L1) + 1, 0);
   for (int c = 1; c < kAlphabet; ++c) {
+    for (int64_t j = 0; j < L1; ++j) d[j] = t.score(c, seq1[j]) - t.score(c, j + 1 < L1 ? seq1[j + 1] : 0);
     uint16_t* r = out.entries.data() + static_cast<size_t>(c - 1) * static_cast<size_t>(L1);
-    for (int64_t j = 0; j < L1; ++j) {
-      const int32_t s = t.score(c, seq1[j]);
-      const int32_t d = s - t.score(c, j + 1 < L1 ? seq1[j + 1] : 0);
-      r[j] = static_cast<uint16_t>((static_cast<uint32_t>(d & 0xff) << 8) | static_cast<uint32_t>(s + out.bias));
-    }
+    for (int64_t j = 0; j < L1; ++j)
+      r[j] = static_cast<uint16_t>((static_cast<uint32_t>(d[j + 1] & 0xff) << 8) | static_cast<uint32_t>(d[j] & 0xff));
   }
   return true;
 }

@@ -187,10 +187,11 @@ void test_engine_vs_brute_force() {
   }
 }
 
-// Host replay of the tile16 kernel's arithmetic (tile16_kernels.hip): per offset, packed (D, S) uint16
-// halves with wrap-around, a per-half int16 running max, flushed into int32 every 64 steps; pass 1 keys
-// (score, ~(2o + mutated)); then the k of the winning offset re-found on its diagonal. Must equal the
-// CPU engine exactly, including ties.
+// Host replay of the tile16 kernel's arithmetic (tile16_kernels.hip): per offset, the int8 D terms of
+// its profile byte summed in a wrapping int16 half with an int16 running max, flushed into int32 every
+// 64 steps; Tot_o from an anchor diagonal per 512-offset wave tile plus a suffix sum of the D totals;
+// pass 1 keys (score, ~(2o + mutated)); then the k of the winning offset re-found on its diagonal.
+// Must equal the CPU engine exactly, including ties.
 void test_profile16() {
   std::mt19937 rng(11);
   for (int trial = 0; trial < 40; ++trial) {
@@ -202,11 +203,11 @@ void test_profile16() {
     std::vector<uint8_t> s1(static_cast<size_t>(L1));
     for (auto& x : s1) x = static_cast<uint8_t>(1 + rng() % (trial % 3 ? 26 : 3));  // few letters: many ties
     Profile16 prof;
-    if (!build_profile16(t, s1.data(), L1, 256, prof)) {
+    if (!build_profile16(t, s1.data(), L1, 1024, prof)) {
       CHECK(w.w[0] + std::max({w.w[1], w.w[2], w.w[3]}) > 127);
       continue;
     }
-    CHECK(prof.entries.size() == static_cast<size_t>(26 * L1 + 256));
+    CHECK(prof.entries.size() == static_cast<size_t>(26 * L1 + 1024));
     auto entry = [&](int c, int64_t j) { return prof.entries[static_cast<size_t>((c - 1) * L1 + j)]; };
     RecordBatch batch;
     for (int r = 0; r < 6; ++r) {
@@ -222,33 +223,47 @@ void test_profile16() {
         const uint8_t* s2 = batch.record(r);
         const int64_t L2 = batch.length(r);
         uint64_t best_key = 0;
-        for (int64_t o = 0; L2 <= L1 && o <= L1 - L2; ++o) {
-          int32_t Dc = 0, Pc = 0, maxD = INT32_MIN;
+        const int64_t need = L2 <= L1 ? L1 - L2 + 1 : 0;
+        std::vector<int32_t> Dc(static_cast<size_t>(need) + 1, 0), maxD(static_cast<size_t>(need) + 1, INT32_MIN);
+        for (int64_t o = 0; o < need; ++o) {
           for (int64_t i0 = 0; i0 < L2; i0 += 64) {
             const int64_t m = std::min<int64_t>(64, L2 - i0);
-            uint16_t accD = 0, accS = 0;
+            uint16_t accD = 0;
             int16_t bestD = INT16_MIN;
             bool any = false;
-            for (int64_t j = 0; j < m; ++j) {
-              const uint16_t e = entry(s2[i0 + j], o + i0 + j);
-              accS = static_cast<uint16_t>(accS + (e & 0xff));
-              accD = static_cast<uint16_t>(accD + static_cast<uint16_t>(static_cast<int16_t>(static_cast<int8_t>(e >> 8))));
+            for (int64_t j = 0; j < m; ++j) {  // lane pair (o & ~1, o | 1): byte (o & 1) of one entry
+              const uint16_t e = entry(s2[i0 + j], (o & ~int64_t{1}) + i0 + j);
+              const int8_t d = static_cast<int8_t>(o & 1 ? e >> 8 : e & 0xff);
+              accD = static_cast<uint16_t>(accD + static_cast<uint16_t>(static_cast<int16_t>(d)));
               if (i0 + j + 1 < L2) {  // k = i+1 <= L2-1 is a candidate
                 bestD = std::max(bestD, static_cast<int16_t>(accD));
                 any = true;
               }
             }
-            if (any) maxD = std::max(maxD, Dc + bestD);
-            Dc += static_cast<int16_t>(accD);
-            Pc += static_cast<int16_t>(static_cast<uint16_t>(accS - prof.bias * m));
+            if (any) maxD[o] = std::max(maxD[o], Dc[o] + bestD);
+            Dc[o] += static_cast<int16_t>(accD);
           }
+        }
+        // Tot per 512-offset tile: anchor diagonal at min(tile end, L1 - L2 + 1), then suffix sums of D totals
+        std::vector<int32_t> tot(static_cast<size_t>(need) + 1, 0);
+        for (int64_t o0 = 0; o0 < need; o0 += 512) {
+          const int64_t oA = std::min<int64_t>(o0 + 512, need);
+          int32_t acc = 0;
+          for (int64_t i = 0; i < L2; ++i) acc += t.score(s2[i], oA + i < L1 ? s1[oA + i] : 0);
+          for (int64_t o = oA - 1; o >= o0; --o) {
+            acc += Dc[o];
+            tot[o] = acc;
+          }
+        }
+        for (int64_t o = 0; o < need; ++o) {
+          const int32_t Pc = tot[o], Tn = tot[o] - Dc[o];  // Tot_o, Tot_{o+1}
           const int64_t last = L1 - L2;
           const bool v0 = o < last || (o == last && (sem == Semantics::Spec || L2 == L1));
           auto key1 = [](int32_t s, uint32_t idx) {
             return (static_cast<uint64_t>(static_cast<uint32_t>(s) ^ 0x80000000u) << 32) | (0xffffffffu - idx);
           };
           if (v0) best_key = std::max(best_key, key1(Pc, static_cast<uint32_t>(2 * o)));
-          if (o < last && L2 >= 2) best_key = std::max(best_key, key1(maxD + Pc - Dc, static_cast<uint32_t>(2 * o + 1)));
+          if (o < last && L2 >= 2) best_key = std::max(best_key, key1(maxD[o] + Tn, static_cast<uint32_t>(2 * o + 1)));
         }
         Result got{kNoCandidateScore, 0, 0};
         if (best_key) {
