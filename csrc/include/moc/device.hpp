@@ -25,7 +25,7 @@
 //     of an LDS-resident int8 difference profile feeds both, summed in the halves of one register
 //     (2 SDWA adds + 1 v_pk_max_i16 per two cells, no cross-lane moves); Tot_o from one anchor diagonal
 //     per tile + a suffix scan; the k of each record's winning offset recovered afterwards on that one
-//     diagonal. Used whenever the weights and Seq1 fit it (T range <= 127, L1 <= 3111).
+//     diagonal. Used whenever the weights and Seq1 fit it (T range <= 127, L1 <= 3052).
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -88,10 +88,16 @@ struct ProblemView {
 };
 
 // Entries after the tile16 profile's last row: reads of wave-tile lanes past the valid offsets reach
-// at most L1 + 128*U - 2 (U <= 8) into a row.
-constexpr int kProf16Overhang = 1024;
+// at most L1 + 128*U - 2 (U <= 4) into a row.
+constexpr int kProf16Overhang = 512;
 // LDS budget of one tile16 workgroup (the whole CU: a single workgroup may declare all 160 KiB).
 constexpr int kProf16MaxLds = 160 * 1024;
+// tile16 LDS image: profile (prof16_bytes, 16-aligned) | int8 LUT T[32][32] | Seq1 codes + pad (for
+// the per-tile anchor diagonal). Bytes of the whole image.
+constexpr int kProf16Lut8 = 1024;
+inline int64_t tile16_lds_bytes(int64_t prof16_bytes, int64_t L1) {
+  return prof16_bytes + kProf16Lut8 + ((L1 + 16 + 15) & ~int64_t{15});
+}
 
 // One batch of records on the device. Offsets are absolute (int64) and rebased by offsets[0], so
 // a chunk of a bigger CSR array can be transferred and launched without host-side rebasing.
@@ -122,7 +128,7 @@ struct Plan {
   const int32_t* long_recs = nullptr;  // device: records handled by the tile kernel (null = identity)
   int64_t n_long = 0;
   unsigned long long* keys = nullptr;  // device scratch, n_long entries (tile-kernel partial maxima)
-  int32_t u = 2;                       // sub-tiles per wave tile (1, 2 or 4; tile16 also 8)
+  int32_t u = 2;                       // sub-tiles per wave tile (1, 2 or 4)
   R2Params r2;                         // finalize: parameters of the R2 result format
 };
 
@@ -178,7 +184,7 @@ void launch_finalize_keys(const BatchView& bv, const Plan& plan, void* out, int 
 // then one wave per record recovers k on the winning diagonal and writes final keys.
 void launch_tile16_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream);
 // Waves per CU the tile16 kernel keeps resident (16-wave workgroups, as many as the LDS allows).
-int tile16_waves_per_cu(int prof16_bytes);
+int tile16_waves_per_cu(int lds_bytes);
 
 // One-wave self-test of the DPP / shuffle primitives (192 ints, see align_kernels.hip).
 void launch_dpp_probe(int* d_out, hipStream_t stream);

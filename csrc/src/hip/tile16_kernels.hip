@@ -17,7 +17,8 @@
 //     sub-tiles (128 offsets each) sit at immediate LDS offsets;
 //   * every 64 steps the int16 halves are folded into int32 (|partial sums| <= 64*128 < 2^15: exact);
 //   * Tot_o is not summed per cell: per tile one anchor diagonal Tot_{oA} (oA = first offset past the
-//     tile or past the valid range) is summed by the wave from the int32 LUT, and
+//     tile or past the valid range) is summed alongside the sweep (each chunk's lanes add their step's
+//     pair score from an int8 LUT + Seq1 staged next to the profile), and
 //     Tot_o = Tot_{oA} + sum_{o <= o' < oA} D_{o'}(L2) comes from a wave suffix scan.
 // Per offset this gives the best score, but not which k: the sweep reduces keys (score, ~(2o + mutated))
 // — the reference order: score, then smallest o, then k = 0 first — and resolve16_kernel re-walks only
@@ -26,8 +27,8 @@
 // csrc/tests/test_core.cpp test_profile16.
 //
 // Replaces calc_result (cudaFunctions.cu:63-176) for long records when the weights fit the profile
-// bytes (W1 + max(W2,W3,W4) <= 127) and the profile fits one CU's LDS (26*L1 + 1024 halfwords
-// <= 160 KiB: L1 <= 3111, covering the reference's 3000-letter Seq1 buffer, myProto.h:3).
+// bytes (W1 + max(W2,W3,W4) <= 127) and the LDS image fits one CU (2*(26*L1 + 512) + 1 KiB + L1 bytes
+// <= 160 KiB: L1 <= 3052, covering the reference's 3000-letter Seq1 buffer, myProto.h:3).
 #include <hip/hip_runtime.h>
 
 #include "kernel_common.hpp"
@@ -91,11 +92,16 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
                                                                  const int32_t* __restrict__ long_recs,
                                                                  unsigned long long* __restrict__ keys) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  {  // stage the profile (16-byte copies; the global buffer is padded to 16 bytes)
-    const uint4* src = reinterpret_cast<const uint4*>(pv.prof16);
+  // LDS image (tile16_lds_bytes): profile | int8 LUT | Seq1 codes (the anchor diagonals' operands)
+  int8_t* lut8 = reinterpret_cast<int8_t*>(smem + pv.prof16_bytes);
+  uint8_t* s1l = smem + pv.prof16_bytes + kProf16Lut8;
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(pv.prof16);  // 16-byte padded
     uint4* dst = reinterpret_cast<uint4*>(smem);
     const int n16 = pv.prof16_bytes >> 4;
     for (int t = threadIdx.x; t < n16; t += blockDim.x) dst[t] = src[t];
+    for (int t = threadIdx.x; t < kProf16Lut8; t += blockDim.x) lut8[t] = static_cast<int8_t>(pv.lut[t]);  // |T| <= 127
+    stage_bytes(s1l, pv.seq1, pv.L1 + 16);  // Seq1 + zero pad (device copy has kSeq1Pad zeros)
   }
   __syncthreads();
   const int64_t w = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock16 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -116,12 +122,10 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
     const int need = L2 <= L1 ? L1 - L2 + 1 : 1;
     const int ntiles = (need + kSpan - 1) / kSpan;
     const int t_stop = li == end_li ? min(end_t, ntiles) : ntiles;
-    // byte offset of (letter row, step) for this lane's step of the first chunk
-    auto row_off = [&](int i) {
-      const int c = i < steps ? static_cast<int>(rec[i]) : 1;
-      return max(c - 1, 0) * rowb + 2 * i;
-    };
-    const int so_first = row_off(lane);
+    // lane j of a chunk holds step i0 + j's letter (0 past the record) and its profile row/step offset
+    auto letter = [&](int i) { return i < steps ? static_cast<int>(rec[i]) : 0; };
+    auto row_off = [&](int c, int i) { return max(c - 1, 0) * rowb + 2 * i; };
+    const int c_first = letter(lane);
     unsigned long long acc64 = 0;
     for (; t < t_stop && L2 <= L1; ++t) {
       const int o0 = t * kSpan;
@@ -162,25 +166,33 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
           best[u] = kBestInit;
         }
       };
-      int so = so_first;
+      // Tot of the anchor offset oA (first offset past the tile or past the valid range): each chunk's
+      // lanes add their step's pair score from LDS while the sweep runs
+      const int oA = min(o0 + kSpan, need);
+      int anchor = 0;
+      auto anchor_add = [&](int c, int i) {
+        if (c != 0) anchor += lut8[c * kLutStride + s1l[oA + i]];
+      };
+      int c = c_first;
       int i0 = 0;
       for (; i0 + 64 < steps; i0 += 64) {  // full chunks (the record's last letter lies beyond)
-        const int so_next = row_off(i0 + 64 + lane);
+        const int c_next = letter(i0 + 64 + lane);
+        const int so = row_off(c, i0 + lane);
+        anchor_add(c, i0 + lane);
 #pragma unroll 16
         for (int j = 0; j < 64; ++j) step(so, j, true);
         flush(true);
-        so = so_next;
+        c = c_next;
       }
       if (steps > 0) {  // last chunk: 1..64 steps; no hyphen after the final letter
         const int m = steps - i0;
+        const int so = row_off(c, i0 + lane);
+        anchor_add(c, i0 + lane);
         for (int j = 0; j < m - 1; ++j) step(so, j, true);
         step(so, m - 1, false);
         flush(m > 1);
       }
       // ---- Tot per offset: anchor diagonal oA, then suffix sums of the D totals (valid offsets only)
-      const int oA = min(o0 + kSpan, need);
-      int anchor = 0;
-      for (int i = lane; i < steps; i += 64) anchor += pv.lut[rec[i] * kLutStride + pv.seq1[oA + i]];
 #pragma unroll
       for (int d = 32; d >= 1; d >>= 1) anchor += __shfl_xor(anchor, d, 64);
       int carry = anchor;  // Tot at the end of the sub-tile being processed
@@ -254,8 +266,8 @@ __global__ __launch_bounds__(256) void resolve16_kernel(ProblemView pv, BatchVie
     keys[li] = final_key(score, static_cast<uint32_t>(o) * static_cast<uint32_t>(L2) + static_cast<uint32_t>(k));
 }
 
-int tile16_waves_per_cu(int prof16_bytes) {
-  const int blocks = prof16_bytes > 0 ? kProf16MaxLds / prof16_bytes : 2;
+int tile16_waves_per_cu(int lds_bytes) {
+  const int blocks = lds_bytes > 0 ? kProf16MaxLds / lds_bytes : 2;
   return kWavesPerBlock16 * max(1, min(2, blocks));
 }
 
@@ -270,20 +282,20 @@ void launch16_t(const ProblemView& pv, const BatchView& bv, const Plan& plan, hi
   }
   const int64_t blocks = (plan.n_waves + kWavesPerBlock16 - 1) / kWavesPerBlock16;
   hipLaunchKernelGGL((tile16_search_kernel<U>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock16),
-                     static_cast<size_t>(pv.prof16_bytes), stream, pv, bv, plan.starts, plan.n_waves, plan.long_recs,
+                     static_cast<size_t>(tile16_lds_bytes(pv.prof16_bytes, pv.L1)), stream, pv, bv, plan.starts, plan.n_waves, plan.long_recs,
                      plan.keys);
 }
 }  // namespace
 
 void launch_tile16_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream) {
-  if (!pv.prof16 || pv.prof16_bytes <= 0 || pv.prof16_bytes > kProf16MaxLds || (pv.prof16_bytes & 15))
+  if (!pv.prof16 || pv.prof16_bytes <= 0 || tile16_lds_bytes(pv.prof16_bytes, pv.L1) > kProf16MaxLds ||
+      (pv.prof16_bytes & 15))
     throw Error("launch_tile16_keys: no usable profile");
   if (plan.n_long > 0) MOC_HIP_CHECK(hipMemsetAsync(plan.keys, 0, sizeof(unsigned long long) * plan.n_long, stream));
   if (plan.n_waves <= 0) return;
   switch (plan.u) {
     case 1: launch16_t<1>(pv, bv, plan, stream); break;
     case 2: launch16_t<2>(pv, bv, plan, stream); break;
-    case 8: launch16_t<8>(pv, bv, plan, stream); break;
     default: launch16_t<4>(pv, bv, plan, stream); break;
   }
   const int64_t rb = (plan.n_long + 3) / 4;

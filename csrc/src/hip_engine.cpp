@@ -110,7 +110,7 @@ HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
   if (const char* g = std::getenv("MOC_GRAPHS")) opt_.use_graphs = std::atoi(g) != 0;
   if (const char* u = std::getenv("MOC_TILE_U")) {  // tuning override of the per-batch choice
     const int v = std::atoi(u);
-    if (v == 1 || v == 2 || v == 4 || (v == 8 && tile16_)) tile_u_ = v;
+    if (v == 1 || v == 2 || v == 4) tile_u_ = v;
   }
   if (const char* t16 = std::getenv("MOC_TILE16")) tile16_ = std::atoi(t16) != 0;
   if (const char* w = std::getenv("MOC_TILE_WAVES_PER_CU")) {
@@ -228,7 +228,7 @@ void HipEngine::set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, S
   prof16_bytes_ = 0;
   Profile16 prof;
   const int64_t pbytes = ((2 * ((kAlphabet - 1) * L1 + dev::kProf16Overhang)) + 15) & ~int64_t{15};
-  if (tile16_ && L1 > 0 && pbytes <= dev::kProf16MaxLds &&
+  if (tile16_ && L1 > 0 && dev::tile16_lds_bytes(pbytes, L1) <= dev::kProf16MaxLds &&
       build_profile16(table_, padded.data(), L1, dev::kProf16Overhang, prof)) {
     prof.entries.resize(static_cast<size_t>(pbytes / 2), 0);
     MOC_HIP_CHECK(hipMalloc(&d_prof16_, static_cast<size_t>(pbytes)));
@@ -386,7 +386,7 @@ std::vector<dev::WaveStart> HipEngine::plan_waves(const int64_t* offsets, const 
     return dev::WaveStart{static_cast<int32_t>(li), static_cast<int32_t>(t)};
   };
   const int64_t part_tiles = std::max<int64_t>(1, total_tiles * (hi - lo) / std::max<int64_t>(C, 1));
-  const int waves_per_cu = d_prof16_ ? dev::tile16_waves_per_cu(prof16_bytes_) : tile_waves_per_cu_;
+  const int waves_per_cu = d_prof16_ ? dev::tile16_waves_per_cu(static_cast<int>(dev::tile16_lds_bytes(prof16_bytes_, L1_))) : tile_waves_per_cu_;
   const int64_t n_waves = std::min<int64_t>(part_tiles, static_cast<int64_t>(num_cus_) * waves_per_cu);
   starts.resize(static_cast<size_t>(n_waves) + 1);
   for (int64_t w = 0; w <= n_waves; ++w) starts[w] = locate(lo + (hi - lo) * w / n_waves);

@@ -203,11 +203,11 @@ void test_profile16() {
     std::vector<uint8_t> s1(static_cast<size_t>(L1));
     for (auto& x : s1) x = static_cast<uint8_t>(1 + rng() % (trial % 3 ? 26 : 3));  // few letters: many ties
     Profile16 prof;
-    if (!build_profile16(t, s1.data(), L1, 1024, prof)) {
+    if (!build_profile16(t, s1.data(), L1, 512, prof)) {
       CHECK(w.w[0] + std::max({w.w[1], w.w[2], w.w[3]}) > 127);
       continue;
     }
-    CHECK(prof.entries.size() == static_cast<size_t>(26 * L1 + 1024));
+    CHECK(prof.entries.size() == static_cast<size_t>(26 * L1 + 512));
     auto entry = [&](int c, int64_t j) { return prof.entries[static_cast<size_t>((c - 1) * L1 + j)]; };
     RecordBatch batch;
     for (int r = 0; r < 6; ++r) {
