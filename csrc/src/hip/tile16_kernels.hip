@@ -31,6 +31,9 @@
 // <= 160 KiB: L1 <= 3052, covering the reference's 3000-letter Seq1 buffer, myProto.h:3).
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+#include <set>
+
 #include "kernel_common.hpp"
 #include "moc/runtime/hip_check.hpp"
 
@@ -274,11 +277,17 @@ int tile16_waves_per_cu(int lds_bytes) {
 namespace {
 template <int U>
 void launch16_t(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream) {
-  static bool attr_set = false;  // dynamic LDS above 64 KiB must be declared once per kernel
-  if (!attr_set) {
-    MOC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&tile16_search_kernel<U>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, kProf16MaxLds));
-    attr_set = true;
+  // dynamic LDS above 64 KiB is declared per kernel and device (engines may live on several devices
+  // and threads of one process)
+  static std::mutex mu;
+  static std::set<int> declared;
+  int dev = 0;
+  MOC_HIP_CHECK(hipGetDevice(&dev));
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    if (declared.insert(dev).second)
+      MOC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&tile16_search_kernel<U>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, kProf16MaxLds));
   }
   const int64_t blocks = (plan.n_waves + kWavesPerBlock16 - 1) / kWavesPerBlock16;
   hipLaunchKernelGGL((tile16_search_kernel<U>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock16),
