@@ -134,6 +134,12 @@ def main():
         else:
             dist.init_process_group("gloo")
 
+    t_setup = time.perf_counter()
+
+    def progress(msg):  # setup of big batches takes minutes: keep stderr alive (rank 0)
+        if rank == 0:
+            print(f"[bench] {time.perf_counter() - t_setup:7.1f}s {msg}", file=sys.stderr, flush=True)
+
     def barrier():
         if distributed:
             if nccl:
@@ -157,8 +163,10 @@ def main():
     lengths = rrng.integers(shape.l2_min, shape.l2_max + 1, size=R, dtype=np.int64)
     tag = os.environ.get("MASTER_PORT", str(os.getpid()))
     narrow4 = bool(args.narrow) and shape.l2_max - shape.l2_min <= 15
+    progress(f"generating {R} records per rank")
     host = HostArrays(tag, rank, lengths, bool(args.shm), args.packed, args.seed + 101 + rank,
                       shape.l2_min if narrow4 else None)
+    progress(f"{int(host.offsets[-1])} letters per rank ready")
     del lengths
     eng = HipSearchEngine(device=gpu)
     eng.set_problem(weights, seq1)
@@ -171,6 +179,7 @@ def main():
     else:
         host.results = np.empty(R, dtype=rdt)
     pin = Pinned(host.codes, host.offsets, host.lengths, host.results)
+    progress("host arrays page-locked; warm-up")
     done = torch.zeros(1, dtype=torch.int64, device=cdev)
     hdr_host = np.empty(4 + shape.L1, dtype=np.int32)
 
@@ -189,6 +198,7 @@ def main():
     for _ in range(args.warmup):
         step()
     barrier()
+    progress(f"timing {args.steps} steps")
     t0 = time.perf_counter()
     kms, tms = [], []
     for _ in range(args.steps):
