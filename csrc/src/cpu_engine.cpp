@@ -15,18 +15,6 @@ int64_t candidate_offsets(int64_t L1, int64_t L2, Semantics sem) {
 
 namespace {
 
-// prefix[k] = P_d(k) for k = 0..L2 (diagonal d: Seq2[i] faces Seq1[i+d]).
-inline void diag_prefix(const ScoreTable& t, const uint8_t* s1, const uint8_t* s2, int64_t L2, int64_t d,
-                        int32_t* prefix) {
-  int32_t acc = 0;
-  prefix[0] = 0;
-  const uint8_t* a = s1 + d;
-  for (int64_t i = 0; i < L2; ++i) {
-    acc += t.lut[s2[i] * kLutStride + a[i]];
-    prefix[i + 1] = acc;
-  }
-}
-
 inline void consider(Result& best, int32_t score, int64_t o, int64_t k) {
   Result c{score, static_cast<int32_t>(o), static_cast<int32_t>(k)};
   if (best.n < 0 || better(c, best)) best = c;
@@ -47,16 +35,40 @@ Result solve_offsets(const ScoreTable& t, const uint8_t* s1, int64_t L1, const u
     return best;
   }
   const int64_t last_mut_off = L1 - L2;  // offsets with a hyphen need o + L2 + 1 <= L1
-  std::vector<int32_t> cur(L2 + 1), nxt(L2 + 1);
-  diag_prefix(t, s1, s2, L2, o_begin, cur.data());
+  // per-thread scratch (no allocation per record): LUT row of every Seq2 letter, and P_o(1..L2) of the
+  // current diagonal; each offset then takes ONE fused pass over its neighbour diagonal: prefix
+  // P_{o+1}(i+1), difference D_o(i+1) = P_o(i+1) - P_{o+1}(i+1) and its running max (strict '>': the
+  // smallest k wins ties, as the reference loop order does)
+  thread_local std::vector<const int32_t*> rows;
+  thread_local std::vector<int32_t> cur;
+  if (static_cast<int64_t>(rows.size()) < L2) rows.resize(static_cast<size_t>(L2));
+  if (static_cast<int64_t>(cur.size()) < L2 + 1) cur.resize(static_cast<size_t>(L2) + 1);
+  for (int64_t i = 0; i < L2; ++i) rows[i] = t.lut.data() + s2[i] * kLutStride;
+  const int32_t* const* rw = rows.data();
+  int32_t* P = cur.data();
+  {
+    int32_t acc = 0;
+    const uint8_t* a = s1 + o_begin;
+    for (int64_t i = 0; i < L2; ++i) P[i + 1] = acc += rw[i][a[i]];
+  }
   for (int64_t o = o_begin; o < o_end; ++o) {
-    consider(best, cur[L2], o, 0);
-    if (o < last_mut_off) {
-      diag_prefix(t, s1, s2, L2, o + 1, nxt.data());
-      const int32_t tot_next = nxt[L2];
-      for (int64_t k = 1; k < L2; ++k) consider(best, cur[k] - nxt[k] + tot_next, o, k);
-      std::swap(cur, nxt);
+    consider(best, P[L2], o, 0);
+    if (o >= last_mut_off) continue;
+    const uint8_t* a = s1 + o + 1;
+    int32_t q = 0, bd = INT32_MIN;
+    int64_t bk = 0;
+    for (int64_t i = 0; i + 1 < L2; ++i) {  // candidates k = i + 1 = 1 .. L2-1
+      q += rw[i][a[i]];
+      const int32_t d = P[i + 1] - q;
+      P[i + 1] = q;  // becomes P_{o+1}(i+1) for the next offset
+      if (d > bd) {
+        bd = d;
+        bk = i + 1;
+      }
     }
+    q += rw[L2 - 1][a[L2 - 1]];
+    P[L2] = q;  // Tot_{o+1}
+    if (L2 >= 2) consider(best, bd + q, o, bk);
   }
   return best;
 }
