@@ -138,6 +138,9 @@ class HipEngine {
   ScoreTable table_{};
   int32_t min_t_ = 0, max_t_ = 0;  // pair-score range over letters (R2 parameters)
   R2Params r2_{};                  // R2 parameters of the current solve
+  void* d_image_ = nullptr;  // problem image: LUT | Seq1 | profile (views below)
+  size_t d_image_cap_ = 0;
+  std::vector<uint8_t> image_;
   int32_t* d_lut_ = nullptr;
   uint8_t* d_seq1_ = nullptr;
   uint16_t* d_prof16_ = nullptr;  // tile16 profile (null: the problem does not fit it, or MOC_TILE16=0)

@@ -161,9 +161,7 @@ HipEngine::~HipEngine() {
   (void)hipEventDestroy(ev_plan_);
   (void)hipEventDestroy(ev_a_);
   (void)hipEventDestroy(ev_b_);
-  (void)hipFree(d_lut_);
-  (void)hipFree(d_seq1_);
-  (void)hipFree(d_prof16_);
+  (void)hipFree(d_image_);
   (void)hipStreamDestroy(s_copy_);
   (void)hipStreamDestroy(s_compute_);
   (void)hipStreamDestroy(s_return_);
@@ -211,30 +209,36 @@ void HipEngine::set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, S
     }
   L1_ = L1;
   sem_ = sem;
-  if (!d_lut_) MOC_HIP_CHECK(hipMalloc(&d_lut_, sizeof(int32_t) * kLutStride * kLutStride));
+  // One device image per problem, uploaded with one copy: LUT | Seq1 + zero pad | tile16 profile. The
+  // buffer only grows, so repeated problems (one per job step) cost no allocation, and kernel arguments
+  // (and a captured direct-path graph) keep pointing at the same addresses.
   const size_t s1bytes = static_cast<size_t>(L1) + dev::kSeq1Pad;
-  std::vector<uint8_t> padded(s1bytes, 0);
-  if (L1) std::memcpy(padded.data(), seq1, static_cast<size_t>(L1));
-  // Kernels of a previous problem may still be queued on our streams: order the uploads behind them
-  // on the compute stream (no device-wide synchronisation).
-  MOC_HIP_CHECK(hipStreamSynchronize(s_compute_));
-  MOC_HIP_CHECK(hipFree(d_seq1_));
-  MOC_HIP_CHECK(hipMalloc(&d_seq1_, s1bytes));
-  MOC_HIP_CHECK(hipMemcpy(d_lut_, table_.lut.data(), sizeof(int32_t) * table_.lut.size(), hipMemcpyHostToDevice));
-  MOC_HIP_CHECK(hipMemcpy(d_seq1_, padded.data(), s1bytes, hipMemcpyHostToDevice));
-  // tile16 long-record kernel: packed (D, S) Seq1 profile, staged whole into one CU's LDS
-  MOC_HIP_CHECK(hipFree(d_prof16_));
-  d_prof16_ = nullptr;
-  prof16_bytes_ = 0;
+  const size_t lut_bytes = sizeof(int32_t) * table_.lut.size();
+  const size_t s1_off = (lut_bytes + 255) & ~size_t{255};
+  const size_t prof_off = (s1_off + s1bytes + 255) & ~size_t{255};
   Profile16 prof;
   const int64_t pbytes = ((2 * ((kAlphabet - 1) * L1 + dev::kProf16Overhang)) + 15) & ~int64_t{15};
-  if (tile16_ && L1 > 0 && dev::tile16_lds_bytes(pbytes, L1) <= dev::kProf16MaxLds &&
-      build_profile16(table_, padded.data(), L1, dev::kProf16Overhang, prof)) {
-    prof.entries.resize(static_cast<size_t>(pbytes / 2), 0);
-    MOC_HIP_CHECK(hipMalloc(&d_prof16_, static_cast<size_t>(pbytes)));
-    MOC_HIP_CHECK(hipMemcpy(d_prof16_, prof.entries.data(), static_cast<size_t>(pbytes), hipMemcpyHostToDevice));
-    prof16_bytes_ = static_cast<int32_t>(pbytes);
+  const bool t16 = tile16_ && L1 > 0 && dev::tile16_lds_bytes(pbytes, L1) <= dev::kProf16MaxLds &&
+                   build_profile16(table_, seq1, L1, dev::kProf16Overhang, prof);
+  const size_t total = t16 ? prof_off + static_cast<size_t>(pbytes) : prof_off;
+  image_.assign(total, 0);
+  std::memcpy(image_.data(), table_.lut.data(), lut_bytes);
+  if (L1) std::memcpy(image_.data() + s1_off, seq1, static_cast<size_t>(L1));
+  if (t16) std::memcpy(image_.data() + prof_off, prof.entries.data(), sizeof(uint16_t) * prof.entries.size());
+  // Kernels of the previous problem may still be queued — on our streams or on a solve_device caller's —
+  // and read the image in place: let them finish before it is overwritten.
+  MOC_HIP_CHECK(hipDeviceSynchronize());
+  if (total > d_image_cap_) {
+    MOC_HIP_CHECK(hipFree(d_image_));
+    d_image_cap_ = std::max(total, size_t{64} << 10);
+    MOC_HIP_CHECK(hipMalloc(&d_image_, d_image_cap_));
   }
+  MOC_HIP_CHECK(hipMemcpy(d_image_, image_.data(), total, hipMemcpyHostToDevice));
+  char* base = static_cast<char*>(d_image_);
+  d_lut_ = reinterpret_cast<int32_t*>(base);
+  d_seq1_ = reinterpret_cast<uint8_t*>(base + s1_off);
+  d_prof16_ = t16 ? reinterpret_cast<uint16_t*>(base + prof_off) : nullptr;
+  prof16_bytes_ = t16 ? static_cast<int32_t>(pbytes) : 0;
   have_problem_ = true;
 }
 
