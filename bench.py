@@ -282,7 +282,7 @@ def main():
             "letters": "packed5" if host.packed else "bytes",
             "rank0_numa_node": numa,
             "rank0_kernels": st["kernels"],
-            "zero_copy": bool(st["direct"]),
+            "host_stream": ("dma" if st["dma"] else "zero_copy") if st["direct"] else "staged",
             "verified": bool(okt.item()),
         }
         print(json.dumps(out), flush=True)

@@ -93,7 +93,7 @@ int moc_engine_search_keys_device(void* e, const uint8_t* d_codes, const int64_t
 int moc_engine_finalize_keys_device(void* e, const int64_t* d_offsets, int64_t n, const uint64_t* d_keys, void* d_out,
                                     int fmt, void* stream);
 /* stats: kernel_ms, total_ms, h2d_bytes, d2h_bytes, chunks, cells, records, direct, format, kernels */
-int moc_engine_stats(void* e, double* out10);
+int moc_engine_stats(void* e, double* out14);
 
 #ifdef __cplusplus
 }

@@ -345,9 +345,11 @@ int moc_engine_finalize_keys_device(void* e, const int64_t* d_offsets, int64_t n
   });
 }
 
-int moc_engine_stats(void* e, double* out13) {
+int moc_engine_stats(void* e, double* out14) {
   return guard([&] {
-    double* out10 = out13;
+    double* out13 = out14;
+    double* out10 = out14;
+    out14[13] = static_cast<double>(static_cast<moc::HipEngine*>(e)->stats().dma);
     const auto& s = static_cast<moc::HipEngine*>(e)->stats();
     out13[10] = s.r2.smin;
     out13[11] = s.r2.kw;

@@ -4,6 +4,10 @@
 //   kind 2: H2D + D2H concurrently (two streams, reports the sum)
 //   kind 3: zero-copy kernel read of pinned host   kind 4: zero-copy kernel write to pinned host
 //   kind 5: D2D hipMemcpyAsync (HBM copy, reports read+write bytes)
+//   the streaming search's mix (3 bytes in per byte out), reported as bytes IN per second:
+//   kind 6: zero-copy read + zero-copy write (one third) concurrently
+//   kind 7: H2D hipMemcpyAsync + zero-copy write (one third) concurrently
+//   kind 8: H2D + D2H hipMemcpyAsync (one third) concurrently
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -57,6 +61,18 @@ double transfer_probe(int kind, size_t bytes, int iters) {
         break;
       case 3: hipLaunchKernelGGL(zc_read_kernel, dim3(2048), dim3(256), 0, s1, static_cast<const uint4*>(h), n16, sink); break;
       case 4: hipLaunchKernelGGL(zc_write_kernel, dim3(2048), dim3(256), 0, s1, static_cast<uint4*>(h), n16); break;
+      case 6:
+        hipLaunchKernelGGL(zc_read_kernel, dim3(2048), dim3(256), 0, s1, static_cast<const uint4*>(h), n16, sink);
+        hipLaunchKernelGGL(zc_write_kernel, dim3(1024), dim3(256), 0, s2, static_cast<uint4*>(h2), n16 / 3);
+        break;
+      case 7:
+        MOC_HIP_CHECK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s1));
+        hipLaunchKernelGGL(zc_write_kernel, dim3(1024), dim3(256), 0, s2, static_cast<uint4*>(h2), n16 / 3);
+        break;
+      case 8:
+        MOC_HIP_CHECK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s1));
+        MOC_HIP_CHECK(hipMemcpyAsync(h2, d2, (n16 / 3) * 16, hipMemcpyDeviceToHost, s2));
+        break;
       default: MOC_HIP_CHECK(hipMemcpyAsync(d2, d, bytes, hipMemcpyDeviceToDevice, s1)); break;
     }
   };

@@ -113,6 +113,8 @@ HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
     if (v == 1 || v == 2 || v == 4) tile_u_ = v;
   }
   if (const char* t16 = std::getenv("MOC_TILE16")) tile16_ = std::atoi(t16) != 0;
+  if (const char* d = std::getenv("MOC_DMA_STREAM")) opt_.dma_stream = std::atoi(d);
+  if (const char* d = std::getenv("MOC_DMA_CHUNK_BYTES")) opt_.dma_chunk_bytes = std::max<int64_t>(std::atoll(d), 1);
   if (const char* w = std::getenv("MOC_TILE_WAVES_PER_CU")) {
     const int v = std::atoi(w);
     if (v >= 1 && v <= 32) tile_waves_per_cu_ = v;
@@ -120,7 +122,7 @@ HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
   MOC_HIP_CHECK(hipStreamCreateWithFlags(&s_copy_, hipStreamNonBlocking));
   MOC_HIP_CHECK(hipStreamCreateWithFlags(&s_compute_, hipStreamNonBlocking));
   MOC_HIP_CHECK(hipStreamCreateWithFlags(&s_return_, hipStreamNonBlocking));
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < 3; ++i) {  // run_staged cycles two, run_dma_stream three
     auto s = std::make_unique<Slot>();
     MOC_HIP_CHECK(hipEventCreateWithFlags(&s->ev_h2d, hipEventDisableTiming));
     MOC_HIP_CHECK(hipEventCreate(&s->ev_k0));
@@ -505,6 +507,12 @@ void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uin
   if (opt_.allow_direct && (swipe || (!packed5 && dev::configure_short(L1_, ls.mn, ls.mx, a))) &&
       direct_pointers(codes, offsets, lengths, len_bits, len_base, n, out, fb, packed5, a)) {
     const dev::ProblemView pv = problem_view(ls.mx);
+    if (opt_.dma_stream) {
+      run_dma_stream(pv, a, swipe, codes, offsets, lengths, len_bits, n, out, fb, packed5);
+      wall.stop();
+      stats_.total_ms = wall.total_ms();
+      return;
+    }
     MOC_HIP_CHECK(hipEventRecord(ev_a_, s_compute_));
     launch_direct(pv, a, swipe);
     stats_.kernels = swipe ? 1 : 2;
@@ -525,6 +533,83 @@ void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uin
   run_staged(codes, offsets, n, out, fmt, packed5);
   wall.stop();
   stats_.total_ms = wall.total_ms();
+}
+
+// Pinned-host batches through the copy engines: chunks of whole kernel tiles are copied H2D (letters +
+// narrow lengths) on s_copy_, searched from HBM by the same streaming kernel on s_compute_, and their
+// results copied D2H on s_return_, three slots deep, ordered by events only (no host waits inside). The
+// SDMA engines sustain ~57 GB/s in against a concurrent result stream, where the kernel's own zero-copy
+// reads reach 45-51 (profiles/transfer_probe.log "mix3to1_*"). The kernel still reads two offsets per
+// tile from pinned host memory (a.offsets); letters, lengths and results live in the slot buffers, with
+// base pointers shifted so the kernel's absolute indexing lands inside them.
+void HipEngine::run_dma_stream(const dev::ProblemView& pv, const dev::ShortArgs& a0, bool swipe, const uint8_t* codes,
+                               const int64_t* offsets, const uint8_t* lengths, int len_bits, int64_t n, void* out,
+                               int fb, bool packed5) {
+  const int64_t tile = std::max<int64_t>(a0.tile_records, 2);  // even: nibble lengths stay byte aligned
+  const int64_t letters = offsets[n] - offsets[0];
+  const int64_t total_bytes = packed5 ? (5 * letters + 7) / 8 : letters;
+  const int64_t per_rec = std::max<int64_t>(1, total_bytes / std::max<int64_t>(n, 1));
+  int64_t chunk = std::max<int64_t>(tile, (opt_.dma_chunk_bytes / per_rec) / tile * tile);
+  const int64_t n_chunks = (n + chunk - 1) / chunk;
+  for (int64_t c = 0; c < n_chunks; ++c) {
+    const int64_t r0 = c * chunk, r1 = std::min(n, r0 + chunk), cn = r1 - r0;
+    Slot& s = *slots_[c % slots_.size()];
+    // letters: bytes [B0, b1 + 16) of the stream, B0 aligned down to 16 (the kernel stages 16-byte words)
+    const int64_t b0 = packed5 ? (5 * offsets[r0]) >> 3 : offsets[r0];
+    const int64_t b1 = packed5 ? ((5 * offsets[r1] + 7) >> 3) + 1 : offsets[r1];
+    const int64_t B0 = b0 & ~int64_t{15};
+    const size_t lbytes = static_cast<size_t>(b1 - B0) + 16;
+    const size_t nbytes = lengths ? (len_bits == 4 ? static_cast<size_t>((cn + 1) / 2) : static_cast<size_t>(cn)) : 0;
+    const size_t rbytes = static_cast<size_t>(fb) * static_cast<size_t>(cn);
+    if (s.busy) {  // the slot's previous chunk: its letters consumed, its results returned
+      MOC_HIP_CHECK(hipEventSynchronize(s.ev_done));
+      s.busy = false;
+    }
+    ensure(s.d_packed, s.d_packed_cap, lbytes);
+    ensure(s.d_offsets, s.d_offsets_cap, std::max<size_t>(nbytes, 16));
+    ensure(s.d_out, s.d_out_cap, std::max<size_t>(rbytes, 16));
+    MOC_HIP_CHECK(hipMemcpyAsync(s.d_packed, codes + B0, lbytes, hipMemcpyHostToDevice, s_copy_));
+    if (nbytes) {
+      const size_t nb0 = len_bits == 4 ? static_cast<size_t>(r0 / 2) : static_cast<size_t>(r0);
+      MOC_HIP_CHECK(hipMemcpyAsync(s.d_offsets, lengths + nb0, nbytes, hipMemcpyHostToDevice, s_copy_));
+    }
+    MOC_HIP_CHECK(hipEventRecord(s.ev_h2d, s_copy_));
+    MOC_HIP_CHECK(hipStreamWaitEvent(s_compute_, s.ev_h2d, 0));
+    dev::ShortArgs a = a0;
+    a.codes = static_cast<const uint8_t*>(s.d_packed) - B0;
+    a.dbg_codes_end = B0 + static_cast<int64_t>(lbytes);
+    a.offsets = a0.offsets + r0;  // pinned host (zero-copy): two reads per tile
+    a.lengths8 = lengths && len_bits == 8 ? static_cast<const uint8_t*>(s.d_offsets) : nullptr;
+    a.lengths4 = lengths && len_bits == 4 ? static_cast<const uint8_t*>(s.d_offsets) : nullptr;
+    a.n = cn;
+    a.out = s.d_out;
+    if (c == 0) MOC_HIP_CHECK(hipEventRecord(ev_a_, s_compute_));
+    if (swipe)
+      dev::launch_swipe(pv, a, num_cus_, s_compute_);
+    else
+      dev::launch_short(pv, a, num_cus_, s_compute_);
+    MOC_HIP_CHECK(hipGetLastError());
+    MOC_HIP_CHECK(hipEventRecord(s.ev_k1, s_compute_));
+    MOC_HIP_CHECK(hipStreamWaitEvent(s_return_, s.ev_k1, 0));
+    MOC_HIP_CHECK(hipMemcpyAsync(static_cast<char*>(out) + r0 * fb, s.d_out, rbytes, hipMemcpyDeviceToHost, s_return_));
+    MOC_HIP_CHECK(hipEventRecord(s.ev_done, s_return_));
+    s.busy = true;
+    stats_.h2d_bytes += static_cast<int64_t>(lbytes + nbytes);
+    stats_.d2h_bytes += static_cast<int64_t>(rbytes);
+  }
+  MOC_HIP_CHECK(hipEventRecord(ev_b_, s_compute_));
+  for (auto& sp : slots_)
+    if (sp->busy) {
+      MOC_HIP_CHECK(hipEventSynchronize(sp->ev_done));
+      sp->busy = false;
+    }
+  float ms = 0;
+  MOC_HIP_CHECK(hipEventElapsedTime(&ms, ev_a_, ev_b_));
+  stats_.kernel_ms = ms;  // compute-stream span: first kernel start .. last kernel end
+  stats_.kernels = swipe ? 1 : 2;
+  stats_.direct = 1;
+  stats_.dma = 1;
+  stats_.chunks = n_chunks;
 }
 
 // The direct path's launch sequence (work-counter reset + persistent streaming kernel) as a hipGraph:

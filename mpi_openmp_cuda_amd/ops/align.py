@@ -260,12 +260,13 @@ class HipSearchEngine:
         return out_t
 
     def stats(self) -> dict:
-        v = (ctypes.c_double * 13)()
+        v = (ctypes.c_double * 14)()
         _lib.check(_lib.lib().moc_engine_stats(self._h, v))
         keys = ["kernel_ms", "total_ms", "h2d_bytes", "d2h_bytes", "chunks", "cells", "records", "direct", "format",
                 "kernels"]
         d = dict(zip(keys, list(v)[:10]))
         d["r2"] = tuple(int(x) for x in list(v)[10:13])
+        d["dma"] = int(v[13])
         d["format"] = _lib.FORMAT_NAMES[int(d["format"])]
         d["kernels"] = [k for b, k in ((1, "swipe"), (2, "short"), (4, "tiles"), (8, "tile16")) if int(d["kernels"]) & b]
         return d

@@ -357,6 +357,44 @@ def test_r2_results_and_nibble_lengths(pinned, packed, shape, n):
     eng.close()
 
 
+@pytest.mark.parametrize("mode", ["dma", "zero_copy"])
+@pytest.mark.parametrize("packed,len_bits", [(False, 0), (False, 8), (True, 4), (True, 8)])
+@pytest.mark.parametrize("shape,n", [("input6", 100_003), ("input1", 20_001)])
+def test_host_stream_modes(monkeypatch, mode, packed, len_bits, shape, n):
+    # pinned host batches: chunked SDMA in/out around the HBM-resident kernel (64 KiB chunks: many of
+    # them, odd tail) or the kernel's own zero-copy reads/writes — same answers
+    from mpi_openmp_cuda_amd import _lib
+    from mpi_openmp_cuda_amd.models.problem import pack5, pack_lengths4
+    from mpi_openmp_cuda_amd.utils.synthetic import SHAPES
+
+    monkeypatch.setenv("MOC_DMA_STREAM", "1" if mode == "dma" else "0")
+    monkeypatch.setenv("MOC_DMA_CHUNK_BYTES", str(64 << 10))
+    sh = SHAPES[shape]
+    prob = make_synthetic(shape, n, seed=n + len_bits)
+    if packed and shape != "input6":
+        pytest.skip("packed letters stream into the swipe kernel only")
+    eng = HipSearchEngine(device=0)
+    eng.set_problem(prob.weights, prob.seq1)
+    codes = pack5(prob.codes) if packed else prob.codes
+    kw = {}
+    lengths = None
+    if len_bits == 8:
+        lengths = np.diff(prob.offsets).astype(np.uint8)
+        kw = dict(lengths=lengths)
+    elif len_bits == 4:
+        lengths = pack_lengths4(np.diff(prob.offsets), sh.l2_min)
+        kw = dict(lengths=lengths, lengths_bits=4, lengths_base=sh.l2_min)
+    out = np.zeros(prob.n, dtype=_lib.FORMAT_DTYPES[_lib.FORMAT_NAMES.index("r8")])
+    eng.pin(codes, prob.offsets, out, *([lengths] if lengths is not None else []))
+    eng.solve(codes, prob.offsets, out=out, fmt="r8", packed5=packed, **kw)
+    st = eng.stats()
+    assert st["direct"] == 1 and st["dma"] == (1 if mode == "dma" else 0), st
+    if mode == "dma":
+        assert st["chunks"] > 3, st
+    assert np.array_equal(as_triples(out), as_triples(search_cpu(prob))), st
+    eng.close()
+
+
 @pytest.mark.parametrize("L1,lo,hi,kernel", [(90, 3, 11, "tile16"), (40, 33, 38, "short")])
 def test_r2_tiles_and_short_kernels(engine, L1, lo, hi, kernel):
     # R2 through the tile kernel's finalize and the lane/offset kernel (staged path)
