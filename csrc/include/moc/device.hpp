@@ -85,6 +85,7 @@ struct ProblemView {
   // entries + overhang, padded to 16 bytes; null when the problem does not fit it (weights or LDS)
   const uint16_t* prof16 = nullptr;
   int32_t prof16_bytes = 0;
+  int32_t max_abs_t = 0;  // max |T| over the table (int16-exactness checks of the packed kernels)
 };
 
 // Entries after the tile16 profile's last row: reads of wave-tile lanes past the valid offsets reach

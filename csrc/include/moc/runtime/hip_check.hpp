@@ -14,6 +14,7 @@
 namespace moc {
 
 [[noreturn]] inline void throw_hip(hipError_t e, const char* what, const char* file, int line) {
+  (void)hipGetLastError();  // the failure is reported here: do not leave it to the next API call on this thread
   throw Error(std::string(file) + ":" + std::to_string(line) + " " + what + ": " + hipGetErrorName(e) + " (" +
               hipGetErrorString(e) + ")");
 }

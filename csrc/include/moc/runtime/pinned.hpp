@@ -10,6 +10,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <utility>
 #include <vector>
 
 namespace moc {
@@ -26,6 +27,11 @@ bool covers(const void* p, size_t bytes);
 // address space this is p itself; a runtime that maps registrations elsewhere gets single-registration
 // ranges only.
 const void* device_address(const void* p, size_t bytes);
+// Splits [p, p+bytes) at the boundaries of the registrations it touches: each piece (offset, length)
+// lies inside ONE registration or outside all of them. The runtime resolves a host pointer of an async
+// copy to the single registration containing it and rejects copies that run past its end
+// (hipErrorInvalidValue), which neighbouring arrays pinned as separate runs (sharing a page) produce.
+std::vector<std::pair<size_t, size_t>> segments(const void* p, size_t bytes);
 
 }  // namespace pinned
 }  // namespace moc

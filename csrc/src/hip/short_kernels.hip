@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "kernel_common.hpp"
 
@@ -25,6 +26,7 @@ namespace dev {
 using namespace kc;
 
 namespace {
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 constexpr int kBlock = 256;
 constexpr int kMaxTile = 1024;            // records per block tile (4 per thread in the scan)
 constexpr int kShortLdsBudget = 60 * 1024;  // stay under the 64 KiB default dynamic-LDS limit
@@ -57,7 +59,11 @@ ShortLayout short_layout(int L1, int tile_records, int codes_cap, int fmt_bytes,
 }
 }  // namespace
 
-template <bool Wide, bool Profile>
+// Pk (profile mode, int16-exact batches): the profile holds packed pairs (Dt << 16 | S), Dt[c][j] =
+// S[c][j] - S[c][j+1], so one v_pk_add_u16 advances both Tot_o (low half) and D_o(k) = P_o(k) - P_{o+1}(k)
+// (high half) and the hot key is one v_and_or_b32 of the accumulator with the step's (0xffff - k): no
+// DPP neighbour move and no subtraction per cell (3 VALU instead of 5); Tot_{o+1} = Tot_o - D_o(L2).
+template <bool Wide, bool Profile, bool Pk>
 __global__ __launch_bounds__(kBlock) void short_search_kernel(ProblemView pv, ShortArgs a, ShortLayout lay) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   int* table = reinterpret_cast<int*>(smem);
@@ -74,7 +80,13 @@ __global__ __launch_bounds__(kBlock) void short_search_kernel(ProblemView pv, Sh
     const int row = lay.row;
     for (int e = tid; e < kAlphabet * row; e += kBlock) {
       const int c = e / row, j = e - c * row;
-      table[e] = (c >= 1 && j < L1) ? pv.lut[c * kLutStride + pv.seq1[j]] : 0;
+      const int sj = (c >= 1 && j < L1) ? pv.lut[c * kLutStride + pv.seq1[j]] : 0;
+      if (Pk) {
+        const int sn = (c >= 1 && j + 1 < L1) ? pv.lut[c * kLutStride + pv.seq1[j + 1]] : 0;
+        table[e] = static_cast<int>((static_cast<uint32_t>(sj - sn) << 16) | (static_cast<uint32_t>(sj) & 0xffffu));
+      } else {
+        table[e] = sj;
+      }
     }
   } else {
     for (int e = tid; e < kLutInts; e += kBlock) {
@@ -152,6 +164,8 @@ __global__ __launch_bounds__(kBlock) void short_search_kernel(ProblemView pv, Sh
       const uint8_t* rec = codes_l + shift_b + roff;
       int P = 0;
       typename K::T best = K::min();
+      uint32_t acc = 0;         // Pk: (D_o, Tot_o) halves
+      int32_t best16 = INT32_MIN;  // Pk: max of (D << 16 | 0xffff - k)
       // 8 steps per round: the letter and table reads of the round are issued together (independent
       // LDS reads in flight), then the dependent prefix / neighbour / key chain consumes them
       auto gather = [&](int i) {
@@ -159,10 +173,16 @@ __global__ __launch_bounds__(kBlock) void short_search_kernel(ProblemView pv, Sh
         return Profile ? table[c * lay.row + o + i] : table[(c << 5) | s1l[o + i]];
       };
       auto step = [&](int v, int i) {
-        P += v;
-        const int Pn = wave_shl1(P);
-        const typename K::T key = K::make(P - Pn, i + 1, shift, mask);
-        best = key > best ? key : best;
+        if (Pk) {
+          acc = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, acc) + __builtin_bit_cast(u16x2, static_cast<uint32_t>(v)));
+          const int32_t key = static_cast<int32_t>((acc & 0xffff0000u) | (0xffffu - static_cast<uint32_t>(i + 1)));
+          best16 = key > best16 ? key : best16;
+        } else {
+          P += v;
+          const int Pn = wave_shl1(P);
+          const typename K::T key = K::make(P - Pn, i + 1, shift, mask);
+          best = key > best ? key : best;
+        }
       };
       int i = 0;
       for (; i + 8 <= steps; i += 8) {
@@ -173,8 +193,23 @@ __global__ __launch_bounds__(kBlock) void short_search_kernel(ProblemView pv, Sh
         for (int j = 0; j < 8; ++j) step(v[j], i + j);
       }
       for (; i < steps; ++i) step(gather(i), i);
-      const int Pn = wave_shl1(P);
-      unsigned long long key = lane_candidate<Wide>(on, o, L1, L2, pv.semantics, P, Pn, best, shift, mask);
+      unsigned long long key = 0;
+      if (Pk) {
+        const int tot = static_cast<int16_t>(acc & 0xffffu), dfin = static_cast<int>(acc) >> 16;
+        const int last = L1 - L2;
+        if (on) {
+          const bool v0 = (o < last) || (o == last && (pv.semantics == static_cast<int>(Semantics::Spec) || L2 == L1));
+          if (v0) key = final_key(tot, static_cast<uint32_t>(o) * static_cast<uint32_t>(L2));
+          if (o < last && L2 >= 2 && best16 != INT32_MIN) {
+            const int k = 0xffff - (best16 & 0xffff);
+            key = max_u64(key, final_key((best16 >> 16) + tot - dfin,
+                                         static_cast<uint32_t>(o) * static_cast<uint32_t>(L2) + static_cast<uint32_t>(k)));
+          }
+        }
+      } else {
+        const int Pn = wave_shl1(P);
+        key = lane_candidate<Wide>(on, o, L1, L2, pv.semantics, P, Pn, best, shift, mask);
+      }
       for (int d = 1; d < slot; d <<= 1) {  // segmented suffix max within the slot
         const unsigned long long other = shfl_down_u64(key, d);
         if (o + d < slot) key = max_u64(key, other);
@@ -237,16 +272,23 @@ void launch_short(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStr
   const int per_cu = std::max(1, std::min(8, 160 * 1024 / std::max(lay.total, 1)));
   const int64_t blocks = std::min<int64_t>(n_tiles, static_cast<int64_t>(num_cus) * per_cu);
   const dim3 grid(static_cast<unsigned>(std::max<int64_t>(blocks, 1))), block(kBlock);
-  if (pv.key_shift > 0) {
+  // packed (Dt, S) profile when every partial sum is int16-exact: |D| <= 2 max|T| L2, |Tot| <= max|T| L2
+  // (MOC_SHORT_PK=0 forces the int32 DPP form, for A/B runs)
+  const char* pk_env = std::getenv("MOC_SHORT_PK");
+  const bool pk = profile && (!pk_env || std::atoi(pk_env) != 0) &&
+                  2 * static_cast<int64_t>(std::max(pv.max_abs_t, 1)) * std::max(a.max_l2, 1) < 32767;
+  if (pk) {
+    hipLaunchKernelGGL((short_search_kernel<false, true, true>), grid, block, lay.total, stream, pv, a, lay);
+  } else if (pv.key_shift > 0) {
     if (profile)
-      hipLaunchKernelGGL((short_search_kernel<false, true>), grid, block, lay.total, stream, pv, a, lay);
+      hipLaunchKernelGGL((short_search_kernel<false, true, false>), grid, block, lay.total, stream, pv, a, lay);
     else
-      hipLaunchKernelGGL((short_search_kernel<false, false>), grid, block, lay.total, stream, pv, a, lay);
+      hipLaunchKernelGGL((short_search_kernel<false, false, false>), grid, block, lay.total, stream, pv, a, lay);
   } else {
     if (profile)
-      hipLaunchKernelGGL((short_search_kernel<true, true>), grid, block, lay.total, stream, pv, a, lay);
+      hipLaunchKernelGGL((short_search_kernel<true, true, false>), grid, block, lay.total, stream, pv, a, lay);
     else
-      hipLaunchKernelGGL((short_search_kernel<true, false>), grid, block, lay.total, stream, pv, a, lay);
+      hipLaunchKernelGGL((short_search_kernel<true, false, false>), grid, block, lay.total, stream, pv, a, lay);
   }
 }
 

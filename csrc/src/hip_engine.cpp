@@ -72,6 +72,19 @@ void expand_results(const void* in, ResultFormat f, int64_t n, Result* out, cons
 }
 
 namespace {
+// hipMemcpyAsync between device memory and a caller's host range, one copy per piece of the range that
+// lies within a single page-locked registration (or outside all): see pinned::segments.
+void copy_h2d(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  for (const auto& seg : pinned::segments(src, bytes))
+    MOC_HIP_CHECK(hipMemcpyAsync(static_cast<char*>(dst) + seg.first, static_cast<const char*>(src) + seg.first,
+                                 seg.second, hipMemcpyHostToDevice, s));
+}
+void copy_d2h(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  for (const auto& seg : pinned::segments(dst, bytes))
+    MOC_HIP_CHECK(hipMemcpyAsync(static_cast<char*>(dst) + seg.first, static_cast<const char*>(src) + seg.first,
+                                 seg.second, hipMemcpyDeviceToHost, s));
+}
+
 // True when every byte of [p, p+bytes) is page-locked through the registry (moc/runtime/pinned.hpp);
 // *dev gets the device-side address of p.
 bool pinned_range(const void* p, size_t bytes, const void** dev) {
@@ -260,6 +273,7 @@ dev::ProblemView HipEngine::problem_view(int64_t max_l2) const {
   pv.r2 = r2_;
   pv.prof16 = d_prof16_;
   pv.prof16_bytes = prof16_bytes_;
+  pv.max_abs_t = table_.max_abs();
   return pv;
 }
 
@@ -568,10 +582,10 @@ void HipEngine::run_dma_stream(const dev::ProblemView& pv, const dev::ShortArgs&
     ensure(s.d_packed, s.d_packed_cap, lbytes);
     ensure(s.d_offsets, s.d_offsets_cap, std::max<size_t>(nbytes, 16));
     ensure(s.d_out, s.d_out_cap, std::max<size_t>(rbytes, 16));
-    MOC_HIP_CHECK(hipMemcpyAsync(s.d_packed, codes + B0, lbytes, hipMemcpyHostToDevice, s_copy_));
+    copy_h2d(s.d_packed, codes + B0, lbytes, s_copy_);
     if (nbytes) {
       const size_t nb0 = len_bits == 4 ? static_cast<size_t>(r0 / 2) : static_cast<size_t>(r0);
-      MOC_HIP_CHECK(hipMemcpyAsync(s.d_offsets, lengths + nb0, nbytes, hipMemcpyHostToDevice, s_copy_));
+      copy_h2d(s.d_offsets, lengths + nb0, nbytes, s_copy_);
     }
     MOC_HIP_CHECK(hipEventRecord(s.ev_h2d, s_copy_));
     MOC_HIP_CHECK(hipStreamWaitEvent(s_compute_, s.ev_h2d, 0));
@@ -591,7 +605,7 @@ void HipEngine::run_dma_stream(const dev::ProblemView& pv, const dev::ShortArgs&
     MOC_HIP_CHECK(hipGetLastError());
     MOC_HIP_CHECK(hipEventRecord(s.ev_k1, s_compute_));
     MOC_HIP_CHECK(hipStreamWaitEvent(s_return_, s.ev_k1, 0));
-    MOC_HIP_CHECK(hipMemcpyAsync(static_cast<char*>(out) + r0 * fb, s.d_out, rbytes, hipMemcpyDeviceToHost, s_return_));
+    copy_d2h(static_cast<char*>(out) + r0 * fb, s.d_out, rbytes, s_return_);
     MOC_HIP_CHECK(hipEventRecord(s.ev_done, s_return_));
     s.busy = true;
     stats_.h2d_bytes += static_cast<int64_t>(lbytes + nbytes);
@@ -714,11 +728,11 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
     if (packed5) {
       letter_bytes = static_cast<size_t>(pb1 - pb0);
       if (cbytes)
-        MOC_HIP_CHECK(hipMemcpyAsync(s.d_packed, codes + pb0, letter_bytes, hipMemcpyHostToDevice, s_copy_));
+        copy_h2d(s.d_packed, codes + pb0, letter_bytes, s_copy_);
     } else if (cbytes) {
-      MOC_HIP_CHECK(hipMemcpyAsync(s.d_codes, codes + offsets[rb], cbytes, hipMemcpyHostToDevice, s_copy_));
+      copy_h2d(s.d_codes, codes + offsets[rb], cbytes, s_copy_);
     }
-    MOC_HIP_CHECK(hipMemcpyAsync(s.d_offsets, offsets + rb, sizeof(int64_t) * (cn + 1), hipMemcpyHostToDevice, s_copy_));
+    copy_h2d(s.d_offsets, offsets + rb, sizeof(int64_t) * (cn + 1), s_copy_);
     if (!starts.empty())
       MOC_HIP_CHECK(hipMemcpyAsync(s.d_plan, s.h_plan, lay.upload_bytes, hipMemcpyHostToDevice, s_copy_));
     MOC_HIP_CHECK(hipEventRecord(s.ev_h2d, s_copy_));
@@ -756,8 +770,7 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
     MOC_HIP_CHECK(hipEventRecord(s.ev_k1, s_compute_));
     // ---- return stream: D2H straight into the caller's result array
     MOC_HIP_CHECK(hipStreamWaitEvent(s_return_, s.ev_k1, 0));
-    MOC_HIP_CHECK(hipMemcpyAsync(static_cast<char*>(out) + rb * fb, s.d_out, static_cast<size_t>(fb) * cn,
-                                 hipMemcpyDeviceToHost, s_return_));
+    copy_d2h(static_cast<char*>(out) + rb * fb, s.d_out, static_cast<size_t>(fb) * cn, s_return_);
     MOC_HIP_CHECK(hipEventRecord(s.ev_done, s_return_));
     stats_.d2h_bytes += static_cast<int64_t>(fb) * cn;
     s.busy = true;
@@ -893,13 +906,13 @@ void HipEngine::search_keys(const uint8_t* codes, const int64_t* offsets, int64_
   ensure(s.d_offsets, s.d_offsets_cap, sizeof(int64_t) * static_cast<size_t>(n + 1));
   ensure(s.d_out, s.d_out_cap, sizeof(uint64_t) * static_cast<size_t>(n));
   if (cbytes)
-    MOC_HIP_CHECK(hipMemcpyAsync(s.d_codes, codes + offsets[0], cbytes, hipMemcpyHostToDevice, s_compute_));
-  MOC_HIP_CHECK(hipMemcpyAsync(s.d_offsets, offsets, sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, s_compute_));
+    copy_h2d(s.d_codes, codes + offsets[0], cbytes, s_compute_);
+  copy_h2d(s.d_offsets, offsets, sizeof(int64_t) * (n + 1), s_compute_);
   MOC_HIP_CHECK(hipEventRecord(ev_a_, s_compute_));
   search_keys_device(static_cast<const uint8_t*>(s.d_codes) - offsets[0], static_cast<const int64_t*>(s.d_offsets),
                      offsets, n, part, parts, static_cast<unsigned long long*>(s.d_out), s_compute_);
   MOC_HIP_CHECK(hipEventRecord(ev_b_, s_compute_));
-  MOC_HIP_CHECK(hipMemcpyAsync(keys, s.d_out, sizeof(uint64_t) * n, hipMemcpyDeviceToHost, s_compute_));
+  copy_d2h(keys, s.d_out, sizeof(uint64_t) * n, s_compute_);
   MOC_HIP_CHECK(hipStreamSynchronize(s_compute_));
   float ms = 0;
   MOC_HIP_CHECK(hipEventElapsedTime(&ms, ev_a_, ev_b_));

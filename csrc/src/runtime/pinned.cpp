@@ -113,5 +113,27 @@ const void* device_address(const void* p, size_t bytes) {
   return d;
 }
 
+std::vector<std::pair<size_t, size_t>> segments(const void* p, size_t bytes) {
+  std::vector<std::pair<size_t, size_t>> out;
+  if (!p || bytes == 0) return out;
+  const uintptr_t b = reinterpret_cast<uintptr_t>(p), e = b + bytes;
+  std::lock_guard<std::mutex> lock(mu());
+  auto& r = regs();
+  auto it = at_or_after(b);
+  uintptr_t x = b;
+  while (x < e) {
+    uintptr_t y;
+    if (it != r.end() && it->first <= x) {  // inside a registration: up to its end
+      y = std::min(e, it->second);
+      ++it;
+    } else {  // unregistered: up to the next registration
+      y = std::min(e, it == r.end() ? e : it->first);
+    }
+    out.emplace_back(static_cast<size_t>(x - b), static_cast<size_t>(y - x));
+    x = y;
+  }
+  return out;
+}
+
 }  // namespace pinned
 }  // namespace moc

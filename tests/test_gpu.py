@@ -357,6 +357,30 @@ def test_r2_results_and_nibble_lengths(pinned, packed, shape, n):
     eng.close()
 
 
+def test_pinned_neighbours_staged_copies():
+    # offsets and results carved from one buffer and pinned separately: the results' first page belongs
+    # to the offsets' registration, the rest to a second one. Async copies must not span the two
+    # (the runtime rejects that with hipErrorInvalidValue): they are split per registration.
+    from mpi_openmp_cuda_amd import _lib
+
+    prob = make_synthetic("input4", 2000, seed=5)
+    n = prob.n
+    buf = np.zeros(64 << 10, np.uint8)
+    offs = buf[: 8 * (n + 1)].view(np.int64)
+    offs[:] = prob.offsets
+    ob = 8 * (n + 1)
+    out = buf[ob: ob + 12 * n].view(_lib.FORMAT_DTYPES[_lib.FORMAT_NAMES.index("r12")])
+    eng = HipSearchEngine(device=0)
+    eng.set_problem(prob.weights, prob.seq1)
+    eng.pin(prob.codes)
+    eng.pin(offs)
+    eng.pin(out)
+    eng.solve(prob.codes, offs, out=out)
+    assert eng.stats()["direct"] == 0
+    assert np.array_equal(as_triples(out), as_triples(search_cpu(prob)))
+    eng.close()
+
+
 @pytest.mark.parametrize("mode", ["dma", "zero_copy"])
 @pytest.mark.parametrize("packed,len_bits", [(False, 0), (False, 8), (True, 4), (True, 8)])
 @pytest.mark.parametrize("shape,n", [("input6", 100_003), ("input1", 20_001)])
