@@ -39,6 +39,7 @@ def parse_args():
     ap.add_argument("--records-per-gpu", type=int, default=1 << 25)
     ap.add_argument("--shape", default="input6")
     ap.add_argument("--shm", type=int, default=1, help="1: node-shared /dev/shm arrays; 0: private pinned")
+    ap.add_argument("--host-alloc", default="", help="'hip': private hipHostMalloc arrays (overrides --shm)")
     ap.add_argument("--verify", type=int, default=20000, help="records per rank checked against the CPU engine")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, default) | gloo (multi-rank rehearsal)")
@@ -52,7 +53,7 @@ def parse_args():
 class HostArrays:
     """Per-rank slice of the node-shared input/result arrays (/dev/shm files, or private memory)."""
 
-    def __init__(self, tag, rank, lengths, use_shm, packed, seed, len_base):
+    def __init__(self, tag, rank, lengths, use_shm, packed, seed, len_base, hip_alloc=False):
         from mpi_openmp_cuda_amd.models.problem import pack5, pack_lengths4, packed5_bytes
         from mpi_openmp_cuda_amd.utils.synthetic import fill_codes
 
@@ -66,7 +67,16 @@ class HostArrays:
             # leave room for every local rank's slice (up to 8) plus headroom
             if st.f_bavail * st.f_frsize > 10 * nbytes:
                 self.shm = True
-        if self.shm:
+        self.bufs = []
+        if hip_alloc:
+            self.shm = False
+            from mpi_openmp_cuda_amd._lib import HostBuffer
+
+            def mk(name, dtype, count):
+                b = HostBuffer(np.dtype(dtype).itemsize * max(count, 1))
+                self.bufs.append(b)
+                return b.array(dtype, max(count, 1))[:count]
+        elif self.shm:
             def mk(name, dtype, count):
                 p = f"/dev/shm/moc_bench_{tag}_{rank}_{name}"
                 self.paths.append(p)
@@ -99,7 +109,24 @@ class HostArrays:
         del letters
         self.results = None  # allocated once the result wire format is known
 
+    def alloc_results(self, count, dtype, tag, rank):
+        if self.bufs:
+            from mpi_openmp_cuda_amd._lib import HostBuffer
+
+            b = HostBuffer(np.dtype(dtype).itemsize * count)
+            self.bufs.append(b)
+            self.results = b.array(dtype, count)
+        elif self.shm:
+            p = f"/dev/shm/moc_bench_{tag}_{rank}_results"
+            self.paths.append(p)
+            self.results = np.memmap(p, dtype=dtype, mode="w+", shape=(count,))
+        else:
+            self.results = np.empty(count, dtype=dtype)
+
     def cleanup(self):
+        for b in self.bufs:
+            b.free()
+        self.bufs = []
         for p in self.paths:
             try:
                 os.unlink(p)
@@ -165,20 +192,15 @@ def main():
     narrow4 = bool(args.narrow) and shape.l2_max - shape.l2_min <= 15
     progress(f"generating {R} records per rank")
     host = HostArrays(tag, rank, lengths, bool(args.shm), args.packed, args.seed + 101 + rank,
-                      shape.l2_min if narrow4 else None)
+                      shape.l2_min if narrow4 else None, hip_alloc=args.host_alloc == "hip")
     progress(f"{int(host.offsets[-1])} letters per rank ready")
     del lengths
     eng = HipSearchEngine(device=gpu)
     eng.set_problem(weights, seq1)
     fmt = eng.auto_format(shape.l2_max, shape.l2_min if args.narrow else 0)
     rdt = _lib.FORMAT_DTYPES[_lib.FORMAT_NAMES.index(fmt)]
-    if host.shm:
-        p = f"/dev/shm/moc_bench_{tag}_{rank}_results"
-        host.paths.append(p)
-        host.results = np.memmap(p, dtype=rdt, mode="w+", shape=(R,))
-    else:
-        host.results = np.empty(R, dtype=rdt)
-    pin = Pinned(host.codes, host.offsets, host.lengths, host.results)
+    host.alloc_results(R, rdt, tag, rank)
+    pin = Pinned(*([] if host.bufs else [host.codes, host.offsets, host.lengths, host.results]))
     progress("host arrays page-locked; warm-up")
     done = torch.zeros(1, dtype=torch.int64, device=cdev)
     hdr_host = np.empty(4 + shape.L1, dtype=np.int32)
@@ -276,7 +298,7 @@ def main():
             "rank0_solve_ms_median": round(float(np.median(tms)), 4),
             "rank0_h2d_bytes_per_step": int(st["h2d_bytes"]),
             "rank0_d2h_bytes_per_step": int(st["d2h_bytes"]),
-            "host_arrays": "shm" if host.shm else "private",
+            "host_arrays": "hip_host_malloc" if host.bufs else ("shm" if host.shm else "private"),
             "result_format": fmt,
             "lengths_bits": host.len_bits,
             "letters": "packed5" if host.packed else "bytes",

@@ -57,6 +57,9 @@ int moc_partition(const int64_t* lengths, int64_t n, int64_t L1, int parts, doub
 int moc_device_count(void);
 /* Page-locks [p, p+bytes) for direct DMA (hipHostRegister on the enclosing page range). */
 int moc_host_register(void* p, size_t bytes);
+// Page-locked host allocation known to the streaming paths (nullptr on failure; moc_last_error).
+void* moc_host_alloc(size_t bytes);
+int moc_host_free(void* p);
 /* Binds CPUs + future host allocations of this process to the device's NUMA node; returns node or -1. */
 int moc_bind_numa(int device);
 int moc_device_numa_node(int device);

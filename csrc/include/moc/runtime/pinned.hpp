@@ -21,6 +21,10 @@ namespace pinned {
 std::vector<void*> register_range(const void* p, size_t bytes);
 // Releases registrations made by register_range.
 void unregister(const std::vector<void*>& bases);
+// Page-locked allocation (hipHostMalloc, NUMA placement by the caller's memory policy), recorded in the
+// registry like a registration so the streaming paths accept it; release with free_host.
+void* alloc_host(size_t bytes);
+void free_host(void* p);
 // True when every byte of [p, p+bytes) lies in registrations made through this registry.
 bool covers(const void* p, size_t bytes);
 // Device address of host pointer p inside a covered range (nullptr if not covered). On ROCm's unified

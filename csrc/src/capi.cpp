@@ -194,6 +194,16 @@ double moc_transfer_probe(int kind, size_t bytes, int iters) {
 int moc_bind_numa(int device) { return moc::bind_numa_to_device(device); }
 int moc_device_numa_node(int device) { return moc::device_numa_node(device); }
 
+void* moc_host_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (guard([&] { p = moc::pinned::alloc_host(bytes); }) != 0) return nullptr;
+  return p;
+}
+
+int moc_host_free(void* p) {
+  return guard([&] { moc::pinned::free_host(p); });
+}
+
 int moc_host_register(void* p, size_t bytes) {
   return guard([&] {
     std::vector<void*> made = moc::pinned::register_range(p, bytes);

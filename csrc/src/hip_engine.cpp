@@ -572,14 +572,15 @@ void HipEngine::run_dma_stream(const dev::ProblemView& pv, const dev::ShortArgs&
     const int64_t b0 = packed5 ? (5 * offsets[r0]) >> 3 : offsets[r0];
     const int64_t b1 = packed5 ? ((5 * offsets[r1] + 7) >> 3) + 1 : offsets[r1];
     const int64_t B0 = b0 & ~int64_t{15};
-    const size_t lbytes = static_cast<size_t>(b1 - B0) + 16;
+    const size_t lbytes = static_cast<size_t>(b1 - B0);  // + 16 bytes of device slack, never copied: the
+                                                         // host range may end at its allocation's end
     const size_t nbytes = lengths ? (len_bits == 4 ? static_cast<size_t>((cn + 1) / 2) : static_cast<size_t>(cn)) : 0;
     const size_t rbytes = static_cast<size_t>(fb) * static_cast<size_t>(cn);
     if (s.busy) {  // the slot's previous chunk: its letters consumed, its results returned
       MOC_HIP_CHECK(hipEventSynchronize(s.ev_done));
       s.busy = false;
     }
-    ensure(s.d_packed, s.d_packed_cap, lbytes);
+    ensure(s.d_packed, s.d_packed_cap, lbytes + 16);
     ensure(s.d_offsets, s.d_offsets_cap, std::max<size_t>(nbytes, 16));
     ensure(s.d_out, s.d_out_cap, std::max<size_t>(rbytes, 16));
     copy_h2d(s.d_packed, codes + B0, lbytes, s_copy_);
@@ -591,7 +592,7 @@ void HipEngine::run_dma_stream(const dev::ProblemView& pv, const dev::ShortArgs&
     MOC_HIP_CHECK(hipStreamWaitEvent(s_compute_, s.ev_h2d, 0));
     dev::ShortArgs a = a0;
     a.codes = static_cast<const uint8_t*>(s.d_packed) - B0;
-    a.dbg_codes_end = B0 + static_cast<int64_t>(lbytes);
+    a.dbg_codes_end = B0 + static_cast<int64_t>(lbytes) + 16;
     a.offsets = a0.offsets + r0;  // pinned host (zero-copy): two reads per tile
     a.lengths8 = lengths && len_bits == 8 ? static_cast<const uint8_t*>(s.d_offsets) : nullptr;
     a.lengths4 = lengths && len_bits == 4 ? static_cast<const uint8_t*>(s.d_offsets) : nullptr;

@@ -87,6 +87,25 @@ void unregister(const std::vector<void*>& bases) {
   }
 }
 
+void* alloc_host(size_t bytes) {
+  void* p = nullptr;
+  MOC_HIP_CHECK(hipHostMalloc(&p, std::max<size_t>(bytes, 1), hipHostMallocMapped | hipHostMallocNumaUser));
+  const uintptr_t b = reinterpret_cast<uintptr_t>(p) & ~(kPage - 1);
+  const uintptr_t e = (reinterpret_cast<uintptr_t>(p) + std::max<size_t>(bytes, 1) + kPage - 1) & ~(kPage - 1);
+  std::lock_guard<std::mutex> lock(mu());
+  regs().emplace(b, e);
+  return p;
+}
+
+void free_host(void* p) {
+  if (!p) return;
+  {
+    std::lock_guard<std::mutex> lock(mu());
+    regs().erase(reinterpret_cast<uintptr_t>(p) & ~(kPage - 1));
+  }
+  (void)hipHostFree(p);
+}
+
 bool covers(const void* p, size_t bytes) {
   if (!p) return false;
   const uintptr_t b = reinterpret_cast<uintptr_t>(p);

@@ -60,6 +60,8 @@ def _decl(lib):
         "moc_device_count": (c_int, []),
         "moc_host_register": (c_int, [c_void_p, c_size_t]),
         "moc_host_unregister": (c_int, [c_void_p]),
+        "moc_host_alloc": (c_void_p, [c_size_t]),
+        "moc_host_free": (c_int, [c_void_p]),
         "moc_pointer_info": (c_int, [c_void_p, c_size_t, c_void_p]),
         "moc_pinned_covers": (c_int, [c_void_p, c_size_t]),
         "moc_bind_numa": (c_int, [c_int]),
@@ -144,6 +146,29 @@ class Pinned:
 
     def __exit__(self, *exc):
         self.release()
+
+
+class HostBuffer:
+    """Page-locked host allocation (hipHostMalloc) usable as numpy arrays by the streaming paths."""
+
+    def __init__(self, nbytes: int):
+        L = lib()
+        p = L.moc_host_alloc(max(int(nbytes), 1))
+        if not p:
+            raise NativeError(L.moc_last_error().decode(errors="replace"))
+        self._p = p
+        self.nbytes = int(nbytes)
+
+    def array(self, dtype, count: int, offset: int = 0):
+        import numpy as np
+
+        buf = (ctypes.c_uint8 * self.nbytes).from_address(self._p)
+        return np.frombuffer(buf, dtype=dtype, count=count, offset=offset)
+
+    def free(self):
+        if self._p:
+            lib().moc_host_free(self._p)
+            self._p = None
 
 
 def loaded_path():
