@@ -30,6 +30,7 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 constexpr int kBlock = 256;
 constexpr int kMaxTile = 1024;            // records per block tile (4 per thread in the scan)
 constexpr int kShortLdsBudget = 60 * 1024;  // stay under the 64 KiB default dynamic-LDS limit
+constexpr int kShortLdsOccupancy = 160 * 1024 / 6;  // preferred: 6 blocks per CU
 
 struct ShortLayout {
   int row = 0;          // profile row length (entries), Profile mode
@@ -248,16 +249,24 @@ bool configure_short(int64_t L1, int64_t min_l2, int64_t max_l2, ShortArgs& a) {
   const int64_t l2cap = std::max<int64_t>(1, std::min(max_l2, L1 + 1));
   const int fb = result_bytes(static_cast<ResultFormat>(a.fmt));
   const bool profile = kAlphabet * ((L1 + kWave + 3) & ~3) * 4 <= 24 * 1024;
-  for (int tr = kMaxTile; tr >= 1; tr /= 2) {
-    // worst-case letters of a tile: records longer than L1 are never scored but still staged
-    const int64_t cap = static_cast<int64_t>(tr) * std::max(max_l2, int64_t{1}) + 48;
-    if (cap > kShortLdsBudget) continue;
-    ShortLayout l = short_layout(static_cast<int>(L1), tr, static_cast<int>(cap), fb, profile);
-    if (l.total <= kShortLdsBudget) {
-      a.tile_records = tr;
-      a.codes_cap = static_cast<int32_t>(cap);
-      a.max_l2 = static_cast<int32_t>(l2cap);
-      return true;
+  int max_tile = kMaxTile;  // MOC_SHORT_TILE: cap on records per block tile (A/B runs)
+  if (const char* v = std::getenv("MOC_SHORT_TILE")) max_tile = std::max(1, std::min(kMaxTile, std::atoi(v)));
+  // Occupancy first: the largest tile whose LDS lets 6 blocks (24 waves) share a CU — the hot loop's
+  // two dependent LDS reads per step need that many waves in flight (input1 shape: 1.47 T cells/s at
+  // 1024-record tiles / 2 blocks per CU, 2.02 T at 256 / 6 per CU) — else the largest that fits at all.
+  for (const int budget : {kShortLdsOccupancy, kShortLdsBudget}) {
+    const int min_tile = budget == kShortLdsOccupancy ? std::min(64, max_tile) : 1;  // keep tiles useful
+    for (int tr = max_tile; tr >= min_tile; tr /= 2) {
+      // worst-case letters of a tile: records longer than L1 are never scored but still staged
+      const int64_t cap = static_cast<int64_t>(tr) * std::max(max_l2, int64_t{1}) + 48;
+      if (cap > budget) continue;
+      ShortLayout l = short_layout(static_cast<int>(L1), tr, static_cast<int>(cap), fb, profile);
+      if (l.total <= budget) {
+        a.tile_records = tr;
+        a.codes_cap = static_cast<int32_t>(cap);
+        a.max_l2 = static_cast<int32_t>(l2cap);
+        return true;
+      }
     }
   }
   return false;
