@@ -7,11 +7,14 @@
 //   * the profile row segment S[c][i .. i+NOFF) a lane needs at step i is read with NOFF/8 aligned
 //     ds_read_b128: the block keeps 8 copies of the int16 profile, copy s shifted left by s columns, so
 //     step i reads copy (i mod 8) at column i - (i mod 8) (a multiple of 8 -> 16-byte aligned).
-// Per step and per pair of offsets (2m, 2m+1):
-//     P2[m]  += (S[c][i+2m], S[c][i+2m+1])                         v_pk_add_u16
-//     D2      = P2[m] - (P_{2m+1}, P_{2m+2})                        v_alignbit + v_pk_sub_u16
-//     B2[m]   = max(B2[m], D2 * 2^ks + (mask - (i+1)))             v_pk_mad_u16 + v_pk_max_i16
-// i.e. ~2.5 VALU ops per cell. Records stream through the same persistent, LDS-tiled block loop as the
+// The profile holds the diagonal DIFFERENCES Dt[c][j] = S[c][j] - S[c][j+1] (S = T[c][Seq1[j]], 0 past
+// Seq1 and in the padding row 0), so per step and per pair of offsets (2m, 2m+1):
+//     D2[m]  += (Dt[c][i+2m], Dt[c][i+2m+1])     = (D_2m(i+1), D_2m+1(i+1))     v_pk_add_u16
+//     B2[m]   = max(B2[m], D2 * 2^ks + (mask - (i+1)))                      v_pk_mad_u16 + v_pk_max_i16
+// i.e. 1.5 VALU ops per cell (2.5 when the running sums were P_o and the neighbour came from an
+// alignbit + subtract). Tot_o is not summed per cell: each lane sums the anchor diagonal
+// Tot_NOFF = sum_i T[c_i][Seq1[NOFF + i]] (an int8 LUT + Seq1 staged in LDS; 0 past Seq1, consistent with
+// the profile) and recovers Tot_o = Tot_{o+1} + D_o(L2) by a suffix pass over its offsets in the epilogue. Records stream through the same persistent, LDS-tiled block loop as the
 // short kernel (zero-copy from pinned host memory when the batch lives there).
 // Exactness: int16 arithmetic is exact because the host only selects this kernel when
 // 2*max|W|*max|Seq2|*2^ks + mask < 2^15 (no key can wrap) — see configure_swipe.
@@ -41,7 +44,8 @@ __device__ __forceinline__ uint32_t as_u32(s16x2 v) { return __builtin_bit_cast(
 struct SwipeLayout {
   int row = 0;          // profile row length (int16 entries), multiple of 8
   int copy_elems = 0;   // 27 * row
-  int prof_bytes = 0;
+  int prof_bytes = 0;   // 8 shifted copies of the Dt profile
+  int s_off = 0;        // int8 LUT (32 x 32, column 31 = 0) + Seq1 codes (31 past Seq1): anchor diagonal
   int loff_off = 0, codes_off = 0, res_off = 0, total = 0;
 };
 
@@ -53,7 +57,8 @@ SwipeLayout swipe_layout(int L1, int noff, int l2w, int tile_records, int codes_
   l.row = (std::max(L1, 4 * l2w) + noff + 8 + 63) & ~63;
   l.copy_elems = kAlphabet * l.row;
   l.prof_bytes = al16(8 * l.copy_elems * 2);
-  l.loff_off = l.prof_bytes;
+  l.s_off = l.prof_bytes;
+  l.loff_off = l.s_off + al16(kLutInts + l.row);
   l.codes_off = l.loff_off + al16((tile_records + 1) * 4 + 32);
   l.res_off = l.codes_off + al16(codes_cap);
   l.total = l.res_off + al16(tile_records * fb);
@@ -72,6 +77,8 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
   constexpr int NW = P5 ? (20 * L2W + 31) / 32 : L2W;  // record words held per lane
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   short* prof = reinterpret_cast<short*>(smem);
+  int8_t* lut8 = reinterpret_cast<int8_t*>(smem + lay.s_off);
+  uint8_t* s1l = smem + lay.s_off + kLutInts;
   int* loff = reinterpret_cast<int*>(smem + lay.loff_off);
   int* misc = loff + a.tile_records + 1;
   uint8_t* codes_l = smem + lay.codes_off;
@@ -82,7 +89,7 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
   constexpr int KMASK = (1 << KB) - 1;
   constexpr int NP = NOFF / 2;  // packed accumulators
 
-  // ---- 8 shifted int16 profile copies: prof[s][c][j] = S[c][j + s] (row 0 and j >= L1: 0).
+  // ---- 8 shifted int16 difference-profile copies: prof[s][c][j] = Dt[c][j + s], and the plain S rows.
   //      Rows are 128-byte multiples, so the 16-byte chunk q of every row would start on the same LDS
   //      bank; chunk q of row c is stored at chunk q ^ (c & 7) instead, spreading the 16 lanes of a
   //      ds_read_b128 group (16 records reading 16 rows) over 8 bank quads — 8-way -> ~2-way conflicts.
@@ -91,8 +98,14 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
     for (int e = tid; e < 8 * ce; e += kBlock) {
       const int s = e / ce, rem = e - s * ce, c = rem / row, jj = rem - c * row;
       const int j = ((((jj >> 3) ^ (c & 7)) << 3) | (jj & 7)) + s;  // element stored at jj holds column j
-      prof[e] = static_cast<short>((c >= 1 && j < L1) ? pv.lut[c * kLutStride + pv.seq1[j]] : 0);
+      const int sj = (c >= 1 && j < L1) ? pv.lut[c * kLutStride + pv.seq1[j]] : 0;
+      const int sn = (c >= 1 && j + 1 < L1) ? pv.lut[c * kLutStride + pv.seq1[j + 1]] : 0;
+      prof[e] = static_cast<short>(sj - sn);
     }
+    // row 0 (padding letter: steps past a lane's record) and column 31 (past Seq1) contribute 0
+    for (int e = tid; e < kLutInts; e += kBlock)
+      lut8[e] = static_cast<int8_t>((e & 31) == 31 || (e >> 5) == 0 ? 0 : pv.lut[e]);
+    for (int j = tid; j < row; j += kBlock) s1l[j] = j < L1 ? pv.seq1[j] : 31;
   }
   const int fb = fmt_bytes(a.fmt);
   const int64_t n_tiles = (a.n + a.tile_records - 1) / a.tile_records;
@@ -222,10 +235,11 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
       }
       const int steps = wave_max_i32(on ? L2 : 0);
 
-      uint32_t P2[NP], B2[NP];
+      uint32_t D2[NP], B2[NP];
+      int anchor = 0;  // Tot_NOFF: the diagonal just past this lane's offsets
 #pragma unroll
       for (int q = 0; q < NP; ++q) {
-        P2[q] = 0u;
+        D2[q] = 0u;
         B2[q] = 0x80008000u;  // (INT16_MIN, INT16_MIN)
       }
 #pragma unroll
@@ -252,17 +266,15 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
             v[4 * q + 2] = x.z;
             v[4 * q + 3] = x.w;
           }
+          anchor += lut8[(c << 5) | s1l[NOFF + i]];
 #pragma unroll
-          for (int q = 0; q < NP; ++q) P2[q] = as_u32(as_s16x2(P2[q]) + as_s16x2(v[q]));
+          for (int q = 0; q < NP; ++q) D2[q] = as_u32(as_s16x2(D2[q]) + as_s16x2(v[q]));
           const short kc = static_cast<short>(KMASK - (i + 1));
           const s16x2 kadd = {kc, kc};
           const s16x2 kmul = {static_cast<short>(1 << KB), static_cast<short>(1 << KB)};
 #pragma unroll
           for (int q = 0; q < NP; ++q) {
-            const uint32_t nxt = q + 1 < NP ? P2[q + 1] : 0u;
-            const uint32_t Q = __builtin_amdgcn_alignbit(nxt, P2[q], 16);  // (P_{2q+1}, P_{2q+2})
-            const s16x2 D = as_s16x2(P2[q]) - as_s16x2(Q);
-            const s16x2 K = D * kmul + kadd;
+            const s16x2 K = as_s16x2(D2[q]) * kmul + kadd;
             B2[q] = as_u32(__builtin_elementwise_max(as_s16x2(B2[q]), K));
           }
         }
@@ -271,11 +283,12 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
       // ---- per-lane selection over the record's offsets: 32-bit keys (score+2^15 | ~(o<<KB | k))
       const int last = L1 - L2;
       uint32_t best = 0;
+      int tot = anchor;  // Tot_{o+1} entering offset o (suffix pass: Tot_o = Tot_{o+1} + D_o(L2))
 #pragma unroll
-      for (int o = 0; o < NOFF; ++o) {
-        const int Po = static_cast<short>(o & 1 ? (P2[o >> 1] >> 16) : (P2[o >> 1] & 0xffff));
-        const int o1 = o + 1;
-        const int Pn = o1 < NOFF ? static_cast<short>(o1 & 1 ? (P2[o1 >> 1] >> 16) : (P2[o1 >> 1] & 0xffff)) : 0;
+      for (int o = NOFF - 1; o >= 0; --o) {
+        const int Pn = tot;
+        const int Po = Pn + static_cast<short>(o & 1 ? (D2[o >> 1] >> 16) : (D2[o >> 1] & 0xffff));
+        tot = Po;
         const int bk = static_cast<short>(o & 1 ? (B2[o >> 1] >> 16) : (B2[o >> 1] & 0xffff));
         const bool own = on && o < need;
         const bool v0 = own && (o < last || (o == last && (sem == static_cast<int>(Semantics::Spec) || L2 == L1)));
@@ -321,6 +334,7 @@ SwipeChoice swipe_choice(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max
   const int64_t dmax = 2 * static_cast<int64_t>(std::max(max_abs_weight, 1)) * std::max<int64_t>(max_l2, 1);
   if ((dmax << kb) + (1 << kb) >= 32767) return c;                              // hot keys fit int16
   if (static_cast<int64_t>(std::max(max_abs_weight, 1)) * max_l2 * 2 >= 32767) return c;  // sums fit int16
+  if (max_abs_weight > 127) return c;  // the anchor diagonal's LUT is int8
   c.noff = noff;
   c.l2w = l2w;
   return c;
