@@ -8,6 +8,7 @@
 //   kind 6: zero-copy read + zero-copy write (one third) concurrently
 //   kind 7: H2D hipMemcpyAsync + zero-copy write (one third) concurrently
 //   kind 8: H2D + D2H hipMemcpyAsync (one third) concurrently
+//   kind 9: zero-copy read + D2H hipMemcpyAsync (one third) concurrently
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -71,6 +72,10 @@ double transfer_probe(int kind, size_t bytes, int iters) {
         break;
       case 8:
         MOC_HIP_CHECK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s1));
+        MOC_HIP_CHECK(hipMemcpyAsync(h2, d2, (n16 / 3) * 16, hipMemcpyDeviceToHost, s2));
+        break;
+      case 9:
+        hipLaunchKernelGGL(zc_read_kernel, dim3(2048), dim3(256), 0, s1, static_cast<const uint4*>(h), n16, sink);
         MOC_HIP_CHECK(hipMemcpyAsync(h2, d2, (n16 / 3) * 16, hipMemcpyDeviceToHost, s2));
         break;
       default: MOC_HIP_CHECK(hipMemcpyAsync(d2, d, bytes, hipMemcpyDeviceToDevice, s1)); break;
