@@ -290,6 +290,11 @@ void test_formatter() {
   const Result r[3] = {{1, 2, 3}, {kNoCandidateScore, 0, 0}, {-5, 10, 0}};
   CHECK(format_results(r, 3, 7) == "#7: score: 1, n: 2, k: 3\n#8: score: -2147483648, n: 0, k: 0\n"
                                    "#9: score: -5, n: 10, k: 0\n");
+  // the row counter carries across digit counts; numbers of every width
+  const Result q[3] = {{2147483647, 123456789, 99}, {-100, 0, 1}, {10, 100, 1000}};
+  CHECK(format_results(q, 3, 998) == "#998: score: 2147483647, n: 123456789, k: 99\n"
+                                     "#999: score: -100, n: 0, k: 1\n#1000: score: 10, n: 100, k: 1000\n");
+  CHECK(format_results(q, 1, 0) == "#0: score: 2147483647, n: 123456789, k: 99\n");
 }
 }  // namespace
 
