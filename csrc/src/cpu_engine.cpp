@@ -84,7 +84,9 @@ void solve_batch_cpu(const ScoreTable& t, const uint8_t* s1, int64_t L1, const R
   const int64_t n = batch.size();
   const int nt = num_threads > 0 ? num_threads : omp_get_max_threads();
   if (n >= 4 * nt || nt == 1) {
-#pragma omp parallel for schedule(dynamic, 1) num_threads(nt)
+    // dynamic balance in chunks: per-record dispatch would dominate tiny records (input6: ~150 cells)
+    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(1024, n / (64 * nt)));
+#pragma omp parallel for schedule(dynamic, chunk) num_threads(nt)
     for (int64_t i = 0; i < n; ++i) out[i] = solve_record(t, s1, L1, batch.record(i), batch.length(i), sem);
     return;
   }
@@ -131,7 +133,8 @@ void solve_keys_cpu(const ScoreTable& t, const uint8_t* s1, int64_t L1, const Re
     e = c * (part + 1) / parts;
   };
   if (n >= 4 * nt || nt == 1) {
-#pragma omp parallel for schedule(dynamic, 1) num_threads(nt)
+    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(1024, n / (64 * nt)));
+#pragma omp parallel for schedule(dynamic, chunk) num_threads(nt)
     for (int64_t i = 0; i < n; ++i) {
       int64_t b, e;
       range(i, b, e);
