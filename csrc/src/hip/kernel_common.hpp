@@ -194,10 +194,21 @@ __device__ __forceinline__ int record_length(const ShortArgs& a, int64_t idx) {
 // Copies a block's staged results (LDS) to the output: dwords, plus a trailing halfword for R2 tiles
 // of odd length. `dst` is 4-byte aligned (tiles start at multiples of 64 records).
 __device__ __forceinline__ void copy_results(void* dst, const uint8_t* src, int bytes, int tid, int nthreads) {
-  const int nd = bytes >> 2;
-  for (int q = tid; q < nd; q += nthreads) static_cast<uint32_t*>(dst)[q] = reinterpret_cast<const uint32_t*>(src)[q];
-  if ((bytes & 2) && tid == 0)
-    static_cast<uint16_t*>(dst)[2 * nd] = reinterpret_cast<const uint16_t*>(src)[2 * nd];
+  // 16-byte stores when the destination allows (tile starts are multiples of 128 bytes): to host memory
+  // (zero-copy) fewer, fuller write requests share the link with the tile loads' read requests
+  int done = 0;
+  if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+    const int n16 = bytes >> 4;
+    for (int q = tid; q < n16; q += nthreads)
+      static_cast<uint4*>(dst)[q] = reinterpret_cast<const uint4*>(src)[q];
+    done = n16 << 4;
+  }
+  const int nd = (bytes - done) >> 2;
+  uint32_t* d32 = reinterpret_cast<uint32_t*>(static_cast<char*>(dst) + done);
+  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src + done);
+  for (int q = tid; q < nd; q += nthreads) d32[q] = s32[q];
+  if (((bytes - done) & 2) && tid == 0)
+    reinterpret_cast<uint16_t*>(d32)[2 * nd] = reinterpret_cast<const uint16_t*>(s32)[2 * nd];
 }
 
 __device__ __forceinline__ void stage_lut(int* lut, const int32_t* g) {
