@@ -357,6 +357,22 @@ def test_r2_results_and_nibble_lengths(pinned, packed, shape, n):
     eng.close()
 
 
+@pytest.mark.parametrize("seed", range(12))
+def test_long_records_random_sweep(engine, seed):
+    # random long-record problems (tile16 or its DPP fallback by weight range), tie-heavy alphabets,
+    # lengths around the 64-step flush and the 128-offset sub-tiles, both semantics, vs the CPU engine
+    rng = np.random.default_rng(1000 + seed)
+    L1 = int(rng.integers(70, 3000))
+    alphabet = int(rng.choice([2, 3, 5, 26]))
+    w = [int(x) for x in rng.integers(0, 70, 4)]
+    s1 = _letters(rng, L1, alphabet)
+    lens = list(rng.integers(1, L1 + 2, 24)) + [63, 64, 65, 128, 129, L1 - 127, L1 - 128, L1 - 129]
+    recs = [_letters(rng, max(int(n), 1), alphabet) for n in lens]
+    prob = Problem.from_strings(w, s1, recs)
+    for sem in (Semantics.REFERENCE, Semantics.SPEC):
+        check(engine, prob, sem)
+
+
 def test_pinned_neighbours_staged_copies():
     # offsets and results carved from one buffer and pinned separately: the results' first page belongs
     # to the offsets' registration, the rest to a second one. Async copies must not span the two
