@@ -45,6 +45,9 @@ using namespace kc;
 namespace {
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
+#ifndef MOC_T16_UNROLL
+#define MOC_T16_UNROLL 64  // hot-loop steps per unrolled group; 64 = the whole chunk (best of 8/16/32/64)
+#endif
 constexpr int kBlock16 = 1024;  // 16 waves: the profile takes most of the CU's LDS, one workgroup holds it
 constexpr int kWavesPerBlock16 = kBlock16 / 64;
 constexpr int kSub = 128;                    // offsets per sub-tile (2 per lane)
@@ -182,7 +185,7 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
         const int c_next = letter(i0 + 64 + lane);
         const int so = row_off(c, i0 + lane);
         anchor_add(c, i0 + lane);
-#pragma unroll 16
+#pragma unroll MOC_T16_UNROLL
         for (int j = 0; j < 64; ++j) step(so, j, true);
         flush(true);
         c = c_next;
