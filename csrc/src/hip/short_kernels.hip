@@ -28,6 +28,10 @@ using namespace kc;
 namespace {
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 constexpr int kBlock = 256;
+#ifndef MOC_SHORT_GROUP
+#define MOC_SHORT_GROUP 8
+#endif
+constexpr int kShortGroup = MOC_SHORT_GROUP;  // steps whose LDS reads are issued together
 constexpr int kMaxTile = 1024;            // records per block tile (4 per thread in the scan)
 constexpr int kShortLdsBudget = 60 * 1024;  // stay under the 64 KiB default dynamic-LDS limit
 constexpr int kShortLdsOccupancy = 160 * 1024 / 6;  // preferred: 6 blocks per CU
@@ -186,12 +190,12 @@ __global__ __launch_bounds__(kBlock) void short_search_kernel(ProblemView pv, Sh
         }
       };
       int i = 0;
-      for (; i + 8 <= steps; i += 8) {
-        int v[8];
+      for (; i + kShortGroup <= steps; i += kShortGroup) {
+        int v[kShortGroup];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = gather(i + j);
+        for (int j = 0; j < kShortGroup; ++j) v[j] = gather(i + j);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) step(v[j], i + j);
+        for (int j = 0; j < kShortGroup; ++j) step(v[j], i + j);
       }
       for (; i < steps; ++i) step(gather(i), i);
       unsigned long long key = 0;
