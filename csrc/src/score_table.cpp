@@ -68,15 +68,19 @@ int32_t ScoreTable::max_abs() const {
 
 bool build_profile16(const ScoreTable& t, const uint8_t* seq1, int64_t L1, int64_t overhang, Profile16& out) {
   if (L1 <= 0 || overhang < 0) return false;
-  int32_t dmin = INT32_MAX, dmax = INT32_MIN;
+  int32_t dmin = INT32_MAX, dmax = INT32_MIN, tabs = 0;
   for (int c = 1; c < kAlphabet; ++c)
-    for (int x = 0; x < kAlphabet; ++x)  // 0: the pad code after Seq1
+    for (int x = 0; x < kAlphabet; ++x) {  // 0: the pad code after Seq1
+      tabs = std::max(tabs, std::abs(t.score(c, x)));
       for (int y = 0; y < kAlphabet; ++y) {
         const int32_t d = t.score(c, x) - t.score(c, y);
         dmin = std::min(dmin, d);
         dmax = std::max(dmax, d);
       }
-  if (dmin < -128 || dmax > 127) return false;
+    }
+  // the kernel's anchor diagonals read T itself as int8 too (negative weights through the API could give
+  // a narrow range of large values)
+  if (dmin < -128 || dmax > 127 || tabs > 127) return false;
   out.row = L1;
   out.entries.assign(static_cast<size_t>((kAlphabet - 1) * L1 + overhang), 0);
   std::vector<int32_t> d(static_cast<size_t>(L1) + 1, 0);
