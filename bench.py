@@ -154,7 +154,9 @@ def main():
     dev = torch.device("cuda", gpu)
     distributed = world > 1
     nccl = args.dist_backend == "nccl"
-    cdev = dev if nccl else torch.device("cpu")  # where collective tensors live
+    # where collective tensors live: the GPU for RCCL; the host for gloo and for a single rank (no
+    # collective runs then, so a device copy of the header would only add a D2H sync per step)
+    cdev = dev if (nccl and distributed) else torch.device("cpu")
     if distributed:
         if nccl:
             dist.init_process_group("nccl", device_id=dev)
