@@ -54,7 +54,8 @@ class HostArrays:
     """Per-rank slice of the node-shared input/result arrays (/dev/shm files, or private memory)."""
 
     def __init__(self, tag, rank, lengths, use_shm, packed, seed, len_base, hip_alloc=False):
-        from mpi_openmp_cuda_amd.models.problem import pack5, pack_lengths4, packed5_bytes
+        from mpi_openmp_cuda_amd.models.problem import (lengths3_bytes, pack5, pack_lengths3, pack_lengths4,
+                                                        packed5_bytes)
         from mpi_openmp_cuda_amd.utils.synthetic import fill_codes
 
         n = lengths.shape[0]
@@ -87,9 +88,14 @@ class HostArrays:
         self.offsets = mk("offsets", np.int64, n + 1)
         self.offsets[0] = 0
         np.cumsum(lengths, out=self.offsets[1:])
-        # narrow lengths (the parser's by-product): 4 bits above the batch's minimum when the range allows
-        self.len_bits = 4 if len_base is not None else 8
-        if self.len_bits == 4:
+        # narrow lengths (the parser's by-product): 3 or 4 bits above the batch's minimum when the range
+        # allows (input6: 6..11 -> 3 bits)
+        span = int(lengths.max() - lengths.min()) if n else 0
+        self.len_bits = 8 if len_base is None else (3 if span <= 7 else 4)
+        if self.len_bits == 3:
+            self.lengths = mk("lengths3", np.uint8, lengths3_bytes(n))
+            pack_lengths3(lengths, len_base, out=self.lengths)
+        elif self.len_bits == 4:
             self.lengths = mk("lengths4", np.uint8, (n + 1) // 2)
             pack_lengths4(lengths, len_base, out=self.lengths)
         else:

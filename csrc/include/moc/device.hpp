@@ -140,6 +140,8 @@ struct ShortArgs {
   const int64_t* offsets = nullptr;   // n+1 absolute offsets
   const uint8_t* lengths8 = nullptr;  // optional narrow lengths (saves 7 B/record of reads)
   const uint8_t* lengths4 = nullptr;  // optional nibble lengths: record i = len_base + nibble i (low first)
+  const uint8_t* lengths3 = nullptr;  // optional 3-bit lengths: record i = len_base + bits [3i, 3i+3), LSB
+                                      // first (one readable slack byte after the last record's)
   int32_t len_base = 0;
   int64_t n = 0;
   void* out = nullptr;                // results, format `fmt`, record i at index i

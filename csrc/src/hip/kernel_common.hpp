@@ -186,9 +186,42 @@ __device__ __forceinline__ void release_work_counter(unsigned* counter) {
 
 // Length of record `idx` of the batch from the narrowest available source.
 __device__ __forceinline__ int record_length(const ShortArgs& a, int64_t idx) {
+  if (a.lengths3) {
+    const int64_t bit = 3 * idx;
+    const uint32_t w = a.lengths3[bit >> 3] | (static_cast<uint32_t>(a.lengths3[(bit >> 3) + 1]) << 8);
+    return a.len_base + static_cast<int>((w >> (bit & 7)) & 7u);
+  }
   if (a.lengths4) return a.len_base + ((a.lengths4[idx >> 1] >> (4 * (idx & 1))) & 15);
   if (a.lengths8) return a.lengths8[idx];
   return static_cast<int>(a.offsets[idx + 1] - a.offsets[idx]);
+}
+
+// Lengths of the 4 consecutive records i0 .. i0+3 of a thread (entries past n_valid are 0) with one or
+// two loads instead of one or two per record: for host-resident (zero-copy) batches every load instruction
+// becomes PCIe read requests, and the length loads outnumber the letter loads otherwise.
+__device__ __forceinline__ void record_lengths4(const ShortArgs& a, int64_t i0, int n_valid, int (&L)[4]) {
+  if (n_valid >= 4 && (i0 & 3) == 0 && !(a.lengths3 == nullptr && a.lengths4 == nullptr && a.lengths8 == nullptr)) {
+    if (a.lengths8) {
+      const uint32_t w = *reinterpret_cast<const uint32_t*>(a.lengths8 + i0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) L[q] = static_cast<int>((w >> (8 * q)) & 0xffu);
+      return;
+    }
+    if (a.lengths4) {
+      const uint32_t w = *reinterpret_cast<const uint16_t*>(a.lengths4 + (i0 >> 1));
+#pragma unroll
+      for (int q = 0; q < 4; ++q) L[q] = a.len_base + static_cast<int>((w >> (4 * q)) & 15u);
+      return;
+    }
+    const int64_t bit = 3 * i0;  // multiple of 4 records: the 12 bits start at bit 0 or 4 of a byte
+    const uint8_t* b = a.lengths3 + (bit >> 3);
+    const uint32_t w = (static_cast<uint32_t>(b[0]) | (static_cast<uint32_t>(b[1]) << 8)) >> (bit & 7);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) L[q] = a.len_base + static_cast<int>((w >> (3 * q)) & 7u);
+    return;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) L[q] = q < n_valid ? record_length(a, i0 + q) : 0;
 }
 
 // Copies a block's staged results (LDS) to the output: dwords, plus a trailing halfword for R2 tiles

@@ -122,15 +122,8 @@ __global__ __launch_bounds__(kBlock) void short_search_kernel(ProblemView pv, Sh
 
     // ---- 1. lengths -> block exclusive scan -> loff[0..m]
     int len4[4];
-    int sum = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = tid * 4 + q;
-      int L = 0;
-      if (r < m) L = record_length(a, rb + r);
-      len4[q] = L;
-      sum += L;
-    }
+    record_lengths4(a, rb + tid * 4, min(4, max(0, m - tid * 4)), len4);
+    const int sum = len4[0] + len4[1] + len4[2] + len4[3];
     const int incl = wave_inclusive_sum(sum, lane);
     if (lane == 63) misc[4 + wave] = incl;
     __syncthreads();

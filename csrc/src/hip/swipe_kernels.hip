@@ -136,11 +136,7 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
     f.m = static_cast<int>(min(static_cast<int64_t>(a.tile_records), a.n - f.rb));
     f.start = a.offsets[f.rb];
     f.end = a.offsets[f.rb + f.m];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = tid * 4 + q;
-      f.len4[q] = r < f.m ? record_length(a, f.rb + r) : 0;
-    }
+    record_lengths4(a, f.rb + tid * 4, min(4, max(0, f.m - tid * 4)), f.len4);
     const int64_t b_first = P5 ? (5 * f.start) >> 3 : f.start;
     const int64_t b_end = P5 ? (5 * f.end + 7) >> 3 : f.end;
     f.a0 = reinterpret_cast<uintptr_t>(a.codes + b_first) & ~uintptr_t{15};

@@ -456,18 +456,22 @@ bool HipEngine::direct_pointers(const uint8_t* codes, const int64_t* offsets, co
   const int64_t c0 = offsets[0], c1 = offsets[n];
   // byte range of the letters: [b0, b1)
   const int64_t b0 = packed5 ? (5 * c0) >> 3 : c0, b1 = packed5 ? ((5 * c1 + 7) >> 3) + 1 : c1;
-  // the kernels stage letters with 16-byte loads: up to 15 bytes past the range end must be mapped too
-  if (c1 > c0 && !pinned_range(codes + b0, static_cast<size_t>(b1 - b0) + 16, &dc)) return false;
+  // the kernels stage letters with 16-byte loads of the aligned granules covering [b0, b1): a granule
+  // never crosses a page, so the pages of [b0, b1) are all that must be mapped
+  if (c1 > c0 && !pinned_range(codes + b0, static_cast<size_t>(b1 - b0), &dc)) return false;
   if (!pinned_range(offsets, sizeof(int64_t) * static_cast<size_t>(n + 1), &doff)) return false;
-  const size_t len_bytes = len_bits == 4 ? static_cast<size_t>((n + 1) / 2) : static_cast<size_t>(n);
+  const size_t len_bytes = len_bits == 4   ? static_cast<size_t>((n + 1) / 2)
+                           : len_bits == 3 ? static_cast<size_t>((3 * n + 7) / 8 + 1)
+                                           : static_cast<size_t>(n);
   if (lengths && !pinned_range(lengths, len_bytes, &dlen)) return false;
   if (!pinned_range(out, static_cast<size_t>(fb) * static_cast<size_t>(n), &dout)) return false;
   // device view of the codes base pointer (record i at base + offsets[i], or at bit 5*offsets[i])
   a.codes = c1 > c0 ? static_cast<const uint8_t*>(dc) - b0 : nullptr;
-  a.dbg_codes_end = b1;
+  a.dbg_codes_end = b1 + 15;  // the last granule may extend up to 15 bytes past b1
   a.offsets = static_cast<const int64_t*>(doff);
   a.lengths8 = len_bits == 8 ? static_cast<const uint8_t*>(dlen) : nullptr;
   a.lengths4 = len_bits == 4 ? static_cast<const uint8_t*>(dlen) : nullptr;
+  a.lengths3 = len_bits == 3 ? static_cast<const uint8_t*>(dlen) : nullptr;
   a.len_base = len_base;
   a.out = const_cast<void*>(dout);
   return c1 > c0;
@@ -479,7 +483,7 @@ void HipEngine::solve(const uint8_t* codes, const int64_t* offsets, int64_t n, R
 
 void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths, int64_t n, void* out,
                          ResultFormat fmt, const BatchHints& hints, bool packed5, int len_bits, int len_base) {
-  if (lengths && len_bits != 8 && len_bits != 4) throw Error("lengths must be 8- or 4-bit");
+  if (lengths && len_bits != 8 && len_bits != 4 && len_bits != 3) throw Error("lengths must be 8-, 4- or 3-bit");
   if (!have_problem_) throw Error("HipEngine::solve before set_problem");
   MOC_HIP_CHECK(hipSetDevice(device_));
   TraceRange tr("moc.solve");
@@ -502,6 +506,8 @@ void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uin
   if (len_bits == 8 && lengths && ls.mx > 255) lengths = nullptr;
   if (len_bits == 4 && lengths && (ls.mn < len_base || ls.mx > len_base + 15))
     throw Error("nibble lengths cannot hold this batch's lengths");
+  if (len_bits == 3 && lengths && (ls.mn < len_base || ls.mx > len_base + 7))
+    throw Error("3-bit lengths cannot hold this batch's lengths");
   if (fmt == ResultFormat::R4 && (L1_ > 255 || ls.mx > 255 || table_.max_abs() * ls.mx >= 32767))
     throw Error("result format R4 cannot hold this batch");
   if (fmt == ResultFormat::R8 && (L1_ > 65535 || ls.mx > 65535)) throw Error("result format R8 cannot hold this batch");
@@ -538,7 +544,7 @@ void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uin
     stats_.direct = 1;
     stats_.chunks = 1;
     const int64_t letters = offsets[n] - offsets[0];
-    stats_.h2d_bytes = (packed5 ? (5 * letters + 7) / 8 : letters) + (a.lengths4 ? (n + 1) / 2 : a.lengths8 ? n : 8 * n);
+    stats_.h2d_bytes = (packed5 ? (5 * letters + 7) / 8 : letters) + (a.lengths3 ? (3 * n + 7) / 8 : a.lengths4 ? (n + 1) / 2 : a.lengths8 ? n : 8 * n);
     stats_.d2h_bytes = static_cast<int64_t>(fb) * n;
     wall.stop();
     stats_.total_ms = wall.total_ms();
@@ -559,7 +565,10 @@ void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uin
 void HipEngine::run_dma_stream(const dev::ProblemView& pv, const dev::ShortArgs& a0, bool swipe, const uint8_t* codes,
                                const int64_t* offsets, const uint8_t* lengths, int len_bits, int64_t n, void* out,
                                int fb, bool packed5) {
-  const int64_t tile = std::max<int64_t>(a0.tile_records, 2);  // even: nibble lengths stay byte aligned
+  // chunk starts at whole tiles and at multiples of 8 records: 3-, 4- and 8-bit lengths stay byte aligned
+  const int64_t tile = (std::max<int64_t>(a0.tile_records, 1) + 7) / 8 * 8 == a0.tile_records
+                           ? a0.tile_records
+                           : std::max<int64_t>(a0.tile_records, 1) * 8;
   const int64_t letters = offsets[n] - offsets[0];
   const int64_t total_bytes = packed5 ? (5 * letters + 7) / 8 : letters;
   const int64_t per_rec = std::max<int64_t>(1, total_bytes / std::max<int64_t>(n, 1));
@@ -574,7 +583,10 @@ void HipEngine::run_dma_stream(const dev::ProblemView& pv, const dev::ShortArgs&
     const int64_t B0 = b0 & ~int64_t{15};
     const size_t lbytes = static_cast<size_t>(b1 - B0);  // + 16 bytes of device slack, never copied: the
                                                          // host range may end at its allocation's end
-    const size_t nbytes = lengths ? (len_bits == 4 ? static_cast<size_t>((cn + 1) / 2) : static_cast<size_t>(cn)) : 0;
+    const size_t nbytes = !lengths        ? 0
+                          : len_bits == 4 ? static_cast<size_t>((cn + 1) / 2)
+                          : len_bits == 3 ? static_cast<size_t>((3 * cn + 7) / 8 + 1)
+                                          : static_cast<size_t>(cn);
     const size_t rbytes = static_cast<size_t>(fb) * static_cast<size_t>(cn);
     if (s.busy) {  // the slot's previous chunk: its letters consumed, its results returned
       MOC_HIP_CHECK(hipEventSynchronize(s.ev_done));
@@ -585,7 +597,9 @@ void HipEngine::run_dma_stream(const dev::ProblemView& pv, const dev::ShortArgs&
     ensure(s.d_out, s.d_out_cap, std::max<size_t>(rbytes, 16));
     copy_h2d(s.d_packed, codes + B0, lbytes, s_copy_);
     if (nbytes) {
-      const size_t nb0 = len_bits == 4 ? static_cast<size_t>(r0 / 2) : static_cast<size_t>(r0);
+      const size_t nb0 = len_bits == 4   ? static_cast<size_t>(r0 / 2)
+                         : len_bits == 3 ? static_cast<size_t>(3 * r0 / 8)
+                                         : static_cast<size_t>(r0);
       copy_h2d(s.d_offsets, lengths + nb0, nbytes, s_copy_);
     }
     MOC_HIP_CHECK(hipEventRecord(s.ev_h2d, s_copy_));
@@ -596,6 +610,7 @@ void HipEngine::run_dma_stream(const dev::ProblemView& pv, const dev::ShortArgs&
     a.offsets = a0.offsets + r0;  // pinned host (zero-copy): two reads per tile
     a.lengths8 = lengths && len_bits == 8 ? static_cast<const uint8_t*>(s.d_offsets) : nullptr;
     a.lengths4 = lengths && len_bits == 4 ? static_cast<const uint8_t*>(s.d_offsets) : nullptr;
+    a.lengths3 = lengths && len_bits == 3 ? static_cast<const uint8_t*>(s.d_offsets) : nullptr;
     a.n = cn;
     a.out = s.d_out;
     if (c == 0) MOC_HIP_CHECK(hipEventRecord(ev_a_, s_compute_));
@@ -752,6 +767,7 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
       a.offsets = doffs;
       a.lengths8 = nullptr;
       a.lengths4 = nullptr;
+      a.lengths3 = nullptr;
       a.n = cn;
       a.out = s.d_out;
       a.counter = s.d_counter;

@@ -35,6 +35,40 @@ def pack5(codes: np.ndarray, out: np.ndarray = None) -> np.ndarray:
     return out
 
 
+def pack_lengths3(lengths: np.ndarray, base: int, out: np.ndarray = None) -> np.ndarray:
+    """Record lengths in [base, base + 7] -> 3 bits each (record i at bits [3i, 3i+3), LSB first), plus
+    one slack byte (the kernels read two bytes per length) — for batches whose lengths span <= 8 values
+    (input6-shaped: 6..11), 25% fewer length bytes than nibbles."""
+    v = np.asarray(lengths).astype(np.int64) - int(base)
+    if v.size and (v.min() < 0 or v.max() > 7):
+        raise ValueError("lengths do not fit 3 bits above the base")
+    n = v.shape[0]
+    nbytes = lengths3_bytes(n)
+    if out is None:
+        out = np.empty(nbytes, dtype=np.uint8)
+    assert out.dtype == np.uint8 and out.shape[0] >= nbytes
+    groups = (n + 7) // 8
+    g = np.zeros(groups * 8, dtype=np.uint32)
+    g[:n] = v
+    g = g.reshape(groups, 8)
+    word = np.zeros(groups, dtype=np.uint32)
+    for k in range(8):
+        word |= g[:, k] << np.uint32(3 * k)
+    body = np.zeros((groups, 3), dtype=np.uint8)
+    body[:, 0] = word & 0xFF
+    body[:, 1] = (word >> 8) & 0xFF
+    body[:, 2] = (word >> 16) & 0xFF
+    flat = body.reshape(-1)
+    m = min(flat.shape[0], nbytes)  # bytes past the last record's bits are zero anyway
+    out[:m] = flat[:m]
+    out[m:nbytes] = 0
+    return out
+
+
+def lengths3_bytes(n: int) -> int:
+    return (3 * int(n) + 7) // 8 + 1 if n else 1
+
+
 def pack_lengths4(lengths: np.ndarray, base: int, out: np.ndarray = None) -> np.ndarray:
     """Record lengths in [base, base + 15] -> 4 bits each, two per byte (record i in the low nibble of
     byte i // 2 when i is even, the high nibble when odd) — the streaming kernels' narrowest length form."""

@@ -180,7 +180,8 @@ class HipSearchEngine:
         """Host CSR -> host results. ``codes[offsets[i]:offsets[i+1]]`` is record i (``offsets`` may be a
         slice of a larger absolute offset array). ``fmt``: r12 | r8 | r4 | r2 | auto (smallest that fits);
         ``lengths``: optional narrow record lengths, uint8 (``lengths_bits`` 8) or two per byte
-        (``lengths_bits`` 4, low nibble first, length = ``lengths_base`` + nibble; see pack_lengths4);
+        (``lengths_bits`` 4, low nibble first, length = ``lengths_base`` + nibble; see pack_lengths4) or
+        3-bit fields (``lengths_bits`` 3, see pack_lengths3);
         ``l2_range``: optional known (min, max) length (R2 results are encoded for it: decode with
         ``r2_params(*l2_range)`` or ``stats()["r2"]``); ``packed5``: ``codes`` is a 5-bit packed stream
         (models.problem.pack5) instead of bytes."""
@@ -196,7 +197,8 @@ class HipSearchEngine:
             out = np.empty(n, dtype=_lib.FORMAT_DTYPES[fid])
         assert out.dtype.itemsize == _lib.FORMAT_DTYPES[fid].itemsize and out.size >= n
         if lengths is not None:
-            assert lengths.dtype == np.uint8 and lengths.shape[0] >= (n if lengths_bits == 8 else (n + 1) // 2)
+            need = n if lengths_bits == 8 else (n + 1) // 2 if lengths_bits == 4 else (3 * n + 7) // 8 + 1
+            assert lengths.dtype == np.uint8 and lengths.shape[0] >= need
         lo, hi = l2_range if l2_range is not None else (-1, -1)
         _lib.check(_lib.lib().moc_engine_solve_ex(self._h, _lib.ptr(codes), _lib.ptr(offsets), _lib.ptr(lengths),
                                                   int(lengths_bits), int(lengths_base), n, _lib.ptr(out), fid, int(lo),

@@ -398,13 +398,13 @@ def test_pinned_neighbours_staged_copies():
 
 
 @pytest.mark.parametrize("mode", ["dma", "zero_copy"])
-@pytest.mark.parametrize("packed,len_bits", [(False, 0), (False, 8), (True, 4), (True, 8)])
+@pytest.mark.parametrize("packed,len_bits", [(False, 0), (False, 8), (True, 4), (True, 8), (True, 3), (False, 3)])
 @pytest.mark.parametrize("shape,n", [("input6", 100_003), ("input1", 20_001)])
 def test_host_stream_modes(monkeypatch, mode, packed, len_bits, shape, n):
     # pinned host batches: chunked SDMA in/out around the HBM-resident kernel (64 KiB chunks: many of
     # them, odd tail) or the kernel's own zero-copy reads/writes — same answers
     from mpi_openmp_cuda_amd import _lib
-    from mpi_openmp_cuda_amd.models.problem import pack5, pack_lengths4
+    from mpi_openmp_cuda_amd.models.problem import pack5, pack_lengths3, pack_lengths4
     from mpi_openmp_cuda_amd.utils.synthetic import SHAPES
 
     monkeypatch.setenv("MOC_DMA_STREAM", "1" if mode == "dma" else "0")
@@ -424,6 +424,11 @@ def test_host_stream_modes(monkeypatch, mode, packed, len_bits, shape, n):
     elif len_bits == 4:
         lengths = pack_lengths4(np.diff(prob.offsets), sh.l2_min)
         kw = dict(lengths=lengths, lengths_bits=4, lengths_base=sh.l2_min)
+    elif len_bits == 3:
+        if sh.l2_max - sh.l2_min > 7:
+            pytest.skip("lengths span more than 3 bits")
+        lengths = pack_lengths3(np.diff(prob.offsets), sh.l2_min)
+        kw = dict(lengths=lengths, lengths_bits=3, lengths_base=sh.l2_min)
     out = np.zeros(prob.n, dtype=_lib.FORMAT_DTYPES[_lib.FORMAT_NAMES.index("r8")])
     eng.pin(codes, prob.offsets, out, *([lengths] if lengths is not None else []))
     eng.solve(codes, prob.offsets, out=out, fmt="r8", packed5=packed, **kw)

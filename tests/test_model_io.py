@@ -139,3 +139,18 @@ def test_r2_decode_python_and_native():
     assert np.array_equal(as_triples(out), trip)
     with pytest.raises(ValueError):
         as_triples(codes)
+
+
+def test_pack_lengths3_roundtrip():
+    from mpi_openmp_cuda_amd.models.problem import lengths3_bytes, pack_lengths3
+
+    rng = np.random.default_rng(3)
+    for n in (0, 1, 7, 8, 9, 1001):
+        lens = rng.integers(6, 14, n)
+        out = pack_lengths3(lens, 6)
+        assert out.shape[0] == lengths3_bytes(n)
+        bits = np.unpackbits(out, bitorder="little")
+        got = [int(bits[3 * i] + 2 * bits[3 * i + 1] + 4 * bits[3 * i + 2]) + 6 for i in range(n)]
+        assert got == [int(x) for x in lens]
+    with pytest.raises(ValueError):
+        pack_lengths3(np.array([6, 14]), 6)
