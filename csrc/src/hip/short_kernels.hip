@@ -57,7 +57,7 @@ ShortLayout short_layout(int L1, int tile_records, int codes_cap, int fmt_bytes,
     l.s1_bytes = align16(L1 + kWave + 4);
   }
   l.loff_off = l.table_bytes + l.s1_bytes;
-  l.codes_off = l.loff_off + align16((tile_records + 1) * 4 + 32);
+  l.codes_off = l.loff_off + align16((tile_records + 1) * 4 + 64);  // + misc: 16 ints
   l.res_off = l.codes_off + align16(codes_cap);
   l.total = l.res_off + align16(tile_records * fmt_bytes);
   return l;
@@ -111,14 +111,27 @@ __global__ __launch_bounds__(kBlock) void short_search_kernel(ProblemView pv, Sh
 
   for (;;) {
     __syncthreads();  // previous tile fully consumed (and tables built on the first pass)
-    if (tid == 0) misc[0] = static_cast<int>(atomicAdd(a.counter, 1u));
+    if (tid == 0) {  // tile id, and its letter range (one host-memory read per block, not per wave)
+      const int64_t tt = atomicAdd(a.counter, 1u);
+      misc[0] = static_cast<int>(tt);
+      if (tt < n_tiles) {
+        const int64_t r0 = tt * a.tile_records;
+        const int64_t st = a.offsets[r0], en = a.offsets[min(r0 + a.tile_records, a.n)];
+        misc[8] = static_cast<int>(static_cast<uint32_t>(st));
+        misc[9] = static_cast<int>(static_cast<uint64_t>(st) >> 32);
+        misc[10] = static_cast<int>(static_cast<uint32_t>(en));
+        misc[11] = static_cast<int>(static_cast<uint64_t>(en) >> 32);
+      }
+    }
     __syncthreads();
     const int64_t t = misc[0];
     if (t >= n_tiles) break;  // block-uniform exit; every wave reaches it
     const int64_t rb = t * a.tile_records;
     const int m = static_cast<int>(min(static_cast<int64_t>(a.tile_records), a.n - rb));
-    const int64_t start = a.offsets[rb];
-    const int64_t end = a.offsets[rb + m];
+    const int64_t start = static_cast<int64_t>((static_cast<uint64_t>(static_cast<uint32_t>(misc[9])) << 32) |
+                                               static_cast<uint32_t>(misc[8]));
+    const int64_t end = static_cast<int64_t>((static_cast<uint64_t>(static_cast<uint32_t>(misc[11])) << 32) |
+                                             static_cast<uint32_t>(misc[10]));
 
     // ---- 1. lengths -> block exclusive scan -> loff[0..m]
     int len4[4];

@@ -59,7 +59,7 @@ SwipeLayout swipe_layout(int L1, int noff, int l2w, int tile_records, int codes_
   l.prof_bytes = al16(8 * l.copy_elems * 2);
   l.s_off = l.prof_bytes;
   l.loff_off = l.s_off + al16(kLutInts + l.row);
-  l.codes_off = l.loff_off + al16((tile_records + 1) * 4 + 32);
+  l.codes_off = l.loff_off + al16((tile_records + 1) * 4 + 64);  // + misc: 16 ints
   l.res_off = l.codes_off + al16(codes_cap);
   l.total = l.res_off + al16(tile_records * fb);
   return l;
@@ -134,8 +134,12 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
     if (t >= n_tiles) return;
     f.rb = t * a.tile_records;
     f.m = static_cast<int>(min(static_cast<int64_t>(a.tile_records), a.n - f.rb));
-    f.start = a.offsets[f.rb];
-    f.end = a.offsets[f.rb + f.m];
+    // the tile's letter range: loaded once per block by grab(), not once per wave (each load of host
+    // memory is a PCIe read request of its own)
+    f.start = static_cast<int64_t>((static_cast<uint64_t>(static_cast<uint32_t>(misc[9])) << 32) |
+                                   static_cast<uint32_t>(misc[8]));
+    f.end = static_cast<int64_t>((static_cast<uint64_t>(static_cast<uint32_t>(misc[11])) << 32) |
+                                 static_cast<uint32_t>(misc[10]));
     record_lengths4(a, f.rb + tid * 4, min(4, max(0, f.m - tid * 4)), f.len4);
     const int64_t b_first = P5 ? (5 * f.start) >> 3 : f.start;
     const int64_t b_end = P5 ? (5 * f.end + 7) >> 3 : f.end;
@@ -149,10 +153,20 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
     }
   };
   auto grab = [&]() -> int64_t {
-    if (tid == 0) misc[0] = static_cast<int>(atomicAdd(a.counter, 1u));
+    if (tid == 0) {
+      const int64_t t = atomicAdd(a.counter, 1u);
+      misc[0] = static_cast<int>(t);
+      if (t < n_tiles) {  // the tile's letter range [offsets[rb], offsets[rb + m]) for fetch()
+        const int64_t rb = t * a.tile_records;
+        const int64_t st = a.offsets[rb], en = a.offsets[min(rb + a.tile_records, a.n)];
+        misc[8] = static_cast<int>(static_cast<uint32_t>(st));
+        misc[9] = static_cast<int>(static_cast<uint64_t>(st) >> 32);
+        misc[10] = static_cast<int>(static_cast<uint32_t>(en));
+        misc[11] = static_cast<int>(static_cast<uint64_t>(en) >> 32);
+      }
+    }
     __syncthreads();
     const int64_t t = misc[0];
-    __syncthreads();  // misc[0] is reused by the next grab
     return t;
   };
 
