@@ -126,6 +126,15 @@ debug-kernels:
 	done
 	$(CXX) -shared -fopenmp -o $(BUILD)/debug/libmoc.so $(CORE_OBJS) $(BUILD)/debug/*.hip.o $(LDROCM) -ldl
 
+# Kernel A/B builds: make variant NAME=p4 VDEFS="-DMOC_T16_PREFETCH=4" -> build/variant_p4/libmoc.so
+# (select with MOC_LIB_PATH).
+variant: lib
+	@mkdir -p $(BUILD)/variant_$(NAME)
+	for f in $(HIP_SRCS); do \
+	  $(HIPCC) $(HIPFLAGS) $(VDEFS) -c $$f -o $(BUILD)/variant_$(NAME)/$$(basename $$f .hip).hip.o || exit 1; \
+	done
+	$(CXX) -shared -fopenmp -o $(BUILD)/variant_$(NAME)/libmoc.so $(CORE_OBJS) $(BUILD)/variant_$(NAME)/*.hip.o $(LDROCM) -ldl
+
 clean:
 	rm -rf $(BUILD) final final_asan final_tsan $(PKG_LIB) $(GPU_PLUGIN)
 

@@ -90,7 +90,10 @@ struct ProblemView {
 
 // Entries after the tile16 profile's last row: reads of wave-tile lanes past the valid offsets reach
 // at most L1 + 128*U - 2 (U <= 4) into a row.
-constexpr int kProf16Overhang = 512;
+#ifndef MOC_PROF16_OVERHANG
+#define MOC_PROF16_OVERHANG 512
+#endif
+constexpr int kProf16Overhang = MOC_PROF16_OVERHANG;  // minimum; >= the widest tile span (128 * U entries)
 // LDS budget of one tile16 workgroup (the whole CU: a single workgroup may declare all 160 KiB).
 constexpr int kProf16MaxLds = 160 * 1024;
 // tile16 LDS image: profile (prof16_bytes, 16-aligned) | int8 LUT T[32][32] | Seq1 codes + pad (for

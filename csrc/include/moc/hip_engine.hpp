@@ -157,6 +157,7 @@ class HipEngine {
   uint8_t* d_seq1_ = nullptr;
   uint16_t* d_prof16_ = nullptr;  // tile16 profile (null: the problem does not fit it, or MOC_TILE16=0)
   int32_t prof16_bytes_ = 0;
+  int32_t prof16_overhang_ = 0;  // zero profile entries past the last row (bounds the tile span)
   bool tile16_ = true;            // MOC_TILE16 (A/B switch of the long-record kernel)
   int64_t L1_ = 0;
   Semantics sem_ = Semantics::Reference;

@@ -19,7 +19,10 @@
 //   * Tot_o is not summed per cell: per tile one anchor diagonal Tot_{oA} (oA = first offset past the
 //     tile or past the valid range) is summed alongside the sweep (each chunk's lanes add their step's
 //     pair score from an int8 LUT + Seq1 staged next to the profile), and
-//     Tot_o = Tot_{oA} + sum_{o <= o' < oA} D_{o'}(L2) comes from a wave suffix scan.
+//     Tot_o = Tot_{oA} + sum_{o <= o' < oA} D_{o'}(L2) comes from a wave scan on the DPP network;
+//   * short records (mean |Seq2| < 96) take U = 8 sub-tiles (1024-offset tiles: half the per-tile
+//     epilogues) when the profile's 1024-entry overhang fits the LDS; their last chunk issues the reads
+//     of 8 steps before the adds (profiles/tile16_variants_v2.log).
 // Per offset this gives the best score, but not which k: the sweep reduces keys (score, ~(2o + mutated))
 // — the reference order: score, then smallest o, then k = 0 first — and resolve16_kernel re-walks only
 // the winning diagonal of each record (one wave, O(L2)) to find the smallest k with that score and
@@ -47,6 +50,15 @@ typedef short s16x2 __attribute__((ext_vector_type(2)));
 
 #ifndef MOC_T16_UNROLL
 #define MOC_T16_UNROLL 64  // hot-loop steps per unrolled group; 64 = the whole chunk (best of 8/16/32/64)
+#endif
+#ifndef MOC_T16_PREFETCH
+#define MOC_T16_PREFETCH 0  // steps of profile reads in flight ahead of the adds (0: compiler schedule)
+#endif
+#ifndef MOC_T16_TAIL8
+#define MOC_T16_TAIL8 1  // last chunk in groups of 8 steps (reads first) instead of one step at a time
+#endif
+#ifndef MOC_T16_DPP_SCAN
+#define MOC_T16_DPP_SCAN 1  // tile epilogue scans on DPP instead of ds_bpermute shuffles
 #endif
 constexpr int kBlock16 = 1024;  // 16 waves: the profile takes most of the CU's LDS, one workgroup holds it
 constexpr int kWavesPerBlock16 = kBlock16 / 64;
@@ -88,6 +100,23 @@ __device__ __forceinline__ int wave_suffix_sum(int v, int lane) {
     const int t = __shfl_down(v, d, 64);
     if (lane + d < 64) v += t;
   }
+  return v;
+}
+
+// Inclusive prefix sum over the lanes of a wave on the DPP network: row shifts 1/2/4/8 (zero-filled),
+// then lane 15 of each row into the next row and lane 31 into rows 2-3. VALU only — no LDS round trip
+// per level as with __shfl (ds_bpermute).
+template <int Ctrl, int RowMask>
+__device__ __forceinline__ int dpp_or0(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, Ctrl, RowMask, 0xf, false);
+}
+__device__ __forceinline__ int wave_prefix_sum_dpp(int v) {
+  v += dpp_or0<0x111, 0xf>(v);  // row_shr:1
+  v += dpp_or0<0x112, 0xf>(v);  // row_shr:2
+  v += dpp_or0<0x114, 0xf>(v);  // row_shr:4
+  v += dpp_or0<0x118, 0xf>(v);  // row_shr:8
+  v += dpp_or0<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
+  v += dpp_or0<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
   return v;
 }
 }  // namespace
@@ -185,8 +214,34 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
         const int c_next = letter(i0 + 64 + lane);
         const int so = row_off(c, i0 + lane);
         anchor_add(c, i0 + lane);
+#if MOC_T16_PREFETCH > 0
+        // explicit load ring: step j's profile entries were read MOC_T16_PREFETCH steps earlier, so the
+        // LDS latency overlaps the adds of the steps in between
+        constexpr int P = MOC_T16_PREFETCH;
+        uint32_t ring[P][U];
+        auto load = [&](int j, uint32_t* dst) {
+          const unsigned char* p = lbase + __builtin_amdgcn_readlane(so, j);
+#pragma unroll
+          for (int u = 0; u < U; ++u) dst[u] = *reinterpret_cast<const uint16_t*>(p + 2 * kSub * u);
+        };
+#pragma unroll
+        for (int q = 0; q < P; ++q) load(q, ring[q]);
+#pragma unroll
+        for (int j = 0; j < 64; ++j) {
+          uint32_t cur[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) cur[u] = ring[j % P][u];
+          if (j + P < 64) load(j + P, ring[j % P]);
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            add_pair(acc[u], cur[u]);
+            best[u] = pk_max(best[u], acc[u]);
+          }
+        }
+#else
 #pragma unroll MOC_T16_UNROLL
         for (int j = 0; j < 64; ++j) step(so, j, true);
+#endif
         flush(true);
         c = c_next;
       }
@@ -194,23 +249,56 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
         const int m = steps - i0;
         const int so = row_off(c, i0 + lane);
         anchor_add(c, i0 + lane);
-        for (int j = 0; j < m - 1; ++j) step(so, j, true);
+        int j = 0;
+#if MOC_T16_TAIL8
+        // groups of 8 steps: all 8*U profile reads issue before the first add (short records live here)
+        for (; j + 8 <= m - 1; j += 8) {
+          uint32_t e[8][U];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const unsigned char* p = lbase + __builtin_amdgcn_readlane(so, j + q);
+#pragma unroll
+            for (int u = 0; u < U; ++u) e[q][u] = *reinterpret_cast<const uint16_t*>(p + 2 * kSub * u);
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              add_pair(acc[u], e[q][u]);
+              best[u] = pk_max(best[u], acc[u]);
+            }
+        }
+#endif
+        for (; j < m - 1; ++j) step(so, j, true);
         step(so, m - 1, false);
         flush(m > 1);
       }
       // ---- Tot per offset: anchor diagonal oA, then suffix sums of the D totals (valid offsets only)
+#if MOC_T16_DPP_SCAN
+      anchor = __builtin_amdgcn_readlane(wave_prefix_sum_dpp(anchor), 63);
+#else
 #pragma unroll
       for (int d = 32; d >= 1; d >>= 1) anchor += __shfl_xor(anchor, d, 64);
+#endif
       int carry = anchor;  // Tot at the end of the sub-tile being processed
 #pragma unroll
       for (int u = U - 1; u >= 0; --u) {
         const int oa = o0 + kSub * u + 2 * lane;
         const int ca = oa < oA ? DcA[u] : 0, cb = oa + 1 < oA ? DcB[u] : 0;
         const int pair = ca + cb;
+#if MOC_T16_DPP_SCAN
+        const int incl = wave_prefix_sum_dpp(pair);
+        const int sub_total = __builtin_amdgcn_readlane(incl, 63);
+        const int excl = sub_total - incl;   // lanes above this one
+        const int totB = carry + excl + cb;  // Tot_{oa+1}
+        const int totA = totB + ca;          // Tot_{oa}
+        carry += sub_total;
+#else
         const int excl = wave_suffix_sum(pair, lane) - pair;
         const int totB = carry + excl + cb;  // Tot_{oa+1}
         const int totA = totB + ca;          // Tot_{oa}
         carry = __shfl(totA, 0, 64);
+#endif
         acc64 = max_u64(acc64, pass1_candidate(oa, L1, L2, pv.semantics, totA, totB, mxA[u]));
         acc64 = max_u64(acc64, pass1_candidate(oa + 1, L1, L2, pv.semantics, totB, totB - cb, mxB[u]));
       }
@@ -308,6 +396,7 @@ void launch_tile16_keys(const ProblemView& pv, const BatchView& bv, const Plan& 
   switch (plan.u) {
     case 1: launch16_t<1>(pv, bv, plan, stream); break;
     case 2: launch16_t<2>(pv, bv, plan, stream); break;
+    case 8: launch16_t<8>(pv, bv, plan, stream); break;
     default: launch16_t<4>(pv, bv, plan, stream); break;
   }
   const int64_t rb = (plan.n_long + 3) / 4;

@@ -123,7 +123,7 @@ HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
   if (const char* g = std::getenv("MOC_GRAPHS")) opt_.use_graphs = std::atoi(g) != 0;
   if (const char* u = std::getenv("MOC_TILE_U")) {  // tuning override of the per-batch choice
     const int v = std::atoi(u);
-    if (v == 1 || v == 2 || v == 4) tile_u_ = v;
+    if (v == 1 || v == 2 || v == 4 || v == 8) tile_u_ = v;
   }
   if (const char* t16 = std::getenv("MOC_TILE16")) tile16_ = std::atoi(t16) != 0;
   if (const char* d = std::getenv("MOC_DMA_STREAM")) opt_.dma_stream = std::atoi(d);
@@ -232,9 +232,15 @@ void HipEngine::set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, S
   const size_t s1_off = (lut_bytes + 255) & ~size_t{255};
   const size_t prof_off = (s1_off + s1bytes + 255) & ~size_t{255};
   Profile16 prof;
-  const int64_t pbytes = ((2 * ((kAlphabet - 1) * L1 + dev::kProf16Overhang)) + 15) & ~int64_t{15};
+  // the overhang (zero entries past the last row) must cover the widest tile span, 128*U entries: 1024
+  // when that still fits the LDS (U = 8 for short records), else 512 (U <= 4, L1 up to 3052)
+  auto prof_bytes = [&](int64_t oh) { return ((2 * ((kAlphabet - 1) * L1 + oh)) + 15) & ~int64_t{15}; };
+  int64_t overhang = 2 * dev::kProf16Overhang;
+  if (dev::tile16_lds_bytes(prof_bytes(overhang), L1) > dev::kProf16MaxLds) overhang = dev::kProf16Overhang;
+  const int64_t pbytes = prof_bytes(overhang);
   const bool t16 = tile16_ && L1 > 0 && dev::tile16_lds_bytes(pbytes, L1) <= dev::kProf16MaxLds &&
-                   build_profile16(table_, seq1, L1, dev::kProf16Overhang, prof);
+                   build_profile16(table_, seq1, L1, overhang, prof);
+  prof16_overhang_ = t16 ? static_cast<int>(overhang) : 0;
   const size_t total = t16 ? prof_off + static_cast<size_t>(pbytes) : prof_off;
   image_.assign(total, 0);
   std::memcpy(image_.data(), table_.lut.data(), lut_bytes);
@@ -381,7 +387,9 @@ std::vector<dev::WaveStart> HipEngine::plan_waves(const int64_t* offsets, const 
   // sub-tiles per wave tile: 4 amortises the per-tile setup over short records, 2 keeps more waves busy
   // on long ones (measured: profiles/tile_variants.log)
   // (measured, both kernels: profiles/tile_variants.log, profiles/tile16_variants.log)
-  const int u = tile_u_ > 0 ? tile_u_ : (sum_l2 < 96 * n_long ? 4 : 2);
+  int u = tile_u_ > 0 ? tile_u_ : (sum_l2 < 96 * n_long ? 4 : 2);
+  if (tile_u_ <= 0 && u == 4 && d_prof16_ && 128 * 8 <= prof16_overhang_) u = 8;  // tile16: wider tiles for short records
+  if (u > 4 && !(d_prof16_ && 128 * u <= prof16_overhang_)) u = 4;                 // the overhang bounds the span
   u_out = u;
   std::vector<int64_t> pre(static_cast<size_t>(n_long) + 1, 0), tcost(static_cast<size_t>(n_long));
   std::vector<int32_t> ntiles(static_cast<size_t>(n_long));

@@ -203,11 +203,12 @@ void test_profile16() {
     std::vector<uint8_t> s1(static_cast<size_t>(L1));
     for (auto& x : s1) x = static_cast<uint8_t>(1 + rng() % (trial % 3 ? 26 : 3));  // few letters: many ties
     Profile16 prof;
-    if (!build_profile16(t, s1.data(), L1, 512, prof)) {
+    const int64_t span = trial % 4 < 2 ? 512 : 1024;  // tile span = 128*U offsets (U = 4 or 8) = overhang
+    if (!build_profile16(t, s1.data(), L1, span, prof)) {
       CHECK(w.w[0] + std::max({w.w[1], w.w[2], w.w[3]}) > 127);
       continue;
     }
-    CHECK(prof.entries.size() == static_cast<size_t>(26 * L1 + 512));
+    CHECK(prof.entries.size() == static_cast<size_t>(26 * L1 + span));
     auto entry = [&](int c, int64_t j) { return prof.entries[static_cast<size_t>((c - 1) * L1 + j)]; };
     RecordBatch batch;
     for (int r = 0; r < 6; ++r) {
@@ -244,10 +245,10 @@ void test_profile16() {
             Dc[o] += static_cast<int16_t>(accD);
           }
         }
-        // Tot per 512-offset tile: anchor diagonal at min(tile end, L1 - L2 + 1), then suffix sums of D totals
+        // Tot per tile: anchor diagonal at min(tile end, L1 - L2 + 1), then suffix sums of D totals
         std::vector<int32_t> tot(static_cast<size_t>(need) + 1, 0);
-        for (int64_t o0 = 0; o0 < need; o0 += 512) {
-          const int64_t oA = std::min<int64_t>(o0 + 512, need);
+        for (int64_t o0 = 0; o0 < need; o0 += span) {
+          const int64_t oA = std::min<int64_t>(o0 + span, need);
           int32_t acc = 0;
           for (int64_t i = 0; i < L2; ++i) acc += t.score(s2[i], oA + i < L1 ? s1[oA + i] : 0);
           for (int64_t o = oA - 1; o >= o0; --o) {

@@ -213,6 +213,20 @@ def test_tile16_edges(engine, L1, weights, alphabet, sem):
     assert "tile16" in engine.stats()["kernels"]
 
 
+@pytest.mark.parametrize("L1,alphabet", [(3000, 26), (3040, 3), (1030, 2), (300, 5)])
+def test_tile16_wide_tiles(engine, L1, alphabet):
+    # short records (mean |Seq2| < 96) take 1024-offset tiles (U = 8) when the profile's 1024-entry
+    # overhang fits the LDS (L1 3000, 1030, 300), 512-offset ones otherwise (L1 3040)
+    rng = np.random.default_rng(L1 * 7 + alphabet)
+    s1 = _letters(rng, L1, alphabet)
+    lens = [1, 2, 63, 64, 65, 95, L1 - 1, L1, L1 + 1] + list(rng.integers(1, 60, 300))
+    recs = [_letters(rng, n, alphabet) for n in lens]
+    prob = Problem.from_strings([7, 2, 3, 1], s1, recs)
+    for sem in (Semantics.REFERENCE, Semantics.SPEC):
+        check(engine, prob, sem)
+    assert "tile16" in engine.stats()["kernels"]
+
+
 def test_short_config_fallback(engine):
     # records far longer than Seq1 blow the short kernel's LDS tile budget -> everything via tiles
     rng = np.random.default_rng(9)
