@@ -51,9 +51,6 @@ typedef short s16x2 __attribute__((ext_vector_type(2)));
 #ifndef MOC_T16_UNROLL
 #define MOC_T16_UNROLL 64  // hot-loop steps per unrolled group; 64 = the whole chunk (best of 8/16/32/64)
 #endif
-#ifndef MOC_T16_PREFETCH
-#define MOC_T16_PREFETCH 0  // steps of profile reads in flight ahead of the adds (0: compiler schedule)
-#endif
 #ifndef MOC_T16_TAIL8
 #define MOC_T16_TAIL8 1  // last chunk in groups of 8 steps (reads first) instead of one step at a time
 #endif
@@ -214,34 +211,8 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
         const int c_next = letter(i0 + 64 + lane);
         const int so = row_off(c, i0 + lane);
         anchor_add(c, i0 + lane);
-#if MOC_T16_PREFETCH > 0
-        // explicit load ring: step j's profile entries were read MOC_T16_PREFETCH steps earlier, so the
-        // LDS latency overlaps the adds of the steps in between
-        constexpr int P = MOC_T16_PREFETCH;
-        uint32_t ring[P][U];
-        auto load = [&](int j, uint32_t* dst) {
-          const unsigned char* p = lbase + __builtin_amdgcn_readlane(so, j);
-#pragma unroll
-          for (int u = 0; u < U; ++u) dst[u] = *reinterpret_cast<const uint16_t*>(p + 2 * kSub * u);
-        };
-#pragma unroll
-        for (int q = 0; q < P; ++q) load(q, ring[q]);
-#pragma unroll
-        for (int j = 0; j < 64; ++j) {
-          uint32_t cur[U];
-#pragma unroll
-          for (int u = 0; u < U; ++u) cur[u] = ring[j % P][u];
-          if (j + P < 64) load(j + P, ring[j % P]);
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            add_pair(acc[u], cur[u]);
-            best[u] = pk_max(best[u], acc[u]);
-          }
-        }
-#else
 #pragma unroll MOC_T16_UNROLL
         for (int j = 0; j < 64; ++j) step(so, j, true);
-#endif
         flush(true);
         c = c_next;
       }
