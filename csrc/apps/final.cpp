@@ -334,17 +334,13 @@ std::vector<int64_t> Job::make_bounds(const int64_t* offsets, int64_t n, bool cp
   std::vector<int64_t> bounds(static_cast<size_t>(p) + 1, 0);
   if (ctx_.rank == kRoot) {
     const int64_t L1 = static_cast<int64_t>(eng_.seq1.size());
-    std::vector<int64_t> len(static_cast<size_t>(n));
     int64_t cells = 0;
 #pragma omp parallel for reduction(+ : cells) schedule(static) if (n > 65536)
-    for (int64_t i = 0; i < n; ++i) {
-      len[i] = offsets[i + 1] - offsets[i];
-      cells += record_cells(L1, len[i]);
-    }
+    for (int64_t i = 0; i < n; ++i) cells += record_cells(L1, offsets[i + 1] - offsets[i]);
     cells_ += cells;
     if (!cp) {
       CostModel cm = all_gpu_ ? CostModel{1.0, 200.0, 2400.0} : CostModel{1.0, 4.0, 64.0};
-      bounds = partition_ == "even" ? partition_even(n, p) : partition_by_cost(len.data(), n, L1, p, cm);
+      bounds = partition_ == "even" ? partition_even(n, p) : partition_by_cost_offsets(offsets, n, L1, p, cm);
     }
   }
   if (!cp) bcast_bytes(bounds.data(), sizeof(int64_t) * (p + 1), kRoot, ctx_.world);
@@ -395,7 +391,9 @@ void Job::batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, bool cp) {
   fault_.at("distribute", ctx_.rank);
   win->fence();
   pt_.end();
+  pt_.begin("bounds");
   const std::vector<int64_t> bounds = make_bounds(ctx_.rank == kRoot ? w_offs : nullptr, n, cp);
+  pt_.end();
   pt_.begin("compute");
   fault_.at("compute", ctx_.rank);
   Stopwatch sw;
@@ -435,6 +433,9 @@ void Job::batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, bool cp) {
   }
   compute_ms_ += sw.total_ms();
   print(w_res, n, 0);
+  pt_.begin("release");
+  win.reset();  // collective: unmaps the node-shared window
+  pt_.end();
 }
 
 void Job::batch_mpi(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds, bool cp) {

@@ -27,6 +27,9 @@ double record_cost(int64_t L1, int64_t L2, const CostModel& m);
 // Returns parts+1 boundaries b[0]=0 <= ... <= b[parts]=N; rank r owns records [b[r], b[r+1]).
 std::vector<int64_t> partition_by_cost(const int64_t* lengths, int64_t n, int64_t L1, int parts,
                                        const CostModel& m = {});
+// The same split from CSR offsets (record i = [offsets[i], offsets[i+1])), without a lengths copy.
+std::vector<int64_t> partition_by_cost_offsets(const int64_t* offsets, int64_t n, int64_t L1, int parts,
+                                               const CostModel& m = {});
 std::vector<int64_t> partition_batch(const RecordBatch& batch, int64_t L1, int parts, const CostModel& m = {});
 
 // Equal-count split (reference-like but correct for any p).

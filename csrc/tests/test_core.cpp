@@ -119,6 +119,28 @@ void test_partition() {
   }
   auto z = partition_by_cost(nullptr, 0, 10, 4);
   CHECK(z.size() == 5 && z.back() == 0);
+  // large batches take the chunked OpenMP path: same splits as one serial prefix scan (+-1 for rounding)
+  std::mt19937 rng(5);
+  const int64_t n = 3000000, L1 = 1500;
+  std::vector<int64_t> big(static_cast<size_t>(n)), offs(static_cast<size_t>(n) + 1, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    big[i] = 1 + static_cast<int64_t>(rng() % (i % 1000 == 0 ? 1400 : 30));
+    offs[i + 1] = offs[i] + big[i];
+  }
+  const CostModel cm{1.0, 200.0, 2400.0};
+  std::vector<double> prefix(static_cast<size_t>(n) + 1, 0.0);
+  for (int64_t i = 0; i < n; ++i) prefix[i + 1] = prefix[i] + record_cost(L1, big[i], cm);
+  for (int p : {2, 3, 8, 13}) {
+    auto b1 = partition_by_cost(big.data(), n, L1, p, cm);
+    auto b2 = partition_by_cost_offsets(offs.data(), n, L1, p, cm);
+    CHECK(b1 == b2);
+    for (int r = 1; r < p; ++r) {
+      const double target = prefix[n] * r / p;
+      int64_t i = std::lower_bound(prefix.begin(), prefix.end(), target) - prefix.begin();
+      if (i > 0 && (target - prefix[i - 1]) < (prefix[std::min(i, n)] - target)) --i;
+      CHECK(std::llabs(b1[r] - i) <= 1);
+    }
+  }
 }
 
 void test_keys() {
