@@ -58,6 +58,8 @@ const char* kUsage =
     "  --batch-chars=C             streaming mode: also cap a batch at C letters\n"
     "  --skip-records=S            start at record #S (resume a partially printed run)\n"
     "  --input=PATH                read PATH instead of stdin\n"
+    "  --output=PATH               root writes the result lines to PATH (in parallel) instead of stdout,\n"
+    "                              which mpiexec's proxies forward through a pipe\n"
     "  --timing                    per-phase JSON on stderr (root)\n"
     "  --strict-limits             enforce |Seq1|<=3000, |Seq2|<=2000 (PDF p.5-6)\n"
     "  --max-l1=L --max-l2=L       explicit length limits (0 = unlimited)\n"
@@ -72,7 +74,7 @@ const char* kUsage =
 
 const std::vector<std::string> kKnown = {
     "backend", "gpu-min-cells", "transport", "semantics", "partition", "batch-records", "batch-chars", "skip-records", "input",
-    "timing", "strict-limits", "max-l1", "max-l2", "device", "device-map", "pin-window", "chunk-records",
+    "output", "timing", "strict-limits", "max-l1", "max-l2", "device", "device-map", "pin-window", "chunk-records",
     "chunk-bytes", "threads", "log-level", "inject-fault", "help"};
 
 struct Header {
@@ -250,6 +252,7 @@ class Job {
   int64_t cells_ = 0, chars_ = 0, records_ = 0, batches_ = 0;
   int64_t first_index_ = 0;      // global index of the current batch's first record
   uvector<char> text_;                 // root: the input (kept for deferred parsing)
+  FILE* out_ = stdout;                 // root: --output file, else stdout
   std::unique_ptr<BulkParser> parser_;  // root: pass 1 done, letters encoded straight into the window
   std::vector<Result> results_;  // root: results of the current batch (mpi/rccl transports)
 };
@@ -305,7 +308,7 @@ void Job::setup_engine(int64_t cells) {
 void Job::print(const Result* r, int64_t n, int64_t first_index) {
   if (ctx_.rank != kRoot) return;
   pt_.begin("print");
-  write_results(stdout, r, n, first_index_ + first_index);
+  write_results(out_, r, n, first_index_ + first_index);
   pt_.end();
 }
 
@@ -583,6 +586,11 @@ int Job::run() {
       fault_.at("parse", ctx_.rank);
       const std::string path = flags_.get("input", "");
       if (!path.empty() && !(in = std::fopen(path.c_str(), "rb"))) throw Error("cannot open --input " + path);
+      const std::string opath = flags_.get("output", "");
+      if (!opath.empty() && !(out_ = std::fopen(opath.c_str(), "wb"))) {
+        out_ = stdout;
+        throw Error("cannot open --output " + opath);
+      }
       Weights w{};
       if (streaming) {
         reader = std::make_unique<StreamReader>(in, po);
@@ -697,6 +705,11 @@ int Job::run() {
     }
   }
   if (in != stdin && in) std::fclose(in);
+  if (out_ != stdout && std::fclose(out_) != 0 && rc == 0) {
+    std::fprintf(stderr, "error while writing --output\n");
+    rc = 1;
+  }
+  out_ = stdout;
   total_.stop();
   report(h);
   MPI_Barrier(ctx_.world);

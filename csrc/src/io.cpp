@@ -1,5 +1,6 @@
 #include "moc/io.hpp"
 
+#include <fcntl.h>
 #include <omp.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -472,7 +473,10 @@ void write_results(FILE* f, const Result* results, int64_t n, int64_t first_inde
   const int fd = fileno(f);
   struct stat st;
   off_t file_pos = -1;
-  if (nthreads > 1 && fstat(fd, &st) == 0 && S_ISREG(st.st_mode)) file_pos = lseek(fd, 0, SEEK_CUR);
+  // (not with O_APPEND: Linux pwrite then ignores the offset and the parts would land in completion order)
+  const int fl = fcntl(fd, F_GETFL);
+  if (nthreads > 1 && fl >= 0 && !(fl & O_APPEND) && fstat(fd, &st) == 0 && S_ISREG(st.st_mode))
+    file_pos = lseek(fd, 0, SEEK_CUR);
   std::vector<uvector<char>> parts(static_cast<size_t>(nthreads));
   std::vector<size_t> used(static_cast<size_t>(nthreads) + 1);
   bool write_error = false;

@@ -123,6 +123,40 @@ def test_input_flag_large_file(tmp_path):
         assert r.stdout.decode() == want
 
 
+@pytest.mark.parametrize("mode", ["w", "a"])
+def test_output_to_regular_file(tmp_path, mode):
+    # stdout a regular file: the writer's parallel pwrite path (at the current offset, after text already
+    # in the file) — or, opened O_APPEND (`>>`), the ordered path; both must give the rows in order
+    import os
+
+    from conftest import ROOT
+    from mpi_openmp_cuda_amd import format_results, make_synthetic, search_cpu
+
+    prob = make_synthetic("input6", 140000, seed=9)
+    path = tmp_path / "in.txt"
+    path.write_text(prob.to_text())
+    want = format_results(search_cpu(prob))
+    out = tmp_path / "out.txt"
+    out.write_text("previous line\n")
+    with open(out, mode) as f:
+        if mode == "w":
+            f.write("header\n")
+            f.flush()
+        env = dict(os.environ, OMP_NUM_THREADS="4")
+        # singleton MPI start (no mpiexec: its proxies would turn stdout into a pipe)
+        r = subprocess.run([os.path.join(ROOT, "final"), "--backend=cpu", f"--input={path}"],
+                           stdin=subprocess.DEVNULL, stdout=f, stderr=subprocess.PIPE, env=env, timeout=120)
+    assert r.returncode == 0, r.stderr.decode()
+    prefix = "header\n" if mode == "w" else "previous line\n"
+    assert out.read_text() == prefix + want
+    # --output: the root writes the file itself, also under mpiexec
+    out2 = tmp_path / "out2.txt"
+    r = run_final(["--backend=cpu", f"--input={path}", f"--output={out2}"], stdin_bytes=b"", np_=2,
+                  env={"OMP_NUM_THREADS": "4"})
+    assert r.returncode == 0 and r.stdout == b"", r.stderr.decode()
+    assert out2.read_text() == want
+
+
 def test_streaming_parse_error_mid_stream():
     text = b"1 2 3 4\nABCDEFG\n5\nABC\nABD\nAB1\nAC\nAD\n"
     r = run_final(["--backend=cpu", "--batch-records=2"], stdin_bytes=text, np_=2)
