@@ -64,7 +64,7 @@ Problem parse_problem(const char* data, size_t len, const ParseOptions& opt = {}
 // encoding them (`--skip-records`, resuming a partially printed run).
 class StreamReader {
  public:
-  explicit StreamReader(FILE* f, const ParseOptions& opt = {}, size_t block_bytes = size_t{8} << 20);
+  explicit StreamReader(FILE* f, const ParseOptions& opt = {}, size_t block_bytes = size_t{32} << 20);
   const Weights& weights() const { return weights_; }
   const std::vector<uint8_t>& seq1() const { return seq1_; }
   int64_t count() const { return count_; }         // number_of_sequences from the header

@@ -318,32 +318,168 @@ int64_t StreamReader::skip(int64_t records) {
 }
 
 int64_t StreamReader::next_batch(int64_t max_records, RecordBatch& out, int64_t max_chars) {
+  // Region by region: the loaded buffer's complete tokens are split into per-thread chunks at
+  // whitespace, counted (tokens, letters) in parallel, cut where the batch ends (max_records, or the first
+  // record that starts with >= max_chars letters already in the batch), then encoded in parallel. Errors
+  // name the smallest offending record, the length check first, as a record-by-record scan would.
   out.codes.clear();
   out.offsets.assign(1, 0);
-  const char *b, *e;
+  const int64_t want = std::min(max_records, count_ - next_);
   int64_t got = 0, max_len = 0;
-  while (got < max_records && next_ < count_) {
+  auto missing = [&] {
+    return Error("expected " + std::to_string(count_) + " Seq2 records, found only " + std::to_string(next_));
+  };
+  while (got < want) {
     if (got > 0 && static_cast<int64_t>(out.codes.size()) >= max_chars) break;
-    if (!token(b, e))
-      throw Error("expected " + std::to_string(count_) + " Seq2 records, found only " + std::to_string(next_));
-    const int64_t L = e - b;
-    if (l2_cap_ > 0 && L > l2_cap_)
-      throw Error("Seq2 record #" + std::to_string(next_) + " has " + std::to_string(L) + " letters, limit is " +
-                  std::to_string(l2_cap_));
-    const size_t at = out.codes.size();
-    out.codes.resize(at + static_cast<size_t>(L));
-    uint8_t* dst = out.codes.data() + at;
-    int bad = 0;
-    for (int64_t j = 0; j < L; ++j) {
-      const int c = letter_code(static_cast<unsigned char>(b[j]));
-      bad |= (c == 0);
-      dst[j] = static_cast<uint8_t>(c);
+    // ---- the region [pos_, cut) of complete tokens (refill / grow until there is one, or EOF)
+    while (pos_ < len_ && is_space(static_cast<unsigned char>(buf_[pos_]))) ++pos_;
+    size_t cut = 0;
+    while (true) {
+      if (pos_ < len_) {
+        if (eof_) {
+          cut = len_;
+        } else {
+          cut = len_;
+          while (cut > pos_ && !is_space(static_cast<unsigned char>(buf_[cut - 1]))) --cut;
+        }
+        if (cut > pos_) break;
+      } else if (eof_) {
+        throw missing();
+      }
+      const size_t keep = len_ - pos_;  // a partial token (or nothing) moves to the front
+      if (pos_ > 0 && keep) std::memmove(buf_.data(), buf_.data() + pos_, keep);
+      if (keep == buf_.size()) buf_.resize(buf_.size() * 2);
+      pos_ = 0;
+      const size_t rd = std::fread(buf_.data() + keep, 1, buf_.size() - keep, f_);
+      len_ = keep + rd;
+      if (len_ < buf_.size()) {
+        if (std::ferror(f_)) throw Error("error while reading input stream");
+        eof_ = true;
+      }
+      while (pos_ < len_ && is_space(static_cast<unsigned char>(buf_[pos_]))) ++pos_;
     }
-    if (bad) throw Error("Seq2 record #" + std::to_string(next_) + " contains a non-letter character");
-    out.offsets.push_back(static_cast<int64_t>(out.codes.size()));
-    max_len = std::max(max_len, L);
-    ++next_;
-    ++got;
+    const unsigned char* ua = reinterpret_cast<const unsigned char*>(buf_.data());
+    const size_t rlen = cut - pos_;
+    const int nt = rlen > (size_t{1} << 20) ? std::max(1, omp_get_max_threads()) : 1;
+    std::vector<size_t> cb(static_cast<size_t>(nt) + 1);
+    for (int t = 0; t <= nt; ++t) cb[t] = pos_ + rlen * static_cast<size_t>(t) / nt;
+    for (int t = 1; t < nt; ++t) {  // chunk starts move forward past the token they cut
+      size_t x = cb[t];
+      while (x < cut && !is_space(ua[x - 1])) ++x;
+      cb[t] = std::max(x, cb[t - 1]);
+    }
+    cb[nt] = cut;
+    std::vector<int64_t> ctok(static_cast<size_t>(nt) + 1, 0), cchr(static_cast<size_t>(nt) + 1, 0);
+#pragma omp parallel for num_threads(nt) schedule(static, 1)
+    for (int t = 0; t < nt; ++t) {
+      int64_t k = 0, c = 0;
+      if (cb[t] < cb[t + 1]) {
+        k = c = is_space(ua[cb[t]]) ? 0 : 1;
+        for (size_t i = cb[t] + 1; i < cb[t + 1]; ++i) {
+          const unsigned lt = !is_space(ua[i]);
+          k += lt & is_space(ua[i - 1]);
+          c += lt;
+        }
+      }
+      ctok[t + 1] = k;
+      cchr[t + 1] = c;
+    }
+    // ---- where this batch ends inside the region: whole chunks, then a token scan of the last one
+    const int64_t base_chars = static_cast<int64_t>(out.codes.size());
+    int64_t tk = 0, ch = 0;  // tokens / letters taken from the region so far
+    int last = nt;           // chunks [0, last) are taken whole
+    size_t end_pos = cut;
+    for (int t = 0; t < nt; ++t) {
+      // whole chunk: it stays within the record limit, and even its last token (which starts at most
+      // one letter before the chunk's end) starts below max_chars
+      const bool whole = ctok[t + 1] == 0 ||
+                         (got + tk + ctok[t + 1] <= want && base_chars + ch + cchr[t + 1] - 1 < max_chars);
+      if (whole) {
+        tk += ctok[t + 1];
+        ch += cchr[t + 1];
+        continue;
+      }
+      // token scan of chunk t
+      size_t i = cb[t];
+      const size_t e = cb[t + 1];
+      while (got + tk < want) {
+        while (i < e && is_space(ua[i])) ++i;
+        if (i >= e) break;
+        if (got + tk > 0 && base_chars + ch >= max_chars) break;
+        size_t j = i;
+        while (j < e && !is_space(ua[j])) ++j;
+        ++tk;
+        ch += static_cast<int64_t>(j - i);
+        i = j;
+      }
+      end_pos = i;
+      last = t;
+      break;
+    }
+    if (last < nt) cb[last + 1] = end_pos;  // chunk `last` is encoded up to the cut; later ones not at all
+    const int nenc = last < nt ? last + 1 : nt;
+    // per-chunk prefix of the (possibly truncated) counts
+    if (last < nt) {
+      int64_t k0 = 0, c0 = 0;
+      for (int t = 0; t < last; ++t) {
+        k0 += ctok[t + 1];
+        c0 += cchr[t + 1];
+      }
+      ctok[last + 1] = tk - k0;
+      cchr[last + 1] = ch - c0;
+    }
+    for (int t = 0; t < nenc; ++t) {
+      ctok[t + 1] += ctok[t];
+      cchr[t + 1] += cchr[t];
+    }
+    // ---- encode (parallel), checking lengths and letters
+    const size_t at_tok = out.offsets.size() - 1;
+    out.codes.resize(static_cast<size_t>(base_chars + ch));
+    out.offsets.resize(at_tok + 1 + static_cast<size_t>(tk));
+    uint8_t* codes = out.codes.data() + base_chars;
+    int64_t* offs = out.offsets.data() + at_tok;
+    std::vector<int64_t> err_tok(static_cast<size_t>(nenc), -1), err_len(static_cast<size_t>(nenc), 0),
+        mx(static_cast<size_t>(nenc), 0);
+    std::vector<int> err_kind(static_cast<size_t>(nenc), 0);
+#pragma omp parallel for num_threads(nt) schedule(static, 1)
+    for (int t = 0; t < nenc; ++t) {
+      int64_t k = ctok[t], pos = cchr[t], m = 0;
+      size_t i = cb[t];
+      const size_t e = cb[t + 1];
+      while (i < e) {
+        while (i < e && is_space(ua[i])) ++i;
+        if (i >= e) break;
+        const int64_t p0 = pos;
+        unsigned bad = 0;
+        while (i < e && !is_space(ua[i])) {
+          const uint8_t code = kCodeOf[ua[i++]];
+          bad |= (code == 0);
+          codes[pos++] = code;
+        }
+        const int64_t L = pos - p0;
+        if (err_tok[t] < 0 && ((l2_cap_ > 0 && L > l2_cap_) || bad)) {
+          err_tok[t] = k;
+          err_kind[t] = (l2_cap_ > 0 && L > l2_cap_) ? 1 : 2;
+          err_len[t] = L;
+        }
+        m = std::max(m, L);
+        offs[++k] = base_chars + pos;
+      }
+      mx[t] = m;
+    }
+    for (int t = 0; t < nenc; ++t) {
+      if (err_tok[t] >= 0) {
+        const int64_t rec = next_ + err_tok[t];
+        if (err_kind[t] == 1)
+          throw Error("Seq2 record #" + std::to_string(rec) + " has " + std::to_string(err_len[t]) +
+                      " letters, limit is " + std::to_string(l2_cap_));
+        throw Error("Seq2 record #" + std::to_string(rec) + " contains a non-letter character");
+      }
+      max_len = std::max(max_len, mx[t]);
+    }
+    pos_ = end_pos;
+    next_ += tk;
+    got += tk;
   }
   if (got) validate_score_range(weights_, std::max<int64_t>(max_len, 1));
   return got;

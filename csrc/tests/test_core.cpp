@@ -106,6 +106,75 @@ void test_stream_reader() {
   CHECK(rb.next_batch(1, x) == 1);
   CHECK(throws([&] { rb.next_batch(5, x); }, "record #1"));
   std::fclose(g);
+
+  // multi-MB regions take the chunked OpenMP path: batches (record and letter caps, buffers smaller and
+  // larger than a batch) must concatenate to exactly what the bulk parser produces
+  std::mt19937 rng(3);
+  std::string big = "5 1 2 3\nHELLOWORLD\n150000\n";
+  const char* ws[5] = {"\n", " ", "\r\n", "  \t", "\n\n"};
+  std::vector<size_t> rec_start;
+  for (int i = 0; i < 150000; ++i) {
+    rec_start.push_back(big.size());
+    const int L = 1 + static_cast<int>(rng() % (i % 5000 == 0 ? 900 : 40));
+    for (int j = 0; j < L; ++j) big += static_cast<char>((rng() % 2 ? 'A' : 'a') + rng() % 26);
+    big += ws[rng() % 5];
+  }
+  big += "EXTRA TOKENS\n";
+  const Problem ref = parse_problem(big.data(), big.size());
+  for (const auto& cfg : std::vector<std::array<int64_t, 3>>{{int64_t{1} << 20, 1000, INT64_MAX},
+                                                             {int64_t{4} << 20, 77777, INT64_MAX},
+                                                             {int64_t{4} << 20, INT64_MAX, 500000},
+                                                             {int64_t{2} << 20, 150000, 2000000},
+                                                             {int64_t{8} << 20, INT64_MAX, INT64_MAX}}) {
+    FILE* h = fmemopen(big.data(), big.size(), "rb");
+    StreamReader sr(h, {}, static_cast<size_t>(cfg[0]));
+    std::vector<uint8_t> codes;
+    std::vector<int64_t> offs = {0};
+    RecordBatch bb;
+    int64_t batches = 0;
+    bool caps_ok = true;
+    while (int64_t k = sr.next_batch(cfg[1], bb, cfg[2])) {
+      ++batches;
+      caps_ok &= k <= cfg[1] && bb.size() == k;
+      // the letter cap: every record but the first starts below it
+      caps_ok &= bb.offsets[k - 1] < cfg[2] || k == 1;
+      for (int64_t r = 0; r < k; ++r) offs.push_back(static_cast<int64_t>(codes.size()) + bb.offsets[r + 1]);
+      codes.insert(codes.end(), bb.codes.begin(), bb.codes.end());
+    }
+    CHECK(caps_ok && batches >= 1);
+    CHECK(std::equal(offs.begin(), offs.end(), ref.seq2.offsets.begin(), ref.seq2.offsets.end()) &&
+          std::equal(codes.begin(), codes.end(), ref.seq2.codes.begin(), ref.seq2.codes.end()));
+    std::fclose(h);
+  }
+  // a bad letter / an over-long record deep inside a chunked region: the smallest record is named,
+  // and a length-limit violation in an earlier record wins over a later bad letter
+  auto run_all = [&](std::string& text, int64_t cap) {
+    FILE* h = fmemopen(text.data(), text.size(), "rb");
+    ParseOptions o;
+    o.max_l2 = cap;
+    StreamReader sr(h, o, size_t{2} << 20);
+    RecordBatch bb;
+    std::string msg;
+    try {
+      while (sr.next_batch(40000, bb)) {
+      }
+    } catch (const Error& e) {
+      msg = e.what();
+    }
+    std::fclose(h);
+    return msg;
+  };
+  std::string bad2 = big;
+  bad2[rec_start[123457]] = '7';
+  CHECK(run_all(bad2, 0).find("record #123457 contains a non-letter") != std::string::npos);
+  bad2[rec_start[70001]] = '#';
+  CHECK(run_all(bad2, 0).find("record #70001 contains a non-letter") != std::string::npos);
+  // records i % 5000 == 0 may be up to 900 letters long: with a cap of 45 the first such record over it
+  int64_t first_long = -1;
+  for (int64_t r = 0; r < 150000 && first_long < 0; ++r)
+    if (ref.seq2.offsets[r + 1] - ref.seq2.offsets[r] > 45) first_long = r;
+  CHECK(first_long >= 0);
+  CHECK(run_all(big, 45).find("record #" + std::to_string(first_long) + " has") != std::string::npos);
 }
 
 void test_partition() {
