@@ -19,6 +19,7 @@
 //   6. Every rank runs its engine (HIP kernels, or the OpenMP CPU engine), root prints in order.
 // Any error on any rank -> message + MPI_Abort (reference: exit(1) without abort, peers hang, B11).
 #include <dlfcn.h>
+#include <sys/stat.h>
 #include <omp.h>
 #include <unistd.h>
 
@@ -51,6 +52,8 @@ const char* kUsage =
     "usage: mpiexec -np N ./final [options] < input.txt\n"
     "  --backend=auto|hip|cpu      compute engine (auto: hip when a GPU is visible and the job has\n"
     "                              >= --gpu-min-cells cells per rank, default 3e8; else the OpenMP engine)\n"
+    "  --gpu-prewarm-bytes=B       start the HIP runtime during the parse when the input file has >= B bytes\n"
+    "                              (default 64 MiB; 0 = never)\n"
     "  --transport=auto|shm|rccl|mpi   record distribution (auto: shm on one node, else rccl/mpi)\n"
     "  --semantics=reference|spec  candidate set (spec adds the un-mutated final offset, bug B8)\n"
     "  --partition=cost|even|offsets   rank decomposition (offsets: split every record's offset range)\n"
@@ -73,7 +76,7 @@ const char* kUsage =
     "every flag can also be given as environment variable MOC_<FLAG> (e.g. MOC_BACKEND=cpu)\n";
 
 const std::vector<std::string> kKnown = {
-    "backend", "gpu-min-cells", "transport", "semantics", "partition", "batch-records", "batch-chars", "skip-records", "input",
+    "backend", "gpu-min-cells", "gpu-prewarm-bytes", "transport", "semantics", "partition", "batch-records", "batch-chars", "skip-records", "input",
     "output", "timing", "strict-limits", "max-l1", "max-l2", "device", "device-map", "pin-window", "chunk-records",
     "chunk-bytes", "threads", "log-level", "inject-fault", "help"};
 
@@ -255,9 +258,11 @@ class Job {
   FILE* out_ = stdout;                 // root: --output file, else stdout
   std::unique_ptr<BulkParser> parser_;  // root: pass 1 done, letters encoded straight into the window
   std::vector<Result> results_;  // root: results of the current batch (mpi/rccl transports)
+  std::future<void> prewarm_;     // HIP runtime start-up overlapped with the parse (large inputs)
 };
 
 void Job::setup_engine(int64_t cells) {
+  if (prewarm_.valid()) prewarm_.get();
   const int threads = static_cast<int>(flags_.get_int("threads", 0));
   std::string backend = to_lower(flags_.get("backend", "auto"));
   if (backend != "auto" && backend != "hip" && backend != "cpu") throw Error("--backend must be auto|hip|cpu");
@@ -572,6 +577,21 @@ int Job::run() {
   if (threads <= 0 && !std::getenv("OMP_NUM_THREADS")) threads = std::max(1, omp_get_num_procs() / ctx_.local_size);
   if (threads > 0) omp_set_num_threads(threads);
   total_.start();
+
+  // ---- a large input (a regular file of >= --gpu-prewarm-bytes) will run on the GPU: every rank brings the
+  // HIP runtime up on a helper thread while the root reads and parses, instead of after the header bcast
+  {
+    int64_t hint = 0;
+    if (ctx_.rank == kRoot && to_lower(flags_.get("backend", "auto")) != "cpu") {
+      const std::string path = flags_.get("input", "");
+      struct stat st {};
+      const int rc = path.empty() ? fstat(STDIN_FILENO, &st) : stat(path.c_str(), &st);
+      const int64_t min_bytes = flags_.get_int("gpu-prewarm-bytes", int64_t{64} << 20);
+      hint = rc == 0 && S_ISREG(st.st_mode) && min_bytes > 0 && st.st_size >= min_bytes;
+    }
+    bcast_bytes(&hint, sizeof hint, kRoot, ctx_.world);
+    if (hint) prewarm_ = std::async(std::launch::async, [] { (void)gpu_device_count(); });
+  }
 
   // ---- root opens the input; parses it whole (bulk) or just its header (streaming)
   Header h{};

@@ -1,5 +1,6 @@
 #include "moc/comm.hpp"
 
+#include <sys/mman.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -133,6 +134,20 @@ void gatherv_bytes(const void* sendbuf, int64_t count, void* recvbuf, const std:
 
 // ------------------------------------------------------------------------------------------------
 SharedWindow::SharedWindow(const MpiContext& ctx, int64_t bytes) : comm_(ctx.node) {
+  if (ctx.local_size == 1) {
+    constexpr size_t kHuge = size_t{2} << 20;
+    const size_t want = (static_cast<size_t>(std::max<int64_t>(bytes, 8)) + kHuge - 1) & ~(kHuge - 1);
+    map_bytes_ = want + kHuge;  // slack to start on a 2 MiB boundary
+    map_ = mmap(nullptr, map_bytes_, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    if (map_ == MAP_FAILED) {
+      map_ = nullptr;
+      throw Error("SharedWindow: cannot map " + std::to_string(map_bytes_) + " bytes");
+    }
+    base_ = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(map_) + kHuge - 1) & ~(kHuge - 1));
+    (void)madvise(base_, want, MADV_HUGEPAGE);  // advisory: 4 KiB pages if THP is off
+    bytes_ = bytes;
+    return;
+  }
   const MPI_Aint mine = ctx.local_rank == 0 ? static_cast<MPI_Aint>(std::max<int64_t>(bytes, 8)) : 0;
   void* base = nullptr;
   MOC_MPI_CHECK(MPI_Win_allocate_shared(mine, 1, MPI_INFO_NULL, comm_, &base, &win_));
@@ -146,6 +161,10 @@ SharedWindow::SharedWindow(const MpiContext& ctx, int64_t bytes) : comm_(ctx.nod
 }
 
 SharedWindow::~SharedWindow() {
+  if (map_) {
+    munmap(map_, map_bytes_);
+    return;
+  }
   // Never enter a collective while an exception unwinds: peers may be blocked elsewhere and the caller
   // is about to MPI_Abort (freeing here would deadlock the failing rank).
   if (std::uncaught_exceptions() > 0) return;
@@ -156,6 +175,7 @@ SharedWindow::~SharedWindow() {
 }
 
 void SharedWindow::fence() const {
+  if (map_) return;  // one rank on the node
   MOC_MPI_CHECK(MPI_Win_sync(win_));
   MOC_MPI_CHECK(MPI_Barrier(comm_));
   MOC_MPI_CHECK(MPI_Win_sync(win_));

@@ -123,6 +123,31 @@ def test_input_flag_large_file(tmp_path):
         assert r.stdout.decode() == want
 
 
+
+def test_gpu_prewarm_hint(tmp_path):
+    # --gpu-prewarm-bytes: every rank starts the HIP runtime on a helper thread during the parse; with no
+    # usable GPU (or an auto backend that then picks the OpenMP engine) the output is unchanged
+    from mpi_openmp_cuda_amd import format_results, make_synthetic, search_cpu
+
+    prob = make_synthetic("input6", 20000, seed=5)
+    path = tmp_path / "in.txt"
+    path.write_text(prob.to_text())
+    want = format_results(search_cpu(prob))
+    for extra in ([f"--input={path}"], ["--batch-records=3000", f"--input={path}"]):
+        r = run_final(["--gpu-prewarm-bytes=1", "--gpu-min-cells=1000000000000"] + extra, stdin_bytes=b"", np_=2)
+        assert r.returncode == 0, r.stderr.decode()
+        assert r.stdout.decode() == want
+    # the hint from a redirected stdin (a regular file; singleton start, as mpiexec's proxy forwards a pipe)
+    import os
+
+    from conftest import ROOT
+
+    with open(path, "rb") as f:
+        r = subprocess.run([os.path.join(ROOT, "final"), "--gpu-prewarm-bytes=1", "--gpu-min-cells=1000000000000"],
+                           stdin=f, capture_output=True, timeout=120)
+    assert r.returncode == 0, r.stderr.decode()
+    assert r.stdout.decode() == want
+
 @pytest.mark.parametrize("mode", ["w", "a"])
 def test_output_to_regular_file(tmp_path, mode):
     # stdout a regular file: the writer's parallel pwrite path (at the current offset, after text already

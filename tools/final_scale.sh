@@ -6,7 +6,7 @@ F=/tmp/moc_big6.txt
 timeout -k 10 300 python3 tools/gen_synthetic.py --shape input6 --records ${RECORDS:-134217728} --out $F
 # "--output": the root writes the file itself (parallel pwrite) instead of stdout, which mpiexec's proxy
 # forwards through a pipe
-for mode in "" "--output=/tmp/moc_big6.out" "--pin-window=0" "--batch-records=16777216"; do
+for mode in "" "--output=/tmp/moc_big6.out" "--output=/tmp/moc_big6.out --gpu-prewarm-bytes=0" "--batch-records=16777216"; do
   rm -f /tmp/moc_big6.out  # untimed: dropping the previous 4.6 GB output
   so=/tmp/moc_big6.out
   case "$mode" in --output=*) so=/dev/null;; esac
