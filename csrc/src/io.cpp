@@ -2,6 +2,7 @@
 
 #include <fcntl.h>
 #include <omp.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -61,8 +62,59 @@ uvector<char> read_stream(FILE* f) {
     // regular file: one allocation of the remaining size (+1 to detect growth), one read
     const long pos = std::ftell(f);
     const size_t want = static_cast<size_t>(st.st_size) - static_cast<size_t>(pos > 0 ? pos : 0) + 1;
-    buf.resize(want);
-    len = std::fread(buf.data(), 1, want, f);
+    buf.resize(want);  // not touched yet (default-init): the advice below applies to every page
+    if (want > (size_t{64} << 20) && pos >= 0) {
+      // large file: 2 MiB pages for the buffer, and the copy out of the page cache split over the OpenMP
+      // threads (one fread is a single-threaded 4 KiB-page-faulting memcpy of the whole file)
+      constexpr uintptr_t kHuge = uintptr_t{2} << 20;
+      const uintptr_t lo = (reinterpret_cast<uintptr_t>(buf.data()) + kHuge - 1) & ~(kHuge - 1);
+      const uintptr_t hi = (reinterpret_cast<uintptr_t>(buf.data()) + want) & ~(kHuge - 1);
+      if (hi > lo) (void)madvise(reinterpret_cast<void*>(lo), hi - lo, MADV_HUGEPAGE);
+      const int fd = fileno(f);
+      const size_t body = want - 1;
+      constexpr size_t kChunk = size_t{16} << 20;
+      const int64_t nchunks = static_cast<int64_t>((body + kChunk - 1) / kChunk);
+      std::vector<size_t> got(static_cast<size_t>(nchunks), 0);
+      int failed = 0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(| : failed)
+      for (int64_t c = 0; c < nchunks; ++c) {
+        const size_t b = static_cast<size_t>(c) * kChunk, e = std::min(body, b + kChunk);
+        size_t at = b;
+        while (at < e) {
+          const ssize_t r = pread(fd, buf.data() + at, e - at, static_cast<off_t>(pos) + static_cast<off_t>(at));
+          if (r < 0 && errno == EINTR) continue;
+          if (r < 0) {
+            failed = 1;
+            break;
+          }
+          if (r == 0) break;
+          at += static_cast<size_t>(r);
+        }
+        got[static_cast<size_t>(c)] = at - b;
+      }
+      if (failed) throw Error("error while reading input stream");
+      // the file as it was at fstat time; a short chunk means it shrank: keep the contiguous prefix
+      for (int64_t c = 0; c < nchunks; ++c) {
+        len += got[static_cast<size_t>(c)];
+        if (got[static_cast<size_t>(c)] < std::min(body, static_cast<size_t>(c + 1) * kChunk) - static_cast<size_t>(c) * kChunk)
+          break;
+      }
+      (void)std::fseek(f, static_cast<long>(pos) + static_cast<long>(len), SEEK_SET);
+      if (len == body) {
+        // a file that grew after fstat continues through the stream loop below
+        const size_t more = std::fread(buf.data() + len, 1, 1, f);
+        len += more;
+        if (!more) {
+          buf.resize(len);
+          return buf;
+        }
+      } else {
+        buf.resize(len);
+        return buf;
+      }
+    } else {
+      len = std::fread(buf.data(), 1, want, f);
+    }
     if (len < want) {
       if (std::ferror(f)) throw Error("error while reading input stream");
       buf.resize(len);

@@ -244,3 +244,27 @@ def test_record_error_after_header(transport, np_):
     ok = b"1 2 3 4\nABCDEFG\n3\nAB\nABCD\nAC\n"
     r = run_final(["--backend=cpu", f"--transport={transport}", "--max-l2=2"], stdin_bytes=ok, np_=np_)
     assert r.returncode == 1 and b"record #1 has 4 letters, limit is 2" in r.stderr
+
+
+def test_large_file_parallel_read(tmp_path):
+    # an input file over 64 MiB is read with parallel preads into a huge-page buffer: the bulk path must
+    # agree with the streaming reader (an independent tokeniser) line for line
+    import os
+    import sys
+
+    from conftest import ROOT
+
+    path = tmp_path / "big.txt"
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_synthetic.py"), "--shape", "input6",
+                    "--records", "7500000", "--seed", "11", "--out", str(path)], check=True, timeout=300,
+                   capture_output=True)
+    assert path.stat().st_size > (64 << 20)
+    outs = []
+    for extra in ([], ["--batch-records=2000000"]):
+        out = tmp_path / f"out{len(outs)}.txt"
+        r = run_final(["--backend=cpu", f"--input={path}", f"--output={out}"] + extra, stdin_bytes=b"", np_=1,
+                      timeout=300)
+        assert r.returncode == 0, r.stderr.decode()
+        outs.append(out.read_bytes())
+    assert outs[0] == outs[1]
+    assert outs[0].count(b"\n") == 7500000
