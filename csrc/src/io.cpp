@@ -6,6 +6,8 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <emmintrin.h>
+
 #include <algorithm>
 #include <cerrno>
 #include <cstdlib>
@@ -227,6 +229,22 @@ BulkParser::BulkParser(const char* data, size_t len, const ParseOptions& opt) {
   }
 }
 
+namespace {
+// Letter codes of 16 input bytes ((c & 0x1F): 'A'/'a' -> 1 ... 'Z'/'z' -> 26), with bit masks of the
+// whitespace bytes (as is_space) and of the bytes that are letters.
+inline __m128i encode16(const unsigned char* src, unsigned& space_mask, unsigned& letter_mask) {
+  const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src));
+  const __m128i t = _mm_sub_epi8(v, _mm_set1_epi8(9));  // \t \n \v \f \r -> 0..4
+  const __m128i ws = _mm_or_si128(_mm_cmpeq_epi8(v, _mm_set1_epi8(' ')),
+                                  _mm_cmpeq_epi8(_mm_min_epu8(t, _mm_set1_epi8(4)), t));
+  const __m128i u = _mm_sub_epi8(_mm_and_si128(v, _mm_set1_epi8(static_cast<char>(0xDF))), _mm_set1_epi8('A'));
+  const __m128i letter = _mm_cmpeq_epi8(_mm_min_epu8(u, _mm_set1_epi8(25)), u);
+  space_mask = static_cast<unsigned>(_mm_movemask_epi8(ws));
+  letter_mask = static_cast<unsigned>(_mm_movemask_epi8(letter));
+  return _mm_and_si128(v, _mm_set1_epi8(0x1F));
+}
+}  // namespace
+
 void BulkParser::fill(uint8_t* codes, int64_t* offs) const {
   // pass 2: encode letters and record token ends (token by token; table lookups), tracking each
   // thread's longest record and first offending record for the checks below
@@ -243,12 +261,27 @@ void BulkParser::fill(uint8_t* codes, int64_t* offs) const {
     int64_t first_bad = -1, mx = 0, lt = -1, ll = 0;
     size_t i = start_[t];
     const size_t e = start_[t + 1];
+    // 16-byte SSE2 blocks wherever a full block can be read from the area and stored into `codes`
+    const size_t vec_in_end = area_len_ >= 16 ? area_len_ - 16 : 0;
+    // (this thread's part of `codes` only: a store past it would race with thread t+1's first records)
+    const int64_t vec_out_end = std::min(char_count_[t + 1], total_chars_) - 16;
     while (tok < n) {
       while (i < e && is_space(ua[i])) ++i;
       if (i >= e) break;
       const int64_t p0 = pos;
       unsigned bad = 0;
-      while (i < e && !is_space(ua[i])) {
+      while (i <= vec_in_end && pos <= vec_out_end) {
+        unsigned sp, ok;
+        const __m128i codes16 = encode16(ua + i, sp, ok);
+        _mm_storeu_si128(reinterpret_cast<__m128i*>(codes + pos), codes16);
+        // letters up to the first space (or the chunk end); a token of >= 16 letters takes another block
+        const size_t take = std::min<size_t>(sp ? static_cast<size_t>(__builtin_ctz(sp)) : 16, e - i);
+        bad |= ~ok & ((1u << take) - 1u);
+        i += take;
+        pos += static_cast<int64_t>(take);
+        if (take < 16) break;
+      }
+      while (i < e && !is_space(ua[i])) {  // tail: near the end of the area or of `codes`
         const uint8_t code = kCodeOf[ua[i++]];
         bad |= (code == 0);
         codes[pos++] = code;
