@@ -228,7 +228,7 @@ struct RankEngine {
 
 class Job {
  public:
-  Job(MpiContext& ctx, const Flags& flags) : ctx_(ctx), flags_(flags) {}
+  Job(MpiContext& ctx, const Flags& flags, BackgroundReleaser& rel) : ctx_(ctx), flags_(flags), rel_(rel) {}
   int run();
 
  private:
@@ -243,6 +243,7 @@ class Job {
 
   MpiContext& ctx_;
   const Flags& flags_;
+  BackgroundReleaser& rel_;  // large frees off the critical path (outlives the job: drained after finalize)
   FaultHook fault_;
   RankEngine eng_;
   int device_ = -1;
@@ -257,6 +258,8 @@ class Job {
   uvector<char> text_;                 // root: the input (kept for deferred parsing)
   FILE* out_ = stdout;                 // root: --output file, else stdout
   std::unique_ptr<BulkParser> parser_;  // root: pass 1 done, letters encoded straight into the window
+  std::shared_ptr<BulkParser> spent_parser_;     // root: filled into the window, freed while printing
+  std::shared_ptr<uvector<char>> spent_text_;
   std::vector<Result> results_;  // root: results of the current batch (mpi/rccl transports)
   std::future<void> prewarm_;     // HIP runtime start-up overlapped with the parse (large inputs)
 };
@@ -361,6 +364,7 @@ void Job::batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, bool cp) {
   const int64_t res_bytes = ((12 * n) + 7) & ~int64_t{7};
   pt_.begin("distribute");
   auto win = std::make_unique<SharedWindow>(ctx_, off_bytes + res_bytes + total_chars);
+  win->set_releaser(&rel_);
   int64_t* w_offs = reinterpret_cast<int64_t*>(win->base());
   Result* w_res = reinterpret_cast<Result*>(win->base() + off_bytes);
   uint8_t* w_codes = reinterpret_cast<uint8_t*>(win->base() + off_bytes + res_bytes);
@@ -374,7 +378,10 @@ void Job::batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, bool cp) {
         status = 1;
         error = e.what();
       }
-      parser_.reset();
+      // the input buffers (≈1 GB per 10^9 letters) are freed by the background releaser while the
+      // results print (not now: unmapping them while the engine page-locks the window slows both)
+      spent_parser_ = std::move(parser_);
+      spent_text_ = std::make_shared<uvector<char>>(std::move(text_));
       text_ = uvector<char>();
     } else {
       const int64_t* src_off = rb->offsets.data();
@@ -440,6 +447,14 @@ void Job::batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, bool cp) {
     pt_.end();
   }
   compute_ms_ += sw.total_ms();
+  // printing reads only the results: the input, offsets and letters go back to the OS while it runs
+  if (spent_parser_ || spent_text_)
+    rel_.defer([parser = std::move(spent_parser_), text = std::move(spent_text_)]() mutable {
+      parser.reset();
+      text.reset();
+    });
+  win->discard(0, off_bytes);
+  win->discard(off_bytes + res_bytes, total_chars);
   print(w_res, n, 0);
   pt_.begin("release");
   win.reset();  // collective: unmaps the node-shared window
@@ -739,6 +754,8 @@ int Job::run() {
 }  // namespace
 
 int main(int argc, char** argv) {
+  // declared before the MPI context: its queued unmaps overlap the job's teardown and MPI_Finalize
+  BackgroundReleaser releaser;
   MpiContext ctx(&argc, &argv);
   int rc = 0;
   try {
@@ -752,7 +769,7 @@ int main(int argc, char** argv) {
       if (ctx.rank == kRoot) std::fprintf(stderr, "unknown flag --%s\n%s", unknown[0].c_str(), kUsage);
       return 2;
     }
-    Job job(ctx, flags);
+    Job job(ctx, flags, releaser);
     rc = job.run();
   } catch (const std::exception& e) {
     ctx.abort(3, e.what());

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "moc/common.hpp"
+#include "moc/runtime/releaser.hpp"
 
 namespace moc {
 
@@ -66,6 +67,13 @@ class SharedWindow {
   char* base() const { return base_; }
   int64_t bytes() const { return bytes_; }
   void fence() const;  // MPI_Win_sync + node barrier: makes the owner's writes visible
+  // Single-rank nodes (private mapping) only, no-op otherwise: every later release of this window's pages
+  // goes through `rel` (FIFO, background thread) instead of the caller's thread. `rel` must outlive the
+  // queued tasks (drain it before the process ends).
+  void set_releaser(BackgroundReleaser* rel) { releaser_ = map_ ? rel : nullptr; }
+  // Returns the whole 2 MiB pages inside [off, off+len) to the OS (asynchronously with a releaser). The
+  // caller must not touch that range again. No-op for an MPI window (its pages are shared with peers).
+  void discard(int64_t off, int64_t len);
 
  private:
   MPI_Win win_ = MPI_WIN_NULL;
@@ -74,6 +82,7 @@ class SharedWindow {
   int64_t bytes_ = 0;
   void* map_ = nullptr;  // a node with one rank: private anonymous mapping (transparent huge pages)
   size_t map_bytes_ = 0;
+  BackgroundReleaser* releaser_ = nullptr;
 };
 
 

@@ -162,7 +162,13 @@ SharedWindow::SharedWindow(const MpiContext& ctx, int64_t bytes) : comm_(ctx.nod
 
 SharedWindow::~SharedWindow() {
   if (map_) {
-    munmap(map_, map_bytes_);
+    if (releaser_) {
+      void* m = map_;
+      const size_t len = map_bytes_;
+      releaser_->defer([m, len] { munmap(m, len); });
+    } else {
+      munmap(map_, map_bytes_);
+    }
     return;
   }
   // Never enter a collective while an exception unwinds: peers may be blocked elsewhere and the caller
@@ -172,6 +178,22 @@ SharedWindow::~SharedWindow() {
     MPI_Win_unlock_all(win_);
     MPI_Win_free(&win_);
   }
+}
+
+void SharedWindow::discard(int64_t off, int64_t len) {
+  if (!map_ || len <= 0) return;
+  constexpr uintptr_t kHuge = uintptr_t{2} << 20;  // whole huge pages only: a partial one would be split
+  const uintptr_t lo = (reinterpret_cast<uintptr_t>(base_) + static_cast<uintptr_t>(off) + kHuge - 1) & ~(kHuge - 1);
+  const uintptr_t hi = (reinterpret_cast<uintptr_t>(base_) + static_cast<uintptr_t>(off + len)) & ~(kHuge - 1);
+  if (hi <= lo) return;
+  // MADV_DONTNEED keeps the range mapped (zero-fill on a stray touch instead of a fault) and leaves the
+  // mapping whole for the final munmap.
+  void* p = reinterpret_cast<void*>(lo);
+  const size_t n = hi - lo;
+  if (releaser_)
+    releaser_->defer([p, n] { (void)madvise(p, n, MADV_DONTNEED); });
+  else
+    (void)madvise(p, n, MADV_DONTNEED);
 }
 
 void SharedWindow::fence() const {
