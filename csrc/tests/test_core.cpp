@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <random>
 #include <string>
 #include <vector>
@@ -13,6 +14,7 @@
 #include "moc/io.hpp"
 #include "moc/partition.hpp"
 #include "moc/problem.hpp"
+#include "moc/runtime/releaser.hpp"
 #include "moc/score_table.hpp"
 
 using namespace moc;
@@ -390,12 +392,36 @@ void test_formatter() {
 }
 }  // namespace
 
+// BackgroundReleaser: FIFO order on one worker, drain() waits for everything queued, captured owners are
+// released on the worker, and stop() after drain is idempotent.
+void test_releaser() {
+  std::vector<int> order;
+  auto owned = std::make_shared<int>(7);
+  std::weak_ptr<int> watch = owned;
+  {
+    BackgroundReleaser rel;
+    for (int i = 0; i < 100; ++i) rel.defer([&order, i] { order.push_back(i); });
+    rel.defer([o = std::move(owned)]() mutable { o.reset(); });
+    rel.drain();
+    CHECK(order.size() == 100);
+    bool sorted = true;
+    for (int i = 0; i < 100; ++i) sorted = sorted && order[i] == i;
+    CHECK(sorted);
+    CHECK(watch.expired());
+    rel.defer([&order] { order.push_back(100); });  // queued, then run by the destructor's stop()
+  }
+  CHECK(order.size() == 101 && order.back() == 100);
+  BackgroundReleaser idle;  // never started: stop() is a no-op
+  idle.drain();
+  idle.stop();
+}
+
 int main() {
   const std::vector<std::pair<const char*, std::function<void()>>> tests = {
       {"score_table", test_score_table}, {"parser", test_parser},     {"stream_reader", test_stream_reader},
       {"partition", test_partition},     {"keys", test_keys},         {"pack5", test_pack5},
       {"engine_vs_brute_force", test_engine_vs_brute_force},          {"formatter", test_formatter},
-      {"profile16", test_profile16}};
+      {"profile16", test_profile16},     {"releaser", test_releaser}};
   for (const auto& t : tests) {
     const int before = g_failed;
     t.second();
