@@ -1,4 +1,5 @@
-// Deferred release of large host memory on a background thread.
+// Deferred release of large host memory on a background thread (and, as a plain FIFO worker, the ordered
+// background writes of the result writer's pipe path, io.cpp write_results).
 //
 // Returning gigabytes of pages to the OS (munmap of the node window, freeing the input buffer) costs
 // ~40 ms per GB of 4 KiB pages and sits on the job's critical path when done inline (reference: there is

@@ -9,9 +9,12 @@
 #include <emmintrin.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <cstdlib>
 #include <cstring>
+
+#include "moc/runtime/releaser.hpp"
 
 namespace moc {
 
@@ -688,6 +691,8 @@ void write_results(FILE* f, const Result* results, int64_t n, int64_t first_inde
   // multi-GB outputs are written in parallel; otherwise (pipe, terminal) parts go out in order.
   // Blocks of 64 K rows per thread keep the buffers small (~5 MB per thread, reused): page-faulting
   // fresh multi-100 MB buffers cost more than the formatting (1.2 s of 1.6 s for 33 M rows here).
+  // A stream that is not a regular file (under mpiexec stdout is a pipe to the MPICH proxy) is written by
+  // one background thread in order, double-buffered: block k goes out while block k+1 is formatted.
   const int nthreads = n > 65536 ? omp_get_max_threads() : 1;
   const int64_t kBlock = int64_t{65536} * nthreads;
   std::fflush(f);
@@ -698,11 +703,21 @@ void write_results(FILE* f, const Result* results, int64_t n, int64_t first_inde
   const int fl = fcntl(fd, F_GETFL);
   if (nthreads > 1 && fl >= 0 && !(fl & O_APPEND) && fstat(fd, &st) == 0 && S_ISREG(st.st_mode))
     file_pos = lseek(fd, 0, SEEK_CUR);
-  std::vector<uvector<char>> parts(static_cast<size_t>(nthreads));
-  std::vector<size_t> used(static_cast<size_t>(nthreads) + 1);
+  const bool ordered_async = file_pos < 0 && n > kBlock;
+  std::vector<uvector<char>> part_sets[2];
+  std::vector<size_t> used_sets[2];
+  for (int s2 = 0; s2 < (ordered_async ? 2 : 1); ++s2) {
+    part_sets[s2].resize(static_cast<size_t>(nthreads));
+    used_sets[s2].assign(static_cast<size_t>(nthreads) + 1, 0);
+  }
+  BackgroundReleaser writer;  // FIFO worker: ordered writes of the pipe path
   bool write_error = false;
+  std::atomic<bool> async_error{false};
+  int set = 0;
   for (int64_t b = 0; b < n; b += kBlock) {
     const int64_t e = std::min(n, b + kBlock), m = e - b;
+    std::vector<uvector<char>>& parts = part_sets[set];
+    std::vector<size_t>& used = used_sets[set];
 #pragma omp parallel num_threads(nthreads)
     {
       const int t = omp_get_thread_num();
@@ -733,11 +748,23 @@ void write_results(FILE* f, const Result* results, int64_t n, int64_t first_inde
     }
     if (file_pos >= 0) {
       file_pos += static_cast<off_t>(used[nthreads]);
+    } else if (ordered_async) {
+      writer.drain();  // the previous block (the other buffer set) is out: that set is free again
+      writer.defer([f, nthreads, &parts, &used, &async_error] {
+        for (int t = 0; t < nthreads; ++t)
+          if (std::fwrite(parts[t].data(), 1, used[t + 1], f) != used[t + 1]) async_error = true;
+        used[0] = 0;
+      });
+      set ^= 1;
+      continue;
     } else {
-      for (int t = 0; t < nthreads; ++t) std::fwrite(parts[t].data(), 1, used[t + 1], f);
+      for (int t = 0; t < nthreads; ++t)
+        if (std::fwrite(parts[t].data(), 1, used[t + 1], f) != used[t + 1]) write_error = true;
     }
     used[0] = 0;
   }
+  writer.stop();
+  if (async_error) write_error = true;
   if (file_pos >= 0 && lseek(fd, file_pos, SEEK_SET) < 0) write_error = true;
   if (write_error) throw Error("error while writing the results");
   std::fflush(f);
