@@ -268,3 +268,24 @@ def test_large_file_parallel_read(tmp_path):
         outs.append(out.read_bytes())
     assert outs[0] == outs[1]
     assert outs[0].count(b"\n") == 7500000
+
+
+def test_pipe_output_double_buffered(tmp_path):
+    # stdout a pipe (mpiexec's proxy) with more rows than one block (64 K rows per thread): the blocks go
+    # out through the background writer, double-buffered against the formatting — order must hold, and the
+    # bytes must equal the pwrite path's and the Python formatter's
+    from mpi_openmp_cuda_amd import format_results, make_synthetic, search_cpu
+
+    prob = make_synthetic("input6", 700000, seed=13)
+    path = tmp_path / "in.txt"
+    path.write_text(prob.to_text())
+    want = format_results(search_cpu(prob)).encode()
+    r = run_final(["--backend=cpu", f"--input={path}"], stdin_bytes=b"", np_=1, env={"OMP_NUM_THREADS": "2"},
+                  timeout=300)
+    assert r.returncode == 0, r.stderr.decode()
+    assert r.stdout == want
+    out = tmp_path / "out.txt"
+    r = run_final(["--backend=cpu", f"--input={path}", f"--output={out}"], stdin_bytes=b"", np_=1,
+                  env={"OMP_NUM_THREADS": "2"}, timeout=300)
+    assert r.returncode == 0, r.stderr.decode()
+    assert out.read_bytes() == want
