@@ -15,11 +15,18 @@ and printing (reference flow main.c:149-197):
   4. an all-reduce of the per-rank record counts closes the job (the reference's MPI_Gather point).
 Weak scaling: --records-per-gpu is fixed per rank, the global batch grows with N.
 
-Run: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under torch.distributed.run.
+Run: python bench.py [--gpus N --steps K --warmup W]. With N > 1 and no torch.distributed environment
+(WORLD_SIZE unset) the script launches itself: a child `python -m torch.distributed.run
+--nproc-per-node N --master-addr 127.0.0.1 bench.py ...` started before anything touches the GPU, whose
+exit code it returns (reference: `mpiexec -np 2 ./final`, /root/reference/makefile:11). Under a launcher
+the world size must equal --gpus and every rank needs its own GPU, or the run fails (no silent 1-rank
+fallback).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -47,7 +54,50 @@ def parse_args():
     ap.add_argument("--packed", type=int, default=1, help="letters as 5-bit packed CSR (1) or one byte each (0)")
     ap.add_argument("--narrow", type=int, default=1,
                     help="1: narrowest wire formats that fit (4-bit lengths, R2 results); 0: uint8 lengths, R4")
+    ap.add_argument("--dry-launch", action="store_true",
+                    help="print the self-launch command (JSON) for --gpus N > 1 and exit; touches no GPU")
+    ap.add_argument("--allow-shared-gpu", action="store_true",
+                    help="rehearsals only (gloo): let several ranks share a GPU instead of failing")
     return ap.parse_args()
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_command(args, argv, port=None):
+    """The torch.distributed.run command line that runs this script as `args.gpus` ranks (one per GPU)."""
+    port = port or _free_port()
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + \
+        [a for a in argv if a != "--dry-launch"]
+
+
+def visible_gpus():
+    """GPU count without initialising the HIP runtime in this process (torch.cuda.device_count() does not
+    create a context on this image; the launcher must not hold the GPU while its children use it)."""
+    import torch
+
+    return torch.cuda.device_count()
+
+
+def self_launch(args, argv):
+    """--gpus N > 1 outside a launcher: run N ranks as a child torch.distributed.run job and return its
+    exit code. Fails (exit 2) when fewer than N GPUs are visible, instead of measuring fewer ranks."""
+    cmd = launch_command(args, argv)
+    if args.dry_launch:
+        print(json.dumps({"launch": cmd, "nproc": args.gpus}), flush=True)
+        return 0
+    n_dev = visible_gpus()
+    if n_dev < args.gpus and not args.allow_shared_gpu:
+        print(f"bench.py: --gpus {args.gpus} but only {n_dev} GPU(s) visible", file=sys.stderr, flush=True)
+        return 2
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    print(f"[bench] launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=env).returncode
 
 
 class HostArrays:
@@ -142,6 +192,11 @@ class HostArrays:
 
 def main():
     args = parse_args()
+    if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.dry_launch):
+        if args.gpus <= 1:
+            print(json.dumps({"launch": None, "nproc": 1}), flush=True)
+            return 0
+        return self_launch(args, sys.argv[1:])
     import torch
     import torch.distributed as dist
 
@@ -154,8 +209,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
-    gpu = local_rank % max(torch.cuda.device_count(), 1)
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}: refusing to report a different rank count",
+              file=sys.stderr, flush=True)
+        return 2
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    n_dev = torch.cuda.device_count()
+    if n_dev < 1 or (n_dev < local_world and not args.allow_shared_gpu):
+        print(f"bench.py: {local_world} local ranks but {n_dev} GPU(s) visible (one rank per GPU)",
+              file=sys.stderr, flush=True)
+        return 2
+    gpu = local_rank % n_dev
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     distributed = world > 1
@@ -168,6 +231,9 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+        if dist.get_world_size() != args.gpus:
+            print(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}", file=sys.stderr)
+            return 2
 
     t_setup = time.perf_counter()
 
@@ -274,6 +340,15 @@ def main():
         te = torch.tensor([int(host.offsets[-1])], dtype=torch.int64, device=cdev)
         dist.all_reduce(te)
         total_elems = int(te.item())
+    # per-rank evidence: NUMA node of the host arrays, median kernel ms per step, device index
+    mine = torch.tensor([float(numa), float(np.median(kms)), float(gpu), float(int(host.offsets[-1]))],
+                        dtype=torch.float64, device=cdev)
+    if distributed:
+        allv = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allv, mine)
+        per_rank = torch.stack(allv).cpu().numpy()
+    else:
+        per_rank = mine.cpu().numpy()[None, :]
     ms_per_step = elapsed / args.steps * 1e3
     value = total_elems * args.steps / elapsed
     cells_per_rec = float(np.mean([(shape.L1 - l + 1) * l for l in range(shape.l2_min, shape.l2_max + 1)]))
@@ -311,6 +386,12 @@ def main():
             "lengths_bits": host.len_bits,
             "letters": "packed5" if host.packed else "bytes",
             "rank0_numa_node": numa,
+            "rccl_world": dist.get_world_size() if (distributed and nccl) else (1 if nccl else None),
+            "dist_backend": ("nccl" if nccl else "gloo") if distributed else "none",
+            "rank_numa_nodes": [int(x) for x in per_rank[:, 0]],
+            "rank_kernel_ms": [round(float(x), 4) for x in per_rank[:, 1]],
+            "rank_devices": [int(x) for x in per_rank[:, 2]],
+            "rank_letters": [int(x) for x in per_rank[:, 3]],
             "rank0_kernels": st["kernels"],
             "host_stream": ("dma" if st["dma"] else "zero_copy") if st["direct"] else "staged",
             "verified": bool(okt.item()),
@@ -324,4 +405,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)
