@@ -35,7 +35,7 @@ LDROCM    := -L$(ROCM)/lib -lamdhip64 -Wl,-rpath,$(ROCM)/lib
 GPU_PLUGIN := mpi_openmp_cuda_amd/lib/libmoc_final_gpu.so
 
 # host core without any ROCm dependency (parser, CPU engine, partitioner, runtime utilities)
-CPU_SRCS  := csrc/src/cpu_engine.cpp csrc/src/io.cpp csrc/src/partition.cpp csrc/src/problem.cpp \
+CPU_SRCS  := csrc/src/cpu_engine.cpp csrc/src/io.cpp csrc/src/partition.cpp csrc/src/problem.cpp csrc/src/wire.cpp \
              csrc/src/score_table.cpp csrc/src/runtime/runtime.cpp
 # host code of the GPU engine (HIP runtime API) and the C ABI of libmoc.so
 GPU_SRCS  := csrc/src/hip_engine.cpp csrc/src/capi.cpp csrc/src/runtime/device.cpp csrc/src/runtime/pinned.cpp

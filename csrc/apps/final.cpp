@@ -387,9 +387,8 @@ void Job::batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, bool cp) {
       const int64_t* src_off = rb->offsets.data();
       const uint8_t* src_codes = rb->codes.data();
       const int nt = total_chars > (1 << 20) ? omp_get_max_threads() : 1;
-#pragma omp parallel num_threads(nt)
-      {
-        const int t = omp_get_thread_num();
+#pragma omp parallel for schedule(static, 1) num_threads(nt)
+      for (int t = 0; t < nt; ++t) {
         const int64_t cb = total_chars * t / nt, ce = total_chars * (t + 1) / nt;
         std::memcpy(w_codes + cb, src_codes + cb, static_cast<size_t>(ce - cb));
         const int64_t ob = (n + 1) * t / nt, oe = (n + 1) * (t + 1) / nt;

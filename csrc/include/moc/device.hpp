@@ -33,39 +33,9 @@
 #include <cstdint>
 
 #include "moc/common.hpp"
+#include "moc/wire.hpp"
 
 namespace moc {
-
-// Result wire formats (device -> host). R12 is moc::Result; R8/R4/R2 are chosen automatically when the
-// problem's bounds fit, to cut the D2H bytes per record by 1.5x / 3x / 6x.
-enum class ResultFormat : int32_t { R12 = 0, R8 = 1, R4 = 2, R2 = 3 };
-struct R8 {
-  int32_t score;
-  uint16_t n, k;
-};
-struct R4 {
-  int16_t score;  // INT16_MIN encodes "no candidate" (INT_MIN)
-  uint8_t n, k;
-};
-static_assert(sizeof(R8) == 8 && sizeof(R4) == 4, "packed result formats");
-// R2: one uint16 per record, code = (score - smin) * j + n * kw + k (mixed radix), 0xFFFF = no
-// candidate. Valid for a batch whose lengths lie in the [min_l2, max_l2] the parameters were made for.
-struct R2Params {
-  int32_t smin = 0;  // lowest possible score
-  int32_t kw = 0;    // radix of k (>= max_l2)
-  int32_t j = 0;     // radix of the score code (> every n * kw + k)
-};
-constexpr uint16_t kR2None = 0xFFFF;
-inline int result_bytes(ResultFormat f) {
-  return f == ResultFormat::R12 ? 12 : f == ResultFormat::R8 ? 8 : f == ResultFormat::R4 ? 4 : 2;
-}
-// R2 parameters for a problem (L1, pair-score range [min_t, max_t]) and a record-length range; false
-// when the codes would not fit 16 bits.
-bool r2_params(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t min_t, int32_t max_t, R2Params& p);
-// Smallest of R12/R8/R4 able to hold every result of a problem with these bounds.
-ResultFormat pick_result_format(int64_t L1, int64_t max_l2, int32_t max_abs_weight);
-// Expands packed results to moc::Result (host side); `r2` is required for R2.
-void expand_results(const void* in, ResultFormat f, int64_t n, Result* out, const R2Params* r2 = nullptr);
 
 namespace dev {
 

@@ -9,6 +9,7 @@
 // order is always input order and the thread count only changes speed.
 #pragma once
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <string>
@@ -16,6 +17,7 @@
 
 #include "moc/common.hpp"
 #include "moc/problem.hpp"
+#include "moc/wire.hpp"
 
 namespace moc {
 
@@ -28,30 +30,76 @@ struct ParseOptions {
 // Reads the whole stream into memory (bulk fread; no per-token stdio).
 uvector<char> read_stream(FILE* f);
 
-// Two-phase parser of an in-memory input: the constructor reads the header and counts the records and
-// letters (parallel pass 1); fill() encodes them into caller-provided buffers (parallel pass 2) — e.g.
-// straight into a node-shared window, with no intermediate copy. `data` must outlive fill().
+// Pieces of the record area that hold a contiguous run of records (a rank's slice): piece q covers
+// bytes [byte_begin, byte_end) of the area; its first token is record `tok` and its first letter is letter
+// `chr` of the slice (both relative to the slice's first record / letter).
+struct AreaPiece {
+  int64_t byte_begin = 0, byte_end = 0, tok = 0, chr = 0;
+};
+struct AreaSlice {
+  int64_t first_record = 0, records = 0, letters = 0;
+  std::vector<AreaPiece> pieces;
+};
+// What pass 2 saw in a slice: the length range, and the first offending records (global indices, -1: none).
+struct FillReport {
+  int64_t min_len = INT64_MAX, max_len = 0;
+  int64_t bad_record = -1;                 // first record holding a non-letter
+  int64_t long_record = -1, long_len = 0;  // first record over the Seq2 length limit
+};
+
+// Two-phase parser of an in-memory input. The constructor reads the header; pass 1 counts the tokens and
+// letters of the record area in chunks (cut at whitespace); pass 2 encodes any contiguous slice of the
+// records into caller-provided buffers — as byte codes or straight into the 5-bit packed wire format.
+// Pass 1 can run on one process (count = true) or cooperatively: every rank of a node counts a share of
+// the chunks of the node-shared text, the counts are exchanged, and each rank then encodes its own slice
+// into its own (NUMA-local, page-locked) buffers. `data` must outlive the parser.
 class BulkParser {
  public:
-  BulkParser(const char* data, size_t len, const ParseOptions& opt = {});
+  BulkParser(const char* data, size_t len, const ParseOptions& opt = {}, bool count = true);
   const Weights& weights() const { return weights_; }
   const std::vector<uint8_t>& seq1() const { return seq1_; }
   int64_t count() const { return n_; }
-  int64_t total_chars() const { return total_chars_; }
-  // codes[0..total_chars()), offsets[0..count()] (offsets[0] = 0); throws on non-letters / limits.
+  int64_t total_chars() const { return total_chars_; }  // after pass 1
+  int64_t area_bytes() const { return static_cast<int64_t>(area_len_); }
+  int64_t l2_cap() const { return l2_cap_; }
+
+  // ---- pass 1
+  // nchunks+1 chunk boundaries (byte offsets in the area), each moved forward past the token it cuts.
+  std::vector<int64_t> chunk_starts(int nchunks) const;
+  // Tokens / letters of chunks [c0, c1) -> toks[c - c0], chars[c - c0] (OpenMP over the chunks).
+  void count_chunks(const std::vector<int64_t>& starts, int c0, int c1, int64_t* toks, int64_t* chars) const;
+  // Installs the chunk table (per-chunk counts of ALL chunks); throws when the area holds fewer than
+  // count() records. Only the first count() tokens are records (trailing tokens are ignored).
+  void set_chunks(std::vector<int64_t> starts, const int64_t* toks, const int64_t* chars);
+  int nchunks() const { return static_cast<int>(start_.size()) - 1; }
+  // Records / letters before chunk c (prefix arrays of the table, clipped to count() records).
+  int64_t chunk_first_record(int c) const { return std::min(tok_pre_[c], n_); }
+  int64_t chunk_first_letter(int c) const;
+
+  // ---- pass 2
+  AreaSlice slice(int64_t rec_begin, int64_t rec_end) const;
+  // Encodes slice s: letters as bytes into codes[0..s.letters) and/or 5-bit packed into
+  // packed5[0..packed5_bytes(s.letters)) (either may be null), offsets[0..s.records] rebased to 0.
+  FillReport fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* packed5, int64_t* offsets) const;
+  // Throws the error a sequential reader would report first for this report (`first` = the report's
+  // slice start; validates the score range for its longest record).
+  void check(const FillReport& r) const;
+  // All records: codes[0..total_chars()), offsets[0..count()] (offsets[0] = 0); throws on errors.
   void fill(uint8_t* codes, int64_t* offsets) const;
-  // n * (L1 - avg + 1) * avg from the mean record length (before fill; for engine selection).
+  // n * (L1 - avg + 1) * avg from the mean record length (pass 1's letters, or the area size before it).
   int64_t cells_estimate() const;
 
  private:
+  struct Located {
+    int64_t byte = 0, chr = 0;  // area byte just after token t-1 (or the chunk start) and letters before t
+  };
+  Located locate(int64_t t) const;  // position of the boundary before record t (t <= tokens in the area)
   Weights weights_{};
   std::vector<uint8_t> seq1_;
   int64_t n_ = 0, total_chars_ = 0, l2_cap_ = 0;
   const char* area_ = nullptr;
   size_t area_len_ = 0;
-  int nthreads_ = 1;
-  std::vector<size_t> start_;
-  std::vector<int64_t> tok_count_, char_count_;
+  std::vector<int64_t> start_, tok_pre_, chr_pre_;  // chunk table: nchunks+1 entries each
 };
 
 // Parses "W1 W2 W3 W4 / Seq1 / N / Seq2 x N" (PDF p.5-6). Whitespace of any kind (incl. CRLF)
@@ -89,6 +137,9 @@ class StreamReader {
 // Formats "#i: score: S, n: N, k: K\n" rows (main.c:204) for results[0..n), numbering from
 // first_index, in parallel, then writes them with one fwrite.
 void write_results(FILE* f, const Result* results, int64_t n, int64_t first_index = 0);
+// The same for consecutive runs of results in any wire format (e.g. every rank's slice in its own format),
+// decoded row by row while formatting.
+void write_results(FILE* f, const std::vector<ResultRun>& runs, int64_t first_index = 0);
 std::string format_results(const Result* results, int64_t n, int64_t first_index = 0);
 
 }  // namespace moc

@@ -24,53 +24,6 @@ int32_t choose_key_shift(int32_t max_abs_weight, int64_t max_l2) {
   return shift;
 }
 
-ResultFormat pick_result_format(int64_t L1, int64_t max_l2, int32_t max_abs_weight) {
-  const int64_t smax = static_cast<int64_t>(std::max(max_abs_weight, 1)) * std::max<int64_t>(max_l2, 1);
-  if (L1 <= 255 && max_l2 <= 255 && smax < 32767) return ResultFormat::R4;
-  if (L1 <= 65535 && max_l2 <= 65535) return ResultFormat::R8;
-  return ResultFormat::R12;
-}
-
-bool r2_params(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t min_t, int32_t max_t, R2Params& p) {
-  min_l2 = std::max<int64_t>(min_l2, 1);
-  max_l2 = std::max(max_l2, min_l2);
-  const int64_t smin = std::min(static_cast<int64_t>(min_t) * min_l2, static_cast<int64_t>(min_t) * max_l2);
-  const int64_t smax = std::max(static_cast<int64_t>(max_t) * min_l2, static_cast<int64_t>(max_t) * max_l2);
-  const int64_t kw = max_l2;
-  const int64_t j = std::max<int64_t>(L1 - min_l2 + 1, 1) * kw;  // > (L1 - min_l2) * kw + (kw - 1) >= n*kw + k
-  if ((smax - smin + 1) * j > kR2None) return false;            // 0xFFFF stays free for "no candidate"
-  p.smin = static_cast<int32_t>(smin);
-  p.kw = static_cast<int32_t>(kw);
-  p.j = static_cast<int32_t>(j);
-  return true;
-}
-
-void expand_results(const void* in, ResultFormat f, int64_t n, Result* out, const R2Params* r2) {
-  if (f == ResultFormat::R12) {
-    if (in != out) std::memmove(out, in, sizeof(Result) * static_cast<size_t>(n));
-    return;
-  }
-  if (f == ResultFormat::R2 && (!r2 || r2->j <= 0 || r2->kw <= 0)) throw Error("expand_results: R2 needs its parameters");
-#pragma omp parallel for schedule(static) if (n > 65536)
-  for (int64_t i = 0; i < n; ++i) {
-    if (f == ResultFormat::R2) {
-      const uint16_t c = static_cast<const uint16_t*>(in)[i];
-      if (c == kR2None) {
-        out[i] = Result{INT32_MIN, 0, 0};
-      } else {
-        const int32_t idx = c % r2->j;
-        out[i] = Result{c / r2->j + r2->smin, idx / r2->kw, idx % r2->kw};
-      }
-    } else if (f == ResultFormat::R8) {
-      const R8 x = static_cast<const R8*>(in)[i];
-      out[i] = Result{x.score, x.n, x.k};
-    } else {
-      const R4 x = static_cast<const R4*>(in)[i];
-      out[i] = Result{x.score == INT16_MIN ? INT32_MIN : x.score, x.n, x.k};
-    }
-  }
-}
-
 namespace {
 // hipMemcpyAsync between device memory and a caller's host range, one copy per piece of the range that
 // lies within a single page-locked registration (or outside all): see pinned::segments.
@@ -303,9 +256,8 @@ void HipEngine::plan_chunk(const int64_t* offsets, int64_t n, ChunkPlan& cp) con
   const int nt = n > (1 << 16) ? omp_get_max_threads() : 1;
   std::vector<std::vector<int32_t>> part(nt);
   std::vector<int64_t> mins(nt, INT64_MAX), maxs(nt, 0), nshort(nt, 0), cells(nt, 0);
-#pragma omp parallel num_threads(nt)
-  {
-    const int t = omp_get_thread_num();
+#pragma omp parallel for schedule(static, 1) num_threads(nt)  // parts, not thread ids (any team size)
+  for (int t = 0; t < nt; ++t) {
     const int64_t b = n * t / nt, e = n * (t + 1) / nt;
     int64_t mn = INT64_MAX, mx = 0, ns = 0, cl = 0;
     for (int64_t i = b; i < e; ++i) {
@@ -428,9 +380,8 @@ struct LenStats {
 LenStats scan_lengths(const int64_t* offsets, const uint8_t* lengths8, int64_t n) {
   const int nt = n > (1 << 16) ? omp_get_max_threads() : 1;
   std::vector<int64_t> mins(nt, INT64_MAX), maxs(nt, 0);
-#pragma omp parallel num_threads(nt)
-  {
-    const int t = omp_get_thread_num();
+#pragma omp parallel for schedule(static, 1) num_threads(nt)  // parts, not thread ids (any team size)
+  for (int t = 0; t < nt; ++t) {
     const int64_t b = n * t / nt, e = n * (t + 1) / nt;
     int64_t mn = INT64_MAX, mx = 0;
     if (lengths8) {

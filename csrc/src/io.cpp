@@ -143,7 +143,7 @@ uvector<char> read_stream(FILE* f) {
   return buf;
 }
 
-BulkParser::BulkParser(const char* data, size_t len, const ParseOptions& opt) {
+BulkParser::BulkParser(const char* data, size_t len, const ParseOptions& opt, bool count) {
   Cursor cur{data, data + len};
   const char *b, *e;
   static const char* wname[4] = {"W1", "W2", "W3", "W4"};
@@ -163,31 +163,41 @@ BulkParser::BulkParser(const char* data, size_t len, const ParseOptions& opt) {
   l2_cap_ = opt.strict_limits ? kSpecMaxSeq2 : opt.max_l2;
   if (l1_cap > 0 && static_cast<int64_t>(seq1_.size()) > l1_cap)
     throw Error("Seq1 has " + std::to_string(seq1_.size()) + " letters, limit is " + std::to_string(l1_cap));
-
-  // ---- pass 1 over the record area (parallel) -------------------------------------------------
   area_ = cur.p;
   area_len_ = static_cast<size_t>(cur.end - cur.p);
-  int nthreads = omp_get_max_threads();
-  if (area_len_ < (size_t{1} << 16)) nthreads = 1;
-  nthreads_ = std::max(1, nthreads);
-  const unsigned char* ua = reinterpret_cast<const unsigned char*>(area_);
-
-  // Chunk boundaries moved forward past any token they cut, so every token lies inside one chunk.
-  start_.assign(static_cast<size_t>(nthreads_) + 1, 0);
-  for (int t = 0; t <= nthreads_; ++t) start_[t] = area_len_ * static_cast<size_t>(t) / nthreads_;
-  for (int t = 1; t < nthreads_; ++t) {
-    size_t s0 = start_[t];
-    while (s0 < area_len_ && s0 > 0 && !is_space(ua[s0 - 1])) ++s0;
-    start_[t] = std::max(s0, start_[t - 1]);
+  total_chars_ = -1;
+  if (count) {  // pass 1 on this process: one chunk per OpenMP thread
+    const int nt = area_len_ < (size_t{1} << 16) ? 1 : std::max(1, omp_get_max_threads());
+    std::vector<int64_t> st = chunk_starts(nt), tk(static_cast<size_t>(nt)), ch(static_cast<size_t>(nt));
+    count_chunks(st, 0, nt, tk.data(), ch.data());
+    set_chunks(std::move(st), tk.data(), ch.data());
   }
-  start_[nthreads_] = area_len_;
-  // pass 1 (branch-free, vectorisable): tokens = space->letter transitions, letters = non-space bytes
-  tok_count_.assign(static_cast<size_t>(nthreads_) + 1, 0);
-  char_count_.assign(static_cast<size_t>(nthreads_) + 1, 0);
-#pragma omp parallel num_threads(nthreads_)
-  {
-    const int t = omp_get_thread_num();
-    const size_t b = start_[t], e = start_[t + 1];
+}
+
+std::vector<int64_t> BulkParser::chunk_starts(int nchunks) const {
+  nchunks = std::max(1, nchunks);
+  const int64_t len = static_cast<int64_t>(area_len_);
+  const unsigned char* ua = reinterpret_cast<const unsigned char*>(area_);
+  std::vector<int64_t> s(static_cast<size_t>(nchunks) + 1, 0);
+  for (int t = 1; t < nchunks; ++t) {
+    // from the previous boundary when that already lies past this one: every byte is scanned at most
+    // once, even inside a token longer than many chunks
+    int64_t x = std::max(len * t / nchunks, s[t - 1]);
+    while (x < len && x > 0 && !is_space(ua[x - 1])) ++x;
+    s[t] = x;
+  }
+  s[nchunks] = len;
+  return s;
+}
+
+void BulkParser::count_chunks(const std::vector<int64_t>& starts, int c0, int c1, int64_t* toks,
+                              int64_t* chars) const {
+  const unsigned char* ua = reinterpret_cast<const unsigned char*>(area_);
+  // pass 1 (branch-free, vectorisable): tokens = space->letter transitions, letters = non-space bytes.
+  // Iterations are chunks, not thread ids: correct whatever number of threads OpenMP delivers.
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int c = c0; c < c1; ++c) {
+    const size_t b = static_cast<size_t>(starts[c]), e = static_cast<size_t>(starts[c + 1]);
     int64_t nt = 0, nc = 0;
     if (b < e) {  // a chunk starts at a token start or at whitespace
       const int64_t first = is_space(ua[b]) ? 0 : 1;
@@ -199,9 +209,9 @@ BulkParser::BulkParser(const char* data, size_t len, const ParseOptions& opt) {
         const size_t be = std::min(e, blk + 255);
         unsigned t_cnt = 0, c_cnt = 0;
         for (size_t i = blk; i < be; ++i) {
-          const unsigned char c = ua[i], p = ua[i - 1];
-          const unsigned lt = (c != ' ') & (static_cast<unsigned char>(c - 9) > 4);  // c is a token byte
-          const unsigned ps = (p == ' ') | (static_cast<unsigned char>(p - 9) <= 4);  // p is whitespace
+          const unsigned char ch = ua[i], p = ua[i - 1];
+          const unsigned lt = (ch != ' ') & (static_cast<unsigned char>(ch - 9) > 4);  // ch is a token byte
+          const unsigned ps = (p == ' ') | (static_cast<unsigned char>(p - 9) <= 4);   // p is whitespace
           t_cnt += lt & ps;
           c_cnt += lt;
         }
@@ -209,27 +219,72 @@ BulkParser::BulkParser(const char* data, size_t len, const ParseOptions& opt) {
         nc += c_cnt;
       }
     }
-    tok_count_[t + 1] = nt;
-    char_count_[t + 1] = nc;
+    toks[c - c0] = nt;
+    chars[c - c0] = nc;
   }
-  for (int t = 0; t < nthreads_; ++t) {
-    tok_count_[t + 1] += tok_count_[t];
-    char_count_[t + 1] += char_count_[t];
+}
+
+void BulkParser::set_chunks(std::vector<int64_t> starts, const int64_t* toks, const int64_t* chars) {
+  start_ = std::move(starts);
+  const int nch = static_cast<int>(start_.size()) - 1;
+  tok_pre_.assign(static_cast<size_t>(nch) + 1, 0);
+  chr_pre_.assign(static_cast<size_t>(nch) + 1, 0);
+  for (int c = 0; c < nch; ++c) {
+    tok_pre_[c + 1] = tok_pre_[c] + toks[c];
+    chr_pre_[c + 1] = chr_pre_[c] + chars[c];
   }
-  const int64_t total_tokens = tok_count_[nthreads_];
+  const int64_t total_tokens = tok_pre_[nch];
   if (total_tokens < n_)
     throw Error("expected " + std::to_string(n_) + " Seq2 records, found only " + std::to_string(total_tokens));
+  // only the first n tokens are records (extra trailing tokens are ignored, like the reference)
+  total_chars_ = total_tokens == n_ ? chr_pre_[nch] : locate(n_).chr;
+}
 
-  // Only the first n tokens are records (extra trailing tokens are ignored, like the reference).
-  total_chars_ = char_count_[nthreads_];
-  if (total_tokens > n_) {  // rare path: count the letters of the first n tokens exactly
-    total_chars_ = 0;
-    Cursor c{area_, area_ + area_len_};
-    for (int64_t i = 0; i < n_; ++i) {
-      c.next(b, e);
-      total_chars_ += e - b;
-    }
+int64_t BulkParser::chunk_first_letter(int c) const { return tok_pre_[c] <= n_ ? chr_pre_[c] : total_chars_; }
+
+BulkParser::Located BulkParser::locate(int64_t t) const {
+  Located l;
+  if (t <= 0) return l;
+  // chunk c holds token t-1: tok_pre_[c] <= t-1 < tok_pre_[c+1]
+  const int c = static_cast<int>(std::upper_bound(tok_pre_.begin(), tok_pre_.end(), t - 1) - tok_pre_.begin()) - 1;
+  const unsigned char* ua = reinterpret_cast<const unsigned char*>(area_);
+  int64_t i = start_[c];
+  const int64_t e = start_[c + 1];
+  int64_t k = tok_pre_[c], chr = chr_pre_[c];
+  while (k < t && i < e) {
+    while (i < e && is_space(ua[i])) ++i;
+    const int64_t b = i;
+    while (i < e && !is_space(ua[i])) ++i;
+    chr += i - b;
+    ++k;
   }
+  l.byte = i;
+  l.chr = chr;
+  return l;
+}
+
+AreaSlice BulkParser::slice(int64_t rec_begin, int64_t rec_end) const {
+  if (start_.empty()) throw Error("BulkParser::slice before pass 1");
+  rec_begin = std::clamp<int64_t>(rec_begin, 0, n_);
+  rec_end = std::clamp<int64_t>(rec_end, rec_begin, n_);
+  AreaSlice s;
+  s.first_record = rec_begin;
+  s.records = rec_end - rec_begin;
+  if (s.records == 0) return s;
+  const Located lo = locate(rec_begin), hi = locate(rec_end);
+  s.letters = hi.chr - lo.chr;
+  const int nch = nchunks();
+  for (int c = 0; c < nch; ++c) {
+    const int64_t b = std::max(start_[c], lo.byte), e = std::min(start_[c + 1], hi.byte);
+    if (b >= e) continue;
+    AreaPiece p;
+    p.byte_begin = b;
+    p.byte_end = e;
+    p.tok = b == lo.byte ? 0 : tok_pre_[c] - rec_begin;
+    p.chr = b == lo.byte ? 0 : chr_pre_[c] - lo.chr;
+    s.pieces.push_back(p);
+  }
+  return s;
 }
 
 namespace {
@@ -248,46 +303,106 @@ inline __m128i encode16(const unsigned char* src, unsigned& space_mask, unsigned
 }
 }  // namespace
 
-void BulkParser::fill(uint8_t* codes, int64_t* offs) const {
-  // pass 2: encode letters and record token ends (token by token; table lookups), tracking each
-  // thread's longest record and first offending record for the checks below
-  const int nthreads = nthreads_;
-  const int64_t n = n_, l2_cap = l2_cap_;
-  const unsigned char* ua = reinterpret_cast<const unsigned char*>(area_);
-  std::vector<int64_t> bad_tok(nthreads, -1), max_len(nthreads, 0), long_tok(nthreads, -1), long_len(nthreads, 0);
+namespace {
+// 8 letter codes (one per byte, < 32) -> their 40-bit 5-bit packed form (char j at bits [5j, 5j+5)).
+inline uint64_t compress8(uint64_t x) {
+  x &= 0x1F1F1F1F1F1F1F1Full;
+  x = (x & 0x001F001F001F001Full) | ((x >> 3) & 0x03E003E003E003E0ull);
+  x = (x & 0x000003FF000003FFull) | ((x >> 6) & 0x000FFC00000FFC00ull);
+  x = (x & 0x00000000000FFFFFull) | ((x >> 12) & 0x000000FFFFF00000ull);
+  return x;
+}
+constexpr int64_t kStage = int64_t{1} << 16;  // letters staged per thread before packing
+
+struct PieceOut {
+  FillReport rep;
+  int64_t rec_base = 0;                       // global index of the piece's first record
+  std::vector<std::pair<int64_t, uint8_t>> stragglers;  // packed mode: letters of partial groups
+};
+}  // namespace
+
+FillReport BulkParser::fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* packed5, int64_t* offs) const {
   offs[0] = 0;
-#pragma omp parallel num_threads(nthreads_)
-  {
-    const int t = omp_get_thread_num();
-    int64_t tok = tok_count_[t];
-    int64_t pos = char_count_[t];
-    int64_t first_bad = -1, mx = 0, lt = -1, ll = 0;
-    size_t i = start_[t];
-    const size_t e = start_[t + 1];
-    // 16-byte SSE2 blocks wherever a full block can be read from the area and stored into `codes`
-    const size_t vec_in_end = area_len_ >= 16 ? area_len_ - 16 : 0;
-    // (this thread's part of `codes` only: a store past it would race with thread t+1's first records)
-    const int64_t vec_out_end = std::min(char_count_[t + 1], total_chars_) - 16;
-    while (tok < n) {
+  const int np = static_cast<int>(s.pieces.size());
+  const unsigned char* ua = reinterpret_cast<const unsigned char*>(area_);
+  const int64_t l2_cap = l2_cap_;
+  const size_t vec_in_end = area_len_ >= 16 ? area_len_ - 16 : 0;  // 16-byte loads stay in the area
+  std::vector<PieceOut> out(static_cast<size_t>(np));
+  // one piece per iteration (dynamic): correct for any number of delivered threads
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int q = 0; q < np; ++q) {
+    const AreaPiece& pc = s.pieces[q];
+    PieceOut& po = out[q];
+    const int64_t a = pc.chr, b = q + 1 < np ? s.pieces[q + 1].chr : s.letters;  // this piece's letters [a, b)
+    po.rec_base = s.first_record + pc.tok;
+    std::vector<uint8_t> stage(packed5 ? static_cast<size_t>(kStage + 64) : 0);
+    // sink of the encoded letters: `codes` at the slice position, else the staging buffer
+    int64_t base = packed5 ? a : 0;  // slice letter index of stage[0]
+    bool head_done = false;
+    auto flush = [&](int64_t hi, bool final) {  // packs staged letters [base, hi) (and copies them to codes)
+      if (codes) std::memcpy(codes + base, stage.data(), static_cast<size_t>(hi - base));
+      int64_t cur = base;
+      if (!head_done) {  // letters before the piece's first whole group: fixed up after the loop
+        const int64_t g0 = (a + 7) & ~int64_t{7}, hend = std::min(g0, hi);
+        if (hend < g0 && !final) return;
+        for (int64_t c = cur; c < hend; ++c) po.stragglers.emplace_back(c, stage[static_cast<size_t>(c - base)]);
+        cur = hend;
+        head_done = true;
+      }
+      const int64_t ng = (hi - cur) / 8;
+      const uint8_t* src = stage.data() + (cur - base);
+      uint8_t* dst = packed5 + 5 * (cur / 8);
+      for (int64_t g = 0; g < ng; ++g) {
+        uint64_t x;
+        std::memcpy(&x, src + 8 * g, 8);
+        x = compress8(x);
+        // 8-byte stores run 3 zero bytes into the next group, which the next store rewrites; the last
+        // group of the run writes its 5 bytes only (the next group may belong to another piece)
+        std::memcpy(dst + 5 * g, &x, g + 1 < ng ? 8 : 5);
+      }
+      cur += 8 * ng;
+      if (final) {
+        for (int64_t c = cur; c < hi; ++c) po.stragglers.emplace_back(c, stage[static_cast<size_t>(c - base)]);
+      } else {
+        std::memmove(stage.data(), stage.data() + (cur - base), static_cast<size_t>(hi - cur));
+        base = cur;
+      }
+    };
+    uint8_t* sink = packed5 ? stage.data() : codes;
+    int64_t tok = pc.tok, pos = a;
+    int64_t first_bad = -1, lt = -1, ll = 0, mn = INT64_MAX, mx = 0;
+    size_t i = static_cast<size_t>(pc.byte_begin);
+    const size_t e = static_cast<size_t>(pc.byte_end);
+    while (i < e) {
       while (i < e && is_space(ua[i])) ++i;
       if (i >= e) break;
       const int64_t p0 = pos;
       unsigned bad = 0;
-      while (i <= vec_in_end && pos <= vec_out_end) {
-        unsigned sp, ok;
-        const __m128i codes16 = encode16(ua + i, sp, ok);
-        _mm_storeu_si128(reinterpret_cast<__m128i*>(codes + pos), codes16);
-        // letters up to the first space (or the chunk end); a token of >= 16 letters takes another block
-        const size_t take = std::min<size_t>(sp ? static_cast<size_t>(__builtin_ctz(sp)) : 16, e - i);
-        bad |= ~ok & ((1u << take) - 1u);
-        i += take;
-        pos += static_cast<int64_t>(take);
-        if (take < 16) break;
-      }
-      while (i < e && !is_space(ua[i])) {  // tail: near the end of the area or of `codes`
-        const uint8_t code = kCodeOf[ua[i++]];
-        bad |= (code == 0);
-        codes[pos++] = code;
+      while (true) {
+        if (packed5 && pos - base > kStage) flush(pos, false);  // mid-token is fine: groups are by position
+        // 16-byte SSE2 blocks wherever a full block can be read from the area and stored into the sink
+        // (byte mode: within this piece's letters only — a store past them would race with the next piece)
+        const int64_t lim = packed5 ? base + kStage + 48 : b;
+        if (i <= vec_in_end && pos + 16 <= lim) {
+          unsigned sp, ok;
+          const __m128i codes16 = encode16(ua + i, sp, ok);
+          _mm_storeu_si128(reinterpret_cast<__m128i*>(sink + (pos - base)), codes16);
+          // letters up to the first space (or the piece end); a token of >= 16 letters takes another block
+          const size_t take = std::min<size_t>(sp ? static_cast<size_t>(__builtin_ctz(sp)) : 16, e - i);
+          bad |= ~ok & ((1u << take) - 1u);
+          i += take;
+          pos += static_cast<int64_t>(take);
+          if (take < 16) break;
+          continue;
+        }
+        // tail: near the end of the area or of the piece (or of the staging buffer)
+        int64_t room = lim - pos;
+        while (i < e && !is_space(ua[i]) && room-- > 0) {
+          const uint8_t code = kCodeOf[ua[i++]];
+          bad |= (code == 0);
+          sink[pos++ - base] = code;
+        }
+        if (i >= e || is_space(ua[i])) break;
       }
       const int64_t L = pos - p0;
       if (bad && first_bad < 0) first_bad = tok;
@@ -295,30 +410,70 @@ void BulkParser::fill(uint8_t* codes, int64_t* offs) const {
         lt = tok;
         ll = L;
       }
+      mn = std::min(mn, L);
       mx = std::max(mx, L);
       offs[++tok] = pos;
     }
-    bad_tok[t] = first_bad;
-    max_len[t] = mx;
-    long_tok[t] = lt;
-    long_len[t] = ll;
+    if (packed5) flush(pos, true);
+    po.rep.min_len = mn;
+    po.rep.max_len = mx;
+    po.rep.bad_record = first_bad < 0 ? -1 : s.first_record + first_bad;
+    po.rep.long_record = lt < 0 ? -1 : s.first_record + lt;
+    po.rep.long_len = ll;
   }
-  int64_t longest = 0;
-  for (int t = 0; t < nthreads; ++t) {
-    if (bad_tok[t] >= 0 && bad_tok[t] < n)
-      throw Error("Seq2 record #" + std::to_string(bad_tok[t]) + " contains a non-letter character");
-    if (long_tok[t] >= 0 && long_tok[t] < n)
-      throw Error("Seq2 record #" + std::to_string(long_tok[t]) + " has " + std::to_string(long_len[t]) +
-                  " letters, limit is " + std::to_string(l2_cap));
-    longest = std::max(longest, max_len[t]);
+  FillReport r;
+  for (const PieceOut& po : out) {
+    r.min_len = std::min(r.min_len, po.rep.min_len);
+    r.max_len = std::max(r.max_len, po.rep.max_len);
+    if (po.rep.bad_record >= 0 && (r.bad_record < 0 || po.rep.bad_record < r.bad_record)) r.bad_record = po.rep.bad_record;
+    if (po.rep.long_record >= 0 && (r.long_record < 0 || po.rep.long_record < r.long_record)) {
+      r.long_record = po.rep.long_record;
+      r.long_len = po.rep.long_len;
+    }
   }
-  validate_score_range(weights_, std::max<int64_t>(longest, 1));
+  if (packed5) {
+    // groups holding letters of two pieces (or the slice's last, partial group): zeroed, then assembled
+    for (const PieceOut& po : out)
+      for (const auto& sc : po.stragglers) std::memset(packed5 + 5 * (sc.first / 8), 0, 5);
+    for (const PieceOut& po : out)
+      for (const auto& sc : po.stragglers) {
+        const int64_t bit = 5 * sc.first;
+        const uint32_t v = static_cast<uint32_t>(sc.second & 31u) << (bit & 7);
+        packed5[bit >> 3] |= static_cast<uint8_t>(v);
+        packed5[(bit >> 3) + 1] |= static_cast<uint8_t>(v >> 8);
+      }
+    const int64_t used = 5 * ((s.letters + 7) / 8);
+    std::memset(packed5 + used, 0, static_cast<size_t>(packed5_bytes(s.letters) - used));
+  }
+  return r;
+}
+
+void BulkParser::check(const FillReport& r) const {
+  // the record a sequential reader meets first; on that record the length limit is reported first
+  if (r.long_record >= 0 && (r.bad_record < 0 || r.long_record <= r.bad_record))
+    throw Error("Seq2 record #" + std::to_string(r.long_record) + " has " + std::to_string(r.long_len) +
+                " letters, limit is " + std::to_string(l2_cap_));
+  if (r.bad_record >= 0)
+    throw Error("Seq2 record #" + std::to_string(r.bad_record) + " contains a non-letter character");
+  validate_score_range(weights_, std::max<int64_t>(r.max_len, 1));
+}
+
+void BulkParser::fill(uint8_t* codes, int64_t* offs) const {
+  const AreaSlice s = slice(0, n_);
+  if (s.records == 0) {
+    offs[0] = 0;
+    validate_score_range(weights_, 1);
+    return;
+  }
+  check(fill_slice(s, codes, nullptr, offs));
 }
 
 int64_t BulkParser::cells_estimate() const {
   const int64_t L1 = static_cast<int64_t>(seq1_.size());
   if (n_ <= 0) return 0;
-  const int64_t avg = std::max<int64_t>(1, total_chars_ / n_);
+  // before pass 1: the area's bytes less one separator per record
+  const int64_t letters = total_chars_ >= 0 ? total_chars_ : std::max<int64_t>(0, static_cast<int64_t>(area_len_) - n_);
+  const int64_t avg = std::max<int64_t>(1, letters / n_);
   return avg <= L1 ? n_ * (L1 - avg + 1) * avg : 0;
 }
 
@@ -661,20 +816,42 @@ inline char* format_row(char* p, RowCounter& idx, const Result& r) {
 }
 // '#' + 19 index digits + ": score: " + 11 + ", n: " + 11 + ", k: " + 11 + '\n'
 constexpr int kMaxRow = 1 + 19 + 9 + 11 + 5 + 11 + 5 + 11 + 1;
+
+// Rows of a sequence of result runs (one per rank slice, each in its own wire format), by global row.
+struct RowSource {
+  const std::vector<ResultRun>& runs;
+  std::vector<int64_t> pre;  // pre[r] = rows before run r
+  explicit RowSource(const std::vector<ResultRun>& r) : runs(r), pre(r.size() + 1, 0) {
+    for (size_t i = 0; i < r.size(); ++i) pre[i + 1] = pre[i] + r[i].n;
+  }
+  int64_t total() const { return pre.back(); }
+  // formats rows [rb, re) at p
+  char* format(char* p, int64_t rb, int64_t re, int64_t first_index) const {
+    RowCounter idx(first_index + rb);
+    size_t r = static_cast<size_t>(std::upper_bound(pre.begin(), pre.end(), rb) - pre.begin()) - 1;
+    for (int64_t i = rb; i < re;) {
+      while (r + 1 < pre.size() && pre[r + 1] <= i) ++r;
+      const ResultRun& run = runs[r];
+      const int64_t e = std::min(re, pre[r + 1]);
+      for (int64_t j = i - pre[r]; i < e; ++i, ++j) p = format_row(p, idx, decode_result(run.data, run.fmt, run.r2, j));
+    }
+    return p;
+  }
+};
 }  // namespace
 
 std::string format_results(const Result* results, int64_t n, int64_t first_index) {
-  int nthreads = n > 65536 ? omp_get_max_threads() : 1;
-  std::vector<std::string> parts(nthreads);
-#pragma omp parallel num_threads(nthreads)
-  {
-    const int t = omp_get_thread_num();
-    const int64_t b = n * t / nthreads, e = n * (t + 1) / nthreads;
+  const std::vector<ResultRun> runs = {ResultRun{results, ResultFormat::R12, R2Params{}, n}};
+  const RowSource src(runs);
+  const int parts_n = n > 65536 ? std::max(1, omp_get_max_threads()) : 1;
+  std::vector<std::string> parts(static_cast<size_t>(parts_n));
+  // iterations are parts, not thread ids: every part is formatted whatever number of threads runs
+#pragma omp parallel for schedule(static, 1) num_threads(parts_n)
+  for (int t = 0; t < parts_n; ++t) {
+    const int64_t b = n * t / parts_n, e = n * (t + 1) / parts_n;
     std::string& s = parts[t];
     s.resize(static_cast<size_t>(e - b) * kMaxRow);
-    char* p = s.data();
-    RowCounter idx(first_index + b);
-    for (int64_t i = b; i < e; ++i) p = format_row(p, idx, results[i]);
+    char* p = src.format(s.data(), b, e, first_index);
     s.resize(static_cast<size_t>(p - s.data()));
   }
   size_t total = 0;
@@ -686,82 +863,83 @@ std::string format_results(const Result* results, int64_t n, int64_t first_index
 }
 
 void write_results(FILE* f, const Result* results, int64_t n, int64_t first_index) {
-  // Rows are formatted in parallel into per-thread buffers (never zero-filled, never concatenated).
-  // When the stream is a regular file, every thread writes its part at its own file offset (pwrite), so
+  write_results(f, std::vector<ResultRun>{ResultRun{results, ResultFormat::R12, R2Params{}, n}}, first_index);
+}
+
+void write_results(FILE* f, const std::vector<ResultRun>& runs, int64_t first_index) {
+  // Rows are formatted in parallel into per-part buffers (never zero-filled, never concatenated), decoding
+  // each run's wire format on the fly (R2/R4/R8 straight from the ranks' result slices, no expansion).
+  // When the stream is a regular file, every part is written at its own file offset (pwrite), so
   // multi-GB outputs are written in parallel; otherwise (pipe, terminal) parts go out in order.
-  // Blocks of 64 K rows per thread keep the buffers small (~5 MB per thread, reused): page-faulting
+  // Blocks of 64 K rows per part keep the buffers small (~5 MB per part, reused): page-faulting
   // fresh multi-100 MB buffers cost more than the formatting (1.2 s of 1.6 s for 33 M rows here).
   // A stream that is not a regular file (under mpiexec stdout is a pipe to the MPICH proxy) is written by
   // one background thread in order, double-buffered: block k goes out while block k+1 is formatted.
-  const int nthreads = n > 65536 ? omp_get_max_threads() : 1;
-  const int64_t kBlock = int64_t{65536} * nthreads;
+  // Parallel loops iterate over parts, not thread ids (OMP_DYNAMIC / thread limits deliver fewer threads).
+  const RowSource src(runs);
+  const int64_t n = src.total();
+  const int nparts = n > 65536 ? std::max(1, omp_get_max_threads()) : 1;
+  const int64_t kBlock = int64_t{65536} * nparts;
   std::fflush(f);
   const int fd = fileno(f);
   struct stat st;
   off_t file_pos = -1;
   // (not with O_APPEND: Linux pwrite then ignores the offset and the parts would land in completion order)
   const int fl = fcntl(fd, F_GETFL);
-  if (nthreads > 1 && fl >= 0 && !(fl & O_APPEND) && fstat(fd, &st) == 0 && S_ISREG(st.st_mode))
+  if (nparts > 1 && fl >= 0 && !(fl & O_APPEND) && fstat(fd, &st) == 0 && S_ISREG(st.st_mode))
     file_pos = lseek(fd, 0, SEEK_CUR);
   const bool ordered_async = file_pos < 0 && n > kBlock;
   std::vector<uvector<char>> part_sets[2];
   std::vector<size_t> used_sets[2];
   for (int s2 = 0; s2 < (ordered_async ? 2 : 1); ++s2) {
-    part_sets[s2].resize(static_cast<size_t>(nthreads));
-    used_sets[s2].assign(static_cast<size_t>(nthreads) + 1, 0);
+    part_sets[s2].resize(static_cast<size_t>(nparts));
+    used_sets[s2].assign(static_cast<size_t>(nparts) + 1, 0);
   }
   BackgroundReleaser writer;  // FIFO worker: ordered writes of the pipe path
-  bool write_error = false;
+  std::atomic<bool> write_error{false};
   std::atomic<bool> async_error{false};
   int set = 0;
   for (int64_t b = 0; b < n; b += kBlock) {
     const int64_t e = std::min(n, b + kBlock), m = e - b;
     std::vector<uvector<char>>& parts = part_sets[set];
     std::vector<size_t>& used = used_sets[set];
-#pragma omp parallel num_threads(nthreads)
-    {
-      const int t = omp_get_thread_num();
-      const int64_t rb = b + m * t / nthreads, re = b + m * (t + 1) / nthreads;
+#pragma omp parallel for schedule(static, 1) num_threads(nparts)
+    for (int t = 0; t < nparts; ++t) {
+      const int64_t rb = b + m * t / nparts, re = b + m * (t + 1) / nparts;
       uvector<char>& buf = parts[t];
       buf.resize(static_cast<size_t>(re - rb) * kMaxRow);
-      char* p = buf.data();
-      RowCounter idx(first_index + rb);
-      for (int64_t i = rb; i < re; ++i) p = format_row(p, idx, results[i]);
+      char* p = src.format(buf.data(), rb, re, first_index);
       used[t + 1] = static_cast<size_t>(p - buf.data());
-      if (file_pos >= 0) {
-#pragma omp barrier
-#pragma omp single
-        for (int q = 0; q < nthreads; ++q) used[q + 1] += used[q];  // used[t] = byte offset of part t
-        // (implicit barrier after single)
+    }
+    used[0] = 0;
+    if (file_pos >= 0) {
+      for (int q = 0; q < nparts; ++q) used[q + 1] += used[q];  // used[t] = byte offset of part t
+#pragma omp parallel for schedule(static, 1) num_threads(nparts)
+      for (int t = 0; t < nparts; ++t) {
         size_t done = 0;
         const size_t len = used[t + 1] - used[t];
         while (done < len) {
-          const ssize_t w = pwrite(fd, buf.data() + done, len - done, file_pos + static_cast<off_t>(used[t] + done));
+          const ssize_t w =
+              pwrite(fd, parts[t].data() + done, len - done, file_pos + static_cast<off_t>(used[t] + done));
           if (w <= 0) {
-#pragma omp atomic write
             write_error = true;
             break;
           }
           done += static_cast<size_t>(w);
         }
       }
-    }
-    if (file_pos >= 0) {
-      file_pos += static_cast<off_t>(used[nthreads]);
+      file_pos += static_cast<off_t>(used[nparts]);
     } else if (ordered_async) {
       writer.drain();  // the previous block (the other buffer set) is out: that set is free again
-      writer.defer([f, nthreads, &parts, &used, &async_error] {
-        for (int t = 0; t < nthreads; ++t)
+      writer.defer([f, nparts, &parts, &used, &async_error] {
+        for (int t = 0; t < nparts; ++t)
           if (std::fwrite(parts[t].data(), 1, used[t + 1], f) != used[t + 1]) async_error = true;
-        used[0] = 0;
       });
       set ^= 1;
-      continue;
     } else {
-      for (int t = 0; t < nthreads; ++t)
+      for (int t = 0; t < nparts; ++t)
         if (std::fwrite(parts[t].data(), 1, used[t + 1], f) != used[t + 1]) write_error = true;
     }
-    used[0] = 0;
   }
   writer.stop();
   if (async_error) write_error = true;

@@ -16,6 +16,7 @@
 #include "moc/problem.hpp"
 #include "moc/runtime/releaser.hpp"
 #include "moc/score_table.hpp"
+#include "moc/wire.hpp"
 
 using namespace moc;
 
@@ -416,12 +417,130 @@ void test_releaser() {
   idle.stop();
 }
 
+// Cooperative pass 1 + slice fills (the node-parallel parse of `final`): any chunk count, any slice,
+// byte and 5-bit packed output (incl. letters of one group split over pieces) equal a sequential parse.
+void test_slices() {
+  std::mt19937 rng(7);
+  for (int trial = 0; trial < 40; ++trial) {
+    const int n = 1 + static_cast<int>(rng() % 400);
+    const int maxlen = trial % 3 == 0 ? 40 : (trial % 3 == 1 ? 3 : 300);
+    std::string text = "1 2 3 4\nABCDEFGHIJKLMNOPQRSTUVWXYZABCDEFGHIJKLMNOPQRSTUVWXYZ\n" + std::to_string(n) + "\n";
+    std::vector<std::string> recs;
+    for (int i = 0; i < n; ++i) {
+      std::string r;
+      const int L = 1 + static_cast<int>(rng() % maxlen);
+      for (int j = 0; j < L; ++j) r += static_cast<char>((rng() & 1 ? 'A' : 'a') + rng() % 26);
+      recs.push_back(r);
+      text += r;
+      const int sep = static_cast<int>(rng() % 4);
+      text += sep == 0 ? "\n" : sep == 1 ? " \r\n" : sep == 2 ? "\t" : "\n\n  ";
+    }
+    if (trial % 5 == 0) text += "EXTRA TRAILING TOKENS\n";
+    const Problem ref = parse_problem(text.data(), text.size());
+    BulkParser p(text.data(), text.size(), ParseOptions{}, false);
+    CHECK(p.total_chars() < 0);
+    const int nch = 1 + static_cast<int>(rng() % 97);
+    std::vector<int64_t> st = p.chunk_starts(nch), tk(static_cast<size_t>(nch)), ch(static_cast<size_t>(nch));
+    // counted in two "ranks'" shares, like the distributed pass 1
+    const int mid = nch / 2;
+    p.count_chunks(st, 0, mid, tk.data(), ch.data());
+    p.count_chunks(st, mid, nch, tk.data() + mid, ch.data() + mid);
+    p.set_chunks(st, tk.data(), ch.data());
+    CHECK(p.total_chars() == ref.seq2.total_chars());
+    CHECK(p.chunk_first_record(0) == 0 && p.chunk_first_record(nch) == n);
+    for (int rep = 0; rep < 6; ++rep) {
+      int64_t b = rng() % (n + 1), e = rng() % (n + 1);
+      if (b > e) std::swap(b, e);
+      if (rep == 0) { b = 0; e = n; }
+      const AreaSlice s = p.slice(b, e);
+      CHECK(s.records == e - b);
+      CHECK(s.letters == ref.seq2.offsets[e] - ref.seq2.offsets[b]);
+      std::vector<uint8_t> codes(static_cast<size_t>(s.letters) + 1, 0xEE), packed(packed5_bytes(s.letters), 0xEE);
+      std::vector<int64_t> offs(static_cast<size_t>(s.records) + 1, -7);
+      const FillReport r = p.fill_slice(s, codes.data(), packed.data(), offs.data());
+      CHECK(r.bad_record < 0 && r.long_record < 0);
+      bool ok = true;
+      for (int64_t i = 0; i <= s.records; ++i) ok = ok && offs[i] == ref.seq2.offsets[b + i] - ref.seq2.offsets[b];
+      for (int64_t i = 0; i < s.letters; ++i) ok = ok && codes[i] == ref.seq2.codes[ref.seq2.offsets[b] + i];
+      CHECK(ok);
+      std::vector<uint8_t> want(packed5_bytes(s.letters));
+      pack5(ref.seq2.codes.data() + ref.seq2.offsets[b], s.letters, want.data());
+      CHECK(want == packed);
+      if (s.records) {
+        int64_t mn = INT64_MAX, mx = 0;
+        for (int64_t i = b; i < e; ++i) {
+          mn = std::min(mn, ref.seq2.length(i));
+          mx = std::max(mx, ref.seq2.length(i));
+        }
+        CHECK(r.min_len == mn && r.max_len == mx);
+        // packed-only fill (no byte codes) gives the same stream
+        std::vector<uint8_t> p2(packed5_bytes(s.letters), 0x55);
+        p.fill_slice(s, nullptr, p2.data(), offs.data());
+        CHECK(p2 == want);
+      }
+    }
+  }
+  // errors name the first offending record of the slice, in global numbering
+  const std::string bad = "1 2 3 4\nABCDEFGH\n5\nAB\nCD\nE1\nFG\nHIJKLMNOP\n";
+  BulkParser p(bad.data(), bad.size(), ParseOptions{false, 0, 4}, true);
+  FillReport r = p.fill_slice(p.slice(1, 5), nullptr, std::vector<uint8_t>(64).data(), std::vector<int64_t>(8).data());
+  CHECK(r.bad_record == 2 && r.long_record == 4 && r.long_len == 9);
+  CHECK(throws([&] { p.check(r); }, "record #2 contains a non-letter"));
+  r = p.fill_slice(p.slice(3, 5), nullptr, std::vector<uint8_t>(64).data(), std::vector<int64_t>(8).data());
+  CHECK(throws([&] { p.check(r); }, "record #4 has 9 letters"));
+}
+
+// Narrow record lengths (3 / 4 / 8 bits) round-trip through the host decoder.
+void test_narrow_lengths() {
+  std::mt19937 rng(3);
+  for (int bits : {3, 4, 8})
+    for (int n : {0, 1, 7, 8, 9, 1000, 100003}) {
+      const int span = bits == 3 ? 8 : bits == 4 ? 16 : 200;
+      std::vector<int64_t> offs(static_cast<size_t>(n) + 1, 0);
+      for (int i = 0; i < n; ++i) offs[i + 1] = offs[i] + 6 + static_cast<int64_t>(rng() % span);
+      std::vector<uint8_t> out(static_cast<size_t>(narrow_lengths_bytes(n, bits)) + 1, 0xAB);
+      pack_lengths(offs.data(), n, bits, 6, out.data());
+      bool ok = true;
+      for (int i = 0; i < n; ++i) ok = ok && narrow_length(out.data(), bits, 6, i) == offs[i + 1] - offs[i];
+      CHECK(ok);
+      if (bits == 3) CHECK(out[narrow_lengths_bytes(n, 3) - 1] == 0);
+    }
+  CHECK(narrow_length_bits(6, 11) == 3 && narrow_length_bits(6, 21) == 4 && narrow_length_bits(1, 255) == 8);
+  CHECK(narrow_length_bits(1, 256) == 0);
+}
+
+// Every result wire format decodes back to the rows it encodes.
+void test_result_formats() {
+  R2Params p;
+  CHECK(r2_params(26, 6, 11, -10, 4, p));
+  const Result rows[3] = {{-20, 3, 5}, {44, 0, 0}, no_candidate()};
+  uint16_t r2[3];
+  for (int i = 0; i < 2; ++i)
+    r2[i] = static_cast<uint16_t>((rows[i].score - p.smin) * p.j + rows[i].n * p.kw + rows[i].k);
+  r2[2] = kR2None;
+  R4 r4[3];
+  R8 r8[3];
+  for (int i = 0; i < 3; ++i) {
+    r4[i] = R4{static_cast<int16_t>(i == 2 ? INT16_MIN : rows[i].score), static_cast<uint8_t>(rows[i].n),
+               static_cast<uint8_t>(rows[i].k)};
+    r8[i] = R8{rows[i].score, static_cast<uint16_t>(rows[i].n), static_cast<uint16_t>(rows[i].k)};
+  }
+  bool ok = true;
+  for (int i = 0; i < 3; ++i) {
+    const Result a = decode_result(r2, ResultFormat::R2, p, i), b = decode_result(r4, ResultFormat::R4, p, i),
+                 c = decode_result(r8, ResultFormat::R8, p, i), d = decode_result(rows, ResultFormat::R12, p, i);
+    for (const Result& x : {a, b, c, d}) ok = ok && x.score == rows[i].score && x.n == rows[i].n && x.k == rows[i].k;
+  }
+  CHECK(ok);
+}
+
 int main() {
   const std::vector<std::pair<const char*, std::function<void()>>> tests = {
       {"score_table", test_score_table}, {"parser", test_parser},     {"stream_reader", test_stream_reader},
       {"partition", test_partition},     {"keys", test_keys},         {"pack5", test_pack5},
       {"engine_vs_brute_force", test_engine_vs_brute_force},          {"formatter", test_formatter},
-      {"profile16", test_profile16},     {"releaser", test_releaser}};
+      {"profile16", test_profile16},     {"releaser", test_releaser},   {"slices", test_slices},
+      {"narrow_lengths", test_narrow_lengths}, {"result_formats", test_result_formats}};
   for (const auto& t : tests) {
     const int before = g_failed;
     t.second();

@@ -289,3 +289,22 @@ def test_pipe_output_double_buffered(tmp_path):
                   env={"OMP_NUM_THREADS": "2"}, timeout=300)
     assert r.returncode == 0, r.stderr.decode()
     assert out.read_bytes() == want
+
+
+@pytest.mark.parametrize("omp_env", [{"OMP_DYNAMIC": "true", "OMP_NUM_THREADS": "8"},
+                                     {"OMP_THREAD_LIMIT": "2", "OMP_NUM_THREADS": "6"}])
+def test_fewer_omp_threads_than_requested(tmp_path, omp_env):
+    # parser passes, formatter and pwrite writer iterate over parts, not thread ids: a runtime that delivers
+    # fewer threads than asked (OMP_DYNAMIC, OMP_THREAD_LIMIT) must still process every part
+    from mpi_openmp_cuda_amd import format_results, make_synthetic, search_cpu
+
+    prob = make_synthetic("input6", 150000, seed=12)
+    path = tmp_path / "in.txt"
+    path.write_text(prob.to_text())
+    want = format_results(search_cpu(prob))
+    out = tmp_path / "out.txt"
+    for extra in ([], [f"--output={out}"], ["--batch-records=40000"]):
+        r = run_final(["--backend=cpu", f"--input={path}"] + extra, stdin_bytes=b"", np_=2, env=omp_env)
+        assert r.returncode == 0, r.stderr.decode()
+        got = out.read_text() if extra and extra[0].startswith("--output") else r.stdout.decode()
+        assert got == want
