@@ -36,7 +36,7 @@ GPU_PLUGIN := mpi_openmp_cuda_amd/lib/libmoc_final_gpu.so
 
 # host core without any ROCm dependency (parser, CPU engine, partitioner, runtime utilities)
 CPU_SRCS  := csrc/src/cpu_engine.cpp csrc/src/io.cpp csrc/src/partition.cpp csrc/src/problem.cpp csrc/src/wire.cpp \
-             csrc/src/score_table.cpp csrc/src/runtime/runtime.cpp
+             csrc/src/score_table.cpp csrc/src/runtime/runtime.cpp csrc/src/runtime/host_region.cpp
 # host code of the GPU engine (HIP runtime API) and the C ABI of libmoc.so
 GPU_SRCS  := csrc/src/hip_engine.cpp csrc/src/capi.cpp csrc/src/runtime/device.cpp csrc/src/runtime/pinned.cpp
 CORE_SRCS := $(CPU_SRCS) $(GPU_SRCS)
@@ -75,6 +75,20 @@ $(MPILIB)/libmpi.so:
 	ln -sf $(MPI_HOME)/lib/libmpi.so.12 $(MPILIB)/libmpi.so
 	ln -sf $(MPI_HOME)/lib/libgfortran.so.4 $(MPILIB)/libgfortran.so.4
 	ln -sf $(MPI_HOME)/lib/libquadmath.so.0 $(MPILIB)/libquadmath.so.0
+
+# Build identity baked into ./final (--help, --timing): a hash of the native sources (every file under
+# csrc/ plus this Makefile, in sorted order — tests/test_cli.py recomputes it, so a stale prebuilt binary
+# shipped next to newer sources is caught even where no .git exists) and the git commit when known.
+# The stamp file changes only when the identity does, so an unchanged tree does not relink.
+SRC_FILES := $(sort $(wildcard csrc/* csrc/*/* csrc/*/*/* csrc/*/*/*/* csrc/*/*/*/*/*) Makefile)
+SRC_HASH  := $(shell cat $(SRC_FILES) 2>/dev/null | sha1sum | cut -c1-12)
+GIT_HASH  := $(shell git rev-parse --short=12 HEAD 2>/dev/null || echo unknown)
+BUILD_ID  := $(BUILD)/build_id
+$(shell mkdir -p $(BUILD); echo 'src=$(SRC_HASH) git=$(GIT_HASH)' | cmp -s - $(BUILD_ID) || echo 'src=$(SRC_HASH) git=$(GIT_HASH)' > $(BUILD_ID))
+
+$(OBJ)/apps/final.o: csrc/apps/final.cpp $(HEADERS) $(BUILD_ID)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) $(MPIFLAGS) -DMOC_BUILD_ID='"src=$(SRC_HASH) git=$(GIT_HASH)"' -c $< -o $@
 
 $(OBJ)/apps/%.o: csrc/apps/%.cpp $(HEADERS)
 	@mkdir -p $(dir $@)

@@ -39,6 +39,7 @@
 #include "moc/partition.hpp"
 #include "moc/problem.hpp"
 #include "moc/runtime/flags.hpp"
+#include "moc/runtime/host_region.hpp"
 #include "moc/runtime/log.hpp"
 #include "moc/runtime/timer.hpp"
 #include "moc/runtime/trace.hpp"
@@ -47,6 +48,13 @@
 using namespace moc;
 
 namespace {
+
+#ifndef MOC_BUILD_ID
+#define MOC_BUILD_ID "src=unknown git=unknown"
+#endif
+// The sources this binary was built from (Makefile: a hash over csrc/ + Makefile, and the git commit):
+// printed by --help and --timing so a test can tell a stale prebuilt binary from the checked-out source.
+const char* kBuildId = MOC_BUILD_ID;
 
 const char* kUsage =
     "usage: mpiexec -np N ./final [options] < input.txt\n"
@@ -88,6 +96,7 @@ struct Header {
   int64_t n_total;      // number_of_sequences
   int64_t first_index;  // --skip-records actually applied
   int64_t cells;        // search cells of the job (-1: unknown, streaming)
+  int64_t text_bytes;   // bytes of the input text (sliced mode)
 };
 
 struct BatchHeader {
@@ -234,6 +243,7 @@ class Job {
  private:
   void setup_engine(int64_t cells);
   void run_batch(RecordBatch* rb, int64_t n, int64_t total_chars, int64_t first_index);
+  void run_sliced(BulkParser& parser, int64_t first_index);
   void batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, bool cp);
   std::vector<int64_t> make_bounds(const int64_t* offsets, int64_t n, bool cp);
   void batch_mpi(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds, bool cp);
@@ -258,6 +268,9 @@ class Job {
   uvector<char> text_;                 // root: the input (kept for deferred parsing)
   FILE* out_ = stdout;                 // root: --output file, else stdout
   std::unique_ptr<BulkParser> parser_;  // root: pass 1 done, letters encoded straight into the window
+  std::unique_ptr<SharedWindow> text_win_;  // sliced mode, several ranks on the node: the input text
+  int64_t pinned_bytes_ = 0, h2d_bytes_ = 0, d2h_bytes_ = 0;  // this rank (--timing)
+  std::vector<int64_t> rank_pinned_, rank_h2d_, rank_records_;  // root: per-rank figures (--timing)
   std::shared_ptr<BulkParser> spent_parser_;     // root: filled into the window, freed while printing
   std::shared_ptr<uvector<char>> spent_text_;
   std::vector<Result> results_;  // root: results of the current batch (mpi/rccl transports)
@@ -460,6 +473,246 @@ void Job::batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, bool cp) {
   pt_.end();
 }
 
+// Bulk job on one node, records split into contiguous rank slices (transport shm, partition cost|even).
+// Every rank encodes its OWN slice straight from the node-shared input text into its own buffers, in the
+// wire formats its engine streams (SURVEY.md §7.3 / moc/wire.hpp):
+//   GPU rank: 5-bit packed letters + 3/4/8-bit lengths + sparse offsets (1 per 64 records) in private,
+//             huge-page memory on its GPU's NUMA node, page-locked (only this slice), results in the
+//             narrowest format (R2/R4/R8/R12) in this rank's segment of a node-shared result window;
+//   CPU rank: byte letters + CSR offsets, results as R12.
+// Pass 1 (token/letter counts) is cooperative: each rank counts a share of the text's chunks and the
+// counts are all-gathered, so every rank holds the same chunk table and computes its own bounds from it
+// (BulkParser::cost_split) without a further collective. The root prints from every rank's result segment
+// in place (reference: MPI_Scatter of 2000-byte records + 3 MPI_Gathers, main.c:174,195-197).
+void Job::run_sliced(BulkParser& parser, int64_t first_index) {
+  const int p = ctx_.size, r = ctx_.rank;
+  ++batches_;
+  first_index_ = first_index;
+  const int64_t L1 = static_cast<int64_t>(eng_.seq1.size());
+  const bool gpu = eng_.gpu;
+  const int numa = gpu ? eng_.hip->numa_node() : -1;
+
+  const CostModel cost_model = all_gpu_ ? CostModel{1.0, 200.0, 2400.0} : CostModel{1.0, 4.0, 64.0};
+  // ---- pass 1, cooperative
+  pt_.begin("count");
+  const int64_t area = parser.area_bytes();
+  const int nch = static_cast<int>(std::clamp<int64_t>(std::max(area >> 20, std::min<int64_t>(area >> 16, 64 * p)), 1,
+                                                       int64_t{1} << 14));
+  std::vector<int64_t> starts = parser.chunk_starts(nch);
+  std::vector<int64_t> tk(static_cast<size_t>(nch)), ch(static_cast<size_t>(nch));
+  {
+    std::vector<int> cnt(p), dsp(p);
+    for (int q = 0; q < p; ++q) {
+      dsp[q] = static_cast<int>(int64_t{nch} * q / p);
+      cnt[q] = static_cast<int>(int64_t{nch} * (q + 1) / p) - dsp[q];
+    }
+    parser.count_chunks(starts, dsp[r], dsp[r] + cnt[r], tk.data() + dsp[r], ch.data() + dsp[r]);
+    MPI_Allgatherv(MPI_IN_PLACE, 0, MPI_DATATYPE_NULL, tk.data(), cnt.data(), dsp.data(), MPI_INT64_T, ctx_.world);
+    MPI_Allgatherv(MPI_IN_PLACE, 0, MPI_DATATYPE_NULL, ch.data(), cnt.data(), dsp.data(), MPI_INT64_T, ctx_.world);
+    // inputs up to 256 MiB also get exact chunk costs (a token walk) for the bounds: few, coarse chunks
+    // of records of very different lengths are what the mean-length estimate gets wrong
+    if (partition_ != "even" && p > 1 && area <= (int64_t{256} << 20)) {
+      std::vector<double> costs(static_cast<size_t>(nch));
+      parser.chunk_costs(starts, dsp[r], dsp[r] + cnt[r], cost_model, costs.data() + dsp[r]);
+      MPI_Allgatherv(MPI_IN_PLACE, 0, MPI_DATATYPE_NULL, costs.data(), cnt.data(), dsp.data(), MPI_DOUBLE, ctx_.world);
+      parser.set_chunk_costs(std::move(costs));
+    }
+  }
+  try {
+    parser.set_chunks(std::move(starts), tk.data(), ch.data());
+  } catch (const std::exception& e) {
+    throw InputError(e.what());
+  }
+  const int64_t n_all = parser.count();
+  first_index = std::min(first_index, n_all);
+  records_ += n_all - first_index;
+  pt_.end();
+
+  // ---- this rank's slice
+  pt_.begin("bounds");
+  int64_t b0, b1;
+  if (partition_ == "even") {
+    b0 = first_index + (n_all - first_index) * r / p;
+    b1 = first_index + (n_all - first_index) * (r + 1) / p;
+  } else {
+    b0 = parser.cost_split(first_index, r, p, cost_model);
+    b1 = std::max(b0, parser.cost_split(first_index, r + 1, p, cost_model));
+  }
+  const AreaSlice slice = parser.slice(b0, b1);
+  const int64_t n = slice.records;
+  pt_.end();
+
+  // ---- fill: every rank encodes its slice (GPU ranks guess the narrow form from the mean length)
+  pt_.begin("fill");
+  fault_.at("distribute", r);
+  const bool narrow_guess = gpu && n > 0 && L1 <= 200 && slice.letters <= 32 * n;
+  HostRegion letters, sparse, len16, dense, lens;
+  RecordBatch cpu_batch;
+  FillReport rep;
+  if (n > 0) {
+    if (!gpu) {
+      cpu_batch.codes.resize(static_cast<size_t>(slice.letters));
+      cpu_batch.offsets.resize(static_cast<size_t>(n) + 1);
+      rep = parser.fill_slice(slice, cpu_batch.codes.data(), nullptr, cpu_batch.offsets.data());
+    } else {
+      letters = HostRegion(static_cast<size_t>(packed5_bytes(slice.letters)) + 16, numa);
+      if (narrow_guess) {
+        sparse = HostRegion(8 * static_cast<size_t>(sparse_count(n, kSparseShift)), numa);
+        len16 = HostRegion(2 * static_cast<size_t>(n), numa);
+        rep = parser.fill_slice(slice, nullptr, letters.as<uint8_t>(), nullptr, sparse.as<int64_t>(),
+                                len16.as<uint16_t>());
+      } else {
+        dense = HostRegion(8 * (static_cast<size_t>(n) + 1), numa);
+        rep = parser.fill_slice(slice, nullptr, letters.as<uint8_t>(), dense.as<int64_t>());
+      }
+    }
+  }
+  // the job's first input error (the one a sequential reader meets first) on every rank
+  {
+    int64_t mine[7] = {rep.min_len, rep.max_len, rep.bad_record, rep.long_record, rep.long_len, rep.cells,
+                       slice.letters};
+    std::vector<int64_t> all(static_cast<size_t>(7 * p));
+    MPI_Allgather(mine, 7, MPI_INT64_T, all.data(), 7, MPI_INT64_T, ctx_.world);
+    FillReport job;
+    for (int q = 0; q < p; ++q) {
+      const int64_t* x = all.data() + 7 * q;
+      chars_ += x[6];
+      job.min_len = std::min(job.min_len, x[0]);
+      job.max_len = std::max(job.max_len, x[1]);
+      if (x[2] >= 0 && (job.bad_record < 0 || x[2] < job.bad_record)) job.bad_record = x[2];
+      if (x[3] >= 0 && (job.long_record < 0 || x[3] < job.long_record)) {
+        job.long_record = x[3];
+        job.long_len = x[4];
+      }
+      job.cells += x[5];
+    }
+    cells_ += job.cells;
+    try {
+      parser.check(job);
+    } catch (const std::exception& e) {
+      throw InputError(e.what());
+    }
+  }
+  // GPU ranks: the wire form the engine streams
+  WireBatch wb;
+  ResultFormat fmt = ResultFormat::R12;
+  if (gpu && n > 0) {
+    wb.letters = letters.as<uint8_t>();
+    wb.packed5 = true;
+    wb.n = n;
+    wb.min_l2 = rep.min_len;
+    wb.max_l2 = rep.max_len;
+    if (narrow_guess && rep.max_len <= 255 && eng_.hip->streams_packed(rep.min_len, rep.max_len)) {
+      const int bits = narrow_length_bits(rep.min_len, rep.max_len);
+      lens = HostRegion(static_cast<size_t>(narrow_lengths_bytes(n, bits)), numa);
+      pack_lengths16(len16.as<uint16_t>(), n, bits, rep.min_len, lens.as<uint8_t>());
+      len16 = HostRegion();
+      wb.offsets = sparse.as<int64_t>();
+      wb.off_shift = kSparseShift;
+      wb.lengths = lens.as<uint8_t>();
+      wb.len_bits = bits;
+      wb.len_base = bits == 8 ? 0 : rep.min_len;
+    } else {
+      if (narrow_guess) {  // guessed wrong: CSR offsets after all (staged pipeline)
+        sparse = HostRegion();
+        len16 = HostRegion();
+        dense = HostRegion(8 * (static_cast<size_t>(n) + 1), numa);
+        parser.fill_slice(slice, nullptr, letters.as<uint8_t>(), dense.as<int64_t>());
+      }
+      wb.offsets = dense.as<int64_t>();
+    }
+    fmt = eng_.hip->result_format(rep.min_len, rep.max_len);
+  }
+  pt_.end();
+
+  // ---- results: this rank's segment of the node-shared window
+  const int fb = result_bytes(fmt);
+  SegmentWindow res(ctx_, fb * n, numa);
+  res.set_releaser(&rel_);
+  pt_.begin("compute");
+  fault_.at("compute", r);
+  Stopwatch sw;
+  sw.start();
+  GpuSolveStats gs;
+  if (n > 0) {
+    if (gpu) {
+      if (pin_window_) {  // this slice's pieces only
+        try {
+          auto pin = [&](const void* ptr, int64_t bytes) {
+            if (ptr && bytes > 0) {
+              eng_.hip->pin(ptr, static_cast<size_t>(bytes));
+              pinned_bytes_ += bytes;
+            }
+          };
+          pin(wb.letters, packed5_bytes(slice.letters));
+          pin(wb.offsets, 8 * wb.offset_entries());
+          pin(wb.lengths, wb.length_bytes());
+          pin(res.mine(), fb * n);
+        } catch (const std::exception& e) {
+          MOC_LOG_WARN("could not page-lock this rank's slice (%s); using the staged pipeline", e.what());
+        }
+      }
+      eng_.hip->solve_wire(wb, res.mine(), fmt);
+      gs = eng_.hip->last_stats();
+      eng_.kernel_ms += gs.kernel_ms;
+      h2d_bytes_ += gs.h2d_bytes;
+      d2h_bytes_ += gs.d2h_bytes;
+      eng_.hip->unpin_all();
+    } else {
+      solve_batch_cpu(eng_.table, eng_.seq1.data(), L1, cpu_batch, reinterpret_cast<Result*>(res.mine()), eng_.sem,
+                      eng_.threads);
+    }
+  }
+  sw.stop();
+  compute_ms_ += sw.total_ms();
+  pt_.end();
+  // inputs nobody reads any more go back to the OS while the root prints
+  letters.set_releaser(&rel_);
+  sparse.set_releaser(&rel_);
+  dense.set_releaser(&rel_);
+  lens.set_releaser(&rel_);
+  { HostRegion drop[4] = {std::move(letters), std::move(sparse), std::move(dense), std::move(lens)}; }
+  cpu_batch = RecordBatch{};
+
+  // ---- every rank's result run -> root, which prints them in order straight from the segments
+  pt_.begin("gather");
+  fault_.at("gather", r);
+  int64_t info[7] = {n, static_cast<int64_t>(fmt), gs.r2.smin, gs.r2.kw, gs.r2.j, pinned_bytes_, h2d_bytes_};
+  std::vector<int64_t> infos(r == kRoot ? static_cast<size_t>(7 * p) : 0);
+  MPI_Gather(info, 7, MPI_INT64_T, infos.data(), 7, MPI_INT64_T, kRoot, ctx_.world);
+  res.fence();
+  pt_.end();
+  if (r == kRoot) {
+    std::vector<ResultRun> runs(static_cast<size_t>(p));
+    rank_pinned_.assign(static_cast<size_t>(p), 0);
+    rank_h2d_.assign(static_cast<size_t>(p), 0);
+    rank_records_.assign(static_cast<size_t>(p), 0);
+    for (int q = 0; q < p; ++q) {
+      const int64_t* x = infos.data() + 7 * q;
+      runs[q].data = res.segment(q);
+      runs[q].n = x[0];
+      runs[q].fmt = static_cast<ResultFormat>(x[1]);
+      runs[q].r2 = R2Params{static_cast<int32_t>(x[2]), static_cast<int32_t>(x[3]), static_cast<int32_t>(x[4])};
+      rank_records_[q] = x[0];
+      rank_pinned_[q] = x[5];
+      rank_h2d_[q] = x[6];
+    }
+    // a private input text goes back to the OS while the results print
+    if (!text_.empty()) {
+      auto t = std::make_shared<uvector<char>>(std::move(text_));
+      rel_.defer([t]() mutable { t.reset(); });
+      text_ = uvector<char>();
+    }
+    pt_.begin("print");
+    write_results(out_, runs, first_index);
+    pt_.end();
+  }
+  pt_.begin("release");
+  res.fence();  // nobody unmaps a segment the root still prints from
+  text_win_.reset();  // collective (node-shared input text)
+  pt_.end();
+}
+
 void Job::batch_mpi(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds, bool cp) {
   const int p = ctx_.size;
   pt_.begin("distribute");
@@ -554,15 +807,25 @@ void Job::report(const Header& h) {
   MPI_Reduce(ctx_.rank == kRoot ? MPI_IN_PLACE : mx, mx, 2, MPI_DOUBLE, MPI_MAX, kRoot, ctx_.world);
   if (ctx_.rank != kRoot || !flags_.get_bool("timing", false)) return;
   const double wall_s = total_.total_ms() / 1e3;
+  auto list = [](const std::vector<int64_t>& v) {
+    std::string s = "[";
+    for (size_t i = 0; i < v.size(); ++i) s += (i ? ", " : "") + std::to_string(v[i]);
+    return s + "]";
+  };
+  std::string per_rank;
+  if (!rank_records_.empty())  // sliced mode: what each rank owned, page-locked and moved host->device
+    per_rank = ", \"rank_records\": " + list(rank_records_) + ", \"rank_pinned_bytes\": " + list(rank_pinned_) +
+               ", \"rank_h2d_bytes\": " + list(rank_h2d_);
   std::fprintf(stderr,
                "{\"timing\": %s, \"ranks\": %d, \"nodes\": %d, \"engine\": \"%s\", \"transport\": \"%s\", "
-               "\"partition\": \"%s\", \"batches\": %lld, \"first_index\": %lld, \"records\": %lld, "
+               "\"partition\": \"%s\", \"sliced\": %s, \"batches\": %lld, \"first_index\": %lld, \"records\": %lld, "
                "\"elements\": %lld, \"cells\": %lld, \"max_rank_compute_ms\": %.3f, \"max_rank_kernel_ms\": %.3f, "
-               "\"wall_s\": %.6f, \"elements_per_s\": %.1f, \"cells_per_s\": %.1f}\n",
+               "\"wall_s\": %.6f, \"elements_per_s\": %.1f, \"cells_per_s\": %.1f%s, \"build\": \"%s\"}\n",
                pt_.json().c_str(), ctx_.size, ctx_.node_count, eng_.gpu ? "hip" : "cpu", transport_.c_str(),
-               partition_.c_str(), static_cast<long long>(batches_), static_cast<long long>(h.first_index),
-               static_cast<long long>(records_), static_cast<long long>(chars_), static_cast<long long>(cells_),
-               mx[0], mx[1], wall_s, wall_s > 0 ? chars_ / wall_s : 0.0, wall_s > 0 ? cells_ / wall_s : 0.0);
+               partition_.c_str(), rank_records_.empty() ? "false" : "true", static_cast<long long>(batches_),
+               static_cast<long long>(h.first_index), static_cast<long long>(records_), static_cast<long long>(chars_),
+               static_cast<long long>(cells_), mx[0], mx[1], wall_s, wall_s > 0 ? chars_ / wall_s : 0.0,
+               wall_s > 0 ? cells_ / wall_s : 0.0, per_rank.c_str(), kBuildId);
 }
 
 int Job::run() {
@@ -607,15 +870,22 @@ int Job::run() {
     if (hint) prewarm_ = std::async(std::launch::async, [] { (void)gpu_device_count(); });
   }
 
-  // ---- root opens the input; parses it whole (bulk) or just its header (streaming)
+  // ---- root opens the input; parses it whole (bulk) or just its header (streaming). A bulk job on one
+  // node (shm transport) with record slices runs "sliced": every rank encodes its own slice from the
+  // input text, which is then read into a node-shared window when the node has several ranks.
+  const std::string tr_flag = to_lower(flags_.get("transport", "auto"));
+  const bool sliced = !streaming && to_lower(flags_.get("partition", "cost")) != "offsets" &&
+                      (tr_flag == "shm" || (tr_flag == "auto" && ctx_.single_node()));
   Header h{};
   std::string error;
   FILE* in = stdin;
   std::unique_ptr<StreamReader> reader;
   RecordBatch bulk;
   std::vector<uint8_t> seq1;
+  const char* text = nullptr;  // sliced: the input text (every rank)
+  int64_t text_len = 0;
   if (ctx_.rank == kRoot) {
-    pt_.begin("parse");
+    pt_.begin("read");
     try {
       fault_.at("parse", ctx_.rank);
       const std::string path = flags_.get("input", "");
@@ -625,6 +895,58 @@ int Job::run() {
         out_ = stdout;
         throw Error("cannot open --output " + opath);
       }
+      if (sliced && ctx_.local_size > 1) {
+        text_len = regular_input_bytes(in);  // read straight into the shared window below
+        if (text_len < 0) {                  // a pipe: read it all first
+          text_ = read_stream(in);
+          text_len = static_cast<int64_t>(text_.size());
+        }
+      } else if (!streaming) {
+        text_ = read_stream(in);
+        text_len = static_cast<int64_t>(text_.size());
+        text = text_.data();
+      }
+    } catch (const std::exception& e) {
+      error = e.what();
+      h.status = 1;
+    }
+    pt_.end();
+  }
+  if (sliced && ctx_.local_size > 1) {
+    int64_t sz[2] = {h.status, text_len};
+    bcast_bytes(sz, sizeof sz, kRoot, ctx_.world);
+    if (sz[0] != 0) {
+      if (ctx_.rank == kRoot) std::fprintf(stderr, "input error: %s\n", error.c_str());
+      if (in != stdin && in) std::fclose(in);
+      return 1;
+    }
+    text_len = sz[1];
+    text_win_ = std::make_unique<SharedWindow>(ctx_, text_len + 64);
+    text = text_win_->base();
+    if (ctx_.rank == kRoot) {
+      pt_.begin("read");
+      try {
+        if (!text_.empty()) {
+          const int64_t nt = text_len > (int64_t{1} << 24) ? omp_get_max_threads() : 1;
+#pragma omp parallel for schedule(static, 1) num_threads(static_cast<int>(nt))
+          for (int64_t t = 0; t < nt; ++t) {
+            const int64_t b = text_len * t / nt, e = text_len * (t + 1) / nt;
+            std::memcpy(text_win_->base() + b, text_.data() + b, static_cast<size_t>(e - b));
+          }
+          text_ = uvector<char>();
+        } else {
+          text_len = static_cast<int64_t>(read_regular_into(in, text_win_->base(), static_cast<size_t>(text_len)));
+        }
+      } catch (const std::exception& e) {
+        error = e.what();
+        h.status = 1;
+      }
+      pt_.end();
+    }
+  }
+  if (ctx_.rank == kRoot && h.status == 0) {
+    pt_.begin("parse");
+    try {
       Weights w{};
       if (streaming) {
         reader = std::make_unique<StreamReader>(in, po);
@@ -634,17 +956,16 @@ int Job::run() {
         h.first_index = reader->skip(skip);
         h.cells = -1;
       } else {
-        text_ = read_stream(in);
-        auto parser = std::make_unique<BulkParser>(text_.data(), text_.size(), po);  // header + pass 1
+        // header (+ pass 1 unless sliced: the ranks count their shares of the text then)
+        auto parser = std::make_unique<BulkParser>(text, static_cast<size_t>(text_len), po, !sliced);
         w = parser->weights();
         seq1 = parser->seq1();
         h.n_total = parser->count();
         h.first_index = std::min<int64_t>(skip, h.n_total);
         h.cells = parser->cells_estimate();
-        // shm transport (the single-node default) without a skip: pass 2 later writes straight into
-        // the node-shared window; otherwise encode now into a private batch
-        const std::string tr = to_lower(flags_.get("transport", "auto"));
-        const bool into_window = h.first_index == 0 && (tr == "shm" || (tr == "auto" && ctx_.single_node()));
+        // shm transport without a skip: pass 2 later writes straight into the node-shared window (sliced:
+        // into every rank's own buffers); otherwise encode now into a private batch
+        const bool into_window = sliced || (h.first_index == 0 && (tr_flag == "shm" || (tr_flag == "auto" && ctx_.single_node())));
         if (into_window) {
           parser_ = std::move(parser);
         } else {
@@ -656,6 +977,7 @@ int Job::run() {
         }
       }
       for (int i = 0; i < 4; ++i) h.w[i] = w.w[i];
+      h.text_bytes = text_len;
     } catch (const std::exception& e) {
       error = e.what();
       h.status = 1;
@@ -685,7 +1007,23 @@ int Job::run() {
   pt_.end();
 
   int rc = 0;
-  if (!streaming) {
+  if (sliced) {
+    std::unique_ptr<BulkParser> own;
+    if (ctx_.rank != kRoot) {  // the header again, from the shared text (no pass 1: counted together)
+      if (text_win_) text_win_->fence();
+      own = std::make_unique<BulkParser>(text, static_cast<size_t>(h.text_bytes), po, false);
+    } else if (text_win_) {
+      text_win_->fence();
+    }
+    try {
+      run_sliced(ctx_.rank == kRoot ? *parser_ : *own, h.first_index);
+    } catch (const InputError& e) {
+      if (ctx_.rank == kRoot) std::fprintf(stderr, "input error: %s\n", e.what());
+      if (in != stdin && in) std::fclose(in);
+      return 1;
+    }
+    parser_.reset();
+  } else if (!streaming) {
     int64_t sizes[2] = {bulk.size(), bulk.total_chars()};
     if (parser_) {
       sizes[0] = parser_->count();
@@ -760,7 +1098,7 @@ int main(int argc, char** argv) {
   try {
     Flags flags(argc, argv);
     if (flags.get_bool("help", false)) {
-      if (ctx.rank == kRoot) std::fputs(kUsage, stdout);
+      if (ctx.rank == kRoot) std::printf("%sbuild: %s\n", kUsage, kBuildId);
       return 0;
     }
     auto unknown = flags.unknown(kKnown);

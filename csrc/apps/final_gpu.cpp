@@ -33,6 +33,9 @@ class GpuRankImpl final : public GpuRank {
     if (opt.chunk_records > 0) eo.chunk_records = opt.chunk_records;
     if (opt.chunk_bytes > 0) eo.chunk_bytes = opt.chunk_bytes;
     engine_ = std::make_unique<HipEngine>(eo);
+    // host buffers this rank's GPU streams over PCIe, and the threads that fill them, on the NUMA node
+    // of the GPU's root complex
+    numa_ = bind_numa_to_device(device_);
   }
   void init_rccl() override {
     if (!nccl_) nccl_ = std::make_unique<RcclComm>(ctx_, device_);
@@ -49,6 +52,25 @@ class GpuRankImpl final : public GpuRank {
     engine_->search_keys(codes, offsets, n, part, parts, keys);
   }
   double last_kernel_ms() const override { return engine_->stats().kernel_ms; }
+  int numa_node() const override { return numa_; }
+  void solve_wire(const WireBatch& b, void* out, ResultFormat fmt) override { engine_->solve_wire(b, out, fmt); }
+  bool streams_packed(int64_t min_l2, int64_t max_l2) const override {
+    return engine_->streams_packed(min_l2, max_l2);
+  }
+  ResultFormat result_format(int64_t min_l2, int64_t max_l2) const override {
+    return engine_->auto_format(max_l2, min_l2);
+  }
+  GpuSolveStats last_stats() const override {
+    const EngineStats& st = engine_->stats();
+    GpuSolveStats g;
+    g.kernel_ms = st.kernel_ms;
+    g.h2d_bytes = st.h2d_bytes;
+    g.d2h_bytes = st.d2h_bytes;
+    g.kernels = st.kernels;
+    g.direct = st.direct;
+    g.r2 = st.r2;
+    return g;
+  }
   void pin(const void* p, size_t bytes) override { engine_->pin(p, bytes); }
   void unpin_all() override { engine_->unpin_all(); }
   double rccl_batch(const RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds, bool cp,
@@ -57,6 +79,7 @@ class GpuRankImpl final : public GpuRank {
  private:
   const MpiContext& ctx_;
   int device_ = -1;
+  int numa_ = -1;
   std::unique_ptr<HipEngine> engine_;
   std::unique_ptr<RcclComm> nccl_;
 };

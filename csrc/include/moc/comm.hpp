@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "moc/common.hpp"
+#include "moc/runtime/host_region.hpp"
 #include "moc/runtime/releaser.hpp"
 
 namespace moc {
@@ -85,5 +86,28 @@ class SharedWindow {
   BackgroundReleaser* releaser_ = nullptr;
 };
 
+// Per-rank segments of one node-shared window: every rank of the node allocates its own segment (its
+// result slice), placed on the owner's NUMA node (MPI's noncontiguous allocation + a memory-policy
+// binding by the owner before its first touch), and every rank can address every segment — the root
+// prints straight from them, so no gather copy exists. A node with one rank maps private memory.
+class SegmentWindow {
+ public:
+  // Collective over ctx.node. numa_node >= 0 binds this rank's segment there.
+  SegmentWindow(const MpiContext& ctx, int64_t my_bytes, int numa_node = -1);
+  ~SegmentWindow();
+  SegmentWindow(const SegmentWindow&) = delete;
+  SegmentWindow& operator=(const SegmentWindow&) = delete;
+  char* mine() const { return segment(local_rank_); }
+  char* segment(int local_rank) const { return seg_[static_cast<size_t>(local_rank)]; }
+  void fence() const;  // MPI_Win_sync + node barrier: makes every owner's writes visible
+  void set_releaser(BackgroundReleaser* rel) { region_.set_releaser(rel); }
+
+ private:
+  MPI_Win win_ = MPI_WIN_NULL;
+  MPI_Comm comm_ = MPI_COMM_NULL;
+  int local_rank_ = 0;
+  std::vector<char*> seg_;
+  HostRegion region_;  // one rank on the node
+};
 
 }  // namespace moc

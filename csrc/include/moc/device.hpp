@@ -110,7 +110,9 @@ struct Plan {
 // pinned host memory (hipHostMalloc / hipHostRegister) for zero-copy streaming.
 struct ShortArgs {
   const uint8_t* codes = nullptr;     // base pointer: record i starts at codes + offsets[i]
-  const int64_t* offsets = nullptr;   // n+1 absolute offsets
+  const int64_t* offsets = nullptr;   // n+1 absolute offsets, or sparse (off_shift > 0, moc/wire.hpp):
+                                      // entry j = offset of record min(j << off_shift, n)
+  int32_t off_shift = 0;              // sparse offsets need lengths and tile_records % (1 << off_shift) == 0
   const uint8_t* lengths8 = nullptr;  // optional narrow lengths (saves 7 B/record of reads)
   const uint8_t* lengths4 = nullptr;  // optional nibble lengths: record i = len_base + nibble i (low first)
   const uint8_t* lengths3 = nullptr;  // optional 3-bit lengths: record i = len_base + bits [3i, 3i+3), LSB

@@ -15,6 +15,7 @@
 #include "moc/comm.hpp"
 #include "moc/common.hpp"
 #include "moc/problem.hpp"
+#include "moc/wire.hpp"
 
 namespace moc {
 
@@ -32,6 +33,15 @@ struct PhaseHooks {
   std::function<void()> end;
 };
 
+// What the last solve moved and ran (for --timing).
+struct GpuSolveStats {
+  double kernel_ms = 0;
+  int64_t h2d_bytes = 0, d2h_bytes = 0;
+  int32_t kernels = 0;  // bitmask: 1 swipe, 2 short, 4 tiles
+  int32_t direct = 0;   // 1: streamed zero-copy / DMA from pinned host memory
+  R2Params r2{};        // parameters of R2 results
+};
+
 class GpuRank {
  public:
   virtual ~GpuRank() = default;
@@ -43,6 +53,15 @@ class GpuRank {
   virtual void search_keys(const uint8_t* codes, const int64_t* offsets, int64_t n, int part, int parts,
                            uint64_t* keys) = 0;
   virtual double last_kernel_ms() const = 0;
+  // NUMA node of the device's PCIe root complex (-1: unknown); the rank's threads are bound to it.
+  virtual int numa_node() const = 0;
+  // Wire-format batch (moc/wire.hpp) -> results in `fmt` (zero-copy when every buffer is pinned).
+  virtual void solve_wire(const WireBatch& b, void* out, ResultFormat fmt) = 0;
+  // True when batches of this length range stream packed letters + narrow lengths + sparse offsets.
+  virtual bool streams_packed(int64_t min_l2, int64_t max_l2) const = 0;
+  // Smallest result format for records of lengths [min_l2, max_l2].
+  virtual ResultFormat result_format(int64_t min_l2, int64_t max_l2) const = 0;
+  virtual GpuSolveStats last_stats() const = 0;
   virtual void pin(const void* p, size_t bytes) = 0;
   virtual void unpin_all() = 0;
   // Creates the RCCL communicator (collective over ctx.world: every rank must call it).

@@ -87,6 +87,12 @@ class HipEngine {
   void solve_ex(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths, int64_t n, void* out,
                 ResultFormat fmt, const BatchHints& hints = {}, bool packed5 = false, int len_bits = 8,
                 int len_base = 0);
+  // Any wire-format batch (moc/wire.hpp): packed or byte letters, dense or sparse offsets, narrow lengths.
+  // Sparse offsets stream zero-copy when the buffers are pinned and the swipe kernel takes the batch;
+  // otherwise dense offsets are rebuilt from the lengths for the staged pipeline.
+  void solve_wire(const WireBatch& b, void* out, ResultFormat fmt);
+  // True when batches of this length range stream packed letters (the swipe kernel takes them).
+  bool streams_packed(int64_t min_l2, int64_t max_l2) const;
   // Smallest result format for this problem given the batch's length range (min_l2 <= 0: unknown,
   // R2 not considered).
   ResultFormat auto_format(int64_t max_l2, int64_t min_l2 = 0) const;
@@ -131,12 +137,10 @@ class HipEngine {
   dev::ProblemView problem_view(int64_t max_l2) const;
   void ensure(void*& ptr, size_t& cap, size_t bytes);
   void ensure_host(void*& ptr, size_t& cap, size_t bytes);
-  bool direct_pointers(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths, int len_bits,
-                       int len_base, int64_t n, void* out, int fb, bool packed5, dev::ShortArgs& a) const;
+  bool direct_pointers(const WireBatch& b, void* out, int fb, dev::ShortArgs& a) const;
   void launch_direct(const dev::ProblemView& pv, const dev::ShortArgs& a, bool swipe);
-  void run_dma_stream(const dev::ProblemView& pv, const dev::ShortArgs& a, bool swipe, const uint8_t* codes,
-                      const int64_t* offsets, const uint8_t* lengths, int len_bits, int64_t n, void* out, int fb,
-                      bool packed5);
+  void run_dma_stream(const dev::ProblemView& pv, const dev::ShortArgs& a, bool swipe, const WireBatch& b, void* out,
+                      int fb);
   void run_staged(const uint8_t* codes, const int64_t* offsets, int64_t n, void* out, ResultFormat fmt,
                   bool packed5);
 

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "moc/common.hpp"
+#include "moc/partition.hpp"
 #include "moc/problem.hpp"
 #include "moc/wire.hpp"
 
@@ -29,6 +30,10 @@ struct ParseOptions {
 
 // Reads the whole stream into memory (bulk fread; no per-token stdio).
 uvector<char> read_stream(FILE* f);
+// Bytes left in a regular-file stream (from its position), or -1 for pipes / terminals / empty files.
+int64_t regular_input_bytes(FILE* f);
+// Reads up to `want` bytes of a regular file into dst (large reads: parallel preads); returns the count.
+size_t read_regular_into(FILE* f, char* dst, size_t want);
 
 // Pieces of the record area that hold a contiguous run of records (a rank's slice): piece q covers
 // bytes [byte_begin, byte_end) of the area; its first token is record `tok` and its first letter is letter
@@ -45,6 +50,7 @@ struct FillReport {
   int64_t min_len = INT64_MAX, max_len = 0;
   int64_t bad_record = -1;                 // first record holding a non-letter
   int64_t long_record = -1, long_len = 0;  // first record over the Seq2 length limit
+  int64_t cells = 0;                       // search cells of the slice (record_cells over its records)
 };
 
 // Two-phase parser of an in-memory input. The constructor reads the header; pass 1 counts the tokens and
@@ -79,8 +85,12 @@ class BulkParser {
   // ---- pass 2
   AreaSlice slice(int64_t rec_begin, int64_t rec_end) const;
   // Encodes slice s: letters as bytes into codes[0..s.letters) and/or 5-bit packed into
-  // packed5[0..packed5_bytes(s.letters)) (either may be null), offsets[0..s.records] rebased to 0.
-  FillReport fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* packed5, int64_t* offsets) const;
+  // packed5[0..packed5_bytes(s.letters)) (either may be null). Record boundaries (each output optional):
+  // dense offsets[0..s.records] rebased to 0; sparse offsets (moc/wire.hpp, stride 2^kSparseShift)
+  // sparse[0..sparse_count(s.records, kSparseShift)); lengths len16[0..s.records), saturated at 65535
+  // (the report's max_len tells whether they are exact).
+  FillReport fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* packed5, int64_t* offsets,
+                        int64_t* sparse = nullptr, uint16_t* len16 = nullptr) const;
   // Throws the error a sequential reader would report first for this report (`first` = the report's
   // slice start; validates the score range for its longest record).
   void check(const FillReport& r) const;
@@ -88,6 +98,16 @@ class BulkParser {
   void fill(uint8_t* codes, int64_t* offsets) const;
   // n * (L1 - avg + 1) * avg from the mean record length (pass 1's letters, or the area size before it).
   int64_t cells_estimate() const;
+  // Exact cost (moc/partition.hpp) of all tokens of chunks [c0, c1) -> costs[c - c0] (OpenMP over chunks).
+  void chunk_costs(const std::vector<int64_t>& starts, int c0, int c1, const CostModel& m, double* costs) const;
+  // Installs exact chunk costs for cost_split (all chunks, same model); without them it estimates.
+  void set_chunk_costs(std::vector<double> costs);
+  // Rank bounds without a lengths array (after pass 1): the record index where the cost of records
+  // [first, count()) reaches part/parts of their total. Chunk costs are exact when installed (else the
+  // records at the chunk's mean length), walks are exact inside the chunk that holds the split. Monotone
+  // in part, and the same on every rank holding the same chunk table, so each rank computes its own
+  // [split(r), split(r + 1)) without a collective.
+  int64_t cost_split(int64_t first, int part, int parts, const CostModel& m) const;
 
  private:
   struct Located {
@@ -100,6 +120,7 @@ class BulkParser {
   const char* area_ = nullptr;
   size_t area_len_ = 0;
   std::vector<int64_t> start_, tok_pre_, chr_pre_;  // chunk table: nchunks+1 entries each
+  std::vector<double> cost_;                        // optional exact chunk costs (nchunks entries)
 };
 
 // Parses "W1 W2 W3 W4 / Seq1 / N / Seq2 x N" (PDF p.5-6). Whitespace of any kind (incl. CRLF)

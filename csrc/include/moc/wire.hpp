@@ -93,5 +93,43 @@ inline int narrow_length_bits(int64_t min_l2, int64_t max_l2) {
 void pack_lengths(const int64_t* offsets, int64_t n, int bits, int64_t base, uint8_t* out);
 // Length of record i of a narrow lengths array (test helper / host decode).
 int64_t narrow_length(const uint8_t* lengths, int bits, int64_t base, int64_t i);
+// The same packing from plain uint16 lengths (the parser's per-slice scratch).
+void pack_lengths16(const uint16_t* lengths, int64_t n, int bits, int64_t base, uint8_t* out);
+
+// ---- sparse offsets ---------------------------------------------------------------------------------
+// The streaming kernels read a record's letter offset only at tile boundaries (multiples of 64 records)
+// and at the batch end, and take every length from the narrow lengths. So the parser's narrow wire
+// format keeps one int64 offset per 2^shift records: entry j = offset of record min(j << shift, n),
+// j = 0 .. ceil(n / 2^shift) — 1/64 of the bytes of CSR offsets (which cost 8 B per record against the
+// 5.3 B of packed letters of an input6-shaped record).
+constexpr int kSparseShift = 6;
+inline int64_t sparse_count(int64_t n, int shift) { return ((n + (int64_t{1} << shift) - 1) >> shift) + 1; }
+// Entry of record r (a multiple of 2^shift, or r == n).
+inline int64_t sparse_index(int64_t r, int shift) { return (r + (int64_t{1} << shift) - 1) >> shift; }
+// Dense CSR offsets out[0..n] (absolute, out[0] = sparse[0]) from sparse offsets + narrow lengths.
+void expand_offsets(const int64_t* sparse, int shift, const uint8_t* lengths, int bits, int64_t base, int64_t n,
+                    int64_t* out);
+
+// One host batch in the wire formats above: what `final`'s parser writes for a rank's slice and what the
+// engines take. `offsets` is dense (off_shift 0, n+1 entries) or sparse (off_shift > 0, lengths required).
+struct WireBatch {
+  const uint8_t* letters = nullptr;  // 5-bit packed (packed5) or one byte per letter; record i at offsets
+  bool packed5 = false;
+  const int64_t* offsets = nullptr;
+  int off_shift = 0;
+  const uint8_t* lengths = nullptr;  // narrow lengths (optional with dense offsets)
+  int len_bits = 8;
+  int64_t len_base = 0;
+  int64_t n = 0;
+  int64_t min_l2 = -1, max_l2 = -1;  // length range (-1: unknown; required with sparse offsets)
+  int64_t first_letter() const { return offsets[0]; }
+  int64_t end_letter() const { return offsets[off_shift ? sparse_count(n, off_shift) - 1 : n]; }
+  int64_t letter_bytes() const {
+    const int64_t L = end_letter() - first_letter();
+    return packed5 ? (5 * L + 7) / 8 : L;
+  }
+  int64_t offset_entries() const { return off_shift ? sparse_count(n, off_shift) : n + 1; }
+  int64_t length_bytes() const { return lengths ? narrow_lengths_bytes(n, len_bits) : 0; }
+};
 
 }  // namespace moc

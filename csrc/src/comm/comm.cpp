@@ -203,4 +203,45 @@ void SharedWindow::fence() const {
   MOC_MPI_CHECK(MPI_Win_sync(win_));
 }
 
+// ------------------------------------------------------------------------------------------------
+SegmentWindow::SegmentWindow(const MpiContext& ctx, int64_t my_bytes, int numa_node)
+    : comm_(ctx.node), local_rank_(ctx.local_rank) {
+  seg_.assign(static_cast<size_t>(ctx.local_size), nullptr);
+  if (ctx.local_size == 1) {
+    region_ = HostRegion(static_cast<size_t>(std::max<int64_t>(my_bytes, 8)), numa_node);
+    seg_[0] = region_.data();
+    return;
+  }
+  MPI_Info info;
+  MPI_Info_create(&info);
+  MPI_Info_set(info, "alloc_shared_noncontig", "true");  // each segment page-aligned on its own
+  void* base = nullptr;
+  const int rc = MPI_Win_allocate_shared(static_cast<MPI_Aint>(std::max<int64_t>(my_bytes, 8)), 1, info, comm_, &base,
+                                         &win_);
+  MPI_Info_free(&info);
+  MOC_MPI_CHECK(rc);
+  if (numa_node >= 0) (void)bind_range_to_node(base, static_cast<size_t>(std::max<int64_t>(my_bytes, 8)), numa_node);
+  for (int r = 0; r < ctx.local_size; ++r) {
+    MPI_Aint sz = 0;
+    int disp = 0;
+    void* p = nullptr;
+    MOC_MPI_CHECK(MPI_Win_shared_query(win_, r, &sz, &disp, &p));
+    seg_[static_cast<size_t>(r)] = static_cast<char*>(p);
+  }
+  MOC_MPI_CHECK(MPI_Win_lock_all(MPI_MODE_NOCHECK, win_));
+}
+
+SegmentWindow::~SegmentWindow() {
+  if (win_ == MPI_WIN_NULL || std::uncaught_exceptions() > 0) return;  // see ~SharedWindow
+  MPI_Win_unlock_all(win_);
+  MPI_Win_free(&win_);
+}
+
+void SegmentWindow::fence() const {
+  if (win_ == MPI_WIN_NULL) return;
+  MOC_MPI_CHECK(MPI_Win_sync(win_));
+  MOC_MPI_CHECK(MPI_Barrier(comm_));
+  MOC_MPI_CHECK(MPI_Win_sync(win_));
+}
+
 }  // namespace moc

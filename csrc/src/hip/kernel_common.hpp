@@ -184,6 +184,13 @@ __device__ __forceinline__ void release_work_counter(unsigned* counter) {
   }
 }
 
+// Letter offset of record r, where r is a tile boundary (a multiple of 1 << off_shift) or the batch end n:
+// dense offsets hold every record, sparse ones (the parser's narrow wire format) every 2^off_shift-th
+// plus the end, so entry ceil(r / 2^off_shift) is record r's.
+__device__ __forceinline__ int64_t tile_offset(const ShortArgs& a, int64_t r) {
+  return a.offsets[(r + (int64_t{1} << a.off_shift) - 1) >> a.off_shift];
+}
+
 // Length of record `idx` of the batch from the narrowest available source.
 __device__ __forceinline__ int record_length(const ShortArgs& a, int64_t idx) {
   if (a.lengths3) {

@@ -116,7 +116,7 @@ __global__ __launch_bounds__(kBlock) void short_search_kernel(ProblemView pv, Sh
       misc[0] = static_cast<int>(tt);
       if (tt < n_tiles) {
         const int64_t r0 = tt * a.tile_records;
-        const int64_t st = a.offsets[r0], en = a.offsets[min(r0 + a.tile_records, a.n)];
+        const int64_t st = tile_offset(a, r0), en = tile_offset(a, min(r0 + a.tile_records, a.n));
         misc[8] = static_cast<int>(static_cast<uint32_t>(st));
         misc[9] = static_cast<int>(static_cast<uint64_t>(st) >> 32);
         misc[10] = static_cast<int>(static_cast<uint32_t>(en));

@@ -158,7 +158,7 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
       misc[0] = static_cast<int>(t);
       if (t < n_tiles) {  // the tile's letter range [offsets[rb], offsets[rb + m]) for fetch()
         const int64_t rb = t * a.tile_records;
-        const int64_t st = a.offsets[rb], en = a.offsets[min(rb + a.tile_records, a.n)];
+        const int64_t st = tile_offset(a, rb), en = tile_offset(a, min(rb + a.tile_records, a.n));
         misc[8] = static_cast<int>(static_cast<uint32_t>(st));
         misc[9] = static_cast<int>(static_cast<uint64_t>(st) >> 32);
         misc[10] = static_cast<int>(static_cast<uint32_t>(en));

@@ -409,29 +409,26 @@ LenStats scan_lengths(const int64_t* offsets, const uint8_t* lengths8, int64_t n
 }
 }  // namespace
 
-bool HipEngine::direct_pointers(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths, int len_bits,
-                                int len_base, int64_t n, void* out, int fb, bool packed5, dev::ShortArgs& a) const {
+bool HipEngine::direct_pointers(const WireBatch& b, void* out, int fb, dev::ShortArgs& a) const {
   const void *dc = nullptr, *doff = nullptr, *dlen = nullptr, *dout = nullptr;
-  const int64_t c0 = offsets[0], c1 = offsets[n];
+  const int64_t c0 = b.first_letter(), c1 = b.end_letter(), n = b.n;
   // byte range of the letters: [b0, b1)
-  const int64_t b0 = packed5 ? (5 * c0) >> 3 : c0, b1 = packed5 ? ((5 * c1 + 7) >> 3) + 1 : c1;
+  const int64_t b0 = b.packed5 ? (5 * c0) >> 3 : c0, b1 = b.packed5 ? ((5 * c1 + 7) >> 3) + 1 : c1;
   // the kernels stage letters with 16-byte loads of the aligned granules covering [b0, b1): a granule
   // never crosses a page, so the pages of [b0, b1) are all that must be mapped
-  if (c1 > c0 && !pinned_range(codes + b0, static_cast<size_t>(b1 - b0), &dc)) return false;
-  if (!pinned_range(offsets, sizeof(int64_t) * static_cast<size_t>(n + 1), &doff)) return false;
-  const size_t len_bytes = len_bits == 4   ? static_cast<size_t>((n + 1) / 2)
-                           : len_bits == 3 ? static_cast<size_t>((3 * n + 7) / 8 + 1)
-                                           : static_cast<size_t>(n);
-  if (lengths && !pinned_range(lengths, len_bytes, &dlen)) return false;
+  if (c1 > c0 && !pinned_range(b.letters + b0, static_cast<size_t>(b1 - b0), &dc)) return false;
+  if (!pinned_range(b.offsets, sizeof(int64_t) * static_cast<size_t>(b.offset_entries()), &doff)) return false;
+  if (b.lengths && !pinned_range(b.lengths, static_cast<size_t>(b.length_bytes()), &dlen)) return false;
   if (!pinned_range(out, static_cast<size_t>(fb) * static_cast<size_t>(n), &dout)) return false;
   // device view of the codes base pointer (record i at base + offsets[i], or at bit 5*offsets[i])
   a.codes = c1 > c0 ? static_cast<const uint8_t*>(dc) - b0 : nullptr;
   a.dbg_codes_end = b1 + 15;  // the last granule may extend up to 15 bytes past b1
   a.offsets = static_cast<const int64_t*>(doff);
-  a.lengths8 = len_bits == 8 ? static_cast<const uint8_t*>(dlen) : nullptr;
-  a.lengths4 = len_bits == 4 ? static_cast<const uint8_t*>(dlen) : nullptr;
-  a.lengths3 = len_bits == 3 ? static_cast<const uint8_t*>(dlen) : nullptr;
-  a.len_base = len_base;
+  a.off_shift = b.off_shift;
+  a.lengths8 = b.lengths && b.len_bits == 8 ? static_cast<const uint8_t*>(dlen) : nullptr;
+  a.lengths4 = b.lengths && b.len_bits == 4 ? static_cast<const uint8_t*>(dlen) : nullptr;
+  a.lengths3 = b.lengths && b.len_bits == 3 ? static_cast<const uint8_t*>(dlen) : nullptr;
+  a.len_base = static_cast<int32_t>(b.len_base);
   a.out = const_cast<void*>(dout);
   return c1 > c0;
 }
@@ -442,7 +439,30 @@ void HipEngine::solve(const uint8_t* codes, const int64_t* offsets, int64_t n, R
 
 void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths, int64_t n, void* out,
                          ResultFormat fmt, const BatchHints& hints, bool packed5, int len_bits, int len_base) {
-  if (lengths && len_bits != 8 && len_bits != 4 && len_bits != 3) throw Error("lengths must be 8-, 4- or 3-bit");
+  WireBatch b;
+  b.letters = codes;
+  b.packed5 = packed5;
+  b.offsets = offsets;
+  b.lengths = lengths;
+  b.len_bits = len_bits;
+  b.len_base = len_base;
+  b.n = n;
+  b.min_l2 = hints.min_l2;
+  b.max_l2 = hints.max_l2;
+  solve_wire(b, out, fmt);
+}
+
+bool HipEngine::streams_packed(int64_t min_l2, int64_t max_l2) const {
+  dev::ShortArgs a;
+  return have_problem_ && dev::configure_swipe(L1_, min_l2, max_l2, table_.max_abs(), a);
+}
+
+void HipEngine::solve_wire(const WireBatch& batch, void* out, ResultFormat fmt) {
+  WireBatch b = batch;
+  const int64_t n = b.n;
+  if (b.lengths && b.len_bits != 8 && b.len_bits != 4 && b.len_bits != 3) throw Error("lengths must be 8-, 4- or 3-bit");
+  if (b.off_shift && (!b.lengths || b.min_l2 < 0 || b.max_l2 < 0 || b.off_shift > 6))
+    throw Error("sparse offsets need narrow lengths, the length range and a stride of at most 64 records");
   if (!have_problem_) throw Error("HipEngine::solve before set_problem");
   MOC_HIP_CHECK(hipSetDevice(device_));
   TraceRange tr("moc.solve");
@@ -456,16 +476,17 @@ void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uin
 
   // ---- batch bounds (hints, or one parallel pass over the lengths)
   LenStats ls;
-  if (hints.min_l2 >= 0 && hints.max_l2 >= 0) {
-    ls.mn = hints.min_l2;
-    ls.mx = hints.max_l2;
+  if (b.min_l2 >= 0 && b.max_l2 >= 0) {
+    ls.mn = b.min_l2;
+    ls.mx = b.max_l2;
   } else {
-    ls = scan_lengths(offsets, len_bits == 8 ? lengths : nullptr, n);
+    ls = scan_lengths(b.offsets, b.len_bits == 8 ? b.lengths : nullptr, n);
   }
-  if (len_bits == 8 && lengths && ls.mx > 255) lengths = nullptr;
-  if (len_bits == 4 && lengths && (ls.mn < len_base || ls.mx > len_base + 15))
+  if (b.len_bits == 8 && b.lengths && ls.mx > 255 && !b.off_shift) b.lengths = nullptr;
+  if (b.len_bits == 8 && b.lengths && ls.mx > 255) throw Error("8-bit lengths cannot hold this batch's lengths");
+  if (b.len_bits == 4 && b.lengths && (ls.mn < b.len_base || ls.mx > b.len_base + 15))
     throw Error("nibble lengths cannot hold this batch's lengths");
-  if (len_bits == 3 && lengths && (ls.mn < len_base || ls.mx > len_base + 7))
+  if (b.len_bits == 3 && b.lengths && (ls.mn < b.len_base || ls.mx > b.len_base + 7))
     throw Error("3-bit lengths cannot hold this batch's lengths");
   if (fmt == ResultFormat::R4 && (L1_ > 255 || ls.mx > 255 || table_.max_abs() * ls.mx >= 32767))
     throw Error("result format R4 cannot hold this batch");
@@ -480,14 +501,16 @@ void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uin
   a.n = n;
   a.fmt = static_cast<int32_t>(fmt);
   a.counter = d_counter_;
-  a.packed5 = packed5 ? 1 : 0;
+  a.packed5 = b.packed5 ? 1 : 0;
   const bool swipe = dev::configure_swipe(L1_, ls.mn, ls.mx, table_.max_abs(), a);
-  // packed letters stream straight into the swipe kernel only; other kernels read unpacked bytes
-  if (opt_.allow_direct && (swipe || (!packed5 && dev::configure_short(L1_, ls.mn, ls.mx, a))) &&
-      direct_pointers(codes, offsets, lengths, len_bits, len_base, n, out, fb, packed5, a)) {
+  // packed letters stream straight into the swipe kernel only; other kernels read unpacked bytes. Sparse
+  // offsets need whole tiles of 2^off_shift records (the swipe tiles are powers of two >= 64).
+  const bool kernel_ok = (swipe || (!b.packed5 && dev::configure_short(L1_, ls.mn, ls.mx, a))) &&
+                         (a.tile_records % (1 << b.off_shift)) == 0;
+  if (opt_.allow_direct && kernel_ok && direct_pointers(b, out, fb, a)) {
     const dev::ProblemView pv = problem_view(ls.mx);
     if (opt_.dma_stream) {
-      run_dma_stream(pv, a, swipe, codes, offsets, lengths, len_bits, n, out, fb, packed5);
+      run_dma_stream(pv, a, swipe, b, out, fb);
       wall.stop();
       stats_.total_ms = wall.total_ms();
       return;
@@ -502,14 +525,19 @@ void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uin
     stats_.kernel_ms = ms;
     stats_.direct = 1;
     stats_.chunks = 1;
-    const int64_t letters = offsets[n] - offsets[0];
-    stats_.h2d_bytes = (packed5 ? (5 * letters + 7) / 8 : letters) + (a.lengths3 ? (3 * n + 7) / 8 : a.lengths4 ? (n + 1) / 2 : a.lengths8 ? n : 8 * n);
+    stats_.h2d_bytes = b.letter_bytes() + (a.lengths3 || a.lengths4 || a.lengths8 ? b.length_bytes() : 8 * n);
     stats_.d2h_bytes = static_cast<int64_t>(fb) * n;
     wall.stop();
     stats_.total_ms = wall.total_ms();
     return;
   }
-  run_staged(codes, offsets, n, out, fmt, packed5);
+  if (b.off_shift) {  // the staged pipeline plans from dense offsets: rebuild them from the lengths
+    uvector<int64_t> dense(static_cast<size_t>(n) + 1);
+    expand_offsets(b.offsets, b.off_shift, b.lengths, b.len_bits, b.len_base, n, dense.data());
+    run_staged(b.letters, dense.data(), n, out, fmt, b.packed5);
+  } else {
+    run_staged(b.letters, b.offsets, n, out, fmt, b.packed5);
+  }
   wall.stop();
   stats_.total_ms = wall.total_ms();
 }
@@ -521,14 +549,20 @@ void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uin
 // reads reach 45-51 (profiles/transfer_probe.log "mix3to1_*"). The kernel still reads two offsets per
 // tile from pinned host memory (a.offsets); letters, lengths and results live in the slot buffers, with
 // base pointers shifted so the kernel's absolute indexing lands inside them.
-void HipEngine::run_dma_stream(const dev::ProblemView& pv, const dev::ShortArgs& a0, bool swipe, const uint8_t* codes,
-                               const int64_t* offsets, const uint8_t* lengths, int len_bits, int64_t n, void* out,
-                               int fb, bool packed5) {
+void HipEngine::run_dma_stream(const dev::ProblemView& pv, const dev::ShortArgs& a0, bool swipe, const WireBatch& b,
+                               void* out, int fb) {
+  const uint8_t* codes = b.letters;
+  const uint8_t* lengths = b.lengths;
+  const int len_bits = b.len_bits;
+  const int64_t n = b.n;
+  const bool packed5 = b.packed5;
+  const int sh = b.off_shift;
+  auto off = [&](int64_t r) { return b.offsets[sparse_index(r, sh)]; };  // r: a chunk boundary or n
   // chunk starts at whole tiles and at multiples of 8 records: 3-, 4- and 8-bit lengths stay byte aligned
   const int64_t tile = (std::max<int64_t>(a0.tile_records, 1) + 7) / 8 * 8 == a0.tile_records
                            ? a0.tile_records
                            : std::max<int64_t>(a0.tile_records, 1) * 8;
-  const int64_t letters = offsets[n] - offsets[0];
+  const int64_t letters = off(n) - off(0);
   const int64_t total_bytes = packed5 ? (5 * letters + 7) / 8 : letters;
   const int64_t per_rec = std::max<int64_t>(1, total_bytes / std::max<int64_t>(n, 1));
   int64_t chunk = std::max<int64_t>(tile, (opt_.dma_chunk_bytes / per_rec) / tile * tile);
@@ -537,8 +571,8 @@ void HipEngine::run_dma_stream(const dev::ProblemView& pv, const dev::ShortArgs&
     const int64_t r0 = c * chunk, r1 = std::min(n, r0 + chunk), cn = r1 - r0;
     Slot& s = *slots_[c % slots_.size()];
     // letters: bytes [B0, b1 + 16) of the stream, B0 aligned down to 16 (the kernel stages 16-byte words)
-    const int64_t b0 = packed5 ? (5 * offsets[r0]) >> 3 : offsets[r0];
-    const int64_t b1 = packed5 ? ((5 * offsets[r1] + 7) >> 3) + 1 : offsets[r1];
+    const int64_t b0 = packed5 ? (5 * off(r0)) >> 3 : off(r0);
+    const int64_t b1 = packed5 ? ((5 * off(r1) + 7) >> 3) + 1 : off(r1);
     const int64_t B0 = b0 & ~int64_t{15};
     const size_t lbytes = static_cast<size_t>(b1 - B0);  // + 16 bytes of device slack, never copied: the
                                                          // host range may end at its allocation's end
@@ -566,7 +600,7 @@ void HipEngine::run_dma_stream(const dev::ProblemView& pv, const dev::ShortArgs&
     dev::ShortArgs a = a0;
     a.codes = static_cast<const uint8_t*>(s.d_packed) - B0;
     a.dbg_codes_end = B0 + static_cast<int64_t>(lbytes) + 16;
-    a.offsets = a0.offsets + r0;  // pinned host (zero-copy): two reads per tile
+    a.offsets = a0.offsets + (r0 >> sh);  // pinned host (zero-copy): two reads per tile
     a.lengths8 = lengths && len_bits == 8 ? static_cast<const uint8_t*>(s.d_offsets) : nullptr;
     a.lengths4 = lengths && len_bits == 4 ? static_cast<const uint8_t*>(s.d_offsets) : nullptr;
     a.lengths3 = lengths && len_bits == 3 ? static_cast<const uint8_t*>(s.d_offsets) : nullptr;

@@ -13,6 +13,7 @@
 #include <cerrno>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 
 #include "moc/runtime/releaser.hpp"
 
@@ -59,68 +60,78 @@ int64_t parse_int(const char* b, const char* e, const char* what) {
 
 }  // namespace
 
+size_t read_regular_into(FILE* f, char* dst, size_t want) {
+  const long pos = std::ftell(f);
+  if (pos < 0 || want <= (size_t{64} << 20)) {
+    const size_t got = std::fread(dst, 1, want, f);
+    if (got < want && std::ferror(f)) throw Error("error while reading input stream");
+    return got;
+  }
+  // large file: the copy out of the page cache split over the OpenMP threads (one fread is a
+  // single-threaded, page-faulting memcpy of the whole file)
+  const int fd = fileno(f);
+  constexpr size_t kChunk = size_t{16} << 20;
+  const int64_t nchunks = static_cast<int64_t>((want + kChunk - 1) / kChunk);
+  std::vector<size_t> got(static_cast<size_t>(nchunks), 0);
+  int failed = 0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(| : failed)
+  for (int64_t c = 0; c < nchunks; ++c) {
+    const size_t b = static_cast<size_t>(c) * kChunk, e = std::min(want, b + kChunk);
+    size_t at = b;
+    while (at < e) {
+      const ssize_t r = pread(fd, dst + at, e - at, static_cast<off_t>(pos) + static_cast<off_t>(at));
+      if (r < 0 && errno == EINTR) continue;
+      if (r < 0) {
+        failed = 1;
+        break;
+      }
+      if (r == 0) break;
+      at += static_cast<size_t>(r);
+    }
+    got[static_cast<size_t>(c)] = at - b;
+  }
+  if (failed) throw Error("error while reading input stream");
+  // the file as it was at fstat time; a short chunk means it shrank: keep the contiguous prefix
+  size_t len = 0;
+  for (int64_t c = 0; c < nchunks; ++c) {
+    len += got[static_cast<size_t>(c)];
+    if (got[static_cast<size_t>(c)] < std::min(want, static_cast<size_t>(c + 1) * kChunk) - static_cast<size_t>(c) * kChunk)
+      break;
+  }
+  (void)std::fseek(f, static_cast<long>(pos) + static_cast<long>(len), SEEK_SET);
+  return len;
+}
+
+int64_t regular_input_bytes(FILE* f) {
+  struct stat st;
+  if (fstat(fileno(f), &st) != 0 || !S_ISREG(st.st_mode) || st.st_size <= 0) return -1;
+  const long pos = std::ftell(f);
+  return pos < 0 ? -1 : std::max<int64_t>(0, static_cast<int64_t>(st.st_size) - pos);
+}
+
 uvector<char> read_stream(FILE* f) {
   uvector<char> buf;
   size_t len = 0;
-  struct stat st;
-  if (fstat(fileno(f), &st) == 0 && S_ISREG(st.st_mode) && st.st_size > 0) {
+  const int64_t size = regular_input_bytes(f);
+  if (size > 0) {
     // regular file: one allocation of the remaining size (+1 to detect growth), one read
-    const long pos = std::ftell(f);
-    const size_t want = static_cast<size_t>(st.st_size) - static_cast<size_t>(pos > 0 ? pos : 0) + 1;
+    const size_t want = static_cast<size_t>(size) + 1;
     buf.resize(want);  // not touched yet (default-init): the advice below applies to every page
-    if (want > (size_t{64} << 20) && pos >= 0) {
-      // large file: 2 MiB pages for the buffer, and the copy out of the page cache split over the OpenMP
-      // threads (one fread is a single-threaded 4 KiB-page-faulting memcpy of the whole file)
-      constexpr uintptr_t kHuge = uintptr_t{2} << 20;
+    if (want > (size_t{64} << 20)) {
+      constexpr uintptr_t kHuge = uintptr_t{2} << 20;  // 2 MiB pages for the buffer
       const uintptr_t lo = (reinterpret_cast<uintptr_t>(buf.data()) + kHuge - 1) & ~(kHuge - 1);
       const uintptr_t hi = (reinterpret_cast<uintptr_t>(buf.data()) + want) & ~(kHuge - 1);
       if (hi > lo) (void)madvise(reinterpret_cast<void*>(lo), hi - lo, MADV_HUGEPAGE);
-      const int fd = fileno(f);
-      const size_t body = want - 1;
-      constexpr size_t kChunk = size_t{16} << 20;
-      const int64_t nchunks = static_cast<int64_t>((body + kChunk - 1) / kChunk);
-      std::vector<size_t> got(static_cast<size_t>(nchunks), 0);
-      int failed = 0;
-#pragma omp parallel for schedule(dynamic, 1) reduction(| : failed)
-      for (int64_t c = 0; c < nchunks; ++c) {
-        const size_t b = static_cast<size_t>(c) * kChunk, e = std::min(body, b + kChunk);
-        size_t at = b;
-        while (at < e) {
-          const ssize_t r = pread(fd, buf.data() + at, e - at, static_cast<off_t>(pos) + static_cast<off_t>(at));
-          if (r < 0 && errno == EINTR) continue;
-          if (r < 0) {
-            failed = 1;
-            break;
-          }
-          if (r == 0) break;
-          at += static_cast<size_t>(r);
-        }
-        got[static_cast<size_t>(c)] = at - b;
-      }
-      if (failed) throw Error("error while reading input stream");
-      // the file as it was at fstat time; a short chunk means it shrank: keep the contiguous prefix
-      for (int64_t c = 0; c < nchunks; ++c) {
-        len += got[static_cast<size_t>(c)];
-        if (got[static_cast<size_t>(c)] < std::min(body, static_cast<size_t>(c + 1) * kChunk) - static_cast<size_t>(c) * kChunk)
-          break;
-      }
-      (void)std::fseek(f, static_cast<long>(pos) + static_cast<long>(len), SEEK_SET);
-      if (len == body) {
-        // a file that grew after fstat continues through the stream loop below
-        const size_t more = std::fread(buf.data() + len, 1, 1, f);
-        len += more;
-        if (!more) {
-          buf.resize(len);
-          return buf;
-        }
-      } else {
-        buf.resize(len);
-        return buf;
-      }
-    } else {
-      len = std::fread(buf.data(), 1, want, f);
     }
-    if (len < want) {
+    len = read_regular_into(f, buf.data(), want - 1);
+    if (len < want - 1) {  // it shrank
+      buf.resize(len);
+      return buf;
+    }
+    // a file that grew after fstat continues through the stream loop below
+    const size_t more = std::fread(buf.data() + len, 1, 1, f);
+    len += more;
+    if (!more) {
       if (std::ferror(f)) throw Error("error while reading input stream");
       buf.resize(len);
       return buf;
@@ -321,11 +332,14 @@ struct PieceOut {
 };
 }  // namespace
 
-FillReport BulkParser::fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* packed5, int64_t* offs) const {
-  offs[0] = 0;
+FillReport BulkParser::fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* packed5, int64_t* offs, int64_t* sparse,
+                                  uint16_t* len16) const {
+  if (offs) offs[0] = 0;
+  constexpr int64_t kSparseMask = (int64_t{1} << kSparseShift) - 1;
   const int np = static_cast<int>(s.pieces.size());
   const unsigned char* ua = reinterpret_cast<const unsigned char*>(area_);
   const int64_t l2_cap = l2_cap_;
+  const int64_t L1 = static_cast<int64_t>(seq1_.size());
   const size_t vec_in_end = area_len_ >= 16 ? area_len_ - 16 : 0;  // 16-byte loads stay in the area
   std::vector<PieceOut> out(static_cast<size_t>(np));
   // one piece per iteration (dynamic): correct for any number of delivered threads
@@ -370,7 +384,7 @@ FillReport BulkParser::fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* p
     };
     uint8_t* sink = packed5 ? stage.data() : codes;
     int64_t tok = pc.tok, pos = a;
-    int64_t first_bad = -1, lt = -1, ll = 0, mn = INT64_MAX, mx = 0;
+    int64_t first_bad = -1, lt = -1, ll = 0, mn = INT64_MAX, mx = 0, cells = 0;
     size_t i = static_cast<size_t>(pc.byte_begin);
     const size_t e = static_cast<size_t>(pc.byte_end);
     while (i < e) {
@@ -412,7 +426,11 @@ FillReport BulkParser::fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* p
       }
       mn = std::min(mn, L);
       mx = std::max(mx, L);
-      offs[++tok] = pos;
+      cells += record_cells(L1, L);
+      if (sparse && (tok & kSparseMask) == 0) sparse[tok >> kSparseShift] = p0;
+      if (len16) len16[tok] = static_cast<uint16_t>(std::min<int64_t>(L, 65535));
+      if (offs) offs[tok + 1] = pos;
+      ++tok;
     }
     if (packed5) flush(pos, true);
     po.rep.min_len = mn;
@@ -420,11 +438,13 @@ FillReport BulkParser::fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* p
     po.rep.bad_record = first_bad < 0 ? -1 : s.first_record + first_bad;
     po.rep.long_record = lt < 0 ? -1 : s.first_record + lt;
     po.rep.long_len = ll;
+    po.rep.cells = cells;
   }
   FillReport r;
   for (const PieceOut& po : out) {
     r.min_len = std::min(r.min_len, po.rep.min_len);
     r.max_len = std::max(r.max_len, po.rep.max_len);
+    r.cells += po.rep.cells;
     if (po.rep.bad_record >= 0 && (r.bad_record < 0 || po.rep.bad_record < r.bad_record)) r.bad_record = po.rep.bad_record;
     if (po.rep.long_record >= 0 && (r.long_record < 0 || po.rep.long_record < r.long_record)) {
       r.long_record = po.rep.long_record;
@@ -445,6 +465,7 @@ FillReport BulkParser::fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* p
     const int64_t used = 5 * ((s.letters + 7) / 8);
     std::memset(packed5 + used, 0, static_cast<size_t>(packed5_bytes(s.letters) - used));
   }
+  if (sparse) sparse[sparse_count(s.records, kSparseShift) - 1] = s.letters;
   return r;
 }
 
@@ -475,6 +496,83 @@ int64_t BulkParser::cells_estimate() const {
   const int64_t letters = total_chars_ >= 0 ? total_chars_ : std::max<int64_t>(0, static_cast<int64_t>(area_len_) - n_);
   const int64_t avg = std::max<int64_t>(1, letters / n_);
   return avg <= L1 ? n_ * (L1 - avg + 1) * avg : 0;
+}
+
+void BulkParser::chunk_costs(const std::vector<int64_t>& starts, int c0, int c1, const CostModel& m,
+                             double* costs) const {
+  const unsigned char* ua = reinterpret_cast<const unsigned char*>(area_);
+  const int64_t L1 = static_cast<int64_t>(seq1_.size());
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int c = c0; c < c1; ++c) {
+    int64_t i = starts[c];
+    const int64_t e = starts[c + 1];
+    double acc = 0.0;
+    while (i < e) {
+      while (i < e && is_space(ua[i])) ++i;
+      if (i >= e) break;
+      const int64_t b = i;
+      while (i < e && !is_space(ua[i])) ++i;
+      acc += record_cost(L1, i - b, m);
+    }
+    costs[c - c0] = acc;
+  }
+}
+
+void BulkParser::set_chunk_costs(std::vector<double> costs) { cost_ = std::move(costs); }
+
+int64_t BulkParser::cost_split(int64_t first, int part, int parts, const CostModel& m) const {
+  if (start_.empty()) throw Error("BulkParser::cost_split before pass 1");
+  first = std::clamp<int64_t>(first, 0, n_);
+  if (part <= 0 || first >= n_) return first;
+  if (part >= parts) return n_;
+  const int64_t L1 = static_cast<int64_t>(seq1_.size());
+  const int nch = nchunks();
+  const unsigned char* ua = reinterpret_cast<const unsigned char*>(area_);
+  // exact cost of the records of chunk c inside [first, n) (walks the chunk's tokens); stops once the
+  // running total (from `acc`) reaches `target` and returns the split record there, else -1
+  auto walk = [&](int c, double& acc, double target) -> int64_t {
+    const int64_t t_end = std::min(tok_pre_[c + 1], n_);
+    int64_t i = start_[c], t = tok_pre_[c];
+    const int64_t e = start_[c + 1];
+    while (t < t_end && i < e) {
+      while (i < e && is_space(ua[i])) ++i;
+      const int64_t b = i;
+      while (i < e && !is_space(ua[i])) ++i;
+      if (t >= first) {
+        const double next = acc + record_cost(L1, i - b, m);
+        if (next >= target) return (target - acc) < (next - target) ? t : t + 1;
+        acc = next;
+      }
+      ++t;
+    }
+    return -1;
+  };
+  // chunk costs: exact ones from pass 1 (chunk_costs) for chunks wholly inside [first, n), a walk for the
+  // two boundary chunks, else the records at the chunk's mean length
+  std::vector<double> pre(static_cast<size_t>(nch) + 1, 0.0);
+  for (int c = 0; c < nch; ++c) {
+    const int64_t t0 = std::max(tok_pre_[c], first), t1 = std::min(tok_pre_[c + 1], n_);
+    const int64_t toks = tok_pre_[c + 1] - tok_pre_[c];
+    double est = 0.0;
+    if (t1 > t0) {
+      if (t1 - t0 < toks) {
+        walk(c, est, std::numeric_limits<double>::infinity());
+      } else if (!cost_.empty()) {
+        est = cost_[static_cast<size_t>(c)];
+      } else {
+        const int64_t avg = (chr_pre_[c + 1] - chr_pre_[c] + toks / 2) / toks;
+        est = static_cast<double>(toks) * record_cost(L1, avg, m);
+      }
+    }
+    pre[c + 1] = pre[c] + est;
+  }
+  const double target = pre[nch] * part / parts;
+  if (target <= 0.0) return first;
+  const int c = static_cast<int>(std::lower_bound(pre.begin() + 1, pre.end(), target) - pre.begin()) - 1;
+  if (c >= nch) return n_;
+  double acc = pre[c];  // exact inside the chunk holding the target
+  const int64_t t = walk(c, acc, target);
+  return t >= 0 ? t : std::max(first, std::min(tok_pre_[c + 1], n_));
 }
 
 Problem parse_problem(const char* data, size_t len, const ParseOptions& opt) {

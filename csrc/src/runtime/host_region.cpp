@@ -1,0 +1,73 @@
+// HostRegion (moc/runtime/host_region.hpp): huge-page-advised, optionally NUMA-bound private buffers.
+#include "moc/runtime/host_region.hpp"
+
+#include <sys/mman.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <string>
+
+#include "moc/common.hpp"
+
+namespace moc {
+
+namespace {
+constexpr size_t kHuge = size_t{2} << 20;
+}
+
+bool bind_range_to_node(void* p, size_t bytes, int node) {
+  if (node < 0 || bytes == 0 || node >= 1024) return false;
+  unsigned long mask[1024 / (8 * sizeof(unsigned long))] = {0};
+  mask[node / (8 * sizeof(unsigned long))] |= 1ul << (node % (8 * sizeof(unsigned long)));
+  constexpr int kMpolPreferred = 1;
+  const uintptr_t lo = reinterpret_cast<uintptr_t>(p) & ~uintptr_t{4095};
+  const uintptr_t hi = reinterpret_cast<uintptr_t>(p) + bytes;
+  return syscall(SYS_mbind, reinterpret_cast<void*>(lo), hi - lo, kMpolPreferred, mask, sizeof(mask) * 8, 0) == 0;
+}
+
+HostRegion::HostRegion(size_t bytes, int numa_node) {
+  const size_t want = (std::max<size_t>(bytes, 1) + kHuge - 1) & ~(kHuge - 1);
+  map_bytes_ = want + kHuge;  // slack to start on a 2 MiB boundary
+  map_ = mmap(nullptr, map_bytes_, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+  if (map_ == MAP_FAILED) {
+    map_ = nullptr;
+    throw Error("HostRegion: cannot map " + std::to_string(map_bytes_) + " bytes");
+  }
+  base_ = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(map_) + kHuge - 1) & ~(kHuge - 1));
+  bytes_ = bytes;
+  (void)madvise(base_, want, MADV_HUGEPAGE);  // advisory: 4 KiB pages if THP is off
+  if (numa_node >= 0) (void)bind_range_to_node(base_, want, numa_node);
+}
+
+HostRegion& HostRegion::operator=(HostRegion&& o) noexcept {
+  if (this != &o) {
+    release();
+    map_ = o.map_;
+    map_bytes_ = o.map_bytes_;
+    base_ = o.base_;
+    bytes_ = o.bytes_;
+    releaser_ = o.releaser_;
+    o.map_ = nullptr;
+    o.base_ = nullptr;
+    o.bytes_ = o.map_bytes_ = 0;
+  }
+  return *this;
+}
+
+HostRegion::~HostRegion() { release(); }
+
+void HostRegion::release() {
+  if (!map_) return;
+  void* m = map_;
+  const size_t len = map_bytes_;
+  map_ = nullptr;
+  base_ = nullptr;
+  bytes_ = map_bytes_ = 0;
+  if (releaser_)
+    releaser_->defer([m, len] { munmap(m, len); });
+  else
+    munmap(m, len);
+}
+
+}  // namespace moc

@@ -74,6 +74,37 @@ void pack_lengths(const int64_t* offsets, int64_t n, int bits, int64_t base, uin
   if (bits == 3 && n >= 0) out[narrow_lengths_bytes(n, 3) - 1] = 0;  // slack byte
 }
 
+void pack_lengths16(const uint16_t* lengths, int64_t n, int bits, int64_t base, uint8_t* out) {
+  if (bits != 3 && bits != 4 && bits != 8) throw Error("pack_lengths16: bits must be 3, 4 or 8");
+  const int64_t groups = (n + 7) / 8;
+#pragma omp parallel for schedule(static) if (groups > 65536)
+  for (int64_t g = 0; g < groups; ++g) {
+    const int64_t b = g * 8;
+    const int m = static_cast<int>(std::min<int64_t>(8, n - b));
+    uint64_t v = 0;
+    for (int j = 0; j < m; ++j) v |= static_cast<uint64_t>(lengths[b + j] - (bits == 8 ? 0 : base)) << (bits * j);
+    const int nb = bits == 3 ? (3 * m + 7) / 8 : bits == 4 ? (m + 1) / 2 : m;
+    for (int j = 0; j < nb; ++j) out[g * bits + j] = static_cast<uint8_t>(v >> (8 * j));
+  }
+  if (bits == 3 && n >= 0) out[narrow_lengths_bytes(n, 3) - 1] = 0;  // slack byte
+}
+
+void expand_offsets(const int64_t* sparse, int shift, const uint8_t* lengths, int bits, int64_t base, int64_t n,
+                    int64_t* out) {
+  const int64_t S = int64_t{1} << shift, blocks = (n + S - 1) / S;
+  // every block of 2^shift records starts at its sparse entry: independent prefix sums
+#pragma omp parallel for schedule(static) if (blocks > 4096)
+  for (int64_t j = 0; j < blocks; ++j) {
+    int64_t o = sparse[j];
+    const int64_t e = std::min(n, (j + 1) * S);
+    for (int64_t i = j * S; i < e; ++i) {
+      out[i] = o;
+      o += narrow_length(lengths, bits, base, i);
+    }
+  }
+  out[n] = sparse[sparse_count(n, shift) - 1];
+}
+
 int64_t narrow_length(const uint8_t* lengths, int bits, int64_t base, int64_t i) {
   if (bits == 8) return lengths[i];
   if (bits == 4) return base + ((lengths[i / 2] >> (4 * (i & 1))) & 15);

@@ -448,6 +448,29 @@ void test_slices() {
     p.set_chunks(st, tk.data(), ch.data());
     CHECK(p.total_chars() == ref.seq2.total_chars());
     CHECK(p.chunk_first_record(0) == 0 && p.chunk_first_record(nch) == n);
+    // rank bounds from the chunk table: estimated splits are monotone and cover [first, n); with exact
+    // chunk costs they equal the lengths-based cost partition of the same records
+    {
+      const CostModel cm{1.0, 200.0, 2400.0};
+      const int parts = 1 + static_cast<int>(rng() % 9);
+      const int64_t first = trial % 4 == 0 ? static_cast<int64_t>(rng() % (n + 1)) : 0;
+      int64_t prev = first;
+      bool mono = p.cost_split(first, 0, parts, cm) == first && p.cost_split(first, parts, parts, cm) == n;
+      for (int q = 1; q <= parts; ++q) {
+        const int64_t x = p.cost_split(first, q, parts, cm);
+        mono = mono && x >= prev && x <= n;
+        prev = x;
+      }
+      CHECK(mono);
+      std::vector<double> costs(static_cast<size_t>(nch));
+      p.chunk_costs(st, 0, nch, cm, costs.data());
+      p.set_chunk_costs(costs);
+      const std::vector<int64_t> want =
+          partition_by_cost_offsets(ref.seq2.offsets.data() + first, n - first, 52, parts, cm);
+      bool same = true;
+      for (int q = 0; q <= parts; ++q) same = same && p.cost_split(first, q, parts, cm) == first + want[q];
+      CHECK(same);
+    }
     for (int rep = 0; rep < 6; ++rep) {
       int64_t b = rng() % (n + 1), e = rng() % (n + 1);
       if (b > e) std::swap(b, e);
@@ -477,6 +500,25 @@ void test_slices() {
         std::vector<uint8_t> p2(packed5_bytes(s.letters), 0x55);
         p.fill_slice(s, nullptr, p2.data(), offs.data());
         CHECK(p2 == want);
+      }
+      // the narrow wire form: packed letters + sparse offsets + uint16 lengths, no dense offsets
+      std::vector<int64_t> sp(static_cast<size_t>(sparse_count(s.records, kSparseShift)), -9);
+      std::vector<uint16_t> l16(static_cast<size_t>(s.records) + 1, 0xBEEF);
+      std::vector<uint8_t> p3(packed5_bytes(s.letters), 0x33);
+      const FillReport r3 = p.fill_slice(s, nullptr, p3.data(), nullptr, sp.data(), l16.data());
+      CHECK(r3.min_len == r.min_len && r3.max_len == r.max_len && p3 == want);
+      ok = true;
+      for (size_t j = 0; j < sp.size(); ++j)
+        ok = ok && sp[j] == offs[std::min<int64_t>(static_cast<int64_t>(j) << kSparseShift, s.records)];
+      for (int64_t i = 0; i < s.records; ++i) ok = ok && l16[i] == offs[i + 1] - offs[i];
+      CHECK(ok);
+      if (s.records && r3.max_len <= 255) {  // -> narrow lengths -> dense offsets again
+        const int bits = narrow_length_bits(r3.min_len, r3.max_len);
+        std::vector<uint8_t> nl(static_cast<size_t>(narrow_lengths_bytes(s.records, bits)) + 1);
+        pack_lengths16(l16.data(), s.records, bits, r3.min_len, nl.data());
+        std::vector<int64_t> dense(static_cast<size_t>(s.records) + 1, -1);
+        expand_offsets(sp.data(), kSparseShift, nl.data(), bits, r3.min_len, s.records, dense.data());
+        CHECK(dense == offs);
       }
     }
   }

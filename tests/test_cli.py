@@ -308,3 +308,52 @@ def test_fewer_omp_threads_than_requested(tmp_path, omp_env):
         assert r.returncode == 0, r.stderr.decode()
         got = out.read_text() if extra and extra[0].startswith("--output") else r.stdout.decode()
         assert got == want
+
+
+def _source_hash():
+    """The hash `make` bakes into ./final: every file under csrc/ plus the Makefile, in sorted order."""
+    import glob
+    import hashlib
+    import os
+
+    from conftest import ROOT
+
+    pats = ["csrc/*", "csrc/*/*", "csrc/*/*/*", "csrc/*/*/*/*", "csrc/*/*/*/*/*"]
+    files = sorted([f for p in pats for f in glob.glob(p, root_dir=ROOT) if os.path.isfile(os.path.join(ROOT, f))]
+                   + ["Makefile"])
+    h = hashlib.sha1()
+    for f in files:
+        with open(os.path.join(ROOT, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:12]
+
+
+def test_build_id_matches_sources():
+    # a prebuilt ./final shipped next to newer sources would print another source hash
+    r = run_final(["--help"], np_=1)
+    line = [l for l in r.stdout.decode().splitlines() if l.startswith("build:")][-1]
+    assert f"src={_source_hash()}" in line, line
+
+
+@pytest.mark.parametrize("np_", [2, 3, 8])
+@pytest.mark.parametrize("i", [1, 3, 4])
+def test_sliced_bounds_and_timing(np_, i):
+    # bulk shm jobs are "sliced": each rank encodes its own record slice from the shared text; the slices
+    # tile the job in order, CPU ranks pin nothing, and the bounds equal the lengths-based cost split
+    import json
+
+    import numpy as np
+
+    from mpi_openmp_cuda_amd import Problem
+    from mpi_openmp_cuda_amd.parallel.partition import CPU_COST, partition
+
+    r = run_final(["--backend=cpu", "--timing"], stdin_path=input_path(i), np_=np_)
+    assert r.returncode == 0, r.stderr.decode()
+    assert r.stdout.decode() == expected(i)
+    d = json.loads([l for l in r.stderr.decode().splitlines() if l.startswith("{")][-1])
+    assert d["sliced"] is True and d["transport"] == "shm"
+    prob = Problem.read(input_path(i))
+    assert sum(d["rank_records"]) == prob.n and d["elements"] == int(prob.offsets[-1])
+    assert d["rank_pinned_bytes"] == [0] * np_ and d["rank_h2d_bytes"] == [0] * np_
+    want = np.diff(partition(np.diff(prob.offsets), len(prob.seq1), np_, CPU_COST))
+    assert d["rank_records"] == [int(x) for x in want]

@@ -8,14 +8,20 @@ import pytest
 
 from conftest import ROOT, expected, input_path
 
-_port = [29700]
+def _free_port():
+    # an OS-assigned port: fixed counters collide across pytest-xdist workers (EADDRINUSE)
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
 def torchrun(nproc, args, timeout=180):
-    _port[0] += 1
+    port = _free_port()
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-           "--master-addr=127.0.0.1", f"--master-port={_port[0]}", "-m", "mpi_openmp_cuda_amd"] + args
+           "--master-addr=127.0.0.1", f"--master-port={port}", "-m", "mpi_openmp_cuda_amd"] + args
     return subprocess.run(cmd, capture_output=True, timeout=timeout, env=env, cwd="/tmp")
 
 

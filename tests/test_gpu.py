@@ -328,14 +328,28 @@ def test_final_cli_hip_two_ranks_offsets():
     assert r.stdout.decode() == expected(3)
 
 
-def test_final_cli_zero_copy_window(tmp_path):
-    # GPU ranks page-lock the shm window and stream their slice zero-copy; output == CPU
+@pytest.mark.parametrize("np_", [1, 2])
+def test_final_cli_zero_copy_window(tmp_path, np_):
+    # GPU ranks encode their own slice (5-bit letters, narrow lengths, sparse offsets), page-lock only that
+    # slice and stream it zero-copy; output == CPU. Two ranks share the one test GPU (--device=0).
+    import json
+
     prob = make_synthetic("input6", 100_000, seed=8)
     path = tmp_path / "in6.txt"
     path.write_text(prob.to_text())
-    r = run_final(["--backend=hip", "--transport=shm", f"--input={path}", "--timing"], stdin_bytes=b"", np_=1)
+    r = run_final(["--backend=hip", "--transport=shm", f"--input={path}", "--timing", "--device=0"], stdin_bytes=b"",
+                  np_=np_)
     assert r.returncode == 0, r.stderr.decode()
     assert r.stdout.decode() == format_results(search_cpu(prob))
+    d = json.loads([l for l in r.stderr.decode().splitlines() if l.startswith("{")][-1])
+    assert d["sliced"] is True and sum(d["rank_records"]) == prob.n
+    b = np.concatenate([[0], np.cumsum(d["rank_records"])])
+    for q in range(np_):
+        n = d["rank_records"][q]
+        letters = int(prob.offsets[b[q + 1]] - prob.offsets[b[q]])
+        # this rank's slice only: packed letters + 1/64 offsets + 3-bit lengths + R2 results
+        assert 5 * letters // 8 <= d["rank_pinned_bytes"][q] <= 5 * letters // 8 + n * (8 / 64 + 3 / 8 + 2) + 64, d
+        assert d["rank_h2d_bytes"][q] <= 5 * letters // 8 + 3 * n // 8 + 64, d
 
 
 @pytest.mark.parametrize("pinned", [False, True])
@@ -512,3 +526,12 @@ def test_graph_replay_sees_new_data():
     newp = Problem(prob.weights, prob.seq1, codes, offsets)
     assert np.array_equal(as_triples(out), as_triples(search_cpu(newp)))
     eng.close()
+
+
+def test_final_binary_built_from_these_sources():
+    # the ./final (and its GPU plugin) under test were built from the checked-out sources, not shipped stale
+    from test_cli import _source_hash
+
+    r = run_final(["--help"], np_=1)
+    assert r.returncode == 0
+    assert f"src={_source_hash()}" in r.stdout.decode()
