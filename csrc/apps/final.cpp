@@ -270,7 +270,7 @@ class Job {
   std::unique_ptr<BulkParser> parser_;  // root: pass 1 done, letters encoded straight into the window
   std::unique_ptr<SharedWindow> text_win_;  // sliced mode, several ranks on the node: the input text
   int64_t pinned_bytes_ = 0, h2d_bytes_ = 0, d2h_bytes_ = 0;  // this rank (--timing)
-  std::vector<int64_t> rank_pinned_, rank_h2d_, rank_records_;  // root: per-rank figures (--timing)
+  std::vector<int64_t> rank_pinned_, rank_h2d_, rank_records_, rank_pin_us_;  // root: per rank (--timing)
   std::shared_ptr<BulkParser> spent_parser_;     // root: filled into the window, freed while printing
   std::shared_ptr<uvector<char>> spent_text_;
   std::vector<Result> results_;  // root: results of the current batch (mpi/rccl transports)
@@ -629,6 +629,28 @@ void Job::run_sliced(BulkParser& parser, int64_t first_index) {
   const int fb = result_bytes(fmt);
   SegmentWindow res(ctx_, fb * n, numa);
   res.set_releaser(&rel_);
+  // GPU ranks page-lock this slice's pieces only (the registration faults in and locks every page)
+  pt_.begin("pin");
+  Stopwatch pin_sw;
+  pin_sw.start();
+  if (gpu && n > 0 && pin_window_) {
+    try {
+      auto pin = [&](const void* ptr, int64_t bytes) {
+        if (ptr && bytes > 0) {
+          eng_.hip->pin(ptr, static_cast<size_t>(bytes));
+          pinned_bytes_ += bytes;
+        }
+      };
+      pin(wb.letters, packed5_bytes(slice.letters));
+      pin(wb.offsets, 8 * wb.offset_entries());
+      pin(wb.lengths, wb.length_bytes());
+      pin(res.mine(), fb * n);
+    } catch (const std::exception& e) {
+      MOC_LOG_WARN("could not page-lock this rank's slice (%s); using the staged pipeline", e.what());
+    }
+  }
+  pin_sw.stop();
+  pt_.end();
   pt_.begin("compute");
   fault_.at("compute", r);
   Stopwatch sw;
@@ -636,28 +658,11 @@ void Job::run_sliced(BulkParser& parser, int64_t first_index) {
   GpuSolveStats gs;
   if (n > 0) {
     if (gpu) {
-      if (pin_window_) {  // this slice's pieces only
-        try {
-          auto pin = [&](const void* ptr, int64_t bytes) {
-            if (ptr && bytes > 0) {
-              eng_.hip->pin(ptr, static_cast<size_t>(bytes));
-              pinned_bytes_ += bytes;
-            }
-          };
-          pin(wb.letters, packed5_bytes(slice.letters));
-          pin(wb.offsets, 8 * wb.offset_entries());
-          pin(wb.lengths, wb.length_bytes());
-          pin(res.mine(), fb * n);
-        } catch (const std::exception& e) {
-          MOC_LOG_WARN("could not page-lock this rank's slice (%s); using the staged pipeline", e.what());
-        }
-      }
       eng_.hip->solve_wire(wb, res.mine(), fmt);
       gs = eng_.hip->last_stats();
       eng_.kernel_ms += gs.kernel_ms;
       h2d_bytes_ += gs.h2d_bytes;
       d2h_bytes_ += gs.d2h_bytes;
-      eng_.hip->unpin_all();
     } else {
       solve_batch_cpu(eng_.table, eng_.seq1.data(), L1, cpu_batch, reinterpret_cast<Result*>(res.mine()), eng_.sem,
                       eng_.threads);
@@ -666,7 +671,9 @@ void Job::run_sliced(BulkParser& parser, int64_t first_index) {
   sw.stop();
   compute_ms_ += sw.total_ms();
   pt_.end();
-  // inputs nobody reads any more go back to the OS while the root prints
+  // inputs nobody reads any more go back to the OS while the root prints: their registrations are
+  // dropped first (the releaser runs its tasks in order), then the pages
+  if (gpu) rel_.defer(eng_.hip->detach_pins());
   letters.set_releaser(&rel_);
   sparse.set_releaser(&rel_);
   dense.set_releaser(&rel_);
@@ -677,9 +684,10 @@ void Job::run_sliced(BulkParser& parser, int64_t first_index) {
   // ---- every rank's result run -> root, which prints them in order straight from the segments
   pt_.begin("gather");
   fault_.at("gather", r);
-  int64_t info[7] = {n, static_cast<int64_t>(fmt), gs.r2.smin, gs.r2.kw, gs.r2.j, pinned_bytes_, h2d_bytes_};
-  std::vector<int64_t> infos(r == kRoot ? static_cast<size_t>(7 * p) : 0);
-  MPI_Gather(info, 7, MPI_INT64_T, infos.data(), 7, MPI_INT64_T, kRoot, ctx_.world);
+  int64_t info[8] = {n,           static_cast<int64_t>(fmt), gs.r2.smin, gs.r2.kw, gs.r2.j, pinned_bytes_, h2d_bytes_,
+                     static_cast<int64_t>(pin_sw.total_ms() * 1000.0)};
+  std::vector<int64_t> infos(r == kRoot ? static_cast<size_t>(8 * p) : 0);
+  MPI_Gather(info, 8, MPI_INT64_T, infos.data(), 8, MPI_INT64_T, kRoot, ctx_.world);
   res.fence();
   pt_.end();
   if (r == kRoot) {
@@ -687,8 +695,9 @@ void Job::run_sliced(BulkParser& parser, int64_t first_index) {
     rank_pinned_.assign(static_cast<size_t>(p), 0);
     rank_h2d_.assign(static_cast<size_t>(p), 0);
     rank_records_.assign(static_cast<size_t>(p), 0);
+    rank_pin_us_.assign(static_cast<size_t>(p), 0);
     for (int q = 0; q < p; ++q) {
-      const int64_t* x = infos.data() + 7 * q;
+      const int64_t* x = infos.data() + 8 * q;
       runs[q].data = res.segment(q);
       runs[q].n = x[0];
       runs[q].fmt = static_cast<ResultFormat>(x[1]);
@@ -696,6 +705,7 @@ void Job::run_sliced(BulkParser& parser, int64_t first_index) {
       rank_records_[q] = x[0];
       rank_pinned_[q] = x[5];
       rank_h2d_[q] = x[6];
+      rank_pin_us_[q] = x[7];
     }
     // a private input text goes back to the OS while the results print
     if (!text_.empty()) {
@@ -815,7 +825,7 @@ void Job::report(const Header& h) {
   std::string per_rank;
   if (!rank_records_.empty())  // sliced mode: what each rank owned, page-locked and moved host->device
     per_rank = ", \"rank_records\": " + list(rank_records_) + ", \"rank_pinned_bytes\": " + list(rank_pinned_) +
-               ", \"rank_h2d_bytes\": " + list(rank_h2d_);
+               ", \"rank_h2d_bytes\": " + list(rank_h2d_) + ", \"rank_pin_us\": " + list(rank_pin_us_);
   std::fprintf(stderr,
                "{\"timing\": %s, \"ranks\": %d, \"nodes\": %d, \"engine\": \"%s\", \"transport\": \"%s\", "
                "\"partition\": \"%s\", \"sliced\": %s, \"batches\": %lld, \"first_index\": %lld, \"records\": %lld, "

@@ -14,6 +14,7 @@
 #include "moc/runtime/device.hpp"
 #include "moc/runtime/hip_check.hpp"
 #include "moc/runtime/log.hpp"
+#include "moc/runtime/pinned.hpp"
 #include "moc/runtime/timer.hpp"
 
 namespace moc {
@@ -73,6 +74,14 @@ class GpuRankImpl final : public GpuRank {
   }
   void pin(const void* p, size_t bytes) override { engine_->pin(p, bytes); }
   void unpin_all() override { engine_->unpin_all(); }
+  std::function<void()> detach_pins() override {
+    auto regs = std::make_shared<std::vector<void*>>(engine_->detach_pins());
+    const int dev = device_;
+    return [regs, dev] {
+      (void)hipSetDevice(dev);
+      pinned::unregister(*regs);
+    };
+  }
   double rccl_batch(const RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds, bool cp,
                     Result* out, const PhaseHooks& hooks) override;
 

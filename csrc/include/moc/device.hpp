@@ -164,6 +164,19 @@ void launch_tile16_keys(const ProblemView& pv, const BatchView& bv, const Plan& 
 // Waves per CU the tile16 kernel keeps resident (16-wave workgroups, as many as the LDS allows).
 int tile16_waves_per_cu(int lds_bytes);
 
+// Loads every kernel file's code object onto the current device now (HIP loads them lazily, at the first
+// launch from each file: milliseconds inside the first timed search of a job otherwise).
+void preload_align_kernels();
+void preload_short_kernels();
+void preload_swipe_kernels();
+void preload_tile16_kernels();
+inline void preload_kernels() {
+  preload_align_kernels();
+  preload_short_kernels();
+  preload_swipe_kernels();
+  preload_tile16_kernels();
+}
+
 // One-wave self-test of the DPP / shuffle primitives (192 ints, see align_kernels.hip).
 void launch_dpp_probe(int* d_out, hipStream_t stream);
 

@@ -64,6 +64,9 @@ class GpuRank {
   virtual GpuSolveStats last_stats() const = 0;
   virtual void pin(const void* p, size_t bytes) = 0;
   virtual void unpin_all() = 0;
+  // Hands over this rank's page-lock registrations: the returned task unregisters them (e.g. on a
+  // BackgroundReleaser, ahead of the unmap of the pages); the engine forgets them at once.
+  virtual std::function<void()> detach_pins() = 0;
   // Creates the RCCL communicator (collective over ctx.world: every rank must call it).
   virtual void init_rccl() = 0;
   // One batch over RCCL (transport=rccl): root uploads, slices scatter over xGMI (or, with `cp`, the

@@ -22,6 +22,7 @@
 
 #include <cstdint>
 #include <memory>
+#include <utility>
 #include <vector>
 
 #include "moc/common.hpp"
@@ -117,6 +118,8 @@ class HipEngine {
   // Page-locks a host range for the lifetime of the engine (or until unpin); enables the direct path.
   void pin(const void* p, size_t bytes);
   void unpin_all();
+  // The registrations made by pin(), handed over to the caller (pinned::unregister them); forgotten here.
+  std::vector<void*> detach_pins() { return std::exchange(pinned_, {}); }
 
   const EngineStats& stats() const { return stats_; }
   int device() const { return device_; }
@@ -138,6 +141,7 @@ class HipEngine {
   void ensure(void*& ptr, size_t& cap, size_t bytes);
   void ensure_host(void*& ptr, size_t& cap, size_t bytes);
   bool direct_pointers(const WireBatch& b, void* out, int fb, dev::ShortArgs& a) const;
+  void prepare_direct(const dev::ProblemView& pv, const dev::ShortArgs& a, bool swipe);
   void launch_direct(const dev::ProblemView& pv, const dev::ShortArgs& a, bool swipe);
   void run_dma_stream(const dev::ProblemView& pv, const dev::ShortArgs& a, bool swipe, const WireBatch& b, void* out,
                       int fb);

@@ -146,6 +146,11 @@ __global__ void dpp_probe_kernel(int* out) {
   out[128 + lane] = wave_max_i32((lane * 7) % 61);
 }
 
+void preload_align_kernels() {
+  hipFuncAttributes fa;
+  (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&dpp_probe_kernel));
+}
+
 void launch_dpp_probe(int* d_out, hipStream_t stream) {
   hipLaunchKernelGGL(dpp_probe_kernel, dim3(1), dim3(64), 0, stream, d_out);
 }

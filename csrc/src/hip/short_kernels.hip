@@ -245,6 +245,11 @@ __global__ void unpack5_kernel(const uint8_t* __restrict__ packed, int64_t bit0,
   }
 }
 
+void preload_short_kernels() {
+  hipFuncAttributes fa;
+  (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&unpack5_kernel));
+}
+
 void launch_unpack5(const uint8_t* packed, int64_t bit0, int64_t n, uint8_t* out, hipStream_t stream) {
   if (n <= 0) return;
   const int64_t blocks = std::min<int64_t>((n + kBlock - 1) / kBlock, 4096);

@@ -373,6 +373,11 @@ bool configure_swipe(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs
   return false;
 }
 
+void preload_swipe_kernels() {
+  hipFuncAttributes fa;
+  (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&swipe_search_kernel<24, 4, true>));
+}
+
 void launch_swipe(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStream_t stream) {
   if (a.n <= 0) return;
   const int noff = a.slot, l2w = a.rpw;

@@ -358,6 +358,11 @@ void launch16_t(const ProblemView& pv, const BatchView& bv, const Plan& plan, hi
 }
 }  // namespace
 
+void preload_tile16_kernels() {
+  hipFuncAttributes fa;
+  (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&resolve16_kernel));
+}
+
 void launch_tile16_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream) {
   if (!pv.prof16 || pv.prof16_bytes <= 0 || tile16_lds_bytes(pv.prof16_bytes, pv.L1) > kProf16MaxLds ||
       (pv.prof16_bytes & 15))

@@ -66,7 +66,19 @@ std::vector<void*> register_range(const void* p, size_t bytes) {
       continue;
     }
     const uintptr_t run_end = std::min(e, it == r.end() ? e : it->first);
-    MOC_HIP_CHECK(hipHostRegister(reinterpret_cast<void*>(x), run_end - x, hipHostRegisterMapped));
+    const hipError_t rc = hipHostRegister(reinterpret_cast<void*>(x), run_end - x, hipHostRegisterMapped);
+    if (rc != hipSuccess) {
+      // all or nothing: the runs registered by this call are dropped again (a caller that catches the
+      // error never receives them, so nobody else could unregister them; a later mapping at the same
+      // addresses would then count as page-locked)
+      (void)hipGetLastError();
+      for (void* q : made) {
+        (void)hipHostUnregister(q);
+        r.erase(reinterpret_cast<uintptr_t>(q));
+      }
+      (void)hipGetLastError();
+      MOC_HIP_CHECK(rc);
+    }
     r.emplace(x, run_end);
     made.push_back(reinterpret_cast<void*>(x));
     x = run_end;

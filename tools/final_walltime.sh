@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 for np in 1 2; do
   for i in 1 2 3 4 5 6; do
     s=$(date +%s%N)
-    timeout -k 10 120 /opt/conda/bin/mpiexec -np $np ./final --backend=$BACKEND --timing \
+    timeout -k 10 120 /opt/conda/bin/mpiexec -np $np ./final --backend=$BACKEND --timing --device=0 \
       --input=tests/data/input$i.txt > gpurun_out/final_out_$i.txt 2> gpurun_out/final_timing_$i.txt
     e=$(date +%s%N)
     cmp -s gpurun_out/final_out_$i.txt tests/data/expected/input$i.out && ok=ok || ok=MISMATCH
