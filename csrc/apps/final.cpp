@@ -587,6 +587,9 @@ void Job::run_sliced(BulkParser& parser, int64_t first_index) {
       job.cells += x[5];
     }
     cells_ += job.cells;
+    // every slice is encoded: the helpers return the node-shared input text's pages to the OS while
+    // their GPUs search and the root prints
+    if (text_win_) text_win_->release_shares(ctx_);
     try {
       parser.check(job);
     } catch (const std::exception& e) {
@@ -932,6 +935,7 @@ int Job::run() {
     }
     text_len = sz[1];
     text_win_ = std::make_unique<SharedWindow>(ctx_, text_len + 64);
+    text_win_->prefault_shares(ctx_);  // every rank faults in a share of the pages the root reads into
     text = text_win_->base();
     if (ctx_.rank == kRoot) {
       pt_.begin("read");

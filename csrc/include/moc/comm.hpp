@@ -68,6 +68,14 @@ class SharedWindow {
   char* base() const { return base_; }
   int64_t bytes() const { return bytes_; }
   void fence() const;  // MPI_Win_sync + node barrier: makes the owner's writes visible
+  // Collective over the node: every rank allocates (faults in) its 1/local_size share of the window's
+  // pages with its threads, so the owner's later fill runs into present pages (a shared mapping has no
+  // huge pages here: 4 KiB faults, ~1 us each, are what a single-threaded fill would pay one by one).
+  void prefault_shares(const MpiContext& ctx);
+  // Not collective: ranks other than the node's local rank 0 return the window's pages to the OS in
+  // shares (MADV_REMOVE), in parallel, while local rank 0 goes on (e.g. the root printing). The contents
+  // are gone afterwards; the later collective free then has nothing left to release.
+  void release_shares(const MpiContext& ctx);
   // Single-rank nodes (private mapping) only, no-op otherwise: every later release of this window's pages
   // goes through `rel` (FIFO, background thread) instead of the caller's thread. `rel` must outlive the
   // queued tasks (drain it before the process ends).

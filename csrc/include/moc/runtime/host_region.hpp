@@ -44,6 +44,11 @@ class HostRegion {
   BackgroundReleaser* releaser_ = nullptr;
 };
 
+// Writes one byte of every 4 KiB page of [p, p + bytes) (zero), OpenMP-parallel: allocates the pages of
+// a fresh shared mapping up front, several threads (and ranks) faulting at once instead of one copy loop
+// faulting them in one by one. The contents become zero.
+void prefault_pages(char* p, size_t bytes);
+
 // Binds [p, p + bytes) to NUMA node `node` (MPOL_PREFERRED: falls back elsewhere when the node is
 // full); best effort, returns false when the kernel refuses. Pages already present are not moved.
 bool bind_range_to_node(void* p, size_t bytes, int node);

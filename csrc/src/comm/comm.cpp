@@ -196,6 +196,23 @@ void SharedWindow::discard(int64_t off, int64_t len) {
     (void)madvise(p, n, MADV_DONTNEED);
 }
 
+void SharedWindow::prefault_shares(const MpiContext& ctx) {
+  if (map_) return;  // private mapping: huge pages, faulted by the fill
+  const int64_t pages = (bytes_ + 4095) / 4096;
+  const int64_t b = pages * ctx.local_rank / ctx.local_size, e = pages * (ctx.local_rank + 1) / ctx.local_size;
+  prefault_pages(base_ + 4096 * b, static_cast<size_t>(std::min(bytes_, 4096 * e) - std::min(bytes_, 4096 * b)));
+  fence();
+}
+
+void SharedWindow::release_shares(const MpiContext& ctx) {
+  if (map_ || ctx.local_size < 2 || ctx.local_rank == 0) return;
+  const int64_t pages = bytes_ / 4096;  // whole pages inside the window only
+  const uintptr_t first = (reinterpret_cast<uintptr_t>(base_) + 4095) & ~uintptr_t{4095};
+  const int64_t helpers = ctx.local_size - 1, q = ctx.local_rank - 1;
+  const int64_t b = pages * q / helpers, e = pages * (q + 1) / helpers;
+  if (e > b) (void)madvise(reinterpret_cast<void*>(first + 4096 * b), static_cast<size_t>(4096 * (e - b)), MADV_REMOVE);
+}
+
 void SharedWindow::fence() const {
   if (map_) return;  // one rank on the node
   MOC_MPI_CHECK(MPI_Win_sync(win_));
@@ -221,6 +238,7 @@ SegmentWindow::SegmentWindow(const MpiContext& ctx, int64_t my_bytes, int numa_n
   MPI_Info_free(&info);
   MOC_MPI_CHECK(rc);
   if (numa_node >= 0) (void)bind_range_to_node(base, static_cast<size_t>(std::max<int64_t>(my_bytes, 8)), numa_node);
+  prefault_pages(static_cast<char*>(base), static_cast<size_t>(my_bytes));  // this rank's threads, in parallel
   for (int r = 0; r < ctx.local_size; ++r) {
     MPI_Aint sz = 0;
     int disp = 0;

@@ -26,6 +26,13 @@ bool bind_range_to_node(void* p, size_t bytes, int node) {
   return syscall(SYS_mbind, reinterpret_cast<void*>(lo), hi - lo, kMpolPreferred, mask, sizeof(mask) * 8, 0) == 0;
 }
 
+void prefault_pages(char* p, size_t bytes) {
+  constexpr size_t kPage = 4096;
+  const int64_t pages = static_cast<int64_t>((bytes + kPage - 1) / kPage);
+#pragma omp parallel for schedule(static) if (pages > 1024)
+  for (int64_t q = 0; q < pages; ++q) p[static_cast<size_t>(q) * kPage] = 0;
+}
+
 HostRegion::HostRegion(size_t bytes, int numa_node) {
   const size_t want = (std::max<size_t>(bytes, 1) + kHuge - 1) & ~(kHuge - 1);
   map_bytes_ = want + kHuge;  // slack to start on a 2 MiB boundary
