@@ -35,7 +35,7 @@ LDROCM    := -L$(ROCM)/lib -lamdhip64 -Wl,-rpath,$(ROCM)/lib
 GPU_PLUGIN := mpi_openmp_cuda_amd/lib/libmoc_final_gpu.so
 
 # host core without any ROCm dependency (parser, CPU engine, partitioner, runtime utilities)
-CPU_SRCS  := csrc/src/cpu_engine.cpp csrc/src/io.cpp csrc/src/partition.cpp csrc/src/problem.cpp csrc/src/wire.cpp \
+CPU_SRCS  := csrc/src/cpu_engine.cpp csrc/src/device_batch.cpp csrc/src/io.cpp csrc/src/partition.cpp csrc/src/problem.cpp csrc/src/wire.cpp \
              csrc/src/score_table.cpp csrc/src/runtime/runtime.cpp csrc/src/runtime/host_region.cpp
 # host code of the GPU engine (HIP runtime API) and the C ABI of libmoc.so
 GPU_SRCS  := csrc/src/hip_engine.cpp csrc/src/capi.cpp csrc/src/runtime/device.cpp csrc/src/runtime/pinned.cpp
@@ -44,7 +44,7 @@ HIP_SRCS  := $(wildcard csrc/src/hip/*.hip)
 CPU_OBJS  := $(patsubst csrc/src/%.cpp,$(OBJ)/%.o,$(CPU_SRCS))
 CORE_OBJS := $(patsubst csrc/src/%.cpp,$(OBJ)/%.o,$(CORE_SRCS))
 HIP_OBJS  := $(patsubst csrc/src/%.hip,$(OBJ)/%.o,$(HIP_SRCS))
-COMM_OBJS := $(OBJ)/comm/comm.o
+COMM_OBJS := $(OBJ)/comm/comm.o $(OBJ)/comm/mpi_device_comm.o
 RCCL_OBJS := $(OBJ)/comm/rccl_comm.o
 HEADERS   := $(shell find csrc/include -name '*.h' -o -name '*.hpp')
 
@@ -106,7 +106,7 @@ $(GPU_PLUGIN): $(OBJ)/apps/final_gpu.o $(RCCL_OBJS) $(COMM_OBJS) $(PKG_LIB) $(MP
 
 # Host-side sanitizers (GPU ASan is not available on the target pool). ./final links no ROCm code, so
 # the sanitized binaries cover everything the CPU backend runs; a GPU rank would dlopen the plugin.
-SAN_SRCS := $(CPU_SRCS) csrc/src/comm/comm.cpp csrc/apps/final.cpp
+SAN_SRCS := $(CPU_SRCS) csrc/src/comm/comm.cpp csrc/src/comm/mpi_device_comm.cpp csrc/apps/final.cpp
 asan: $(MPILIB)/libmpi.so
 	@rm -rf $(BUILD)/asan && mkdir -p $(BUILD)/asan
 	for f in $(SAN_SRCS); do \

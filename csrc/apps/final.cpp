@@ -14,7 +14,9 @@
 //   5. Distribution by transport:
 //        shm  — root parses once into an MPI shared window; each rank reads its slice over its own PCIe
 //               link (zero-copy when the window is pinned) and writes results back in place;
-//        rccl — root uploads, RCCL grouped send/recv scatters slices over xGMI, results gathered back;
+//        rccl — root packs each rank's slice into its wire form, a pipeline overlaps packing, upload and
+//               the RCCL send over xGMI, every rank searches in device memory, narrow results are gathered
+//               (device_batch.cpp); rccl-emul runs that same driver over MPI on CPU ranks;
 //        mpi  — host Scatterv/Gatherv (CPU backend, or GPU ranks without a shared window).
 //   6. Every rank runs its engine (HIP kernels, or the OpenMP CPU engine), root prints in order.
 // Any error on any rank -> message + MPI_Abort (reference: exit(1) without abort, peers hang, B11).
@@ -34,6 +36,8 @@
 
 #include "moc/comm.hpp"
 #include "moc/cpu_engine.hpp"
+#include "moc/device_comm.hpp"
+#include "moc/mpi_device_comm.hpp"
 #include "moc/gpu_rank.hpp"
 #include "moc/io.hpp"
 #include "moc/partition.hpp"
@@ -62,7 +66,8 @@ const char* kUsage =
     "                              >= --gpu-min-cells cells per rank, default 3e8; else the OpenMP engine)\n"
     "  --gpu-prewarm-bytes=B       start the HIP runtime during the parse when the input file has >= B bytes\n"
     "                              (default 64 MiB; 0 = never)\n"
-    "  --transport=auto|shm|rccl|mpi   record distribution (auto: shm on one node, else rccl/mpi)\n"
+    "  --transport=auto|shm|rccl|rccl-emul|mpi   record distribution (auto: shm on one node, else rccl/mpi;\n"
+    "                              rccl-emul: the rccl driver over MPI on CPU ranks)\n"
     "  --semantics=reference|spec  candidate set (spec adds the un-mutated final offset, bug B8)\n"
     "  --partition=cost|even|offsets   rank decomposition (offsets: split every record's offset range)\n"
     "  --batch-records=B           streaming mode: parse/search/print B records at a time (0 = all at once)\n"
@@ -273,7 +278,8 @@ class Job {
   std::vector<int64_t> rank_pinned_, rank_h2d_, rank_records_, rank_pin_us_;  // root: per rank (--timing)
   std::shared_ptr<BulkParser> spent_parser_;     // root: filled into the window, freed while printing
   std::shared_ptr<uvector<char>> spent_text_;
-  std::vector<Result> results_;  // root: results of the current batch (mpi/rccl transports)
+  std::vector<Result> results_;  // root: results of the current batch (mpi transport)
+  std::unique_ptr<MpiDeviceComm> emul_comm_;  // --transport=rccl-emul
   std::future<void> prewarm_;     // HIP runtime start-up overlapped with the parse (large inputs)
 };
 
@@ -310,7 +316,8 @@ void Job::setup_engine(int64_t cells) {
   if (transport_ == "auto") transport_ = ctx_.single_node() ? "shm" : (all_gpu_ ? "rccl" : "mpi");
   if (transport_ == "shm" && !ctx_.single_node()) throw Error("--transport=shm needs all ranks on one node");
   if (transport_ == "rccl" && !all_gpu_) throw Error("--transport=rccl needs a GPU on every rank");
-  if (transport_ != "shm" && transport_ != "rccl" && transport_ != "mpi")
+  if (transport_ == "rccl-emul" && any_gpu) throw Error("--transport=rccl-emul runs on CPU ranks (--backend=cpu)");
+  if (transport_ != "shm" && transport_ != "rccl" && transport_ != "rccl-emul" && transport_ != "mpi")
     throw Error("unknown --transport " + transport_);
   partition_ = to_lower(flags_.get("partition", "cost"));
   if (partition_ != "cost" && partition_ != "even" && partition_ != "offsets")
@@ -321,6 +328,7 @@ void Job::setup_engine(int64_t cells) {
     throw Error("--partition=offsets needs the same backend on every rank (use --backend=hip or --backend=cpu)");
   pin_window_ = flags_.get_bool("pin-window", true);
   if (transport_ == "rccl") eng_.hip->init_rccl();
+  if (transport_ == "rccl-emul") emul_comm_ = std::make_unique<MpiDeviceComm>(ctx_);
   MOC_LOG_INFO("rank %d/%d host %s local %d/%d engine=%s device=%d transport=%s partition=%s", ctx_.rank, ctx_.size,
                ctx_.hostname.c_str(), ctx_.local_rank, ctx_.local_size, eng_.gpu ? "hip" : "cpu", device_,
                transport_.c_str(), partition_.c_str());
@@ -810,9 +818,21 @@ void Job::batch_rccl(RecordBatch* rb, int64_t n, int64_t total_chars, const std:
     fault_.at(phase, ctx_.rank);
   };
   hooks.end = [this] { pt_.end(); };
-  if (ctx_.rank == kRoot) results_.resize(static_cast<size_t>(n));
-  compute_ms_ += eng_.hip->rccl_batch(rb, n, total_chars, bounds, cp, results_.data(), hooks);
-  print(results_.data(), n, 0);
+  DeviceBatchOut out;
+  if (emul_comm_) {
+    CpuDeviceSearch ds(eng_.table, eng_.seq1, eng_.sem, eng_.threads);
+    out = device_batch(*emul_comm_, ds, rb, n, total_chars, bounds, cp, hooks);
+  } else {
+    out = device_batch(eng_.hip->device_comm(), eng_.hip->device_search(), rb, n, total_chars, bounds, cp, hooks);
+  }
+  compute_ms_ += out.compute_ms;
+  eng_.kernel_ms += out.kernel_ms;
+  if (ctx_.rank == kRoot) {
+    if (!out.rank_records.empty()) rank_records_ = out.rank_records;
+    pt_.begin("print");
+    write_results(out_, out.runs, first_index_);
+    pt_.end();
+  }
 }
 
 void Job::report(const Header& h) {

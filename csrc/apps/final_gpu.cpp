@@ -1,6 +1,6 @@
-// GPU side of `final` (plugin, see moc/gpu_rank.hpp): HIP engine per rank, RCCL communicator, and the
-// rccl transport's batch (root upload, grouped send/recv scatter over xGMI, gather of packed results; or
-// in context-parallel mode a broadcast of the batch and a MAX all-reduce of packed keys).
+// GPU side of `final` (plugin, see moc/gpu_rank.hpp): HIP engine per rank, and the rccl transport's device
+// layer (moc/device_comm.hpp): RCCL over xGMI + the engine over device-resident wire batches. The batch
+// driver itself (device_batch.cpp) is shared with the MPI-emulated device layer of CPU ranks.
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
@@ -8,6 +8,8 @@
 #include <vector>
 
 #include "moc/comm.hpp"
+#include "moc/device.hpp"
+#include "moc/device_comm.hpp"
 #include "moc/gpu_rank.hpp"
 #include "moc/hip_engine.hpp"
 #include "moc/rccl_comm.hpp"
@@ -19,6 +21,139 @@
 
 namespace moc {
 namespace {
+
+// RCCL over xGMI as the rccl transport's device layer: comm lane = the engine's compute stream (so the
+// searches and the collectives are ordered without host waits), copy lane = a stream of its own.
+class RcclDeviceComm final : public DeviceComm {
+ public:
+  RcclDeviceComm(const MpiContext& ctx, int device, hipStream_t comm_lane)
+      : ctx_(ctx), device_(device), s_(comm_lane), nccl_(ctx, device) {
+    MOC_HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
+  }
+  ~RcclDeviceComm() override {
+    (void)hipStreamSynchronize(copy_);
+    for (hipEvent_t e : events_) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(copy_);
+  }
+  int rank() const override { return ctx_.rank; }
+  int size() const override { return ctx_.size; }
+  const char* name() const override { return "rccl"; }
+  void* dev_alloc(int64_t bytes) override {
+    void* p = nullptr;
+    MOC_HIP_CHECK(hipMalloc(&p, static_cast<size_t>(std::max<int64_t>(bytes, 16))));
+    return p;
+  }
+  void dev_free(void* p) override { (void)hipFree(p); }
+  void* host_alloc(int64_t bytes) override {
+    void* p = nullptr;
+    MOC_HIP_CHECK(hipHostMalloc(&p, static_cast<size_t>(std::max<int64_t>(bytes, 16)), hipHostMallocDefault));
+    return p;
+  }
+  void host_free(void* p) override { (void)hipHostFree(p); }
+  int upload(void* d, const void* h, int64_t bytes) override {
+    if (bytes > 0) MOC_HIP_CHECK(hipMemcpyAsync(d, h, static_cast<size_t>(bytes), hipMemcpyHostToDevice, copy_));
+    return record(copy_);
+  }
+  void wait_upload(int ticket) override { MOC_HIP_CHECK(hipStreamWaitEvent(s_, events_[ticket], 0)); }
+  void download(void* h, const void* d, int64_t bytes) override {
+    if (bytes > 0) MOC_HIP_CHECK(hipMemcpyAsync(h, d, static_cast<size_t>(bytes), hipMemcpyDeviceToHost, s_));
+    sync();
+  }
+  void group_start() override { nccl(ncclGroupStart(), "ncclGroupStart"); }
+  void group_end() override { nccl(ncclGroupEnd(), "ncclGroupEnd"); }
+  void send(const void* d, int64_t bytes, int peer) override {
+    if (bytes > 0) nccl(ncclSend(d, static_cast<size_t>(bytes), ncclUint8, peer, nccl_.comm(), s_), "ncclSend");
+  }
+  void recv(void* d, int64_t bytes, int peer) override {
+    if (bytes > 0) nccl(ncclRecv(d, static_cast<size_t>(bytes), ncclUint8, peer, nccl_.comm(), s_), "ncclRecv");
+  }
+  void bcast(void* d, int64_t bytes, int root) override { nccl_.bcast(d, bytes, root, s_); }
+  void allreduce_max_u64(uint64_t* d, int64_t n) override { nccl_.allreduce_max_u64(d, n, s_); }
+  void sync() override {
+    MOC_HIP_CHECK(hipStreamSynchronize(s_));
+    nccl_.check_async();
+  }
+  int mark() override { return record(s_); }
+  void wait_mark(int m) override { MOC_HIP_CHECK(hipEventSynchronize(events_[m])); }
+
+ private:
+  static void nccl(ncclResult_t r, const char* what) {
+    if (r != ncclSuccess) throw Error(std::string(what) + ": " + ncclGetErrorString(r));
+  }
+  int record(hipStream_t st) {
+    hipEvent_t e = nullptr;
+    MOC_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    MOC_HIP_CHECK(hipEventRecord(e, st));
+    events_.push_back(e);
+    return static_cast<int>(events_.size()) - 1;
+  }
+  const MpiContext& ctx_;
+  int device_;
+  hipStream_t s_, copy_ = nullptr;
+  RcclComm nccl_;
+  std::vector<hipEvent_t> events_;
+};
+
+// The HIP engine over device-resident wire batches: the packed narrow form streams through the swipe
+// kernel straight from device memory; the dense form is unpacked on the device and searched by the
+// record/tile kernels (R12 results).
+class HipDeviceSearch final : public DeviceSearch {
+ public:
+  explicit HipDeviceSearch(HipEngine& e) : e_(e) {}
+  ~HipDeviceSearch() override { (void)hipFree(scratch_); }
+  bool streams_packed(int64_t min_l2, int64_t max_l2) const override { return e_.streams_packed(min_l2, max_l2); }
+  ResultFormat result_format(int64_t min_l2, int64_t max_l2, bool packed_form) const override {
+    return packed_form ? e_.auto_format(max_l2, min_l2) : ResultFormat::R12;
+  }
+  void solve(const WireBatch& b, void* d_out, ResultFormat fmt) override {
+    kernel_ms_ = 0;
+    r2_ = R2Params{};
+    if (b.off_shift) {
+      e_.solve_wire(b, d_out, fmt);
+      kernel_ms_ = e_.stats().kernel_ms;
+      r2_ = e_.stats().r2;
+      return;
+    }
+    if (fmt != ResultFormat::R12) throw Error("the dense device form returns R12 results");
+    hipStream_t s = e_.compute_stream();
+    std::vector<int64_t> h_offs(static_cast<size_t>(b.n) + 1);
+    MOC_HIP_CHECK(hipMemcpyAsync(h_offs.data(), b.offsets, 8 * h_offs.size(), hipMemcpyDeviceToHost, s));
+    MOC_HIP_CHECK(hipStreamSynchronize(s));
+    const int64_t letters = h_offs[b.n] - h_offs[0];
+    if (b.packed5) {
+      if (static_cast<size_t>(letters) + 64 > scratch_cap_) {
+        (void)hipFree(scratch_);
+        scratch_cap_ = static_cast<size_t>(letters) + 64;
+        MOC_HIP_CHECK(hipMalloc(&scratch_, scratch_cap_));
+      }
+      dev::launch_unpack5(b.letters, 5 * h_offs[0], letters, static_cast<uint8_t*>(scratch_), s);
+      MOC_HIP_CHECK(hipGetLastError());
+      // record i of the unpacked copy at scratch + offsets[i] - offsets[0]: offsets start at 0 here
+      e_.solve_device(static_cast<const uint8_t*>(scratch_), b.offsets, h_offs.data(), b.n, static_cast<Result*>(d_out), s);
+    } else {
+      e_.solve_device(b.letters, b.offsets, h_offs.data(), b.n, static_cast<Result*>(d_out), s);
+    }
+    MOC_HIP_CHECK(hipStreamSynchronize(s));
+  }
+  void search_keys(const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets, int64_t n, int part,
+                   int parts, uint64_t* d_keys) override {
+    e_.search_keys_device(d_codes, d_offsets, h_offsets, n, part, parts, reinterpret_cast<unsigned long long*>(d_keys),
+                          e_.compute_stream());
+  }
+  void finalize_keys(const int64_t* d_offsets, int64_t n, const uint64_t* d_keys, Result* d_out) override {
+    e_.finalize_keys_device(d_offsets, n, reinterpret_cast<const unsigned long long*>(d_keys), d_out, ResultFormat::R12,
+                            e_.compute_stream());
+  }
+  double last_kernel_ms() const override { return kernel_ms_; }
+  R2Params last_r2() const override { return r2_; }
+
+ private:
+  HipEngine& e_;
+  void* scratch_ = nullptr;
+  size_t scratch_cap_ = 0;
+  double kernel_ms_ = 0;
+  R2Params r2_{};
+};
 
 class GpuRankImpl final : public GpuRank {
  public:
@@ -39,7 +174,16 @@ class GpuRankImpl final : public GpuRank {
     numa_ = bind_numa_to_device(device_);
   }
   void init_rccl() override {
-    if (!nccl_) nccl_ = std::make_unique<RcclComm>(ctx_, device_);
+    if (!dc_) dc_ = std::make_unique<RcclDeviceComm>(ctx_, device_, engine_->compute_stream());
+    if (!ds_) ds_ = std::make_unique<HipDeviceSearch>(*engine_);
+  }
+  DeviceComm& device_comm() override {
+    init_rccl();
+    return *dc_;
+  }
+  DeviceSearch& device_search() override {
+    init_rccl();
+    return *ds_;
   }
   int device() const override { return device_; }
   void set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, Semantics sem) override {
@@ -82,138 +226,15 @@ class GpuRankImpl final : public GpuRank {
       pinned::unregister(*regs);
     };
   }
-  double rccl_batch(const RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds, bool cp,
-                    Result* out, const PhaseHooks& hooks) override;
 
  private:
   const MpiContext& ctx_;
   int device_ = -1;
   int numa_ = -1;
   std::unique_ptr<HipEngine> engine_;
-  std::unique_ptr<RcclComm> nccl_;
+  std::unique_ptr<DeviceSearch> ds_;  // destroyed after dc_ (declared before it)
+  std::unique_ptr<DeviceComm> dc_;
 };
-
-// Device buffers of one rccl batch (freed on scope exit, also when unwinding).
-struct DeviceBufs {
-  std::vector<void*> ptrs;
-  template <typename T>
-  T* alloc(int64_t bytes) {
-    void* p = nullptr;
-    MOC_HIP_CHECK(hipMalloc(&p, static_cast<size_t>(std::max<int64_t>(bytes, 16))));
-    ptrs.push_back(p);
-    return static_cast<T*>(p);
-  }
-  ~DeviceBufs() {
-    for (void* p : ptrs) (void)hipFree(p);
-  }
-};
-
-double GpuRankImpl::rccl_batch(const RecordBatch* rb, int64_t n, int64_t total_chars,
-                               const std::vector<int64_t>& bounds, bool cp, Result* out, const PhaseHooks& hooks) {
-  if (!nccl_) throw Error("rccl_batch: the RCCL communicator was not created");
-  RcclComm& nccl = *nccl_;
-  hipStream_t s = engine_->compute_stream();
-  double compute_ms = 0;
-  const int p = ctx_.size;
-  DeviceBufs bufs;
-  hooks.begin("distribute");
-  if (cp) {
-    // root uploads the batch once; RCCL broadcasts it to every device over xGMI; each GPU searches its
-    // share of every record's offset tiles; ncclAllReduce(MAX, uint64) combines the packed keys.
-    uint8_t* d_codes = bufs.alloc<uint8_t>(total_chars);
-    int64_t* d_offs = bufs.alloc<int64_t>(8 * (n + 1));
-    std::vector<int64_t> h_offs(static_cast<size_t>(n) + 1);
-    if (ctx_.rank == kRoot) {
-      h_offs.assign(rb->offsets.begin(), rb->offsets.end());
-      MOC_HIP_CHECK(hipMemcpyAsync(d_codes, rb->codes.data(), total_chars, hipMemcpyHostToDevice, s));
-      MOC_HIP_CHECK(hipMemcpyAsync(d_offs, rb->offsets.data(), 8 * (n + 1), hipMemcpyHostToDevice, s));
-    }
-    nccl.bcast(d_codes, total_chars, kRoot, s);
-    nccl.bcast(d_offs, 8 * (n + 1), kRoot, s);
-    bcast_bytes(h_offs.data(), 8 * (n + 1), kRoot, ctx_.world);  // host copy for tile planning
-    MOC_HIP_CHECK(hipStreamSynchronize(s));
-    nccl.check_async();
-    hooks.end();
-    hooks.begin("compute");
-    Stopwatch sw;
-    sw.start();
-    auto* d_keys = bufs.alloc<unsigned long long>(8 * n);
-    engine_->search_keys_device(d_codes, d_offs, h_offs.data(), n, ctx_.rank, ctx_.size, d_keys, s);
-    MOC_HIP_CHECK(hipStreamSynchronize(s));
-    sw.stop();
-    compute_ms += sw.total_ms();
-    hooks.end();
-    hooks.begin("gather");
-    nccl.allreduce_max_u64(d_keys, n, s);
-    if (ctx_.rank == kRoot) {
-      auto* d_res = bufs.alloc<Result>(12 * n);
-      engine_->finalize_keys_device(d_offs, n, d_keys, d_res, ResultFormat::R12, s);
-      MOC_HIP_CHECK(hipMemcpyAsync(out, d_res, 12 * n, hipMemcpyDeviceToHost, s));
-    }
-    MOC_HIP_CHECK(hipStreamSynchronize(s));
-    nccl.check_async();
-    hooks.end();
-    return compute_ms;
-  }
-  const int64_t my_b = bounds[ctx_.rank], my_n = bounds[ctx_.rank + 1] - my_b;
-  // counts in bytes for codes and (absolute) offsets; each rank receives n_r+1 offsets
-  std::vector<int64_t> ccount(p), cdispl(p), ocount(p), odispl(p);
-  if (ctx_.rank == kRoot) {
-    for (int r = 0; r < p; ++r) {
-      ccount[r] = rb->offsets[bounds[r + 1]] - rb->offsets[bounds[r]];
-      cdispl[r] = rb->offsets[bounds[r]];
-    }
-  }
-  bcast_bytes(ccount.data(), 8 * p, kRoot, ctx_.world);
-  bcast_bytes(cdispl.data(), 8 * p, kRoot, ctx_.world);
-  for (int r = 0; r < p; ++r) {
-    ocount[r] = 8 * (bounds[r + 1] - bounds[r] + 1);
-    odispl[r] = 8 * bounds[r];
-  }
-  uint8_t* d_all_codes = nullptr;
-  int64_t* d_all_offs = nullptr;
-  Result* d_all_out = nullptr;
-  if (ctx_.rank == kRoot) {
-    d_all_codes = bufs.alloc<uint8_t>(total_chars);
-    d_all_offs = bufs.alloc<int64_t>(8 * (n + 1));
-    d_all_out = bufs.alloc<Result>(12 * n);
-    MOC_HIP_CHECK(hipMemcpyAsync(d_all_codes, rb->codes.data(), total_chars, hipMemcpyHostToDevice, s));
-    MOC_HIP_CHECK(hipMemcpyAsync(d_all_offs, rb->offsets.data(), 8 * (n + 1), hipMemcpyHostToDevice, s));
-  }
-  uint8_t* d_codes = bufs.alloc<uint8_t>(ccount[ctx_.rank]);
-  int64_t* d_offs = bufs.alloc<int64_t>(8 * (my_n + 1));
-  Result* d_out = bufs.alloc<Result>(12 * my_n);
-  nccl.scatterv(d_all_codes, ccount, cdispl, d_codes, kRoot, s);
-  nccl.scatterv(d_all_offs, ocount, odispl, d_offs, kRoot, s);
-  std::vector<int64_t> h_offs(static_cast<size_t>(my_n) + 1);
-  MOC_HIP_CHECK(hipMemcpyAsync(h_offs.data(), d_offs, 8 * (my_n + 1), hipMemcpyDeviceToHost, s));
-  MOC_HIP_CHECK(hipStreamSynchronize(s));
-  nccl.check_async();
-  hooks.end();
-  hooks.begin("compute");
-  Stopwatch sw;
-  sw.start();
-  // d_codes holds this rank's letters starting at absolute offset h_offs[0]
-  if (my_n > 0) engine_->solve_device(d_codes - h_offs[0], d_offs, h_offs.data(), my_n, d_out, s);
-  MOC_HIP_CHECK(hipStreamSynchronize(s));
-  sw.stop();
-  compute_ms += sw.total_ms();
-  hooks.end();
-  hooks.begin("gather");
-  std::vector<int64_t> rcount(p), rdispl(p);
-  for (int r = 0; r < p; ++r) {
-    rcount[r] = 12 * (bounds[r + 1] - bounds[r]);
-    rdispl[r] = 12 * bounds[r];
-  }
-  nccl.gatherv(d_out, 12 * my_n, d_all_out, rcount, rdispl, kRoot, s);
-  if (ctx_.rank == kRoot) {
-    MOC_HIP_CHECK(hipMemcpyAsync(out, d_all_out, 12 * n, hipMemcpyDeviceToHost, s));
-  }
-  MOC_HIP_CHECK(hipStreamSynchronize(s));
-  nccl.check_async();
-  hooks.end();
-  return compute_ms;
-}
 
 }  // namespace
 }  // namespace moc

@@ -1,0 +1,98 @@
+// The rccl transport's device layer, ROCm-free so `final` (and its CPU-only builds and tests) can drive it.
+//
+// Reference: MPI_Bcast x4, MPI_Scatter of fixed 2000-byte records and MPI_Gather x3 of three int arrays, on
+// host memory, blocking, rooted at 0 (main.c:149-152, 174, 195-197), then a cudaMemcpy of the chunk
+// (cudaFunctions.cu:201) — every byte crosses the host twice.
+//
+// Here the distribution of a batch is written once (device_batch.cpp) against two narrow interfaces:
+//   DeviceComm   — one rank's device memory and its communicator, stream-ordered: RCCL over xGMI on GPU
+//                  ranks (the GPU plugin), or MpiDeviceComm, which emulates it over host memory and MPI
+//                  point-to-point, so the very same driver runs on CPU-only ranks (--transport=rccl-emul)
+//                  and the multi-rank logic is tested without GPUs;
+//   DeviceSearch — the rank's engine over device-resident wire-format batches (moc/wire.hpp).
+#pragma once
+
+#include <cstdint>
+#include <functional>
+#include <vector>
+
+#include "moc/common.hpp"
+#include "moc/problem.hpp"
+#include "moc/wire.hpp"
+
+namespace moc {
+
+// Phase hooks of the caller's timer / fault injection (the device batch runs its own phases).
+struct PhaseHooks {
+  std::function<void(const char*)> begin;  // starts a phase (and fires the fault hook for it)
+  std::function<void()> end;
+};
+
+class DeviceComm {
+ public:
+  virtual ~DeviceComm() = default;
+  virtual int rank() const = 0;
+  virtual int size() const = 0;
+  virtual const char* name() const = 0;
+  // device memory of this rank, and page-locked host staging for asynchronous uploads
+  virtual void* dev_alloc(int64_t bytes) = 0;
+  virtual void dev_free(void* p) = 0;
+  virtual void* host_alloc(int64_t bytes) = 0;
+  virtual void host_free(void* p) = 0;
+  // host -> device on the copy lane (returns at once); the ticket orders later comm-lane work after it
+  virtual int upload(void* d, const void* h, int64_t bytes) = 0;
+  virtual void wait_upload(int ticket) = 0;
+  // device -> host on the comm lane; the host waits for it (and for everything queued before)
+  virtual void download(void* h, const void* d, int64_t bytes) = 0;
+  // comm-lane collectives on device buffers (send/recv between group_start and group_end are one group)
+  virtual void group_start() = 0;
+  virtual void group_end() = 0;
+  virtual void send(const void* d, int64_t bytes, int peer) = 0;
+  virtual void recv(void* d, int64_t bytes, int peer) = 0;
+  virtual void bcast(void* d, int64_t bytes, int root) = 0;
+  virtual void allreduce_max_u64(uint64_t* d, int64_t n) = 0;
+  // host waits for the comm lane; throws on asynchronous communicator errors
+  virtual void sync() = 0;
+  // a point of the comm lane, and a host wait for just that point (pipelines reuse staging buffers)
+  virtual int mark() = 0;
+  virtual void wait_mark(int mark) = 0;
+};
+
+class DeviceSearch {
+ public:
+  virtual ~DeviceSearch() = default;
+  // Whether batches of this length range travel as packed letters + narrow lengths + sparse offsets
+  // (else packed letters + dense offsets), and the result format the rank returns for that form.
+  virtual bool streams_packed(int64_t min_l2, int64_t max_l2) const = 0;
+  virtual ResultFormat result_format(int64_t min_l2, int64_t max_l2, bool packed_form) const = 0;
+  // A device-resident wire batch (offsets rebased to 0) -> results in `fmt` at d_out (comm lane order).
+  virtual void solve(const WireBatch& d_batch, void* d_out, ResultFormat fmt) = 0;
+  // Context-parallel share of every record (byte codes, dense offsets from 0; h_offsets: host copy) ->
+  // packed 64-bit keys; and the root's decode of the MAX-reduced keys into results (R12).
+  virtual void search_keys(const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets, int64_t n,
+                           int part, int parts, uint64_t* d_keys) = 0;
+  virtual void finalize_keys(const int64_t* d_offsets, int64_t n, const uint64_t* d_keys, Result* d_out) = 0;
+  virtual double last_kernel_ms() const = 0;
+  virtual R2Params last_r2() const = 0;
+};
+
+// What one device batch produced: on the root, every rank's results in its own format (host memory).
+struct DeviceBatchOut {
+  std::vector<ResultRun> runs;
+  std::vector<std::vector<char>> storage;  // backing memory of runs
+  double compute_ms = 0, kernel_ms = 0;    // this rank
+  int64_t scattered_bytes = 0;             // root: device bytes sent to the other ranks
+  std::vector<int64_t> rank_records;       // every rank's records (root)
+};
+
+// One batch over the device layer. Record slices (cp = false): the root packs each rank's slice into the
+// wire form that rank's engine streams, and a three-stage pipeline overlaps packing the next slice (host
+// threads), its upload (copy lane) and the send of the previous one (comm lane, in <= 64 MiB chunks);
+// every rank searches its slice in device memory and the narrow results are gathered to the root.
+// Context parallel (cp = true): the batch is broadcast, each rank searches its share of every record's
+// offsets, the packed keys are MAX-all-reduced, the root decodes them.
+// `rb` (bytes + offsets from 0) and `bounds` (p+1 record bounds) are read on the root only.
+DeviceBatchOut device_batch(DeviceComm& dc, DeviceSearch& ds, const RecordBatch* rb, int64_t n, int64_t total_chars,
+                            const std::vector<int64_t>& bounds, bool cp, const PhaseHooks& hooks);
+
+}  // namespace moc

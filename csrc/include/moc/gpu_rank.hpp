@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "moc/comm.hpp"
+#include "moc/device_comm.hpp"
 #include "moc/common.hpp"
 #include "moc/problem.hpp"
 #include "moc/wire.hpp"
@@ -25,12 +26,6 @@ struct GpuRankOptions {
   int64_t chunk_records = 0;    // 0: engine defaults
   int64_t chunk_bytes = 0;
   std::string log_level = "warn";
-};
-
-// Phase hooks of the caller's timer / fault injection (the rccl batch runs its own phases).
-struct PhaseHooks {
-  std::function<void(const char*)> begin;  // starts a phase (and fires the fault hook for it)
-  std::function<void()> end;
 };
 
 // What the last solve moved and ran (for --timing).
@@ -69,11 +64,10 @@ class GpuRank {
   virtual std::function<void()> detach_pins() = 0;
   // Creates the RCCL communicator (collective over ctx.world: every rank must call it).
   virtual void init_rccl() = 0;
-  // One batch over RCCL (transport=rccl): root uploads, slices scatter over xGMI (or, with `cp`, the
-  // batch is broadcast and packed keys are MAX-all-reduced), results gather to the root's `out`.
-  // `rb` is read on the root only; returns this rank's compute milliseconds.
-  virtual double rccl_batch(const RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds,
-                            bool cp, Result* out, const PhaseHooks& hooks) = 0;
+  // The rccl transport's device layer (moc/device_comm.hpp): RCCL over xGMI on the engine's stream, and the
+  // engine over device-resident wire batches (init_rccl first).
+  virtual DeviceComm& device_comm() = 0;
+  virtual DeviceSearch& device_search() = 0;
 };
 
 // Plugin entry points (extern "C", resolved with dlsym).

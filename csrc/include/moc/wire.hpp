@@ -122,6 +122,7 @@ struct WireBatch {
   int64_t len_base = 0;
   int64_t n = 0;
   int64_t min_l2 = -1, max_l2 = -1;  // length range (-1: unknown; required with sparse offsets)
+  bool device = false;               // every pointer is device memory of the engine's GPU
   int64_t first_letter() const { return offsets[0]; }
   int64_t end_letter() const { return offsets[off_shift ? sparse_count(n, off_shift) - 1 : n]; }
   int64_t letter_bytes() const {

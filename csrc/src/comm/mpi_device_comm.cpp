@@ -1,0 +1,102 @@
+// MpiDeviceComm / CpuDeviceSearch (moc/mpi_device_comm.hpp).
+#include "moc/mpi_device_comm.hpp"
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
+#include "moc/cpu_engine.hpp"
+
+namespace moc {
+
+namespace {
+constexpr int64_t kMpiChunk = int64_t{1} << 30;  // every MPI count < 2^31
+constexpr int kTag = 21;
+}  // namespace
+
+MpiDeviceComm::~MpiDeviceComm() {
+  if (!reqs_.empty()) MPI_Waitall(static_cast<int>(reqs_.size()), reqs_.data(), MPI_STATUSES_IGNORE);
+}
+
+void* MpiDeviceComm::dev_alloc(int64_t bytes) {
+  void* p = std::aligned_alloc(64, static_cast<size_t>((std::max<int64_t>(bytes, 1) + 63) & ~int64_t{63}));
+  if (!p) throw Error("MpiDeviceComm: out of memory");
+  return p;
+}
+void MpiDeviceComm::dev_free(void* p) { std::free(p); }
+
+int MpiDeviceComm::upload(void* d, const void* h, int64_t bytes) {
+  if (bytes > 0 && d != h) std::memcpy(d, h, static_cast<size_t>(bytes));
+  return 0;
+}
+void MpiDeviceComm::download(void* h, const void* d, int64_t bytes) {
+  if (bytes > 0 && d != h) std::memcpy(h, d, static_cast<size_t>(bytes));
+}
+
+void MpiDeviceComm::group_start() { ++depth_; }
+void MpiDeviceComm::group_end() {
+  if (--depth_ > 0 || reqs_.empty()) return;
+  mpi_check(MPI_Waitall(static_cast<int>(reqs_.size()), reqs_.data(), MPI_STATUSES_IGNORE), "MPI_Waitall");
+  reqs_.clear();
+}
+
+void MpiDeviceComm::send(const void* d, int64_t bytes, int peer) {
+  const char* p = static_cast<const char*>(d);
+  for (int64_t off = 0; off < bytes; off += kMpiChunk) {
+    MPI_Request r;
+    mpi_check(MPI_Isend(p + off, static_cast<int>(std::min(kMpiChunk, bytes - off)), MPI_BYTE, peer, kTag, ctx_.world, &r),
+              "MPI_Isend");
+    reqs_.push_back(r);
+  }
+  if (depth_ == 0) group_end();
+}
+void MpiDeviceComm::recv(void* d, int64_t bytes, int peer) {
+  char* p = static_cast<char*>(d);
+  for (int64_t off = 0; off < bytes; off += kMpiChunk) {
+    MPI_Request r;
+    mpi_check(MPI_Irecv(p + off, static_cast<int>(std::min(kMpiChunk, bytes - off)), MPI_BYTE, peer, kTag, ctx_.world, &r),
+              "MPI_Irecv");
+    reqs_.push_back(r);
+  }
+  if (depth_ == 0) group_end();
+}
+
+void MpiDeviceComm::bcast(void* d, int64_t bytes, int root) { bcast_bytes(d, bytes, root, ctx_.world); }
+void MpiDeviceComm::allreduce_max_u64(uint64_t* d, int64_t n) { moc::allreduce_max_u64(d, n, ctx_.world); }
+
+// ---- CPU search over decoded wire batches
+void CpuDeviceSearch::solve(const WireBatch& b, void* out, ResultFormat fmt) {
+  if (fmt != ResultFormat::R12) throw Error("CpuDeviceSearch returns R12 results");
+  RecordBatch rb;
+  rb.offsets.resize(static_cast<size_t>(b.n) + 1);
+  if (b.off_shift) {
+    expand_offsets(b.offsets, b.off_shift, b.lengths, b.len_bits, b.len_base, b.n, rb.offsets.data());
+  } else {
+    std::memcpy(rb.offsets.data(), b.offsets, 8 * (static_cast<size_t>(b.n) + 1));
+  }
+  const int64_t c0 = rb.offsets[0], letters = rb.offsets[b.n] - c0;
+  for (auto& o : rb.offsets) o -= c0;
+  rb.codes.resize(static_cast<size_t>(letters));
+  if (b.packed5)
+    unpack5(b.letters, c0, letters, rb.codes.data());
+  else
+    std::memcpy(rb.codes.data(), b.letters + c0, static_cast<size_t>(letters));
+  solve_batch_cpu(table_, seq1_.data(), static_cast<int64_t>(seq1_.size()), rb, static_cast<Result*>(out), sem_,
+                  threads_);
+}
+
+void CpuDeviceSearch::search_keys(const uint8_t* codes, const int64_t* offsets, const int64_t*, int64_t n, int part,
+                                  int parts, uint64_t* keys) {
+  RecordBatch rb;
+  rb.offsets.assign(offsets, offsets + n + 1);
+  const int64_t c0 = rb.offsets[0];
+  for (auto& o : rb.offsets) o -= c0;
+  rb.codes.assign(codes + c0, codes + c0 + rb.offsets[n]);
+  solve_keys_cpu(table_, seq1_.data(), static_cast<int64_t>(seq1_.size()), rb, part, parts, keys, sem_, threads_);
+}
+
+void CpuDeviceSearch::finalize_keys(const int64_t* offsets, int64_t n, const uint64_t* keys, Result* out) {
+  for (int64_t i = 0; i < n; ++i) out[i] = decode_key(keys[i], offsets[i + 1] - offsets[i]);
+}
+
+}  // namespace moc

@@ -1,0 +1,311 @@
+// device_batch (moc/device_comm.hpp): the rccl transport's batch — slices packed into wire formats and
+// pipelined to the ranks' devices, device-resident search, narrow results gathered; or the
+// context-parallel broadcast + MAX all-reduce of packed keys.
+#include <omp.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+
+#include "moc/device_comm.hpp"
+#include "moc/runtime/timer.hpp"
+
+namespace moc {
+
+namespace {
+
+// send/recv pieces: the pipeline's xGMI stage (MOC_SEND_CHUNK overrides it, e.g. for tests of the
+// multi-piece path on small batches)
+int64_t send_chunk() {
+  static const int64_t c = [] {
+    const char* v = std::getenv("MOC_SEND_CHUNK");
+    return v && std::atoll(v) > 0 ? static_cast<int64_t>(std::atoll(v)) : int64_t{64} << 20;
+  }();
+  return c;
+}
+inline int64_t al16(int64_t x) { return (x + 15) & ~int64_t{15}; }
+
+// Per-rank plan, decided by the root (every rank runs the same engine type on the same problem, so the
+// root's DeviceSearch answers for all of them) and broadcast through the device layer.
+struct RankPlan {
+  int64_t n = 0, first = 0, letters = 0, min_l2 = 0, max_l2 = 0;
+  int64_t narrow = 0;  // 1: packed letters + narrow lengths + sparse offsets; 0: + dense offsets
+  int64_t bits = 0, fmt = 0;
+  int64_t off_letters = 0, off_offsets = 0, off_lengths = 0, block = 0;  // block layout (bytes)
+};
+static_assert(sizeof(RankPlan) == 12 * sizeof(int64_t), "plan table entries are int64");
+
+void layout(RankPlan& pl) {
+  pl.off_letters = 0;
+  pl.off_offsets = al16(packed5_bytes(pl.letters));
+  const int64_t offs = pl.narrow ? sparse_count(pl.n, kSparseShift) : pl.n + 1;
+  pl.off_lengths = pl.off_offsets + al16(8 * offs);
+  pl.block = pl.off_lengths + (pl.narrow ? al16(narrow_lengths_bytes(pl.n, static_cast<int>(pl.bits))) : 0);
+  if (pl.n == 0) pl.block = 0;
+}
+
+// Root: rank slice [b, b + pl.n) of rb in the plan's wire form -> dst (host staging).
+void pack_block(const RecordBatch& rb, const RankPlan& pl, char* dst) {
+  const int64_t b = pl.first, c0 = rb.offsets[b];
+  pack5(rb.codes.data() + c0, pl.letters, reinterpret_cast<uint8_t*>(dst + pl.off_letters));
+  int64_t* offs = reinterpret_cast<int64_t*>(dst + pl.off_offsets);
+  if (pl.narrow) {
+    const int64_t ns = sparse_count(pl.n, kSparseShift);
+    for (int64_t j = 0; j < ns; ++j) offs[j] = rb.offsets[b + std::min(j << kSparseShift, pl.n)] - c0;
+    pack_lengths(rb.offsets.data() + b, pl.n, static_cast<int>(pl.bits), pl.bits == 8 ? 0 : pl.min_l2,
+                 reinterpret_cast<uint8_t*>(dst + pl.off_lengths));
+  } else {
+#pragma omp parallel for schedule(static) if (pl.n > 65536)
+    for (int64_t i = 0; i <= pl.n; ++i) offs[i] = rb.offsets[b + i] - c0;
+  }
+}
+
+WireBatch device_view(const RankPlan& pl, char* d_block) {
+  WireBatch w;
+  w.letters = reinterpret_cast<const uint8_t*>(d_block + pl.off_letters);
+  w.packed5 = true;
+  w.offsets = reinterpret_cast<const int64_t*>(d_block + pl.off_offsets);
+  w.off_shift = pl.narrow ? kSparseShift : 0;
+  w.lengths = pl.narrow ? reinterpret_cast<const uint8_t*>(d_block + pl.off_lengths) : nullptr;
+  w.len_bits = static_cast<int>(pl.narrow ? pl.bits : 8);
+  w.len_base = pl.bits == 8 ? 0 : pl.min_l2;
+  w.n = pl.n;
+  w.min_l2 = pl.min_l2;
+  w.max_l2 = pl.max_l2;
+  w.device = true;
+  return w;
+}
+
+// Device buffers of one batch, freed on scope exit (also when unwinding).
+struct DevBufs {
+  DeviceComm& dc;
+  std::vector<void*> dev, host;
+  explicit DevBufs(DeviceComm& c) : dc(c) {}
+  template <typename T>
+  T* d(int64_t bytes) {
+    void* p = dc.dev_alloc(std::max<int64_t>(bytes, 16));
+    dev.push_back(p);
+    return static_cast<T*>(p);
+  }
+  char* h(int64_t bytes) {
+    void* p = dc.host_alloc(std::max<int64_t>(bytes, 16));
+    host.push_back(p);
+    return static_cast<char*>(p);
+  }
+  ~DevBufs() {
+    for (void* p : dev) dc.dev_free(p);
+    for (void* p : host) dc.host_free(p);
+  }
+};
+
+// Chunked point-to-point transfer of one block (both sides derive the same pieces from its size).
+void send_block(DeviceComm& dc, const char* d, int64_t bytes, int peer) {
+  const int64_t chunk = send_chunk();
+  for (int64_t off = 0; off < bytes; off += chunk) {
+    dc.group_start();
+    dc.send(d + off, std::min(chunk, bytes - off), peer);
+    dc.group_end();
+  }
+}
+void recv_block(DeviceComm& dc, char* d, int64_t bytes, int peer) {
+  const int64_t chunk = send_chunk();
+  for (int64_t off = 0; off < bytes; off += chunk) {
+    dc.group_start();
+    dc.recv(d + off, std::min(chunk, bytes - off), peer);
+    dc.group_end();
+  }
+}
+
+DeviceBatchOut batch_cp(DeviceComm& dc, DeviceSearch& ds, const RecordBatch* rb, int64_t n, int64_t total_chars,
+                        const PhaseHooks& hooks) {
+  DeviceBatchOut out;
+  DevBufs bufs(dc);
+  const int rank = dc.rank(), p = dc.size();
+  hooks.begin("distribute");
+  // the root uploads the batch once; the device layer broadcasts it; every rank needs a host copy of the
+  // offsets for its tile planning
+  uint8_t* d_codes = bufs.d<uint8_t>(total_chars + 16);
+  int64_t* d_offs = bufs.d<int64_t>(8 * (n + 1));
+  if (rank == 0) {
+    dc.wait_upload(dc.upload(d_codes, rb->codes.data(), total_chars));
+    dc.wait_upload(dc.upload(d_offs, rb->offsets.data(), 8 * (n + 1)));
+  }
+  dc.bcast(d_codes, total_chars, 0);
+  dc.bcast(d_offs, 8 * (n + 1), 0);
+  std::vector<int64_t> h_offs(static_cast<size_t>(n) + 1);
+  dc.download(h_offs.data(), d_offs, 8 * (n + 1));
+  hooks.end();
+  hooks.begin("compute");
+  Stopwatch sw;
+  sw.start();
+  uint64_t* d_keys = bufs.d<uint64_t>(8 * n);
+  ds.search_keys(d_codes, d_offs, h_offs.data(), n, rank, p, d_keys);
+  dc.sync();
+  sw.stop();
+  out.compute_ms = sw.total_ms();
+  out.kernel_ms = ds.last_kernel_ms();
+  hooks.end();
+  hooks.begin("gather");
+  dc.allreduce_max_u64(d_keys, n);
+  if (rank == 0) {
+    Result* d_res = bufs.d<Result>(12 * n);
+    ds.finalize_keys(d_offs, n, d_keys, d_res);
+    out.storage.emplace_back(static_cast<size_t>(12 * n));
+    dc.download(out.storage.back().data(), d_res, 12 * n);
+    out.runs.push_back(ResultRun{out.storage.back().data(), ResultFormat::R12, R2Params{}, n});
+  }
+  dc.sync();
+  hooks.end();
+  return out;
+}
+
+}  // namespace
+
+DeviceBatchOut device_batch(DeviceComm& dc, DeviceSearch& ds, const RecordBatch* rb, int64_t n, int64_t total_chars,
+                            const std::vector<int64_t>& bounds, bool cp, const PhaseHooks& hooks) {
+  if (cp) return batch_cp(dc, ds, rb, n, total_chars, hooks);
+  DeviceBatchOut out;
+  DevBufs bufs(dc);
+  const int rank = dc.rank(), p = dc.size();
+
+  // ---- plan (root) -> every rank, through the device layer
+  hooks.begin("distribute");
+  std::vector<RankPlan> plan(static_cast<size_t>(p));
+  if (rank == 0) {
+    for (int r = 0; r < p; ++r) {
+      RankPlan& pl = plan[r];
+      pl.first = bounds[r];
+      pl.n = bounds[r + 1] - bounds[r];
+      pl.letters = rb->offsets[bounds[r + 1]] - rb->offsets[bounds[r]];
+      int64_t mn = INT64_MAX, mx = 0;
+#pragma omp parallel for reduction(min : mn) reduction(max : mx) schedule(static) if (pl.n > 65536)
+      for (int64_t i = bounds[r]; i < bounds[r + 1]; ++i) {
+        const int64_t L = rb->offsets[i + 1] - rb->offsets[i];
+        mn = std::min(mn, L);
+        mx = std::max(mx, L);
+      }
+      pl.min_l2 = pl.n ? mn : 0;
+      pl.max_l2 = mx;
+      pl.narrow = pl.n > 0 && mx <= 255 && ds.streams_packed(mn, mx) ? 1 : 0;
+      pl.bits = pl.narrow ? narrow_length_bits(mn, mx) : 0;
+      pl.fmt = pl.n ? static_cast<int64_t>(ds.result_format(mn, mx, pl.narrow != 0)) : 0;
+      layout(pl);
+    }
+  }
+  {
+    const int64_t bytes = static_cast<int64_t>(sizeof(RankPlan)) * p;
+    char* d_plan = bufs.d<char>(bytes);
+    if (rank == 0) dc.wait_upload(dc.upload(d_plan, plan.data(), bytes));
+    dc.bcast(d_plan, bytes, 0);
+    dc.download(plan.data(), d_plan, bytes);
+  }
+  const RankPlan& mine = plan[rank];
+  char* d_block = bufs.d<char>(mine.block + 16);
+
+  // ---- root: pack slice r+1 (host threads) | upload slice r (copy lane) | send slice r-1 (comm lane)
+  if (rank == 0) {
+    int64_t stage_bytes = 0;
+    for (const RankPlan& pl : plan) stage_bytes = std::max(stage_bytes, pl.block);
+    char* stage[2] = {bufs.h(stage_bytes + 16), bufs.h(stage_bytes + 16)};
+    char* d_stage[2] = {bufs.d<char>(stage_bytes + 16), bufs.d<char>(stage_bytes + 16)};
+    int done[2] = {-1, -1};  // comm-lane mark after the last use of stage s
+    // ranks in order 1..p-1, then the root's own slice (uploaded straight into its block)
+    std::vector<int> order;
+    for (int r = 1; r < p; ++r) order.push_back(r);
+    order.push_back(0);
+    for (size_t k = 0; k < order.size(); ++k) {
+      const int r = order[k];
+      const RankPlan& pl = plan[r];
+      if (pl.block == 0) continue;
+      const int s = static_cast<int>(k & 1);
+      if (done[s] >= 0) dc.wait_mark(done[s]);  // slice k-2 has left stage s: it may be rewritten
+      pack_block(*rb, pl, stage[s]);          // while slice k-1 uploads / sends
+      char* dst = r == 0 ? d_block : d_stage[s];
+      dc.wait_upload(dc.upload(dst, stage[s], pl.block));
+      if (r != 0) {
+        send_block(dc, dst, pl.block, r);
+        out.scattered_bytes += pl.block;
+      }
+      done[s] = dc.mark();
+    }
+  } else if (mine.block > 0) {
+    recv_block(dc, d_block, mine.block, 0);
+  }
+  dc.sync();
+  hooks.end();
+
+  // ---- search this rank's slice on its device
+  hooks.begin("compute");
+  Stopwatch sw;
+  sw.start();
+  const ResultFormat fmt = static_cast<ResultFormat>(mine.fmt);
+  const int fb = result_bytes(fmt);
+  char* d_out = bufs.d<char>(fb * mine.n + 16);
+  if (mine.n > 0) ds.solve(device_view(mine, d_block), d_out, fmt);
+  dc.sync();
+  sw.stop();
+  out.compute_ms = sw.total_ms();
+  out.kernel_ms = ds.last_kernel_ms();
+  const R2Params r2 = ds.last_r2();
+  hooks.end();
+
+  // ---- narrow results -> root (+ each rank's R2 parameters, 3 ints, through the device layer)
+  hooks.begin("gather");
+  std::vector<int64_t> rstart(static_cast<size_t>(p) + 1, 0);
+  for (int r = 0; r < p; ++r) rstart[r + 1] = rstart[r] + al16(result_bytes(static_cast<ResultFormat>(plan[r].fmt)) * plan[r].n);
+  std::vector<int64_t> r2v(static_cast<size_t>(3 * p), 0);
+  char* d_r2 = bufs.d<char>(24 * p);
+  {
+    const int64_t mine_r2[3] = {r2.smin, r2.kw, r2.j};
+    // every rank's parameters land at its slot of the root's table
+    char* d_mine_r2 = bufs.d<char>(24);
+    dc.wait_upload(dc.upload(d_mine_r2, mine_r2, 24));
+    dc.group_start();
+    if (rank == 0) {
+      for (int r = 1; r < p; ++r) dc.recv(d_r2 + 24 * r, 24, r);
+    } else {
+      dc.send(d_mine_r2, 24, 0);
+    }
+    dc.group_end();
+    if (rank == 0) {
+      r2v[0] = r2.smin;
+      r2v[1] = r2.kw;
+      r2v[2] = r2.j;
+    }
+  }
+  char* d_gather = rank == 0 ? bufs.d<char>(rstart[p] + 16) : nullptr;
+  dc.group_start();
+  if (rank == 0) {
+    for (int r = 1; r < p; ++r) {
+      const int64_t bytes = result_bytes(static_cast<ResultFormat>(plan[r].fmt)) * plan[r].n;
+      if (bytes > 0) dc.recv(d_gather + rstart[r], bytes, r);
+    }
+  } else if (fb * mine.n > 0) {
+    dc.send(d_out, fb * mine.n, 0);
+  }
+  dc.group_end();
+  if (rank == 0) {
+    out.storage.emplace_back(static_cast<size_t>(rstart[p] + 16));
+    char* h = out.storage.back().data();
+    if (p > 1) dc.download(r2v.data() + 3, d_r2 + 24, 24 * (p - 1));
+    if (fb * mine.n > 0) dc.download(h, d_out, fb * mine.n);
+    if (rstart[p] > rstart[1]) dc.download(h + rstart[1], d_gather + rstart[1], rstart[p] - rstart[1]);
+    out.rank_records.resize(static_cast<size_t>(p));
+    for (int r = 0; r < p; ++r) {
+      ResultRun run;
+      run.data = h + rstart[r];
+      run.fmt = static_cast<ResultFormat>(plan[r].fmt);
+      run.r2 = R2Params{static_cast<int32_t>(r2v[3 * r]), static_cast<int32_t>(r2v[3 * r + 1]),
+                        static_cast<int32_t>(r2v[3 * r + 2])};
+      run.n = plan[r].n;
+      out.runs.push_back(run);
+      out.rank_records[r] = plan[r].n;
+    }
+  }
+  dc.sync();
+  hooks.end();
+  return out;
+}
+
+}  // namespace moc

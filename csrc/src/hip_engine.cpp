@@ -415,12 +415,19 @@ bool HipEngine::direct_pointers(const WireBatch& b, void* out, int fb, dev::Shor
   const int64_t c0 = b.first_letter(), c1 = b.end_letter(), n = b.n;
   // byte range of the letters: [b0, b1)
   const int64_t b0 = b.packed5 ? (5 * c0) >> 3 : c0, b1 = b.packed5 ? ((5 * c1 + 7) >> 3) + 1 : c1;
-  // the kernels stage letters with 16-byte loads of the aligned granules covering [b0, b1): a granule
-  // never crosses a page, so the pages of [b0, b1) are all that must be mapped
-  if (c1 > c0 && !pinned_range(b.letters + b0, static_cast<size_t>(b1 - b0), &dc)) return false;
-  if (!pinned_range(b.offsets, sizeof(int64_t) * static_cast<size_t>(b.offset_entries()), &doff)) return false;
-  if (b.lengths && !pinned_range(b.lengths, static_cast<size_t>(b.length_bytes()), &dlen)) return false;
-  if (!pinned_range(out, static_cast<size_t>(fb) * static_cast<size_t>(n), &dout)) return false;
+  if (b.device) {  // device-resident (e.g. received over RCCL): the pointers are the kernel's already
+    dc = b.letters + b0;
+    doff = b.offsets;
+    dlen = b.lengths;
+    dout = out;
+  } else {
+    // the kernels stage letters with 16-byte loads of the aligned granules covering [b0, b1): a granule
+    // never crosses a page, so the pages of [b0, b1) are all that must be mapped
+    if (c1 > c0 && !pinned_range(b.letters + b0, static_cast<size_t>(b1 - b0), &dc)) return false;
+    if (!pinned_range(b.offsets, sizeof(int64_t) * static_cast<size_t>(b.offset_entries()), &doff)) return false;
+    if (b.lengths && !pinned_range(b.lengths, static_cast<size_t>(b.length_bytes()), &dlen)) return false;
+    if (!pinned_range(out, static_cast<size_t>(fb) * static_cast<size_t>(n), &dout)) return false;
+  }
   // device view of the codes base pointer (record i at base + offsets[i], or at bit 5*offsets[i])
   a.codes = c1 > c0 ? static_cast<const uint8_t*>(dc) - b0 : nullptr;
   a.dbg_codes_end = b1 + 15;  // the last granule may extend up to 15 bytes past b1
@@ -464,6 +471,7 @@ void HipEngine::solve_wire(const WireBatch& batch, void* out, ResultFormat fmt) 
   if (b.lengths && b.len_bits != 8 && b.len_bits != 4 && b.len_bits != 3) throw Error("lengths must be 8-, 4- or 3-bit");
   if (b.off_shift && (!b.lengths || b.min_l2 < 0 || b.max_l2 < 0 || b.off_shift > 6))
     throw Error("sparse offsets need narrow lengths, the length range and a stride of at most 64 records");
+  if (b.device && (b.min_l2 < 0 || b.max_l2 < 0)) throw Error("a device-resident batch needs its length range");
   if (!have_problem_) throw Error("HipEngine::solve before set_problem");
   MOC_HIP_CHECK(hipSetDevice(device_));
   TraceRange tr("moc.solve");
@@ -508,9 +516,9 @@ void HipEngine::solve_wire(const WireBatch& batch, void* out, ResultFormat fmt) 
   // offsets need whole tiles of 2^off_shift records (the swipe tiles are powers of two >= 64).
   const bool kernel_ok = (swipe || (!b.packed5 && dev::configure_short(L1_, ls.mn, ls.mx, a))) &&
                          (a.tile_records % (1 << b.off_shift)) == 0;
-  if (opt_.allow_direct && kernel_ok && direct_pointers(b, out, fb, a)) {
+  if ((opt_.allow_direct || b.device) && kernel_ok && direct_pointers(b, out, fb, a)) {
     const dev::ProblemView pv = problem_view(ls.mx);
-    if (opt_.dma_stream) {
+    if (opt_.dma_stream && !b.device) {
       run_dma_stream(pv, a, swipe, b, out, fb);
       wall.stop();
       stats_.total_ms = wall.total_ms();
@@ -527,12 +535,13 @@ void HipEngine::solve_wire(const WireBatch& batch, void* out, ResultFormat fmt) 
     stats_.kernel_ms = ms;
     stats_.direct = 1;
     stats_.chunks = 1;
-    stats_.h2d_bytes = b.letter_bytes() + (a.lengths3 || a.lengths4 || a.lengths8 ? b.length_bytes() : 8 * n);
-    stats_.d2h_bytes = static_cast<int64_t>(fb) * n;
+    stats_.h2d_bytes = b.device ? 0 : b.letter_bytes() + (a.lengths3 || a.lengths4 || a.lengths8 ? b.length_bytes() : 8 * n);
+    stats_.d2h_bytes = b.device ? 0 : static_cast<int64_t>(fb) * n;
     wall.stop();
     stats_.total_ms = wall.total_ms();
     return;
   }
+  if (b.device) throw Error("device-resident wire batches stream through the swipe kernel only");
   if (b.off_shift) {  // the staged pipeline plans from dense offsets: rebuild them from the lengths
     uvector<int64_t> dense(static_cast<size_t>(n) + 1);
     expand_offsets(b.offsets, b.off_shift, b.lengths, b.len_bits, b.len_base, n, dense.data());

@@ -21,11 +21,17 @@ _built = {"done": False}
 
 
 def ensure_built():
-    """Builds libmoc.so and ./final in-tree once per session if they are missing or stale."""
+    """Builds libmoc.so and ./final in-tree once per session if they are missing or stale. pytest-xdist
+    workers take turns (file lock): concurrent makes would relink ./final under tests that run it."""
+    import fcntl
+
     if _built["done"]:
         return
-    subprocess.run(["make", "-C", ROOT, f"-j{min(16, os.cpu_count() or 8)}", "build"], check=True,
-                   stdout=subprocess.DEVNULL)
+    os.makedirs(os.path.join(ROOT, "build"), exist_ok=True)
+    with open(os.path.join(ROOT, "build", ".make.lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        subprocess.run(["make", "-C", ROOT, f"-j{min(16, os.cpu_count() or 8)}", "build"], check=True,
+                       stdout=subprocess.DEVNULL)
     _built["done"] = True
 
 

@@ -357,3 +357,36 @@ def test_sliced_bounds_and_timing(np_, i):
     assert d["rank_pinned_bytes"] == [0] * np_ and d["rank_h2d_bytes"] == [0] * np_
     want = np.diff(partition(np.diff(prob.offsets), len(prob.seq1), np_, CPU_COST))
     assert d["rank_records"] == [int(x) for x in want]
+
+
+# ---- the rccl transport's batch driver, run over the MPI-emulated device layer (no GPU needed)
+
+@pytest.mark.parametrize("np_", [1, 2, 3, 8])
+@pytest.mark.parametrize("partition", ["cost", "offsets"])
+def test_rccl_driver_emulated(np_, partition):
+    # same device_batch code as --transport=rccl: per-rank wire plans (3/4/8-bit narrow forms and the dense
+    # form), chunked pipelined sends (tiny chunks force many pieces), narrow-result gather, CP MAX reduce
+    for i in (1, 3, 4, 6):
+        r = run_final(["--backend=cpu", "--transport=rccl-emul", f"--partition={partition}"], stdin_path=input_path(i),
+                      np_=np_, env={"MOC_SEND_CHUNK": "4096"})
+        assert r.returncode == 0, r.stderr.decode()
+        assert r.stdout.decode() == expected(i), (i, np_, partition)
+
+
+@pytest.mark.parametrize("np_", [2, 3])
+def test_rccl_driver_emulated_streaming_and_synthetic(np_, tmp_path):
+    # streaming batches through the device driver, and a larger mixed-length synthetic input
+    from mpi_openmp_cuda_amd import format_results, search_cpu
+    from mpi_openmp_cuda_amd.utils.synthetic import make_synthetic
+
+    for i in (1, 3):
+        r = run_final(["--backend=cpu", "--transport=rccl-emul", "--batch-records=4"], stdin_path=input_path(i), np_=np_)
+        assert r.returncode == 0, r.stderr.decode()
+        assert r.stdout.decode() == expected(i)
+    prob = make_synthetic("input6", 20_000, seed=5)
+    path = tmp_path / "in.txt"
+    path.write_text(prob.to_text())
+    r = run_final(["--backend=cpu", "--transport=rccl-emul", f"--input={path}", "--timing"], stdin_bytes=b"", np_=np_,
+                  env={"MOC_SEND_CHUNK": "65536"})
+    assert r.returncode == 0, r.stderr.decode()
+    assert r.stdout.decode() == format_results(search_cpu(prob))
