@@ -70,6 +70,8 @@ const char* kUsage =
     "                              rccl-emul: the rccl driver over MPI on CPU ranks)\n"
     "  --semantics=reference|spec  candidate set (spec adds the un-mutated final offset, bug B8)\n"
     "  --partition=cost|even|offsets   rank decomposition (offsets: split every record's offset range)\n"
+    "  --collectives=auto|mpi|rccl the ranks' collectives on the shm transport (auto: RCCL over xGMI when\n"
+    "                              every rank drives a GPU and there are several ranks, else MPI)\n"
     "  --batch-records=B           streaming mode: parse/search/print B records at a time (0 = all at once)\n"
     "  --batch-chars=C             streaming mode: also cap a batch at C letters\n"
     "  --skip-records=S            start at record #S (resume a partially printed run)\n"
@@ -89,7 +91,7 @@ const char* kUsage =
     "every flag can also be given as environment variable MOC_<FLAG> (e.g. MOC_BACKEND=cpu)\n";
 
 const std::vector<std::string> kKnown = {
-    "backend", "gpu-min-cells", "gpu-prewarm-bytes", "transport", "semantics", "partition", "batch-records", "batch-chars", "skip-records", "input",
+    "backend", "collectives", "gpu-min-cells", "gpu-prewarm-bytes", "transport", "semantics", "partition", "batch-records", "batch-chars", "skip-records", "input",
     "output", "timing", "strict-limits", "max-l1", "max-l2", "device", "device-map", "pin-window", "chunk-records",
     "chunk-bytes", "threads", "log-level", "inject-fault", "help"};
 
@@ -280,6 +282,9 @@ class Job {
   std::shared_ptr<uvector<char>> spent_text_;
   std::vector<Result> results_;  // root: results of the current batch (mpi transport)
   std::unique_ptr<MpiDeviceComm> emul_comm_;  // --transport=rccl-emul
+  bool coll_rccl_ = false;                     // shm transport: collectives over RCCL (--collectives)
+  void allgather_i64(const int64_t* mine, int count, int64_t* all);
+  void allreduce_keys(uint64_t* keys, int64_t n);
   std::future<void> prewarm_;     // HIP runtime start-up overlapped with the parse (large inputs)
 };
 
@@ -328,10 +333,57 @@ void Job::setup_engine(int64_t cells) {
     throw Error("--partition=offsets needs the same backend on every rank (use --backend=hip or --backend=cpu)");
   pin_window_ = flags_.get_bool("pin-window", true);
   if (transport_ == "rccl") eng_.hip->init_rccl();
+  // the shm transport moves no record data between ranks; its collectives (the slices' fill reports and
+  // result descriptors, the context-parallel key reduction) run over RCCL when every rank has a GPU. The
+  // connect runs on a helper thread while the ranks parse their slices.
+  const std::string coll = to_lower(flags_.get("collectives", "auto"));
+  if (coll != "auto" && coll != "mpi" && coll != "rccl") throw Error("--collectives must be auto|mpi|rccl");
+  if (coll == "rccl" && !all_gpu_) throw Error("--collectives=rccl needs a GPU on every rank");
+  coll_rccl_ = transport_ == "shm" && all_gpu_ && (coll == "rccl" || (coll == "auto" && ctx_.size > 1));
+  if (coll_rccl_) eng_.hip->init_rccl_begin();
   if (transport_ == "rccl-emul") emul_comm_ = std::make_unique<MpiDeviceComm>(ctx_);
   MOC_LOG_INFO("rank %d/%d host %s local %d/%d engine=%s device=%d transport=%s partition=%s", ctx_.rank, ctx_.size,
                ctx_.hostname.c_str(), ctx_.local_rank, ctx_.local_size, eng_.gpu ? "hip" : "cpu", device_,
                transport_.c_str(), partition_.c_str());
+}
+
+// MPI_Allgather of `count` int64 per rank, or the same over RCCL (--collectives).
+void Job::allgather_i64(const int64_t* mine, int count, int64_t* all) {
+  if (!coll_rccl_) {
+    MPI_Allgather(mine, count, MPI_INT64_T, all, count, MPI_INT64_T, ctx_.world);
+    return;
+  }
+  DeviceComm& dc = eng_.hip->device_comm();  // waits for the connect
+  const int64_t bytes = 8 * static_cast<int64_t>(count);
+  char* d = static_cast<char*>(dc.dev_alloc(bytes * (ctx_.size + 1)));
+  try {
+    dc.wait_upload(dc.upload(d, mine, bytes));
+    dc.allgather(d, d + bytes, bytes);
+    dc.download(all, d + bytes, bytes * ctx_.size);
+  } catch (...) {
+    dc.dev_free(d);
+    throw;
+  }
+  dc.dev_free(d);
+}
+
+// In-place MAX of packed keys over the ranks (context-parallel combine), MPI or RCCL.
+void Job::allreduce_keys(uint64_t* keys, int64_t n) {
+  if (!coll_rccl_) {
+    allreduce_max_u64(keys, n, ctx_.world);
+    return;
+  }
+  DeviceComm& dc = eng_.hip->device_comm();
+  uint64_t* d = static_cast<uint64_t*>(dc.dev_alloc(8 * n));
+  try {
+    dc.wait_upload(dc.upload(d, keys, 8 * n));
+    dc.allreduce_max_u64(d, n);
+    dc.download(keys, d, 8 * n);
+  } catch (...) {
+    dc.dev_free(d);
+    throw;
+  }
+  dc.dev_free(d);
 }
 
 void Job::print(const Result* r, int64_t n, int64_t first_index) {
@@ -440,7 +492,7 @@ void Job::batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, bool cp) {
     pt_.end();
     pt_.begin("gather");
     fault_.at("gather", ctx_.rank);
-    allreduce_max_u64(keys.data(), n, ctx_.world);
+    allreduce_keys(keys.data(), n);
     if (ctx_.rank == kRoot)
       for (int64_t i = 0; i < n; ++i) w_res[i] = decode_key(keys[i], w_offs[i + 1] - w_offs[i]);
     pt_.end();
@@ -580,7 +632,7 @@ void Job::run_sliced(BulkParser& parser, int64_t first_index) {
     int64_t mine[7] = {rep.min_len, rep.max_len, rep.bad_record, rep.long_record, rep.long_len, rep.cells,
                        slice.letters};
     std::vector<int64_t> all(static_cast<size_t>(7 * p));
-    MPI_Allgather(mine, 7, MPI_INT64_T, all.data(), 7, MPI_INT64_T, ctx_.world);
+    allgather_i64(mine, 7, all.data());
     FillReport job;
     for (int q = 0; q < p; ++q) {
       const int64_t* x = all.data() + 7 * q;
@@ -697,8 +749,8 @@ void Job::run_sliced(BulkParser& parser, int64_t first_index) {
   fault_.at("gather", r);
   int64_t info[8] = {n,           static_cast<int64_t>(fmt), gs.r2.smin, gs.r2.kw, gs.r2.j, pinned_bytes_, h2d_bytes_,
                      static_cast<int64_t>(pin_sw.total_ms() * 1000.0)};
-  std::vector<int64_t> infos(r == kRoot ? static_cast<size_t>(8 * p) : 0);
-  MPI_Gather(info, 8, MPI_INT64_T, infos.data(), 8, MPI_INT64_T, kRoot, ctx_.world);
+  std::vector<int64_t> infos(static_cast<size_t>(8 * p));
+  allgather_i64(info, 8, infos.data());
   res.fence();
   pt_.end();
   if (r == kRoot) {
@@ -851,11 +903,11 @@ void Job::report(const Header& h) {
                ", \"rank_h2d_bytes\": " + list(rank_h2d_) + ", \"rank_pin_us\": " + list(rank_pin_us_);
   std::fprintf(stderr,
                "{\"timing\": %s, \"ranks\": %d, \"nodes\": %d, \"engine\": \"%s\", \"transport\": \"%s\", "
-               "\"partition\": \"%s\", \"sliced\": %s, \"batches\": %lld, \"first_index\": %lld, \"records\": %lld, "
+               "\"partition\": \"%s\", \"collectives\": \"%s\", \"sliced\": %s, \"batches\": %lld, \"first_index\": %lld, \"records\": %lld, "
                "\"elements\": %lld, \"cells\": %lld, \"max_rank_compute_ms\": %.3f, \"max_rank_kernel_ms\": %.3f, "
                "\"wall_s\": %.6f, \"elements_per_s\": %.1f, \"cells_per_s\": %.1f%s, \"build\": \"%s\"}\n",
                pt_.json().c_str(), ctx_.size, ctx_.node_count, eng_.gpu ? "hip" : "cpu", transport_.c_str(),
-               partition_.c_str(), rank_records_.empty() ? "false" : "true", static_cast<long long>(batches_),
+               partition_.c_str(), coll_rccl_ || transport_ == "rccl" ? "rccl" : "mpi", rank_records_.empty() ? "false" : "true", static_cast<long long>(batches_),
                static_cast<long long>(h.first_index), static_cast<long long>(records_), static_cast<long long>(chars_),
                static_cast<long long>(cells_), mx[0], mx[1], wall_s, wall_s > 0 ? chars_ / wall_s : 0.0,
                wall_s > 0 ? cells_ / wall_s : 0.0, per_rank.c_str(), kBuildId);

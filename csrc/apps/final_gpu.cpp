@@ -4,6 +4,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <future>
 #include <memory>
 #include <vector>
 
@@ -26,8 +27,8 @@ namespace {
 // searches and the collectives are ordered without host waits), copy lane = a stream of its own.
 class RcclDeviceComm final : public DeviceComm {
  public:
-  RcclDeviceComm(const MpiContext& ctx, int device, hipStream_t comm_lane)
-      : ctx_(ctx), device_(device), s_(comm_lane), nccl_(ctx, device) {
+  RcclDeviceComm(const MpiContext& ctx, int device, hipStream_t comm_lane, const ncclUniqueId& id)
+      : ctx_(ctx), device_(device), s_(comm_lane), nccl_(ctx, device, id) {
     MOC_HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
   }
   ~RcclDeviceComm() override {
@@ -68,6 +69,9 @@ class RcclDeviceComm final : public DeviceComm {
     if (bytes > 0) nccl(ncclRecv(d, static_cast<size_t>(bytes), ncclUint8, peer, nccl_.comm(), s_), "ncclRecv");
   }
   void bcast(void* d, int64_t bytes, int root) override { nccl_.bcast(d, bytes, root, s_); }
+  void allgather(const void* d_send, void* d_recv, int64_t bytes_each) override {
+    nccl_.allgather(d_send, d_recv, bytes_each, s_);
+  }
   void allreduce_max_u64(uint64_t* d, int64_t n) override { nccl_.allreduce_max_u64(d, n, s_); }
   void sync() override {
     MOC_HIP_CHECK(hipStreamSynchronize(s_));
@@ -173,8 +177,18 @@ class GpuRankImpl final : public GpuRank {
     // of the GPU's root complex
     numa_ = bind_numa_to_device(device_);
   }
+  void init_rccl_begin() override {
+    if (dc_ || pending_.valid()) return;
+    const ncclUniqueId id = RcclComm::exchange_id(ctx_);  // MPI: this (the main) thread
+    pending_ = std::async(std::launch::async, [this, id] {
+      return std::make_unique<RcclDeviceComm>(ctx_, device_, engine_->compute_stream(), id);
+    });
+  }
   void init_rccl() override {
-    if (!dc_) dc_ = std::make_unique<RcclDeviceComm>(ctx_, device_, engine_->compute_stream());
+    if (!dc_) {
+      init_rccl_begin();
+      dc_ = pending_.get();
+    }
     if (!ds_) ds_ = std::make_unique<HipDeviceSearch>(*engine_);
   }
   DeviceComm& device_comm() override {
@@ -234,6 +248,7 @@ class GpuRankImpl final : public GpuRank {
   std::unique_ptr<HipEngine> engine_;
   std::unique_ptr<DeviceSearch> ds_;  // destroyed after dc_ (declared before it)
   std::unique_ptr<DeviceComm> dc_;
+  std::future<std::unique_ptr<RcclDeviceComm>> pending_;  // connect in flight (init_rccl_begin)
 };
 
 }  // namespace

@@ -50,6 +50,7 @@ class DeviceComm {
   virtual void send(const void* d, int64_t bytes, int peer) = 0;
   virtual void recv(void* d, int64_t bytes, int peer) = 0;
   virtual void bcast(void* d, int64_t bytes, int root) = 0;
+  virtual void allgather(const void* d_send, void* d_recv, int64_t bytes_each) = 0;
   virtual void allreduce_max_u64(uint64_t* d, int64_t n) = 0;
   // host waits for the comm lane; throws on asynchronous communicator errors
   virtual void sync() = 0;

@@ -62,7 +62,9 @@ class GpuRank {
   // Hands over this rank's page-lock registrations: the returned task unregisters them (e.g. on a
   // BackgroundReleaser, ahead of the unmap of the pages); the engine forgets them at once.
   virtual std::function<void()> detach_pins() = 0;
-  // Creates the RCCL communicator (collective over ctx.world: every rank must call it).
+  // Creates the RCCL communicator (collective over ctx.world: every rank must call it). _begin exchanges
+  // the unique id over MPI and connects on a helper thread; init_rccl waits for (or does) the connect.
+  virtual void init_rccl_begin() = 0;
   virtual void init_rccl() = 0;
   // The rccl transport's device layer (moc/device_comm.hpp): RCCL over xGMI on the engine's stream, and the
   // engine over device-resident wire batches (init_rccl first).

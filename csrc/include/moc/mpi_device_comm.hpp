@@ -34,6 +34,7 @@ class MpiDeviceComm final : public DeviceComm {
   void send(const void* d, int64_t bytes, int peer) override;
   void recv(void* d, int64_t bytes, int peer) override;
   void bcast(void* d, int64_t bytes, int root) override;
+  void allgather(const void* d_send, void* d_recv, int64_t bytes_each) override;
   void allreduce_max_u64(uint64_t* d, int64_t n) override;
   void sync() override {}
   int mark() override { return 0; }

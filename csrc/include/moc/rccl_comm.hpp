@@ -15,7 +15,12 @@ namespace moc {
 
 class RcclComm {
  public:
-  RcclComm(const MpiContext& ctx, int device);
+  // The unique id travels over MPI (the bootstrap): collective, on the thread that calls MPI.
+  static ncclUniqueId exchange_id(const MpiContext& ctx);
+  // ncclCommInitRank on `device` (collective over the ranks, any thread: e.g. a helper overlapping the
+  // connect with the parse).
+  RcclComm(const MpiContext& ctx, int device, const ncclUniqueId& id);
+  RcclComm(const MpiContext& ctx, int device) : RcclComm(ctx, device, exchange_id(ctx)) {}
   ~RcclComm();
   RcclComm(const RcclComm&) = delete;
   RcclComm& operator=(const RcclComm&) = delete;
@@ -28,6 +33,7 @@ class RcclComm {
   // Inverse: every rank != root sends its slice to root, which receives it at displs[r].
   void gatherv(const void* d_send, int64_t count, void* d_recv, const std::vector<int64_t>& counts,
                const std::vector<int64_t>& displs, int root, hipStream_t s);
+  void allgather(const void* d_send, void* d_recv, int64_t bytes_each, hipStream_t s);
   // In-place element-wise MAX of n uint64 device values over all ranks (packed candidate keys).
   void allreduce_max_u64(void* dbuf, int64_t n, hipStream_t s);
   void check_async() const;  // ncclCommGetAsyncError -> throw

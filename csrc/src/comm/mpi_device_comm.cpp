@@ -62,6 +62,12 @@ void MpiDeviceComm::recv(void* d, int64_t bytes, int peer) {
 }
 
 void MpiDeviceComm::bcast(void* d, int64_t bytes, int root) { bcast_bytes(d, bytes, root, ctx_.world); }
+void MpiDeviceComm::allgather(const void* d_send, void* d_recv, int64_t bytes_each) {
+  if (bytes_each >= kMpiChunk) throw Error("MpiDeviceComm::allgather: pieces must stay below 1 GiB");
+  mpi_check(MPI_Allgather(d_send, static_cast<int>(bytes_each), MPI_BYTE, d_recv, static_cast<int>(bytes_each), MPI_BYTE,
+                          ctx_.world),
+            "MPI_Allgather");
+}
 void MpiDeviceComm::allreduce_max_u64(uint64_t* d, int64_t n) { moc::allreduce_max_u64(d, n, ctx_.world); }
 
 // ---- CPU search over decoded wire batches

@@ -20,11 +20,15 @@ void nccl_check(ncclResult_t r, const char* what) {
 #define MOC_NCCL_CHECK(call) nccl_check((call), #call)
 }  // namespace
 
-RcclComm::RcclComm(const MpiContext& ctx, int device) : ctx_(ctx) {
-  MOC_HIP_CHECK(hipSetDevice(device));
+ncclUniqueId RcclComm::exchange_id(const MpiContext& ctx) {
   ncclUniqueId id;
   if (ctx.rank == 0) MOC_NCCL_CHECK(ncclGetUniqueId(&id));
   MOC_MPI_CHECK(MPI_Bcast(&id, sizeof id, MPI_BYTE, 0, ctx.world));
+  return id;
+}
+
+RcclComm::RcclComm(const MpiContext& ctx, int device, const ncclUniqueId& id) : ctx_(ctx) {
+  MOC_HIP_CHECK(hipSetDevice(device));
   // RCCL prints a version banner on stdout during init; stdout carries results only (main.c:204).
   std::fflush(stdout);
   const int saved = dup(1);
@@ -53,6 +57,11 @@ void RcclComm::check_async() const {
 void RcclComm::allreduce_max_u64(void* dbuf, int64_t n, hipStream_t s) {
   if (n <= 0) return;
   MOC_NCCL_CHECK(ncclAllReduce(dbuf, dbuf, static_cast<size_t>(n), ncclUint64, ncclMax, comm_, s));
+}
+
+void RcclComm::allgather(const void* d_send, void* d_recv, int64_t bytes_each, hipStream_t s) {
+  if (bytes_each <= 0) return;
+  MOC_NCCL_CHECK(ncclAllGather(d_send, d_recv, static_cast<size_t>(bytes_each), ncclUint8, comm_, s));
 }
 
 void RcclComm::bcast(void* dbuf, int64_t bytes, int root, hipStream_t s) {

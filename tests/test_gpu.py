@@ -313,7 +313,8 @@ def test_context_parallel_device_finalize(engine):
 
 @pytest.mark.parametrize("args", [["--partition=offsets", "--transport=shm"], ["--partition=offsets", "--transport=rccl"],
                                   ["--partition=offsets", "--transport=mpi"], ["--batch-records=3"],
-                                  ["--batch-records=2", "--transport=rccl"], ["--pin-window=0"]])
+                                  ["--batch-records=2", "--transport=rccl"], ["--pin-window=0"], ["--collectives=rccl"],
+                                  ["--partition=offsets", "--transport=shm", "--collectives=rccl"]])
 def test_final_cli_hip_modes(args):
     for i in (1, 3, 4, 6):
         r = run_final(["--backend=hip"] + args, stdin_path=input_path(i), np_=1)
@@ -535,3 +536,15 @@ def test_final_binary_built_from_these_sources():
     r = run_final(["--help"], np_=1)
     assert r.returncode == 0
     assert f"src={_source_hash()}" in r.stdout.decode()
+
+
+@pytest.mark.parametrize("shape,n", [("input6", 100_000), ("input1", 3000), ("input3", 40)])
+def test_final_cli_rccl_device_batches(tmp_path, shape, n):
+    # the rccl transport's device driver on one rank: the packed narrow form streams through the swipe
+    # kernel from device memory (R2 results), the dense form is unpacked on the device (tile/short kernels)
+    prob = make_synthetic(shape, n, seed=n)
+    path = tmp_path / "in.txt"
+    path.write_text(prob.to_text())
+    r = run_final(["--backend=hip", "--transport=rccl", f"--input={path}"], stdin_bytes=b"", np_=1)
+    assert r.returncode == 0, r.stderr.decode()
+    assert r.stdout.decode() == format_results(search_cpu(prob))
