@@ -28,6 +28,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <future>
 #include <memory>
 #include <sstream>
@@ -339,7 +340,16 @@ void Job::setup_engine(int64_t cells) {
   const std::string coll = to_lower(flags_.get("collectives", "auto"));
   if (coll != "auto" && coll != "mpi" && coll != "rccl") throw Error("--collectives must be auto|mpi|rccl");
   if (coll == "rccl" && !all_gpu_) throw Error("--collectives=rccl needs a GPU on every rank");
-  coll_rccl_ = transport_ == "shm" && all_gpu_ && (coll == "rccl" || (coll == "auto" && ctx_.size > 1));
+  bool shared_gpu = false;  // RCCL needs one rank per GPU (ranks sharing a GPU keep MPI under auto)
+  if (all_gpu_ && coll != "mpi") {
+    const int64_t mine = static_cast<int64_t>(std::hash<std::string>{}(ctx_.hostname) & 0xffffffffffffull) * 4096 + device_;
+    std::vector<int64_t> all(static_cast<size_t>(ctx_.size));
+    MPI_Allgather(&mine, 1, MPI_INT64_T, all.data(), 1, MPI_INT64_T, ctx_.world);
+    std::sort(all.begin(), all.end());
+    shared_gpu = std::adjacent_find(all.begin(), all.end()) != all.end();
+  }
+  if (coll == "rccl" && shared_gpu) throw Error("--collectives=rccl needs one rank per GPU");
+  coll_rccl_ = transport_ == "shm" && all_gpu_ && !shared_gpu && (coll == "rccl" || (coll == "auto" && ctx_.size > 1));
   if (coll_rccl_) eng_.hip->init_rccl_begin();
   if (transport_ == "rccl-emul") emul_comm_ = std::make_unique<MpiDeviceComm>(ctx_);
   MOC_LOG_INFO("rank %d/%d host %s local %d/%d engine=%s device=%d transport=%s partition=%s", ctx_.rank, ctx_.size,
