@@ -65,6 +65,8 @@ int moc_bind_numa(int device);
 int moc_device_numa_node(int device);
 /* Runs the DPP/shuffle self-test kernel; fills 192 ints (layout: align_kernels.hip dpp_probe_kernel). */
 int moc_dpp_probe(int32_t* out192);
+/* i8 MFMA layout self-test: c = a * b for row-major 32x32 int8 a, b (tile_mfma_kernels.hip). */
+int moc_mfma_i8_probe(const int8_t* a32x32, const int8_t* b32x32, int32_t* c32x32);
 /* Transfer calibration: GB/s for kind 0 H2D, 1 D2H, 2 both, 3 zero-copy read, 4 zero-copy write, 5 D2D. */
 double moc_transfer_probe(int kind, size_t bytes, int iters);
 /* out6: type, hostPointer, devicePointer, hipHostGetDevicePointer, hipMemGetAddressRange base, size */

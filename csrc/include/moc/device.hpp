@@ -56,6 +56,7 @@ struct ProblemView {
   const uint16_t* prof16 = nullptr;
   int32_t prof16_bytes = 0;
   int32_t max_abs_t = 0;  // max |T| over the table (int16-exactness checks of the packed kernels)
+  int32_t mfma_sweep = 0; // 1: long records sweep on the matrix cores (tile_mfma_kernels.hip, MOC_MFMA=1)
 };
 
 // Entries after the tile16 profile's last row: reads of wave-tile lanes past the valid offsets reach
@@ -160,7 +161,12 @@ void launch_tile_keys(const ProblemView& pv, const BatchView& bv, const Plan& pl
 void launch_finalize_keys(const BatchView& bv, const Plan& plan, void* out, int fmt, hipStream_t stream);
 // tile16 variant of launch_tile_keys (pv.prof16 must be set): packed-int16 sweep over the LDS profile,
 // then one wave per record recovers k on the winning diagonal and writes final keys.
-void launch_tile16_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream);
+// mfma_sweep: the matrix-core sweep (tile_mfma_kernels.hip, plan.u <= 4) in place of the packed-int16 one.
+void launch_tile16_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream,
+                        bool mfma_sweep = false);
+void launch_tile_mfma_sweep(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream);
+// i8 MFMA operand/accumulator layout self-test: C = A * B (row-major 32x32 int8 -> int32), one wave.
+void launch_mfma_i8_probe(const int8_t* d_a, const int8_t* d_b, int* d_c, hipStream_t stream);
 // Waves per CU the tile16 kernel keeps resident (16-wave workgroups, as many as the LDS allows).
 int tile16_waves_per_cu(int lds_bytes);
 
@@ -170,7 +176,9 @@ void preload_align_kernels();
 void preload_short_kernels();
 void preload_swipe_kernels();
 void preload_tile16_kernels();
+void preload_mfma_kernels();
 inline void preload_kernels() {
+  preload_mfma_kernels();
   preload_align_kernels();
   preload_short_kernels();
   preload_swipe_kernels();

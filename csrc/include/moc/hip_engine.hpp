@@ -167,6 +167,7 @@ class HipEngine {
   int32_t prof16_bytes_ = 0;
   int32_t prof16_overhang_ = 0;  // zero profile entries past the last row (bounds the tile span)
   bool tile16_ = true;            // MOC_TILE16 (A/B switch of the long-record kernel)
+  bool mfma_ = false;             // MOC_MFMA: tile16 plans swept on the matrix cores (tile_mfma_kernels.hip)
   int64_t L1_ = 0;
   Semantics sem_ = Semantics::Reference;
   bool have_problem_ = false;

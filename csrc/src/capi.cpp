@@ -185,6 +185,20 @@ int moc_dpp_probe(int32_t* out192) {
   });
 }
 
+int moc_mfma_i8_probe(const int8_t* a32x32, const int8_t* b32x32, int32_t* c32x32) {
+  return guard([&] {
+    char* d = nullptr;
+    MOC_HIP_CHECK(hipMalloc(&d, 2 * 1024 + 4 * 1024));
+    MOC_HIP_CHECK(hipMemcpy(d, a32x32, 1024, hipMemcpyHostToDevice));
+    MOC_HIP_CHECK(hipMemcpy(d + 1024, b32x32, 1024, hipMemcpyHostToDevice));
+    moc::dev::launch_mfma_i8_probe(reinterpret_cast<const int8_t*>(d), reinterpret_cast<const int8_t*>(d + 1024),
+                                   reinterpret_cast<int*>(d + 2048), nullptr);
+    MOC_HIP_CHECK(hipGetLastError());
+    MOC_HIP_CHECK(hipMemcpy(c32x32, d + 2048, 4 * 1024, hipMemcpyDeviceToHost));
+    MOC_HIP_CHECK(hipFree(d));
+  });
+}
+
 double moc_transfer_probe(int kind, size_t bytes, int iters) {
   double gbs = -1;
   guard([&] { gbs = moc::dev::transfer_probe(kind, bytes, iters); });

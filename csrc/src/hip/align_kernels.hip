@@ -192,7 +192,7 @@ void launch_finalize(const BatchView& bv, const Plan& plan, void* out, int fmt, 
 
 void launch_tile_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream) {
   if (pv.prof16) {  // packed-int16 profile variant (tile16_kernels.hip) when the problem fits it
-    launch_tile16_keys(pv, bv, plan, stream);
+    launch_tile16_keys(pv, bv, plan, stream, pv.mfma_sweep != 0);
     return;
   }
   if (plan.n_long > 0) MOC_HIP_CHECK(hipMemsetAsync(plan.keys, 0, sizeof(unsigned long long) * plan.n_long, stream));

@@ -363,17 +363,22 @@ void preload_tile16_kernels() {
   (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&resolve16_kernel));
 }
 
-void launch_tile16_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream) {
+void launch_tile16_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream,
+                        bool mfma_sweep) {
   if (!pv.prof16 || pv.prof16_bytes <= 0 || tile16_lds_bytes(pv.prof16_bytes, pv.L1) > kProf16MaxLds ||
       (pv.prof16_bytes & 15))
     throw Error("launch_tile16_keys: no usable profile");
   if (plan.n_long > 0) MOC_HIP_CHECK(hipMemsetAsync(plan.keys, 0, sizeof(unsigned long long) * plan.n_long, stream));
   if (plan.n_waves <= 0) return;
-  switch (plan.u) {
-    case 1: launch16_t<1>(pv, bv, plan, stream); break;
-    case 2: launch16_t<2>(pv, bv, plan, stream); break;
-    case 8: launch16_t<8>(pv, bv, plan, stream); break;
-    default: launch16_t<4>(pv, bv, plan, stream); break;
+  if (mfma_sweep) {
+    launch_tile_mfma_sweep(pv, bv, plan, stream);
+  } else {
+    switch (plan.u) {
+      case 1: launch16_t<1>(pv, bv, plan, stream); break;
+      case 2: launch16_t<2>(pv, bv, plan, stream); break;
+      case 8: launch16_t<8>(pv, bv, plan, stream); break;
+      default: launch16_t<4>(pv, bv, plan, stream); break;
+    }
   }
   const int64_t rb = (plan.n_long + 3) / 4;
   hipLaunchKernelGGL(resolve16_kernel, dim3(static_cast<unsigned>(rb)), dim3(256), 0, stream, pv, bv, plan.long_recs,

@@ -80,6 +80,7 @@ HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
     if (v == 1 || v == 2 || v == 4 || v == 8) tile_u_ = v;
   }
   if (const char* t16 = std::getenv("MOC_TILE16")) tile16_ = std::atoi(t16) != 0;
+  if (const char* m = std::getenv("MOC_MFMA")) mfma_ = std::atoi(m) != 0;
   if (const char* d = std::getenv("MOC_DMA_STREAM")) opt_.dma_stream = std::atoi(d);
   if (const char* d = std::getenv("MOC_DMA_CHUNK_BYTES")) opt_.dma_chunk_bytes = std::max<int64_t>(std::atoll(d), 1);
   if (const char* w = std::getenv("MOC_TILE_WAVES_PER_CU")) {
@@ -234,6 +235,7 @@ dev::ProblemView HipEngine::problem_view(int64_t max_l2) const {
   pv.prof16 = d_prof16_;
   pv.prof16_bytes = prof16_bytes_;
   pv.max_abs_t = table_.max_abs();
+  pv.mfma_sweep = mfma_ && d_prof16_ ? 1 : 0;
   return pv;
 }
 
@@ -343,6 +345,7 @@ std::vector<dev::WaveStart> HipEngine::plan_waves(const int64_t* offsets, const 
   int u = tile_u_ > 0 ? tile_u_ : (sum_l2 < 96 * n_long ? 4 : 2);
   if (tile_u_ <= 0 && u == 4 && d_prof16_ && 128 * 8 <= prof16_overhang_) u = 8;  // tile16: wider tiles for short records
   if (u > 4 && !(d_prof16_ && 128 * u <= prof16_overhang_)) u = 4;                 // the overhang bounds the span
+  if (u > 2 && mfma_) u = 2;  // the matrix-core sweep's register budget (U = 4 spills)
   u_out = u;
   std::vector<int64_t> pre(static_cast<size_t>(n_long) + 1, 0), tcost(static_cast<size_t>(n_long));
   std::vector<int32_t> ntiles(static_cast<size_t>(n_long));

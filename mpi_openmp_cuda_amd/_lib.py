@@ -67,6 +67,7 @@ def _decl(lib):
         "moc_bind_numa": (c_int, [c_int]),
         "moc_device_numa_node": (c_int, [c_int]),
         "moc_dpp_probe": (c_int, [c_void_p]),
+        "moc_mfma_i8_probe": (c_int, [c_void_p, c_void_p, c_void_p]),
         "moc_transfer_probe": (c_double, [c_int, c_size_t, c_int]),
         "moc_device_info_json": (c_int, [c_int, c_char_p, c_int64]),
         "moc_engine_create": (c_void_p, [c_int, c_int64, c_int64, c_int]),

@@ -44,6 +44,38 @@ def test_dpp_primitives():
     assert (out[128:] == 60).all()
 
 
+def test_mfma_i8_layout():
+    # the matrix-core sweep relies on the i8 32x32x32 operand packing (element j of lane half h <-> k = 16h + j,
+    # the same for A and B) and the C layout row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5): checked with
+    # asymmetric integer data against a host product
+    from mpi_openmp_cuda_amd import _lib
+
+    rng = np.random.default_rng(11)
+    a = rng.integers(-128, 128, size=(32, 32)).astype(np.int8)
+    b = rng.integers(-128, 128, size=(32, 32)).astype(np.int8)
+    c = np.zeros((32, 32), np.int32)
+    _lib.check(_lib.lib().moc_mfma_i8_probe(_lib.ptr(a), _lib.ptr(b), _lib.ptr(c)))
+    assert np.array_equal(c, a.astype(np.int32) @ b.astype(np.int32))
+
+
+@pytest.mark.parametrize("shape,n,L1", [("input3", 24, None), ("input4", 60, None), ("input3", 6, 3000),
+                                        ("input1", 300, 700)])
+def test_mfma_sweep_matches_cpu(monkeypatch, shape, n, L1):
+    # MOC_MFMA=1: the long-record sweep on the matrix cores (tile_mfma_kernels.hip) == the CPU engine,
+    # both semantics, records longer and shorter than Seq1, ties resolved to the reference's order
+    monkeypatch.setenv("MOC_MFMA", "1")
+    eng = HipSearchEngine(device=0)
+    prob = make_synthetic(shape, n, seed=n + 3)
+    if L1:
+        rng = np.random.default_rng(L1)
+        prob = Problem(prob.weights, rng.integers(1, 27, size=L1, dtype=np.uint8), prob.codes, prob.offsets)
+    for sem in (Semantics.REFERENCE, Semantics.SPEC):
+        eng.set_problem(prob.weights, prob.seq1, sem)
+        got = as_triples(eng.solve(prob.codes, prob.offsets))
+        assert np.array_equal(got, as_triples(search_cpu(prob, sem))), sem
+    assert "tile16" in eng.stats()["kernels"], eng.stats()
+
+
 def test_device_is_gfx950():
     info = device_info(0)
     assert info["arch"].startswith("gfx950"), info

@@ -3,8 +3,17 @@ shape, timed with HIP events around HipSearchEngine.solve_device on HBM-resident
 
 cells = sum over records of (L1 - L2 + 1) * L2 — the O(L1*L2) candidate cells; the
 reference kernel does O(L1*L2^2) work for the same answers.
+
+Every shape is repeated until at least --min-ms (default 60) of kernel time is measured, so launch skew
+and tail effects stay small. --variants tile16,mfma runs the long-record sweep both ways (MOC_MFMA: the
+matrix-core sweep, tile_mfma_kernels.hip) for an A/B on the same data.
+
+  python tools/kernel_bench.py [--variants tile16,mfma] [--min-ms 60] [shape ...]
 """
+import argparse
 import json
+import math
+import os
 import sys
 import time
 
@@ -13,16 +22,26 @@ import numpy as np
 sys.path.insert(0, ".")
 import torch  # noqa: E402
 
-from mpi_openmp_cuda_amd import HipSearchEngine, make_synthetic, search_cpu  # noqa: E402
+from mpi_openmp_cuda_amd import HipSearchEngine, Problem, make_synthetic, search_cpu  # noqa: E402
 from mpi_openmp_cuda_amd.ops.align import as_triples  # noqa: E402
 
-CASES = [("input6", 1 << 24), ("input1", 1 << 21), ("input4", 1 << 17), ("input3", 1 << 13), ("limits", 1 << 12)]
-if len(sys.argv) > 1:
-    CASES = [c for c in CASES if c[0] in sys.argv[1:]]
+# shape -> (records, Seq1 override length or None)
+CASES = {"input6": (1 << 24, None), "input1": (1 << 21, None), "input4": (1 << 17, None),
+         "input3": (1 << 15, None), "limits": (1 << 12, None)}
 
 
-def run(shape, n, iters=5):
+def make(shape, n):
     prob = make_synthetic(shape, n, seed=7)
+    L1 = CASES[shape][1]
+    if L1:
+        rng = np.random.default_rng(L1)
+        prob = Problem(prob.weights, rng.integers(1, 27, size=L1, dtype=np.uint8), prob.codes, prob.offsets)
+    return prob
+
+
+def run(shape, n, variant, min_ms):
+    os.environ["MOC_MFMA"] = "1" if variant == "mfma" else "0"
+    prob = make(shape, n)
     eng = HipSearchEngine(device=0)
     eng.set_problem(prob.weights, prob.seq1)
     dev = torch.device("cuda:0")
@@ -30,27 +49,39 @@ def run(shape, n, iters=5):
     offs = torch.from_numpy(prob.offsets).to(dev)
     out = torch.empty((prob.n, 3), dtype=torch.int32, device=dev)
     s = torch.cuda.current_stream()
-    eng.solve_device(codes, offs, prob.offsets, out, s)  # warm-up (and host planning cache warm)
-    torch.cuda.synchronize()
-    t_host = time.perf_counter()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    eng.solve_device(codes, offs, prob.offsets, out, s)  # warm-up (and host planning cache warm)
+    e0.record(s)
+    eng.solve_device(codes, offs, prob.offsets, out, s)
+    e1.record(s)
+    torch.cuda.synchronize()
+    iters = max(5, math.ceil(min_ms / max(e0.elapsed_time(e1), 1e-3)))
+    t_host = time.perf_counter()
     e0.record(s)
     for _ in range(iters):
         eng.solve_device(codes, offs, prob.offsets, out, s)
     e1.record(s)
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t_host) / iters
-    ms = e0.elapsed_time(e1) / iters
+    total = e0.elapsed_time(e1)
+    ms = total / iters
     nv = min(prob.n, 4000)
     ref = as_triples(search_cpu(prob.slice(0, nv)))
     ok = bool(np.array_equal(out[:nv].cpu().numpy(), ref))
     cells = prob.cells()
-    return {"shape": shape, "records": prob.n, "L1": prob.L1, "letters": prob.total_chars, "cells": cells,
-            "gpu_ms": round(ms, 4), "host_wall_ms": round(wall * 1e3, 4), "cells_per_s": cells / (ms / 1e3),
-            "records_per_s": prob.n / (ms / 1e3), "verified": ok}
+    return {"shape": shape, "variant": variant, "records": prob.n, "L1": prob.L1, "letters": prob.total_chars,
+            "cells": cells, "iters": iters, "kernel_ms_total": round(total, 2), "gpu_ms": round(ms, 4),
+            "host_wall_ms": round(wall * 1e3, 4), "cells_per_s": cells / (ms / 1e3),
+            "records_per_s": prob.n / (ms / 1e3), "kernels": eng.stats()["kernels"], "verified": ok}
 
 
 if __name__ == "__main__":
-    res = [run(s, n) for s, n in CASES]
-    for r in res:
-        print(json.dumps(r))
+    ap = argparse.ArgumentParser()
+    ap.add_argument("shapes", nargs="*")
+    ap.add_argument("--variants", default="tile16")
+    ap.add_argument("--min-ms", type=float, default=60.0)
+    args = ap.parse_args()
+    shapes = args.shapes or list(CASES)
+    for shape in shapes:
+        for variant in args.variants.split(","):
+            print(json.dumps(run(shape, CASES[shape][0], variant, args.min_ms)), flush=True)
