@@ -286,6 +286,13 @@ class Job {
   bool coll_rccl_ = false;                     // shm transport: collectives over RCCL (--collectives)
   void allgather_i64(const int64_t* mine, int count, int64_t* all);
   void allreduce_keys(uint64_t* keys, int64_t n);
+  // root: MAX-combined pass-1 keys -> results (k resolved on the winning diagonals)
+  void resolve_keys(const uint64_t* keys, const uint8_t* codes, const int64_t* offsets, int64_t n, Result* out) {
+    const int64_t L1 = static_cast<int64_t>(eng_.seq1.size());
+#pragma omp parallel for schedule(dynamic, 64) if (n > 4096)
+    for (int64_t i = 0; i < n; ++i)
+      out[i] = resolve_key(eng_.table, eng_.seq1.data(), L1, codes + offsets[i], offsets[i + 1] - offsets[i], keys[i]);
+  }
   std::future<void> prewarm_;     // HIP runtime start-up overlapped with the parse (large inputs)
 };
 
@@ -504,7 +511,7 @@ void Job::batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, bool cp) {
     fault_.at("gather", ctx_.rank);
     allreduce_keys(keys.data(), n);
     if (ctx_.rank == kRoot)
-      for (int64_t i = 0; i < n; ++i) w_res[i] = decode_key(keys[i], w_offs[i + 1] - w_offs[i]);
+      resolve_keys(keys.data(), w_codes, w_offs, n, w_res);
     pt_.end();
   } else {
     const int64_t my_b = bounds[ctx_.rank], my_n = bounds[ctx_.rank + 1] - my_b;
@@ -823,7 +830,7 @@ void Job::batch_mpi(RecordBatch* rb, int64_t n, int64_t total_chars, const std::
     pt_.end();
     if (ctx_.rank == kRoot) {
       results_.resize(static_cast<size_t>(n));
-      for (int64_t i = 0; i < n; ++i) results_[i] = decode_key(keys[i], all.length(i));
+      resolve_keys(keys.data(), all.codes.data(), all.offsets.data(), n, results_.data());
     }
     print(results_.data(), n, 0);
     return;

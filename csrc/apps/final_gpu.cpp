@@ -144,9 +144,10 @@ class HipDeviceSearch final : public DeviceSearch {
     e_.search_keys_device(d_codes, d_offsets, h_offsets, n, part, parts, reinterpret_cast<unsigned long long*>(d_keys),
                           e_.compute_stream());
   }
-  void finalize_keys(const int64_t* d_offsets, int64_t n, const uint64_t* d_keys, Result* d_out) override {
-    e_.finalize_keys_device(d_offsets, n, reinterpret_cast<const unsigned long long*>(d_keys), d_out, ResultFormat::R12,
-                            e_.compute_stream());
+  void finalize_keys(const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets, int64_t n,
+                     const uint64_t* d_keys, Result* d_out) override {
+    e_.finalize_keys_device(d_codes, d_offsets, h_offsets, n, reinterpret_cast<const unsigned long long*>(d_keys), d_out,
+                            ResultFormat::R12, e_.compute_stream());
   }
   double last_kernel_ms() const override { return kernel_ms_; }
   R2Params last_r2() const override { return r2_; }

@@ -47,7 +47,9 @@ int moc_brute_force(const int32_t* weights4, const uint8_t* seq1, int64_t L1, co
 int moc_cpu_solve_keys(const int32_t* weights4, const uint8_t* seq1, int64_t L1, const uint8_t* codes,
                        const int64_t* offsets, int64_t n, int semantics, int part, int parts, int threads,
                        uint64_t* keys);
-int moc_decode_keys(const uint64_t* keys, const int64_t* offsets, int64_t n, moc_result* out);
+/* MAX-combined pass-1 keys -> results: k resolved on each record's winning diagonal (needs the batch). */
+int moc_resolve_keys(const int32_t* weights4, const uint8_t* seq1, int64_t L1, const uint8_t* codes,
+                     const int64_t* offsets, int64_t n, const uint64_t* keys, moc_result* out);
 
 /* ---- partition ---- */
 int moc_partition(const int64_t* lengths, int64_t n, int64_t L1, int parts, double cell_w, double byte_w,
@@ -95,7 +97,8 @@ int moc_engine_search_keys(void* e, const uint8_t* codes, const int64_t* offsets
                            uint64_t* keys);
 int moc_engine_search_keys_device(void* e, const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets,
                                   int64_t n, int part, int parts, uint64_t* d_keys, void* stream);
-int moc_engine_finalize_keys_device(void* e, const int64_t* d_offsets, int64_t n, const uint64_t* d_keys, void* d_out,
+int moc_engine_finalize_keys_device(void* e, const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets,
+                                    int64_t n, const uint64_t* d_keys, void* d_out,
                                     int fmt, void* stream);
 /* stats: kernel_ms, total_ms, h2d_bytes, d2h_bytes, chunks, cells, records, direct, format, kernels */
 int moc_engine_stats(void* e, double* out14);

@@ -44,22 +44,19 @@ void solve_batch_cpu(const ScoreTable& t, const uint8_t* s1, int64_t L1, const R
                      Semantics sem, int num_threads = 0);
 
 // ---- packed candidate keys: the context-parallel combine
-// key = (score ^ 2^31) << 32 | (2^32 - 1 - (n*L2 + k)); 0 = "no candidate". The unsigned max over keys
-// is the reference's winner (higher score, then smaller offset, then smaller k), so partial searches
-// over disjoint offset ranges combine with one MAX reduction (MPI_Allreduce / ncclAllReduce, UINT64).
-// Identical to the device encoding (csrc/src/hip/kernel_common.hpp final_key/decode_key).
-inline uint64_t encode_key(const Result& r, int64_t L2) {
+// PASS-1 key = (score ^ 2^31) << 32 | (2^32 - 1 - (2n + mutated)); 0 = "no candidate". The unsigned max
+// over keys is the reference's winner up to its k (higher score, then smaller offset, then the un-mutated
+// candidate first), so partial searches over disjoint offset ranges combine with one MAX reduction
+// (MPI_Allreduce / ncclAllReduce, UINT64); resolve_key then finds k on the winning diagonal (the smallest k
+// with that score — the reference's order inside an offset). No o*L2 + k index: L1 * L2 may exceed 2^32.
+// Identical to the device encoding (csrc/src/hip/kernel_common.hpp lane_pass1_candidate, resolve_long_kernel).
+inline uint64_t encode_key(const Result& r) {
   if (r.n < 0 || r.score == kNoCandidateScore) return 0;
-  const uint32_t idx = static_cast<uint32_t>(r.n) * static_cast<uint32_t>(L2) + static_cast<uint32_t>(r.k);
+  const uint32_t idx = 2u * static_cast<uint32_t>(r.n) + (r.k > 0 ? 1u : 0u);
   return (static_cast<uint64_t>(static_cast<uint32_t>(r.score) ^ 0x80000000u) << 32) | (0xffffffffu - idx);
 }
-inline Result decode_key(uint64_t key, int64_t L2) {
-  if (key == 0) return no_candidate();
-  const int32_t score = static_cast<int32_t>(static_cast<uint32_t>(key >> 32) ^ 0x80000000u);
-  const uint32_t idx = 0xffffffffu - static_cast<uint32_t>(key);
-  const uint32_t l2 = static_cast<uint32_t>(L2 > 0 ? L2 : 1);
-  return Result{score, static_cast<int32_t>(idx / l2), static_cast<int32_t>(idx % l2)};
-}
+// The result a MAX-combined key stands for (record s2 of length L2 against Seq1 s1): O(L2).
+Result resolve_key(const ScoreTable& t, const uint8_t* s1, int64_t L1, const uint8_t* s2, int64_t L2, uint64_t key);
 
 // Part `part` of `parts` of every record's candidate set (offsets [C*part/parts, C*(part+1)/parts) of
 // its C candidate offsets) -> keys[i] (0 where the part holds no candidate). max over all parts of

@@ -156,12 +156,14 @@ void launch_short(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStr
 void launch_tiles(const ProblemView& pv, const BatchView& bv, const Plan& plan, void* out, int fmt,
                   hipStream_t stream);
 // The two halves separately (context-parallel mode: keys are max-reduced across ranks in between).
-// launch_tile_keys zeroes plan.keys[0..n_long) and max-accumulates the plan's tiles into them.
+// launch_tile_keys zeroes plan.keys[0..n_long) and max-accumulates the plan's tiles into them as PASS-1
+// keys (score, ~(2o + mutated)); launch_finalize_keys resolves each record's k on its winning diagonal
+// (one wave per record, O(L2)) and writes the results — no o*L2 + k index, so L1 * L2 >= 2^32 is fine.
 void launch_tile_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream);
-void launch_finalize_keys(const BatchView& bv, const Plan& plan, void* out, int fmt, hipStream_t stream);
-// tile16 variant of launch_tile_keys (pv.prof16 must be set): packed-int16 sweep over the LDS profile,
-// then one wave per record recovers k on the winning diagonal and writes final keys.
-// mfma_sweep: the matrix-core sweep (tile_mfma_kernels.hip, plan.u <= 4) in place of the packed-int16 one.
+void launch_finalize_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, void* out, int fmt,
+                          hipStream_t stream);
+// tile16 variant of launch_tile_keys (pv.prof16 must be set): packed-int16 sweep over the LDS profile.
+// mfma_sweep: the matrix-core sweep (tile_mfma_kernels.hip, plan.u <= 2) in place of the packed-int16 one.
 void launch_tile16_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream,
                         bool mfma_sweep = false);
 void launch_tile_mfma_sweep(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream);

@@ -69,10 +69,11 @@ class DeviceSearch {
   // A device-resident wire batch (offsets rebased to 0) -> results in `fmt` at d_out (comm lane order).
   virtual void solve(const WireBatch& d_batch, void* d_out, ResultFormat fmt) = 0;
   // Context-parallel share of every record (byte codes, dense offsets from 0; h_offsets: host copy) ->
-  // packed 64-bit keys; and the root's decode of the MAX-reduced keys into results (R12).
+  // packed pass-1 keys; and the root's resolve of the MAX-reduced keys into results (R12; needs the batch).
   virtual void search_keys(const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets, int64_t n,
                            int part, int parts, uint64_t* d_keys) = 0;
-  virtual void finalize_keys(const int64_t* d_offsets, int64_t n, const uint64_t* d_keys, Result* d_out) = 0;
+  virtual void finalize_keys(const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets, int64_t n,
+                             const uint64_t* d_keys, Result* d_out) = 0;
   virtual double last_kernel_ms() const = 0;
   virtual R2Params last_r2() const = 0;
 };

@@ -110,8 +110,9 @@ class HipEngine {
   // full answer; this splits single huge records across GPUs.
   void search_keys_device(const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets, int64_t n,
                           int part, int parts, unsigned long long* d_keys, hipStream_t stream);
-  void finalize_keys_device(const int64_t* d_offsets, int64_t n, const unsigned long long* d_keys, void* d_out,
-                            ResultFormat fmt, hipStream_t stream);
+  // MAX-combined pass-1 keys -> results (k resolved on each record's winning diagonal: needs the batch).
+  void finalize_keys_device(const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets, int64_t n,
+                            const unsigned long long* d_keys, void* d_out, ResultFormat fmt, hipStream_t stream);
   // Host-memory form of search_keys_device (uploads the batch, returns host keys; synchronous).
   void search_keys(const uint8_t* codes, const int64_t* offsets, int64_t n, int part, int parts, uint64_t* keys);
 

@@ -56,7 +56,8 @@ class CpuDeviceSearch final : public DeviceSearch {
   void solve(const WireBatch& b, void* out, ResultFormat fmt) override;
   void search_keys(const uint8_t* codes, const int64_t* offsets, const int64_t* h_offsets, int64_t n, int part,
                    int parts, uint64_t* keys) override;
-  void finalize_keys(const int64_t* offsets, int64_t n, const uint64_t* keys, Result* out) override;
+  void finalize_keys(const uint8_t* codes, const int64_t* offsets, const int64_t* h_offsets, int64_t n,
+                     const uint64_t* keys, Result* out) override;
   double last_kernel_ms() const override { return 0.0; }
   R2Params last_r2() const override { return R2Params{}; }
 

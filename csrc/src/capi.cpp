@@ -142,10 +142,12 @@ int moc_cpu_solve_keys(const int32_t* weights4, const uint8_t* seq1, int64_t L1,
   });
 }
 
-int moc_decode_keys(const uint64_t* keys, const int64_t* offsets, int64_t n, moc_result* out) {
+int moc_resolve_keys(const int32_t* weights4, const uint8_t* seq1, int64_t L1, const uint8_t* codes,
+                     const int64_t* offsets, int64_t n, const uint64_t* keys, moc_result* out) {
   return guard([&] {
+    const moc::ScoreTable t = moc::ScoreTable::build(weights_of(weights4));
     for (int64_t i = 0; i < n; ++i) {
-      moc::Result r = moc::decode_key(keys[i], offsets[i + 1] - offsets[i]);
+      const moc::Result r = moc::resolve_key(t, seq1, L1, codes + offsets[i], offsets[i + 1] - offsets[i], keys[i]);
       std::memcpy(out + i, &r, sizeof r);
     }
   });
@@ -359,10 +361,11 @@ int moc_engine_search_keys_device(void* e, const uint8_t* d_codes, const int64_t
   });
 }
 
-int moc_engine_finalize_keys_device(void* e, const int64_t* d_offsets, int64_t n, const uint64_t* d_keys, void* d_out,
+int moc_engine_finalize_keys_device(void* e, const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets,
+                                    int64_t n, const uint64_t* d_keys, void* d_out,
                                     int fmt, void* stream) {
   return guard([&] {
-    static_cast<moc::HipEngine*>(e)->finalize_keys_device(d_offsets, n,
+    static_cast<moc::HipEngine*>(e)->finalize_keys_device(d_codes, d_offsets, h_offsets, n,
                                                           reinterpret_cast<const unsigned long long*>(d_keys), d_out,
                                                           static_cast<moc::ResultFormat>(fmt),
                                                           static_cast<hipStream_t>(stream));

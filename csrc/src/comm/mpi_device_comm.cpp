@@ -101,8 +101,12 @@ void CpuDeviceSearch::search_keys(const uint8_t* codes, const int64_t* offsets, 
   solve_keys_cpu(table_, seq1_.data(), static_cast<int64_t>(seq1_.size()), rb, part, parts, keys, sem_, threads_);
 }
 
-void CpuDeviceSearch::finalize_keys(const int64_t* offsets, int64_t n, const uint64_t* keys, Result* out) {
-  for (int64_t i = 0; i < n; ++i) out[i] = decode_key(keys[i], offsets[i + 1] - offsets[i]);
+void CpuDeviceSearch::finalize_keys(const uint8_t* codes, const int64_t* offsets, const int64_t*, int64_t n,
+                                    const uint64_t* keys, Result* out) {
+  const int64_t L1 = static_cast<int64_t>(seq1_.size());
+#pragma omp parallel for schedule(dynamic, 64) if (n > 4096)
+  for (int64_t i = 0; i < n; ++i)
+    out[i] = resolve_key(table_, seq1_.data(), L1, codes + offsets[i], offsets[i + 1] - offsets[i], keys[i]);
 }
 
 }  // namespace moc

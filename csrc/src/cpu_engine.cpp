@@ -1,5 +1,7 @@
 #include "moc/cpu_engine.hpp"
 
+#include <string>
+
 #include <omp.h>
 
 #include <algorithm>
@@ -139,7 +141,7 @@ void solve_keys_cpu(const ScoreTable& t, const uint8_t* s1, int64_t L1, const Re
       int64_t b, e;
       range(i, b, e);
       const int64_t L2 = batch.length(i);
-      keys[i] = encode_key(solve_offsets(t, s1, L1, batch.record(i), L2, b, e, sem), L2);
+      keys[i] = encode_key(solve_offsets(t, s1, L1, batch.record(i), L2, b, e, sem));
     }
     return;
   }
@@ -159,7 +161,7 @@ void solve_keys_cpu(const ScoreTable& t, const uint8_t* s1, int64_t L1, const Re
   for (int64_t j = 0; j < static_cast<int64_t>(items.size()); ++j) {
     const Item& it = items[j];
     const int64_t L2 = batch.length(it.rec);
-    pk[j] = encode_key(solve_offsets(t, s1, L1, batch.record(it.rec), L2, it.ob, it.oe, sem), L2);
+    pk[j] = encode_key(solve_offsets(t, s1, L1, batch.record(it.rec), L2, it.ob, it.oe, sem));
   }
   for (int64_t i = 0; i < n; ++i) keys[i] = 0;
   for (size_t j = 0; j < items.size(); ++j) keys[items[j].rec] = std::max(keys[items[j].rec], pk[j]);
@@ -195,6 +197,24 @@ Result brute_force_record(const ScoreTable& t, const uint8_t* s1, int64_t L1, co
     if (!have || best.score < s) best = Result{s, static_cast<int32_t>(o), 0};
   }
   return best;
+}
+
+Result resolve_key(const ScoreTable& t, const uint8_t* s1, int64_t L1, const uint8_t* s2, int64_t L2, uint64_t key) {
+  if (key == 0) return no_candidate();
+  const int32_t score = static_cast<int32_t>(static_cast<uint32_t>(key >> 32) ^ 0x80000000u);
+  const uint32_t idx = 0xffffffffu - static_cast<uint32_t>(key);
+  const int64_t o = idx >> 1;
+  if (!(idx & 1u)) return Result{score, static_cast<int32_t>(o), 0};
+  if (o + L2 >= L1) throw Error("resolve_key: a mutated candidate needs o + L2 < L1");
+  // score = D_o(k) + Tot_{o+1}; the smallest k in 1..L2-1 with that value
+  int64_t tot1 = 0;
+  for (int64_t i = 0; i < L2; ++i) tot1 += t.score(s2[i], s1[o + 1 + i]);
+  int64_t d = 0;
+  for (int64_t k = 1; k < L2; ++k) {
+    d += t.score(s2[k - 1], s1[o + k - 1]) - t.score(s2[k - 1], s1[o + k]);
+    if (d + tot1 == score) return Result{score, static_cast<int32_t>(o), static_cast<int32_t>(k)};
+  }
+  throw Error("resolve_key: no k on diagonal " + std::to_string(o) + " reaches the key's score");
 }
 
 }  // namespace moc

@@ -150,7 +150,7 @@ DeviceBatchOut batch_cp(DeviceComm& dc, DeviceSearch& ds, const RecordBatch* rb,
   dc.allreduce_max_u64(d_keys, n);
   if (rank == 0) {
     Result* d_res = bufs.d<Result>(12 * n);
-    ds.finalize_keys(d_offs, n, d_keys, d_res);
+    ds.finalize_keys(d_codes, d_offs, h_offs.data(), n, d_keys, d_res);
     out.storage.emplace_back(static_cast<size_t>(12 * n));
     dc.download(out.storage.back().data(), d_res, 12 * n);
     out.runs.push_back(ResultRun{out.storage.back().data(), ResultFormat::R12, R2Params{}, n});

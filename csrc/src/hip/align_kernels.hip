@@ -116,7 +116,7 @@ __global__ __launch_bounds__(256) void tile_search_kernel(ProblemView pv, BatchV
         const int o = o0 + kTileOffsets * u + lane;
         const int Pn = wave_shl1(P[u]);
         const bool own = lane < kTileOffsets && L2 <= L1 && o <= L1 - L2;
-        acc = max_u64(acc, lane_candidate<Wide>(own, o, L1, L2, pv.semantics, P[u], Pn, best[u], shift, mask));
+        acc = max_u64(acc, lane_pass1_candidate<Wide>(own, o, L1, L2, pv.semantics, P[u], Pn, best[u], shift));
       }
     }
     const unsigned long long k = wave_max_u64(acc);
@@ -126,13 +126,59 @@ __global__ __launch_bounds__(256) void tile_search_kernel(ProblemView pv, BatchV
   }
 }
 
-__global__ void finalize_long_kernel(R2Params r2, BatchView bv, const int32_t* __restrict__ long_recs,
-                                     const unsigned long long* __restrict__ keys, int64_t n_long, void* out, int fmt) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n_long) return;
-  const int r = long_recs ? long_recs[i] : static_cast<int>(i);
+// One wave per long record: its pass-1 key (score, ~(2o + mutated)) from the sweep (tile, tile16 or
+// tile-mfma; or a context-parallel MAX of several) -> the result (score, n = o, k). For a mutated winner
+// k is the smallest k in 1..L2-1 with P_o(k) - P_{o+1}(k) + Tot_{o+1} == score, found with a wave prefix
+// scan of the diagonal differences (ballot picks the first match): O(L2) per record, and no o*L2 + k
+// index anywhere, so L1 * L2 may exceed 2^32.
+__global__ __launch_bounds__(256) void resolve_long_kernel(ProblemView pv, BatchView bv,
+                                                           const int32_t* __restrict__ long_recs,
+                                                           const unsigned long long* __restrict__ keys, int64_t n_long,
+                                                           void* out, int fmt) {
+  const int64_t li = static_cast<int64_t>(blockIdx.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (li >= n_long) return;
+  const int lane = threadIdx.x & 63;
+  const int r = long_recs ? long_recs[li] : static_cast<int>(li);
+  const unsigned long long key = keys[li];
+  if (key == 0ull) {
+    if (lane == 0) store_result(out, r, fmt, Result{INT32_MIN, 0, 0}, pv.r2);
+    return;
+  }
+  const int score = static_cast<int>(static_cast<uint32_t>(key >> 32) ^ 0x80000000u);
+  const uint32_t idx = 0xffffffffu - static_cast<uint32_t>(key);
+  const int o = static_cast<int>(idx >> 1);
+  const uint8_t* rec = bv.codes + (bv.offsets[r] - bv.offsets[0]);
   const int L2 = static_cast<int>(bv.offsets[r + 1] - bv.offsets[r]);
-  store_result(out, r, fmt, decode_key(keys[i], L2 > 0 ? L2 : 1), r2);
+  int k = 0;
+  if (idx & 1u) {  // mutated: o < L1 - L2, so Seq1[o + 1 + i] stays inside Seq1 for i < L2
+    MOC_DCHECK(o + L2 < pv.L1 && L2 >= 2);
+    const uint8_t* s1 = pv.seq1 + o;
+    int tot1 = 0;
+    for (int i = lane; i < L2; i += 64) tot1 += pv.lut[rec[i] * kLutStride + s1[i + 1]];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) tot1 += __shfl_xor(tot1, d, 64);
+    const int target = score - tot1;  // D_o(k) of the winning k
+    int carry = 0;
+    k = -1;
+    for (int i0 = 0; i0 < L2 - 1; i0 += 64) {  // candidate k = i + 1, i in [0, L2 - 2]
+      const int i = i0 + lane;
+      int d = 0;
+      if (i < L2 - 1) {
+        const int* row = pv.lut + rec[i] * kLutStride;
+        d = row[s1[i]] - row[s1[i + 1]];
+      }
+      const int incl = wave_inclusive_sum(d, lane) + carry;
+      const unsigned long long hit = __ballot(i < L2 - 1 && incl == target);
+      if (hit) {
+        k = i0 + __builtin_ctzll(hit) + 1;
+        break;
+      }
+      carry = __shfl(incl, 63, 64);
+    }
+    MOC_DCHECK(k >= 1);
+    if (k < 1) k = 0;  // unreachable (the sweep saw this score on this diagonal)
+  }
+  if (lane == 0) store_result(out, r, fmt, Result{score, o, k}, pv.r2);
 }
 
 // Self-test of the cross-lane primitives the search kernels rely on (one wave):
@@ -182,11 +228,14 @@ void launch_search_u(const ProblemView& pv, const BatchView& bv, const Plan& pla
   }
 }
 
-void launch_finalize(const BatchView& bv, const Plan& plan, void* out, int fmt, hipStream_t stream) {
+void launch_finalize(const ProblemView& pv, const BatchView& bv, const Plan& plan, void* out, int fmt,
+                     hipStream_t stream) {
   if (plan.n_long <= 0) return;
-  const int64_t fb = (plan.n_long + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(finalize_long_kernel, dim3(static_cast<unsigned>(fb)), dim3(kBlock), 0, stream, plan.r2, bv,
-                     plan.long_recs, plan.keys, plan.n_long, out, fmt);
+  ProblemView p = pv;
+  p.r2 = plan.r2;
+  const int64_t rb = (plan.n_long + 3) / 4;
+  hipLaunchKernelGGL(resolve_long_kernel, dim3(static_cast<unsigned>(rb)), dim3(256), 0, stream, p, bv, plan.long_recs,
+                     plan.keys, plan.n_long, out, fmt);
 }
 }  // namespace
 
@@ -203,15 +252,16 @@ void launch_tile_keys(const ProblemView& pv, const BatchView& bv, const Plan& pl
     launch_search_u<true>(pv, bv, plan, stream);
 }
 
-void launch_finalize_keys(const BatchView& bv, const Plan& plan, void* out, int fmt, hipStream_t stream) {
-  launch_finalize(bv, plan, out, fmt, stream);
+void launch_finalize_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, void* out, int fmt,
+                          hipStream_t stream) {
+  launch_finalize(pv, bv, plan, out, fmt, stream);
 }
 
 void launch_tiles(const ProblemView& pv, const BatchView& bv, const Plan& plan, void* out, int fmt,
                   hipStream_t stream) {
   if (plan.n_long <= 0) return;
   launch_tile_keys(pv, bv, plan, stream);
-  launch_finalize(bv, plan, out, fmt, stream);
+  launch_finalize(pv, bv, plan, out, fmt, stream);
 }
 
 }  // namespace dev

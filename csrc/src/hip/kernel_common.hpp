@@ -142,6 +142,24 @@ __device__ __forceinline__ unsigned long long lane_candidate(bool own, int o, in
   return key;
 }
 
+// The same candidate as a PASS-1 key (score, ~(2o + mutated)) of the long-record sweeps: which k wins on
+// the winning diagonal is resolved afterwards (resolve_long_kernel), so the key never holds o*L2 + k and
+// L1 * L2 may exceed 2^32 (o < 2^31 is the only bound). Same order as final keys: score, then the
+// smallest o, then the un-mutated candidate first.
+template <bool Wide>
+__device__ __forceinline__ unsigned long long lane_pass1_candidate(bool own, int o, int L1, int L2, int sem, int P,
+                                                                   int Pn, typename HotKey<Wide>::T best, int shift) {
+  using K = HotKey<Wide>;
+  unsigned long long key = 0;
+  if (!own) return key;
+  const int last = L1 - L2;
+  const bool v0 = (o < last) || (o == last && (sem == static_cast<int>(Semantics::Spec) || L2 == L1));
+  if (v0) key = final_key(P, 2u * static_cast<uint32_t>(o));
+  if (o < last && L2 >= 2 && best != K::min())
+    key = max_u64(key, final_key(K::d(best, shift) + Pn, 2u * static_cast<uint32_t>(o) + 1u));
+  return key;
+}
+
 // ---- result formats -------------------------------------------------------------------------------
 __device__ __forceinline__ void store_result(void* out, int64_t r, int fmt, const Result& v, const R2Params& p) {
   if (fmt == static_cast<int>(ResultFormat::R2)) {

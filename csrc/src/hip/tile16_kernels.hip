@@ -23,10 +23,10 @@
 //   * short records (mean |Seq2| < 96) take U = 8 sub-tiles (1024-offset tiles: half the per-tile
 //     epilogues) when the profile's 1024-entry overhang fits the LDS; their last chunk issues the reads
 //     of 8 steps before the adds (profiles/tile16_variants_v2.log).
-// Per offset this gives the best score, but not which k: the sweep reduces keys (score, ~(2o + mutated))
-// — the reference order: score, then smallest o, then k = 0 first — and resolve16_kernel re-walks only
-// the winning diagonal of each record (one wave, O(L2)) to find the smallest k with that score and
-// write the engine's final key (score, ~(o*L2 + k)). Host replay of all of it, ties included:
+// Per offset this gives the best score, but not which k: the sweep reduces pass-1 keys (score,
+// ~(2o + mutated)) — the reference order: score, then smallest o, then k = 0 first — and
+// resolve_long_kernel (align_kernels.hip) re-walks only the winning diagonal of each record (one wave,
+// O(L2)) to find the smallest k with that score. Host replay of all of it, ties included:
 // csrc/tests/test_core.cpp test_profile16.
 //
 // Replaces calc_result (cudaFunctions.cu:63-176) for long records when the weights fit the profile
@@ -281,56 +281,6 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
   }
 }
 
-// One wave per long record: pass-1 key (score, ~(2o + m)) -> final key (score, ~(o*L2 + k)). For a
-// mutated winner, k is the smallest k in 1..L2-1 with P_o(k) - P_{o+1}(k) + Tot_{o+1} == score, found
-// with a wave prefix scan of the diagonal differences (ballot picks the first match).
-__global__ __launch_bounds__(256) void resolve16_kernel(ProblemView pv, BatchView bv,
-                                                        const int32_t* __restrict__ long_recs,
-                                                        unsigned long long* __restrict__ keys, int64_t n_long) {
-  const int64_t li = static_cast<int64_t>(blockIdx.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (li >= n_long) return;
-  const int lane = threadIdx.x & 63;
-  const unsigned long long key = keys[li];
-  if (key == 0ull) return;
-  const int score = static_cast<int>(static_cast<uint32_t>(key >> 32) ^ 0x80000000u);
-  const uint32_t idx = 0xffffffffu - static_cast<uint32_t>(key);
-  const int o = static_cast<int>(idx >> 1);
-  const int r = long_recs ? long_recs[li] : static_cast<int>(li);
-  const uint8_t* rec = bv.codes + (bv.offsets[r] - bv.offsets[0]);
-  const int L2 = static_cast<int>(bv.offsets[r + 1] - bv.offsets[r]);
-  int k = 0;
-  if (idx & 1u) {  // mutated: o < L1 - L2, so Seq1[o + 1 + i] stays inside Seq1 for i < L2
-    MOC_DCHECK(o + L2 < pv.L1 && L2 >= 2);
-    const uint8_t* s1 = pv.seq1 + o;
-    int tot1 = 0;
-    for (int i = lane; i < L2; i += 64) tot1 += pv.lut[rec[i] * kLutStride + s1[i + 1]];
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) tot1 += __shfl_xor(tot1, d, 64);
-    const int target = score - tot1;  // D_o(k) of the winning k
-    int carry = 0;
-    k = -1;
-    for (int i0 = 0; i0 < L2 - 1; i0 += 64) {  // candidate k = i + 1, i in [0, L2 - 2]
-      const int i = i0 + lane;
-      int d = 0;
-      if (i < L2 - 1) {
-        const int* row = pv.lut + rec[i] * kLutStride;
-        d = row[s1[i]] - row[s1[i + 1]];
-      }
-      const int incl = wave_inclusive_sum(d, lane) + carry;
-      const unsigned long long hit = __ballot(i < L2 - 1 && incl == target);
-      if (hit) {
-        k = i0 + __builtin_ctzll(hit) + 1;
-        break;
-      }
-      carry = __shfl(incl, 63, 64);
-    }
-    MOC_DCHECK(k >= 1);
-    if (k < 1) k = 0;  // unreachable (the sweep saw this score on this diagonal)
-  }
-  if (lane == 0)
-    keys[li] = final_key(score, static_cast<uint32_t>(o) * static_cast<uint32_t>(L2) + static_cast<uint32_t>(k));
-}
-
 int tile16_waves_per_cu(int lds_bytes) {
   const int blocks = lds_bytes > 0 ? kProf16MaxLds / lds_bytes : 2;
   return kWavesPerBlock16 * max(1, min(2, blocks));
@@ -360,7 +310,7 @@ void launch16_t(const ProblemView& pv, const BatchView& bv, const Plan& plan, hi
 
 void preload_tile16_kernels() {
   hipFuncAttributes fa;
-  (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&resolve16_kernel));
+  (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&tile16_search_kernel<2>));
 }
 
 void launch_tile16_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream,
@@ -380,9 +330,6 @@ void launch_tile16_keys(const ProblemView& pv, const BatchView& bv, const Plan& 
       default: launch16_t<4>(pv, bv, plan, stream); break;
     }
   }
-  const int64_t rb = (plan.n_long + 3) / 4;
-  hipLaunchKernelGGL(resolve16_kernel, dim3(static_cast<unsigned>(rb)), dim3(256), 0, stream, pv, bv, plan.long_recs,
-                     plan.keys, plan.n_long);
 }
 
 }  // namespace dev

@@ -1,6 +1,6 @@
 // Long-record search sweep on the matrix cores ("tile-mfma"; gfx950 v_mfma_i32_32x32x32_i8), the measured
 // MFMA variant of tile16_search_kernel (SURVEY.md §7.3 formulation (b); docs/MFMA_ANALYSIS.md). Selected
-// with MOC_MFMA=1 in place of the tile16 sweep; plan, pass-1 keys and resolve16_kernel are shared.
+// with MOC_MFMA=1 in place of the tile16 sweep; plan, pass-1 keys and resolve_long_kernel are shared.
 //
 // Per record, wave tile of 128*U offsets and chunk of 32 steps i0 .. i0+31, the running differences
 //     D_o(k) = sum_{i<k} Dt[c_i][o + i]      (Dt: the int8 difference profile in LDS, tile16's image)

@@ -290,8 +290,8 @@ void HipEngine::plan_chunk(const int64_t* offsets, int64_t n, ChunkPlan& cp) con
     cp.cells += cells[t];
     cp.long_recs.insert(cp.long_recs.end(), part[t].begin(), part[t].end());
   }
-  if (cp.max_l2 * std::max<int64_t>(L1_, 1) >= (int64_t{1} << 32))
-    throw Error("L1 * max L2 exceeds the 32-bit candidate index of the device engine");
+  if (L1_ >= (int64_t{1} << 30) || cp.max_l2 >= (int64_t{1} << 30))
+    throw Error("Seq1 / Seq2 lengths beyond 2^30 exceed the device engine's offset range");
 }
 
 namespace {
@@ -880,8 +880,7 @@ void HipEngine::search_keys_device(const uint8_t* d_codes, const int64_t* d_offs
   TraceRange tr("moc.search_keys");
   int64_t max_l2 = 0;
   for (int64_t i = 0; i < n; ++i) max_l2 = std::max(max_l2, h_offsets[i + 1] - h_offsets[i]);
-  if (max_l2 * std::max<int64_t>(L1_, 1) >= (int64_t{1} << 32))
-    throw Error("L1 * max L2 exceeds the 32-bit candidate index of the device engine");
+  if (max_l2 >= (int64_t{1} << 30)) throw Error("Seq2 lengths beyond 2^30 exceed the device engine's offset range");
   // the record-major tile list of all records; this part takes a contiguous, cost-balanced share of it
   int tile_u = 0;
   const std::vector<dev::WaveStart> starts = plan_waves(h_offsets, nullptr, n, part, parts, tile_u);
@@ -910,17 +909,21 @@ void HipEngine::search_keys_device(const uint8_t* d_codes, const int64_t* d_offs
   stats_.kernels = plan.n_waves ? (d_prof16_ ? 8 : 4) : 0;
 }
 
-void HipEngine::finalize_keys_device(const int64_t* d_offsets, int64_t n, const unsigned long long* d_keys,
-                                     void* d_out, ResultFormat fmt, hipStream_t stream) {
+void HipEngine::finalize_keys_device(const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets,
+                                     int64_t n, const unsigned long long* d_keys, void* d_out, ResultFormat fmt,
+                                     hipStream_t stream) {
   MOC_HIP_CHECK(hipSetDevice(device_));
   if (n <= 0) return;
   if (!stream) stream = s_compute_;
+  int64_t max_l2 = 0;
+  for (int64_t i = 0; i < n; ++i) max_l2 = std::max(max_l2, h_offsets[i + 1] - h_offsets[i]);
   dev::Plan plan;
   plan.long_recs = nullptr;
   plan.n_long = n;
   plan.keys = const_cast<unsigned long long*>(d_keys);
-  dev::BatchView bv{nullptr, d_offsets, n};
-  dev::launch_finalize_keys(bv, plan, d_out, static_cast<int>(fmt), stream);
+  if (fmt == ResultFormat::R2) throw Error("finalize_keys_device: R2 needs the batch's parameters; use R4/R8/R12");
+  dev::BatchView bv{d_codes + h_offsets[0], d_offsets, n};
+  dev::launch_finalize_keys(problem_view(max_l2), bv, plan, d_out, static_cast<int>(fmt), stream);
   MOC_HIP_CHECK(hipGetLastError());
 }
 
@@ -935,12 +938,16 @@ void HipEngine::search_keys(const uint8_t* codes, const int64_t* offsets, int64_
   ensure(s.d_codes, s.d_codes_cap, std::max<size_t>(cbytes, 16) + 32);
   ensure(s.d_offsets, s.d_offsets_cap, sizeof(int64_t) * static_cast<size_t>(n + 1));
   ensure(s.d_out, s.d_out_cap, sizeof(uint64_t) * static_cast<size_t>(n));
+  // offsets rebased to 0, so the device base pointer is the buffer itself (record i at d_codes + rebased[i])
+  std::vector<int64_t> rebased(static_cast<size_t>(n) + 1);
+  for (int64_t i = 0; i <= n; ++i) rebased[i] = offsets[i] - offsets[0];
   if (cbytes)
     copy_h2d(s.d_codes, codes + offsets[0], cbytes, s_compute_);
-  copy_h2d(s.d_offsets, offsets, sizeof(int64_t) * (n + 1), s_compute_);
+  MOC_HIP_CHECK(hipMemcpyAsync(s.d_offsets, rebased.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice,
+                               s_compute_));
   MOC_HIP_CHECK(hipEventRecord(ev_a_, s_compute_));
-  search_keys_device(static_cast<const uint8_t*>(s.d_codes) - offsets[0], static_cast<const int64_t*>(s.d_offsets),
-                     offsets, n, part, parts, static_cast<unsigned long long*>(s.d_out), s_compute_);
+  search_keys_device(static_cast<const uint8_t*>(s.d_codes), static_cast<const int64_t*>(s.d_offsets), rebased.data(),
+                     n, part, parts, static_cast<unsigned long long*>(s.d_out), s_compute_);
   MOC_HIP_CHECK(hipEventRecord(ev_b_, s_compute_));
   copy_d2h(keys, s.d_out, sizeof(uint64_t) * n, s_compute_);
   MOC_HIP_CHECK(hipStreamSynchronize(s_compute_));

@@ -216,19 +216,26 @@ void test_partition() {
 }
 
 void test_keys() {
-  // higher score wins; then the smaller offset; then the smaller k (k = 0 first)
-  const int64_t L2 = 7;
-  const uint64_t a = encode_key(Result{5, 2, 3}, L2), b = encode_key(Result{5, 2, 4}, L2),
-                 c = encode_key(Result{5, 1, 6}, L2), d = encode_key(Result{6, 9, 6}, L2),
-                 e = encode_key(Result{-100, 0, 0}, L2);
+  // pass-1 keys: higher score wins; then the smaller offset; then the un-mutated candidate (k = 0) first
+  const uint64_t a = encode_key(Result{5, 2, 0}), b = encode_key(Result{5, 2, 4}), c = encode_key(Result{5, 1, 6}),
+                 d = encode_key(Result{6, 9, 6}), e = encode_key(Result{-100, 0, 0});
   CHECK(a > b && c > a && d > c && e < a && e > 0);
-  CHECK(encode_key(no_candidate(), L2) == 0);
-  for (const Result& r : {Result{5, 2, 3}, Result{-7, 0, 0}, Result{123456, 999, 6}}) {
-    const Result q = decode_key(encode_key(r, L2), L2);
-    CHECK(q.score == r.score && q.n == r.n && q.k == r.k);
-  }
-  const Result none = decode_key(0, L2);
+  CHECK(encode_key(Result{5, 2, 3}) == encode_key(Result{5, 2, 4}));  // k is resolved afterwards
+  CHECK(encode_key(no_candidate()) == 0);
+  // resolve_key recovers the smallest k on the winning diagonal, also where o*L2 + k exceeds 32 bits
+  const ScoreTable t = ScoreTable::build(Weights{{4, 3, 2, 10}});
+  const Result none = resolve_key(t, nullptr, 10, nullptr, 3, 0);
   CHECK(none.score == kNoCandidateScore && none.n == 0 && none.k == 0);
+  std::mt19937 rng(5);
+  for (int trial = 0; trial < 4; ++trial) {
+    const int64_t L1 = trial < 2 ? 60 : 70000, L2 = trial < 2 ? 17 : 65000;  // 70000 * 65000 > 2^32
+    std::vector<uint8_t> s1(static_cast<size_t>(L1)), s2(static_cast<size_t>(L2));
+    for (auto& x : s1) x = static_cast<uint8_t>(1 + rng() % 26);
+    for (auto& x : s2) x = static_cast<uint8_t>(1 + rng() % 26);
+    const Result full = solve_record(t, s1.data(), L1, s2.data(), L2, Semantics::Reference);
+    const Result r = resolve_key(t, s1.data(), L1, s2.data(), L2, encode_key(full));
+    CHECK(r.score == full.score && r.n == full.n && r.k == full.k);
+  }
 }
 
 void test_pack5() {
@@ -274,7 +281,7 @@ void test_engine_vs_brute_force() {
         for (size_t i = 0; i < keys.size(); ++i) keys[i] = std::max(keys[i], part[i]);
       }
       for (int64_t i = 0; i < batch.size(); ++i) {
-        const Result r = decode_key(keys[i], batch.length(i));
+        const Result r = resolve_key(t, s1.data(), L1, batch.record(i), batch.length(i), keys[i]);
         CHECK(r.score == out[i].score && r.n == out[i].n && r.k == out[i].k);
       }
     }

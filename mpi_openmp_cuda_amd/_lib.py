@@ -54,7 +54,7 @@ def _decl(lib):
         "moc_cpu_solve": (c_int, [P(c_int32), c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p]),
         "moc_cpu_solve_keys": (c_int, [P(c_int32), c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_int, c_int,
                                        c_int, c_void_p]),
-        "moc_decode_keys": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
+        "moc_resolve_keys": (c_int, [P(c_int32), c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
         "moc_brute_force": (c_int, [P(c_int32), c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
         "moc_partition": (c_int, [c_void_p, c_int64, c_int64, c_int, c_double, c_double, c_double, c_void_p]),
         "moc_device_count": (c_int, []),
@@ -85,7 +85,8 @@ def _decl(lib):
         "moc_engine_search_keys": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p]),
         "moc_engine_search_keys_device": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int,
                                                   c_void_p, c_void_p]),
-        "moc_engine_finalize_keys_device": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_void_p]),
+        "moc_engine_finalize_keys_device": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
+                                                    c_int, c_void_p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

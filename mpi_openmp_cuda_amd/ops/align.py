@@ -61,7 +61,7 @@ def search_cpu(problem: Problem, semantics=Semantics.REFERENCE, threads: int = 0
 def search_keys_cpu(problem: Problem, part: int, parts: int, semantics=Semantics.REFERENCE,
                     threads: int = 0) -> np.ndarray:
     """Context-parallel partial search: part ``part`` of ``parts`` of every record's offset
-    range -> packed uint64 keys (0 = no candidate in this part). ``np.maximum`` over all parts, then
+    range -> packed uint64 pass-1 keys (0 = no candidate in this part). ``np.maximum`` over all parts, then
     :func:`decode_keys`, equals :func:`search_cpu`."""
     keys = np.zeros(problem.n, np.uint64)
     _lib.check(_lib.lib().moc_cpu_solve_keys(
@@ -71,12 +71,15 @@ def search_keys_cpu(problem: Problem, part: int, parts: int, semantics=Semantics
     return keys
 
 
-def decode_keys(keys: np.ndarray, offsets: np.ndarray) -> np.ndarray:
-    """Packed keys ((score^2^31)<<32 | ~(n*L2+k)) -> structured (score, n, k) results."""
+def decode_keys(keys: np.ndarray, problem: Problem) -> np.ndarray:
+    """MAX-combined pass-1 keys ((score^2^31)<<32 | ~(2n + mutated)) -> structured (score, n, k) results; the k
+    of a mutated winner is the smallest one on its diagonal with that score, so the problem's records are
+    needed (no n*L2 + k index: any L1 * L2)."""
     keys = np.ascontiguousarray(keys, dtype=np.uint64)
-    offsets = np.ascontiguousarray(offsets, dtype=np.int64)
     out = empty_results(keys.shape[0])
-    _lib.check(_lib.lib().moc_decode_keys(_lib.ptr(keys), _lib.ptr(offsets), keys.shape[0], _lib.ptr(out)))
+    _lib.check(_lib.lib().moc_resolve_keys(
+        _lib.weights_arg(problem.weights.as_list()), _lib.ptr(problem.seq1), problem.L1, _lib.ptr(problem.codes),
+        _lib.ptr(problem.offsets), keys.shape[0], _lib.ptr(keys), _lib.ptr(out)))
     return out
 
 
@@ -248,17 +251,20 @@ class HipSearchEngine:
             n, int(part), int(parts), ctypes.c_void_p(keys_t.data_ptr()), ctypes.c_void_p(stream.cuda_stream)))
         return keys_t
 
-    def finalize_keys_device(self, offsets_t, keys_t, out_t, stream=None):
-        """Device keys -> int32 [n, 3] results (score, n, k)."""
+    def finalize_keys_device(self, codes_t, offsets_t, h_offsets: np.ndarray, keys_t, out_t, stream=None):
+        """MAX-combined device keys -> int32 [n, 3] results (score, n, k); k is resolved on each record's
+        winning diagonal, so the batch (codes_t, offsets_t from 0, host copy h_offsets) is needed."""
         import torch
 
         n = keys_t.numel()
         assert out_t.dtype == torch.int32 and out_t.shape == (n, 3)
+        h_offsets = np.ascontiguousarray(h_offsets, dtype=np.int64)
         if stream is None:
             stream = torch.cuda.current_stream(keys_t.device)
         _lib.check(_lib.lib().moc_engine_finalize_keys_device(
-            self._h, ctypes.c_void_p(offsets_t.data_ptr()), n, ctypes.c_void_p(keys_t.data_ptr()),
-            ctypes.c_void_p(out_t.data_ptr()), 0, ctypes.c_void_p(stream.cuda_stream)))
+            self._h, ctypes.c_void_p(codes_t.data_ptr()), ctypes.c_void_p(offsets_t.data_ptr()), _lib.ptr(h_offsets),
+            n, ctypes.c_void_p(keys_t.data_ptr()), ctypes.c_void_p(out_t.data_ptr()), 0,
+            ctypes.c_void_p(stream.cuda_stream)))
         return out_t
 
     def stats(self) -> dict:

@@ -204,7 +204,8 @@ class DistributedSearch:
             keys = self._keys(prob, sem, np.asarray(codes), np.asarray(offsets)) if n else np.zeros(0, np.uint64)
         with T.phase("gather"):
             best = ordered_int64_to_keys(D.allreduce_max_int64(ctx, keys_to_ordered_int64(keys)))
-            out = decode_keys(best, np.asarray(offsets)) if ctx.is_root else None
+            out = decode_keys(best, Problem(prob.weights, prob.seq1, np.asarray(codes), np.asarray(offsets))) \
+                if ctx.is_root else None
             if win is not None:
                 D.barrier(ctx)
                 win.close(unlink=ctx.is_root)

@@ -15,7 +15,7 @@ def test_parts_combine_to_full_search(shape, n, parts, sem):
     keys = np.zeros(prob.n, np.uint64)
     for part in range(parts):
         keys = np.maximum(keys, search_keys_cpu(prob, part, parts, sem))
-    assert np.array_equal(as_triples(decode_keys(keys, prob.offsets)), as_triples(search_cpu(prob, sem)))
+    assert np.array_equal(as_triples(decode_keys(keys, prob)), as_triples(search_cpu(prob, sem)))
 
 
 def test_edge_records():
@@ -25,7 +25,7 @@ def test_edge_records():
         keys = np.zeros(prob.n, np.uint64)
         for part in range(parts):
             keys = np.maximum(keys, search_keys_cpu(prob, part, parts))
-        got = as_triples(decode_keys(keys, prob.offsets))
+        got = as_triples(decode_keys(keys, prob))
         assert np.array_equal(got, as_triples(search_cpu(prob)))
         assert tuple(got[1]) == (-2**31, 0, 0)
 

@@ -315,7 +315,7 @@ def test_context_parallel_keys(engine, shape, n, parts):
         for part in range(parts):
             keys = np.maximum(keys, engine.search_keys(prob.codes, prob.offsets, part, parts))
         ref = as_triples(search_cpu(prob, sem))
-        assert np.array_equal(as_triples(decode_keys(keys, prob.offsets)), ref)
+        assert np.array_equal(as_triples(decode_keys(keys, prob)), ref)
         # each GPU share is a lower bound of the CPU full-range key (same encoding on both sides)
         full = search_keys_cpu(prob, 0, 1, sem)
         assert np.array_equal(keys, full)
@@ -338,7 +338,7 @@ def test_context_parallel_device_finalize(engine):
     flip = torch.tensor(-2**63, dtype=torch.int64, device=dev)
     best = torch.stack([p ^ flip for p in parts]).max(dim=0).values ^ flip
     out = torch.empty(prob.n, 3, dtype=torch.int32, device=dev)
-    engine.finalize_keys_device(offs_t, best, out)
+    engine.finalize_keys_device(codes_t, offs_t, prob.offsets, best, out)
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), as_triples(search_cpu(prob)))
 
@@ -578,5 +578,37 @@ def test_final_cli_rccl_device_batches(tmp_path, shape, n):
     path = tmp_path / "in.txt"
     path.write_text(prob.to_text())
     r = run_final(["--backend=hip", "--transport=rccl", f"--input={path}"], stdin_bytes=b"", np_=1)
+    assert r.returncode == 0, r.stderr.decode()
+    assert r.stdout.decode() == format_results(search_cpu(prob))
+
+
+def _long_problem(L1, lengths, seed):
+    rng = np.random.default_rng(seed)
+    seq1 = rng.integers(1, 27, size=L1, dtype=np.uint8)
+    lengths = np.asarray(lengths, dtype=np.int64)
+    codes = rng.integers(1, 27, size=int(lengths.sum()), dtype=np.uint8)
+    offsets = np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)
+    return Problem([4, 3, 2, 10], seq1, codes, offsets)
+
+
+@pytest.mark.parametrize("L1,lengths", [(20_000, [10_000, 9_000, 150]), (150_000, [40_000])])
+def test_long_context_engine(engine, L1, lengths):
+    # beyond the reference's 3000/2000-letter buffers (myProto.h:3-4): L1 * L2 up to 6e9 (> 2^32: pass-1 keys,
+    # k resolved on the winning diagonal), records of 40 000 letters; both semantics vs the CPU engine
+    prob = _long_problem(L1, lengths, seed=L1)
+    for sem in (Semantics.REFERENCE, Semantics.SPEC):
+        engine.set_problem(prob.weights, prob.seq1, sem)
+        got = as_triples(engine.solve(prob.codes, prob.offsets))
+        assert np.array_equal(got, as_triples(search_cpu(prob, sem))), sem
+
+
+def test_long_context_cli_offsets_three_ranks(tmp_path):
+    # one huge pair (L1 = 150 000, L2 = 40 000: 4.4e9 cells, L1 * L2 > 2^32) split by offsets over 3 ranks
+    # sharing the GPU; pass-1 keys MAX-combined, k resolved on the root
+    prob = _long_problem(150_000, [40_000, 39_000], seed=3)
+    path = tmp_path / "long.txt"
+    path.write_text(prob.to_text())
+    r = run_final(["--backend=hip", "--partition=offsets", "--transport=shm", "--device=0", f"--input={path}"],
+                  stdin_bytes=b"", np_=3, timeout=300)
     assert r.returncode == 0, r.stderr.decode()
     assert r.stdout.decode() == format_results(search_cpu(prob))
