@@ -57,6 +57,12 @@ struct ProblemView {
   int32_t prof16_bytes = 0;
   int32_t max_abs_t = 0;  // max |T| over the table (int16-exactness checks of the packed kernels)
   int32_t mfma_sweep = 0; // 1: long records sweep on the matrix cores (tile_mfma_kernels.hip, MOC_MFMA=1)
+  // Windowed tile16 (Seq1 longer than one LDS image holds): prof16 is the whole profile in device memory
+  // (26 rows of L1 entries + overhang, prof16_entries in all) and every workgroup stages one window of
+  // prof16_window columns of it (its plan's tiles all fall inside that window); prof16_bytes is then the
+  // LDS size of a window's rows + overhang. 0 = the whole profile is the LDS image.
+  int32_t prof16_window = 0;
+  int64_t prof16_entries = 0;
 };
 
 // Entries after the tile16 profile's last row: reads of wave-tile lanes past the valid offsets reach
@@ -72,6 +78,12 @@ constexpr int kProf16MaxLds = 160 * 1024;
 constexpr int kProf16Lut8 = 1024;
 inline int64_t tile16_lds_bytes(int64_t prof16_bytes, int64_t L1) {
   return prof16_bytes + kProf16Lut8 + ((L1 + 16 + 15) & ~int64_t{15});
+}
+// Widest window (columns) whose rows + 512-entry overhang + LUT + Seq1 window fit one CU's LDS.
+inline int64_t tile16_max_window() {
+  int64_t w = (kProf16MaxLds - kProf16Lut8 - 32 - 2 * kProf16Overhang) / (2 * 26 + 1);
+  while (w > 0 && tile16_lds_bytes(((2 * (26 * w + kProf16Overhang)) + 15) & ~int64_t{15}, w) > kProf16MaxLds) --w;
+  return w & ~int64_t{15};
 }
 
 // One batch of records on the device. Offsets are absolute (int64) and rebased by offsets[0], so
@@ -104,6 +116,8 @@ struct Plan {
   int64_t n_long = 0;
   unsigned long long* keys = nullptr;  // device scratch, n_long entries (tile-kernel partial maxima)
   int32_t u = 2;                       // sub-tiles per wave tile (1, 2 or 4)
+  int32_t win_tiles = 0;               // windowed tile16: tiles per window stride (the waves of one
+                                       // workgroup all walk tiles t in [m*win_tiles, (m+1)*win_tiles))
   R2Params r2;                         // finalize: parameters of the R2 result format
 };
 

@@ -135,9 +135,23 @@ class HipEngine {
     std::vector<int32_t> long_recs;
   };
   void plan_chunk(const int64_t* offsets, int64_t n, ChunkPlan& cp) const;
+  struct TilePlan {
+    int u = 2;              // sub-tiles per wave tile
+    int win_tiles = 0;      // windowed tile16: tiles per window stride
+    bool tile16 = false;    // the plan is for the tile16 sweep (else the LUT tile kernel)
+  };
   std::vector<dev::WaveStart> plan_waves(const int64_t* offsets, const int32_t* long_recs, int64_t n_long, int part,
-                                         int parts, int& u_out) const;
-  dev::Plan device_plan(void* d_plan, size_t n_starts, bool has_long_recs, int64_t n_long, int u) const;
+                                         int parts, TilePlan& tp) const;
+  dev::Plan device_plan(void* d_plan, size_t n_starts, bool has_long_recs, int64_t n_long, const TilePlan& tp) const;
+  // problem view for a plan: without the profile when the plan is for the LUT tile kernel
+  dev::ProblemView tile_view(int64_t max_l2, const TilePlan& tp) const {
+    dev::ProblemView pv = problem_view(max_l2);
+    if (!tp.tile16) {
+      pv.prof16 = nullptr;
+      pv.mfma_sweep = 0;
+    }
+    return pv;
+  }
   dev::ProblemView problem_view(int64_t max_l2) const;
   void ensure(void*& ptr, size_t& cap, size_t bytes);
   void ensure_host(void*& ptr, size_t& cap, size_t bytes);
@@ -167,6 +181,9 @@ class HipEngine {
   uint16_t* d_prof16_ = nullptr;  // tile16 profile (null: the problem does not fit it, or MOC_TILE16=0)
   int32_t prof16_bytes_ = 0;
   int32_t prof16_overhang_ = 0;  // zero profile entries past the last row (bounds the tile span)
+  int32_t prof16_window_ = 0;    // > 0: windowed tile16 (columns per workgroup window; Seq1 > one LDS image)
+  int64_t prof16_entries_ = 0;   // entries of the device profile (windowed staging bounds)
+  int32_t prof16_lds_bytes_ = 0; // LDS bytes of the profile part of a workgroup's image
   bool tile16_ = true;            // MOC_TILE16 (A/B switch of the long-record kernel)
   bool mfma_ = false;             // MOC_MFMA: tile16 plans swept on the matrix cores (tile_mfma_kernels.hip)
   int64_t L1_ = 0;

@@ -118,30 +118,54 @@ __device__ __forceinline__ int wave_prefix_sum_dpp(int v) {
 }
 }  // namespace
 
-template <int U>
+// Win (windowed): Seq1 is longer than one LDS image holds. The workgroup's waves all walk tiles of one
+// window m (plan: window-major wave runs, 16-wave aligned, tiles t in [m*T, (m+1)*T) of every record), so it
+// stages only columns [S, S + W) of each profile row (S = m*T*span, W = pv.prof16_window) and the Seq1
+// letters the anchor diagonals read; profile column j lives at LDS column j - S.
+template <int U, bool Win>
 __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv, BatchView bv,
                                                                  const WaveStart* __restrict__ starts, int64_t n_waves,
                                                                  const int32_t* __restrict__ long_recs,
-                                                                 unsigned long long* __restrict__ keys) {
+                                                                 unsigned long long* __restrict__ keys, int win_tiles) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  // LDS image (tile16_lds_bytes): profile | int8 LUT | Seq1 codes (the anchor diagonals' operands)
+  // LDS image (tile16_lds_bytes): profile (or its window) | int8 LUT | Seq1 codes (the anchor diagonals)
   int8_t* lut8 = reinterpret_cast<int8_t*>(smem + pv.prof16_bytes);
   uint8_t* s1l = smem + pv.prof16_bytes + kProf16Lut8;
-  {
+  constexpr int kSpan = kSub * U;
+  const int64_t w0 = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock16;  // the workgroup's first wave: real
+  const int t_base = Win ? (starts[w0].t / win_tiles) * win_tiles : 0;     // first tile of the window
+  const int S = t_base * kSpan;                                             // first column of the window
+  const int W = Win ? pv.prof16_window : pv.L1;                             // columns per LDS row
+  if (Win) {
+    // rows' window columns; entries past the global profile read as 0, then the overhang (zeros)
+    uint16_t* dst = reinterpret_cast<uint16_t*>(smem);
+    const int rows_entries = (kAlphabet - 1) * W;
+    const int n_entries = pv.prof16_bytes >> 1;
+    for (int e = threadIdx.x; e < n_entries; e += blockDim.x) {
+      uint16_t v = 0;
+      if (e < rows_entries) {
+        const int c = e / W, x = e - c * W;
+        const int64_t g = static_cast<int64_t>(c) * pv.L1 + S + x;
+        if (g < pv.prof16_entries) v = pv.prof16[g];
+      }
+      dst[e] = v;
+    }
+    for (int t = threadIdx.x; t < W + 16; t += blockDim.x) s1l[t] = S + t < pv.L1 ? pv.seq1[S + t] : 0;
+  } else {
     const uint4* src = reinterpret_cast<const uint4*>(pv.prof16);  // 16-byte padded
     uint4* dst = reinterpret_cast<uint4*>(smem);
     const int n16 = pv.prof16_bytes >> 4;
     for (int t = threadIdx.x; t < n16; t += blockDim.x) dst[t] = src[t];
-    for (int t = threadIdx.x; t < kProf16Lut8; t += blockDim.x) lut8[t] = static_cast<int8_t>(pv.lut[t]);  // |T| <= 127
     stage_bytes(s1l, pv.seq1, pv.L1 + 16);  // Seq1 + zero pad (device copy has kSeq1Pad zeros)
   }
+  for (int t = threadIdx.x; t < kProf16Lut8; t += blockDim.x) lut8[t] = static_cast<int8_t>(pv.lut[t]);  // |T| <= 127
   __syncthreads();
-  const int64_t w = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock16 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t w = w0 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (w >= n_waves) return;  // wave-uniform; no barrier follows
   const int L1 = pv.L1;
-  const int rowb = 2 * L1;  // bytes per profile row
+  const int rowb = 2 * W;  // bytes per LDS profile row
   const int lane = threadIdx.x & 63;
-  constexpr int kSpan = kSub * U;
+  const int t_win_end = Win ? t_base + win_tiles : INT32_MAX;
 
   const WaveStart ws = starts[w], we = starts[w + 1];
   int li = __builtin_amdgcn_readfirstlane(ws.li), t = __builtin_amdgcn_readfirstlane(ws.t);
@@ -152,7 +176,7 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
     const int L2 = __builtin_amdgcn_readfirstlane(static_cast<int>(bv.offsets[r + 1] - bv.offsets[r]));
     const int steps = L2 <= L1 ? L2 : 0;
     const int need = L2 <= L1 ? L1 - L2 + 1 : 1;
-    const int ntiles = (need + kSpan - 1) / kSpan;
+    const int ntiles = min((need + kSpan - 1) / kSpan, t_win_end);
     const int t_stop = li == end_li ? min(end_t, ntiles) : ntiles;
     // lane j of a chunk holds step i0 + j's letter (0 past the record) and its profile row/step offset
     auto letter = [&](int i) { return i < steps ? static_cast<int>(rec[i]) : 0; };
@@ -163,7 +187,7 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
       const int o0 = t * kSpan;
       MOC_DCHECK(o0 >= 0 && o0 <= L1);
       // sub-tile u: lane owns offsets o0 + 128u + 2*lane (low half) and + 1 (high half)
-      const unsigned char* lbase = smem + 2 * o0 + 4 * lane;
+      const unsigned char* lbase = smem + 2 * (o0 - S) + 4 * lane;
       uint32_t acc[U], best[U];
       int DcA[U], DcB[U], mxA[U], mxB[U];
 #pragma unroll
@@ -203,7 +227,7 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
       const int oA = min(o0 + kSpan, need);
       int anchor = 0;
       auto anchor_add = [&](int c, int i) {
-        if (c != 0) anchor += lut8[c * kLutStride + s1l[oA + i]];
+        if (c != 0) anchor += lut8[c * kLutStride + s1l[oA - S + i]];
       };
       int c = c_first;
       int i0 = 0;
@@ -277,7 +301,7 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
     const unsigned long long k = wave_max_u64(acc64);
     if (lane == 0 && k != 0ull) atomicMax(keys + li, k);
     ++li;
-    t = 0;
+    t = t_base;
   }
 }
 
@@ -287,7 +311,7 @@ int tile16_waves_per_cu(int lds_bytes) {
 }
 
 namespace {
-template <int U>
+template <int U, bool Win>
 void launch16_t(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream) {
   // dynamic LDS above 64 KiB is declared per kernel and device (engines may live on several devices
   // and threads of one process)
@@ -298,36 +322,46 @@ void launch16_t(const ProblemView& pv, const BatchView& bv, const Plan& plan, hi
   {
     std::lock_guard<std::mutex> lock(mu);
     if (declared.insert(dev).second)
-      MOC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&tile16_search_kernel<U>),
+      MOC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&tile16_search_kernel<U, Win>),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, kProf16MaxLds));
   }
   const int64_t blocks = (plan.n_waves + kWavesPerBlock16 - 1) / kWavesPerBlock16;
-  hipLaunchKernelGGL((tile16_search_kernel<U>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock16),
-                     static_cast<size_t>(tile16_lds_bytes(pv.prof16_bytes, pv.L1)), stream, pv, bv, plan.starts, plan.n_waves, plan.long_recs,
-                     plan.keys);
+  const int64_t s1_len = Win ? pv.prof16_window : pv.L1;
+  hipLaunchKernelGGL((tile16_search_kernel<U, Win>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock16),
+                     static_cast<size_t>(tile16_lds_bytes(pv.prof16_bytes, s1_len)), stream, pv, bv, plan.starts,
+                     plan.n_waves, plan.long_recs, plan.keys, plan.win_tiles);
 }
 }  // namespace
 
 void preload_tile16_kernels() {
   hipFuncAttributes fa;
-  (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&tile16_search_kernel<2>));
+  (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&tile16_search_kernel<2, false>));
 }
 
 void launch_tile16_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream,
                         bool mfma_sweep) {
-  if (!pv.prof16 || pv.prof16_bytes <= 0 || tile16_lds_bytes(pv.prof16_bytes, pv.L1) > kProf16MaxLds ||
-      (pv.prof16_bytes & 15))
+  const int64_t s1_len = pv.prof16_window > 0 ? pv.prof16_window : pv.L1;
+  if (!pv.prof16 || pv.prof16_bytes <= 0 || tile16_lds_bytes(pv.prof16_bytes, s1_len) > kProf16MaxLds ||
+      (pv.prof16_bytes & 15) || (pv.prof16_window > 0 && (plan.win_tiles <= 0 || mfma_sweep || plan.u > 4)))
     throw Error("launch_tile16_keys: no usable profile");
   if (plan.n_long > 0) MOC_HIP_CHECK(hipMemsetAsync(plan.keys, 0, sizeof(unsigned long long) * plan.n_long, stream));
   if (plan.n_waves <= 0) return;
   if (mfma_sweep) {
     launch_tile_mfma_sweep(pv, bv, plan, stream);
   } else {
-    switch (plan.u) {
-      case 1: launch16_t<1>(pv, bv, plan, stream); break;
-      case 2: launch16_t<2>(pv, bv, plan, stream); break;
-      case 8: launch16_t<8>(pv, bv, plan, stream); break;
-      default: launch16_t<4>(pv, bv, plan, stream); break;
+    if (pv.prof16_window > 0) {
+      switch (plan.u) {
+        case 1: launch16_t<1, true>(pv, bv, plan, stream); break;
+        case 2: launch16_t<2, true>(pv, bv, plan, stream); break;
+        default: launch16_t<4, true>(pv, bv, plan, stream); break;
+      }
+    } else {
+      switch (plan.u) {
+        case 1: launch16_t<1, false>(pv, bv, plan, stream); break;
+        case 2: launch16_t<2, false>(pv, bv, plan, stream); break;
+        case 8: launch16_t<8, false>(pv, bv, plan, stream); break;
+        default: launch16_t<4, false>(pv, bv, plan, stream); break;
+      }
     }
   }
 }

@@ -192,9 +192,19 @@ void HipEngine::set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, S
   auto prof_bytes = [&](int64_t oh) { return ((2 * ((kAlphabet - 1) * L1 + oh)) + 15) & ~int64_t{15}; };
   int64_t overhang = 2 * dev::kProf16Overhang;
   if (dev::tile16_lds_bytes(prof_bytes(overhang), L1) > dev::kProf16MaxLds) overhang = dev::kProf16Overhang;
-  const int64_t pbytes = prof_bytes(overhang);
-  const bool t16 = tile16_ && L1 > 0 && dev::tile16_lds_bytes(pbytes, L1) <= dev::kProf16MaxLds &&
-                   build_profile16(table_, seq1, L1, overhang, prof);
+  int64_t pbytes = prof_bytes(overhang);
+  // Seq1 too long for one LDS image: the whole profile lives in device memory and each workgroup stages
+  // a window of it (tile16_search_kernel<U, true>); records must then fit a window with two tiles' slack
+  const bool whole = dev::tile16_lds_bytes(pbytes, L1) <= dev::kProf16MaxLds;
+  const int64_t window = whole ? 0 : dev::tile16_max_window();
+  const bool t16 = tile16_ && L1 > 0 && build_profile16(table_, seq1, L1, overhang, prof);
+  prof16_window_ = t16 ? static_cast<int32_t>(window) : 0;
+  prof16_entries_ = t16 ? static_cast<int64_t>(prof.entries.size()) : 0;
+  prof16_lds_bytes_ = t16 ? static_cast<int32_t>(whole ? pbytes
+                                                       : ((2 * ((kAlphabet - 1) * window + dev::kProf16Overhang)) + 15) &
+                                                             ~int64_t{15})
+                          : 0;
+  pbytes = (2 * static_cast<int64_t>(prof.entries.size()) + 15) & ~int64_t{15};
   prof16_overhang_ = t16 ? static_cast<int>(overhang) : 0;
   const size_t total = t16 ? prof_off + static_cast<size_t>(pbytes) : prof_off;
   image_.assign(total, 0);
@@ -214,7 +224,7 @@ void HipEngine::set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, S
   d_lut_ = reinterpret_cast<int32_t*>(base);
   d_seq1_ = reinterpret_cast<uint8_t*>(base + s1_off);
   d_prof16_ = t16 ? reinterpret_cast<uint16_t*>(base + prof_off) : nullptr;
-  prof16_bytes_ = t16 ? static_cast<int32_t>(pbytes) : 0;
+  prof16_bytes_ = prof16_lds_bytes_;
   have_problem_ = true;
 }
 
@@ -234,8 +244,10 @@ dev::ProblemView HipEngine::problem_view(int64_t max_l2) const {
   pv.r2 = r2_;
   pv.prof16 = d_prof16_;
   pv.prof16_bytes = prof16_bytes_;
+  pv.prof16_window = prof16_window_;
+  pv.prof16_entries = prof16_entries_;
   pv.max_abs_t = table_.max_abs();
-  pv.mfma_sweep = mfma_ && d_prof16_ ? 1 : 0;
+  pv.mfma_sweep = mfma_ && d_prof16_ && !prof16_window_ ? 1 : 0;
   return pv;
 }
 
@@ -313,11 +325,12 @@ constexpr int64_t kTileOverheadSteps = 24;
 // Device view of an uploaded plan buffer (starts | long_recs | keys). Identity record lists upload no
 // long_recs (PlanLayout built with n_long = 0): their keys follow the starts.
 dev::Plan HipEngine::device_plan(void* d_plan, size_t n_starts, bool has_long_recs, int64_t n_long,
-                                 int u) const {
+                                 const TilePlan& tp) const {
   const PlanLayout lay(n_starts, has_long_recs ? static_cast<size_t>(n_long) : 0);
   char* base = static_cast<char*>(d_plan);
   dev::Plan plan;
-  plan.u = u;
+  plan.u = tp.u;
+  plan.win_tiles = tp.win_tiles;
   plan.n_waves = static_cast<int64_t>(n_starts) - 1;
   plan.starts = reinterpret_cast<const dev::WaveStart*>(base + lay.starts_off);
   plan.long_recs = has_long_recs ? reinterpret_cast<const int32_t*>(base + lay.long_off) : nullptr;
@@ -330,50 +343,111 @@ dev::Plan HipEngine::device_plan(void* d_plan, size_t n_starts, bool has_long_re
 // Cost-balanced contiguous wave runs over the record-major tile list of the long records (record li =
 // offsets-relative index long_recs[li], or li when long_recs is null), restricted to part `part` of
 // `parts` of the total cost (context-parallel shares). Returns n_waves + 1 starts (empty: no work).
+// tp: sub-tiles per wave tile, and which sweep the plan is for (tile16 when the problem has a profile and,
+// for a windowed one, the records fit a window — else the LUT tile kernel).
+// Windowed tile16 (Seq1 longer than one LDS image): the list is window-major — window m holds the tiles
+// t in [m*T, (m+1)*T) of every record, T = (W - span - max L2) / span so that their profile columns
+// [t*span, t*span + span + L2) all lie in [m*T*span, m*T*span + W) — and every window gets whole
+// workgroups of waves (16-aligned; its last wave is an empty marker ending at (n_long, m*T)), each
+// workgroup staging its window once.
 std::vector<dev::WaveStart> HipEngine::plan_waves(const int64_t* offsets, const int32_t* long_recs, int64_t n_long,
-                                                  int part, int parts, int& u_out) const {
+                                                  int part, int parts, TilePlan& tp) const {
   std::vector<dev::WaveStart> starts;
+  tp = TilePlan{};
   if (n_long <= 0) return starts;
-  int64_t sum_l2 = 0;
+  int64_t sum_l2 = 0, max_l2 = 0;
   for (int64_t li = 0; li < n_long; ++li) {
     const int64_t r = long_recs ? long_recs[li] : li;
-    sum_l2 += offsets[r + 1] - offsets[r];
+    const int64_t L2 = offsets[r + 1] - offsets[r];
+    sum_l2 += L2;
+    max_l2 = std::max(max_l2, L2 <= L1_ ? L2 : 0);
   }
+  const int64_t W = prof16_window_;
+  tp.tile16 = d_prof16_ != nullptr && (W == 0 || max_l2 + 2 * 128 <= W);
   // sub-tiles per wave tile: 4 amortises the per-tile setup over short records, 2 keeps more waves busy
-  // on long ones (measured: profiles/tile_variants.log)
-  // (measured, both kernels: profiles/tile_variants.log, profiles/tile16_variants.log)
+  // on long ones (measured, both kernels: profiles/tile_variants.log, profiles/tile16_variants.log)
   int u = tile_u_ > 0 ? tile_u_ : (sum_l2 < 96 * n_long ? 4 : 2);
-  if (tile_u_ <= 0 && u == 4 && d_prof16_ && 128 * 8 <= prof16_overhang_) u = 8;  // tile16: wider tiles for short records
-  if (u > 4 && !(d_prof16_ && 128 * u <= prof16_overhang_)) u = 4;                 // the overhang bounds the span
-  if (u > 2 && mfma_) u = 2;  // the matrix-core sweep's register budget (U = 4 spills)
-  u_out = u;
-  std::vector<int64_t> pre(static_cast<size_t>(n_long) + 1, 0), tcost(static_cast<size_t>(n_long));
+  if (tile_u_ <= 0 && u == 4 && tp.tile16 && W == 0 && 128 * 8 <= prof16_overhang_) u = 8;  // tile16: wider tiles
+  if (u > 4 && !(tp.tile16 && W == 0 && 128 * u <= prof16_overhang_)) u = 4;  // the overhang bounds the span
+  if (u > 2 && mfma_ && tp.tile16 && W == 0) u = 2;  // the matrix-core sweep's register budget (U = 4 spills)
+  if (tp.tile16 && W > 0)
+    while (u > 1 && max_l2 + 2 * 128 * u > W) u /= 2;  // a window holds at least two tiles' columns
+  tp.u = u;
+  const int span = dev::tile_span(tp.tile16, u);
+  std::vector<int64_t> tcost(static_cast<size_t>(n_long));
   std::vector<int32_t> ntiles(static_cast<size_t>(n_long));
   int64_t total_tiles = 0;
   for (int64_t li = 0; li < n_long; ++li) {
     const int64_t r = long_recs ? long_recs[li] : li;
     const int64_t L2 = offsets[r + 1] - offsets[r];
-    const int64_t nt = dev::tiles_of(dev::lanes_needed(L1_, L2), dev::tile_span(d_prof16_ != nullptr, u));
-    ntiles[li] = static_cast<int32_t>(nt);
+    ntiles[li] = static_cast<int32_t>(dev::tiles_of(dev::lanes_needed(L1_, L2), span));
     tcost[li] = (L2 <= L1_ ? L2 : 0) + kTileOverheadSteps;
-    pre[li + 1] = pre[li] + nt * tcost[li];
-    total_tiles += nt;
+    total_tiles += ntiles[li];
   }
-  const int64_t C = pre[n_long];
+  const int s1_len = tp.tile16 && W > 0 ? static_cast<int>(W) : static_cast<int>(L1_);
+  const int waves_per_cu = tp.tile16 ? dev::tile16_waves_per_cu(static_cast<int>(dev::tile16_lds_bytes(prof16_bytes_, s1_len)))
+                                     : tile_waves_per_cu_;
+  if (!(tp.tile16 && W > 0)) {
+    std::vector<int64_t> pre(static_cast<size_t>(n_long) + 1, 0);
+    for (int64_t li = 0; li < n_long; ++li) pre[li + 1] = pre[li] + ntiles[li] * tcost[li];
+    const int64_t C = pre[n_long];
+    const int64_t lo = C * part / parts, hi = C * (part + 1) / parts;
+    // position of cost threshold X in (li, t): first tile whose start cost is >= X
+    auto locate = [&](int64_t X) {
+      if (X >= C) return dev::WaveStart{static_cast<int32_t>(n_long), 0};
+      const int64_t li = std::upper_bound(pre.begin(), pre.end(), X) - pre.begin() - 1;
+      const int64_t t = (X - pre[li] + tcost[li] - 1) / tcost[li];
+      if (t >= ntiles[li]) return dev::WaveStart{static_cast<int32_t>(li + 1), 0};
+      return dev::WaveStart{static_cast<int32_t>(li), static_cast<int32_t>(t)};
+    };
+    const int64_t part_tiles = std::max<int64_t>(1, total_tiles * (hi - lo) / std::max<int64_t>(C, 1));
+    const int64_t n_waves = std::min<int64_t>(part_tiles, static_cast<int64_t>(num_cus_) * waves_per_cu);
+    starts.resize(static_cast<size_t>(n_waves) + 1);
+    for (int64_t w = 0; w <= n_waves; ++w) starts[w] = locate(lo + (hi - lo) * w / n_waves);
+    return starts;
+  }
+  // ---- windowed tile16: window-major runs, whole workgroups per window
+  const int64_t T = std::max<int64_t>(1, (W - span - max_l2) / span);
+  tp.win_tiles = static_cast<int32_t>(T);
+  int32_t max_nt = 0;
+  for (int64_t li = 0; li < n_long; ++li) max_nt = std::max(max_nt, ntiles[li]);
+  const int64_t M = (max_nt + T - 1) / T;
+  auto count = [&](int64_t li, int64_t m) { return std::clamp<int64_t>(ntiles[li] - m * T, 0, T); };
+  std::vector<int64_t> wcost(static_cast<size_t>(M), 0);
+  for (int64_t li = 0; li < n_long; ++li)
+    for (int64_t m = 0; m * T < ntiles[li]; ++m) wcost[m] += count(li, m) * tcost[li];
+  std::vector<int64_t> wstart(static_cast<size_t>(M) + 1, 0);
+  for (int64_t m = 0; m < M; ++m) wstart[m + 1] = wstart[m] + wcost[m];
+  const int64_t C = wstart[M];
   const int64_t lo = C * part / parts, hi = C * (part + 1) / parts;
-  // position of cost threshold X in (li, t): first tile whose start cost is >= X
-  auto locate = [&](int64_t X) {
-    if (X >= C) return dev::WaveStart{static_cast<int32_t>(n_long), 0};
-    const int64_t li = std::upper_bound(pre.begin(), pre.end(), X) - pre.begin() - 1;
-    const int64_t t = (X - pre[li] + tcost[li] - 1) / tcost[li];
-    if (t >= ntiles[li]) return dev::WaveStart{static_cast<int32_t>(li + 1), 0};
-    return dev::WaveStart{static_cast<int32_t>(li), static_cast<int32_t>(t)};
-  };
-  const int64_t part_tiles = std::max<int64_t>(1, total_tiles * (hi - lo) / std::max<int64_t>(C, 1));
-  const int waves_per_cu = d_prof16_ ? dev::tile16_waves_per_cu(static_cast<int>(dev::tile16_lds_bytes(prof16_bytes_, L1_))) : tile_waves_per_cu_;
-  const int64_t n_waves = std::min<int64_t>(part_tiles, static_cast<int64_t>(num_cus_) * waves_per_cu);
-  starts.resize(static_cast<size_t>(n_waves) + 1);
-  for (int64_t w = 0; w <= n_waves; ++w) starts[w] = locate(lo + (hi - lo) * w / n_waves);
+  constexpr int kWg = 16;  // waves per tile16 workgroup
+  const int64_t target_wgs = std::max<int64_t>(1, static_cast<int64_t>(num_cus_) * waves_per_cu / kWg);
+  std::vector<int64_t> pre(static_cast<size_t>(n_long) + 1);
+  for (int64_t m = 0; m < M; ++m) {
+    const int64_t a = std::max(lo, wstart[m]) - wstart[m], b = std::min(hi, wstart[m + 1]) - wstart[m];
+    if (b <= a) continue;
+    pre[0] = 0;
+    for (int64_t li = 0; li < n_long; ++li) pre[li + 1] = pre[li] + count(li, m) * tcost[li];
+    const dev::WaveStart end_marker{static_cast<int32_t>(n_long), static_cast<int32_t>(m * T)};
+    auto locate = [&](int64_t X) {
+      if (X >= pre[n_long]) return end_marker;
+      const int64_t li = std::upper_bound(pre.begin(), pre.end(), X) - pre.begin() - 1;
+      const int64_t t = (X - pre[li] + tcost[li] - 1) / tcost[li];
+      if (t >= count(li, m)) return dev::WaveStart{static_cast<int32_t>(li + 1), static_cast<int32_t>(m * T)};
+      return dev::WaveStart{static_cast<int32_t>(li), static_cast<int32_t>(m * T + t)};
+    };
+    const int64_t share_tiles = std::max<int64_t>(1, (b - a) / std::max<int64_t>(1, C / std::max<int64_t>(total_tiles, 1)));
+    const int64_t wgs = std::clamp<int64_t>((target_wgs * (b - a) + (hi - lo) - 1) / std::max<int64_t>(hi - lo, 1), 1,
+                                            (share_tiles + kWg - 2) / (kWg - 1));
+    const int64_t real = wgs * kWg - 1;  // + one empty marker wave that ends the window's list
+    for (int64_t q = 0; q < real; ++q) starts.push_back(locate(a + (b - a) * q / real));
+    starts.push_back(locate(b));  // the last real wave ends at the share's end ...
+    starts.back() = b >= pre[n_long] ? end_marker : starts.back();
+    // ... and the marker wave [end, next window's first start) is empty: its start is the end of this window
+  }
+  if (starts.empty()) return starts;
+  // every window contributed wgs*16 entries: the real waves' starts + its end; the final entry ends the list
+  starts.push_back(starts.back());
   return starts;
 }
 
@@ -733,8 +807,8 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
     const bool all_tiles = cp.n_short > 0 && !short_ok;
     const int32_t* lrecs = all_tiles ? nullptr : cp.long_recs.data();
     const int64_t n_long = all_tiles ? cn : static_cast<int64_t>(cp.long_recs.size());
-    int tile_u = 0;
-    const std::vector<dev::WaveStart> starts = plan_waves(offsets + rb, lrecs, n_long, 0, 1, tile_u);
+    TilePlan tp;
+    const std::vector<dev::WaveStart> starts = plan_waves(offsets + rb, lrecs, n_long, 0, 1, tp);
     const PlanLayout lay(starts.size(), lrecs ? static_cast<size_t>(n_long) : 0);
     const size_t keys_extra = lrecs ? 0 : sizeof(unsigned long long) * static_cast<size_t>(n_long);
     const size_t cbytes = static_cast<size_t>(offsets[re] - offsets[rb]);
@@ -791,10 +865,15 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
       stats_.kernels |= swipe ? 1 : 2;
     }
     if (!starts.empty()) {
-      dev::Plan plan = device_plan(s.d_plan, starts.size(), lrecs != nullptr, n_long, tile_u);
+      dev::Plan plan = device_plan(s.d_plan, starts.size(), lrecs != nullptr, n_long, tp);
       dev::BatchView bv{dcodes, doffs, cn};
-      dev::launch_tiles(pv, bv, plan, s.d_out, static_cast<int>(fmt), s_compute_);
-      stats_.kernels |= d_prof16_ ? 8 : 4;
+      dev::ProblemView tpv = pv;
+      if (!tp.tile16) {
+        tpv.prof16 = nullptr;
+        tpv.mfma_sweep = 0;
+      }
+      dev::launch_tiles(tpv, bv, plan, s.d_out, static_cast<int>(fmt), s_compute_);
+      stats_.kernels |= tp.tile16 ? 8 : 4;
     }
     MOC_HIP_CHECK(hipGetLastError());
     MOC_HIP_CHECK(hipEventRecord(s.ev_k1, s_compute_));
@@ -828,8 +907,8 @@ void HipEngine::solve_device(const uint8_t* d_codes, const int64_t* d_offsets, c
   const bool all_tiles = cp.n_short > 0 && !short_ok;  // everything through the tile kernel
   const int32_t* lrecs = all_tiles ? nullptr : cp.long_recs.data();
   const int64_t n_long = all_tiles ? n : static_cast<int64_t>(cp.long_recs.size());
-  int tile_u = 0;
-  const std::vector<dev::WaveStart> starts = plan_waves(h_offsets, lrecs, n_long, 0, 1, tile_u);
+  TilePlan tp;
+  const std::vector<dev::WaveStart> starts = plan_waves(h_offsets, lrecs, n_long, 0, 1, tp);
   const PlanLayout lay(starts.size(), lrecs ? static_cast<size_t>(n_long) : 0);
   const size_t keys_extra = lrecs ? 0 : sizeof(unsigned long long) * static_cast<size_t>(n_long);
   MOC_HIP_CHECK(hipEventSynchronize(ev_plan_));  // previous call's plan buffers are free again
@@ -854,16 +933,16 @@ void HipEngine::solve_device(const uint8_t* d_codes, const int64_t* d_offsets, c
       dev::launch_short(pv, a, num_cus_, stream);
   }
   if (!starts.empty()) {
-    dev::Plan plan = device_plan(d_plan_, starts.size(), lrecs != nullptr, n_long, tile_u);
+    dev::Plan plan = device_plan(d_plan_, starts.size(), lrecs != nullptr, n_long, tp);
     dev::BatchView bv{d_codes + h_offsets[0], d_offsets, n};
-    dev::launch_tiles(pv, bv, plan, d_out, static_cast<int>(ResultFormat::R12), stream);
+    dev::launch_tiles(tile_view(cp.max_l2, tp), bv, plan, d_out, static_cast<int>(ResultFormat::R12), stream);
   }
   MOC_HIP_CHECK(hipGetLastError());
   MOC_HIP_CHECK(hipEventRecord(ev_plan_, stream));
   stats_ = EngineStats{};
   stats_.cells = cp.cells;
   stats_.records = n;
-  stats_.kernels = (short_ok ? (swipe ? 1 : 2) : 0) | (starts.empty() ? 0 : (d_prof16_ ? 8 : 4));
+  stats_.kernels = (short_ok ? (swipe ? 1 : 2) : 0) | (starts.empty() ? 0 : (tp.tile16 ? 8 : 4));
 }
 
 }  // namespace moc
@@ -882,8 +961,8 @@ void HipEngine::search_keys_device(const uint8_t* d_codes, const int64_t* d_offs
   for (int64_t i = 0; i < n; ++i) max_l2 = std::max(max_l2, h_offsets[i + 1] - h_offsets[i]);
   if (max_l2 >= (int64_t{1} << 30)) throw Error("Seq2 lengths beyond 2^30 exceed the device engine's offset range");
   // the record-major tile list of all records; this part takes a contiguous, cost-balanced share of it
-  int tile_u = 0;
-  const std::vector<dev::WaveStart> starts = plan_waves(h_offsets, nullptr, n, part, parts, tile_u);
+  TilePlan tp;
+  const std::vector<dev::WaveStart> starts = plan_waves(h_offsets, nullptr, n, part, parts, tp);
   MOC_HIP_CHECK(hipEventSynchronize(ev_plan_));  // previous call's plan buffers are free again
   const size_t bytes = std::max<size_t>(starts.size() * sizeof(dev::WaveStart), 8);
   ensure(d_plan_, d_plan_cap_, bytes);
@@ -894,19 +973,20 @@ void HipEngine::search_keys_device(const uint8_t* d_codes, const int64_t* d_offs
                                  stream));
   }
   dev::Plan plan;
-  plan.u = tile_u;
+  plan.u = tp.u;
+  plan.win_tiles = tp.win_tiles;
   plan.n_waves = starts.empty() ? 0 : static_cast<int64_t>(starts.size()) - 1;
   plan.starts = static_cast<const dev::WaveStart*>(d_plan_);
   plan.long_recs = nullptr;
   plan.n_long = n;
   plan.keys = d_keys;
   dev::BatchView bv{d_codes + h_offsets[0], d_offsets, n};
-  dev::launch_tile_keys(problem_view(max_l2), bv, plan, stream);
+  dev::launch_tile_keys(tile_view(max_l2, tp), bv, plan, stream);
   MOC_HIP_CHECK(hipGetLastError());
   MOC_HIP_CHECK(hipEventRecord(ev_plan_, stream));
   stats_ = EngineStats{};
   stats_.records = n;
-  stats_.kernels = plan.n_waves ? (d_prof16_ ? 8 : 4) : 0;
+  stats_.kernels = plan.n_waves ? (tp.tile16 ? 8 : 4) : 0;
 }
 
 void HipEngine::finalize_keys_device(const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets,

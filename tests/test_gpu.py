@@ -612,3 +612,25 @@ def test_long_context_cli_offsets_three_ranks(tmp_path):
                   stdin_bytes=b"", np_=3, timeout=300)
     assert r.returncode == 0, r.stderr.decode()
     assert r.stdout.decode() == format_results(search_cpu(prob))
+
+
+@pytest.mark.parametrize("L1,shape,n", [(20_000, "input3", 40), (5_000, "input4", 300), (3_100, "input3", 12),
+                                        (60_000, "input1", 100)])
+def test_tile16_windowed(engine, L1, shape, n):
+    # Seq1 longer than one LDS image (3052 letters): the windowed tile16 sweep (each workgroup stages a
+    # window of the profile; window-major plan) == the CPU engine, both semantics; and context-parallel
+    # shares of it MAX-combine to the same answers
+    from mpi_openmp_cuda_amd import decode_keys
+
+    base = make_synthetic(shape, n, seed=L1 + n)
+    rng = np.random.default_rng(L1)
+    prob = Problem(base.weights, rng.integers(1, 27, size=L1, dtype=np.uint8), base.codes, base.offsets)
+    for sem in (Semantics.REFERENCE, Semantics.SPEC):
+        engine.set_problem(prob.weights, prob.seq1, sem)
+        ref = as_triples(search_cpu(prob, sem))
+        assert np.array_equal(as_triples(engine.solve(prob.codes, prob.offsets)), ref), sem
+        assert "tile16" in engine.stats()["kernels"], engine.stats()
+        keys = np.zeros(prob.n, np.uint64)
+        for part in range(3):
+            keys = np.maximum(keys, engine.search_keys(prob.codes, prob.offsets, part, 3))
+        assert np.array_equal(as_triples(decode_keys(keys, prob)), ref), sem

@@ -27,11 +27,14 @@ from mpi_openmp_cuda_amd.ops.align import as_triples  # noqa: E402
 
 # shape -> (records, Seq1 override length or None)
 CASES = {"input6": (1 << 24, None), "input1": (1 << 21, None), "input4": (1 << 17, None),
-         "input3": (1 << 15, None), "limits": (1 << 12, None)}
+         "input3": (1 << 15, None), "limits": (1 << 12, None),
+         # long context: Seq1 beyond one LDS image -> the windowed tile16 sweep
+         "long20k": (1 << 12, 20_000), "long150k": (1 << 9, 150_000)}
+BASE = {"long20k": "input3", "long150k": "input3"}  # record-length distribution of the long-context shapes
 
 
 def make(shape, n):
-    prob = make_synthetic(shape, n, seed=7)
+    prob = make_synthetic(BASE.get(shape, shape), n, seed=7)
     L1 = CASES[shape][1]
     if L1:
         rng = np.random.default_rng(L1)
