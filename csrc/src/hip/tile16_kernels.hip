@@ -141,14 +141,26 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
     uint16_t* dst = reinterpret_cast<uint16_t*>(smem);
     const int rows_entries = (kAlphabet - 1) * W;
     const int n_entries = pv.prof16_bytes >> 1;
-    for (int e = threadIdx.x; e < n_entries; e += blockDim.x) {
-      uint16_t v = 0;
-      if (e < rows_entries) {
-        const int c = e / W, x = e - c * W;
+    if ((pv.L1 & 7) == 0) {  // rows 16-byte aligned (W and S are multiples of 16): 8 entries per load
+      const int w8 = W >> 3;
+      for (int e = threadIdx.x; e < (kAlphabet - 1) * w8; e += blockDim.x) {
+        const int c = e / w8, x = (e - c * w8) << 3;
         const int64_t g = static_cast<int64_t>(c) * pv.L1 + S + x;
-        if (g < pv.prof16_entries) v = pv.prof16[g];
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (g + 8 <= pv.prof16_entries) v = *reinterpret_cast<const uint4*>(pv.prof16 + g);
+        *reinterpret_cast<uint4*>(dst + c * W + x) = v;
       }
-      dst[e] = v;
+      for (int e = rows_entries + threadIdx.x; e < n_entries; e += blockDim.x) dst[e] = 0;
+    } else {
+      for (int e = threadIdx.x; e < n_entries; e += blockDim.x) {
+        uint16_t v = 0;
+        if (e < rows_entries) {
+          const int c = e / W, x = e - c * W;
+          const int64_t g = static_cast<int64_t>(c) * pv.L1 + S + x;
+          if (g < pv.prof16_entries) v = pv.prof16[g];
+        }
+        dst[e] = v;
+      }
     }
     for (int t = threadIdx.x; t < W + 16; t += blockDim.x) s1l[t] = S + t < pv.L1 ? pv.seq1[S + t] : 0;
   } else {

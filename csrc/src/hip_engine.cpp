@@ -370,8 +370,12 @@ std::vector<dev::WaveStart> HipEngine::plan_waves(const int64_t* offsets, const 
   if (tile_u_ <= 0 && u == 4 && tp.tile16 && W == 0 && 128 * 8 <= prof16_overhang_) u = 8;  // tile16: wider tiles
   if (u > 4 && !(tp.tile16 && W == 0 && 128 * u <= prof16_overhang_)) u = 4;  // the overhang bounds the span
   if (u > 2 && mfma_ && tp.tile16 && W == 0) u = 2;  // the matrix-core sweep's register budget (U = 4 spills)
-  if (tp.tile16 && W > 0)
-    while (u > 1 && max_l2 + 2 * 128 * u > W) u /= 2;  // a window holds at least two tiles' columns
+  if (tp.tile16 && W > 0) {
+    // windowed: the widest tiles a window holds twice (L1 = 20 000, input3 records: U = 4 -> 9.3 T cells/s,
+    // U = 2 -> 8.4, U = 1 -> 7.0; profiles/kernel_bench_long.log)
+    if (tile_u_ <= 0) u = 4;
+    while (u > 1 && max_l2 + 2 * 128 * u > W) u /= 2;
+  }
   tp.u = u;
   const int span = dev::tile_span(tp.tile16, u);
   std::vector<int64_t> tcost(static_cast<size_t>(n_long));
