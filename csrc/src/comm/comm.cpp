@@ -4,8 +4,10 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <thread>
 
 #include "moc/runtime/log.hpp"
 
@@ -52,6 +54,9 @@ MpiContext::~MpiContext() {
 void MpiContext::abort(int code, const std::string& msg) const {
   std::fprintf(stderr, "[moc rank %d] fatal: %s\n", rank, msg.c_str());
   std::fflush(stderr);
+  // the launcher forwards stderr through its proxy, which the abort tears down: give it a moment to
+  // forward the message first (under load the line was sometimes lost)
+  std::this_thread::sleep_for(std::chrono::milliseconds(100));
   MPI_Abort(MPI_COMM_WORLD, code);
   std::_Exit(code);
 }

@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <memory>
 
 #include "moc/runtime/releaser.hpp"
 
@@ -837,9 +838,21 @@ constexpr char kDigitPairs[201] =
     "40414243444546474849505152535455565758596061626364656667686970717273747576777879"
     "8081828384858687888990919293949596979899";
 
+// Every writer below may store up to kSlack bytes past the text it emits (fixed-size copies instead of
+// variable-length memcpy calls); each row's next piece overwrites them, and buffers carry kSlack spare.
+constexpr int kSlack = 64;
+
 inline char* put_uint(char* p, uint64_t u) {
-  char tmp[24];
-  char* e = tmp + sizeof tmp;
+  if (u < 10) {
+    *p = static_cast<char>('0' + u);
+    return p + 1;
+  }
+  if (u < 100) {
+    std::memcpy(p, kDigitPairs + 2 * u, 2);
+    return p + 2;
+  }
+  char tmp[48];
+  char* e = tmp + 24;
   char* q = e;
   while (u >= 100) {
     const unsigned d = static_cast<unsigned>(u % 100);
@@ -855,9 +868,8 @@ inline char* put_uint(char* p, uint64_t u) {
   } else {
     *--q = static_cast<char>('0' + u);
   }
-  const size_t n = static_cast<size_t>(e - q);
-  std::memcpy(p, q, n);
-  return p + n;
+  std::memcpy(p, q, 24);  // fixed size: at most 20 digits, the rest is slack
+  return p + (e - q);
 }
 inline char* put_int(char* p, int64_t v) {
   if (v < 0) {
@@ -874,19 +886,19 @@ inline char* put_lit(char* p, const char (&s)[N]) {
 
 // Decimal counter for the row index: digits live right-aligned in buf[0, 20).
 struct RowCounter {
-  char buf[20];
-  int first;  // index of the most significant digit
+  char buf[48];  // [20, 48): padding read by the fixed-size copy in put()
+  int first;     // index of the most significant digit
   explicit RowCounter(int64_t v) {
-    char tmp[24];
+    char tmp[48];
     char* e = put_uint(tmp, static_cast<uint64_t>(v));
     const int n = static_cast<int>(e - tmp);
     first = 20 - n;
+    std::memset(buf, 0, sizeof buf);
     std::memcpy(buf + first, tmp, static_cast<size_t>(n));
   }
   char* put(char* p) const {
-    const size_t n = static_cast<size_t>(20 - first);
-    std::memcpy(p, buf + first, n);
-    return p + n;
+    std::memcpy(p, buf + first, 24);
+    return p + (20 - first);
   }
   void next() {
     int i = 19;
@@ -915,15 +927,50 @@ inline char* format_row(char* p, RowCounter& idx, const Result& r) {
 // '#' + 19 index digits + ": score: " + 11 + ", n: " + 11 + ", k: " + 11 + '\n'
 constexpr int kMaxRow = 1 + 19 + 9 + 11 + 5 + 11 + 5 + 11 + 1;
 
+// R2 results take at most 65 536 distinct values, so a large R2 run prints from a table of every code's
+// row tail ": score: S, n: N, k: K\n" (one 48-byte slot each, built in parallel once per parameter set):
+// a row is then '#', the index counter and one fixed-size copy (no decode divisions, no digit loops).
+struct R2Tails {
+  static constexpr int kSlot = 48;  // longest tail: 9 + 6 + 5 + 6 + 5 + 6 + 1 = 38 bytes
+  R2Params r2;
+  uvector<char> text;        // 65536 * kSlot
+  std::vector<uint8_t> len;  // tail length per code
+  explicit R2Tails(const R2Params& p) : r2(p), text(size_t{65536} * kSlot), len(65536) {
+#pragma omp parallel for schedule(static)
+    for (int c = 0; c < 65536; ++c) {
+      const uint16_t code = static_cast<uint16_t>(c);
+      const Result x = decode_result(&code, ResultFormat::R2, r2, 0);
+      char tmp[kSlot + kSlack + 64];
+      char* q = put_lit(tmp, ": score: ");
+      q = put_int(q, x.score);
+      q = put_lit(q, ", n: ");
+      q = put_int(q, x.n);
+      q = put_lit(q, ", k: ");
+      q = put_int(q, x.k);
+      *q++ = '\n';
+      std::memcpy(text.data() + size_t{kSlot} * c, tmp, kSlot);
+      len[c] = static_cast<uint8_t>(q - tmp);
+    }
+  }
+};
+
 // Rows of a sequence of result runs (one per rank slice, each in its own wire format), by global row.
 struct RowSource {
   const std::vector<ResultRun>& runs;
   std::vector<int64_t> pre;  // pre[r] = rows before run r
-  explicit RowSource(const std::vector<ResultRun>& r) : runs(r), pre(r.size() + 1, 0) {
-    for (size_t i = 0; i < r.size(); ++i) pre[i + 1] = pre[i] + r[i].n;
+  std::vector<std::shared_ptr<const R2Tails>> tails;  // per run: table path for large R2 runs
+  explicit RowSource(const std::vector<ResultRun>& r) : runs(r), pre(r.size() + 1, 0), tails(r.size()) {
+    for (size_t i = 0; i < r.size(); ++i) {
+      pre[i + 1] = pre[i] + r[i].n;
+      if (r[i].fmt != ResultFormat::R2 || r[i].n < (int64_t{1} << 18) || r[i].r2.j <= 0 || r[i].r2.kw <= 0) continue;
+      for (size_t q = 0; q < i && !tails[i]; ++q)  // ranks of one job usually share the parameters
+        if (tails[q] && tails[q]->r2.smin == r[i].r2.smin && tails[q]->r2.kw == r[i].r2.kw && tails[q]->r2.j == r[i].r2.j)
+          tails[i] = tails[q];
+      if (!tails[i]) tails[i] = std::make_shared<const R2Tails>(r[i].r2);
+    }
   }
   int64_t total() const { return pre.back(); }
-  // formats rows [rb, re) at p
+  // formats rows [rb, re) at p (writes up to kSlack bytes past the returned end)
   char* format(char* p, int64_t rb, int64_t re, int64_t first_index) const {
     RowCounter idx(first_index + rb);
     size_t r = static_cast<size_t>(std::upper_bound(pre.begin(), pre.end(), rb) - pre.begin()) - 1;
@@ -931,7 +978,22 @@ struct RowSource {
       while (r + 1 < pre.size() && pre[r + 1] <= i) ++r;
       const ResultRun& run = runs[r];
       const int64_t e = std::min(re, pre[r + 1]);
-      for (int64_t j = i - pre[r]; i < e; ++i, ++j) p = format_row(p, idx, decode_result(run.data, run.fmt, run.r2, j));
+      int64_t j = i - pre[r];
+      if (tails[r]) {
+        const uint16_t* codes = static_cast<const uint16_t*>(run.data);
+        const char* text = tails[r]->text.data();
+        const uint8_t* len = tails[r]->len.data();
+        for (; i < e; ++i, ++j) {
+          const unsigned c = codes[j];
+          *p = '#';
+          p = idx.put(p + 1);
+          idx.next();
+          std::memcpy(p, text + size_t{R2Tails::kSlot} * c, R2Tails::kSlot);
+          p += len[c];
+        }
+      } else {
+        for (; i < e; ++i, ++j) p = format_row(p, idx, decode_result(run.data, run.fmt, run.r2, j));
+      }
     }
     return p;
   }
@@ -948,7 +1010,7 @@ std::string format_results(const Result* results, int64_t n, int64_t first_index
   for (int t = 0; t < parts_n; ++t) {
     const int64_t b = n * t / parts_n, e = n * (t + 1) / parts_n;
     std::string& s = parts[t];
-    s.resize(static_cast<size_t>(e - b) * kMaxRow);
+    s.resize(static_cast<size_t>(e - b) * kMaxRow + kSlack);
     char* p = src.format(s.data(), b, e, first_index);
     s.resize(static_cast<size_t>(p - s.data()));
   }
@@ -966,13 +1028,13 @@ void write_results(FILE* f, const Result* results, int64_t n, int64_t first_inde
 
 void write_results(FILE* f, const std::vector<ResultRun>& runs, int64_t first_index) {
   // Rows are formatted in parallel into per-part buffers (never zero-filled, never concatenated), decoding
-  // each run's wire format on the fly (R2/R4/R8 straight from the ranks' result slices, no expansion).
-  // When the stream is a regular file, every part is written at its own file offset (pwrite), so
-  // multi-GB outputs are written in parallel; otherwise (pipe, terminal) parts go out in order.
-  // Blocks of 64 K rows per part keep the buffers small (~5 MB per part, reused): page-faulting
-  // fresh multi-100 MB buffers cost more than the formatting (1.2 s of 1.6 s for 33 M rows here).
-  // A stream that is not a regular file (under mpiexec stdout is a pipe to the MPICH proxy) is written by
-  // one background thread in order, double-buffered: block k goes out while block k+1 is formatted.
+  // each run's wire format on the fly (R2 through a table of row tails, R4/R8 straight from the ranks'
+  // result slices, no expansion). Blocks of 64 K rows per part keep the buffers small (~2 MB per part,
+  // reused): page-faulting fresh multi-100 MB buffers cost more than the formatting (1.2 s of 1.6 s for
+  // 33 M rows here). A regular file gets each part written at its own offset (pwrite, in parallel; a
+  // shared file mapping with parallel page faults was 4.6x slower on the MI355X box's /tmp,
+  // tools/write_probe.cpp). Anything else (under mpiexec stdout is a pipe to the MPICH proxy) is written
+  // by one background thread in order, double-buffered: block k goes out while block k+1 is formatted.
   // Parallel loops iterate over parts, not thread ids (OMP_DYNAMIC / thread limits deliver fewer threads).
   const RowSource src(runs);
   const int64_t n = src.total();
@@ -982,22 +1044,45 @@ void write_results(FILE* f, const std::vector<ResultRun>& runs, int64_t first_in
   const int fd = fileno(f);
   struct stat st;
   off_t file_pos = -1;
-  // (not with O_APPEND: Linux pwrite then ignores the offset and the parts would land in completion order)
+  // (not with O_APPEND: Linux pwrite then ignores the offset)
   const int fl = fcntl(fd, F_GETFL);
-  if (nparts > 1 && fl >= 0 && !(fl & O_APPEND) && fstat(fd, &st) == 0 && S_ISREG(st.st_mode))
-    file_pos = lseek(fd, 0, SEEK_CUR);
-  const bool ordered_async = file_pos < 0 && n > kBlock;
+  if (fl >= 0 && !(fl & O_APPEND) && fstat(fd, &st) == 0 && S_ISREG(st.st_mode)) file_pos = lseek(fd, 0, SEEK_CUR);
+  // regular files: every part is written at its own offset by the thread that formatted it (parallel
+  // pwrite measured faster than one ordered writer on tmpfs: 0.32 vs 0.40 s for 20 M rows here);
+  // MOC_WRITER=ordered selects the ordered background writer for them too (A/B)
+  const char* wenv = std::getenv("MOC_WRITER");
+  const bool parallel_file = file_pos >= 0 && nparts > 1 && !(wenv && std::strcmp(wenv, "ordered") == 0);
+  const bool async = !parallel_file && n > kBlock;
   std::vector<uvector<char>> part_sets[2];
   std::vector<size_t> used_sets[2];
-  for (int s2 = 0; s2 < (ordered_async ? 2 : 1); ++s2) {
+  for (int s2 = 0; s2 < (async ? 2 : 1); ++s2) {
     part_sets[s2].resize(static_cast<size_t>(nparts));
     used_sets[s2].assign(static_cast<size_t>(nparts) + 1, 0);
   }
-  BackgroundReleaser writer;  // FIFO worker: ordered writes of the pipe path
   std::atomic<bool> write_error{false};
-  std::atomic<bool> async_error{false};
+  // writes one formatted block in order (the writer thread, or inline for small outputs)
+  auto write_block = [f, fd, nparts, &file_pos, &write_error](const std::vector<uvector<char>>& parts,
+                                                               const std::vector<size_t>& used) {
+    for (int t = 0; t < nparts && !write_error; ++t) {
+      const size_t len = used[t + 1];
+      if (file_pos < 0) {
+        if (std::fwrite(parts[t].data(), 1, len, f) != len) write_error = true;
+        continue;
+      }
+      for (size_t done = 0; done < len;) {
+        const ssize_t w = pwrite(fd, parts[t].data() + done, len - done, file_pos);
+        if (w <= 0) {
+          write_error = true;
+          break;
+        }
+        done += static_cast<size_t>(w);
+        file_pos += static_cast<off_t>(w);
+      }
+    }
+  };
+  BackgroundReleaser writer;  // FIFO worker: the ordered writes
   int set = 0;
-  for (int64_t b = 0; b < n; b += kBlock) {
+  for (int64_t b = 0; b < n && !write_error; b += kBlock) {
     const int64_t e = std::min(n, b + kBlock), m = e - b;
     std::vector<uvector<char>>& parts = part_sets[set];
     std::vector<size_t>& used = used_sets[set];
@@ -1005,18 +1090,17 @@ void write_results(FILE* f, const std::vector<ResultRun>& runs, int64_t first_in
     for (int t = 0; t < nparts; ++t) {
       const int64_t rb = b + m * t / nparts, re = b + m * (t + 1) / nparts;
       uvector<char>& buf = parts[t];
-      buf.resize(static_cast<size_t>(re - rb) * kMaxRow);
+      buf.resize(static_cast<size_t>(re - rb) * kMaxRow + kSlack);
       char* p = src.format(buf.data(), rb, re, first_index);
       used[t + 1] = static_cast<size_t>(p - buf.data());
     }
-    used[0] = 0;
-    if (file_pos >= 0) {
+    if (parallel_file) {
+      used[0] = 0;
       for (int q = 0; q < nparts; ++q) used[q + 1] += used[q];  // used[t] = byte offset of part t
 #pragma omp parallel for schedule(static, 1) num_threads(nparts)
       for (int t = 0; t < nparts; ++t) {
-        size_t done = 0;
         const size_t len = used[t + 1] - used[t];
-        while (done < len) {
+        for (size_t done = 0; done < len;) {
           const ssize_t w =
               pwrite(fd, parts[t].data() + done, len - done, file_pos + static_cast<off_t>(used[t] + done));
           if (w <= 0) {
@@ -1027,20 +1111,15 @@ void write_results(FILE* f, const std::vector<ResultRun>& runs, int64_t first_in
         }
       }
       file_pos += static_cast<off_t>(used[nparts]);
-    } else if (ordered_async) {
+    } else if (async) {
       writer.drain();  // the previous block (the other buffer set) is out: that set is free again
-      writer.defer([f, nparts, &parts, &used, &async_error] {
-        for (int t = 0; t < nparts; ++t)
-          if (std::fwrite(parts[t].data(), 1, used[t + 1], f) != used[t + 1]) async_error = true;
-      });
+      writer.defer([&write_block, &parts, &used] { write_block(parts, used); });
       set ^= 1;
     } else {
-      for (int t = 0; t < nparts; ++t)
-        if (std::fwrite(parts[t].data(), 1, used[t + 1], f) != used[t + 1]) write_error = true;
+      write_block(parts, used);
     }
   }
   writer.stop();
-  if (async_error) write_error = true;
   if (file_pos >= 0 && lseek(fd, file_pos, SEEK_SET) < 0) write_error = true;
   if (write_error) throw Error("error while writing the results");
   std::fflush(f);

@@ -583,13 +583,64 @@ void test_result_formats() {
   CHECK(ok);
 }
 
+// write_results over mixed runs (two large R2 runs with different parameters -> the row-tail tables, one
+// small R4 run -> the direct path) equals format_results of the expanded rows, with both file writers.
+void test_write_runs() {
+  R2Params pa, pb;
+  CHECK(r2_params(26, 6, 11, -10, 4, pa));
+  CHECK(r2_params(20, 1, 8, -3, 5, pb));
+  const int64_t na = 300000, nb = 4, nc = 270001;
+  std::vector<uint16_t> a(na), c(nc);
+  std::vector<R4> b(nb);
+  std::vector<Result> all;
+  uint32_t x = 12345;
+  auto rnd = [&x] { return x = x * 1664525u + 1013904223u; };
+  auto fill_r2 = [&](std::vector<uint16_t>& v, const R2Params& p, int max_l2) {
+    for (auto& code : v) {
+      const int r = static_cast<int>(rnd() >> 8);
+      if (r % 97 == 0) {
+        code = kR2None;
+      } else {
+        const int k = r % (max_l2 + 1), n = (r >> 5) % 16, s = (r >> 10) % 200;
+        code = static_cast<uint16_t>(s * p.j + n * p.kw + k);
+      }
+      all.push_back(decode_result(&code, ResultFormat::R2, p, 0));
+    }
+  };
+  fill_r2(a, pa, 11);
+  for (int i = 0; i < nb; ++i) {
+    b[i] = R4{static_cast<int16_t>(i == 1 ? INT16_MIN : -i * 7), static_cast<uint8_t>(i), static_cast<uint8_t>(2 * i)};
+    all.push_back(decode_result(b.data(), ResultFormat::R4, pa, i));
+  }
+  fill_r2(c, pb, 8);
+  const std::string want = format_results(all.data(), static_cast<int64_t>(all.size()), 41);
+  const std::vector<ResultRun> runs = {ResultRun{a.data(), ResultFormat::R2, pa, na},
+                                       ResultRun{b.data(), ResultFormat::R4, pa, nb},
+                                       ResultRun{c.data(), ResultFormat::R2, pb, nc}};
+  for (const char* writer : {"", "ordered"}) {
+    setenv("MOC_WRITER", writer, 1);
+    FILE* f = std::tmpfile();
+    std::fputs("head\n", f);
+    write_results(f, runs, 41);
+    std::fputs("tail\n", f);
+    std::fflush(f);
+    std::string got(static_cast<size_t>(std::ftell(f)), '\0');
+    std::rewind(f);
+    CHECK(std::fread(got.data(), 1, got.size(), f) == got.size());
+    std::fclose(f);
+    CHECK(got == "head\n" + want + "tail\n");
+  }
+  unsetenv("MOC_WRITER");
+}
+
 int main() {
   const std::vector<std::pair<const char*, std::function<void()>>> tests = {
       {"score_table", test_score_table}, {"parser", test_parser},     {"stream_reader", test_stream_reader},
       {"partition", test_partition},     {"keys", test_keys},         {"pack5", test_pack5},
       {"engine_vs_brute_force", test_engine_vs_brute_force},          {"formatter", test_formatter},
       {"profile16", test_profile16},     {"releaser", test_releaser},   {"slices", test_slices},
-      {"narrow_lengths", test_narrow_lengths}, {"result_formats", test_result_formats}};
+      {"narrow_lengths", test_narrow_lengths}, {"result_formats", test_result_formats},
+      {"write_runs", test_write_runs}};
   for (const auto& t : tests) {
     const int before = g_failed;
     t.second();
