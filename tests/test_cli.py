@@ -176,6 +176,8 @@ def test_output_to_regular_file(tmp_path, mode):
     assert out.read_text() == prefix + want
     # --output: the root writes the file itself, also under mpiexec
     out2 = tmp_path / "out2.txt"
+    # an existing longer file is overwritten and cut to the new length (opened without O_TRUNC)
+    out2.write_text("stale\n" * (len(want) // 3 + 100))
     r = run_final(["--backend=cpu", f"--input={path}", f"--output={out2}"], stdin_bytes=b"", np_=2,
                   env={"OMP_NUM_THREADS": "4"})
     assert r.returncode == 0 and r.stdout == b"", r.stderr.decode()
