@@ -298,6 +298,7 @@ class Job {
   FILE* out_ = stdout;                 // root: --output file, else stdout
   std::unique_ptr<BulkParser> parser_;  // root: pass 1 done, letters encoded straight into the window
   std::unique_ptr<SharedWindow> text_win_;  // sliced mode, several ranks on the node: the input text
+  std::unique_ptr<MappedFile> text_map_;    // ... or, for an --input file, every rank's mapping of it
   int64_t pinned_bytes_ = 0, h2d_bytes_ = 0, d2h_bytes_ = 0;  // this rank (--timing)
   std::vector<int64_t> rank_pinned_, rank_h2d_, rank_records_, rank_pin_us_;  // root: per rank (--timing)
   std::shared_ptr<BulkParser> spent_parser_;     // root: filled into the window, freed while printing
@@ -1043,7 +1044,11 @@ int Job::run() {
     pt_.end();
   }
   if (sliced && ctx_.local_size > 1) {
-    int64_t sz[2] = {h.status, text_len};
+    // an --input file read from its start: every rank maps it (page cache, nothing copied); otherwise the
+    // root reads the input into a node-shared window
+    const std::string path = flags_.get("input", "");
+    int64_t sz[3] = {h.status, text_len,
+                     ctx_.rank == kRoot && !path.empty() && text_.empty() && text_len > 0 && in && std::ftell(in) == 0};
     bcast_bytes(sz, sizeof sz, kRoot, ctx_.world);
     if (sz[0] != 0) {
       if (ctx_.rank == kRoot) std::fprintf(stderr, "input error: %s\n", error.c_str());
@@ -1051,30 +1056,38 @@ int Job::run() {
       return 1;
     }
     text_len = sz[1];
-    pt_.begin("window");
-    text_win_ = std::make_unique<SharedWindow>(ctx_, text_len + 64);
-    text_win_->prefault_shares(ctx_);  // every rank faults in a share of the pages the root reads into
-    pt_.end();
-    text = text_win_->base();
-    if (ctx_.rank == kRoot) {
-      pt_.begin("read");
-      try {
-        if (!text_.empty()) {
-          const int64_t nt = text_len > (int64_t{1} << 24) ? omp_get_max_threads() : 1;
-#pragma omp parallel for schedule(static, 1) num_threads(static_cast<int>(nt))
-          for (int64_t t = 0; t < nt; ++t) {
-            const int64_t b = text_len * t / nt, e = text_len * (t + 1) / nt;
-            std::memcpy(text_win_->base() + b, text_.data() + b, static_cast<size_t>(e - b));
-          }
-          text_ = uvector<char>();
-        } else {
-          text_len = static_cast<int64_t>(read_regular_into(in, text_win_->base(), static_cast<size_t>(text_len)));
-        }
-      } catch (const std::exception& e) {
-        error = e.what();
-        h.status = 1;
-      }
+    if (sz[2]) {
+      pt_.begin("map");
+      text_map_ = std::make_unique<MappedFile>(path.c_str(), static_cast<size_t>(text_len));
+      text_map_->set_releaser(&rel_);
+      text = text_map_->data();
       pt_.end();
+    } else {
+      pt_.begin("window");
+      text_win_ = std::make_unique<SharedWindow>(ctx_, text_len + 64);
+      text_win_->prefault_shares(ctx_);  // every rank faults in a share of the pages the root reads into
+      pt_.end();
+      text = text_win_->base();
+      if (ctx_.rank == kRoot) {
+        pt_.begin("read");
+        try {
+          if (!text_.empty()) {
+            const int64_t nt = text_len > (int64_t{1} << 24) ? omp_get_max_threads() : 1;
+#pragma omp parallel for schedule(static, 1) num_threads(static_cast<int>(nt))
+            for (int64_t t = 0; t < nt; ++t) {
+              const int64_t b = text_len * t / nt, e = text_len * (t + 1) / nt;
+              std::memcpy(text_win_->base() + b, text_.data() + b, static_cast<size_t>(e - b));
+            }
+            text_ = uvector<char>();
+          } else {
+            text_len = static_cast<int64_t>(read_regular_into(in, text_win_->base(), static_cast<size_t>(text_len)));
+          }
+        } catch (const std::exception& e) {
+          error = e.what();
+          h.status = 1;
+        }
+        pt_.end();
+      }
     }
   }
   if (ctx_.rank == kRoot && h.status == 0) {
@@ -1134,8 +1147,13 @@ int Job::run() {
   seq1.resize(static_cast<size_t>(h.L1));
   bcast_bytes(seq1.data(), h.L1, kRoot, ctx_.world);
   pt_.end();
+  pt_.begin("gpu_wait");  // the HIP runtime's start-up, when a helper thread began it during the read
+  if (prewarm_.valid()) prewarm_.get();
+  pt_.end();
   pt_.begin("setup");
   setup_engine(h.cells);  // collective: engine kind, transport, RCCL communicator
+  pt_.end();
+  pt_.begin("problem");
   eng_.set_problem(w, seq1, sem);
   pt_.end();
 

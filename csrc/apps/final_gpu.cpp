@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <future>
 #include <memory>
+#include <mutex>
 #include <vector>
 
 #include "moc/comm.hpp"
@@ -160,6 +161,10 @@ class HipDeviceSearch final : public DeviceSearch {
   R2Params r2_{};
 };
 
+// The HIP engine's construction (streams, events, device buffers, kernel code objects: 0.1-0.2 s on the
+// MI355X box, tools/init_probe.cpp) runs on a helper thread started by the constructor, so it overlaps the
+// rank's pass 1 and slice encoding; the first call that needs the engine waits for it. set_problem before
+// that point is kept and applied when the engine is ready.
 class GpuRankImpl final : public GpuRank {
  public:
   GpuRankImpl(const MpiContext& ctx, const GpuRankOptions& opt) : ctx_(ctx) {
@@ -173,16 +178,21 @@ class GpuRankImpl final : public GpuRank {
     eo.device = device_;
     if (opt.chunk_records > 0) eo.chunk_records = opt.chunk_records;
     if (opt.chunk_bytes > 0) eo.chunk_bytes = opt.chunk_bytes;
-    engine_ = std::make_unique<HipEngine>(eo);
+    pending_engine_ = std::async(std::launch::async, [eo] { return std::make_unique<HipEngine>(eo); });
     // host buffers this rank's GPU streams over PCIe, and the threads that fill them, on the NUMA node
-    // of the GPU's root complex
+    // of the GPU's root complex (this, the calling thread)
     numa_ = bind_numa_to_device(device_);
+  }
+  ~GpuRankImpl() override {
+    ds_.reset();
+    dc_.reset();
+    if (pending_engine_.valid()) pending_engine_.wait();
   }
   void init_rccl_begin() override {
     if (dc_ || pending_.valid()) return;
     const ncclUniqueId id = RcclComm::exchange_id(ctx_);  // MPI: this (the main) thread
     pending_ = std::async(std::launch::async, [this, id] {
-      return std::make_unique<RcclDeviceComm>(ctx_, device_, engine_->compute_stream(), id);
+      return std::make_unique<RcclDeviceComm>(ctx_, device_, engine().compute_stream(), id);
     });
   }
   void init_rccl() override {
@@ -190,7 +200,7 @@ class GpuRankImpl final : public GpuRank {
       init_rccl_begin();
       dc_ = pending_.get();
     }
-    if (!ds_) ds_ = std::make_unique<HipDeviceSearch>(*engine_);
+    if (!ds_) ds_ = std::make_unique<HipDeviceSearch>(engine());
   }
   DeviceComm& device_comm() override {
     init_rccl();
@@ -202,26 +212,31 @@ class GpuRankImpl final : public GpuRank {
   }
   int device() const override { return device_; }
   void set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, Semantics sem) override {
-    engine_->set_problem(w, seq1, L1, sem);
+    std::lock_guard<std::mutex> lock(mu_);
+    if (engine_) {
+      engine_->set_problem(w, seq1, L1, sem);
+      return;
+    }
+    problem_ = Problem{w, std::vector<uint8_t>(seq1, seq1 + L1), sem, true};
   }
   void solve(const uint8_t* codes, const int64_t* offsets, int64_t n, Result* out) override {
-    engine_->solve(codes, offsets, n, out);
+    engine().solve(codes, offsets, n, out);
   }
   void search_keys(const uint8_t* codes, const int64_t* offsets, int64_t n, int part, int parts,
                    uint64_t* keys) override {
-    engine_->search_keys(codes, offsets, n, part, parts, keys);
+    engine().search_keys(codes, offsets, n, part, parts, keys);
   }
-  double last_kernel_ms() const override { return engine_->stats().kernel_ms; }
+  double last_kernel_ms() const override { return engine().stats().kernel_ms; }
   int numa_node() const override { return numa_; }
-  void solve_wire(const WireBatch& b, void* out, ResultFormat fmt) override { engine_->solve_wire(b, out, fmt); }
+  void solve_wire(const WireBatch& b, void* out, ResultFormat fmt) override { engine().solve_wire(b, out, fmt); }
   bool streams_packed(int64_t min_l2, int64_t max_l2) const override {
-    return engine_->streams_packed(min_l2, max_l2);
+    return engine().streams_packed(min_l2, max_l2);
   }
   ResultFormat result_format(int64_t min_l2, int64_t max_l2) const override {
-    return engine_->auto_format(max_l2, min_l2);
+    return engine().auto_format(max_l2, min_l2);
   }
   GpuSolveStats last_stats() const override {
-    const EngineStats& st = engine_->stats();
+    const EngineStats& st = engine().stats();
     GpuSolveStats g;
     g.kernel_ms = st.kernel_ms;
     g.h2d_bytes = st.h2d_bytes;
@@ -231,10 +246,10 @@ class GpuRankImpl final : public GpuRank {
     g.r2 = st.r2;
     return g;
   }
-  void pin(const void* p, size_t bytes) override { engine_->pin(p, bytes); }
-  void unpin_all() override { engine_->unpin_all(); }
+  void pin(const void* p, size_t bytes) override { engine().pin(p, bytes); }
+  void unpin_all() override { engine().unpin_all(); }
   std::function<void()> detach_pins() override {
-    auto regs = std::make_shared<std::vector<void*>>(engine_->detach_pins());
+    auto regs = std::make_shared<std::vector<void*>>(engine().detach_pins());
     const int dev = device_;
     return [regs, dev] {
       (void)hipSetDevice(dev);
@@ -243,10 +258,34 @@ class GpuRankImpl final : public GpuRank {
   }
 
  private:
+  struct Problem {
+    Weights w{};
+    std::vector<uint8_t> seq1;
+    Semantics sem = Semantics::Reference;
+    bool set = false;
+  };
+  // the engine, once its construction has finished (any thread; the first caller applies a kept problem)
+  HipEngine& engine() const {
+    std::call_once(ready_, [this] {
+      std::unique_ptr<HipEngine> e = pending_engine_.get();  // rethrows a construction error
+      std::lock_guard<std::mutex> lock(mu_);
+      if (problem_.set) e->set_problem(problem_.w, problem_.seq1.data(), static_cast<int64_t>(problem_.seq1.size()),
+                                       problem_.sem);
+      problem_ = Problem{};
+      engine_ = std::move(e);
+    });
+    if (!engine_) throw Error("the HIP engine failed to start");
+    return *engine_;
+  }
+
   const MpiContext& ctx_;
   int device_ = -1;
   int numa_ = -1;
-  std::unique_ptr<HipEngine> engine_;
+  mutable std::future<std::unique_ptr<HipEngine>> pending_engine_;
+  mutable std::once_flag ready_;
+  mutable std::mutex mu_;
+  mutable Problem problem_;
+  mutable std::unique_ptr<HipEngine> engine_;
   std::unique_ptr<DeviceSearch> ds_;  // destroyed after dc_ (declared before it)
   std::unique_ptr<DeviceComm> dc_;
   std::future<std::unique_ptr<RcclDeviceComm>> pending_;  // connect in flight (init_rccl_begin)

@@ -1,6 +1,7 @@
 // HostRegion (moc/runtime/host_region.hpp): huge-page-advised, optionally NUMA-bound private buffers.
 #include "moc/runtime/host_region.hpp"
 
+#include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/syscall.h>
 #include <unistd.h>
@@ -75,6 +76,36 @@ void HostRegion::release() {
     releaser_->defer([m, len] { munmap(m, len); });
   else
     munmap(m, len);
+}
+
+MappedFile::MappedFile(const char* path, size_t bytes) {
+  const size_t page = static_cast<size_t>(sysconf(_SC_PAGESIZE));
+  map_bytes_ = (bytes + 64 + page - 1) / page * page;
+  // zero pages first, then the file over their front: the tail past the file's last page stays anonymous
+  void* m = mmap(nullptr, map_bytes_, PROT_READ, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+  if (m == MAP_FAILED) throw Error("cannot reserve " + std::to_string(map_bytes_) + " bytes for " + path);
+  base_ = static_cast<char*>(m);
+  bytes_ = bytes;
+  if (bytes == 0) return;
+  const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
+  void* f = fd < 0 ? MAP_FAILED : mmap(base_, bytes, PROT_READ, MAP_PRIVATE | MAP_FIXED, fd, 0);
+  if (fd >= 0) ::close(fd);
+  if (f == MAP_FAILED) {
+    munmap(base_, map_bytes_);
+    base_ = nullptr;
+    throw Error(std::string("cannot map ") + path);
+  }
+}
+
+MappedFile::~MappedFile() {
+  if (!base_) return;
+  void* b = base_;
+  const size_t n = map_bytes_;
+  if (releaser_) {
+    releaser_->defer([b, n] { munmap(b, n); });
+  } else {
+    munmap(b, n);
+  }
 }
 
 }  // namespace moc
