@@ -266,7 +266,8 @@ struct RankEngine {
 
 class Job {
  public:
-  Job(MpiContext& ctx, const Flags& flags, BackgroundReleaser& rel) : ctx_(ctx), flags_(flags), rel_(rel) {}
+  Job(MpiContext& ctx, const Flags& flags, BackgroundReleaser& rel, std::future<void> prewarm)
+      : ctx_(ctx), flags_(flags), rel_(rel), prewarm_(std::move(prewarm)) {}
   int run();
 
  private:
@@ -695,7 +696,9 @@ void Job::run_sliced(BulkParser& parser, int64_t first_index) {
       throw InputError(e.what());
     }
   }
-  // GPU ranks: the wire form the engine streams
+  pt_.end();
+  // GPU ranks: the wire form the engine streams (the first question to the engine: waits for its start-up)
+  pt_.begin("wire");
   WireBatch wb;
   ResultFormat fmt = ResultFormat::R12;
   if (gpu && n > 0) {
@@ -998,7 +1001,7 @@ int Job::run() {
       hint = rc == 0 && S_ISREG(st.st_mode) && min_bytes > 0 && st.st_size >= min_bytes;
     }
     bcast_bytes(&hint, sizeof hint, kRoot, ctx_.world);
-    if (hint) prewarm_ = std::async(std::launch::async, [] { (void)gpu_device_count(); });
+    if (hint && !prewarm_.valid()) prewarm_ = std::async(std::launch::async, [] { (void)gpu_device_count(); });
   }
 
   // ---- root opens the input; parses it whole (bulk) or just its header (streaming). A bulk job on one
@@ -1247,9 +1250,26 @@ int Job::run() {
 
 }  // namespace
 
+// An --input file of >= --gpu-prewarm-bytes will run on the GPU (unless --backend=cpu): the HIP runtime
+// starts on a helper thread before MPI_Init, every rank deciding from the same flags and file.
+std::future<void> early_prewarm(int argc, char** argv) {
+  try {
+    Flags flags(argc, argv);
+    const std::string path = flags.get("input", "");
+    if (path.empty() || to_lower(flags.get("backend", "auto")) == "cpu" || flags.get_bool("help", false)) return {};
+    struct stat st {};
+    const int64_t min_bytes = flags.get_int("gpu-prewarm-bytes", int64_t{64} << 20);
+    if (stat(path.c_str(), &st) != 0 || !S_ISREG(st.st_mode) || min_bytes <= 0 || st.st_size < min_bytes) return {};
+    return std::async(std::launch::async, [] { (void)gpu_device_count(); });
+  } catch (const std::exception&) {
+    return {};  // bad flags are reported after MPI_Init
+  }
+}
+
 int main(int argc, char** argv) {
   // declared before the MPI context: its queued unmaps overlap the job's teardown and MPI_Finalize
   BackgroundReleaser releaser;
+  std::future<void> prewarm = early_prewarm(argc, argv);
   MpiContext ctx(&argc, &argv);
   int rc = 0;
   try {
@@ -1263,7 +1283,7 @@ int main(int argc, char** argv) {
       if (ctx.rank == kRoot) std::fprintf(stderr, "unknown flag --%s\n%s", unknown[0].c_str(), kUsage);
       return 2;
     }
-    Job job(ctx, flags, releaser);
+    Job job(ctx, flags, releaser, std::move(prewarm));
     rc = job.run();
   } catch (const std::exception& e) {
     ctx.abort(3, e.what());

@@ -68,12 +68,16 @@ struct HipEngine::Slot {
 };
 
 HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
+  Stopwatch init_sw;
+  init_sw.start();
   if (opt_.device >= 0) MOC_HIP_CHECK(hipSetDevice(opt_.device));
   MOC_HIP_CHECK(hipGetDevice(&device_));
   hipDeviceProp_t prop;
   MOC_HIP_CHECK(hipGetDeviceProperties(&prop, device_));
   num_cus_ = prop.multiProcessorCount;
+  const double t_dev = init_sw.total_ms();
   dev::preload_kernels();  // code objects on the device now, not inside the first timed launch
+  const double t_preload = init_sw.total_ms();
   if (const char* g = std::getenv("MOC_GRAPHS")) opt_.use_graphs = std::atoi(g) != 0;
   if (const char* u = std::getenv("MOC_TILE_U")) {  // tuning override of the per-batch choice
     const int v = std::atoi(u);
@@ -90,6 +94,7 @@ HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
   MOC_HIP_CHECK(hipStreamCreateWithFlags(&s_copy_, hipStreamNonBlocking));
   MOC_HIP_CHECK(hipStreamCreateWithFlags(&s_compute_, hipStreamNonBlocking));
   MOC_HIP_CHECK(hipStreamCreateWithFlags(&s_return_, hipStreamNonBlocking));
+  const double t_streams = init_sw.total_ms();
   for (int i = 0; i < 3; ++i) {  // run_staged cycles two, run_dma_stream three
     auto s = std::make_unique<Slot>();
     MOC_HIP_CHECK(hipEventCreateWithFlags(&s->ev_h2d, hipEventDisableTiming));
@@ -105,6 +110,8 @@ HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
   MOC_HIP_CHECK(hipEventCreate(&ev_a_));
   MOC_HIP_CHECK(hipEventCreate(&ev_b_));
   MOC_HIP_CHECK(hipEventCreateWithFlags(&ev_plan_, hipEventDisableTiming));
+  MOC_LOG_DEBUG("engine on device %d up in %.1f ms (device %.1f, kernels %.1f, streams %.1f, buffers %.1f)", device_,
+                init_sw.total_ms(), t_dev, t_preload - t_dev, t_streams - t_preload, init_sw.total_ms() - t_streams);
 }
 
 HipEngine::~HipEngine() {
