@@ -351,11 +351,11 @@ SwipeChoice swipe_choice(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max
 }
 }  // namespace
 
-bool configure_swipe(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs_weight, ShortArgs& a) {
+bool configure_swipe(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs_weight, ShortArgs& a, bool hbm) {
   const SwipeChoice ch = swipe_choice(L1, min_l2, max_l2, max_abs_weight);
   if (!ch.noff) return false;
   const int fb = result_bytes(static_cast<ResultFormat>(a.fmt));
-  int max_tile = kMaxTile;
+  int max_tile = hbm ? kMaxTile / 2 : kMaxTile;
   if (const char* v = std::getenv("MOC_SWIPE_TILE")) max_tile = std::max(64, std::min(kMaxTile, std::atoi(v)));
   for (int tr = max_tile; tr >= 64; tr /= 2) {
     const int cap = tr * static_cast<int>(std::max<int64_t>(max_l2, 1)) + 64;
