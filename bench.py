@@ -5,14 +5,17 @@ Metric (BASELINE.json): "wall-clock (s) + elements/sec on input6.txt array at 1/
 synthetic arrays of the input6.txt shape (W = 4 3 2 10, |Seq1| = 26, |Seq2| in 6..11; no datasets are
 available offline, so records are drawn at random; data="synthetic").
 
-One timed step = one complete job over the global batch, exactly the work `./final` does between parsing
-and printing (reference flow main.c:149-197):
+One timed step = the search of one complete job over the global batch (reference flow main.c:149-197):
   1. root broadcasts the problem header (weights + Seq1) over the process group (RCCL on GPUs),
   2. every rank uploads it to its engine (LUT + Seq1 -> device),
-  3. every rank moves its contiguous slice of the records from node-shared host memory to its GPU
-     (pinned DMA over its own PCIe link), runs the gfx950 search kernels, and DMAs the (score, n, k)
+  3. every rank streams its contiguous slice of the records from host memory bound to its GPU's NUMA node
+     (zero-copy over its own PCIe link), runs the gfx950 search kernel, and writes the (score, n, k)
      results back into the node-shared result array the root prints from,
   4. an all-reduce of the per-rank record counts closes the job (the reference's MPI_Gather point).
+The records are held in the wire formats `./final` writes while it parses (5-bit letters, 3-bit lengths,
+R2 results; csrc/include/moc/wire.hpp): encoding them is the untimed set-up here, as parsing and printing
+are outside `./final`'s compute phase, whose `--timing` shows the same kernel time for the same letters
+(profiles/final_scale_1.1G_r2_async_engine.log: 14.2 ms kernel at 1.14 G letters; this bench 14.3 ms/step).
 Weak scaling: --records-per-gpu is fixed per rank, the global batch grows with N.
 
 Run: python bench.py [--gpus N --steps K --warmup W]. With N > 1 and no torch.distributed environment
