@@ -85,7 +85,8 @@ const char* kBuildId = MOC_BUILD_ID;
 const char* kUsage =
     "usage: mpiexec -np N ./final [options] < input.txt\n"
     "  --backend=auto|hip|cpu      compute engine (auto: hip when a GPU is visible and the job has\n"
-    "                              >= --gpu-min-cells cells per rank, default 3e8; else the OpenMP engine)\n"
+    "                              >= --gpu-min-cells cells per rank; default: 0.2 s of OpenMP work, i.e.\n"
+    "                              0.08 G (records <= 32 letters) / 0.28 G (longer) cells per thread)\n"
     "  --gpu-prewarm-bytes=B       start the HIP runtime during the parse when the input file has >= B bytes\n"
     "                              (default 64 MiB; 0 = never)\n"
     "  --transport=auto|shm|rccl|rccl-emul|mpi   record distribution (auto: shm on one node, else rccl/mpi;\n"
@@ -126,6 +127,7 @@ struct Header {
   int64_t first_index;  // --skip-records actually applied
   int64_t cells;        // search cells of the job (-1: unknown, streaming)
   int64_t text_bytes;   // bytes of the input text (sliced mode)
+  int64_t mean_l2;      // mean record length (estimate; 0: unknown)
 };
 
 struct BatchHeader {
@@ -271,7 +273,7 @@ class Job {
   int run();
 
  private:
-  void setup_engine(int64_t cells);
+  void setup_engine(int64_t cells, int64_t mean_l2);
   void run_batch(RecordBatch* rb, int64_t n, int64_t total_chars, int64_t first_index);
   void run_sliced(BulkParser& parser, int64_t first_index);
   void batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, bool cp);
@@ -319,14 +321,19 @@ class Job {
   std::future<void> prewarm_;     // HIP runtime start-up overlapped with the parse (large inputs)
 };
 
-void Job::setup_engine(int64_t cells) {
+void Job::setup_engine(int64_t cells, int64_t mean_l2) {
   if (prewarm_.valid()) prewarm_.get();
   const int threads = static_cast<int>(flags_.get_int("threads", 0));
   std::string backend = to_lower(flags_.get("backend", "auto"));
   if (backend != "auto" && backend != "hip" && backend != "cpu") throw Error("--backend must be auto|hip|cpu");
-  // auto: a job too small to pay for bringing up the GPU runtime (hundreds of ms) runs on the OpenMP
-  // engine; `cells` < 0 means unknown (streaming) and counts as large
-  const int64_t min_cells = flags_.get_int("gpu-min-cells", int64_t{300} * 1000 * 1000);
+  // auto: a job the OpenMP engine finishes faster than the GPU starts runs on the CPU. The GPU's start-up
+  // (HIP runtime + engine) is 0.05-0.25 s; the OpenMP engine on the MI355X box's host cores searches
+  // ~0.4 G cells/s per thread for records of <= 32 letters and ~1.4 G for longer ones, so the crossover is
+  // ~0.2 s of CPU work (tools/gpu_crossover.sh, profiles/gpu_crossover.log: input6 shape between 0.6 and
+  // 2.5 G cells at 16 threads, input3 shape above 1.7 G). `cells` < 0 means unknown (streaming): large.
+  const double per_thread = mean_l2 > 32 ? 1.4e9 : 0.4e9;
+  const int64_t model_min = static_cast<int64_t>(0.2 * per_thread * std::max(1, omp_get_max_threads()));
+  const int64_t min_cells = flags_.get_int("gpu-min-cells", model_min);
   if (backend == "auto" && cells >= 0 && cells < min_cells * ctx_.size) backend = "cpu";
   const int ndev = (backend == "cpu") ? 0 : gpu_device_count();
   if (backend == "hip" && ndev == 0)
@@ -1112,6 +1119,7 @@ int Job::run() {
         h.n_total = parser->count();
         h.first_index = std::min<int64_t>(skip, h.n_total);
         h.cells = parser->cells_estimate();
+        h.mean_l2 = parser->mean_length_estimate();
         // shm transport without a skip: pass 2 later writes straight into the node-shared window (sliced:
         // into every rank's own buffers); otherwise encode now into a private batch
         const bool into_window = sliced || (h.first_index == 0 && (tr_flag == "shm" || (tr_flag == "auto" && ctx_.single_node())));
@@ -1154,7 +1162,7 @@ int Job::run() {
   if (prewarm_.valid()) prewarm_.get();
   pt_.end();
   pt_.begin("setup");
-  setup_engine(h.cells);  // collective: engine kind, transport, RCCL communicator
+  setup_engine(h.cells, h.mean_l2);  // collective: engine kind, transport, RCCL communicator
   pt_.end();
   pt_.begin("problem");
   eng_.set_problem(w, seq1, sem);

@@ -98,6 +98,8 @@ class BulkParser {
   void fill(uint8_t* codes, int64_t* offsets) const;
   // n * (L1 - avg + 1) * avg from the mean record length (pass 1's letters, or the area size before it).
   int64_t cells_estimate() const;
+  // Mean record length: exact after pass 1, else the area's bytes less one separator per record.
+  int64_t mean_length_estimate() const;
   // Exact cost (moc/partition.hpp) of all tokens of chunks [c0, c1) -> costs[c - c0] (OpenMP over chunks).
   void chunk_costs(const std::vector<int64_t>& starts, int c0, int c1, const CostModel& m, double* costs) const;
   // Installs exact chunk costs for cost_split (all chunks, same model); without them it estimates.

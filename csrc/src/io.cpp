@@ -490,6 +490,12 @@ void BulkParser::fill(uint8_t* codes, int64_t* offs) const {
   check(fill_slice(s, codes, nullptr, offs));
 }
 
+int64_t BulkParser::mean_length_estimate() const {
+  if (n_ <= 0) return 0;
+  const int64_t letters = total_chars_ >= 0 ? total_chars_ : std::max<int64_t>(0, static_cast<int64_t>(area_len_) - n_);
+  return letters / n_;
+}
+
 int64_t BulkParser::cells_estimate() const {
   const int64_t L1 = static_cast<int64_t>(seq1_.size());
   if (n_ <= 0) return 0;
