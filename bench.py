@@ -104,11 +104,12 @@ def self_launch(args, argv):
 
 
 class HostArrays:
-    """Per-rank slice of the node-shared input/result arrays (/dev/shm files, or private memory)."""
+    """Per-rank slice of the node-shared input/result arrays (/dev/shm files, or private memory), in the
+    wire formats `./final` writes while it parses (mpi_openmp_cuda_amd/parallel/wire.py: the same
+    WireSlice the distributed driver's golden tests run)."""
 
-    def __init__(self, tag, rank, lengths, use_shm, packed, seed, len_base, hip_alloc=False):
-        from mpi_openmp_cuda_amd.models.problem import (lengths3_bytes, pack5, pack_lengths3, pack_lengths4,
-                                                        packed5_bytes)
+    def __init__(self, tag, rank, lengths, use_shm, packed, seed, narrow, hip_alloc=False):
+        from mpi_openmp_cuda_amd.parallel.wire import WireSlice
         from mpi_openmp_cuda_amd.utils.synthetic import fill_codes
 
         n = lengths.shape[0]
@@ -138,49 +139,12 @@ class HostArrays:
         else:
             def mk(name, dtype, count):
                 return np.empty(count, dtype=dtype)
-        self.offsets = mk("offsets", np.int64, n + 1)
-        self.offsets[0] = 0
-        np.cumsum(lengths, out=self.offsets[1:])
-        # narrow lengths (the parser's by-product): 3 or 4 bits above the batch's minimum when the range
-        # allows (input6: 6..11 -> 3 bits)
-        span = int(lengths.max() - lengths.min()) if n else 0
-        self.len_bits = 8 if len_base is None else (3 if span <= 7 else 4)
-        if self.len_bits == 3:
-            self.lengths = mk("lengths3", np.uint8, lengths3_bytes(n))
-            pack_lengths3(lengths, len_base, out=self.lengths)
-        elif self.len_bits == 4:
-            self.lengths = mk("lengths4", np.uint8, (n + 1) // 2)
-            pack_lengths4(lengths, len_base, out=self.lengths)
-        else:
-            self.lengths = mk("lengths", np.uint8, n)
-            self.lengths[:] = lengths
-        # letters: the parser's packed CSR (5 bits per letter) or one byte per letter
+        # letters: random codes 1..26, encoded once (5-bit packed, narrow lengths) like final's parser does
         letters = np.empty(total, dtype=np.uint8)
         fill_codes(letters, seed)
-        self.packed = bool(packed)
-        if self.packed:
-            self.codes = mk("codes5", np.uint8, packed5_bytes(total))
-            pack5(letters, out=self.codes)
-        else:
-            self.codes = mk("codes", np.uint8, total)
-            self.codes[:] = letters
+        self.wire = WireSlice(lengths, letters, packed=packed, narrow=narrow, alloc=mk)
         self.check_letters = letters[:min(total, 1 << 22)].copy()  # kept for the untimed verification
         del letters
-        self.results = None  # allocated once the result wire format is known
-
-    def alloc_results(self, count, dtype, tag, rank):
-        if self.bufs:
-            from mpi_openmp_cuda_amd._lib import HostBuffer
-
-            b = HostBuffer(np.dtype(dtype).itemsize * count)
-            self.bufs.append(b)
-            self.results = b.array(dtype, count)
-        elif self.shm:
-            p = f"/dev/shm/moc_bench_{tag}_{rank}_results"
-            self.paths.append(p)
-            self.results = np.memmap(p, dtype=dtype, mode="w+", shape=(count,))
-        else:
-            self.results = np.empty(count, dtype=dtype)
 
     def cleanup(self):
         for b in self.bufs:
@@ -266,18 +230,17 @@ def main():
     rrng = np.random.default_rng(args.seed + 1 + rank)
     lengths = rrng.integers(shape.l2_min, shape.l2_max + 1, size=R, dtype=np.int64)
     tag = os.environ.get("MASTER_PORT", str(os.getpid()))
-    narrow4 = bool(args.narrow) and shape.l2_max - shape.l2_min <= 15
     progress(f"generating {R} records per rank")
-    host = HostArrays(tag, rank, lengths, bool(args.shm), args.packed, args.seed + 101 + rank,
-                      shape.l2_min if narrow4 else None, hip_alloc=args.host_alloc == "hip")
-    progress(f"{int(host.offsets[-1])} letters per rank ready")
+    host = HostArrays(tag, rank, lengths, bool(args.shm), args.packed, args.seed + 101 + rank, bool(args.narrow),
+                      hip_alloc=args.host_alloc == "hip")
+    wire = host.wire
+    progress(f"{wire.total} letters per rank ready")
     del lengths
     eng = HipSearchEngine(device=gpu)
     eng.set_problem(weights, seq1)
-    fmt = eng.auto_format(shape.l2_max, shape.l2_min if args.narrow else 0)
-    rdt = _lib.FORMAT_DTYPES[_lib.FORMAT_NAMES.index(fmt)]
-    host.alloc_results(R, rdt, tag, rank)
-    pin = Pinned(*([] if host.bufs else [host.codes, host.offsets, host.lengths, host.results]))
+    wire.alloc_results(eng)  # the narrowest result format for this slice (R2 on input6)
+    fmt = wire.fmt
+    pin = Pinned(*([] if host.bufs else wire.arrays()))
     progress("host arrays page-locked; warm-up")
     done = torch.zeros(1, dtype=torch.int64, device=cdev)
     hdr_host = np.empty(4 + shape.L1, dtype=np.int32)
@@ -287,9 +250,7 @@ def main():
             dist.broadcast(header, src=0)
         hdr_host[:] = header.cpu().numpy()
         eng.set_problem(hdr_host[:4], hdr_host[4:].astype(np.uint8))
-        eng.solve(host.codes, host.offsets, out=host.results, lengths=host.lengths, fmt=fmt,
-                  l2_range=(shape.l2_min, shape.l2_max), packed5=host.packed, lengths_bits=host.len_bits,
-                  lengths_base=shape.l2_min)
+        wire.solve(eng)
         done.fill_(R)
         if distributed:
             dist.all_reduce(done)
@@ -315,22 +276,22 @@ def main():
 
     # ---- verification (untimed): the result array is poisoned and one more step is run, so a step that
     # skipped work (stale results from an earlier step) cannot pass; a sample is checked vs the CPU engine
-    host.results[:] = np.iinfo(host.results.dtype).max if host.results.dtype.kind == "u" else 0
+    res = wire.results
+    res[:] = np.iinfo(res.dtype).max if res.dtype.kind == "u" else 0
     step()
     barrier()
     nv = min(args.verify, R)
-    while nv > 0 and int(host.offsets[nv]) > host.check_letters.shape[0]:
+    while nv > 0 and int(wire.offsets[nv]) > host.check_letters.shape[0]:
         nv //= 2
     ok = 1
     if nv > 0:
-        sub = Problem(shape.weights, seq1, host.check_letters[:int(host.offsets[nv])], host.offsets[:nv + 1].copy())
+        sub = Problem(shape.weights, seq1, host.check_letters[:int(wire.offsets[nv])], wire.offsets[:nv + 1].copy())
         ref = as_triples(search_cpu(sub))
-        r2 = eng.r2_params(shape.l2_min, shape.l2_max) if fmt == "r2" else None
-        ok = int(np.array_equal(as_triples(host.results[:nv], r2=r2), ref))
+        ok = int(np.array_equal(wire.triples(eng, nv), ref))
         # and the tail of the batch was written by the last step too (no sentinel left anywhere)
-        tail = host.results[R - min(R, 1 << 16):]
-        if host.results.dtype.kind == "u":
-            ok &= int(not (tail == np.iinfo(host.results.dtype).max).any())
+        tail = res[R - min(R, 1 << 16):]
+        if res.dtype.kind == "u":
+            ok &= int(not (tail == np.iinfo(res.dtype).max).any())
         else:
             ok &= int(not (tail.view(np.uint8).reshape(tail.shape[0], -1) == 0).all(axis=1).any())
     okt = torch.tensor([ok], dtype=torch.int32, device=cdev)
@@ -338,13 +299,13 @@ def main():
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
 
     total_records = R * world
-    total_elems = int(host.offsets[-1]) * world  # per-rank chars ~ equal (same length distribution)
+    total_elems = wire.total * world  # per-rank chars ~ equal (same length distribution)
     if distributed:
-        te = torch.tensor([int(host.offsets[-1])], dtype=torch.int64, device=cdev)
+        te = torch.tensor([wire.total], dtype=torch.int64, device=cdev)
         dist.all_reduce(te)
         total_elems = int(te.item())
     # per-rank evidence: NUMA node of the host arrays, median kernel ms per step, device index
-    mine = torch.tensor([float(numa), float(np.median(kms)), float(gpu), float(int(host.offsets[-1]))],
+    mine = torch.tensor([float(numa), float(np.median(kms)), float(gpu), float(wire.total)],
                         dtype=torch.float64, device=cdev)
     if distributed:
         allv = [torch.zeros_like(mine) for _ in range(world)]
@@ -386,8 +347,8 @@ def main():
             "rank0_d2h_bytes_per_step": int(st["d2h_bytes"]),
             "host_arrays": "hip_host_malloc" if host.bufs else ("shm" if host.shm else "private"),
             "result_format": fmt,
-            "lengths_bits": host.len_bits,
-            "letters": "packed5" if host.packed else "bytes",
+            "lengths_bits": wire.len_bits,
+            "letters": "packed5" if wire.packed else "bytes",
             "rank0_numa_node": numa,
             "rccl_world": dist.get_world_size() if (distributed and nccl) else (1 if nccl else None),
             "dist_backend": ("nccl" if nccl else "gloo") if distributed else "none",

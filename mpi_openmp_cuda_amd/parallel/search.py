@@ -30,6 +30,7 @@ from ..ops.align import (HipSearchEngine, decode_keys, device_count, empty_resul
 from ..utils.timer import PhaseTimer
 from . import dist as D
 from .partition import CPU_COST, GPU_COST, partition
+from .wire import WireSlice
 
 
 class NodeWindow:
@@ -72,7 +73,9 @@ class DistributedSearch:
             raise ValueError("transport=shm needs every rank on one node")
         self.transport = transport
         self.threads = threads
-        self.engine = HipSearchEngine(ctx.local_rank if device is None else device) if backend == "hip" else None
+        if backend == "hip" and device is None:
+            device = ctx.local_rank % max(device_count(), 1)  # node-local rank -> GPU (ranks may share one)
+        self.engine = HipSearchEngine(device) if backend == "hip" else None
         self.timer = PhaseTimer()
         if partition == "offsets" and ctx.distributed:
             # GPU ranks split tile lists, CPU ranks offset ranges: one engine kind for the whole group
@@ -82,7 +85,13 @@ class DistributedSearch:
 
     def _compute(self, prob: Problem, sem: Semantics, codes, offsets, out):
         if self.engine is not None:
-            self.engine.solve(codes, offsets, out=out)
+            # GPU ranks: the slice in the wire formats ./final's parser writes and bench.py streams
+            # (parallel/wire.py), page-locked, searched zero-copy, decoded into the R12 result window
+            ws = WireSlice.from_csr(codes, offsets)
+            ws.alloc_results(self.engine)
+            with _lib.Pinned(*ws.arrays()):
+                ws.solve(self.engine)
+            out.view(np.int32).reshape(-1, 3)[:] = ws.triples(self.engine)
         else:
             sub = Problem(prob.weights, prob.seq1, codes[offsets[0]:offsets[-1]], offsets - offsets[0])
             out[:] = search_cpu(sub, sem, self.threads)

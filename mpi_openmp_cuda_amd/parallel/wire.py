@@ -1,0 +1,143 @@
+"""One rank's slice of records in the wire formats the GPU streams (csrc/include/moc/wire.hpp).
+
+``./final`` writes these forms straight from its parser (``BulkParser::fill_slice``): letters 5-bit packed,
+record lengths as 3/4-bit fields above the slice's shortest length (8-bit, or offsets only, when the range
+is wider), results in the narrowest format the problem's bounds allow (R2: one uint16 per record). The
+streaming kernel reads them zero-copy from page-locked host memory, so every byte saved is PCIe time saved.
+
+Shared by ``bench.py`` (the headline step) and :mod:`.search` (the distributed driver that the golden tests
+run on GPU ranks), so the headline's data path is the one the goldens pin. Reference: the fixed 2000-byte
+record stride and three int result arrays (main.c:93,123-125).
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import numpy as np
+
+from ..models.problem import lengths3_bytes, pack5, pack_lengths3, pack_lengths4, packed5_bytes, unpack5
+
+# allocator(name, dtype, count) -> array: private numpy memory, /dev/shm memmaps, hipHostMalloc buffers, ...
+Alloc = Callable[[str, np.dtype, int], np.ndarray]
+
+
+def private_alloc(name: str, dtype, count: int) -> np.ndarray:
+    return np.empty(count, dtype=dtype)
+
+
+def length_bits(l2_min: int, l2_max: int, narrow: bool = True) -> int:
+    """Bits per record length: 3 or 4 above the minimum when the range allows, else 8 (0: offsets only)."""
+    span = l2_max - l2_min
+    if narrow and span <= 7:
+        return 3
+    if narrow and span <= 15:
+        return 4
+    return 8 if l2_max <= 255 else 0
+
+
+class WireSlice:
+    """A CSR slice (record lengths + byte letter codes 1..26) encoded once into the wire formats.
+
+    ``letters`` may be None when the caller fills ``codes`` itself (``packed`` False); ``alloc`` places
+    every array (so a benchmark can put them in node-shared or hipHostMalloc memory)."""
+
+    def __init__(self, lengths: np.ndarray, letters: Optional[np.ndarray], packed: bool = True, narrow: bool = True,
+                 alloc: Alloc = private_alloc):
+        lengths = np.asarray(lengths)
+        n = int(lengths.shape[0])
+        self.n = n
+        self.alloc = alloc
+        self.l2_min = int(lengths.min()) if n else 0
+        self.l2_max = int(lengths.max()) if n else 0
+        self.narrow = bool(narrow)
+        self.offsets = alloc("offsets", np.int64, n + 1)
+        self.offsets[0] = 0
+        np.cumsum(lengths, out=self.offsets[1:])
+        self.total = int(self.offsets[-1])
+        self.len_bits = length_bits(self.l2_min, self.l2_max, narrow)
+        self.len_base = self.l2_min if self.len_bits in (3, 4) else 0
+        if self.len_bits == 3:
+            self.lengths = alloc("lengths3", np.uint8, lengths3_bytes(n))
+            pack_lengths3(lengths, self.len_base, out=self.lengths)
+        elif self.len_bits == 4:
+            self.lengths = alloc("lengths4", np.uint8, (n + 1) // 2)
+            pack_lengths4(lengths, self.len_base, out=self.lengths)
+        elif self.len_bits == 8:
+            self.lengths = alloc("lengths", np.uint8, n)
+            self.lengths[:] = lengths
+        else:
+            self.lengths = None
+        self.packed = bool(packed)
+        if self.packed:
+            self.codes = alloc("codes5", np.uint8, packed5_bytes(self.total))
+            if letters is not None:
+                pack5(letters, out=self.codes)
+        else:
+            self.codes = alloc("codes", np.uint8, self.total)
+            if letters is not None:
+                self.codes[:] = letters
+        self.fmt: Optional[str] = None
+        self.results: Optional[np.ndarray] = None
+
+    @classmethod
+    def from_csr(cls, codes: np.ndarray, offsets: np.ndarray, **kw) -> "WireSlice":
+        """Records [codes[offsets[i]:offsets[i+1]]] (offsets may be a slice of an absolute offset array)."""
+        offsets = np.asarray(offsets, dtype=np.int64)
+        return cls(np.diff(offsets), np.asarray(codes)[offsets[0]:offsets[-1]], **kw)
+
+    # ---- results
+    def alloc_results(self, engine, fmt: str = "auto") -> np.ndarray:
+        """Results in ``fmt`` (auto: the narrowest the engine can produce for this slice's lengths)."""
+        from .. import _lib
+
+        if fmt == "auto":
+            fmt = engine.auto_format(self.l2_max, self.l2_min if self.narrow else 0)
+        self.fmt = fmt
+        self.results = self.alloc("results", _lib.FORMAT_DTYPES[_lib.FORMAT_NAMES.index(fmt)], self.n)
+        return self.results
+
+    def arrays(self):
+        """Every host array the engine streams (for page-locking)."""
+        return [a for a in (self.codes, self.offsets, self.lengths, self.results) if a is not None]
+
+    def solve(self, engine) -> np.ndarray:
+        """One search of the slice into ``results`` (zero-copy when every array is page-locked)."""
+        if self.results is None:
+            self.alloc_results(engine)
+        return engine.solve(self.codes, self.offsets, out=self.results, lengths=self.lengths, fmt=self.fmt,
+                            l2_range=(self.l2_min, self.l2_max), packed5=self.packed,
+                            lengths_bits=self.len_bits or 8, lengths_base=self.len_base)
+
+    def triples(self, engine, count: Optional[int] = None) -> np.ndarray:
+        """The first ``count`` results as int32 [n, 3] (score, n, k)."""
+        from ..ops.align import as_triples
+
+        m = self.n if count is None else count
+        r2 = engine.r2_params(self.l2_min, self.l2_max) if self.fmt == "r2" else None
+        return as_triples(self.results[:m], r2=r2)
+
+    # ---- decoding (tests, verification)
+    def letters(self, begin: int = 0, end: Optional[int] = None) -> np.ndarray:
+        end = self.total if end is None else end
+        if self.packed:
+            return unpack5(self.codes, begin, end - begin)
+        return np.asarray(self.codes[begin:end])
+
+    def decoded_lengths(self) -> np.ndarray:
+        """Record lengths back from the narrow fields (or the offsets when there are none)."""
+        n = self.n
+        if self.len_bits == 3:
+            b = np.zeros(lengths3_bytes(n) + 4, np.uint8)
+            b[:self.lengths.shape[0]] = self.lengths
+            bit = 3 * np.arange(n, dtype=np.int64)
+            w = b[bit >> 3].astype(np.int64) | (b[(bit >> 3) + 1].astype(np.int64) << 8)
+            return ((w >> (bit & 7)) & 7) + self.len_base
+        if self.len_bits == 4:
+            v = np.asarray(self.lengths[:(n + 1) // 2])
+            out = np.empty(2 * v.shape[0], np.int64)
+            out[0::2] = v & 15
+            out[1::2] = v >> 4
+            return out[:n] + self.len_base
+        if self.len_bits == 8:
+            return np.asarray(self.lengths[:n]).astype(np.int64)
+        return np.diff(self.offsets)

@@ -634,3 +634,44 @@ def test_tile16_windowed(engine, L1, shape, n):
         for part in range(3):
             keys = np.maximum(keys, engine.search_keys(prob.codes, prob.offsets, part, 3))
         assert np.array_equal(as_triples(decode_keys(keys, prob)), ref), sem
+
+
+# ---- the Python distributed driver on GPU ranks (parallel/search.py -> parallel/wire.py WireSlice): the same
+# wire-format step bench.py times, pinned here to the goldens and to the CPU engine
+@pytest.mark.parametrize("transport", ["shm", "p2p"])
+def test_python_driver_hip_goldens(transport):
+    from mpi_openmp_cuda_amd.parallel.dist import DistContext
+    from mpi_openmp_cuda_amd.parallel.search import DistributedSearch
+
+    ds = DistributedSearch(DistContext(), backend="hip", transport=transport)
+    for i in range(1, 7):
+        prob = Problem.read(input_path(i))
+        assert format_results(ds.run(prob)) == expected(i), f"input{i}"
+    big = make_synthetic("input6", 300000, seed=21)  # R2 results, 3-bit lengths, zero-copy swipe stream
+    assert np.array_equal(as_triples(ds.run(big)), as_triples(search_cpu(big)))
+
+
+def test_python_driver_hip_two_ranks(tmp_path):
+    import os
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+
+    prob = make_synthetic("input6", 200000, seed=22)
+    path = tmp_path / "in.txt"
+    path.write_text(prob.to_text())
+    want = format_results(search_cpu(prob))
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="4")
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    for transport in ("shm", "p2p"):
+        r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                            "--master-addr=127.0.0.1", f"--master-port={port}", "-m", "mpi_openmp_cuda_amd",
+                            "--backend=hip", "--dist-backend=gloo", f"--transport={transport}", f"--input={path}"],
+                           capture_output=True, timeout=110, env=env, cwd="/tmp")
+        assert r.returncode == 0, r.stderr.decode()[-3000:]
+        assert r.stdout.decode() == want, transport

@@ -1,0 +1,50 @@
+"""WireSlice (mpi_openmp_cuda_amd/parallel/wire.py): the wire formats shared by bench.py's headline step and
+the distributed driver's GPU ranks must encode any CSR slice losslessly — letters 5-bit packed or bytes,
+lengths in 3/4/8-bit fields or offsets only — whatever allocator places the arrays."""
+import numpy as np
+import pytest
+
+from mpi_openmp_cuda_amd.parallel.wire import WireSlice, length_bits
+from mpi_openmp_cuda_amd.utils.synthetic import make_synthetic
+
+
+@pytest.mark.parametrize("lo,hi,narrow,bits", [(6, 11, True, 3), (6, 11, False, 8), (5, 20, True, 4),
+                                               (1, 200, True, 8), (1, 300, True, 0), (7, 7, True, 3)])
+def test_length_fields_round_trip(lo, hi, narrow, bits):
+    rng = np.random.default_rng(lo * 1000 + hi)
+    n = 1001
+    lengths = rng.integers(lo, hi + 1, size=n)
+    letters = rng.integers(1, 27, size=int(lengths.sum()), dtype=np.uint8)
+    assert length_bits(int(lengths.min()), int(lengths.max()), narrow) == bits
+    for packed in (True, False):
+        ws = WireSlice(lengths, letters, packed=packed, narrow=narrow)
+        assert ws.len_bits == bits
+        assert np.array_equal(ws.decoded_lengths(), lengths)
+        assert np.array_equal(ws.offsets[1:], np.cumsum(lengths))
+        assert np.array_equal(ws.letters(), letters)
+        i = n // 2  # any record's letters from its offset
+        b, e = int(ws.offsets[i]), int(ws.offsets[i + 1])
+        assert np.array_equal(ws.letters(b, e), letters[b:e])
+
+
+def test_from_csr_slice_of_absolute_offsets():
+    prob = make_synthetic("input6", 5000, seed=3)
+    b, e = 1234, 4321
+    ws = WireSlice.from_csr(prob.codes, prob.offsets[b:e + 1])
+    assert ws.n == e - b
+    assert np.array_equal(ws.decoded_lengths(), np.diff(prob.offsets[b:e + 1]))
+    assert np.array_equal(ws.letters(), prob.codes[prob.offsets[b]:prob.offsets[e]])
+    assert ws.packed and ws.len_bits == 3 and ws.len_base == 6
+
+
+def test_custom_allocator_places_every_array():
+    names = []
+
+    def alloc(name, dtype, count):
+        names.append(name)
+        return np.zeros(count, dtype=dtype)
+
+    prob = make_synthetic("input6", 100, seed=1)
+    ws = WireSlice.from_csr(prob.codes, prob.offsets, alloc=alloc)
+    assert names == ["offsets", "lengths3", "codes5"]
+    assert len(ws.arrays()) == 3  # results come later (their format is the engine's choice)
