@@ -93,8 +93,9 @@ const char* kUsage =
     "                              rccl-emul: the rccl driver over MPI on CPU ranks)\n"
     "  --semantics=reference|spec  candidate set (spec adds the un-mutated final offset, bug B8)\n"
     "  --partition=cost|even|offsets   rank decomposition (offsets: split every record's offset range)\n"
-    "  --collectives=auto|mpi|rccl the ranks' collectives on the shm transport (auto: RCCL over xGMI when\n"
-    "                              every rank drives a GPU and there are several ranks, else MPI)\n"
+    "  --collectives=auto|mpi|rccl the ranks' host-table collectives on the shm transport (auto = mpi: a few\n"
+    "                              int64 per rank, where RCCL's communicator set-up costs 1.7-5.8 s; rccl:\n"
+    "                              over xGMI, needs one GPU per rank)\n"
     "  --batch-records=B           streaming mode: parse/search/print B records at a time (0 = all at once)\n"
     "  --batch-chars=C             streaming mode: also cap a batch at C letters\n"
     "  --skip-records=S            start at record #S (resume a partially printed run)\n"
@@ -372,13 +373,15 @@ void Job::setup_engine(int64_t cells, int64_t mean_l2) {
   pin_window_ = flags_.get_bool("pin-window", true);
   if (transport_ == "rccl") eng_.hip->init_rccl();
   // the shm transport moves no record data between ranks; its collectives (the slices' fill reports and
-  // result descriptors, the context-parallel key reduction) run over RCCL when every rank has a GPU. The
-  // connect runs on a helper thread while the ranks parse their slices.
+  // result descriptors, the context-parallel key reduction) are a few host int64 per rank (or one key per
+  // record), so they stay on MPI unless --collectives=rccl: setting up an RCCL communicator took 1.7-5.8 s
+  // on the MI355X box even for one rank (profiles/final_scale_collrccl.log), microseconds of MPI work
+  // would wait for it. With rccl the connect runs on a helper thread while the ranks parse their slices.
   const std::string coll = to_lower(flags_.get("collectives", "auto"));
   if (coll != "auto" && coll != "mpi" && coll != "rccl") throw Error("--collectives must be auto|mpi|rccl");
   if (coll == "rccl" && !all_gpu_) throw Error("--collectives=rccl needs a GPU on every rank");
-  bool shared_gpu = false;  // RCCL needs one rank per GPU (ranks sharing a GPU keep MPI under auto)
-  if (all_gpu_ && coll != "mpi") {
+  bool shared_gpu = false;  // RCCL needs one rank per GPU
+  if (all_gpu_ && coll == "rccl") {
     const int64_t mine = static_cast<int64_t>(std::hash<std::string>{}(ctx_.hostname) & 0xffffffffffffull) * 4096 + device_;
     std::vector<int64_t> all(static_cast<size_t>(ctx_.size));
     MPI_Allgather(&mine, 1, MPI_INT64_T, all.data(), 1, MPI_INT64_T, ctx_.world);
@@ -386,7 +389,7 @@ void Job::setup_engine(int64_t cells, int64_t mean_l2) {
     shared_gpu = std::adjacent_find(all.begin(), all.end()) != all.end();
   }
   if (coll == "rccl" && shared_gpu) throw Error("--collectives=rccl needs one rank per GPU");
-  coll_rccl_ = transport_ == "shm" && all_gpu_ && !shared_gpu && (coll == "rccl" || (coll == "auto" && ctx_.size > 1));
+  coll_rccl_ = transport_ == "shm" && all_gpu_ && !shared_gpu && coll == "rccl";
   if (coll_rccl_) eng_.hip->init_rccl_begin();
   if (transport_ == "rccl-emul") emul_comm_ = std::make_unique<MpiDeviceComm>(ctx_);
   MOC_LOG_INFO("rank %d/%d host %s local %d/%d engine=%s device=%d transport=%s partition=%s", ctx_.rank, ctx_.size,

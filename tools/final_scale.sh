@@ -7,8 +7,10 @@ F=/tmp/moc_big6.txt
 timeout -k 10 300 python3 tools/gen_synthetic.py --shape input6 --records ${RECORDS:-134217728} --out $F
 # "--output": the root writes the file itself (parallel pwrite) instead of stdout, which mpiexec's proxy
 # forwards through a pipe
+# MODES: '|'-separated flag sets (each may hold several flags)
+IFS='|' read -r -a MODE_LIST <<< "${MODES:- |--output=/tmp/moc_big6.out|--output=/tmp/moc_big6.out --gpu-prewarm-bytes=0|--batch-records=16777216}"
 for np in ${NPS:-1}; do
-for mode in ${MODES:-"" "--output=/tmp/moc_big6.out" "--output=/tmp/moc_big6.out --gpu-prewarm-bytes=0" "--batch-records=16777216"}; do
+for mode in "${MODE_LIST[@]}"; do
   rm -f /tmp/moc_big6.out  # untimed: dropping the previous 4.6 GB output
   so=/tmp/moc_big6.out
   case "$mode" in --output=*) so=/dev/null;; esac
