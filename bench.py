@@ -54,7 +54,8 @@ def parse_args():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, default) | gloo (multi-rank rehearsal)")
     ap.add_argument("--numa", type=int, default=1, help="bind each rank to its GPU's NUMA node")
-    ap.add_argument("--packed", type=int, default=1, help="letters as 5-bit packed CSR (1) or one byte each (0)")
+    ap.add_argument("--letters", default="p24", choices=["p24", "p5", "bytes"],
+                    help="letter wire format: base-26 groups of 5 in 3 bytes (p24), 5-bit packed (p5), bytes")
     ap.add_argument("--narrow", type=int, default=1,
                     help="1: narrowest wire formats that fit (4-bit lengths, R2 results); 0: uint8 lengths, R4")
     ap.add_argument("--dry-launch", action="store_true",
@@ -108,7 +109,7 @@ class HostArrays:
     wire formats `./final` writes while it parses (mpi_openmp_cuda_amd/parallel/wire.py: the same
     WireSlice the distributed driver's golden tests run)."""
 
-    def __init__(self, tag, rank, lengths, use_shm, packed, seed, narrow, hip_alloc=False):
+    def __init__(self, tag, rank, lengths, use_shm, letter_format, seed, narrow, hip_alloc=False):
         from mpi_openmp_cuda_amd.parallel.wire import WireSlice
         from mpi_openmp_cuda_amd.utils.synthetic import fill_codes
 
@@ -139,10 +140,10 @@ class HostArrays:
         else:
             def mk(name, dtype, count):
                 return np.empty(count, dtype=dtype)
-        # letters: random codes 1..26, encoded once (5-bit packed, narrow lengths) like final's parser does
+        # letters: random codes 1..26, encoded once (P24 groups, narrow lengths) like final's parser does
         letters = np.empty(total, dtype=np.uint8)
         fill_codes(letters, seed)
-        self.wire = WireSlice(lengths, letters, packed=packed, narrow=narrow, alloc=mk)
+        self.wire = WireSlice(lengths, letters, letter_format=letter_format, narrow=narrow, alloc=mk)
         self.check_letters = letters[:min(total, 1 << 22)].copy()  # kept for the untimed verification
         del letters
 
@@ -231,7 +232,7 @@ def main():
     lengths = rrng.integers(shape.l2_min, shape.l2_max + 1, size=R, dtype=np.int64)
     tag = os.environ.get("MASTER_PORT", str(os.getpid()))
     progress(f"generating {R} records per rank")
-    host = HostArrays(tag, rank, lengths, bool(args.shm), args.packed, args.seed + 101 + rank, bool(args.narrow),
+    host = HostArrays(tag, rank, lengths, bool(args.shm), args.letters, args.seed + 101 + rank, bool(args.narrow),
                       hip_alloc=args.host_alloc == "hip")
     wire = host.wire
     progress(f"{wire.total} letters per rank ready")
@@ -348,7 +349,7 @@ def main():
             "host_arrays": "hip_host_malloc" if host.bufs else ("shm" if host.shm else "private"),
             "result_format": fmt,
             "lengths_bits": wire.len_bits,
-            "letters": "packed5" if wire.packed else "bytes",
+            "letters": wire.letter_format,
             "rank0_numa_node": numa,
             "rccl_world": dist.get_world_size() if (distributed and nccl) else (1 if nccl else None),
             "dist_backend": ("nccl" if nccl else "gloo") if distributed else "none",

@@ -657,6 +657,8 @@ void Job::run_sliced(BulkParser& parser, int64_t first_index) {
   fault_.at("distribute", r);
   const bool narrow_guess = gpu && n > 0 && L1 <= 200 && slice.letters <= 32 * n;
   HostRegion letters, sparse, len16, dense, lens;
+  int letters_pack = 5;      // GPU ranks: 24 = P24 groups, 5 = 5-bit packed
+  int64_t letter_bytes = 0;
   RecordBatch cpu_batch;
   FillReport rep;
   if (n > 0) {
@@ -665,15 +667,20 @@ void Job::run_sliced(BulkParser& parser, int64_t first_index) {
       cpu_batch.offsets.resize(static_cast<size_t>(n) + 1);
       rep = parser.fill_slice(slice, cpu_batch.codes.data(), nullptr, cpu_batch.offsets.data());
     } else {
-      letters = HostRegion(static_cast<size_t>(packed5_bytes(slice.letters)) + 16, numa);
+      // letters as P24 groups (4.8 bits each) for the streaming kernel, else 5-bit packed
+      const int pack = narrow_guess ? 24 : 5;
+      const int64_t lbytes = pack == 24 ? packed24_bytes(slice.letters) : packed5_bytes(slice.letters);
+      letters = HostRegion(static_cast<size_t>(lbytes) + 16, numa);
+      letters_pack = pack;
+      letter_bytes = lbytes;
       if (narrow_guess) {
         sparse = HostRegion(8 * static_cast<size_t>(sparse_count(n, kSparseShift)), numa);
         len16 = HostRegion(2 * static_cast<size_t>(n), numa);
         rep = parser.fill_slice(slice, nullptr, letters.as<uint8_t>(), nullptr, sparse.as<int64_t>(),
-                                len16.as<uint16_t>());
+                                len16.as<uint16_t>(), pack);
       } else {
         dense = HostRegion(8 * (static_cast<size_t>(n) + 1), numa);
-        rep = parser.fill_slice(slice, nullptr, letters.as<uint8_t>(), dense.as<int64_t>());
+        rep = parser.fill_slice(slice, nullptr, letters.as<uint8_t>(), dense.as<int64_t>(), nullptr, nullptr, pack);
       }
     }
   }
@@ -713,7 +720,8 @@ void Job::run_sliced(BulkParser& parser, int64_t first_index) {
   ResultFormat fmt = ResultFormat::R12;
   if (gpu && n > 0) {
     wb.letters = letters.as<uint8_t>();
-    wb.packed5 = true;
+    wb.packed24 = letters_pack == 24;
+    wb.packed5 = letters_pack == 5;
     wb.n = n;
     wb.min_l2 = rep.min_len;
     wb.max_l2 = rep.max_len;
@@ -728,11 +736,16 @@ void Job::run_sliced(BulkParser& parser, int64_t first_index) {
       wb.len_bits = bits;
       wb.len_base = bits == 8 ? 0 : rep.min_len;
     } else {
-      if (narrow_guess) {  // guessed wrong: CSR offsets after all (staged pipeline)
+      if (narrow_guess) {  // guessed wrong: CSR offsets and 5-bit letters after all (staged pipeline)
         sparse = HostRegion();
         len16 = HostRegion();
         dense = HostRegion(8 * (static_cast<size_t>(n) + 1), numa);
+        letter_bytes = packed5_bytes(slice.letters);
+        letters = HostRegion(static_cast<size_t>(letter_bytes) + 16, numa);
         parser.fill_slice(slice, nullptr, letters.as<uint8_t>(), dense.as<int64_t>());
+        wb.letters = letters.as<uint8_t>();
+        wb.packed24 = false;
+        wb.packed5 = true;
       }
       wb.offsets = dense.as<int64_t>();
     }
@@ -758,7 +771,7 @@ void Job::run_sliced(BulkParser& parser, int64_t first_index) {
           pinned_bytes_ += bytes;
         }
       };
-      pin(wb.letters, packed5_bytes(slice.letters));
+      pin(wb.letters, letter_bytes);
       pin(wb.offsets, 8 * wb.offset_entries());
       pin(wb.lengths, wb.length_bytes());
       pin(res.mine(), fb * n);

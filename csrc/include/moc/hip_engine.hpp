@@ -82,11 +82,12 @@ class HipEngine {
   // codes + offsets[i]); `offsets` has n+1 absolute entries.
   void solve(const uint8_t* codes, const int64_t* offsets, int64_t n, Result* out);
   // General form: optional narrow lengths — len_bits 8 (uint8, max L2 <= 255) or 4 (two per byte, low
-  // nibble first, record i = len_base + nibble) — results in `fmt`. With `packed5`, `codes` is a 5-bit
-  // packed stream (moc::pack5; char j at bit 5j) instead of one byte per letter. R2 results are encoded
-  // for the hints' [min_l2, max_l2] (or the batch's own range): stats().r2 holds the parameters.
+  // nibble first, record i = len_base + nibble) — results in `fmt`. `packed`: 1 = `codes` is a 5-bit
+  // packed stream (moc::pack5; char j at bit 5j), 2 = P24 groups (moc::pack24), 0 = one byte per letter.
+  // R2 results are encoded for the hints' [min_l2, max_l2] (or the batch's own range): stats().r2 holds
+  // the parameters.
   void solve_ex(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths, int64_t n, void* out,
-                ResultFormat fmt, const BatchHints& hints = {}, bool packed5 = false, int len_bits = 8,
+                ResultFormat fmt, const BatchHints& hints = {}, int packed = 0, int len_bits = 8,
                 int len_base = 0);
   // Any wire-format batch (moc/wire.hpp): packed or byte letters, dense or sparse offsets, narrow lengths.
   // Sparse offsets stream zero-copy when the buffers are pinned and the swipe kernel takes the batch;

@@ -84,13 +84,14 @@ class BulkParser {
 
   // ---- pass 2
   AreaSlice slice(int64_t rec_begin, int64_t rec_end) const;
-  // Encodes slice s: letters as bytes into codes[0..s.letters) and/or 5-bit packed into
-  // packed5[0..packed5_bytes(s.letters)) (either may be null). Record boundaries (each output optional):
-  // dense offsets[0..s.records] rebased to 0; sparse offsets (moc/wire.hpp, stride 2^kSparseShift)
+  // Encodes slice s: letters as bytes into codes[0..s.letters) and/or packed into `packed` (either may be
+  // null): `pack` 5 = 5-bit packed, packed[0..packed5_bytes(s.letters)); 24 = P24 groups (moc::pack24),
+  // packed[0..packed24_bytes(s.letters)). Record boundaries (each output optional): dense
+  // offsets[0..s.records] rebased to 0; sparse offsets (moc/wire.hpp, stride 2^kSparseShift)
   // sparse[0..sparse_count(s.records, kSparseShift)); lengths len16[0..s.records), saturated at 65535
   // (the report's max_len tells whether they are exact).
-  FillReport fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* packed5, int64_t* offsets,
-                        int64_t* sparse = nullptr, uint16_t* len16 = nullptr) const;
+  FillReport fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* packed, int64_t* offsets,
+                        int64_t* sparse = nullptr, uint16_t* len16 = nullptr, int pack = 5) const;
   // Throws the error a sequential reader would report first for this report (`first` = the report's
   // slice start; validates the score range for its longest record).
   void check(const FillReport& r) const;

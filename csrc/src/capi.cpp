@@ -109,6 +109,13 @@ int moc_pack5(const uint8_t* codes, int64_t n, uint8_t* out) {
 int moc_unpack5(const uint8_t* packed, int64_t begin, int64_t n, uint8_t* out) {
   return guard([&] { moc::unpack5(packed, begin, n, out); });
 }
+int64_t moc_packed24_bytes(int64_t n_chars) { return moc::packed24_bytes(n_chars); }
+int moc_pack24(const uint8_t* codes, int64_t n, uint8_t* out) {
+  return guard([&] { moc::pack24(codes, n, out); });
+}
+int moc_unpack24(const uint8_t* packed, int64_t begin, int64_t n, uint8_t* out) {
+  return guard([&] { moc::unpack24(packed, begin, n, out); });
+}
 
 int moc_score_table(const int32_t* weights4, int32_t* lut1024, uint8_t* cls1024) {
   return guard([&] {
@@ -311,13 +318,13 @@ int moc_engine_solve(void* e, const uint8_t* codes, const int64_t* offsets, int6
 }
 
 int moc_engine_solve_ex(void* e, const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths, int len_bits,
-                        int len_base, int64_t n, void* out, int fmt, int64_t min_l2, int64_t max_l2, int packed5) {
+                        int len_base, int64_t n, void* out, int fmt, int64_t min_l2, int64_t max_l2, int packed) {
   return guard([&] {
     moc::BatchHints h;
     h.min_l2 = min_l2;
     h.max_l2 = max_l2;
     static_cast<moc::HipEngine*>(e)->solve_ex(codes, offsets, lengths, n, out, static_cast<moc::ResultFormat>(fmt), h,
-                                              packed5 != 0, len_bits, len_base);
+                                              packed, len_bits, len_base);
   });
 }
 

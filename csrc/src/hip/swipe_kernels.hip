@@ -46,12 +46,15 @@ struct SwipeLayout {
   int copy_elems = 0;   // 27 * row
   int prof_bytes = 0;   // 8 shifted copies of the Dt profile
   int s_off = 0;        // int8 LUT (32 x 32, column 31 = 0) + Seq1 codes (31 past Seq1): anchor diagonal
-  int loff_off = 0, codes_off = 0, res_off = 0, total = 0;
+  int loff_off = 0, codes_off = 0, res_off = 0, raw_off = 0, total = 0;  // raw: P24 groups as loaded
 };
 
 inline int al16(int x) { return (x + 15) & ~15; }
 
-SwipeLayout swipe_layout(int L1, int noff, int l2w, int tile_records, int codes_cap, int fb) {
+// P24 tiles: the loaded group bytes (3 per 5 letters, + alignment) of at most codes_cap letters
+inline int p24_raw_cap(int codes_cap) { return 3 * (codes_cap / 5 + 2) + 32; }
+
+SwipeLayout swipe_layout(int L1, int noff, int l2w, int tile_records, int codes_cap, int fb, bool p24) {
   SwipeLayout l;
   // a multiple of 64 int16 (8 chunks of 16 B) so the per-letter XOR swizzle of chunk indices stays in the row
   l.row = (std::max(L1, 4 * l2w) + noff + 8 + 63) & ~63;
@@ -61,7 +64,8 @@ SwipeLayout swipe_layout(int L1, int noff, int l2w, int tile_records, int codes_
   l.loff_off = l.s_off + al16(kLutInts + l.row);
   l.codes_off = l.loff_off + al16((tile_records + 1) * 4 + 64);  // + misc: 16 ints
   l.res_off = l.codes_off + al16(codes_cap);
-  l.total = l.res_off + al16(tile_records * fb);
+  l.raw_off = l.res_off + al16(tile_records * fb);
+  l.total = l.raw_off + (p24 ? al16(p24_raw_cap(codes_cap)) : 0);
   return l;
 }
 
@@ -72,8 +76,10 @@ inline int kbits_for(int l2w) {  // bits for k in the int16 keys: k <= 4*l2w
 }
 }  // namespace
 
-template <int NOFF, int L2W, bool P5>
+// LF: letter format of `a.codes` — 0 bytes, 1 5-bit packed, 2 P24 groups (decoded to bytes in LDS per tile)
+template <int NOFF, int L2W, int LF>
 __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, ShortArgs a, SwipeLayout lay) {
+  constexpr bool P5 = LF == 1, P24 = LF == 2;
   constexpr int NW = P5 ? (20 * L2W + 31) / 32 : L2W;  // record words held per lane
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   short* prof = reinterpret_cast<short*>(smem);
@@ -83,6 +89,7 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
   int* misc = loff + a.tile_records + 1;
   uint8_t* codes_l = smem + lay.codes_off;
   uint8_t* res_l = smem + lay.res_off;
+  uint8_t* raw_l = smem + lay.raw_off;  // P24: the tile's groups as loaded
   const int L1 = pv.L1;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int KB = (4 * L2W < 8) ? 3 : (4 * L2W < 16) ? 4 : (4 * L2W < 32) ? 5 : (4 * L2W < 64) ? 6 : 7;
@@ -141,8 +148,8 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
     f.end = static_cast<int64_t>((static_cast<uint64_t>(static_cast<uint32_t>(misc[11])) << 32) |
                                  static_cast<uint32_t>(misc[10]));
     record_lengths4(a, f.rb + tid * 4, min(4, max(0, f.m - tid * 4)), f.len4);
-    const int64_t b_first = P5 ? (5 * f.start) >> 3 : f.start;
-    const int64_t b_end = P5 ? (5 * f.end + 7) >> 3 : f.end;
+    const int64_t b_first = P24 ? 3 * (f.start / 5) : P5 ? (5 * f.start) >> 3 : f.start;
+    const int64_t b_end = P24 ? 3 * ((f.end + 4) / 5) : P5 ? (5 * f.end + 7) >> 3 : f.end;
     f.a0 = reinterpret_cast<uintptr_t>(a.codes + b_first) & ~uintptr_t{15};
     f.nvec = static_cast<int>((reinterpret_cast<uintptr_t>(a.codes + b_end) + 15 - f.a0) >> 4);
     MOC_DCHECK(f.nvec <= kMaxV * kBlock);
@@ -182,15 +189,18 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
     int sum = cur.len4[0] + cur.len4[1] + cur.len4[2] + cur.len4[3];
     const int incl = wave_inclusive_sum(sum, lane);
     if (lane == 63) misc[4 + wave] = incl;
-    // ---- letters -> LDS. Byte codes: char j at byte j. Packed: char j at bit 5j.
+    // ---- letters -> LDS. Byte codes: char j at byte j. Packed: char j at bit 5j. P24: the groups land in
+    //      raw_l and are decoded into bytes below (group gs = start / 5 -> codes_l[0..]).
     //      shift_b = position (bytes, or bits when P5) of the tile's first char inside the LDS copy.
 #pragma unroll
     for (int k = 0; k < kMaxV; ++k) {
       const int v = tid + k * kBlock;
-      if (v < cur.nvec) reinterpret_cast<uint4*>(codes_l)[v] = cur.v[k];
+      if (v < cur.nvec) reinterpret_cast<uint4*>(P24 ? raw_l : codes_l)[v] = cur.v[k];
     }
     const uintptr_t p0 = reinterpret_cast<uintptr_t>(a.codes + (P5 ? (5 * start) >> 3 : start));
-    const int shift_b = P5 ? static_cast<int>(8 * (p0 - cur.a0) + ((5 * start) & 7)) : static_cast<int>(p0 - cur.a0);
+    const int shift_b = P24  ? static_cast<int>(start - 5 * (start / 5))
+                        : P5 ? static_cast<int>(8 * (p0 - cur.a0) + ((5 * start) & 7))
+                             : static_cast<int>(p0 - cur.a0);
     if (tid == 0) {
       MOC_DCHECK(a.dbg_codes_end < 0 || cur.a0 + 16 * static_cast<uintptr_t>(cur.nvec) <=
                                             reinterpret_cast<uintptr_t>(a.codes) + a.dbg_codes_end);
@@ -210,8 +220,24 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
       loff[m] = excl;
       MOC_DCHECK(excl == end - start);  // lengths agree with offsets
     }
+    if (P24) {  // groups -> byte codes 1..26 (the staged bytes are complete: synchronised above)
+      const int64_t gs = start / 5;
+      const int ng = static_cast<int>((end + 4) / 5 - gs);
+      const int ro = static_cast<int>(reinterpret_cast<uintptr_t>(a.codes + 3 * gs) - cur.a0);
+      for (int g = tid; g < ng; g += kBlock) {
+        const uint8_t* r = raw_l + ro + 3 * g;
+        uint32_t v = r[0] | (static_cast<uint32_t>(r[1]) << 8) | (static_cast<uint32_t>(r[2]) << 16);
+        uint8_t* d = codes_l + 5 * g;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+          const uint32_t q = v / 26u;
+          d[j] = static_cast<uint8_t>(v - 26u * q + 1u);
+          v = q;
+        }
+      }
+    }
     // next tile: its loads are in flight while this one is scored
-    fetch(grab(), nxt);  // grab() synchronises: loff / letters are complete
+    fetch(grab(), nxt);  // grab() synchronises: loff / letters (decoded P24) are complete
 
     // ---- one record per lane
     for (int g = wave; g * 64 < m; g += 4) {
@@ -360,7 +386,7 @@ bool configure_swipe(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs
   for (int tr = max_tile; tr >= 64; tr /= 2) {
     const int cap = tr * static_cast<int>(std::max<int64_t>(max_l2, 1)) + 64;
     if (cap + 32 > kMaxV * kBlock * 16) continue;  // a tile's letters must fit the register prefetch
-    SwipeLayout l = swipe_layout(static_cast<int>(L1), ch.noff, ch.l2w, tr, cap, fb);
+    SwipeLayout l = swipe_layout(static_cast<int>(L1), ch.noff, ch.l2w, tr, cap, fb, a.packed24 != 0);
     if (l.total <= kLdsBudget) {
       a.tile_records = tr;
       a.codes_cap = cap;
@@ -375,25 +401,28 @@ bool configure_swipe(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs
 
 void preload_swipe_kernels() {
   hipFuncAttributes fa;
-  (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&swipe_search_kernel<24, 4, true>));
+  (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&swipe_search_kernel<24, 4, 1>));
+  (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&swipe_search_kernel<24, 4, 2>));
 }
 
 void launch_swipe(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStream_t stream) {
   if (a.n <= 0) return;
   const int noff = a.slot, l2w = a.rpw;
   const int fb = result_bytes(static_cast<ResultFormat>(a.fmt));
-  const SwipeLayout lay = swipe_layout(pv.L1, noff, l2w, a.tile_records, a.codes_cap, fb);
+  const SwipeLayout lay = swipe_layout(pv.L1, noff, l2w, a.tile_records, a.codes_cap, fb, a.packed24 != 0);
   const int64_t n_tiles = (a.n + a.tile_records - 1) / a.tile_records;
   const int per_cu = std::max(1, std::min(8, 160 * 1024 / std::max(lay.total, 1)));
   const int64_t blocks = std::min<int64_t>(n_tiles, static_cast<int64_t>(num_cus) * per_cu);
   const dim3 grid(static_cast<unsigned>(std::max<int64_t>(blocks, 1))), block(kBlock);
-#define MOC_SWIPE_CASE(NO, LW)                                                                              \
-  if (noff == NO && l2w == LW) {                                                                          \
-    if (a.packed5)                                                                                        \
-      hipLaunchKernelGGL((swipe_search_kernel<NO, LW, true>), grid, block, lay.total, stream, pv, a, lay); \
-    else                                                                                                  \
-      hipLaunchKernelGGL((swipe_search_kernel<NO, LW, false>), grid, block, lay.total, stream, pv, a, lay); \
-    return;                                                                                               \
+#define MOC_SWIPE_CASE(NO, LW)                                                                          \
+  if (noff == NO && l2w == LW) {                                                                      \
+    if (a.packed24)                                                                                   \
+      hipLaunchKernelGGL((swipe_search_kernel<NO, LW, 2>), grid, block, lay.total, stream, pv, a, lay); \
+    else if (a.packed5)                                                                               \
+      hipLaunchKernelGGL((swipe_search_kernel<NO, LW, 1>), grid, block, lay.total, stream, pv, a, lay); \
+    else                                                                                              \
+      hipLaunchKernelGGL((swipe_search_kernel<NO, LW, 0>), grid, block, lay.total, stream, pv, a, lay); \
+    return;                                                                                           \
   }
   MOC_SWIPE_CASE(8, 4)
   MOC_SWIPE_CASE(16, 4)

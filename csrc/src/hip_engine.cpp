@@ -502,7 +502,10 @@ bool HipEngine::direct_pointers(const WireBatch& b, void* out, int fb, dev::Shor
   const void *dc = nullptr, *doff = nullptr, *dlen = nullptr, *dout = nullptr;
   const int64_t c0 = b.first_letter(), c1 = b.end_letter(), n = b.n;
   // byte range of the letters: [b0, b1)
-  const int64_t b0 = b.packed5 ? (5 * c0) >> 3 : c0, b1 = b.packed5 ? ((5 * c1 + 7) >> 3) + 1 : c1;
+  const int64_t b0 = b.packed24 ? kP24Bytes * (c0 / kP24Letters) : b.packed5 ? (5 * c0) >> 3 : c0;
+  const int64_t b1 = b.packed24  ? kP24Bytes * ((c1 + kP24Letters - 1) / kP24Letters)
+                     : b.packed5 ? ((5 * c1 + 7) >> 3) + 1
+                                 : c1;
   if (b.device) {  // device-resident (e.g. received over RCCL): the pointers are the kernel's already
     dc = b.letters + b0;
     doff = b.offsets;
@@ -534,10 +537,11 @@ void HipEngine::solve(const uint8_t* codes, const int64_t* offsets, int64_t n, R
 }
 
 void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths, int64_t n, void* out,
-                         ResultFormat fmt, const BatchHints& hints, bool packed5, int len_bits, int len_base) {
+                         ResultFormat fmt, const BatchHints& hints, int packed, int len_bits, int len_base) {
   WireBatch b;
   b.letters = codes;
-  b.packed5 = packed5;
+  b.packed5 = packed == 1;
+  b.packed24 = packed == 2;
   b.offsets = offsets;
   b.lengths = lengths;
   b.len_bits = len_bits;
@@ -550,6 +554,7 @@ void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uin
 
 bool HipEngine::streams_packed(int64_t min_l2, int64_t max_l2) const {
   dev::ShortArgs a;
+  a.packed24 = 1;  // the widest LDS layout of the packed forms
   return have_problem_ && dev::configure_swipe(L1_, min_l2, max_l2, table_.max_abs(), a);
 }
 
@@ -599,14 +604,16 @@ void HipEngine::solve_wire(const WireBatch& batch, void* out, ResultFormat fmt) 
   a.fmt = static_cast<int32_t>(fmt);
   a.counter = d_counter_;
   a.packed5 = b.packed5 ? 1 : 0;
-  const bool swipe = dev::configure_swipe(L1_, ls.mn, ls.mx, table_.max_abs(), a, b.device || opt_.dma_stream);
+  a.packed24 = b.packed24 ? 1 : 0;
+  const bool dma = opt_.dma_stream && !b.device && !b.packed24;  // the SDMA chunker cuts 5-bit / byte streams
+  const bool swipe = dev::configure_swipe(L1_, ls.mn, ls.mx, table_.max_abs(), a, b.device || dma);
   // packed letters stream straight into the swipe kernel only; other kernels read unpacked bytes. Sparse
   // offsets need whole tiles of 2^off_shift records (the swipe tiles are powers of two >= 64).
-  const bool kernel_ok = (swipe || (!b.packed5 && dev::configure_short(L1_, ls.mn, ls.mx, a))) &&
+  const bool kernel_ok = (swipe || (!b.packed5 && !b.packed24 && dev::configure_short(L1_, ls.mn, ls.mx, a))) &&
                          (a.tile_records % (1 << b.off_shift)) == 0;
   if ((opt_.allow_direct || b.device) && kernel_ok && direct_pointers(b, out, fb, a)) {
     const dev::ProblemView pv = problem_view(ls.mx);
-    if (opt_.dma_stream && !b.device) {
+    if (dma) {
       run_dma_stream(pv, a, swipe, b, out, fb);
       wall.stop();
       stats_.total_ms = wall.total_ms();
@@ -630,6 +637,14 @@ void HipEngine::solve_wire(const WireBatch& batch, void* out, ResultFormat fmt) 
     return;
   }
   if (b.device) throw Error("device-resident wire batches stream through the swipe kernel only");
+  uvector<uint8_t> bytes;  // P24 letters: the staged pipeline takes bytes (or 5-bit packing)
+  if (b.packed24) {
+    const int64_t c0 = b.first_letter(), c1 = b.end_letter();
+    bytes.resize(static_cast<size_t>(c1) + 16);
+    unpack24(b.letters, c0, c1 - c0, bytes.data() + c0);
+    b.letters = bytes.data();
+    b.packed24 = false;
+  }
   if (b.off_shift) {  // the staged pipeline plans from dense offsets: rebuild them from the lengths
     uvector<int64_t> dense(static_cast<size_t>(n) + 1);
     expand_offsets(b.offsets, b.off_shift, b.lengths, b.len_bits, b.len_base, n, dense.data());

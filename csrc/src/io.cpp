@@ -334,7 +334,11 @@ struct PieceOut {
 }  // namespace
 
 FillReport BulkParser::fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* packed5, int64_t* offs, int64_t* sparse,
-                                  uint16_t* len16) const {
+                                  uint16_t* len16, int pack) const {
+  if (pack != 5 && pack != 24) throw Error("fill_slice: pack must be 5 or 24");
+  // letters per group and bytes per group of the packed stream: 8 -> 5 (5-bit), 5 -> 3 (P24)
+  const bool p24 = pack == 24;
+  const int64_t G = p24 ? kP24Letters : 8, GB = p24 ? kP24Bytes : 5;
   if (offs) offs[0] = 0;
   constexpr int64_t kSparseMask = (int64_t{1} << kSparseShift) - 1;
   const int np = static_cast<int>(s.pieces.size());
@@ -358,24 +362,31 @@ FillReport BulkParser::fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* p
       if (codes) std::memcpy(codes + base, stage.data(), static_cast<size_t>(hi - base));
       int64_t cur = base;
       if (!head_done) {  // letters before the piece's first whole group: fixed up after the loop
-        const int64_t g0 = (a + 7) & ~int64_t{7}, hend = std::min(g0, hi);
+        const int64_t g0 = (a + G - 1) / G * G, hend = std::min(g0, hi);
         if (hend < g0 && !final) return;
         for (int64_t c = cur; c < hend; ++c) po.stragglers.emplace_back(c, stage[static_cast<size_t>(c - base)]);
         cur = hend;
         head_done = true;
       }
-      const int64_t ng = (hi - cur) / 8;
+      const int64_t ng = (hi - cur) / G;
       const uint8_t* src = stage.data() + (cur - base);
-      uint8_t* dst = packed5 + 5 * (cur / 8);
-      for (int64_t g = 0; g < ng; ++g) {
-        uint64_t x;
-        std::memcpy(&x, src + 8 * g, 8);
-        x = compress8(x);
-        // 8-byte stores run 3 zero bytes into the next group, which the next store rewrites; the last
-        // group of the run writes its 5 bytes only (the next group may belong to another piece)
-        std::memcpy(dst + 5 * g, &x, g + 1 < ng ? 8 : 5);
+      uint8_t* dst = packed5 + GB * (cur / G);
+      if (p24) {
+        for (int64_t g = 0; g < ng; ++g) {
+          const uint32_t v = p24_group(src + 5 * g);  // < 2^24: the 4-byte store's top byte is 0
+          std::memcpy(dst + 3 * g, &v, g + 1 < ng ? 4 : 3);
+        }
+      } else {
+        for (int64_t g = 0; g < ng; ++g) {
+          uint64_t x;
+          std::memcpy(&x, src + 8 * g, 8);
+          x = compress8(x);
+          // 8-byte stores run 3 zero bytes into the next group, which the next store rewrites; the last
+          // group of the run writes its 5 bytes only (the next group may belong to another piece)
+          std::memcpy(dst + 5 * g, &x, g + 1 < ng ? 8 : 5);
+        }
       }
-      cur += 8 * ng;
+      cur += G * ng;
       if (final) {
         for (int64_t c = cur; c < hi; ++c) po.stragglers.emplace_back(c, stage[static_cast<size_t>(c - base)]);
       } else {
@@ -455,16 +466,27 @@ FillReport BulkParser::fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* p
   if (packed5) {
     // groups holding letters of two pieces (or the slice's last, partial group): zeroed, then assembled
     for (const PieceOut& po : out)
-      for (const auto& sc : po.stragglers) std::memset(packed5 + 5 * (sc.first / 8), 0, 5);
+      for (const auto& sc : po.stragglers) std::memset(packed5 + GB * (sc.first / G), 0, static_cast<size_t>(GB));
+    static constexpr uint32_t kPow26[5] = {1u, 26u, 676u, 17576u, 456976u};
     for (const PieceOut& po : out)
       for (const auto& sc : po.stragglers) {
+        if (p24) {  // add (code - 1) * 26^j to the group value
+          uint8_t* q = packed5 + kP24Bytes * (sc.first / kP24Letters);
+          uint32_t v = q[0] | (static_cast<uint32_t>(q[1]) << 8) | (static_cast<uint32_t>(q[2]) << 16);
+          v += (sc.second > 1 ? sc.second - 1u : 0u) * kPow26[sc.first % kP24Letters];
+          q[0] = static_cast<uint8_t>(v);
+          q[1] = static_cast<uint8_t>(v >> 8);
+          q[2] = static_cast<uint8_t>(v >> 16);
+          continue;
+        }
         const int64_t bit = 5 * sc.first;
         const uint32_t v = static_cast<uint32_t>(sc.second & 31u) << (bit & 7);
         packed5[bit >> 3] |= static_cast<uint8_t>(v);
         packed5[(bit >> 3) + 1] |= static_cast<uint8_t>(v >> 8);
       }
-    const int64_t used = 5 * ((s.letters + 7) / 8);
-    std::memset(packed5 + used, 0, static_cast<size_t>(packed5_bytes(s.letters) - used));
+    const int64_t used = GB * ((s.letters + G - 1) / G);
+    const int64_t total = p24 ? packed24_bytes(s.letters) : packed5_bytes(s.letters);
+    std::memset(packed5 + used, 0, static_cast<size_t>(total - used));
   }
   if (sparse) sparse[sparse_count(s.records, kSparseShift) - 1] = s.letters;
   return r;

@@ -177,6 +177,56 @@ def test_packed5_letters(shape, n, pinned):
     eng.close()
 
 
+@pytest.mark.parametrize("shape,n", [("input6", 250_003), ("input1", 3000), ("input4", 200), ("input3", 20)])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_packed24_letters(shape, n, pinned):
+    # P24 letters (base-26 groups, 5 per 3 bytes): decoded per tile in LDS by the swipe kernel (pinned, tiny
+    # problems), or unpacked on the host for the staged pipeline (everything else)
+    from mpi_openmp_cuda_amd.models.problem import pack24
+
+    prob = make_synthetic(shape, n, seed=n + 1)
+    packed = pack24(prob.codes)
+    eng = HipSearchEngine(device=0, chunk_records=max(n // 3, 1))
+    eng.set_problem(prob.weights, prob.seq1)
+    out = np.zeros(prob.n, dtype=np.dtype([("score", "<i4"), ("n", "<i4"), ("k", "<i4")]))
+    if pinned:
+        eng.pin(packed, prob.offsets, out)
+    eng.solve(packed, prob.offsets, out=out, packed24=True)
+    st = eng.stats()
+    assert np.array_equal(as_triples(out), as_triples(search_cpu(prob))), st
+    if pinned and shape == "input6":
+        assert st["direct"] == 1 and st["kernels"] == ["swipe"]
+    eng.close()
+
+
+@pytest.mark.parametrize("L1,lo,hi,w", [(26, 6, 11, (4, 3, 2, 10)), (12, 1, 14, (3, 1, 1, 2)),
+                                        (40, 20, 32, (5, 2, 3, 4)), (60, 10, 16, (2, 2, 1, 3)),
+                                        (9, 9, 9, (7, 1, 2, 3))])
+@pytest.mark.parametrize("letters", ["p24", "p5"])
+def test_swipe_wire_slices(L1, lo, hi, w, letters):
+    # the headline's wire path (parallel/wire.py: narrow lengths, R2/R4 results, zero-copy) across swipe
+    # instantiations (NOFF 8..64, record widths <= 16 / <= 32) for both packed letter formats
+    from mpi_openmp_cuda_amd._lib import Pinned
+    from mpi_openmp_cuda_amd.parallel.wire import WireSlice
+
+    rng = np.random.default_rng(L1 * 7 + lo)
+    s1 = "".join(chr(65 + x) for x in rng.integers(0, 26, L1))
+    lens = rng.integers(max(1, min(lo, hi)), max(lo, hi) + 1, 20000)
+    recs = ["".join(chr(65 + x) for x in rng.integers(0, 26, n)) for n in lens]
+    prob = Problem.from_strings(w, s1, recs)
+    eng = HipSearchEngine(device=0)
+    eng.set_problem(prob.weights, prob.seq1)
+    ws = WireSlice.from_csr(prob.codes, prob.offsets, letter_format=letters)
+    ws.alloc_results(eng)
+    with Pinned(*ws.arrays()):
+        ws.solve(eng)
+    st = eng.stats()
+    assert np.array_equal(ws.triples(eng), as_triples(search_cpu(prob))), st
+    if L1 - min(lo, hi) + 1 <= 64:
+        assert st["kernels"] == ["swipe"] and st["direct"] == 1, st
+    eng.close()
+
+
 @pytest.mark.parametrize("fmt", ["r8", "r4", "auto"])
 def test_staged_formats(engine, fmt):
     prob = make_synthetic("input1", 5000, seed=4)

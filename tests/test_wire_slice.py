@@ -16,8 +16,8 @@ def test_length_fields_round_trip(lo, hi, narrow, bits):
     lengths = rng.integers(lo, hi + 1, size=n)
     letters = rng.integers(1, 27, size=int(lengths.sum()), dtype=np.uint8)
     assert length_bits(int(lengths.min()), int(lengths.max()), narrow) == bits
-    for packed in (True, False):
-        ws = WireSlice(lengths, letters, packed=packed, narrow=narrow)
+    for fmt in ("p24", "p5", "bytes"):
+        ws = WireSlice(lengths, letters, letter_format=fmt, narrow=narrow)
         assert ws.len_bits == bits
         assert np.array_equal(ws.decoded_lengths(), lengths)
         assert np.array_equal(ws.offsets[1:], np.cumsum(lengths))
@@ -34,7 +34,7 @@ def test_from_csr_slice_of_absolute_offsets():
     assert ws.n == e - b
     assert np.array_equal(ws.decoded_lengths(), np.diff(prob.offsets[b:e + 1]))
     assert np.array_equal(ws.letters(), prob.codes[prob.offsets[b]:prob.offsets[e]])
-    assert ws.packed and ws.len_bits == 3 and ws.len_base == 6
+    assert ws.letter_format == "p24" and ws.len_bits == 3 and ws.len_base == 6
 
 
 def test_custom_allocator_places_every_array():
@@ -46,5 +46,23 @@ def test_custom_allocator_places_every_array():
 
     prob = make_synthetic("input6", 100, seed=1)
     ws = WireSlice.from_csr(prob.codes, prob.offsets, alloc=alloc)
-    assert names == ["offsets", "lengths3", "codes5"]
+    assert names == ["offsets", "lengths3", "codes24"]
     assert len(ws.arrays()) == 3  # results come later (their format is the engine's choice)
+
+
+def test_p24_groups():
+    from mpi_openmp_cuda_amd.models.problem import pack24, packed24_bytes, unpack24
+
+    rng = np.random.default_rng(5)
+    for n in (0, 1, 4, 5, 6, 1000, 1 << 16):
+        codes = rng.integers(1, 27, size=n, dtype=np.uint8)
+        p = pack24(codes)
+        assert p.shape[0] == packed24_bytes(n) == 3 * ((n + 4) // 5) + 16
+        assert not p[3 * ((n + 4) // 5):].any()  # slack zeroed
+        for b in (0, 1, 3, n // 2):
+            if b <= n:
+                assert np.array_equal(unpack24(p, b, n - b), codes[b:])
+    # group value: sum (code - 1) * 26^i, little endian
+    p = pack24(np.array([2, 1, 1, 1, 26], np.uint8))
+    v = int(p[0]) | int(p[1]) << 8 | int(p[2]) << 16
+    assert v == 1 + 25 * 26 ** 4
