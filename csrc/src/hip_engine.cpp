@@ -214,10 +214,17 @@ void HipEngine::set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, S
   pbytes = (2 * static_cast<int64_t>(prof.entries.size()) + 15) & ~int64_t{15};
   prof16_overhang_ = t16 ? static_cast<int>(overhang) : 0;
   const size_t total = t16 ? prof_off + static_cast<size_t>(pbytes) : prof_off;
-  image_.assign(total, 0);
-  std::memcpy(image_.data(), table_.lut.data(), lut_bytes);
-  if (L1) std::memcpy(image_.data() + s1_off, seq1, static_cast<size_t>(L1));
-  if (t16) std::memcpy(image_.data() + prof_off, prof.entries.data(), sizeof(uint16_t) * prof.entries.size());
+  std::vector<uint8_t> next(total, 0);
+  std::memcpy(next.data(), table_.lut.data(), lut_bytes);
+  if (L1) std::memcpy(next.data() + s1_off, seq1, static_cast<size_t>(L1));
+  if (t16) std::memcpy(next.data() + prof_off, prof.entries.data(), sizeof(uint16_t) * prof.entries.size());
+  // the same problem again (one per job step of a repeated job): the device image is already current —
+  // no device-wide synchronisation, no copy
+  if (have_problem_ && next == image_) {
+    prof16_bytes_ = prof16_lds_bytes_;
+    return;
+  }
+  image_.swap(next);
   // Kernels of the previous problem may still be queued — on our streams or on a solve_device caller's —
   // and read the image in place: let them finish before it is overwritten.
   MOC_HIP_CHECK(hipDeviceSynchronize());
