@@ -278,6 +278,8 @@ class Job {
   void run_batch(RecordBatch* rb, int64_t n, int64_t total_chars, int64_t first_index);
   void run_sliced(BulkParser& parser, int64_t first_index);
   void batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, bool cp);
+  void gpu_window_slice(const uint8_t* w_codes, const int64_t* offs, int64_t n, Result* res, ResultFormat& fmt,
+                        R2Params& r2);
   std::vector<int64_t> make_bounds(const int64_t* offsets, int64_t n, bool cp);
   void batch_mpi(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds, bool cp);
   void batch_rccl(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds, bool cp);
@@ -482,6 +484,39 @@ std::vector<int64_t> Job::make_bounds(const int64_t* offsets, int64_t n, bool cp
 }
 
 void Job::batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, bool cp) {
+  if (ctx_.size == 1 && !cp && rb && !parser_) {  // one rank: no window to share, search the batch in place
+    const int64_t* offs = rb->offsets.data();
+    const int64_t L1 = static_cast<int64_t>(eng_.seq1.size());
+    int64_t cells = 0;
+#pragma omp parallel for reduction(+ : cells) schedule(static) if (n > 65536)
+    for (int64_t i = 0; i < n; ++i) cells += record_cells(L1, offs[i + 1] - offs[i]);
+    cells_ += cells;
+    pt_.begin("compute");
+    fault_.at("compute", 0);
+    Stopwatch sw;
+    sw.start();
+    HostRegion res(12 * static_cast<size_t>(std::max<int64_t>(n, 1)), eng_.gpu ? eng_.hip->numa_node() : -1);
+    ResultFormat fmt = ResultFormat::R12;
+    R2Params r2{};
+    Result* out = res.as<Result>();
+    if (eng_.gpu && n > 0)
+      gpu_window_slice(rb->codes.data(), offs, n, out, fmt, r2);
+    else if (n > 0)
+      eng_.solve(rb->codes.data(), offs, n, out);
+    sw.stop();
+    compute_ms_ += sw.total_ms();
+    pt_.end();
+    {  // the batch's letters go back to the OS while its results print
+      auto spent = std::make_shared<RecordBatch>(std::move(*rb));
+      rel_.defer([spent]() mutable { spent.reset(); });
+      *rb = RecordBatch{};
+    }
+    pt_.begin("print");
+    write_results(out_, std::vector<ResultRun>{ResultRun{out, fmt, r2, n}}, first_index_);
+    pt_.end();
+    res.set_releaser(&rel_);
+    return;
+  }
   // layout: offsets[(N+1)] | results[N] (or keys[N] in cp mode) | codes[total]   (8-byte aligned sections)
   const int64_t off_bytes = 8 * (n + 1);
   const int64_t res_bytes = ((12 * n) + 7) & ~int64_t{7};
@@ -548,25 +583,47 @@ void Job::batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, bool cp) {
     pt_.end();
   } else {
     const int64_t my_b = bounds[ctx_.rank], my_n = bounds[ctx_.rank + 1] - my_b;
-    // GPU ranks: page-lock the window so the engine streams its slice zero-copy (one kernel reading the
-    // letters over PCIe and writing the results in place) instead of staging through device buffers.
-    bool pinned = false;
-    if (eng_.gpu && pin_window_ && my_n > 0) {
-      try {
-        eng_.hip->pin(win->base(), static_cast<size_t>(win->bytes()));
-        pinned = true;
-      } catch (const std::exception& e) {
-        MOC_LOG_WARN("could not page-lock the shared window (%s); using the staged pipeline", e.what());
-      }
+    // this rank's results go to the start of its R12 region of the window, in the format it chose
+    ResultFormat fmt = ResultFormat::R12;
+    R2Params r2{};
+    if (eng_.gpu && my_n > 0) {
+      gpu_window_slice(w_codes, w_offs + my_b, my_n, w_res + my_b, fmt, r2);
+    } else if (my_n > 0) {
+      eng_.solve(w_codes, w_offs + my_b, my_n, w_res + my_b);
     }
-    eng_.solve(w_codes, w_offs + my_b, my_n, w_res + my_b);
-    if (pinned) eng_.hip->unpin_all();
     sw.stop();
     pt_.end();
     pt_.begin("gather");
     fault_.at("gather", ctx_.rank);
+    int64_t info[4] = {static_cast<int64_t>(fmt), r2.smin, r2.kw, r2.j};
+    std::vector<int64_t> infos(static_cast<size_t>(4 * ctx_.size));
+    allgather_i64(info, 4, infos.data());
     win->fence();
     pt_.end();
+    compute_ms_ += sw.total_ms();
+    if (spent_parser_ || spent_text_)
+      rel_.defer([parser = std::move(spent_parser_), text = std::move(spent_text_)]() mutable {
+        parser.reset();
+        text.reset();
+      });
+    win->discard(0, off_bytes);
+    win->discard(off_bytes + res_bytes, total_chars);
+    if (ctx_.rank == kRoot) {
+      std::vector<ResultRun> runs(static_cast<size_t>(ctx_.size));
+      for (int q = 0; q < ctx_.size; ++q) {
+        const int64_t* x = infos.data() + 4 * q;
+        runs[q] = ResultRun{w_res + bounds[q], static_cast<ResultFormat>(x[0]),
+                            R2Params{static_cast<int32_t>(x[1]), static_cast<int32_t>(x[2]), static_cast<int32_t>(x[3])},
+                            bounds[q + 1] - bounds[q]};
+      }
+      pt_.begin("print");
+      write_results(out_, runs, first_index_);
+      pt_.end();
+    }
+    pt_.begin("release");
+    win.reset();  // collective: unmaps the node-shared window
+    pt_.end();
+    return;
   }
   compute_ms_ += sw.total_ms();
   // printing reads only the results: the input, offsets and letters go back to the OS while it runs
@@ -581,6 +638,81 @@ void Job::batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, bool cp) {
   pt_.begin("release");
   win.reset();  // collective: unmaps the node-shared window
   pt_.end();
+}
+
+// A GPU rank's slice of a node-shared CSR window (streaming batches): encoded into the headline's wire
+// formats in NUMA-local memory when the streaming kernel takes the batch (P24 letters, narrow lengths,
+// sparse offsets; narrow results written to the start of `res`), else the window's own bytes and offsets.
+// Either way only this slice's pieces are page-locked — never the whole window.
+void Job::gpu_window_slice(const uint8_t* w_codes, const int64_t* offs, int64_t n, Result* res, ResultFormat& fmt,
+                           R2Params& r2) {
+  const int64_t c0 = offs[0], c1 = offs[n];
+  int64_t mn = INT64_MAX, mx = 0;
+#pragma omp parallel for reduction(min : mn) reduction(max : mx) schedule(static) if (n > 65536)
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t L = offs[i + 1] - offs[i];
+    mn = std::min(mn, L);
+    mx = std::max(mx, L);
+  }
+  const int numa = eng_.hip->numa_node();
+  auto pin = [&](const void* ptr, int64_t bytes) {
+    if (!pin_window_ || !ptr || bytes <= 0) return;
+    try {
+      eng_.hip->pin(ptr, static_cast<size_t>(bytes));
+      pinned_bytes_ += bytes;
+    } catch (const std::exception& e) {
+      MOC_LOG_WARN("could not page-lock this rank's slice (%s); using the staged pipeline", e.what());
+    }
+  };
+  GpuSolveStats gs;
+  if (mx <= 255 && eng_.hip->streams_packed(mn, mx)) {
+    const int64_t letters = c1 - c0;
+    HostRegion p24(static_cast<size_t>(packed24_bytes(letters)) + 16, numa);
+    pack24(w_codes + c0, letters, p24.as<uint8_t>());
+    const int bits = narrow_length_bits(mn, mx);
+    const int64_t base = bits == 8 ? 0 : mn;
+    HostRegion lens(static_cast<size_t>(narrow_lengths_bytes(n, bits)) + 8, numa);
+    pack_lengths(offs, n, bits, base, lens.as<uint8_t>());
+    const int64_t ns = sparse_count(n, kSparseShift);
+    HostRegion sparse(8 * static_cast<size_t>(ns), numa);
+    int64_t* sp = sparse.as<int64_t>();
+    for (int64_t j = 0; j < ns; ++j) sp[j] = offs[std::min(j << kSparseShift, n)] - c0;
+    WireBatch wb;
+    wb.letters = p24.as<uint8_t>();
+    wb.packed24 = true;
+    wb.offsets = sp;
+    wb.off_shift = kSparseShift;
+    wb.lengths = lens.as<uint8_t>();
+    wb.len_bits = bits;
+    wb.len_base = base;
+    wb.n = n;
+    wb.min_l2 = mn;
+    wb.max_l2 = mx;
+    fmt = eng_.hip->result_format(mn, mx);
+    pin(wb.letters, wb.letter_bytes());
+    pin(sp, 8 * ns);
+    pin(wb.lengths, wb.length_bytes());
+    pin(res, static_cast<int64_t>(result_bytes(fmt)) * n);
+    eng_.hip->solve_wire(wb, res, fmt);
+    gs = eng_.hip->last_stats();
+    r2 = gs.r2;
+    // unregistered now: the window's memory (the results' pages) is freed by its collective teardown
+    eng_.hip->unpin_all();
+    p24.set_releaser(&rel_);
+    lens.set_releaser(&rel_);
+    sparse.set_releaser(&rel_);
+  } else {
+    pin(w_codes + c0, c1 - c0);
+    pin(offs, 8 * (n + 1));
+    pin(res, 12 * n);
+    eng_.hip->solve(w_codes, offs, n, res);
+    gs.kernel_ms = eng_.hip->last_kernel_ms();
+    eng_.hip->unpin_all();
+    fmt = ResultFormat::R12;
+  }
+  eng_.kernel_ms += gs.kernel_ms;
+  h2d_bytes_ += gs.h2d_bytes;
+  d2h_bytes_ += gs.d2h_bytes;
 }
 
 // Bulk job on one node, records split into contiguous rank slices (transport shm, partition cost|even).
@@ -962,6 +1094,11 @@ void Job::batch_rccl(RecordBatch* rb, int64_t n, int64_t total_chars, const std:
 void Job::report(const Header& h) {
   double mx[2] = {compute_ms_, eng_.kernel_ms};
   MPI_Reduce(ctx_.rank == kRoot ? MPI_IN_PLACE : mx, mx, 2, MPI_DOUBLE, MPI_MAX, kRoot, ctx_.world);
+  // every mode: what each rank page-locked and moved host->device over the job (sliced mode also has
+  // its per-rank records and pin times, gathered with its results)
+  int64_t moved[2] = {pinned_bytes_, h2d_bytes_};
+  std::vector<int64_t> all_moved(static_cast<size_t>(2 * ctx_.size));
+  MPI_Gather(moved, 2, MPI_INT64_T, all_moved.data(), 2, MPI_INT64_T, kRoot, ctx_.world);
   if (ctx_.rank != kRoot || !flags_.get_bool("timing", false)) return;
   const double wall_s = total_.total_ms() / 1e3;
   auto list = [](const std::vector<int64_t>& v) {
@@ -970,9 +1107,17 @@ void Job::report(const Header& h) {
     return s + "]";
   };
   std::string per_rank;
-  if (!rank_records_.empty())  // sliced mode: what each rank owned, page-locked and moved host->device
+  if (!rank_records_.empty()) {  // sliced mode: what each rank owned, page-locked and moved host->device
     per_rank = ", \"rank_records\": " + list(rank_records_) + ", \"rank_pinned_bytes\": " + list(rank_pinned_) +
                ", \"rank_h2d_bytes\": " + list(rank_h2d_) + ", \"rank_pin_us\": " + list(rank_pin_us_);
+  } else {
+    std::vector<int64_t> pinned(static_cast<size_t>(ctx_.size)), h2d(static_cast<size_t>(ctx_.size));
+    for (int q = 0; q < ctx_.size; ++q) {
+      pinned[q] = all_moved[2 * q];
+      h2d[q] = all_moved[2 * q + 1];
+    }
+    per_rank = ", \"rank_pinned_bytes\": " + list(pinned) + ", \"rank_h2d_bytes\": " + list(h2d);
+  }
   std::fprintf(stderr,
                "{\"timing\": %s, \"ranks\": %d, \"nodes\": %d, \"engine\": \"%s\", \"transport\": \"%s\", "
                "\"partition\": \"%s\", \"collectives\": \"%s\", \"sliced\": %s, \"batches\": %lld, \"first_index\": %lld, \"records\": %lld, "

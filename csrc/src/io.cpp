@@ -63,7 +63,7 @@ int64_t parse_int(const char* b, const char* e, const char* what) {
 
 size_t read_regular_into(FILE* f, char* dst, size_t want) {
   const long pos = std::ftell(f);
-  if (pos < 0 || want <= (size_t{64} << 20)) {
+  if (pos < 0 || want <= (size_t{8} << 20)) {
     const size_t got = std::fread(dst, 1, want, f);
     if (got < want && std::ferror(f)) throw Error("error while reading input stream");
     return got;
@@ -71,7 +71,9 @@ size_t read_regular_into(FILE* f, char* dst, size_t want) {
   // large file: the copy out of the page cache split over the OpenMP threads (one fread is a
   // single-threaded, page-faulting memcpy of the whole file)
   const int fd = fileno(f);
-  constexpr size_t kChunk = size_t{16} << 20;
+  // chunks of 1..16 MiB, at least two per thread
+  const size_t kChunk = std::clamp(want / (2 * static_cast<size_t>(std::max(1, omp_get_max_threads()))), size_t{1} << 20,
+                                   size_t{16} << 20);
   const int64_t nchunks = static_cast<int64_t>((want + kChunk - 1) / kChunk);
   std::vector<size_t> got(static_cast<size_t>(nchunks), 0);
   int failed = 0;
@@ -720,7 +722,9 @@ int64_t StreamReader::next_batch(int64_t max_records, RecordBatch& out, int64_t 
       if (pos_ > 0 && keep) std::memmove(buf_.data(), buf_.data() + pos_, keep);
       if (keep == buf_.size()) buf_.resize(buf_.size() * 2);
       pos_ = 0;
-      const size_t rd = std::fread(buf_.data() + keep, 1, buf_.size() - keep, f_);
+      // a regular file refills with parallel preads (one fread is a single-threaded copy out of the page
+      // cache: it was the streaming mode's critical path at 1.1 G letters)
+      const size_t rd = read_regular_into(f_, buf_.data() + keep, buf_.size() - keep);
       len_ = keep + rd;
       if (len_ < buf_.size()) {
         if (std::ferror(f_)) throw Error("error while reading input stream");

@@ -413,7 +413,7 @@ def test_final_cli_hip_two_ranks_offsets():
 
 @pytest.mark.parametrize("np_", [1, 2])
 def test_final_cli_zero_copy_window(tmp_path, np_):
-    # GPU ranks encode their own slice (5-bit letters, narrow lengths, sparse offsets), page-lock only that
+    # GPU ranks encode their own slice (P24 letters, narrow lengths, sparse offsets), page-lock only that
     # slice and stream it zero-copy; output == CPU. Two ranks share the one test GPU (--device=0).
     import json
 
@@ -430,9 +430,31 @@ def test_final_cli_zero_copy_window(tmp_path, np_):
     for q in range(np_):
         n = d["rank_records"][q]
         letters = int(prob.offsets[b[q + 1]] - prob.offsets[b[q]])
-        # this rank's slice only: packed letters + 1/64 offsets + 3-bit lengths + R2 results
-        assert 5 * letters // 8 <= d["rank_pinned_bytes"][q] <= 5 * letters // 8 + n * (8 / 64 + 3 / 8 + 2) + 64, d
-        assert d["rank_h2d_bytes"][q] <= 5 * letters // 8 + 3 * n // 8 + 64, d
+        # this rank's slice only: P24 letters + 1/64 offsets + 3-bit lengths + R2 results
+        assert 3 * letters // 5 <= d["rank_pinned_bytes"][q] <= 3 * letters // 5 + n * (8 / 64 + 3 / 8 + 2) + 64, d
+        assert d["rank_h2d_bytes"][q] <= 3 * letters // 5 + 3 * n // 8 + 64, d
+
+
+@pytest.mark.parametrize("np_", [1, 2])
+def test_final_cli_streaming_slices(tmp_path, np_):
+    # streaming batches (--batch-records): every GPU rank re-encodes its slice of each batch's node-shared
+    # window into the wire formats and page-locks only those pieces (never the whole window)
+    import json
+
+    prob = make_synthetic("input6", 120_000, seed=9)
+    path = tmp_path / "in6.txt"
+    path.write_text(prob.to_text())
+    r = run_final(["--backend=hip", "--transport=shm", f"--input={path}", "--timing", "--device=0",
+                   "--batch-records=50000"], stdin_bytes=b"", np_=np_)
+    assert r.returncode == 0, r.stderr.decode()
+    assert r.stdout.decode() == format_results(search_cpu(prob))
+    d = json.loads([l for l in r.stderr.decode().splitlines() if l.startswith("{")][-1])
+    assert d["batches"] == 3 and d["records"] == prob.n
+    # summed over the batches: about this rank's share of P24 letters + narrow lengths/offsets + R2 results
+    # (a whole-window pin would be ~1 + 8 + 12 bytes per letter/record for every rank)
+    total = int(prob.offsets[-1])
+    assert 0 < d["max_rank_kernel_ms"]
+    assert sum(d["rank_pinned_bytes"]) <= 3 * total // 5 + prob.n * (8 / 64 + 3 / 8 + 2) + 1024 * np_ * 3, d
 
 
 @pytest.mark.parametrize("pinned", [False, True])
