@@ -12,10 +12,11 @@ One timed step = the search of one complete job over the global batch (reference
      (zero-copy over its own PCIe link), runs the gfx950 search kernel, and writes the (score, n, k)
      results back into the node-shared result array the root prints from,
   4. an all-reduce of the per-rank record counts closes the job (the reference's MPI_Gather point).
-The records are held in the wire formats `./final` writes while it parses (5-bit letters, 3-bit lengths,
+The records are held in the wire formats `./final` writes while it parses (P24 letters: 5 per 3 bytes, 3-bit lengths,
 R2 results; csrc/include/moc/wire.hpp): encoding them is the untimed set-up here, as parsing and printing
 are outside `./final`'s compute phase, whose `--timing` shows the same kernel time for the same letters
-(profiles/final_scale_1.1G_r2_async_engine.log: 14.2 ms kernel at 1.14 G letters; this bench 14.3 ms/step).
+(profiles/final_scale_1.1G_r2_p24.log: 13.8 ms kernel at 1.14 G letters; profiles/bench_input6_1gpu_1.1G_p24.log:
+13.9 ms/step here).
 Weak scaling: --records-per-gpu is fixed per rank, the global batch grows with N.
 
 Run: python bench.py [--gpus N --steps K --warmup W]. With N > 1 and no torch.distributed environment

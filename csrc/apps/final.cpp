@@ -718,7 +718,7 @@ void Job::gpu_window_slice(const uint8_t* w_codes, const int64_t* offs, int64_t 
 // Bulk job on one node, records split into contiguous rank slices (transport shm, partition cost|even).
 // Every rank encodes its OWN slice straight from the node-shared input text into its own buffers, in the
 // wire formats its engine streams (SURVEY.md §7.3 / moc/wire.hpp):
-//   GPU rank: 5-bit packed letters + 3/4/8-bit lengths + sparse offsets (1 per 64 records) in private,
+//   GPU rank: P24 letters (5 per 3 bytes) + 3/4/8-bit lengths + sparse offsets (1 per 64 records) in private,
 //             huge-page memory on its GPU's NUMA node, page-locked (only this slice), results in the
 //             narrowest format (R2/R4/R8/R12) in this rank's segment of a node-shared result window;
 //   CPU rank: byte letters + CSR offsets, results as R12.
