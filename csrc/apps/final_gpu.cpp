@@ -267,14 +267,20 @@ class GpuRankImpl final : public GpuRank {
   // the engine, once its construction has finished (any thread; the first caller applies a kept problem)
   HipEngine& engine() const {
     std::call_once(ready_, [this] {
-      std::unique_ptr<HipEngine> e = pending_engine_.get();  // rethrows a construction error
+      std::unique_ptr<HipEngine> e;
+      try {
+        e = pending_engine_.get();  // rethrows a construction error: kept for every caller
+      } catch (const std::exception& ex) {
+        start_error_ = ex.what();
+        return;
+      }
       std::lock_guard<std::mutex> lock(mu_);
       if (problem_.set) e->set_problem(problem_.w, problem_.seq1.data(), static_cast<int64_t>(problem_.seq1.size()),
                                        problem_.sem);
       problem_ = Problem{};
       engine_ = std::move(e);
     });
-    if (!engine_) throw Error("the HIP engine failed to start");
+    if (!engine_) throw Error("the HIP engine failed to start: " + start_error_);
     return *engine_;
   }
 
@@ -286,6 +292,7 @@ class GpuRankImpl final : public GpuRank {
   mutable std::mutex mu_;
   mutable Problem problem_;
   mutable std::unique_ptr<HipEngine> engine_;
+  mutable std::string start_error_;
   std::unique_ptr<DeviceSearch> ds_;  // destroyed after dc_ (declared before it)
   std::unique_ptr<DeviceComm> dc_;
   std::future<std::unique_ptr<RcclDeviceComm>> pending_;  // connect in flight (init_rccl_begin)
