@@ -885,11 +885,35 @@ void Job::run_sliced(BulkParser& parser, int64_t first_index) {
   }
   pt_.end();
 
-  // ---- results: this rank's segment of the node-shared window
+  // ---- results: with several ranks and an --output file every rank prints its own rows into the file
+  // (distributed print: formatting split over the ranks, no result window); otherwise this rank's
+  // segment of a node-shared window, printed by the root
   const int fb = result_bytes(fmt);
   pt_.begin("results");
-  SegmentWindow res(ctx_, fb * n, numa);
-  res.set_releaser(&rel_);
+  int64_t dp[2] = {0, 0};  // {distributed print, the file offset of the first row}
+  if (r == kRoot && p > 1 && out_ != stdout) {
+    struct stat st {};
+    const int fd = fileno(out_);
+    const int fl = fcntl(fd, F_GETFL);
+    std::fflush(out_);
+    if (fl >= 0 && !(fl & O_APPEND) && fstat(fd, &st) == 0 && S_ISREG(st.st_mode)) {
+      dp[0] = 1;
+      dp[1] = static_cast<int64_t>(std::ftell(out_));
+    }
+  }
+  bcast_bytes(dp, sizeof dp, kRoot, ctx_.world);
+  std::unique_ptr<SegmentWindow> seg;
+  HostRegion own;
+  char* res_mine = nullptr;
+  if (dp[0]) {
+    own = HostRegion(static_cast<size_t>(std::max<int64_t>(fb * n, 16)), numa);
+    own.set_releaser(&rel_);
+    res_mine = own.data();
+  } else {
+    seg = std::make_unique<SegmentWindow>(ctx_, fb * n, numa);
+    seg->set_releaser(&rel_);
+    res_mine = seg->mine();
+  }
   pt_.end();
   // GPU ranks page-lock this slice's pieces only (the registration faults in and locks every page)
   pt_.begin("pin");
@@ -906,7 +930,7 @@ void Job::run_sliced(BulkParser& parser, int64_t first_index) {
       pin(wb.letters, letter_bytes);
       pin(wb.offsets, 8 * wb.offset_entries());
       pin(wb.lengths, wb.length_bytes());
-      pin(res.mine(), fb * n);
+      pin(res_mine, fb * n);
     } catch (const std::exception& e) {
       MOC_LOG_WARN("could not page-lock this rank's slice (%s); using the staged pipeline", e.what());
     }
@@ -920,13 +944,13 @@ void Job::run_sliced(BulkParser& parser, int64_t first_index) {
   GpuSolveStats gs;
   if (n > 0) {
     if (gpu) {
-      eng_.hip->solve_wire(wb, res.mine(), fmt);
+      eng_.hip->solve_wire(wb, res_mine, fmt);
       gs = eng_.hip->last_stats();
       eng_.kernel_ms += gs.kernel_ms;
       h2d_bytes_ += gs.h2d_bytes;
       d2h_bytes_ += gs.d2h_bytes;
     } else {
-      solve_batch_cpu(eng_.table, eng_.seq1.data(), L1, cpu_batch, reinterpret_cast<Result*>(res.mine()), eng_.sem,
+      solve_batch_cpu(eng_.table, eng_.seq1.data(), L1, cpu_batch, reinterpret_cast<Result*>(res_mine), eng_.sem,
                       eng_.threads);
     }
   }
@@ -955,20 +979,15 @@ void Job::run_sliced(BulkParser& parser, int64_t first_index) {
                      static_cast<int64_t>(pin_sw.total_ms() * 1000.0)};
   std::vector<int64_t> infos(static_cast<size_t>(8 * p));
   allgather_i64(info, 8, infos.data());
-  res.fence();
+  if (seg) seg->fence();
   pt_.end();
-  if (r == kRoot) {
-    std::vector<ResultRun> runs(static_cast<size_t>(p));
+  if (r == kRoot) {  // --timing: what every rank owned, page-locked and moved
     rank_pinned_.assign(static_cast<size_t>(p), 0);
     rank_h2d_.assign(static_cast<size_t>(p), 0);
     rank_records_.assign(static_cast<size_t>(p), 0);
     rank_pin_us_.assign(static_cast<size_t>(p), 0);
     for (int q = 0; q < p; ++q) {
       const int64_t* x = infos.data() + 8 * q;
-      runs[q].data = res.segment(q);
-      runs[q].n = x[0];
-      runs[q].fmt = static_cast<ResultFormat>(x[1]);
-      runs[q].r2 = R2Params{static_cast<int32_t>(x[2]), static_cast<int32_t>(x[3]), static_cast<int32_t>(x[4])};
       rank_records_[q] = x[0];
       rank_pinned_[q] = x[5];
       rank_h2d_[q] = x[6];
@@ -980,12 +999,48 @@ void Job::run_sliced(BulkParser& parser, int64_t first_index) {
       rel_.defer([t]() mutable { t.reset(); });
       text_ = uvector<char>();
     }
+  }
+  if (dp[0]) {  // every rank: its rows at its offset of the output file (sizes all-gathered first)
+    pt_.begin("print");
+    const std::vector<ResultRun> mine = {ResultRun{res_mine, fmt, gs.r2, n}};
+    int64_t bytes = formatted_bytes(mine, b0);
+    std::vector<int64_t> sizes(static_cast<size_t>(p));
+    allgather_i64(&bytes, 1, sizes.data());
+    int64_t at = dp[1], total = 0;
+    for (int q = 0; q < p; ++q) {
+      if (q < r) at += sizes[q];
+      total += sizes[q];
+    }
+    int fd = r == kRoot ? fileno(out_) : -1;
+    if (r != kRoot && n > 0) {
+      fd = ::open(flags_.get("output", "").c_str(), O_WRONLY | O_CLOEXEC);
+      if (fd < 0) throw Error("cannot open --output " + flags_.get("output", "") + " on rank " + std::to_string(r));
+    }
+    if (n > 0) write_results_at(fd, at, mine, b0);
+    if (r != kRoot && fd >= 0) ::close(fd);
+    MPI_Barrier(ctx_.world);  // every row is in the file
+    if (r == kRoot) std::fseek(out_, static_cast<long>(dp[1] + total), SEEK_SET);
+    pt_.end();
+    pt_.begin("release");
+    text_win_.reset();  // collective (node-shared input text)
+    pt_.end();
+    return;
+  }
+  if (r == kRoot) {
+    std::vector<ResultRun> runs(static_cast<size_t>(p));
+    for (int q = 0; q < p; ++q) {
+      const int64_t* x = infos.data() + 8 * q;
+      runs[q].data = seg->segment(q);
+      runs[q].n = x[0];
+      runs[q].fmt = static_cast<ResultFormat>(x[1]);
+      runs[q].r2 = R2Params{static_cast<int32_t>(x[2]), static_cast<int32_t>(x[3]), static_cast<int32_t>(x[4])};
+    }
     pt_.begin("print");
     write_results(out_, runs, first_index);
     pt_.end();
   }
   pt_.begin("release");
-  res.fence();  // nobody unmaps a segment the root still prints from
+  seg->fence();  // nobody unmaps a segment the root still prints from
   text_win_.reset();  // collective (node-shared input text)
   pt_.end();
 }

@@ -165,5 +165,10 @@ void write_results(FILE* f, const Result* results, int64_t n, int64_t first_inde
 // decoded row by row while formatting.
 void write_results(FILE* f, const std::vector<ResultRun>& runs, int64_t first_index = 0);
 std::string format_results(const Result* results, int64_t n, int64_t first_index = 0);
+// Exact bytes of the rows write_results produces for these runs (a sizing pass, no formatting).
+int64_t formatted_bytes(const std::vector<ResultRun>& runs, int64_t first_index = 0);
+// Formats the rows and writes them into the regular file `fd` at byte offset `at` (parallel pwrite), so
+// several processes can each write their own rows of one output file; returns the bytes written.
+int64_t write_results_at(int fd, int64_t at, const std::vector<ResultRun>& runs, int64_t first_index = 0);
 
 }  // namespace moc

@@ -1157,4 +1157,90 @@ void write_results(FILE* f, const std::vector<ResultRun>& runs, int64_t first_in
   std::fflush(f);
 }
 
+namespace {
+inline int64_t dec_digits(uint64_t u) {
+  int64_t d = 1;
+  while (u >= 10) {
+    u /= 10;
+    ++d;
+  }
+  return d;
+}
+inline int64_t int_chars(int64_t v) { return v < 0 ? 1 + dec_digits(static_cast<uint64_t>(-(v + 1)) + 1) : dec_digits(static_cast<uint64_t>(v)); }
+// total decimal digits of the integers [a, b)
+int64_t digits_of_range(int64_t a, int64_t b) {
+  int64_t total = 0;
+  for (int64_t lo = 1, d = 1; lo <= b && d <= 19; lo *= 10, ++d) {
+    const int64_t hi = d == 19 ? INT64_MAX : lo * 10;  // numbers with d digits: [lo, hi) (0 counts as 1 digit)
+    const int64_t s = std::max(a, d == 1 ? int64_t{0} : lo), e = std::min(b, hi);
+    if (e > s) total += d * (e - s);
+  }
+  return total;
+}
+}  // namespace
+
+int64_t formatted_bytes(const std::vector<ResultRun>& runs, int64_t first_index) {
+  const RowSource src(runs);
+  const int64_t n = src.total();
+  int64_t tails = 0;
+  for (size_t r = 0; r < runs.size(); ++r) {
+    const ResultRun& run = runs[r];
+    int64_t t = 0;
+    if (src.tails[r]) {
+      const uint16_t* codes = static_cast<const uint16_t*>(run.data);
+      const uint8_t* len = src.tails[r]->len.data();
+#pragma omp parallel for reduction(+ : t) schedule(static) if (run.n > 65536)
+      for (int64_t i = 0; i < run.n; ++i) t += len[codes[i]];
+    } else {
+#pragma omp parallel for reduction(+ : t) schedule(static) if (run.n > 65536)
+      for (int64_t i = 0; i < run.n; ++i) {
+        const Result x = decode_result(run.data, run.fmt, run.r2, i);
+        t += 9 + int_chars(x.score) + 5 + int_chars(x.n) + 5 + int_chars(x.k) + 1;
+      }
+    }
+    tails += t;
+  }
+  return n + digits_of_range(first_index, first_index + n) + tails;  // '#' + index + tail per row
+}
+
+int64_t write_results_at(int fd, int64_t at, const std::vector<ResultRun>& runs, int64_t first_index) {
+  // write_results' parallel-file path at a given offset: several processes fill one file, each its rows
+  const RowSource src(runs);
+  const int64_t n = src.total();
+  const int nparts = n > 65536 ? std::max(1, omp_get_max_threads()) : 1;
+  const int64_t kBlock = int64_t{65536} * nparts;
+  std::vector<uvector<char>> parts(static_cast<size_t>(nparts));
+  std::vector<size_t> used(static_cast<size_t>(nparts) + 1, 0);
+  std::atomic<bool> write_error{false};
+  int64_t pos = at;
+  for (int64_t b = 0; b < n && !write_error; b += kBlock) {
+    const int64_t e = std::min(n, b + kBlock), m = e - b;
+#pragma omp parallel for schedule(static, 1) num_threads(nparts)
+    for (int t = 0; t < nparts; ++t) {
+      const int64_t rb = b + m * t / nparts, re = b + m * (t + 1) / nparts;
+      uvector<char>& buf = parts[t];
+      buf.resize(static_cast<size_t>(re - rb) * kMaxRow + kSlack);
+      char* p = src.format(buf.data(), rb, re, first_index);
+      used[t + 1] = static_cast<size_t>(p - buf.data());
+    }
+    used[0] = 0;
+    for (int q = 0; q < nparts; ++q) used[q + 1] += used[q];
+#pragma omp parallel for schedule(static, 1) num_threads(nparts)
+    for (int t = 0; t < nparts; ++t) {
+      const size_t len = used[t + 1] - used[t];
+      for (size_t done = 0; done < len;) {
+        const ssize_t w = pwrite(fd, parts[t].data() + done, len - done, pos + static_cast<off_t>(used[t] + done));
+        if (w <= 0) {
+          write_error = true;
+          break;
+        }
+        done += static_cast<size_t>(w);
+      }
+    }
+    pos += static_cast<int64_t>(used[nparts]);
+  }
+  if (write_error) throw Error("error while writing the results");
+  return pos - at;
+}
+
 }  // namespace moc

@@ -1,6 +1,8 @@
 // Native unit tests of the host core (SURVEY.md §4.3 "unit (C++)"): score table vs the spec groups,
 // parser and streaming reader edge cases, partitioner, packed-key ordering, 5-bit packing, CPU engine vs
 // the brute-force replay of the reference loops. No GPU, no MPI. Run: `make unit` or `ctest`.
+#include <unistd.h>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
@@ -658,6 +660,19 @@ void test_write_runs() {
     CHECK(got == "head\n" + want + "tail\n");
   }
   unsetenv("MOC_WRITER");
+  // the sizing pass and the offset writer (ranks writing their own rows of one file), also across
+  // index digit boundaries
+  for (int64_t first : {int64_t{41}, int64_t{999990}, int64_t{99999999999}}) {
+    const std::string w2 = format_results(all.data(), static_cast<int64_t>(all.size()), first);
+    CHECK(formatted_bytes(runs, first) == static_cast<int64_t>(w2.size()));
+    FILE* f = std::tmpfile();
+    const int64_t at = 7;
+    CHECK(write_results_at(fileno(f), at, runs, first) == static_cast<int64_t>(w2.size()));
+    std::string got(w2.size(), '\0');
+    CHECK(pread(fileno(f), got.data(), got.size(), at) == static_cast<ssize_t>(got.size()));
+    std::fclose(f);
+    CHECK(got == w2);
+  }
 }
 
 int main() {
