@@ -397,10 +397,11 @@ def test_rccl_driver_emulated_streaming_and_synthetic(np_, tmp_path):
 @pytest.mark.parametrize("np_", [2, 3, 8])
 @pytest.mark.parametrize("i", [2, 3, 6])
 def test_distributed_print_to_output_file(tmp_path, np_, i):
-    # several ranks + --output: every rank writes its own rows at its offset of the file (sizes all-gathered);
+    # --parallel-print, several ranks + --output: every rank writes its own rows at its offset of the file (sizes all-gathered);
     # ranks without records (input2 has one) write nothing, a longer old file is cut to the new length
     out = tmp_path / "out.txt"
     out.write_text("x" * 100000)
-    r = run_final(["--backend=cpu", f"--input={input_path(i)}", f"--output={out}"], stdin_bytes=b"", np_=np_)
+    r = run_final(["--backend=cpu", f"--input={input_path(i)}", f"--output={out}", "--parallel-print"], stdin_bytes=b"",
+                  np_=np_)
     assert r.returncode == 0, r.stderr.decode()
     assert r.stdout == b"" and out.read_text() == expected(i)
