@@ -33,7 +33,9 @@ using namespace kc;
 namespace {
 constexpr int kBlock = 256;
 constexpr int kMaxTile = 2048;  // records per tile: up to 8 per thread in the tile's length scan
-constexpr int kRpt = kMaxTile / 256;
+// length fields per thread in a tile's scan: 8 for the packed letter forms (host streams take 2048-record
+// tiles), 4 for byte letters (device-resident batches: 512-record tiles, fewer registers)
+constexpr int rpt_of(int lf) { return lf == 0 ? 4 : 8; }
 constexpr int kLdsBudget = 80 * 1024;
 constexpr int kMaxV = 4;  // 16-byte letter vectors per thread per tile (register prefetch)
 
@@ -81,6 +83,7 @@ inline int kbits_for(int l2w) {  // bits for k in the int16 keys: k <= 4*l2w
 template <int NOFF, int L2W, int LF>
 __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, ShortArgs a, SwipeLayout lay) {
   constexpr bool P5 = LF == 1, P24 = LF == 2;
+  constexpr int kRpt = rpt_of(LF);
   constexpr int NW = P5 ? (20 * L2W + 31) / 32 : L2W;  // record words held per lane
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   short* prof = reinterpret_cast<short*>(smem);
@@ -148,12 +151,13 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
                                    static_cast<uint32_t>(misc[8]));
     f.end = static_cast<int64_t>((static_cast<uint64_t>(static_cast<uint32_t>(misc[11])) << 32) |
                                  static_cast<uint32_t>(misc[10]));
-    {  // this thread's kRpt records' lengths, 4 per load
-      int (&l4a)[4] = *reinterpret_cast<int(*)[4]>(&f.lens[0]);
-      int (&l4b)[4] = *reinterpret_cast<int(*)[4]>(&f.lens[4]);
-      const int r0 = tid * kRpt;
-      record_lengths4(a, f.rb + r0, min(4, max(0, f.m - r0)), l4a);
-      record_lengths4(a, f.rb + r0 + 4, min(4, max(0, f.m - r0 - 4)), l4b);
+#pragma unroll
+    for (int h = 0; h < kRpt / 4; ++h) {  // this thread's kRpt records' lengths, 4 per load
+      int l4[4];
+      const int r0 = tid * kRpt + 4 * h;
+      record_lengths4(a, f.rb + r0, min(4, max(0, f.m - r0)), l4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) f.lens[4 * h + q] = l4[q];
     }
     const int64_t b_first = P24 ? 3 * (f.start / 5) : P5 ? (5 * f.start) >> 3 : f.start;
     const int64_t b_end = P24 ? 3 * ((f.end + 4) / 5) : P5 ? (5 * f.end + 7) >> 3 : f.end;
@@ -392,8 +396,9 @@ bool configure_swipe(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs
   const int fb = result_bytes(static_cast<ResultFormat>(a.fmt));
   // host streams: 2048-record tiles (P24 letters fit the register prefetch; 3.59 vs 3.69 ms per headline
   // step at 1024), device-resident: 512 (more blocks per CU); MOC_SWIPE_TILE overrides (64..2048)
-  int max_tile = hbm ? 512 : kMaxTile;
-  if (const char* v = std::getenv("MOC_SWIPE_TILE")) max_tile = std::max(64, std::min(kMaxTile, std::atoi(v)));
+  const int tile_cap = 256 * rpt_of(a.packed24 ? 2 : a.packed5 ? 1 : 0);
+  int max_tile = std::min(hbm ? 512 : kMaxTile, tile_cap);
+  if (const char* v = std::getenv("MOC_SWIPE_TILE")) max_tile = std::max(64, std::min(tile_cap, std::atoi(v)));
   for (int tr = max_tile; tr >= 64; tr /= 2) {
     const int cap = tr * static_cast<int>(std::max<int64_t>(max_l2, 1)) + 64;
     // a tile's letter bytes must fit the register prefetch (P24: 3 bytes per 5 letters)
