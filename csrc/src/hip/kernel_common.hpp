@@ -249,6 +249,18 @@ __device__ __forceinline__ void record_lengths4(const ShortArgs& a, int64_t i0, 
   for (int q = 0; q < 4; ++q) L[q] = q < n_valid ? record_length(a, i0 + q) : 0;
 }
 
+// 16-byte non-temporal (streaming) accesses: host memory read or written once over PCIe (zero-copy)
+// needs no L2 residency
+typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 nt_load16(const void* p) {
+  const u32x4_nt v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_nt*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void nt_store16(void* p, uint4 x) {
+  const u32x4_nt v = {x.x, x.y, x.z, x.w};
+  __builtin_nontemporal_store(v, reinterpret_cast<u32x4_nt*>(p));
+}
+
 // Copies a block's staged results (LDS) to the output: dwords, plus a trailing halfword for R2 tiles
 // of odd length. `dst` is 4-byte aligned (tiles start at multiples of 64 records).
 __device__ __forceinline__ void copy_results(void* dst, const uint8_t* src, int bytes, int tid, int nthreads) {
@@ -258,7 +270,7 @@ __device__ __forceinline__ void copy_results(void* dst, const uint8_t* src, int 
   if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
     const int n16 = bytes >> 4;
     for (int q = tid; q < n16; q += nthreads)
-      static_cast<uint4*>(dst)[q] = reinterpret_cast<const uint4*>(src)[q];
+      nt_store16(static_cast<uint4*>(dst) + q, reinterpret_cast<const uint4*>(src)[q]);
     done = n16 << 4;
   }
   const int nd = (bytes - done) >> 2;

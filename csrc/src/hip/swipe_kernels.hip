@@ -167,7 +167,7 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
 #pragma unroll
     for (int k = 0; k < kMaxV; ++k) {
       const int v = tid + k * kBlock;
-      if (v < f.nvec) f.v[k] = reinterpret_cast<const uint4*>(f.a0)[v];
+      if (v < f.nvec) f.v[k] = nt_load16(reinterpret_cast<const uint4*>(f.a0) + v);
     }
   };
   auto grab = [&]() -> int64_t {
