@@ -100,24 +100,6 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
   constexpr int KMASK = (1 << KB) - 1;
   constexpr int NP = NOFF / 2;  // packed accumulators
 
-  // ---- 8 shifted int16 difference-profile copies: prof[s][c][j] = Dt[c][j + s], and the plain S rows.
-  //      Rows are 128-byte multiples, so the 16-byte chunk q of every row would start on the same LDS
-  //      bank; chunk q of row c is stored at chunk q ^ (c & 7) instead, spreading the 16 lanes of a
-  //      ds_read_b128 group (16 records reading 16 rows) over 8 bank quads — 8-way -> ~2-way conflicts.
-  {
-    const int row = lay.row, ce = lay.copy_elems;
-    for (int e = tid; e < 8 * ce; e += kBlock) {
-      const int s = e / ce, rem = e - s * ce, c = rem / row, jj = rem - c * row;
-      const int j = ((((jj >> 3) ^ (c & 7)) << 3) | (jj & 7)) + s;  // element stored at jj holds column j
-      const int sj = (c >= 1 && j < L1) ? pv.lut[c * kLutStride + pv.seq1[j]] : 0;
-      const int sn = (c >= 1 && j + 1 < L1) ? pv.lut[c * kLutStride + pv.seq1[j + 1]] : 0;
-      prof[e] = static_cast<short>(sj - sn);
-    }
-    // row 0 (padding letter: steps past a lane's record) and column 31 (past Seq1) contribute 0
-    for (int e = tid; e < kLutInts; e += kBlock)
-      lut8[e] = static_cast<int8_t>((e & 31) == 31 || (e >> 5) == 0 ? 0 : pv.lut[e]);
-    for (int j = tid; j < row; j += kBlock) s1l[j] = j < L1 ? pv.seq1[j] : 31;
-  }
   const int fb = fmt_bytes(a.fmt);
   const int64_t n_tiles = (a.n + a.tile_records - 1) / a.tile_records;
   const int sem = pv.semantics;
@@ -189,7 +171,26 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
   };
 
   Fetch cur, nxt;
-  fetch(grab(), cur);
+  fetch(grab(), cur);  // the first tile's loads are in flight while the block builds its profile
+
+  // ---- 8 shifted int16 difference-profile copies: prof[s][c][j] = Dt[c][j + s], and the plain S rows.
+  //      Rows are 128-byte multiples, so the 16-byte chunk q of every row would start on the same LDS
+  //      bank; chunk q of row c is stored at chunk q ^ (c & 7) instead, spreading the 16 lanes of a
+  //      ds_read_b128 group (16 records reading 16 rows) over 8 bank quads — 8-way -> ~2-way conflicts.
+  {
+    const int row = lay.row, ce = lay.copy_elems;
+    for (int e = tid; e < 8 * ce; e += kBlock) {
+      const int s = e / ce, rem = e - s * ce, c = rem / row, jj = rem - c * row;
+      const int j = ((((jj >> 3) ^ (c & 7)) << 3) | (jj & 7)) + s;  // element stored at jj holds column j
+      const int sj = (c >= 1 && j < L1) ? pv.lut[c * kLutStride + pv.seq1[j]] : 0;
+      const int sn = (c >= 1 && j + 1 < L1) ? pv.lut[c * kLutStride + pv.seq1[j + 1]] : 0;
+      prof[e] = static_cast<short>(sj - sn);
+    }
+    // row 0 (padding letter: steps past a lane's record) and column 31 (past Seq1) contribute 0
+    for (int e = tid; e < kLutInts; e += kBlock)
+      lut8[e] = static_cast<int8_t>((e & 31) == 31 || (e >> 5) == 0 ? 0 : pv.lut[e]);
+    for (int j = tid; j < row; j += kBlock) s1l[j] = j < L1 ? pv.seq1[j] : 31;
+  }
   for (;;) {
     if (cur.t >= n_tiles) break;
     const int64_t rb = cur.rb, start = cur.start, end = cur.end;
