@@ -177,6 +177,8 @@ class HipEngine {
   void* d_image_ = nullptr;  // problem image: LUT | Seq1 | profile (views below)
   size_t d_image_cap_ = 0;
   std::vector<uint8_t> image_;
+  Weights last_w_{};                // the last set_problem's inputs: a repeat returns at once
+  std::vector<uint8_t> last_seq1_;
   int32_t* d_lut_ = nullptr;
   uint8_t* d_seq1_ = nullptr;
   uint16_t* d_prof16_ = nullptr;  // tile16 profile (null: the problem does not fit it, or MOC_TILE16=0)

@@ -174,8 +174,14 @@ void HipEngine::ensure_host(void*& ptr, size_t& cap, size_t bytes) {
 }
 
 void HipEngine::set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, Semantics sem) {
+  // the same problem again (every step of a repeated job): nothing to rebuild or upload
+  if (have_problem_ && sem == sem_ && L1 == L1_ && std::equal(w.w, w.w + 4, last_w_.w) &&
+      (L1 == 0 || std::memcmp(seq1, last_seq1_.data(), static_cast<size_t>(L1)) == 0))
+    return;
   MOC_HIP_CHECK(hipSetDevice(device_));
   if (L1 > (int64_t{1} << 30)) throw Error("Seq1 too long for the device engine");
+  last_w_ = w;
+  last_seq1_.assign(seq1, seq1 + L1);
   table_ = ScoreTable::build(w);
   min_t_ = INT32_MAX;
   max_t_ = INT32_MIN;
