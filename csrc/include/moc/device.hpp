@@ -139,6 +139,8 @@ struct ShortArgs {
   int32_t slot = 0;                   // lanes per record (max lanes_needed over the batch, <= 64)
   int32_t rpw = 0;                    // records per wave = 64 / slot
   int32_t tile_records = 0;           // records per block tile
+  int64_t tail_from = INT64_MAX;      // swipe: tiles [tail_from, ...) hold tail_records records each (set
+  int32_t tail_records = 0;           // by launch_swipe: the batch's last work is cut finer for the tail)
   int32_t codes_cap = 0;              // LDS bytes for one tile's letters (>= tile_records*max_l2+32)
   int32_t max_l2 = 0;
   int32_t packed5 = 0;                // 1: `codes` is a 5-bit packed stream (char j at bit 5j); swipe only

@@ -101,7 +101,15 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
   constexpr int NP = NOFF / 2;  // packed accumulators
 
   const int fb = fmt_bytes(a.fmt);
-  const int64_t n_tiles = (a.n + a.tile_records - 1) / a.tile_records;
+  // tiles [0, tail_from) hold tile_records records, the rest tail_records (the batch's last work, cut finer
+  // so the blocks finish together)
+  const int64_t big_end = a.tail_records ? min(a.n, a.tail_from * a.tile_records) : a.n;
+  const int64_t n_tiles = a.tail_records ? a.tail_from + (a.n - big_end + a.tail_records - 1) / a.tail_records
+                                         : (a.n + a.tile_records - 1) / a.tile_records;
+  auto tile_first = [&](int64_t t) -> int64_t {
+    return t < a.tail_from ? t * a.tile_records : big_end + (t - a.tail_from) * a.tail_records;
+  };
+  auto tile_size = [&](int64_t t) -> int64_t { return t < a.tail_from ? a.tile_records : a.tail_records; };
   const int sem = pv.semantics;
 
   // ---- tile fetch: the next tile's lengths and letters are loaded into registers while the current
@@ -125,8 +133,8 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
 #pragma unroll
     for (int q = 0; q < kRpt; ++q) f.lens[q] = 0;
     if (t >= n_tiles) return;
-    f.rb = t * a.tile_records;
-    f.m = static_cast<int>(min(static_cast<int64_t>(a.tile_records), a.n - f.rb));
+    f.rb = tile_first(t);
+    f.m = static_cast<int>(min(tile_size(t), a.n - f.rb));
     // the tile's letter range: loaded once per block by grab(), not once per wave (each load of host
     // memory is a PCIe read request of its own)
     f.start = static_cast<int64_t>((static_cast<uint64_t>(static_cast<uint32_t>(misc[9])) << 32) |
@@ -157,8 +165,8 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
       const int64_t t = atomicAdd(a.counter, 1u);
       misc[0] = static_cast<int>(t);
       if (t < n_tiles) {  // the tile's letter range [offsets[rb], offsets[rb + m]) for fetch()
-        const int64_t rb = t * a.tile_records;
-        const int64_t st = tile_offset(a, rb), en = tile_offset(a, min(rb + a.tile_records, a.n));
+        const int64_t rb = tile_first(t);
+        const int64_t st = tile_offset(a, rb), en = tile_offset(a, min(rb + tile_size(t), a.n));
         misc[8] = static_cast<int>(static_cast<uint32_t>(st));
         misc[9] = static_cast<int>(static_cast<uint64_t>(st) >> 32);
         misc[10] = static_cast<int>(static_cast<uint32_t>(en));
@@ -423,23 +431,43 @@ void preload_swipe_kernels() {
   (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&swipe_search_kernel<24, 4, 2>));
 }
 
+// MOC_SWIPE_TAIL=0 keeps every tile at full size (A/B)
+static bool tail_enabled() {
+  static const bool on = [] {
+    const char* v = std::getenv("MOC_SWIPE_TAIL");
+    return !(v && std::atoi(v) == 0);
+  }();
+  return on;
+}
+
 void launch_swipe(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStream_t stream) {
   if (a.n <= 0) return;
   const int noff = a.slot, l2w = a.rpw;
   const int fb = result_bytes(static_cast<ResultFormat>(a.fmt));
   const SwipeLayout lay = swipe_layout(pv.L1, noff, l2w, a.tile_records, a.codes_cap, fb, a.packed24 != 0);
-  const int64_t n_tiles = (a.n + a.tile_records - 1) / a.tile_records;
   const int per_cu = std::max(1, std::min(8, 160 * 1024 / std::max(lay.total, 1)));
-  const int64_t blocks = std::min<int64_t>(n_tiles, static_cast<int64_t>(num_cus) * per_cu);
+  const int64_t slots = static_cast<int64_t>(num_cus) * per_cu;
+  ShortArgs b = a;
+  // the last `slots` tiles' records go in quarter tiles: the tail of the persistent grid (blocks idling
+  // while the last tiles finish) shrinks 4x
+  const int64_t n_big = (a.n + a.tile_records - 1) / a.tile_records;
+  if (a.tile_records >= 256 && n_big > 2 * slots && tail_enabled()) {
+    b.tail_from = n_big - slots;
+    b.tail_records = a.tile_records / 4;
+  }
+  const int64_t big_end = b.tail_records ? b.tail_from * b.tile_records : b.n;
+  const int64_t n_tiles =
+      b.tail_records ? b.tail_from + (b.n - big_end + b.tail_records - 1) / b.tail_records : n_big;
+  const int64_t blocks = std::min<int64_t>(n_tiles, slots);
   const dim3 grid(static_cast<unsigned>(std::max<int64_t>(blocks, 1))), block(kBlock);
 #define MOC_SWIPE_CASE(NO, LW)                                                                          \
   if (noff == NO && l2w == LW) {                                                                      \
     if (a.packed24)                                                                                   \
-      hipLaunchKernelGGL((swipe_search_kernel<NO, LW, 2>), grid, block, lay.total, stream, pv, a, lay); \
+      hipLaunchKernelGGL((swipe_search_kernel<NO, LW, 2>), grid, block, lay.total, stream, pv, b, lay); \
     else if (a.packed5)                                                                               \
-      hipLaunchKernelGGL((swipe_search_kernel<NO, LW, 1>), grid, block, lay.total, stream, pv, a, lay); \
+      hipLaunchKernelGGL((swipe_search_kernel<NO, LW, 1>), grid, block, lay.total, stream, pv, b, lay); \
     else                                                                                              \
-      hipLaunchKernelGGL((swipe_search_kernel<NO, LW, 0>), grid, block, lay.total, stream, pv, a, lay); \
+      hipLaunchKernelGGL((swipe_search_kernel<NO, LW, 0>), grid, block, lay.total, stream, pv, b, lay); \
     return;                                                                                           \
   }
   MOC_SWIPE_CASE(8, 4)
