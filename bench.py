@@ -12,7 +12,7 @@ One timed step = the search of one complete job over the global batch (reference
      (zero-copy over its own PCIe link), runs the gfx950 search kernel, and writes the (score, n, k)
      results back into the node-shared result array the root prints from,
   4. an all-reduce of the per-rank record counts closes the job (the reference's MPI_Gather point).
-The records are held in the wire formats `./final` writes while it parses (P24 letters: 5 per 3 bytes, 3-bit lengths,
+The records are held in the wire formats `./final` writes while it parses (P33 letters: 7 per 33 bits, 3-bit lengths,
 R2 results; csrc/include/moc/wire.hpp): encoding them is the untimed set-up here, as parsing and printing
 are outside `./final`'s compute phase, whose `--timing` shows the same kernel time for the same letters
 (profiles/final_scale_1.1G_r2_p24.log: 13.8 ms kernel at 1.14 G letters; profiles/bench_input6_1gpu_1.1G_p24.log:
@@ -55,8 +55,9 @@ def parse_args():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, default) | gloo (multi-rank rehearsal)")
     ap.add_argument("--numa", type=int, default=1, help="bind each rank to its GPU's NUMA node")
-    ap.add_argument("--letters", default="p24", choices=["p24", "p5", "bytes"],
-                    help="letter wire format: base-26 groups of 5 in 3 bytes (p24), 5-bit packed (p5), bytes")
+    ap.add_argument("--letters", default="p33", choices=["p33", "p24", "p5", "bytes"],
+                    help="letter wire format: 7 letters per 33-bit field (p33), base-26 groups of 5 in 3 bytes "
+                         "(p24), 5-bit packed (p5), bytes")
     ap.add_argument("--narrow", type=int, default=1,
                     help="1: narrowest wire formats that fit (4-bit lengths, R2 results); 0: uint8 lengths, R4")
     ap.add_argument("--dry-launch", action="store_true",

@@ -108,6 +108,7 @@ const char* kUsage =
     "  --max-l1=L --max-l2=L       explicit length limits (0 = unlimited)\n"
     "  --device=K                  force device K (default: node-local rank %% devices)\n"
     "  --device-map=a,b,...        node-local rank i -> device map[i %% len]\n"
+    "  --letters=p33|p24           letter code of GPU slices (p33: 7 letters per 33 bits; p24: 5 per 3 bytes)\n"
     "  --pin-window=0|1            page-lock the shm window so GPU ranks stream it zero-copy (default 1)\n"
     "  --chunk-records=R --chunk-bytes=B   pipeline chunk sizes\n"
     "  --threads=T                 OpenMP threads (default: OMP_NUM_THREADS / all)\n"
@@ -117,7 +118,7 @@ const char* kUsage =
 
 const std::vector<std::string> kKnown = {
     "backend", "collectives", "parallel-print", "gpu-min-cells", "gpu-prewarm-bytes", "transport", "semantics", "partition", "batch-records", "batch-chars", "skip-records", "input",
-    "output", "timing", "strict-limits", "max-l1", "max-l2", "device", "device-map", "pin-window", "chunk-records",
+    "output", "timing", "strict-limits", "max-l1", "max-l2", "device", "device-map", "letters", "pin-window", "chunk-records",
     "chunk-bytes", "threads", "log-level", "inject-fault", "help"};
 
 struct Header {
@@ -279,6 +280,12 @@ class Job {
   void run_batch(RecordBatch* rb, int64_t n, int64_t total_chars, int64_t first_index);
   void run_sliced(BulkParser& parser, int64_t first_index);
   void batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, bool cp);
+  // group letter code of GPU slices for the streaming kernel: 33 (P33 fields, default) or 24 (--letters=p24)
+  int group_pack() const {
+    const std::string v = to_lower(flags_.get("letters", "p33"));
+    if (v != "p33" && v != "p24") throw Error("--letters must be p33|p24");
+    return v == "p24" ? 24 : 33;
+  }
   void gpu_window_slice(const uint8_t* w_codes, const int64_t* offs, int64_t n, Result* res, ResultFormat& fmt,
                         R2Params& r2);
   std::vector<int64_t> make_bounds(const int64_t* offsets, int64_t n, bool cp);
@@ -642,7 +649,7 @@ void Job::batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, bool cp) {
 }
 
 // A GPU rank's slice of a node-shared CSR window (streaming batches): encoded into the headline's wire
-// formats in NUMA-local memory when the streaming kernel takes the batch (P24 letters, narrow lengths,
+// formats in NUMA-local memory when the streaming kernel takes the batch (P33 letters, narrow lengths,
 // sparse offsets; narrow results written to the start of `res`), else the window's own bytes and offsets.
 // Either way only this slice's pieces are page-locked — never the whole window.
 void Job::gpu_window_slice(const uint8_t* w_codes, const int64_t* offs, int64_t n, Result* res, ResultFormat& fmt,
@@ -668,8 +675,12 @@ void Job::gpu_window_slice(const uint8_t* w_codes, const int64_t* offs, int64_t 
   GpuSolveStats gs;
   if (mx <= 255 && eng_.hip->streams_packed(mn, mx)) {
     const int64_t letters = c1 - c0;
-    HostRegion p24(static_cast<size_t>(packed24_bytes(letters)) + 16, numa);
-    pack24(w_codes + c0, letters, p24.as<uint8_t>());
+    const bool p33 = group_pack() == 33;
+    HostRegion pk(static_cast<size_t>(p33 ? packed33_bytes(letters) : packed24_bytes(letters)) + 16, numa);
+    if (p33)
+      pack33(w_codes + c0, letters, pk.as<uint8_t>());
+    else
+      pack24(w_codes + c0, letters, pk.as<uint8_t>());
     const int bits = narrow_length_bits(mn, mx);
     const int64_t base = bits == 8 ? 0 : mn;
     HostRegion lens(static_cast<size_t>(narrow_lengths_bytes(n, bits)) + 8, numa);
@@ -679,8 +690,9 @@ void Job::gpu_window_slice(const uint8_t* w_codes, const int64_t* offs, int64_t 
     int64_t* sp = sparse.as<int64_t>();
     for (int64_t j = 0; j < ns; ++j) sp[j] = offs[std::min(j << kSparseShift, n)] - c0;
     WireBatch wb;
-    wb.letters = p24.as<uint8_t>();
-    wb.packed24 = true;
+    wb.letters = pk.as<uint8_t>();
+    wb.packed24 = !p33;
+    wb.packed33 = p33;
     wb.offsets = sp;
     wb.off_shift = kSparseShift;
     wb.lengths = lens.as<uint8_t>();
@@ -699,7 +711,7 @@ void Job::gpu_window_slice(const uint8_t* w_codes, const int64_t* offs, int64_t 
     r2 = gs.r2;
     // unregistered now: the window's memory (the results' pages) is freed by its collective teardown
     eng_.hip->unpin_all();
-    p24.set_releaser(&rel_);
+    pk.set_releaser(&rel_);
     lens.set_releaser(&rel_);
     sparse.set_releaser(&rel_);
   } else {
@@ -719,7 +731,7 @@ void Job::gpu_window_slice(const uint8_t* w_codes, const int64_t* offs, int64_t 
 // Bulk job on one node, records split into contiguous rank slices (transport shm, partition cost|even).
 // Every rank encodes its OWN slice straight from the node-shared input text into its own buffers, in the
 // wire formats its engine streams (SURVEY.md §7.3 / moc/wire.hpp):
-//   GPU rank: P24 letters (5 per 3 bytes) + 3/4/8-bit lengths + sparse offsets (1 per 64 records) in private,
+//   GPU rank: P33 letters (56 per 33 bytes) + 3/4/8-bit lengths + sparse offsets (1 per 64 records) in private,
 //             huge-page memory on its GPU's NUMA node, page-locked (only this slice), results in the
 //             narrowest format (R2/R4/R8/R12) in this rank's segment of a node-shared result window;
 //   CPU rank: byte letters + CSR offsets, results as R12.
@@ -790,7 +802,7 @@ void Job::run_sliced(BulkParser& parser, int64_t first_index) {
   fault_.at("distribute", r);
   const bool narrow_guess = gpu && n > 0 && L1 <= 200 && slice.letters <= 32 * n;
   HostRegion letters, sparse, len16, dense, lens;
-  int letters_pack = 5;      // GPU ranks: 24 = P24 groups, 5 = 5-bit packed
+  int letters_pack = 5;      // GPU ranks: 33 = P33 fields, 24 = P24 groups, 5 = 5-bit packed
   int64_t letter_bytes = 0;
   RecordBatch cpu_batch;
   FillReport rep;
@@ -800,9 +812,12 @@ void Job::run_sliced(BulkParser& parser, int64_t first_index) {
       cpu_batch.offsets.resize(static_cast<size_t>(n) + 1);
       rep = parser.fill_slice(slice, cpu_batch.codes.data(), nullptr, cpu_batch.offsets.data());
     } else {
-      // letters as P24 groups (4.8 bits each) for the streaming kernel, else 5-bit packed
-      const int pack = narrow_guess ? 24 : 5;
-      const int64_t lbytes = pack == 24 ? packed24_bytes(slice.letters) : packed5_bytes(slice.letters);
+      // letters as P33 fields (4.714 bits each; --letters=p24: P24 groups, 4.8) for the streaming kernel,
+      // else 5-bit packed
+      const int pack = narrow_guess ? group_pack() : 5;
+      const int64_t lbytes = pack == 33   ? packed33_bytes(slice.letters)
+                             : pack == 24 ? packed24_bytes(slice.letters)
+                                          : packed5_bytes(slice.letters);
       letters = HostRegion(static_cast<size_t>(lbytes) + 16, numa);
       letters_pack = pack;
       letter_bytes = lbytes;
@@ -854,6 +869,7 @@ void Job::run_sliced(BulkParser& parser, int64_t first_index) {
   if (gpu && n > 0) {
     wb.letters = letters.as<uint8_t>();
     wb.packed24 = letters_pack == 24;
+    wb.packed33 = letters_pack == 33;
     wb.packed5 = letters_pack == 5;
     wb.n = n;
     wb.min_l2 = rep.min_len;
@@ -877,7 +893,7 @@ void Job::run_sliced(BulkParser& parser, int64_t first_index) {
         letters = HostRegion(static_cast<size_t>(letter_bytes) + 16, numa);
         parser.fill_slice(slice, nullptr, letters.as<uint8_t>(), dense.as<int64_t>());
         wb.letters = letters.as<uint8_t>();
-        wb.packed24 = false;
+        wb.packed24 = wb.packed33 = false;
         wb.packed5 = true;
       }
       wb.offsets = dense.as<int64_t>();

@@ -83,7 +83,8 @@ class HipEngine {
   void solve(const uint8_t* codes, const int64_t* offsets, int64_t n, Result* out);
   // General form: optional narrow lengths — len_bits 8 (uint8, max L2 <= 255) or 4 (two per byte, low
   // nibble first, record i = len_base + nibble) — results in `fmt`. `packed`: 1 = `codes` is a 5-bit
-  // packed stream (moc::pack5; char j at bit 5j), 2 = P24 groups (moc::pack24), 0 = one byte per letter.
+  // packed stream (moc::pack5; char j at bit 5j), 2 = P24 groups (moc::pack24), 3 = P33 fields
+  // (moc::pack33), 0 = one byte per letter.
   // R2 results are encoded for the hints' [min_l2, max_l2] (or the batch's own range): stats().r2 holds
   // the parameters.
   void solve_ex(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths, int64_t n, void* out,

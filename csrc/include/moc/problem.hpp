@@ -96,6 +96,30 @@ void pack24(const uint8_t* codes, int64_t n, uint8_t* out);
 // Letters [begin, begin + n) back as codes 1..26.
 void unpack24(const uint8_t* packed, int64_t begin, int64_t n, uint8_t* out);
 
+// ---- 33-bit letter fields ("P33": 4.714 bits per letter) -------------------------------------------------
+// Letters 7f .. 7f+6 form field f, the value sum_i (code - 1) * 26^i (26^7 = 8 031 810 176 < 2^33) stored
+// at bits [33f, 33f+33) of a little-endian bit stream. Eight fields (56 letters) fill exactly 33 bytes, so
+// blocks of 56 letters are byte-aligned: the unit of parallel encoding and of a reader's byte ranges.
+// 1.8% fewer bytes than P24 (log2 26 = 4.700 is the floor); a field decodes with 32-bit arithmetic only
+// (the first division as (v >> 1) / 13, the other six on a value < 2^29).
+constexpr int kP33Field = 7, kP33Letters = 56, kP33Bytes = 33;
+inline int64_t packed33_bytes(int64_t n_chars) { return kP33Bytes * ((n_chars + kP33Letters - 1) / kP33Letters) + 16; }
+// Field value of up to 7 codes (codes 0 count as 1).
+inline uint64_t p33_field(const uint8_t* c, int m = kP33Field) {
+  uint64_t v = 0;
+  for (int j = m - 1; j >= 0; --j) v = v * 26u + (c[j] > 1 ? c[j] - 1u : 0u);
+  return v;
+}
+// One 33-byte block from 56 codes (m < 56: the codes past m count as 1).
+void p33_block(const uint8_t* c, uint8_t* out, int m = kP33Letters);
+// codes[0..n) -> out[0..packed33_bytes(n)) (OpenMP; slack bytes zeroed).
+void pack33(const uint8_t* codes, int64_t n, uint8_t* out);
+// Letters [begin, begin + n) back as codes 1..26.
+void unpack33(const uint8_t* packed, int64_t begin, int64_t n, uint8_t* out);
+// Byte range of a P33 stream holding letters [c0, c1): [first, end).
+inline int64_t p33_first_byte(int64_t c0) { return (33 * (c0 / kP33Field)) >> 3; }
+inline int64_t p33_end_byte(int64_t c1) { return (33 * ((c1 + kP33Field - 1) / kP33Field) + 7) >> 3; }
+
 // Encodes an ASCII string (letters only, any case) into codes; throws on a non-letter.
 std::vector<uint8_t> encode_sequence(const char* s, int64_t n);
 std::string decode_sequence(const uint8_t* codes, int64_t n);

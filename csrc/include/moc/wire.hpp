@@ -115,9 +115,10 @@ void expand_offsets(const int64_t* sparse, int shift, const uint8_t* lengths, in
 // One host batch in the wire formats above: what `final`'s parser writes for a rank's slice and what the
 // engines take. `offsets` is dense (off_shift 0, n+1 entries) or sparse (off_shift > 0, lengths required).
 struct WireBatch {
-  const uint8_t* letters = nullptr;  // P24 groups (packed24), 5-bit packed (packed5) or one byte per letter;
+  const uint8_t* letters = nullptr;  // P33 fields, P24 groups, 5-bit packed (packed5) or one byte per letter;
   bool packed5 = false;              // record i at letter offsets[i]
   bool packed24 = false;
+  bool packed33 = false;             // P33 fields (moc::pack33)
   const int64_t* offsets = nullptr;
   int off_shift = 0;
   const uint8_t* lengths = nullptr;  // narrow lengths (optional with dense offsets)
@@ -132,6 +133,7 @@ struct WireBatch {
     const int64_t L = end_letter() - first_letter();
     if (packed24)
       return kP24Bytes * ((end_letter() + kP24Letters - 1) / kP24Letters - first_letter() / kP24Letters);
+    if (packed33) return p33_end_byte(end_letter()) - p33_first_byte(first_letter());
     return packed5 ? (5 * L + 7) / 8 : L;
   }
   int64_t offset_entries() const { return off_shift ? sparse_count(n, off_shift) : n + 1; }

@@ -116,6 +116,13 @@ int moc_pack24(const uint8_t* codes, int64_t n, uint8_t* out) {
 int moc_unpack24(const uint8_t* packed, int64_t begin, int64_t n, uint8_t* out) {
   return guard([&] { moc::unpack24(packed, begin, n, out); });
 }
+int64_t moc_packed33_bytes(int64_t n_chars) { return moc::packed33_bytes(n_chars); }
+int moc_pack33(const uint8_t* codes, int64_t n, uint8_t* out) {
+  return guard([&] { moc::pack33(codes, n, out); });
+}
+int moc_unpack33(const uint8_t* packed, int64_t begin, int64_t n, uint8_t* out) {
+  return guard([&] { moc::unpack33(packed, begin, n, out); });
+}
 
 int moc_score_table(const int32_t* weights4, int32_t* lut1024, uint8_t* cls1024) {
   return guard([&] {

@@ -49,15 +49,20 @@ struct SwipeLayout {
   int copy_elems = 0;   // 27 * row
   int prof_bytes = 0;   // 8 shifted copies of the Dt profile
   int s_off = 0;        // int8 LUT (32 x 32, column 31 = 0) + Seq1 codes (31 past Seq1): anchor diagonal
-  int loff_off = 0, codes_off = 0, res_off = 0, raw_off = 0, total = 0;  // raw: P24 groups as loaded
+  int loff_off = 0, codes_off = 0, res_off = 0, raw_off = 0, total = 0;  // raw: P24 / P33 bytes as loaded
 };
 
 inline int al16(int x) { return (x + 15) & ~15; }
 
 // P24 tiles: the loaded group bytes (3 per 5 letters, + alignment) of at most codes_cap letters
 inline int p24_raw_cap(int codes_cap) { return 3 * (codes_cap / 5 + 2) + 32; }
+// P33 tiles: 33 bits per 7 letters
+inline int p33_raw_cap(int codes_cap) { return (33 * (codes_cap / 7 + 2) + 7) / 8 + 32; }
+// LDS bytes of a tile's raw (still encoded) letters by letter form
+inline int raw_cap(int lf, int codes_cap) { return lf == 2 ? p24_raw_cap(codes_cap) : lf == 3 ? p33_raw_cap(codes_cap) : 0; }
+inline int letter_form(const ShortArgs& a) { return a.packed33 ? 3 : a.packed24 ? 2 : a.packed5 ? 1 : 0; }
 
-SwipeLayout swipe_layout(int L1, int noff, int l2w, int tile_records, int codes_cap, int fb, bool p24) {
+SwipeLayout swipe_layout(int L1, int noff, int l2w, int tile_records, int codes_cap, int fb, int lf) {
   SwipeLayout l;
   // a multiple of 64 int16 (8 chunks of 16 B) so the per-letter XOR swizzle of chunk indices stays in the row
   l.row = (std::max(L1, 4 * l2w) + noff + 8 + 63) & ~63;
@@ -68,7 +73,7 @@ SwipeLayout swipe_layout(int L1, int noff, int l2w, int tile_records, int codes_
   l.codes_off = l.loff_off + al16((tile_records + 1) * 4 + 64);  // + misc: 16 ints
   l.res_off = l.codes_off + al16(codes_cap);
   l.raw_off = l.res_off + al16(tile_records * fb);
-  l.total = l.raw_off + (p24 ? al16(p24_raw_cap(codes_cap)) : 0);
+  l.total = l.raw_off + al16(raw_cap(lf, codes_cap));
   return l;
 }
 
@@ -79,10 +84,11 @@ inline int kbits_for(int l2w) {  // bits for k in the int16 keys: k <= 4*l2w
 }
 }  // namespace
 
-// LF: letter format of `a.codes` — 0 bytes, 1 5-bit packed, 2 P24 groups (decoded to bytes in LDS per tile)
+// LF: letter format of `a.codes` — 0 bytes, 1 5-bit packed, 2 P24 groups, 3 P33 fields (2 and 3 decoded to
+// bytes in LDS per tile)
 template <int NOFF, int L2W, int LF>
 __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, ShortArgs a, SwipeLayout lay) {
-  constexpr bool P5 = LF == 1, P24 = LF == 2;
+  constexpr bool P5 = LF == 1, P24 = LF == 2, P33 = LF == 3;
   constexpr int kRpt = rpt_of(LF);
   constexpr int NW = P5 ? (20 * L2W + 31) / 32 : L2W;  // record words held per lane
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -93,7 +99,7 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
   int* misc = loff + a.tile_records + 1;
   uint8_t* codes_l = smem + lay.codes_off;
   uint8_t* res_l = smem + lay.res_off;
-  uint8_t* raw_l = smem + lay.raw_off;  // P24: the tile's groups as loaded
+  uint8_t* raw_l = smem + lay.raw_off;  // P24 / P33: the tile's encoded bytes as loaded
   const int L1 = pv.L1;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int KB = (4 * L2W < 8) ? 3 : (4 * L2W < 16) ? 4 : (4 * L2W < 32) ? 5 : (4 * L2W < 64) ? 6 : 7;
@@ -149,8 +155,14 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
 #pragma unroll
       for (int q = 0; q < 4; ++q) f.lens[4 * h + q] = l4[q];
     }
-    const int64_t b_first = P24 ? 3 * (f.start / 5) : P5 ? (5 * f.start) >> 3 : f.start;
-    const int64_t b_end = P24 ? 3 * ((f.end + 4) / 5) : P5 ? (5 * f.end + 7) >> 3 : f.end;
+    const int64_t b_first = P33   ? (33 * (f.start / 7)) >> 3
+                            : P24 ? 3 * (f.start / 5)
+                            : P5  ? (5 * f.start) >> 3
+                                  : f.start;
+    const int64_t b_end = P33   ? (33 * ((f.end + 6) / 7) + 7) >> 3
+                          : P24 ? 3 * ((f.end + 4) / 5)
+                          : P5  ? (5 * f.end + 7) >> 3
+                                : f.end;
     f.a0 = reinterpret_cast<uintptr_t>(a.codes + b_first) & ~uintptr_t{15};
     f.nvec = static_cast<int>((reinterpret_cast<uintptr_t>(a.codes + b_end) + 15 - f.a0) >> 4);
     MOC_DCHECK(f.nvec <= kMaxV * kBlock);
@@ -217,10 +229,11 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
 #pragma unroll
     for (int k = 0; k < kMaxV; ++k) {
       const int v = tid + k * kBlock;
-      if (v < cur.nvec) reinterpret_cast<uint4*>(P24 ? raw_l : codes_l)[v] = cur.v[k];
+      if (v < cur.nvec) reinterpret_cast<uint4*>(P24 || P33 ? raw_l : codes_l)[v] = cur.v[k];
     }
     const uintptr_t p0 = reinterpret_cast<uintptr_t>(a.codes + (P5 ? (5 * start) >> 3 : start));
-    const int shift_b = P24  ? static_cast<int>(start - 5 * (start / 5))
+    const int shift_b = P33   ? static_cast<int>(start - 7 * (start / 7))
+                        : P24 ? static_cast<int>(start - 5 * (start / 5))
                         : P5 ? static_cast<int>(8 * (p0 - cur.a0) + ((5 * start) & 7))
                              : static_cast<int>(p0 - cur.a0);
     if (tid == 0) {
@@ -258,8 +271,32 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
         }
       }
     }
+    if (P33) {  // 33-bit fields -> byte codes 1..26 (field f0 = start / 7 -> codes_l[0..])
+      const int64_t f0 = start / 7;
+      const int nf = static_cast<int>((end + 6) / 7 - f0);
+      const int64_t byte0 = (33 * f0) >> 3;
+      const int ro = static_cast<int>(reinterpret_cast<uintptr_t>(a.codes + byte0) - cur.a0);
+      const int bit0 = static_cast<int>((33 * f0) & 7);
+      for (int f = tid; f < nf; f += kBlock) {
+        const int bit = bit0 + 33 * f;
+        const uint8_t* r = raw_l + ro + (bit >> 3);
+        // 33 bits at a 0..7-bit offset lie in 5 bytes (bits past the field are masked off)
+        const uint64_t w = r[0] | (static_cast<uint32_t>(r[1]) << 8) | (static_cast<uint32_t>(r[2]) << 16) |
+                           (static_cast<uint32_t>(r[3]) << 24) | (static_cast<uint64_t>(r[4]) << 32);
+        const uint64_t x = (w >> (bit & 7)) & 0x1FFFFFFFFull;
+        uint32_t v = static_cast<uint32_t>(x >> 1) / 13u;  // x / 26 in 32-bit arithmetic
+        uint8_t* d = codes_l + 7 * f;
+        d[0] = static_cast<uint8_t>(static_cast<uint32_t>(x) - 26u * v + 1u);  // x - 26q < 26: exact mod 2^32
+#pragma unroll
+        for (int j = 1; j < 7; ++j) {
+          const uint32_t q = v / 26u;
+          d[j] = static_cast<uint8_t>(v - 26u * q + 1u);
+          v = q;
+        }
+      }
+    }
     // next tile: its loads are in flight while this one is scored
-    fetch(grab(), nxt);  // grab() synchronises: loff / letters (decoded P24) are complete
+    fetch(grab(), nxt);  // grab() synchronises: loff / letters (decoded P24 / P33) are complete
 
     // ---- one record per lane
     for (int g = wave; g * 64 < m; g += 4) {
@@ -405,14 +442,15 @@ bool configure_swipe(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs
   const int fb = result_bytes(static_cast<ResultFormat>(a.fmt));
   // host streams: 2048-record tiles (P24 letters fit the register prefetch; 3.59 vs 3.69 ms per headline
   // step at 1024), device-resident: 512 (more blocks per CU); MOC_SWIPE_TILE overrides (64..2048)
-  const int tile_cap = 256 * rpt_of(a.packed24 ? 2 : a.packed5 ? 1 : 0);
+  const int lf = letter_form(a);
+  const int tile_cap = 256 * rpt_of(lf);
   int max_tile = std::min(hbm ? 512 : kMaxTile, tile_cap);
   if (const char* v = std::getenv("MOC_SWIPE_TILE")) max_tile = std::max(64, std::min(tile_cap, std::atoi(v)));
   for (int tr = max_tile; tr >= 64; tr /= 2) {
     const int cap = tr * static_cast<int>(std::max<int64_t>(max_l2, 1)) + 64;
-    // a tile's letter bytes must fit the register prefetch (P24: 3 bytes per 5 letters)
-    if ((a.packed24 ? p24_raw_cap(cap) : cap + 32) > kMaxV * kBlock * 16) continue;
-    SwipeLayout l = swipe_layout(static_cast<int>(L1), ch.noff, ch.l2w, tr, cap, fb, a.packed24 != 0);
+    // a tile's letter bytes must fit the register prefetch (P24: 3 bytes per 5 letters, P33: 33 bits per 7)
+    if ((lf >= 2 ? raw_cap(lf, cap) : cap + 32) > kMaxV * kBlock * 16) continue;
+    SwipeLayout l = swipe_layout(static_cast<int>(L1), ch.noff, ch.l2w, tr, cap, fb, lf);
     if (l.total <= kLdsBudget) {
       a.tile_records = tr;
       a.codes_cap = cap;
@@ -429,6 +467,7 @@ void preload_swipe_kernels() {
   hipFuncAttributes fa;
   (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&swipe_search_kernel<24, 4, 1>));
   (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&swipe_search_kernel<24, 4, 2>));
+  (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&swipe_search_kernel<24, 4, 3>));
 }
 
 // MOC_SWIPE_TAIL=0 keeps every tile at full size (A/B)
@@ -444,7 +483,7 @@ void launch_swipe(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStr
   if (a.n <= 0) return;
   const int noff = a.slot, l2w = a.rpw;
   const int fb = result_bytes(static_cast<ResultFormat>(a.fmt));
-  const SwipeLayout lay = swipe_layout(pv.L1, noff, l2w, a.tile_records, a.codes_cap, fb, a.packed24 != 0);
+  const SwipeLayout lay = swipe_layout(pv.L1, noff, l2w, a.tile_records, a.codes_cap, fb, letter_form(a));
   const int per_cu = std::max(1, std::min(8, 160 * 1024 / std::max(lay.total, 1)));
   const int64_t slots = static_cast<int64_t>(num_cus) * per_cu;
   ShortArgs b = a;
@@ -462,7 +501,9 @@ void launch_swipe(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStr
   const dim3 grid(static_cast<unsigned>(std::max<int64_t>(blocks, 1))), block(kBlock);
 #define MOC_SWIPE_CASE(NO, LW)                                                                          \
   if (noff == NO && l2w == LW) {                                                                      \
-    if (a.packed24)                                                                                   \
+    if (a.packed33)                                                                                   \
+      hipLaunchKernelGGL((swipe_search_kernel<NO, LW, 3>), grid, block, lay.total, stream, pv, b, lay); \
+    else if (a.packed24)                                                                              \
       hipLaunchKernelGGL((swipe_search_kernel<NO, LW, 2>), grid, block, lay.total, stream, pv, b, lay); \
     else if (a.packed5)                                                                               \
       hipLaunchKernelGGL((swipe_search_kernel<NO, LW, 1>), grid, block, lay.total, stream, pv, b, lay); \

@@ -515,8 +515,12 @@ bool HipEngine::direct_pointers(const WireBatch& b, void* out, int fb, dev::Shor
   const void *dc = nullptr, *doff = nullptr, *dlen = nullptr, *dout = nullptr;
   const int64_t c0 = b.first_letter(), c1 = b.end_letter(), n = b.n;
   // byte range of the letters: [b0, b1)
-  const int64_t b0 = b.packed24 ? kP24Bytes * (c0 / kP24Letters) : b.packed5 ? (5 * c0) >> 3 : c0;
-  const int64_t b1 = b.packed24  ? kP24Bytes * ((c1 + kP24Letters - 1) / kP24Letters)
+  const int64_t b0 = b.packed33   ? p33_first_byte(c0)
+                     : b.packed24 ? kP24Bytes * (c0 / kP24Letters)
+                     : b.packed5  ? (5 * c0) >> 3
+                                  : c0;
+  const int64_t b1 = b.packed33    ? p33_end_byte(c1)
+                     : b.packed24  ? kP24Bytes * ((c1 + kP24Letters - 1) / kP24Letters)
                      : b.packed5 ? ((5 * c1 + 7) >> 3) + 1
                                  : c1;
   if (b.device) {  // device-resident (e.g. received over RCCL): the pointers are the kernel's already
@@ -555,6 +559,7 @@ void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uin
   b.letters = codes;
   b.packed5 = packed == 1;
   b.packed24 = packed == 2;
+  b.packed33 = packed == 3;
   b.offsets = offsets;
   b.lengths = lengths;
   b.len_bits = len_bits;
@@ -618,11 +623,14 @@ void HipEngine::solve_wire(const WireBatch& batch, void* out, ResultFormat fmt) 
   a.counter = d_counter_;
   a.packed5 = b.packed5 ? 1 : 0;
   a.packed24 = b.packed24 ? 1 : 0;
-  const bool dma = opt_.dma_stream && !b.device && !b.packed24;  // the SDMA chunker cuts 5-bit / byte streams
+  a.packed33 = b.packed33 ? 1 : 0;
+  // the SDMA chunker cuts 5-bit / byte streams
+  const bool dma = opt_.dma_stream && !b.device && !b.packed24 && !b.packed33;
   const bool swipe = dev::configure_swipe(L1_, ls.mn, ls.mx, table_.max_abs(), a, b.device || dma);
   // packed letters stream straight into the swipe kernel only; other kernels read unpacked bytes. Sparse
   // offsets need whole tiles of 2^off_shift records (the swipe tiles are powers of two >= 64).
-  const bool kernel_ok = (swipe || (!b.packed5 && !b.packed24 && dev::configure_short(L1_, ls.mn, ls.mx, a))) &&
+  const bool kernel_ok = (swipe || (!b.packed5 && !b.packed24 && !b.packed33 &&
+                                    dev::configure_short(L1_, ls.mn, ls.mx, a))) &&
                          (a.tile_records % (1 << b.off_shift)) == 0;
   if ((opt_.allow_direct || b.device) && kernel_ok && direct_pointers(b, out, fb, a)) {
     const dev::ProblemView pv = problem_view(ls.mx);
@@ -650,13 +658,16 @@ void HipEngine::solve_wire(const WireBatch& batch, void* out, ResultFormat fmt) 
     return;
   }
   if (b.device) throw Error("device-resident wire batches stream through the swipe kernel only");
-  uvector<uint8_t> bytes;  // P24 letters: the staged pipeline takes bytes (or 5-bit packing)
-  if (b.packed24) {
+  uvector<uint8_t> bytes;  // P24 / P33 letters: the staged pipeline takes bytes (or 5-bit packing)
+  if (b.packed24 || b.packed33) {
     const int64_t c0 = b.first_letter(), c1 = b.end_letter();
     bytes.resize(static_cast<size_t>(c1) + 16);
-    unpack24(b.letters, c0, c1 - c0, bytes.data() + c0);
+    if (b.packed33)
+      unpack33(b.letters, c0, c1 - c0, bytes.data() + c0);
+    else
+      unpack24(b.letters, c0, c1 - c0, bytes.data() + c0);
     b.letters = bytes.data();
-    b.packed24 = false;
+    b.packed24 = b.packed33 = false;
   }
   if (b.off_shift) {  // the staged pipeline plans from dense offsets: rebuild them from the lengths
     uvector<int64_t> dense(static_cast<size_t>(n) + 1);

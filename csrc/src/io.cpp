@@ -337,10 +337,11 @@ struct PieceOut {
 
 FillReport BulkParser::fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* packed5, int64_t* offs, int64_t* sparse,
                                   uint16_t* len16, int pack) const {
-  if (pack != 5 && pack != 24) throw Error("fill_slice: pack must be 5 or 24");
-  // letters per group and bytes per group of the packed stream: 8 -> 5 (5-bit), 5 -> 3 (P24)
-  const bool p24 = pack == 24;
-  const int64_t G = p24 ? kP24Letters : 8, GB = p24 ? kP24Bytes : 5;
+  if (pack != 5 && pack != 24 && pack != 33) throw Error("fill_slice: pack must be 5, 24 or 33");
+  // letters per group and bytes per group of the packed stream: 8 -> 5 (5-bit), 5 -> 3 (P24), 56 -> 33 (P33:
+  // a block of eight 33-bit fields)
+  const bool p24 = pack == 24, p33 = pack == 33;
+  const int64_t G = p33 ? kP33Letters : p24 ? kP24Letters : 8, GB = p33 ? kP33Bytes : p24 ? kP24Bytes : 5;
   if (offs) offs[0] = 0;
   constexpr int64_t kSparseMask = (int64_t{1} << kSparseShift) - 1;
   const int np = static_cast<int>(s.pieces.size());
@@ -373,7 +374,9 @@ FillReport BulkParser::fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* p
       const int64_t ng = (hi - cur) / G;
       const uint8_t* src = stage.data() + (cur - base);
       uint8_t* dst = packed5 + GB * (cur / G);
-      if (p24) {
+      if (p33) {
+        for (int64_t g = 0; g < ng; ++g) p33_block(src + kP33Letters * g, dst + kP33Bytes * g);
+      } else if (p24) {
         for (int64_t g = 0; g < ng; ++g) {
           const uint32_t v = p24_group(src + 5 * g);  // < 2^24: the 4-byte store's top byte is 0
           std::memcpy(dst + 3 * g, &v, g + 1 < ng ? 4 : 3);
@@ -469,9 +472,18 @@ FillReport BulkParser::fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* p
     // groups holding letters of two pieces (or the slice's last, partial group): zeroed, then assembled
     for (const PieceOut& po : out)
       for (const auto& sc : po.stragglers) std::memset(packed5 + GB * (sc.first / G), 0, static_cast<size_t>(GB));
-    static constexpr uint32_t kPow26[5] = {1u, 26u, 676u, 17576u, 456976u};
+    static constexpr uint32_t kPow26[7] = {1u, 26u, 676u, 17576u, 456976u, 11881376u, 308915776u};
     for (const PieceOut& po : out)
       for (const auto& sc : po.stragglers) {
+        if (p33) {  // add (code - 1) * 26^j to field x / 7 (bits [33f, 33f+33); serial: the 8-byte window
+                    // rewrites neighbouring fields' bytes unchanged, and a field's sum never leaves its bits)
+          const int64_t bit = 33 * (sc.first / kP33Field);
+          uint64_t w;
+          std::memcpy(&w, packed5 + (bit >> 3), 8);
+          w += (static_cast<uint64_t>(sc.second > 1 ? sc.second - 1u : 0u) * kPow26[sc.first % kP33Field]) << (bit & 7);
+          std::memcpy(packed5 + (bit >> 3), &w, 8);
+          continue;
+        }
         if (p24) {  // add (code - 1) * 26^j to the group value
           uint8_t* q = packed5 + kP24Bytes * (sc.first / kP24Letters);
           uint32_t v = q[0] | (static_cast<uint32_t>(q[1]) << 8) | (static_cast<uint32_t>(q[2]) << 16);
@@ -487,7 +499,7 @@ FillReport BulkParser::fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* p
         packed5[(bit >> 3) + 1] |= static_cast<uint8_t>(v >> 8);
       }
     const int64_t used = GB * ((s.letters + G - 1) / G);
-    const int64_t total = p24 ? packed24_bytes(s.letters) : packed5_bytes(s.letters);
+    const int64_t total = p33 ? packed33_bytes(s.letters) : p24 ? packed24_bytes(s.letters) : packed5_bytes(s.letters);
     std::memset(packed5 + used, 0, static_cast<size_t>(total - used));
   }
   if (sparse) sparse[sparse_count(s.records, kSparseShift) - 1] = s.letters;

@@ -2,6 +2,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 
 namespace moc {
@@ -85,6 +86,41 @@ void unpack24(const uint8_t* packed, int64_t begin, int64_t n, uint8_t* out) {
     const uint8_t* p = packed + kP24Bytes * g;
     uint32_t v = p[0] | (static_cast<uint32_t>(p[1]) << 8) | (static_cast<uint32_t>(p[2]) << 16);
     for (int64_t j = x - g * kP24Letters; j > 0; --j) v /= 26u;
+    out[i] = static_cast<uint8_t>(v % 26u + 1u);
+  }
+}
+
+void p33_block(const uint8_t* c, uint8_t* out, int m) {
+  uint64_t w[5] = {0, 0, 0, 0, 0};  // 264 bits + room for the last field's spill
+  for (int f = 0; f < kP33Letters / kP33Field; ++f) {
+    const int have = std::max(0, std::min(kP33Field, m - kP33Field * f));
+    const uint64_t v = p33_field(c + kP33Field * f, have);
+    const int bit = 33 * f;
+    w[bit >> 6] |= v << (bit & 63);
+    if ((bit & 63) + 33 > 64) w[(bit >> 6) + 1] |= v >> (64 - (bit & 63));
+  }
+  std::memcpy(out, w, kP33Bytes);
+}
+
+void pack33(const uint8_t* codes, int64_t n, uint8_t* out) {
+  const int64_t blocks = (n + kP33Letters - 1) / kP33Letters;
+#pragma omp parallel for schedule(static) if (blocks > 16384)
+  for (int64_t g = 0; g < blocks; ++g) {
+    const int64_t b = g * kP33Letters;
+    p33_block(codes + b, out + g * kP33Bytes, static_cast<int>(std::min<int64_t>(kP33Letters, n - b)));
+  }
+  const int64_t used = blocks * kP33Bytes, total = packed33_bytes(n);
+  for (int64_t i = used; i < total; ++i) out[i] = 0;
+}
+
+void unpack33(const uint8_t* packed, int64_t begin, int64_t n, uint8_t* out) {
+#pragma omp parallel for schedule(static) if (n > (1 << 20))
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t x = begin + i, f = x / kP33Field, bit = 33 * f;
+    uint64_t w = 0;
+    std::memcpy(&w, packed + (bit >> 3), 5);  // 33 bits from a 0..7 bit offset fit 5 bytes
+    uint64_t v = (w >> (bit & 7)) & ((uint64_t{1} << 33) - 1);
+    for (int64_t j = x - f * kP33Field; j > 0; --j) v /= 26u;
     out[i] = static_cast<uint8_t>(v % 26u + 1u);
   }
 }

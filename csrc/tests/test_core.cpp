@@ -316,6 +316,39 @@ void test_pack24() {
   CHECK(p24_group(five) == 11881375u);  // 26^5 - 1: the largest group value fits 24 bits
 }
 
+void test_pack33() {
+  std::mt19937 rng(33);
+  for (int64_t n : {0, 1, 6, 7, 8, 55, 56, 57, 112, 1000, 70001}) {
+    std::vector<uint8_t> codes(static_cast<size_t>(n));
+    for (auto& c : codes) c = static_cast<uint8_t>(1 + rng() % 26);
+    if (n > 20) std::fill(codes.begin() + 7, codes.begin() + 21, uint8_t{26});  // largest fields
+    std::vector<uint8_t> p(static_cast<size_t>(packed33_bytes(n)), 0xAB);
+    pack33(codes.data(), n, p.data());
+    bool slack_zero = true;
+    for (size_t i = static_cast<size_t>(33 * ((n + 55) / 56)); i < p.size(); ++i) slack_zero &= p[i] == 0;
+    CHECK(slack_zero);
+    for (int64_t b : {int64_t{0}, int64_t{1}, int64_t{6}, int64_t{7}, int64_t{57}, n / 3}) {
+      if (b > n) continue;
+      std::vector<uint8_t> back(static_cast<size_t>(n - b));
+      unpack33(p.data(), b, n - b, back.data());
+      CHECK(std::equal(back.begin(), back.end(), codes.begin() + b));
+    }
+    // byte ranges of any letter range cover exactly its fields
+    for (int64_t c0 : {int64_t{0}, int64_t{3}, int64_t{7}, int64_t{50}}) {
+      if (c0 >= n) continue;
+      CHECK(p33_first_byte(c0) == (33 * (c0 / 7)) / 8);
+      CHECK(p33_end_byte(n) <= 33 * ((n + 55) / 56) + 1);
+    }
+  }
+  const uint8_t seven[7] = {26, 26, 26, 26, 26, 26, 26};
+  CHECK(p33_field(seven) == 8031810175ull);  // 26^7 - 1 < 2^33
+  // the kernel's first digit: (x >> 1) / 13 == x / 26 for every field value class
+  const uint64_t probes[] = {0, 25, 26, 51, 52, 8031810175ull, 8031810150ull, 4294967295ull, 4294967296ull,
+                             4294967297ull};
+  for (uint64_t x : probes)
+    CHECK(static_cast<uint32_t>(x >> 1) / 13u == x / 26u);
+}
+
 void test_profile16() {
   std::mt19937 rng(11);
   for (int trial = 0; trial < 40; ++trial) {
@@ -543,6 +576,12 @@ void test_slices() {
       pack24(ref.seq2.codes.data() + ref.seq2.offsets[b], s.letters, want24.data());
       const FillReport r24 = p.fill_slice(s, nullptr, p24.data(), nullptr, sp.data(), l16.data(), 24);
       CHECK(r24.min_len == r.min_len && r24.max_len == r.max_len && p24 == want24);
+      // ... and with P33 fields (56-letter blocks straddling the pieces assembled afterwards)
+      std::vector<uint8_t> p33(static_cast<size_t>(packed33_bytes(s.letters)), 0x33),
+          want33(static_cast<size_t>(packed33_bytes(s.letters)));
+      pack33(ref.seq2.codes.data() + ref.seq2.offsets[b], s.letters, want33.data());
+      const FillReport r33 = p.fill_slice(s, nullptr, p33.data(), nullptr, sp.data(), l16.data(), 33);
+      CHECK(r33.min_len == r.min_len && r33.max_len == r.max_len && p33 == want33);
       ok = true;
       for (size_t j = 0; j < sp.size(); ++j)
         ok = ok && sp[j] == offs[std::min<int64_t>(static_cast<int64_t>(j) << kSparseShift, s.records)];
@@ -682,7 +721,7 @@ int main() {
       {"engine_vs_brute_force", test_engine_vs_brute_force},          {"formatter", test_formatter},
       {"profile16", test_profile16},     {"releaser", test_releaser},   {"slices", test_slices},
       {"narrow_lengths", test_narrow_lengths}, {"result_formats", test_result_formats},
-      {"write_runs", test_write_runs},   {"pack24", test_pack24}};
+      {"write_runs", test_write_runs},   {"pack24", test_pack24}, {"pack33", test_pack33}};
   for (const auto& t : tests) {
     const int before = g_failed;
     t.second();

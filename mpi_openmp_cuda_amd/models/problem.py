@@ -108,6 +108,29 @@ def unpack24(packed: np.ndarray, begin: int, n: int) -> np.ndarray:
     return out
 
 
+def packed33_bytes(n_chars: int) -> int:
+    """Bytes of a P33 letter stream (56 letters per 33 bytes, incl. 16 bytes of read slack)."""
+    return int(_lib.lib().moc_packed33_bytes(int(n_chars)))
+
+
+def pack33(codes: np.ndarray, out: np.ndarray = None) -> np.ndarray:
+    """Byte letter codes (1..26) -> 33-bit fields: letters 7f..7f+6 as the value sum (code - 1) * 26^i at
+    bits [33f, 33f+33) of a little-endian bit stream — 4.714 bits per letter (log2 26 = 4.700)."""
+    codes = np.ascontiguousarray(codes, dtype=np.uint8)
+    nb = packed33_bytes(codes.shape[0])
+    if out is None:
+        out = np.empty(nb, dtype=np.uint8)
+    assert out.dtype == np.uint8 and out.shape[0] >= nb
+    _lib.check(_lib.lib().moc_pack33(_lib.ptr(codes), codes.shape[0], _lib.ptr(out)))
+    return out
+
+
+def unpack33(packed: np.ndarray, begin: int, n: int) -> np.ndarray:
+    out = np.empty(n, dtype=np.uint8)
+    _lib.check(_lib.lib().moc_unpack33(_lib.ptr(np.ascontiguousarray(packed)), int(begin), int(n), _lib.ptr(out)))
+    return out
+
+
 def unpack5(packed: np.ndarray, begin: int, n: int) -> np.ndarray:
     out = np.empty(n, dtype=np.uint8)
     _lib.check(_lib.lib().moc_unpack5(_lib.ptr(np.ascontiguousarray(packed)), int(begin), int(n), _lib.ptr(out)))

@@ -1,7 +1,7 @@
 """One rank's slice of records in the wire formats the GPU streams (csrc/include/moc/wire.hpp).
 
-``./final`` writes these forms straight from its parser (``BulkParser::fill_slice``): letters as base-26
-groups of 5 in 3 bytes (P24, 4.8 bits per letter; or 5-bit packed, or bytes),
+``./final`` writes these forms straight from its parser (``BulkParser::fill_slice``): letters as 33-bit
+fields of 7 (P33, 4.714 bits per letter; or base-26 groups of 5 in 3 bytes, P24, or 5-bit packed, or bytes),
 record lengths as 3/4-bit fields above the slice's shortest length (8-bit, or offsets only, when the range
 is wider), results in the narrowest format the problem's bounds allow (R2: one uint16 per record). The
 streaming kernel reads them zero-copy from page-locked host memory, so every byte saved is PCIe time saved.
@@ -16,10 +16,10 @@ from typing import Callable, Optional
 
 import numpy as np
 
-from ..models.problem import (lengths3_bytes, pack5, pack24, pack_lengths3, pack_lengths4, packed5_bytes,
-                              packed24_bytes, unpack5, unpack24)
+from ..models.problem import (lengths3_bytes, pack5, pack24, pack33, pack_lengths3, pack_lengths4, packed5_bytes,
+                              packed24_bytes, packed33_bytes, unpack5, unpack24, unpack33)
 
-LETTER_FORMATS = ("p24", "p5", "bytes")
+LETTER_FORMATS = ("p33", "p24", "p5", "bytes")
 
 # allocator(name, dtype, count) -> array: private numpy memory, /dev/shm memmaps, hipHostMalloc buffers, ...
 Alloc = Callable[[str, np.dtype, int], np.ndarray]
@@ -42,10 +42,10 @@ def length_bits(l2_min: int, l2_max: int, narrow: bool = True) -> int:
 class WireSlice:
     """A CSR slice (record lengths + byte letter codes 1..26) encoded once into the wire formats.
 
-    ``letters``: ``p24`` (default), ``p5`` or ``bytes``; ``alloc`` places every array (so a benchmark
+    ``letters``: ``p33`` (default), ``p24``, ``p5`` or ``bytes``; ``alloc`` places every array (so a benchmark
     can put them in node-shared or hipHostMalloc memory)."""
 
-    def __init__(self, lengths: np.ndarray, letters: Optional[np.ndarray], letter_format: str = "p24",
+    def __init__(self, lengths: np.ndarray, letters: Optional[np.ndarray], letter_format: str = "p33",
                  narrow: bool = True, alloc: Alloc = private_alloc):
         if letter_format not in LETTER_FORMATS:
             raise ValueError(f"letter_format must be one of {LETTER_FORMATS}")
@@ -74,7 +74,11 @@ class WireSlice:
         else:
             self.lengths = None
         self.letter_format = letter_format
-        if letter_format == "p24":
+        if letter_format == "p33":
+            self.codes = alloc("codes33", np.uint8, packed33_bytes(self.total))
+            if letters is not None:
+                pack33(letters, out=self.codes)
+        elif letter_format == "p24":
             self.codes = alloc("codes24", np.uint8, packed24_bytes(self.total))
             if letters is not None:
                 pack24(letters, out=self.codes)
@@ -116,7 +120,7 @@ class WireSlice:
             self.alloc_results(engine)
         return engine.solve(self.codes, self.offsets, out=self.results, lengths=self.lengths, fmt=self.fmt,
                             l2_range=(self.l2_min, self.l2_max), packed5=self.letter_format == "p5",
-                            packed24=self.letter_format == "p24",
+                            packed24=self.letter_format == "p24", packed33=self.letter_format == "p33",
                             lengths_bits=self.len_bits or 8, lengths_base=self.len_base)
 
     def triples(self, engine, count: Optional[int] = None) -> np.ndarray:
@@ -130,6 +134,8 @@ class WireSlice:
     # ---- decoding (tests, verification)
     def letters(self, begin: int = 0, end: Optional[int] = None) -> np.ndarray:
         end = self.total if end is None else end
+        if self.letter_format == "p33":
+            return unpack33(self.codes, begin, end - begin)
         if self.letter_format == "p24":
             return unpack24(self.codes, begin, end - begin)
         if self.letter_format == "p5":

@@ -179,19 +179,20 @@ def test_packed5_letters(shape, n, pinned):
 
 @pytest.mark.parametrize("shape,n", [("input6", 250_003), ("input1", 3000), ("input4", 200), ("input3", 20)])
 @pytest.mark.parametrize("pinned", [False, True])
-def test_packed24_letters(shape, n, pinned):
-    # P24 letters (base-26 groups, 5 per 3 bytes): decoded per tile in LDS by the swipe kernel (pinned, tiny
-    # problems), or unpacked on the host for the staged pipeline (everything else)
-    from mpi_openmp_cuda_amd.models.problem import pack24
+@pytest.mark.parametrize("code", ["p24", "p33"])
+def test_group_coded_letters(shape, n, pinned, code):
+    # P24 letters (base-26 groups, 5 per 3 bytes) and P33 letters (7 per 33-bit field): decoded per tile in
+    # LDS by the swipe kernel (pinned, tiny problems), or unpacked on the host for the staged pipeline
+    from mpi_openmp_cuda_amd.models.problem import pack24, pack33
 
     prob = make_synthetic(shape, n, seed=n + 1)
-    packed = pack24(prob.codes)
+    packed = pack33(prob.codes) if code == "p33" else pack24(prob.codes)
     eng = HipSearchEngine(device=0, chunk_records=max(n // 3, 1))
     eng.set_problem(prob.weights, prob.seq1)
     out = np.zeros(prob.n, dtype=np.dtype([("score", "<i4"), ("n", "<i4"), ("k", "<i4")]))
     if pinned:
         eng.pin(packed, prob.offsets, out)
-    eng.solve(packed, prob.offsets, out=out, packed24=True)
+    eng.solve(packed, prob.offsets, out=out, packed24=code == "p24", packed33=code == "p33")
     st = eng.stats()
     assert np.array_equal(as_triples(out), as_triples(search_cpu(prob))), st
     if pinned and shape == "input6":
@@ -202,10 +203,10 @@ def test_packed24_letters(shape, n, pinned):
 @pytest.mark.parametrize("L1,lo,hi,w", [(26, 6, 11, (4, 3, 2, 10)), (12, 1, 14, (3, 1, 1, 2)),
                                         (40, 20, 32, (5, 2, 3, 4)), (60, 10, 16, (2, 2, 1, 3)),
                                         (9, 9, 9, (7, 1, 2, 3))])
-@pytest.mark.parametrize("letters", ["p24", "p5"])
+@pytest.mark.parametrize("letters", ["p33", "p24", "p5"])
 def test_swipe_wire_slices(L1, lo, hi, w, letters):
     # the headline's wire path (parallel/wire.py: narrow lengths, R2/R4 results, zero-copy) across swipe
-    # instantiations (NOFF 8..64, record widths <= 16 / <= 32) for both packed letter formats
+    # instantiations (NOFF 8..64, record widths <= 16 / <= 32) for every packed letter format
     from mpi_openmp_cuda_amd._lib import Pinned
     from mpi_openmp_cuda_amd.parallel.wire import WireSlice
 
@@ -413,7 +414,7 @@ def test_final_cli_hip_two_ranks_offsets():
 
 @pytest.mark.parametrize("np_", [1, 2])
 def test_final_cli_zero_copy_window(tmp_path, np_):
-    # GPU ranks encode their own slice (P24 letters, narrow lengths, sparse offsets), page-lock only that
+    # GPU ranks encode their own slice (P33 letters, narrow lengths, sparse offsets), page-lock only that
     # slice and stream it zero-copy; output == CPU. Two ranks share the one test GPU (--device=0).
     import json
 
@@ -430,9 +431,21 @@ def test_final_cli_zero_copy_window(tmp_path, np_):
     for q in range(np_):
         n = d["rank_records"][q]
         letters = int(prob.offsets[b[q + 1]] - prob.offsets[b[q]])
-        # this rank's slice only: P24 letters + 1/64 offsets + 3-bit lengths + R2 results
-        assert 3 * letters // 5 <= d["rank_pinned_bytes"][q] <= 3 * letters // 5 + n * (8 / 64 + 3 / 8 + 2) + 64, d
-        assert d["rank_h2d_bytes"][q] <= 3 * letters // 5 + 3 * n // 8 + 64, d
+        # this rank's slice only: P33 letters (33 bytes per 56) + 1/64 offsets + 3-bit lengths + R2 results
+        lb = 33 * letters // 56
+        assert lb <= d["rank_pinned_bytes"][q] <= lb + n * (8 / 64 + 3 / 8 + 2) + 64, d
+        assert d["rank_h2d_bytes"][q] <= lb + 3 * n // 8 + 64, d
+
+
+def test_final_cli_letters_p24(tmp_path):
+    # --letters=p24 keeps the 5-per-3-bytes groups on the GPU slices (A/B against the default P33)
+    prob = make_synthetic("input6", 50_001, seed=12)
+    path = tmp_path / "in6.txt"
+    path.write_text(prob.to_text())
+    for letters in ("p24", "p33"):
+        r = run_final(["--backend=hip", f"--letters={letters}", f"--input={path}", "--device=0"], stdin_bytes=b"")
+        assert r.returncode == 0, r.stderr.decode()
+        assert r.stdout.decode() == format_results(search_cpu(prob)), letters
 
 
 @pytest.mark.parametrize("np_", [1, 2])
@@ -450,11 +463,11 @@ def test_final_cli_streaming_slices(tmp_path, np_):
     assert r.stdout.decode() == format_results(search_cpu(prob))
     d = json.loads([l for l in r.stderr.decode().splitlines() if l.startswith("{")][-1])
     assert d["batches"] == 3 and d["records"] == prob.n
-    # summed over the batches: about this rank's share of P24 letters + narrow lengths/offsets + R2 results
+    # summed over the batches: about this rank's share of P33 letters + narrow lengths/offsets + R2 results
     # (a whole-window pin would be ~1 + 8 + 12 bytes per letter/record for every rank)
     total = int(prob.offsets[-1])
     assert 0 < d["max_rank_kernel_ms"]
-    assert sum(d["rank_pinned_bytes"]) <= 3 * total // 5 + prob.n * (8 / 64 + 3 / 8 + 2) + 1024 * np_ * 3, d
+    assert sum(d["rank_pinned_bytes"]) <= 33 * total // 56 + prob.n * (8 / 64 + 3 / 8 + 2) + 1024 * np_ * 3, d
 
 
 @pytest.mark.parametrize("pinned", [False, True])
