@@ -7,6 +7,7 @@
 #pragma once
 
 #include <cstdint>
+#include <cstring>
 #include <memory>
 #include <vector>
 
@@ -109,6 +110,23 @@ inline uint64_t p33_field(const uint8_t* c, int m = kP33Field) {
   uint64_t v = 0;
   for (int j = m - 1; j >= 0; --j) v = v * 26u + (c[j] > 1 ? c[j] - 1u : 0u);
   return v;
+}
+// One whole 33-byte block from 56 codes: the field as two 32-bit Horner chains (letters 0..3 < 26^4,
+// 4..6 < 26^3) joined once, eight fields at bits 33k assembled into 4 words + 1 byte. Inline: the parser
+// calls it per 56 letters.
+inline uint32_t p33_digit(uint8_t c) { return c > 1 ? c - 1u : 0u; }
+inline void p33_block_full(const uint8_t* c, uint8_t* out) {
+  uint64_t f[8];
+  for (int k = 0; k < 8; ++k) {
+    const uint8_t* p = c + 7 * k;
+    const uint32_t lo = ((p33_digit(p[3]) * 26u + p33_digit(p[2])) * 26u + p33_digit(p[1])) * 26u + p33_digit(p[0]);
+    const uint32_t hi = (p33_digit(p[6]) * 26u + p33_digit(p[5])) * 26u + p33_digit(p[4]);
+    f[k] = lo + static_cast<uint64_t>(hi) * 456976u;
+  }
+  const uint64_t w[4] = {f[0] | f[1] << 33, f[1] >> 31 | f[2] << 2 | f[3] << 35, f[3] >> 29 | f[4] << 4 | f[5] << 37,
+                         f[5] >> 27 | f[6] << 6 | f[7] << 39};
+  std::memcpy(out, w, 32);
+  out[32] = static_cast<uint8_t>(f[7] >> 25);
 }
 // One 33-byte block from 56 codes (m < 56: the codes past m count as 1).
 void p33_block(const uint8_t* c, uint8_t* out, int m = kP33Letters);

@@ -375,7 +375,7 @@ FillReport BulkParser::fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* p
       const uint8_t* src = stage.data() + (cur - base);
       uint8_t* dst = packed5 + GB * (cur / G);
       if (p33) {
-        for (int64_t g = 0; g < ng; ++g) p33_block(src + kP33Letters * g, dst + kP33Bytes * g);
+        for (int64_t g = 0; g < ng; ++g) p33_block_full(src + kP33Letters * g, dst + kP33Bytes * g);
       } else if (p24) {
         for (int64_t g = 0; g < ng; ++g) {
           const uint32_t v = p24_group(src + 5 * g);  // < 2^24: the 4-byte store's top byte is 0

@@ -91,6 +91,10 @@ void unpack24(const uint8_t* packed, int64_t begin, int64_t n, uint8_t* out) {
 }
 
 void p33_block(const uint8_t* c, uint8_t* out, int m) {
+  if (m >= kP33Letters) {
+    p33_block_full(c, out);
+    return;
+  }
   uint64_t w[5] = {0, 0, 0, 0, 0};  // 264 bits + room for the last field's spill
   for (int f = 0; f < kP33Letters / kP33Field; ++f) {
     const int have = std::max(0, std::min(kP33Field, m - kP33Field * f));

@@ -342,6 +342,16 @@ void test_pack33() {
   }
   const uint8_t seven[7] = {26, 26, 26, 26, 26, 26, 26};
   CHECK(p33_field(seven) == 8031810175ull);  // 26^7 - 1 < 2^33
+  // the straight-line whole-block encoder equals the generic field path (m = 55 counts letter 55 as 1)
+  for (int rep = 0; rep < 200; ++rep) {
+    uint8_t c[56], a[33], b[33];
+    for (auto& x : c) x = static_cast<uint8_t>(1 + rng() % 26);
+    if (rep % 3 == 0) std::fill(c, c + 56, uint8_t{26});
+    c[55] = 1;
+    p33_block(c, a);
+    p33_block(c, b, 55);
+    CHECK(std::equal(a, a + 33, b));
+  }
   // the kernel's first digit: (x >> 1) / 13 == x / 26 for every field value class
   const uint64_t probes[] = {0, 25, 26, 51, 52, 8031810175ull, 8031810150ull, 4294967295ull, 4294967296ull,
                              4294967297ull};
