@@ -15,8 +15,8 @@ One timed step = the search of one complete job over the global batch (reference
 The records are held in the wire formats `./final` writes while it parses (P33 letters: 7 per 33 bits, 3-bit lengths,
 R2 results; csrc/include/moc/wire.hpp): encoding them is the untimed set-up here, as parsing and printing
 are outside `./final`'s compute phase, whose `--timing` shows the same kernel time for the same letters
-(profiles/final_scale_1.1G_r2_p24.log: 13.8 ms kernel at 1.14 G letters; profiles/bench_input6_1gpu_1.1G_p24.log:
-13.9 ms/step here).
+(profiles/final_scale_1.1G_r2_p33.log: 13.13 ms kernel at 1.14 G letters; profiles/bench_input6_1gpu_1.1G_p33.log:
+13.15 ms kernel, 13.26 ms/step here).
 Weak scaling: --records-per-gpu is fixed per rank, the global batch grows with N.
 
 Run: python bench.py [--gpus N --steps K --warmup W]. With N > 1 and no torch.distributed environment
