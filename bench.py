@@ -60,6 +60,7 @@ def parse_args():
                          "(p24), 5-bit packed (p5), bytes")
     ap.add_argument("--narrow", type=int, default=1,
                     help="1: narrowest wire formats that fit (4-bit lengths, R2 results); 0: uint8 lengths, R4")
+    ap.add_argument("--dump-steps", default="", help="rank 0 writes its per-step kernel and host ms to this JSON file")
     ap.add_argument("--dry-launch", action="store_true",
                     help="print the self-launch command (JSON) for --gpus N > 1 and exit; touches no GPU")
     ap.add_argument("--allow-shared-gpu", action="store_true",
@@ -263,12 +264,16 @@ def main():
     barrier()
     progress(f"timing {args.steps} steps")
     t0 = time.perf_counter()
-    kms, tms = [], []
+    kms, tms, sms = [], [], []
+    t_prev = t0
     for _ in range(args.steps):
         step()
         st = eng.stats()
         kms.append(st["kernel_ms"])
         tms.append(st["total_ms"])
+        t_now = time.perf_counter()  # host clock per step (rank 0's view; the job is timed by t0 / elapsed)
+        sms.append((t_now - t_prev) * 1e3)
+        t_prev = t_now
     barrier()
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
@@ -345,6 +350,8 @@ def main():
             "cells_per_s_est": round(total_records * cells_per_rec * args.steps / elapsed, 1),
             "rank0_kernel_ms_per_step": round(float(np.median(kms)), 4),
             "rank0_kernel_ms_min_max": [round(min(kms), 4), round(max(kms), 4)],
+            "rank0_kernel_ms_p90_p99": [round(float(np.percentile(kms, 90)), 4), round(float(np.percentile(kms, 99)), 4)],
+            "rank0_step_ms_p50_p99": [round(float(np.percentile(sms, 50)), 4), round(float(np.percentile(sms, 99)), 4)],
             "rank0_solve_ms_median": round(float(np.median(tms)), 4),
             "rank0_h2d_bytes_per_step": int(st["h2d_bytes"]),
             "rank0_d2h_bytes_per_step": int(st["d2h_bytes"]),
@@ -364,6 +371,9 @@ def main():
             "verified": bool(okt.item()),
         }
         print(json.dumps(out), flush=True)
+        if args.dump_steps:
+            with open(args.dump_steps, "w") as f:
+                json.dump({"kernel_ms": kms, "step_ms": sms, "solve_ms": tms}, f)
     pin.release()
     if distributed:
         barrier()
