@@ -468,22 +468,28 @@ FillReport BulkParser::fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* p
       r.long_len = po.rep.long_len;
     }
   }
-  if (packed5) {
+  if (packed5 && p33) {
+    // blocks holding letters of two pieces (or the slice's last, partial block) hold stragglers only (a piece
+    // packs whole blocks): each one's letters gathered in order and encoded once (letters past the slice = 1)
+    uint8_t tmp[kP33Letters];
+    int64_t blk = -1;
+    for (const PieceOut& po : out)
+      for (const auto& sc : po.stragglers) {
+        if (sc.first / kP33Letters != blk) {
+          if (blk >= 0) p33_block_full(tmp, packed5 + kP33Bytes * blk);
+          blk = sc.first / kP33Letters;
+          std::memset(tmp, 1, sizeof tmp);
+        }
+        tmp[sc.first % kP33Letters] = sc.second;
+      }
+    if (blk >= 0) p33_block_full(tmp, packed5 + kP33Bytes * blk);
+  } else if (packed5) {
     // groups holding letters of two pieces (or the slice's last, partial group): zeroed, then assembled
     for (const PieceOut& po : out)
       for (const auto& sc : po.stragglers) std::memset(packed5 + GB * (sc.first / G), 0, static_cast<size_t>(GB));
-    static constexpr uint32_t kPow26[7] = {1u, 26u, 676u, 17576u, 456976u, 11881376u, 308915776u};
+    static constexpr uint32_t kPow26[5] = {1u, 26u, 676u, 17576u, 456976u};
     for (const PieceOut& po : out)
       for (const auto& sc : po.stragglers) {
-        if (p33) {  // add (code - 1) * 26^j to field x / 7 (bits [33f, 33f+33); serial: the 8-byte window
-                    // rewrites neighbouring fields' bytes unchanged, and a field's sum never leaves its bits)
-          const int64_t bit = 33 * (sc.first / kP33Field);
-          uint64_t w;
-          std::memcpy(&w, packed5 + (bit >> 3), 8);
-          w += (static_cast<uint64_t>(sc.second > 1 ? sc.second - 1u : 0u) * kPow26[sc.first % kP33Field]) << (bit & 7);
-          std::memcpy(packed5 + (bit >> 3), &w, 8);
-          continue;
-        }
         if (p24) {  // add (code - 1) * 26^j to the group value
           uint8_t* q = packed5 + kP24Bytes * (sc.first / kP24Letters);
           uint32_t v = q[0] | (static_cast<uint32_t>(q[1]) << 8) | (static_cast<uint32_t>(q[2]) << 16);
@@ -498,6 +504,8 @@ FillReport BulkParser::fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* p
         packed5[bit >> 3] |= static_cast<uint8_t>(v);
         packed5[(bit >> 3) + 1] |= static_cast<uint8_t>(v >> 8);
       }
+  }
+  if (packed5) {  // read slack past the last group
     const int64_t used = GB * ((s.letters + G - 1) / G);
     const int64_t total = p33 ? packed33_bytes(s.letters) : p24 ? packed24_bytes(s.letters) : packed5_bytes(s.letters);
     std::memset(packed5 + used, 0, static_cast<size_t>(total - used));
