@@ -41,6 +41,8 @@ int moc_unpack24(const uint8_t* packed, int64_t begin, int64_t n, uint8_t* out);
 int64_t moc_packed33_bytes(int64_t n_chars);
 int moc_pack33(const uint8_t* codes, int64_t n, uint8_t* out);
 int moc_unpack33(const uint8_t* packed, int64_t begin, int64_t n, uint8_t* out);
+// narrow record lengths from CSR offsets (moc::pack_lengths): bits 3 / 4 / 8, or 6 = base-6 octets
+int moc_pack_lengths(const int64_t* offsets, int64_t n, int bits, int64_t base, uint8_t* out);
 
 /* ---- score table ---- */
 int moc_score_table(const int32_t* weights4, int32_t* lut1024, uint8_t* cls1024);

@@ -132,6 +132,8 @@ struct ShortArgs {
   const uint8_t* lengths4 = nullptr;  // optional nibble lengths: record i = len_base + nibble i (low first)
   const uint8_t* lengths3 = nullptr;  // optional 3-bit lengths: record i = len_base + bits [3i, 3i+3), LSB
                                       // first (one readable slack byte after the last record's)
+  const uint8_t* lengths6 = nullptr;  // optional base-6 lengths (moc::kLenBase6): 8-byte words of three 21-bit
+                                      // octets, record i = len_base + digit i % 8 of octet i / 8
   int32_t len_base = 0;
   int64_t n = 0;
   void* out = nullptr;                // results, format `fmt`, record i at index i

@@ -81,14 +81,19 @@ struct ResultRun {
 };
 
 // ---- narrow record lengths -------------------------------------------------------------------------
+// `bits` 6 is not a bit width but the base-6 form: lengths of at most 6 values above the base, 8 records'
+// lengths as one 21-bit base-6 number (6^8 = 1 679 616 < 2^21, record 8o+j as digit j of octet o), three
+// octets per aligned little-endian 64-bit word (bits [21f, 21f+21)): 2.667 bits per length (log2 6 = 2.585)
+// against 3 for the 3-bit fields; the kernels load a tile's words with aligned 8-byte loads.
+constexpr int kLenBase6 = 6;
 // Bytes of n lengths at `bits` (3: + one readable slack byte, the kernels load two bytes per length).
 inline int64_t narrow_lengths_bytes(int64_t n, int bits) {
-  return bits == 3 ? (3 * n + 7) / 8 + 1 : bits == 4 ? (n + 1) / 2 : n;
+  return bits == kLenBase6 ? 8 * ((n + 23) / 24) : bits == 3 ? (3 * n + 7) / 8 + 1 : bits == 4 ? (n + 1) / 2 : n;
 }
-// Narrowest of 3/4/8 bits able to hold lengths in [min_l2, max_l2] above base min_l2; 0 when none does.
+// Narrowest of base-6 / 3 / 4 / 8 bits able to hold lengths in [min_l2, max_l2] above base min_l2; 0 when none does.
 inline int narrow_length_bits(int64_t min_l2, int64_t max_l2) {
   const int64_t span = max_l2 - min_l2;
-  return span <= 7 ? 3 : span <= 15 ? 4 : max_l2 <= 255 ? 8 : 0;
+  return span <= 5 ? kLenBase6 : span <= 7 ? 3 : span <= 15 ? 4 : max_l2 <= 255 ? 8 : 0;
 }
 // lengths from CSR offsets (offsets[i+1] - offsets[i] - base) -> out[0..narrow_lengths_bytes(n, bits)),
 // OpenMP over groups of 8 records (no two threads share an output byte). bits 8 stores the raw length.

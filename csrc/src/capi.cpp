@@ -123,6 +123,9 @@ int moc_pack33(const uint8_t* codes, int64_t n, uint8_t* out) {
 int moc_unpack33(const uint8_t* packed, int64_t begin, int64_t n, uint8_t* out) {
   return guard([&] { moc::unpack33(packed, begin, n, out); });
 }
+int moc_pack_lengths(const int64_t* offsets, int64_t n, int bits, int64_t base, uint8_t* out) {
+  return guard([&] { moc::pack_lengths(offsets, n, bits, base, out); });
+}
 
 int moc_score_table(const int32_t* weights4, int32_t* lut1024, uint8_t* cls1024) {
   return guard([&] {

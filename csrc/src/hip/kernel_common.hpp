@@ -210,7 +210,17 @@ __device__ __forceinline__ int64_t tile_offset(const ShortArgs& a, int64_t r) {
 }
 
 // Length of record `idx` of the batch from the narrowest available source.
+__device__ __forceinline__ uint32_t base6_octet(const uint8_t* words, int64_t octet) {
+  const uint64_t w = *reinterpret_cast<const uint64_t*>(words + 8 * (octet / 3));
+  return static_cast<uint32_t>(w >> (21 * static_cast<int>(octet % 3))) & 0x1FFFFFu;
+}
+
 __device__ __forceinline__ int record_length(const ShortArgs& a, int64_t idx) {
+  if (a.lengths6) {
+    uint32_t v = base6_octet(a.lengths6, idx >> 3);
+    for (int j = static_cast<int>(idx & 7); j > 0; --j) v /= 6u;
+    return a.len_base + static_cast<int>(v % 6u);
+  }
   if (a.lengths3) {
     const int64_t bit = 3 * idx;
     const uint32_t w = a.lengths3[bit >> 3] | (static_cast<uint32_t>(a.lengths3[(bit >> 3) + 1]) << 8);
@@ -225,7 +235,19 @@ __device__ __forceinline__ int record_length(const ShortArgs& a, int64_t idx) {
 // two loads instead of one or two per record: for host-resident (zero-copy) batches every load instruction
 // becomes PCIe read requests, and the length loads outnumber the letter loads otherwise.
 __device__ __forceinline__ void record_lengths4(const ShortArgs& a, int64_t i0, int n_valid, int (&L)[4]) {
-  if (n_valid >= 4 && (i0 & 3) == 0 && !(a.lengths3 == nullptr && a.lengths4 == nullptr && a.lengths8 == nullptr)) {
+  if (n_valid >= 4 && (i0 & 3) == 0 &&
+      !(a.lengths3 == nullptr && a.lengths4 == nullptr && a.lengths8 == nullptr && a.lengths6 == nullptr)) {
+    if (a.lengths6) {  // one aligned 8-byte load; the upper half of an octet starts at digit 4 (6^4 = 1296)
+      uint32_t v = base6_octet(a.lengths6, i0 >> 3);
+      if (i0 & 4) v /= 1296u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t d = v / 6u;
+        L[q] = a.len_base + static_cast<int>(v - 6u * d);
+        v = d;
+      }
+      return;
+    }
     if (a.lengths8) {
       const uint32_t w = *reinterpret_cast<const uint32_t*>(a.lengths8 + i0);
 #pragma unroll

@@ -544,6 +544,7 @@ bool HipEngine::direct_pointers(const WireBatch& b, void* out, int fb, dev::Shor
   a.lengths8 = b.lengths && b.len_bits == 8 ? static_cast<const uint8_t*>(dlen) : nullptr;
   a.lengths4 = b.lengths && b.len_bits == 4 ? static_cast<const uint8_t*>(dlen) : nullptr;
   a.lengths3 = b.lengths && b.len_bits == 3 ? static_cast<const uint8_t*>(dlen) : nullptr;
+  a.lengths6 = b.lengths && b.len_bits == kLenBase6 ? static_cast<const uint8_t*>(dlen) : nullptr;
   a.len_base = static_cast<int32_t>(b.len_base);
   a.out = const_cast<void*>(dout);
   return c1 > c0;
@@ -579,7 +580,10 @@ bool HipEngine::streams_packed(int64_t min_l2, int64_t max_l2) const {
 void HipEngine::solve_wire(const WireBatch& batch, void* out, ResultFormat fmt) {
   WireBatch b = batch;
   const int64_t n = b.n;
-  if (b.lengths && b.len_bits != 8 && b.len_bits != 4 && b.len_bits != 3) throw Error("lengths must be 8-, 4- or 3-bit");
+  if (b.lengths && b.len_bits != 8 && b.len_bits != 4 && b.len_bits != 3 && b.len_bits != kLenBase6)
+    throw Error("lengths must be 8-, 4-, 3-bit or base-6");
+  if (b.lengths && b.len_bits == kLenBase6 && (reinterpret_cast<uintptr_t>(b.lengths) & 7))
+    throw Error("base-6 lengths must be 8-byte aligned (the kernels load whole words)");
   if (b.off_shift && (!b.lengths || b.min_l2 < 0 || b.max_l2 < 0 || b.off_shift > 6))
     throw Error("sparse offsets need narrow lengths, the length range and a stride of at most 64 records");
   if (b.device && (b.min_l2 < 0 || b.max_l2 < 0)) throw Error("a device-resident batch needs its length range");
@@ -608,6 +612,8 @@ void HipEngine::solve_wire(const WireBatch& batch, void* out, ResultFormat fmt) 
     throw Error("nibble lengths cannot hold this batch's lengths");
   if (b.len_bits == 3 && b.lengths && (ls.mn < b.len_base || ls.mx > b.len_base + 7))
     throw Error("3-bit lengths cannot hold this batch's lengths");
+  if (b.len_bits == kLenBase6 && b.lengths && (ls.mn < b.len_base || ls.mx > b.len_base + 5))
+    throw Error("base-6 lengths cannot hold this batch's lengths");
   if (fmt == ResultFormat::R4 && (L1_ > 255 || ls.mx > 255 || table_.max_abs() * ls.mx >= 32767))
     throw Error("result format R4 cannot hold this batch");
   if (fmt == ResultFormat::R8 && (L1_ > 65535 || ls.mx > 65535)) throw Error("result format R8 cannot hold this batch");
@@ -624,8 +630,8 @@ void HipEngine::solve_wire(const WireBatch& batch, void* out, ResultFormat fmt) 
   a.packed5 = b.packed5 ? 1 : 0;
   a.packed24 = b.packed24 ? 1 : 0;
   a.packed33 = b.packed33 ? 1 : 0;
-  // the SDMA chunker cuts 5-bit / byte streams
-  const bool dma = opt_.dma_stream && !b.device && !b.packed24 && !b.packed33;
+  // the SDMA chunker cuts 5-bit / byte streams with 3/4/8-bit lengths (its chunks are not 24-record aligned)
+  const bool dma = opt_.dma_stream && !b.device && !b.packed24 && !b.packed33 && !(b.lengths && b.len_bits == kLenBase6);
   const bool swipe = dev::configure_swipe(L1_, ls.mn, ls.mx, table_.max_abs(), a, b.device || dma);
   // packed letters stream straight into the swipe kernel only; other kernels read unpacked bytes. Sparse
   // offsets need whole tiles of 2^off_shift records (the swipe tiles are powers of two >= 64).
@@ -651,7 +657,7 @@ void HipEngine::solve_wire(const WireBatch& batch, void* out, ResultFormat fmt) 
     stats_.kernel_ms = ms;
     stats_.direct = 1;
     stats_.chunks = 1;
-    stats_.h2d_bytes = b.device ? 0 : b.letter_bytes() + (a.lengths3 || a.lengths4 || a.lengths8 ? b.length_bytes() : 8 * n);
+    stats_.h2d_bytes = b.device ? 0 : b.letter_bytes() + (a.lengths3 || a.lengths4 || a.lengths6 || a.lengths8 ? b.length_bytes() : 8 * n);
     stats_.d2h_bytes = b.device ? 0 : static_cast<int64_t>(fb) * n;
     wall.stop();
     stats_.total_ms = wall.total_ms();

@@ -56,8 +56,33 @@ void expand_results(const void* in, ResultFormat f, int64_t n, Result* out, cons
   }
 }
 
+namespace {
+// Base-6 words: word w holds records [24w, 24w+24) (digits past n are 0). len(i) - base, i in [0, n).
+template <typename LenOf>
+void pack_base6(int64_t n, uint8_t* out, LenOf len_of) {
+  const int64_t words = (n + 23) / 24;
+#pragma omp parallel for schedule(static) if (words > 65536)
+  for (int64_t w = 0; w < words; ++w) {
+    uint64_t word = 0;
+    for (int f = 0; f < 3; ++f) {
+      uint32_t v = 0;
+      for (int j = 7; j >= 0; --j) {
+        const int64_t i = 24 * w + 8 * f + j;
+        v = v * 6u + (i < n ? static_cast<uint32_t>(len_of(i)) : 0u);
+      }
+      word |= static_cast<uint64_t>(v) << (21 * f);
+    }
+    std::memcpy(out + 8 * w, &word, 8);
+  }
+}
+}  // namespace
+
 void pack_lengths(const int64_t* offsets, int64_t n, int bits, int64_t base, uint8_t* out) {
-  if (bits != 3 && bits != 4 && bits != 8) throw Error("pack_lengths: bits must be 3, 4 or 8");
+  if (bits == kLenBase6) {
+    pack_base6(n, out, [&](int64_t i) { return offsets[i + 1] - offsets[i] - base; });
+    return;
+  }
+  if (bits != 3 && bits != 4 && bits != 8) throw Error("pack_lengths: bits must be 3, 4, 6 (base 6) or 8");
   const int64_t groups = (n + 7) / 8;  // 8 records -> 3 / 4 / 8 bytes, independent per group
 #pragma omp parallel for schedule(static) if (groups > 65536)
   for (int64_t g = 0; g < groups; ++g) {
@@ -75,7 +100,11 @@ void pack_lengths(const int64_t* offsets, int64_t n, int bits, int64_t base, uin
 }
 
 void pack_lengths16(const uint16_t* lengths, int64_t n, int bits, int64_t base, uint8_t* out) {
-  if (bits != 3 && bits != 4 && bits != 8) throw Error("pack_lengths16: bits must be 3, 4 or 8");
+  if (bits == kLenBase6) {
+    pack_base6(n, out, [&](int64_t i) { return static_cast<int64_t>(lengths[i]) - base; });
+    return;
+  }
+  if (bits != 3 && bits != 4 && bits != 8) throw Error("pack_lengths16: bits must be 3, 4, 6 (base 6) or 8");
   const int64_t groups = (n + 7) / 8;
 #pragma omp parallel for schedule(static) if (groups > 65536)
   for (int64_t g = 0; g < groups; ++g) {
@@ -107,6 +136,13 @@ void expand_offsets(const int64_t* sparse, int shift, const uint8_t* lengths, in
 
 int64_t narrow_length(const uint8_t* lengths, int bits, int64_t base, int64_t i) {
   if (bits == 8) return lengths[i];
+  if (bits == kLenBase6) {
+    uint64_t word;
+    std::memcpy(&word, lengths + 8 * (i / 24), 8);
+    uint32_t v = static_cast<uint32_t>(word >> (21 * ((i / 8) % 3))) & 0x1FFFFFu;
+    for (int64_t j = i % 8; j > 0; --j) v /= 6u;
+    return base + v % 6u;
+  }
   if (bits == 4) return base + ((lengths[i / 2] >> (4 * (i & 1))) & 15);
   const int64_t bit = 3 * i;
   const uint32_t w = lengths[bit >> 3] | (static_cast<uint32_t>(lengths[(bit >> 3) + 1]) << 8);

@@ -620,9 +620,9 @@ void test_slices() {
 // Narrow record lengths (3 / 4 / 8 bits) round-trip through the host decoder.
 void test_narrow_lengths() {
   std::mt19937 rng(3);
-  for (int bits : {3, 4, 8})
-    for (int n : {0, 1, 7, 8, 9, 1000, 100003}) {
-      const int span = bits == 3 ? 8 : bits == 4 ? 16 : 200;
+  for (int bits : {3, 4, 8, kLenBase6})
+    for (int n : {0, 1, 7, 8, 9, 23, 24, 25, 1000, 100003}) {
+      const int span = bits == 3 ? 8 : bits == 4 ? 16 : bits == kLenBase6 ? 6 : 200;
       std::vector<int64_t> offs(static_cast<size_t>(n) + 1, 0);
       for (int i = 0; i < n; ++i) offs[i + 1] = offs[i] + 6 + static_cast<int64_t>(rng() % span);
       std::vector<uint8_t> out(static_cast<size_t>(narrow_lengths_bytes(n, bits)) + 1, 0xAB);
@@ -631,8 +631,32 @@ void test_narrow_lengths() {
       for (int i = 0; i < n; ++i) ok = ok && narrow_length(out.data(), bits, 6, i) == offs[i + 1] - offs[i];
       CHECK(ok);
       if (bits == 3) CHECK(out[narrow_lengths_bytes(n, 3) - 1] == 0);
+      // the same packing from uint16 lengths
+      std::vector<uint16_t> l16(static_cast<size_t>(n) + 1);
+      for (int i = 0; i < n; ++i) l16[i] = static_cast<uint16_t>(offs[i + 1] - offs[i]);
+      std::vector<uint8_t> out16(out.size(), 0xAB);
+      pack_lengths16(l16.data(), n, bits, 6, out16.data());
+      CHECK(std::equal(out.begin(), out.begin() + narrow_lengths_bytes(n, bits), out16.begin()));
+      // sparse offsets + narrow lengths -> dense offsets
+      if (n > 0) {
+        std::vector<int64_t> sp(static_cast<size_t>(sparse_count(n, kSparseShift)));
+        for (size_t j = 0; j < sp.size(); ++j) sp[j] = offs[std::min<int64_t>(static_cast<int64_t>(j) << kSparseShift, n)];
+        std::vector<int64_t> dense(static_cast<size_t>(n) + 1, -1);
+        expand_offsets(sp.data(), kSparseShift, out.data(), bits, bits == 8 ? 0 : 6, n, dense.data());
+        if (bits != 8) CHECK(dense == offs);
+      }
     }
-  CHECK(narrow_length_bits(6, 11) == 3 && narrow_length_bits(6, 21) == 4 && narrow_length_bits(1, 255) == 8);
+  if (true) {  // base 6: 8 lengths per 21-bit octet, 3 octets per little-endian word
+    const int64_t offs[9] = {0, 11, 17, 23, 29, 35, 41, 47, 58};  // lengths 11, 6, 6, 6, 6, 6, 6, 11
+    uint8_t w[8];
+    pack_lengths(offs, 8, kLenBase6, 6, w);
+    uint64_t word;
+    std::memcpy(&word, w, 8);
+    CHECK(word == 5ull + 5ull * 279936ull);  // digit 0 and digit 7 (6^7) hold 5
+  }
+  CHECK(narrow_lengths_bytes(25, kLenBase6) == 16);
+  CHECK(narrow_length_bits(6, 11) == kLenBase6 && narrow_length_bits(6, 13) == 3 && narrow_length_bits(6, 21) == 4 &&
+        narrow_length_bits(1, 255) == 8);
   CHECK(narrow_length_bits(1, 256) == 0);
 }
 

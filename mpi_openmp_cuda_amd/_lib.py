@@ -57,6 +57,7 @@ def _decl(lib):
         "moc_packed33_bytes": (c_int64, [c_int64]),
         "moc_pack33": (c_int, [c_void_p, c_int64, c_void_p]),
         "moc_unpack33": (c_int, [c_void_p, c_int64, c_int64, c_void_p]),
+        "moc_pack_lengths": (c_int, [c_void_p, c_int64, c_int, c_int64, c_void_p]),
         "moc_cpu_solve": (c_int, [P(c_int32), c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p]),
         "moc_cpu_solve_keys": (c_int, [P(c_int32), c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_int, c_int,
                                        c_int, c_void_p]),

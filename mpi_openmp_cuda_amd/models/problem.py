@@ -69,6 +69,35 @@ def lengths3_bytes(n: int) -> int:
     return (3 * int(n) + 7) // 8 + 1 if n else 1
 
 
+LEN_BASE6 = 6  # len_bits value of the base-6 form (moc::kLenBase6)
+
+
+def lengths6_bytes(n: int) -> int:
+    """Bytes of n base-6 lengths: 8-byte words of three 21-bit octets (24 records per word)."""
+    return 8 * ((int(n) + 23) // 24)
+
+
+def pack_lengths6(lengths: np.ndarray, base: int, out: np.ndarray = None) -> np.ndarray:
+    """Record lengths in [base, base + 5] -> base 6: 8 records' lengths as one 21-bit number (record 8o + j
+    = digit j of octet o, 6^8 < 2^21), three octets per little-endian 64-bit word at bits [21f, 21f+21) —
+    2.667 bits per length for batches whose lengths span <= 6 values (input6-shaped: 6..11)."""
+    v = np.asarray(lengths).astype(np.int64) - int(base)
+    if v.size and (v.min() < 0 or v.max() > 5):
+        raise ValueError("lengths do not fit base 6 above the base")
+    n = v.shape[0]
+    words = (n + 23) // 24
+    if out is None:
+        out = np.empty(8 * words, dtype=np.uint8)
+    assert out.dtype == np.uint8 and out.shape[0] >= 8 * words
+    d = np.zeros(words * 24, dtype=np.uint64)
+    d[:n] = v
+    d = d.reshape(words, 3, 8)
+    octets = (d * (6 ** np.arange(8, dtype=np.uint64))).sum(axis=2, dtype=np.uint64)
+    w = octets[:, 0] | (octets[:, 1] << np.uint64(21)) | (octets[:, 2] << np.uint64(42))
+    out[:8 * words] = w.astype("<u8").view(np.uint8)
+    return out
+
+
 def pack_lengths4(lengths: np.ndarray, base: int, out: np.ndarray = None) -> np.ndarray:
     """Record lengths in [base, base + 15] -> 4 bits each, two per byte (record i in the low nibble of
     byte i // 2 when i is even, the high nibble when odd) — the streaming kernels' narrowest length form."""

@@ -202,7 +202,8 @@ class HipSearchEngine:
             out = np.empty(n, dtype=_lib.FORMAT_DTYPES[fid])
         assert out.dtype.itemsize == _lib.FORMAT_DTYPES[fid].itemsize and out.size >= n
         if lengths is not None:
-            need = n if lengths_bits == 8 else (n + 1) // 2 if lengths_bits == 4 else (3 * n + 7) // 8 + 1
+            need = (n if lengths_bits == 8 else (n + 1) // 2 if lengths_bits == 4
+                    else 8 * ((n + 23) // 24) if lengths_bits == 6 else (3 * n + 7) // 8 + 1)
             assert lengths.dtype == np.uint8 and lengths.shape[0] >= need
         lo, hi = l2_range if l2_range is not None else (-1, -1)
         _lib.check(_lib.lib().moc_engine_solve_ex(self._h, _lib.ptr(codes), _lib.ptr(offsets), _lib.ptr(lengths),

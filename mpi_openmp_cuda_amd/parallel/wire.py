@@ -16,8 +16,9 @@ from typing import Callable, Optional
 
 import numpy as np
 
-from ..models.problem import (lengths3_bytes, pack5, pack24, pack33, pack_lengths3, pack_lengths4, packed5_bytes,
-                              packed24_bytes, packed33_bytes, unpack5, unpack24, unpack33)
+from ..models.problem import (LEN_BASE6, lengths3_bytes, lengths6_bytes, pack5, pack24, pack33, pack_lengths3,
+                              pack_lengths4, pack_lengths6, packed5_bytes, packed24_bytes, packed33_bytes, unpack5,
+                              unpack24, unpack33)
 
 LETTER_FORMATS = ("p33", "p24", "p5", "bytes")
 
@@ -30,8 +31,11 @@ def private_alloc(name: str, dtype, count: int) -> np.ndarray:
 
 
 def length_bits(l2_min: int, l2_max: int, narrow: bool = True) -> int:
-    """Bits per record length: 3 or 4 above the minimum when the range allows, else 8 (0: offsets only)."""
+    """Length form: 6 (base 6, 2.667 bits), 3 or 4 bits above the minimum when the range allows, else 8
+    (0: offsets only)."""
     span = l2_max - l2_min
+    if narrow and span <= 5:
+        return LEN_BASE6
     if narrow and span <= 7:
         return 3
     if narrow and span <= 15:
@@ -61,8 +65,11 @@ class WireSlice:
         np.cumsum(lengths, out=self.offsets[1:])
         self.total = int(self.offsets[-1])
         self.len_bits = length_bits(self.l2_min, self.l2_max, narrow)
-        self.len_base = self.l2_min if self.len_bits in (3, 4) else 0
-        if self.len_bits == 3:
+        self.len_base = self.l2_min if self.len_bits in (3, 4, LEN_BASE6) else 0
+        if self.len_bits == LEN_BASE6:
+            self.lengths = alloc("lengths6", np.uint8, lengths6_bytes(n))
+            pack_lengths6(lengths, self.len_base, out=self.lengths)
+        elif self.len_bits == 3:
             self.lengths = alloc("lengths3", np.uint8, lengths3_bytes(n))
             pack_lengths3(lengths, self.len_base, out=self.lengths)
         elif self.len_bits == 4:
@@ -145,6 +152,11 @@ class WireSlice:
     def decoded_lengths(self) -> np.ndarray:
         """Record lengths back from the narrow fields (or the offsets when there are none)."""
         n = self.n
+        if self.len_bits == LEN_BASE6:
+            w = np.asarray(self.lengths[:lengths6_bytes(n)]).view("<u8").astype(np.uint64)
+            octets = np.stack([(w >> np.uint64(21 * f)) & np.uint64(0x1FFFFF) for f in range(3)], axis=1).reshape(-1)
+            digits = (octets[:, None] // (6 ** np.arange(8, dtype=np.uint64))) % np.uint64(6)
+            return digits.reshape(-1)[:n].astype(np.int64) + self.len_base
         if self.len_bits == 3:
             b = np.zeros(lengths3_bytes(n) + 4, np.uint8)
             b[:self.lengths.shape[0]] = self.lengths

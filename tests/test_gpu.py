@@ -228,6 +228,31 @@ def test_swipe_wire_slices(L1, lo, hi, w, letters):
     eng.close()
 
 
+@pytest.mark.parametrize("L1,lo,hi", [(80, 40, 45), (100, 50, 55)])
+def test_short_kernel_base6_lengths(L1, lo, hi):
+    # byte letters + base-6 lengths through the lane-per-offset short kernel (records longer than 32 letters
+    # leave the swipe kernel; at most 64 lanes per record keep them on the short one)
+    from mpi_openmp_cuda_amd._lib import Pinned
+    from mpi_openmp_cuda_amd.parallel.wire import WireSlice
+
+    rng = np.random.default_rng(L1 + lo)
+    s1 = "".join(chr(65 + x) for x in rng.integers(0, 26, L1))
+    lens = rng.integers(lo, hi + 1, 30011)
+    recs = ["".join(chr(65 + x) for x in rng.integers(0, 26, n)) for n in lens]
+    prob = Problem.from_strings((3, 2, 1, 4), s1, recs)
+    eng = HipSearchEngine(device=0)
+    eng.set_problem(prob.weights, prob.seq1)
+    ws = WireSlice.from_csr(prob.codes, prob.offsets, letter_format="bytes")
+    assert ws.len_bits == 6
+    ws.alloc_results(eng)
+    with Pinned(*ws.arrays()):
+        ws.solve(eng)
+    st = eng.stats()
+    assert np.array_equal(ws.triples(eng), as_triples(search_cpu(prob))), st
+    assert st["direct"] == 1 and st["kernels"] == ["short"], st
+    eng.close()
+
+
 @pytest.mark.parametrize("fmt", ["r8", "r4", "auto"])
 def test_staged_formats(engine, fmt):
     prob = make_synthetic("input1", 5000, seed=4)
@@ -544,13 +569,14 @@ def test_pinned_neighbours_staged_copies():
 
 
 @pytest.mark.parametrize("mode", ["dma", "zero_copy"])
-@pytest.mark.parametrize("packed,len_bits", [(False, 0), (False, 8), (True, 4), (True, 8), (True, 3), (False, 3)])
+@pytest.mark.parametrize("packed,len_bits", [(False, 0), (False, 8), (True, 4), (True, 8), (True, 3), (False, 3),
+                                             (True, 6), (False, 6)])
 @pytest.mark.parametrize("shape,n", [("input6", 100_003), ("input1", 20_001)])
 def test_host_stream_modes(monkeypatch, mode, packed, len_bits, shape, n):
     # pinned host batches: chunked SDMA in/out around the HBM-resident kernel (64 KiB chunks: many of
     # them, odd tail) or the kernel's own zero-copy reads/writes — same answers
     from mpi_openmp_cuda_amd import _lib
-    from mpi_openmp_cuda_amd.models.problem import pack5, pack_lengths3, pack_lengths4
+    from mpi_openmp_cuda_amd.models.problem import pack5, pack_lengths3, pack_lengths4, pack_lengths6
     from mpi_openmp_cuda_amd.utils.synthetic import SHAPES
 
     monkeypatch.setenv("MOC_DMA_STREAM", "1" if mode == "dma" else "0")
@@ -575,12 +601,19 @@ def test_host_stream_modes(monkeypatch, mode, packed, len_bits, shape, n):
             pytest.skip("lengths span more than 3 bits")
         lengths = pack_lengths3(np.diff(prob.offsets), sh.l2_min)
         kw = dict(lengths=lengths, lengths_bits=3, lengths_base=sh.l2_min)
+    elif len_bits == 6:
+        if sh.l2_max - sh.l2_min > 5:
+            pytest.skip("lengths span more than 6 values")
+        lengths = pack_lengths6(np.diff(prob.offsets), sh.l2_min)
+        kw = dict(lengths=lengths, lengths_bits=6, lengths_base=sh.l2_min)
     out = np.zeros(prob.n, dtype=_lib.FORMAT_DTYPES[_lib.FORMAT_NAMES.index("r8")])
     eng.pin(codes, prob.offsets, out, *([lengths] if lengths is not None else []))
     eng.solve(codes, prob.offsets, out=out, fmt="r8", packed5=packed, **kw)
     st = eng.stats()
-    assert st["direct"] == 1 and st["dma"] == (1 if mode == "dma" else 0), st
-    if mode == "dma":
+    # base-6 lengths stay on the zero-copy path (the SDMA chunks are not 24-record aligned)
+    dma = mode == "dma" and len_bits != 6
+    assert st["direct"] == 1 and st["dma"] == (1 if dma else 0), st
+    if dma:
         assert st["chunks"] > 3, st
     assert np.array_equal(as_triples(out), as_triples(search_cpu(prob))), st
     eng.close()

@@ -8,8 +8,9 @@ from mpi_openmp_cuda_amd.parallel.wire import WireSlice, length_bits
 from mpi_openmp_cuda_amd.utils.synthetic import make_synthetic
 
 
-@pytest.mark.parametrize("lo,hi,narrow,bits", [(6, 11, True, 3), (6, 11, False, 8), (5, 20, True, 4),
-                                               (1, 200, True, 8), (1, 300, True, 0), (7, 7, True, 3)])
+@pytest.mark.parametrize("lo,hi,narrow,bits", [(6, 11, True, 6), (6, 13, True, 3), (6, 11, False, 8),
+                                               (5, 20, True, 4), (1, 200, True, 8), (1, 300, True, 0),
+                                               (7, 7, True, 6)])
 def test_length_fields_round_trip(lo, hi, narrow, bits):
     rng = np.random.default_rng(lo * 1000 + hi)
     n = 1001
@@ -34,7 +35,7 @@ def test_from_csr_slice_of_absolute_offsets():
     assert ws.n == e - b
     assert np.array_equal(ws.decoded_lengths(), np.diff(prob.offsets[b:e + 1]))
     assert np.array_equal(ws.letters(), prob.codes[prob.offsets[b]:prob.offsets[e]])
-    assert ws.letter_format == "p33" and ws.len_bits == 3 and ws.len_base == 6
+    assert ws.letter_format == "p33" and ws.len_bits == 6 and ws.len_base == 6
 
 
 def test_custom_allocator_places_every_array():
@@ -46,7 +47,7 @@ def test_custom_allocator_places_every_array():
 
     prob = make_synthetic("input6", 100, seed=1)
     ws = WireSlice.from_csr(prob.codes, prob.offsets, alloc=alloc)
-    assert names == ["offsets", "lengths3", "codes33"]
+    assert names == ["offsets", "lengths6", "codes33"]
     assert len(ws.arrays()) == 3  # results come later (their format is the engine's choice)
 
 
@@ -91,3 +92,22 @@ def test_p33_fields():
     # 4.714 bits per letter: 1.8% fewer bytes than P24 on a large stream
     n = 56 * 1000
     assert packed33_bytes(n) - 16 == 33000 and (3 * n // 5) == 33600
+
+
+def test_base6_lengths_match_native_packer():
+    # the numpy packer (WireSlice, bench.py) and the native one (final's parser) write the same words
+    from mpi_openmp_cuda_amd import _lib
+    from mpi_openmp_cuda_amd.models.problem import lengths6_bytes, pack_lengths6
+
+    rng = np.random.default_rng(6)
+    for n in (1, 7, 8, 23, 24, 25, 1000, 99_991):
+        lengths = rng.integers(6, 12, size=n)
+        offsets = np.zeros(n + 1, np.int64)
+        np.cumsum(lengths, out=offsets[1:])
+        got = pack_lengths6(lengths, 6)
+        assert got.shape[0] == lengths6_bytes(n) == 8 * ((n + 23) // 24)
+        want = np.zeros_like(got)
+        _lib.check(_lib.lib().moc_pack_lengths(_lib.ptr(offsets), n, 6, 6, _lib.ptr(want)))
+        assert np.array_equal(got, want), n
+    with pytest.raises(ValueError):
+        pack_lengths6(np.array([6, 12]), 6)
