@@ -12,7 +12,7 @@ One timed step = the search of one complete job over the global batch (reference
      (zero-copy over its own PCIe link), runs the gfx950 search kernel, and writes the (score, n, k)
      results back into the node-shared result array the root prints from,
   4. an all-reduce of the per-rank record counts closes the job (the reference's MPI_Gather point).
-The records are held in the wire formats `./final` writes while it parses (P33 letters: 7 per 33 bits, 3-bit lengths,
+The records are held in the wire formats `./final` writes while it parses (P33 letters: 7 per 33 bits, base-6 lengths,
 R2 results; csrc/include/moc/wire.hpp): encoding them is the untimed set-up here, as parsing and printing
 are outside `./final`'s compute phase, whose `--timing` shows the same kernel time for the same letters
 (profiles/final_scale_1.1G_r2_p33.log: 13.13 ms kernel at 1.14 G letters; profiles/bench_input6_1gpu_1.1G_p33.log:
@@ -58,6 +58,8 @@ def parse_args():
     ap.add_argument("--letters", default="p33", choices=["p33", "p24", "p5", "bytes"],
                     help="letter wire format: 7 letters per 33-bit field (p33), base-26 groups of 5 in 3 bytes "
                          "(p24), 5-bit packed (p5), bytes")
+    ap.add_argument("--lengths", default="auto", choices=["auto", "bits3"],
+                    help="record length form: auto (base-6 octets when the lengths span <= 6 values) or 3-bit fields")
     ap.add_argument("--narrow", type=int, default=1,
                     help="1: narrowest wire formats that fit (4-bit lengths, R2 results); 0: uint8 lengths, R4")
     ap.add_argument("--dump-steps", default="", help="rank 0 writes its per-step kernel and host ms to this JSON file")
@@ -112,7 +114,7 @@ class HostArrays:
     wire formats `./final` writes while it parses (mpi_openmp_cuda_amd/parallel/wire.py: the same
     WireSlice the distributed driver's golden tests run)."""
 
-    def __init__(self, tag, rank, lengths, use_shm, letter_format, seed, narrow, hip_alloc=False):
+    def __init__(self, tag, rank, lengths, use_shm, letter_format, seed, narrow, hip_alloc=False, base6=True):
         from mpi_openmp_cuda_amd.parallel.wire import WireSlice
         from mpi_openmp_cuda_amd.utils.synthetic import fill_codes
 
@@ -146,7 +148,7 @@ class HostArrays:
         # letters: random codes 1..26, encoded once (P24 groups, narrow lengths) like final's parser does
         letters = np.empty(total, dtype=np.uint8)
         fill_codes(letters, seed)
-        self.wire = WireSlice(lengths, letters, letter_format=letter_format, narrow=narrow, alloc=mk)
+        self.wire = WireSlice(lengths, letters, letter_format=letter_format, narrow=narrow, alloc=mk, base6=base6)
         self.check_letters = letters[:min(total, 1 << 22)].copy()  # kept for the untimed verification
         del letters
 
@@ -236,7 +238,7 @@ def main():
     tag = os.environ.get("MASTER_PORT", str(os.getpid()))
     progress(f"generating {R} records per rank")
     host = HostArrays(tag, rank, lengths, bool(args.shm), args.letters, args.seed + 101 + rank, bool(args.narrow),
-                      hip_alloc=args.host_alloc == "hip")
+                      hip_alloc=args.host_alloc == "hip", base6=args.lengths == "auto")
     wire = host.wire
     progress(f"{wire.total} letters per rank ready")
     del lengths

@@ -46,11 +46,12 @@ def length_bits(l2_min: int, l2_max: int, narrow: bool = True) -> int:
 class WireSlice:
     """A CSR slice (record lengths + byte letter codes 1..26) encoded once into the wire formats.
 
-    ``letters``: ``p33`` (default), ``p24``, ``p5`` or ``bytes``; ``alloc`` places every array (so a benchmark
+    ``letters``: ``p33`` (default), ``p24``, ``p5`` or ``bytes``; ``base6``: False keeps 3-bit length fields
+    where base-6 octets would fit; ``alloc`` places every array (so a benchmark
     can put them in node-shared or hipHostMalloc memory)."""
 
     def __init__(self, lengths: np.ndarray, letters: Optional[np.ndarray], letter_format: str = "p33",
-                 narrow: bool = True, alloc: Alloc = private_alloc):
+                 narrow: bool = True, alloc: Alloc = private_alloc, base6: bool = True):
         if letter_format not in LETTER_FORMATS:
             raise ValueError(f"letter_format must be one of {LETTER_FORMATS}")
         lengths = np.asarray(lengths)
@@ -65,6 +66,8 @@ class WireSlice:
         np.cumsum(lengths, out=self.offsets[1:])
         self.total = int(self.offsets[-1])
         self.len_bits = length_bits(self.l2_min, self.l2_max, narrow)
+        if self.len_bits == LEN_BASE6 and not base6:  # 3-bit fields instead (A/B)
+            self.len_bits = 3
         self.len_base = self.l2_min if self.len_bits in (3, 4, LEN_BASE6) else 0
         if self.len_bits == LEN_BASE6:
             self.lengths = alloc("lengths6", np.uint8, lengths6_bytes(n))
