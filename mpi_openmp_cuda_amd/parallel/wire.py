@@ -2,7 +2,7 @@
 
 ``./final`` writes these forms straight from its parser (``BulkParser::fill_slice``): letters as 33-bit
 fields of 7 (P33, 4.714 bits per letter; or base-26 groups of 5 in 3 bytes, P24, or 5-bit packed, or bytes),
-record lengths as 3/4-bit fields above the slice's shortest length (8-bit, or offsets only, when the range
+record lengths as base-6 octets or 3/4-bit fields above the slice's shortest length (8-bit, or offsets only, when the range
 is wider), results in the narrowest format the problem's bounds allow (R2: one uint16 per record). The
 streaming kernel reads them zero-copy from page-locked host memory, so every byte saved is PCIe time saved.
 
