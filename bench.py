@@ -359,7 +359,7 @@ def main():
             "rank0_d2h_bytes_per_step": int(st["d2h_bytes"]),
             "host_arrays": "hip_host_malloc" if host.bufs else ("shm" if host.shm else "private"),
             "result_format": fmt,
-            "lengths_bits": wire.len_bits,
+            "lengths": "base6" if wire.len_bits == 6 else (f"{wire.len_bits}bit" if wire.len_bits else "offsets"),
             "letters": wire.letter_format,
             "rank0_numa_node": numa,
             "rccl_world": dist.get_world_size() if (distributed and nccl) else (1 if nccl else None),
