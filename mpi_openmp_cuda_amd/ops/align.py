@@ -142,6 +142,8 @@ class HipSearchEngine:
         if not self._h:
             raise _lib.NativeError(L.moc_last_error().decode())
         self.problem_L1 = None
+        self._problem_key = None  # (weights, seq1, semantics) bytes of the problem in the engine
+        self._stats_buf = (ctypes.c_double * 14)()
 
     def close(self):
         if getattr(self, "_h", None):
@@ -156,10 +158,19 @@ class HipSearchEngine:
 
     def set_problem(self, weights, seq1: np.ndarray, semantics=Semantics.REFERENCE):
         seq1 = np.ascontiguousarray(seq1, dtype=np.uint8)
+        if isinstance(weights, np.ndarray) and semantics is Semantics.REFERENCE:
+            # a job loop re-sending the same problem (the engine keeps an unchanged image anyway): no
+            # conversion or native call at all
+            key = (weights.tobytes(), seq1.tobytes())
+            if key == self._problem_key:
+                return
+        else:
+            key = None
         _lib.check(_lib.lib().moc_engine_set_problem(
             self._h, _lib.weights_arg(Weights.of(weights).as_list()), _lib.ptr(seq1), seq1.shape[0],
             int(Semantics.parse(semantics))))
         self.problem_L1 = int(seq1.shape[0])
+        self._problem_key = key
 
     def pin(self, *arrays):
         """Page-locks host arrays for the engine's lifetime (enables the zero-copy path)."""
@@ -269,6 +280,16 @@ class HipSearchEngine:
             n, ctypes.c_void_p(keys_t.data_ptr()), ctypes.c_void_p(out_t.data_ptr()), 0,
             ctypes.c_void_p(stream.cuda_stream)))
         return out_t
+
+    def kernel_times(self) -> tuple:
+        """(kernel_ms, total_ms) of the last solve: the two fields a timed loop reads, without stats()'s dict."""
+        v = self._stats_buf
+        _lib.check(_lib.lib().moc_engine_stats(self._h, v))
+        return v[0], v[1]
+
+    def solve_prepared(self, args: tuple):
+        """Re-runs a solve whose native arguments were marshalled once (WireSlice.solve): same call."""
+        _lib.check(_lib.lib().moc_engine_solve_ex(self._h, *args))
 
     def stats(self) -> dict:
         v = (ctypes.c_double * 14)()

@@ -125,9 +125,27 @@ class WireSlice:
         return [a for a in (self.codes, self.offsets, self.lengths, self.results) if a is not None]
 
     def solve(self, engine) -> np.ndarray:
-        """One search of the slice into ``results`` (zero-copy when every array is page-locked)."""
+        """One search of the slice into ``results`` (zero-copy when every array is page-locked). The native
+        arguments are marshalled on the first call and reused while the engine and result array stay the same
+        (a job loop over one slice pays no per-call argument conversion)."""
         if self.results is None:
             self.alloc_results(engine)
+        prepared = getattr(self, "_prepared", None)
+        if prepared is not None and prepared[0] is engine and prepared[1] is self.results:
+            engine.solve_prepared(prepared[2])
+            return self.results
+        from .. import _lib
+
+        fid = _lib.FORMAT_NAMES.index(self.fmt)
+        letters = {"p5": 1, "p24": 2, "p33": 3}.get(self.letter_format, 0)
+        args = (_lib.ptr(self.codes), _lib.ptr(self.offsets), _lib.ptr(self.lengths), int(self.len_bits or 8),
+                int(self.len_base), self.n, _lib.ptr(self.results), fid, int(self.l2_min), int(self.l2_max), letters)
+        self._prepared = (engine, self.results, args)
+        self._solve_checked(engine)
+        return self.results
+
+    def _solve_checked(self, engine) -> np.ndarray:
+        """The first solve through the engine's checked entry point (asserts shapes and formats)."""
         return engine.solve(self.codes, self.offsets, out=self.results, lengths=self.lengths, fmt=self.fmt,
                             l2_range=(self.l2_min, self.l2_max), packed5=self.letter_format == "p5",
                             packed24=self.letter_format == "p24", packed33=self.letter_format == "p33",
