@@ -111,3 +111,42 @@ def test_base6_lengths_match_native_packer():
         assert np.array_equal(got, want), n
     with pytest.raises(ValueError):
         pack_lengths6(np.array([6, 12]), 6)
+
+
+def test_prepared_solve_passes_the_checked_arguments(monkeypatch):
+    # WireSlice.solve marshals the native arguments once and replays them: the replay must equal what the
+    # checked HipSearchEngine.solve passes, and a new result array must go through the checked path again
+    import ctypes
+
+    from mpi_openmp_cuda_amd import _lib
+    from mpi_openmp_cuda_amd.ops.align import HipSearchEngine
+
+    calls = []
+
+    class Stub:
+        def __getattr__(self, name):
+            return lambda *a: (calls.append((name, a)) or 0)
+
+    monkeypatch.setattr(_lib, "lib", lambda: Stub())
+    eng = HipSearchEngine.__new__(HipSearchEngine)
+    eng._h, eng._problem_key, eng._stats_buf = ctypes.c_void_p(1), None, (ctypes.c_double * 14)()
+    prob = make_synthetic("input6", 5000, seed=2)
+    for fmt in ("p33", "p24", "p5", "bytes"):
+        ws = WireSlice.from_csr(prob.codes, prob.offsets, letter_format=fmt)
+        ws.fmt, ws.results = "r2", np.zeros(ws.n, np.uint16)
+        ws.solve(eng)
+        ws.solve(eng)
+        (n1, a1), (n2, a2) = calls[-2], calls[-1]
+        val = lambda args: [getattr(x, "value", x) for x in args[1:]]
+        assert n1 == n2 == "moc_engine_solve_ex" and val(a1) == val(a2), fmt
+        ws.results = np.zeros(ws.n, np.uint16)  # another result array: re-marshalled
+        ws.solve(eng)
+        assert val(calls[-1][1])[6] == ws.results.ctypes.data
+    # set_problem: an unchanged problem makes no native call
+    w, s1 = np.array([4, 3, 2, 10], np.int32), prob.seq1
+    eng.set_problem(w, s1)
+    k = len(calls)
+    eng.set_problem(w.copy(), s1.copy())
+    assert len(calls) == k
+    eng.set_problem(np.array([4, 3, 2, 9], np.int32), s1)
+    assert len(calls) == k + 1
