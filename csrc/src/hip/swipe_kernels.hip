@@ -470,13 +470,16 @@ void preload_swipe_kernels() {
   (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&swipe_search_kernel<24, 4, 3>));
 }
 
-// MOC_SWIPE_TAIL=0 keeps every tile at full size (A/B)
-static bool tail_enabled() {
-  static const bool on = [] {
+// MOC_SWIPE_TAIL=0 keeps every tile at full size (A/B); otherwise the tail tiles are 1/MOC_SWIPE_TAIL of a
+// tile (default 4; 2..16)
+static int tail_div() {
+  static const int d = [] {
     const char* v = std::getenv("MOC_SWIPE_TAIL");
-    return !(v && std::atoi(v) == 0);
+    if (!v) return 4;
+    const int x = std::atoi(v);
+    return x == 0 ? 0 : std::max(2, std::min(16, x));
   }();
-  return on;
+  return d;
 }
 
 void launch_swipe(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStream_t stream) {
@@ -487,12 +490,13 @@ void launch_swipe(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStr
   const int per_cu = std::max(1, std::min(8, 160 * 1024 / std::max(lay.total, 1)));
   const int64_t slots = static_cast<int64_t>(num_cus) * per_cu;
   ShortArgs b = a;
-  // the last `slots` tiles' records go in quarter tiles: the tail of the persistent grid (blocks idling
-  // while the last tiles finish) shrinks 4x
+  // the last `slots` tiles' records go in quarter tiles (MOC_SWIPE_TAIL): the tail of the persistent grid
+  // (blocks idling while the last tiles finish) shrinks 4x
   const int64_t n_big = (a.n + a.tile_records - 1) / a.tile_records;
-  if (a.tile_records >= 256 && n_big > 2 * slots && tail_enabled()) {
+  const int div = tail_div();
+  if (div && a.tile_records / div >= 64 && n_big > 2 * slots) {
     b.tail_from = n_big - slots;
-    b.tail_records = a.tile_records / 4;
+    b.tail_records = a.tile_records / div;
   }
   const int64_t big_end = b.tail_records ? b.tail_from * b.tile_records : b.n;
   const int64_t n_tiles =
