@@ -83,7 +83,9 @@ void CpuDeviceSearch::solve(const WireBatch& b, void* out, ResultFormat fmt) {
   const int64_t c0 = rb.offsets[0], letters = rb.offsets[b.n] - c0;
   for (auto& o : rb.offsets) o -= c0;
   rb.codes.resize(static_cast<size_t>(letters));
-  if (b.packed24)
+  if (b.packed33)
+    unpack33(b.letters, c0, letters, rb.codes.data());
+  else if (b.packed24)
     unpack24(b.letters, c0, letters, rb.codes.data());
   else if (b.packed5)
     unpack5(b.letters, c0, letters, rb.codes.data());

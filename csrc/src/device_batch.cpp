@@ -30,7 +30,7 @@ inline int64_t al16(int64_t x) { return (x + 15) & ~int64_t{15}; }
 // root's DeviceSearch answers for all of them) and broadcast through the device layer.
 struct RankPlan {
   int64_t n = 0, first = 0, letters = 0, min_l2 = 0, max_l2 = 0;
-  int64_t narrow = 0;  // 1: P24 letters + narrow lengths + sparse offsets; 0: 5-bit letters + dense offsets
+  int64_t narrow = 0;  // 1: P33 letters + narrow lengths + sparse offsets; 0: 5-bit letters + dense offsets
   int64_t bits = 0, fmt = 0;
   int64_t off_letters = 0, off_offsets = 0, off_lengths = 0, block = 0;  // block layout (bytes)
 };
@@ -38,7 +38,7 @@ static_assert(sizeof(RankPlan) == 12 * sizeof(int64_t), "plan table entries are 
 
 void layout(RankPlan& pl) {
   pl.off_letters = 0;
-  pl.off_offsets = al16(pl.narrow ? packed24_bytes(pl.letters) : packed5_bytes(pl.letters));
+  pl.off_offsets = al16(pl.narrow ? packed33_bytes(pl.letters) : packed5_bytes(pl.letters));
   const int64_t offs = pl.narrow ? sparse_count(pl.n, kSparseShift) : pl.n + 1;
   pl.off_lengths = pl.off_offsets + al16(8 * offs);
   pl.block = pl.off_lengths + (pl.narrow ? al16(narrow_lengths_bytes(pl.n, static_cast<int>(pl.bits))) : 0);
@@ -48,8 +48,8 @@ void layout(RankPlan& pl) {
 // Root: rank slice [b, b + pl.n) of rb in the plan's wire form -> dst (host staging).
 void pack_block(const RecordBatch& rb, const RankPlan& pl, char* dst) {
   const int64_t b = pl.first, c0 = rb.offsets[b];
-  if (pl.narrow)  // the streaming kernel's form: P24 letter groups
-    pack24(rb.codes.data() + c0, pl.letters, reinterpret_cast<uint8_t*>(dst + pl.off_letters));
+  if (pl.narrow)  // the streaming kernel's form: P33 letter fields
+    pack33(rb.codes.data() + c0, pl.letters, reinterpret_cast<uint8_t*>(dst + pl.off_letters));
   else  // the record/tile kernels' form: unpacked on the device
     pack5(rb.codes.data() + c0, pl.letters, reinterpret_cast<uint8_t*>(dst + pl.off_letters));
   int64_t* offs = reinterpret_cast<int64_t*>(dst + pl.off_offsets);
@@ -67,7 +67,7 @@ void pack_block(const RecordBatch& rb, const RankPlan& pl, char* dst) {
 WireBatch device_view(const RankPlan& pl, char* d_block) {
   WireBatch w;
   w.letters = reinterpret_cast<const uint8_t*>(d_block + pl.off_letters);
-  w.packed24 = pl.narrow != 0;
+  w.packed33 = pl.narrow != 0;
   w.packed5 = pl.narrow == 0;
   w.offsets = reinterpret_cast<const int64_t*>(d_block + pl.off_offsets);
   w.off_shift = pl.narrow ? kSparseShift : 0;
