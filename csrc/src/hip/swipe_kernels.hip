@@ -470,14 +470,14 @@ void preload_swipe_kernels() {
   (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&swipe_search_kernel<24, 4, 3>));
 }
 
-// MOC_SWIPE_TAIL=0 keeps every tile at full size (A/B); otherwise the tail tiles are 1/MOC_SWIPE_TAIL of a
-// tile (default 4; 2..16)
+// MOC_SWIPE_TAIL=0 keeps every tile at full size (A/B); 2, 4 (default), 8 or 16 cut the tail tiles to that
+// fraction of a tile. Powers of two only: tiles stay multiples of 64 records (sparse-offset boundaries).
 static int tail_div() {
   static const int d = [] {
     const char* v = std::getenv("MOC_SWIPE_TAIL");
     if (!v) return 4;
     const int x = std::atoi(v);
-    return x == 0 ? 0 : std::max(2, std::min(16, x));
+    return (x == 0 || x == 2 || x == 4 || x == 8 || x == 16) ? x : 4;
   }();
   return d;
 }
