@@ -494,7 +494,7 @@ void launch_swipe(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStr
   // (blocks idling while the last tiles finish) shrinks 4x
   const int64_t n_big = (a.n + a.tile_records - 1) / a.tile_records;
   const int div = tail_div();
-  if (div && a.tile_records / div >= 64 && n_big > 2 * slots) {
+  if (div && a.tile_records % (64 * div) == 0 && n_big > 2 * slots) {  // tail tiles: multiples of 64 records
     b.tail_from = n_big - slots;
     b.tail_records = a.tile_records / div;
   }
