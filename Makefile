@@ -86,17 +86,19 @@ GIT_HASH  := $(shell git rev-parse --short=12 HEAD 2>/dev/null || echo unknown)
 BUILD_ID  := $(BUILD)/build_id
 $(shell mkdir -p $(BUILD); echo 'src=$(SRC_HASH) git=$(GIT_HASH)' | cmp -s - $(BUILD_ID) || echo 'src=$(SRC_HASH) git=$(GIT_HASH)' > $(BUILD_ID))
 
-$(OBJ)/apps/final.o: csrc/apps/final.cpp $(HEADERS) $(BUILD_ID)
+$(OBJ)/apps/final.o: csrc/apps/final.cpp csrc/apps/job.hpp $(HEADERS) $(BUILD_ID)
 	@mkdir -p $(dir $@)
 	$(CXX) $(CXXFLAGS) $(MPIFLAGS) -DMOC_BUILD_ID='"src=$(SRC_HASH) git=$(GIT_HASH)"' -c $< -o $@
 
-$(OBJ)/apps/%.o: csrc/apps/%.cpp $(HEADERS)
+$(OBJ)/apps/%.o: csrc/apps/%.cpp csrc/apps/job.hpp $(HEADERS)
 	@mkdir -p $(dir $@)
 	$(CXX) $(CXXFLAGS) $(MPIFLAGS) -c $< -o $@
 
 # ./final links MPI and the CPU core only; the GPU side is a plugin it dlopens when a rank uses a GPU
-final: $(OBJ)/apps/final.o $(COMM_OBJS) $(CPU_OBJS) $(MPILIB)/libmpi.so
-	$(CXX) -fopenmp -o $@ $(OBJ)/apps/final.o $(COMM_OBJS) $(CPU_OBJS) \
+APP_OBJS  := $(OBJ)/apps/final.o $(OBJ)/apps/job_common.o $(OBJ)/apps/flow_sliced.o $(OBJ)/apps/flow_stream.o \
+             $(OBJ)/apps/flow_batch.o
+final: $(APP_OBJS) $(COMM_OBJS) $(CPU_OBJS) $(MPILIB)/libmpi.so
+	$(CXX) -fopenmp -o $@ $(APP_OBJS) $(COMM_OBJS) $(CPU_OBJS) \
 	    -L$(MPILIB) -lmpi -Wl,-rpath-link,$(MPI_HOME)/lib -Wl,-rpath,'$$ORIGIN/$(MPILIB)' -ldl
 
 $(GPU_PLUGIN): $(OBJ)/apps/final_gpu.o $(RCCL_OBJS) $(COMM_OBJS) $(PKG_LIB) $(MPILIB)/libmpi.so
@@ -106,7 +108,8 @@ $(GPU_PLUGIN): $(OBJ)/apps/final_gpu.o $(RCCL_OBJS) $(COMM_OBJS) $(PKG_LIB) $(MP
 
 # Host-side sanitizers (GPU ASan is not available on the target pool). ./final links no ROCm code, so
 # the sanitized binaries cover everything the CPU backend runs; a GPU rank would dlopen the plugin.
-SAN_SRCS := $(CPU_SRCS) csrc/src/comm/comm.cpp csrc/src/comm/mpi_device_comm.cpp csrc/apps/final.cpp
+SAN_SRCS := $(CPU_SRCS) csrc/src/comm/comm.cpp csrc/src/comm/mpi_device_comm.cpp csrc/apps/final.cpp \
+            csrc/apps/job_common.cpp csrc/apps/flow_sliced.cpp csrc/apps/flow_stream.cpp csrc/apps/flow_batch.cpp
 asan: $(MPILIB)/libmpi.so
 	@rm -rf $(BUILD)/asan && mkdir -p $(BUILD)/asan
 	for f in $(SAN_SRCS); do \

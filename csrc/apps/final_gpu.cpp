@@ -229,6 +229,11 @@ class GpuRankImpl final : public GpuRank {
   double last_kernel_ms() const override { return engine().stats().kernel_ms; }
   int numa_node() const override { return numa_; }
   void solve_wire(const WireBatch& b, void* out, ResultFormat fmt) override { engine().solve_wire(b, out, fmt); }
+  void begin_wire(const WireBatch& b, void* out, ResultFormat fmt) override { engine().begin_wire(b, out, fmt); }
+  GpuSolveStats finish_wire() override {
+    engine().finish_wire();
+    return last_stats();
+  }
   bool streams_packed(int64_t min_l2, int64_t max_l2) const override {
     return engine().streams_packed(min_l2, max_l2);
   }

@@ -1,0 +1,429 @@
+// One in-memory batch of records over the job's transport (job.hpp): the path of multi-node jobs (mpi,
+// rccl), of the context-parallel decomposition, of --transport=rccl-emul and of the StreamReader-fed
+// streaming mode on those transports. Decomposition + distribution + search + combine + print.
+// Reference: MPI_Scatter of fixed 2000-byte records (main.c:174), one kernel launch per record per rank
+// (cudaFunctions.cu:204-218), MPI_Gather x3 (main.c:195-197).
+#include <omp.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "job.hpp"
+#include "moc/device_comm.hpp"
+#include "moc/runtime/host_region.hpp"
+#include "moc/runtime/log.hpp"
+
+namespace moc {
+
+namespace {
+
+class BatchFlow {
+ public:
+  BatchFlow(JobCore& j, std::unique_ptr<BulkParser>* parser, uvector<char>* text)
+      : j_(j), parser_(parser), text_(text) {}
+  void run(RecordBatch* rb, int64_t n, int64_t total_chars);
+
+ private:
+  std::vector<int64_t> make_bounds(const int64_t* offsets, int64_t n, bool cp);
+  void batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, bool cp);
+  void gpu_window_slice(const uint8_t* w_codes, const int64_t* offs, int64_t n, Result* res, ResultFormat& fmt,
+                        R2Params& r2);
+  void batch_mpi(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds, bool cp);
+  void batch_rccl(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds, bool cp);
+  // the input (deferred parser + text) goes back to the OS on the releaser
+  void release_input();
+
+  JobCore& j_;
+  std::unique_ptr<BulkParser>* parser_;  // root: deferred pass 2 into the shared window (or null)
+  uvector<char>* text_;                  // root: the text that parser reads
+};
+
+void BatchFlow::release_input() {
+  std::shared_ptr<BulkParser> p(parser_ && *parser_ ? std::move(*parser_) : nullptr);
+  std::shared_ptr<uvector<char>> t;
+  if (text_ && !text_->empty()) {
+    t = std::make_shared<uvector<char>>(std::move(*text_));
+    *text_ = uvector<char>();
+  }
+  if (p || t)
+    j_.rel.defer([p, t]() mutable {
+      p.reset();
+      t.reset();
+    });
+}
+
+void BatchFlow::run(RecordBatch* rb, int64_t n, int64_t total_chars) {
+  const bool cp = j_.partition == "offsets";
+  if (j_.transport == "shm") {  // the window is filled first; the bounds come from it
+    batch_shm(rb, n, total_chars, cp);
+    return;
+  }
+  const std::vector<int64_t> bounds = make_bounds(j_.ctx.rank == kRoot ? rb->offsets.data() : nullptr, n, cp);
+  if (j_.transport == "mpi")
+    batch_mpi(rb, n, total_chars, bounds, cp);
+  else
+    batch_rccl(rb, n, total_chars, bounds, cp);
+}
+
+// Root: record lengths -> search cells (for --timing) and the cost-balanced rank bounds; broadcast.
+std::vector<int64_t> BatchFlow::make_bounds(const int64_t* offsets, int64_t n, bool cp) {
+  const int p = j_.ctx.size;
+  std::vector<int64_t> bounds(static_cast<size_t>(p) + 1, 0);
+  if (j_.ctx.rank == kRoot) {
+    const int64_t L1 = static_cast<int64_t>(j_.eng.seq1.size());
+    int64_t cells = 0;
+#pragma omp parallel for reduction(+ : cells) schedule(static) if (n > 65536)
+    for (int64_t i = 0; i < n; ++i) cells += record_cells(L1, offsets[i + 1] - offsets[i]);
+    j_.cells += cells;
+    if (!cp)
+      bounds = j_.partition == "even" ? partition_even(n, p) : partition_by_cost_offsets(offsets, n, L1, p, j_.cost_model());
+  }
+  if (!cp) bcast_bytes(bounds.data(), sizeof(int64_t) * (p + 1), kRoot, j_.ctx.world);
+  return bounds;
+}
+
+void BatchFlow::batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, bool cp) {
+  PhaseTimer& pt = j_.pt;
+  const MpiContext& ctx = j_.ctx;
+  const bool deferred = parser_ && *parser_;
+  if (ctx.size == 1 && !cp && rb && !deferred) {  // one rank: no window to share, search the batch in place
+    const int64_t* offs = rb->offsets.data();
+    const int64_t L1 = static_cast<int64_t>(j_.eng.seq1.size());
+    int64_t cells = 0;
+#pragma omp parallel for reduction(+ : cells) schedule(static) if (n > 65536)
+    for (int64_t i = 0; i < n; ++i) cells += record_cells(L1, offs[i + 1] - offs[i]);
+    j_.cells += cells;
+    pt.begin("compute");
+    j_.fault.at("compute", 0);
+    Stopwatch sw;
+    sw.start();
+    HostRegion res(12 * static_cast<size_t>(std::max<int64_t>(n, 1)), j_.eng.gpu ? j_.eng.hip->numa_node() : -1);
+    ResultFormat fmt = ResultFormat::R12;
+    R2Params r2{};
+    Result* out = res.as<Result>();
+    if (j_.eng.gpu && n > 0)
+      gpu_window_slice(rb->codes.data(), offs, n, out, fmt, r2);
+    else if (n > 0)
+      j_.eng.solve(rb->codes.data(), offs, n, out);
+    sw.stop();
+    j_.compute_ms += sw.total_ms();
+    pt.end();
+    {  // the batch's letters go back to the OS while its results print
+      auto spent = std::make_shared<RecordBatch>(std::move(*rb));
+      j_.rel.defer([spent]() mutable { spent.reset(); });
+      *rb = RecordBatch{};
+    }
+    pt.begin("print");
+    write_results(j_.out, std::vector<ResultRun>{ResultRun{out, fmt, r2, n}}, j_.first_index);
+    pt.end();
+    res.set_releaser(&j_.rel);
+    return;
+  }
+  // layout: offsets[(N+1)] | results[N] (or keys[N] in cp mode) | codes[total]   (8-byte aligned sections)
+  const int64_t off_bytes = 8 * (n + 1);
+  const int64_t res_bytes = ((12 * n) + 7) & ~int64_t{7};
+  pt.begin("distribute");
+  auto win = std::make_unique<SharedWindow>(ctx, off_bytes + res_bytes + total_chars);
+  win->set_releaser(&j_.rel);
+  int64_t* w_offs = reinterpret_cast<int64_t*>(win->base());
+  Result* w_res = reinterpret_cast<Result*>(win->base() + off_bytes);
+  uint8_t* w_codes = reinterpret_cast<uint8_t*>(win->base() + off_bytes + res_bytes);
+  int32_t status = 0;
+  std::string error;
+  if (ctx.rank == kRoot) {
+    if (deferred) {  // deferred pass 2: letters encoded straight into the window, no intermediate copy
+      try {
+        (*parser_)->fill(w_codes, w_offs);
+      } catch (const std::exception& e) {
+        status = 1;
+        error = e.what();
+      }
+    } else {
+      const int64_t* src_off = rb->offsets.data();
+      const uint8_t* src_codes = rb->codes.data();
+      const int nt = total_chars > (1 << 20) ? omp_get_max_threads() : 1;
+#pragma omp parallel for schedule(static, 1) num_threads(nt)
+      for (int t = 0; t < nt; ++t) {
+        const int64_t cb = total_chars * t / nt, ce = total_chars * (t + 1) / nt;
+        std::memcpy(w_codes + cb, src_codes + cb, static_cast<size_t>(ce - cb));
+        const int64_t ob = (n + 1) * t / nt, oe = (n + 1) * (t + 1) / nt;
+        std::memcpy(w_offs + ob, src_off + ob, static_cast<size_t>(oe - ob) * 8);
+      }
+      *rb = RecordBatch{};  // the window is now the only copy
+    }
+  }
+  bcast_bytes(&status, sizeof status, kRoot, ctx.world);
+  if (status != 0) {
+    win.reset();  // collective, on every rank, before leaving
+    throw InputError(error);
+  }
+  j_.fault.at("distribute", ctx.rank);
+  win->fence();
+  pt.end();
+  pt.begin("bounds");
+  const std::vector<int64_t> bounds = make_bounds(ctx.rank == kRoot ? w_offs : nullptr, n, cp);
+  pt.end();
+  pt.begin("compute");
+  j_.fault.at("compute", ctx.rank);
+  Stopwatch sw;
+  sw.start();
+  if (cp) {
+    std::vector<uint64_t> keys(static_cast<size_t>(n), 0);
+    j_.eng.solve_keys(w_codes, w_offs, n, ctx.rank, ctx.size, keys.data());
+    sw.stop();
+    pt.end();
+    pt.begin("gather");
+    j_.fault.at("gather", ctx.rank);
+    j_.allreduce_keys(keys.data(), n);
+    if (ctx.rank == kRoot) j_.resolve_keys(keys.data(), w_codes, w_offs, n, w_res);
+    pt.end();
+    j_.compute_ms += sw.total_ms();
+    // printing reads only the results: the input, offsets and letters go back to the OS while it runs
+    release_input();
+    win->discard(0, off_bytes);
+    win->discard(off_bytes + res_bytes, total_chars);
+    j_.print(w_res, n, 0);
+    pt.begin("release");
+    win.reset();  // collective: unmaps the node-shared window
+    pt.end();
+    return;
+  }
+  const int64_t my_b = bounds[ctx.rank], my_n = bounds[ctx.rank + 1] - my_b;
+  // this rank's results go to the start of its R12 region of the window, in the format it chose
+  ResultFormat fmt = ResultFormat::R12;
+  R2Params r2{};
+  if (j_.eng.gpu && my_n > 0) {
+    gpu_window_slice(w_codes, w_offs + my_b, my_n, w_res + my_b, fmt, r2);
+  } else if (my_n > 0) {
+    j_.eng.solve(w_codes, w_offs + my_b, my_n, w_res + my_b);
+  }
+  sw.stop();
+  pt.end();
+  pt.begin("gather");
+  j_.fault.at("gather", ctx.rank);
+  int64_t info[4] = {static_cast<int64_t>(fmt), r2.smin, r2.kw, r2.j};
+  std::vector<int64_t> infos(static_cast<size_t>(4 * ctx.size));
+  j_.allgather_i64(info, 4, infos.data());
+  win->fence();
+  pt.end();
+  j_.compute_ms += sw.total_ms();
+  release_input();
+  win->discard(0, off_bytes);
+  win->discard(off_bytes + res_bytes, total_chars);
+  if (ctx.rank == kRoot) {
+    std::vector<ResultRun> runs(static_cast<size_t>(ctx.size));
+    for (int q = 0; q < ctx.size; ++q) {
+      const int64_t* x = infos.data() + 4 * q;
+      runs[q] = ResultRun{w_res + bounds[q], static_cast<ResultFormat>(x[0]),
+                          R2Params{static_cast<int32_t>(x[1]), static_cast<int32_t>(x[2]), static_cast<int32_t>(x[3])},
+                          bounds[q + 1] - bounds[q]};
+    }
+    pt.begin("print");
+    write_results(j_.out, runs, j_.first_index);
+    pt.end();
+  }
+  pt.begin("release");
+  win.reset();  // collective: unmaps the node-shared window
+  pt.end();
+}
+
+// A GPU rank's slice of a node-shared CSR window: encoded into the headline's wire formats in NUMA-local
+// memory when the streaming kernel takes the batch (P33 letters, narrow lengths, sparse offsets; narrow
+// results written to the start of `res`), else the window's own bytes and offsets. Either way only this
+// slice's pieces are page-locked — never the whole window.
+void BatchFlow::gpu_window_slice(const uint8_t* w_codes, const int64_t* offs, int64_t n, Result* res,
+                                 ResultFormat& fmt, R2Params& r2) {
+  GpuRank& hip = *j_.eng.hip;
+  const int64_t c0 = offs[0], c1 = offs[n];
+  int64_t mn = INT64_MAX, mx = 0;
+#pragma omp parallel for reduction(min : mn) reduction(max : mx) schedule(static) if (n > 65536)
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t L = offs[i + 1] - offs[i];
+    mn = std::min(mn, L);
+    mx = std::max(mx, L);
+  }
+  const int numa = hip.numa_node();
+  auto pin = [&](const void* ptr, int64_t bytes) {
+    if (!j_.pin_window || !ptr || bytes <= 0) return;
+    try {
+      hip.pin(ptr, static_cast<size_t>(bytes));
+      j_.pinned_bytes += bytes;
+    } catch (const std::exception& e) {
+      MOC_LOG_WARN("could not page-lock this rank's slice (%s); using the staged pipeline", e.what());
+    }
+  };
+  GpuSolveStats gs;
+  if (mx <= 255 && hip.streams_packed(mn, mx)) {
+    const int64_t letters = c1 - c0;
+    const bool p33 = j_.group_pack() == 33;
+    HostRegion pk(static_cast<size_t>(p33 ? packed33_bytes(letters) : packed24_bytes(letters)) + 16, numa);
+    if (p33)
+      pack33(w_codes + c0, letters, pk.as<uint8_t>());
+    else
+      pack24(w_codes + c0, letters, pk.as<uint8_t>());
+    const int bits = narrow_length_bits(mn, mx);
+    const int64_t base = bits == 8 ? 0 : mn;
+    HostRegion lens(static_cast<size_t>(narrow_lengths_bytes(n, bits)) + 8, numa);
+    pack_lengths(offs, n, bits, base, lens.as<uint8_t>());
+    const int64_t ns = sparse_count(n, kSparseShift);
+    HostRegion sparse(8 * static_cast<size_t>(ns), numa);
+    int64_t* sp = sparse.as<int64_t>();
+#pragma omp parallel for schedule(static) if (ns > 65536)
+    for (int64_t q = 0; q < ns; ++q) sp[q] = offs[std::min(q << kSparseShift, n)] - c0;
+    WireBatch wb;
+    wb.letters = pk.as<uint8_t>();
+    wb.packed24 = !p33;
+    wb.packed33 = p33;
+    wb.offsets = sp;
+    wb.off_shift = kSparseShift;
+    wb.lengths = lens.as<uint8_t>();
+    wb.len_bits = bits;
+    wb.len_base = base;
+    wb.n = n;
+    wb.min_l2 = mn;
+    wb.max_l2 = mx;
+    fmt = hip.result_format(mn, mx);
+    pin(wb.letters, wb.letter_bytes());
+    pin(sp, 8 * ns);
+    pin(wb.lengths, wb.length_bytes());
+    pin(res, static_cast<int64_t>(result_bytes(fmt)) * n);
+    hip.solve_wire(wb, res, fmt);
+    gs = hip.last_stats();
+    r2 = gs.r2;
+    // unregistered now: the window's memory (the results' pages) is freed by its collective teardown
+    hip.unpin_all();
+    pk.set_releaser(&j_.rel);
+    lens.set_releaser(&j_.rel);
+    sparse.set_releaser(&j_.rel);
+  } else {
+    pin(w_codes + c0, c1 - c0);
+    pin(offs, 8 * (n + 1));
+    pin(res, 12 * n);
+    hip.solve(w_codes, offs, n, res);
+    gs.kernel_ms = hip.last_kernel_ms();
+    hip.unpin_all();
+    fmt = ResultFormat::R12;
+  }
+  j_.eng.kernel_ms += gs.kernel_ms;
+  j_.h2d_bytes += gs.h2d_bytes;
+  j_.d2h_bytes += gs.d2h_bytes;
+}
+
+void BatchFlow::batch_mpi(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds,
+                          bool cp) {
+  PhaseTimer& pt = j_.pt;
+  const MpiContext& ctx = j_.ctx;
+  const int p = ctx.size;
+  pt.begin("distribute");
+  j_.fault.at("distribute", ctx.rank);
+  std::vector<Result> results;
+  if (cp) {  // every rank needs every record
+    RecordBatch all;
+    if (ctx.rank == kRoot) all = std::move(*rb);
+    all.offsets.resize(static_cast<size_t>(n) + 1);
+    all.codes.resize(static_cast<size_t>(total_chars));
+    bcast_bytes(all.offsets.data(), 8 * (n + 1), kRoot, ctx.world);
+    bcast_bytes(all.codes.data(), total_chars, kRoot, ctx.world);
+    pt.end();
+    pt.begin("compute");
+    j_.fault.at("compute", ctx.rank);
+    Stopwatch sw;
+    sw.start();
+    std::vector<uint64_t> keys(static_cast<size_t>(n), 0);
+    j_.eng.solve_keys(all.codes.data(), all.offsets.data(), n, ctx.rank, ctx.size, keys.data());
+    sw.stop();
+    j_.compute_ms += sw.total_ms();
+    pt.end();
+    pt.begin("gather");
+    j_.fault.at("gather", ctx.rank);
+    allreduce_max_u64(keys.data(), n, ctx.world);
+    pt.end();
+    if (ctx.rank == kRoot) {
+      results.resize(static_cast<size_t>(n));
+      j_.resolve_keys(keys.data(), all.codes.data(), all.offsets.data(), n, results.data());
+    }
+    j_.print(results.data(), n, 0);
+    return;
+  }
+  const int64_t my_b = bounds[ctx.rank], my_n = bounds[ctx.rank + 1] - my_b;
+  std::vector<int64_t> lcount(p), ldispl(p), ccount(p), cdispl(p);
+  for (int r = 0; r < p; ++r) {
+    lcount[r] = 8 * (bounds[r + 1] - bounds[r]);
+    ldispl[r] = 8 * bounds[r];
+  }
+  std::vector<int64_t> lengths;
+  if (ctx.rank == kRoot) {
+    lengths.resize(static_cast<size_t>(n));
+    for (int64_t i = 0; i < n; ++i) lengths[i] = rb->length(i);
+    for (int r = 0; r < p; ++r) {
+      ccount[r] = rb->offsets[bounds[r + 1]] - rb->offsets[bounds[r]];
+      cdispl[r] = rb->offsets[bounds[r]];
+    }
+  }
+  bcast_bytes(ccount.data(), 8 * p, kRoot, ctx.world);
+  std::vector<int64_t> my_len(static_cast<size_t>(my_n));
+  scatterv_bytes(lengths.data(), lcount, ldispl, my_len.data(), kRoot, ctx.world);
+  std::vector<uint8_t> my_codes(static_cast<size_t>(ccount[ctx.rank]));
+  scatterv_bytes(ctx.rank == kRoot ? rb->codes.data() : nullptr, ccount, cdispl, my_codes.data(), kRoot, ctx.world);
+  std::vector<int64_t> my_off(static_cast<size_t>(my_n) + 1, 0);
+  for (int64_t i = 0; i < my_n; ++i) my_off[i + 1] = my_off[i] + my_len[i];
+  pt.end();
+  pt.begin("compute");
+  j_.fault.at("compute", ctx.rank);
+  std::vector<Result> mine(static_cast<size_t>(my_n));
+  Stopwatch sw;
+  sw.start();
+  j_.eng.solve(my_codes.data(), my_off.data(), my_n, mine.data());
+  sw.stop();
+  j_.compute_ms += sw.total_ms();
+  pt.end();
+  pt.begin("gather");
+  j_.fault.at("gather", ctx.rank);
+  std::vector<int64_t> rcount(p), rdispl(p);
+  for (int r = 0; r < p; ++r) {
+    rcount[r] = 12 * (bounds[r + 1] - bounds[r]);
+    rdispl[r] = 12 * bounds[r];
+  }
+  if (ctx.rank == kRoot) results.resize(static_cast<size_t>(n));
+  gatherv_bytes(mine.data(), 12 * my_n, results.data(), rcount, rdispl, kRoot, ctx.world);
+  pt.end();
+  j_.print(results.data(), n, 0);
+}
+
+void BatchFlow::batch_rccl(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds,
+                           bool cp) {
+  PhaseHooks hooks;
+  hooks.begin = [this](const char* phase) {
+    j_.pt.begin(phase);
+    j_.fault.at(phase, j_.ctx.rank);
+  };
+  hooks.end = [this] { j_.pt.end(); };
+  DeviceBatchOut out;
+  if (j_.emul_comm) {
+    CpuDeviceSearch ds(j_.eng.table, j_.eng.seq1, j_.eng.sem, j_.eng.threads);
+    out = device_batch(*j_.emul_comm, ds, rb, n, total_chars, bounds, cp, hooks);
+  } else {
+    out = device_batch(j_.eng.hip->device_comm(), j_.eng.hip->device_search(), rb, n, total_chars, bounds, cp, hooks);
+  }
+  j_.compute_ms += out.compute_ms;
+  j_.eng.kernel_ms += out.kernel_ms;
+  if (j_.ctx.rank == kRoot) {
+    if (!out.rank_records.empty()) j_.rank_records = out.rank_records;
+    j_.pt.begin("print");
+    write_results(j_.out, out.runs, j_.first_index);
+    j_.pt.end();
+  }
+}
+
+}  // namespace
+
+void run_record_batch(JobCore& job, RecordBatch* rb, int64_t n, int64_t total_chars, int64_t first_index,
+                      std::unique_ptr<BulkParser>* parser, uvector<char>* text) {
+  ++job.batches;
+  job.first_index = first_index;
+  job.records += n;
+  job.chars += total_chars;
+  BatchFlow(job, parser, text).run(rb, n, total_chars);
+}
+
+}  // namespace moc

@@ -1,0 +1,707 @@
+// Streaming job on one node (`final --batch-records=B [--batch-chars=C]`, transport shm, record slices):
+// the input is searched and printed in batches, with host memory bounded by the batch, through a
+// software pipeline whose buffers are allocated and page-locked once.
+//
+// Reference: read everything, then one blocking scatter and one kernel launch per record
+// (/root/reference/main.c:90-108,174; cudaFunctions.cu:201-218) — no overlap, memory O(input).
+//
+// Per batch b (every rank of the node):
+//   A  root: cut batch b from the input text — pass 1 (token/letter counts) in parallel chunks, kept for
+//      the next batch past the cut — and broadcast its chunk table (a few KB). The text is an --input file
+//      mapped by every rank, or the root's stream buffer (copied into a node-shared slot when the node has
+//      several ranks).
+//   B  every rank encodes its cost-balanced slice of batch b straight from the text into its ring slot
+//      b % 2: P33 letters + sparse offsets + narrow lengths in NUMA-local, page-locked memory (GPU ranks),
+//      or byte letters + CSR offsets (CPU ranks). The slot is the kernel's zero-copy input: no copy, no
+//      per-batch allocation, registration or unmap.
+//   C  fill reports are all-gathered (first input error of the batch, on every rank; result-ring growth).
+//   F  batch b-1's kernel is waited for and the ranks' result descriptors are all-gathered.
+//   D  batch b's kernel is queued on the GPU (it streams slot b % 2 while the host goes on).
+//   E  root prints batch b-1 from the ranks' node-shared result slots (b-1) % 2, while batch b streams.
+// So the host encodes batch b+1 while the kernel streams batch b, and prints batch b while batch b+1
+// streams. Ordering makes the rings safe without extra barriers: a rank writes slot s again only after
+// the root's broadcast of a later batch, which the root sends after printing the batch that used slot s.
+#include <omp.h>
+
+#include <algorithm>
+#include <cstring>
+#include <deque>
+
+#include "job.hpp"
+#include "moc/runtime/host_region.hpp"
+#include "moc/runtime/log.hpp"
+
+namespace moc {
+
+namespace {
+
+constexpr int64_t kMiB = int64_t{1} << 20;
+
+// ---- root: the text of the record area ------------------------------------------------------------
+// Absolute offsets count from the first byte after the header ("area offsets").
+class AreaText {
+ public:
+  AreaText(const char* mapped, int64_t bytes) : map_(mapped), hi_(bytes), eof_(true) {}
+  AreaText(uvector<char> head, bool eof, FILE* f) : buf_(std::move(head)), len_(static_cast<int64_t>(buf_.size())),
+                                                      hi_(len_), eof_(eof), f_(f) {}
+  bool mapped() const { return map_ != nullptr; }
+  const char* at(int64_t abs) const { return map_ ? map_ + abs : buf_.data() + (abs - base_); }
+  int64_t hi() const { return hi_; }  // end of the loaded text
+  bool eof() const { return eof_; }   // hi() is the end of the input
+  // stream input: text before `abs` is no longer needed (dropped lazily, when the buffer needs room)
+  void drop_before(int64_t abs) { drop_ = std::max(drop_, abs); }
+  // stream input: loads at least `want` more bytes unless the input ends first; false if nothing new
+  bool load_more(int64_t want) {
+    if (map_ || eof_) return false;
+    want = std::max<int64_t>(want, 4 * kMiB);
+    if (len_ + want > static_cast<int64_t>(buf_.size()) && drop_ > base_) {  // room: drop the consumed prefix
+      const int64_t keep = hi_ - drop_;
+      std::memmove(buf_.data(), buf_.data() + (drop_ - base_), static_cast<size_t>(keep));
+      base_ = drop_;
+      len_ = keep;
+    }
+    if (len_ + want > static_cast<int64_t>(buf_.size()))
+      buf_.resize(static_cast<size_t>(std::max<int64_t>(len_ + want, 2 * static_cast<int64_t>(buf_.size()))));
+    const size_t room = buf_.size() - static_cast<size_t>(len_);
+    const size_t got = read_regular_into(f_, buf_.data() + len_, room);
+    if (got < room) {
+      if (std::ferror(f_)) throw Error("error while reading input stream");
+      eof_ = true;
+    }
+    len_ += static_cast<int64_t>(got);
+    hi_ = base_ + len_;
+    return got > 0;
+  }
+
+ private:
+  const char* map_ = nullptr;
+  uvector<char> buf_;
+  int64_t base_ = 0, len_ = 0, drop_ = 0;
+  int64_t hi_ = 0;
+  bool eof_ = true;
+  FILE* f_ = nullptr;
+};
+
+struct Chunk {
+  int64_t begin = 0, end = 0, toks = 0, chars = 0;  // area offsets; begin at a token start or whitespace
+};
+
+// One batch as the root cut it: area [begin, end) (whole counted chunks; the records are its first n
+// tokens), its chunk table, and where the next batch starts.
+struct BatchCut {
+  int64_t n = 0, letters = 0, begin = 0, end = 0, next = 0;
+  std::vector<Chunk> chunks;
+};
+
+// Root: pass 1 ahead of the batches, and the cuts.
+class Cutter {
+ public:
+  explicit Cutter(AreaText& t) : t_(t) {}
+  // Cuts the next batch: records are taken while fewer than max_rec are taken and (none is taken yet or
+  // fewer than max_chr letters are) — StreamReader::next_batch's rule.
+  BatchCut take(int64_t max_rec, int64_t max_chr) {
+    while (!(tok_ahead_ >= max_rec || chr_ahead_ >= max_chr) && !(t_.eof() && counted_ >= t_.hi())) extend(max_rec, max_chr);
+    BatchCut cut;
+    cut.begin = cut.next = chunks_.empty() ? counted_ : chunks_.front().begin;
+    int64_t taken = 0, letters = 0;
+    size_t used = 0;
+    bool split = false;
+    Chunk rest;
+    for (; used < chunks_.size(); ++used) {
+      if (taken >= max_rec || (taken > 0 && letters >= max_chr)) break;
+      const Chunk& c = chunks_[used];
+      cut.chunks.push_back(c);
+      if (c.toks == 0 || (taken + c.toks <= max_rec && letters + c.chars - 1 < max_chr)) {  // whole chunk
+        taken += c.toks;
+        letters += c.chars;
+        cut.next = c.end;
+        continue;
+      }
+      // the batch ends inside this chunk (or its last token is the first over a limit): token walk
+      const unsigned char* ua = reinterpret_cast<const unsigned char*>(t_.at(c.begin));
+      int64_t i = 0, tk = 0, ch = 0;
+      const int64_t e = c.end - c.begin;
+      bool stop = false;
+      while (i < e) {
+        while (i < e && is_input_space(ua[i])) ++i;
+        if (i >= e) break;
+        if (taken + tk >= max_rec || (taken + tk > 0 && letters + ch >= max_chr)) {
+          stop = true;
+          break;
+        }
+        int64_t j = i;
+        while (j < e && !is_input_space(ua[j])) ++j;
+        ++tk;
+        ch += j - i;
+        i = j;
+      }
+      taken += tk;
+      letters += ch;
+      if (stop) {
+        cut.next = c.begin + i;
+        rest = Chunk{c.begin + i, c.end, c.toks - tk, c.chars - ch};
+        split = true;
+        ++used;
+        break;
+      }
+      cut.next = c.end;
+    }
+    chunks_.erase(chunks_.begin(), chunks_.begin() + static_cast<std::ptrdiff_t>(used));
+    if (split) chunks_.push_front(rest);
+    tok_ahead_ = chr_ahead_ = 0;
+    for (const Chunk& c : chunks_) {
+      tok_ahead_ += c.toks;
+      chr_ahead_ += c.chars;
+    }
+    cut.n = taken;
+    cut.letters = letters;
+    cut.end = cut.chunks.empty() ? cut.begin : cut.chunks.back().end;
+    return cut;
+  }
+
+ private:
+  // Counts the next region of the text (parallel chunks cut at whitespace), sized from the density seen.
+  void extend(int64_t max_rec, int64_t max_chr) {
+    const double bpt = seen_toks_ > 0 ? static_cast<double>(seen_bytes_) / seen_toks_ : 16.0;
+    const double bpl = seen_chars_ > 0 ? static_cast<double>(seen_bytes_) / seen_chars_ : 2.0;
+    double want = std::min(max_rec < INT64_MAX ? (max_rec - tok_ahead_) * bpt : 1e18,
+                           max_chr < INT64_MAX ? (max_chr - chr_ahead_) * bpl : 1e18);
+    if (seen_toks_ == 0) want = std::min(want, 8.0 * kMiB);  // a first probe of the density
+    const int64_t region = std::clamp<int64_t>(static_cast<int64_t>(want * 1.02) + kMiB, kMiB, int64_t{1} << 30);
+    int64_t end = counted_ + region;
+    while (end > t_.hi() && t_.load_more(end - t_.hi())) {
+    }
+    if (end >= t_.hi()) {
+      end = t_.hi();
+      if (!t_.eof()) {  // the loaded text ends inside a token: the region ends before it
+        const unsigned char* ua = reinterpret_cast<const unsigned char*>(t_.at(counted_));
+        int64_t e = end - counted_;
+        while (e > 0 && !is_input_space(ua[e - 1])) --e;
+        if (e == 0) {  // one token longer than everything loaded: load until it ends
+          t_.load_more(end - counted_);
+          return;
+        }
+        end = counted_ + e;
+      }
+    } else {  // move forward past the token the region end cuts
+      while (true) {
+        const unsigned char* ua = reinterpret_cast<const unsigned char*>(t_.at(counted_));
+        int64_t e = end - counted_;
+        const int64_t lim = t_.hi() - counted_;
+        while (e < lim && e > 0 && !is_input_space(ua[e - 1])) ++e;
+        end = counted_ + e;
+        if (e < lim || t_.eof() || is_input_space(ua[e - 1])) break;
+        if (!t_.load_more(kMiB)) break;
+      }
+    }
+    const int64_t len = end - counted_;
+    if (len <= 0) return;
+    const int nt = len > 2 * kMiB ? std::max(1, std::min<int>(omp_get_max_threads(), static_cast<int>(len / kMiB))) : 1;
+    const unsigned char* ua = reinterpret_cast<const unsigned char*>(t_.at(counted_));
+    std::vector<Chunk> parts(static_cast<size_t>(nt));
+    std::vector<int64_t> b(static_cast<size_t>(nt) + 1);
+    b[0] = 0;
+    for (int q = 1; q < nt; ++q) {  // chunk starts move forward past the token they cut
+      int64_t x = std::max(len * q / nt, b[q - 1]);
+      while (x < len && x > 0 && !is_input_space(ua[x - 1])) ++x;
+      b[q] = x;
+    }
+    b[nt] = len;
+#pragma omp parallel for schedule(static, 1) num_threads(nt) if (nt > 1)
+    for (int q = 0; q < nt; ++q) {
+      Chunk& c = parts[q];
+      c.begin = counted_ + b[q];
+      c.end = counted_ + b[q + 1];
+      count_tokens(reinterpret_cast<const char*>(ua) + b[q], static_cast<size_t>(b[q + 1] - b[q]), &c.toks, &c.chars);
+    }
+    for (const Chunk& c : parts) {
+      if (c.end <= c.begin) continue;
+      chunks_.push_back(c);
+      tok_ahead_ += c.toks;
+      chr_ahead_ += c.chars;
+      seen_toks_ += c.toks;
+      seen_chars_ += c.chars;
+    }
+    seen_bytes_ += len;
+    counted_ = end;
+  }
+
+  AreaText& t_;
+  std::deque<Chunk> chunks_;  // counted, not yet taken
+  int64_t counted_ = 0;       // area offset where counting continues
+  int64_t tok_ahead_ = 0, chr_ahead_ = 0;
+  int64_t seen_bytes_ = 0, seen_toks_ = 0, seen_chars_ = 0;
+};
+
+// The fixed part of a batch's broadcast (the chunk table follows).
+struct BatchMsg {
+  int64_t n = 0, letters = 0, begin = 0, end = 0, nchunks = 0, status = 0;
+};
+
+// A host buffer of a ring slot: grows (rarely) and stays page-locked for the GPU between batches.
+struct RingBuf {
+  HostRegion region;
+  int64_t cap = 0;
+  std::function<void()> unpin;  // the buffer's registrations (GPU ranks)
+  template <typename T>
+  T* as() const {
+    return region.as<T>();
+  }
+};
+
+class StreamFlow {
+ public:
+  StreamFlow(JobCore& j, const Header& h, StreamSource& src, int64_t batch_records, int64_t batch_chars,
+             const ParseOptions& po)
+      : j_(j), h_(h), src_(src), max_rec_(batch_records > 0 ? batch_records : INT64_MAX),
+        max_chr_(batch_chars > 0 ? batch_chars : INT64_MAX), l2_cap_(po.strict_limits ? kSpecMaxSeq2 : po.max_l2) {
+    w_ = Weights{};
+    for (int i = 0; i < 4; ++i) w_.w[i] = h.w[i];
+    gpu_ = j_.eng.gpu ? j_.eng.hip.get() : nullptr;
+    numa_ = gpu_ ? gpu_->numa_node() : -1;
+    pin_ = gpu_ && j_.pin_window;
+  }
+  ~StreamFlow() {
+    if (gpu_) (void)safe_finish();
+    for (auto& s : in_)
+      for (RingBuf* b : {&s.letters, &s.sparse, &s.len16, &s.lens, &s.dense, &s.codes})
+        if (b->unpin) b->unpin();
+    for (auto& u : res_unpin_)
+      if (u) u();
+  }
+  int run();
+
+ private:
+  struct InSlot {
+    RingBuf letters, sparse, len16, lens, dense, codes;
+  };
+  // what one rank did with batch b (kept until its results are printed)
+  struct Done {
+    int64_t n = 0, first = 0;  // this rank's records; the batch's first global index
+    ResultFormat fmt = ResultFormat::R12;
+    WireBatch wb;
+    bool launched = false;
+  };
+  bool safe_finish() {
+    try {
+      if (gpu_) gpu_->finish_wire();
+      return true;
+    } catch (...) {
+      return false;
+    }
+  }
+  void ensure(RingBuf& b, int64_t bytes, bool pin);
+  char* ensure_results(int s, const std::vector<int64_t>& need, const std::vector<int64_t>& caps);
+  BatchMsg next_batch(std::vector<int64_t>& table);   // A (root cuts, everyone receives)
+  const char* batch_area(const BatchMsg& m, int s);    // the batch's text on this rank
+  bool fill(const BatchMsg& m, const std::vector<int64_t>& table, int s, Done& d);  // B + C; false: input error
+  void launch(int s, Done& d);                         // D
+  void finish(int s, Done& d);                         // F
+  void print(int s);                                   // E (root)
+
+  JobCore& j_;
+  const Header& h_;
+  StreamSource& src_;
+  const int64_t max_rec_, max_chr_, l2_cap_;
+  Weights w_{};
+  GpuRank* gpu_ = nullptr;
+  int numa_ = -1;
+  bool pin_ = false;
+  std::unique_ptr<AreaText> text_;  // root
+  std::unique_ptr<Cutter> cutter_;  // root
+  int64_t next_index_ = 0;          // global index of the next batch's first record
+  InSlot in_[2];
+  std::unique_ptr<SegmentWindow> res_[2];
+  int64_t res_cap_[2] = {0, 0};  // this rank's segment bytes
+  std::function<void()> res_unpin_[2];
+  std::unique_ptr<SharedWindow> text_slot_[2];  // stream input, several ranks: the batch's text
+  int64_t text_cap_[2] = {0, 0};
+  // every rank's result run of the batch waiting to be printed (root)
+  std::vector<ResultRun> runs_[2];
+  int64_t runs_first_[2] = {0, 0};
+  std::string error_;
+  std::vector<double> kernel_ms_;  // per batch (this rank)
+  double overlap_ms_ = 0;          // host work done while a kernel was in flight
+};
+
+void StreamFlow::ensure(RingBuf& b, int64_t bytes, bool pin) {
+  bytes = std::max<int64_t>(bytes, 64);
+  if (bytes <= b.cap) return;
+  if (b.unpin) {
+    b.unpin();
+    b.unpin = nullptr;
+  }
+  const int64_t cap = bytes + bytes / 4;
+  b.region = HostRegion(static_cast<size_t>(cap), numa_);
+  b.region.set_releaser(&j_.rel);
+  b.cap = cap;
+  if (pin && pin_) {
+    try {
+      gpu_->pin(b.region.data(), static_cast<size_t>(cap));
+      b.unpin = gpu_->detach_pins();
+      j_.pinned_bytes += cap;
+    } catch (const std::exception& e) {
+      MOC_LOG_WARN("could not page-lock a ring slot (%s); using the staged pipeline", e.what());
+    }
+  }
+}
+
+// Result slot s: every rank's segment holds at least need[q] bytes. Every rank knows every rank's need and
+// capacity (exchanged with the fill reports), so all of them decide alike whether the collective
+// re-allocation runs.
+char* StreamFlow::ensure_results(int s, const std::vector<int64_t>& need, const std::vector<int64_t>& caps) {
+  const int me = j_.ctx.rank;
+  bool grow = !res_[s];
+  for (size_t q = 0; q < need.size(); ++q) grow = grow || need[q] > caps[q];
+  if (grow) {
+    if (res_unpin_[s]) {
+      res_unpin_[s]();
+      res_unpin_[s] = nullptr;
+    }
+    res_[s].reset();  // collective
+    const int64_t cap = std::max<int64_t>(std::max(need[me] + need[me] / 4, res_cap_[s]), 64);
+    res_[s] = std::make_unique<SegmentWindow>(j_.ctx, cap, numa_);
+    res_[s]->set_releaser(&j_.rel);
+    res_cap_[s] = cap;
+    if (pin_) {
+      try {
+        gpu_->pin(res_[s]->mine(), static_cast<size_t>(cap));
+        res_unpin_[s] = gpu_->detach_pins();
+        j_.pinned_bytes += cap;
+      } catch (const std::exception& e) {
+        MOC_LOG_WARN("could not page-lock a result slot (%s)", e.what());
+      }
+    }
+  }
+  return res_[s]->mine();
+}
+
+BatchMsg StreamFlow::next_batch(std::vector<int64_t>& table) {
+  BatchMsg m;
+  BatchCut cut;
+  if (j_.ctx.rank == kRoot) {
+    j_.pt.begin("count");
+    try {
+      const int64_t left = h_.n_total - next_index_;
+      cut = cutter_->take(std::min(max_rec_, left), max_chr_);
+      if (cut.n < std::min(max_rec_, left) && !(max_chr_ < INT64_MAX && cut.letters >= max_chr_))
+        throw Error("expected " + std::to_string(h_.n_total) + " Seq2 records, found only " +
+                    std::to_string(next_index_ + cut.n));
+      m.n = cut.n;
+      m.letters = cut.letters;
+      m.begin = cut.begin;
+      m.end = cut.end;
+      m.nchunks = static_cast<int64_t>(cut.chunks.size());
+    } catch (const std::exception& e) {
+      m = BatchMsg{};
+      m.status = 1;
+      error_ = e.what();
+    }
+    j_.pt.end();
+  }
+  j_.pt.begin("bcast");
+  bcast_bytes(&m, sizeof m, kRoot, j_.ctx.world);
+  table.assign(static_cast<size_t>(3 * m.nchunks + 1), 0);
+  if (j_.ctx.rank == kRoot) {
+    for (int64_t c = 0; c < m.nchunks; ++c) {
+      const Chunk& ch = cut.chunks[c];
+      table[c] = ch.begin - m.begin;
+      table[m.nchunks + 1 + c] = ch.toks;
+      table[2 * m.nchunks + 1 + c] = ch.chars;
+    }
+    table[m.nchunks] = m.end - m.begin;
+    if (!text_->mapped()) text_->drop_before(cut.next);  // kept until this batch is encoded (see run)
+  }
+  if (m.nchunks > 0) bcast_bytes(table.data(), 8 * static_cast<int64_t>(table.size()), kRoot, j_.ctx.world);
+  j_.pt.end();
+  return m;
+}
+
+const char* StreamFlow::batch_area(const BatchMsg& m, int s) {
+  if (src_.mapped) return src_.mapped + src_.area_begin + m.begin;
+  if (j_.ctx.size == 1) return text_->at(m.begin);
+  // several ranks, stream input: the root copies the batch's text into the node-shared slot s
+  const int64_t len = m.end - m.begin;
+  j_.pt.begin("share");
+  if (len + 64 > text_cap_[s]) {
+    text_slot_[s].reset();  // collective
+    text_cap_[s] = (len + 64) + (len + 64) / 4;
+    text_slot_[s] = std::make_unique<SharedWindow>(j_.ctx, text_cap_[s]);
+  }
+  if (j_.ctx.rank == kRoot) {
+    const char* src = text_->at(m.begin);
+    char* dst = text_slot_[s]->base();
+    const int nt = len > (int64_t{1} << 24) ? omp_get_max_threads() : 1;
+#pragma omp parallel for schedule(static, 1) num_threads(nt) if (nt > 1)
+    for (int t = 0; t < nt; ++t) {
+      const int64_t b = len * t / nt, e = len * (t + 1) / nt;
+      std::memcpy(dst + b, src + b, static_cast<size_t>(e - b));
+    }
+  }
+  text_slot_[s]->fence();
+  j_.pt.end();
+  return text_slot_[s]->base();
+}
+
+bool StreamFlow::fill(const BatchMsg& m, const std::vector<int64_t>& table, int s, Done& d) {
+  const MpiContext& ctx = j_.ctx;
+  const int p = ctx.size, r = ctx.rank;
+  const char* area = batch_area(m, s);
+  j_.pt.begin("fill");
+  j_.fault.at("distribute", r);
+  const int64_t nch = m.nchunks;
+  BulkParser bp(area, static_cast<size_t>(m.end - m.begin), w_, j_.eng.seq1, l2_cap_, m.n);
+  bp.set_chunks(std::vector<int64_t>(table.begin(), table.begin() + nch + 1), table.data() + nch + 1,
+                table.data() + 2 * nch + 1);
+  int64_t b0, b1;
+  if (j_.partition == "even") {
+    b0 = m.n * r / p;
+    b1 = m.n * (r + 1) / p;
+  } else {
+    b0 = bp.cost_split(0, r, p, j_.cost_model());
+    b1 = std::max(b0, bp.cost_split(0, r + 1, p, j_.cost_model()));
+  }
+  const AreaSlice slice = bp.slice(b0, b1);
+  const int64_t n = slice.records;
+  const int64_t L1 = static_cast<int64_t>(j_.eng.seq1.size());
+  InSlot& in = in_[s];
+  FillReport rep;
+  d = Done{};
+  d.n = n;
+  d.first = next_index_ + b0;
+  if (n > 0 && !gpu_) {
+    ensure(in.codes, slice.letters + 16, false);
+    ensure(in.dense, 8 * (n + 1), false);
+    rep = bp.fill_slice(slice, in.codes.as<uint8_t>(), nullptr, in.dense.as<int64_t>());
+  } else if (n > 0) {
+    bool narrow = L1 <= 200 && slice.letters <= 32 * n;
+    const int pack = narrow ? j_.group_pack() : 5;
+    if (narrow) {
+      ensure(in.letters, (pack == 33 ? packed33_bytes(slice.letters) : packed24_bytes(slice.letters)) + 16, true);
+      ensure(in.sparse, 8 * sparse_count(n, kSparseShift), true);
+      ensure(in.len16, 2 * n, false);
+      rep = bp.fill_slice(slice, nullptr, in.letters.as<uint8_t>(), nullptr, in.sparse.as<int64_t>(),
+                          in.len16.as<uint16_t>(), pack);
+      if (!(rep.max_len <= 255 && gpu_->streams_packed(rep.min_len, rep.max_len))) narrow = false;
+    }
+    if (!narrow) {  // 5-bit letters + CSR offsets (the staged pipeline's form)
+      ensure(in.letters, packed5_bytes(slice.letters) + 16, true);
+      ensure(in.dense, 8 * (n + 1), true);
+      rep = bp.fill_slice(slice, nullptr, in.letters.as<uint8_t>(), in.dense.as<int64_t>());
+    }
+    WireBatch& wb = d.wb;
+    wb.letters = in.letters.as<uint8_t>();
+    wb.packed33 = narrow && pack == 33;
+    wb.packed24 = narrow && pack == 24;
+    wb.packed5 = !narrow;
+    wb.n = n;
+    wb.min_l2 = rep.min_len;
+    wb.max_l2 = rep.max_len;
+    if (narrow) {
+      const int bits = narrow_length_bits(rep.min_len, rep.max_len);
+      ensure(in.lens, narrow_lengths_bytes(n, bits) + 8, true);
+      pack_lengths16(in.len16.as<uint16_t>(), n, bits, rep.min_len, in.lens.as<uint8_t>());
+      wb.offsets = in.sparse.as<int64_t>();
+      wb.off_shift = kSparseShift;
+      wb.lengths = in.lens.as<uint8_t>();
+      wb.len_bits = bits;
+      wb.len_base = bits == 8 ? 0 : rep.min_len;
+    } else {
+      wb.offsets = in.dense.as<int64_t>();
+    }
+    d.fmt = gpu_->result_format(rep.min_len, rep.max_len);
+  }
+  j_.pt.end();
+  // ---- C: the batch's first input error, on every rank; result-slot sizes
+  j_.pt.begin("report");
+  const int fb = result_bytes(d.fmt);
+  int64_t mine[9] = {rep.min_len, rep.max_len, rep.bad_record, rep.long_record, rep.long_len, rep.cells,
+                     slice.letters, fb * n, res_[s] ? res_cap_[s] : -1};
+  std::vector<int64_t> all(static_cast<size_t>(9 * p));
+  j_.allgather_i64(mine, 9, all.data());
+  FillReport whole;
+  std::vector<int64_t> need(static_cast<size_t>(p)), caps(static_cast<size_t>(p));
+  for (int q = 0; q < p; ++q) {
+    const int64_t* x = all.data() + 9 * q;
+    caps[q] = x[8];
+    whole.min_len = std::min(whole.min_len, x[0]);
+    whole.max_len = std::max(whole.max_len, x[1]);
+    if (x[2] >= 0 && (whole.bad_record < 0 || x[2] < whole.bad_record)) whole.bad_record = x[2];
+    if (x[3] >= 0 && (whole.long_record < 0 || x[3] < whole.long_record)) {
+      whole.long_record = x[3];
+      whole.long_len = x[4];
+    }
+    whole.cells += x[5];
+    need[q] = x[7];
+  }
+  // batch-relative record indices -> the job's
+  if (whole.bad_record >= 0) whole.bad_record += next_index_;
+  if (whole.long_record >= 0) whole.long_record += next_index_;
+  try {
+    bp.check(whole);
+  } catch (const std::exception& e) {
+    error_ = e.what();
+    j_.pt.end();
+    return false;
+  }
+  j_.cells += whole.cells;
+  j_.chars += m.letters;
+  j_.records += m.n;
+  ++j_.batches;
+  ensure_results(s, need, caps);
+  j_.pt.end();
+  return true;
+}
+
+void StreamFlow::launch(int s, Done& d) {
+  if (d.n <= 0) return;
+  j_.pt.begin("compute");
+  j_.fault.at("compute", j_.ctx.rank);
+  Stopwatch sw;
+  sw.start();
+  char* out = res_[s]->mine();
+  if (gpu_) {
+    gpu_->begin_wire(d.wb, out, d.fmt);
+    d.launched = true;
+  } else {
+    RecordBatch b;  // the CPU engine reads a RecordBatch: the slot's codes/offsets, viewed (no copy needed
+                    // for correctness; one copy of a batch is cheap next to its O(L1*L2) search)
+    const InSlot& in = in_[s];
+    b.codes.assign(in.codes.as<uint8_t>(), in.codes.as<uint8_t>() + in.dense.as<int64_t>()[d.n]);
+    b.offsets.assign(in.dense.as<int64_t>(), in.dense.as<int64_t>() + d.n + 1);
+    solve_batch_cpu(j_.eng.table, j_.eng.seq1.data(), static_cast<int64_t>(j_.eng.seq1.size()), b,
+                    reinterpret_cast<Result*>(out), j_.eng.sem, j_.eng.threads);
+  }
+  sw.stop();
+  j_.compute_ms += sw.total_ms();
+  j_.pt.end();
+}
+
+void StreamFlow::finish(int s, Done& d) {
+  GpuSolveStats gs;
+  if (d.launched) {
+    j_.pt.begin("compute");
+    Stopwatch sw;
+    sw.start();
+    gs = gpu_->finish_wire();
+    sw.stop();
+    j_.compute_ms += sw.total_ms();
+    j_.eng.kernel_ms += gs.kernel_ms;
+    j_.h2d_bytes += gs.h2d_bytes;
+    j_.d2h_bytes += gs.d2h_bytes;
+    kernel_ms_.push_back(gs.kernel_ms);
+    d.launched = false;
+    j_.pt.end();
+  }
+  j_.pt.begin("gather");
+  j_.fault.at("gather", j_.ctx.rank);
+  const int p = j_.ctx.size;
+  int64_t info[5] = {d.n, static_cast<int64_t>(d.fmt), gs.r2.smin, gs.r2.kw, gs.r2.j};
+  std::vector<int64_t> infos(static_cast<size_t>(5 * p));
+  j_.allgather_i64(info, 5, infos.data());
+  res_[s]->fence();
+  if (j_.ctx.rank == kRoot) {
+    runs_[s].assign(static_cast<size_t>(p), ResultRun{});
+    if (j_.rank_records.size() != static_cast<size_t>(p)) j_.rank_records.assign(static_cast<size_t>(p), 0);
+    for (int q = 0; q < p; ++q) {
+      const int64_t* x = infos.data() + 5 * q;
+      runs_[s][q] = ResultRun{res_[s]->segment(q), static_cast<ResultFormat>(x[1]),
+                              R2Params{static_cast<int32_t>(x[2]), static_cast<int32_t>(x[3]), static_cast<int32_t>(x[4])},
+                              x[0]};
+      j_.rank_records[q] += x[0];
+    }
+    runs_first_[s] = d.first;
+  }
+  j_.pt.end();
+}
+
+void StreamFlow::print(int s) {
+  if (j_.ctx.rank != kRoot || runs_[s].empty()) return;
+  j_.pt.begin("print");
+  write_results(j_.out, runs_[s], runs_first_[s]);
+  runs_[s].clear();
+  j_.pt.end();
+}
+
+int StreamFlow::run() {
+  const MpiContext& ctx = j_.ctx;
+  if (src_.mapped) bcast_bytes(&src_.area_begin, sizeof src_.area_begin, kRoot, ctx.world);
+  if (ctx.rank == kRoot) {
+    if (src_.mapped)
+      text_ = std::make_unique<AreaText>(src_.mapped + src_.area_begin, src_.mapped_bytes - src_.area_begin);
+    else
+      text_ = std::make_unique<AreaText>(std::move(src_.head), src_.eof, src_.in);
+    cutter_ = std::make_unique<Cutter>(*text_);
+  }
+  // --skip-records: the root cuts the skipped records like a batch that nobody encodes
+  next_index_ = h_.first_index;
+  if (ctx.rank == kRoot && h_.first_index > 0) {
+    j_.pt.begin("skip");
+    const BatchCut skipped = cutter_->take(h_.first_index, INT64_MAX);
+    if (!text_->mapped()) text_->drop_before(skipped.next);
+    j_.pt.end();
+  }
+  j_.first_index = next_index_;
+  std::vector<int64_t> table;
+  Done done[2];
+  int b = 0;
+  int rc = 0;
+  bool have_prev = false;  // batch b-1 is launched and not yet finished / printed
+  while (true) {
+    const int s = b & 1;
+    BatchMsg m = next_batch(table);
+    bool ok = m.status == 0;
+    if (ok && m.n > 0) {
+      Stopwatch ov;
+      ov.start();
+      ok = fill(m, table, s, done[s]);  // overlaps the kernel of batch b-1
+      ov.stop();
+      if (have_prev) overlap_ms_ += ov.total_ms();
+    }
+    if (have_prev) {  // F + E of batch b-1 (also before leaving on an input error of batch b)
+      finish(s ^ 1, done[s ^ 1]);
+      if (ok && m.n > 0) launch(s, done[s]);
+      print(s ^ 1);
+      have_prev = false;
+    } else if (ok && m.n > 0) {
+      launch(s, done[s]);
+    }
+    if (!ok) {
+      if (ctx.rank == kRoot) std::fprintf(stderr, "input error: %s\n", error_.c_str());
+      rc = 1;
+      break;
+    }
+    if (m.n == 0) break;
+    next_index_ += m.n;
+    have_prev = true;
+    ++b;
+  }
+  if (rc == 0 && ctx.rank == kRoot && next_index_ < h_.n_total) {
+    // unreachable: next_batch reports a short input (kept as a guard)
+    std::fprintf(stderr, "input error: expected %lld Seq2 records\n", static_cast<long long>(h_.n_total));
+    rc = 1;
+  }
+  if (!kernel_ms_.empty()) {
+    std::vector<double> k = kernel_ms_;
+    std::sort(k.begin(), k.end());
+    char buf[160];
+    std::snprintf(buf, sizeof buf, "{\"p50\": %.4f, \"max\": %.4f, \"batches\": %zu}", k[k.size() / 2], k.back(), k.size());
+    j_.extra_timing.emplace_back("rank0_batch_kernel_ms", buf);
+  }
+  {
+    char buf[64];
+    std::snprintf(buf, sizeof buf, "%.3f", overlap_ms_);
+    j_.extra_timing.emplace_back("rank0_fill_overlapped_ms", buf);
+  }
+  return rc;
+}
+
+}  // namespace
+
+int run_streaming(JobCore& job, const Header& h, StreamSource& src, int64_t batch_records, int64_t batch_chars,
+                  const ParseOptions& po) {
+  StreamFlow f(job, h, src, batch_records, batch_chars, po);
+  return f.run();
+}
+
+}  // namespace moc

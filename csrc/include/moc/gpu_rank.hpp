@@ -52,6 +52,10 @@ class GpuRank {
   virtual int numa_node() const = 0;
   // Wire-format batch (moc/wire.hpp) -> results in `fmt` (zero-copy when every buffer is pinned).
   virtual void solve_wire(const WireBatch& b, void* out, ResultFormat fmt) = 0;
+  // The same in two halves (HipEngine::begin_wire / finish_wire): begin queues the zero-copy streaming
+  // kernel and returns; finish waits for it and returns its stats.
+  virtual void begin_wire(const WireBatch& b, void* out, ResultFormat fmt) = 0;
+  virtual GpuSolveStats finish_wire() = 0;
   // True when batches of this length range stream packed letters + narrow lengths + sparse offsets.
   virtual bool streams_packed(int64_t min_l2, int64_t max_l2) const = 0;
   // Smallest result format for records of lengths [min_l2, max_l2].

@@ -27,6 +27,7 @@
 
 #include "moc/common.hpp"
 #include "moc/device.hpp"
+#include "moc/runtime/timer.hpp"
 #include "moc/score_table.hpp"
 
 namespace moc {
@@ -94,6 +95,11 @@ class HipEngine {
   // Sparse offsets stream zero-copy when the buffers are pinned and the swipe kernel takes the batch;
   // otherwise dense offsets are rebuilt from the lengths for the staged pipeline.
   void solve_wire(const WireBatch& b, void* out, ResultFormat fmt);
+  // The same in two halves: begin_wire queues the zero-copy streaming kernel and returns (any other path
+  // completes inside it); finish_wire waits for it and completes stats(). Every other call on the engine
+  // finishes an open solve first. A streaming job encodes batch b+1 on the host while batch b streams.
+  void begin_wire(const WireBatch& b, void* out, ResultFormat fmt);
+  void finish_wire();
   // True when batches of this length range stream packed letters (the swipe kernel takes them).
   bool streams_packed(int64_t min_l2, int64_t max_l2) const;
   // Smallest result format for this problem given the batch's length range (min_l2 <= 0: unknown,
@@ -122,7 +128,10 @@ class HipEngine {
   void pin(const void* p, size_t bytes);
   void unpin_all();
   // The registrations made by pin(), handed over to the caller (pinned::unregister them); forgotten here.
-  std::vector<void*> detach_pins() { return std::exchange(pinned_, {}); }
+  std::vector<void*> detach_pins() {
+    finish_wire();
+    return std::exchange(pinned_, {});
+  }
 
   const EngineStats& stats() const { return stats_; }
   int device() const { return device_; }
@@ -164,6 +173,7 @@ class HipEngine {
                       int fb);
   void run_staged(const uint8_t* codes, const int64_t* offsets, int64_t n, void* out, ResultFormat fmt,
                   bool packed5);
+  void solve_wire_impl(const WireBatch& b, void* out, ResultFormat fmt, bool async);
 
   EngineOptions opt_;
   int device_ = 0;
@@ -208,8 +218,12 @@ class HipEngine {
     dev::ShortArgs a;
     int32_t swipe;
   };
-  DirectKey graph_key_{};
-  hipGraphExec_t graph_exec_ = nullptr;
+  static constexpr int kGraphs = 2;
+  DirectKey graph_key_[kGraphs]{};
+  hipGraphExec_t graph_exec_[kGraphs] = {nullptr, nullptr};
+  int graph_cur_ = 0;
+  bool pending_ = false;  // a begin_wire solve is in flight (ev_a_ .. ev_b_)
+  Stopwatch pending_wall_;
   EngineStats stats_;
 };
 

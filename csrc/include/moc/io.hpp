@@ -62,6 +62,11 @@ struct FillReport {
 class BulkParser {
  public:
   BulkParser(const char* data, size_t len, const ParseOptions& opt = {}, bool count = true);
+  // A parser over a bare record area without a header — one batch of a streaming job: its first `n`
+  // tokens are the records, the problem (weights, Seq1, Seq2 length cap) comes from the job's header, and
+  // pass 1 is the caller's chunk table (set_chunks).
+  BulkParser(const char* area, size_t len, const Weights& w, const std::vector<uint8_t>& seq1, int64_t l2_cap,
+             int64_t n);
   const Weights& weights() const { return weights_; }
   const std::vector<uint8_t>& seq1() const { return seq1_; }
   int64_t count() const { return n_; }
@@ -127,6 +132,12 @@ class BulkParser {
   std::vector<double> cost_;                        // optional exact chunk costs (nchunks entries)
 };
 
+// fscanf's separators: ' ' and \t \n \v \f \r (0x09..0x0d)
+inline bool is_input_space(unsigned char c) { return c == ' ' || static_cast<unsigned char>(c - 9) <= 4; }
+// Tokens and letters (non-space bytes) of text [p, p + len) that starts at a token start or at whitespace
+// (pass 1; vectorised, no branches per byte).
+void count_tokens(const char* p, size_t len, int64_t* tokens, int64_t* letters);
+
 // Parses "W1 W2 W3 W4 / Seq1 / N / Seq2 x N" (PDF p.5-6). Whitespace of any kind (incl. CRLF)
 // separates tokens, exactly like fscanf %d/%s. Throws moc::Error with a precise message.
 Problem parse_problem(const char* data, size_t len, const ParseOptions& opt = {});
@@ -146,6 +157,9 @@ class StreamReader {
   // Parses up to max_records (and, after the first record, at most max_chars letters) of the following
   // records into `out` (offsets rebased to 0). Returns the number of records (0 once all are read).
   int64_t next_batch(int64_t max_records, RecordBatch& out, int64_t max_chars = INT64_MAX);
+  // Hands the bytes read past the last consumed token to the caller (appended to `out`), which reads the
+  // rest of the stream itself; true when the stream is already at its end.
+  bool take_rest(uvector<char>& out);
 
  private:
   bool token(const char*& b, const char*& e);  // next token, refilling the buffer as needed

@@ -131,7 +131,8 @@ HipEngine::~HipEngine() {
     (void)hipEventDestroy(s->ev_done);
   }
   unpin_all();
-  if (graph_exec_) (void)hipGraphExecDestroy(graph_exec_);
+  for (hipGraphExec_t g : graph_exec_)
+    if (g) (void)hipGraphExecDestroy(g);
   (void)hipFree(d_counter_);
   (void)hipFree(d_plan_);
   (void)hipHostFree(h_plan_);
@@ -150,6 +151,7 @@ void HipEngine::pin(const void* p, size_t bytes) {
 }
 
 void HipEngine::unpin_all() {
+  finish_wire();
   pinned::unregister(pinned_);
   pinned_.clear();
 }
@@ -174,14 +176,16 @@ void HipEngine::ensure_host(void*& ptr, size_t& cap, size_t bytes) {
 }
 
 void HipEngine::set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, Semantics sem) {
+  finish_wire();
   // the same problem again (every step of a repeated job): nothing to rebuild or upload
   if (have_problem_ && sem == sem_ && L1 == L1_ && std::equal(w.w, w.w + 4, last_w_.w) &&
       (L1 == 0 || std::memcmp(seq1, last_seq1_.data(), static_cast<size_t>(L1)) == 0))
     return;
   MOC_HIP_CHECK(hipSetDevice(device_));
   if (L1 > (int64_t{1} << 30)) throw Error("Seq1 too long for the device engine");
-  last_w_ = w;
-  last_seq1_.assign(seq1, seq1 + L1);
+  // the inputs are recorded as current only once the device image holds them (below): a set_problem that
+  // throws half-way cannot be skipped by the next call for the same problem
+  have_problem_ = false;
   table_ = ScoreTable::build(w);
   min_t_ = INT32_MAX;
   max_t_ = INT32_MIN;
@@ -226,25 +230,33 @@ void HipEngine::set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, S
   if (t16) std::memcpy(next.data() + prof_off, prof.entries.data(), sizeof(uint16_t) * prof.entries.size());
   // the same problem again (one per job step of a repeated job): the device image is already current —
   // no device-wide synchronisation, no copy
-  if (have_problem_ && next == image_) {
+  if (!image_.empty() && next == image_ && d_image_) {
     prof16_bytes_ = prof16_lds_bytes_;
+    last_w_ = w;
+    last_seq1_.assign(seq1, seq1 + L1);
+    have_problem_ = true;
     return;
   }
-  image_.swap(next);
+  image_.clear();  // the device image is about to change: not current until the upload completes
   // Kernels of the previous problem may still be queued — on our streams or on a solve_device caller's —
   // and read the image in place: let them finish before it is overwritten.
   MOC_HIP_CHECK(hipDeviceSynchronize());
   if (total > d_image_cap_) {
-    MOC_HIP_CHECK(hipFree(d_image_));
+    void* old = std::exchange(d_image_, nullptr);
+    d_image_cap_ = 0;
+    MOC_HIP_CHECK(hipFree(old));
+    MOC_HIP_CHECK(hipMalloc(&d_image_, std::max(total, size_t{64} << 10)));
     d_image_cap_ = std::max(total, size_t{64} << 10);
-    MOC_HIP_CHECK(hipMalloc(&d_image_, d_image_cap_));
   }
-  MOC_HIP_CHECK(hipMemcpy(d_image_, image_.data(), total, hipMemcpyHostToDevice));
+  MOC_HIP_CHECK(hipMemcpy(d_image_, next.data(), total, hipMemcpyHostToDevice));
+  image_.swap(next);
   char* base = static_cast<char*>(d_image_);
   d_lut_ = reinterpret_cast<int32_t*>(base);
   d_seq1_ = reinterpret_cast<uint8_t*>(base + s1_off);
   d_prof16_ = t16 ? reinterpret_cast<uint16_t*>(base + prof_off) : nullptr;
   prof16_bytes_ = prof16_lds_bytes_;
+  last_w_ = w;
+  last_seq1_.assign(seq1, seq1 + L1);
   have_problem_ = true;
 }
 
@@ -577,7 +589,23 @@ bool HipEngine::streams_packed(int64_t min_l2, int64_t max_l2) const {
   return have_problem_ && dev::configure_swipe(L1_, min_l2, max_l2, table_.max_abs(), a);
 }
 
-void HipEngine::solve_wire(const WireBatch& batch, void* out, ResultFormat fmt) {
+void HipEngine::solve_wire(const WireBatch& batch, void* out, ResultFormat fmt) { solve_wire_impl(batch, out, fmt, false); }
+
+void HipEngine::begin_wire(const WireBatch& batch, void* out, ResultFormat fmt) { solve_wire_impl(batch, out, fmt, true); }
+
+void HipEngine::finish_wire() {
+  if (!pending_) return;
+  pending_ = false;
+  MOC_HIP_CHECK(hipEventSynchronize(ev_b_));
+  float ms = 0;
+  MOC_HIP_CHECK(hipEventElapsedTime(&ms, ev_a_, ev_b_));
+  stats_.kernel_ms = ms;
+  pending_wall_.stop();
+  stats_.total_ms = pending_wall_.total_ms();
+}
+
+void HipEngine::solve_wire_impl(const WireBatch& batch, void* out, ResultFormat fmt, bool async) {
+  finish_wire();  // a solve still in flight completes first (its stats are replaced below)
   WireBatch b = batch;
   const int64_t n = b.n;
   if (b.lengths && b.len_bits != 8 && b.len_bits != 4 && b.len_bits != 3 && b.len_bits != kLenBase6)
@@ -651,16 +679,13 @@ void HipEngine::solve_wire(const WireBatch& batch, void* out, ResultFormat fmt) 
     launch_direct(pv, a, swipe);
     stats_.kernels = swipe ? 1 : 2;
     MOC_HIP_CHECK(hipEventRecord(ev_b_, s_compute_));
-    MOC_HIP_CHECK(hipEventSynchronize(ev_b_));
-    float ms = 0;
-    MOC_HIP_CHECK(hipEventElapsedTime(&ms, ev_a_, ev_b_));
-    stats_.kernel_ms = ms;
     stats_.direct = 1;
     stats_.chunks = 1;
     stats_.h2d_bytes = b.device ? 0 : b.letter_bytes() + (a.lengths3 || a.lengths4 || a.lengths6 || a.lengths8 ? b.length_bytes() : 8 * n);
     stats_.d2h_bytes = b.device ? 0 : static_cast<int64_t>(fb) * n;
-    wall.stop();
-    stats_.total_ms = wall.total_ms();
+    pending_ = true;
+    pending_wall_ = wall;
+    if (!async) finish_wire();
     return;
   }
   if (b.device) throw Error("device-resident wire batches stream through the swipe kernel only");
@@ -790,10 +815,17 @@ void HipEngine::prepare_direct(const dev::ProblemView& pv, const dev::ShortArgs&
   key.pv = pv;
   key.a = a;
   key.swipe = swipe ? 1 : 0;
-  if (graph_exec_ && std::memcmp(&key, &graph_key_, sizeof key) == 0) return;
-  if (graph_exec_) {
-    MOC_HIP_CHECK(hipGraphExecDestroy(graph_exec_));
-    graph_exec_ = nullptr;
+  for (int i = 0; i < kGraphs; ++i)
+    if (graph_exec_[i] && std::memcmp(&key, &graph_key_[i], sizeof key) == 0) {
+      graph_cur_ = i;
+      return;
+    }
+  // two argument sets stay instantiated (a streaming job alternates between the two slots of its ring):
+  // the one not used last is replaced
+  const int slot = graph_exec_[graph_cur_] ? 1 - graph_cur_ : graph_cur_;
+  if (graph_exec_[slot]) {
+    MOC_HIP_CHECK(hipGraphExecDestroy(graph_exec_[slot]));
+    graph_exec_[slot] = nullptr;
   }
   hipGraph_t g = nullptr;
   MOC_HIP_CHECK(hipStreamBeginCapture(s_compute_, hipStreamCaptureModeThreadLocal));
@@ -804,10 +836,11 @@ void HipEngine::prepare_direct(const dev::ProblemView& pv, const dev::ShortArgs&
   const hipError_t launch_err = hipGetLastError();
   MOC_HIP_CHECK(hipStreamEndCapture(s_compute_, &g));
   MOC_HIP_CHECK(launch_err);
-  const hipError_t inst = hipGraphInstantiate(&graph_exec_, g, nullptr, nullptr, 0);
+  const hipError_t inst = hipGraphInstantiate(&graph_exec_[slot], g, nullptr, nullptr, 0);
   (void)hipGraphDestroy(g);
   MOC_HIP_CHECK(inst);
-  std::memcpy(static_cast<void*>(&graph_key_), &key, sizeof key);
+  std::memcpy(static_cast<void*>(&graph_key_[slot]), &key, sizeof key);
+  graph_cur_ = slot;
 }
 
 // The direct path's launch (work-counter reset + persistent streaming kernel): the hipGraph captured
@@ -822,7 +855,7 @@ void HipEngine::launch_direct(const dev::ProblemView& pv, const dev::ShortArgs& 
     MOC_HIP_CHECK(hipGetLastError());
     return;
   }
-  MOC_HIP_CHECK(hipGraphLaunch(graph_exec_, s_compute_));
+  MOC_HIP_CHECK(hipGraphLaunch(graph_exec_[graph_cur_], s_compute_));
 }
 
 void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t n, void* out, ResultFormat fmt,
@@ -949,6 +982,7 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
 void HipEngine::solve_device(const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets, int64_t n,
                              Result* d_out, hipStream_t stream) {
   if (!have_problem_) throw Error("HipEngine::solve_device before set_problem");
+  finish_wire();
   MOC_HIP_CHECK(hipSetDevice(device_));
   if (n <= 0) return;
   if (!stream) stream = s_compute_;
@@ -1007,6 +1041,7 @@ namespace moc {
 
 void HipEngine::search_keys_device(const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets,
                                    int64_t n, int part, int parts, unsigned long long* d_keys, hipStream_t stream) {
+  finish_wire();
   if (!have_problem_) throw Error("HipEngine::search_keys before set_problem");
   if (parts < 1 || part < 0 || part >= parts) throw Error("search_keys: bad part");
   MOC_HIP_CHECK(hipSetDevice(device_));
@@ -1048,6 +1083,7 @@ void HipEngine::search_keys_device(const uint8_t* d_codes, const int64_t* d_offs
 void HipEngine::finalize_keys_device(const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets,
                                      int64_t n, const unsigned long long* d_keys, void* d_out, ResultFormat fmt,
                                      hipStream_t stream) {
+  finish_wire();
   MOC_HIP_CHECK(hipSetDevice(device_));
   if (n <= 0) return;
   if (!stream) stream = s_compute_;
@@ -1065,6 +1101,7 @@ void HipEngine::finalize_keys_device(const uint8_t* d_codes, const int64_t* d_of
 
 void HipEngine::search_keys(const uint8_t* codes, const int64_t* offsets, int64_t n, int part, int parts,
                             uint64_t* keys) {
+  finish_wire();
   MOC_HIP_CHECK(hipSetDevice(device_));
   if (n <= 0) return;
   Stopwatch wall;

@@ -22,8 +22,7 @@ namespace moc {
 
 namespace {
 
-// fscanf's separators: ' ' and \t \n \v \f \r (0x09..0x0d)
-inline bool is_space(unsigned char c) { return c == ' ' || static_cast<unsigned char>(c - 9) <= 4; }
+inline bool is_space(unsigned char c) { return is_input_space(c); }
 
 // letter -> code (1..26, either case), 0 for anything else
 struct CodeTable {
@@ -188,6 +187,10 @@ BulkParser::BulkParser(const char* data, size_t len, const ParseOptions& opt, bo
   }
 }
 
+BulkParser::BulkParser(const char* area, size_t len, const Weights& w, const std::vector<uint8_t>& seq1,
+                       int64_t l2_cap, int64_t n)
+    : weights_(w), seq1_(seq1), n_(n), total_chars_(-1), l2_cap_(l2_cap), area_(area), area_len_(len) {}
+
 std::vector<int64_t> BulkParser::chunk_starts(int nchunks) const {
   nchunks = std::max(1, nchunks);
   const int64_t len = static_cast<int64_t>(area_len_);
@@ -204,38 +207,40 @@ std::vector<int64_t> BulkParser::chunk_starts(int nchunks) const {
   return s;
 }
 
+void count_tokens(const char* p, size_t len, int64_t* tokens, int64_t* letters) {
+  const unsigned char* ua = reinterpret_cast<const unsigned char*>(p);
+  int64_t nt = 0, nc = 0;
+  if (len > 0) {  // the text starts at a token start or at whitespace
+    const int64_t first = is_space(ua[0]) ? 0 : 1;
+    nt = first;
+    nc = first;
+    // pass 1 (branch-free): tokens = space->letter transitions, letters = non-space bytes. Independent
+    // iterations (the previous byte is re-read, not carried) vectorise; 8-bit lanes summed per 255-byte
+    // block so the counters cannot overflow
+    for (size_t blk = 1; blk < len; blk += 255) {
+      const size_t be = std::min(len, blk + 255);
+      unsigned t_cnt = 0, c_cnt = 0;
+      for (size_t i = blk; i < be; ++i) {
+        const unsigned char ch = ua[i], q = ua[i - 1];
+        const unsigned lt = (ch != ' ') & (static_cast<unsigned char>(ch - 9) > 4);  // ch is a token byte
+        const unsigned ps = (q == ' ') | (static_cast<unsigned char>(q - 9) <= 4);   // q is whitespace
+        t_cnt += lt & ps;
+        c_cnt += lt;
+      }
+      nt += t_cnt;
+      nc += c_cnt;
+    }
+  }
+  *tokens = nt;
+  *letters = nc;
+}
+
 void BulkParser::count_chunks(const std::vector<int64_t>& starts, int c0, int c1, int64_t* toks,
                               int64_t* chars) const {
-  const unsigned char* ua = reinterpret_cast<const unsigned char*>(area_);
-  // pass 1 (branch-free, vectorisable): tokens = space->letter transitions, letters = non-space bytes.
   // Iterations are chunks, not thread ids: correct whatever number of threads OpenMP delivers.
-#pragma omp parallel for schedule(dynamic, 1)
-  for (int c = c0; c < c1; ++c) {
-    const size_t b = static_cast<size_t>(starts[c]), e = static_cast<size_t>(starts[c + 1]);
-    int64_t nt = 0, nc = 0;
-    if (b < e) {  // a chunk starts at a token start or at whitespace
-      const int64_t first = is_space(ua[b]) ? 0 : 1;
-      nt = first;
-      nc = first;
-      // independent iterations (the previous byte is re-read, not carried): vectorises; 8-bit lanes
-      // summed per 255-byte block so the counters cannot overflow
-      for (size_t blk = b + 1; blk < e; blk += 255) {
-        const size_t be = std::min(e, blk + 255);
-        unsigned t_cnt = 0, c_cnt = 0;
-        for (size_t i = blk; i < be; ++i) {
-          const unsigned char ch = ua[i], p = ua[i - 1];
-          const unsigned lt = (ch != ' ') & (static_cast<unsigned char>(ch - 9) > 4);  // ch is a token byte
-          const unsigned ps = (p == ' ') | (static_cast<unsigned char>(p - 9) <= 4);   // p is whitespace
-          t_cnt += lt & ps;
-          c_cnt += lt;
-        }
-        nt += t_cnt;
-        nc += c_cnt;
-      }
-    }
-    toks[c - c0] = nt;
-    chars[c - c0] = nc;
-  }
+#pragma omp parallel for schedule(dynamic, 1) if (c1 - c0 > 1)
+  for (int c = c0; c < c1; ++c)
+    count_tokens(area_ + starts[c], static_cast<size_t>(starts[c + 1] - starts[c]), toks + (c - c0), chars + (c - c0));
 }
 
 void BulkParser::set_chunks(std::vector<int64_t> starts, const int64_t* toks, const int64_t* chars) {
@@ -695,6 +700,14 @@ bool StreamReader::token(const char*& b, const char*& e) {
   e = buf_.data() + q;
   pos_ = q;
   return true;
+}
+
+bool StreamReader::take_rest(uvector<char>& out) {
+  const size_t at = out.size();
+  out.resize(at + (len_ - pos_));
+  if (len_ > pos_) std::memcpy(out.data() + at, buf_.data() + pos_, len_ - pos_);
+  pos_ = len_;
+  return eof_;
 }
 
 int64_t StreamReader::skip(int64_t records) {

@@ -166,6 +166,7 @@ class HipSearchEngine:
                 return
         else:
             key = None
+        self._problem_key = None  # not current until the native call succeeds
         _lib.check(_lib.lib().moc_engine_set_problem(
             self._h, _lib.weights_arg(Weights.of(weights).as_list()), _lib.ptr(seq1), seq1.shape[0],
             int(Semantics.parse(semantics))))

@@ -208,7 +208,9 @@ def test_timing_json_has_throughput():
     r = run_final(["--backend=cpu", "--timing", "--batch-records=3"], stdin_path=input_path(1), np_=2)
     t = json.loads(r.stderr.decode().strip().splitlines()[-1])
     assert t["records"] == 10 and t["batches"] == 4 and t["cells"] > 0 and t["cells_per_s"] > 0
-    assert set(t["timing"]) >= {"parse_ms", "bcast_ms", "distribute_ms", "compute_ms", "gather_ms", "print_ms"}
+    # the node's streaming flow: root cuts (count), every rank encodes its slice (fill), search, gather, print
+    assert set(t["timing"]) >= {"parse_ms", "bcast_ms", "count_ms", "fill_ms", "compute_ms", "gather_ms", "print_ms"}
+    assert t["rank_records"] and sum(t["rank_records"]) == 10
 
 
 def test_cmake_build_matches(tmp_path):
@@ -405,3 +407,60 @@ def test_distributed_print_to_output_file(tmp_path, np_, i):
                   np_=np_)
     assert r.returncode == 0, r.stderr.decode()
     assert r.stdout == b"" and out.read_text() == expected(i)
+
+
+# ---- the node's streaming flow (csrc/apps/flow_stream.cpp): batches cut by the root, every rank encoding its
+# slice into its ring slot, printed while the next batch is searched
+
+@pytest.mark.parametrize("np_", [1, 3, 8])
+@pytest.mark.parametrize("mode", ["stdin", "input"])
+def test_streaming_goldens_every_rank_count(np_, mode):
+    # stdin: the root's stream buffer (copied into node-shared text slots at np > 1); input: every rank maps
+    # the file. Batches of 2 / 3 records and of 40 letters, more ranks than records included.
+    for i in range(1, 7):
+        for b in ("--batch-records=2", "--batch-records=3", "--batch-chars=40"):
+            args = ["--backend=cpu", b]
+            if mode == "input":
+                r = run_final(args + [f"--input={input_path(i)}"], stdin_bytes=b"", np_=np_)
+            else:
+                r = run_final(args, stdin_path=input_path(i), np_=np_)
+            assert r.returncode == 0, (i, b, r.stderr.decode())
+            assert r.stdout.decode() == expected(i), (i, b)
+
+
+def test_streaming_pipe_large_singleton(tmp_path):
+    # a stream (pipe) larger than the root's first probe and read buffer: many count extensions, buffer
+    # compaction past the consumed batches, records cut by letters too; the same bytes as the bulk path
+    import os
+
+    from conftest import ROOT
+    from mpi_openmp_cuda_amd import format_results, make_synthetic, search_cpu
+
+    prob = make_synthetic("input6", 1_300_000, seed=21)
+    text = prob.to_text().encode()
+    path = tmp_path / "in.txt"
+    path.write_bytes(text)
+    want = format_results(search_cpu(prob)).encode()
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    for extra in (["--batch-records=100000"], ["--batch-chars=700000"], ["--batch-records=250000", "--skip-records=123457"]):
+        r = subprocess.run([os.path.join(ROOT, "final"), "--backend=cpu"] + extra, input=text, capture_output=True,
+                           timeout=300, env=env)
+        assert r.returncode == 0, r.stderr.decode()
+        if "--skip-records=123457" in extra:
+            assert r.stdout == b"".join(want.splitlines(keepends=True)[123457:])
+        else:
+            assert r.stdout == want, extra
+    # mapped (--input) at two ranks, batches cut mid-chunk
+    r = run_final(["--backend=cpu", f"--input={path}", "--batch-records=333333"], stdin_bytes=b"", np_=2, timeout=300)
+    assert r.returncode == 0 and r.stdout == want
+
+
+def test_streaming_short_input_and_bad_record():
+    # fewer records than announced: the batches before are printed, then the error, exit code 1
+    r = run_final(["--backend=cpu", "--batch-records=2"], stdin_bytes=b"1 2 3 4\nABCDEFG\n5\nABC\nABD\nAC\n", np_=2)
+    assert r.returncode == 1 and b"expected 5 Seq2 records, found only 3" in r.stderr
+    assert r.stdout.decode().count("\n") == 2
+    r = run_final(["--backend=cpu", "--batch-records=2"], stdin_bytes=b"1 2 3 4\nABCDEFG\n4\nABC\nABD\nA1\nAC\n",
+                  np_=3)
+    assert r.returncode == 1 and b"record #2 contains a non-letter" in r.stderr
+    assert r.stdout.decode().count("\n") == 2

@@ -473,26 +473,32 @@ def test_final_cli_letters_p24(tmp_path):
         assert r.stdout.decode() == format_results(search_cpu(prob)), letters
 
 
+@pytest.mark.parametrize("source", ["input", "stdin"])
 @pytest.mark.parametrize("np_", [1, 2])
-def test_final_cli_streaming_slices(tmp_path, np_):
-    # streaming batches (--batch-records): every GPU rank re-encodes its slice of each batch's node-shared
-    # window into the wire formats and page-locks only those pieces (never the whole window)
+def test_final_cli_streaming_slices(tmp_path, np_, source):
+    # streaming batches (--batch-records) through the node's streaming flow: every GPU rank encodes its slice
+    # of each batch into its two persistent, page-locked ring slots (P33 letters, sparse offsets, base-6
+    # lengths, R2 results) and the kernel of batch b streams while batch b+1 is encoded
     import json
 
     prob = make_synthetic("input6", 120_000, seed=9)
     path = tmp_path / "in6.txt"
     path.write_text(prob.to_text())
-    r = run_final(["--backend=hip", "--transport=shm", f"--input={path}", "--timing", "--device=0",
-                   "--batch-records=50000"], stdin_bytes=b"", np_=np_)
+    args = ["--backend=hip", "--transport=shm", "--timing", "--device=0", "--batch-records=50000"]
+    if source == "input":
+        r = run_final(args + [f"--input={path}"], stdin_bytes=b"", np_=np_)
+    else:
+        r = run_final(args, stdin_path=str(path), np_=np_)
     assert r.returncode == 0, r.stderr.decode()
     assert r.stdout.decode() == format_results(search_cpu(prob))
     d = json.loads([l for l in r.stderr.decode().splitlines() if l.startswith("{")][-1])
-    assert d["batches"] == 3 and d["records"] == prob.n
-    # summed over the batches: about this rank's share of P33 letters + narrow lengths/offsets + R2 results
-    # (a whole-window pin would be ~1 + 8 + 12 bytes per letter/record for every rank)
-    total = int(prob.offsets[-1])
-    assert 0 < d["max_rank_kernel_ms"]
-    assert sum(d["rank_pinned_bytes"]) <= 33 * total // 56 + prob.n * (8 / 64 + 3 / 8 + 2) + 1024 * np_ * 3, d
+    assert d["batches"] == 3 and d["records"] == prob.n and sum(d["rank_records"]) == prob.n
+    assert 0 < d["max_rank_kernel_ms"] and d["rank0_batch_kernel_ms"]["batches"] == 3, d
+    # pinned once, O(batch): two slots of (P33 letters + sparse offsets + base-6 lengths + R2 results) of
+    # the largest batch share, with the rings' 25 % growth slack — not per batch, not the whole input
+    share = 50000 / np_ + 64
+    per_slot = (33 * 12 * share // 56 + 8 * (share / 64 + 2) + share / 3 + 8 + 2 * share + 64 * 4) * 1.25
+    assert sum(d["rank_pinned_bytes"]) <= np_ * 2 * per_slot, d
 
 
 @pytest.mark.parametrize("pinned", [False, True])
@@ -793,3 +799,23 @@ def test_python_driver_hip_two_ranks(tmp_path):
                            capture_output=True, timeout=110, env=env, cwd="/tmp")
         assert r.returncode == 0, r.stderr.decode()[-3000:]
         assert r.stdout.decode() == want, transport
+
+
+@pytest.mark.parametrize("mode", ["bulk", "stream"])
+def test_final_narrow_guess_fails_stdin_two_ranks(mode):
+    # a GPU rank whose narrow-form guess (L1 <= 200, mean length <= 32) is refused by the
+    # engine (here L1 - min_l2 + 1 > 64 lanes) re-encodes its slice as 5-bit letters + CSR offsets. That
+    # must happen while the node-shared stdin text is still there — before the helpers release their
+    # shares of it — and every row must match the CPU engine.
+    rng = np.random.default_rng(31)
+    seq1 = rng.integers(1, 27, size=150, dtype=np.uint8)
+    lengths = rng.integers(10, 31, size=6000)
+    offsets = np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)
+    codes = rng.integers(1, 27, size=int(offsets[-1]), dtype=np.uint8)
+    from mpi_openmp_cuda_amd.models.scoring import Weights
+
+    prob = Problem(Weights.of((10, 2, 3, 4)), seq1, codes, offsets)
+    extra = ["--batch-records=2500"] if mode == "stream" else []
+    r = run_final(["--backend=hip", "--device=0"] + extra, stdin_bytes=prob.to_text().encode(), np_=2)
+    assert r.returncode == 0, r.stderr.decode()
+    assert r.stdout.decode() == format_results(search_cpu(prob))

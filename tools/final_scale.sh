@@ -4,7 +4,7 @@
 set -e
 mkdir -p gpurun_out
 F=/tmp/moc_big6.txt
-timeout -k 10 300 python3 tools/gen_synthetic.py --shape input6 --records ${RECORDS:-134217728} --out $F
+timeout -k 10 600 python3 tools/gen_synthetic.py --shape input6 --records ${RECORDS:-134217728} --jobs ${GEN_JOBS:-16} --out $F
 # "--output": the root writes the file itself (parallel pwrite) instead of stdout, which mpiexec's proxy
 # forwards through a pipe
 # MODES: '|'-separated flag sets (each may hold several flags)
