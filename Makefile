@@ -170,3 +170,7 @@ $(BUILD)/test_core: csrc/tests/test_core.cpp $(CPU_OBJS) $(HEADERS)
 
 unit: $(BUILD)/test_core
 	$(BUILD)/test_core
+
+# parser throughput (count vs fill, SIMD A/B): build/fill_bench [records]
+$(BUILD)/fill_bench: tools/fill_bench.cpp $(CPU_OBJS) $(HEADERS)
+	$(CXX) $(CXXFLAGS) -o $@ tools/fill_bench.cpp $(CPU_OBJS) -ldl

@@ -84,12 +84,89 @@ def launch_command(args, argv, port=None):
         [a for a in argv if a != "--dry-launch"]
 
 
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def kfd_gpu_count(root=KFD_NODES, env=None):
+    """GPUs from the KFD topology in sysfs — no HIP runtime, no torch in the launcher: topology nodes whose
+    properties report SIMDs (CPU nodes report simd_count 0). ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES /
+    CUDA_VISIBLE_DEVICES narrow the count as the runtime would. None when there is no KFD topology."""
+    env = os.environ if env is None else env
+    try:
+        nodes = os.listdir(root)
+    except OSError:
+        return None
+    n = 0
+    for node in nodes:
+        try:
+            with open(os.path.join(root, node, "properties")) as f:
+                props = dict(line.split(None, 1) for line in f if len(line.split(None, 1)) == 2)
+        except (OSError, ValueError):
+            continue
+        if int(props.get("simd_count", "0").strip() or 0) > 0:
+            n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
+
+
 def visible_gpus():
-    """GPU count without initialising the HIP runtime in this process (torch.cuda.device_count() does not
-    create a context on this image; the launcher must not hold the GPU while its children use it)."""
+    """GPU count for the launcher, from sysfs (kfd_gpu_count): the launcher must not hold the GPU while its
+    children use it, and it does not depend on torch.cuda.device_count() staying context-free."""
+    n = kfd_gpu_count()
+    if n is not None:
+        return n
     import torch
 
     return torch.cuda.device_count()
+
+
+SHM_PREFIX = "/dev/shm/moc_bench_"
+
+
+def cleanup_stale_shm(before=None, prefix=SHM_PREFIX):
+    """Removes node-shared bench arrays left by a crashed run: this user's /dev/shm/moc_bench_* files last
+    modified before `before` (the launcher's start). Names only — a process that still maps one keeps it.
+    Returns the removed paths."""
+    before = time.time() if before is None else before
+    d, base = os.path.split(prefix)
+    removed = []
+    try:
+        names = os.listdir(d)
+    except OSError:
+        return removed
+    for name in names:
+        if not name.startswith(base):
+            continue
+        p = os.path.join(d, name)
+        try:
+            st = os.stat(p)
+            if st.st_uid == os.getuid() and st.st_mtime < before:
+                os.unlink(p)
+                removed.append(p)
+        except OSError:
+            pass
+    return removed
+
+
+def pci_bus_id(code):
+    """PCIe address 'dddd:bb:dd.f' of an int from pci_bus_code, or None."""
+    if code is None or code < 0:
+        return None
+    code = int(code)
+    return f"{code >> 16:04x}:{(code >> 8) & 0xff:02x}:{(code >> 3) & 0x1f:02x}.{code & 7:x}"
+
+
+def pci_bus_code(bus_id):
+    """'dddd:bb:dd.f' -> int (domain << 16 | bus << 8 | device << 3 | function), -1 when unknown."""
+    try:
+        dom, bus, rest = bus_id.lower().split(":")
+        dev, fn = rest.split(".")
+        return (int(dom, 16) << 16) | (int(bus, 16) << 8) | (int(dev, 16) << 3) | int(fn, 16)
+    except (AttributeError, ValueError):
+        return -1
 
 
 def self_launch(args, argv):
@@ -103,6 +180,9 @@ def self_launch(args, argv):
     if n_dev < args.gpus and not args.allow_shared_gpu:
         print(f"bench.py: --gpus {args.gpus} but only {n_dev} GPU(s) visible", file=sys.stderr, flush=True)
         return 2
+    stale = cleanup_stale_shm()
+    if stale:
+        print(f"[bench] removed {len(stale)} stale node-shared array(s) of an earlier run", file=sys.stderr, flush=True)
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     print(f"[bench] launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
@@ -208,6 +288,8 @@ def main():
             print(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}", file=sys.stderr)
             return 2
 
+    if world == 1:
+        cleanup_stale_shm()  # a single rank is its own launcher
     t_setup = time.perf_counter()
 
     def progress(msg):  # setup of big batches takes minutes: keep stderr alive (rank 0)
@@ -314,9 +396,16 @@ def main():
         te = torch.tensor([wire.total], dtype=torch.int64, device=cdev)
         dist.all_reduce(te)
         total_elems = int(te.item())
-    # per-rank evidence: NUMA node of the host arrays, median kernel ms per step, device index
-    mine = torch.tensor([float(numa), float(np.median(kms)), float(gpu), float(wire.total)],
-                        dtype=torch.float64, device=cdev)
+    # per-rank evidence: NUMA node of the host arrays, median kernel ms per step, device index, letters, step
+    # time p50/p99 (this rank's clock), PCIe link rate of the stream (bytes in / kernel time), PCIe address —
+    # so a slow step or a slow link in a scaling run is attributable to a rank from the record alone
+    from mpi_openmp_cuda_amd.ops.align import device_info
+
+    bus = pci_bus_code(device_info(gpu).get("pci_bus_id"))
+    k_med = float(np.median(kms))
+    h2d_gbps = st["h2d_bytes"] / (k_med * 1e6) if k_med > 0 else 0.0
+    mine = torch.tensor([float(numa), k_med, float(gpu), float(wire.total), float(np.percentile(sms, 50)),
+                         float(np.percentile(sms, 99)), h2d_gbps, float(bus)], dtype=torch.float64, device=cdev)
     if distributed:
         allv = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(allv, mine)
@@ -368,6 +457,9 @@ def main():
             "rank_kernel_ms": [round(float(x), 4) for x in per_rank[:, 1]],
             "rank_devices": [int(x) for x in per_rank[:, 2]],
             "rank_letters": [int(x) for x in per_rank[:, 3]],
+            "rank_step_ms_p50_p99": [[round(float(a), 4), round(float(b), 4)] for a, b in per_rank[:, 4:6]],
+            "rank_h2d_gbps": [round(float(x), 2) for x in per_rank[:, 6]],
+            "rank_pci_bus": [pci_bus_id(int(x)) for x in per_rank[:, 7]],
             "rank0_kernels": st["kernels"],
             "host_stream": ("dma" if st["dma"] else "zero_copy") if st["direct"] else "staged",
             "verified": bool(okt.item()),

@@ -196,7 +196,9 @@ class Cutter {
     }
     const int64_t len = end - counted_;
     if (len <= 0) return;
-    const int nt = len > 2 * kMiB ? std::max(1, std::min<int>(omp_get_max_threads(), static_cast<int>(len / kMiB))) : 1;
+    // ~1 MiB chunks: the walk to a batch's cut scans at most one, and the ranks' encode of a batch gets
+    // pieces small enough to balance over their threads
+    const int nt = static_cast<int>(std::clamp<int64_t>(len / kMiB, 1, 1 << 14));
     const unsigned char* ua = reinterpret_cast<const unsigned char*>(t_.at(counted_));
     std::vector<Chunk> parts(static_cast<size_t>(nt));
     std::vector<int64_t> b(static_cast<size_t>(nt) + 1);
@@ -207,7 +209,7 @@ class Cutter {
       b[q] = x;
     }
     b[nt] = len;
-#pragma omp parallel for schedule(static, 1) num_threads(nt) if (nt > 1)
+#pragma omp parallel for schedule(dynamic, 4) if (nt > 2)
     for (int q = 0; q < nt; ++q) {
       Chunk& c = parts[q];
       c.begin = counted_ + b[q];

@@ -18,6 +18,7 @@ struct DeviceInfo {
   int64_t global_mem = 0;
   int64_t lds_per_block = 0;
   int clock_khz = 0;
+  std::string pci_bus_id;  // "dddd:bb:dd.f" (lower case), empty when unknown
   std::string json() const;
 };
 

@@ -140,16 +140,18 @@ void gatherv_bytes(const void* sendbuf, int64_t count, void* recvbuf, const std:
 // ------------------------------------------------------------------------------------------------
 SharedWindow::SharedWindow(const MpiContext& ctx, int64_t bytes) : comm_(ctx.node) {
   if (ctx.local_size == 1) {
-    constexpr size_t kHuge = size_t{2} << 20;
-    const size_t want = (static_cast<size_t>(std::max<int64_t>(bytes, 8)) + kHuge - 1) & ~(kHuge - 1);
-    map_bytes_ = want + kHuge;  // slack to start on a 2 MiB boundary
+    // huge pages from 1 MiB up (a small window's first touch would zero a whole 2 MiB page)
+    const bool huge = bytes >= (int64_t{1} << 20);
+    const size_t align = huge ? size_t{2} << 20 : size_t{4096};
+    const size_t want = (static_cast<size_t>(std::max<int64_t>(bytes, 8)) + align - 1) & ~(align - 1);
+    map_bytes_ = huge ? want + align : want;  // slack to start on a 2 MiB boundary
     map_ = mmap(nullptr, map_bytes_, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
     if (map_ == MAP_FAILED) {
       map_ = nullptr;
       throw Error("SharedWindow: cannot map " + std::to_string(map_bytes_) + " bytes");
     }
-    base_ = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(map_) + kHuge - 1) & ~(kHuge - 1));
-    (void)madvise(base_, want, MADV_HUGEPAGE);  // advisory: 4 KiB pages if THP is off
+    base_ = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(map_) + align - 1) & ~(align - 1));
+    if (huge) (void)madvise(base_, want, MADV_HUGEPAGE);  // advisory: 4 KiB pages if THP is off
     bytes_ = bytes;
     return;
   }

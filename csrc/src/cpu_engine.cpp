@@ -81,14 +81,28 @@ Result solve_record(const ScoreTable& t, const uint8_t* s1, int64_t L1, const ui
   return r.n < 0 ? no_candidate() : r;
 }
 
+namespace {
+// Threads worth waking for `cells` of search work: a thread per ~0.25 M cells (~0.5 ms at the engine's
+// rate), so a reference-sized job (input6: 730 cells) runs on the calling thread without forking a team —
+// the team's start-up and spin-down cost more than the whole search (49-63 ms vs 26 ms).
+int threads_for(const RecordBatch& batch, int64_t L1, Semantics sem, int nt) {
+  if (nt <= 1) return 1;
+  const int64_t n = batch.size();
+  int64_t cells = 0;
+  for (int64_t i = 0; i < n && cells < int64_t{nt} << 18; ++i)
+    cells += candidate_offsets(L1, batch.length(i), sem) * std::max<int64_t>(batch.length(i), 1);
+  return static_cast<int>(std::clamp<int64_t>(cells >> 18, 1, nt));
+}
+}  // namespace
+
 void solve_batch_cpu(const ScoreTable& t, const uint8_t* s1, int64_t L1, const RecordBatch& batch, Result* out,
                      Semantics sem, int num_threads) {
   const int64_t n = batch.size();
-  const int nt = num_threads > 0 ? num_threads : omp_get_max_threads();
+  const int nt = threads_for(batch, L1, sem, num_threads > 0 ? num_threads : omp_get_max_threads());
   if (n >= 4 * nt || nt == 1) {
     // dynamic balance in chunks: per-record dispatch would dominate tiny records (input6: ~150 cells)
     const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(1024, n / (64 * nt)));
-#pragma omp parallel for schedule(dynamic, chunk) num_threads(nt)
+#pragma omp parallel for schedule(dynamic, chunk) num_threads(nt) if (nt > 1)
     for (int64_t i = 0; i < n; ++i) out[i] = solve_record(t, s1, L1, batch.record(i), batch.length(i), sem);
     return;
   }
@@ -109,7 +123,7 @@ void solve_batch_cpu(const ScoreTable& t, const uint8_t* s1, int64_t L1, const R
     for (int64_t ob = 0; ob < n_off; ob += chunk) items.push_back(Item{i, ob, std::min(n_off, ob + chunk)});
   }
   std::vector<Result> part(items.size());
-#pragma omp parallel for schedule(dynamic, 1) num_threads(nt)
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nt) if (nt > 1)
   for (int64_t j = 0; j < static_cast<int64_t>(items.size()); ++j) {
     const Item& it = items[j];
     part[j] = solve_offsets(t, s1, L1, batch.record(it.rec), batch.length(it.rec), it.ob, it.oe, sem);
@@ -128,7 +142,7 @@ void solve_keys_cpu(const ScoreTable& t, const uint8_t* s1, int64_t L1, const Re
                     int parts, uint64_t* keys, Semantics sem, int num_threads) {
   if (parts < 1 || part < 0 || part >= parts) throw Error("solve_keys_cpu: bad part");
   const int64_t n = batch.size();
-  const int nt = num_threads > 0 ? num_threads : omp_get_max_threads();
+  const int nt = threads_for(batch, L1, sem, num_threads > 0 ? num_threads : omp_get_max_threads());
   auto range = [&](int64_t i, int64_t& b, int64_t& e) {
     const int64_t c = candidate_offsets(L1, batch.length(i), sem);
     b = c * part / parts;
@@ -136,7 +150,7 @@ void solve_keys_cpu(const ScoreTable& t, const uint8_t* s1, int64_t L1, const Re
   };
   if (n >= 4 * nt || nt == 1) {
     const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(1024, n / (64 * nt)));
-#pragma omp parallel for schedule(dynamic, chunk) num_threads(nt)
+#pragma omp parallel for schedule(dynamic, chunk) num_threads(nt) if (nt > 1)
     for (int64_t i = 0; i < n; ++i) {
       int64_t b, e;
       range(i, b, e);
@@ -157,7 +171,7 @@ void solve_keys_cpu(const ScoreTable& t, const uint8_t* s1, int64_t L1, const Re
     for (int64_t ob = b; ob < e; ob += chunk) items.push_back(Item{i, ob, std::min(e, ob + chunk)});
   }
   std::vector<uint64_t> pk(items.size());
-#pragma omp parallel for schedule(dynamic, 1) num_threads(nt)
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nt) if (nt > 1)
   for (int64_t j = 0; j < static_cast<int64_t>(items.size()); ++j) {
     const Item& it = items[j];
     const int64_t L2 = batch.length(it.rec);

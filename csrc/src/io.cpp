@@ -6,7 +6,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
-#include <emmintrin.h>
+#include <immintrin.h>
 
 #include <algorithm>
 #include <atomic>
@@ -207,8 +207,43 @@ std::vector<int64_t> BulkParser::chunk_starts(int nchunks) const {
   return s;
 }
 
+namespace {
+bool count_simd_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("MOC_FILL_SIMD");
+    if (e && std::strcmp(e, "0") == 0) return false;
+    __builtin_cpu_init();
+    return __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw");
+  }();
+  return on;
+}
+
+// count_tokens, 64 bytes per step: whitespace mask by byte compares; tokens = non-space bytes after
+// whitespace, letters = non-space bytes (two popcounts per 64 bytes).
+__attribute__((target("avx512f,avx512bw,popcnt"))) void count_tokens_avx512(const unsigned char* ua, size_t len,
+                                                                              int64_t* tokens, int64_t* letters) {
+  const __m512i k9 = _mm512_set1_epi8(9), k4 = _mm512_set1_epi8(4), kSp = _mm512_set1_epi8(' ');
+  uint64_t prev_ws = 1, nt = 0, nc = 0;
+  for (size_t i = 0; i < len; i += 64) {
+    const size_t nb = std::min<size_t>(64, len - i);
+    const __mmask64 in = nb == 64 ? ~__mmask64{0} : (__mmask64{1} << nb) - 1;
+    const __m512i v = _mm512_maskz_loadu_epi8(in, ua + i);
+    const __mmask64 ws = _mm512_cmpeq_epi8_mask(v, kSp) | _mm512_cmple_epu8_mask(_mm512_sub_epi8(v, k9), k4) | ~in;
+    nt += _mm_popcnt_u64(~ws & ((ws << 1) | prev_ws));
+    nc += _mm_popcnt_u64(~ws);
+    prev_ws = ws >> 63;
+  }
+  *tokens = static_cast<int64_t>(nt);
+  *letters = static_cast<int64_t>(nc);
+}
+}  // namespace
+
 void count_tokens(const char* p, size_t len, int64_t* tokens, int64_t* letters) {
   const unsigned char* ua = reinterpret_cast<const unsigned char*>(p);
+  if (count_simd_enabled()) {
+    count_tokens_avx512(ua, len, tokens, letters);
+    return;
+  }
   int64_t nt = 0, nc = 0;
   if (len > 0) {  // the text starts at a token start or at whitespace
     const int64_t first = is_space(ua[0]) ? 0 : 1;
@@ -238,7 +273,7 @@ void count_tokens(const char* p, size_t len, int64_t* tokens, int64_t* letters) 
 void BulkParser::count_chunks(const std::vector<int64_t>& starts, int c0, int c1, int64_t* toks,
                               int64_t* chars) const {
   // Iterations are chunks, not thread ids: correct whatever number of threads OpenMP delivers.
-#pragma omp parallel for schedule(dynamic, 1) if (c1 - c0 > 1)
+#pragma omp parallel for schedule(dynamic, 1) if (c1 - c0 > 1 && starts[c1] - starts[c0] > (int64_t{1} << 16))
   for (int c = c0; c < c1; ++c)
     count_tokens(area_ + starts[c], static_cast<size_t>(starts[c + 1] - starts[c]), toks + (c - c0), chars + (c - c0));
 }
@@ -338,6 +373,177 @@ struct PieceOut {
   int64_t rec_base = 0;                       // global index of the piece's first record
   std::vector<std::pair<int64_t, uint8_t>> stragglers;  // packed mode: letters of partial groups
 };
+
+// One piece of a slice for the vector encoder: text bytes [bb, be) (starting at a token start or at
+// whitespace, ending after its last token), its letters [a, b) and first token (slice-relative), and the
+// outputs of fill_slice.
+struct PieceJob {
+  const unsigned char* ua;
+  size_t bb, be;
+  int64_t a, b, tok0;
+  uint8_t* codes;
+  uint8_t* packed;
+  int64_t* offs;
+  int64_t* sparse;
+  uint16_t* len16;
+  int64_t G, GB;
+  bool p24, p33;
+  int64_t l2_cap, L1;
+};
+
+// MOC_FILL_SIMD=0 selects the portable SSE2 encoder (A/B, and hosts without AVX-512 VBMI2 use it anyway).
+bool fill_simd_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("MOC_FILL_SIMD");
+    if (e && std::strcmp(e, "0") == 0) return false;
+    __builtin_cpu_init();
+    return __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&
+           __builtin_cpu_supports("avx512vbmi") && __builtin_cpu_supports("avx512vbmi2");
+  }();
+  return on;
+}
+
+#define MOC_AVX512 __attribute__((target("avx512f,avx512bw,avx512vbmi,avx512vbmi2,bmi,bmi2,popcnt,lzcnt")))
+
+// One P33 block (moc::p33_block_full) with the digit arithmetic on 64-bit lanes: the 56 codes are permuted
+// into 8 lanes of 7 digits, vpmaddubsw / vpmaddwd form each lane's base-26 halves (digits 0..3 and 4..6)
+// and one 32x32 multiply joins them; the eight 33-bit fields are then laid out as p33_block_full does.
+MOC_AVX512 inline void p33_block_avx512(const uint8_t* c, uint8_t* out) {
+  // lane k, byte j <- code 7k + j (byte 7 of every lane is zeroed by the mask below)
+  alignas(64) static constexpr uint8_t kIdxBytes[64] = {
+      0,  1,  2,  3,  4,  5,  6,  0, 7,  8,  9,  10, 11, 12, 13, 0, 14, 15, 16, 17, 18, 19, 20, 0,
+      21, 22, 23, 24, 25, 26, 27, 0, 28, 29, 30, 31, 32, 33, 34, 0, 35, 36, 37, 38, 39, 40, 41, 0,
+      42, 43, 44, 45, 46, 47, 48, 0, 49, 50, 51, 52, 53, 54, 55, 0};
+  const __m512i kIdx = _mm512_load_si512(reinterpret_cast<const void*>(kIdxBytes));
+  const __m512i x = _mm512_subs_epu8(_mm512_maskz_loadu_epi8((__mmask64{1} << 56) - 1, c), _mm512_set1_epi8(1));
+  const __m512i y = _mm512_maskz_permutexvar_epi8(0x7F7F7F7F7F7F7F7Full, kIdx, x);
+  const __m512i w = _mm512_maddubs_epi16(y, _mm512_set1_epi16(static_cast<short>(1 | (26 << 8))));
+  const __m512i d = _mm512_madd_epi16(w, _mm512_set1_epi32(1 | (676 << 16)));
+  const __m512i f = _mm512_add_epi64(_mm512_and_si512(d, _mm512_set1_epi64(0xFFFFFFFFll)),
+                                     _mm512_mul_epu32(_mm512_srli_epi64(d, 32), _mm512_set1_epi64(456976)));
+  alignas(64) uint64_t fv[8];
+  _mm512_store_si512(reinterpret_cast<void*>(fv), f);
+  const uint64_t wv[4] = {fv[0] | fv[1] << 33, fv[1] >> 31 | fv[2] << 2 | fv[3] << 35,
+                          fv[3] >> 29 | fv[4] << 4 | fv[5] << 37, fv[5] >> 27 | fv[6] << 6 | fv[7] << 39};
+  std::memcpy(out, wv, 32);
+  out[32] = static_cast<uint8_t>(fv[7] >> 25);
+}
+
+// Pass 2 of one piece, 64 text bytes per step: whitespace / letter masks by byte compares, the letter codes
+// compacted with vpcompressb (register form) and stored under a mask, token starts as mask bits (a
+// non-space byte after whitespace); each token's start letter is a popcount of the compacted bytes before
+// it, so a record costs a few scalar operations and a byte costs none. Returns false — the caller then
+// runs the scalar encoder for the piece, which names the offending record — on a non-letter byte or a
+// record over the length limit.
+// Packs the staged letters [st.base, hi) of a piece (and copies them to codes when both are wanted): whole
+// groups straight into the packed stream; letters of the piece's first partial group and, at the end, of
+// its last one go to the stragglers (fixed up once the whole slice is encoded).
+struct Stager {
+  uint8_t* stage;
+  int64_t base;
+  bool head_done;
+};
+MOC_AVX512 void stage_flush(const PieceJob& j, PieceOut& po, Stager& st, int64_t hi, bool final) {
+  const int64_t G = j.G, GB = j.GB;
+  if (j.codes) std::memcpy(j.codes + st.base, st.stage, static_cast<size_t>(hi - st.base));
+  int64_t cur = st.base;
+  if (!st.head_done) {
+    const int64_t g0 = (j.a + G - 1) / G * G, hend = std::min(g0, hi);
+    if (hend < g0 && !final) return;
+    for (int64_t c = cur; c < hend; ++c) po.stragglers.emplace_back(c, st.stage[c - st.base]);
+    cur = hend;
+    st.head_done = true;
+  }
+  const int64_t ng = (hi - cur) / G;
+  const uint8_t* src = st.stage + (cur - st.base);
+  uint8_t* dst = j.packed + GB * (cur / G);
+  if (j.p33) {
+    for (int64_t g = 0; g < ng; ++g) p33_block_avx512(src + kP33Letters * g, dst + kP33Bytes * g);
+  } else if (j.p24) {
+    for (int64_t g = 0; g < ng; ++g) {
+      const uint32_t v = p24_group(src + 5 * g);
+      std::memcpy(dst + 3 * g, &v, g + 1 < ng ? 4 : 3);
+    }
+  } else {
+    for (int64_t g = 0; g < ng; ++g) {
+      uint64_t x;
+      std::memcpy(&x, src + 8 * g, 8);
+      x = compress8(x);
+      std::memcpy(dst + 5 * g, &x, g + 1 < ng ? 8 : 5);
+    }
+  }
+  cur += G * ng;
+  if (final) {
+    for (int64_t c = cur; c < hi; ++c) po.stragglers.emplace_back(c, st.stage[c - st.base]);
+  } else {
+    std::memmove(st.stage, st.stage + (cur - st.base), static_cast<size_t>(hi - cur));
+    st.base = cur;
+  }
+}
+
+MOC_AVX512 bool fill_piece_avx512(const PieceJob& j, PieceOut& po) {
+  thread_local std::vector<uint8_t> stage_tl;
+  if (j.packed && stage_tl.size() < static_cast<size_t>(kStage + 128)) stage_tl.resize(static_cast<size_t>(kStage + 128));
+  Stager st{j.packed ? stage_tl.data() : nullptr, j.packed ? j.a : 0, false};  // sink[x - base] = letter x
+  uint8_t* const sink_base = j.packed ? st.stage : j.codes;
+  const __m512i k1F = _mm512_set1_epi8(0x1F), kDF = _mm512_set1_epi8(static_cast<char>(0xDF));
+  const __m512i kA = _mm512_set1_epi8('A'), k25 = _mm512_set1_epi8(25), k9 = _mm512_set1_epi8(9);
+  const __m512i k4 = _mm512_set1_epi8(4), kSp = _mm512_set1_epi8(' ');
+  const int64_t L1 = j.L1, cap = j.l2_cap > 0 ? j.l2_cap : INT64_MAX;
+  constexpr int64_t kMask = (int64_t{1} << kSparseShift) - 1;
+  int64_t* const offs = j.offs;
+  int64_t* const sparse = j.sparse;
+  uint16_t* const len16 = j.len16;
+  int64_t pos = j.a, tok = j.tok0, cur = -1;
+  int64_t mn = INT64_MAX, mx = 0, cells = 0;
+  uint64_t prev_ws = 1;
+  for (size_t i = j.bb; i < j.be; i += 64) {
+    const size_t nb = std::min<size_t>(64, j.be - i);
+    const __mmask64 in = nb == 64 ? ~__mmask64{0} : (__mmask64{1} << nb) - 1;
+    const __m512i v = _mm512_maskz_loadu_epi8(in, j.ua + i);
+    const __mmask64 ws = _mm512_cmpeq_epi8_mask(v, kSp) | _mm512_cmple_epu8_mask(_mm512_sub_epi8(v, k9), k4) | ~in;
+    const __mmask64 nonws = ~ws;
+    const __mmask64 letter = _mm512_cmple_epu8_mask(_mm512_sub_epi8(_mm512_and_si512(v, kDF), kA), k25);
+    if (nonws & ~letter) return false;  // a non-letter: the scalar encoder reports it
+    const __mmask64 starts = nonws & ((ws << 1) | prev_ws);
+    prev_ws = ws >> 63;
+    const int cnt = static_cast<int>(_mm_popcnt_u64(nonws));
+    if (j.packed && pos - st.base > kStage) stage_flush(j, po, st, pos, false);
+    _mm512_mask_storeu_epi8(sink_base + (pos - st.base), cnt == 64 ? ~__mmask64{0} : (__mmask64{1} << cnt) - 1,
+                            _mm512_maskz_compress_epi8(nonws, _mm512_and_si512(v, k1F)));
+    for (uint64_t m = starts; m; m &= m - 1) {
+      const int64_t S = pos + static_cast<int64_t>(_mm_popcnt_u64(nonws & (_blsi_u64(m) - 1)));
+      if (cur >= 0) {  // the previous token, letters [cur, S), is record `tok`
+        const int64_t L = S - cur;
+        mn = std::min(mn, L);
+        mx = std::max(mx, L);
+        cells += L <= L1 ? (L1 - L + 1) * L : 0;
+        if (sparse && (tok & kMask) == 0) sparse[tok >> kSparseShift] = cur;
+        if (len16) len16[tok] = static_cast<uint16_t>(L < 65535 ? L : 65535);
+        if (offs) offs[tok + 1] = S;
+        ++tok;
+      }
+      cur = S;
+    }
+    pos += cnt;
+  }
+  if (cur >= 0) {
+    const int64_t L = pos - cur;
+    mn = std::min(mn, L);
+    mx = std::max(mx, L);
+    cells += L <= L1 ? (L1 - L + 1) * L : 0;
+    if (sparse && (tok & kMask) == 0) sparse[tok >> kSparseShift] = cur;
+    if (len16) len16[tok] = static_cast<uint16_t>(L < 65535 ? L : 65535);
+    if (offs) offs[tok + 1] = pos;
+    ++tok;
+  }
+  if (mx > cap) return false;  // a record over the limit: the scalar encoder reports the first one
+  if (j.packed) stage_flush(j, po, st, pos, true);
+  po.rep.min_len = mn;
+  po.rep.max_len = mx;
+  po.rep.cells = cells;
+  return true;
+}
 }  // namespace
 
 FillReport BulkParser::fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* packed5, int64_t* offs, int64_t* sparse,
@@ -355,13 +561,22 @@ FillReport BulkParser::fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* p
   const int64_t L1 = static_cast<int64_t>(seq1_.size());
   const size_t vec_in_end = area_len_ >= 16 ? area_len_ - 16 : 0;  // 16-byte loads stay in the area
   std::vector<PieceOut> out(static_cast<size_t>(np));
-  // one piece per iteration (dynamic): correct for any number of delivered threads
-#pragma omp parallel for schedule(dynamic, 1)
+  const bool simd = fill_simd_enabled();
+  // one piece per iteration (dynamic): correct for any number of delivered threads; a small slice is
+  // encoded on the calling thread (no team start-up for a reference-sized input)
+#pragma omp parallel for schedule(dynamic, 1) if (np > 1 && s.letters > (int64_t{1} << 16))
   for (int q = 0; q < np; ++q) {
     const AreaPiece& pc = s.pieces[q];
     PieceOut& po = out[q];
     const int64_t a = pc.chr, b = q + 1 < np ? s.pieces[q + 1].chr : s.letters;  // this piece's letters [a, b)
     po.rec_base = s.first_record + pc.tok;
+    if (simd) {
+      const PieceJob pj{ua,    static_cast<size_t>(pc.byte_begin), static_cast<size_t>(pc.byte_end), a, b, pc.tok,
+                        codes, packed5, offs, sparse, len16, G, GB, p24, p33, l2_cap, L1};
+      if (fill_piece_avx512(pj, po)) continue;
+      po = PieceOut{};  // an input error in this piece: the scalar pass below finds and reports it
+      po.rec_base = s.first_record + pc.tok;
+    }
     std::vector<uint8_t> stage(packed5 ? static_cast<size_t>(kStage + 64) : 0);
     // sink of the encoded letters: `codes` at the slice position, else the staging buffer
     int64_t base = packed5 ? a : 0;  // slice letter index of stage[0]
@@ -558,7 +773,7 @@ void BulkParser::chunk_costs(const std::vector<int64_t>& starts, int c0, int c1,
                              double* costs) const {
   const unsigned char* ua = reinterpret_cast<const unsigned char*>(area_);
   const int64_t L1 = static_cast<int64_t>(seq1_.size());
-#pragma omp parallel for schedule(dynamic, 1)
+#pragma omp parallel for schedule(dynamic, 1) if (c1 - c0 > 1 && starts[c1] - starts[c0] > (int64_t{1} << 16))
   for (int c = c0; c < c1; ++c) {
     int64_t i = starts[c];
     const int64_t e = starts[c + 1];

@@ -34,6 +34,13 @@ DeviceInfo device_info(int id) {
   d.global_mem = static_cast<int64_t>(p.totalGlobalMem);
   d.lds_per_block = static_cast<int64_t>(p.sharedMemPerBlock);
   d.clock_khz = p.clockRate;
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof bus, id) == hipSuccess) {
+    d.pci_bus_id = bus;
+    for (auto& c : d.pci_bus_id) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
+  } else {
+    (void)hipGetLastError();
+  }
   return d;
 }
 
@@ -41,7 +48,7 @@ std::string DeviceInfo::json() const {
   std::ostringstream os;
   os << "{\"id\": " << id << ", \"name\": \"" << name << "\", \"arch\": \"" << arch << "\", \"cus\": " << compute_units
      << ", \"wave\": " << wave_size << ", \"mem_gb\": " << (global_mem / 1e9) << ", \"lds_per_block\": " << lds_per_block
-     << "}";
+     << ", \"pci_bus_id\": \"" << pci_bus_id << "\"}";
   return os.str();
 }
 

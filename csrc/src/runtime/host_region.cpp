@@ -35,16 +35,20 @@ void prefault_pages(char* p, size_t bytes) {
 }
 
 HostRegion::HostRegion(size_t bytes, int numa_node) {
-  const size_t want = (std::max<size_t>(bytes, 1) + kHuge - 1) & ~(kHuge - 1);
-  map_bytes_ = want + kHuge;  // slack to start on a 2 MiB boundary
+  // below 1 MiB: plain 4 KiB pages (a huge page's first touch zeroes 2 MiB — 0.2-2 ms for a buffer of a
+  // few bytes, the whole search time of a reference-sized input)
+  const bool huge = bytes >= (size_t{1} << 20);
+  const size_t align = huge ? kHuge : size_t{4096};
+  const size_t want = (std::max<size_t>(bytes, 1) + align - 1) & ~(align - 1);
+  map_bytes_ = huge ? want + kHuge : want;  // slack to start on a 2 MiB boundary
   map_ = mmap(nullptr, map_bytes_, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
   if (map_ == MAP_FAILED) {
     map_ = nullptr;
     throw Error("HostRegion: cannot map " + std::to_string(map_bytes_) + " bytes");
   }
-  base_ = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(map_) + kHuge - 1) & ~(kHuge - 1));
+  base_ = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(map_) + align - 1) & ~(align - 1));
   bytes_ = bytes;
-  (void)madvise(base_, want, MADV_HUGEPAGE);  // advisory: 4 KiB pages if THP is off
+  if (huge) (void)madvise(base_, want, MADV_HUGEPAGE);  // advisory: 4 KiB pages if THP is off
   if (numa_node >= 0) (void)bind_range_to_node(base_, want, numa_node);
 }
 

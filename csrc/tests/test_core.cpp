@@ -505,11 +505,20 @@ void test_slices() {
       for (int j = 0; j < L; ++j) r += static_cast<char>((rng() & 1 ? 'A' : 'a') + rng() % 26);
       recs.push_back(r);
       text += r;
-      const int sep = static_cast<int>(rng() % 4);
-      text += sep == 0 ? "\n" : sep == 1 ? " \r\n" : sep == 2 ? "\t" : "\n\n  ";
+      const int sep = static_cast<int>(rng() % 6);
+      text += sep == 0 ? "\n" : sep == 1 ? " \r\n" : sep == 2 ? "\t" : sep == 3 ? "\n\n  " : sep == 4 ? "\v" : "\f \n";
     }
     if (trial % 5 == 0) text += "EXTRA TRAILING TOKENS\n";
     const Problem ref = parse_problem(text.data(), text.size());
+    {  // the reference parse (same encoder as below: SIMD or scalar, MOC_FILL_SIMD) against the records
+      bool same = ref.seq2.size() == n;
+      for (int i = 0; same && i < n; ++i) {
+        same = ref.seq2.length(i) == static_cast<int64_t>(recs[i].size());
+        for (size_t j = 0; same && j < recs[i].size(); ++j)
+          same = ref.seq2.record(i)[j] == letter_code(static_cast<unsigned char>(recs[i][j]));
+      }
+      CHECK(same);
+    }
     BulkParser p(text.data(), text.size(), ParseOptions{}, false);
     CHECK(p.total_chars() < 0);
     const int nch = 1 + static_cast<int>(rng() % 97);

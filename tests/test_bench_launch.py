@@ -48,3 +48,54 @@ def test_rank_refuses_world_mismatch():
     r = run(["--gpus", "4"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 2
     assert b"refusing to report a different rank count" in r.stderr
+
+
+def _bench_module():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", BENCH)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_kfd_gpu_count_from_sysfs(tmp_path):
+    # the launcher counts GPUs from the KFD topology (no HIP runtime, no torch): nodes with SIMDs are GPUs,
+    # the *_VISIBLE_DEVICES variables narrow the count, a missing topology gives None (torch fallback)
+    b = _bench_module()
+    nodes = tmp_path / "nodes"
+    for i, simds in enumerate([0, 0, 1024, 1024, 1024]):  # two CPU nodes, three GPUs
+        (nodes / str(i)).mkdir(parents=True)
+        (nodes / str(i) / "properties").write_text(f"cpu_cores_count 64\nsimd_count {simds}\ngfx_target_version 90500\n")
+    (nodes / "9").mkdir()  # a node without properties is skipped
+    assert b.kfd_gpu_count(str(nodes), env={}) == 3
+    assert b.kfd_gpu_count(str(nodes), env={"HIP_VISIBLE_DEVICES": "0,2"}) == 2
+    assert b.kfd_gpu_count(str(nodes), env={"ROCR_VISIBLE_DEVICES": ""}) == 0
+    assert b.kfd_gpu_count(str(tmp_path / "absent"), env={}) is None
+    # this container: no GPU nodes (or no KFD at all) -> the 2-GPU launch refusal above comes from sysfs
+    assert b.kfd_gpu_count(env={}) in (None, 0)
+
+
+def test_stale_shm_cleanup(tmp_path):
+    # arrays of a crashed run (older than the launcher) are removed; newer ones and other names are kept
+    import time
+
+    b = _bench_module()
+    prefix = str(tmp_path / "moc_bench_")
+    old = tmp_path / "moc_bench_1234_0_letters"
+    new = tmp_path / "moc_bench_5678_0_letters"
+    other = tmp_path / "unrelated"
+    for p in (old, new, other):
+        p.write_bytes(b"x")
+    t = time.time()
+    os.utime(old, (t - 100, t - 100))
+    os.utime(other, (t - 100, t - 100))
+    removed = b.cleanup_stale_shm(before=t - 10, prefix=prefix)
+    assert removed == [str(old)] and not old.exists() and new.exists() and other.exists()
+
+
+def test_pci_bus_code_roundtrip():
+    b = _bench_module()
+    for bus in ("0000:0d:00.0", "0001:8e:1f.7"):
+        assert b.pci_bus_id(b.pci_bus_code(bus)) == bus
+    assert b.pci_bus_code("") == -1 and b.pci_bus_id(-1) is None

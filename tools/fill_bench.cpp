@@ -1,7 +1,10 @@
-// Parser fill throughput by letter code: BulkParser::fill_slice into the GPU wire form (packed letters +
-// sparse offsets + uint16 lengths) for 5-bit / P24 / P33 letters on an input6-shaped text (CPU only).
-// Build: g++ -O3 -std=c++17 -fopenmp -Icsrc/include tools/fill_bench.cpp build/obj/io.o build/obj/problem.o \
-//          build/obj/score_table.o build/obj/partition.o build/obj/runtime/runtime.o -ldl -o build/fill_bench
+// Parser throughput on an input6-shaped text (CPU only): pass 1 (count_tokens over thread chunks) against
+// pass 2 (BulkParser::fill_slice into the GPU wire form: packed letters + sparse offsets + uint16 lengths)
+// for 5-bit / P24 / P33 letters, and the byte form the CPU engine takes. MOC_FILL_SIMD=0 forces the
+// portable SSE2 encoder (A/B against the AVX-512 one).
+// Build: make build/fill_bench   (or see the Makefile rule)   Run: build/fill_bench [records]
+#include <omp.h>
+
 #include <chrono>
 #include <cstdio>
 #include <random>
@@ -22,17 +25,37 @@ int main(int argc, char** argv) {
     for (int j = 0; j < L; ++j) text += static_cast<char>('A' + rng() % 26);
     text += '\n';
   }
-  moc::BulkParser p(text.data(), text.size());
+  const double gb = text.size() / 1e9;
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto ms_since = [](auto t0) { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
+  moc::BulkParser p(text.data(), text.size(), {}, false);
+  const int nch = 4 * omp_get_max_threads();
+  std::vector<int64_t> st = p.chunk_starts(nch), tk(nch), ch(nch);
+  for (int rep = 0; rep < 3; ++rep) {
+    const auto t0 = now();
+    p.count_chunks(st, 0, nch, tk.data(), ch.data());
+    const double ms = ms_since(t0);
+    std::printf("count threads=%d ms=%.1f GB/s=%.1f\n", omp_get_max_threads(), ms, gb / (ms / 1e3));
+  }
+  p.set_chunks(st, tk.data(), ch.data());
   const moc::AreaSlice s = p.slice(0, p.count());
   std::vector<int64_t> sp(static_cast<size_t>(moc::sparse_count(s.records, moc::kSparseShift)));
   std::vector<uint16_t> l16(static_cast<size_t>(s.records));
   std::vector<uint8_t> out(static_cast<size_t>(moc::packed5_bytes(s.letters)) + 64);
-  for (int rep = 0; rep < 3; ++rep)
+  std::vector<uint8_t> codes(static_cast<size_t>(s.letters) + 64);
+  std::vector<int64_t> offs(static_cast<size_t>(s.records) + 1);
+  for (int rep = 0; rep < 3; ++rep) {
     for (int pack : {5, 24, 33}) {
-      const auto t0 = std::chrono::steady_clock::now();
+      const auto t0 = now();
       p.fill_slice(s, nullptr, out.data(), nullptr, sp.data(), l16.data(), pack);
-      const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-      std::printf("pack=%d letters=%lld fill_ms=%.1f\n", pack, static_cast<long long>(s.letters), ms);
+      const double ms = ms_since(t0);
+      std::printf("fill pack=%d letters=%lld ms=%.1f GB/s=%.1f\n", pack, static_cast<long long>(s.letters), ms,
+                  gb / (ms / 1e3));
     }
+    const auto t0 = now();
+    p.fill_slice(s, codes.data(), nullptr, offs.data());
+    const double ms = ms_since(t0);
+    std::printf("fill bytes+offsets ms=%.1f GB/s=%.1f\n", ms, gb / (ms / 1e3));
+  }
   return 0;
 }
