@@ -1,5 +1,7 @@
 #include "moc/problem.hpp"
 
+#include "moc/simd.hpp"
+
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -106,12 +108,39 @@ void p33_block(const uint8_t* c, uint8_t* out, int m) {
   std::memcpy(out, w, kP33Bytes);
 }
 
+namespace simd {
+bool p33_available() {
+  static const bool on = [] {
+    const char* e = std::getenv("MOC_FILL_SIMD");
+    if (e && std::strcmp(e, "0") == 0) return false;
+    __builtin_cpu_init();
+    return __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") && __builtin_cpu_supports("avx512vbmi");
+  }();
+  return on;
+}
+}  // namespace simd
+
+namespace {
+// whole 56-letter blocks [g0, g1) of pack33 with the vector field arithmetic
+MOC_SIMD_P33 void pack33_blocks_simd(const uint8_t* codes, int64_t g0, int64_t g1, uint8_t* out) {
+  for (int64_t g = g0; g < g1; ++g) simd::p33_block_avx512(codes + g * kP33Letters, out + g * kP33Bytes);
+}
+}  // namespace
+
 void pack33(const uint8_t* codes, int64_t n, uint8_t* out) {
   const int64_t blocks = (n + kP33Letters - 1) / kP33Letters;
+  const int64_t full = n / kP33Letters;
+  if (simd::p33_available()) {  // whole blocks in parallel runs of 4096, the last partial one below
+    const int64_t runs = (full + 4095) / 4096;
+#pragma omp parallel for schedule(static) if (runs > 4)
+    for (int64_t r = 0; r < runs; ++r) pack33_blocks_simd(codes, 4096 * r, std::min(full, 4096 * (r + 1)), out);
+    if (full < blocks) p33_block(codes + full * kP33Letters, out + full * kP33Bytes, static_cast<int>(n - full * kP33Letters));
+  } else {
 #pragma omp parallel for schedule(static) if (blocks > 16384)
-  for (int64_t g = 0; g < blocks; ++g) {
-    const int64_t b = g * kP33Letters;
-    p33_block(codes + b, out + g * kP33Bytes, static_cast<int>(std::min<int64_t>(kP33Letters, n - b)));
+    for (int64_t g = 0; g < blocks; ++g) {
+      const int64_t b = g * kP33Letters;
+      p33_block(codes + b, out + g * kP33Bytes, static_cast<int>(std::min<int64_t>(kP33Letters, n - b)));
+    }
   }
   const int64_t used = blocks * kP33Bytes, total = packed33_bytes(n);
   for (int64_t i = used; i < total; ++i) out[i] = 0;
