@@ -57,6 +57,11 @@ class RcclDeviceComm final : public DeviceComm {
     return record(copy_);
   }
   void wait_upload(int ticket) override { MOC_HIP_CHECK(hipStreamWaitEvent(s_, events_[ticket], 0)); }
+  int upload_after(void* d, const void* h, int64_t bytes, int after) override {
+    if (after >= 0) MOC_HIP_CHECK(hipStreamWaitEvent(copy_, events_[after], 0));
+    return upload(d, h, bytes);
+  }
+  void wait_upload_host(int ticket) override { MOC_HIP_CHECK(hipEventSynchronize(events_[ticket])); }
   void download(void* h, const void* d, int64_t bytes) override {
     if (bytes > 0) MOC_HIP_CHECK(hipMemcpyAsync(h, d, static_cast<size_t>(bytes), hipMemcpyDeviceToHost, s_));
     sync();

@@ -42,6 +42,11 @@ class DeviceComm {
   // host -> device on the copy lane (returns at once); the ticket orders later comm-lane work after it
   virtual int upload(void* d, const void* h, int64_t bytes) = 0;
   virtual void wait_upload(int ticket) = 0;
+  // the same, queued behind the comm-lane point `after` (a mark; -1: nothing): a device staging buffer the
+  // comm lane still sends from is overwritten only once that send is done
+  virtual int upload_after(void* d, const void* h, int64_t bytes, int after) = 0;
+  // the host waits until an upload has read its host buffer (before reusing the staging)
+  virtual void wait_upload_host(int ticket) = 0;
   // device -> host on the comm lane; the host waits for it (and for everything queued before)
   virtual void download(void* h, const void* d, int64_t bytes) = 0;
   // comm-lane collectives on device buffers (send/recv between group_start and group_end are one group)
@@ -88,9 +93,11 @@ struct DeviceBatchOut {
 };
 
 // One batch over the device layer. Record slices (cp = false): the root packs each rank's slice into the
-// wire form that rank's engine streams, and a three-stage pipeline overlaps packing the next slice (host
-// threads), its upload (copy lane) and the send of the previous one (comm lane, in <= 64 MiB chunks);
-// every rank searches its slice in device memory and the narrow results are gathered to the root.
+// wire form that rank's engine streams, piece by piece (<= 64 MiB: letter blocks, offsets, lengths), the
+// ranks' pieces interleaved round-robin with the root's own; a three-slot pipeline packs piece i+1 (host
+// threads) while piece i uploads (copy lane) and piece i-1 goes out over xGMI (comm lane, ordered after its
+// upload on the device, no host wait); every rank searches its slice in device memory and the narrow
+// results are gathered to the root.
 // Context parallel (cp = true): the batch is broadcast, each rank searches its share of every record's
 // offsets, the packed keys are MAX-all-reduced, the root decodes them.
 // `rb` (bytes + offsets from 0) and `bounds` (p+1 record bounds) are read on the root only.

@@ -28,6 +28,8 @@ class MpiDeviceComm final : public DeviceComm {
   void host_free(void* p) override { dev_free(p); }
   int upload(void* d, const void* h, int64_t bytes) override;
   void wait_upload(int) override {}
+  int upload_after(void* d, const void* h, int64_t bytes, int) override { return upload(d, h, bytes); }
+  void wait_upload_host(int) override {}
   void download(void* h, const void* d, int64_t bytes) override;
   void group_start() override;
   void group_end() override;

@@ -45,23 +45,56 @@ void layout(RankPlan& pl) {
   if (pl.n == 0) pl.block = 0;
 }
 
-// Root: rank slice [b, b + pl.n) of rb in the plan's wire form -> dst (host staging).
-void pack_block(const RecordBatch& rb, const RankPlan& pl, char* dst) {
-  const int64_t b = pl.first, c0 = rb.offsets[b];
-  if (pl.narrow)  // the streaming kernel's form: P33 letter fields
-    pack33(rb.codes.data() + c0, pl.letters, reinterpret_cast<uint8_t*>(dst + pl.off_letters));
-  else  // the record/tile kernels' form: unpacked on the device
-    pack5(rb.codes.data() + c0, pl.letters, reinterpret_cast<uint8_t*>(dst + pl.off_letters));
-  int64_t* offs = reinterpret_cast<int64_t*>(dst + pl.off_offsets);
+// A piece of a rank's block: bytes [b0, b1) of one region (0 letters, 1 offsets, 2 lengths).
+struct Piece {
+  int rank = 0, region = 0;
+  int64_t b0 = 0, b1 = 0;
+};
+
+// The pieces of rank r's block: letter blocks and offsets in chunks of `chunk` bytes (a multiple of 33, 5
+// and 16: P33 blocks, 5-bit groups and int64 entries never straddle two pieces), the narrow lengths whole.
+std::vector<Piece> pieces_of(const RankPlan& pl, int r, int64_t chunk) {
+  std::vector<Piece> v;
+  if (pl.block == 0) return v;
+  const int64_t lb = pl.narrow ? packed33_bytes(pl.letters) : packed5_bytes(pl.letters);
+  for (int64_t b = 0; b < lb; b += chunk) v.push_back(Piece{r, 0, b, std::min(lb, b + chunk)});
+  const int64_t ob = 8 * (pl.narrow ? sparse_count(pl.n, kSparseShift) : pl.n + 1);
+  for (int64_t b = 0; b < ob; b += chunk) v.push_back(Piece{r, 1, pl.off_offsets + b, pl.off_offsets + std::min(ob, b + chunk)});
   if (pl.narrow) {
-    const int64_t ns = sparse_count(pl.n, kSparseShift);
-    for (int64_t j = 0; j < ns; ++j) offs[j] = rb.offsets[b + std::min(j << kSparseShift, pl.n)] - c0;
-    pack_lengths(rb.offsets.data() + b, pl.n, static_cast<int>(pl.bits), pl.bits == 8 ? 0 : pl.min_l2,
-                 reinterpret_cast<uint8_t*>(dst + pl.off_lengths));
-  } else {
-#pragma omp parallel for schedule(static) if (pl.n > 65536)
-    for (int64_t i = 0; i <= pl.n; ++i) offs[i] = rb.offsets[b + i] - c0;
+    const int64_t nb = narrow_lengths_bytes(pl.n, static_cast<int>(pl.bits));
+    v.push_back(Piece{r, 2, pl.off_lengths, pl.off_lengths + nb});
   }
+  return v;
+}
+
+// Root: piece `pc` of the plan's wire form of rank slice [first, first + n) of rb -> dst (host staging with
+// 64 bytes of slack: the packers write a piece's read slack past its end).
+void pack_piece(const RecordBatch& rb, const RankPlan& pl, const Piece& pc, char* dst) {
+  const int64_t b = pl.first, c0 = rb.offsets[b];
+  if (pc.region == 0) {
+    const int64_t lb = pl.narrow ? packed33_bytes(pl.letters) : packed5_bytes(pl.letters);
+    const bool last = pc.b1 == lb;
+    const int64_t L0 = pl.narrow ? kP33Letters * (pc.b0 / kP33Bytes) : 8 * (pc.b0 / 5);
+    const int64_t n = last ? pl.letters - L0 : (pl.narrow ? kP33Letters * ((pc.b1 - pc.b0) / kP33Bytes) : 8 * ((pc.b1 - pc.b0) / 5));
+    if (pl.narrow)  // the streaming kernel's form: P33 letter fields
+      pack33(rb.codes.data() + c0 + L0, n, reinterpret_cast<uint8_t*>(dst));
+    else  // the record/tile kernels' form: unpacked on the device
+      pack5(rb.codes.data() + c0 + L0, n, reinterpret_cast<uint8_t*>(dst));
+    return;
+  }
+  if (pc.region == 1) {
+    int64_t* offs = reinterpret_cast<int64_t*>(dst);
+    const int64_t e0 = (pc.b0 - pl.off_offsets) / 8, e1 = (pc.b1 - pl.off_offsets) / 8;
+    if (pl.narrow) {
+      for (int64_t j = e0; j < e1; ++j) offs[j - e0] = rb.offsets[b + std::min(j << kSparseShift, pl.n)] - c0;
+    } else {
+#pragma omp parallel for schedule(static) if (e1 - e0 > 65536)
+      for (int64_t i = e0; i < e1; ++i) offs[i - e0] = rb.offsets[b + i] - c0;
+    }
+    return;
+  }
+  pack_lengths(rb.offsets.data() + b, pl.n, static_cast<int>(pl.bits), pl.bits == 8 ? 0 : pl.min_l2,
+               reinterpret_cast<uint8_t*>(dst));
 }
 
 WireBatch device_view(const RankPlan& pl, char* d_block) {
@@ -102,24 +135,6 @@ struct DevBufs {
     for (void* p : host) dc.host_free(p);
   }
 };
-
-// Chunked point-to-point transfer of one block (both sides derive the same pieces from its size).
-void send_block(DeviceComm& dc, const char* d, int64_t bytes, int peer) {
-  const int64_t chunk = send_chunk();
-  for (int64_t off = 0; off < bytes; off += chunk) {
-    dc.group_start();
-    dc.send(d + off, std::min(chunk, bytes - off), peer);
-    dc.group_end();
-  }
-}
-void recv_block(DeviceComm& dc, char* d, int64_t bytes, int peer) {
-  const int64_t chunk = send_chunk();
-  for (int64_t off = 0; off < bytes; off += chunk) {
-    dc.group_start();
-    dc.recv(d + off, std::min(chunk, bytes - off), peer);
-    dc.group_end();
-  }
-}
 
 DeviceBatchOut batch_cp(DeviceComm& dc, DeviceSearch& ds, const RecordBatch* rb, int64_t n, int64_t total_chars,
                         const PhaseHooks& hooks) {
@@ -207,34 +222,57 @@ DeviceBatchOut device_batch(DeviceComm& dc, DeviceSearch& ds, const RecordBatch*
   const RankPlan& mine = plan[rank];
   char* d_block = bufs.d<char>(mine.block + 16);
 
-  // ---- root: pack slice r+1 (host threads) | upload slice r (copy lane) | send slice r-1 (comm lane)
+  // ---- root: pack piece i+1 (host threads) | upload piece i (copy lane) | send piece i-1 (comm lane).
+  // Pieces go round-robin over the ranks (the root's own, uploaded straight into its block, among them), so
+  // every rank's transfer starts at once and the root's slice is not the last to arrive.
+  const int64_t chunk = std::max<int64_t>(2640, send_chunk() / 2640 * 2640);  // lcm(33, 5, 16) = 2640
   if (rank == 0) {
+    std::vector<std::vector<Piece>> per(static_cast<size_t>(p));
     int64_t stage_bytes = 0;
-    for (const RankPlan& pl : plan) stage_bytes = std::max(stage_bytes, pl.block);
-    char* stage[2] = {bufs.h(stage_bytes + 16), bufs.h(stage_bytes + 16)};
-    char* d_stage[2] = {bufs.d<char>(stage_bytes + 16), bufs.d<char>(stage_bytes + 16)};
-    int done[2] = {-1, -1};  // comm-lane mark after the last use of stage s
-    // ranks in order 1..p-1, then the root's own slice (uploaded straight into its block)
-    std::vector<int> order;
-    for (int r = 1; r < p; ++r) order.push_back(r);
-    order.push_back(0);
-    for (size_t k = 0; k < order.size(); ++k) {
-      const int r = order[k];
-      const RankPlan& pl = plan[r];
-      if (pl.block == 0) continue;
-      const int s = static_cast<int>(k & 1);
-      if (done[s] >= 0) dc.wait_mark(done[s]);  // slice k-2 has left stage s: it may be rewritten
-      pack_block(*rb, pl, stage[s]);          // while slice k-1 uploads / sends
-      char* dst = r == 0 ? d_block : d_stage[s];
-      dc.wait_upload(dc.upload(dst, stage[s], pl.block));
-      if (r != 0) {
-        send_block(dc, dst, pl.block, r);
-        out.scattered_bytes += pl.block;
-      }
-      done[s] = dc.mark();
+    size_t rounds = 0;
+    for (int r = 0; r < p; ++r) {
+      per[r] = pieces_of(plan[r], r, chunk);
+      rounds = std::max(rounds, per[r].size());
+      for (const Piece& pc : per[r]) stage_bytes = std::max(stage_bytes, pc.b1 - pc.b0);
     }
-  } else if (mine.block > 0) {
-    recv_block(dc, d_block, mine.block, 0);
+    constexpr int kSlots = 3;
+    char* stage[kSlots];
+    char* d_stage[kSlots];
+    int up[kSlots], sent[kSlots];
+    for (int q = 0; q < kSlots; ++q) {
+      stage[q] = bufs.h(stage_bytes + 64);
+      d_stage[q] = p > 1 ? bufs.d<char>(stage_bytes + 64) : nullptr;
+      up[q] = sent[q] = -1;
+    }
+    int64_t i = 0;
+    for (size_t k = 0; k < rounds; ++k)
+      for (int step = 1; step <= p; ++step) {
+        const int r = step % p;  // peers 1..p-1, then the root
+        if (k >= per[r].size()) continue;
+        const Piece& pc = per[r][k];
+        const int q = static_cast<int>(i++ % kSlots);
+        if (up[q] >= 0) dc.wait_upload_host(up[q]);  // the staging's previous piece has left the host
+        pack_piece(*rb, plan[r], pc, stage[q]);
+        const int64_t len = pc.b1 - pc.b0;
+        if (r == 0) {
+          up[q] = dc.upload_after(d_block + pc.b0, stage[q], len, -1);
+          dc.wait_upload(up[q]);
+          continue;
+        }
+        up[q] = dc.upload_after(d_stage[q], stage[q], len, sent[q]);  // after that buffer's last send
+        dc.wait_upload(up[q]);
+        dc.group_start();
+        dc.send(d_stage[q], len, r);
+        dc.group_end();
+        sent[q] = dc.mark();
+        out.scattered_bytes += len;
+      }
+  } else {
+    for (const Piece& pc : pieces_of(mine, rank, chunk)) {  // the root's order of this rank's pieces
+      dc.group_start();
+      dc.recv(d_block + pc.b0, pc.b1 - pc.b0, 0);
+      dc.group_end();
+    }
   }
   dc.sync();
   hooks.end();

@@ -464,3 +464,21 @@ def test_streaming_short_input_and_bad_record():
                   np_=3)
     assert r.returncode == 1 and b"record #2 contains a non-letter" in r.stderr
     assert r.stdout.decode().count("\n") == 2
+
+
+@pytest.mark.parametrize("np_", [2, 3, 8])
+def test_rccl_driver_emulated_many_pieces(np_, tmp_path):
+    # the root's piece pipeline (device_batch.cpp): every rank's block cut into 2640-byte pieces (P33 blocks,
+    # 5-bit groups and offsets never straddle two), interleaved round-robin with the root's own, three
+    # staging slots reused — narrow form (input6 shape) and dense form (input3 shape: records over 255)
+    from mpi_openmp_cuda_amd import format_results, search_cpu
+    from mpi_openmp_cuda_amd.utils.synthetic import make_synthetic
+
+    for shape, n in (("input6", 20_000), ("input3", 300)):
+        prob = make_synthetic(shape, n, seed=17)
+        path = tmp_path / f"{shape}.txt"
+        path.write_text(prob.to_text())
+        r = run_final(["--backend=cpu", "--transport=rccl-emul", f"--input={path}"], stdin_bytes=b"", np_=np_,
+                      env={"MOC_SEND_CHUNK": "5000"}, timeout=300)
+        assert r.returncode == 0, r.stderr.decode()
+        assert r.stdout.decode() == format_results(search_cpu(prob)), shape
