@@ -488,7 +488,12 @@ void launch_swipe(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStr
   const int fb = result_bytes(static_cast<ResultFormat>(a.fmt));
   const SwipeLayout lay = swipe_layout(pv.L1, noff, l2w, a.tile_records, a.codes_cap, fb, letter_form(a));
   const int per_cu = std::max(1, std::min(8, 160 * 1024 / std::max(lay.total, 1)));
-  const int64_t slots = static_cast<int64_t>(num_cus) * per_cu;
+  // MOC_SWIPE_SLOTS (test hook): a smaller persistent grid, so modest batches reach the tail-tile region
+  static const int64_t slots_override = [] {
+    const char* v = std::getenv("MOC_SWIPE_SLOTS");
+    return v ? std::max<int64_t>(1, std::atoll(v)) : int64_t{0};
+  }();
+  const int64_t slots = slots_override ? slots_override : static_cast<int64_t>(num_cus) * per_cu;
   ShortArgs b = a;
   // the last `slots` tiles' records go in quarter tiles (MOC_SWIPE_TAIL): the tail of the persistent grid
   // (blocks idling while the last tiles finish) shrinks 4x

@@ -832,3 +832,41 @@ def test_final_narrow_guess_fails_stdin_two_ranks(mode):
     r = run_final(["--backend=hip", "--device=0"] + extra, stdin_bytes=prob.to_text().encode(), np_=2)
     assert r.returncode == 0, r.stderr.decode()
     assert r.stdout.decode() == format_results(search_cpu(prob))
+
+
+@pytest.mark.parametrize("tail", ["4", "8", "0"])
+def test_swipe_tail_tiles_every_record(tail):
+    # the persistent grid's tail tiles (the last `slots` tiles cut to 1/4 or 1/8) only
+    # start beyond 2 * slots tiles — millions of records at full size. A small grid (MOC_SWIPE_SLOTS) and
+    # 256-record tiles reach them with 60 K records; every result, head to tail, against the CPU engine.
+    import os
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+
+    code = r"""
+import numpy as np, sys
+sys.path.insert(0, %r)
+from mpi_openmp_cuda_amd import HipSearchEngine, search_cpu
+from mpi_openmp_cuda_amd._lib import Pinned
+from mpi_openmp_cuda_amd.ops.align import as_triples
+from mpi_openmp_cuda_amd.parallel.wire import WireSlice
+from mpi_openmp_cuda_amd.utils.synthetic import make_synthetic
+prob = make_synthetic("input6", 60_003, seed=23)
+eng = HipSearchEngine(device=0)
+eng.set_problem(prob.weights, prob.seq1)
+ws = WireSlice.from_csr(prob.codes, prob.offsets)
+ws.alloc_results(eng)
+with Pinned(*ws.arrays()):
+    for _ in range(2):
+        ws.results[:] = 0x7777
+        ws.solve(eng)
+        assert eng.stats()["direct"] == 1 and eng.stats()["kernels"] == ["swipe"], eng.stats()
+        assert np.array_equal(ws.triples(eng), as_triples(search_cpu(prob)))
+print("ok")
+""" % ROOT
+    # tail tiles need tiles of a multiple of 64 * divisor records
+    env = dict(os.environ, MOC_SWIPE_TILE="512" if tail == "8" else "256", MOC_SWIPE_SLOTS="16", MOC_SWIPE_TAIL=tail)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, timeout=300, env=env)
+    assert r.returncode == 0 and b"ok" in r.stdout, r.stderr.decode()[-3000:]
