@@ -112,10 +112,13 @@ void run_sliced(JobCore& job, BulkParser& parser, int64_t first_index, SharedWin
         len16 = HostRegion(2 * static_cast<size_t>(n), numa);
         rep = parser.fill_slice(slice, nullptr, letters.as<uint8_t>(), nullptr, sparse.as<int64_t>(),
                                 len16.as<uint16_t>(), pack);
-        // the engine's answer for the lengths seen (waits for its start-up): a wrong guess re-encodes the
-        // slice as 5-bit letters + CSR offsets NOW, while the input text is still mapped — every rank
-        // releases its share of the node-shared text after the report exchange below
-        if (!(rep.max_len <= 255 && eng.hip->streams_packed(rep.min_len, rep.max_len))) {
+        // the engine's answer for the lengths seen (waits for its start-up, its own phase): a wrong guess
+        // re-encodes the slice as 5-bit letters + CSR offsets NOW, while the input text is still mapped —
+        // every rank releases its share of the node-shared text after the report exchange below
+        pt.begin("engine_wait");
+        const bool streams = rep.max_len <= 255 && eng.hip->streams_packed(rep.min_len, rep.max_len);
+        pt.begin("fill");
+        if (!streams) {
           narrow = false;
           sparse = HostRegion();
           len16 = HostRegion();

@@ -323,7 +323,7 @@ class StreamFlow {
   int64_t runs_first_[2] = {0, 0};
   std::string error_;
   std::vector<double> kernel_ms_;  // per batch (this rank)
-  double overlap_ms_ = 0;          // host work done while a kernel was in flight
+  double hidden_ms_ = 0;           // kernel time the host spent on other work (not waiting for it)
 };
 
 void StreamFlow::ensure(RingBuf& b, int64_t bytes, bool pin) {
@@ -484,7 +484,9 @@ bool StreamFlow::fill(const BatchMsg& m, const std::vector<int64_t>& table, int 
       ensure(in.len16, 2 * n, false);
       rep = bp.fill_slice(slice, nullptr, in.letters.as<uint8_t>(), nullptr, in.sparse.as<int64_t>(),
                           in.len16.as<uint16_t>(), pack);
+      j_.pt.begin("engine_wait");  // the first batch: the engine's start-up, overlapped with the encode
       if (!(rep.max_len <= 255 && gpu_->streams_packed(rep.min_len, rep.max_len))) narrow = false;
+      j_.pt.begin("fill");
     }
     if (!narrow) {  // 5-bit letters + CSR offsets (the staged pipeline's form)
       ensure(in.letters, packed5_bytes(slice.letters) + 16, true);
@@ -588,6 +590,7 @@ void StreamFlow::finish(int s, Done& d) {
     gs = gpu_->finish_wire();
     sw.stop();
     j_.compute_ms += sw.total_ms();
+    hidden_ms_ += std::max(0.0, gs.kernel_ms - sw.total_ms());
     j_.eng.kernel_ms += gs.kernel_ms;
     j_.h2d_bytes += gs.h2d_bytes;
     j_.d2h_bytes += gs.d2h_bytes;
@@ -653,13 +656,7 @@ int StreamFlow::run() {
     const int s = b & 1;
     BatchMsg m = next_batch(table);
     bool ok = m.status == 0;
-    if (ok && m.n > 0) {
-      Stopwatch ov;
-      ov.start();
-      ok = fill(m, table, s, done[s]);  // overlaps the kernel of batch b-1
-      ov.stop();
-      if (have_prev) overlap_ms_ += ov.total_ms();
-    }
+    if (ok && m.n > 0) ok = fill(m, table, s, done[s]);  // while the kernel of batch b-1 streams
     if (have_prev) {  // F + E of batch b-1 (also before leaving on an input error of batch b)
       finish(s ^ 1, done[s ^ 1]);
       if (ok && m.n > 0) launch(s, done[s]);
@@ -692,8 +689,8 @@ int StreamFlow::run() {
   }
   {
     char buf[64];
-    std::snprintf(buf, sizeof buf, "%.3f", overlap_ms_);
-    j_.extra_timing.emplace_back("rank0_fill_overlapped_ms", buf);
+    std::snprintf(buf, sizeof buf, "%.3f", hidden_ms_);
+    j_.extra_timing.emplace_back("rank0_kernel_hidden_ms", buf);
   }
   return rc;
 }

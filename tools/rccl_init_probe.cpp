@@ -5,6 +5,10 @@
 //   --busy=T   a team of T OpenMP threads computes on other threads during the whole start-up (what the
 //              parse does in ./final when the connect overlaps it); --passive: the team sleeps between
 //              bursts instead of spinning (OMP_WAIT_POLICY-like behaviour, simulated).
+//   --dlopen-first   load librccl before the HIP runtime starts (as ./final's plugin does)
+//   --warm           a 1-rank communicator on a helper thread first (what ./final can start before MPI is
+//                    up), then the timed one
+//   --teardown=destroy|abort|none   how the communicators end
 // Build (here): hipcc -O2 -std=c++17 -fopenmp tools/rccl_init_probe.cpp -ldl -o build/rccl_init_probe
 // Run (box):    build/rccl_init_probe [--busy=16]
 #include <dlfcn.h>
@@ -39,10 +43,14 @@ F sym(void* h, const char* name) {
 
 int main(int argc, char** argv) {
   int busy = 0;
-  bool passive = false;
+  bool passive = false, dlopen_first = false, warm = false;
+  std::string teardown = "destroy";
   for (int i = 1; i < argc; ++i) {
     if (std::strncmp(argv[i], "--busy=", 7) == 0) busy = std::atoi(argv[i] + 7);
     if (std::strcmp(argv[i], "--passive") == 0) passive = true;
+    if (std::strcmp(argv[i], "--dlopen-first") == 0) dlopen_first = true;
+    if (std::strcmp(argv[i], "--warm") == 0) warm = true;
+    if (std::strncmp(argv[i], "--teardown=", 11) == 0) teardown = argv[i] + 11;
   }
   std::atomic<bool> stop{false};
   std::atomic<long> bursts{0};
@@ -72,6 +80,11 @@ int main(int argc, char** argv) {
     std::fflush(stdout);
     t = n;
   };
+  void* h = nullptr;
+  if (dlopen_first) {
+    h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    lap("dlopen librccl.so.1 (before HIP)");
+  }
   int ndev = 0;
   (void)hipGetDeviceCount(&ndev);
   lap("hipGetDeviceCount (HIP runtime)");
@@ -79,17 +92,30 @@ int main(int argc, char** argv) {
   void* p = nullptr;
   (void)hipMalloc(&p, 256);
   lap("hipSetDevice + hipMalloc (context)");
-  void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+  if (!h) {
+    h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    lap("dlopen librccl.so.1");
+  }
   if (!h) {
     std::fprintf(stderr, "dlopen librccl: %s\n", dlerror());
     return 2;
   }
-  lap("dlopen librccl.so.1");
   auto get_id = sym<ncclResult_t (*)(ncclUniqueId*)>(h, "ncclGetUniqueId");
   auto init = sym<ncclResult_t (*)(ncclComm_t*, int, ncclUniqueId, int)>(h, "ncclCommInitRank");
   auto allreduce = sym<ncclResult_t (*)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                                         hipStream_t)>(h, "ncclAllReduce");
   auto destroy = sym<ncclResult_t (*)(ncclComm_t)>(h, "ncclCommDestroy");
+  auto abort_fn = sym<ncclResult_t (*)(ncclComm_t)>(h, "ncclCommAbort");
+  ncclComm_t warm_comm = nullptr;
+  if (warm) {  // a helper thread's throw-away communicator: the library's one-time loading happens there
+    std::thread t([&] {
+      (void)hipSetDevice(0);
+      ncclUniqueId wid;
+      if (get_id(&wid) == ncclSuccess) (void)init(&warm_comm, 1, wid, 0);
+    });
+    t.join();
+    lap("warm-up communicator (helper thread)");
+  }
   ncclUniqueId id;
   if (get_id(&id) != ncclSuccess) return 3;
   lap("ncclGetUniqueId");
@@ -111,9 +137,21 @@ int main(int argc, char** argv) {
   ncclComm_t comm2 = nullptr;
   if (init(&comm2, 1, id2, 0) != ncclSuccess) return 4;
   lap("getId + ncclCommInitRank (2nd)");
-  (void)destroy(comm2);
-  (void)destroy(comm);
-  lap("ncclCommDestroy x2");
+  if (warm_comm) {
+    if (teardown == "abort") (void)abort_fn(warm_comm);
+    else if (teardown == "destroy") (void)destroy(warm_comm);
+  }
+  if (teardown == "abort") {
+    (void)abort_fn(comm2);
+    (void)abort_fn(comm);
+    lap("ncclCommAbort x2");
+  } else if (teardown == "destroy") {
+    (void)destroy(comm2);
+    (void)destroy(comm);
+    lap("ncclCommDestroy x2");
+  } else {
+    lap("communicators left to process exit");
+  }
   std::printf("%-34s %9.1f ms  (busy=%d%s, %ld bursts)\n", "TOTAL", now_ms() - t_start, busy,
               passive ? " passive" : "", bursts.load());
   stop = true;
