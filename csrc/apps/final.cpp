@@ -467,17 +467,43 @@ int Job::run() {
 
 }  // namespace
 
-// An --input file of >= --gpu-prewarm-bytes will run on the GPU (unless --backend=cpu): the HIP runtime
-// starts on a helper thread before MPI_Init, every rank deciding from the same flags and file.
+// Start-up work for a helper thread, decided before MPI_Init from the same flags and environment on every
+// rank:
+//   * an --input file of >= --gpu-prewarm-bytes will run on the GPU (unless --backend=cpu): the HIP runtime
+//     starts;
+//   * a job that will use RCCL (--transport=rccl, --collectives=rccl, or the auto transport across nodes)
+//     also pays RCCL's one-time start-up there — 1.7 s of library registration and code-object loading,
+//     profiles/rccl_init_rootcause.log — on the rank's device (node-local rank from the launcher's
+//     environment), so the communicator set-up after the header broadcast takes ~60 ms.
+int env_int(const char* name, int fallback) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoi(v) : fallback;
+}
+
 std::future<void> early_prewarm(int argc, char** argv) {
   try {
     Flags flags(argc, argv);
+    if (to_lower(flags.get("backend", "auto")) == "cpu" || flags.get_bool("help", false)) return {};
+    const std::string tr = to_lower(flags.get("transport", "auto"));
+    // MPICH's hydra exports the node-local rank and size, Open MPI its own names
+    const int local = env_int("MPI_LOCALRANKID", env_int("OMPI_COMM_WORLD_LOCAL_RANK", 0));
+    const int local_n = env_int("MPI_LOCALNRANKS", env_int("OMPI_COMM_WORLD_LOCAL_SIZE", 1));
+    const int world = env_int("PMI_SIZE", env_int("OMPI_COMM_WORLD_SIZE", 1));
+    const bool rccl = tr == "rccl" || to_lower(flags.get("collectives", "auto")) == "rccl" ||
+                      (tr == "auto" && world > local_n);
     const std::string path = flags.get("input", "");
-    if (path.empty() || to_lower(flags.get("backend", "auto")) == "cpu" || flags.get_bool("help", false)) return {};
     struct stat st {};
     const int64_t min_bytes = flags.get_int("gpu-prewarm-bytes", int64_t{64} << 20);
-    if (stat(path.c_str(), &st) != 0 || !S_ISREG(st.st_mode) || min_bytes <= 0 || st.st_size < min_bytes) return {};
-    return std::async(std::launch::async, [] { (void)gpu_device_count(); });
+    const bool big = !path.empty() && stat(path.c_str(), &st) == 0 && S_ISREG(st.st_mode) && min_bytes > 0 &&
+                     st.st_size >= min_bytes;
+    if (!big && !rccl) return {};
+    int device = static_cast<int>(flags.get_int("device", -1));
+    const std::vector<int> map = parse_int_list(flags.get("device-map", ""));
+    if (device < 0 && !map.empty()) device = map[static_cast<size_t>(local) % map.size()];
+    return std::async(std::launch::async, [rccl, device, local] {
+      const int n = gpu_device_count();
+      if (rccl && n > 0) (void)gpu_rccl_warmup(device >= 0 ? device : local % n);
+    });
   } catch (const std::exception&) {
     return {};  // bad flags are reported after MPI_Init
   }

@@ -399,11 +399,13 @@ void BatchFlow::batch_rccl(RecordBatch* rb, int64_t n, int64_t total_chars, cons
   };
   hooks.end = [this] { j_.pt.end(); };
   DeviceBatchOut out;
+  DeviceComm& dc = j_.emul_comm ? static_cast<DeviceComm&>(*j_.emul_comm) : j_.eng.hip->device_comm();
+  if (!j_.scratch) j_.scratch = std::make_unique<DeviceScratch>(dc);
   if (j_.emul_comm) {
     CpuDeviceSearch ds(j_.eng.table, j_.eng.seq1, j_.eng.sem, j_.eng.threads);
-    out = device_batch(*j_.emul_comm, ds, rb, n, total_chars, bounds, cp, hooks);
+    out = device_batch(dc, ds, rb, n, total_chars, bounds, cp, hooks, j_.scratch.get());
   } else {
-    out = device_batch(j_.eng.hip->device_comm(), j_.eng.hip->device_search(), rb, n, total_chars, bounds, cp, hooks);
+    out = device_batch(dc, j_.eng.hip->device_search(), rb, n, total_chars, bounds, cp, hooks, j_.scratch.get());
   }
   j_.compute_ms += out.compute_ms;
   j_.eng.kernel_ms += out.kernel_ms;

@@ -64,6 +64,8 @@ std::vector<int> parse_int_list(const std::string& s);
 // The GPU plugin (moc/gpu_rank.hpp), loaded on the first question about GPUs.
 int gpu_device_count();
 std::string gpu_plugin_error();
+// RCCL's one-time start-up (library load + code objects) on `device`, for a helper thread (false: none).
+bool gpu_rccl_warmup(int device);
 GpuRank* gpu_rank_create(const MpiContext& ctx, const GpuRankOptions& opt);
 
 // The selected engine of this rank over contiguous host slices.
@@ -96,6 +98,7 @@ struct JobCore {
   bool pin_window = true;
   bool coll_rccl = false;  // shm transport: host-table collectives over RCCL (--collectives=rccl)
   std::unique_ptr<MpiDeviceComm> emul_comm;  // --transport=rccl-emul
+  std::unique_ptr<DeviceScratch> scratch;    // rccl(-emul) batches: device / page-locked buffers kept across batches
   PhaseTimer pt;
   Stopwatch total;
   FILE* out = stdout;  // root: --output file, else stdout

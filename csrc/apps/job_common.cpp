@@ -36,6 +36,7 @@ namespace {
 struct GpuPlugin {
   GpuDeviceCountFn device_count = nullptr;
   GpuRankCreateFn create = nullptr;
+  GpuRcclWarmupFn rccl_warmup = nullptr;
   std::string error;
 };
 
@@ -64,6 +65,7 @@ const GpuPlugin& gpu_plugin() {
     }
     g.device_count = reinterpret_cast<GpuDeviceCountFn>(dlsym(h, kGpuDeviceCountSym));
     g.create = reinterpret_cast<GpuRankCreateFn>(dlsym(h, kGpuRankCreateSym));
+    g.rccl_warmup = reinterpret_cast<GpuRcclWarmupFn>(dlsym(h, kGpuRcclWarmupSym));
     if (!g.device_count || !g.create) g.error = "GPU plugin " + path + " lacks its entry points";
     return g;
   }();
@@ -76,6 +78,10 @@ int gpu_device_count() {
   return g.device_count && g.create ? g.device_count() : 0;
 }
 std::string gpu_plugin_error() { return gpu_plugin().error; }
+bool gpu_rccl_warmup(int device) {
+  const GpuPlugin& g = gpu_plugin();
+  return g.rccl_warmup && g.rccl_warmup(device) == 0;
+}
 GpuRank* gpu_rank_create(const MpiContext& ctx, const GpuRankOptions& opt) { return gpu_plugin().create(ctx, opt); }
 
 // ---- RankEngine

@@ -83,10 +83,33 @@ class DeviceSearch {
   virtual R2Params last_r2() const = 0;
 };
 
-// What one device batch produced: on the root, every rank's results in its own format (host memory).
+// Device and page-locked host buffers of the batch driver, kept across batches (a streaming job allocates
+// and page-locks them once): numbered slots that only grow. Every batch ends with the comm lane drained,
+// so a slot is free again when the next batch asks for it.
+class DeviceScratch {
+ public:
+  explicit DeviceScratch(DeviceComm& dc) : dc_(dc) {}
+  ~DeviceScratch();
+  DeviceScratch(const DeviceScratch&) = delete;
+  DeviceScratch& operator=(const DeviceScratch&) = delete;
+  char* dev(int slot, int64_t bytes) { return get(dev_, slot, bytes, false); }
+  char* host(int slot, int64_t bytes) { return get(host_, slot, bytes, true); }
+
+ private:
+  struct Buf {
+    void* p = nullptr;
+    int64_t cap = 0;
+  };
+  char* get(std::vector<Buf>& v, int slot, int64_t bytes, bool host);
+  DeviceComm& dc_;
+  std::vector<Buf> dev_, host_;
+};
+
+// What one device batch produced: on the root, every rank's results in its own format (host memory of the
+// scratch, valid until the next batch).
 struct DeviceBatchOut {
   std::vector<ResultRun> runs;
-  std::vector<std::vector<char>> storage;  // backing memory of runs
+  std::vector<std::vector<char>> storage;  // backing memory of runs (the context-parallel path)
   double compute_ms = 0, kernel_ms = 0;    // this rank
   int64_t scattered_bytes = 0;             // root: device bytes sent to the other ranks
   std::vector<int64_t> rank_records;       // every rank's records (root)
@@ -101,7 +124,9 @@ struct DeviceBatchOut {
 // Context parallel (cp = true): the batch is broadcast, each rank searches its share of every record's
 // offsets, the packed keys are MAX-all-reduced, the root decodes them.
 // `rb` (bytes + offsets from 0) and `bounds` (p+1 record bounds) are read on the root only.
+// `scratch` (optional): buffers kept across the caller's batches.
 DeviceBatchOut device_batch(DeviceComm& dc, DeviceSearch& ds, const RecordBatch* rb, int64_t n, int64_t total_chars,
-                            const std::vector<int64_t>& bounds, bool cp, const PhaseHooks& hooks);
+                            const std::vector<int64_t>& bounds, bool cp, const PhaseHooks& hooks,
+                            DeviceScratch* scratch = nullptr);
 
 }  // namespace moc

@@ -79,7 +79,10 @@ class GpuRank {
 // Plugin entry points (extern "C", resolved with dlsym).
 using GpuDeviceCountFn = int (*)();
 using GpuRankCreateFn = GpuRank* (*)(const MpiContext& ctx, const GpuRankOptions& opt);
+// RCCL's one-time start-up on `device` (moc::rccl_warmup), for a helper thread before MPI starts; 0 = ok.
+using GpuRcclWarmupFn = int (*)(int device);
 constexpr const char* kGpuDeviceCountSym = "moc_final_gpu_device_count";
 constexpr const char* kGpuRankCreateSym = "moc_final_gpu_create";
+constexpr const char* kGpuRcclWarmupSym = "moc_final_gpu_rccl_warmup";
 
 }  // namespace moc

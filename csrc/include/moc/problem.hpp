@@ -11,6 +11,8 @@
 #include <memory>
 #include <vector>
 
+#include <sys/mman.h>
+
 #include "moc/common.hpp"
 
 namespace moc {
@@ -33,6 +35,29 @@ struct DefaultInitAllocator : std::allocator<T> {
   template <typename U, typename... Args>
   void construct(U* p, Args&&... args) {
     ::new (static_cast<void*>(p)) U(std::forward<Args>(args)...);
+  }
+  // Large arrays (>= 32 MiB: a parsed batch's letters and offsets, input text) are their own mappings,
+  // advised for 2 MiB pages: 512x fewer first-touch faults than malloc's 4 KiB ones (a 2.2 GB parse of
+  // 1.14 G letters spent most of its time faulting pages in).
+  static constexpr size_t kMapBytes = size_t{32} << 20;
+  T* allocate(size_t n) {
+    const size_t bytes = n * sizeof(T);
+    if (bytes < kMapBytes) return std::allocator<T>::allocate(n);
+    void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    if (p == MAP_FAILED) throw std::bad_alloc();
+    const uintptr_t huge = uintptr_t{2} << 20;
+    const uintptr_t lo = (reinterpret_cast<uintptr_t>(p) + huge - 1) & ~(huge - 1);
+    const uintptr_t hi = (reinterpret_cast<uintptr_t>(p) + bytes) & ~(huge - 1);
+    if (hi > lo) (void)madvise(reinterpret_cast<void*>(lo), hi - lo, MADV_HUGEPAGE);
+    return static_cast<T*>(p);
+  }
+  void deallocate(T* p, size_t n) {
+    const size_t bytes = n * sizeof(T);
+    if (bytes < kMapBytes) {
+      std::allocator<T>::deallocate(p, n);
+      return;
+    }
+    munmap(p, bytes);
   }
 };
 template <typename T>

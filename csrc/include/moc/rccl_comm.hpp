@@ -38,10 +38,21 @@ class RcclComm {
   void allreduce_max_u64(void* dbuf, int64_t n, hipStream_t s);
   void check_async() const;  // ncclCommGetAsyncError -> throw
   ncclComm_t comm() const { return comm_; }
+  // A communicator that lives until the process ends (the `final` CLI's): its destructor leaves it to the
+  // process exit instead of ncclCommDestroy, which costs ~0.45 s per communicator on the MI355X box
+  // (profiles/rccl_init_variants.log). MOC_RCCL_DESTROY=1 destroys it anyway.
+  void keep_until_exit() { keep_ = true; }
 
  private:
   const MpiContext& ctx_;
   ncclComm_t comm_ = nullptr;
+  bool keep_ = false;
 };
+
+// A one-rank communicator on `device`, created and kept until the process ends: RCCL's one-time cost —
+// registering librccl's 569 MB fat binary, loading its 108 MB gfx950 code object — is paid here, on a
+// helper thread that can start before MPI does (profiles/rccl_init_rootcause.log); later communicators of
+// the process then start in ~60 ms. Returns false when RCCL cannot start.
+bool rccl_warmup(int device);
 
 }  // namespace moc

@@ -3,6 +3,8 @@
 #include <unistd.h>
 
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <exception>
 #include <string>
 
@@ -45,7 +47,27 @@ RcclComm::~RcclComm() {
     if (comm_) ncclCommAbort(comm_);
     return;
   }
+  const char* d = std::getenv("MOC_RCCL_DESTROY");
+  if (keep_ && !(d && std::strcmp(d, "1") == 0)) return;  // the process exit releases it
   if (comm_) ncclCommDestroy(comm_);
+}
+
+bool rccl_warmup(int device) {
+  static ncclComm_t warm = nullptr;  // kept: destroying it would cost as much as it saves
+  if (warm) return true;
+  if (hipSetDevice(device) != hipSuccess) return false;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return false;
+  // RCCL prints a version banner on stdout during init; stdout carries results only (main.c:204)
+  std::fflush(stdout);
+  const int saved = dup(1);
+  dup2(2, 1);
+  const ncclResult_t rc = ncclCommInitRank(&warm, 1, id, 0);
+  std::fflush(stdout);
+  dup2(saved, 1);
+  close(saved);
+  if (rc != ncclSuccess) warm = nullptr;
+  return rc == ncclSuccess;
 }
 
 void RcclComm::check_async() const {

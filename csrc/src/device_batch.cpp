@@ -181,11 +181,44 @@ DeviceBatchOut batch_cp(DeviceComm& dc, DeviceSearch& ds, const RecordBatch* rb,
 
 }  // namespace
 
+DeviceScratch::~DeviceScratch() {
+  for (Buf& b : dev_)
+    if (b.p) dc_.dev_free(b.p);
+  for (Buf& b : host_)
+    if (b.p) dc_.host_free(b.p);
+}
+
+char* DeviceScratch::get(std::vector<Buf>& v, int slot, int64_t bytes, bool host) {
+  if (static_cast<size_t>(slot) >= v.size()) v.resize(static_cast<size_t>(slot) + 1);
+  Buf& b = v[static_cast<size_t>(slot)];
+  bytes = std::max<int64_t>(bytes, 64);
+  if (bytes > b.cap) {
+    if (b.p) host ? dc_.host_free(b.p) : dc_.dev_free(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+    const int64_t cap = bytes + bytes / 8;
+    b.p = host ? dc_.host_alloc(cap) : dc_.dev_alloc(cap);
+    b.cap = cap;
+  }
+  return static_cast<char*>(b.p);
+}
+
+namespace {
+enum Slot { kPlanBuf, kBlock, kOut, kR2, kMineR2, kGather, kStage0, kStageEnd = kStage0 + 3, kHostResults = 0,
+            kHostStage0 = 1 };
+}  // namespace
+
 DeviceBatchOut device_batch(DeviceComm& dc, DeviceSearch& ds, const RecordBatch* rb, int64_t n, int64_t total_chars,
-                            const std::vector<int64_t>& bounds, bool cp, const PhaseHooks& hooks) {
+                            const std::vector<int64_t>& bounds, bool cp, const PhaseHooks& hooks,
+                            DeviceScratch* scratch) {
   if (cp) return batch_cp(dc, ds, rb, n, total_chars, hooks);
+  std::unique_ptr<DeviceScratch> own;
+  if (!scratch) {
+    own = std::make_unique<DeviceScratch>(dc);
+    scratch = own.get();
+  }
+  DeviceScratch& sc = *scratch;
   DeviceBatchOut out;
-  DevBufs bufs(dc);
   const int rank = dc.rank(), p = dc.size();
 
   // ---- plan (root) -> every rank, through the device layer
@@ -214,13 +247,13 @@ DeviceBatchOut device_batch(DeviceComm& dc, DeviceSearch& ds, const RecordBatch*
   }
   {
     const int64_t bytes = static_cast<int64_t>(sizeof(RankPlan)) * p;
-    char* d_plan = bufs.d<char>(bytes);
+    char* d_plan = sc.dev(kPlanBuf, bytes);
     if (rank == 0) dc.wait_upload(dc.upload(d_plan, plan.data(), bytes));
     dc.bcast(d_plan, bytes, 0);
     dc.download(plan.data(), d_plan, bytes);
   }
   const RankPlan& mine = plan[rank];
-  char* d_block = bufs.d<char>(mine.block + 16);
+  char* d_block = sc.dev(kBlock, mine.block + 16);
 
   // ---- root: pack piece i+1 (host threads) | upload piece i (copy lane) | send piece i-1 (comm lane).
   // Pieces go round-robin over the ranks (the root's own, uploaded straight into its block, among them), so
@@ -240,10 +273,11 @@ DeviceBatchOut device_batch(DeviceComm& dc, DeviceSearch& ds, const RecordBatch*
     char* d_stage[kSlots];
     int up[kSlots], sent[kSlots];
     for (int q = 0; q < kSlots; ++q) {
-      stage[q] = bufs.h(stage_bytes + 64);
-      d_stage[q] = p > 1 ? bufs.d<char>(stage_bytes + 64) : nullptr;
+      stage[q] = sc.host(kHostStage0 + q, stage_bytes + 64);
+      d_stage[q] = p > 1 ? sc.dev(kStage0 + q, stage_bytes + 64) : nullptr;
       up[q] = sent[q] = -1;
     }
+    hooks.begin("pack");  // host packing, and the waits for staging slots (a packing-bound distribution)
     int64_t i = 0;
     for (size_t k = 0; k < rounds; ++k)
       for (int step = 1; step <= p; ++step) {
@@ -267,6 +301,7 @@ DeviceBatchOut device_batch(DeviceComm& dc, DeviceSearch& ds, const RecordBatch*
         sent[q] = dc.mark();
         out.scattered_bytes += len;
       }
+    hooks.begin("distribute");
   } else {
     for (const Piece& pc : pieces_of(mine, rank, chunk)) {  // the root's order of this rank's pieces
       dc.group_start();
@@ -283,7 +318,7 @@ DeviceBatchOut device_batch(DeviceComm& dc, DeviceSearch& ds, const RecordBatch*
   sw.start();
   const ResultFormat fmt = static_cast<ResultFormat>(mine.fmt);
   const int fb = result_bytes(fmt);
-  char* d_out = bufs.d<char>(fb * mine.n + 16);
+  char* d_out = sc.dev(kOut, fb * mine.n + 16);
   if (mine.n > 0) ds.solve(device_view(mine, d_block), d_out, fmt);
   dc.sync();
   sw.stop();
@@ -297,11 +332,11 @@ DeviceBatchOut device_batch(DeviceComm& dc, DeviceSearch& ds, const RecordBatch*
   std::vector<int64_t> rstart(static_cast<size_t>(p) + 1, 0);
   for (int r = 0; r < p; ++r) rstart[r + 1] = rstart[r] + al16(result_bytes(static_cast<ResultFormat>(plan[r].fmt)) * plan[r].n);
   std::vector<int64_t> r2v(static_cast<size_t>(3 * p), 0);
-  char* d_r2 = bufs.d<char>(24 * p);
+  char* d_r2 = sc.dev(kR2, 24 * p);
   {
     const int64_t mine_r2[3] = {r2.smin, r2.kw, r2.j};
     // every rank's parameters land at its slot of the root's table
-    char* d_mine_r2 = bufs.d<char>(24);
+    char* d_mine_r2 = sc.dev(kMineR2, 24);
     dc.wait_upload(dc.upload(d_mine_r2, mine_r2, 24));
     dc.group_start();
     if (rank == 0) {
@@ -316,7 +351,7 @@ DeviceBatchOut device_batch(DeviceComm& dc, DeviceSearch& ds, const RecordBatch*
       r2v[2] = r2.j;
     }
   }
-  char* d_gather = rank == 0 ? bufs.d<char>(rstart[p] + 16) : nullptr;
+  char* d_gather = rank == 0 ? sc.dev(kGather, rstart[p] + 16) : nullptr;
   dc.group_start();
   if (rank == 0) {
     for (int r = 1; r < p; ++r) {
@@ -328,8 +363,7 @@ DeviceBatchOut device_batch(DeviceComm& dc, DeviceSearch& ds, const RecordBatch*
   }
   dc.group_end();
   if (rank == 0) {
-    out.storage.emplace_back(static_cast<size_t>(rstart[p] + 16));
-    char* h = out.storage.back().data();
+    char* h = sc.host(kHostResults, rstart[p] + 16);  // page-locked: the downloads are plain DMA
     if (p > 1) dc.download(r2v.data() + 3, d_r2 + 24, 24 * (p - 1));
     if (fb * mine.n > 0) dc.download(h, d_out, fb * mine.n);
     if (rstart[p] > rstart[1]) dc.download(h + rstart[1], d_gather + rstart[1], rstart[p] - rstart[1]);

@@ -56,6 +56,12 @@ int main(int argc, char** argv) {
     p.fill_slice(s, codes.data(), nullptr, offs.data());
     const double ms = ms_since(t0);
     std::printf("fill bytes+offsets ms=%.1f GB/s=%.1f\n", ms, gb / (ms / 1e3));
+    // the rccl transport's root packs byte codes into P33 per rank piece (pack33: whole blocks in parallel)
+    const auto t1 = now();
+    moc::pack33(codes.data(), s.letters, out.data());
+    const double ms1 = ms_since(t1);
+    std::printf("pack33 from bytes ms=%.1f G letters/s=%.2f out GB/s=%.1f\n", ms1, s.letters / 1e6 / ms1,
+                moc::packed33_bytes(s.letters) / 1e6 / ms1);
   }
   return 0;
 }
