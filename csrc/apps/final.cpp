@@ -265,6 +265,9 @@ int Job::run() {
                                (tr_flag == "shm" || (tr_flag == "auto" && ctx.single_node()));
   const bool sliced = !streaming && one_node_slices;
   const bool shm_stream = streaming && one_node_slices;
+  // a bulk record-slice job off the node's shm transport: the root encodes the ranks' slices straight from
+  // the text after the engines are up (run_text_batch)
+  const bool text_batch = !streaming && !one_node_slices && to_lower(flags.get("partition", "cost")) != "offsets";
   const std::string in_path = flags.get("input", "");
   Header h{};
   std::string error;
@@ -365,7 +368,7 @@ int Job::run() {
         }
       } else {
         // header (+ pass 1 unless sliced: the ranks count their shares of the text then)
-        auto parser = std::make_unique<BulkParser>(text, static_cast<size_t>(text_len), po, !sliced);
+        auto parser = std::make_unique<BulkParser>(text, static_cast<size_t>(text_len), po, !sliced && !text_batch);
         w = parser->weights();
         seq1 = parser->seq1();
         h.n_total = parser->count();
@@ -374,7 +377,7 @@ int Job::run() {
         h.mean_l2 = parser->mean_length_estimate();
         // shm transport without a skip: pass 2 later writes straight into the node-shared window (sliced:
         // into every rank's own buffers); otherwise encode now into a private batch
-        if (sliced || (h.first_index == 0 && one_node_slices)) {
+        if (sliced || text_batch) {
           parser_ = std::move(parser);
         } else {
           bulk.codes.resize(static_cast<size_t>(parser->total_chars()));
@@ -435,6 +438,8 @@ int Job::run() {
       // the parser's per-chunk tables go back to the OS on the releaser
       job_.rel.defer([p = std::shared_ptr<BulkParser>(parser_ ? std::move(parser_) : std::move(own))]() mutable { p.reset(); });
       pt.end();
+    } else if (text_batch) {
+      run_text_batch(job_, parser_, h.first_index, &text_);
     } else if (!streaming) {
       int64_t sizes[2] = {bulk.size(), bulk.total_chars()};
       if (parser_) {

@@ -7,6 +7,7 @@
 #include <future>
 #include <memory>
 #include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include "moc/comm.hpp"
@@ -17,6 +18,7 @@
 #include "moc/rccl_comm.hpp"
 #include "moc/runtime/device.hpp"
 #include "moc/runtime/hip_check.hpp"
+#include "moc/runtime/host_region.hpp"
 #include "moc/runtime/log.hpp"
 #include "moc/runtime/pinned.hpp"
 #include "moc/runtime/timer.hpp"
@@ -47,12 +49,32 @@ class RcclDeviceComm final : public DeviceComm {
     return p;
   }
   void dev_free(void* p) override { (void)hipFree(p); }
+  // Page-locked staging. Large buffers are 2 MiB pages on the device's NUMA node, registered with the
+  // runtime (the sliced path's registration rate, profiles/final_scale_1.1G_r3_stream.log pin_ms); small
+  // ones come from hipHostMalloc.
   void* host_alloc(int64_t bytes) override {
+    bytes = std::max<int64_t>(bytes, 16);
+    if (bytes >= kBigHost) {
+      Big b;
+      b.region = HostRegion(static_cast<size_t>(bytes), device_numa_node(device_));
+      b.bases = pinned::register_range(b.region.data(), static_cast<size_t>(bytes));
+      void* p = b.region.data();
+      big_.emplace(p, std::move(b));
+      return p;
+    }
     void* p = nullptr;
-    MOC_HIP_CHECK(hipHostMalloc(&p, static_cast<size_t>(std::max<int64_t>(bytes, 16)), hipHostMallocDefault));
+    MOC_HIP_CHECK(hipHostMalloc(&p, static_cast<size_t>(bytes), hipHostMallocDefault));
     return p;
   }
-  void host_free(void* p) override { (void)hipHostFree(p); }
+  void host_free(void* p) override {
+    auto it = big_.find(p);
+    if (it == big_.end()) {
+      (void)hipHostFree(p);
+      return;
+    }
+    pinned::unregister(it->second.bases);
+    big_.erase(it);
+  }
   int upload(void* d, const void* h, int64_t bytes) override {
     if (bytes > 0) MOC_HIP_CHECK(hipMemcpyAsync(d, h, static_cast<size_t>(bytes), hipMemcpyHostToDevice, copy_));
     return record(copy_);
@@ -98,11 +120,17 @@ class RcclDeviceComm final : public DeviceComm {
     events_.push_back(e);
     return static_cast<int>(events_.size()) - 1;
   }
+  static constexpr int64_t kBigHost = int64_t{4} << 20;
+  struct Big {
+    HostRegion region;
+    std::vector<void*> bases;
+  };
   const MpiContext& ctx_;
   int device_;
   hipStream_t s_, copy_ = nullptr;
   RcclComm nccl_;
   std::vector<hipEvent_t> events_;
+  std::unordered_map<void*, Big> big_;
 };
 
 // The HIP engine over device-resident wire batches: the packed narrow form streams through the swipe

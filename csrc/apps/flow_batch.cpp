@@ -22,6 +22,7 @@ class BatchFlow {
   BatchFlow(JobCore& j, std::unique_ptr<BulkParser>* parser, uvector<char>* text)
       : j_(j), parser_(parser), text_(text) {}
   void run(RecordBatch* rb, int64_t n, int64_t total_chars);
+  void release_input_now() { release_input(); }
 
  private:
   std::vector<int64_t> make_bounds(const int64_t* offsets, int64_t n, bool cp);
@@ -418,6 +419,93 @@ void BatchFlow::batch_rccl(RecordBatch* rb, int64_t n, int64_t total_chars, cons
 }
 
 }  // namespace
+
+void run_text_batch(JobCore& job, std::unique_ptr<BulkParser>& parser, int64_t first_index, uvector<char>* text) {
+  const MpiContext& ctx = job.ctx;
+  const int p = ctx.size;
+  const bool device = job.transport == "rccl" || job.transport == "rccl-emul";
+  // ---- root: pass 1 over the whole text in ~1 MiB chunks (the encode's unit of parallel work), the rank
+  // bounds; or, on the mpi transport, the whole batch as byte codes
+  std::vector<int64_t> bounds(static_cast<size_t>(p) + 1, 0);
+  RecordBatch bulk;
+  int64_t st[3] = {0, 0, 0};  // status, records, letters
+  std::string error;
+  if (ctx.rank == kRoot) {
+    job.pt.begin("count");
+    try {
+      const int64_t area = parser->area_bytes();
+      const int nch = static_cast<int>(std::clamp<int64_t>(area >> 20, std::min<int64_t>(64, std::max<int64_t>(area >> 16, 1)),
+                                                           int64_t{1} << 14));
+      std::vector<int64_t> starts = parser->chunk_starts(nch);
+      std::vector<int64_t> tk(static_cast<size_t>(nch)), ch(static_cast<size_t>(nch));
+      parser->count_chunks(starts, 0, nch, tk.data(), ch.data());
+      const CostModel m = job.cost_model();
+      if (device && job.partition != "even" && p > 1 && area <= (int64_t{256} << 20)) {
+        std::vector<double> costs(static_cast<size_t>(nch));
+        parser->chunk_costs(starts, 0, nch, m, costs.data());
+        parser->set_chunk_costs(std::move(costs));
+      }
+      parser->set_chunks(std::move(starts), tk.data(), ch.data());
+      const int64_t n_all = parser->count();
+      first_index = std::min(first_index, n_all);
+      st[1] = n_all - first_index;
+      if (device) {
+        for (int r = 0; r <= p; ++r)
+          bounds[r] = job.partition == "even" ? first_index + st[1] * r / p : parser->cost_split(first_index, r, p, m);
+        for (int r = 1; r <= p; ++r) bounds[r] = std::max(bounds[r], bounds[r - 1]);
+      } else {
+        const AreaSlice s = parser->slice(first_index, n_all);
+        bulk.codes.resize(static_cast<size_t>(s.letters));
+        bulk.offsets.resize(static_cast<size_t>(s.records) + 1);
+        parser->check(parser->fill_slice(s, bulk.codes.data(), nullptr, bulk.offsets.data()));
+        st[2] = s.letters;
+      }
+    } catch (const std::exception& e) {
+      st[0] = 1;
+      error = e.what();
+    }
+    job.pt.end();
+  }
+  bcast_bytes(st, sizeof st, kRoot, ctx.world);
+  if (st[0] != 0) throw InputError(error);
+  if (!device) {
+    parser.reset();
+    if (text) *text = uvector<char>();
+    run_record_batch(job, ctx.rank == kRoot ? &bulk : nullptr, st[1], st[2], first_index);
+    return;
+  }
+  ++job.batches;
+  job.first_index = first_index;
+  job.records += st[1];
+  PhaseHooks hooks;
+  hooks.begin = [&job](const char* phase) {
+    job.pt.begin(phase);
+    job.fault.at(phase, job.ctx.rank);
+  };
+  hooks.end = [&job] { job.pt.end(); };
+  DeviceComm& dc = job.emul_comm ? static_cast<DeviceComm&>(*job.emul_comm) : job.eng.hip->device_comm();
+  if (!job.scratch) job.scratch = std::make_unique<DeviceScratch>(dc);
+  DeviceBatchOut out;
+  if (job.emul_comm) {
+    CpuDeviceSearch ds(job.eng.table, job.eng.seq1, job.eng.sem, job.eng.threads);
+    out = device_batch_text(dc, ds, parser.get(), bounds, hooks, job.scratch.get());
+  } else {
+    out = device_batch_text(dc, job.eng.hip->device_search(), parser.get(), bounds, hooks, job.scratch.get());
+  }
+  if (out.input_error) throw InputError(out.error);
+  // the input text and the parser's tables go back to the OS while the results print
+  BatchFlow(job, &parser, text).release_input_now();
+  job.compute_ms += out.compute_ms;
+  job.eng.kernel_ms += out.kernel_ms;
+  if (ctx.rank == kRoot) {
+    job.cells += out.cells;
+    job.chars += out.letters;
+    if (!out.rank_records.empty()) job.rank_records = out.rank_records;
+    job.pt.begin("print");
+    write_results(job.out, out.runs, first_index);
+    job.pt.end();
+  }
+}
 
 void run_record_batch(JobCore& job, RecordBatch* rb, int64_t n, int64_t total_chars, int64_t first_index,
                       std::unique_ptr<BulkParser>* parser, uvector<char>* text) {

@@ -135,6 +135,11 @@ void run_sliced(JobCore& job, BulkParser& parser, int64_t first_index, SharedWin
 // One in-memory batch (root: rb with offsets from 0) over the job's transport (flow_batch.cpp).
 // `parser`: root, shm transport, bulk job without a skip — the records are encoded straight into the
 // shared window (deferred pass 2) instead of from rb.
+// A bulk job over the rccl / rccl-emul transport straight from the input text (device_batch_text: the root
+// counts, splits and encodes every rank's slice into its wire block, no byte-code batch); on the mpi
+// transport the root encodes one byte-code batch for run_record_batch. `parser` (root: header read, no
+// pass 1 yet) and `text` go back to the OS once encoded.
+void run_text_batch(JobCore& job, std::unique_ptr<BulkParser>& parser, int64_t first_index, uvector<char>* text);
 void run_record_batch(JobCore& job, RecordBatch* rb, int64_t n, int64_t total_chars, int64_t first_index,
                       std::unique_ptr<BulkParser>* parser = nullptr, uvector<char>* text = nullptr);
 

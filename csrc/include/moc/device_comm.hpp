@@ -14,6 +14,7 @@
 
 #include <cstdint>
 #include <functional>
+#include <string>
 #include <vector>
 
 #include "moc/common.hpp"
@@ -113,6 +114,11 @@ struct DeviceBatchOut {
   double compute_ms = 0, kernel_ms = 0;    // this rank
   int64_t scattered_bytes = 0;             // root: device bytes sent to the other ranks
   std::vector<int64_t> rank_records;       // every rank's records (root)
+  // device_batch_text: the batch's search cells and letters (root); an input error (every rank; the
+  // message on the root), in which case nothing was searched
+  int64_t cells = 0, letters = 0;
+  bool input_error = false;
+  std::string error;
 };
 
 // One batch over the device layer. Record slices (cp = false): the root packs each rank's slice into the
@@ -128,5 +134,15 @@ struct DeviceBatchOut {
 DeviceBatchOut device_batch(DeviceComm& dc, DeviceSearch& ds, const RecordBatch* rb, int64_t n, int64_t total_chars,
                             const std::vector<int64_t>& bounds, bool cp, const PhaseHooks& hooks,
                             DeviceScratch* scratch = nullptr);
+
+class BulkParser;
+// The same record-slice batch straight from the input text: the root encodes each rank's slice
+// (BulkParser::fill_slice after pass 1; `parser` and the p+1 record `bounds` are read on the root only)
+// into that rank's wire block in page-locked memory, peers first, and sends a block's pieces while it
+// encodes the next rank's slice (no intermediate byte-code batch). Phases: "fill" (root), "distribute",
+// "compute", "gather". An input error found in any slice comes back on every rank (nothing searched).
+DeviceBatchOut device_batch_text(DeviceComm& dc, DeviceSearch& ds, const BulkParser* parser,
+                                 const std::vector<int64_t>& bounds, const PhaseHooks& hooks,
+                                 DeviceScratch* scratch = nullptr);
 
 }  // namespace moc

@@ -9,6 +9,7 @@
 #include <memory>
 
 #include "moc/device_comm.hpp"
+#include "moc/io.hpp"
 #include "moc/runtime/timer.hpp"
 
 namespace moc {
@@ -64,6 +65,13 @@ std::vector<Piece> pieces_of(const RankPlan& pl, int r, int64_t chunk) {
     const int64_t nb = narrow_lengths_bytes(pl.n, static_cast<int>(pl.bits));
     v.push_back(Piece{r, 2, pl.off_lengths, pl.off_lengths + nb});
   }
+  return v;
+}
+
+// The text batch's pieces: its blocks are encoded whole before they move, so plain byte ranges of <= chunk.
+std::vector<Piece> byte_pieces(const RankPlan& pl, int r, int64_t chunk) {
+  std::vector<Piece> v;
+  for (int64_t b = 0; b < pl.block; b += chunk) v.push_back(Piece{r, 0, b, std::min(pl.block, b + chunk)});
   return v;
 }
 
@@ -204,8 +212,85 @@ char* DeviceScratch::get(std::vector<Buf>& v, int slot, int64_t bytes, bool host
 }
 
 namespace {
-enum Slot { kPlanBuf, kBlock, kOut, kR2, kMineR2, kGather, kStage0, kStageEnd = kStage0 + 3, kHostResults = 0,
-            kHostStage0 = 1 };
+enum Slot { kPlanBuf, kBlock, kOut, kR2, kMineR2, kGather, kStage0, kStageEnd = kStage0 + 3, kStatus = kStageEnd,
+            kHostResults = 0, kHostStage0 = 1, kHostPlan = kHostStage0 + 3, kHostStatus,
+            kHostBlock0 };
+}  // namespace
+
+namespace {
+// ---- search this rank's slice on its device, then its narrow results -> root (+ each rank's R2
+// parameters, 3 ints, through the device layer). `plan` is complete on the root; other ranks read `mine`.
+void solve_gather(DeviceComm& dc, DeviceSearch& ds, DeviceScratch& sc, const std::vector<RankPlan>& plan,
+                  const RankPlan& mine, char* d_block, const PhaseHooks& hooks, DeviceBatchOut& out) {
+  const int rank = dc.rank(), p = dc.size();
+  hooks.begin("compute");
+  Stopwatch sw;
+  sw.start();
+  const ResultFormat fmt = static_cast<ResultFormat>(mine.fmt);
+  const int fb = result_bytes(fmt);
+  char* d_out = sc.dev(kOut, fb * mine.n + 16);
+  if (mine.n > 0) ds.solve(device_view(mine, d_block), d_out, fmt);
+  dc.sync();
+  sw.stop();
+  out.compute_ms = sw.total_ms();
+  out.kernel_ms = ds.last_kernel_ms();
+  const R2Params r2 = ds.last_r2();
+  hooks.end();
+
+  hooks.begin("gather");
+  std::vector<int64_t> rstart(static_cast<size_t>(p) + 1, 0);
+  for (int r = 0; r < p; ++r) rstart[r + 1] = rstart[r] + al16(result_bytes(static_cast<ResultFormat>(plan[r].fmt)) * plan[r].n);
+  std::vector<int64_t> r2v(static_cast<size_t>(3 * p), 0);
+  char* d_r2 = sc.dev(kR2, 24 * p);
+  {
+    const int64_t mine_r2[3] = {r2.smin, r2.kw, r2.j};
+    // every rank's parameters land at its slot of the root's table
+    char* d_mine_r2 = sc.dev(kMineR2, 24);
+    dc.wait_upload(dc.upload(d_mine_r2, mine_r2, 24));
+    dc.group_start();
+    if (rank == 0) {
+      for (int r = 1; r < p; ++r) dc.recv(d_r2 + 24 * r, 24, r);
+    } else {
+      dc.send(d_mine_r2, 24, 0);
+    }
+    dc.group_end();
+    if (rank == 0) {
+      r2v[0] = r2.smin;
+      r2v[1] = r2.kw;
+      r2v[2] = r2.j;
+    }
+  }
+  char* d_gather = rank == 0 ? sc.dev(kGather, rstart[p] + 16) : nullptr;
+  dc.group_start();
+  if (rank == 0) {
+    for (int r = 1; r < p; ++r) {
+      const int64_t bytes = result_bytes(static_cast<ResultFormat>(plan[r].fmt)) * plan[r].n;
+      if (bytes > 0) dc.recv(d_gather + rstart[r], bytes, r);
+    }
+  } else if (fb * mine.n > 0) {
+    dc.send(d_out, fb * mine.n, 0);
+  }
+  dc.group_end();
+  if (rank == 0) {
+    char* h = sc.host(kHostResults, rstart[p] + 16);  // page-locked: the downloads are plain DMA
+    if (p > 1) dc.download(r2v.data() + 3, d_r2 + 24, 24 * (p - 1));
+    if (fb * mine.n > 0) dc.download(h, d_out, fb * mine.n);
+    if (rstart[p] > rstart[1]) dc.download(h + rstart[1], d_gather + rstart[1], rstart[p] - rstart[1]);
+    out.rank_records.resize(static_cast<size_t>(p));
+    for (int r = 0; r < p; ++r) {
+      ResultRun run;
+      run.data = h + rstart[r];
+      run.fmt = static_cast<ResultFormat>(plan[r].fmt);
+      run.r2 = R2Params{static_cast<int32_t>(r2v[3 * r]), static_cast<int32_t>(r2v[3 * r + 1]),
+                        static_cast<int32_t>(r2v[3 * r + 2])};
+      run.n = plan[r].n;
+      out.runs.push_back(run);
+      out.rank_records[r] = plan[r].n;
+    }
+  }
+  dc.sync();
+  hooks.end();
+}
 }  // namespace
 
 DeviceBatchOut device_batch(DeviceComm& dc, DeviceSearch& ds, const RecordBatch* rb, int64_t n, int64_t total_chars,
@@ -312,75 +397,163 @@ DeviceBatchOut device_batch(DeviceComm& dc, DeviceSearch& ds, const RecordBatch*
   dc.sync();
   hooks.end();
 
-  // ---- search this rank's slice on its device
-  hooks.begin("compute");
-  Stopwatch sw;
-  sw.start();
-  const ResultFormat fmt = static_cast<ResultFormat>(mine.fmt);
-  const int fb = result_bytes(fmt);
-  char* d_out = sc.dev(kOut, fb * mine.n + 16);
-  if (mine.n > 0) ds.solve(device_view(mine, d_block), d_out, fmt);
-  dc.sync();
-  sw.stop();
-  out.compute_ms = sw.total_ms();
-  out.kernel_ms = ds.last_kernel_ms();
-  const R2Params r2 = ds.last_r2();
-  hooks.end();
+  solve_gather(dc, ds, sc, plan, mine, d_block, hooks, out);
+  return out;
+}
 
-  // ---- narrow results -> root (+ each rank's R2 parameters, 3 ints, through the device layer)
-  hooks.begin("gather");
-  std::vector<int64_t> rstart(static_cast<size_t>(p) + 1, 0);
-  for (int r = 0; r < p; ++r) rstart[r + 1] = rstart[r] + al16(result_bytes(static_cast<ResultFormat>(plan[r].fmt)) * plan[r].n);
-  std::vector<int64_t> r2v(static_cast<size_t>(3 * p), 0);
-  char* d_r2 = sc.dev(kR2, 24 * p);
-  {
-    const int64_t mine_r2[3] = {r2.smin, r2.kw, r2.j};
-    // every rank's parameters land at its slot of the root's table
-    char* d_mine_r2 = sc.dev(kMineR2, 24);
-    dc.wait_upload(dc.upload(d_mine_r2, mine_r2, 24));
-    dc.group_start();
-    if (rank == 0) {
-      for (int r = 1; r < p; ++r) dc.recv(d_r2 + 24 * r, 24, r);
-    } else {
-      dc.send(d_mine_r2, 24, 0);
-    }
-    dc.group_end();
-    if (rank == 0) {
-      r2v[0] = r2.smin;
-      r2v[1] = r2.kw;
-      r2v[2] = r2.j;
-    }
+// ---- text batch: the root encodes every rank's slice straight from the input text into that rank's wire
+// block (page-locked, two blocks in turn), peers first and its own last; a block's pieces upload and leave
+// over the comm lane while the next rank's slice is encoded. Each peer learns its plan from a 96-byte
+// message ahead of its pieces (the plan depends on the slice's length range, known after its encode).
+DeviceBatchOut device_batch_text(DeviceComm& dc, DeviceSearch& ds, const BulkParser* parser,
+                                 const std::vector<int64_t>& bounds, const PhaseHooks& hooks, DeviceScratch* scratch) {
+  std::unique_ptr<DeviceScratch> own;
+  if (!scratch) {
+    own = std::make_unique<DeviceScratch>(dc);
+    scratch = own.get();
   }
-  char* d_gather = rank == 0 ? sc.dev(kGather, rstart[p] + 16) : nullptr;
-  dc.group_start();
+  DeviceScratch& sc = *scratch;
+  DeviceBatchOut out;
+  const int rank = dc.rank(), p = dc.size();
+  constexpr int64_t kPlanBytes = static_cast<int64_t>(sizeof(RankPlan));
+  const int64_t chunk = std::max<int64_t>(2640, send_chunk() / 2640 * 2640);
+  std::vector<RankPlan> plan(static_cast<size_t>(p));
+  char* d_block = nullptr;
+  char* d_status = sc.dev(kStatus, 16);
+  int64_t status = 0;
   if (rank == 0) {
-    for (int r = 1; r < p; ++r) {
-      const int64_t bytes = result_bytes(static_cast<ResultFormat>(plan[r].fmt)) * plan[r].n;
-      if (bytes > 0) dc.recv(d_gather + rstart[r], bytes, r);
-    }
-  } else if (fb * mine.n > 0) {
-    dc.send(d_out, fb * mine.n, 0);
-  }
-  dc.group_end();
-  if (rank == 0) {
-    char* h = sc.host(kHostResults, rstart[p] + 16);  // page-locked: the downloads are plain DMA
-    if (p > 1) dc.download(r2v.data() + 3, d_r2 + 24, 24 * (p - 1));
-    if (fb * mine.n > 0) dc.download(h, d_out, fb * mine.n);
-    if (rstart[p] > rstart[1]) dc.download(h + rstart[1], d_gather + rstart[1], rstart[p] - rstart[1]);
-    out.rank_records.resize(static_cast<size_t>(p));
+    hooks.begin("fill");  // encode (host threads), and the waits for a block to be free again
+    const int64_t L1 = static_cast<int64_t>(parser->seq1().size());
+    char* d_plan = sc.dev(kPlanBuf, kPlanBytes * p);
+    RankPlan* h_plan = reinterpret_cast<RankPlan*>(sc.host(kHostPlan, kPlanBytes * p));
+    // every slice's extent first (cheap: pass 1's chunk table): staging and host blocks at their final size
+    std::vector<AreaSlice> slices(static_cast<size_t>(p));
+    int64_t block_cap = 64, stage_bytes = 64;
     for (int r = 0; r < p; ++r) {
-      ResultRun run;
-      run.data = h + rstart[r];
-      run.fmt = static_cast<ResultFormat>(plan[r].fmt);
-      run.r2 = R2Params{static_cast<int32_t>(r2v[3 * r]), static_cast<int32_t>(r2v[3 * r + 1]),
-                        static_cast<int32_t>(r2v[3 * r + 2])};
-      run.n = plan[r].n;
-      out.runs.push_back(run);
-      out.rank_records[r] = plan[r].n;
+      slices[r] = parser->slice(bounds[r], bounds[r + 1]);
+      const int64_t n = slices[r].records;
+      const int64_t cap = al16(packed5_bytes(slices[r].letters)) + al16(8 * (n + 1)) + al16(n + 16) + 64;
+      block_cap = std::max(block_cap, cap);
+      if (r != 0) stage_bytes = std::max(stage_bytes, std::min(chunk, cap));
+    }
+    constexpr int kSlots = 3;
+    char* d_stage[kSlots];
+    int sent[kSlots] = {-1, -1, -1};
+    for (int q = 0; q < kSlots; ++q) d_stage[q] = p > 1 ? sc.dev(kStage0 + q, stage_bytes + 64) : nullptr;
+    int block_up[2] = {-1, -1};  // the last upload out of each host block
+    int own_up = -1;
+    int64_t qi = 0;
+    FillReport whole;
+    uvector<uint16_t> len16;
+    for (int k = 0; k < p; ++k) {
+      const int r = (k + 1) % p;  // peers 1..p-1, then the root
+      const int hb = k % 2;
+      if (block_up[hb] >= 0) dc.wait_upload_host(block_up[hb]);
+      const AreaSlice& sl = slices[r];
+      RankPlan& pl = plan[r];
+      pl.first = bounds[r];
+      pl.n = sl.records;
+      pl.letters = sl.letters;
+      const int64_t n = pl.n;
+      char* h = sc.host(kHostBlock0 + hb, block_cap);
+      FillReport rep;
+      if (n > 0) {
+        // the narrow form when the mean length says it can hold the slice, checked against the slice's range
+        pl.narrow = L1 <= 200 && sl.letters <= 32 * n ? 1 : 0;
+        if (pl.narrow) {
+          layout(pl);
+          if (static_cast<int64_t>(len16.size()) < n) len16 = uvector<uint16_t>(static_cast<size_t>(n));
+          rep = parser->fill_slice(sl, nullptr, reinterpret_cast<uint8_t*>(h), nullptr,
+                                   reinterpret_cast<int64_t*>(h + pl.off_offsets), len16.data(), 33);
+          if (!(rep.max_len <= 255 && ds.streams_packed(rep.min_len, rep.max_len))) pl.narrow = 0;
+        }
+        if (!pl.narrow) {
+          layout(pl);
+          rep = parser->fill_slice(sl, nullptr, reinterpret_cast<uint8_t*>(h),
+                                   reinterpret_cast<int64_t*>(h + pl.off_offsets), nullptr, nullptr, 5);
+        }
+        pl.min_l2 = rep.min_len;
+        pl.max_l2 = rep.max_len;
+        pl.bits = pl.narrow ? narrow_length_bits(rep.min_len, rep.max_len) : 0;
+        layout(pl);
+        if (pl.narrow)
+          pack_lengths16(len16.data(), n, static_cast<int>(pl.bits), pl.bits == 8 ? 0 : pl.min_l2,
+                         reinterpret_cast<uint8_t*>(h + pl.off_lengths));
+        pl.fmt = static_cast<int64_t>(ds.result_format(rep.min_len, rep.max_len, pl.narrow != 0));
+      } else {
+        layout(pl);
+      }
+      whole.min_len = std::min(whole.min_len, rep.min_len);
+      whole.max_len = std::max(whole.max_len, rep.max_len);
+      if (rep.bad_record >= 0 && (whole.bad_record < 0 || rep.bad_record < whole.bad_record)) whole.bad_record = rep.bad_record;
+      if (rep.long_record >= 0 && (whole.long_record < 0 || rep.long_record < whole.long_record)) {
+        whole.long_record = rep.long_record;
+        whole.long_len = rep.long_len;
+      }
+      whole.cells += rep.cells;
+      out.letters += sl.letters;
+      int last = -1;
+      if (r != 0) {
+        h_plan[r] = pl;
+        const int t = dc.upload(d_plan + kPlanBytes * r, h_plan + r, kPlanBytes);
+        dc.wait_upload(t);
+        dc.group_start();
+        dc.send(d_plan + kPlanBytes * r, kPlanBytes, r);
+        dc.group_end();
+        for (const Piece& pc : byte_pieces(pl, r, chunk)) {
+          const int q = static_cast<int>(qi++ % kSlots);
+          const int64_t len = pc.b1 - pc.b0;
+          last = dc.upload_after(d_stage[q], h + pc.b0, len, sent[q]);  // after that buffer's last send
+          dc.wait_upload(last);
+          dc.group_start();
+          dc.send(d_stage[q], len, r);
+          dc.group_end();
+          sent[q] = dc.mark();
+          out.scattered_bytes += len;
+        }
+      } else {
+        d_block = sc.dev(kBlock, pl.block + 16);
+        for (const Piece& pc : byte_pieces(pl, r, chunk)) last = dc.upload(d_block + pc.b0, h + pc.b0, pc.b1 - pc.b0);
+        own_up = last;
+      }
+      block_up[hb] = last;
+    }
+    hooks.begin("distribute");
+    if (own_up >= 0) dc.wait_upload(own_up);  // the root's search waits for its own block on the device
+    try {
+      parser->check(whole);
+    } catch (const std::exception& e) {
+      status = 1;
+      out.error = e.what();
+    }
+    out.cells = whole.cells;
+    int64_t* h_status = reinterpret_cast<int64_t*>(sc.host(kHostStatus, 16));
+    h_status[0] = status;
+    dc.wait_upload(dc.upload(d_status, h_status, 8));
+  } else {
+    hooks.begin("distribute");
+    char* d_plan = sc.dev(kPlanBuf, kPlanBytes);
+    dc.group_start();
+    dc.recv(d_plan, kPlanBytes, 0);
+    dc.group_end();
+    dc.download(&plan[rank], d_plan, kPlanBytes);
+    const RankPlan& mine = plan[rank];
+    d_block = sc.dev(kBlock, mine.block + 16);
+    for (const Piece& pc : byte_pieces(mine, rank, chunk)) {  // the root's order of this rank's pieces
+      dc.group_start();
+      dc.recv(d_block + pc.b0, pc.b1 - pc.b0, 0);
+      dc.group_end();
     }
   }
-  dc.sync();
+  // the input's verdict (the error a sequential reader meets first) on every rank
+  dc.bcast(d_status, 8, 0);
+  dc.download(&status, d_status, 8);
   hooks.end();
+  if (status != 0) {
+    out.input_error = true;
+    return out;
+  }
+  solve_gather(dc, ds, sc, plan, plan[rank], d_block, hooks, out);
   return out;
 }
 

@@ -482,3 +482,54 @@ def test_rccl_driver_emulated_many_pieces(np_, tmp_path):
                       env={"MOC_SEND_CHUNK": "5000"}, timeout=300)
         assert r.returncode == 0, r.stderr.decode()
         assert r.stdout.decode() == format_results(search_cpu(prob)), shape
+
+
+# ---- bulk jobs off the shm transport start from the text (run_text_batch / device_batch_text): the root
+# counts, splits and encodes every rank's slice straight into its wire block; mpi encodes one byte batch
+
+@pytest.mark.parametrize("np_", [1, 2, 3, 8])
+def test_text_batch_transports_goldens(np_):
+    for tr in ("--transport=rccl-emul", "--transport=mpi"):
+        for part in ("--partition=cost", "--partition=even"):
+            for i in range(1, 7):
+                r = run_final(["--backend=cpu", tr, part], stdin_path=input_path(i), np_=np_,
+                              env={"MOC_SEND_CHUNK": "2640"})
+                assert r.returncode == 0, (tr, part, i, r.stderr.decode())
+                assert r.stdout.decode() == expected(i), (tr, part, i)
+
+
+@pytest.mark.parametrize("np_", [2, 3])
+def test_text_batch_skip_and_errors(np_, tmp_path):
+    # --skip-records through the text path; an input error in a later rank's slice (found after earlier
+    # slices were sent) reaches every rank: the sequential reader's first error, exit code 1, nothing printed
+    for tr in ("--transport=rccl-emul", "--transport=mpi"):
+        r = run_final(["--backend=cpu", tr, "--skip-records=2"], stdin_path=input_path(6), np_=np_)
+        assert r.returncode == 0, r.stderr.decode()
+        assert r.stdout.decode() == "".join(expected(6).splitlines(keepends=True)[2:])
+        recs = ["ABCDEFGH"] * 40
+        recs[31] = "ABC1DEF"
+        recs[35] = "A" * 3001
+        text = "1 2 3 4\nABCDEFGHIJ\n40\n" + "\n".join(recs) + "\n"
+        r = run_final(["--backend=cpu", tr], stdin_bytes=text.encode(), np_=np_)
+        assert r.returncode == 1 and b"record #31 contains a non-letter" in r.stderr, r.stderr.decode()
+        assert r.stdout == b""
+        r = run_final(["--backend=cpu", tr], stdin_bytes=b"1 2 3 4\nABCDEFGHIJ\n40\nABC\nABD\n", np_=np_)
+        assert r.returncode == 1 and b"expected 40 Seq2 records, found only 2" in r.stderr, r.stderr.decode()
+
+
+def test_text_batch_timing_phases(tmp_path):
+    import json
+
+    from mpi_openmp_cuda_amd.utils.synthetic import make_synthetic
+
+    prob = make_synthetic("input6", 30_000, seed=9)
+    path = tmp_path / "in.txt"
+    path.write_text(prob.to_text())
+    r = run_final(["--backend=cpu", "--transport=rccl-emul", f"--input={path}", "--timing"], stdin_bytes=b"", np_=3,
+                  env={"MOC_SEND_CHUNK": "65536"})
+    assert r.returncode == 0, r.stderr.decode()
+    d = json.loads([ln for ln in r.stderr.decode().splitlines() if ln.startswith("{")][-1])
+    for ph in ("count", "fill", "distribute", "compute", "gather", "print"):
+        assert ph + "_ms" in d["timing"], (ph, d["timing"])
+    assert "parse_ms" in d["timing"] and d["timing"]["parse_ms"] < 1000
+    assert sum(d["rank_records"]) == prob.n and d["elements"] == int(prob.offsets[-1]) and d["records"] == prob.n

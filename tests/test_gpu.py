@@ -707,14 +707,17 @@ def test_final_binary_built_from_these_sources():
     assert f"src={_source_hash()}" in r.stdout.decode()
 
 
+@pytest.mark.parametrize("chunk", [None, "2640"])
 @pytest.mark.parametrize("shape,n", [("input6", 100_000), ("input1", 3000), ("input3", 40)])
-def test_final_cli_rccl_device_batches(tmp_path, shape, n):
-    # the rccl transport's device driver on one rank: the packed narrow form streams through the swipe
-    # kernel from device memory (R2 results), the dense form is unpacked on the device (tile/short kernels)
+def test_final_cli_rccl_device_batches(tmp_path, shape, n, chunk):
+    # the rccl transport's device driver on one rank: the root encodes its slice from the text into a
+    # page-locked block that uploads in pieces (2640-byte pieces: many), the packed narrow form streams
+    # through the swipe kernel from device memory (R2 results), the dense form is unpacked on the device
     prob = make_synthetic(shape, n, seed=n)
     path = tmp_path / "in.txt"
     path.write_text(prob.to_text())
-    r = run_final(["--backend=hip", "--transport=rccl", f"--input={path}"], stdin_bytes=b"", np_=1)
+    r = run_final(["--backend=hip", "--transport=rccl", f"--input={path}"], stdin_bytes=b"", np_=1,
+                  env={"MOC_SEND_CHUNK": chunk} if chunk else None)
     assert r.returncode == 0, r.stderr.decode()
     assert r.stdout.decode() == format_results(search_cpu(prob))
 
