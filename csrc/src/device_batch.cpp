@@ -220,6 +220,13 @@ enum Slot { kPlanBuf, kBlock, kOut, kR2, kMineR2, kGather, kStage0, kStageEnd = 
 namespace {
 // ---- search this rank's slice on its device, then its narrow results -> root (+ each rank's R2
 // parameters, 3 ints, through the device layer). `plan` is complete on the root; other ranks read `mine`.
+// Bytes of every rank's narrow results, 16-aligned runs in rank order (the root's gather buffer).
+int64_t results_bytes(const std::vector<RankPlan>& plan) {
+  int64_t b = 0;
+  for (const RankPlan& pl : plan) b += al16(result_bytes(static_cast<ResultFormat>(pl.fmt)) * pl.n);
+  return b;
+}
+
 void solve_gather(DeviceComm& dc, DeviceSearch& ds, DeviceScratch& sc, const std::vector<RankPlan>& plan,
                   const RankPlan& mine, char* d_block, const PhaseHooks& hooks, DeviceBatchOut& out) {
   const int rank = dc.rank(), p = dc.size();
@@ -362,6 +369,7 @@ DeviceBatchOut device_batch(DeviceComm& dc, DeviceSearch& ds, const RecordBatch*
       d_stage[q] = p > 1 ? sc.dev(kStage0 + q, stage_bytes + 64) : nullptr;
       up[q] = sent[q] = -1;
     }
+    sc.host(kHostResults, results_bytes(plan) + 16);  // the gather's page-locked buffer, ahead of the search
     hooks.begin("pack");  // host packing, and the waits for staging slots (a packing-bound distribution)
     int64_t i = 0;
     for (size_t k = 0; k < rounds; ++k)
@@ -428,13 +436,20 @@ DeviceBatchOut device_batch_text(DeviceComm& dc, DeviceSearch& ds, const BulkPar
     RankPlan* h_plan = reinterpret_cast<RankPlan*>(sc.host(kHostPlan, kPlanBytes * p));
     // every slice's extent first (cheap: pass 1's chunk table): staging and host blocks at their final size
     std::vector<AreaSlice> slices(static_cast<size_t>(p));
+    // a block's size in the narrow form (P33 + sparse offsets + lengths) or the dense one (5-bit + offsets)
+    auto wire_cap = [](const AreaSlice& sl, bool narrow) {
+      const int64_t n = sl.records;
+      return narrow ? al16(packed33_bytes(sl.letters)) + al16(8 * sparse_count(n, kSparseShift)) + al16(n + 16) + 64
+                    : al16(packed5_bytes(sl.letters)) + al16(8 * (n + 1)) + 64;
+    };
+    // the narrow form when the mean length says it can hold the slice (checked against the slice's range)
+    auto guess_narrow = [L1](const AreaSlice& sl) { return sl.records > 0 && L1 <= 200 && sl.letters <= 32 * sl.records; };
     int64_t block_cap = 64, stage_bytes = 64;
     for (int r = 0; r < p; ++r) {
       slices[r] = parser->slice(bounds[r], bounds[r + 1]);
-      const int64_t n = slices[r].records;
-      const int64_t cap = al16(packed5_bytes(slices[r].letters)) + al16(8 * (n + 1)) + al16(n + 16) + 64;
+      const int64_t cap = wire_cap(slices[r], guess_narrow(slices[r]));
       block_cap = std::max(block_cap, cap);
-      if (r != 0) stage_bytes = std::max(stage_bytes, std::min(chunk, cap));
+      if (r != 0) stage_bytes = std::max(stage_bytes, std::min(chunk, std::max(cap, wire_cap(slices[r], false))));
     }
     constexpr int kSlots = 3;
     char* d_stage[kSlots];
@@ -458,8 +473,7 @@ DeviceBatchOut device_batch_text(DeviceComm& dc, DeviceSearch& ds, const BulkPar
       char* h = sc.host(kHostBlock0 + hb, block_cap);
       FillReport rep;
       if (n > 0) {
-        // the narrow form when the mean length says it can hold the slice, checked against the slice's range
-        pl.narrow = L1 <= 200 && sl.letters <= 32 * n ? 1 : 0;
+        pl.narrow = guess_narrow(sl) ? 1 : 0;
         if (pl.narrow) {
           layout(pl);
           if (static_cast<int64_t>(len16.size()) < n) len16 = uvector<uint16_t>(static_cast<size_t>(n));
@@ -469,6 +483,7 @@ DeviceBatchOut device_batch_text(DeviceComm& dc, DeviceSearch& ds, const BulkPar
         }
         if (!pl.narrow) {
           layout(pl);
+          h = sc.host(kHostBlock0 + hb, std::max(block_cap, wire_cap(sl, false)));  // grows when it must
           rep = parser->fill_slice(sl, nullptr, reinterpret_cast<uint8_t*>(h),
                                    reinterpret_cast<int64_t*>(h + pl.off_offsets), nullptr, nullptr, 5);
         }
@@ -519,6 +534,7 @@ DeviceBatchOut device_batch_text(DeviceComm& dc, DeviceSearch& ds, const BulkPar
       block_up[hb] = last;
     }
     hooks.begin("distribute");
+    sc.host(kHostResults, results_bytes(plan) + 16);  // the gather's page-locked buffer, while the blocks move
     if (own_up >= 0) dc.wait_upload(own_up);  // the root's search waits for its own block on the device
     try {
       parser->check(whole);
