@@ -10,8 +10,6 @@
 
 #include "job.hpp"
 #include "moc/device_comm.hpp"
-#include "moc/runtime/host_region.hpp"
-#include "moc/runtime/log.hpp"
 
 namespace moc {
 
@@ -26,16 +24,14 @@ class BatchFlow {
 
  private:
   std::vector<int64_t> make_bounds(const int64_t* offsets, int64_t n, bool cp);
-  void batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, bool cp);
-  void gpu_window_slice(const uint8_t* w_codes, const int64_t* offs, int64_t n, Result* res, ResultFormat& fmt,
-                        R2Params& r2);
+  void batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars);
   void batch_mpi(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds, bool cp);
   void batch_rccl(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds, bool cp);
   // the input (deferred parser + text) goes back to the OS on the releaser
   void release_input();
 
   JobCore& j_;
-  std::unique_ptr<BulkParser>* parser_;  // root: deferred pass 2 into the shared window (or null)
+  std::unique_ptr<BulkParser>* parser_;  // root: the parser of a text batch (or null), released with the text
   uvector<char>* text_;                  // root: the text that parser reads
 };
 
@@ -56,7 +52,8 @@ void BatchFlow::release_input() {
 void BatchFlow::run(RecordBatch* rb, int64_t n, int64_t total_chars) {
   const bool cp = j_.partition == "offsets";
   if (j_.transport == "shm") {  // the window is filled first; the bounds come from it
-    batch_shm(rb, n, total_chars, cp);
+    if (!cp) throw Error("record-slice batches on the shm transport run sliced or streamed");
+    batch_shm(rb, n, total_chars);
     return;
   }
   const std::vector<int64_t> bounds = make_bounds(j_.ctx.rank == kRoot ? rb->offsets.data() : nullptr, n, cp);
@@ -83,44 +80,13 @@ std::vector<int64_t> BatchFlow::make_bounds(const int64_t* offsets, int64_t n, b
   return bounds;
 }
 
-void BatchFlow::batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, bool cp) {
+// Context parallel on one node (shm transport, --partition=offsets; the record-slice jobs of the node run
+// sliced or streamed): the batch in a node-shared window, every rank searches its share of every record's
+// offsets, packed keys MAX-all-reduced, the root resolves and prints.
+void BatchFlow::batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars) {
   PhaseTimer& pt = j_.pt;
   const MpiContext& ctx = j_.ctx;
-  const bool deferred = parser_ && *parser_;
-  if (ctx.size == 1 && !cp && rb && !deferred) {  // one rank: no window to share, search the batch in place
-    const int64_t* offs = rb->offsets.data();
-    const int64_t L1 = static_cast<int64_t>(j_.eng.seq1.size());
-    int64_t cells = 0;
-#pragma omp parallel for reduction(+ : cells) schedule(static) if (n > 65536)
-    for (int64_t i = 0; i < n; ++i) cells += record_cells(L1, offs[i + 1] - offs[i]);
-    j_.cells += cells;
-    pt.begin("compute");
-    j_.fault.at("compute", 0);
-    Stopwatch sw;
-    sw.start();
-    HostRegion res(12 * static_cast<size_t>(std::max<int64_t>(n, 1)), j_.eng.gpu ? j_.eng.hip->numa_node() : -1);
-    ResultFormat fmt = ResultFormat::R12;
-    R2Params r2{};
-    Result* out = res.as<Result>();
-    if (j_.eng.gpu && n > 0)
-      gpu_window_slice(rb->codes.data(), offs, n, out, fmt, r2);
-    else if (n > 0)
-      j_.eng.solve(rb->codes.data(), offs, n, out);
-    sw.stop();
-    j_.compute_ms += sw.total_ms();
-    pt.end();
-    {  // the batch's letters go back to the OS while its results print
-      auto spent = std::make_shared<RecordBatch>(std::move(*rb));
-      j_.rel.defer([spent]() mutable { spent.reset(); });
-      *rb = RecordBatch{};
-    }
-    pt.begin("print");
-    write_results(j_.out, std::vector<ResultRun>{ResultRun{out, fmt, r2, n}}, j_.first_index);
-    pt.end();
-    res.set_releaser(&j_.rel);
-    return;
-  }
-  // layout: offsets[(N+1)] | results[N] (or keys[N] in cp mode) | codes[total]   (8-byte aligned sections)
+  // layout: offsets[(N+1)] | results[N] | codes[total]   (8-byte aligned sections)
   const int64_t off_bytes = 8 * (n + 1);
   const int64_t res_bytes = ((12 * n) + 7) & ~int64_t{7};
   pt.begin("distribute");
@@ -129,185 +95,47 @@ void BatchFlow::batch_shm(RecordBatch* rb, int64_t n, int64_t total_chars, bool 
   int64_t* w_offs = reinterpret_cast<int64_t*>(win->base());
   Result* w_res = reinterpret_cast<Result*>(win->base() + off_bytes);
   uint8_t* w_codes = reinterpret_cast<uint8_t*>(win->base() + off_bytes + res_bytes);
-  int32_t status = 0;
-  std::string error;
   if (ctx.rank == kRoot) {
-    if (deferred) {  // deferred pass 2: letters encoded straight into the window, no intermediate copy
-      try {
-        (*parser_)->fill(w_codes, w_offs);
-      } catch (const std::exception& e) {
-        status = 1;
-        error = e.what();
-      }
-    } else {
-      const int64_t* src_off = rb->offsets.data();
-      const uint8_t* src_codes = rb->codes.data();
-      const int nt = total_chars > (1 << 20) ? omp_get_max_threads() : 1;
+    const int64_t* src_off = rb->offsets.data();
+    const uint8_t* src_codes = rb->codes.data();
+    const int nt = total_chars > (1 << 20) ? omp_get_max_threads() : 1;
 #pragma omp parallel for schedule(static, 1) num_threads(nt)
-      for (int t = 0; t < nt; ++t) {
-        const int64_t cb = total_chars * t / nt, ce = total_chars * (t + 1) / nt;
-        std::memcpy(w_codes + cb, src_codes + cb, static_cast<size_t>(ce - cb));
-        const int64_t ob = (n + 1) * t / nt, oe = (n + 1) * (t + 1) / nt;
-        std::memcpy(w_offs + ob, src_off + ob, static_cast<size_t>(oe - ob) * 8);
-      }
-      *rb = RecordBatch{};  // the window is now the only copy
+    for (int t = 0; t < nt; ++t) {
+      const int64_t cb = total_chars * t / nt, ce = total_chars * (t + 1) / nt;
+      std::memcpy(w_codes + cb, src_codes + cb, static_cast<size_t>(ce - cb));
+      const int64_t ob = (n + 1) * t / nt, oe = (n + 1) * (t + 1) / nt;
+      std::memcpy(w_offs + ob, src_off + ob, static_cast<size_t>(oe - ob) * 8);
     }
-  }
-  bcast_bytes(&status, sizeof status, kRoot, ctx.world);
-  if (status != 0) {
-    win.reset();  // collective, on every rank, before leaving
-    throw InputError(error);
+    *rb = RecordBatch{};  // the window is now the only copy
   }
   j_.fault.at("distribute", ctx.rank);
   win->fence();
   pt.end();
   pt.begin("bounds");
-  const std::vector<int64_t> bounds = make_bounds(ctx.rank == kRoot ? w_offs : nullptr, n, cp);
+  make_bounds(ctx.rank == kRoot ? w_offs : nullptr, n, true);  // the search cells (--timing)
   pt.end();
   pt.begin("compute");
   j_.fault.at("compute", ctx.rank);
   Stopwatch sw;
   sw.start();
-  if (cp) {
-    std::vector<uint64_t> keys(static_cast<size_t>(n), 0);
-    j_.eng.solve_keys(w_codes, w_offs, n, ctx.rank, ctx.size, keys.data());
-    sw.stop();
-    pt.end();
-    pt.begin("gather");
-    j_.fault.at("gather", ctx.rank);
-    j_.allreduce_keys(keys.data(), n);
-    if (ctx.rank == kRoot) j_.resolve_keys(keys.data(), w_codes, w_offs, n, w_res);
-    pt.end();
-    j_.compute_ms += sw.total_ms();
-    // printing reads only the results: the input, offsets and letters go back to the OS while it runs
-    release_input();
-    win->discard(0, off_bytes);
-    win->discard(off_bytes + res_bytes, total_chars);
-    j_.print(w_res, n, 0);
-    pt.begin("release");
-    win.reset();  // collective: unmaps the node-shared window
-    pt.end();
-    return;
-  }
-  const int64_t my_b = bounds[ctx.rank], my_n = bounds[ctx.rank + 1] - my_b;
-  // this rank's results go to the start of its R12 region of the window, in the format it chose
-  ResultFormat fmt = ResultFormat::R12;
-  R2Params r2{};
-  if (j_.eng.gpu && my_n > 0) {
-    gpu_window_slice(w_codes, w_offs + my_b, my_n, w_res + my_b, fmt, r2);
-  } else if (my_n > 0) {
-    j_.eng.solve(w_codes, w_offs + my_b, my_n, w_res + my_b);
-  }
+  std::vector<uint64_t> keys(static_cast<size_t>(n), 0);
+  j_.eng.solve_keys(w_codes, w_offs, n, ctx.rank, ctx.size, keys.data());
   sw.stop();
   pt.end();
   pt.begin("gather");
   j_.fault.at("gather", ctx.rank);
-  int64_t info[4] = {static_cast<int64_t>(fmt), r2.smin, r2.kw, r2.j};
-  std::vector<int64_t> infos(static_cast<size_t>(4 * ctx.size));
-  j_.allgather_i64(info, 4, infos.data());
-  win->fence();
+  j_.allreduce_keys(keys.data(), n);
+  if (ctx.rank == kRoot) j_.resolve_keys(keys.data(), w_codes, w_offs, n, w_res);
   pt.end();
   j_.compute_ms += sw.total_ms();
+  // printing reads only the results: the input, offsets and letters go back to the OS while it runs
   release_input();
   win->discard(0, off_bytes);
   win->discard(off_bytes + res_bytes, total_chars);
-  if (ctx.rank == kRoot) {
-    std::vector<ResultRun> runs(static_cast<size_t>(ctx.size));
-    for (int q = 0; q < ctx.size; ++q) {
-      const int64_t* x = infos.data() + 4 * q;
-      runs[q] = ResultRun{w_res + bounds[q], static_cast<ResultFormat>(x[0]),
-                          R2Params{static_cast<int32_t>(x[1]), static_cast<int32_t>(x[2]), static_cast<int32_t>(x[3])},
-                          bounds[q + 1] - bounds[q]};
-    }
-    pt.begin("print");
-    write_results(j_.out, runs, j_.first_index);
-    pt.end();
-  }
+  j_.print(w_res, n, 0);
   pt.begin("release");
   win.reset();  // collective: unmaps the node-shared window
   pt.end();
-}
-
-// A GPU rank's slice of a node-shared CSR window: encoded into the headline's wire formats in NUMA-local
-// memory when the streaming kernel takes the batch (P33 letters, narrow lengths, sparse offsets; narrow
-// results written to the start of `res`), else the window's own bytes and offsets. Either way only this
-// slice's pieces are page-locked — never the whole window.
-void BatchFlow::gpu_window_slice(const uint8_t* w_codes, const int64_t* offs, int64_t n, Result* res,
-                                 ResultFormat& fmt, R2Params& r2) {
-  GpuRank& hip = *j_.eng.hip;
-  const int64_t c0 = offs[0], c1 = offs[n];
-  int64_t mn = INT64_MAX, mx = 0;
-#pragma omp parallel for reduction(min : mn) reduction(max : mx) schedule(static) if (n > 65536)
-  for (int64_t i = 0; i < n; ++i) {
-    const int64_t L = offs[i + 1] - offs[i];
-    mn = std::min(mn, L);
-    mx = std::max(mx, L);
-  }
-  const int numa = hip.numa_node();
-  auto pin = [&](const void* ptr, int64_t bytes) {
-    if (!j_.pin_window || !ptr || bytes <= 0) return;
-    try {
-      hip.pin(ptr, static_cast<size_t>(bytes));
-      j_.pinned_bytes += bytes;
-    } catch (const std::exception& e) {
-      MOC_LOG_WARN("could not page-lock this rank's slice (%s); using the staged pipeline", e.what());
-    }
-  };
-  GpuSolveStats gs;
-  if (mx <= 255 && hip.streams_packed(mn, mx)) {
-    const int64_t letters = c1 - c0;
-    const bool p33 = j_.group_pack() == 33;
-    HostRegion pk(static_cast<size_t>(p33 ? packed33_bytes(letters) : packed24_bytes(letters)) + 16, numa);
-    if (p33)
-      pack33(w_codes + c0, letters, pk.as<uint8_t>());
-    else
-      pack24(w_codes + c0, letters, pk.as<uint8_t>());
-    const int bits = narrow_length_bits(mn, mx);
-    const int64_t base = bits == 8 ? 0 : mn;
-    HostRegion lens(static_cast<size_t>(narrow_lengths_bytes(n, bits)) + 8, numa);
-    pack_lengths(offs, n, bits, base, lens.as<uint8_t>());
-    const int64_t ns = sparse_count(n, kSparseShift);
-    HostRegion sparse(8 * static_cast<size_t>(ns), numa);
-    int64_t* sp = sparse.as<int64_t>();
-#pragma omp parallel for schedule(static) if (ns > 65536)
-    for (int64_t q = 0; q < ns; ++q) sp[q] = offs[std::min(q << kSparseShift, n)] - c0;
-    WireBatch wb;
-    wb.letters = pk.as<uint8_t>();
-    wb.packed24 = !p33;
-    wb.packed33 = p33;
-    wb.offsets = sp;
-    wb.off_shift = kSparseShift;
-    wb.lengths = lens.as<uint8_t>();
-    wb.len_bits = bits;
-    wb.len_base = base;
-    wb.n = n;
-    wb.min_l2 = mn;
-    wb.max_l2 = mx;
-    fmt = hip.result_format(mn, mx);
-    pin(wb.letters, wb.letter_bytes());
-    pin(sp, 8 * ns);
-    pin(wb.lengths, wb.length_bytes());
-    pin(res, static_cast<int64_t>(result_bytes(fmt)) * n);
-    hip.solve_wire(wb, res, fmt);
-    gs = hip.last_stats();
-    r2 = gs.r2;
-    // unregistered now: the window's memory (the results' pages) is freed by its collective teardown
-    hip.unpin_all();
-    pk.set_releaser(&j_.rel);
-    lens.set_releaser(&j_.rel);
-    sparse.set_releaser(&j_.rel);
-  } else {
-    pin(w_codes + c0, c1 - c0);
-    pin(offs, 8 * (n + 1));
-    pin(res, 12 * n);
-    hip.solve(w_codes, offs, n, res);
-    gs.kernel_ms = hip.last_kernel_ms();
-    hip.unpin_all();
-    fmt = ResultFormat::R12;
-  }
-  j_.eng.kernel_ms += gs.kernel_ms;
-  j_.h2d_bytes += gs.h2d_bytes;
-  j_.d2h_bytes += gs.d2h_bytes;
 }
 
 void BatchFlow::batch_mpi(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds,
