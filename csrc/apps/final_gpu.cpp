@@ -57,6 +57,7 @@ class RcclDeviceComm final : public DeviceComm {
     if (bytes >= kBigHost) {
       Big b;
       b.region = HostRegion(static_cast<size_t>(bytes), device_numa_node(device_));
+      b.region.prefault();
       b.bases = pinned::register_range(b.region.data(), static_cast<size_t>(bytes));
       void* p = b.region.data();
       big_.emplace(p, std::move(b));

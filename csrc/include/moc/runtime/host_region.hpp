@@ -32,6 +32,9 @@ class HostRegion {
   T* as() const {
     return reinterpret_cast<T*>(base_);
   }
+  // Faults every page in now, OpenMP threads over the region (a registration that finds the pages absent
+  // faults them in on one thread).
+  void prefault();
   // Later release (destruction) goes through `rel` (FIFO, background thread); rel must outlive it.
   void set_releaser(BackgroundReleaser* rel) { releaser_ = rel; }
 

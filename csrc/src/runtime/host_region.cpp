@@ -52,6 +52,10 @@ HostRegion::HostRegion(size_t bytes, int numa_node) {
   if (numa_node >= 0) (void)bind_range_to_node(base_, want, numa_node);
 }
 
+void HostRegion::prefault() {
+  if (base_) prefault_pages(base_, bytes_);
+}
+
 HostRegion& HostRegion::operator=(HostRegion&& o) noexcept {
   if (this != &o) {
     release();
