@@ -96,7 +96,7 @@ $(OBJ)/apps/%.o: csrc/apps/%.cpp csrc/apps/job.hpp $(HEADERS)
 
 # ./final links MPI and the CPU core only; the GPU side is a plugin it dlopens when a rank uses a GPU
 APP_OBJS  := $(OBJ)/apps/final.o $(OBJ)/apps/job_common.o $(OBJ)/apps/flow_sliced.o $(OBJ)/apps/flow_stream.o \
-             $(OBJ)/apps/flow_batch.o
+             $(OBJ)/apps/text_cut.o $(OBJ)/apps/flow_device_stream.o $(OBJ)/apps/flow_batch.o
 final: $(APP_OBJS) $(COMM_OBJS) $(CPU_OBJS) $(MPILIB)/libmpi.so
 	$(CXX) -fopenmp -o $@ $(APP_OBJS) $(COMM_OBJS) $(CPU_OBJS) \
 	    -L$(MPILIB) -lmpi -Wl,-rpath-link,$(MPI_HOME)/lib -Wl,-rpath,'$$ORIGIN/$(MPILIB)' -ldl
@@ -109,7 +109,8 @@ $(GPU_PLUGIN): $(OBJ)/apps/final_gpu.o $(RCCL_OBJS) $(COMM_OBJS) $(PKG_LIB) $(MP
 # Host-side sanitizers (GPU ASan is not available on the target pool). ./final links no ROCm code, so
 # the sanitized binaries cover everything the CPU backend runs; a GPU rank would dlopen the plugin.
 SAN_SRCS := $(CPU_SRCS) csrc/src/comm/comm.cpp csrc/src/comm/mpi_device_comm.cpp csrc/apps/final.cpp \
-            csrc/apps/job_common.cpp csrc/apps/flow_sliced.cpp csrc/apps/flow_stream.cpp csrc/apps/flow_batch.cpp
+            csrc/apps/job_common.cpp csrc/apps/flow_sliced.cpp csrc/apps/flow_stream.cpp csrc/apps/text_cut.cpp \
+            csrc/apps/flow_device_stream.cpp csrc/apps/flow_batch.cpp
 asan: $(MPILIB)/libmpi.so
 	@rm -rf $(BUILD)/asan && mkdir -p $(BUILD)/asan
 	for f in $(SAN_SRCS); do \

@@ -11,8 +11,10 @@
 //        sliced  (bulk, one node)      every rank encodes its own slice of the node-shared text;
 //        stream  (--batch-records/-chars, one node)  batch by batch through persistent page-locked rings,
 //                                      encode / kernel / print overlapped;
-//        batch   (multi-node transports mpi / rccl, --transport=rccl-emul, --partition=offsets, and the
-//                 bulk/streaming jobs those take)  in-memory record batches over the chosen transport.
+//        text    (transports rccl / rccl-emul / mpi: multi-node, or chosen)  the root cuts bulk or streamed
+//                batches from the text and encodes every rank's slice straight into its wire block
+//                (device transports) or a byte-code batch (mpi);
+//        batch   (--partition=offsets on any transport)  in-memory record batches, context parallel.
 //      Decomposition: cost-balanced contiguous record ranges (valid for any -np, B4/B5/B6), or context
 //      parallel (--partition=offsets: every rank searches a share of EVERY record's offsets, one MAX
 //      all-reduce of packed 64-bit keys combines them — the Reduce the reference never had).
@@ -183,8 +185,8 @@ bool Job::open_io(std::string& error) {
   }
 }
 
-// Streaming: root parses the header, then either the node's streaming flow (shm transport, record slices)
-// or batches from a StreamReader over the job's transport.
+// Streaming with record slices on one node (the node's streaming flow), or context-parallel streaming
+// (--partition=offsets): batches from a StreamReader over the job's transport.
 int Job::run_streamed(const Header& h0, bool shm_flow, int64_t batch_records, int64_t batch_chars,
                       const ParseOptions& po) {
   const MpiContext& ctx = job_.ctx;
@@ -268,6 +270,8 @@ int Job::run() {
   // a bulk record-slice job off the node's shm transport: the root encodes the ranks' slices straight from
   // the text after the engines are up (run_text_batch)
   const bool text_batch = !streaming && !one_node_slices && to_lower(flags.get("partition", "cost")) != "offsets";
+  // ... and a streamed one: the root cuts the batches from the text (run_device_streaming)
+  const bool dev_stream = streaming && !one_node_slices && to_lower(flags.get("partition", "cost")) != "offsets";
   const std::string in_path = flags.get("input", "");
   Header h{};
   std::string error;
@@ -285,6 +289,13 @@ int Job::run() {
         if (text_len < 0 && sliced) {         // a pipe: read it all first
           text_ = read_stream(in_);
           text_len = static_cast<int64_t>(text_.size());
+        }
+      } else if (dev_stream && !in_path.empty()) {  // the root maps an --input file read from its start
+        text_len = regular_input_bytes(in_);
+        if (text_len > 0 && std::ftell(in_) == 0) {
+          text_map_ = std::make_unique<MappedFile>(in_path.c_str(), static_cast<size_t>(text_len));
+          text_map_->set_releaser(&job_.rel);
+          text = text_map_->data();
         }
       } else if (!streaming) {
         text_ = read_stream(in_);
@@ -343,7 +354,7 @@ int Job::run() {
     pt.begin("parse");
     try {
       Weights w{};
-      if (shm_stream && text) {  // mapped: the header from the mapping, the records by the streaming flow
+      if ((shm_stream || dev_stream) && text) {  // mapped: the header from the mapping, the records by the flow
         BulkParser hdr(text, static_cast<size_t>(text_len), po, false);
         w = hdr.weights();
         seq1 = hdr.seq1();
@@ -359,7 +370,7 @@ int Job::run() {
         seq1 = reader_->seq1();
         h.n_total = reader_->count();
         h.cells = -1;
-        if (shm_stream) {  // the node's flow reads the rest of the stream itself
+        if (shm_stream || dev_stream) {  // the flow reads the rest of the stream itself
           h.first_index = std::min<int64_t>(skip, h.n_total);
           stream_.in = in_;
           stream_.eof = reader_->take_rest(stream_.head);
@@ -449,7 +460,8 @@ int Job::run() {
       bcast_bytes(sizes, sizeof sizes, kRoot, ctx.world);
       run_record_batch(job_, ctx.rank == kRoot ? &bulk : nullptr, sizes[0], sizes[1], h.first_index, &parser_, &text_);
     } else {
-      rc = run_streamed(h, shm_stream, batch_records, batch_chars, po);
+      rc = dev_stream ? run_device_streaming(job_, h, stream_, batch_records, batch_chars, po)
+                      : run_streamed(h, shm_stream, batch_records, batch_chars, po);
     }
   } catch (const InputError& e) {
     return fail(e.what());

@@ -157,5 +157,10 @@ struct StreamSource {
 // Returns 0, or 1 after an input error (reported on root's stderr).
 int run_streaming(JobCore& job, const Header& h, StreamSource& src, int64_t batch_records, int64_t batch_chars,
                   const ParseOptions& po);
+// Streaming job off the shm transport (flow_device_stream.cpp): the root cuts each batch from the text
+// (StreamSource on the root only) and sends it — device_batch_text on rccl / rccl-emul, byte-code batches on
+// mpi; batch b prints while batch b+1 is encoded and searched. Returns 0, or 1 after an input error.
+int run_device_streaming(JobCore& job, const Header& h, StreamSource& src, int64_t batch_records,
+                         int64_t batch_chars, const ParseOptions& po);
 
 }  // namespace moc

@@ -141,8 +141,11 @@ class BulkParser;
 // into that rank's wire block in page-locked memory, peers first, and sends a block's pieces while it
 // encodes the next rank's slice (no intermediate byte-code batch). Phases: "fill" (root), "distribute",
 // "compute", "gather". An input error found in any slice comes back on every rank (nothing searched).
+// `record_base`: the global index of the parser's record 0 (a streamed batch's area parser), for the
+// error messages; `results_slot` 0/1: which of two page-locked result buffers the root's runs point into
+// (a streaming caller prints batch b from one while batch b+1 is gathered into the other).
 DeviceBatchOut device_batch_text(DeviceComm& dc, DeviceSearch& ds, const BulkParser* parser,
                                  const std::vector<int64_t>& bounds, const PhaseHooks& hooks,
-                                 DeviceScratch* scratch = nullptr);
+                                 DeviceScratch* scratch = nullptr, int64_t record_base = 0, int results_slot = 0);
 
 }  // namespace moc

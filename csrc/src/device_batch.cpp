@@ -214,7 +214,7 @@ char* DeviceScratch::get(std::vector<Buf>& v, int slot, int64_t bytes, bool host
 namespace {
 enum Slot { kPlanBuf, kBlock, kOut, kR2, kMineR2, kGather, kStage0, kStageEnd = kStage0 + 3, kStatus = kStageEnd,
             kHostResults = 0, kHostStage0 = 1, kHostPlan = kHostStage0 + 3, kHostStatus,
-            kHostBlock0 };
+            kHostBlock0, kHostResults1 = kHostBlock0 + 2 };
 }  // namespace
 
 namespace {
@@ -228,7 +228,8 @@ int64_t results_bytes(const std::vector<RankPlan>& plan) {
 }
 
 void solve_gather(DeviceComm& dc, DeviceSearch& ds, DeviceScratch& sc, const std::vector<RankPlan>& plan,
-                  const RankPlan& mine, char* d_block, const PhaseHooks& hooks, DeviceBatchOut& out) {
+                  const RankPlan& mine, char* d_block, const PhaseHooks& hooks, DeviceBatchOut& out,
+                  int host_results = kHostResults) {
   const int rank = dc.rank(), p = dc.size();
   hooks.begin("compute");
   Stopwatch sw;
@@ -279,7 +280,7 @@ void solve_gather(DeviceComm& dc, DeviceSearch& ds, DeviceScratch& sc, const std
   }
   dc.group_end();
   if (rank == 0) {
-    char* h = sc.host(kHostResults, rstart[p] + 16);  // page-locked: the downloads are plain DMA
+    char* h = sc.host(host_results, rstart[p] + 16);  // page-locked: the downloads are plain DMA
     if (p > 1) dc.download(r2v.data() + 3, d_r2 + 24, 24 * (p - 1));
     if (fb * mine.n > 0) dc.download(h, d_out, fb * mine.n);
     if (rstart[p] > rstart[1]) dc.download(h + rstart[1], d_gather + rstart[1], rstart[p] - rstart[1]);
@@ -414,7 +415,9 @@ DeviceBatchOut device_batch(DeviceComm& dc, DeviceSearch& ds, const RecordBatch*
 // over the comm lane while the next rank's slice is encoded. Each peer learns its plan from a 96-byte
 // message ahead of its pieces (the plan depends on the slice's length range, known after its encode).
 DeviceBatchOut device_batch_text(DeviceComm& dc, DeviceSearch& ds, const BulkParser* parser,
-                                 const std::vector<int64_t>& bounds, const PhaseHooks& hooks, DeviceScratch* scratch) {
+                                 const std::vector<int64_t>& bounds, const PhaseHooks& hooks, DeviceScratch* scratch,
+                                 int64_t record_base, int results_slot) {
+  const int host_results = results_slot ? kHostResults1 : kHostResults;
   std::unique_ptr<DeviceScratch> own;
   if (!scratch) {
     own = std::make_unique<DeviceScratch>(dc);
@@ -534,8 +537,10 @@ DeviceBatchOut device_batch_text(DeviceComm& dc, DeviceSearch& ds, const BulkPar
       block_up[hb] = last;
     }
     hooks.begin("distribute");
-    sc.host(kHostResults, results_bytes(plan) + 16);  // the gather's page-locked buffer, while the blocks move
+    sc.host(host_results, results_bytes(plan) + 16);  // the gather's page-locked buffer, while the blocks move
     if (own_up >= 0) dc.wait_upload(own_up);  // the root's search waits for its own block on the device
+    if (whole.bad_record >= 0) whole.bad_record += record_base;
+    if (whole.long_record >= 0) whole.long_record += record_base;
     try {
       parser->check(whole);
     } catch (const std::exception& e) {
@@ -569,7 +574,7 @@ DeviceBatchOut device_batch_text(DeviceComm& dc, DeviceSearch& ds, const BulkPar
     out.input_error = true;
     return out;
   }
-  solve_gather(dc, ds, sc, plan, plan[rank], d_block, hooks, out);
+  solve_gather(dc, ds, sc, plan, plan[rank], d_block, hooks, out, host_results);
   return out;
 }
 

@@ -533,3 +533,66 @@ def test_text_batch_timing_phases(tmp_path):
         assert ph + "_ms" in d["timing"], (ph, d["timing"])
     assert "parse_ms" in d["timing"] and d["timing"]["parse_ms"] < 1000
     assert sum(d["rank_records"]) == prob.n and d["elements"] == int(prob.offsets[-1]) and d["records"] == prob.n
+
+
+# ---- streamed jobs off the shm transport (flow_device_stream.cpp): the root cuts the batches from the text
+# (pass 1 kept past each cut), device transports encode the ranks' slices straight into their wire blocks,
+# batch b prints while batch b+1 runs; mpi scatters byte-code batches
+
+@pytest.mark.parametrize("np_", [1, 3, 8])
+@pytest.mark.parametrize("tr", ["rccl-emul", "mpi"])
+def test_device_streaming_goldens(np_, tr):
+    for i in range(1, 7):
+        for b in ("--batch-records=2", "--batch-records=3", "--batch-chars=40"):
+            for mode in ("stdin", "input"):
+                args = ["--backend=cpu", f"--transport={tr}", b]
+                if mode == "input":
+                    r = run_final(args + [f"--input={input_path(i)}"], stdin_bytes=b"", np_=np_,
+                                  env={"MOC_SEND_CHUNK": "2640"})
+                else:
+                    r = run_final(args, stdin_path=input_path(i), np_=np_, env={"MOC_SEND_CHUNK": "2640"})
+                assert r.returncode == 0, (i, b, mode, r.stderr.decode())
+                assert r.stdout.decode() == expected(i), (i, b, mode)
+
+
+@pytest.mark.parametrize("tr", ["rccl-emul", "mpi"])
+def test_device_streaming_large_skip_errors(tr, tmp_path):
+    import json
+    import os
+
+    from conftest import ROOT
+
+    from mpi_openmp_cuda_amd import format_results, make_synthetic, search_cpu
+
+    prob = make_synthetic("input6", 300_000, seed=23)
+    text = prob.to_text().encode()
+    path = tmp_path / "in.txt"
+    path.write_bytes(text)
+    want = format_results(search_cpu(prob)).encode()
+    lines = want.splitlines(keepends=True)
+    for extra, np_ in ((["--batch-records=70000", "--timing"], 2), (["--batch-chars=500000"], 3),
+                       (["--batch-records=50000", "--skip-records=123457"], 2)):
+        for src in ("stdin", "input"):
+            args = ["--backend=cpu", f"--transport={tr}"] + extra
+            if src == "input":
+                r = run_final(args + [f"--input={path}"], stdin_bytes=b"", np_=np_, timeout=300)
+            else:  # one singleton rank: mpiexec's stdin forwarding aborts on MBs of input at np > 1
+                r = subprocess.run([os.path.join(ROOT, "final")] + args, input=text, capture_output=True, timeout=300)
+            assert r.returncode == 0, (extra, src, r.stderr.decode())
+            assert r.stdout == (b"".join(lines[123457:]) if "--skip-records=123457" in extra else want), (extra, src)
+            if "--timing" in extra:
+                d = json.loads([ln for ln in r.stderr.decode().splitlines() if ln.startswith("{")][-1])
+                assert d["batches"] == 5 and d["records"] == prob.n and d["elements"] == int(prob.offsets[-1])
+                if tr != "mpi":
+                    assert sum(d["rank_records"]) == prob.n
+    # a bad record in the third batch: the first two batches print, then the error
+    recs = ["ABCDEFGH"] * 12
+    recs[9] = "ABC1DEF"
+    bad = ("1 2 3 4\nABCDEFGHIJ\n12\n" + "\n".join(recs) + "\n").encode()
+    r = run_final(["--backend=cpu", f"--transport={tr}", "--batch-records=4"], stdin_bytes=bad, np_=3)
+    assert r.returncode == 1 and b"record #9 contains a non-letter" in r.stderr, r.stderr.decode()
+    assert r.stdout.decode().count("\n") == 8
+    r = run_final(["--backend=cpu", f"--transport={tr}", "--batch-records=2"],
+                  stdin_bytes=b"1 2 3 4\nABCDEFG\n5\nABC\nABD\nAC\n", np_=2)
+    assert r.returncode == 1 and b"expected 5 Seq2 records, found only 3" in r.stderr
+    assert r.stdout.decode().count("\n") == 2
