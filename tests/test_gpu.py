@@ -722,6 +722,21 @@ def test_final_cli_rccl_device_batches(tmp_path, shape, n, chunk):
     assert r.stdout.decode() == format_results(search_cpu(prob))
 
 
+@pytest.mark.parametrize("extra", [["--batch-records=30000"], ["--batch-chars=200000", "--skip-records=777"]])
+def test_final_cli_rccl_streaming(tmp_path, extra):
+    # the rccl transport streamed (flow_device_stream.cpp): batches cut from the text, encoded into wire blocks,
+    # searched from HBM, results alternating between two page-locked buffers while the previous batch prints
+    prob = make_synthetic("input6", 100_000, seed=3)
+    path = tmp_path / "in.txt"
+    path.write_text(prob.to_text())
+    r = run_final(["--backend=hip", "--transport=rccl", f"--input={path}"] + extra, stdin_bytes=b"", np_=1)
+    assert r.returncode == 0, r.stderr.decode()
+    want = format_results(search_cpu(prob))
+    if "--skip-records=777" in extra:
+        want = "".join(want.splitlines(keepends=True)[777:])
+    assert r.stdout.decode() == want
+
+
 def _long_problem(L1, lengths, seed):
     rng = np.random.default_rng(seed)
     seq1 = rng.integers(1, 27, size=L1, dtype=np.uint8)
