@@ -1,5 +1,6 @@
 """Host sanitizer builds of ./final: ASan/UBSan and TSan (LLVM libomp + Archer) on the
-CPU backend, multi-rank (the sliced shm path, mpi transport), streaming and context-parallel paths — no
+CPU backend, multi-rank (the sliced shm path, mpi transport, the rccl driver over MPI: bulk text batch and
+streamed with the print thread), streaming and context-parallel paths — no
 reports allowed. ASan runs with LeakSanitizer on: every allocation of a job must be released by exit (the
 reference frees nothing, bug B7, main.c:213-240)."""
 import os
@@ -25,7 +26,9 @@ def test_sanitized_final(kind):
         "TSAN_OPTIONS": f"suppressions={ROOT}/tools/tsan.supp halt_on_error=1",
         "OMP_TOOL_LIBRARIES": "/opt/rocm/lib/llvm/lib/libarcher.so"}
     for args, i, np_ in ((["--transport=shm"], 3, 2), (["--transport=shm"], 4, 3),
-                         (["--transport=mpi", "--batch-records=2"], 1, 3), (["--partition=offsets"], 4, 2)):
+                         (["--transport=mpi", "--batch-records=2"], 1, 3), (["--partition=offsets"], 4, 2),
+                         (["--batch-records=2"], 6, 2), (["--transport=rccl-emul"], 6, 3),
+                         (["--transport=rccl-emul", "--batch-records=2"], 3, 2)):
         res = _run(f"final_{kind}", args, i, np_, env)
         err = res.stderr.decode()
         assert res.returncode == 0, err[-3000:]
