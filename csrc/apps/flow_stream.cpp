@@ -146,6 +146,7 @@ void StreamFlow::ensure(RingBuf& b, int64_t bytes, bool pin) {
   b.cap = cap;
   if (pin && pin_) {
     try {
+      b.region.prefault();  // OpenMP threads fault the pages in; the registration would on one thread
       gpu_->pin(b.region.data(), static_cast<size_t>(cap));
       b.unpin = gpu_->detach_pins();
       j_.pinned_bytes += cap;
