@@ -17,18 +17,18 @@
 //   C  fill reports are all-gathered (first input error of the batch, on every rank; result-ring growth).
 //   F  batch b-1's kernel is waited for and the ranks' result descriptors are all-gathered.
 //   D  batch b's kernel is queued on the GPU (it streams slot b % 2 while the host goes on).
-//   E  root prints batch b-1 from the ranks' node-shared result slots (b-1) % 2 on a helper thread, while
-//      batch b streams and batch b+1 is cut and encoded.
-// So the host encodes batch b+1 while the kernel streams batch b and batch b-1's rows are written. Ordering
-// makes the rings safe without extra barriers: a rank rewrites input slot s (batch b+1) only after its own
-// kernel of batch b-1 finished (F, the iteration before), and its result slot s only after the report
-// exchange of batch b+1, which the root enters after its printer finished slot s.
+//   E  root prints batch b-1 from the ranks' node-shared result slots (b-1) % 2, while batch b streams
+//      (on this thread: printing beside the next batch's encode on a helper thread was measured no faster
+//      on the box's 16-CPU share, 0.63-0.72 vs 0.60 s at 1.14 G letters — both use every core,
+//      profiles/final_modes_1.1G_r3f_async_print.log).
+// So the host encodes batch b+1 while the kernel streams batch b, and prints batch b while batch b+1
+// streams. Ordering makes the rings safe without extra barriers: a rank writes slot s again only after
+// the root's broadcast of a later batch, which the root sends after printing the batch that used slot s.
 #include <omp.h>
 
 #include <algorithm>
 #include <cstring>
 #include <deque>
-#include <future>
 
 #include "job.hpp"
 #include "text_cut.hpp"
@@ -103,8 +103,7 @@ class StreamFlow {
   bool fill(const BatchMsg& m, const std::vector<int64_t>& table, int s, Done& d);  // B + C; false: input error
   void launch(int s, Done& d);                         // D
   void finish(int s, Done& d);                         // F
-  void print(int s);                                   // E (root, on a helper thread)
-  void wait_print();                                   // root: the rows of the batch being printed are out
+  void print(int s);                                   // E (root)
 
   JobCore& j_;
   const Header& h_;
@@ -127,8 +126,6 @@ class StreamFlow {
   std::vector<ResultRun> runs_[2];
   int64_t runs_first_[2] = {0, 0};
   std::string error_;
-  std::future<double> printing_;  // root: E of the previous batch (the ms it took)
-  double print_async_ms_ = 0;
   std::vector<double> kernel_ms_;  // per batch (this rank)
   double hidden_ms_ = 0;           // kernel time the host spent on other work (not waiting for it)
 };
@@ -324,10 +321,7 @@ bool StreamFlow::fill(const BatchMsg& m, const std::vector<int64_t>& table, int 
     d.fmt = gpu_->result_format(rep.min_len, rep.max_len);
   }
   j_.pt.end();
-  // ---- C: the batch's first input error, on every rank; result-slot sizes. The root joins its printer
-  // first: no rank passes this exchange (and then writes result slot s) while slot s is still printed.
-  j_.pt.begin("print");
-  wait_print();
+  // ---- C: the batch's first input error, on every rank; result-slot sizes
   j_.pt.begin("report");
   const int fb = result_bytes(d.fmt);
   int64_t mine[9] = {rep.min_len, rep.max_len, rep.bad_record, rep.long_record, rep.long_len, rep.cells,
@@ -433,19 +427,10 @@ void StreamFlow::finish(int s, Done& d) {
 
 void StreamFlow::print(int s) {
   if (j_.ctx.rank != kRoot || runs_[s].empty()) return;
-  wait_print();
-  printing_ = std::async(std::launch::async, [out = j_.out, runs = runs_[s], first = runs_first_[s]]() {
-    Stopwatch sw;
-    sw.start();
-    write_results(out, runs, first);
-    sw.stop();
-    return sw.total_ms();
-  });
+  j_.pt.begin("print");
+  write_results(j_.out, runs_[s], runs_first_[s]);
   runs_[s].clear();
-}
-
-void StreamFlow::wait_print() {
-  if (printing_.valid()) print_async_ms_ += printing_.get();
+  j_.pt.end();
 }
 
 int StreamFlow::run() {
@@ -486,7 +471,6 @@ int StreamFlow::run() {
       launch(s, done[s]);
     }
     if (!ok) {
-      wait_print();  // the batches before the error are out first
       if (ctx.rank == kRoot) std::fprintf(stderr, "input error: %s\n", error_.c_str());
       rc = 1;
       break;
@@ -495,14 +479,6 @@ int StreamFlow::run() {
     next_index_ += m.n;
     have_prev = true;
     ++b;
-  }
-  j_.pt.begin("print");
-  wait_print();
-  j_.pt.end();
-  if (ctx.rank == kRoot) {
-    char buf[32];
-    std::snprintf(buf, sizeof buf, "%.3f", print_async_ms_);
-    j_.extra_timing.emplace_back("print_overlapped_ms", buf);
   }
   if (rc == 0 && ctx.rank == kRoot && next_index_ < h_.n_total) {
     // unreachable: next_batch reports a short input (kept as a guard)
