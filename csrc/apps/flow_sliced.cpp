@@ -180,6 +180,7 @@ void run_sliced(JobCore& job, BulkParser& parser, int64_t first_index, SharedWin
       const int bits = narrow_length_bits(rep.min_len, rep.max_len);
       lens = HostRegion(static_cast<size_t>(narrow_lengths_bytes(n, bits)), numa);
       pack_lengths16(len16.as<uint16_t>(), n, bits, rep.min_len, lens.as<uint8_t>());
+      len16.set_releaser(&job.rel);  // its pages go back to the OS on the releaser thread
       len16 = HostRegion();
       wb.offsets = sparse.as<int64_t>();
       wb.off_shift = kSparseShift;

@@ -58,17 +58,29 @@ void expand_results(const void* in, ResultFormat f, int64_t n, Result* out, cons
 
 namespace {
 // Base-6 words: word w holds records [24w, 24w+24) (digits past n are 0). len(i) - base, i in [0, n).
+// Each field is a sum of independent digit * 6^j terms (no serial Horner chain), and only the last word
+// checks for records past n.
 template <typename LenOf>
 void pack_base6(int64_t n, uint8_t* out, LenOf len_of) {
-  const int64_t words = (n + 23) / 24;
+  static constexpr uint32_t kPow6[8] = {1u, 6u, 36u, 216u, 1296u, 7776u, 46656u, 279936u};
+  const int64_t words = (n + 23) / 24, full = n / 24;
 #pragma omp parallel for schedule(static) if (words > 65536)
-  for (int64_t w = 0; w < words; ++w) {
+  for (int64_t w = 0; w < full; ++w) {
     uint64_t word = 0;
     for (int f = 0; f < 3; ++f) {
       uint32_t v = 0;
-      for (int j = 7; j >= 0; --j) {
+      for (int j = 0; j < 8; ++j) v += static_cast<uint32_t>(len_of(24 * w + 8 * f + j)) * kPow6[j];
+      word |= static_cast<uint64_t>(v) << (21 * f);
+    }
+    std::memcpy(out + 8 * w, &word, 8);
+  }
+  for (int64_t w = full; w < words; ++w) {
+    uint64_t word = 0;
+    for (int f = 0; f < 3; ++f) {
+      uint32_t v = 0;
+      for (int j = 0; j < 8; ++j) {
         const int64_t i = 24 * w + 8 * f + j;
-        v = v * 6u + (i < n ? static_cast<uint32_t>(len_of(i)) : 0u);
+        if (i < n) v += static_cast<uint32_t>(len_of(i)) * kPow6[j];
       }
       word |= static_cast<uint64_t>(v) << (21 * f);
     }

@@ -52,6 +52,12 @@ int main(int argc, char** argv) {
       std::printf("fill pack=%d letters=%lld ms=%.1f GB/s=%.1f\n", pack, static_cast<long long>(s.letters), ms,
                   gb / (ms / 1e3));
     }
+    {  // the sliced path's "wire" step: uint16 lengths -> base-6 narrow lengths
+      std::vector<uint8_t> lens(static_cast<size_t>(moc::narrow_lengths_bytes(s.records, moc::kLenBase6)) + 8);
+      const auto tl = now();
+      moc::pack_lengths16(l16.data(), s.records, moc::kLenBase6, 6, lens.data());
+      std::printf("pack_lengths16 base6 records=%lld ms=%.1f\n", static_cast<long long>(s.records), ms_since(tl));
+    }
     const auto t0 = now();
     p.fill_slice(s, codes.data(), nullptr, offs.data());
     const double ms = ms_since(t0);
