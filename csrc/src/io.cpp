@@ -459,6 +459,21 @@ MOC_AVX512 void stage_flush(const PieceJob& j, PieceOut& po, Stager& st, int64_t
   }
 }
 
+// Record bookkeeping of the per-block path: lengths (and the sparse offsets' record starts) of a piece.
+struct Book {
+  int64_t tok, mn, mx, cells;
+};
+// One record closed by scalar code (a token that crossed a block boundary): letters [start, start + L).
+MOC_AVX512 inline void close_record(Book& bk, const PieceJob& j, int64_t start, int64_t L) {
+  constexpr int64_t kMask = (int64_t{1} << kSparseShift) - 1;
+  bk.mn = std::min(bk.mn, L);
+  bk.mx = std::max(bk.mx, L);
+  bk.cells += L <= j.L1 ? (j.L1 - L + 1) * L : 0;
+  if (j.sparse && (bk.tok & kMask) == 0) j.sparse[bk.tok >> kSparseShift] = start;
+  if (j.len16) j.len16[bk.tok] = static_cast<uint16_t>(L < 65535 ? L : 65535);
+  ++bk.tok;
+}
+
 MOC_AVX512 bool fill_piece_avx512(const PieceJob& j, PieceOut& po) {
   thread_local std::vector<uint8_t> stage_tl;
   if (j.packed && stage_tl.size() < static_cast<size_t>(kStage + 128)) stage_tl.resize(static_cast<size_t>(kStage + 128));
@@ -475,6 +490,20 @@ MOC_AVX512 bool fill_piece_avx512(const PieceJob& j, PieceOut& po) {
   int64_t pos = j.a, tok = j.tok0, cur = -1;
   int64_t mn = INT64_MAX, mx = 0, cells = 0;
   uint64_t prev_ws = 1;
+  // Without dense offsets (the narrow wire form: lengths + sparse offsets) records are booked per block:
+  // the tokens that start and end inside a block get their lengths as (end byte - start byte + 1) from two
+  // vpcompressb of the byte positions, stored as uint16 in one masked store, with min / max / search cells
+  // accumulated in vector registers; only a token crossing a block boundary is closed by scalar code.
+  const bool per_block = offs == nullptr;
+  alignas(64) static constexpr uint8_t kIota[64] = {
+      0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21,
+      22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38, 39, 40, 41, 42, 43,
+      44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 59, 60, 61, 62, 63};
+  const __m512i iota = _mm512_load_si512(reinterpret_cast<const void*>(kIota)), one8 = _mm512_set1_epi8(1);
+  const __m512i vL1 = _mm512_set1_epi64(L1), vL1p1 = _mm512_set1_epi64(L1 + 1);
+  __m512i vmin = _mm512_set1_epi8(static_cast<char>(0xFF)), vmax = _mm512_setzero_si512(), vcells = _mm512_setzero_si512();
+  Book bk{tok, INT64_MAX, 0, 0};
+  int64_t open_len = -1, open_start = 0;  // the token running past the previous block: letters so far, start
   for (size_t i = j.bb; i < j.be; i += 64) {
     const size_t nb = std::min<size_t>(64, j.be - i);
     const __mmask64 in = nb == 64 ? ~__mmask64{0} : (__mmask64{1} << nb) - 1;
@@ -489,6 +518,56 @@ MOC_AVX512 bool fill_piece_avx512(const PieceJob& j, PieceOut& po) {
     if (j.packed && pos - st.base > kStage) stage_flush(j, po, st, pos, false);
     _mm512_mask_storeu_epi8(sink_base + (pos - st.base), cnt == 64 ? ~__mmask64{0} : (__mmask64{1} << cnt) - 1,
                             _mm512_maskz_compress_epi8(nonws, _mm512_and_si512(v, k1F)));
+    if (per_block) {
+      const uint64_t nw = nonws;
+      uint64_t E = nw & ~(nw >> 1) & 0x7FFFFFFFFFFFFFFFull;  // last letter of a token ending in this block
+      if (open_len >= 0) {
+        if (!(nw & 1)) {
+          close_record(bk, j, open_start, open_len);
+          open_len = -1;
+        } else if (E) {
+          close_record(bk, j, open_start, open_len + static_cast<int64_t>(_tzcnt_u64(E)) + 1);
+          E &= E - 1;
+          open_len = -1;
+        } else {
+          open_len += 64;  // no whitespace in the block
+        }
+      }
+      if (starts) {
+        const int ns = static_cast<int>(_mm_popcnt_u64(starts)), ne = static_cast<int>(_mm_popcnt_u64(E));
+        const __m512i sp = _mm512_maskz_compress_epi8(starts, iota);
+        if (ne > 0) {  // ne <= 32: a token and its separator take two bytes at least
+          const __m512i L8 = _mm512_add_epi8(_mm512_sub_epi8(_mm512_maskz_compress_epi8(E, iota), sp), one8);
+          const __mmask64 cm = (__mmask64{1} << ne) - 1;
+          vmin = _mm512_mask_min_epu8(vmin, cm, vmin, L8);
+          vmax = _mm512_mask_max_epu8(vmax, cm, vmax, L8);
+          if (len16)
+            _mm512_mask_storeu_epi16(len16 + bk.tok, static_cast<__mmask32>(cm),
+                                     _mm512_cvtepu8_epi16(_mm512_castsi512_si256(L8)));
+          alignas(64) uint8_t lb[64];
+          _mm512_store_si512(reinterpret_cast<void*>(lb), L8);
+          for (int k = 0; k < ne; k += 8) {  // search cells (L1 + 1 - L) * L of the lengths <= L1
+            const __m512i L = _mm512_cvtepu8_epi64(_mm_loadl_epi64(reinterpret_cast<const __m128i*>(lb + k)));
+            const __mmask8 lm = static_cast<__mmask8>((ne - k >= 8 ? 0xFFu : (1u << (ne - k)) - 1u) &
+                                                      _mm512_cmple_epu64_mask(L, vL1));
+            vcells = _mm512_mask_add_epi64(vcells, lm, vcells, _mm512_mul_epu32(_mm512_sub_epi64(vL1p1, L), L));
+          }
+          const int64_t k0 = (-bk.tok) & kMask;  // the record of this block that opens a sparse entry (if any)
+          if (sparse && k0 < ne) {
+            alignas(64) uint8_t sb[64];
+            _mm512_store_si512(reinterpret_cast<void*>(sb), sp);
+            sparse[(bk.tok + k0) >> kSparseShift] = pos + static_cast<int64_t>(_mm_popcnt_u64(nw & ((uint64_t{1} << sb[k0]) - 1)));
+          }
+          bk.tok += ne;
+        }
+        if (ns > ne) {  // the last token runs to the block end (and possibly past it)
+          open_len = 64 - (63 - static_cast<int64_t>(_lzcnt_u64(starts)));
+          open_start = pos + cnt - open_len;
+        }
+      }
+      pos += cnt;
+      continue;
+    }
     for (uint64_t m = starts; m; m &= m - 1) {
       const int64_t S = pos + static_cast<int64_t>(_mm_popcnt_u64(nonws & (_blsi_u64(m) - 1)));
       if (cur >= 0) {  // the previous token, letters [cur, S), is record `tok`
@@ -505,7 +584,19 @@ MOC_AVX512 bool fill_piece_avx512(const PieceJob& j, PieceOut& po) {
     }
     pos += cnt;
   }
-  if (cur >= 0) {
+  if (per_block) {
+    if (open_len >= 0) close_record(bk, j, open_start, open_len);
+    alignas(64) uint8_t lb[64];
+    _mm512_store_si512(reinterpret_cast<void*>(lb), vmin);
+    uint8_t vmn = 255, vmx = 0;
+    for (int k = 0; k < 64; ++k) vmn = std::min(vmn, lb[k]);
+    _mm512_store_si512(reinterpret_cast<void*>(lb), vmax);
+    for (int k = 0; k < 64; ++k) vmx = std::max(vmx, lb[k]);
+    mn = vmn != 255 ? std::min<int64_t>(bk.mn, vmn) : bk.mn;  // in-block lengths are <= 64: 255 = none
+    mx = std::max<int64_t>(bk.mx, vmx);
+    cells = bk.cells + _mm512_reduce_add_epi64(vcells);
+    tok = bk.tok;
+  } else if (cur >= 0) {
     const int64_t L = pos - cur;
     mn = std::min(mn, L);
     mx = std::max(mx, L);

@@ -588,7 +588,7 @@ void test_slices() {
       std::vector<uint16_t> l16(static_cast<size_t>(s.records) + 1, 0xBEEF);
       std::vector<uint8_t> p3(packed5_bytes(s.letters), 0x33);
       const FillReport r3 = p.fill_slice(s, nullptr, p3.data(), nullptr, sp.data(), l16.data());
-      CHECK(r3.min_len == r.min_len && r3.max_len == r.max_len && p3 == want);
+      CHECK(r3.min_len == r.min_len && r3.max_len == r.max_len && r3.cells == r.cells && p3 == want);
       // ... and with P24 letter groups (groups straddling the parallel pieces assembled afterwards)
       std::vector<uint8_t> p24(static_cast<size_t>(packed24_bytes(s.letters)), 0x24),
           want24(static_cast<size_t>(packed24_bytes(s.letters)));
@@ -600,7 +600,7 @@ void test_slices() {
           want33(static_cast<size_t>(packed33_bytes(s.letters)));
       pack33(ref.seq2.codes.data() + ref.seq2.offsets[b], s.letters, want33.data());
       const FillReport r33 = p.fill_slice(s, nullptr, p33.data(), nullptr, sp.data(), l16.data(), 33);
-      CHECK(r33.min_len == r.min_len && r33.max_len == r.max_len && p33 == want33);
+      CHECK(r33.min_len == r.min_len && r33.max_len == r.max_len && r33.cells == r.cells && p33 == want33);
       ok = true;
       for (size_t j = 0; j < sp.size(); ++j)
         ok = ok && sp[j] == offs[std::min<int64_t>(static_cast<int64_t>(j) << kSparseShift, s.records)];
