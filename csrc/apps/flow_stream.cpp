@@ -128,6 +128,7 @@ class StreamFlow {
   std::string error_;
   std::vector<double> kernel_ms_;  // per batch (this rank)
   double hidden_ms_ = 0;           // kernel time the host spent on other work (not waiting for it)
+  double ring_ms_ = 0, encode_ms_ = 0, lengths_ms_ = 0;  // this rank's fill phase, split (--timing)
 };
 
 void StreamFlow::ensure(RingBuf& b, int64_t bytes, bool pin) {
@@ -137,6 +138,16 @@ void StreamFlow::ensure(RingBuf& b, int64_t bytes, bool pin) {
     b.unpin();
     b.unpin = nullptr;
   }
+  Stopwatch sw;
+  sw.start();
+  struct Stop {  // the allocation's time, whichever way it ends
+    Stopwatch& sw;
+    double& acc;
+    ~Stop() {
+      sw.stop();
+      acc += sw.total_ms();
+    }
+  } stop{sw, ring_ms_};
   const int64_t cap = bytes + bytes / 4;
   b.region = HostRegion(static_cast<size_t>(cap), numa_);
   b.region.set_releaser(&j_.rel);
@@ -287,8 +298,12 @@ bool StreamFlow::fill(const BatchMsg& m, const std::vector<int64_t>& table, int 
       ensure(in.letters, (pack == 33 ? packed33_bytes(slice.letters) : packed24_bytes(slice.letters)) + 16, true);
       ensure(in.sparse, 8 * sparse_count(n, kSparseShift), true);
       ensure(in.len16, 2 * n, false);
+      Stopwatch esw;
+      esw.start();
       rep = bp.fill_slice(slice, nullptr, in.letters.as<uint8_t>(), nullptr, in.sparse.as<int64_t>(),
                           in.len16.as<uint16_t>(), pack);
+      esw.stop();
+      encode_ms_ += esw.total_ms();
       j_.pt.begin("engine_wait");  // the first batch: the engine's start-up, overlapped with the encode
       if (!(rep.max_len <= 255 && gpu_->streams_packed(rep.min_len, rep.max_len))) narrow = false;
       j_.pt.begin("fill");
@@ -309,7 +324,11 @@ bool StreamFlow::fill(const BatchMsg& m, const std::vector<int64_t>& table, int 
     if (narrow) {
       const int bits = narrow_length_bits(rep.min_len, rep.max_len);
       ensure(in.lens, narrow_lengths_bytes(n, bits) + 8, true);
+      Stopwatch lsw;
+      lsw.start();
       pack_lengths16(in.len16.as<uint16_t>(), n, bits, rep.min_len, in.lens.as<uint8_t>());
+      lsw.stop();
+      lengths_ms_ += lsw.total_ms();
       wb.offsets = in.sparse.as<int64_t>();
       wb.off_shift = kSparseShift;
       wb.lengths = in.lens.as<uint8_t>();
@@ -496,6 +515,12 @@ int StreamFlow::run() {
     char buf[64];
     std::snprintf(buf, sizeof buf, "%.3f", hidden_ms_);
     j_.extra_timing.emplace_back("rank0_kernel_hidden_ms", buf);
+  }
+  {
+    char buf[128];
+    std::snprintf(buf, sizeof buf, "{\"ring_alloc\": %.3f, \"encode\": %.3f, \"lengths\": %.3f}", ring_ms_, encode_ms_,
+                  lengths_ms_);
+    j_.extra_timing.emplace_back("rank0_fill_split_ms", buf);
   }
   return rc;
 }
