@@ -70,7 +70,7 @@ class StreamFlow {
   ~StreamFlow() {
     if (gpu_) (void)safe_finish();
     for (auto& s : in_)
-      for (RingBuf* b : {&s.letters, &s.sparse, &s.len16, &s.lens, &s.dense, &s.codes})
+      for (RingBuf* b : {&s.arena, &s.len16, &s.dense, &s.codes})
         if (b->unpin) b->unpin();
     for (auto& u : res_unpin_)
       if (u) u();
@@ -79,7 +79,9 @@ class StreamFlow {
 
  private:
   struct InSlot {
-    RingBuf letters, sparse, len16, lens, dense, codes;
+    RingBuf arena;         // GPU ranks: the wire batch (page-locked)
+    RingBuf len16;         // GPU ranks: the encoder's uint16 lengths
+    RingBuf codes, dense;  // CPU ranks: byte letters + CSR offsets
   };
   // what one rank did with batch b (kept until its results are printed)
   struct Done {
@@ -292,16 +294,25 @@ bool StreamFlow::fill(const BatchMsg& m, const std::vector<int64_t>& table, int 
     ensure(in.dense, 8 * (n + 1), false);
     rep = bp.fill_slice(slice, in.codes.as<uint8_t>(), nullptr, in.dense.as<int64_t>());
   } else if (n > 0) {
+    // one page-locked arena per slot, carved into letters | offsets | lengths: one registration per slot
+    // (each registration costs milliseconds, whatever its size)
+    auto al64 = [](int64_t x) { return (x + 63) & ~int64_t{63}; };
     bool narrow = L1 <= 200 && slice.letters <= 32 * n;
     const int pack = narrow ? j_.group_pack() : 5;
+    uint8_t* letters = nullptr;
+    int64_t* offsets = nullptr;
+    uint8_t* lens = nullptr;
     if (narrow) {
-      ensure(in.letters, (pack == 33 ? packed33_bytes(slice.letters) : packed24_bytes(slice.letters)) + 16, true);
-      ensure(in.sparse, 8 * sparse_count(n, kSparseShift), true);
+      const int64_t lb = al64((pack == 33 ? packed33_bytes(slice.letters) : packed24_bytes(slice.letters)) + 16);
+      const int64_t sb = al64(8 * sparse_count(n, kSparseShift));
+      ensure(in.arena, lb + sb + al64(n + 16), true);  // lengths: at most one byte each (+ slack)
+      letters = in.arena.as<uint8_t>();
+      offsets = reinterpret_cast<int64_t*>(in.arena.as<char>() + lb);
+      lens = in.arena.as<uint8_t>() + lb + sb;
       ensure(in.len16, 2 * n, false);
       Stopwatch esw;
       esw.start();
-      rep = bp.fill_slice(slice, nullptr, in.letters.as<uint8_t>(), nullptr, in.sparse.as<int64_t>(),
-                          in.len16.as<uint16_t>(), pack);
+      rep = bp.fill_slice(slice, nullptr, letters, nullptr, offsets, in.len16.as<uint16_t>(), pack);
       esw.stop();
       encode_ms_ += esw.total_ms();
       j_.pt.begin("engine_wait");  // the first batch: the engine's start-up, overlapped with the encode
@@ -309,33 +320,32 @@ bool StreamFlow::fill(const BatchMsg& m, const std::vector<int64_t>& table, int 
       j_.pt.begin("fill");
     }
     if (!narrow) {  // 5-bit letters + CSR offsets (the staged pipeline's form)
-      ensure(in.letters, packed5_bytes(slice.letters) + 16, true);
-      ensure(in.dense, 8 * (n + 1), true);
-      rep = bp.fill_slice(slice, nullptr, in.letters.as<uint8_t>(), in.dense.as<int64_t>());
+      const int64_t lb = al64(packed5_bytes(slice.letters) + 16);
+      ensure(in.arena, lb + 8 * (n + 1), true);
+      letters = in.arena.as<uint8_t>();
+      offsets = reinterpret_cast<int64_t*>(in.arena.as<char>() + lb);
+      rep = bp.fill_slice(slice, nullptr, letters, offsets);
     }
     WireBatch& wb = d.wb;
-    wb.letters = in.letters.as<uint8_t>();
+    wb.letters = letters;
     wb.packed33 = narrow && pack == 33;
     wb.packed24 = narrow && pack == 24;
     wb.packed5 = !narrow;
     wb.n = n;
     wb.min_l2 = rep.min_len;
     wb.max_l2 = rep.max_len;
+    wb.offsets = offsets;
     if (narrow) {
       const int bits = narrow_length_bits(rep.min_len, rep.max_len);
-      ensure(in.lens, narrow_lengths_bytes(n, bits) + 8, true);
       Stopwatch lsw;
       lsw.start();
-      pack_lengths16(in.len16.as<uint16_t>(), n, bits, rep.min_len, in.lens.as<uint8_t>());
+      pack_lengths16(in.len16.as<uint16_t>(), n, bits, rep.min_len, lens);
       lsw.stop();
       lengths_ms_ += lsw.total_ms();
-      wb.offsets = in.sparse.as<int64_t>();
       wb.off_shift = kSparseShift;
-      wb.lengths = in.lens.as<uint8_t>();
+      wb.lengths = lens;
       wb.len_bits = bits;
       wb.len_base = bits == 8 ? 0 : rep.min_len;
-    } else {
-      wb.offsets = in.dense.as<int64_t>();
     }
     d.fmt = gpu_->result_format(rep.min_len, rep.max_len);
   }
