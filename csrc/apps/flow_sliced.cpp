@@ -87,7 +87,11 @@ void run_sliced(JobCore& job, BulkParser& parser, int64_t first_index, SharedWin
   pt.begin("fill");
   job.fault.at("distribute", r);
   bool narrow = gpu && n > 0 && L1 <= 200 && slice.letters <= 32 * n;
-  HostRegion letters, sparse, len16, dense, lens;
+  // GPU ranks: one NUMA-local region for the wire batch, letters | offsets | lengths (one page-lock
+  // registration for the slice: each costs milliseconds whatever its size)
+  HostRegion wire, len16;
+  auto al64 = [](int64_t x) { return (x + 63) & ~int64_t{63}; };
+  int64_t off_bytes = 0, len_at = 0;  // the offsets' and the lengths' byte offsets in `wire`
   int letters_pack = 5;  // GPU ranks: 33 = P33 fields, 24 = P24 groups, 5 = 5-bit packed
   int64_t letter_bytes = 0;
   RecordBatch cpu_batch;
@@ -100,18 +104,23 @@ void run_sliced(JobCore& job, BulkParser& parser, int64_t first_index, SharedWin
     } else {
       // letters as P33 fields (4.714 bits each; --letters=p24: P24 groups, 4.8) for the streaming kernel,
       // else 5-bit packed
-      const int pack = narrow ? job.group_pack() : 5;
-      const int64_t lbytes = pack == 33   ? packed33_bytes(slice.letters)
-                             : pack == 24 ? packed24_bytes(slice.letters)
-                                          : packed5_bytes(slice.letters);
-      letters = HostRegion(static_cast<size_t>(lbytes) + 16, numa);
-      letters_pack = pack;
-      letter_bytes = lbytes;
+      auto dense_form = [&] {
+        letters_pack = 5;
+        letter_bytes = packed5_bytes(slice.letters);
+        off_bytes = al64(letter_bytes + 16);
+        wire = HostRegion(static_cast<size_t>(off_bytes + 8 * (n + 1)), numa);
+        rep = parser.fill_slice(slice, nullptr, wire.as<uint8_t>(), reinterpret_cast<int64_t*>(wire.data() + off_bytes));
+      };
       if (narrow) {
-        sparse = HostRegion(8 * static_cast<size_t>(sparse_count(n, kSparseShift)), numa);
+        const int pack = job.group_pack();
+        letters_pack = pack;
+        letter_bytes = pack == 33 ? packed33_bytes(slice.letters) : packed24_bytes(slice.letters);
+        off_bytes = al64(letter_bytes + 16);
+        len_at = off_bytes + al64(8 * sparse_count(n, kSparseShift));
+        wire = HostRegion(static_cast<size_t>(len_at + al64(n + 16)), numa);  // lengths: <= 1 byte each
         len16 = HostRegion(2 * static_cast<size_t>(n), numa);
-        rep = parser.fill_slice(slice, nullptr, letters.as<uint8_t>(), nullptr, sparse.as<int64_t>(),
-                                len16.as<uint16_t>(), pack);
+        rep = parser.fill_slice(slice, nullptr, wire.as<uint8_t>(), nullptr,
+                                reinterpret_cast<int64_t*>(wire.data() + off_bytes), len16.as<uint16_t>(), pack);
         // the engine's answer for the lengths seen (waits for its start-up, its own phase): a wrong guess
         // re-encodes the slice as 5-bit letters + CSR offsets NOW, while the input text is still mapped —
         // every rank releases its share of the node-shared text after the report exchange below
@@ -120,17 +129,11 @@ void run_sliced(JobCore& job, BulkParser& parser, int64_t first_index, SharedWin
         pt.begin("fill");
         if (!streams) {
           narrow = false;
-          sparse = HostRegion();
           len16 = HostRegion();
-          dense = HostRegion(8 * (static_cast<size_t>(n) + 1), numa);
-          letter_bytes = packed5_bytes(slice.letters);
-          letters = HostRegion(static_cast<size_t>(letter_bytes) + 16, numa);
-          letters_pack = 5;
-          rep = parser.fill_slice(slice, nullptr, letters.as<uint8_t>(), dense.as<int64_t>());
+          dense_form();
         }
       } else {
-        dense = HostRegion(8 * (static_cast<size_t>(n) + 1), numa);
-        rep = parser.fill_slice(slice, nullptr, letters.as<uint8_t>(), dense.as<int64_t>(), nullptr, nullptr, pack);
+        dense_form();
       }
     }
   }
@@ -169,26 +172,23 @@ void run_sliced(JobCore& job, BulkParser& parser, int64_t first_index, SharedWin
   WireBatch wb;
   ResultFormat fmt = ResultFormat::R12;
   if (gpu && n > 0) {
-    wb.letters = letters.as<uint8_t>();
+    wb.letters = wire.as<uint8_t>();
     wb.packed24 = letters_pack == 24;
     wb.packed33 = letters_pack == 33;
     wb.packed5 = letters_pack == 5;
     wb.n = n;
     wb.min_l2 = rep.min_len;
     wb.max_l2 = rep.max_len;
+    wb.offsets = reinterpret_cast<const int64_t*>(wire.data() + off_bytes);
     if (narrow) {
       const int bits = narrow_length_bits(rep.min_len, rep.max_len);
-      lens = HostRegion(static_cast<size_t>(narrow_lengths_bytes(n, bits)), numa);
-      pack_lengths16(len16.as<uint16_t>(), n, bits, rep.min_len, lens.as<uint8_t>());
+      pack_lengths16(len16.as<uint16_t>(), n, bits, rep.min_len, wire.as<uint8_t>() + len_at);
       len16.set_releaser(&job.rel);  // its pages go back to the OS on the releaser thread
       len16 = HostRegion();
-      wb.offsets = sparse.as<int64_t>();
       wb.off_shift = kSparseShift;
-      wb.lengths = lens.as<uint8_t>();
+      wb.lengths = wire.as<uint8_t>() + len_at;
       wb.len_bits = bits;
       wb.len_base = bits == 8 ? 0 : rep.min_len;
-    } else {
-      wb.offsets = dense.as<int64_t>();
     }
     fmt = eng.hip->result_format(rep.min_len, rep.max_len);
   }
@@ -238,9 +238,7 @@ void run_sliced(JobCore& job, BulkParser& parser, int64_t first_index, SharedWin
           job.pinned_bytes += bytes;
         }
       };
-      pin(wb.letters, letter_bytes);
-      pin(wb.offsets, 8 * wb.offset_entries());
-      pin(wb.lengths, wb.length_bytes());
+      pin(wire.data(), static_cast<int64_t>(wire.size()));  // letters, offsets and lengths at once
       pin(res_mine, fb * n);
     } catch (const std::exception& e) {
       MOC_LOG_WARN("could not page-lock this rank's slice (%s); using the staged pipeline", e.what());
@@ -272,11 +270,8 @@ void run_sliced(JobCore& job, BulkParser& parser, int64_t first_index, SharedWin
   // dropped first (the releaser runs its tasks in order), then the pages
   pt.begin("drop");
   if (gpu) job.rel.defer(eng.hip->detach_pins());
-  letters.set_releaser(&job.rel);
-  sparse.set_releaser(&job.rel);
-  dense.set_releaser(&job.rel);
-  lens.set_releaser(&job.rel);
-  { HostRegion drop[4] = {std::move(letters), std::move(sparse), std::move(dense), std::move(lens)}; }
+  wire.set_releaser(&job.rel);
+  { HostRegion drop = std::move(wire); }
   if (!cpu_batch.codes.empty()) {
     auto spent = std::make_shared<RecordBatch>(std::move(cpu_batch));
     job.rel.defer([spent]() mutable { spent.reset(); });
