@@ -238,7 +238,8 @@ void run_sliced(JobCore& job, BulkParser& parser, int64_t first_index, SharedWin
           job.pinned_bytes += bytes;
         }
       };
-      pin(wire.data(), static_cast<int64_t>(wire.size()));  // letters, offsets and lengths at once
+      // letters, offsets and lengths at once: the region's used prefix (the lengths took their narrow size)
+      pin(wire.data(), narrow ? len_at + wb.length_bytes() : off_bytes + 8 * (n + 1));
       pin(res_mine, fb * n);
     } catch (const std::exception& e) {
       MOC_LOG_WARN("could not page-lock this rank's slice (%s); using the staged pipeline", e.what());
