@@ -131,6 +131,7 @@ class StreamFlow {
   std::vector<double> kernel_ms_;  // per batch (this rank)
   double hidden_ms_ = 0;           // kernel time the host spent on other work (not waiting for it)
   double ring_ms_ = 0, encode_ms_ = 0, lengths_ms_ = 0;  // this rank's fill phase, split (--timing)
+  double ring_fault_ms_ = 0, ring_pin_ms_ = 0;            // ... and the ring allocation's page faults / pins
 };
 
 void StreamFlow::ensure(RingBuf& b, int64_t bytes, bool pin) {
@@ -156,8 +157,16 @@ void StreamFlow::ensure(RingBuf& b, int64_t bytes, bool pin) {
   b.cap = cap;
   if (pin && pin_) {
     try {
+      Stopwatch t;
+      t.start();
       b.region.prefault();  // OpenMP threads fault the pages in; the registration would on one thread
+      t.stop();
+      ring_fault_ms_ += t.total_ms();
+      Stopwatch t2;
+      t2.start();
       gpu_->pin(b.region.data(), static_cast<size_t>(cap));
+      t2.stop();
+      ring_pin_ms_ += t2.total_ms();
       b.unpin = gpu_->detach_pins();
       j_.pinned_bytes += cap;
     } catch (const std::exception& e) {
@@ -527,9 +536,10 @@ int StreamFlow::run() {
     j_.extra_timing.emplace_back("rank0_kernel_hidden_ms", buf);
   }
   {
-    char buf[128];
-    std::snprintf(buf, sizeof buf, "{\"ring_alloc\": %.3f, \"encode\": %.3f, \"lengths\": %.3f}", ring_ms_, encode_ms_,
-                  lengths_ms_);
+    char buf[192];
+    std::snprintf(buf, sizeof buf,
+                  "{\"ring_alloc\": %.3f, \"ring_fault\": %.3f, \"ring_pin\": %.3f, \"encode\": %.3f, \"lengths\": %.3f}",
+                  ring_ms_, ring_fault_ms_, ring_pin_ms_, encode_ms_, lengths_ms_);
     j_.extra_timing.emplace_back("rank0_fill_split_ms", buf);
   }
   return rc;
