@@ -27,6 +27,10 @@ void mpi_check(int rc, const char* what) {
 
 #define MOC_MPI_CHECK(call) ::moc::mpi_check((call), #call)
 
+void mpi_prepare_env(bool lean_topology) {
+  if (lean_topology) setenv("HWLOC_COMPONENTS", "-x86,-linuxio", 0);
+}
+
 MpiContext::MpiContext(int* argc, char*** argv) {
   int provided = 0;
   MPI_Init_thread(argc, argv, MPI_THREAD_FUNNELED, &provided);

@@ -596,3 +596,32 @@ def test_device_streaming_large_skip_errors(tr, tmp_path):
                   stdin_bytes=b"1 2 3 4\nABCDEFG\n5\nABC\nABD\nAC\n", np_=2)
     assert r.returncode == 1 and b"expected 5 Seq2 records, found only 3" in r.stderr
     assert r.stdout.decode().count("\n") == 2
+
+
+def _hwloc_components(stderr):
+    for line in stderr.decode(errors="replace").splitlines():
+        if line.startswith("Final list of enabled discovery components:"):
+            return set(line.split(":", 1)[1].strip().split(","))
+    return None
+
+
+@pytest.mark.parametrize("np_", [1, 2])
+def test_mpi_topology_lean_vs_full(np_):
+    # MPI_Init's host discovery (MPICH's embedded hwloc): lean drops the per-PU cpuid and the PCI scan
+    # (profiles/mpi_init_variants_box.log: 200 -> 29 ms on the MI355X box), full keeps MPI's default, and a
+    # HWLOC_COMPONENTS the user set wins; the results are the same either way
+    verbose = {"HWLOC_COMPONENTS_VERBOSE": "1"}
+    lean = run_final(["--backend=cpu"], stdin_path=input_path(6), np_=np_, env=verbose)
+    full = run_final(["--backend=cpu", "--mpi-topology=full"], stdin_path=input_path(6), np_=np_, env=verbose)
+    user = run_final(["--backend=cpu"], stdin_path=input_path(6), np_=np_,
+                     env=dict(verbose, HWLOC_COMPONENTS="-linuxio"))
+    for r in (lean, full, user):
+        assert r.returncode == 0 and r.stdout.decode() == expected(6), r.stderr[-400:]
+    cl, cf, cu = (_hwloc_components(r.stderr) for r in (lean, full, user))
+    if cf is None:
+        pytest.skip("this MPI does not report its hwloc discovery components")
+    assert "x86" in cf and "linuxio" in cf
+    assert "x86" not in cl and "linuxio" not in cl and "linux" in cl
+    assert "x86" in cu and "linuxio" not in cu
+    bad = run_final(["--mpi-topology=fast"], stdin_path=input_path(6))
+    assert bad.returncode == 2 and b"--mpi-topology" in bad.stderr
