@@ -96,8 +96,8 @@ const char* kUsage =
     "  --pin-window=0|1            page-lock the GPU ranks' slices so they stream zero-copy (default 1)\n"
     "  --chunk-records=R --chunk-bytes=B   pipeline chunk sizes\n"
     "  --threads=T                 OpenMP threads (default: OMP_NUM_THREADS / all)\n"
-    "  --mpi-topology=lean|full    lean (default): MPI_Init skips the host's cpuid and PCI-device discovery\n"
-    "                              (0.17-0.22 s of a tiny job on a 256-CPU node); full: MPI's own default\n"
+    "  --mpi-topology=lean|full    lean (default): MPI_Init skips the host's hardware discovery (CPUs, caches,\n"
+    "                              PCI devices: 0.2-0.35 s of a tiny job on a 256-CPU node); full: MPI's own\n"
     "  --log-level=error|warn|info|debug\n"
     "  --inject-fault=PHASE[:RANK] test hook: fail at parse|bcast|distribute|compute|gather\n"
     "every flag can also be given as environment variable MOC_<FLAG> (e.g. MOC_BACKEND=cpu)\n";

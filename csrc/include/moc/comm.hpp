@@ -27,11 +27,13 @@ namespace moc {
 
 // MPI start-up without the hardware discovery nothing here uses. MPICH's MPI_Init loads a full hwloc
 // topology of the host: on the MI355X box (256 PUs, 367 PCI devices) that is 170-220 ms of a tiny job's
-// ~210 ms — the `x86` component binds to every PU to run cpuid (~50 ms) and `linuxio` scans every PCI
-// device (~110 ms); without both MPI_Init takes 26-29 ms (profiles/mpi_init_variants_box.log). Nothing
-// in this framework reads MPI's topology: devices come from the node-local rank and NUMA placement from
-// the device's own sysfs node. `full` keeps the launcher's discovery; a HWLOC_COMPONENTS the user set is
-// always kept. Call before any other thread starts (setenv).
+// ~210 ms at one rank and 350 ms at eight — the `x86` component binds to every PU to run cpuid, `linuxio`
+// scans every PCI device, `linux` reads every PU's sysfs topology (and eight ranks do it at once). With
+// hwloc's `no_os` component alone (a flat topology from the CPU count) MPI_Init takes 2-4 ms at 1-8 ranks
+// (profiles/mpi_init_variants_box.log, profiles/mpi_init_floor_box.log). Nothing in this framework reads
+// MPI's topology: ranks find their node through MPI_COMM_TYPE_SHARED, their device from the node-local
+// rank and their NUMA node from the device's own sysfs entry. `full` keeps MPI's discovery; a
+// HWLOC_COMPONENTS the user set is always kept. Call before any other thread starts (setenv).
 void mpi_prepare_env(bool lean_topology);
 
 class MpiContext {

@@ -28,7 +28,7 @@ void mpi_check(int rc, const char* what) {
 #define MOC_MPI_CHECK(call) ::moc::mpi_check((call), #call)
 
 void mpi_prepare_env(bool lean_topology) {
-  if (lean_topology) setenv("HWLOC_COMPONENTS", "-x86,-linuxio", 0);
+  if (lean_topology) setenv("HWLOC_COMPONENTS", "no_os,stop", 0);
 }
 
 MpiContext::MpiContext(int* argc, char*** argv) {
