@@ -421,8 +421,16 @@ int Job::run() {
   seq1.resize(static_cast<size_t>(h.L1));
   bcast_bytes(seq1.data(), h.L1, kRoot, ctx.world);
   pt.end();
-  pt.begin("gpu_wait");  // the HIP runtime's start-up, when a helper thread began it during the read
-  if (prewarm_.valid()) prewarm_.get();
+  // A job that connects RCCL first lets the warm-up communicator of early_prewarm finish. Other GPU jobs do
+  // not wait here: the HIP runtime keeps starting on the helper thread while the ranks count and encode,
+  // and the engine's own helper thread is the first to need it.
+  pt.begin("gpu_wait");
+  {
+    const std::string tr = to_lower(flags.get("transport", "auto"));
+    const bool rccl_job = tr == "rccl" || to_lower(flags.get("collectives", "auto")) == "rccl" ||
+                          (tr == "auto" && !ctx.single_node());
+    if (prewarm_.valid() && rccl_job) prewarm_.get();
+  }
   pt.end();
   pt.begin("setup");
   job_.setup_engine(h.cells, h.mean_l2);  // collective: engine kind, transport, RCCL communicator

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <atomic>
 #include <future>
 #include <memory>
 #include <mutex>
@@ -19,6 +20,7 @@
 #include "moc/runtime/device.hpp"
 #include "moc/runtime/hip_check.hpp"
 #include "moc/runtime/host_region.hpp"
+#include "moc/runtime/kfd_topology.hpp"
 #include "moc/runtime/log.hpp"
 #include "moc/runtime/pinned.hpp"
 #include "moc/runtime/timer.hpp"
@@ -199,7 +201,10 @@ class HipDeviceSearch final : public DeviceSearch {
 // The HIP engine's construction (streams, events, device buffers, kernel code objects: 0.1-0.2 s on the
 // MI355X box, tools/init_probe.cpp) runs on a helper thread started by the constructor, so it overlaps the
 // rank's pass 1 and slice encoding; the first call that needs the engine waits for it. set_problem before
-// that point is kept and applied when the engine is ready.
+// that point is kept and applied when the engine is ready. When the driver's topology names the rank's
+// GPU (moc/runtime/kfd_topology.hpp) the HIP runtime's own start-up (140-220 ms,
+// profiles/hip_init_variants_box.log) moves onto that thread too: the device and its NUMA node come from
+// sysfs, and the helper finds the same device in the runtime by its PCIe address.
 class GpuRankImpl final : public GpuRank {
  public:
   GpuRankImpl(const MpiContext& ctx, const GpuRankOptions& opt) : ctx_(ctx) {
@@ -208,15 +213,43 @@ class GpuRankImpl final : public GpuRank {
     int requested = opt.device;
     if (requested < 0 && !opt.device_map.empty())
       requested = opt.device_map[static_cast<size_t>(ctx.local_rank) % opt.device_map.size()];
-    device_ = select_device(ctx.local_rank, requested);
     EngineOptions eo;
-    eo.device = device_;
     if (opt.chunk_records > 0) eo.chunk_records = opt.chunk_records;
     if (opt.chunk_bytes > 0) eo.chunk_bytes = opt.chunk_bytes;
-    pending_engine_ = std::async(std::launch::async, [eo] { return std::make_unique<HipEngine>(eo); });
-    // host buffers this rank's GPU streams over PCIe, and the threads that fill them, on the NUMA node
-    // of the GPU's root complex (this, the calling thread)
-    numa_ = bind_numa_to_device(device_);
+    std::string bus;  // the PCIe address of the device chosen from the topology
+    if (const auto kfd = kfd_gpus(); kfd && !kfd->empty()) {
+      const int n = static_cast<int>(kfd->size());
+      const int id = requested >= 0 ? requested : ctx.local_rank % n;
+      if (id < n) {
+        device_ = id;
+        bus = (*kfd)[static_cast<size_t>(id)].pci_bus_id;
+        // host buffers this rank's GPU streams over PCIe, and the threads that fill them, on the NUMA node
+        // of the GPU's root complex (this, the calling thread)
+        numa_ = bind_numa_node((*kfd)[static_cast<size_t>(id)].numa_node);
+      }
+    }
+    if (device_ < 0) {  // the runtime's answer, on this thread
+      device_ = select_device(ctx.local_rank, requested);
+      numa_ = bind_numa_to_device(device_);
+      bus.clear();
+    }
+    eo.device = device_;
+    const int local = ctx.local_rank;
+    pending_engine_ = std::async(std::launch::async, [this, eo, bus, local, requested]() mutable {
+      if (!bus.empty()) {
+        int id = -1;
+        const int n = device_count();
+        for (int i = 0; i < n && id < 0; ++i)
+          if (device_info(i).pci_bus_id == bus) id = i;
+        if (id < 0) id = select_device(local, requested);
+        if (id != eo.device)
+          MOC_LOG_WARN("the HIP runtime lists device %s as %d, the driver topology as %d: using %d", bus.c_str(), id,
+                       eo.device, id);
+        eo.device = id;
+        device_.store(id);
+      }
+      return std::make_unique<HipEngine>(eo);
+    });
   }
   ~GpuRankImpl() override {
     ds_.reset();
@@ -227,7 +260,8 @@ class GpuRankImpl final : public GpuRank {
     if (dc_ || pending_.valid()) return;
     const ncclUniqueId id = RcclComm::exchange_id(ctx_);  // MPI: this (the main) thread
     pending_ = std::async(std::launch::async, [this, id] {
-      return std::make_unique<RcclDeviceComm>(ctx_, device_, engine().compute_stream(), id);
+      HipEngine& e = engine();  // resolves the device first
+      return std::make_unique<RcclDeviceComm>(ctx_, device_.load(), e.compute_stream(), id);
     });
   }
   void init_rccl() override {
@@ -239,13 +273,15 @@ class GpuRankImpl final : public GpuRank {
   }
   DeviceComm& device_comm() override {
     init_rccl();
+    bind_thread();
     return *dc_;
   }
   DeviceSearch& device_search() override {
     init_rccl();
+    bind_thread();
     return *ds_;
   }
-  int device() const override { return device_; }
+  int device() const override { return device_.load(); }
   void set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, Semantics sem) override {
     std::lock_guard<std::mutex> lock(mu_);
     if (engine_) {
@@ -290,7 +326,7 @@ class GpuRankImpl final : public GpuRank {
   void unpin_all() override { engine().unpin_all(); }
   std::function<void()> detach_pins() override {
     auto regs = std::make_shared<std::vector<void*>>(engine().detach_pins());
-    const int dev = device_;
+    const int dev = device_.load();
     return [regs, dev] {
       (void)hipSetDevice(dev);
       pinned::unregister(*regs);
@@ -321,11 +357,23 @@ class GpuRankImpl final : public GpuRank {
       engine_ = std::move(e);
     });
     if (!engine_) throw Error("the HIP engine failed to start: " + start_error_);
+    bind_thread();
     return *engine_;
   }
 
+  // the calling thread's current HIP device = this rank's (the runtime keeps one per thread; the engine
+  // may have started on another thread)
+  void bind_thread() const {
+    thread_local int current = -1;
+    const int d = device_.load();
+    if (current != d) {
+      MOC_HIP_CHECK(hipSetDevice(d));
+      current = d;
+    }
+  }
+
   const MpiContext& ctx_;
-  int device_ = -1;
+  std::atomic<int> device_{-1};
   int numa_ = -1;
   mutable std::future<std::unique_ptr<HipEngine>> pending_engine_;
   mutable std::once_flag ready_;

@@ -63,6 +63,9 @@ std::vector<int> parse_int_list(const std::string& s);
 
 // The GPU plugin (moc/gpu_rank.hpp), loaded on the first question about GPUs.
 int gpu_device_count();
+// GPUs this rank may open, from the driver's topology when it is readable (no HIP runtime start-up), else
+// gpu_device_count()
+int gpu_device_count_fast();
 std::string gpu_plugin_error();
 // RCCL's one-time start-up (library load + code objects) on `device`, for a helper thread (false: none).
 bool gpu_rccl_warmup(int device);

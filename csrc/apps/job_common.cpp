@@ -11,6 +11,7 @@
 #include <sstream>
 
 #include "job.hpp"
+#include "moc/runtime/kfd_topology.hpp"
 #include "moc/runtime/log.hpp"
 
 namespace moc {
@@ -76,6 +77,14 @@ const GpuPlugin& gpu_plugin() {
 int gpu_device_count() {
   const GpuPlugin& g = gpu_plugin();
   return g.device_count && g.create ? g.device_count() : 0;
+}
+int gpu_device_count_fast() {
+  if (const auto kfd = kfd_gpus()) {
+    if (kfd->empty()) return 0;
+    const GpuPlugin& g = gpu_plugin();  // loads the plugin (~13 ms), not the runtime
+    return g.device_count && g.create ? static_cast<int>(kfd->size()) : 0;
+  }
+  return gpu_device_count();
 }
 std::string gpu_plugin_error() { return gpu_plugin().error; }
 bool gpu_rccl_warmup(int device) {
@@ -147,7 +156,9 @@ void JobCore::setup_engine(int64_t job_cells, int64_t mean_l2) {
   const int64_t model_min = static_cast<int64_t>(0.2 * per_thread * std::max(1, omp_get_max_threads()));
   const int64_t min_cells = flags.get_int("gpu-min-cells", model_min);
   if (backend == "auto" && job_cells >= 0 && job_cells < min_cells * ctx.size) backend = "cpu";
-  const int ndev = (backend == "cpu") ? 0 : gpu_device_count();
+  // the driver's topology answers without waiting for the HIP runtime, which starts on the engine's helper
+  // thread behind the parse and the encode (moc/runtime/kfd_topology.hpp)
+  const int ndev = (backend == "cpu") ? 0 : gpu_device_count_fast();
   if (backend == "hip" && ndev == 0)
     throw Error("--backend=hip but no HIP device is visible" +
                 (gpu_plugin_error().empty() ? std::string() : " (" + gpu_plugin_error() + ")"));

@@ -1,0 +1,42 @@
+// The GPUs this process can open, read from the amdgpu kernel driver's topology in sysfs, without starting
+// the HIP runtime. The runtime's start-up (hipGetDeviceCount) costs 140-220 ms on the MI355X box
+// (profiles/hip_init_variants_box.log); `final` needs only "how many GPUs, and which NUMA node is mine"
+// to pick its engine, wire formats and device, so a GPU rank decides from here and lets the runtime start
+// on a helper thread behind the parse and the encode (csrc/apps/final_gpu.cpp).
+//
+// A GPU is a topology node (/sys/class/kfd/kfd/topology/nodes/N/properties) with simd_count > 0 whose
+// render node /dev/dri/renderD<drm_render_minor> this process may open — the runtime's own filter (a box
+// exposes 1 of its host's 8 GPUs that way). Devices are listed in node order, the runtime's device order.
+// When HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES / GPU_DEVICE_ORDINAL re-map the
+// devices only the runtime knows the mapping: kfd_gpus() then answers nullopt, as it does when the
+// topology or /dev/kfd is missing.
+#pragma once
+
+#include <optional>
+#include <string>
+#include <vector>
+
+namespace moc {
+
+struct KfdGpu {
+  int node = -1;           // KFD topology node id
+  int render_minor = -1;   // /dev/dri/renderD<minor>
+  std::string pci_bus_id;  // "dddd:bb:dd.f" (lower case), from the node's domain + location_id
+  int numa_node = -1;      // NUMA node of its PCIe function (/sys/bus/pci/devices/<id>/numa_node), -1 unknown
+};
+
+struct KfdPaths {
+  std::string nodes = "/sys/class/kfd/kfd/topology/nodes";
+  std::string kfd = "/dev/kfd";
+  std::string dri = "/dev/dri";
+  std::string pci = "/sys/bus/pci/devices";
+  bool honour_visible_env = true;  // tests point the paths at a fake tree and switch this off
+};
+
+std::optional<std::vector<KfdGpu>> kfd_gpus(const KfdPaths& paths = KfdPaths());
+
+// Binds the calling thread's CPUs (sched_setaffinity) and its future page allocations (set_mempolicy
+// MPOL_PREFERRED) to NUMA node `node`. Returns the node, or -1 if nothing was changed.
+int bind_numa_node(int node);
+
+}  // namespace moc

@@ -1,15 +1,13 @@
 #include "moc/runtime/device.hpp"
 
 #include <hip/hip_runtime_api.h>
-#include <sched.h>
-#include <sys/syscall.h>
-#include <unistd.h>
 
 #include <cctype>
 #include <fstream>
 #include <sstream>
 
 #include "moc/runtime/hip_check.hpp"
+#include "moc/runtime/kfd_topology.hpp"
 
 namespace moc {
 
@@ -66,35 +64,7 @@ int device_numa_node(int device) {
   return node;
 }
 
-int bind_numa_to_device(int device) {
-  const int node = device_numa_node(device);
-  if (node < 0) return -1;
-  std::ifstream f("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist");
-  std::string list;
-  if (!(f >> list)) return -1;
-  cpu_set_t set;
-  CPU_ZERO(&set);
-  int ncpu = 0;
-  std::stringstream ss(list);
-  std::string part;
-  while (std::getline(ss, part, ',')) {
-    const auto dash = part.find('-');
-    const int a = std::stoi(part.substr(0, dash));
-    const int b = dash == std::string::npos ? a : std::stoi(part.substr(dash + 1));
-    for (int c = a; c <= b && c < CPU_SETSIZE; ++c) {
-      CPU_SET(c, &set);
-      ++ncpu;
-    }
-  }
-  if (ncpu == 0) return -1;
-  if (sched_setaffinity(0, sizeof set, &set) != 0) return -1;
-  unsigned long mask[16] = {0};
-  if (node >= static_cast<int>(sizeof(mask) * 8)) return node;
-  mask[node / (8 * sizeof(unsigned long))] |= 1ul << (node % (8 * sizeof(unsigned long)));
-  constexpr int kMpolPreferred = 1;
-  syscall(SYS_set_mempolicy, kMpolPreferred, mask, sizeof(mask) * 8);  // best effort
-  return node;
-}
+int bind_numa_to_device(int device) { return bind_numa_node(device_numa_node(device)); }
 
 int select_device(int local_rank, int requested) {
   const int n = device_count();

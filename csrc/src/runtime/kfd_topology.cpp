@@ -1,0 +1,109 @@
+#include "moc/runtime/kfd_topology.hpp"
+
+#include <dirent.h>
+#include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <sstream>
+
+namespace moc {
+
+namespace {
+
+// "name value" lines of a topology node's properties file
+bool read_properties(const std::string& path, int64_t& simd, int64_t& minor, int64_t& domain, int64_t& location) {
+  std::ifstream f(path);
+  if (!f) return false;
+  std::string key;
+  int64_t v = 0;
+  simd = 0;
+  minor = domain = location = -1;
+  while (f >> key >> v) {
+    if (key == "simd_count") simd = v;
+    else if (key == "drm_render_minor") minor = v;
+    else if (key == "domain") domain = v;
+    else if (key == "location_id") location = v;
+  }
+  return true;
+}
+
+}  // namespace
+
+std::optional<std::vector<KfdGpu>> kfd_gpus(const KfdPaths& paths) {
+  if (paths.honour_visible_env) {
+    for (const char* var : {"HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL"})
+      if (std::getenv(var)) return std::nullopt;
+  }
+  DIR* d = opendir(paths.nodes.c_str());
+  if (!d) return std::nullopt;
+  std::vector<int> ids;
+  while (const dirent* e = readdir(d)) {
+    char* end = nullptr;
+    const long id = std::strtol(e->d_name, &end, 10);
+    if (end != e->d_name && *end == '\0') ids.push_back(static_cast<int>(id));
+  }
+  closedir(d);
+  std::sort(ids.begin(), ids.end());
+  std::vector<KfdGpu> gpus;
+  if (access(paths.kfd.c_str(), R_OK | W_OK) != 0) return gpus;  // no driver access: the runtime sees none
+  for (int id : ids) {
+    int64_t simd = 0, minor = -1, domain = -1, location = -1;
+    if (!read_properties(paths.nodes + "/" + std::to_string(id) + "/properties", simd, minor, domain, location))
+      return std::nullopt;  // a node that cannot be read: leave the answer to the runtime
+    if (simd <= 0) continue;  // a CPU node
+    if (minor < 0) return std::nullopt;
+    const std::string render = paths.dri + "/renderD" + std::to_string(minor);
+    if (access(render.c_str(), R_OK | W_OK) != 0) continue;  // another tenant's GPU
+    KfdGpu g;
+    g.node = id;
+    g.render_minor = static_cast<int>(minor);
+    if (domain >= 0 && location >= 0) {
+      char bus[32];
+      std::snprintf(bus, sizeof bus, "%04x:%02x:%02x.%x", static_cast<unsigned>(domain),
+                    static_cast<unsigned>((location >> 8) & 0xff), static_cast<unsigned>((location >> 3) & 0x1f),
+                    static_cast<unsigned>(location & 7));
+      g.pci_bus_id = bus;
+      std::ifstream nf(paths.pci + "/" + g.pci_bus_id + "/numa_node");
+      int node = -1;
+      if (nf >> node) g.numa_node = node;
+    }
+    gpus.push_back(std::move(g));
+  }
+  return gpus;
+}
+
+int bind_numa_node(int node) {
+  if (node < 0) return -1;
+  std::ifstream f("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist");
+  std::string list;
+  if (!(f >> list)) return -1;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  int ncpu = 0;
+  std::stringstream ss(list);
+  std::string part;
+  while (std::getline(ss, part, ',')) {
+    const auto dash = part.find('-');
+    const int a = std::stoi(part.substr(0, dash));
+    const int b = dash == std::string::npos ? a : std::stoi(part.substr(dash + 1));
+    for (int c = a; c <= b && c < CPU_SETSIZE; ++c) {
+      CPU_SET(c, &set);
+      ++ncpu;
+    }
+  }
+  if (ncpu == 0) return -1;
+  if (sched_setaffinity(0, sizeof set, &set) != 0) return -1;
+  unsigned long mask[16] = {0};
+  if (node >= static_cast<int>(sizeof(mask) * 8)) return node;
+  mask[node / (8 * sizeof(unsigned long))] |= 1ul << (node % (8 * sizeof(unsigned long)));
+  constexpr int kMpolPreferred = 1;
+  syscall(SYS_set_mempolicy, kMpolPreferred, mask, sizeof(mask) * 8);  // best effort
+  return node;
+}
+
+}  // namespace moc

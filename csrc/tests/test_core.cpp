@@ -1,6 +1,7 @@
 // Native unit tests of the host core (SURVEY.md §4.3 "unit (C++)"): score table vs the spec groups,
 // parser and streaming reader edge cases, partitioner, packed-key ordering, 5-bit packing, CPU engine vs
 // the brute-force replay of the reference loops. No GPU, no MPI. Run: `make unit` or `ctest`.
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -16,6 +17,7 @@
 #include "moc/io.hpp"
 #include "moc/partition.hpp"
 #include "moc/problem.hpp"
+#include "moc/runtime/kfd_topology.hpp"
 #include "moc/runtime/releaser.hpp"
 #include "moc/score_table.hpp"
 #include "moc/wire.hpp"
@@ -757,6 +759,70 @@ void test_write_runs() {
   }
 }
 
+// GPUs from a fake driver topology: CPU nodes skipped, render nodes this process cannot open skipped,
+// nodes in numeric order (10 after 2), PCIe address and NUMA node from domain + location_id
+void test_kfd_topology() {
+  char tmpl[] = "/tmp/moc_kfd_XXXXXX";
+  const char* root_c = mkdtemp(tmpl);
+  CHECK(root_c != nullptr);
+  if (!root_c) return;
+  const std::string root = root_c;
+  auto put = [](const std::string& path, const std::string& text) {
+    FILE* f = std::fopen(path.c_str(), "w");
+    if (!f) return;
+    std::fputs(text.c_str(), f);
+    std::fclose(f);
+  };
+  auto node = [&](int id, const std::string& props) {
+    const std::string d = root + "/nodes/" + std::to_string(id);
+    mkdir(d.c_str(), 0755);
+    put(d + "/properties", props);
+  };
+  mkdir((root + "/nodes").c_str(), 0755);
+  mkdir((root + "/dri").c_str(), 0755);
+  mkdir((root + "/pci").c_str(), 0755);
+  mkdir((root + "/pci/0000:0d:00.0").c_str(), 0755);
+  put(root + "/pci/0000:0d:00.0/numa_node", "1\n");
+  node(0, "cpu_cores_count 64\nsimd_count 0\nlocation_id 0\ndomain 0\n");
+  node(2, "simd_count 1024\ndrm_render_minor 129\nlocation_id 7424\ndomain 0\n");   // 1d:00.0, not ours
+  node(10, "simd_count 1024\ndrm_render_minor 130\nlocation_id 34816\ndomain 1\n");  // 0001:88:00.0
+  node(3, "simd_count 1024\ndrm_render_minor 128\nlocation_id 3328\ndomain 0\n");   // 0000:0d:00.0
+  put(root + "/dri/renderD128", "");
+  put(root + "/dri/renderD130", "");
+  put(root + "/kfd", "");
+  KfdPaths p;
+  p.nodes = root + "/nodes";
+  p.kfd = root + "/kfd";
+  p.dri = root + "/dri";
+  p.pci = root + "/pci";
+  p.honour_visible_env = false;
+  auto g = kfd_gpus(p);
+  CHECK(g.has_value() && g->size() == 2);
+  if (g && g->size() == 2) {
+    CHECK((*g)[0].node == 3 && (*g)[0].render_minor == 128 && (*g)[0].pci_bus_id == "0000:0d:00.0" &&
+          (*g)[0].numa_node == 1);
+    CHECK((*g)[1].node == 10 && (*g)[1].pci_bus_id == "0001:88:00.0" && (*g)[1].numa_node == -1);
+  }
+  // a device variable re-maps the devices: only the runtime knows the order
+  p.honour_visible_env = true;
+  setenv("HIP_VISIBLE_DEVICES", "1", 1);
+  CHECK(!kfd_gpus(p).has_value());
+  unsetenv("HIP_VISIBLE_DEVICES");
+  CHECK(kfd_gpus(p).has_value());
+  p.honour_visible_env = false;
+  // no access to the driver: none; no topology: unknown; a GPU node without a render minor: unknown
+  p.kfd = root + "/no_kfd";
+  g = kfd_gpus(p);
+  CHECK(g.has_value() && g->empty());
+  p.kfd = root + "/kfd";
+  p.nodes = root + "/no_nodes";
+  CHECK(!kfd_gpus(p).has_value());
+  p.nodes = root + "/nodes";
+  node(11, "simd_count 1024\n");
+  CHECK(!kfd_gpus(p).has_value());
+  CHECK(std::system(("rm -rf " + root).c_str()) == 0);
+}
+
 int main() {
   const std::vector<std::pair<const char*, std::function<void()>>> tests = {
       {"score_table", test_score_table}, {"parser", test_parser},     {"stream_reader", test_stream_reader},
@@ -764,7 +830,8 @@ int main() {
       {"engine_vs_brute_force", test_engine_vs_brute_force},          {"formatter", test_formatter},
       {"profile16", test_profile16},     {"releaser", test_releaser},   {"slices", test_slices},
       {"narrow_lengths", test_narrow_lengths}, {"result_formats", test_result_formats},
-      {"write_runs", test_write_runs},   {"pack24", test_pack24}, {"pack33", test_pack33}};
+      {"write_runs", test_write_runs},   {"pack24", test_pack24}, {"pack33", test_pack33},
+      {"kfd_topology", test_kfd_topology}};
   for (const auto& t : tests) {
     const int before = g_failed;
     t.second();
