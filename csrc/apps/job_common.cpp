@@ -158,7 +158,10 @@ void JobCore::setup_engine(int64_t job_cells, int64_t mean_l2) {
   if (backend == "auto" && job_cells >= 0 && job_cells < min_cells * ctx.size) backend = "cpu";
   // the driver's topology answers without waiting for the HIP runtime, which starts on the engine's helper
   // thread behind the parse and the encode (moc/runtime/kfd_topology.hpp)
+  Stopwatch sw_count, sw_create, sw_reduce;
+  sw_count.start();
   const int ndev = (backend == "cpu") ? 0 : gpu_device_count_fast();
+  sw_count.stop();
   if (backend == "hip" && ndev == 0)
     throw Error("--backend=hip but no HIP device is visible" +
                 (gpu_plugin_error().empty() ? std::string() : " (" + gpu_plugin_error() + ")"));
@@ -171,11 +174,21 @@ void JobCore::setup_engine(int64_t job_cells, int64_t mean_l2) {
     go.chunk_records = flags.get_int("chunk-records", 0);
     go.chunk_bytes = flags.get_int("chunk-bytes", 0);
     go.log_level = flags.get("log-level", "warn");
+    sw_create.start();
     eng.hip.reset(gpu_rank_create(ctx, go));
     device = eng.hip->device();
+    sw_create.stop();
   }
   int gpu_minmax[2] = {eng.gpu ? 1 : 0, eng.gpu ? -1 : 0};  // MIN -> {min gpu, -max gpu}
+  sw_reduce.start();
   MPI_Allreduce(MPI_IN_PLACE, gpu_minmax, 2, MPI_INT, MPI_MIN, ctx.world);
+  sw_reduce.stop();
+  {
+    char buf[160];
+    std::snprintf(buf, sizeof buf, "{\"gpu_count\": %.3f, \"rank_create\": %.3f, \"engine_reduce\": %.3f}",
+                  sw_count.total_ms(), sw_create.total_ms(), sw_reduce.total_ms());
+    extra_timing.emplace_back("rank0_setup_split_ms", buf);
+  }
   all_gpu = gpu_minmax[0] != 0;
   const bool any_gpu = gpu_minmax[1] != 0;
   transport = to_lower(flags.get("transport", "auto"));
