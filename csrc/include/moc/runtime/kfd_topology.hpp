@@ -6,10 +6,10 @@
 //
 // A GPU is a topology node (/sys/class/kfd/kfd/topology/nodes/N/properties) with simd_count > 0 whose
 // render node /dev/dri/renderD<drm_render_minor> this process may open — the runtime's own filter (a box
-// exposes 1 of its host's 8 GPUs that way). Devices are listed in node order, the runtime's device order.
-// When HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES / GPU_DEVICE_ORDINAL re-map the
-// devices only the runtime knows the mapping: kfd_gpus() then answers nullopt, as it does when the
-// topology or /dev/kfd is missing.
+// exposes 1 of its host's 8 GPUs that way). Devices are listed in node order, the runtime's device order,
+// then re-mapped the way the runtime does by ROCR_VISIBLE_DEVICES and HIP_VISIBLE_DEVICES (or
+// CUDA_VISIBLE_DEVICES / GPU_DEVICE_ORDINAL) index lists (the box sets both to "0"). kfd_gpus() answers
+// nullopt when only the runtime can tell — UUID lists, indices out of range, an unreadable topology.
 #pragma once
 
 #include <optional>

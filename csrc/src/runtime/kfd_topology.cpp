@@ -32,13 +32,62 @@ bool read_properties(const std::string& path, int64_t& simd, int64_t& minor, int
   return true;
 }
 
+// "i,j,k" -> indices; nullopt for anything else (GPU UUIDs, empty lists: the runtime's to interpret)
+std::optional<std::vector<int>> index_list(const char* v) {
+  std::vector<int> out;
+  std::stringstream ss(v);
+  std::string tok;
+  while (std::getline(ss, tok, ',')) {
+    if (tok.empty() || tok.find_first_not_of("0123456789") != std::string::npos || tok.size() > 6) return std::nullopt;
+    out.push_back(std::stoi(tok));
+  }
+  if (out.empty()) return std::nullopt;
+  return out;
+}
+
+// The runtime's re-mapping by index lists: ROCR_VISIBLE_DEVICES picks from the GPUs the driver gives this
+// process, then HIP_VISIBLE_DEVICES (or CUDA_VISIBLE_DEVICES, GPU_DEVICE_ORDINAL) from those — each list
+// in its own order. Anything else (UUIDs, out-of-range or repeated indices, disagreeing HIP/CUDA lists)
+// is left to the runtime: nullopt.
+std::optional<std::vector<KfdGpu>> apply_visible_env(std::vector<KfdGpu> gpus) {
+  auto pick = [&gpus](const char* var) -> bool {
+    const char* v = std::getenv(var);
+    if (!v) return true;
+    const auto idx = index_list(v);
+    if (!idx) return false;
+    std::vector<KfdGpu> next;
+    std::vector<bool> used(gpus.size(), false);
+    for (int i : *idx) {
+      if (i >= static_cast<int>(gpus.size()) || used[static_cast<size_t>(i)]) return false;
+      used[static_cast<size_t>(i)] = true;
+      next.push_back(gpus[static_cast<size_t>(i)]);
+    }
+    gpus.swap(next);
+    return true;
+  };
+  if (!pick("ROCR_VISIBLE_DEVICES")) return std::nullopt;
+  const char* hip_list = nullptr;
+  for (const char* var : {"HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL"}) {
+    const char* v = std::getenv(var);
+    if (!v) continue;
+    if (hip_list && std::string(hip_list) != v) return std::nullopt;
+    hip_list = v;
+  }
+  if (hip_list) {
+    if (std::getenv("HIP_VISIBLE_DEVICES")) {
+      if (!pick("HIP_VISIBLE_DEVICES")) return std::nullopt;
+    } else if (std::getenv("CUDA_VISIBLE_DEVICES")) {
+      if (!pick("CUDA_VISIBLE_DEVICES")) return std::nullopt;
+    } else if (!pick("GPU_DEVICE_ORDINAL")) {
+      return std::nullopt;
+    }
+  }
+  return gpus;
+}
+
 }  // namespace
 
 std::optional<std::vector<KfdGpu>> kfd_gpus(const KfdPaths& paths) {
-  if (paths.honour_visible_env) {
-    for (const char* var : {"HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL"})
-      if (std::getenv(var)) return std::nullopt;
-  }
   DIR* d = opendir(paths.nodes.c_str());
   if (!d) return std::nullopt;
   std::vector<int> ids;
@@ -74,7 +123,8 @@ std::optional<std::vector<KfdGpu>> kfd_gpus(const KfdPaths& paths) {
     }
     gpus.push_back(std::move(g));
   }
-  return gpus;
+  if (!paths.honour_visible_env) return gpus;
+  return apply_visible_env(std::move(gpus));
 }
 
 int bind_numa_node(int node) {

@@ -803,12 +803,34 @@ void test_kfd_topology() {
           (*g)[0].numa_node == 1);
     CHECK((*g)[1].node == 10 && (*g)[1].pci_bus_id == "0001:88:00.0" && (*g)[1].numa_node == -1);
   }
-  // a device variable re-maps the devices: only the runtime knows the order
+  // the runtime's re-mapping by index lists: ROCR_ first, then HIP_ (or CUDA_) on top; UUIDs, indices out
+  // of range and disagreeing HIP/CUDA lists are left to the runtime
   p.honour_visible_env = true;
+  for (const char* v : {"ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL"})
+    unsetenv(v);
+  g = kfd_gpus(p);
+  CHECK(g && g->size() == 2);
   setenv("HIP_VISIBLE_DEVICES", "1", 1);
+  g = kfd_gpus(p);
+  CHECK(g && g->size() == 1 && (*g)[0].node == 10);
+  setenv("ROCR_VISIBLE_DEVICES", "1,0", 1);
+  g = kfd_gpus(p);
+  CHECK(g && g->size() == 1 && (*g)[0].node == 3);
+  setenv("HIP_VISIBLE_DEVICES", "0", 1);
+  setenv("ROCR_VISIBLE_DEVICES", "0", 1);
+  g = kfd_gpus(p);
+  CHECK(g && g->size() == 1 && (*g)[0].node == 3);
+  setenv("CUDA_VISIBLE_DEVICES", "1", 1);
+  CHECK(!kfd_gpus(p).has_value());
+  unsetenv("CUDA_VISIBLE_DEVICES");
+  setenv("HIP_VISIBLE_DEVICES", "2", 1);
+  CHECK(!kfd_gpus(p).has_value());
+  setenv("HIP_VISIBLE_DEVICES", "GPU-4c3a2b1d00000000", 1);
+  CHECK(!kfd_gpus(p).has_value());
+  setenv("HIP_VISIBLE_DEVICES", "", 1);
   CHECK(!kfd_gpus(p).has_value());
   unsetenv("HIP_VISIBLE_DEVICES");
-  CHECK(kfd_gpus(p).has_value());
+  unsetenv("ROCR_VISIBLE_DEVICES");
   p.honour_visible_env = false;
   // no access to the driver: none; no topology: unknown; a GPU node without a render minor: unknown
   p.kfd = root + "/no_kfd";
