@@ -62,6 +62,8 @@ def parse_args():
                     help="record length form: auto (base-6 octets when the lengths span <= 6 values) or 3-bit fields")
     ap.add_argument("--narrow", type=int, default=1,
                     help="1: narrowest wire formats that fit (4-bit lengths, R2 results); 0: uint8 lengths, R4")
+    ap.add_argument("--final-wall", type=int, default=1,
+                    help="1: also time `mpiexec -np N ./final < input6.txt` (median of 5, checked vs the golden)")
     ap.add_argument("--dump-steps", default="", help="rank 0 writes its per-step kernel and host ms to this JSON file")
     ap.add_argument("--dry-launch", action="store_true",
                     help="print the self-launch command (JSON) for --gpus N > 1 and exit; touches no GPU")
@@ -149,6 +151,35 @@ def cleanup_stale_shm(before=None, prefix=SHM_PREFIX):
         except OSError:
             pass
     return removed
+
+
+def final_input6_wall(np_, reps=5, timeout=60):
+    """The BASELINE metric's wall-clock half: the reference's own invocation `mpiexec -np N ./final <
+    input6.txt` (default flags; /root/reference/makefile:10-11) with N = this run's GPU count, median of
+    `reps` runs, every output compared with the golden. None when ./final or mpiexec is missing."""
+    final = os.path.join(ROOT, "final")
+    inp = os.path.join(ROOT, "tests", "data", "input6.txt")
+    gold = os.path.join(ROOT, "tests", "data", "expected", "input6.out")
+    mpiexec = os.path.join(os.environ.get("MPI_HOME", "/opt/conda"), "bin", "mpiexec")
+    if not (os.path.exists(final) and os.path.exists(mpiexec) and os.path.exists(inp)):
+        return None
+    with open(gold, "rb") as f:
+        want = f.read()
+    walls, ok = [], True
+    env = {k: v for k, v in os.environ.items()
+           if not k.startswith(("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_", "ROLE_", "TORCHELASTIC",
+                                "MASTER_"))}
+    for _ in range(reps):
+        with open(inp, "rb") as fin:
+            t0 = time.perf_counter()
+            try:
+                r = subprocess.run([mpiexec, "-np", str(np_), final], stdin=fin, capture_output=True, timeout=timeout,
+                                   env=env)
+            except subprocess.TimeoutExpired:
+                return {"wall_s": None, "ok": False, "np": np_}
+            walls.append(time.perf_counter() - t0)
+        ok = ok and r.returncode == 0 and r.stdout == want
+    return {"wall_s": round(float(np.median(walls)), 4), "best_s": round(min(walls), 4), "ok": bool(ok), "np": np_}
 
 
 def pci_bus_id(code):
@@ -421,6 +452,9 @@ def main():
         per_rank = torch.stack(allv).cpu().numpy()
     else:
         per_rank = mine.cpu().numpy()[None, :]
+    # the literal wall-clock of the reference invocation on input6.txt at this rank count (rank 0, untimed,
+    # after the steps; the other ranks wait at the barrier below)
+    wall6 = final_input6_wall(world) if (rank == 0 and args.final_wall) else None
     ms_per_step = elapsed / args.steps * 1e3
     value = total_elems * args.steps / elapsed
     cells_per_rec = float(np.mean([(shape.L1 - l + 1) * l for l in range(shape.l2_min, shape.l2_max + 1)]))
@@ -472,6 +506,7 @@ def main():
             "rank0_kernels": st["kernels"],
             "host_stream": ("dma" if st["dma"] else "zero_copy") if st["direct"] else "staged",
             "verified": bool(okt.item()),
+            "final_input6_wall": wall6,
         }
         print(json.dumps(out), flush=True)
         if args.dump_steps:

@@ -5,6 +5,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 from conftest import ROOT
 
 BENCH = os.path.join(ROOT, "bench.py")
@@ -99,3 +101,15 @@ def test_pci_bus_code_roundtrip():
     for bus in ("0000:0d:00.0", "0001:8e:1f.7"):
         assert b.pci_bus_id(b.pci_bus_code(bus)) == bus
     assert b.pci_bus_code("") == -1 and b.pci_bus_id(-1) is None
+
+
+@pytest.mark.parametrize("np_", [1, 2])
+def test_final_input6_wall(np_):
+    # the BASELINE metric's wall-clock half, reported by every bench run: the reference invocation on
+    # input6.txt at the run's rank count, each output checked against the golden
+    import bench
+
+    r = bench.final_input6_wall(np_, reps=2)
+    if r is None:
+        pytest.skip("./final or mpiexec not built here")
+    assert r["ok"] and r["np"] == np_ and 0 < r["best_s"] <= r["wall_s"] < 60
