@@ -237,14 +237,18 @@ class GpuRankImpl final : public GpuRank {
     const int local = ctx.local_rank;
     pending_engine_ = std::async(std::launch::async, [this, eo, bus, local, requested]() mutable {
       if (!bus.empty()) {
+        // --device / --device-map name the runtime's index; otherwise the device the topology chose, found
+        // by its PCIe address (the same GPU whatever order the runtime lists them in)
         int id = -1;
-        const int n = device_count();
-        for (int i = 0; i < n && id < 0; ++i)
-          if (device_info(i).pci_bus_id == bus) id = i;
+        if (requested < 0) {
+          const int n = device_count();
+          for (int i = 0; i < n && id < 0; ++i)
+            if (device_info(i).pci_bus_id == bus) id = i;
+        }
         if (id < 0) id = select_device(local, requested);
         if (id != eo.device)
-          MOC_LOG_WARN("the HIP runtime lists device %s as %d, the driver topology as %d: using %d", bus.c_str(), id,
-                       eo.device, id);
+          MOC_LOG_INFO("device %s is the runtime's %d, the driver topology's %d: using %d", bus.c_str(), id, eo.device,
+                       id);
         eo.device = id;
         device_.store(id);
       }
