@@ -220,7 +220,7 @@ class GpuRankImpl final : public GpuRank {
     if (const auto kfd = kfd_gpus(); kfd && !kfd->empty()) {
       const int n = static_cast<int>(kfd->size());
       const int id = requested >= 0 ? requested : ctx.local_rank % n;
-      if (id < n) {
+      if (id < n && !(*kfd)[static_cast<size_t>(id)].pci_bus_id.empty()) {  // found again by that address
         device_ = id;
         bus = (*kfd)[static_cast<size_t>(id)].pci_bus_id;
         // host buffers this rank's GPU streams over PCIe, and the threads that fill them, on the NUMA node
