@@ -27,9 +27,12 @@
 
 #include <cstdio>
 #include <cstring>
+#include <ctime>
 #include <future>
 #include <memory>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "job.hpp"
 #include "moc/runtime/host_region.hpp"
@@ -88,6 +91,8 @@ const char* kUsage =
     "                              which mpiexec's proxies forward through a pipe\n"
     "  --parallel-print            with several ranks and --output: every rank writes its own rows\n"
     "  --timing                    per-phase JSON on stderr (root)\n"
+    "  --timing-exit               a last stderr line: the teardown after the job (engine, MPI_Finalize,\n"
+    "                              releaser) and the time since the process started\n"
     "  --strict-limits             enforce |Seq1|<=3000, |Seq2|<=2000 (PDF p.5-6)\n"
     "  --max-l1=L --max-l2=L       explicit length limits (0 = unlimited)\n"
     "  --device=K                  force device K (default: node-local rank %% devices)\n"
@@ -106,7 +111,7 @@ const std::vector<std::string> kKnown = {
     "backend", "collectives", "parallel-print", "gpu-min-cells", "gpu-prewarm-bytes", "transport", "semantics",
     "partition", "batch-records", "batch-chars", "skip-records", "input", "output", "timing", "strict-limits",
     "max-l1", "max-l2", "device", "device-map", "letters", "pin-window", "chunk-records", "chunk-bytes", "threads",
-    "log-level", "inject-fault", "mpi-topology", "help"};
+    "log-level", "inject-fault", "mpi-topology", "timing-exit", "help"};
 
 struct BatchHeader {
   int64_t n;
@@ -546,33 +551,94 @@ void prepare_mpi(int argc, char** argv) {
   mpi_prepare_env(lean);
 }
 
+// --timing-exit on the root: where the process's teardown goes after the job's report (the Job's destructor —
+// engine, pinned ranges, rings —, MPI_Finalize, the helper threads, the releaser's queued unmaps), printed
+// as the last stderr line with each mark's time since the process started (/proc/self/stat), so the
+// launcher's wall clock minus the last mark is the exit after main (static destructors, the kernel).
+class ExitClock {
+ public:
+  void enable() { on_ = true; }
+  void mark(const char* what) {
+    if (on_) marks_.emplace_back(what, now_ms());
+  }
+  ~ExitClock() {
+    if (!on_ || marks_.empty()) return;
+    const double t0 = process_start_ms();
+    std::string out = "{\"exit_timing_ms\": {";
+    char buf[96];
+    for (size_t i = 0; i < marks_.size(); ++i) {
+      std::snprintf(buf, sizeof buf, "%s\"%s\": %.3f", i ? ", " : "", marks_[i].first,
+                    i ? marks_[i].second - marks_[i - 1].second : 0.0);
+      out += buf;
+    }
+    std::snprintf(buf, sizeof buf, "}, \"since_process_start_ms\": %.3f}\n", t0 >= 0 ? marks_.back().second - t0 : -1.0);
+    out += buf;
+    std::fputs(out.c_str(), stderr);
+  }
+
+ private:
+  static double now_ms() {
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e3 + ts.tv_nsec / 1e6;
+  }
+  // the process's start on CLOCK_MONOTONIC's scale (boot-relative, field 22 of /proc/self/stat), -1 unknown
+  static double process_start_ms() {
+    FILE* f = std::fopen("/proc/self/stat", "r");
+    if (!f) return -1;
+    char buf[1024];
+    const size_t n = std::fread(buf, 1, sizeof buf - 1, f);
+    std::fclose(f);
+    buf[n] = 0;
+    const char* p = std::strrchr(buf, ')');
+    unsigned long long st = 0;
+    int field = 2;
+    for (const char* q = p ? p + 1 : buf + n; *q && field < 22; ++q)
+      if (*q == ' ' && ++field == 22) std::sscanf(q + 1, "%llu", &st);
+    return st ? st * 1e3 / static_cast<double>(sysconf(_SC_CLK_TCK)) : -1;
+  }
+  bool on_ = false;
+  std::vector<std::pair<const char*, double>> marks_;
+};
+
 int main(int argc, char** argv) {
   prepare_mpi(argc, argv);
+  ExitClock exit_clock;  // destroyed last
   // declared before the MPI context: its queued unmaps overlap the job's teardown and MPI_Finalize
   BackgroundReleaser releaser;
   std::future<void> prewarm = early_prewarm(argc, argv);
-  MpiContext ctx(&argc, &argv);
+  auto ctx = std::make_unique<MpiContext>(&argc, &argv);
   int rc = 0;
   try {
     Flags flags(argc, argv);
     if (flags.get_bool("help", false)) {
-      if (ctx.rank == kRoot) std::printf("%sbuild: %s\n", kUsage, kBuildId);
+      if (ctx->rank == kRoot) std::printf("%sbuild: %s\n", kUsage, kBuildId);
       return 0;
     }
     auto unknown = flags.unknown(kKnown);
     if (!unknown.empty()) {
-      if (ctx.rank == kRoot) std::fprintf(stderr, "unknown flag --%s\n%s", unknown[0].c_str(), kUsage);
+      if (ctx->rank == kRoot) std::fprintf(stderr, "unknown flag --%s\n%s", unknown[0].c_str(), kUsage);
       return 2;
     }
     const std::string topo = to_lower(flags.get("mpi-topology", "lean"));
     if (topo != "lean" && topo != "full") {
-      if (ctx.rank == kRoot) std::fprintf(stderr, "--mpi-topology must be lean|full\n");
+      if (ctx->rank == kRoot) std::fprintf(stderr, "--mpi-topology must be lean|full\n");
       return 2;
     }
-    Job job(ctx, flags, releaser, std::move(prewarm));
-    rc = job.run();
+    if (ctx->rank == kRoot && flags.get_bool("timing-exit", false)) exit_clock.enable();
+    {
+      Job job(*ctx, flags, releaser, std::move(prewarm));
+      rc = job.run();
+      exit_clock.mark("job_done");
+    }
+    exit_clock.mark("job_teardown");
   } catch (const std::exception& e) {
-    ctx.abort(3, e.what());
+    ctx->abort(3, e.what());
   }
+  ctx.reset();
+  exit_clock.mark("mpi_finalize");
+  if (prewarm.valid()) prewarm.wait();
+  releaser.stop();
+  exit_clock.mark("releaser_drain");
   return rc;
 }

@@ -1,5 +1,6 @@
 """CLI behaviour: determinism, semantics flag, error handling, fault injection (no hangs: every run is
 bounded by a timeout), input edge cases through ./final."""
+import json
 import subprocess
 
 import pytest
@@ -625,3 +626,16 @@ def test_mpi_topology_lean_vs_full(np_):
     assert "x86" in cu and "linuxio" not in cu
     bad = run_final(["--mpi-topology=fast"], stdin_path=input_path(6))
     assert bad.returncode == 2 and b"--mpi-topology" in bad.stderr
+
+
+def test_timing_exit_line():
+    # --timing-exit: the teardown after the job, as the last stderr line (--timing's JSON stays the last
+    # line without it)
+    r = run_final(["--backend=cpu", "--timing", "--timing-exit"], stdin_path=input_path(6))
+    assert r.returncode == 0 and r.stdout.decode() == expected(6)
+    lines = [l for l in r.stderr.decode().splitlines() if l.startswith("{")]
+    last = json.loads(lines[-1])
+    assert set(last["exit_timing_ms"]) == {"job_done", "job_teardown", "mpi_finalize", "releaser_drain"}
+    assert last["since_process_start_ms"] > 0 and "timing" in json.loads(lines[-2])
+    r = run_final(["--backend=cpu", "--timing"], stdin_path=input_path(6))
+    assert "timing" in json.loads(r.stderr.decode().strip().splitlines()[-1])
