@@ -93,6 +93,8 @@ const char* kUsage =
     "  --timing                    per-phase JSON on stderr (root)\n"
     "  --timing-exit               a last stderr line: the teardown after the job (engine, MPI_Finalize,\n"
     "                              releaser) and the time since the process started\n"
+    "  --quick-exit=0|1            1 (default): end with _Exit once outputs are closed and MPI is finalized,\n"
+    "                              leaving the runtimes' static teardown to the kernel\n"
     "  --strict-limits             enforce |Seq1|<=3000, |Seq2|<=2000 (PDF p.5-6)\n"
     "  --max-l1=L --max-l2=L       explicit length limits (0 = unlimited)\n"
     "  --device=K                  force device K (default: node-local rank %% devices)\n"
@@ -111,7 +113,7 @@ const std::vector<std::string> kKnown = {
     "backend", "collectives", "parallel-print", "gpu-min-cells", "gpu-prewarm-bytes", "transport", "semantics",
     "partition", "batch-records", "batch-chars", "skip-records", "input", "output", "timing", "strict-limits",
     "max-l1", "max-l2", "device", "device-map", "letters", "pin-window", "chunk-records", "chunk-bytes", "threads",
-    "log-level", "inject-fault", "mpi-topology", "timing-exit", "help"};
+    "log-level", "inject-fault", "mpi-topology", "timing-exit", "quick-exit", "help"};
 
 struct BatchHeader {
   int64_t n;
@@ -561,8 +563,10 @@ class ExitClock {
   void mark(const char* what) {
     if (on_) marks_.emplace_back(what, now_ms());
   }
-  ~ExitClock() {
+  ~ExitClock() { print(); }
+  void print() {
     if (!on_ || marks_.empty()) return;
+    on_ = false;
     const double t0 = process_start_ms();
     std::string out = "{\"exit_timing_ms\": {";
     char buf[96];
@@ -601,6 +605,19 @@ class ExitClock {
   std::vector<std::pair<const char*, double>> marks_;
 };
 
+// Ends the process with _Exit after main's own teardown (--quick-exit=1, the default): not under the host
+// sanitizers, whose leak check runs at exit.
+bool quick_exit_enabled(bool flag) {
+#if defined(__SANITIZE_ADDRESS__) || defined(__SANITIZE_THREAD__)
+  return false;
+#elif defined(__has_feature)
+#if __has_feature(address_sanitizer) || __has_feature(thread_sanitizer)
+  return false;
+#endif
+#endif
+  return flag;
+}
+
 int main(int argc, char** argv) {
   prepare_mpi(argc, argv);
   ExitClock exit_clock;  // destroyed last
@@ -609,6 +626,7 @@ int main(int argc, char** argv) {
   std::future<void> prewarm = early_prewarm(argc, argv);
   auto ctx = std::make_unique<MpiContext>(&argc, &argv);
   int rc = 0;
+  bool quick_exit = true;
   try {
     Flags flags(argc, argv);
     if (flags.get_bool("help", false)) {
@@ -626,6 +644,7 @@ int main(int argc, char** argv) {
       return 2;
     }
     if (ctx->rank == kRoot && flags.get_bool("timing-exit", false)) exit_clock.enable();
+    quick_exit = flags.get_bool("quick-exit", true);
     {
       Job job(*ctx, flags, releaser, std::move(prewarm));
       rc = job.run();
@@ -640,5 +659,13 @@ int main(int argc, char** argv) {
   if (prewarm.valid()) prewarm.wait();
   releaser.stop();
   exit_clock.mark("releaser_drain");
+  if (quick_exit_enabled(quick_exit)) {
+    // every output is flushed and closed and MPI is finalized: the rest of a normal exit is the runtimes'
+    // static teardown (the HIP runtime's queues, streams and device memory), which the kernel driver
+    // does anyway when the process goes
+    exit_clock.print();
+    std::fflush(nullptr);
+    std::_Exit(rc);
+  }
   return rc;
 }

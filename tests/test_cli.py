@@ -639,3 +639,14 @@ def test_timing_exit_line():
     assert last["since_process_start_ms"] > 0 and "timing" in json.loads(lines[-2])
     r = run_final(["--backend=cpu", "--timing"], stdin_path=input_path(6))
     assert "timing" in json.loads(r.stderr.decode().strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("quick", ["0", "1"])
+def test_quick_exit_flushes_everything(tmp_path, quick):
+    # --quick-exit=1 (default) ends with _Exit after the outputs are closed: stdout and --output files
+    # must be complete either way
+    r = run_final(["--backend=cpu", f"--quick-exit={quick}"], stdin_path=input_path(3), np_=2)
+    assert r.returncode == 0 and r.stdout.decode() == expected(3)
+    out = tmp_path / "o.txt"
+    r = run_final(["--backend=cpu", f"--quick-exit={quick}", f"--output={out}"], stdin_path=input_path(1), np_=2)
+    assert r.returncode == 0 and out.read_text() == expected(1)
