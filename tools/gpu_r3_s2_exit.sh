@@ -12,6 +12,8 @@ for mode in "--quick-exit=0" "" "--quick-exit=0" "" "--quick-exit=0 --batch-reco
   e=$(date +%s%N)
   echo "1.14G mode='$mode' wall_ms=$(( (e - s) / 1000000 )) $(grep '"wall_s"' gpurun_out/r3_timing.txt | grep -o '"wall_s": [0-9.]*') $(tail -1 gpurun_out/r3_timing.txt)"
   rm -f /tmp/moc_big6.out
-done > gpurun_out/final_exit_1.1G_r3b_quick.log
-cat gpurun_out/final_exit_1.1G_r3b_quick.log
+done > gpurun_out/final_exit_1.1G_r3c_leave.log
+cat gpurun_out/final_exit_1.1G_r3c_leave.log
 rm -f $F
+timeout -k 10 800 python -u -m pytest tests/test_gpu.py -x -q --timeout 120 --timeout-method thread -k "final or rccl or cli" > gpurun_out/gpu_tests_r3_exit.log 2>&1 || { tail -30 gpurun_out/gpu_tests_r3_exit.log; exit 1; }
+tail -1 gpurun_out/gpu_tests_r3_exit.log
