@@ -24,6 +24,8 @@
 #include "moc/runtime/log.hpp"
 #include "moc/runtime/pinned.hpp"
 #include "moc/runtime/timer.hpp"
+#include "moc/score_table.hpp"
+#include "moc/wire.hpp"
 
 namespace moc {
 namespace {
@@ -288,6 +290,7 @@ class GpuRankImpl final : public GpuRank {
   int device() const override { return device_.load(); }
   void set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, Semantics sem) override {
     std::lock_guard<std::mutex> lock(mu_);
+    facts_ = ProblemFacts::of(w, L1);
     if (engine_) {
       engine_->set_problem(w, seq1, L1, sem);
       return;
@@ -309,11 +312,21 @@ class GpuRankImpl final : public GpuRank {
     engine().finish_wire();
     return last_stats();
   }
+  // answered from the problem alone (the engine's own rules, dev::configure_swipe / r2_params /
+  // pick_result_format), so the encode does not wait for the engine's start-up
   bool streams_packed(int64_t min_l2, int64_t max_l2) const override {
-    return engine().streams_packed(min_l2, max_l2);
+    const ProblemFacts f = facts();
+    if (!f.set) return engine().streams_packed(min_l2, max_l2);
+    dev::ShortArgs a;
+    a.packed24 = 1;  // the widest LDS layout of the packed forms (HipEngine::streams_packed)
+    return dev::configure_swipe(f.L1, min_l2, max_l2, f.max_abs, a);
   }
   ResultFormat result_format(int64_t min_l2, int64_t max_l2) const override {
-    return engine().auto_format(max_l2, min_l2);
+    const ProblemFacts f = facts();
+    if (!f.set) return engine().auto_format(max_l2, min_l2);
+    R2Params r2;
+    if (min_l2 > 0 && r2_params(f.L1, min_l2, max_l2, f.min_t, f.max_t, r2)) return ResultFormat::R2;
+    return pick_result_format(f.L1, max_l2, f.max_abs);
   }
   GpuSolveStats last_stats() const override {
     const EngineStats& st = engine().stats();
@@ -326,10 +339,27 @@ class GpuRankImpl final : public GpuRank {
     g.r2 = st.r2;
     return g;
   }
-  void pin(const void* p, size_t bytes) override { engine().pin(p, bytes); }
-  void unpin_all() override { engine().unpin_all(); }
+  // Page-locking needs the HIP runtime, not the engine: a rank registers its buffers while the engine's
+  // streams and buffers are still being made. The registrations are this rank's until detached.
+  void pin(const void* p, size_t bytes) override {
+    bind_thread();  // waits for the runtime's start-up (on the helper thread since process start)
+    const std::vector<void*> made = pinned::register_range(p, bytes);
+    std::lock_guard<std::mutex> lock(pin_mu_);
+    pins_.insert(pins_.end(), made.begin(), made.end());
+  }
+  void unpin_all() override {
+    quiesce();
+    std::lock_guard<std::mutex> lock(pin_mu_);
+    pinned::unregister(pins_);
+    pins_.clear();
+  }
   std::function<void()> detach_pins() override {
-    auto regs = std::make_shared<std::vector<void*>>(engine().detach_pins());
+    quiesce();  // no kernel in flight reads them any more
+    std::shared_ptr<std::vector<void*>> regs;
+    {
+      std::lock_guard<std::mutex> lock(pin_mu_);
+      regs = std::make_shared<std::vector<void*>>(std::exchange(pins_, {}));
+    }
     const int dev = device_.load();
     return [regs, dev] {
       (void)hipSetDevice(dev);
@@ -338,6 +368,36 @@ class GpuRankImpl final : public GpuRank {
   }
 
  private:
+  // What the engine's format rules read from a problem: Seq1's length and the score table's range.
+  struct ProblemFacts {
+    int64_t L1 = 0;
+    int32_t max_abs = 0, min_t = 0, max_t = 0;
+    bool set = false;
+    static ProblemFacts of(const Weights& w, int64_t L1) {
+      ProblemFacts f;
+      const ScoreTable t = ScoreTable::build(w);
+      f.L1 = L1;
+      f.max_abs = t.max_abs();
+      f.min_t = INT32_MAX;
+      f.max_t = INT32_MIN;
+      for (int x = 1; x < kAlphabet; ++x)  // HipEngine::set_problem's min_t_ / max_t_
+        for (int y = 1; y < kAlphabet; ++y) {
+          f.min_t = std::min(f.min_t, t.lut[x * kLutStride + y]);
+          f.max_t = std::max(f.max_t, t.lut[x * kLutStride + y]);
+        }
+      f.set = true;
+      return f;
+    }
+  };
+  ProblemFacts facts() const {
+    std::lock_guard<std::mutex> lock(mu_);
+    return facts_;
+  }
+  // the engine's wire kernel finished (when there is an engine: none started one before it was up)
+  void quiesce() const {
+    if (engine_up_.load()) engine().finish_wire();
+  }
+
   struct Problem {
     Weights w{};
     std::vector<uint8_t> seq1;
@@ -359,6 +419,7 @@ class GpuRankImpl final : public GpuRank {
                                        problem_.sem);
       problem_ = Problem{};
       engine_ = std::move(e);
+      engine_up_.store(true);
     });
     if (!engine_) throw Error("the HIP engine failed to start: " + start_error_);
     bind_thread();
@@ -385,6 +446,10 @@ class GpuRankImpl final : public GpuRank {
   mutable Problem problem_;
   mutable std::unique_ptr<HipEngine> engine_;
   mutable std::string start_error_;
+  mutable std::atomic<bool> engine_up_{false};  // engine_ is set (kernels can only run after that)
+  ProblemFacts facts_;  // under mu_
+  std::mutex pin_mu_;
+  std::vector<void*> pins_;  // this rank's page-locked ranges (pinned registry bases)
   std::unique_ptr<DeviceSearch> ds_;  // destroyed after dc_ (declared before it)
   std::unique_ptr<DeviceComm> dc_;
   std::future<std::unique_ptr<RcclDeviceComm>> pending_;  // connect in flight (init_rccl_begin)
