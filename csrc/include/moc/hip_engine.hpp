@@ -180,7 +180,8 @@ class HipEngine {
   int num_cus_ = 256;
   int tile_u_ = 0;              // tile-kernel sub-tiles per wave tile (0 = per batch; MOC_TILE_U = 1|2|4)
   int tile_waves_per_cu_ = 32;  // tile-kernel waves per CU (MOC_TILE_WAVES_PER_CU)
-  hipStream_t s_copy_ = nullptr, s_compute_ = nullptr, s_return_ = nullptr;
+  hipStream_t s_copy_ = nullptr, s_compute_ = nullptr, s_return_ = nullptr;  // copy / return: made on first use
+  void ensure_side_streams();
   // problem
   ScoreTable table_{};
   int32_t min_t_ = 0, max_t_ = 0;  // pair-score range over letters (R2 parameters)

@@ -91,9 +91,10 @@ HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
     const int v = std::atoi(w);
     if (v >= 1 && v <= 32) tile_waves_per_cu_ = v;
   }
-  MOC_HIP_CHECK(hipStreamCreateWithFlags(&s_copy_, hipStreamNonBlocking));
+  // the compute stream only: each stream costs ~10 ms of hardware-queue set-up on the MI355X box
+  // (profiles/hip_init_variants_box.log), and the streaming kernels need no other; the staged and DMA
+  // pipelines make their copy and return streams on first use (ensure_side_streams)
   MOC_HIP_CHECK(hipStreamCreateWithFlags(&s_compute_, hipStreamNonBlocking));
-  MOC_HIP_CHECK(hipStreamCreateWithFlags(&s_return_, hipStreamNonBlocking));
   const double t_streams = init_sw.total_ms();
   for (int i = 0; i < 3; ++i) {  // run_staged cycles two, run_dma_stream three
     auto s = std::make_unique<Slot>();
@@ -102,11 +103,11 @@ HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
     MOC_HIP_CHECK(hipEventCreate(&s->ev_k1));
     MOC_HIP_CHECK(hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming));
     MOC_HIP_CHECK(hipMalloc(&s->d_counter, 2 * sizeof(unsigned)));
-    MOC_HIP_CHECK(hipMemset(s->d_counter, 0, 2 * sizeof(unsigned)));
+    MOC_HIP_CHECK(hipMemsetAsync(s->d_counter, 0, 2 * sizeof(unsigned), s_compute_));  // before any kernel
     slots_.push_back(std::move(s));
   }
   MOC_HIP_CHECK(hipMalloc(&d_counter_, 2 * sizeof(unsigned)));  // {next tile, blocks done}, self-resetting
-  MOC_HIP_CHECK(hipMemset(d_counter_, 0, 2 * sizeof(unsigned)));
+  MOC_HIP_CHECK(hipMemsetAsync(d_counter_, 0, 2 * sizeof(unsigned), s_compute_));
   MOC_HIP_CHECK(hipEventCreate(&ev_a_));
   MOC_HIP_CHECK(hipEventCreate(&ev_b_));
   MOC_HIP_CHECK(hipEventCreateWithFlags(&ev_plan_, hipEventDisableTiming));
@@ -140,9 +141,14 @@ HipEngine::~HipEngine() {
   (void)hipEventDestroy(ev_a_);
   (void)hipEventDestroy(ev_b_);
   (void)hipFree(d_image_);
-  (void)hipStreamDestroy(s_copy_);
+  if (s_copy_) (void)hipStreamDestroy(s_copy_);
   (void)hipStreamDestroy(s_compute_);
-  (void)hipStreamDestroy(s_return_);
+  if (s_return_) (void)hipStreamDestroy(s_return_);
+}
+
+void HipEngine::ensure_side_streams() {
+  if (!s_copy_) MOC_HIP_CHECK(hipStreamCreateWithFlags(&s_copy_, hipStreamNonBlocking));
+  if (!s_return_) MOC_HIP_CHECK(hipStreamCreateWithFlags(&s_return_, hipStreamNonBlocking));
 }
 
 void HipEngine::pin(const void* p, size_t bytes) {
@@ -720,6 +726,7 @@ void HipEngine::solve_wire_impl(const WireBatch& batch, void* out, ResultFormat 
 // base pointers shifted so the kernel's absolute indexing lands inside them.
 void HipEngine::run_dma_stream(const dev::ProblemView& pv, const dev::ShortArgs& a0, bool swipe, const WireBatch& b,
                                void* out, int fb) {
+  ensure_side_streams();
   const uint8_t* codes = b.letters;
   const uint8_t* lengths = b.lengths;
   const int len_bits = b.len_bits;
@@ -860,6 +867,7 @@ void HipEngine::launch_direct(const dev::ProblemView& pv, const dev::ShortArgs& 
 
 void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t n, void* out, ResultFormat fmt,
                            bool packed5) {
+  ensure_side_streams();
   const int fb = result_bytes(fmt);
   ChunkPlan cp;
   double kernel_ms = 0;
