@@ -5,18 +5,18 @@ set -o pipefail
 mkdir -p gpurun_out
 F=/tmp/moc_big6.txt
 timeout -k 10 300 python3 tools/gen_synthetic.py --shape input6 --records 134217728 --jobs 16 --out $F > /dev/null || exit 1
-for mode in "--threads=16" "--threads=15" "--threads=16" "--threads=15" "--threads=16 --batch-records=16777216" "--threads=15 --batch-records=16777216" "--threads=16 --batch-records=16777216" "--threads=15 --batch-records=16777216"; do
+for mode in ${MODES:-"--threads=16" "--threads=15" "--threads=16" "--threads=15" "--threads=16 --batch-records=16777216" "--threads=15 --batch-records=16777216" "--threads=16 --batch-records=16777216" "--threads=15 --batch-records=16777216"}; do
   sleep 3
   s=$(date +%s%N)
-  timeout -k 10 300 /opt/conda/bin/mpiexec -np 1 ./final --timing --input=$F --output=/tmp/moc_big6.out $mode \
+  timeout -k 10 300 env $ENVS /opt/conda/bin/mpiexec -np 1 ./final --timing --input=$F --output=/tmp/moc_big6.out $mode \
     2> gpurun_out/r3_timing.txt || { tail -5 gpurun_out/r3_timing.txt; exit 1; }
   e=$(date +%s%N)
   echo "1.14G mode='$mode' wall_ms=$(( (e - s) / 1000000 )) $(tail -1 gpurun_out/r3_timing.txt)"
   rm -f /tmp/moc_big6.out
-done > gpurun_out/final_modes_1.1G_r3n_threads.log
+done > gpurun_out/${OUT:-final_modes_1.1G_r3n_threads.log}
 python3 - <<'PY'
 import json
-for line in open('gpurun_out/final_modes_1.1G_r3n_threads.log'):
+for line in open('gpurun_out/${OUT:-final_modes_1.1G_r3n_threads.log}'):
     head, rest = line.split(' {', 1)
     js = json.loads('{' + rest)
     t = js['timing']
