@@ -25,6 +25,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <ctime>
@@ -68,6 +69,29 @@ int close_output(FILE* f) {
 // The sources this binary was built from (Makefile: a hash over csrc/ + Makefile, and the git commit):
 // printed by --help and --timing so a test can tell a stale prebuilt binary from the checked-out source.
 const char* kBuildId = MOC_BUILD_ID;
+
+// The process's age in ms (CLOCK_MONOTONIC minus the start time in /proc/self/stat), -1 when unknown.
+double ms_since_process_start() {
+  static const double start = [] {
+    FILE* f = std::fopen("/proc/self/stat", "r");
+    if (!f) return -1.0;
+    char buf[1024];
+    const size_t n = std::fread(buf, 1, sizeof buf - 1, f);
+    std::fclose(f);
+    buf[n] = 0;
+    const char* p = std::strrchr(buf, ')');
+    unsigned long long st = 0;
+    int field = 2;
+    for (const char* q = p ? p + 1 : buf + n; *q && field < 22; ++q)
+      if (*q == ' ' && ++field == 22) std::sscanf(q + 1, "%llu", &st);
+    return st ? st * 1e3 / static_cast<double>(sysconf(_SC_CLK_TCK)) : -1.0;
+  }();
+  if (start < 0) return -1;
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1e3 + ts.tv_nsec / 1e6 - start;
+}
+std::atomic<double> g_runtime_up_ms{-1};  // set by the prewarm thread once the HIP runtime answered
 
 const char* kUsage =
     "usage: mpiexec -np N ./final [options] < input.txt\n"
@@ -179,7 +203,11 @@ void Job::prewarm_gpu() {
     hint = rc == 0 && S_ISREG(st.st_mode) && min_bytes > 0 && st.st_size >= min_bytes;
   }
   bcast_bytes(&hint, sizeof hint, kRoot, job_.ctx.world);
-  if (hint && !prewarm_.valid()) prewarm_ = std::async(std::launch::async, [] { (void)gpu_device_count(); });
+  if (hint && !prewarm_.valid())
+    prewarm_ = std::async(std::launch::async, [] {
+      (void)gpu_device_count();
+      g_runtime_up_ms.store(ms_since_process_start());
+    });
 }
 
 bool Job::open_io(std::string& error) {
@@ -498,6 +526,11 @@ int Job::run() {
   }
   job_.out = stdout;
   job_.total.stop();
+  if (const double up = g_runtime_up_ms.load(); up >= 0) {  // --timing: when the prewarm saw the HIP runtime up
+    char buf[32];
+    std::snprintf(buf, sizeof buf, "%.3f", up);
+    job_.extra_timing.emplace_back("runtime_up_since_start_ms", buf);
+  }
   job_.report(h);
   MPI_Barrier(ctx.world);
   return rc;
@@ -540,6 +573,7 @@ std::future<void> early_prewarm(int argc, char** argv) {
     if (device < 0 && !map.empty()) device = map[static_cast<size_t>(local) % map.size()];
     return std::async(std::launch::async, [rccl, device, local] {
       const int n = gpu_device_count();
+      g_runtime_up_ms.store(ms_since_process_start());
       if (rccl && n > 0) (void)gpu_rccl_warmup(device >= 0 ? device : local % n);
     });
   } catch (const std::exception&) {
