@@ -234,6 +234,7 @@ class GpuRankImpl final : public GpuRank {
       device_ = select_device(ctx.local_rank, requested);
       numa_ = bind_numa_to_device(device_);
       bus.clear();
+      runtime_up_.store(true);
     }
     eo.device = device_;
     const int local = ctx.local_rank;
@@ -242,8 +243,9 @@ class GpuRankImpl final : public GpuRank {
         // --device / --device-map name the runtime's index; otherwise the device the topology chose, found
         // by its PCIe address (the same GPU whatever order the runtime lists them in)
         int id = -1;
+        const int n = device_count();  // the runtime's start-up (or the wait for the prewarm thread's)
+        runtime_up_.store(true);
         if (requested < 0) {
-          const int n = device_count();
           for (int i = 0; i < n && id < 0; ++i)
             if (device_info(i).pci_bus_id == bus) id = i;
         }
@@ -306,6 +308,7 @@ class GpuRankImpl final : public GpuRank {
   }
   double last_kernel_ms() const override { return engine().stats().kernel_ms; }
   int numa_node() const override { return numa_; }
+  bool runtime_ready() const override { return runtime_up_.load(); }
   void solve_wire(const WireBatch& b, void* out, ResultFormat fmt) override { engine().solve_wire(b, out, fmt); }
   void begin_wire(const WireBatch& b, void* out, ResultFormat fmt) override { engine().begin_wire(b, out, fmt); }
   GpuSolveStats finish_wire() override {
@@ -446,6 +449,7 @@ class GpuRankImpl final : public GpuRank {
   mutable Problem problem_;
   mutable std::unique_ptr<HipEngine> engine_;
   mutable std::string start_error_;
+  std::atomic<bool> runtime_up_{false};
   mutable std::atomic<bool> engine_up_{false};  // engine_ is set (kernels can only run after that)
   ProblemFacts facts_;  // under mu_
   std::mutex pin_mu_;

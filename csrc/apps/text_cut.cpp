@@ -89,6 +89,17 @@ BatchCut Cutter::take(int64_t max_rec, int64_t max_chr) {
   cut.end = cut.chunks.empty() ? cut.begin : cut.chunks.back().end;
   return cut;
 }
+bool Cutter::count_ahead(int64_t max_rec, int64_t max_chr, int64_t batches) {
+  if (t_.eof() && counted_ >= t_.hi()) return false;
+  const bool by_rec = max_rec < INT64_MAX, by_chr = max_chr < INT64_MAX;
+  if ((by_rec && tok_ahead_ >= batches * max_rec) || (!by_rec && by_chr && chr_ahead_ >= batches * max_chr) ||
+      (!by_rec && !by_chr))
+    return false;
+  const int64_t before = counted_;
+  extend(by_rec ? tok_ahead_ + max_rec : INT64_MAX, by_chr ? chr_ahead_ + max_chr : INT64_MAX);
+  return counted_ > before;
+}
+
 // ~1 MiB chunks: the walk to a batch's cut scans at most one, and the ranks' encode of a batch gets pieces
 // small enough to balance over their threads
 void Cutter::extend(int64_t max_rec, int64_t max_chr) {

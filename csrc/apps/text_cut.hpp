@@ -56,6 +56,9 @@ class Cutter {
   // Cuts the next batch: records are taken while fewer than max_rec are taken and (none is taken yet or
   // fewer than max_chr letters are) — StreamReader::next_batch's rule.
   BatchCut take(int64_t max_rec, int64_t max_chr);
+  // Counts one more batch's worth of text ahead of the batches taken so far (at most `batches` ahead); false
+  // when that much is counted already or the text is done. Work for the wait on the GPU's start-up.
+  bool count_ahead(int64_t max_rec, int64_t max_chr, int64_t batches);
 
  private:
   // Counts the next region of the text (parallel chunks cut at whitespace), sized from the density seen.

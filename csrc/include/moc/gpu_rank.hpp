@@ -50,6 +50,8 @@ class GpuRank {
   virtual double last_kernel_ms() const = 0;
   // NUMA node of the device's PCIe root complex (-1: unknown); the rank's threads are bound to it.
   virtual int numa_node() const = 0;
+  // The HIP runtime has started (page-locking and the engine no longer wait for it); never blocks.
+  virtual bool runtime_ready() const = 0;
   // Wire-format batch (moc/wire.hpp) -> results in `fmt` (zero-copy when every buffer is pinned).
   virtual void solve_wire(const WireBatch& b, void* out, ResultFormat fmt) = 0;
   // The same in two halves (HipEngine::begin_wire / finish_wire): begin queues the zero-copy streaming
