@@ -802,6 +802,8 @@ void HipEngine::run_dma_stream(const dev::ProblemView& pv, const dev::ShortArgs&
       MOC_HIP_CHECK(hipEventSynchronize(sp->ev_done));
       sp->busy = false;
     }
+  // the return copies are done, so every kernel is; the end marker itself must be complete before it is read
+  MOC_HIP_CHECK(hipEventSynchronize(ev_b_));
   float ms = 0;
   MOC_HIP_CHECK(hipEventElapsedTime(&ms, ev_a_, ev_b_));
   stats_.kernel_ms = ms;  // compute-stream span: first kernel start .. last kernel end
@@ -874,6 +876,7 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
   auto retire = [&](Slot& s) {
     if (!s.busy) return;
     MOC_HIP_CHECK(hipEventSynchronize(s.ev_done));
+    MOC_HIP_CHECK(hipEventSynchronize(s.ev_k1));  // complete itself before it is read (not only what it marks)
     float ms = 0;
     MOC_HIP_CHECK(hipEventElapsedTime(&ms, s.ev_k0, s.ev_k1));
     kernel_ms += ms;
