@@ -3,7 +3,7 @@
 # letters bulk/streamed and 1e10 letters streamed (engine_wait, ring_pin, wall).
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 800 python -u -m pytest tests -x -q --timeout 120 --timeout-method thread -m gpu -k "final or rccl or cli or stream" > gpurun_out/gpu_tests_r3_ahead.log 2>&1 || { tail -30 gpurun_out/gpu_tests_r3_ahead.log; exit 1; }
+timeout -k 10 800 python -u -m pytest tests -x -q --timeout 120 --timeout-method thread -m gpu -k "final or rccl or cli or stream or host_stream" > gpurun_out/gpu_tests_r3_ahead.log 2>&1 || { tail -30 gpurun_out/gpu_tests_r3_ahead.log; exit 1; }
 tail -1 gpurun_out/gpu_tests_r3_ahead.log
 F=/tmp/moc_big6.txt
 timeout -k 10 300 python3 tools/gen_synthetic.py --shape input6 --records 134217728 --jobs 16 --out $F > /dev/null || exit 1
