@@ -308,11 +308,12 @@ bool StreamFlow::fill(const BatchMsg& m, const std::vector<int64_t>& table, int 
     // (each registration costs milliseconds, whatever its size)
     auto al64 = [](int64_t x) { return (x + 63) & ~int64_t{63}; };
     // The first slot's page-locking waits for the HIP runtime's start-up: the root counts later batches
-    // meanwhile (mapped input: up to 8 batches ahead; a stream holds what it counts, so 2)
+    // meanwhile (mapped input: up to 32 batches ahead, ~3 ms of counting each; a stream holds what it
+    // counts, so 2)
     if (in.arena.cap == 0 && cutter_ && !gpu_->runtime_ready()) {
       Stopwatch ca;
       ca.start();
-      const int64_t ahead = src_.mapped ? 8 : 2;
+      const int64_t ahead = src_.mapped ? 32 : 2;
       try {
         while (!gpu_->runtime_ready() && cutter_->count_ahead(max_rec_, max_chr_, ahead)) {
         }
