@@ -2,11 +2,16 @@
 #include "text_cut.hpp"
 
 #include <omp.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <cstring>
 
 namespace moc {
+
+namespace {
+constexpr int kMadvPopulateRead = 22;  // MADV_POPULATE_READ (Linux 5.14); older headers lack the name
+}
 
 bool AreaText::load_more(int64_t want) {
   if (map_ || eof_) return false;
@@ -150,12 +155,20 @@ void Cutter::extend(int64_t max_rec, int64_t max_chr) {
     b[q] = x;
   }
   b[nt] = len;
+  const bool mapped = t_.mapped();
 #pragma omp parallel for schedule(dynamic, 4) if (nt > 2)
   for (int q = 0; q < nt; ++q) {
     Chunk& c = parts[q];
     c.begin = counted_ + b[q];
     c.end = counted_ + b[q + 1];
-    count_tokens(reinterpret_cast<const char*>(ua) + b[q], static_cast<size_t>(b[q + 1] - b[q]), &c.toks, &c.chars);
+    const char* at = reinterpret_cast<const char*>(ua) + b[q];
+    if (mapped) {  // the chunk's page tables in one call rather than a fault per 64 KiB (28 % faster reads of a
+                   // mapped file on the box, profiles/populate_probe_box.log; ignored before Linux 5.14)
+      const uintptr_t a0 = reinterpret_cast<uintptr_t>(at) & ~uintptr_t{4095};
+      (void)madvise(reinterpret_cast<void*>(a0), static_cast<size_t>(reinterpret_cast<uintptr_t>(at) + (b[q + 1] - b[q]) - a0),
+                    kMadvPopulateRead);
+    }
+    count_tokens(at, static_cast<size_t>(b[q + 1] - b[q]), &c.toks, &c.chars);
   }
   for (const Chunk& c : parts) {
     if (c.end <= c.begin) continue;
