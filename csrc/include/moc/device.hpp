@@ -204,8 +204,8 @@ void preload_short_kernels();
 void preload_swipe_kernels();
 void preload_tile16_kernels();
 void preload_mfma_kernels();
-inline void preload_kernels() {
-  preload_mfma_kernels();
+inline void preload_kernels(bool mfma = true) {
+  if (mfma) preload_mfma_kernels();  // the measured-slower MFMA variant: only when it is selected (MOC_MFMA=1)
   preload_align_kernels();
   preload_short_kernels();
   preload_swipe_kernels();
