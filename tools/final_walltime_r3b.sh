@@ -22,7 +22,7 @@ run() {  # run <np> <label> <cmd...>  (stdin from $IN)
   echo "$label np=$np $(printf '%s\n' "${t[@]}" | stats) $ok"
 }
 echo "# host: $(nproc) cpus visible, OMP_NUM_THREADS=${OMP_NUM_THREADS:-unset}, reps=$REPS, $(./final --help | tail -1)"
-for np in 1 2 4; do
+for np in ${NPS:-1 2 4}; do
   IN=tests/data/input6.txt EXPECT= run $np "mpi_hello              " build/mpi_hello
   IN=tests/data/input6.txt EXPECT=tests/data/expected/input6.out run $np "final input6 topo=full " ./final --mpi-topology=full
   for i in 1 2 3 4 5 6; do
