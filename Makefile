@@ -167,8 +167,8 @@ test: unit
 	python -m pytest tests/ -x -q -m "not gpu"
 
 # native unit tests of the host core (no GPU, no MPI)
-$(BUILD)/test_core: csrc/tests/test_core.cpp $(CPU_OBJS) $(HEADERS)
-	$(CXX) $(CXXFLAGS) -o $@ csrc/tests/test_core.cpp $(CPU_OBJS) -ldl
+$(BUILD)/test_core: csrc/tests/test_core.cpp csrc/apps/text_cut.cpp csrc/apps/text_cut.hpp $(CPU_OBJS) $(HEADERS)
+	$(CXX) $(CXXFLAGS) -o $@ csrc/tests/test_core.cpp csrc/apps/text_cut.cpp $(CPU_OBJS) -ldl
 
 unit: $(BUILD)/test_core
 	$(BUILD)/test_core

@@ -21,6 +21,7 @@
 #include "moc/runtime/releaser.hpp"
 #include "moc/score_table.hpp"
 #include "moc/wire.hpp"
+#include "../apps/text_cut.hpp"
 
 using namespace moc;
 
@@ -845,6 +846,52 @@ void test_kfd_topology() {
   CHECK(std::system(("rm -rf " + root).c_str()) == 0);
 }
 
+// The streaming root's cutter: batches cut after counting ahead (while a GPU's runtime starts) are the
+// batches cut without it, by record count and by letter count; count_ahead stops at its batch bound
+void test_cutter_count_ahead() {
+  std::mt19937_64 rng(5);
+  std::string text;
+  int64_t records = 0;
+  while (text.size() < (size_t{9} << 20)) {
+    const int len = 1 + static_cast<int>(rng() % 24);
+    for (int i = 0; i < len; ++i) text.push_back(static_cast<char>('A' + rng() % 26));
+    text.push_back(rng() % 7 == 0 ? ' ' : '\n');
+    ++records;
+  }
+  auto cuts = [&](int64_t max_rec, int64_t max_chr, int ahead_at_start) {
+    AreaText t(text.data(), static_cast<int64_t>(text.size()));
+    Cutter c(t);
+    if (ahead_at_start > 0) {
+      int steps = 0;
+      while (c.count_ahead(max_rec, max_chr, ahead_at_start)) ++steps;
+      CHECK(steps > 0);
+      CHECK(!c.count_ahead(max_rec, max_chr, ahead_at_start));  // bound reached (or the text counted)
+    }
+    std::vector<std::vector<int64_t>> out;
+    int64_t taken = 0;
+    while (taken < records) {
+      const BatchCut b = c.take(max_rec, max_chr);
+      if (b.n == 0) break;
+      taken += b.n;
+      out.push_back({b.n, b.letters, b.begin, b.end, b.next, static_cast<int64_t>(b.chunks.size())});
+    }
+    CHECK(taken == records);
+    return out;
+  };
+  for (int64_t max_rec : {int64_t{50000}, int64_t{1} << 40}) {
+    const int64_t max_chr = max_rec == (int64_t{1} << 40) ? 700000 : INT64_MAX;
+    const auto plain = cuts(max_rec, max_chr, 0);
+    CHECK(plain.size() > 3);
+    for (int ahead : {1, 3, 64}) {
+      const auto early = cuts(max_rec, max_chr, ahead);
+      CHECK(early.size() == plain.size());
+      for (size_t i = 0; i < std::min(early.size(), plain.size()); ++i)  // n, letters, begin, next agree
+        CHECK(early[i][0] == plain[i][0] && early[i][1] == plain[i][1] && early[i][2] == plain[i][2] &&
+              early[i][4] == plain[i][4]);
+    }
+  }
+}
+
 int main() {
   const std::vector<std::pair<const char*, std::function<void()>>> tests = {
       {"score_table", test_score_table}, {"parser", test_parser},     {"stream_reader", test_stream_reader},
@@ -853,7 +900,7 @@ int main() {
       {"profile16", test_profile16},     {"releaser", test_releaser},   {"slices", test_slices},
       {"narrow_lengths", test_narrow_lengths}, {"result_formats", test_result_formats},
       {"write_runs", test_write_runs},   {"pack24", test_pack24}, {"pack33", test_pack33},
-      {"kfd_topology", test_kfd_topology}};
+      {"kfd_topology", test_kfd_topology}, {"cutter_count_ahead", test_cutter_count_ahead}};
   for (const auto& t : tests) {
     const int before = g_failed;
     t.second();
