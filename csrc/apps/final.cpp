@@ -123,7 +123,6 @@ const char* kUsage =
     "  --max-l1=L --max-l2=L       explicit length limits (0 = unlimited)\n"
     "  --device=K                  force device K (default: node-local rank %% devices)\n"
     "  --device-map=a,b,...        node-local rank i -> device map[i %% len]\n"
-    "  --letters=p33|p24           letter code of GPU slices (p33: 7 letters per 33 bits; p24: 5 per 3 bytes)\n"
     "  --pin-window=0|1            page-lock the GPU ranks' slices so they stream zero-copy (default 1)\n"
     "  --chunk-records=R --chunk-bytes=B   pipeline chunk sizes\n"
     "  --threads=T                 OpenMP threads (default: OMP_NUM_THREADS / all)\n"
@@ -136,7 +135,7 @@ const char* kUsage =
 const std::vector<std::string> kKnown = {
     "backend", "collectives", "parallel-print", "gpu-min-cells", "gpu-prewarm-bytes", "transport", "semantics",
     "partition", "batch-records", "batch-chars", "skip-records", "input", "output", "timing", "strict-limits",
-    "max-l1", "max-l2", "device", "device-map", "letters", "pin-window", "chunk-records", "chunk-bytes", "threads",
+    "max-l1", "max-l2", "device", "device-map", "pin-window", "chunk-records", "chunk-bytes", "threads",
     "log-level", "inject-fault", "mpi-topology", "timing-exit", "quick-exit", "help"};
 
 struct BatchHeader {
@@ -540,8 +539,8 @@ int Job::run() {
 
 // Start-up work for a helper thread, decided before MPI_Init from the same flags and environment on every
 // rank:
-//   * an --input file of >= --gpu-prewarm-bytes will run on the GPU (unless --backend=cpu): the HIP runtime
-//     starts;
+//   * an --input file of >= --gpu-prewarm-bytes will run on the GPU (unless --backend=cpu), and so will any
+//     job with --backend=hip: the HIP runtime starts;
 //   * a job that will use RCCL (--transport=rccl, --collectives=rccl, or the auto transport across nodes)
 //     also pays RCCL's one-time start-up there — 1.7 s of library registration and code-object loading,
 //     profiles/rccl_init_rootcause.log — on the rank's device (node-local rank from the launcher's
@@ -567,7 +566,10 @@ std::future<void> early_prewarm(int argc, char** argv) {
     const int64_t min_bytes = flags.get_int("gpu-prewarm-bytes", int64_t{64} << 20);
     const bool big = !path.empty() && stat(path.c_str(), &st) == 0 && S_ISREG(st.st_mode) && min_bytes > 0 &&
                      st.st_size >= min_bytes;
-    if (!big && !rccl) return {};
+    // --backend=hip: the job will use the GPU whatever its size, so its runtime starts now, beside MPI_Init,
+    // the read and the header broadcast, instead of at the engine's set-up
+    const bool hip = to_lower(flags.get("backend", "auto")) == "hip";
+    if (!big && !rccl && !hip) return {};
     int device = static_cast<int>(flags.get_int("device", -1));
     const std::vector<int> map = parse_int_list(flags.get("device-map", ""));
     if (device < 0 && !map.empty()) device = map[static_cast<size_t>(local) % map.size()];

@@ -8,6 +8,7 @@
 #include <future>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -250,9 +251,17 @@ class GpuRankImpl final : public GpuRank {
             if (device_info(i).pci_bus_id == bus) id = i;
         }
         if (id < 0) id = select_device(local, requested);
-        if (id != eo.device)
+        if (id != eo.device) {
           MOC_LOG_INFO("device %s is the runtime's %d, the driver topology's %d: using %d", bus.c_str(), id, eo.device,
                        id);
+          // the NUMA node was taken from the topology's device: take the one the runtime resolved, and let
+          // the rank's main thread re-bind at its next device call (bind_thread)
+          const int node = device_numa_node(id);
+          if (node >= 0 && node != numa_.load()) {
+            numa_.store(node);
+            rebind_.store(true);
+          }
+        }
         eo.device = id;
         device_.store(id);
       }
@@ -307,7 +316,7 @@ class GpuRankImpl final : public GpuRank {
     engine().search_keys(codes, offsets, n, part, parts, keys);
   }
   double last_kernel_ms() const override { return engine().stats().kernel_ms; }
-  int numa_node() const override { return numa_; }
+  int numa_node() const override { return numa_.load(); }
   bool runtime_ready() const override { return runtime_up_.load(); }
   void solve_wire(const WireBatch& b, void* out, ResultFormat fmt) override { engine().solve_wire(b, out, fmt); }
   void begin_wire(const WireBatch& b, void* out, ResultFormat fmt) override { engine().begin_wire(b, out, fmt); }
@@ -321,7 +330,7 @@ class GpuRankImpl final : public GpuRank {
     const ProblemFacts f = facts();
     if (!f.set) return engine().streams_packed(min_l2, max_l2);
     dev::ShortArgs a;
-    a.packed24 = 1;  // the widest LDS layout of the packed forms (HipEngine::streams_packed)
+    a.packed33 = 1;  // the widest LDS layout of the letter forms (HipEngine::streams_packed)
     return dev::configure_swipe(f.L1, min_l2, max_l2, f.max_abs, a);
   }
   ResultFormat result_format(int64_t min_l2, int64_t max_l2) const override {
@@ -432,6 +441,8 @@ class GpuRankImpl final : public GpuRank {
   // the calling thread's current HIP device = this rank's (the runtime keeps one per thread; the engine
   // may have started on another thread)
   void bind_thread() const {
+    if (rebind_.load() && std::this_thread::get_id() == main_thread_ && rebind_.exchange(false))
+      (void)bind_numa_node(numa_.load());
     thread_local int current = -1;
     const int d = device_.load();
     if (current != d) {
@@ -442,7 +453,9 @@ class GpuRankImpl final : public GpuRank {
 
   const MpiContext& ctx_;
   std::atomic<int> device_{-1};
-  int numa_ = -1;
+  std::atomic<int> numa_{-1};
+  mutable std::atomic<bool> rebind_{false};  // numa_ changed after the main thread was bound to the old node
+  const std::thread::id main_thread_ = std::this_thread::get_id();
   mutable std::future<std::unique_ptr<HipEngine>> pending_engine_;
   mutable std::once_flag ready_;
   mutable std::mutex mu_;

@@ -92,7 +92,7 @@ void run_sliced(JobCore& job, BulkParser& parser, int64_t first_index, SharedWin
   HostRegion wire, len16;
   auto al64 = [](int64_t x) { return (x + 63) & ~int64_t{63}; };
   int64_t off_bytes = 0, len_at = 0;  // the offsets' and the lengths' byte offsets in `wire`
-  int letters_pack = 5;  // GPU ranks: 33 = P33 fields, 24 = P24 groups, 5 = 5-bit packed
+  int letters_pack = 5;  // GPU ranks: 33 = P33 fields, 5 = 5-bit packed
   int64_t letter_bytes = 0;
   RecordBatch cpu_batch;
   FillReport rep;
@@ -102,8 +102,7 @@ void run_sliced(JobCore& job, BulkParser& parser, int64_t first_index, SharedWin
       cpu_batch.offsets.resize(static_cast<size_t>(n) + 1);
       rep = parser.fill_slice(slice, cpu_batch.codes.data(), nullptr, cpu_batch.offsets.data());
     } else {
-      // letters as P33 fields (4.714 bits each; --letters=p24: P24 groups, 4.8) for the streaming kernel,
-      // else 5-bit packed
+      // letters as P33 fields (4.714 bits each) for the streaming kernel, else 5-bit packed
       auto dense_form = [&] {
         letters_pack = 5;
         letter_bytes = packed5_bytes(slice.letters);
@@ -112,9 +111,9 @@ void run_sliced(JobCore& job, BulkParser& parser, int64_t first_index, SharedWin
         rep = parser.fill_slice(slice, nullptr, wire.as<uint8_t>(), reinterpret_cast<int64_t*>(wire.data() + off_bytes));
       };
       if (narrow) {
-        const int pack = job.group_pack();
+        const int pack = 33;
         letters_pack = pack;
-        letter_bytes = pack == 33 ? packed33_bytes(slice.letters) : packed24_bytes(slice.letters);
+        letter_bytes = packed33_bytes(slice.letters);
         off_bytes = al64(letter_bytes + 16);
         len_at = off_bytes + al64(8 * sparse_count(n, kSparseShift));
         wire = HostRegion(static_cast<size_t>(len_at + al64(n + 16)), numa);  // lengths: <= 1 byte each
@@ -173,7 +172,6 @@ void run_sliced(JobCore& job, BulkParser& parser, int64_t first_index, SharedWin
   ResultFormat fmt = ResultFormat::R12;
   if (gpu && n > 0) {
     wb.letters = wire.as<uint8_t>();
-    wb.packed24 = letters_pack == 24;
     wb.packed33 = letters_pack == 33;
     wb.packed5 = letters_pack == 5;
     wb.n = n;

@@ -118,6 +118,7 @@ class StreamFlow {
   std::unique_ptr<AreaText> text_;  // root
   std::unique_ptr<Cutter> cutter_;  // root
   int64_t next_index_ = 0;          // global index of the next batch's first record
+  int64_t drop_at_ = 0;             // root, stream input: text before this may go once the batch is encoded
   InSlot in_[2];
   std::unique_ptr<SegmentWindow> res_[2];
   int64_t res_cap_[2] = {0, 0};  // this rank's segment bytes
@@ -240,7 +241,10 @@ BatchMsg StreamFlow::next_batch(std::vector<int64_t>& table) {
       table[2 * m.nchunks + 1 + c] = ch.chars;
     }
     table[m.nchunks] = m.end - m.begin;
-    if (!text_->mapped()) text_->drop_before(cut.next);  // kept until this batch is encoded (see run)
+    // A stream's text before cut.next is dropped only after this batch is encoded (run): fill() may load
+    // more text (count_ahead) while batch_area() still points into the buffer, and a load may move or
+    // free the text it has been told it can drop.
+    drop_at_ = cut.next;
   }
   if (m.nchunks > 0) bcast_bytes(table.data(), 8 * static_cast<int64_t>(table.size()), kRoot, j_.ctx.world);
   j_.pt.end();
@@ -276,6 +280,23 @@ const char* StreamFlow::batch_area(const BatchMsg& m, int s) {
 bool StreamFlow::fill(const BatchMsg& m, const std::vector<int64_t>& table, int s, Done& d) {
   const MpiContext& ctx = j_.ctx;
   const int p = ctx.size, r = ctx.rank;
+  // A GPU job's first ring slot is page-locked only once the HIP runtime is up: the root counts later batches
+  // meanwhile (mapped input: up to 32 batches ahead, ~3 ms of counting each; a stream holds what it counts,
+  // so 2). This runs before the batch's text is located (batch_area): counting a stream loads more text,
+  // and a load may move the buffer's text (dropping what earlier batches used) or reallocate the buffer.
+  if (gpu_ && cutter_ && in_[s].arena.cap == 0 && !gpu_->runtime_ready()) {
+    Stopwatch ca;
+    ca.start();
+    const int64_t ahead = src_.mapped ? 32 : 2;
+    try {
+      while (!gpu_->runtime_ready() && cutter_->count_ahead(max_rec_, max_chr_, ahead)) {
+      }
+    } catch (const std::exception&) {
+      // a read error ahead of the batches: the batch that reaches it reports it (next_batch)
+    }
+    ca.stop();
+    count_ahead_ms_ += ca.total_ms();
+  }
   const char* area = batch_area(m, s);
   j_.pt.begin("fill");
   j_.fault.at("distribute", r);
@@ -307,29 +328,13 @@ bool StreamFlow::fill(const BatchMsg& m, const std::vector<int64_t>& table, int 
     // one page-locked arena per slot, carved into letters | offsets | lengths: one registration per slot
     // (each registration costs milliseconds, whatever its size)
     auto al64 = [](int64_t x) { return (x + 63) & ~int64_t{63}; };
-    // The first slot's page-locking waits for the HIP runtime's start-up: the root counts later batches
-    // meanwhile (mapped input: up to 32 batches ahead, ~3 ms of counting each; a stream holds what it
-    // counts, so 2)
-    if (in.arena.cap == 0 && cutter_ && !gpu_->runtime_ready()) {
-      Stopwatch ca;
-      ca.start();
-      const int64_t ahead = src_.mapped ? 32 : 2;
-      try {
-        while (!gpu_->runtime_ready() && cutter_->count_ahead(max_rec_, max_chr_, ahead)) {
-        }
-      } catch (const std::exception&) {
-        // a read error ahead of the batches: the batch that reaches it reports it (next_batch)
-      }
-      ca.stop();
-      count_ahead_ms_ += ca.total_ms();
-    }
     bool narrow = L1 <= 200 && slice.letters <= 32 * n;
-    const int pack = narrow ? j_.group_pack() : 5;
+    const int pack = narrow ? 33 : 5;
     uint8_t* letters = nullptr;
     int64_t* offsets = nullptr;
     uint8_t* lens = nullptr;
     if (narrow) {
-      const int64_t lb = al64((pack == 33 ? packed33_bytes(slice.letters) : packed24_bytes(slice.letters)) + 16);
+      const int64_t lb = al64(packed33_bytes(slice.letters) + 16);
       const int64_t sb = al64(8 * sparse_count(n, kSparseShift));
       ensure(in.arena, lb + sb + al64(n + 16), true);  // lengths: at most one byte each (+ slack)
       letters = in.arena.as<uint8_t>();
@@ -355,7 +360,6 @@ bool StreamFlow::fill(const BatchMsg& m, const std::vector<int64_t>& table, int 
     WireBatch& wb = d.wb;
     wb.letters = letters;
     wb.packed33 = narrow && pack == 33;
-    wb.packed24 = narrow && pack == 24;
     wb.packed5 = !narrow;
     wb.n = n;
     wb.min_l2 = rep.min_len;
@@ -517,6 +521,7 @@ int StreamFlow::run() {
     BatchMsg m = next_batch(table);
     bool ok = m.status == 0;
     if (ok && m.n > 0) ok = fill(m, table, s, done[s]);  // while the kernel of batch b-1 streams
+    if (ctx.rank == kRoot && !text_->mapped()) text_->drop_before(drop_at_);  // batch b's text is encoded
     if (have_prev) {  // F + E of batch b-1 (also before leaving on an input error of batch b)
       finish(s ^ 1, done[s ^ 1]);
       if (ok && m.n > 0) launch(s, done[s]);

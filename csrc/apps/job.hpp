@@ -123,8 +123,6 @@ struct JobCore {
   void resolve_keys(const uint64_t* keys, const uint8_t* codes, const int64_t* offsets, int64_t n, Result* res);
   // root: rows of the current batch (first = index relative to the batch)
   void print(const Result* r, int64_t n, int64_t first);
-  // group letter code of GPU slices: 33 (P33 fields, default) or 24 (--letters=p24)
-  int group_pack() const;
   CostModel cost_model() const { return all_gpu ? CostModel{1.0, 200.0, 2400.0} : CostModel{1.0, 4.0, 64.0}; }
   // collective: the --timing JSON line on root's stderr
   void report(const Header& h);

@@ -137,12 +137,6 @@ void RankEngine::solve_keys(const uint8_t* codes, const int64_t* offsets, int64_
 
 // ---- JobCore
 
-int JobCore::group_pack() const {
-  const std::string v = to_lower(flags.get("letters", "p33"));
-  if (v != "p33" && v != "p24") throw Error("--letters must be p33|p24");
-  return v == "p24" ? 24 : 33;
-}
-
 void JobCore::setup_engine(int64_t job_cells, int64_t mean_l2) {
   const int threads = static_cast<int>(flags.get_int("threads", 0));
   std::string backend = to_lower(flags.get("backend", "auto"));

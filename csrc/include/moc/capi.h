@@ -33,10 +33,6 @@ int64_t moc_format_results(const moc_result* r, int64_t n, int64_t first_index, 
 int64_t moc_packed5_bytes(int64_t n_chars);
 int moc_pack5(const uint8_t* codes, int64_t n, uint8_t* out);
 int moc_unpack5(const uint8_t* packed, int64_t begin, int64_t n, uint8_t* out);
-// base-26 groups: 5 letters per 3 bytes (moc::pack24, 4.8 bits per letter)
-int64_t moc_packed24_bytes(int64_t n_chars);
-int moc_pack24(const uint8_t* codes, int64_t n, uint8_t* out);
-int moc_unpack24(const uint8_t* packed, int64_t begin, int64_t n, uint8_t* out);
 // 33-bit fields: 7 letters per field, 56 letters per 33 bytes (moc::pack33, 4.714 bits per letter)
 int64_t moc_packed33_bytes(int64_t n_chars);
 int moc_pack33(const uint8_t* codes, int64_t n, uint8_t* out);
@@ -96,7 +92,7 @@ int moc_engine_solve(void* e, const uint8_t* codes, const int64_t* offsets, int6
  * optional (NULL / -1). Pinned host buffers + short records -> zero-copy streaming kernel. */
 int moc_engine_solve_ex(void* e, const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths, int len_bits,
                         int len_base, int64_t n, void* out, int fmt, int64_t min_l2, int64_t max_l2,
-                        int packed);  // packed: 0 byte letters, 1 5-bit packed, 2 P24 groups, 3 P33 fields
+                        int packed);  // packed: 0 byte letters, 1 5-bit packed, 3 P33 fields
 int moc_engine_auto_format(void* e, int64_t max_l2, int64_t min_l2);
 /* R2 parameters {smin, kw, j} for records with lengths in [min_l2, max_l2] */
 int moc_engine_r2_params(void* e, int64_t min_l2, int64_t max_l2, int32_t* out3);

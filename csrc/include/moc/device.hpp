@@ -146,8 +146,6 @@ struct ShortArgs {
   int32_t codes_cap = 0;              // LDS bytes for one tile's letters (>= tile_records*max_l2+32)
   int32_t max_l2 = 0;
   int32_t packed5 = 0;                // 1: `codes` is a 5-bit packed stream (char j at bit 5j); swipe only
-  int32_t packed24 = 0;               // 1: `codes` holds P24 groups (moc::pack24: char j in group j / 5,
-                                      // bytes 3 * (j / 5)); decoded into LDS per tile; swipe only
   int32_t packed33 = 0;               // 1: `codes` holds P33 fields (moc::pack33: char j in field j / 7 at
                                       // bit 33 * (j / 7)); decoded into LDS per tile; swipe only
   unsigned* counter = nullptr;        // device work counter {next tile, blocks done}; zero at launch, the

@@ -38,22 +38,16 @@ struct EngineOptions {
   int64_t chunk_bytes = 64ll << 20;  // staged pipeline: max letter bytes per chunk
   bool allow_direct = true;          // use zero-copy streaming when the host buffers are pinned
   bool use_graphs = true;            // replay the direct path's launches as a captured hipGraph
-  // pinned host batches: 0 = the streaming kernel reads / writes host memory itself (zero-copy);
-  // 1 = copy engines (SDMA) move letters in and results out in chunks while the kernel runs from HBM.
-  // On hipHostMalloc buffers SDMA moves the 3:1 in/out mix at 57 GB/s in vs 45 zero-copy
-  // (profiles/transfer_probe.log), but on the registered (hipHostRegister) node-shared arrays the
-  // headline streams from, the chunked SDMA path measured 4.4 ms/step against 4.0 zero-copy
-  // (profiles/host_stream_ab.log): zero-copy stays the default, SDMA is MOC_DMA_STREAM=1.
-  int dma_stream = 0;
-  int64_t dma_chunk_bytes = 16ll << 20;  // letter bytes per DMA chunk
+  // Pinned host batches stream zero-copy: the kernel reads / writes host memory itself. A chunked SDMA
+  // pipeline around the HBM-resident kernel was measured slower on the registered node-shared arrays the
+  // headline streams from (4.4 vs 4.0 ms/step, profiles/host_stream_ab.log) and was retired in round 4.
 };
 
 struct EngineStats {
   double kernel_ms = 0;  // device time of the search kernels (events), last solve
   double total_ms = 0;   // wall time of the last solve call
   int64_t h2d_bytes = 0, d2h_bytes = 0, chunks = 0, cells = 0, records = 0;
-  int32_t direct = 0;    // 1 if the last solve streamed from pinned host memory (zero-copy or DMA)
-  int32_t dma = 0;       // 1 if that stream went through the copy engines (chunked SDMA)
+  int32_t direct = 0;    // 1 if the last solve streamed from pinned host memory (zero-copy)
   int32_t format = 0;    // ResultFormat of the last solve
   int32_t kernels = 0;   // bitmask of kernels used: 1 swipe (lane/record), 2 short (lane/offset), 4 tiles
   R2Params r2;           // parameters of the R2 results of the last solve (when fmt == R2)
@@ -84,8 +78,8 @@ class HipEngine {
   void solve(const uint8_t* codes, const int64_t* offsets, int64_t n, Result* out);
   // General form: optional narrow lengths — len_bits 8 (uint8, max L2 <= 255) or 4 (two per byte, low
   // nibble first, record i = len_base + nibble) — results in `fmt`. `packed`: 1 = `codes` is a 5-bit
-  // packed stream (moc::pack5; char j at bit 5j), 2 = P24 groups (moc::pack24), 3 = P33 fields
-  // (moc::pack33), 0 = one byte per letter.
+  // packed stream (moc::pack5; char j at bit 5j), 3 = P33 fields (moc::pack33; 2 was the retired P24 code)
+  // 0 = one byte per letter.
   // R2 results are encoded for the hints' [min_l2, max_l2] (or the batch's own range): stats().r2 holds
   // the parameters.
   void solve_ex(const uint8_t* codes, const int64_t* offsets, const uint8_t* lengths, int64_t n, void* out,
@@ -169,8 +163,6 @@ class HipEngine {
   bool direct_pointers(const WireBatch& b, void* out, int fb, dev::ShortArgs& a) const;
   void prepare_direct(const dev::ProblemView& pv, const dev::ShortArgs& a, bool swipe);
   void launch_direct(const dev::ProblemView& pv, const dev::ShortArgs& a, bool swipe);
-  void run_dma_stream(const dev::ProblemView& pv, const dev::ShortArgs& a, bool swipe, const WireBatch& b, void* out,
-                      int fb);
   void run_staged(const uint8_t* codes, const int64_t* offsets, int64_t n, void* out, ResultFormat fmt,
                   bool packed5);
   void solve_wire_impl(const WireBatch& b, void* out, ResultFormat fmt, bool async);

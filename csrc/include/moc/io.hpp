@@ -90,8 +90,8 @@ class BulkParser {
   // ---- pass 2
   AreaSlice slice(int64_t rec_begin, int64_t rec_end) const;
   // Encodes slice s: letters as bytes into codes[0..s.letters) and/or packed into `packed` (either may be
-  // null): `pack` 5 = 5-bit packed, packed[0..packed5_bytes(s.letters)); 24 = P24 groups (moc::pack24),
-  // packed[0..packed24_bytes(s.letters)); 33 = P33 fields (moc::pack33), packed[0..packed33_bytes(s.letters)).
+  // null): `pack` 5 = 5-bit packed, packed[0..packed5_bytes(s.letters)); 33 = P33 fields (moc::pack33),
+  // packed[0..packed33_bytes(s.letters)).
   // Record boundaries (each output optional): dense
   // offsets[0..s.records] rebased to 0; sparse offsets (moc/wire.hpp, stride 2^kSparseShift)
   // sparse[0..sparse_count(s.records, kSparseShift)); lengths len16[0..s.records), saturated at 65535

@@ -43,7 +43,7 @@ struct DefaultInitAllocator : std::allocator<T> {
   T* allocate(size_t n) {
     const size_t bytes = n * sizeof(T);
     if (bytes < kMapBytes) return std::allocator<T>::allocate(n);
-    void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
     if (p == MAP_FAILED) throw std::bad_alloc();
     const uintptr_t huge = uintptr_t{2} << 20;
     const uintptr_t lo = (reinterpret_cast<uintptr_t>(p) + huge - 1) & ~(huge - 1);
@@ -103,30 +103,12 @@ void pack5(const uint8_t* codes, int64_t n, uint8_t* out);
 // Inverse for chars [begin, begin + n) of a packed stream.
 void unpack5(const uint8_t* packed, int64_t begin, int64_t n, uint8_t* out);
 
-// ---- base-26 letter groups ("P24": 4.8 bits per letter) --------------------------------------------------
-// Letters 5j .. 5j+4 of the stream form group j, stored in bytes [3j, 3j+3) as the little-endian 24-bit
-// value sum_i (code - 1) * 26^i (26^5 = 11 881 376 < 2^24). Padding (code 0) is stored as letter 1: readers
-// bound every record by its length. 4% fewer bytes than 5-bit packing, still byte-aligned per group, so a
-// reader finds letter x in group x / 5 without a bit cursor. The streaming kernel is PCIe-bound: these
-// bytes are the headline's time.
-constexpr int kP24Letters = 5, kP24Bytes = 3;
-inline int64_t packed24_bytes(int64_t n_chars) { return kP24Bytes * ((n_chars + kP24Letters - 1) / kP24Letters) + 16; }
-// Group value of 5 codes (codes 0 count as 1).
-inline uint32_t p24_group(const uint8_t* c, int m = kP24Letters) {
-  uint32_t v = 0;
-  for (int j = m - 1; j >= 0; --j) v = v * 26u + (c[j] > 1 ? c[j] - 1u : 0u);
-  return v;
-}
-// codes[0..n) -> out[0..packed24_bytes(n)) (OpenMP; slack bytes zeroed).
-void pack24(const uint8_t* codes, int64_t n, uint8_t* out);
-// Letters [begin, begin + n) back as codes 1..26.
-void unpack24(const uint8_t* packed, int64_t begin, int64_t n, uint8_t* out);
-
 // ---- 33-bit letter fields ("P33": 4.714 bits per letter) -------------------------------------------------
 // Letters 7f .. 7f+6 form field f, the value sum_i (code - 1) * 26^i (26^7 = 8 031 810 176 < 2^33) stored
 // at bits [33f, 33f+33) of a little-endian bit stream. Eight fields (56 letters) fill exactly 33 bytes, so
 // blocks of 56 letters are byte-aligned: the unit of parallel encoding and of a reader's byte ranges.
-// 1.8% fewer bytes than P24 (log2 26 = 4.700 is the floor); a field decodes with 32-bit arithmetic only
+// 5.7% fewer bytes than 5-bit packing (log2 26 = 4.700 is the floor; round 3's 5-letters-in-3-bytes groups,
+// retired in round 4, took 4.8); a field decodes with 32-bit arithmetic only
 // (the first division as (v >> 1) / 13, the other six on a value < 2^29).
 constexpr int kP33Field = 7, kP33Letters = 56, kP33Bytes = 33;
 inline int64_t packed33_bytes(int64_t n_chars) { return kP33Bytes * ((n_chars + kP33Letters - 1) / kP33Letters) + 16; }

@@ -5,8 +5,8 @@
 // Reference: one byte per letter in a fixed 2000-byte stride per record (main.c:93, scattered whole at
 // main.c:174) and three separate int arrays of results (main.c:123-125, gathered at main.c:195-197).
 //
-//   letters  base-26 groups of 5 letters in 3 bytes (moc::pack24, 4.8 bits per letter), the 5-bit packed
-//            stream (char j at bits [5j, 5j+5), little endian: moc::pack5), or bytes (problem.hpp)
+//   letters  33-bit fields of 7 letters (moc::pack33, 4.714 bits per letter), the 5-bit packed stream
+//            (char j at bits [5j, 5j+5), little endian: moc::pack5), or bytes (problem.hpp)
 //   lengths  8-, 4- (two per byte, low nibble first) or 3-bit (bits [3i, 3i+3), LSB first) above a base
 //   results  R12 (moc::Result) / R8 / R4 / R2 (one uint16 mixed-radix code per record)
 #pragma once
@@ -120,9 +120,8 @@ void expand_offsets(const int64_t* sparse, int shift, const uint8_t* lengths, in
 // One host batch in the wire formats above: what `final`'s parser writes for a rank's slice and what the
 // engines take. `offsets` is dense (off_shift 0, n+1 entries) or sparse (off_shift > 0, lengths required).
 struct WireBatch {
-  const uint8_t* letters = nullptr;  // P33 fields, P24 groups, 5-bit packed (packed5) or one byte per letter;
+  const uint8_t* letters = nullptr;  // P33 fields, 5-bit packed (packed5) or one byte per letter;
   bool packed5 = false;              // record i at letter offsets[i]
-  bool packed24 = false;
   bool packed33 = false;             // P33 fields (moc::pack33)
   const int64_t* offsets = nullptr;
   int off_shift = 0;
@@ -136,8 +135,6 @@ struct WireBatch {
   int64_t end_letter() const { return offsets[off_shift ? sparse_count(n, off_shift) - 1 : n]; }
   int64_t letter_bytes() const {
     const int64_t L = end_letter() - first_letter();
-    if (packed24)
-      return kP24Bytes * ((end_letter() + kP24Letters - 1) / kP24Letters - first_letter() / kP24Letters);
     if (packed33) return p33_end_byte(end_letter()) - p33_first_byte(first_letter());
     return packed5 ? (5 * L + 7) / 8 : L;
   }

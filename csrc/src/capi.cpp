@@ -109,13 +109,6 @@ int moc_pack5(const uint8_t* codes, int64_t n, uint8_t* out) {
 int moc_unpack5(const uint8_t* packed, int64_t begin, int64_t n, uint8_t* out) {
   return guard([&] { moc::unpack5(packed, begin, n, out); });
 }
-int64_t moc_packed24_bytes(int64_t n_chars) { return moc::packed24_bytes(n_chars); }
-int moc_pack24(const uint8_t* codes, int64_t n, uint8_t* out) {
-  return guard([&] { moc::pack24(codes, n, out); });
-}
-int moc_unpack24(const uint8_t* packed, int64_t begin, int64_t n, uint8_t* out) {
-  return guard([&] { moc::unpack24(packed, begin, n, out); });
-}
 int64_t moc_packed33_bytes(int64_t n_chars) { return moc::packed33_bytes(n_chars); }
 int moc_pack33(const uint8_t* codes, int64_t n, uint8_t* out) {
   return guard([&] { moc::pack33(codes, n, out); });
@@ -393,7 +386,7 @@ int moc_engine_stats(void* e, double* out14) {
   return guard([&] {
     double* out13 = out14;
     double* out10 = out14;
-    out14[13] = static_cast<double>(static_cast<moc::HipEngine*>(e)->stats().dma);
+    out14[13] = 0;  // was the retired SDMA mode's flag
     const auto& s = static_cast<moc::HipEngine*>(e)->stats();
     out13[10] = s.r2.smin;
     out13[11] = s.r2.kw;

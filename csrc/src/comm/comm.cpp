@@ -149,7 +149,7 @@ SharedWindow::SharedWindow(const MpiContext& ctx, int64_t bytes) : comm_(ctx.nod
     const size_t align = huge ? size_t{2} << 20 : size_t{4096};
     const size_t want = (static_cast<size_t>(std::max<int64_t>(bytes, 8)) + align - 1) & ~(align - 1);
     map_bytes_ = huge ? want + align : want;  // slack to start on a 2 MiB boundary
-    map_ = mmap(nullptr, map_bytes_, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    map_ = mmap(nullptr, map_bytes_, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
     if (map_ == MAP_FAILED) {
       map_ = nullptr;
       throw Error("SharedWindow: cannot map " + std::to_string(map_bytes_) + " bytes");

@@ -85,8 +85,6 @@ void CpuDeviceSearch::solve(const WireBatch& b, void* out, ResultFormat fmt) {
   rb.codes.resize(static_cast<size_t>(letters));
   if (b.packed33)
     unpack33(b.letters, c0, letters, rb.codes.data());
-  else if (b.packed24)
-    unpack24(b.letters, c0, letters, rb.codes.data());
   else if (b.packed5)
     unpack5(b.letters, c0, letters, rb.codes.data());
   else

@@ -1,23 +1,28 @@
 // Inter-record SIMD kernel for tiny problems (input6-shaped: |Seq1| <= ~100, |Seq2| <= 32, small W).
 //
 // One LANE = one whole record (vs. one lane per offset in short_kernels.hip): every lane keeps all its
-// offsets' running diagonal sums P_o in registers as packed int16 pairs, so
+// offsets' running diagonal sums in registers as packed int16 pairs, so
 //   * no cross-lane traffic at all in the hot loop (no DPP, no segmented reductions per record),
-//   * two cells per VALU op (v_pk_add_u16 / v_pk_sub_u16 / v_pk_mad_u16 / v_pk_max_i16),
-//   * the profile row segment S[c][i .. i+NOFF) a lane needs at step i is read with NOFF/8 aligned
-//     ds_read_b128: the block keeps 8 copies of the int16 profile, copy s shifted left by s columns, so
-//     step i reads copy (i mod 8) at column i - (i mod 8) (a multiple of 8 -> 16-byte aligned).
+//   * two cells per VALU op (v_pk_add_u16 / v_pk_max_i16),
+//   * the profile row segment a lane needs at step i is read with NOFF/8 aligned ds_read_b128: the block
+//     keeps 8 copies of the int16 profile, copy s shifted left by s columns, so step i reads copy (i mod 8)
+//     at column i - (i mod 8) (a multiple of 8 -> 16-byte aligned).
 // The profile holds the diagonal DIFFERENCES Dt[c][j] = S[c][j] - S[c][j+1] (S = T[c][Seq1[j]], 0 past
-// Seq1 and in the padding row 0), so per step and per pair of offsets (2m, 2m+1):
-//     D2[m]  += (Dt[c][i+2m], Dt[c][i+2m+1])     = (D_2m(i+1), D_2m+1(i+1))     v_pk_add_u16
-//     B2[m]   = max(B2[m], D2 * 2^ks + (mask - (i+1)))                      v_pk_mad_u16 + v_pk_max_i16
-// i.e. 1.5 VALU ops per cell (2.5 when the running sums were P_o and the neighbour came from an
-// alignbit + subtract). Tot_o is not summed per cell: each lane sums the anchor diagonal
-// Tot_NOFF = sum_i T[c_i][Seq1[NOFF + i]] (an int8 LUT + Seq1 staged in LDS; 0 past Seq1, consistent with
-// the profile) and recovers Tot_o = Tot_{o+1} + D_o(L2) by a suffix pass over its offsets in the epilogue. Records stream through the same persistent, LDS-tiled block loop as the
-// short kernel (zero-copy from pinned host memory when the batch lives there).
+// Seq1 and in the padding row 0), pre-scaled and pre-biased: Pf[c][j] = Dt[c][j] * 2^KB - 1. A lane's
+// running sum for offset o after step i is then already the selection key of the mutant k = i + 1,
+//     E_o(i) = D_o(i+1) * 2^KB + (KMASK - (i+1)),    D_o(k) = sum_{i<k} Dt[c_i][o+i],
+// (larger D first, then smaller k), so per step and per pair of offsets (2m, 2m+1):
+//     E2[m] += (Pf[c][i+2m], Pf[c][i+2m+1])            v_pk_add_u16
+//     B2[m]  = max(B2[m], E2[m])                       v_pk_max_i16
+// i.e. 1 VALU op per cell (round 3: 2 more per pair for the shift and the step index). Tot_o is not
+// summed per cell: each lane sums the anchor diagonal Tot_NOFF = sum_i T[c_i][Seq1[NOFF + i]] (an int8
+// LUT + Seq1 staged in LDS; 0 past Seq1, consistent with the profile) and recovers
+// Tot_o = Tot_{o+1} + D_o(L2) by a suffix pass over its offsets in the epilogue, with
+// D_o(L2) = (E_o(steps-1) - (KMASK - steps)) >> KB (steps past a record's end add the padding row, Dt 0).
+// A wave runs steps = its longest record's length. Records stream through the same persistent, LDS-tiled
+// block loop as the short kernel (zero-copy from pinned host memory when the batch lives there).
 // Exactness: int16 arithmetic is exact because the host only selects this kernel when
-// 2*max|W|*max|Seq2|*2^ks + mask < 2^15 (no key can wrap) — see configure_swipe.
+// 2*max|W|*max|Seq2|*2^KB + 2^KB < 2^15 (no key can wrap) — see configure_swipe.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -49,18 +54,16 @@ struct SwipeLayout {
   int copy_elems = 0;   // 27 * row
   int prof_bytes = 0;   // 8 shifted copies of the Dt profile
   int s_off = 0;        // int8 LUT (32 x 32, column 31 = 0) + Seq1 codes (31 past Seq1): anchor diagonal
-  int loff_off = 0, codes_off = 0, res_off = 0, raw_off = 0, total = 0;  // raw: P24 / P33 bytes as loaded
+  int loff_off = 0, codes_off = 0, res_off = 0, raw_off = 0, total = 0;  // raw: P33 bytes as loaded
 };
 
 inline int al16(int x) { return (x + 15) & ~15; }
 
-// P24 tiles: the loaded group bytes (3 per 5 letters, + alignment) of at most codes_cap letters
-inline int p24_raw_cap(int codes_cap) { return 3 * (codes_cap / 5 + 2) + 32; }
-// P33 tiles: 33 bits per 7 letters
+// P33 tiles: the loaded field bytes (33 bits per 7 letters, + alignment) of at most codes_cap letters
 inline int p33_raw_cap(int codes_cap) { return (33 * (codes_cap / 7 + 2) + 7) / 8 + 32; }
 // LDS bytes of a tile's raw (still encoded) letters by letter form
-inline int raw_cap(int lf, int codes_cap) { return lf == 2 ? p24_raw_cap(codes_cap) : lf == 3 ? p33_raw_cap(codes_cap) : 0; }
-inline int letter_form(const ShortArgs& a) { return a.packed33 ? 3 : a.packed24 ? 2 : a.packed5 ? 1 : 0; }
+inline int raw_cap(int lf, int codes_cap) { return lf == 2 ? p33_raw_cap(codes_cap) : 0; }
+inline int letter_form(const ShortArgs& a) { return a.packed33 ? 2 : a.packed5 ? 1 : 0; }
 
 SwipeLayout swipe_layout(int L1, int noff, int l2w, int tile_records, int codes_cap, int fb, int lf) {
   SwipeLayout l;
@@ -84,11 +87,10 @@ inline int kbits_for(int l2w) {  // bits for k in the int16 keys: k <= 4*l2w
 }
 }  // namespace
 
-// LF: letter format of `a.codes` — 0 bytes, 1 5-bit packed, 2 P24 groups, 3 P33 fields (2 and 3 decoded to
-// bytes in LDS per tile)
+// LF: letter format of `a.codes` — 0 bytes, 1 5-bit packed, 2 P33 fields (decoded to bytes in LDS per tile)
 template <int NOFF, int L2W, int LF>
 __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, ShortArgs a, SwipeLayout lay) {
-  constexpr bool P5 = LF == 1, P24 = LF == 2, P33 = LF == 3;
+  constexpr bool P5 = LF == 1, P33 = LF == 2;
   constexpr int kRpt = rpt_of(LF);
   constexpr int NW = P5 ? (20 * L2W + 31) / 32 : L2W;  // record words held per lane
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -99,7 +101,7 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
   int* misc = loff + a.tile_records + 1;
   uint8_t* codes_l = smem + lay.codes_off;
   uint8_t* res_l = smem + lay.res_off;
-  uint8_t* raw_l = smem + lay.raw_off;  // P24 / P33: the tile's encoded bytes as loaded
+  uint8_t* raw_l = smem + lay.raw_off;  // P33: the tile's encoded bytes as loaded
   const int L1 = pv.L1;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int KB = (4 * L2W < 8) ? 3 : (4 * L2W < 16) ? 4 : (4 * L2W < 32) ? 5 : (4 * L2W < 64) ? 6 : 7;
@@ -155,14 +157,8 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
 #pragma unroll
       for (int q = 0; q < 4; ++q) f.lens[4 * h + q] = l4[q];
     }
-    const int64_t b_first = P33   ? (33 * (f.start / 7)) >> 3
-                            : P24 ? 3 * (f.start / 5)
-                            : P5  ? (5 * f.start) >> 3
-                                  : f.start;
-    const int64_t b_end = P33   ? (33 * ((f.end + 6) / 7) + 7) >> 3
-                          : P24 ? 3 * ((f.end + 4) / 5)
-                          : P5  ? (5 * f.end + 7) >> 3
-                                : f.end;
+    const int64_t b_first = P33 ? (33 * (f.start / 7)) >> 3 : P5 ? (5 * f.start) >> 3 : f.start;
+    const int64_t b_end = P33 ? (33 * ((f.end + 6) / 7) + 7) >> 3 : P5 ? (5 * f.end + 7) >> 3 : f.end;
     f.a0 = reinterpret_cast<uintptr_t>(a.codes + b_first) & ~uintptr_t{15};
     f.nvec = static_cast<int>((reinterpret_cast<uintptr_t>(a.codes + b_end) + 15 - f.a0) >> 4);
     MOC_DCHECK(f.nvec <= kMaxV * kBlock);
@@ -193,7 +189,7 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
   Fetch cur, nxt;
   fetch(grab(), cur);  // the first tile's loads are in flight while the block builds its profile
 
-  // ---- 8 shifted int16 difference-profile copies: prof[s][c][j] = Dt[c][j + s], and the plain S rows.
+  // ---- 8 shifted int16 difference-profile copies: prof[s][c][j] = Pf[c][j + s], and the plain S rows.
   //      Rows are 128-byte multiples, so the 16-byte chunk q of every row would start on the same LDS
   //      bank; chunk q of row c is stored at chunk q ^ (c & 7) instead, spreading the 16 lanes of a
   //      ds_read_b128 group (16 records reading 16 rows) over 8 bank quads — 8-way -> ~2-way conflicts.
@@ -204,7 +200,7 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
       const int j = ((((jj >> 3) ^ (c & 7)) << 3) | (jj & 7)) + s;  // element stored at jj holds column j
       const int sj = (c >= 1 && j < L1) ? pv.lut[c * kLutStride + pv.seq1[j]] : 0;
       const int sn = (c >= 1 && j + 1 < L1) ? pv.lut[c * kLutStride + pv.seq1[j + 1]] : 0;
-      prof[e] = static_cast<short>(sj - sn);
+      prof[e] = static_cast<short>((sj - sn) * (1 << KB) - 1);  // Pf = Dt * 2^KB - 1 (see the header)
     }
     // row 0 (padding letter: steps past a lane's record) and column 31 (past Seq1) contribute 0
     for (int e = tid; e < kLutInts; e += kBlock)
@@ -223,17 +219,16 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
     for (int q = 0; q < kRpt; ++q) sum += cur.lens[q];
     const int incl = wave_inclusive_sum(sum, lane);
     if (lane == 63) misc[4 + wave] = incl;
-    // ---- letters -> LDS. Byte codes: char j at byte j. Packed: char j at bit 5j. P24: the groups land in
-    //      raw_l and are decoded into bytes below (group gs = start / 5 -> codes_l[0..]).
+    // ---- letters -> LDS. Byte codes: char j at byte j. Packed: char j at bit 5j. P33: the fields land in
+    //      raw_l and are decoded into bytes below (field f0 = start / 7 -> codes_l[0..]).
     //      shift_b = position (bytes, or bits when P5) of the tile's first char inside the LDS copy.
 #pragma unroll
     for (int k = 0; k < kMaxV; ++k) {
       const int v = tid + k * kBlock;
-      if (v < cur.nvec) reinterpret_cast<uint4*>(P24 || P33 ? raw_l : codes_l)[v] = cur.v[k];
+      if (v < cur.nvec) reinterpret_cast<uint4*>(P33 ? raw_l : codes_l)[v] = cur.v[k];
     }
     const uintptr_t p0 = reinterpret_cast<uintptr_t>(a.codes + (P5 ? (5 * start) >> 3 : start));
-    const int shift_b = P33   ? static_cast<int>(start - 7 * (start / 7))
-                        : P24 ? static_cast<int>(start - 5 * (start / 5))
+    const int shift_b = P33  ? static_cast<int>(start - 7 * (start / 7))
                         : P5 ? static_cast<int>(8 * (p0 - cur.a0) + ((5 * start) & 7))
                              : static_cast<int>(p0 - cur.a0);
     if (tid == 0) {
@@ -255,23 +250,7 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
       loff[m] = excl;
       MOC_DCHECK(excl == end - start);  // lengths agree with offsets
     }
-    if (P24) {  // groups -> byte codes 1..26 (the staged bytes are complete: synchronised above)
-      const int64_t gs = start / 5;
-      const int ng = static_cast<int>((end + 4) / 5 - gs);
-      const int ro = static_cast<int>(reinterpret_cast<uintptr_t>(a.codes + 3 * gs) - cur.a0);
-      for (int g = tid; g < ng; g += kBlock) {
-        const uint8_t* r = raw_l + ro + 3 * g;
-        uint32_t v = r[0] | (static_cast<uint32_t>(r[1]) << 8) | (static_cast<uint32_t>(r[2]) << 16);
-        uint8_t* d = codes_l + 5 * g;
-#pragma unroll
-        for (int j = 0; j < 5; ++j) {
-          const uint32_t q = v / 26u;
-          d[j] = static_cast<uint8_t>(v - 26u * q + 1u);
-          v = q;
-        }
-      }
-    }
-    if (P33) {  // 33-bit fields -> byte codes 1..26 (field f0 = start / 7 -> codes_l[0..])
+    if (P33) {  // 33-bit fields -> byte codes 1..26 (the staged bytes are complete: synchronised above)
       const int64_t f0 = start / 7;
       const int nf = static_cast<int>((end + 6) / 7 - f0);
       const int64_t byte0 = (33 * f0) >> 3;
@@ -296,7 +275,7 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
       }
     }
     // next tile: its loads are in flight while this one is scored
-    fetch(grab(), nxt);  // grab() synchronises: loff / letters (decoded P24 / P33) are complete
+    fetch(grab(), nxt);  // grab() synchronises: loff / letters (decoded P33) are complete
 
     // ---- one record per lane
     for (int g = wave; g * 64 < m; g += 4) {
@@ -328,13 +307,13 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
           prev = nxt;
         }
       }
-      const int steps = wave_max_i32(on ? L2 : 0);
+      const int steps = wave_max_small(on ? L2 : 0);  // L2 <= 4 * L2W <= 32 here
 
-      uint32_t D2[NP], B2[NP];
+      uint32_t E2[NP], B2[NP];
       int anchor = 0;  // Tot_NOFF: the diagonal just past this lane's offsets
 #pragma unroll
       for (int q = 0; q < NP; ++q) {
-        D2[q] = 0u;
+        E2[q] = (static_cast<uint32_t>(KMASK) << 16) | KMASK;  // E_o(-1) = KMASK: D 0, k 0
         B2[q] = 0x80008000u;  // (INT16_MIN, INT16_MIN)
       }
 #pragma unroll
@@ -343,6 +322,9 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
           const int i = i0 + s;
+          // wave-uniform (scalar branch): a wave stops at its longest record, not at the next multiple of
+          // 8 steps (input6: 11 steps instead of 16); the copy index s stays a compile-time constant
+          if (i >= steps) break;
           int c;
           if (P5) {  // compile-time bit position 5i
             const int bit = 5 * i, w = bit >> 5, sh = bit & 31;
@@ -363,38 +345,48 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
           }
           anchor += lut8[(c << 5) | s1l[NOFF + i]];
 #pragma unroll
-          for (int q = 0; q < NP; ++q) D2[q] = as_u32(as_s16x2(D2[q]) + as_s16x2(v[q]));
-          const short kc = static_cast<short>(KMASK - (i + 1));
-          const s16x2 kadd = {kc, kc};
-          const s16x2 kmul = {static_cast<short>(1 << KB), static_cast<short>(1 << KB)};
-#pragma unroll
           for (int q = 0; q < NP; ++q) {
-            const s16x2 K = as_s16x2(D2[q]) * kmul + kadd;
-            B2[q] = as_u32(__builtin_elementwise_max(as_s16x2(B2[q]), K));
+            E2[q] = as_u32(as_s16x2(E2[q]) + as_s16x2(v[q]));
+            B2[q] = as_u32(__builtin_elementwise_max(as_s16x2(B2[q]), as_s16x2(E2[q])));
           }
         }
       }
 
-      // ---- per-lane selection over the record's offsets: 32-bit keys (score+2^15 | ~(o<<KB | k))
+      // ---- per-lane selection over the record's offsets: 32-bit keys (score+2^15 | ~(o<<KB | k)), 0 = none.
+      //      The valid offsets are prefixes: the un-mutated candidate at o < lim0 (o <= last = L1-L2 under
+      //      the spec semantics or when L2 == L1, else o < last), the mutants at o < lim1 = last (L2 >= 2).
+      //      Running sums carry the 2^15 bias, so a key is one shift-or of them (~13 VALU ops per offset).
+      //      Offsets below L1 - max_l2 (the batch's longest record) are valid for every lane that searches
+      //      (`on`): their limits are only applied above it (wave-uniform branch).
       const int last = L1 - L2;
+      const int lim0 = on ? last + ((sem == static_cast<int>(Semantics::Spec) || L2 == L1) ? 1 : 0) : 0;
+      const int lim1 = on && L2 >= 2 ? last : 0;
+      const int all_valid = L1 - a.max_l2;
+      // D_o(L2) pairs from the final running sums: (E - (KMASK - steps)) >> KB
+      const short eb = static_cast<short>(KMASK - steps);
+      const s16x2 ebias = {eb, eb};
       uint32_t best = 0;
-      int tot = anchor;  // Tot_{o+1} entering offset o (suffix pass: Tot_o = Tot_{o+1} + D_o(L2))
+      uint32_t tot = static_cast<uint32_t>(anchor + 32768);  // Tot_{o+1} + 2^15 entering offset o
 #pragma unroll
       for (int o = NOFF - 1; o >= 0; --o) {
-        const int Pn = tot;
-        const int Po = Pn + static_cast<short>(o & 1 ? (D2[o >> 1] >> 16) : (D2[o >> 1] & 0xffff));
-        tot = Po;
+        const s16x2 dq = (as_s16x2(E2[o >> 1]) - ebias) >> static_cast<short>(KB);
+        const uint32_t Pn = tot;  // Tot_{o+1} + 2^15
+        const uint32_t Po = Pn + static_cast<uint32_t>(static_cast<int>(o & 1 ? dq.y : dq.x));
+        tot = Po;  // suffix pass: Tot_o = Tot_{o+1} + D_o(L2)
+        const uint32_t kLow0 = 0xffffu - (static_cast<uint32_t>(o) << KB);  // ~(o << KB | 0)
+        const uint32_t kLow1 = kLow0 - KMASK;  // its low KB bits are 0: ~(o << KB | k) = kLow1 | (KMASK - k)
+        uint32_t k0 = (Po << 16) | kLow0;
+        // bk = d * 2^KB + (KMASK - k): the best mutant's D_o(k) and its k; t = (d + Tot_{o+1} + 2^15) * 2^KB + (KMASK - k)
         const int bk = static_cast<short>(o & 1 ? (B2[o >> 1] >> 16) : (B2[o >> 1] & 0xffff));
-        const bool own = on && o < need;
-        const bool v0 = own && (o < last || (o == last && (sem == static_cast<int>(Semantics::Spec) || L2 == L1)));
-        const uint32_t idx0 = static_cast<uint32_t>(o) << KB;
-        const uint32_t k0 = v0 ? ((static_cast<uint32_t>(Po + 32768) << 16) | (0xffffu - idx0)) : 0u;
-        const bool v1 = own && o < last && L2 >= 2 && bk != -32768;
-        const int d = bk >> KB;
-        const int kk = KMASK - (bk & KMASK);
-        const uint32_t k1 = v1 ? ((static_cast<uint32_t>(d + Pn + 32768) << 16) | (0xffffu - (idx0 | kk))) : 0u;
+        const uint32_t t = static_cast<uint32_t>(bk) + (Pn << KB);
+        uint32_t k1 = ((t >> KB) << 16) | (t & KMASK) | kLow1;
+        if (o >= all_valid) {  // wave-uniform
+          k0 = o < lim0 ? k0 : 0u;
+          k1 = o < lim1 ? k1 : 0u;
+        }
         best = max(best, max(k0, k1));
       }
+      if (!on) best = 0u;
       if (mine) {
         Result res;
         if (best == 0u) {
@@ -440,7 +432,7 @@ bool configure_swipe(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs
   const SwipeChoice ch = swipe_choice(L1, min_l2, max_l2, max_abs_weight);
   if (!ch.noff) return false;
   const int fb = result_bytes(static_cast<ResultFormat>(a.fmt));
-  // host streams: 2048-record tiles (P24 letters fit the register prefetch; 3.59 vs 3.69 ms per headline
+  // host streams: 2048-record tiles (packed letters fit the register prefetch; 3.59 vs 3.69 ms per headline
   // step at 1024), device-resident: 512 (more blocks per CU); MOC_SWIPE_TILE overrides (64..2048)
   const int lf = letter_form(a);
   const int tile_cap = 256 * rpt_of(lf);
@@ -448,8 +440,8 @@ bool configure_swipe(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs
   if (const char* v = std::getenv("MOC_SWIPE_TILE")) max_tile = std::max(64, std::min(tile_cap, std::atoi(v)));
   for (int tr = max_tile; tr >= 64; tr /= 2) {
     const int cap = tr * static_cast<int>(std::max<int64_t>(max_l2, 1)) + 64;
-    // a tile's letter bytes must fit the register prefetch (P24: 3 bytes per 5 letters, P33: 33 bits per 7)
-    if ((lf >= 2 ? raw_cap(lf, cap) : cap + 32) > kMaxV * kBlock * 16) continue;
+    // a tile's letter bytes must fit the register prefetch (P33: 33 bits per 7 letters)
+    if ((lf == 2 ? raw_cap(lf, cap) : cap + 32) > kMaxV * kBlock * 16) continue;
     SwipeLayout l = swipe_layout(static_cast<int>(L1), ch.noff, ch.l2w, tr, cap, fb, lf);
     if (l.total <= kLdsBudget) {
       a.tile_records = tr;
@@ -467,7 +459,6 @@ void preload_swipe_kernels() {
   hipFuncAttributes fa;
   (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&swipe_search_kernel<24, 4, 1>));
   (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&swipe_search_kernel<24, 4, 2>));
-  (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&swipe_search_kernel<24, 4, 3>));
 }
 
 // MOC_SWIPE_TAIL=0 keeps every tile at full size (A/B); 2, 4 (default), 8 or 16 cut the tail tiles to that
@@ -511,8 +502,6 @@ void launch_swipe(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStr
 #define MOC_SWIPE_CASE(NO, LW)                                                                          \
   if (noff == NO && l2w == LW) {                                                                      \
     if (a.packed33)                                                                                   \
-      hipLaunchKernelGGL((swipe_search_kernel<NO, LW, 3>), grid, block, lay.total, stream, pv, b, lay); \
-    else if (a.packed24)                                                                              \
       hipLaunchKernelGGL((swipe_search_kernel<NO, LW, 2>), grid, block, lay.total, stream, pv, b, lay); \
     else if (a.packed5)                                                                               \
       hipLaunchKernelGGL((swipe_search_kernel<NO, LW, 1>), grid, block, lay.total, stream, pv, b, lay); \

@@ -91,18 +91,16 @@ HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
     if (v == 1 || v == 2 || v == 4 || v == 8) tile_u_ = v;
   }
   if (const char* t16 = std::getenv("MOC_TILE16")) tile16_ = std::atoi(t16) != 0;
-  if (const char* d = std::getenv("MOC_DMA_STREAM")) opt_.dma_stream = std::atoi(d);
-  if (const char* d = std::getenv("MOC_DMA_CHUNK_BYTES")) opt_.dma_chunk_bytes = std::max<int64_t>(std::atoll(d), 1);
   if (const char* w = std::getenv("MOC_TILE_WAVES_PER_CU")) {
     const int v = std::atoi(w);
     if (v >= 1 && v <= 32) tile_waves_per_cu_ = v;
   }
   // the compute stream only: each stream costs ~10 ms of hardware-queue set-up on the MI355X box
-  // (profiles/hip_init_variants_box.log), and the streaming kernels need no other; the staged and DMA
-  // pipelines make their copy and return streams on first use (ensure_side_streams)
+  // (profiles/hip_init_variants_box.log), and the streaming kernels need no other; the staged pipeline
+  // makes its copy and return streams on first use (ensure_side_streams)
   MOC_HIP_CHECK(hipStreamCreateWithFlags(&s_compute_, hipStreamNonBlocking));
   const double t_streams = init_sw.total_ms();
-  for (int i = 0; i < 3; ++i) {  // run_staged cycles two, run_dma_stream three
+  for (int i = 0; i < 2; ++i) {  // run_staged cycles two
     auto s = std::make_unique<Slot>();
     MOC_HIP_CHECK(hipEventCreateWithFlags(&s->ev_h2d, hipEventDisableTiming));
     MOC_HIP_CHECK(hipEventCreate(&s->ev_k0));
@@ -540,14 +538,8 @@ bool HipEngine::direct_pointers(const WireBatch& b, void* out, int fb, dev::Shor
   const void *dc = nullptr, *doff = nullptr, *dlen = nullptr, *dout = nullptr;
   const int64_t c0 = b.first_letter(), c1 = b.end_letter(), n = b.n;
   // byte range of the letters: [b0, b1)
-  const int64_t b0 = b.packed33   ? p33_first_byte(c0)
-                     : b.packed24 ? kP24Bytes * (c0 / kP24Letters)
-                     : b.packed5  ? (5 * c0) >> 3
-                                  : c0;
-  const int64_t b1 = b.packed33    ? p33_end_byte(c1)
-                     : b.packed24  ? kP24Bytes * ((c1 + kP24Letters - 1) / kP24Letters)
-                     : b.packed5 ? ((5 * c1 + 7) >> 3) + 1
-                                 : c1;
+  const int64_t b0 = b.packed33 ? p33_first_byte(c0) : b.packed5 ? (5 * c0) >> 3 : c0;
+  const int64_t b1 = b.packed33 ? p33_end_byte(c1) : b.packed5 ? ((5 * c1 + 7) >> 3) + 1 : c1;
   if (b.device) {  // device-resident (e.g. received over RCCL): the pointers are the kernel's already
     dc = b.letters + b0;
     doff = b.offsets;
@@ -583,8 +575,8 @@ void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uin
                          ResultFormat fmt, const BatchHints& hints, int packed, int len_bits, int len_base) {
   WireBatch b;
   b.letters = codes;
+  if (packed < 0 || packed > 3 || packed == 2) throw Error("letters: 0 bytes, 1 5-bit packed or 3 P33 fields");
   b.packed5 = packed == 1;
-  b.packed24 = packed == 2;
   b.packed33 = packed == 3;
   b.offsets = offsets;
   b.lengths = lengths;
@@ -598,7 +590,7 @@ void HipEngine::solve_ex(const uint8_t* codes, const int64_t* offsets, const uin
 
 bool HipEngine::streams_packed(int64_t min_l2, int64_t max_l2) const {
   dev::ShortArgs a;
-  a.packed24 = 1;  // the widest LDS layout of the packed forms
+  a.packed33 = 1;  // the widest LDS layout of the letter forms
   return have_problem_ && dev::configure_swipe(L1_, min_l2, max_l2, table_.max_abs(), a);
 }
 
@@ -669,24 +661,15 @@ void HipEngine::solve_wire_impl(const WireBatch& batch, void* out, ResultFormat 
   a.fmt = static_cast<int32_t>(fmt);
   a.counter = d_counter_;
   a.packed5 = b.packed5 ? 1 : 0;
-  a.packed24 = b.packed24 ? 1 : 0;
   a.packed33 = b.packed33 ? 1 : 0;
-  // the SDMA chunker cuts 5-bit / byte streams with 3/4/8-bit lengths (its chunks are not 24-record aligned)
-  const bool dma = opt_.dma_stream && !b.device && !b.packed24 && !b.packed33 && !(b.lengths && b.len_bits == kLenBase6);
-  const bool swipe = dev::configure_swipe(L1_, ls.mn, ls.mx, table_.max_abs(), a, b.device || dma);
+  const bool swipe = dev::configure_swipe(L1_, ls.mn, ls.mx, table_.max_abs(), a, b.device);
   // packed letters stream straight into the swipe kernel only; other kernels read unpacked bytes. Sparse
   // offsets need whole tiles of 2^off_shift records (the swipe tiles are powers of two >= 64).
-  const bool kernel_ok = (swipe || (!b.packed5 && !b.packed24 && !b.packed33 &&
+  const bool kernel_ok = (swipe || (!b.packed5 && !b.packed33 &&
                                     dev::configure_short(L1_, ls.mn, ls.mx, a))) &&
                          (a.tile_records % (1 << b.off_shift)) == 0;
   if ((opt_.allow_direct || b.device) && kernel_ok && direct_pointers(b, out, fb, a)) {
     const dev::ProblemView pv = problem_view(ls.mx);
-    if (dma) {
-      run_dma_stream(pv, a, swipe, b, out, fb);
-      wall.stop();
-      stats_.total_ms = wall.total_ms();
-      return;
-    }
     prepare_direct(pv, a, swipe);  // graph capture / instantiation stays outside the timed span
     MOC_HIP_CHECK(hipEventRecord(ev_a_, s_compute_));
     launch_direct(pv, a, swipe);
@@ -702,16 +685,13 @@ void HipEngine::solve_wire_impl(const WireBatch& batch, void* out, ResultFormat 
     return;
   }
   if (b.device) throw Error("device-resident wire batches stream through the swipe kernel only");
-  uvector<uint8_t> bytes;  // P24 / P33 letters: the staged pipeline takes bytes (or 5-bit packing)
-  if (b.packed24 || b.packed33) {
+  uvector<uint8_t> bytes;  // P33 letters: the staged pipeline takes bytes (or 5-bit packing)
+  if (b.packed33) {
     const int64_t c0 = b.first_letter(), c1 = b.end_letter();
     bytes.resize(static_cast<size_t>(c1) + 16);
-    if (b.packed33)
-      unpack33(b.letters, c0, c1 - c0, bytes.data() + c0);
-    else
-      unpack24(b.letters, c0, c1 - c0, bytes.data() + c0);
+    unpack33(b.letters, c0, c1 - c0, bytes.data() + c0);
     b.letters = bytes.data();
-    b.packed24 = b.packed33 = false;
+    b.packed33 = false;
   }
   if (b.off_shift) {  // the staged pipeline plans from dense offsets: rebuild them from the lengths
     uvector<int64_t> dense(static_cast<size_t>(n) + 1);
@@ -722,102 +702,6 @@ void HipEngine::solve_wire_impl(const WireBatch& batch, void* out, ResultFormat 
   }
   wall.stop();
   stats_.total_ms = wall.total_ms();
-}
-
-// Pinned-host batches through the copy engines: chunks of whole kernel tiles are copied H2D (letters +
-// narrow lengths) on s_copy_, searched from HBM by the same streaming kernel on s_compute_, and their
-// results copied D2H on s_return_, three slots deep, ordered by events only (no host waits inside). The
-// SDMA engines sustain ~57 GB/s in against a concurrent result stream, where the kernel's own zero-copy
-// reads reach 45-51 (profiles/transfer_probe.log "mix3to1_*"). The kernel still reads two offsets per
-// tile from pinned host memory (a.offsets); letters, lengths and results live in the slot buffers, with
-// base pointers shifted so the kernel's absolute indexing lands inside them.
-void HipEngine::run_dma_stream(const dev::ProblemView& pv, const dev::ShortArgs& a0, bool swipe, const WireBatch& b,
-                               void* out, int fb) {
-  ensure_side_streams();
-  const uint8_t* codes = b.letters;
-  const uint8_t* lengths = b.lengths;
-  const int len_bits = b.len_bits;
-  const int64_t n = b.n;
-  const bool packed5 = b.packed5;
-  const int sh = b.off_shift;
-  auto off = [&](int64_t r) { return b.offsets[sparse_index(r, sh)]; };  // r: a chunk boundary or n
-  // chunk starts at whole tiles and at multiples of 8 records: 3-, 4- and 8-bit lengths stay byte aligned
-  const int64_t tile = (std::max<int64_t>(a0.tile_records, 1) + 7) / 8 * 8 == a0.tile_records
-                           ? a0.tile_records
-                           : std::max<int64_t>(a0.tile_records, 1) * 8;
-  const int64_t letters = off(n) - off(0);
-  const int64_t total_bytes = packed5 ? (5 * letters + 7) / 8 : letters;
-  const int64_t per_rec = std::max<int64_t>(1, total_bytes / std::max<int64_t>(n, 1));
-  int64_t chunk = std::max<int64_t>(tile, (opt_.dma_chunk_bytes / per_rec) / tile * tile);
-  const int64_t n_chunks = (n + chunk - 1) / chunk;
-  for (int64_t c = 0; c < n_chunks; ++c) {
-    const int64_t r0 = c * chunk, r1 = std::min(n, r0 + chunk), cn = r1 - r0;
-    Slot& s = *slots_[c % slots_.size()];
-    // letters: bytes [B0, b1 + 16) of the stream, B0 aligned down to 16 (the kernel stages 16-byte words)
-    const int64_t b0 = packed5 ? (5 * off(r0)) >> 3 : off(r0);
-    const int64_t b1 = packed5 ? ((5 * off(r1) + 7) >> 3) + 1 : off(r1);
-    const int64_t B0 = b0 & ~int64_t{15};
-    const size_t lbytes = static_cast<size_t>(b1 - B0);  // + 16 bytes of device slack, never copied: the
-                                                         // host range may end at its allocation's end
-    const size_t nbytes = !lengths        ? 0
-                          : len_bits == 4 ? static_cast<size_t>((cn + 1) / 2)
-                          : len_bits == 3 ? static_cast<size_t>((3 * cn + 7) / 8 + 1)
-                                          : static_cast<size_t>(cn);
-    const size_t rbytes = static_cast<size_t>(fb) * static_cast<size_t>(cn);
-    if (s.busy) {  // the slot's previous chunk: its letters consumed, its results returned
-      MOC_HIP_CHECK(hipEventSynchronize(s.ev_done));
-      s.busy = false;
-    }
-    ensure(s.d_packed, s.d_packed_cap, lbytes + 16);
-    ensure(s.d_offsets, s.d_offsets_cap, std::max<size_t>(nbytes, 16));
-    ensure(s.d_out, s.d_out_cap, std::max<size_t>(rbytes, 16));
-    copy_h2d(s.d_packed, codes + B0, lbytes, s_copy_);
-    if (nbytes) {
-      const size_t nb0 = len_bits == 4   ? static_cast<size_t>(r0 / 2)
-                         : len_bits == 3 ? static_cast<size_t>(3 * r0 / 8)
-                                         : static_cast<size_t>(r0);
-      copy_h2d(s.d_offsets, lengths + nb0, nbytes, s_copy_);
-    }
-    MOC_HIP_CHECK(hipEventRecord(s.ev_h2d, s_copy_));
-    MOC_HIP_CHECK(hipStreamWaitEvent(s_compute_, s.ev_h2d, 0));
-    dev::ShortArgs a = a0;
-    a.codes = static_cast<const uint8_t*>(s.d_packed) - B0;
-    a.dbg_codes_end = B0 + static_cast<int64_t>(lbytes) + 16;
-    a.offsets = a0.offsets + (r0 >> sh);  // pinned host (zero-copy): two reads per tile
-    a.lengths8 = lengths && len_bits == 8 ? static_cast<const uint8_t*>(s.d_offsets) : nullptr;
-    a.lengths4 = lengths && len_bits == 4 ? static_cast<const uint8_t*>(s.d_offsets) : nullptr;
-    a.lengths3 = lengths && len_bits == 3 ? static_cast<const uint8_t*>(s.d_offsets) : nullptr;
-    a.n = cn;
-    a.out = s.d_out;
-    if (c == 0) MOC_HIP_CHECK(hipEventRecord(ev_a_, s_compute_));
-    if (swipe)
-      dev::launch_swipe(pv, a, num_cus_, s_compute_);
-    else
-      dev::launch_short(pv, a, num_cus_, s_compute_);
-    MOC_HIP_CHECK(hipGetLastError());
-    MOC_HIP_CHECK(hipEventRecord(s.ev_k1, s_compute_));
-    MOC_HIP_CHECK(hipStreamWaitEvent(s_return_, s.ev_k1, 0));
-    copy_d2h(static_cast<char*>(out) + r0 * fb, s.d_out, rbytes, s_return_);
-    MOC_HIP_CHECK(hipEventRecord(s.ev_done, s_return_));
-    s.busy = true;
-    stats_.h2d_bytes += static_cast<int64_t>(lbytes + nbytes);
-    stats_.d2h_bytes += static_cast<int64_t>(rbytes);
-  }
-  MOC_HIP_CHECK(hipEventRecord(ev_b_, s_compute_));
-  for (auto& sp : slots_)
-    if (sp->busy) {
-      MOC_HIP_CHECK(hipEventSynchronize(sp->ev_done));
-      sp->busy = false;
-    }
-  // the return copies are done, so every kernel is; the end marker itself must be complete before it is read
-  MOC_HIP_CHECK(hipEventSynchronize(ev_b_));
-  float ms = 0;
-  MOC_HIP_CHECK(hipEventElapsedTime(&ms, ev_a_, ev_b_));
-  stats_.kernel_ms = ms;  // compute-stream span: first kernel start .. last kernel end
-  stats_.kernels = swipe ? 1 : 2;
-  stats_.direct = 1;
-  stats_.dma = 1;
-  stats_.chunks = n_chunks;
 }
 
 // The direct path's launch sequence (work-counter reset + persistent streaming kernel) as a hipGraph:

@@ -388,7 +388,7 @@ struct PieceJob {
   int64_t* sparse;
   uint16_t* len16;
   int64_t G, GB;
-  bool p24, p33;
+  bool p33;
   int64_t l2_cap, L1;
 };
 
@@ -437,11 +437,6 @@ MOC_AVX512 void stage_flush(const PieceJob& j, PieceOut& po, Stager& st, int64_t
   uint8_t* dst = j.packed + GB * (cur / G);
   if (j.p33) {
     for (int64_t g = 0; g < ng; ++g) p33_block_avx512(src + kP33Letters * g, dst + kP33Bytes * g);
-  } else if (j.p24) {
-    for (int64_t g = 0; g < ng; ++g) {
-      const uint32_t v = p24_group(src + 5 * g);
-      std::memcpy(dst + 3 * g, &v, g + 1 < ng ? 4 : 3);
-    }
   } else {
     for (int64_t g = 0; g < ng; ++g) {
       uint64_t x;
@@ -617,11 +612,11 @@ MOC_AVX512 bool fill_piece_avx512(const PieceJob& j, PieceOut& po) {
 
 FillReport BulkParser::fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* packed5, int64_t* offs, int64_t* sparse,
                                   uint16_t* len16, int pack) const {
-  if (pack != 5 && pack != 24 && pack != 33) throw Error("fill_slice: pack must be 5, 24 or 33");
-  // letters per group and bytes per group of the packed stream: 8 -> 5 (5-bit), 5 -> 3 (P24), 56 -> 33 (P33:
-  // a block of eight 33-bit fields)
-  const bool p24 = pack == 24, p33 = pack == 33;
-  const int64_t G = p33 ? kP33Letters : p24 ? kP24Letters : 8, GB = p33 ? kP33Bytes : p24 ? kP24Bytes : 5;
+  if (pack != 5 && pack != 33) throw Error("fill_slice: pack must be 5 or 33");
+  // letters per group and bytes per group of the packed stream: 8 -> 5 (5-bit), 56 -> 33 (P33: a block of
+  // eight 33-bit fields)
+  const bool p33 = pack == 33;
+  const int64_t G = p33 ? kP33Letters : 8, GB = p33 ? kP33Bytes : 5;
   if (offs) offs[0] = 0;
   constexpr int64_t kSparseMask = (int64_t{1} << kSparseShift) - 1;
   const int np = static_cast<int>(s.pieces.size());
@@ -641,7 +636,7 @@ FillReport BulkParser::fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* p
     po.rec_base = s.first_record + pc.tok;
     if (simd) {
       const PieceJob pj{ua,    static_cast<size_t>(pc.byte_begin), static_cast<size_t>(pc.byte_end), a, b, pc.tok,
-                        codes, packed5, offs, sparse, len16, G, GB, p24, p33, l2_cap, L1};
+                        codes, packed5, offs, sparse, len16, G, GB, p33, l2_cap, L1};
       if (fill_piece_avx512(pj, po)) continue;
       po = PieceOut{};  // an input error in this piece: the scalar pass below finds and reports it
       po.rec_base = s.first_record + pc.tok;
@@ -665,11 +660,6 @@ FillReport BulkParser::fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* p
       uint8_t* dst = packed5 + GB * (cur / G);
       if (p33) {
         for (int64_t g = 0; g < ng; ++g) p33_block_full(src + kP33Letters * g, dst + kP33Bytes * g);
-      } else if (p24) {
-        for (int64_t g = 0; g < ng; ++g) {
-          const uint32_t v = p24_group(src + 5 * g);  // < 2^24: the 4-byte store's top byte is 0
-          std::memcpy(dst + 3 * g, &v, g + 1 < ng ? 4 : 3);
-        }
       } else {
         for (int64_t g = 0; g < ng; ++g) {
           uint64_t x;
@@ -776,18 +766,8 @@ FillReport BulkParser::fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* p
     // groups holding letters of two pieces (or the slice's last, partial group): zeroed, then assembled
     for (const PieceOut& po : out)
       for (const auto& sc : po.stragglers) std::memset(packed5 + GB * (sc.first / G), 0, static_cast<size_t>(GB));
-    static constexpr uint32_t kPow26[5] = {1u, 26u, 676u, 17576u, 456976u};
     for (const PieceOut& po : out)
       for (const auto& sc : po.stragglers) {
-        if (p24) {  // add (code - 1) * 26^j to the group value
-          uint8_t* q = packed5 + kP24Bytes * (sc.first / kP24Letters);
-          uint32_t v = q[0] | (static_cast<uint32_t>(q[1]) << 8) | (static_cast<uint32_t>(q[2]) << 16);
-          v += (sc.second > 1 ? sc.second - 1u : 0u) * kPow26[sc.first % kP24Letters];
-          q[0] = static_cast<uint8_t>(v);
-          q[1] = static_cast<uint8_t>(v >> 8);
-          q[2] = static_cast<uint8_t>(v >> 16);
-          continue;
-        }
         const int64_t bit = 5 * sc.first;
         const uint32_t v = static_cast<uint32_t>(sc.second & 31u) << (bit & 7);
         packed5[bit >> 3] |= static_cast<uint8_t>(v);
@@ -796,7 +776,7 @@ FillReport BulkParser::fill_slice(const AreaSlice& s, uint8_t* codes, uint8_t* p
   }
   if (packed5) {  // read slack past the last group
     const int64_t used = GB * ((s.letters + G - 1) / G);
-    const int64_t total = p33 ? packed33_bytes(s.letters) : p24 ? packed24_bytes(s.letters) : packed5_bytes(s.letters);
+    const int64_t total = p33 ? packed33_bytes(s.letters) : packed5_bytes(s.letters);
     std::memset(packed5 + used, 0, static_cast<size_t>(total - used));
   }
   if (sparse) sparse[sparse_count(s.records, kSparseShift) - 1] = s.letters;

@@ -66,32 +66,6 @@ void unpack5(const uint8_t* packed, int64_t begin, int64_t n, uint8_t* out) {
   }
 }
 
-void pack24(const uint8_t* codes, int64_t n, uint8_t* out) {
-  const int64_t groups = (n + kP24Letters - 1) / kP24Letters;
-#pragma omp parallel for schedule(static) if (groups > 65536)
-  for (int64_t g = 0; g < groups; ++g) {
-    const int64_t b = g * kP24Letters;
-    const uint32_t v = p24_group(codes + b, static_cast<int>(std::min<int64_t>(kP24Letters, n - b)));
-    uint8_t* o = out + g * kP24Bytes;
-    o[0] = static_cast<uint8_t>(v);
-    o[1] = static_cast<uint8_t>(v >> 8);
-    o[2] = static_cast<uint8_t>(v >> 16);
-  }
-  const int64_t used = groups * kP24Bytes, total = packed24_bytes(n);
-  for (int64_t i = used; i < total; ++i) out[i] = 0;
-}
-
-void unpack24(const uint8_t* packed, int64_t begin, int64_t n, uint8_t* out) {
-#pragma omp parallel for schedule(static) if (n > (1 << 20))
-  for (int64_t i = 0; i < n; ++i) {
-    const int64_t x = begin + i, g = x / kP24Letters;
-    const uint8_t* p = packed + kP24Bytes * g;
-    uint32_t v = p[0] | (static_cast<uint32_t>(p[1]) << 8) | (static_cast<uint32_t>(p[2]) << 16);
-    for (int64_t j = x - g * kP24Letters; j > 0; --j) v /= 26u;
-    out[i] = static_cast<uint8_t>(v % 26u + 1u);
-  }
-}
-
 void p33_block(const uint8_t* c, uint8_t* out, int m) {
   if (m >= kP33Letters) {
     p33_block_full(c, out);

@@ -41,7 +41,7 @@ HostRegion::HostRegion(size_t bytes, int numa_node) {
   const size_t align = huge ? kHuge : size_t{4096};
   const size_t want = (std::max<size_t>(bytes, 1) + align - 1) & ~(align - 1);
   map_bytes_ = huge ? want + kHuge : want;  // slack to start on a 2 MiB boundary
-  map_ = mmap(nullptr, map_bytes_, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+  map_ = mmap(nullptr, map_bytes_, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
   if (map_ == MAP_FAILED) {
     map_ = nullptr;
     throw Error("HostRegion: cannot map " + std::to_string(map_bytes_) + " bytes");

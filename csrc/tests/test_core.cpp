@@ -293,32 +293,6 @@ void test_engine_vs_brute_force() {
   }
 }
 
-// Host replay of the tile16 kernel's arithmetic (tile16_kernels.hip): per offset, the int8 D terms of
-// its profile byte summed in a wrapping int16 half with an int16 running max, flushed into int32 every
-// 64 steps; Tot_o from an anchor diagonal per 512-offset wave tile plus a suffix sum of the D totals;
-// pass 1 keys (score, ~(2o + mutated)); then the k of the winning offset re-found on its diagonal.
-// Must equal the CPU engine exactly, including ties.
-void test_pack24() {
-  std::mt19937 rng(9);
-  for (int64_t n : {0, 1, 5, 7, 1000, 70001}) {
-    std::vector<uint8_t> codes(static_cast<size_t>(n));
-    for (auto& c : codes) c = static_cast<uint8_t>(1 + rng() % 26);
-    std::vector<uint8_t> p(static_cast<size_t>(packed24_bytes(n)), 0xAB);
-    pack24(codes.data(), n, p.data());
-    bool slack_zero = true;
-    for (size_t i = static_cast<size_t>(3 * ((n + 4) / 5)); i < p.size(); ++i) slack_zero &= p[i] == 0;
-    CHECK(slack_zero);
-    for (int64_t b : {int64_t{0}, int64_t{1}, int64_t{4}, n / 3}) {
-      if (b > n) continue;
-      std::vector<uint8_t> back(static_cast<size_t>(n - b));
-      unpack24(p.data(), b, n - b, back.data());
-      CHECK(std::equal(back.begin(), back.end(), codes.begin() + b));
-    }
-  }
-  const uint8_t five[5] = {26, 26, 26, 26, 26};
-  CHECK(p24_group(five) == 11881375u);  // 26^5 - 1: the largest group value fits 24 bits
-}
-
 void test_pack33() {
   std::mt19937 rng(33);
   for (int64_t n : {0, 1, 6, 7, 8, 55, 56, 57, 112, 1000, 70001}) {
@@ -592,12 +566,6 @@ void test_slices() {
       std::vector<uint8_t> p3(packed5_bytes(s.letters), 0x33);
       const FillReport r3 = p.fill_slice(s, nullptr, p3.data(), nullptr, sp.data(), l16.data());
       CHECK(r3.min_len == r.min_len && r3.max_len == r.max_len && r3.cells == r.cells && p3 == want);
-      // ... and with P24 letter groups (groups straddling the parallel pieces assembled afterwards)
-      std::vector<uint8_t> p24(static_cast<size_t>(packed24_bytes(s.letters)), 0x24),
-          want24(static_cast<size_t>(packed24_bytes(s.letters)));
-      pack24(ref.seq2.codes.data() + ref.seq2.offsets[b], s.letters, want24.data());
-      const FillReport r24 = p.fill_slice(s, nullptr, p24.data(), nullptr, sp.data(), l16.data(), 24);
-      CHECK(r24.min_len == r.min_len && r24.max_len == r.max_len && p24 == want24);
       // ... and with P33 fields (56-letter blocks straddling the pieces assembled afterwards)
       std::vector<uint8_t> p33(static_cast<size_t>(packed33_bytes(s.letters)), 0x33),
           want33(static_cast<size_t>(packed33_bytes(s.letters)));
@@ -899,7 +867,7 @@ int main() {
       {"engine_vs_brute_force", test_engine_vs_brute_force},          {"formatter", test_formatter},
       {"profile16", test_profile16},     {"releaser", test_releaser},   {"slices", test_slices},
       {"narrow_lengths", test_narrow_lengths}, {"result_formats", test_result_formats},
-      {"write_runs", test_write_runs},   {"pack24", test_pack24}, {"pack33", test_pack33},
+      {"write_runs", test_write_runs},   {"pack33", test_pack33},
       {"kfd_topology", test_kfd_topology}, {"cutter_count_ahead", test_cutter_count_ahead}};
   for (const auto& t : tests) {
     const int before = g_failed;

@@ -51,9 +51,6 @@ def _decl(lib):
         "moc_packed5_bytes": (c_int64, [c_int64]),
         "moc_pack5": (c_int, [c_void_p, c_int64, c_void_p]),
         "moc_unpack5": (c_int, [c_void_p, c_int64, c_int64, c_void_p]),
-        "moc_packed24_bytes": (c_int64, [c_int64]),
-        "moc_pack24": (c_int, [c_void_p, c_int64, c_void_p]),
-        "moc_unpack24": (c_int, [c_void_p, c_int64, c_int64, c_void_p]),
         "moc_packed33_bytes": (c_int64, [c_int64]),
         "moc_pack33": (c_int, [c_void_p, c_int64, c_void_p]),
         "moc_unpack33": (c_int, [c_void_p, c_int64, c_int64, c_void_p]),

@@ -114,29 +114,6 @@ def pack_lengths4(lengths: np.ndarray, base: int, out: np.ndarray = None) -> np.
     return out
 
 
-def packed24_bytes(n_chars: int) -> int:
-    """Bytes of a P24 letter stream (5 letters per 3 bytes, incl. 16 bytes of read slack)."""
-    return int(_lib.lib().moc_packed24_bytes(int(n_chars)))
-
-
-def pack24(codes: np.ndarray, out: np.ndarray = None) -> np.ndarray:
-    """Byte letter codes (1..26) -> base-26 groups: letters 5j..5j+4 as the 24-bit little-endian value
-    sum (code - 1) * 26^i in bytes [3j, 3j+3) — 4.8 bits per letter, 4% fewer bytes than 5-bit packing."""
-    codes = np.ascontiguousarray(codes, dtype=np.uint8)
-    nb = packed24_bytes(codes.shape[0])
-    if out is None:
-        out = np.empty(nb, dtype=np.uint8)
-    assert out.dtype == np.uint8 and out.shape[0] >= nb
-    _lib.check(_lib.lib().moc_pack24(_lib.ptr(codes), codes.shape[0], _lib.ptr(out)))
-    return out
-
-
-def unpack24(packed: np.ndarray, begin: int, n: int) -> np.ndarray:
-    out = np.empty(n, dtype=np.uint8)
-    _lib.check(_lib.lib().moc_unpack24(_lib.ptr(np.ascontiguousarray(packed)), int(begin), int(n), _lib.ptr(out)))
-    return out
-
-
 def packed33_bytes(n_chars: int) -> int:
     """Bytes of a P33 letter stream (56 letters per 33 bytes, incl. 16 bytes of read slack)."""
     return int(_lib.lib().moc_packed33_bytes(int(n_chars)))

@@ -191,7 +191,7 @@ class HipSearchEngine:
 
     def solve(self, codes: np.ndarray, offsets: np.ndarray, out: Optional[np.ndarray] = None,
               lengths: Optional[np.ndarray] = None, fmt="r12", l2_range=None, packed5: bool = False,
-              lengths_bits: int = 8, lengths_base: int = 0, packed24: bool = False,
+              lengths_bits: int = 8, lengths_base: int = 0,
               packed33: bool = False) -> np.ndarray:
         """Host CSR -> host results. ``codes[offsets[i]:offsets[i+1]]`` is record i (``offsets`` may be a
         slice of a larger absolute offset array). ``fmt``: r12 | r8 | r4 | r2 | auto (smallest that fits);
@@ -200,8 +200,8 @@ class HipSearchEngine:
         3-bit fields (``lengths_bits`` 3, see pack_lengths3);
         ``l2_range``: optional known (min, max) length (R2 results are encoded for it: decode with
         ``r2_params(*l2_range)`` or ``stats()["r2"]``); ``packed5``: ``codes`` is a 5-bit packed stream
-        (models.problem.pack5) instead of bytes; ``packed24``: base-26 groups of 5 letters in 3 bytes
-        (models.problem.pack24); ``packed33``: 33-bit fields of 7 letters (models.problem.pack33)."""
+        (models.problem.pack5) instead of bytes; ``packed33``: 33-bit fields of 7 letters
+        (models.problem.pack33)."""
         offsets = np.ascontiguousarray(offsets, dtype=np.int64)
         n = offsets.shape[0] - 1
         if l2_range is None and (fmt == "auto"):
@@ -220,7 +220,7 @@ class HipSearchEngine:
         lo, hi = l2_range if l2_range is not None else (-1, -1)
         _lib.check(_lib.lib().moc_engine_solve_ex(self._h, _lib.ptr(codes), _lib.ptr(offsets), _lib.ptr(lengths),
                                                   int(lengths_bits), int(lengths_base), n, _lib.ptr(out), fid, int(lo),
-                                                  int(hi), 3 if packed33 else 2 if packed24 else 1 if packed5 else 0))
+                                                  int(hi), 3 if packed33 else 1 if packed5 else 0))
         return out
 
     def solve_device(self, codes_t, offsets_t, h_offsets: np.ndarray, out_t, stream=None):
@@ -299,7 +299,6 @@ class HipSearchEngine:
                 "kernels"]
         d = dict(zip(keys, list(v)[:10]))
         d["r2"] = tuple(int(x) for x in list(v)[10:13])
-        d["dma"] = int(v[13])
         d["format"] = _lib.FORMAT_NAMES[int(d["format"])]
         d["kernels"] = [k for b, k in ((1, "swipe"), (2, "short"), (4, "tiles"), (8, "tile16")) if int(d["kernels"]) & b]
         return d

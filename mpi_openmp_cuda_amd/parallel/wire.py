@@ -1,7 +1,7 @@
 """One rank's slice of records in the wire formats the GPU streams (csrc/include/moc/wire.hpp).
 
 ``./final`` writes these forms straight from its parser (``BulkParser::fill_slice``): letters as 33-bit
-fields of 7 (P33, 4.714 bits per letter; or base-26 groups of 5 in 3 bytes, P24, or 5-bit packed, or bytes),
+fields of 7 (P33, 4.714 bits per letter; or 5-bit packed, or bytes: the staged / device-resident forms),
 record lengths as base-6 octets or 3/4-bit fields above the slice's shortest length (8-bit, or offsets only, when the range
 is wider), results in the narrowest format the problem's bounds allow (R2: one uint16 per record). The
 streaming kernel reads them zero-copy from page-locked host memory, so every byte saved is PCIe time saved.
@@ -16,11 +16,10 @@ from typing import Callable, Optional
 
 import numpy as np
 
-from ..models.problem import (LEN_BASE6, lengths3_bytes, lengths6_bytes, pack5, pack24, pack33, pack_lengths3,
-                              pack_lengths4, pack_lengths6, packed5_bytes, packed24_bytes, packed33_bytes, unpack5,
-                              unpack24, unpack33)
+from ..models.problem import (LEN_BASE6, lengths3_bytes, lengths6_bytes, pack5, pack33, pack_lengths3, pack_lengths4,
+                              pack_lengths6, packed5_bytes, packed33_bytes, unpack5, unpack33)
 
-LETTER_FORMATS = ("p33", "p24", "p5", "bytes")
+LETTER_FORMATS = ("p33", "p5", "bytes")
 
 # allocator(name, dtype, count) -> array: private numpy memory, /dev/shm memmaps, hipHostMalloc buffers, ...
 Alloc = Callable[[str, np.dtype, int], np.ndarray]
@@ -46,12 +45,11 @@ def length_bits(l2_min: int, l2_max: int, narrow: bool = True) -> int:
 class WireSlice:
     """A CSR slice (record lengths + byte letter codes 1..26) encoded once into the wire formats.
 
-    ``letters``: ``p33`` (default), ``p24``, ``p5`` or ``bytes``; ``base6``: False keeps 3-bit length fields
-    where base-6 octets would fit; ``alloc`` places every array (so a benchmark
+    ``letters``: ``p33`` (default), ``p5`` or ``bytes``; ``alloc`` places every array (so a benchmark
     can put them in node-shared or hipHostMalloc memory)."""
 
     def __init__(self, lengths: np.ndarray, letters: Optional[np.ndarray], letter_format: str = "p33",
-                 narrow: bool = True, alloc: Alloc = private_alloc, base6: bool = True):
+                 narrow: bool = True, alloc: Alloc = private_alloc):
         if letter_format not in LETTER_FORMATS:
             raise ValueError(f"letter_format must be one of {LETTER_FORMATS}")
         lengths = np.asarray(lengths)
@@ -66,8 +64,6 @@ class WireSlice:
         np.cumsum(lengths, out=self.offsets[1:])
         self.total = int(self.offsets[-1])
         self.len_bits = length_bits(self.l2_min, self.l2_max, narrow)
-        if self.len_bits == LEN_BASE6 and not base6:  # 3-bit fields instead (A/B)
-            self.len_bits = 3
         self.len_base = self.l2_min if self.len_bits in (3, 4, LEN_BASE6) else 0
         if self.len_bits == LEN_BASE6:
             self.lengths = alloc("lengths6", np.uint8, lengths6_bytes(n))
@@ -88,10 +84,6 @@ class WireSlice:
             self.codes = alloc("codes33", np.uint8, packed33_bytes(self.total))
             if letters is not None:
                 pack33(letters, out=self.codes)
-        elif letter_format == "p24":
-            self.codes = alloc("codes24", np.uint8, packed24_bytes(self.total))
-            if letters is not None:
-                pack24(letters, out=self.codes)
         elif letter_format == "p5":
             self.codes = alloc("codes5", np.uint8, packed5_bytes(self.total))
             if letters is not None:
@@ -137,7 +129,7 @@ class WireSlice:
         from .. import _lib
 
         fid = _lib.FORMAT_NAMES.index(self.fmt)
-        letters = {"p5": 1, "p24": 2, "p33": 3}.get(self.letter_format, 0)
+        letters = {"p5": 1, "p33": 3}.get(self.letter_format, 0)
         args = (_lib.ptr(self.codes), _lib.ptr(self.offsets), _lib.ptr(self.lengths), int(self.len_bits or 8),
                 int(self.len_base), self.n, _lib.ptr(self.results), fid, int(self.l2_min), int(self.l2_max), letters)
         self._prepared = (engine, self.results, args)
@@ -148,7 +140,7 @@ class WireSlice:
         """The first solve through the engine's checked entry point (asserts shapes and formats)."""
         return engine.solve(self.codes, self.offsets, out=self.results, lengths=self.lengths, fmt=self.fmt,
                             l2_range=(self.l2_min, self.l2_max), packed5=self.letter_format == "p5",
-                            packed24=self.letter_format == "p24", packed33=self.letter_format == "p33",
+                            packed33=self.letter_format == "p33",
                             lengths_bits=self.len_bits or 8, lengths_base=self.len_base)
 
     def triples(self, engine, count: Optional[int] = None) -> np.ndarray:
@@ -164,8 +156,6 @@ class WireSlice:
         end = self.total if end is None else end
         if self.letter_format == "p33":
             return unpack33(self.codes, begin, end - begin)
-        if self.letter_format == "p24":
-            return unpack24(self.codes, begin, end - begin)
         if self.letter_format == "p5":
             return unpack5(self.codes, begin, end - begin)
         return np.asarray(self.codes[begin:end])

@@ -179,20 +179,19 @@ def test_packed5_letters(shape, n, pinned):
 
 @pytest.mark.parametrize("shape,n", [("input6", 250_003), ("input1", 3000), ("input4", 200), ("input3", 20)])
 @pytest.mark.parametrize("pinned", [False, True])
-@pytest.mark.parametrize("code", ["p24", "p33"])
-def test_group_coded_letters(shape, n, pinned, code):
-    # P24 letters (base-26 groups, 5 per 3 bytes) and P33 letters (7 per 33-bit field): decoded per tile in
-    # LDS by the swipe kernel (pinned, tiny problems), or unpacked on the host for the staged pipeline
-    from mpi_openmp_cuda_amd.models.problem import pack24, pack33
+def test_group_coded_letters(shape, n, pinned):
+    # P33 letters (7 per 33-bit field): decoded per tile in LDS by the swipe kernel (pinned, tiny
+    # problems), or unpacked on the host for the staged pipeline
+    from mpi_openmp_cuda_amd.models.problem import pack33
 
     prob = make_synthetic(shape, n, seed=n + 1)
-    packed = pack33(prob.codes) if code == "p33" else pack24(prob.codes)
+    packed = pack33(prob.codes)
     eng = HipSearchEngine(device=0, chunk_records=max(n // 3, 1))
     eng.set_problem(prob.weights, prob.seq1)
     out = np.zeros(prob.n, dtype=np.dtype([("score", "<i4"), ("n", "<i4"), ("k", "<i4")]))
     if pinned:
         eng.pin(packed, prob.offsets, out)
-    eng.solve(packed, prob.offsets, out=out, packed24=code == "p24", packed33=code == "p33")
+    eng.solve(packed, prob.offsets, out=out, packed33=True)
     st = eng.stats()
     assert np.array_equal(as_triples(out), as_triples(search_cpu(prob))), st
     if pinned and shape == "input6":
@@ -203,7 +202,7 @@ def test_group_coded_letters(shape, n, pinned, code):
 @pytest.mark.parametrize("L1,lo,hi,w", [(26, 6, 11, (4, 3, 2, 10)), (12, 1, 14, (3, 1, 1, 2)),
                                         (40, 20, 32, (5, 2, 3, 4)), (60, 10, 16, (2, 2, 1, 3)),
                                         (9, 9, 9, (7, 1, 2, 3))])
-@pytest.mark.parametrize("letters", ["p33", "p24", "p5"])
+@pytest.mark.parametrize("letters", ["p33", "p5"])
 def test_swipe_wire_slices(L1, lo, hi, w, letters):
     # the headline's wire path (parallel/wire.py: narrow lengths, R2/R4 results, zero-copy) across swipe
     # instantiations (NOFF 8..64, record widths <= 16 / <= 32) for every packed letter format
@@ -462,17 +461,6 @@ def test_final_cli_zero_copy_window(tmp_path, np_):
         assert d["rank_h2d_bytes"][q] <= lb + 3 * n // 8 + 64, d
 
 
-def test_final_cli_letters_p24(tmp_path):
-    # --letters=p24 keeps the 5-per-3-bytes groups on the GPU slices (A/B against the default P33)
-    prob = make_synthetic("input6", 50_001, seed=12)
-    path = tmp_path / "in6.txt"
-    path.write_text(prob.to_text())
-    for letters in ("p24", "p33"):
-        r = run_final(["--backend=hip", f"--letters={letters}", f"--input={path}", "--device=0"], stdin_bytes=b"")
-        assert r.returncode == 0, r.stderr.decode()
-        assert r.stdout.decode() == format_results(search_cpu(prob)), letters
-
-
 @pytest.mark.parametrize("source", ["input", "stdin"])
 @pytest.mark.parametrize("np_", [1, 2])
 def test_final_cli_streaming_slices(tmp_path, np_, source):
@@ -514,9 +502,32 @@ def test_final_cli_streaming_slices(tmp_path, np_, source):
     assert sum(d["rank_pinned_bytes"]) <= np_ * 2 * per_slot, d
 
 
+def test_final_cli_stdin_batches_larger_than_read_buffer():
+    # One rank streaming a pipe: each batch (~14 MB of text) is larger than the stream buffer's first load
+    # (>= 4 MiB), so the root's count-ahead while the GPU runtime starts has to load more text while batch 0
+    # is cut but not yet encoded. The batch's text must survive that load (it was dropped before
+    # the encode, and a load could move or free it under the encoder).
+    import json
+    import os
+    import subprocess
+
+    from conftest import ROOT
+
+    prob = make_synthetic("input6", 4_000_000, seed=31)
+    text = prob.to_text().encode()
+    assert len(text) > 3 * 8 * 2**20
+    args = ["--backend=hip", "--transport=shm", "--timing", "--device=0", "--batch-records=1500000"]
+    r = subprocess.run([os.path.join(ROOT, "final")] + args, input=text, capture_output=True, timeout=120,
+                       env=dict(os.environ, OMP_NUM_THREADS="8"))
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    assert r.stdout.decode() == format_results(search_cpu(prob))
+    d = json.loads([l for l in r.stderr.decode().splitlines() if l.startswith("{")][-1])
+    assert d["batches"] == 3 and d["records"] == prob.n, d
+
+
 @pytest.mark.parametrize("pinned", [False, True])
 @pytest.mark.parametrize("packed", [False, True])
-@pytest.mark.parametrize("shape,n", [("input6", 200_003), ("input1", 3001)])
+@pytest.mark.parametrize("shape,n", [("input6", 200_003)])  # input1's bounds do not fit R2 (auto_format: R4)
 def test_r2_results_and_nibble_lengths(pinned, packed, shape, n):
     # 2-byte results + 4-bit lengths: the narrowest wire formats of the streaming path
     from mpi_openmp_cuda_amd import _lib
@@ -527,11 +538,7 @@ def test_r2_results_and_nibble_lengths(pinned, packed, shape, n):
     prob = make_synthetic(shape, n, seed=n)
     eng = HipSearchEngine(device=0)
     eng.set_problem(prob.weights, prob.seq1)
-    fmt = eng.auto_format(sh.l2_max, sh.l2_min)
-    if shape == "input6":
-        assert fmt == "r2"
-    if fmt != "r2":
-        pytest.skip(f"{shape}: R2 does not fit ({fmt})")
+    assert eng.auto_format(sh.l2_max, sh.l2_min) == "r2"
     codes = pack5(prob.codes) if packed else prob.codes
     lengths = pack_lengths4(np.diff(prob.offsets), sh.l2_min)
     out = np.zeros(prob.n, dtype=_lib.R2_DTYPE)
@@ -587,23 +594,21 @@ def test_pinned_neighbours_staged_copies():
     eng.close()
 
 
-@pytest.mark.parametrize("mode", ["dma", "zero_copy"])
-@pytest.mark.parametrize("packed,len_bits", [(False, 0), (False, 8), (True, 4), (True, 8), (True, 3), (False, 3),
-                                             (True, 6), (False, 6)])
-@pytest.mark.parametrize("shape,n", [("input6", 100_003), ("input1", 20_001)])
-def test_host_stream_modes(monkeypatch, mode, packed, len_bits, shape, n):
-    # pinned host batches: chunked SDMA in/out around the HBM-resident kernel (64 KiB chunks: many of
-    # them, odd tail) or the kernel's own zero-copy reads/writes — same answers
+# every (letters, lengths) combination a pinned batch can stream in: packed letters go to the swipe kernel only
+# (input6), 3-bit lengths need a span of at most 8 values and base-6 at most 6 (input6: 6..11)
+@pytest.mark.parametrize("shape,n,packed,len_bits", [
+    ("input6", 100_003, False, 0), ("input6", 100_003, False, 8), ("input6", 100_003, True, 4),
+    ("input6", 100_003, True, 8), ("input6", 100_003, True, 3), ("input6", 100_003, False, 3),
+    ("input6", 100_003, True, 6), ("input6", 100_003, False, 6),
+    ("input1", 20_001, False, 0), ("input1", 20_001, False, 8)])
+def test_host_stream_lengths(packed, len_bits, shape, n):
+    # pinned host batches streamed zero-copy by the kernel with every narrow length form — same answers
     from mpi_openmp_cuda_amd import _lib
     from mpi_openmp_cuda_amd.models.problem import pack5, pack_lengths3, pack_lengths4, pack_lengths6
     from mpi_openmp_cuda_amd.utils.synthetic import SHAPES
 
-    monkeypatch.setenv("MOC_DMA_STREAM", "1" if mode == "dma" else "0")
-    monkeypatch.setenv("MOC_DMA_CHUNK_BYTES", str(64 << 10))
     sh = SHAPES[shape]
     prob = make_synthetic(shape, n, seed=n + len_bits)
-    if packed and shape != "input6":
-        pytest.skip("packed letters stream into the swipe kernel only")
     eng = HipSearchEngine(device=0)
     eng.set_problem(prob.weights, prob.seq1)
     codes = pack5(prob.codes) if packed else prob.codes
@@ -616,24 +621,18 @@ def test_host_stream_modes(monkeypatch, mode, packed, len_bits, shape, n):
         lengths = pack_lengths4(np.diff(prob.offsets), sh.l2_min)
         kw = dict(lengths=lengths, lengths_bits=4, lengths_base=sh.l2_min)
     elif len_bits == 3:
-        if sh.l2_max - sh.l2_min > 7:
-            pytest.skip("lengths span more than 3 bits")
+        assert sh.l2_max - sh.l2_min <= 7
         lengths = pack_lengths3(np.diff(prob.offsets), sh.l2_min)
         kw = dict(lengths=lengths, lengths_bits=3, lengths_base=sh.l2_min)
     elif len_bits == 6:
-        if sh.l2_max - sh.l2_min > 5:
-            pytest.skip("lengths span more than 6 values")
+        assert sh.l2_max - sh.l2_min <= 5
         lengths = pack_lengths6(np.diff(prob.offsets), sh.l2_min)
         kw = dict(lengths=lengths, lengths_bits=6, lengths_base=sh.l2_min)
     out = np.zeros(prob.n, dtype=_lib.FORMAT_DTYPES[_lib.FORMAT_NAMES.index("r8")])
     eng.pin(codes, prob.offsets, out, *([lengths] if lengths is not None else []))
     eng.solve(codes, prob.offsets, out=out, fmt="r8", packed5=packed, **kw)
     st = eng.stats()
-    # base-6 lengths stay on the zero-copy path (the SDMA chunks are not 24-record aligned)
-    dma = mode == "dma" and len_bits != 6
-    assert st["direct"] == 1 and st["dma"] == (1 if dma else 0), st
-    if dma:
-        assert st["chunks"] > 3, st
+    assert st["direct"] == 1, st
     assert np.array_equal(as_triples(out), as_triples(search_cpu(prob))), st
     eng.close()
 

@@ -17,7 +17,7 @@ def test_length_fields_round_trip(lo, hi, narrow, bits):
     lengths = rng.integers(lo, hi + 1, size=n)
     letters = rng.integers(1, 27, size=int(lengths.sum()), dtype=np.uint8)
     assert length_bits(int(lengths.min()), int(lengths.max()), narrow) == bits
-    for fmt in ("p33", "p24", "p5", "bytes"):
+    for fmt in ("p33", "p5", "bytes"):
         ws = WireSlice(lengths, letters, letter_format=fmt, narrow=narrow)
         assert ws.len_bits == bits
         assert np.array_equal(ws.decoded_lengths(), lengths)
@@ -51,37 +51,9 @@ def test_custom_allocator_places_every_array():
     assert len(ws.arrays()) == 3  # results come later (their format is the engine's choice)
 
 
-def test_p24_groups():
-    from mpi_openmp_cuda_amd.models.problem import pack24, packed24_bytes, unpack24
-
-    rng = np.random.default_rng(5)
-    for n in (0, 1, 4, 5, 6, 1000, 1 << 16):
-        codes = rng.integers(1, 27, size=n, dtype=np.uint8)
-        p = pack24(codes)
-        assert p.shape[0] == packed24_bytes(n) == 3 * ((n + 4) // 5) + 16
-        assert not p[3 * ((n + 4) // 5):].any()  # slack zeroed
-        for b in (0, 1, 3, n // 2):
-            if b <= n:
-                assert np.array_equal(unpack24(p, b, n - b), codes[b:])
-    # group value: sum (code - 1) * 26^i, little endian
-    p = pack24(np.array([2, 1, 1, 1, 26], np.uint8))
-    v = int(p[0]) | int(p[1]) << 8 | int(p[2]) << 16
-    assert v == 1 + 25 * 26 ** 4
-
-
 def test_p33_fields():
-    from mpi_openmp_cuda_amd.models.problem import pack33, packed33_bytes, unpack33
+    from mpi_openmp_cuda_amd.models.problem import pack33, packed33_bytes
 
-    rng = np.random.default_rng(33)
-    for n in (0, 1, 6, 7, 8, 55, 56, 57, 1000, 1 << 16):
-        codes = rng.integers(1, 27, size=n, dtype=np.uint8)
-        p = pack33(codes)
-        assert p.shape[0] == packed33_bytes(n) == 33 * ((n + 55) // 56) + 16
-        assert not p[33 * ((n + 55) // 56):].any()  # slack zeroed
-        for b in (0, 1, 6, 7, 57, n // 2):
-            if b <= n:
-                assert np.array_equal(unpack33(p, b, n - b), codes[b:])
-    # field f: sum (code - 1) * 26^i at bits [33f, 33f + 33) of a little-endian stream
     codes = np.array([2, 1, 1, 1, 1, 1, 26] + [26] * 7 + [3], np.uint8)
     p = pack33(codes)
     stream = int.from_bytes(bytes(p[:33]), "little")
@@ -89,9 +61,9 @@ def test_p33_fields():
     assert stream & mask == 1 + 25 * 26 ** 6
     assert (stream >> 33) & mask == 26 ** 7 - 1
     assert (stream >> 66) & mask == 2
-    # 4.714 bits per letter: 1.8% fewer bytes than P24 on a large stream
+    # 4.714 bits per letter: 33 bytes per 56 letters (5-bit packing: 35)
     n = 56 * 1000
-    assert packed33_bytes(n) - 16 == 33000 and (3 * n // 5) == 33600
+    assert packed33_bytes(n) - 16 == 33000 and (5 * n // 8) == 35000
 
 
 def test_base6_lengths_match_native_packer():
@@ -131,7 +103,7 @@ def test_prepared_solve_passes_the_checked_arguments(monkeypatch):
     eng = HipSearchEngine.__new__(HipSearchEngine)
     eng._h, eng._problem_key, eng._stats_buf = ctypes.c_void_p(1), None, (ctypes.c_double * 14)()
     prob = make_synthetic("input6", 5000, seed=2)
-    for fmt in ("p33", "p24", "p5", "bytes"):
+    for fmt in ("p33", "p5", "bytes"):
         ws = WireSlice.from_csr(prob.codes, prob.offsets, letter_format=fmt)
         ws.fmt, ws.results = "r2", np.zeros(ws.n, np.uint16)
         ws.solve(eng)

@@ -1,6 +1,6 @@
 // Parser throughput on an input6-shaped text (CPU only): pass 1 (count_tokens over thread chunks) against
 // pass 2 (BulkParser::fill_slice into the GPU wire form: packed letters + sparse offsets + uint16 lengths)
-// for 5-bit / P24 / P33 letters, and the byte form the CPU engine takes. MOC_FILL_SIMD=0 forces the
+// for 5-bit / P33 letters, and the byte form the CPU engine takes. MOC_FILL_SIMD=0 forces the
 // portable SSE2 encoder (A/B against the AVX-512 one).
 // Build: make build/fill_bench   (or see the Makefile rule)   Run: build/fill_bench [records]
 #include <omp.h>
@@ -45,7 +45,7 @@ int main(int argc, char** argv) {
   std::vector<uint8_t> codes(static_cast<size_t>(s.letters) + 64);
   std::vector<int64_t> offs(static_cast<size_t>(s.records) + 1);
   for (int rep = 0; rep < 3; ++rep) {
-    for (int pack : {5, 24, 33}) {
+    for (int pack : {5, 33}) {
       const auto t0 = now();
       p.fill_slice(s, nullptr, out.data(), nullptr, sp.data(), l16.data(), pack);
       const double ms = ms_since(t0);
