@@ -82,10 +82,12 @@ def launch_command(args, argv, port=None):
 KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
 
 
-def kfd_gpu_count(root=KFD_NODES, env=None):
+def kfd_gpu_count(root=KFD_NODES, env=None, dri="/dev/dri"):
     """GPUs from the KFD topology in sysfs — no HIP runtime, no torch in the launcher: topology nodes whose
-    properties report SIMDs (CPU nodes report simd_count 0). ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES /
-    CUDA_VISIBLE_DEVICES narrow the count as the runtime would. None when there is no KFD topology."""
+    properties report SIMDs (CPU nodes report simd_count 0) and whose render node /dev/dri/renderD<minor>
+    this process may open (a shared host exposes a job only its own GPUs; the runtime filters the same way,
+    csrc/src/runtime/kfd_topology.cpp). ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES
+    narrow the count as the runtime would. None when there is no KFD topology."""
     env = os.environ if env is None else env
     try:
         nodes = os.listdir(root)
@@ -98,8 +100,12 @@ def kfd_gpu_count(root=KFD_NODES, env=None):
                 props = dict(line.split(None, 1) for line in f if len(line.split(None, 1)) == 2)
         except (OSError, ValueError):
             continue
-        if int(props.get("simd_count", "0").strip() or 0) > 0:
-            n += 1
+        if int(props.get("simd_count", "0").strip() or 0) <= 0:
+            continue
+        minor = props.get("drm_render_minor", "").strip()
+        if minor and not os.access(os.path.join(dri, f"renderD{minor}"), os.R_OK | os.W_OK):
+            continue  # another tenant's GPU
+        n += 1
     for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
         v = env.get(var)
         if v is not None:

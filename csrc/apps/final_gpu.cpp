@@ -221,9 +221,8 @@ class GpuRankImpl final : public GpuRank {
     if (opt.chunk_bytes > 0) eo.chunk_bytes = opt.chunk_bytes;
     std::string bus;  // the PCIe address of the device chosen from the topology
     if (const auto kfd = kfd_gpus(); kfd && !kfd->empty()) {
-      const int n = static_cast<int>(kfd->size());
-      const int id = requested >= 0 ? requested : ctx.local_rank % n;
-      if (id < n && !(*kfd)[static_cast<size_t>(id)].pci_bus_id.empty()) {  // found again by that address
+      const int id = kfd_pick(*kfd, ctx.local_rank, requested);
+      if (id >= 0) {  // found again in the runtime by its PCIe address
         device_ = id;
         bus = (*kfd)[static_cast<size_t>(id)].pci_bus_id;
         // host buffers this rank's GPU streams over PCIe, and the threads that fill them, on the NUMA node

@@ -35,6 +35,11 @@ struct KfdPaths {
 
 std::optional<std::vector<KfdGpu>> kfd_gpus(const KfdPaths& paths = KfdPaths());
 
+// The device a rank takes from that list: `requested` (--device, or the --device-map entry) when >= 0, else
+// node-local rank % device count — the runtime's select_device rule. -1 when the list cannot answer (no
+// GPUs, an index out of range, a GPU without a PCIe address to find it again in the runtime by).
+int kfd_pick(const std::vector<KfdGpu>& gpus, int local_rank, int requested);
+
 // Binds the calling thread's CPUs (sched_setaffinity) and its future page allocations (set_mempolicy
 // MPOL_PREFERRED) to NUMA node `node`. Returns the node, or -1 if nothing was changed.
 int bind_numa_node(int node);

@@ -127,6 +127,14 @@ std::optional<std::vector<KfdGpu>> kfd_gpus(const KfdPaths& paths) {
   return apply_visible_env(std::move(gpus));
 }
 
+int kfd_pick(const std::vector<KfdGpu>& gpus, int local_rank, int requested) {
+  const int n = static_cast<int>(gpus.size());
+  if (n == 0) return -1;
+  const int id = requested >= 0 ? requested : local_rank % n;
+  if (id >= n || gpus[static_cast<size_t>(id)].pci_bus_id.empty()) return -1;
+  return id;
+}
+
 int bind_numa_node(int node) {
   if (node < 0) return -1;
   std::ifstream f("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist");

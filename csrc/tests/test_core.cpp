@@ -814,6 +814,96 @@ void test_kfd_topology() {
   CHECK(std::system(("rm -rf " + root).c_str()) == 0);
 }
 
+// An 8-GPU, two-socket node as the driver describes it (two CPU nodes, then eight GPU nodes; GPUs 0-3 on
+// NUMA node 0, 4-7 on node 1): every node-local rank of an 8- or 16-rank job gets device rank % 8 and that
+// device's NUMA node, also under ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES permutations, with --device,
+// and on a box that exposes one of the eight render nodes (the gpurun box: HIP_/ROCR_VISIBLE_DEVICES=0).
+void test_kfd_topology_8gpu() {
+  char tmpl[] = "/tmp/moc_kfd8_XXXXXX";
+  const char* root_c = mkdtemp(tmpl);
+  CHECK(root_c != nullptr);
+  if (!root_c) return;
+  const std::string root = root_c;
+  auto put = [](const std::string& path, const std::string& text) {
+    FILE* f = std::fopen(path.c_str(), "w");
+    if (!f) return;
+    std::fputs(text.c_str(), f);
+    std::fclose(f);
+  };
+  for (const char* d : {"/nodes", "/dri", "/pci"}) mkdir((root + d).c_str(), 0755);
+  const int bus[8] = {0x05, 0x15, 0x5d, 0x75, 0x85, 0x95, 0xe5, 0xf1};
+  auto bus_id = [&](int g) {
+    char b[16];
+    std::snprintf(b, sizeof b, "0000:%02x:00.0", bus[g]);
+    return std::string(b);
+  };
+  for (int cpu = 0; cpu < 2; ++cpu) {
+    mkdir((root + "/nodes/" + std::to_string(cpu)).c_str(), 0755);
+    put(root + "/nodes/" + std::to_string(cpu) + "/properties", "cpu_cores_count 64\nsimd_count 0\n");
+  }
+  for (int g = 0; g < 8; ++g) {
+    const std::string d = root + "/nodes/" + std::to_string(2 + g);
+    mkdir(d.c_str(), 0755);
+    put(d + "/properties", "simd_count 1024\ndrm_render_minor " + std::to_string(128 + g) + "\nlocation_id " +
+                               std::to_string(bus[g] << 8) + "\ndomain 0\n");
+    put(root + "/dri/renderD" + std::to_string(128 + g), "");
+    mkdir((root + "/pci/" + bus_id(g)).c_str(), 0755);
+    put(root + "/pci/" + bus_id(g) + "/numa_node", g < 4 ? "0\n" : "1\n");
+  }
+  put(root + "/kfd", "");
+  KfdPaths p;
+  p.nodes = root + "/nodes";
+  p.kfd = root + "/kfd";
+  p.dri = root + "/dri";
+  p.pci = root + "/pci";
+  for (const char* v : {"ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL"})
+    unsetenv(v);
+  auto g = kfd_gpus(p);
+  CHECK(g && g->size() == 8);
+  if (!g || g->size() != 8) return;
+  // rank -> device -> NUMA node, 8 and 16 ranks per node
+  for (int r = 0; r < 16; ++r) {
+    const int id = kfd_pick(*g, r, -1);
+    CHECK(id == r % 8);
+    CHECK((*g)[static_cast<size_t>(id)].pci_bus_id == bus_id(r % 8));
+    CHECK((*g)[static_cast<size_t>(id)].numa_node == (r % 8 < 4 ? 0 : 1));
+  }
+  CHECK(kfd_pick(*g, 3, 6) == 6 && kfd_pick(*g, 0, 8) == -1);
+  // the sockets swapped: device 0 is the first GPU of NUMA node 1
+  setenv("ROCR_VISIBLE_DEVICES", "4,5,6,7,0,1,2,3", 1);
+  g = kfd_gpus(p);
+  CHECK(g && g->size() == 8);
+  if (g && g->size() == 8)
+    for (int r = 0; r < 8; ++r) {
+      const KfdGpu& x = (*g)[static_cast<size_t>(kfd_pick(*g, r, -1))];
+      CHECK(x.pci_bus_id == bus_id((r + 4) % 8) && x.numa_node == (r < 4 ? 1 : 0));
+    }
+  // reversed, then every second one on top: [7, 5, 3, 1]
+  setenv("ROCR_VISIBLE_DEVICES", "7,6,5,4,3,2,1,0", 1);
+  setenv("HIP_VISIBLE_DEVICES", "0,2,4,6", 1);
+  g = kfd_gpus(p);
+  CHECK(g && g->size() == 4);
+  if (g && g->size() == 4)
+    for (int r = 0; r < 8; ++r) {
+      const KfdGpu& x = (*g)[static_cast<size_t>(kfd_pick(*g, r, -1))];
+      const int phys = 7 - 2 * (r % 4);
+      CHECK(x.pci_bus_id == bus_id(phys) && x.numa_node == (phys < 4 ? 0 : 1));
+    }
+  unsetenv("HIP_VISIBLE_DEVICES");
+  unsetenv("ROCR_VISIBLE_DEVICES");
+  // a box that may open one of the host's eight GPUs (render node access), indexed 0 by both lists
+  for (int x = 0; x < 8; ++x)
+    if (x != 5) std::remove((root + "/dri/renderD" + std::to_string(128 + x)).c_str());
+  setenv("ROCR_VISIBLE_DEVICES", "0", 1);
+  setenv("HIP_VISIBLE_DEVICES", "0", 1);
+  g = kfd_gpus(p);
+  CHECK(g && g->size() == 1 && (*g)[0].pci_bus_id == bus_id(5) && (*g)[0].numa_node == 1);
+  if (g && g->size() == 1) CHECK(kfd_pick(*g, 0, -1) == 0 && kfd_pick(*g, 3, -1) == 0);
+  unsetenv("HIP_VISIBLE_DEVICES");
+  unsetenv("ROCR_VISIBLE_DEVICES");
+  CHECK(std::system(("rm -rf " + root).c_str()) == 0);
+}
+
 // The streaming root's cutter: batches cut after counting ahead (while a GPU's runtime starts) are the
 // batches cut without it, by record count and by letter count; count_ahead stops at its batch bound
 void test_cutter_count_ahead() {
@@ -868,7 +958,8 @@ int main() {
       {"profile16", test_profile16},     {"releaser", test_releaser},   {"slices", test_slices},
       {"narrow_lengths", test_narrow_lengths}, {"result_formats", test_result_formats},
       {"write_runs", test_write_runs},   {"pack33", test_pack33},
-      {"kfd_topology", test_kfd_topology}, {"cutter_count_ahead", test_cutter_count_ahead}};
+      {"kfd_topology", test_kfd_topology}, {"kfd_topology_8gpu", test_kfd_topology_8gpu},
+      {"cutter_count_ahead", test_cutter_count_ahead}};
   for (const auto& t : tests) {
     const int before = g_failed;
     t.second();

@@ -4,6 +4,7 @@ import json
 import os
 import subprocess
 import sys
+import types
 
 import pytest
 
@@ -76,6 +77,37 @@ def test_kfd_gpu_count_from_sysfs(tmp_path):
     assert b.kfd_gpu_count(str(tmp_path / "absent"), env={}) is None
     # this container: no GPU nodes (or no KFD at all) -> the 2-GPU launch refusal above comes from sysfs
     assert b.kfd_gpu_count(env={}) in (None, 0)
+
+
+def test_kfd_gpu_count_8gpu_node(tmp_path):
+    # the 8-GPU, two-socket node of a SCALE run (csrc/tests/test_core.cpp test_kfd_topology_8gpu: the same
+    # tree): 8 GPUs, narrowed by the visibility lists; a box exposing one render node counts 1
+    b = _bench_module()
+    nodes, dri = tmp_path / "nodes", tmp_path / "dri"
+    dri.mkdir()
+    for cpu in range(2):
+        (nodes / str(cpu)).mkdir(parents=True)
+        (nodes / str(cpu) / "properties").write_text("cpu_cores_count 64\nsimd_count 0\n")
+    for g in range(8):
+        (nodes / str(2 + g)).mkdir()
+        (nodes / str(2 + g) / "properties").write_text(f"simd_count 1024\ndrm_render_minor {128 + g}\n")
+        (dri / f"renderD{128 + g}").write_text("")
+    assert b.kfd_gpu_count(str(nodes), env={}, dri=str(dri)) == 8
+    assert b.kfd_gpu_count(str(nodes), env={"ROCR_VISIBLE_DEVICES": "4,5,6,7,0,1,2,3"}, dri=str(dri)) == 8
+    assert b.kfd_gpu_count(str(nodes), env={"HIP_VISIBLE_DEVICES": "0,2,4,6"}, dri=str(dri)) == 4
+    for g in range(8):
+        if g != 5:
+            (dri / f"renderD{128 + g}").unlink()
+    assert b.kfd_gpu_count(str(nodes), env={"HIP_VISIBLE_DEVICES": "0", "ROCR_VISIBLE_DEVICES": "0"},
+                           dri=str(dri)) == 1
+    # one visible GPU: the 8-rank launch is refused unless it is a shared-GPU rehearsal
+    args = types.SimpleNamespace(gpus=8, dry_launch=False, allow_shared_gpu=False)
+    orig = b.visible_gpus
+    b.visible_gpus = lambda: 1
+    try:
+        assert b.self_launch(args, ["--gpus", "8"]) == 2
+    finally:
+        b.visible_gpus = orig
 
 
 def test_stale_shm_cleanup(tmp_path):

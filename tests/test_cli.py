@@ -2,6 +2,7 @@
 bounded by a timeout), input edge cases through ./final."""
 import json
 import subprocess
+import numpy as np
 
 import pytest
 
@@ -483,6 +484,46 @@ def test_rccl_driver_emulated_many_pieces(np_, tmp_path):
                       env={"MOC_SEND_CHUNK": "5000"}, timeout=300)
         assert r.returncode == 0, r.stderr.decode()
         assert r.stdout.decode() == format_results(search_cpu(prob)), shape
+
+
+def test_rccl_driver_pieces_smaller_than_a_record(tmp_path):
+    # 8 ranks, records of 9-20 K letters (5-bit dense form: 5.6-12.5 KB each) cut into 2640-byte pieces: a
+    # record spans several pieces, which arrive interleaved with the other ranks' — bulk and streamed
+    from mpi_openmp_cuda_amd import Problem, format_results, search_cpu
+
+    rng = np.random.default_rng(41)
+    s1 = "".join(chr(65 + x) for x in rng.integers(0, 26, 21_000))
+    recs = ["".join(chr(65 + x) for x in rng.integers(0, 26, int(n))) for n in rng.integers(9_000, 20_001, 12)]
+    prob = Problem.from_strings([3, 1, 2, 1], s1, recs)
+    path = tmp_path / "long.txt"
+    path.write_text(prob.to_text())
+    want = format_results(search_cpu(prob))
+    for extra in ([], ["--batch-records=5"]):
+        r = run_final(["--backend=cpu", "--transport=rccl-emul", f"--input={path}"] + extra, stdin_bytes=b"", np_=8,
+                      env={"MOC_SEND_CHUNK": "2640"}, timeout=300)
+        assert r.returncode == 0, (extra, r.stderr.decode())
+        assert r.stdout.decode() == want, extra
+
+
+@pytest.mark.parametrize("fault", ["distribute:3", "compute:5", "gather:7", "distribute:0"])
+@pytest.mark.parametrize("mode", ["bulk", "streamed"])
+def test_rccl_driver_fault_at_np8(tmp_path, fault, mode):
+    # a rank failing inside the rccl transport's driver (device_batch_text / the streamed device flow) at
+    # 8 ranks: the whole job aborts with the message, no rank hangs in a collective (reference bug B11)
+    from mpi_openmp_cuda_amd.utils.synthetic import make_synthetic
+
+    prob = make_synthetic("input6", 20_000, seed=5)
+    path = tmp_path / "in.txt"
+    path.write_text(prob.to_text())
+    args = ["--backend=cpu", "--transport=rccl-emul", f"--input={path}", f"--inject-fault={fault}"]
+    if mode == "streamed":
+        args.append("--batch-records=3000")
+    try:
+        r = run_final(args, stdin_bytes=b"", np_=8, env={"MOC_SEND_CHUNK": "2640"}, timeout=120)
+    except subprocess.TimeoutExpired:
+        pytest.fail(f"fault {fault} did not abort the job (hang)")
+    assert r.returncode != 0
+    assert b"injected fault" in r.stderr, r.stderr.decode()[-2000:]
 
 
 # ---- bulk jobs off the shm transport start from the text (run_text_batch / device_batch_text): the root
