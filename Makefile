@@ -60,7 +60,7 @@ $(OBJ)/%.o: csrc/src/%.cpp $(HEADERS)
 	@mkdir -p $(dir $@)
 	$(CXX) $(CXXFLAGS) $(if $(findstring /comm/,$@),$(MPIFLAGS)) -c $< -o $@
 
-$(OBJ)/%.o: csrc/src/%.hip $(HEADERS)
+$(OBJ)/%.o: csrc/src/%.hip $(HEADERS) $(wildcard csrc/src/hip/*.hpp)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -145,7 +145,8 @@ struct ShortArgs {
   int32_t tail_records = 0;           // by launch_swipe: the batch's last work is cut finer for the tail)
   int32_t codes_cap = 0;              // LDS bytes for one tile's letters (>= tile_records*max_l2+32)
   int32_t max_l2 = 0;
-  int32_t packed5 = 0;                // 1: `codes` is a 5-bit packed stream (char j at bit 5j); swipe only
+  int32_t packed5 = 0;                // 1: `codes` is a 5-bit packed stream (char j at bit 5j): staged pipeline only
+  int32_t swipe_rk = 0;               // swipe: 1 = keys without k bits, k re-found on the winning diagonal
   int32_t packed33 = 0;               // 1: `codes` holds P33 fields (moc::pack33: char j in field j / 7 at
                                       // bit 33 * (j / 7)); decoded into LDS per tile; swipe only
   unsigned* counter = nullptr;        // device work counter {next tile, blocks done}; zero at launch, the

@@ -1,0 +1,469 @@
+// Inter-record SIMD kernel for tiny problems (input6-shaped: |Seq1| <= ~100, |Seq2| <= 32, small W).
+//
+// One LANE = one whole record (vs. one lane per offset in short_kernels.hip): every lane keeps all its
+// offsets' running diagonal sums in registers as packed int16 pairs, so
+//   * no cross-lane traffic at all in the hot loop (no DPP, no segmented reductions per record),
+//   * two cells per VALU op (v_pk_add_u16 / v_pk_max_i16),
+//   * the profile row segment a lane needs at step i is read with NOFF/8 aligned ds_read_b128: the block
+//     keeps 8 copies of the int16 profile, copy s shifted left by s columns, so step i reads copy (i mod 8)
+//     at column i - (i mod 8) (a multiple of 8 -> 16-byte aligned).
+// The profile holds the diagonal DIFFERENCES Dt[c][j] = S[c][j] - S[c][j+1] (S = T[c][Seq1[j]], 0 past
+// Seq1 and in the padding row 0), pre-scaled and pre-biased: Pf[c][j] = Dt[c][j] * 2^KB - 1. A lane's
+// running sum for offset o after step i is then already the selection key of the mutant k = i + 1,
+//     E_o(i) = D_o(i+1) * 2^KB + (KMASK - (i+1)),    D_o(k) = sum_{i<k} Dt[c_i][o+i],
+// (larger D first, then smaller k), so per step and per pair of offsets (2m, 2m+1):
+//     E2[m] += (Pf[c][i+2m], Pf[c][i+2m+1])            v_pk_add_u16
+//     B2[m]  = max(B2[m], E2[m])                       v_pk_max_i16
+// i.e. 1 VALU op per cell (round 3: 2 more per pair for the shift and the step index). Tot_o is not
+// summed per cell: each lane sums the anchor diagonal Tot_NOFF = sum_i T[c_i][Seq1[NOFF + i]] (an int8
+// LUT + Seq1 staged in LDS; 0 past Seq1, consistent with the profile) and recovers
+// Tot_o = Tot_{o+1} + D_o(L2) by a suffix pass over its offsets in the epilogue, with
+// D_o(L2) = (E_o(steps-1) - (KMASK - steps)) >> KB (steps past a record's end add the padding row, Dt 0).
+// A wave runs steps = its longest record's length. Records stream through the same persistent, LDS-tiled
+// block loop as the short kernel (zero-copy from pinned host memory when the batch lives there).
+// Exactness: int16 arithmetic is exact because the host only selects this kernel when
+// 2*max|W|*max|Seq2|*2^KB + 2^KB < 2^15 (no key can wrap) — see configure_swipe. When the weights leave
+// no room for k in the keys but the sums still fit int16 (input1: W1 = 100, |Seq2| <= 41), the RK form
+// runs: Pf = Dt, the running sums are D_o(k) themselves, B2 keeps max_k D_o(k), and after the selection
+// each lane whose winner is a mutant re-walks that one diagonal for the first k reaching the best D.
+//
+// This header holds the kernel template; swipe_kernels.hip (byte letters: device-resident batches) and
+// swipe_p33.hip (P33 letters: host streams) instantiate one letter form each, so the two compile in
+// parallel, and swipe_kernels.hip also holds the host-side configuration and launch.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+
+#include "kernel_common.hpp"
+
+namespace moc {
+namespace dev {
+
+using namespace kc;
+
+namespace swipe {
+constexpr int kBlock = 256;
+constexpr int kMaxTile = 2048;  // records per tile: up to 8 per thread in the tile's length scan
+// length fields per thread in a tile's scan: 8 for P33 letters (host streams take 2048-record tiles), 4
+// for byte letters (device-resident batches: 512-record tiles, fewer registers)
+constexpr int rpt_of(int lf) { return lf == 0 ? 4 : 8; }
+constexpr int kLdsBudget = 80 * 1024;
+constexpr int kMaxV = 4;  // 16-byte letter vectors per thread per tile (register prefetch)
+
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ s16x2 as_s16x2(uint32_t v) { return __builtin_bit_cast(s16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+struct SwipeLayout {
+  int row = 0;          // profile row length (int16 entries), multiple of 8
+  int copy_elems = 0;   // 27 * row
+  int prof_bytes = 0;   // 8 shifted copies of the Dt profile
+  int s_off = 0;        // int8 LUT (32 x 32, column 31 = 0) + Seq1 codes (31 past Seq1): anchor diagonal
+  int loff_off = 0, codes_off = 0, res_off = 0, raw_off = 0, total = 0;  // raw: P33 bytes as loaded
+};
+
+inline int al16(int x) { return (x + 15) & ~15; }
+
+// P33 tiles: the loaded field bytes (33 bits per 7 letters, + alignment) of at most codes_cap letters
+inline int p33_raw_cap(int codes_cap) { return (33 * (codes_cap / 7 + 2) + 7) / 8 + 32; }
+// LDS bytes of a tile's raw (still encoded) letters by letter form
+inline int raw_cap(int lf, int codes_cap) { return lf == 2 ? p33_raw_cap(codes_cap) : 0; }
+inline int letter_form(const ShortArgs& a) { return a.packed33 ? 2 : 0; }
+
+inline SwipeLayout swipe_layout(int L1, int noff, int l2w, int tile_records, int codes_cap, int fb, int lf) {
+  SwipeLayout l;
+  // a multiple of 64 int16 (8 chunks of 16 B) so the per-letter XOR swizzle of chunk indices stays in the row
+  l.row = (std::max(L1, 4 * l2w) + noff + 8 + 63) & ~63;
+  l.copy_elems = kAlphabet * l.row;
+  l.prof_bytes = al16(8 * l.copy_elems * 2);
+  l.s_off = l.prof_bytes;
+  l.loff_off = l.s_off + al16(kLutInts + l.row);
+  l.codes_off = l.loff_off + al16((tile_records + 1) * 4 + 64);  // + misc: 16 ints
+  l.res_off = l.codes_off + al16(codes_cap);
+  l.raw_off = l.res_off + al16(tile_records * fb);
+  l.total = l.raw_off + al16(raw_cap(lf, codes_cap));
+  return l;
+}
+
+inline int kbits_for(int l2w) {  // bits for k in the int16 keys: k <= 4*l2w
+  int b = 1;
+  while ((1 << b) <= 4 * l2w) ++b;
+  return b;
+}
+}  // namespace swipe
+
+using namespace swipe;
+
+// LF: letter format of `a.codes` — 0 bytes, 2 P33 fields (decoded to bytes in LDS per tile).
+// RK: keys without k bits (the weights leave no room for them in int16): the running sums are plain
+// D_o(k), B2 keeps max_k D_o(k), and the winner's k is re-found afterwards on its diagonal.
+template <int NOFF, int L2W, int LF, bool RK>
+__global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, ShortArgs a, SwipeLayout lay) {
+  constexpr bool P33 = LF == 2;
+  constexpr int kRpt = rpt_of(LF);
+  constexpr int NW = L2W;  // record words (4 letters each) held per lane
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  short* prof = reinterpret_cast<short*>(smem);
+  int8_t* lut8 = reinterpret_cast<int8_t*>(smem + lay.s_off);
+  uint8_t* s1l = smem + lay.s_off + kLutInts;
+  int* loff = reinterpret_cast<int*>(smem + lay.loff_off);
+  int* misc = loff + a.tile_records + 1;
+  uint8_t* codes_l = smem + lay.codes_off;
+  uint8_t* res_l = smem + lay.res_off;
+  uint8_t* raw_l = smem + lay.raw_off;  // P33: the tile's encoded bytes as loaded
+  const int L1 = pv.L1;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int KB = RK ? 1 : (4 * L2W < 8) ? 3 : (4 * L2W < 16) ? 4 : (4 * L2W < 32) ? 5 : (4 * L2W < 64) ? 6 : 7;
+  constexpr int KMASK = (1 << KB) - 1;
+  constexpr int NP = NOFF / 2;  // packed accumulators
+
+  const int fb = fmt_bytes(a.fmt);
+  // tiles [0, tail_from) hold tile_records records, the rest tail_records (the batch's last work, cut finer
+  // so the blocks finish together)
+  const int64_t big_end = a.tail_records ? min(a.n, a.tail_from * a.tile_records) : a.n;
+  const int64_t n_tiles = a.tail_records ? a.tail_from + (a.n - big_end + a.tail_records - 1) / a.tail_records
+                                         : (a.n + a.tile_records - 1) / a.tile_records;
+  auto tile_first = [&](int64_t t) -> int64_t {
+    return t < a.tail_from ? t * a.tile_records : big_end + (t - a.tail_from) * a.tail_records;
+  };
+  auto tile_size = [&](int64_t t) -> int64_t { return t < a.tail_from ? a.tile_records : a.tail_records; };
+  const int sem = pv.semantics;
+
+  // ---- tile fetch: the next tile's lengths and letters are loaded into registers while the current
+  //      tile is being scored, so the PCIe / HBM read latency hides behind the compute (the streaming
+  //      path is bound by host-link bytes: keep the link busy all the time).
+  struct Fetch {
+    int64_t t, rb, start, end;
+    int m;
+    int lens[kRpt];
+    uintptr_t a0;
+    int nvec;
+    uint4 v[kMaxV];
+  };
+  auto fetch = [&](int64_t t, Fetch& f) {
+    f.t = t;
+    f.rb = f.start = f.end = 0;
+    f.m = f.nvec = 0;
+    f.a0 = 0;
+#pragma unroll
+    for (int k = 0; k < kMaxV; ++k) f.v[k] = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int q = 0; q < kRpt; ++q) f.lens[q] = 0;
+    if (t >= n_tiles) return;
+    f.rb = tile_first(t);
+    f.m = static_cast<int>(min(tile_size(t), a.n - f.rb));
+    // the tile's letter range: loaded once per block by grab(), not once per wave (each load of host
+    // memory is a PCIe read request of its own)
+    f.start = static_cast<int64_t>((static_cast<uint64_t>(static_cast<uint32_t>(misc[9])) << 32) |
+                                   static_cast<uint32_t>(misc[8]));
+    f.end = static_cast<int64_t>((static_cast<uint64_t>(static_cast<uint32_t>(misc[11])) << 32) |
+                                 static_cast<uint32_t>(misc[10]));
+#pragma unroll
+    for (int h = 0; h < kRpt / 4; ++h) {  // this thread's kRpt records' lengths, 4 per load
+      int l4[4];
+      const int r0 = tid * kRpt + 4 * h;
+      record_lengths4(a, f.rb + r0, min(4, max(0, f.m - r0)), l4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) f.lens[4 * h + q] = l4[q];
+    }
+    const int64_t b_first = P33 ? (33 * (f.start / 7)) >> 3 : f.start;
+    const int64_t b_end = P33 ? (33 * ((f.end + 6) / 7) + 7) >> 3 : f.end;
+    f.a0 = reinterpret_cast<uintptr_t>(a.codes + b_first) & ~uintptr_t{15};
+    f.nvec = static_cast<int>((reinterpret_cast<uintptr_t>(a.codes + b_end) + 15 - f.a0) >> 4);
+    MOC_DCHECK(f.nvec <= kMaxV * kBlock);
+#pragma unroll
+    for (int k = 0; k < kMaxV; ++k) {
+      const int v = tid + k * kBlock;
+      if (v < f.nvec) f.v[k] = nt_load16(reinterpret_cast<const uint4*>(f.a0) + v);
+    }
+  };
+  auto grab = [&]() -> int64_t {
+    if (tid == 0) {
+      const int64_t t = atomicAdd(a.counter, 1u);
+      misc[0] = static_cast<int>(t);
+      if (t < n_tiles) {  // the tile's letter range [offsets[rb], offsets[rb + m]) for fetch()
+        const int64_t rb = tile_first(t);
+        const int64_t st = tile_offset(a, rb), en = tile_offset(a, min(rb + tile_size(t), a.n));
+        misc[8] = static_cast<int>(static_cast<uint32_t>(st));
+        misc[9] = static_cast<int>(static_cast<uint64_t>(st) >> 32);
+        misc[10] = static_cast<int>(static_cast<uint32_t>(en));
+        misc[11] = static_cast<int>(static_cast<uint64_t>(en) >> 32);
+      }
+    }
+    __syncthreads();
+    const int64_t t = misc[0];
+    return t;
+  };
+
+  Fetch cur, nxt;
+  fetch(grab(), cur);  // the first tile's loads are in flight while the block builds its profile
+
+  // ---- 8 shifted int16 difference-profile copies: prof[s][c][j] = Pf[c][j + s], and the plain S rows.
+  //      Rows are 128-byte multiples, so the 16-byte chunk q of every row would start on the same LDS
+  //      bank; chunk q of row c is stored at chunk q ^ (c & 7) instead, spreading the 16 lanes of a
+  //      ds_read_b128 group (16 records reading 16 rows) over 8 bank quads — 8-way -> ~2-way conflicts.
+  {
+    const int row = lay.row, ce = lay.copy_elems;
+    for (int e = tid; e < 8 * ce; e += kBlock) {
+      const int s = e / ce, rem = e - s * ce, c = rem / row, jj = rem - c * row;
+      const int j = ((((jj >> 3) ^ (c & 7)) << 3) | (jj & 7)) + s;  // element stored at jj holds column j
+      const int sj = (c >= 1 && j < L1) ? pv.lut[c * kLutStride + pv.seq1[j]] : 0;
+      const int sn = (c >= 1 && j + 1 < L1) ? pv.lut[c * kLutStride + pv.seq1[j + 1]] : 0;
+      prof[e] = static_cast<short>(RK ? sj - sn : (sj - sn) * (1 << KB) - 1);  // Pf = Dt * 2^KB - 1 (header)
+    }
+    // row 0 (padding letter: steps past a lane's record) and column 31 (past Seq1) contribute 0
+    for (int e = tid; e < kLutInts; e += kBlock)
+      lut8[e] = static_cast<int8_t>((e & 31) == 31 || (e >> 5) == 0 ? 0 : pv.lut[e]);
+    for (int j = tid; j < row; j += kBlock) s1l[j] = j < L1 ? pv.seq1[j] : 31;
+  }
+  for (;;) {
+    if (cur.t >= n_tiles) break;
+    const int64_t rb = cur.rb, start = cur.start, end = cur.end;
+    const int m = cur.m;
+    __syncthreads();  // the previous tile's LDS (loff, letters, results) is free again
+
+    // ---- lengths -> block exclusive scan -> loff[0..m]
+    int sum = 0;
+#pragma unroll
+    for (int q = 0; q < kRpt; ++q) sum += cur.lens[q];
+    const int incl = wave_inclusive_sum(sum, lane);
+    if (lane == 63) misc[4 + wave] = incl;
+    // ---- letters -> LDS. Byte codes: char j at byte j. P33: the fields land in raw_l and are decoded into
+    //      bytes below (field f0 = start / 7 -> codes_l[0..]).
+    //      shift_b = position of the tile's first char inside the LDS copy.
+#pragma unroll
+    for (int k = 0; k < kMaxV; ++k) {
+      const int v = tid + k * kBlock;
+      if (v < cur.nvec) reinterpret_cast<uint4*>(P33 ? raw_l : codes_l)[v] = cur.v[k];
+    }
+    const uintptr_t p0 = reinterpret_cast<uintptr_t>(a.codes + start);
+    const int shift_b = P33 ? static_cast<int>(start - 7 * (start / 7)) : static_cast<int>(p0 - cur.a0);
+    if (tid == 0) {
+      MOC_DCHECK(a.dbg_codes_end < 0 || cur.a0 + 16 * static_cast<uintptr_t>(cur.nvec) <=
+                                            reinterpret_cast<uintptr_t>(a.codes) + a.dbg_codes_end);
+      MOC_DCHECK(end >= start && m > 0 && m <= a.tile_records);
+      MOC_DCHECK(end - start + 32 <= a.codes_cap);
+    }
+    __syncthreads();
+    int excl = incl - sum;
+    for (int w = 0; w < wave; ++w) excl += misc[4 + w];
+#pragma unroll
+    for (int q = 0; q < kRpt; ++q) {
+      const int r = tid * kRpt + q;
+      if (r < m) loff[r] = excl;
+      excl += cur.lens[q];
+    }
+    if (tid == kBlock - 1) {
+      loff[m] = excl;
+      MOC_DCHECK(excl == end - start);  // lengths agree with offsets
+    }
+    if (P33) {  // 33-bit fields -> byte codes 1..26 (the staged bytes are complete: synchronised above)
+      const int64_t f0 = start / 7;
+      const int nf = static_cast<int>((end + 6) / 7 - f0);
+      const int64_t byte0 = (33 * f0) >> 3;
+      const int ro = static_cast<int>(reinterpret_cast<uintptr_t>(a.codes + byte0) - cur.a0);
+      const int bit0 = static_cast<int>((33 * f0) & 7);
+      for (int f = tid; f < nf; f += kBlock) {
+        const int bit = bit0 + 33 * f;
+        const uint8_t* r = raw_l + ro + (bit >> 3);
+        // 33 bits at a 0..7-bit offset lie in 5 bytes (bits past the field are masked off)
+        const uint64_t w = r[0] | (static_cast<uint32_t>(r[1]) << 8) | (static_cast<uint32_t>(r[2]) << 16) |
+                           (static_cast<uint32_t>(r[3]) << 24) | (static_cast<uint64_t>(r[4]) << 32);
+        const uint64_t x = (w >> (bit & 7)) & 0x1FFFFFFFFull;
+        uint32_t v = static_cast<uint32_t>(x >> 1) / 13u;  // x / 26 in 32-bit arithmetic
+        uint8_t* d = codes_l + 7 * f;
+        d[0] = static_cast<uint8_t>(static_cast<uint32_t>(x) - 26u * v + 1u);  // x - 26q < 26: exact mod 2^32
+#pragma unroll
+        for (int j = 1; j < 7; ++j) {
+          const uint32_t q = v / 26u;
+          d[j] = static_cast<uint8_t>(v - 26u * q + 1u);
+          v = q;
+        }
+      }
+    }
+    // next tile: its loads are in flight while this one is scored
+    fetch(grab(), nxt);  // grab() synchronises: loff / letters (decoded P33) are complete
+
+    // ---- one record per lane
+    for (int g = wave; g * 64 < m; g += 4) {
+      const int rl = g * 64 + lane;
+      const bool in = rl < m;
+      int L2 = 0, rs = 0;
+      if (in) {
+        rs = shift_b + loff[rl];  // byte position in LDS
+        L2 = loff[rl + 1] - loff[rl];
+      }
+      const int need = L2 <= L1 ? L1 - L2 + 1 : 1;
+      const bool mine = in && need <= NOFF;  // others belong to the tile kernel (mixed batches)
+      const bool on = mine && L2 <= L1;
+      // record letters -> NW aligned words (bits past the record end zeroed: they add row 0 = 0)
+      uint32_t wd[NW];
+      {
+        const uint32_t* l32 = reinterpret_cast<const uint32_t*>(codes_l);
+        const int wb = rs >> 2;
+        const int sh = (rs & 3) * 8;
+        const int rbits = 8 * L2;
+        uint32_t prev = on ? l32[wb] : 0u;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+          const uint32_t nxt = on ? l32[wb + k + 1] : 0u;
+          uint32_t w = sh ? ((prev >> sh) | (nxt << (32 - sh))) : prev;
+          const int left = rbits - 32 * k;  // record bits in this word
+          w = left >= 32 ? w : (left <= 0 ? 0u : (w & ((1u << left) - 1u)));
+          wd[k] = on ? w : 0u;
+          prev = nxt;
+        }
+      }
+      const int steps = wave_max_small(on ? L2 : 0);  // L2 <= 4 * L2W <= 64 here
+
+      uint32_t E2[NP], B2[NP];
+      int anchor = 0;  // Tot_NOFF: the diagonal just past this lane's offsets
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        E2[q] = RK ? 0u : (static_cast<uint32_t>(KMASK) << 16) | KMASK;  // E_o(-1) = KMASK: D 0, k 0
+        B2[q] = 0x80008000u;  // (INT16_MIN, INT16_MIN)
+      }
+#pragma unroll
+      for (int i0 = 0; i0 < 4 * L2W; i0 += 8) {
+        if (i0 >= steps) break;  // wave-uniform
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const int i = i0 + s;
+          // wave-uniform (scalar branch): a wave stops at its longest record, not at the next multiple of
+          // 8 steps (input6: 11 steps instead of 16); the copy index s stays a compile-time constant
+          if (i >= steps) break;
+          const int c = (wd[i >> 2] >> (8 * (i & 3))) & 0xff;
+          const uint4* rowp = reinterpret_cast<const uint4*>(prof + s * lay.copy_elems + c * lay.row);
+          const int sw = c & 7;
+          uint32_t v[NP];
+#pragma unroll
+          for (int q = 0; q < NOFF / 8; ++q) {
+            const uint4 x = rowp[((i0 >> 3) + q) ^ sw];
+            v[4 * q + 0] = x.x;
+            v[4 * q + 1] = x.y;
+            v[4 * q + 2] = x.z;
+            v[4 * q + 3] = x.w;
+          }
+          anchor += lut8[(c << 5) | s1l[NOFF + i]];
+#pragma unroll
+          for (int q = 0; q < NP; ++q) {
+            E2[q] = as_u32(as_s16x2(E2[q]) + as_s16x2(v[q]));
+            B2[q] = as_u32(__builtin_elementwise_max(as_s16x2(B2[q]), as_s16x2(E2[q])));
+          }
+        }
+      }
+
+      // ---- per-lane selection over the record's offsets: 32-bit keys (score+2^15 | ~(o<<KB | k)), 0 = none.
+      //      The valid offsets are prefixes: the un-mutated candidate at o < lim0 (o <= last = L1-L2 under
+      //      the spec semantics or when L2 == L1, else o < last), the mutants at o < lim1 = last (L2 >= 2).
+      //      Running sums carry the 2^15 bias, so a key is one shift-or of them (~13 VALU ops per offset).
+      //      RK: the low bits are ~(o << 1 | mutated); bd keeps the winning mutant's D for the k re-walk.
+      //      Offsets below L1 - max_l2 (the batch's longest record) are valid for every lane that searches
+      //      (`on`): their limits are only applied above it (wave-uniform branch).
+      const int last = L1 - L2;
+      const int lim0 = on ? last + ((sem == static_cast<int>(Semantics::Spec) || L2 == L1) ? 1 : 0) : 0;
+      const int lim1 = on && L2 >= 2 ? last : 0;
+      const int all_valid = L1 - a.max_l2;
+      // D_o(L2) pairs from the final running sums: (E - (KMASK - steps)) >> KB (RK: E itself)
+      const short eb = static_cast<short>(RK ? 0 : KMASK - steps);
+      const s16x2 ebias = {eb, eb};
+      uint32_t best = 0;
+      int bd = 0;  // RK: D_o(k) of the best mutant so far
+      uint32_t tot = static_cast<uint32_t>(anchor + 32768);  // Tot_{o+1} + 2^15 entering offset o
+#pragma unroll
+      for (int o = NOFF - 1; o >= 0; --o) {
+        const s16x2 dq = RK ? as_s16x2(E2[o >> 1]) : (as_s16x2(E2[o >> 1]) - ebias) >> static_cast<short>(KB);
+        const uint32_t Pn = tot;  // Tot_{o+1} + 2^15
+        const uint32_t Po = Pn + static_cast<uint32_t>(static_cast<int>(o & 1 ? dq.y : dq.x));
+        tot = Po;  // suffix pass: Tot_o = Tot_{o+1} + D_o(L2)
+        const uint32_t kLow0 = 0xffffu - (static_cast<uint32_t>(o) << KB);  // ~(o << KB | 0)
+        const uint32_t kLow1 = kLow0 - KMASK;  // its low KB bits are 0: ~(o << KB | k) = kLow1 | (KMASK - k)
+        uint32_t k0 = (Po << 16) | kLow0;
+        // bk = d * 2^KB + (KMASK - k): the best mutant's D_o(k) and its k; t = (d + Tot_{o+1} + 2^15) * 2^KB + (KMASK - k)
+        const int bk = static_cast<short>(o & 1 ? (B2[o >> 1] >> 16) : (B2[o >> 1] & 0xffff));
+        const uint32_t t = static_cast<uint32_t>(bk) + (Pn << KB);
+        uint32_t k1 = RK ? ((static_cast<uint32_t>(bk) + Pn) << 16) | (kLow0 - 1u) : ((t >> KB) << 16) | (t & KMASK) | kLow1;
+        if (o >= all_valid) {  // wave-uniform
+          k0 = o < lim0 ? k0 : 0u;
+          k1 = o < lim1 ? k1 : 0u;
+        }
+        const uint32_t nb = max(best, max(k0, k1));
+        if (RK) bd = (nb == k1 && k1 != 0u) ? bk : bd;
+        best = nb;
+      }
+      if (!on) best = 0u;
+      int kw = 0;  // RK: the winning mutant's k
+      if (RK) {
+        // the first k of the winning offset's diagonal whose D_o(k) is the best D (k < L2: a best D reached
+        // only at k >= L2 equals D_o(L2), and then the un-mutated candidate wins the tie)
+        const bool walk = best != 0u && ((0xffffu - (best & 0xffffu)) & 1u);
+        if (__builtin_amdgcn_ballot_w64(walk) != 0) {  // wave-uniform
+          const int ow = static_cast<int>((0xffffu - (best & 0xffffu)) >> 1);
+          int run = 0;
+#pragma unroll
+          for (int i = 0; i < 4 * L2W; ++i) {
+            if (i >= steps) break;  // wave-uniform
+            const int c = (wd[i >> 2] >> (8 * (i & 3))) & 0xff;
+            const int col = ow + i;  // copy 0 holds column j at ((j >> 3) ^ (c & 7)) << 3 | (j & 7)
+            run += prof[c * lay.row + ((((col >> 3) ^ (c & 7)) << 3) | (col & 7))];
+            kw = (kw == 0 && run == bd) ? i + 1 : kw;
+          }
+        }
+      }
+      if (mine) {
+        Result res;
+        if (best == 0u) {
+          res = Result{INT32_MIN, 0, 0};
+        } else {
+          const uint32_t idx = 0xffffu - (best & 0xffffu);
+          res = RK ? Result{static_cast<int>(best >> 16) - 32768, static_cast<int>(idx >> 1), (idx & 1u) ? kw : 0}
+                   : Result{static_cast<int>(best >> 16) - 32768, static_cast<int>(idx >> KB), static_cast<int>(idx & KMASK)};
+        }
+        store_result(res_l, rl, a.fmt, res, pv.r2);
+      }
+    }
+    __syncthreads();
+    copy_results(static_cast<char*>(a.out) + rb * fb, res_l, m * fb, tid, kBlock);
+    cur = nxt;
+  }
+  release_work_counter(a.counter);
+}
+
+
+// Launches the instance of letter form LF that `a` selects (a.slot = offsets per lane, a.rpw = record
+// words, a.swipe_rk = RK); false when no instance matches.
+template <int LF>
+bool launch_swipe_form(const ProblemView& pv, const ShortArgs& b, const SwipeLayout& lay, dim3 grid, dim3 block,
+                       hipStream_t stream) {
+  const int noff = b.slot, l2w = b.rpw;
+  const bool rk = b.swipe_rk != 0;
+#define MOC_SWIPE_CASE(NO, LW, RKV)                                                                        \
+  if (noff == NO && l2w == LW && rk == RKV) {                                                            \
+    hipLaunchKernelGGL((swipe_search_kernel<NO, LW, LF, RKV>), grid, block, lay.total, stream, pv, b, lay); \
+    return true;                                                                                         \
+  }
+#define MOC_SWIPE_NOFF(LW, RKV)                                                                            \
+  MOC_SWIPE_CASE(8, LW, RKV)                                                                             \
+  MOC_SWIPE_CASE(16, LW, RKV)                                                                            \
+  MOC_SWIPE_CASE(24, LW, RKV)                                                                            \
+  MOC_SWIPE_CASE(32, LW, RKV)                                                                            \
+  MOC_SWIPE_CASE(40, LW, RKV)                                                                            \
+  MOC_SWIPE_CASE(48, LW, RKV)                                                                            \
+  MOC_SWIPE_CASE(56, LW, RKV)                                                                            \
+  MOC_SWIPE_CASE(64, LW, RKV)
+  MOC_SWIPE_NOFF(4, false)
+  MOC_SWIPE_NOFF(8, false)
+  MOC_SWIPE_NOFF(4, true)
+  MOC_SWIPE_NOFF(8, true)
+  MOC_SWIPE_NOFF(16, true)  // records of 33..64 letters run the RK form only (configure_swipe)
+#undef MOC_SWIPE_NOFF
+#undef MOC_SWIPE_CASE
+  return false;
+}
+
+}  // namespace dev
+}  // namespace moc

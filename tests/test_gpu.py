@@ -158,8 +158,8 @@ def test_zero_copy_direct(fmt, use_lengths):
 @pytest.mark.parametrize("shape,n", [("input6", 250_003), ("input1", 3000), ("input4", 200), ("input3", 20)])
 @pytest.mark.parametrize("pinned", [False, True])
 def test_packed5_letters(shape, n, pinned):
-    # 5-bit packed letters: streamed straight into the swipe kernel (pinned, tiny problems) or unpacked
-    # on the device by the staged pipeline (everything else)
+    # 5-bit packed letters (the dense wire form): unpacked on the device by the staged pipeline, pinned or
+    # not (the streaming kernels take P33 or byte letters)
     from mpi_openmp_cuda_amd.models.problem import pack5
 
     prob = make_synthetic(shape, n, seed=n)
@@ -172,8 +172,9 @@ def test_packed5_letters(shape, n, pinned):
     eng.solve(packed, prob.offsets, out=out, packed5=True)
     st = eng.stats()
     assert np.array_equal(as_triples(out), as_triples(search_cpu(prob))), st
-    if pinned and shape == "input6":
-        assert st["direct"] == 1 and st["kernels"] == ["swipe"]
+    assert st["direct"] == 0, st
+    if shape == "input6":
+        assert st["kernels"] == ["swipe"], st
     eng.close()
 
 
@@ -201,11 +202,13 @@ def test_group_coded_letters(shape, n, pinned):
 
 @pytest.mark.parametrize("L1,lo,hi,w", [(26, 6, 11, (4, 3, 2, 10)), (12, 1, 14, (3, 1, 1, 2)),
                                         (40, 20, 32, (5, 2, 3, 4)), (60, 10, 16, (2, 2, 1, 3)),
-                                        (9, 9, 9, (7, 1, 2, 3))])
+                                        (9, 9, 9, (7, 1, 2, 3)), (51, 32, 41, (100, 2, 3, 4)),
+                                        (70, 40, 64, (3, 1, 2, 1)), (30, 5, 12, (120, 1, 1, 1))])
 @pytest.mark.parametrize("letters", ["p33", "p5"])
 def test_swipe_wire_slices(L1, lo, hi, w, letters):
     # the headline's wire path (parallel/wire.py: narrow lengths, R2/R4 results, zero-copy) across swipe
-    # instantiations (NOFF 8..64, record widths <= 16 / <= 32) for every packed letter format
+    # instantiations (NOFF 8..64, record widths <= 16 / <= 32 / <= 64, keys with k bits and the RK form that
+    # re-walks k) with P33 letters; 5-bit letters take the staged pipeline to the same kernel
     from mpi_openmp_cuda_amd._lib import Pinned
     from mpi_openmp_cuda_amd.parallel.wire import WireSlice
 
@@ -223,13 +226,13 @@ def test_swipe_wire_slices(L1, lo, hi, w, letters):
     st = eng.stats()
     assert np.array_equal(ws.triples(eng), as_triples(search_cpu(prob))), st
     if L1 - min(lo, hi) + 1 <= 64:
-        assert st["kernels"] == ["swipe"] and st["direct"] == 1, st
+        assert st["kernels"] == ["swipe"] and st["direct"] == (1 if letters == "p33" else 0), st
     eng.close()
 
 
-@pytest.mark.parametrize("L1,lo,hi", [(80, 40, 45), (100, 50, 55)])
+@pytest.mark.parametrize("L1,lo,hi", [(120, 70, 75), (130, 80, 85)])
 def test_short_kernel_base6_lengths(L1, lo, hi):
-    # byte letters + base-6 lengths through the lane-per-offset short kernel (records longer than 32 letters
+    # byte letters + base-6 lengths through the lane-per-offset short kernel (records longer than 64 letters
     # leave the swipe kernel; at most 64 lanes per record keep them on the short one)
     from mpi_openmp_cuda_amd._lib import Pinned
     from mpi_openmp_cuda_amd.parallel.wire import WireSlice
@@ -263,10 +266,16 @@ def test_staged_formats(engine, fmt):
 
 @pytest.mark.parametrize("L1,lo,hi,w", [(26, 6, 11, (4, 3, 2, 10)), (12, 1, 14, (3, 1, 1, 2)),
                                         (40, 20, 32, (5, 2, 3, 4)), (60, 10, 16, (2, 2, 1, 3)),
-                                        (100, 40, 32, (1, 1, 1, 1)), (9, 9, 9, (7, 1, 2, 3))])
+                                        (100, 40, 32, (1, 1, 1, 1)), (9, 9, 9, (7, 1, 2, 3)),
+                                        # the RK form (no k bits in the keys; k re-walked): input1's shape,
+                                        # records <= 16 / <= 32 / <= 64 letters, 64 offsets per lane
+                                        (51, 32, 41, (100, 2, 3, 4)), (30, 5, 12, (120, 1, 1, 1)),
+                                        (40, 20, 30, (60, 2, 3, 4)), (70, 40, 64, (3, 1, 2, 1)),
+                                        (66, 3, 64, (2, 1, 1, 1)), (64, 1, 64, (90, 7, 3, 5))])
 @pytest.mark.parametrize("sem", [Semantics.REFERENCE, Semantics.SPEC])
 def test_swipe_kernel_shapes(engine, L1, lo, hi, w, sem):
-    # lane-per-record packed-int16 kernel across offset widths (NOFF 8..64) and record widths (<=16, <=32)
+    # lane-per-record packed-int16 kernel across offset widths (NOFF 8..64), record widths (<= 16, <= 32,
+    # <= 64) and both key forms
     rng = np.random.default_rng(L1 * 100 + lo)
     s1 = "".join(chr(65 + x) for x in rng.integers(0, 26, L1))
     lens = rng.integers(max(1, min(lo, hi)), max(lo, hi) + 1, 3000)
@@ -285,8 +294,11 @@ def test_kernel_selection(engine):
     engine.set_problem(p6.weights, p6.seq1)
     engine.solve(p6.codes, p6.offsets)
     assert engine.stats()["kernels"] == ["swipe"]
-    p1 = make_synthetic("input1", 2000, seed=1)  # W1 = 100 overflows the int16 keys -> lane/offset kernel
+    p1 = make_synthetic("input1", 2000, seed=1)  # W1 = 100: no room for k in the int16 keys -> RK swipe
     engine.set_problem(p1.weights, p1.seq1)
+    engine.solve(p1.codes, p1.offsets)
+    assert engine.stats()["kernels"] == ["swipe"]
+    engine.set_problem([300, 2, 3, 4], p1.seq1)  # |T| 300 > 127: the int8 anchor LUT -> lane/offset kernel
     engine.solve(p1.codes, p1.offsets)
     assert engine.stats()["kernels"] == ["short"]
     p4 = make_synthetic("input4", 50, seed=1)  # long records: packed-int16 profile kernel
@@ -550,7 +562,7 @@ def test_r2_results_and_nibble_lengths(pinned, packed, shape, n):
     assert st["r2"] == eng.r2_params(sh.l2_min, sh.l2_max)
     assert np.array_equal(as_triples(out, r2=st["r2"]), as_triples(search_cpu(prob))), st
     if pinned and shape == "input6":
-        assert st["direct"] == 1
+        assert st["direct"] == (0 if packed else 1)  # 5-bit letters: the staged pipeline
     eng.close()
 
 
@@ -594,7 +606,7 @@ def test_pinned_neighbours_staged_copies():
     eng.close()
 
 
-# every (letters, lengths) combination a pinned batch can stream in: packed letters go to the swipe kernel only
+# every (letters, lengths) combination a pinned batch can come in: 5-bit letters take the staged pipeline
 # (input6), 3-bit lengths need a span of at most 8 values and base-6 at most 6 (input6: 6..11)
 @pytest.mark.parametrize("shape,n,packed,len_bits", [
     ("input6", 100_003, False, 0), ("input6", 100_003, False, 8), ("input6", 100_003, True, 4),
@@ -632,12 +644,12 @@ def test_host_stream_lengths(packed, len_bits, shape, n):
     eng.pin(codes, prob.offsets, out, *([lengths] if lengths is not None else []))
     eng.solve(codes, prob.offsets, out=out, fmt="r8", packed5=packed, **kw)
     st = eng.stats()
-    assert st["direct"] == 1, st
+    assert st["direct"] == (0 if packed else 1), st  # 5-bit letters: the staged pipeline
     assert np.array_equal(as_triples(out), as_triples(search_cpu(prob))), st
     eng.close()
 
 
-@pytest.mark.parametrize("L1,lo,hi,kernel", [(90, 3, 11, "tile16"), (40, 33, 38, "short")])
+@pytest.mark.parametrize("L1,lo,hi,kernel", [(90, 3, 11, "tile16"), (100, 66, 70, "short")])
 def test_r2_tiles_and_short_kernels(engine, L1, lo, hi, kernel):
     # R2 through the tile kernel's finalize and the lane/offset kernel (staged path)
     rng = np.random.default_rng(5)
