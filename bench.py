@@ -388,7 +388,7 @@ def main():
     barrier()
     progress(f"timing {args.steps} steps")
     t0 = time.perf_counter()
-    kms, tms, sms = [], [], []
+    kms, tms, sms, ends = [], [], [], []
     t_prev = t0
     for _ in range(args.steps):
         step()
@@ -397,6 +397,7 @@ def main():
         tms.append(t_ms)
         t_now = time.perf_counter()  # host clock per step (rank 0's view; the job is timed by t0 / elapsed)
         sms.append((t_now - t_prev) * 1e3)
+        ends.append(time.time())  # wall-clock end of the step (correlated with tools/gpu_sampler.py samples)
         t_prev = t_now
     barrier()
     elapsed = time.perf_counter() - t0
@@ -523,7 +524,7 @@ def main():
         print(json.dumps(out), flush=True)
         if args.dump_steps:
             with open(args.dump_steps, "w") as f:
-                json.dump({"kernel_ms": kms, "step_ms": sms, "solve_ms": tms}, f)
+                json.dump({"kernel_ms": kms, "step_ms": sms, "solve_ms": tms, "end_time": ends}, f)
     pin.release()
     if distributed:
         barrier()
