@@ -86,7 +86,7 @@ void run_sliced(JobCore& job, BulkParser& parser, int64_t first_index, SharedWin
   // ---- fill: every rank encodes its slice (GPU ranks guess the narrow form from the mean length)
   pt.begin("fill");
   job.fault.at("distribute", r);
-  bool narrow = gpu && n > 0 && L1 <= 200 && slice.letters <= 32 * n;
+  bool narrow = gpu && n > 0 && L1 <= 200 && slice.letters <= 64 * n;
   // GPU ranks: one NUMA-local region for the wire batch, letters | offsets | lengths (one page-lock
   // registration for the slice: each costs milliseconds whatever its size)
   HostRegion wire, len16;

@@ -328,7 +328,7 @@ bool StreamFlow::fill(const BatchMsg& m, const std::vector<int64_t>& table, int 
     // one page-locked arena per slot, carved into letters | offsets | lengths: one registration per slot
     // (each registration costs milliseconds, whatever its size)
     auto al64 = [](int64_t x) { return (x + 63) & ~int64_t{63}; };
-    bool narrow = L1 <= 200 && slice.letters <= 32 * n;
+    bool narrow = L1 <= 200 && slice.letters <= 64 * n;
     const int pack = narrow ? 33 : 5;
     uint8_t* letters = nullptr;
     int64_t* offsets = nullptr;

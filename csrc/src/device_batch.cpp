@@ -446,7 +446,7 @@ DeviceBatchOut device_batch_text(DeviceComm& dc, DeviceSearch& ds, const BulkPar
                     : al16(packed5_bytes(sl.letters)) + al16(8 * (n + 1)) + 64;
     };
     // the narrow form when the mean length says it can hold the slice (checked against the slice's range)
-    auto guess_narrow = [L1](const AreaSlice& sl) { return sl.records > 0 && L1 <= 200 && sl.letters <= 32 * sl.records; };
+    auto guess_narrow = [L1](const AreaSlice& sl) { return sl.records > 0 && L1 <= 200 && sl.letters <= 64 * sl.records; };
     int64_t block_cap = 64, stage_bytes = 64;
     for (int r = 0; r < p; ++r) {
       slices[r] = parser->slice(bounds[r], bounds[r + 1]);

@@ -845,7 +845,7 @@ def test_python_driver_hip_two_ranks(tmp_path):
 
 @pytest.mark.parametrize("mode", ["bulk", "stream"])
 def test_final_narrow_guess_fails_stdin_two_ranks(mode):
-    # a GPU rank whose narrow-form guess (L1 <= 200, mean length <= 32) is refused by the
+    # a GPU rank whose narrow-form guess (L1 <= 200, mean length <= 64) is refused by the
     # engine (here L1 - min_l2 + 1 > 64 lanes) re-encodes its slice as 5-bit letters + CSR offsets. That
     # must happen while the node-shared stdin text is still there — before the helpers release their
     # shares of it — and every row must match the CPU engine.
