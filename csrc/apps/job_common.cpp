@@ -168,6 +168,9 @@ void JobCore::setup_engine(int64_t job_cells, int64_t mean_l2) {
     go.chunk_records = flags.get_int("chunk-records", 0);
     go.chunk_bytes = flags.get_int("chunk-bytes", 0);
     go.log_level = flags.get("log-level", "warn");
+    // a job below the GPU crossover (forced with --backend=hip) runs one kernel once: loading every code
+    // object up front would cost more than that kernel's own load at its launch
+    go.preload_kernels = job_cells < 0 || job_cells >= min_cells * ctx.size;
     sw_create.start();
     eng.hip.reset(gpu_rank_create(ctx, go));
     device = eng.hip->device();

@@ -26,6 +26,7 @@ struct GpuRankOptions {
   int64_t chunk_records = 0;    // 0: engine defaults
   int64_t chunk_bytes = 0;
   std::string log_level = "warn";
+  bool preload_kernels = true;  // false: kernel code objects load at their first launch (tiny jobs)
 };
 
 // What the last solve moved and ran (for --timing).

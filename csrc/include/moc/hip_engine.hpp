@@ -38,6 +38,9 @@ struct EngineOptions {
   int64_t chunk_bytes = 64ll << 20;  // staged pipeline: max letter bytes per chunk
   bool allow_direct = true;          // use zero-copy streaming when the host buffers are pinned
   bool use_graphs = true;            // replay the direct path's launches as a captured hipGraph
+  // load every kernel's code object when the engine starts (on a helper thread, beside the stream set-up),
+  // not inside the first timed launch; false: each loads at its first launch (a tiny job runs one kernel)
+  bool preload = true;
   // Pinned host batches stream zero-copy: the kernel reads / writes host memory itself. A chunked SDMA
   // pipeline around the HBM-resident kernel was measured slower on the registered node-shared arrays the
   // headline streams from (4.4 vs 4.0 ms/step, profiles/host_stream_ab.log) and was retired in round 4.

@@ -73,17 +73,17 @@ HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
   init_sw.start();
   if (opt_.device >= 0) MOC_HIP_CHECK(hipSetDevice(opt_.device));
   MOC_HIP_CHECK(hipGetDevice(&device_));
-  hipDeviceProp_t prop;
-  MOC_HIP_CHECK(hipGetDeviceProperties(&prop, device_));
-  num_cus_ = prop.multiProcessorCount;
+  MOC_HIP_CHECK(hipDeviceGetAttribute(&num_cus_, hipDeviceAttributeMultiprocessorCount, device_));
   const double t_dev = init_sw.total_ms();
   if (const char* m = std::getenv("MOC_MFMA")) mfma_ = std::atoi(m) != 0;
   // code objects on the device now, not inside the first timed launch — on a helper thread, while this one
   // sets up the compute stream and buffers (independent runtime work, ~13 and ~20 ms on the MI355X box)
-  auto preload = std::async(std::launch::async, [dev_id = device_, mfma = mfma_] {
-    MOC_HIP_CHECK(hipSetDevice(dev_id));
-    dev::preload_kernels(mfma);
-  });
+  std::future<void> preload;
+  if (opt_.preload)
+    preload = std::async(std::launch::async, [dev_id = device_, mfma = mfma_] {
+      MOC_HIP_CHECK(hipSetDevice(dev_id));
+      dev::preload_kernels(mfma);
+    });
   const double t_preload = init_sw.total_ms();
   if (const char* g = std::getenv("MOC_GRAPHS")) opt_.use_graphs = std::atoi(g) != 0;
   if (const char* u = std::getenv("MOC_TILE_U")) {  // tuning override of the per-batch choice
@@ -115,7 +115,7 @@ HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
   MOC_HIP_CHECK(hipEventCreate(&ev_a_));
   MOC_HIP_CHECK(hipEventCreate(&ev_b_));
   MOC_HIP_CHECK(hipEventCreateWithFlags(&ev_plan_, hipEventDisableTiming));
-  preload.get();  // rethrows a load error
+  if (preload.valid()) preload.get();  // rethrows a load error
   MOC_LOG_DEBUG("engine on device %d up in %.1f ms (device %.1f, kernel preload started %.1f, streams %.1f, buffers + preload %.1f)", device_,
                 init_sw.total_ms(), t_dev, t_preload - t_dev, t_streams - t_preload, init_sw.total_ms() - t_streams);
 }
