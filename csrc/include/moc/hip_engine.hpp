@@ -164,8 +164,8 @@ class HipEngine {
   void ensure(void*& ptr, size_t& cap, size_t bytes);
   void ensure_host(void*& ptr, size_t& cap, size_t bytes);
   bool direct_pointers(const WireBatch& b, void* out, int fb, dev::ShortArgs& a) const;
-  void prepare_direct(const dev::ProblemView& pv, const dev::ShortArgs& a, bool swipe);
-  void launch_direct(const dev::ProblemView& pv, const dev::ShortArgs& a, bool swipe);
+  bool prepare_direct(const dev::ProblemView& pv, const dev::ShortArgs& a, bool swipe);
+  void launch_direct(const dev::ProblemView& pv, const dev::ShortArgs& a, bool swipe, bool graph);
   void run_staged(const uint8_t* codes, const int64_t* offsets, int64_t n, void* out, ResultFormat fmt,
                   bool packed5);
   void solve_wire_impl(const WireBatch& b, void* out, ResultFormat fmt, bool async);
@@ -218,6 +218,8 @@ class HipEngine {
   DirectKey graph_key_[kGraphs]{};
   hipGraphExec_t graph_exec_[kGraphs] = {nullptr, nullptr};
   int graph_cur_ = 0;
+  DirectKey seen_key_{};  // the last argument set launched without a graph (captured when seen again)
+  bool seen_valid_ = false;
   bool pending_ = false;  // a begin_wire solve is in flight (ev_a_ .. ev_b_)
   Stopwatch pending_wall_;
   EngineStats stats_;

@@ -670,9 +670,9 @@ void HipEngine::solve_wire_impl(const WireBatch& batch, void* out, ResultFormat 
                          (a.tile_records % (1 << b.off_shift)) == 0;
   if ((opt_.allow_direct || b.device) && kernel_ok && direct_pointers(b, out, fb, a)) {
     const dev::ProblemView pv = problem_view(ls.mx);
-    prepare_direct(pv, a, swipe);  // graph capture / instantiation stays outside the timed span
+    const bool graph = prepare_direct(pv, a, swipe);  // capture / instantiation stays outside the timed span
     MOC_HIP_CHECK(hipEventRecord(ev_a_, s_compute_));
-    launch_direct(pv, a, swipe);
+    launch_direct(pv, a, swipe, graph);
     stats_.kernels = swipe ? 1 : 2;
     MOC_HIP_CHECK(hipEventRecord(ev_b_, s_compute_));
     stats_.direct = 1;
@@ -708,8 +708,8 @@ void HipEngine::solve_wire_impl(const WireBatch& batch, void* out, ResultFormat 
 // captured once per distinct argument set, replayed for repeated solves over the same buffers (a
 // bench loop, a service re-scoring a resident batch) — one graph launch instead of re-validating and
 // re-encoding two launches. Arguments are plain structs, compared bytewise.
-void HipEngine::prepare_direct(const dev::ProblemView& pv, const dev::ShortArgs& a, bool swipe) {
-  if (!opt_.use_graphs) return;
+bool HipEngine::prepare_direct(const dev::ProblemView& pv, const dev::ShortArgs& a, bool swipe) {
+  if (!opt_.use_graphs) return false;
   DirectKey key;
   std::memset(static_cast<void*>(&key), 0, sizeof key);  // padding too: keys are compared bytewise
   key.pv = pv;
@@ -718,8 +718,15 @@ void HipEngine::prepare_direct(const dev::ProblemView& pv, const dev::ShortArgs&
   for (int i = 0; i < kGraphs; ++i)
     if (graph_exec_[i] && std::memcmp(&key, &graph_key_[i], sizeof key) == 0) {
       graph_cur_ = i;
-      return;
+      return true;
     }
+  // an argument set seen for the first time launches plainly: a one-shot job (./final on a reference
+  // input) pays no capture and instantiation; a repeated solve captures at its second launch
+  if (!seen_valid_ || std::memcmp(&key, &seen_key_, sizeof key) != 0) {
+    std::memcpy(static_cast<void*>(&seen_key_), &key, sizeof key);
+    seen_valid_ = true;
+    return false;
+  }
   // two argument sets stay instantiated (a streaming job alternates between the two slots of its ring):
   // the one not used last is replaced
   const int slot = graph_exec_[graph_cur_] ? 1 - graph_cur_ : graph_cur_;
@@ -741,13 +748,14 @@ void HipEngine::prepare_direct(const dev::ProblemView& pv, const dev::ShortArgs&
   MOC_HIP_CHECK(inst);
   std::memcpy(static_cast<void*>(&graph_key_[slot]), &key, sizeof key);
   graph_cur_ = slot;
+  return true;
 }
 
 // The direct path's launch (work-counter reset + persistent streaming kernel): the hipGraph captured
 // by prepare_direct for this argument set — one graph launch for repeated solves over the same buffers
 // (a bench loop, a service re-scoring a resident batch) — or a plain launch without graphs.
-void HipEngine::launch_direct(const dev::ProblemView& pv, const dev::ShortArgs& a, bool swipe) {
-  if (!opt_.use_graphs) {
+void HipEngine::launch_direct(const dev::ProblemView& pv, const dev::ShortArgs& a, bool swipe, bool graph) {
+  if (!graph) {
     if (swipe)
       dev::launch_swipe(pv, a, num_cus_, s_compute_);
     else
