@@ -271,7 +271,10 @@ def test_staged_formats(engine, fmt):
                                         # records <= 16 / <= 32 / <= 64 letters, 64 offsets per lane
                                         (51, 32, 41, (100, 2, 3, 4)), (30, 5, 12, (120, 1, 1, 1)),
                                         (40, 20, 30, (60, 2, 3, 4)), (70, 40, 64, (3, 1, 2, 1)),
-                                        (66, 3, 64, (2, 1, 1, 1)), (64, 1, 64, (90, 7, 3, 5))])
+                                        (40, 20, 40, (2, 1, 1, 1)), (56, 25, 56, (90, 7, 3, 5)),
+                                        # 64 offsets and 64-letter records: 8 profile copies of 192-entry
+                                        # rows exceed the LDS budget -> the lane/offset kernel
+                                        (66, 3, 64, (2, 1, 1, 1))])
 @pytest.mark.parametrize("sem", [Semantics.REFERENCE, Semantics.SPEC])
 def test_swipe_kernel_shapes(engine, L1, lo, hi, w, sem):
     # lane-per-record packed-int16 kernel across offset widths (NOFF 8..64), record widths (<= 16, <= 32,
@@ -286,7 +289,7 @@ def test_swipe_kernel_shapes(engine, L1, lo, hi, w, sem):
     kinds = engine.stats()["kernels"]
     assert np.array_equal(as_triples(got, r2=engine.stats()["r2"]), as_triples(search_cpu(prob, sem))), kinds
     if L1 - min(lo, hi) + 1 <= 64:
-        assert kinds == ["swipe"], kinds
+        assert kinds == (["short"] if (L1, lo, hi) == (66, 3, 64) else ["swipe"]), kinds
 
 
 def test_kernel_selection(engine):
@@ -649,9 +652,11 @@ def test_host_stream_lengths(packed, len_bits, shape, n):
     eng.close()
 
 
-@pytest.mark.parametrize("L1,lo,hi,kernel", [(90, 3, 11, "tile16"), (100, 66, 70, "short")])
+@pytest.mark.parametrize("L1,lo,hi,kernel", [(90, 3, 11, "tile16"), (40, 33, 38, "swipe")])
 def test_r2_tiles_and_short_kernels(engine, L1, lo, hi, kernel):
-    # R2 through the tile kernel's finalize and the lane/offset kernel (staged path)
+    # R2 through the tile kernel's finalize and the swipe kernel's RK form from HBM (staged path). Every
+    # problem whose results fit R2 and whose records need <= 64 lanes now runs on swipe, not the lane/offset
+    # kernel (its R2 store is the shared store_result)
     rng = np.random.default_rng(5)
     s1 = "".join(chr(65 + x) for x in rng.integers(0, 26, L1))
     recs = ["".join(chr(65 + x) for x in rng.integers(0, 26, rng.integers(lo, hi + 1))) for _ in range(501)]
