@@ -296,6 +296,10 @@ int Job::run() {
   int threads = static_cast<int>(flags.get_int("threads", 0));
   if (threads <= 0 && !std::getenv("OMP_NUM_THREADS")) threads = std::max(1, omp_get_num_procs() / ctx.local_size);
   if (threads > 0) omp_set_num_threads(threads);
+  // the root formats the rows while the node's other ranks wait for it: it may use their threads too
+  // (not when OMP_NUM_THREADS fixes every process's team by itself)
+  if (threads > 0 && ctx.local_size > 1)
+    job_.print_threads = std::min(omp_get_num_procs(), threads * ctx.local_size);
   job_.total.start();
   prewarm_gpu();
 

@@ -338,6 +338,7 @@ void run_sliced(JobCore& job, BulkParser& parser, int64_t first_index, SharedWin
       runs[q].r2 = R2Params{static_cast<int32_t>(x[2]), static_cast<int32_t>(x[3]), static_cast<int32_t>(x[4])};
     }
     pt.begin("print");
+    ScopedOmpThreads team(job.print_threads);  // the other ranks wait at the segments' fence
     write_results(job.out, runs, first_index);
     pt.end();
   }

@@ -487,6 +487,7 @@ void StreamFlow::finish(int s, Done& d) {
 void StreamFlow::print(int s) {
   if (j_.ctx.rank != kRoot || runs_[s].empty()) return;
   j_.pt.begin("print");
+  ScopedOmpThreads team(j_.print_threads);  // the other ranks wait for the next batch's broadcast
   write_results(j_.out, runs_[s], runs_first_[s]);
   runs_[s].clear();
   j_.pt.end();

@@ -8,6 +8,8 @@
 //                    context-parallel jobs, the StreamReader path)
 #pragma once
 
+#include <omp.h>
+
 #include <cstdio>
 #include <functional>
 #include <future>
@@ -112,6 +114,9 @@ struct JobCore {
   std::vector<int64_t> rank_pinned, rank_h2d, rank_records, rank_pin_us;  // root: per rank (--timing)
   std::vector<std::pair<std::string, std::string>> extra_timing;          // flow-specific --timing fields
   const char* build_id = "";  // the sources of this binary (--timing)
+  // root: OpenMP threads for formatting the rows, which the other ranks of the node wait for (0: the
+  // rank's own count). The node's thread budget, when the ranks' counts were divided from it.
+  int print_threads = 0;
 
   // collective: engine kind, transport, RCCL communicator (cells < 0: unknown)
   void setup_engine(int64_t job_cells, int64_t mean_l2);
@@ -126,6 +131,18 @@ struct JobCore {
   CostModel cost_model() const { return all_gpu ? CostModel{1.0, 200.0, 2400.0} : CostModel{1.0, 4.0, 64.0}; }
   // collective: the --timing JSON line on root's stderr
   void report(const Header& h);
+};
+
+// Sets the calling thread's OpenMP team size for a scope (n <= 0: unchanged).
+class ScopedOmpThreads {
+ public:
+  explicit ScopedOmpThreads(int n) : prev_(omp_get_max_threads()) {
+    if (n > 0) omp_set_num_threads(n);
+  }
+  ~ScopedOmpThreads() { omp_set_num_threads(prev_); }
+
+ private:
+  int prev_;
 };
 
 // ---- flows
