@@ -98,6 +98,8 @@ int moc_engine_auto_format(void* e, int64_t max_l2, int64_t min_l2);
 int moc_engine_r2_params(void* e, int64_t min_l2, int64_t max_l2, int32_t* out3);
 int moc_engine_pin(void* e, const void* p, size_t bytes);
 
+// device time (ms) of the last moc_engine_solve_device's kernels; waits for them
+int moc_engine_device_kernel_ms(void* e, double* ms);
 int moc_engine_solve_device(void* e, const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets,
                             int64_t n, moc_result* d_out, void* stream);
 int moc_engine_search_keys(void* e, const uint8_t* codes, const int64_t* offsets, int64_t n, int part, int parts,

@@ -106,6 +106,9 @@ class HipEngine {
 
   // Device-resident batch: d_codes/d_offsets/d_out on this device; h_offsets is a host copy of the
   // offsets used for planning. Work is queued on `stream` (0 = engine compute stream); no sync.
+  // Device time of the last solve_device's kernels (events recorded around its launches, after the host
+  // planning): waits for them. Kernel throughput without the host's per-call planning in the interval.
+  double device_kernel_ms();
   void solve_device(const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets, int64_t n,
                     Result* d_out, hipStream_t stream);
 
@@ -208,6 +211,7 @@ class HipEngine {
   void* h_plan_ = nullptr;
   size_t h_plan_cap_ = 0;
   hipEvent_t ev_plan_ = nullptr;
+  hipEvent_t ev_d0_ = nullptr, ev_d1_ = nullptr;  // around solve_device's launches (device_kernel_ms)
   std::vector<void*> pinned_;
   struct DirectKey {
     dev::ProblemView pv;

@@ -348,6 +348,10 @@ int moc_engine_pin(void* e, const void* p, size_t bytes) {
   return guard([&] { static_cast<moc::HipEngine*>(e)->pin(p, bytes); });
 }
 
+int moc_engine_device_kernel_ms(void* e, double* ms) {
+  return guard([&] { *ms = static_cast<moc::HipEngine*>(e)->device_kernel_ms(); });
+}
+
 int moc_engine_solve_device(void* e, const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets,
                             int64_t n, moc_result* d_out, void* stream) {
   return guard([&] {

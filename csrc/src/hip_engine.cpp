@@ -143,6 +143,8 @@ HipEngine::~HipEngine() {
   (void)hipFree(d_plan_);
   (void)hipHostFree(h_plan_);
   (void)hipEventDestroy(ev_plan_);
+  if (ev_d0_) (void)hipEventDestroy(ev_d0_);
+  if (ev_d1_) (void)hipEventDestroy(ev_d1_);
   (void)hipEventDestroy(ev_a_);
   (void)hipEventDestroy(ev_b_);
   (void)hipFree(d_image_);
@@ -889,6 +891,14 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
   stats_.chunks = chunk;
 }
 
+double HipEngine::device_kernel_ms() {
+  if (!ev_d1_) return 0;
+  MOC_HIP_CHECK(hipEventSynchronize(ev_d1_));
+  float ms = 0;
+  MOC_HIP_CHECK(hipEventElapsedTime(&ms, ev_d0_, ev_d1_));
+  return ms;
+}
+
 void HipEngine::solve_device(const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets, int64_t n,
                              Result* d_out, hipStream_t stream) {
   if (!have_problem_) throw Error("HipEngine::solve_device before set_problem");
@@ -921,6 +931,11 @@ void HipEngine::solve_device(const uint8_t* d_codes, const int64_t* d_offsets, c
     MOC_HIP_CHECK(hipMemcpyAsync(d_plan_, h_plan_, lay.upload_bytes, hipMemcpyHostToDevice, stream));
   }
   const dev::ProblemView pv = problem_view(cp.max_l2);
+  if (!ev_d0_) {
+    MOC_HIP_CHECK(hipEventCreate(&ev_d0_));
+    MOC_HIP_CHECK(hipEventCreate(&ev_d1_));
+  }
+  MOC_HIP_CHECK(hipEventRecord(ev_d0_, stream));
   if (short_ok) {
     a.codes = d_codes;
     a.offsets = d_offsets;
@@ -938,6 +953,7 @@ void HipEngine::solve_device(const uint8_t* d_codes, const int64_t* d_offsets, c
     dev::launch_tiles(tile_view(cp.max_l2, tp), bv, plan, d_out, static_cast<int>(ResultFormat::R12), stream);
   }
   MOC_HIP_CHECK(hipGetLastError());
+  MOC_HIP_CHECK(hipEventRecord(ev_d1_, stream));
   MOC_HIP_CHECK(hipEventRecord(ev_plan_, stream));
   stats_ = EngineStats{};
   stats_.cells = cp.cells;

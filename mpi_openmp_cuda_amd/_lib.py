@@ -85,6 +85,7 @@ def _decl(lib):
         "moc_engine_pin": (c_int, [c_void_p, c_void_p, c_size_t]),
         "moc_expand_results": (c_int, [c_void_p, c_int, c_int64, c_void_p, c_void_p]),
         "moc_engine_solve_device": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+        "moc_engine_device_kernel_ms": (c_int, [c_void_p, c_void_p]),
         "moc_engine_stats": (c_int, [c_void_p, P(c_double)]),
         "moc_engine_search_keys": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p]),
         "moc_engine_search_keys_device": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int,
@@ -93,6 +94,8 @@ def _decl(lib):
                                                     c_int, c_void_p]),
     }
     for name, (res, args) in sig.items():
+        if os.environ.get("MOC_LIB_PATH") and not hasattr(lib, name):
+            continue  # an older build selected for an A/B run: only what it has
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args

@@ -240,6 +240,13 @@ class HipSearchEngine:
             n, ctypes.c_void_p(out_t.data_ptr()), ctypes.c_void_p(stream.cuda_stream)))
         return out_t
 
+    def device_kernel_ms(self) -> float:
+        """Device time (ms) of the last solve_device's kernels, from events around its launches (after the
+        host's per-call planning); waits for them."""
+        ms = ctypes.c_double(0.0)
+        _lib.check(_lib.lib().moc_engine_device_kernel_ms(self._h, ctypes.addressof(ms)))
+        return float(ms.value)
+
     def search_keys(self, codes: np.ndarray, offsets: np.ndarray, part: int, parts: int) -> np.ndarray:
         """Context-parallel partial search on the GPU: this engine's share (part of parts) of the batch's
         offset tiles -> packed uint64 keys per record (see :func:`search_keys_cpu`)."""
