@@ -113,15 +113,17 @@ def kfd_gpu_count(root=KFD_NODES, env=None, dri="/dev/dri"):
     return n
 
 
-def visible_gpus():
+def visible_gpus(wanted=1):
     """GPU count for the launcher, from sysfs (kfd_gpu_count): the launcher must not hold the GPU while its
-    children use it, and it does not depend on torch.cuda.device_count() staying context-free."""
+    children use it. When sysfs shows fewer than `wanted` (or nothing), torch's count (no GPU context on
+    this image) has the last word, so a render-node permission the sysfs reading gets wrong cannot
+    refuse a launch the runtime would run."""
     n = kfd_gpu_count()
-    if n is not None:
+    if n is not None and n >= wanted:
         return n
     import torch
 
-    return torch.cuda.device_count()
+    return max(n or 0, torch.cuda.device_count())
 
 
 SHM_PREFIX = "/dev/shm/moc_bench_"
@@ -210,7 +212,7 @@ def self_launch(args, argv):
     if args.dry_launch:
         print(json.dumps({"launch": cmd, "nproc": args.gpus}), flush=True)
         return 0
-    n_dev = visible_gpus()
+    n_dev = visible_gpus(args.gpus)
     if n_dev < args.gpus and not args.allow_shared_gpu:
         print(f"bench.py: --gpus {args.gpus} but only {n_dev} GPU(s) visible", file=sys.stderr, flush=True)
         return 2

@@ -222,8 +222,11 @@ class HipEngine {
   DirectKey graph_key_[kGraphs]{};
   hipGraphExec_t graph_exec_[kGraphs] = {nullptr, nullptr};
   int graph_cur_ = 0;
-  DirectKey seen_key_{};  // the last argument set launched without a graph (captured when seen again)
-  bool seen_valid_ = false;
+  // the last two argument sets launched without a graph (captured when seen again; a streaming job's ring
+  // alternates two)
+  DirectKey seen_key_[kGraphs]{};
+  bool seen_valid_[kGraphs] = {false, false};
+  int seen_next_ = 0;
   bool pending_ = false;  // a begin_wire solve is in flight (ev_a_ .. ev_b_)
   Stopwatch pending_wall_;
   EngineStats stats_;

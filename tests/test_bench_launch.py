@@ -103,7 +103,7 @@ def test_kfd_gpu_count_8gpu_node(tmp_path):
     # one visible GPU: the 8-rank launch is refused unless it is a shared-GPU rehearsal
     args = types.SimpleNamespace(gpus=8, dry_launch=False, allow_shared_gpu=False)
     orig = b.visible_gpus
-    b.visible_gpus = lambda: 1
+    b.visible_gpus = lambda wanted=1: 1
     try:
         assert b.self_launch(args, ["--gpus", "8"]) == 2
     finally:
