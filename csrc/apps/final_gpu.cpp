@@ -219,7 +219,7 @@ class GpuRankImpl final : public GpuRank {
     EngineOptions eo;
     if (opt.chunk_records > 0) eo.chunk_records = opt.chunk_records;
     if (opt.chunk_bytes > 0) eo.chunk_bytes = opt.chunk_bytes;
-    eo.preload = opt.preload_kernels;
+    eo.preload = opt.preload_kernels ? dev::kPreloadAll : 0u;
     std::string bus;  // the PCIe address of the device chosen from the topology
     if (const auto kfd = kfd_gpus(); kfd && !kfd->empty()) {
       const int id = kfd_pick(*kfd, ctx.local_rank, requested);

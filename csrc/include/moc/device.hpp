@@ -200,16 +200,31 @@ int tile16_waves_per_cu(int lds_bytes);
 // launch from each file: milliseconds inside the first timed search of a job otherwise).
 void preload_align_kernels();
 void preload_short_kernels();
-void preload_swipe_kernels();
+void preload_swipe_byte_kernels();
+void preload_swipe_p33_kernels();
 void preload_tile16_kernels();
 void preload_mfma_kernels();
-inline void preload_kernels(bool mfma = true) {
-  if (mfma) preload_mfma_kernels();  // the measured-slower MFMA variant: only when it is selected (MOC_MFMA=1)
-  preload_align_kernels();
-  preload_short_kernels();
-  preload_swipe_kernels();
-  preload_tile16_kernels();
+// Kernel files by code object, for a preload of only what a job will launch.
+enum PreloadSet : unsigned {
+  kPreloadAlign = 1,
+  kPreloadShort = 2,
+  kPreloadSwipeByte = 4,
+  kPreloadSwipeP33 = 8,
+  kPreloadTile16 = 16,
+  kPreloadMfma = 32,  // the measured-slower MFMA variant: only when it is selected (MOC_MFMA=1)
+  kPreloadAll = 31,   // all but MFMA
+};
+inline void preload_kernels(unsigned set) {
+  if (set & kPreloadMfma) preload_mfma_kernels();
+  if (set & kPreloadAlign) preload_align_kernels();
+  if (set & kPreloadShort) preload_short_kernels();
+  if (set & kPreloadSwipeByte) preload_swipe_byte_kernels();
+  if (set & kPreloadSwipeP33) preload_swipe_p33_kernels();
+  if (set & kPreloadTile16) preload_tile16_kernels();
 }
+// "all", "none", or a comma list of align, short, swipe (both letter forms), swipe8, swipe33, tile16, mfma;
+// returns -1 for a name it does not know
+int parse_preload_set(const char* s);
 
 // One-wave self-test of the DPP / shuffle primitives (192 ints, see align_kernels.hip).
 void launch_dpp_probe(int* d_out, hipStream_t stream);

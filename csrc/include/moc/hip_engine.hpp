@@ -38,9 +38,10 @@ struct EngineOptions {
   int64_t chunk_bytes = 64ll << 20;  // staged pipeline: max letter bytes per chunk
   bool allow_direct = true;          // use zero-copy streaming when the host buffers are pinned
   bool use_graphs = true;            // replay the direct path's launches as a captured hipGraph
-  // load every kernel's code object when the engine starts (on a helper thread, beside the stream set-up),
-  // not inside the first timed launch; false: each loads at its first launch (a tiny job runs one kernel)
-  bool preload = true;
+  // kernel files (dev::PreloadSet) whose code objects load when the engine starts, on a helper thread beside
+  // the stream set-up, not inside the first timed launch; the rest load at their first launch. MOC_PRELOAD
+  // (dev::parse_preload_set) overrides.
+  unsigned preload = dev::kPreloadAll;
   // Pinned host batches stream zero-copy: the kernel reads / writes host memory itself. A chunked SDMA
   // pipeline around the HBM-resident kernel was measured slower on the registered node-shared arrays the
   // headline streams from (4.4 vs 4.0 ms/step, profiles/host_stream_ab.log) and was retired in round 4.
@@ -186,6 +187,10 @@ class HipEngine {
   R2Params r2_{};                  // R2 parameters of the current solve
   void* d_image_ = nullptr;  // problem image: LUT | Seq1 | profile (views below)
   size_t d_image_cap_ = 0;
+  // page-locked staging of the image: the upload is one DMA on the compute stream (a pageable hipMemcpy
+  // costs the runtime's staging set-up, 8 ms inside a tiny job's first search on the box)
+  void* h_image_ = nullptr;
+  size_t h_image_cap_ = 0;
   std::vector<uint8_t> image_;
   Weights last_w_{};                // the last set_problem's inputs: a repeat returns at once
   std::vector<uint8_t> last_seq1_;

@@ -8,7 +8,6 @@ namespace dev {
 
 bool launch_swipe_p33(const ProblemView& pv, const ShortArgs& b, const SwipeLayout& lay, dim3 grid, dim3 block,
                       hipStream_t stream);
-void preload_swipe_p33_kernels();
 
 namespace {
 struct SwipeChoice {
@@ -67,10 +66,9 @@ bool configure_swipe(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs
   return false;
 }
 
-void preload_swipe_kernels() {
+void preload_swipe_byte_kernels() {
   hipFuncAttributes fa;
   (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&swipe_search_kernel<24, 4, 0, false>));
-  preload_swipe_p33_kernels();
 }
 
 // MOC_SWIPE_TAIL=0 keeps every tile at full size (A/B); 2, 4 (default), 8 or 16 cut the tail tiles to that

@@ -7,6 +7,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <future>
+#include <string>
 
 #include "moc/problem.hpp"
 #include "moc/runtime/hip_check.hpp"
@@ -68,6 +69,33 @@ struct HipEngine::Slot {
   bool busy = false;
 };
 
+namespace dev {
+int parse_preload_set(const char* s) {
+  static const struct {
+    const char* name;
+    unsigned set;
+  } names[] = {{"all", kPreloadAll}, {"none", 0}, {"align", kPreloadAlign}, {"short", kPreloadShort},
+               {"swipe", kPreloadSwipeByte | kPreloadSwipeP33}, {"swipe8", kPreloadSwipeByte},
+               {"swipe33", kPreloadSwipeP33}, {"tile16", kPreloadTile16}, {"mfma", kPreloadMfma}};
+  unsigned set = 0;
+  std::string list(s);
+  size_t at = 0;
+  while (at <= list.size()) {
+    const size_t end = std::min(list.find(',', at), list.size());
+    const std::string item = list.substr(at, end - at);
+    bool known = item.empty();
+    for (const auto& n : names)
+      if (item == n.name) {
+        set |= n.set;
+        known = true;
+      }
+    if (!known) return -1;
+    at = end + 1;
+  }
+  return static_cast<int>(set);
+}
+}  // namespace dev
+
 HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
   Stopwatch init_sw;
   init_sw.start();
@@ -76,14 +104,22 @@ HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
   MOC_HIP_CHECK(hipDeviceGetAttribute(&num_cus_, hipDeviceAttributeMultiprocessorCount, device_));
   const double t_dev = init_sw.total_ms();
   if (const char* m = std::getenv("MOC_MFMA")) mfma_ = std::atoi(m) != 0;
-  // code objects on the device now, not inside the first timed launch — on a helper thread, while this one
-  // sets up the compute stream and buffers (independent runtime work, ~13 and ~20 ms on the MI355X box)
-  std::future<void> preload;
-  if (opt_.preload)
-    preload = std::async(std::launch::async, [dev_id = device_, mfma = mfma_] {
-      MOC_HIP_CHECK(hipSetDevice(dev_id));
-      dev::preload_kernels(mfma);
-    });
+  unsigned set = opt_.preload;
+  if (const char* p = std::getenv("MOC_PRELOAD")) {
+    const int v = dev::parse_preload_set(p);
+    if (v < 0) throw Error(std::string("MOC_PRELOAD: unknown kernel file in '") + p + "'");
+    set = static_cast<unsigned>(v);
+  }
+  if (mfma_ && (set & dev::kPreloadTile16)) set |= dev::kPreloadMfma;
+  // code objects on the device now, not inside the first timed launch, and the image's page-locked staging
+  // — on a helper thread, while this one sets up the compute stream and buffers (independent runtime work,
+  // ~13 and ~20 ms on the MI355X box)
+  std::future<void> preload = std::async(std::launch::async, [this, set] {
+    MOC_HIP_CHECK(hipSetDevice(device_));
+    if (set) dev::preload_kernels(set);
+    MOC_HIP_CHECK(hipHostMalloc(&h_image_, size_t{64} << 10, hipHostMallocDefault));
+    h_image_cap_ = size_t{64} << 10;
+  });
   const double t_preload = init_sw.total_ms();
   if (const char* g = std::getenv("MOC_GRAPHS")) opt_.use_graphs = std::atoi(g) != 0;
   if (const char* u = std::getenv("MOC_TILE_U")) {  // tuning override of the per-batch choice
@@ -115,7 +151,7 @@ HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
   MOC_HIP_CHECK(hipEventCreate(&ev_a_));
   MOC_HIP_CHECK(hipEventCreate(&ev_b_));
   MOC_HIP_CHECK(hipEventCreateWithFlags(&ev_plan_, hipEventDisableTiming));
-  if (preload.valid()) preload.get();  // rethrows a load error
+  preload.get();  // rethrows a load error
   MOC_LOG_DEBUG("engine on device %d up in %.1f ms (device %.1f, kernel preload started %.1f, streams %.1f, buffers + preload %.1f)", device_,
                 init_sw.total_ms(), t_dev, t_preload - t_dev, t_streams - t_preload, init_sw.total_ms() - t_streams);
 }
@@ -148,6 +184,7 @@ HipEngine::~HipEngine() {
   (void)hipEventDestroy(ev_a_);
   (void)hipEventDestroy(ev_b_);
   (void)hipFree(d_image_);
+  (void)hipHostFree(h_image_);
   if (s_copy_) (void)hipStreamDestroy(s_copy_);
   (void)hipStreamDestroy(s_compute_);
   if (s_return_) (void)hipStreamDestroy(s_return_);
@@ -261,7 +298,17 @@ void HipEngine::set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, S
     MOC_HIP_CHECK(hipMalloc(&d_image_, std::max(total, size_t{64} << 10)));
     d_image_cap_ = std::max(total, size_t{64} << 10);
   }
-  MOC_HIP_CHECK(hipMemcpy(d_image_, next.data(), total, hipMemcpyHostToDevice));
+  if (total > h_image_cap_) {
+    void* old = std::exchange(h_image_, nullptr);
+    h_image_cap_ = 0;
+    MOC_HIP_CHECK(hipHostFree(old));
+    MOC_HIP_CHECK(hipHostMalloc(&h_image_, total, hipHostMallocDefault));
+    h_image_cap_ = total;
+  }
+  std::memcpy(h_image_, next.data(), total);
+  MOC_HIP_CHECK(hipMemcpyAsync(d_image_, h_image_, total, hipMemcpyHostToDevice, s_compute_));
+  // complete before any stream's kernel reads it (solve_device callers launch on streams of their own)
+  MOC_HIP_CHECK(hipStreamSynchronize(s_compute_));
   image_.swap(next);
   char* base = static_cast<char*>(d_image_);
   d_lut_ = reinterpret_cast<int32_t*>(base);

@@ -31,7 +31,7 @@ int main() {
   void* p = nullptr;
   (void)hipMalloc(&p, 256);
   lap("first hipMalloc (context)");
-  moc::dev::preload_kernels();
+  moc::dev::preload_kernels(moc::dev::kPreloadAll);
   lap("preload_kernels");
   hipDeviceProp_t prop;
   (void)hipGetDeviceProperties(&prop, 0);
