@@ -45,6 +45,11 @@ HIP_SRCS  := $(wildcard csrc/src/hip/*.hip)
 CPU_OBJS  := $(patsubst csrc/src/%.cpp,$(OBJ)/%.o,$(CPU_SRCS))
 CORE_OBJS := $(patsubst csrc/src/%.cpp,$(OBJ)/%.o,$(CORE_SRCS))
 HIP_OBJS  := $(patsubst csrc/src/%.hip,$(OBJ)/%.o,$(HIP_SRCS))
+# swipe kernel instances: one code object per (letter form, offsets per lane), from one source
+# (csrc/src/hip/swipe_group.inc) — HIP loads only the objects whose kernels a job launches
+SWIPE_GROUP := csrc/src/hip/swipe_group.inc
+SWIPE_NOFFS := 8 16 24 32 40 48 56 64
+SWIPE_OBJS  := $(foreach lf,0 2,$(foreach no,$(SWIPE_NOFFS),$(OBJ)/hip/swipe_lf$(lf)_n$(no).o))
 COMM_OBJS := $(OBJ)/comm/comm.o $(OBJ)/comm/mpi_device_comm.o
 RCCL_OBJS := $(OBJ)/comm/rccl_comm.o
 HEADERS   := $(shell find csrc/include -name '*.h' -o -name '*.hpp')
@@ -64,7 +69,15 @@ $(OBJ)/%.o: csrc/src/%.hip $(HEADERS) $(wildcard csrc/src/hip/*.hpp)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(PKG_LIB): $(CORE_OBJS) $(HIP_OBJS)
+$(OBJ)/hip/swipe_lf0_n%.o: $(SWIPE_GROUP) $(HEADERS) $(wildcard csrc/src/hip/*.hpp)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -DMOC_SWIPE_LF=0 -DMOC_SWIPE_NO=$* -x hip -c $< -o $@
+
+$(OBJ)/hip/swipe_lf2_n%.o: $(SWIPE_GROUP) $(HEADERS) $(wildcard csrc/src/hip/*.hpp)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -DMOC_SWIPE_LF=2 -DMOC_SWIPE_NO=$* -x hip -c $< -o $@
+
+$(PKG_LIB): $(CORE_OBJS) $(HIP_OBJS) $(SWIPE_OBJS)
 	@mkdir -p $(dir $@)
 	$(CXX) -shared -fopenmp -o $@ $^ $(LDROCM) -ldl
 
@@ -143,6 +156,10 @@ debug-kernels:
 	for f in $(HIP_SRCS); do \
 	  $(HIPCC) $(HIPFLAGS) -DMOC_DEBUG_KERNELS -c $$f -o $(BUILD)/debug/$$(basename $$f .hip).hip.o || exit 1; \
 	done
+	for lf in 0 2; do for no in $(SWIPE_NOFFS); do \
+	  $(HIPCC) $(HIPFLAGS) -DMOC_DEBUG_KERNELS -DMOC_SWIPE_LF=$$lf -DMOC_SWIPE_NO=$$no -x hip -c $(SWIPE_GROUP) \
+	    -o $(BUILD)/debug/swipe_lf$${lf}_n$${no}.hip.o || exit 1; \
+	done; done
 	$(CXX) -shared -fopenmp -o $(BUILD)/debug/libmoc.so $(CORE_OBJS) $(BUILD)/debug/*.hip.o $(LDROCM) -ldl
 
 # Kernel A/B builds: make variant NAME=p4 VDEFS="-DMOC_T16_PREFETCH=4" -> build/variant_p4/libmoc.so
@@ -152,6 +169,10 @@ variant: lib
 	for f in $(HIP_SRCS); do \
 	  $(HIPCC) $(HIPFLAGS) $(VDEFS) -c $$f -o $(BUILD)/variant_$(NAME)/$$(basename $$f .hip).hip.o || exit 1; \
 	done
+	for lf in 0 2; do for no in $(SWIPE_NOFFS); do \
+	  $(HIPCC) $(HIPFLAGS) $(VDEFS) -DMOC_SWIPE_LF=$$lf -DMOC_SWIPE_NO=$$no -x hip -c $(SWIPE_GROUP) \
+	    -o $(BUILD)/variant_$(NAME)/swipe_lf$${lf}_n$${no}.hip.o || exit 1; \
+	done; done
 	$(CXX) -shared -fopenmp -o $(BUILD)/variant_$(NAME)/libmoc.so $(CORE_OBJS) $(BUILD)/variant_$(NAME)/*.hip.o $(LDROCM) -ldl
 
 clean:

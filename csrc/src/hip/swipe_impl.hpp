@@ -27,9 +27,9 @@
 // runs: Pf = Dt, the running sums are D_o(k) themselves, B2 keeps max_k D_o(k), and after the selection
 // each lane whose winner is a mutant re-walks that one diagonal for the first k reaching the best D.
 //
-// This header holds the kernel template; swipe_kernels.hip (byte letters: device-resident batches) and
-// swipe_p33.hip (P33 letters: host streams) instantiate one letter form each, so the two compile in
-// parallel, and swipe_kernels.hip also holds the host-side configuration and launch.
+// This header holds the kernel template; swipe_group.inc instantiates it, one code object per letter form
+// (bytes: device-resident batches, P33: host streams) and offsets per lane, and swipe_kernels.hip holds the
+// host-side configuration, dispatch and launch.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -434,36 +434,43 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
 }
 
 
-// Launches the instance of letter form LF that `a` selects (a.slot = offsets per lane, a.rpw = record
-// words, a.swipe_rk = RK); false when no instance matches.
-template <int LF>
-bool launch_swipe_form(const ProblemView& pv, const ShortArgs& b, const SwipeLayout& lay, dim3 grid, dim3 block,
+// Launches the instance of letter form LF with NO offsets per lane that `b` selects (b.rpw = record words,
+// b.swipe_rk = RK); false when no instance matches.
+template <int NO, int LF>
+bool launch_swipe_noff(const ProblemView& pv, const ShortArgs& b, const SwipeLayout& lay, dim3 grid, dim3 block,
                        hipStream_t stream) {
-  const int noff = b.slot, l2w = b.rpw;
+  const int l2w = b.rpw;
   const bool rk = b.swipe_rk != 0;
-#define MOC_SWIPE_CASE(NO, LW, RKV)                                                                        \
-  if (noff == NO && l2w == LW && rk == RKV) {                                                            \
+#define MOC_SWIPE_CASE(LW, RKV)                                                                            \
+  if (l2w == LW && rk == RKV) {                                                                          \
     hipLaunchKernelGGL((swipe_search_kernel<NO, LW, LF, RKV>), grid, block, lay.total, stream, pv, b, lay); \
     return true;                                                                                         \
   }
-#define MOC_SWIPE_NOFF(LW, RKV)                                                                            \
-  MOC_SWIPE_CASE(8, LW, RKV)                                                                             \
-  MOC_SWIPE_CASE(16, LW, RKV)                                                                            \
-  MOC_SWIPE_CASE(24, LW, RKV)                                                                            \
-  MOC_SWIPE_CASE(32, LW, RKV)                                                                            \
-  MOC_SWIPE_CASE(40, LW, RKV)                                                                            \
-  MOC_SWIPE_CASE(48, LW, RKV)                                                                            \
-  MOC_SWIPE_CASE(56, LW, RKV)                                                                            \
-  MOC_SWIPE_CASE(64, LW, RKV)
-  MOC_SWIPE_NOFF(4, false)
-  MOC_SWIPE_NOFF(8, false)
-  MOC_SWIPE_NOFF(4, true)
-  MOC_SWIPE_NOFF(8, true)
-  MOC_SWIPE_NOFF(16, true)  // records of 33..64 letters run the RK form only (configure_swipe)
-#undef MOC_SWIPE_NOFF
+  MOC_SWIPE_CASE(4, false)
+  MOC_SWIPE_CASE(8, false)
+  MOC_SWIPE_CASE(4, true)
+  MOC_SWIPE_CASE(8, true)
+  MOC_SWIPE_CASE(16, true)  // records of 33..64 letters run the RK form only (configure_swipe)
 #undef MOC_SWIPE_CASE
   return false;
 }
+
+// The instances live in one code object per (letter form, NOFF): swipe_group.inc, compiled once per pair by
+// the Makefile and CMakeLists.txt. HIP loads a code object at the first launch of any kernel in it, so a
+// job that runs one instance loads ~1/8 of a letter form's kernels (a 2 MB object of 40 kernels took
+// 3.4 ms inside a tiny job's first launch on the box, profiles/hip_wall_trace_r4/).
+#define MOC_SWIPE_FN_(LF, NO) launch_swipe_lf##LF##_n##NO
+#define MOC_SWIPE_FN(LF, NO) MOC_SWIPE_FN_(LF, NO)
+#define MOC_SWIPE_PRELOAD_FN_(LF, NO) preload_swipe_lf##LF##_n##NO
+#define MOC_SWIPE_PRELOAD_FN(LF, NO) MOC_SWIPE_PRELOAD_FN_(LF, NO)
+#define MOC_SWIPE_FOR_NOFF(X, LF) X(LF, 8) X(LF, 16) X(LF, 24) X(LF, 32) X(LF, 40) X(LF, 48) X(LF, 56) X(LF, 64)
+#define MOC_SWIPE_DECLARE(LF, NO)                                                                            \
+  bool MOC_SWIPE_FN(LF, NO)(const ProblemView& pv, const ShortArgs& b, const SwipeLayout& lay, dim3 grid,    \
+                            dim3 block, hipStream_t stream);                                                 \
+  void MOC_SWIPE_PRELOAD_FN(LF, NO)();
+MOC_SWIPE_FOR_NOFF(MOC_SWIPE_DECLARE, 0)
+MOC_SWIPE_FOR_NOFF(MOC_SWIPE_DECLARE, 2)
+#undef MOC_SWIPE_DECLARE
 
 }  // namespace dev
 }  // namespace moc

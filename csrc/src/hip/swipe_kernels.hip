@@ -1,13 +1,10 @@
-// Inter-record swipe kernel: host-side configuration and launch, and the byte-letter instances
-// (device-resident batches). The kernel template and its derivation are in swipe_impl.hpp; the P33 instances
-// (host streams) in swipe_p33.hip.
+// Inter-record swipe kernel: host-side configuration, dispatch and launch. The kernel template and its
+// derivation are in swipe_impl.hpp; its instances in one code object per (letter form, NOFF),
+// swipe_group.inc.
 #include "swipe_impl.hpp"
 
 namespace moc {
 namespace dev {
-
-bool launch_swipe_p33(const ProblemView& pv, const ShortArgs& b, const SwipeLayout& lay, dim3 grid, dim3 block,
-                      hipStream_t stream);
 
 namespace {
 struct SwipeChoice {
@@ -66,10 +63,23 @@ bool configure_swipe(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs
   return false;
 }
 
-void preload_swipe_byte_kernels() {
-  hipFuncAttributes fa;
-  (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&swipe_search_kernel<24, 4, 0, false>));
+#define MOC_SWIPE_PRELOAD_CALL(LF, NO) MOC_SWIPE_PRELOAD_FN(LF, NO)();
+void preload_swipe_byte_kernels() { MOC_SWIPE_FOR_NOFF(MOC_SWIPE_PRELOAD_CALL, 0) }
+void preload_swipe_p33_kernels() { MOC_SWIPE_FOR_NOFF(MOC_SWIPE_PRELOAD_CALL, 2) }
+#undef MOC_SWIPE_PRELOAD_CALL
+
+namespace {
+// the instance's code object by letter form (0 bytes, 2 P33) and offsets per lane (a.slot)
+bool launch_swipe_instance(int lf, const ProblemView& pv, const ShortArgs& b, const SwipeLayout& lay, dim3 grid,
+                           dim3 block, hipStream_t stream) {
+#define MOC_SWIPE_GROUP_CASE(LF, NO) \
+  if (lf == LF && b.slot == NO) return MOC_SWIPE_FN(LF, NO)(pv, b, lay, grid, block, stream);
+  MOC_SWIPE_FOR_NOFF(MOC_SWIPE_GROUP_CASE, 0)
+  MOC_SWIPE_FOR_NOFF(MOC_SWIPE_GROUP_CASE, 2)
+#undef MOC_SWIPE_GROUP_CASE
+  return false;
 }
+}  // namespace
 
 // MOC_SWIPE_TAIL=0 keeps every tile at full size (A/B); 2, 4 (default), 8 or 16 cut the tail tiles to that
 // fraction of a tile. Powers of two only: tiles stay multiples of 64 records (sparse-offset boundaries).
@@ -108,8 +118,7 @@ void launch_swipe(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStr
       b.tail_records ? b.tail_from + (b.n - big_end + b.tail_records - 1) / b.tail_records : n_big;
   const int64_t blocks = std::min<int64_t>(n_tiles, slots);
   const dim3 grid(static_cast<unsigned>(std::max<int64_t>(blocks, 1))), block(kBlock);
-  const bool ok = a.packed33 ? launch_swipe_p33(pv, b, lay, grid, block, stream)
-                             : launch_swipe_form<0>(pv, b, lay, grid, block, stream);
+  const bool ok = launch_swipe_instance(letter_form(a), pv, b, lay, grid, block, stream);
   if (!ok) throw Error("launch_swipe: no instance for this configuration");
 }
 

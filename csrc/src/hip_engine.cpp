@@ -820,7 +820,12 @@ void HipEngine::launch_direct(const dev::ProblemView& pv, const dev::ShortArgs& 
 
 void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t n, void* out, ResultFormat fmt,
                            bool packed5) {
-  ensure_side_streams();
+  // a batch of one chunk has nothing to overlap: its copies go on the compute stream, and a job that only
+  // ever runs such batches (every tiny --backend=hip job) never pays the two side streams' hardware queues
+  // (~10-20 ms each to set up on the MI355X box)
+  const bool one_chunk = n <= opt_.chunk_records && offsets[n] - offsets[0] <= opt_.chunk_bytes;
+  if (!one_chunk) ensure_side_streams();
+  hipStream_t s_in = one_chunk ? s_compute_ : s_copy_, s_back = one_chunk ? s_compute_ : s_return_;
   const int fb = result_bytes(fmt);
   ChunkPlan cp;
   double kernel_ms = 0;
@@ -882,14 +887,14 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
     if (packed5) {
       letter_bytes = static_cast<size_t>(pb1 - pb0);
       if (cbytes)
-        copy_h2d(s.d_packed, codes + pb0, letter_bytes, s_copy_);
+        copy_h2d(s.d_packed, codes + pb0, letter_bytes, s_in);
     } else if (cbytes) {
-      copy_h2d(s.d_codes, codes + offsets[rb], cbytes, s_copy_);
+      copy_h2d(s.d_codes, codes + offsets[rb], cbytes, s_in);
     }
-    copy_h2d(s.d_offsets, offsets + rb, sizeof(int64_t) * (cn + 1), s_copy_);
+    copy_h2d(s.d_offsets, offsets + rb, sizeof(int64_t) * (cn + 1), s_in);
     if (!starts.empty())
-      MOC_HIP_CHECK(hipMemcpyAsync(s.d_plan, s.h_plan, lay.upload_bytes, hipMemcpyHostToDevice, s_copy_));
-    MOC_HIP_CHECK(hipEventRecord(s.ev_h2d, s_copy_));
+      MOC_HIP_CHECK(hipMemcpyAsync(s.d_plan, s.h_plan, lay.upload_bytes, hipMemcpyHostToDevice, s_in));
+    MOC_HIP_CHECK(hipEventRecord(s.ev_h2d, s_in));
     stats_.h2d_bytes += static_cast<int64_t>(letter_bytes + sizeof(int64_t) * (cn + 1) + lay.upload_bytes);
     // ---- compute stream
     MOC_HIP_CHECK(hipStreamWaitEvent(s_compute_, s.ev_h2d, 0));
@@ -929,9 +934,9 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
     MOC_HIP_CHECK(hipGetLastError());
     MOC_HIP_CHECK(hipEventRecord(s.ev_k1, s_compute_));
     // ---- return stream: D2H straight into the caller's result array
-    MOC_HIP_CHECK(hipStreamWaitEvent(s_return_, s.ev_k1, 0));
-    copy_d2h(static_cast<char*>(out) + rb * fb, s.d_out, static_cast<size_t>(fb) * cn, s_return_);
-    MOC_HIP_CHECK(hipEventRecord(s.ev_done, s_return_));
+    MOC_HIP_CHECK(hipStreamWaitEvent(s_back, s.ev_k1, 0));
+    copy_d2h(static_cast<char*>(out) + rb * fb, s.d_out, static_cast<size_t>(fb) * cn, s_back);
+    MOC_HIP_CHECK(hipEventRecord(s.ev_done, s_back));
     stats_.d2h_bytes += static_cast<int64_t>(fb) * cn;
     s.busy = true;
     rb = re;

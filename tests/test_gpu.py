@@ -904,3 +904,32 @@ print("ok")
     env = dict(os.environ, MOC_SWIPE_TILE="512" if tail == "8" else "256", MOC_SWIPE_SLOTS="16", MOC_SWIPE_TAIL=tail)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, timeout=300, env=env)
     assert r.returncode == 0 and b"ok" in r.stdout, r.stderr.decode()[-3000:]
+
+
+@pytest.mark.parametrize("preload", ["none", "swipe33", "tile16,short", "all"])
+def test_preload_sets(monkeypatch, preload):
+    # MOC_PRELOAD picks which code objects load at engine start; the rest load at their first launch — the
+    # results must not depend on it (input6: swipe P33 / bytes, input3: tile16)
+    monkeypatch.setenv("MOC_PRELOAD", preload)
+    eng = HipSearchEngine(device=0)
+    for shape, n in (("input6", 5_000), ("input3", 40)):
+        check(eng, make_synthetic(shape, n, seed=41))
+    eng.close()
+
+
+def test_preload_set_unknown_name(monkeypatch):
+    from mpi_openmp_cuda_amd._lib import NativeError
+
+    monkeypatch.setenv("MOC_PRELOAD", "swipe33,nosuchfile")
+    with pytest.raises(NativeError, match="MOC_PRELOAD"):
+        HipSearchEngine(device=0)
+
+
+def test_problem_image_staging_grows():
+    # the problem image uploads through a page-locked staging buffer that starts at 64 KiB: a long Seq1
+    # (input4: 2976 letters, a ~150 KB tile16 profile) grows it, and alternating problems re-upload each time
+    eng = HipSearchEngine(device=0)
+    small, big = make_synthetic("input6", 3_000, seed=43), make_synthetic("input4", 300, seed=44)
+    for prob in (small, big, small, big):
+        check(eng, prob)
+    eng.close()
