@@ -154,12 +154,15 @@ def cleanup_stale_shm(before=None, prefix=SHM_PREFIX):
     return removed
 
 
-def final_input6_wall(np_, reps=5, timeout=20, extra=()):
+def final_input6_wall(np_, reps=5, timeout=20, extra=(), spacing=0.0):
     """The BASELINE metric's wall-clock half: the reference's own invocation `mpiexec -np N ./final <
     input6.txt` (default flags; /root/reference/makefile:10-11) with N = this run's GPU count, median of
     `reps` runs, every output compared with the golden. None when ./final or mpiexec is missing.
     `extra` adds flags: ("--backend=hip",) times the same job forced onto the MI355X (the default engine
-    choice runs a job this small on the OpenMP engine: 1 ms of CPU work against the GPU runtime's start)."""
+    choice runs a job this small on the OpenMP engine: 1 ms of CPU work against the GPU runtime's start).
+    `spacing` seconds pass between launches: a GPU process started right after another one waits in the
+    kernel driver for the previous one's teardown (139-208 ms instead of 52-74 ms for the runtime's start,
+    profiles/hip_init_trace_b2b.log), which a single invocation on an idle GPU does not."""
     final = os.path.join(ROOT, "final")
     inp = os.path.join(ROOT, "tests", "data", "input6.txt")
     gold = os.path.join(ROOT, "tests", "data", "expected", "input6.out")
@@ -172,7 +175,9 @@ def final_input6_wall(np_, reps=5, timeout=20, extra=()):
     env = {k: v for k, v in os.environ.items()
            if not k.startswith(("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_", "ROLE_", "TORCHELASTIC",
                                 "MASTER_"))}
-    for _ in range(reps):
+    for i in range(reps):
+        if i and spacing:
+            time.sleep(spacing)
         with open(inp, "rb") as fin:
             t0 = time.perf_counter()
             try:
@@ -184,7 +189,10 @@ def final_input6_wall(np_, reps=5, timeout=20, extra=()):
         ok = ok and r.returncode == 0 and r.stdout == want
         if not ok:  # a failing launcher or binary: report it once instead of retrying
             break
-    return {"wall_s": round(float(np.median(walls)), 4), "best_s": round(min(walls), 4), "ok": bool(ok), "np": np_}
+    out = {"wall_s": round(float(np.median(walls)), 4), "best_s": round(min(walls), 4), "ok": bool(ok), "np": np_}
+    if spacing:
+        out["spacing_s"] = spacing
+    return out
 
 
 def pci_bus_id(code):
@@ -468,7 +476,8 @@ def main():
     # the literal wall-clock of the reference invocation on input6.txt at this rank count (rank 0, untimed,
     # after the steps; the other ranks wait at the barrier below)
     wall6 = final_input6_wall(world) if (rank == 0 and args.final_wall) else None
-    wall6_hip = final_input6_wall(world, extra=("--backend=hip",)) if (rank == 0 and args.final_wall) else None
+    wall6_hip = (final_input6_wall(world, extra=("--backend=hip",), spacing=1.0)
+                 if (rank == 0 and args.final_wall) else None)
     ms_per_step = elapsed / args.steps * 1e3
     value = total_elems * args.steps / elapsed
     cells_per_rec = float(np.mean([(shape.L1 - l + 1) * l for l in range(shape.l2_min, shape.l2_max + 1)]))

@@ -154,6 +154,14 @@ struct ShortArgs {
   int64_t dbg_codes_end = -1;         // debug builds: end of the readable letter bytes (from `codes`)
 };
 
+// Copies `bytes` from src to dst on a kernel (copy_kernels.hip); either side may be page-locked host memory
+// given by its device address. For small transfers only (kernel_copy_fits): the runtime's SDMA path costs
+// 11-34 ms at its first use in a process, this one ~0.3 ms.
+constexpr size_t kKernelCopyMaxAligned = size_t{8} << 20;
+constexpr size_t kKernelCopyMaxBytes = size_t{1} << 20;
+void launch_copy(void* dst, const void* src, size_t bytes, hipStream_t stream);
+bool kernel_copy_fits(const void* dst, const void* src, size_t bytes);
+
 // Unpacks n chars of a 5-bit packed stream (device memory) starting at bit `bit0` into byte codes.
 void launch_unpack5(const uint8_t* packed, int64_t bit0, int64_t n, uint8_t* out, hipStream_t stream);
 

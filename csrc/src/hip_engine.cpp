@@ -27,17 +27,39 @@ int32_t choose_key_shift(int32_t max_abs_weight, int64_t max_l2) {
 }
 
 namespace {
-// hipMemcpyAsync between device memory and a caller's host range, one copy per piece of the range that
-// lies within a single page-locked registration (or outside all): see pinned::segments.
+// Copies between device memory and a caller's host range, one per piece of the range that lies within a
+// single page-locked registration (or outside all): see pinned::segments. A small registered piece moves on
+// a copy kernel through its device address (dev::launch_copy: no SDMA start-up inside a short job), the
+// rest with hipMemcpyAsync.
 void copy_h2d(void* dst, const void* src, size_t bytes, hipStream_t s) {
-  for (const auto& seg : pinned::segments(src, bytes))
-    MOC_HIP_CHECK(hipMemcpyAsync(static_cast<char*>(dst) + seg.first, static_cast<const char*>(src) + seg.first,
-                                 seg.second, hipMemcpyHostToDevice, s));
+  for (const auto& seg : pinned::segments(src, bytes)) {
+    char* d = static_cast<char*>(dst) + seg.first;
+    const char* h = static_cast<const char*>(src) + seg.first;
+    const void* hd = nullptr;
+    if (dev::kernel_copy_fits(d, h, seg.second) && (hd = pinned::device_address(h, seg.second)))
+      dev::launch_copy(d, hd, seg.second, s);
+    else
+      MOC_HIP_CHECK(hipMemcpyAsync(d, h, seg.second, hipMemcpyHostToDevice, s));
+  }
 }
 void copy_d2h(void* dst, const void* src, size_t bytes, hipStream_t s) {
-  for (const auto& seg : pinned::segments(dst, bytes))
-    MOC_HIP_CHECK(hipMemcpyAsync(static_cast<char*>(dst) + seg.first, static_cast<const char*>(src) + seg.first,
-                                 seg.second, hipMemcpyDeviceToHost, s));
+  for (const auto& seg : pinned::segments(dst, bytes)) {
+    char* h = static_cast<char*>(dst) + seg.first;
+    const char* d = static_cast<const char*>(src) + seg.first;
+    const void* hd = nullptr;
+    if (dev::kernel_copy_fits(h, d, seg.second) && (hd = pinned::device_address(h, seg.second)))
+      dev::launch_copy(const_cast<void*>(hd), d, seg.second, s);
+    else
+      MOC_HIP_CHECK(hipMemcpyAsync(h, d, seg.second, hipMemcpyDeviceToHost, s));
+  }
+}
+// host -> device from a hipHostMalloc allocation of the engine's own (h_image_, plan staging)
+void upload_staged(void* dst, const void* h, size_t bytes, hipStream_t s) {
+  void* hd = nullptr;
+  if (dev::kernel_copy_fits(dst, h, bytes) && hipHostGetDevicePointer(&hd, const_cast<void*>(h), 0) == hipSuccess && hd)
+    dev::launch_copy(dst, hd, bytes, s);
+  else
+    MOC_HIP_CHECK(hipMemcpyAsync(dst, h, bytes, hipMemcpyHostToDevice, s));
 }
 
 // True when every byte of [p, p+bytes) is page-locked through the registry (moc/runtime/pinned.hpp);
@@ -117,8 +139,8 @@ HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
   std::future<void> preload = std::async(std::launch::async, [this, set] {
     MOC_HIP_CHECK(hipSetDevice(device_));
     if (set) dev::preload_kernels(set);
-    MOC_HIP_CHECK(hipHostMalloc(&h_image_, size_t{64} << 10, hipHostMallocDefault));
-    h_image_cap_ = size_t{64} << 10;
+    MOC_HIP_CHECK(hipHostMalloc(&h_image_, size_t{256} << 10, hipHostMallocDefault));  // Seq1 up to ~5000 letters
+    h_image_cap_ = size_t{256} << 10;
   });
   const double t_preload = init_sw.total_ms();
   if (const char* g = std::getenv("MOC_GRAPHS")) opt_.use_graphs = std::atoi(g) != 0;
@@ -306,7 +328,7 @@ void HipEngine::set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, S
     h_image_cap_ = total;
   }
   std::memcpy(h_image_, next.data(), total);
-  MOC_HIP_CHECK(hipMemcpyAsync(d_image_, h_image_, total, hipMemcpyHostToDevice, s_compute_));
+  upload_staged(d_image_, h_image_, total, s_compute_);
   // complete before any stream's kernel reads it (solve_device callers launch on streams of their own)
   MOC_HIP_CHECK(hipStreamSynchronize(s_compute_));
   image_.swap(next);
@@ -893,7 +915,7 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
     }
     copy_h2d(s.d_offsets, offsets + rb, sizeof(int64_t) * (cn + 1), s_in);
     if (!starts.empty())
-      MOC_HIP_CHECK(hipMemcpyAsync(s.d_plan, s.h_plan, lay.upload_bytes, hipMemcpyHostToDevice, s_in));
+      upload_staged(s.d_plan, s.h_plan, lay.upload_bytes, s_in);
     MOC_HIP_CHECK(hipEventRecord(s.ev_h2d, s_in));
     stats_.h2d_bytes += static_cast<int64_t>(letter_bytes + sizeof(int64_t) * (cn + 1) + lay.upload_bytes);
     // ---- compute stream
@@ -983,7 +1005,7 @@ void HipEngine::solve_device(const uint8_t* d_codes, const int64_t* d_offsets, c
     std::memcpy(static_cast<char*>(h_plan_) + lay.starts_off, starts.data(), starts.size() * sizeof(dev::WaveStart));
     if (lrecs)
       std::memcpy(static_cast<char*>(h_plan_) + lay.long_off, lrecs, static_cast<size_t>(n_long) * sizeof(int32_t));
-    MOC_HIP_CHECK(hipMemcpyAsync(d_plan_, h_plan_, lay.upload_bytes, hipMemcpyHostToDevice, stream));
+    upload_staged(d_plan_, h_plan_, lay.upload_bytes, stream);
   }
   const dev::ProblemView pv = problem_view(cp.max_l2);
   if (!ev_d0_) {
@@ -1041,8 +1063,7 @@ void HipEngine::search_keys_device(const uint8_t* d_codes, const int64_t* d_offs
   ensure_host(h_plan_, h_plan_cap_, bytes);
   if (!starts.empty()) {
     std::memcpy(h_plan_, starts.data(), starts.size() * sizeof(dev::WaveStart));
-    MOC_HIP_CHECK(hipMemcpyAsync(d_plan_, h_plan_, starts.size() * sizeof(dev::WaveStart), hipMemcpyHostToDevice,
-                                 stream));
+    upload_staged(d_plan_, h_plan_, starts.size() * sizeof(dev::WaveStart), stream);
   }
   dev::Plan plan;
   plan.u = tp.u;

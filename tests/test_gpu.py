@@ -926,10 +926,40 @@ def test_preload_set_unknown_name(monkeypatch):
 
 
 def test_problem_image_staging_grows():
-    # the problem image uploads through a page-locked staging buffer that starts at 64 KiB: a long Seq1
-    # (input4: 2976 letters, a ~150 KB tile16 profile) grows it, and alternating problems re-upload each time
+    # the problem image uploads through a page-locked staging buffer that starts at 256 KiB: a long Seq1
+    # (20000 letters, a ~1 MB tile16 image in device memory) grows it, and alternating problems re-upload
     eng = HipSearchEngine(device=0)
-    small, big = make_synthetic("input6", 3_000, seed=43), make_synthetic("input4", 300, seed=44)
+    small = make_synthetic("input6", 3_000, seed=43)
+    rng = np.random.default_rng(44)
+    seq1 = rng.integers(1, 27, 20_000).astype(np.uint8)
+    lens = rng.integers(50, 400, 64)
+    offsets = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    big = Problem((5, 2, 3, 4), seq1, rng.integers(1, 27, int(offsets[-1])).astype(np.uint8), offsets)
     for prob in (small, big, small, big):
         check(eng, prob)
+    eng.close()
+
+
+@pytest.mark.parametrize("n,shift", [(150, 0), (150, 1), (150, 7), (2500, 3)])
+def test_staged_pinned_kernel_copies(n, shift):
+    # pinned batches through the staged pipeline (long records: tile16) move their small pieces on the copy
+    # kernel (dev::launch_copy) instead of the runtime's SDMA path: letters at a 1..15-byte misalignment take
+    # its byte loop, aligned offsets / results its 16-byte loop; 2500 input4 records (~100 KB of letters at
+    # shift 3: byte loop) and 150 (~6 KB); the results must match the CPU engine either way
+    from mpi_openmp_cuda_amd import _lib
+
+    prob = make_synthetic("input4", n, seed=50 + shift)
+    raw = np.zeros(prob.codes.nbytes + 64, np.uint8)
+    base = (-raw.ctypes.data) % 16 + shift
+    codes = raw[base: base + prob.codes.nbytes]
+    codes[:] = prob.codes
+    assert codes.ctypes.data % 16 == shift % 16
+    offs = prob.offsets.copy()
+    out = np.zeros(n, _lib.FORMAT_DTYPES[_lib.FORMAT_NAMES.index("r12")])
+    eng = HipSearchEngine(device=0)
+    eng.set_problem(prob.weights, prob.seq1)
+    eng.pin(raw, offs, out)
+    eng.solve(codes, offs, out=out)
+    assert eng.stats()["direct"] == 0
+    assert np.array_equal(as_triples(out), as_triples(search_cpu(prob)))
     eng.close()
