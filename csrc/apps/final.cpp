@@ -37,6 +37,7 @@
 
 #include "job.hpp"
 #include "moc/runtime/host_region.hpp"
+#include "moc/runtime/kfd_topology.hpp"
 #include "moc/runtime/log.hpp"
 
 using namespace moc;
@@ -92,6 +93,7 @@ double ms_since_process_start() {
   return ts.tv_sec * 1e3 + ts.tv_nsec / 1e6 - start;
 }
 std::atomic<double> g_runtime_up_ms{-1};  // set by the prewarm thread once the HIP runtime answered
+std::string g_gpu_isolation;  // set by isolate_gpu before MPI_Init: the one GPU this rank's runtime sees
 
 const char* kUsage =
     "usage: mpiexec -np N ./final [options] < input.txt\n"
@@ -117,6 +119,8 @@ const char* kUsage =
     "  --timing                    per-phase JSON on stderr (root)\n"
     "  --timing-exit               a last stderr line: the teardown after the job (engine, MPI_Finalize,\n"
     "                              releaser) and the time since the process started\n"
+    "  --gpu-isolate=auto|0|1      a rank taking its GPU by node-local rank shows the HIP runtime that GPU only\n"
+    "                              (auto: several GPUs on the node, no --device/--device-map, no RCCL)\n"
     "  --quick-exit=0|1            1 (default): end with _Exit once outputs are closed and MPI is finalized,\n"
     "                              leaving the runtimes' static teardown to the kernel\n"
     "  --strict-limits             enforce |Seq1|<=3000, |Seq2|<=2000 (PDF p.5-6)\n"
@@ -136,7 +140,7 @@ const std::vector<std::string> kKnown = {
     "backend", "collectives", "parallel-print", "gpu-min-cells", "gpu-prewarm-bytes", "transport", "semantics",
     "partition", "batch-records", "batch-chars", "skip-records", "input", "output", "timing", "strict-limits",
     "max-l1", "max-l2", "device", "device-map", "pin-window", "chunk-records", "chunk-bytes", "threads",
-    "log-level", "inject-fault", "mpi-topology", "timing-exit", "quick-exit", "help"};
+    "log-level", "inject-fault", "mpi-topology", "timing-exit", "quick-exit", "gpu-isolate", "help"};
 
 struct BatchHeader {
   int64_t n;
@@ -273,6 +277,8 @@ int Job::run() {
   const Flags& flags = job_.flags;
   PhaseTimer& pt = job_.pt;
   log_set_level(flags.get("log-level", "warn"));
+  log_set_rank(ctx.rank);
+  if (!g_gpu_isolation.empty()) MOC_LOG_INFO("runtime isolated to %s", g_gpu_isolation.c_str());
   {
     std::string f = flags.get("inject-fault", "");
     auto colon = f.find(':');
@@ -587,6 +593,46 @@ std::future<void> early_prewarm(int argc, char** argv) {
   }
 }
 
+// --gpu-isolate=auto|0|1: a GPU rank that takes its device by node-local rank lets the HIP runtime see that
+// one GPU (ROCR_VISIBLE_DEVICES = its index among the GPUs the driver gives the process; HIP_/CUDA_
+// VISIBLE_DEVICES and GPU_DEVICE_ORDINAL, when set, become 0): on an 8-GPU node each rank's runtime would
+// otherwise start all 8 devices, 8 processes at once. auto isolates when the node shows more than one GPU,
+// no --device / --device-map names one, the launcher exported the node-local rank, and the job uses no
+// RCCL (its peer-to-peer transport maps the peers' GPUs); 1 isolates whenever the topology answers (tests).
+// Runs before any thread starts (setenv); what it did goes to g_gpu_isolation, for the rank's log.
+void isolate_gpu(int argc, char** argv) {
+  try {
+    Flags flags(argc, argv);
+    const std::string mode = to_lower(flags.get("gpu-isolate", "auto"));
+    if (mode == "0" || to_lower(flags.get("backend", "auto")) == "cpu" || flags.get_bool("help", false)) return;
+    if (flags.get_int("device", -1) >= 0 || !flags.get("device-map", "").empty()) return;
+    const char* local_env = std::getenv("MPI_LOCALRANKID");
+    if (!local_env) local_env = std::getenv("OMPI_COMM_WORLD_LOCAL_RANK");
+    const int world = env_int("PMI_SIZE", env_int("OMPI_COMM_WORLD_SIZE", 1));
+    if (!local_env && world > 1) return;  // the node-local rank is only known after MPI_Init
+    const int local = local_env ? std::atoi(local_env) : 0;
+    const int local_n = env_int("MPI_LOCALNRANKS", env_int("OMPI_COMM_WORLD_LOCAL_SIZE", 1));
+    const std::string tr = to_lower(flags.get("transport", "auto"));
+    if (tr == "rccl" || to_lower(flags.get("collectives", "auto")) == "rccl" || (tr == "auto" && world > local_n))
+      return;
+    KfdPaths raw_paths;
+    raw_paths.honour_visible_env = false;
+    const auto all = kfd_gpus(raw_paths);
+    const auto visible = kfd_gpus();
+    if (!all || !visible || visible->empty() || (mode == "auto" && visible->size() < 2)) return;
+    const int idx = kfd_isolation_index(*all, *visible, local);
+    if (idx < 0) return;
+    setenv("ROCR_VISIBLE_DEVICES", std::to_string(idx).c_str(), 1);
+    for (const char* v : {"HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL"})
+      if (std::getenv(v)) setenv(v, "0", 1);
+    const KfdGpu& g = (*all)[static_cast<size_t>(idx)];
+    g_gpu_isolation = "gpu " + g.pci_bus_id + " (ROCR_VISIBLE_DEVICES=" + std::to_string(idx) + " of " +
+                      std::to_string(visible->size()) + " visible)";
+  } catch (const std::exception&) {
+    // bad flags are reported after MPI_Init
+  }
+}
+
 // --mpi-topology, read before MPI_Init (and before any helper thread: setenv)
 void prepare_mpi(int argc, char** argv) {
   bool lean = true;
@@ -664,6 +710,7 @@ bool quick_exit_enabled(bool flag) {
 
 int main(int argc, char** argv) {
   prepare_mpi(argc, argv);
+  isolate_gpu(argc, argv);
   ExitClock exit_clock;  // destroyed last
   // declared before the MPI context: its queued unmaps overlap the job's teardown and MPI_Finalize
   BackgroundReleaser releaser;

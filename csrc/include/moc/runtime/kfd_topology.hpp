@@ -40,6 +40,12 @@ std::optional<std::vector<KfdGpu>> kfd_gpus(const KfdPaths& paths = KfdPaths());
 // GPUs, an index out of range, a GPU without a PCIe address to find it again in the runtime by).
 int kfd_pick(const std::vector<KfdGpu>& gpus, int local_rank, int requested);
 
+// Per-rank GPU isolation: the index, among the GPUs the driver gives this process (`all`: node order, no
+// visibility lists applied), of the GPU that node-local rank `local_rank` takes from `visible` (the list
+// after them, kfd_gpus()) — the ROCR_VISIBLE_DEVICES value that leaves the runtime that one GPU. -1 when
+// `visible` is empty or its GPU is not in `all`.
+int kfd_isolation_index(const std::vector<KfdGpu>& all, const std::vector<KfdGpu>& visible, int local_rank);
+
 // Binds the calling thread's CPUs (sched_setaffinity) and its future page allocations (set_mempolicy
 // MPOL_PREFERRED) to NUMA node `node`. Returns the node, or -1 if nothing was changed.
 int bind_numa_node(int node);

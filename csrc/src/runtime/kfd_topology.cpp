@@ -135,6 +135,14 @@ int kfd_pick(const std::vector<KfdGpu>& gpus, int local_rank, int requested) {
   return id;
 }
 
+int kfd_isolation_index(const std::vector<KfdGpu>& all, const std::vector<KfdGpu>& visible, int local_rank) {
+  if (visible.empty() || local_rank < 0) return -1;
+  const KfdGpu& g = visible[static_cast<size_t>(local_rank) % visible.size()];
+  for (size_t i = 0; i < all.size(); ++i)
+    if (all[i].node == g.node) return static_cast<int>(i);
+  return -1;
+}
+
 int bind_numa_node(int node) {
   if (node < 0) return -1;
   std::ifstream f("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist");

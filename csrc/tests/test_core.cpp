@@ -889,6 +889,27 @@ void test_kfd_topology_8gpu() {
       const int phys = 7 - 2 * (r % 4);
       CHECK(x.pci_bus_id == bus_id(phys) && x.numa_node == (phys < 4 ? 0 : 1));
     }
+  // per-rank isolation (final --gpu-isolate): the rank's GPU by its index among all the driver's GPUs; with
+  // ROCR_VISIBLE_DEVICES set to it and HIP_VISIBLE_DEVICES to 0 the runtime's view is that one GPU
+  {
+    KfdPaths raw = p;
+    raw.honour_visible_env = false;
+    const auto all = kfd_gpus(raw);
+    const auto vis = kfd_gpus(p);
+    CHECK(all && all->size() == 8 && vis && vis->size() == 4);
+    if (all && vis && vis->size() == 4)
+      for (int r = 0; r < 8; ++r) {
+        const int idx = kfd_isolation_index(*all, *vis, r);
+        CHECK(idx == 7 - 2 * (r % 4));
+        setenv("ROCR_VISIBLE_DEVICES", std::to_string(idx).c_str(), 1);
+        setenv("HIP_VISIBLE_DEVICES", "0", 1);
+        const auto one = kfd_gpus(p);
+        CHECK(one && one->size() == 1 && kfd_pick(*one, r, -1) == 0 && (*one)[0].pci_bus_id == bus_id(idx));
+        setenv("ROCR_VISIBLE_DEVICES", "7,6,5,4,3,2,1,0", 1);
+        setenv("HIP_VISIBLE_DEVICES", "0,2,4,6", 1);
+      }
+    CHECK(all && kfd_isolation_index(*all, {}, 0) == -1 && kfd_isolation_index(*all, *all, -1) == -1);
+  }
   unsetenv("HIP_VISIBLE_DEVICES");
   unsetenv("ROCR_VISIBLE_DEVICES");
   // a box that may open one of the host's eight GPUs (render node access), indexed 0 by both lists

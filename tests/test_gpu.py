@@ -963,3 +963,18 @@ def test_staged_pinned_kernel_copies(n, shift):
     assert eng.stats()["direct"] == 0
     assert np.array_equal(as_triples(out), as_triples(search_cpu(prob)))
     eng.close()
+
+
+@pytest.mark.parametrize("np_", [1, 2])
+def test_final_cli_gpu_isolate(np_):
+    # --gpu-isolate=1 narrows each rank's runtime to the GPU it takes by node-local rank (ROCR_VISIBLE_DEVICES
+    # to its index, HIP_VISIBLE_DEVICES to 0): the box's one GPU stays that GPU, the output stays the golden
+    r = run_final(["--backend=hip", "--gpu-isolate=1", "--log-level=info"], stdin_path=input_path(6), np_=np_)
+    assert r.returncode == 0, r.stderr.decode()
+    assert r.stdout.decode() == expected(6)
+    assert r.stderr.decode().count("runtime isolated to gpu") == np_, r.stderr.decode()
+    # with --device the rank names its GPU itself: no isolation
+    r = run_final(["--backend=hip", "--gpu-isolate=1", "--device=0", "--log-level=info"], stdin_path=input_path(6),
+                  np_=np_)
+    assert r.returncode == 0 and r.stdout.decode() == expected(6)
+    assert "runtime isolated" not in r.stderr.decode()
