@@ -691,3 +691,13 @@ def test_quick_exit_flushes_everything(tmp_path, quick):
     out = tmp_path / "o.txt"
     r = run_final(["--backend=cpu", f"--quick-exit={quick}", f"--output={out}"], stdin_path=input_path(1), np_=2)
     assert r.returncode == 0 and out.read_text() == expected(1)
+
+
+@pytest.mark.parametrize("mode", ["auto", "0", "1"])
+def test_gpu_isolate_flag_on_cpu_ranks(mode):
+    # --gpu-isolate is decided before MPI_Init from the flags and the driver's topology; CPU ranks (and a
+    # host without GPUs) leave the environment alone and print the golden
+    r = run_final(["--backend=cpu", f"--gpu-isolate={mode}", "--log-level=info"], stdin_path=input_path(6), np_=2)
+    assert r.returncode == 0, r.stderr.decode()
+    assert r.stdout.decode() == expected(6)
+    assert "runtime isolated" not in r.stderr.decode()
