@@ -215,9 +215,14 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
       const int sn = (c >= 1 && j + 1 < L1) ? pv.lut[c * kLutStride + pv.seq1[j + 1]] : 0;
       prof[e] = static_cast<short>(RK ? sj - sn : (sj - sn) * (1 << KB) - 1);  // Pf = Dt * 2^KB - 1 (header)
     }
-    // row 0 (padding letter: steps past a lane's record) and column 31 (past Seq1) contribute 0
-    for (int e = tid; e < kLutInts; e += kBlock)
-      lut8[e] = static_cast<int8_t>((e & 31) == 31 || (e >> 5) == 0 ? 0 : pv.lut[e]);
+    // the anchor LUT stored by Seq1 letter: entry (y << 5) | c = T[c][y]. A step's Seq1 letter y is the same
+    // for every lane, so the wave's reads fall in one 32-byte row (8 banks, no conflicts); indexed by the
+    // lane's letter c first, 26 rows 32 bytes apart hit the same banks every 8 letters (up to 4-way).
+    // Letter 0 (padding: steps past a lane's record) and Seq1 letter 31 (past Seq1) contribute 0.
+    for (int e = tid; e < kLutInts; e += kBlock) {
+      const int y = e >> 5, c = e & 31;
+      lut8[e] = static_cast<int8_t>(y == 31 || c == 0 ? 0 : pv.lut[c * kLutStride + y]);
+    }
     for (int j = tid; j < row; j += kBlock) s1l[j] = j < L1 ? pv.seq1[j] : 31;
   }
   for (;;) {
@@ -337,7 +342,11 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
           // 8 steps (input6: 11 steps instead of 16); the copy index s stays a compile-time constant
           if (i >= steps) break;
           const int c = (wd[i >> 2] >> (8 * (i & 3))) & 0xff;
+#if defined(MOC_SWIPE_AB) && (MOC_SWIPE_AB & 2)  // A/B timing only (wrong results): every lane reads row 1
+          const uint4* rowp = reinterpret_cast<const uint4*>(prof + s * lay.copy_elems + 1 * lay.row);
+#else
           const uint4* rowp = reinterpret_cast<const uint4*>(prof + s * lay.copy_elems + c * lay.row);
+#endif
           const int sw = c & 7;
           uint32_t v[NP];
 #pragma unroll
@@ -348,7 +357,11 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
             v[4 * q + 2] = x.z;
             v[4 * q + 3] = x.w;
           }
-          anchor += lut8[(c << 5) | s1l[NOFF + i]];
+#if defined(MOC_SWIPE_AB) && (MOC_SWIPE_AB & 1)  // A/B timing only (wrong results): no per-lane LUT read
+          anchor += c;
+#else
+          anchor += lut8[(s1l[NOFF + i] << 5) | c];
+#endif
 #pragma unroll
           for (int q = 0; q < NP; ++q) {
             E2[q] = as_u32(as_s16x2(E2[q]) + as_s16x2(v[q]));
