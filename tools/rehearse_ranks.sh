@@ -4,7 +4,8 @@
 #      letters): the self-launch, the per-rank fields of the scaling record, the verification at NR ranks.
 #   2. ./final at 1.14 G letters (134 M input6-shaped records, 1.28 GB of text) on NPS ranks, all on
 #      --device=0, bulk and streamed (--batch-records=16777216): output md5 against np 1, per-rank --timing.
-# STEP=bench|final|all (default all). Every GPU step has its own time limit; the script stops at the first
+# FINAL_WALL=1 keeps the bench's ./final wall-clock fields (np = NR ranks on the same GPU: NR <= 4 here, the
+# box allows 16 GPU processes). STEP=bench|final|all (default all). Every GPU step has its own time limit; the script stops at the first
 # failure.
 set -o pipefail
 mkdir -p gpurun_out
@@ -14,7 +15,7 @@ STEP=${STEP:-all}
 if [ "$STEP" = all ] || [ "$STEP" = bench ]; then
   echo "=== bench.py --gpus $NR (gloo, shared GPU)"
   timeout -k 10 600 python3 bench.py --gpus $NR --allow-shared-gpu --dist-backend gloo --steps ${STEPS:-20} \
-    --warmup 3 --final-wall 0 > gpurun_out/rehearse_bench_$NR.json 2> gpurun_out/rehearse_bench_$NR.err || {
+    --warmup 3 --final-wall ${FINAL_WALL:-0} > gpurun_out/rehearse_bench_$NR.json 2> gpurun_out/rehearse_bench_$NR.err || {
     tail -20 gpurun_out/rehearse_bench_$NR.err; exit 1; }
   cat gpurun_out/rehearse_bench_$NR.json
 fi
