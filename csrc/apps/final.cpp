@@ -622,12 +622,16 @@ void isolate_gpu(int argc, char** argv) {
     if (!all || !visible || visible->empty() || (mode == "auto" && visible->size() < 2)) return;
     const int idx = kfd_isolation_index(*all, *visible, local);
     if (idx < 0) return;
-    setenv("ROCR_VISIBLE_DEVICES", std::to_string(idx).c_str(), 1);
+    // by the GPU's UUID when the driver gives one: an index counts the GPUs the runtime can open, which
+    // a device cgroup can narrow without the topology (or the render nodes' permissions) showing it
+    const KfdGpu& g = (*all)[static_cast<size_t>(idx)];
+    const std::string uuid = kfd_uuid(g);
+    const std::string value = uuid.empty() ? std::to_string(idx) : uuid;
+    setenv("ROCR_VISIBLE_DEVICES", value.c_str(), 1);
     for (const char* v : {"HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL"})
       if (std::getenv(v)) setenv(v, "0", 1);
-    const KfdGpu& g = (*all)[static_cast<size_t>(idx)];
-    g_gpu_isolation = "gpu " + g.pci_bus_id + " (ROCR_VISIBLE_DEVICES=" + std::to_string(idx) + " of " +
-                      std::to_string(visible->size()) + " visible)";
+    g_gpu_isolation = "gpu " + g.pci_bus_id + " (ROCR_VISIBLE_DEVICES=" + value + ", " + std::to_string(idx + 1) +
+                      " of " + std::to_string(visible->size()) + " visible)";
   } catch (const std::exception&) {
     // bad flags are reported after MPI_Init
   }

@@ -12,6 +12,7 @@
 // nullopt when only the runtime can tell — UUID lists, indices out of range, an unreadable topology.
 #pragma once
 
+#include <cstdint>
 #include <optional>
 #include <string>
 #include <vector>
@@ -23,7 +24,12 @@ struct KfdGpu {
   int render_minor = -1;   // /dev/dri/renderD<minor>
   std::string pci_bus_id;  // "dddd:bb:dd.f" (lower case), from the node's domain + location_id
   int numa_node = -1;      // NUMA node of its PCIe function (/sys/bus/pci/devices/<id>/numa_node), -1 unknown
+  uint64_t unique_id = 0;  // the driver's unique id (0 unknown): the runtime's UUID is "GPU-" + its 16 hex digits
 };
+
+// "GPU-<16 hex digits>" for a GPU with a unique id (the form ROCR_VISIBLE_DEVICES accepts besides indices),
+// "" without one.
+std::string kfd_uuid(const KfdGpu& g);
 
 struct KfdPaths {
   std::string nodes = "/sys/class/kfd/kfd/topology/nodes";

@@ -6,6 +6,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cctype>
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -15,29 +16,47 @@ namespace moc {
 
 namespace {
 
-// "name value" lines of a topology node's properties file
-bool read_properties(const std::string& path, int64_t& simd, int64_t& minor, int64_t& domain, int64_t& location) {
+// "name value" lines of a topology node's properties file. Values are unsigned 64-bit (hive_id and unique_id
+// use all 64 bits), so each line is parsed on its own: one large value must not end the scan.
+struct NodeProps {
+  int64_t simd = 0, minor = -1, domain = -1, location = -1;
+  uint64_t unique_id = 0;
+};
+bool read_properties(const std::string& path, NodeProps& p) {
   std::ifstream f(path);
   if (!f) return false;
-  std::string key;
-  int64_t v = 0;
-  simd = 0;
-  minor = domain = location = -1;
-  while (f >> key >> v) {
-    if (key == "simd_count") simd = v;
-    else if (key == "drm_render_minor") minor = v;
-    else if (key == "domain") domain = v;
-    else if (key == "location_id") location = v;
+  std::string line;
+  while (std::getline(f, line)) {
+    const size_t sp = line.find(' ');
+    if (sp == std::string::npos) continue;
+    const std::string key = line.substr(0, sp);
+    const uint64_t v = std::strtoull(line.c_str() + sp + 1, nullptr, 10);
+    if (key == "simd_count") p.simd = static_cast<int64_t>(v);
+    else if (key == "drm_render_minor") p.minor = static_cast<int64_t>(v);
+    else if (key == "domain") p.domain = static_cast<int64_t>(v);
+    else if (key == "location_id") p.location = static_cast<int64_t>(v);
+    else if (key == "unique_id") p.unique_id = v;
   }
   return true;
 }
 
-// "i,j,k" -> indices; nullopt for anything else (GPU UUIDs, empty lists: the runtime's to interpret)
-std::optional<std::vector<int>> index_list(const char* v) {
+// "i,j,k" -> indices into `gpus`; a "GPU-<16 hex digits>" entry names a GPU by its UUID (ROCR_VISIBLE_DEVICES
+// takes both). nullopt for anything else (unknown UUIDs, empty lists: the runtime's to interpret).
+std::optional<std::vector<int>> index_list(const char* v, const std::vector<KfdGpu>& gpus) {
   std::vector<int> out;
   std::stringstream ss(v);
   std::string tok;
   while (std::getline(ss, tok, ',')) {
+    if (tok.size() == 20 && (tok.compare(0, 4, "GPU-") == 0 || tok.compare(0, 4, "gpu-") == 0)) {
+      std::string want = "GPU-" + tok.substr(4);
+      for (size_t c = 4; c < want.size(); ++c) want[c] = static_cast<char>(std::tolower(static_cast<unsigned char>(want[c])));
+      int found = -1;
+      for (size_t i = 0; i < gpus.size() && found < 0; ++i)
+        if (kfd_uuid(gpus[i]) == want) found = static_cast<int>(i);
+      if (found < 0) return std::nullopt;
+      out.push_back(found);
+      continue;
+    }
     if (tok.empty() || tok.find_first_not_of("0123456789") != std::string::npos || tok.size() > 6) return std::nullopt;
     out.push_back(std::stoi(tok));
   }
@@ -47,13 +66,13 @@ std::optional<std::vector<int>> index_list(const char* v) {
 
 // The runtime's re-mapping by index lists: ROCR_VISIBLE_DEVICES picks from the GPUs the driver gives this
 // process, then HIP_VISIBLE_DEVICES (or CUDA_VISIBLE_DEVICES, GPU_DEVICE_ORDINAL) from those — each list
-// in its own order. Anything else (UUIDs, out-of-range or repeated indices, disagreeing HIP/CUDA lists)
-// is left to the runtime: nullopt.
+// in its own order; ROCR_VISIBLE_DEVICES may also name GPUs by UUID. Anything else (unknown UUIDs,
+// out-of-range or repeated indices, disagreeing HIP/CUDA lists) is left to the runtime: nullopt.
 std::optional<std::vector<KfdGpu>> apply_visible_env(std::vector<KfdGpu> gpus) {
   auto pick = [&gpus](const char* var) -> bool {
     const char* v = std::getenv(var);
     if (!v) return true;
-    const auto idx = index_list(v);
+    const auto idx = index_list(v, gpus);
     if (!idx) return false;
     std::vector<KfdGpu> next;
     std::vector<bool> used(gpus.size(), false);
@@ -101,9 +120,10 @@ std::optional<std::vector<KfdGpu>> kfd_gpus(const KfdPaths& paths) {
   std::vector<KfdGpu> gpus;
   if (access(paths.kfd.c_str(), R_OK | W_OK) != 0) return gpus;  // no driver access: the runtime sees none
   for (int id : ids) {
-    int64_t simd = 0, minor = -1, domain = -1, location = -1;
-    if (!read_properties(paths.nodes + "/" + std::to_string(id) + "/properties", simd, minor, domain, location))
+    NodeProps np;
+    if (!read_properties(paths.nodes + "/" + std::to_string(id) + "/properties", np))
       return std::nullopt;  // a node that cannot be read: leave the answer to the runtime
+    const int64_t simd = np.simd, minor = np.minor, domain = np.domain, location = np.location;
     if (simd <= 0) continue;  // a CPU node
     if (minor < 0) return std::nullopt;
     const std::string render = paths.dri + "/renderD" + std::to_string(minor);
@@ -111,6 +131,7 @@ std::optional<std::vector<KfdGpu>> kfd_gpus(const KfdPaths& paths) {
     KfdGpu g;
     g.node = id;
     g.render_minor = static_cast<int>(minor);
+    g.unique_id = np.unique_id;
     if (domain >= 0 && location >= 0) {
       char bus[32];
       std::snprintf(bus, sizeof bus, "%04x:%02x:%02x.%x", static_cast<unsigned>(domain),
@@ -133,6 +154,13 @@ int kfd_pick(const std::vector<KfdGpu>& gpus, int local_rank, int requested) {
   const int id = requested >= 0 ? requested : local_rank % n;
   if (id >= n || gpus[static_cast<size_t>(id)].pci_bus_id.empty()) return -1;
   return id;
+}
+
+std::string kfd_uuid(const KfdGpu& g) {
+  if (!g.unique_id) return "";
+  char buf[32];
+  std::snprintf(buf, sizeof buf, "GPU-%016llx", static_cast<unsigned long long>(g.unique_id));
+  return buf;
 }
 
 int kfd_isolation_index(const std::vector<KfdGpu>& all, const std::vector<KfdGpu>& visible, int local_rank) {

@@ -844,8 +844,11 @@ void test_kfd_topology_8gpu() {
   for (int g = 0; g < 8; ++g) {
     const std::string d = root + "/nodes/" + std::to_string(2 + g);
     mkdir(d.c_str(), 0755);
-    put(d + "/properties", "simd_count 1024\ndrm_render_minor " + std::to_string(128 + g) + "\nlocation_id " +
-                               std::to_string(bus[g] << 8) + "\ndomain 0\n");
+    // 64-bit values (hive_id, unique_id) anywhere in the file: one of them must not end the scan
+    const unsigned long long uid = 0xfedcba9876543210ull + static_cast<unsigned long long>(g);
+    put(d + "/properties", "simd_count 1024\nhive_id 18446744073709551615\ndrm_render_minor " +
+                               std::to_string(128 + g) + "\nlocation_id " + std::to_string(bus[g] << 8) +
+                               "\ndomain 0\nunique_id " + std::to_string(uid) + "\n");
     put(root + "/dri/renderD" + std::to_string(128 + g), "");
     mkdir((root + "/pci/" + bus_id(g)).c_str(), 0755);
     put(root + "/pci/" + bus_id(g) + "/numa_node", g < 4 ? "0\n" : "1\n");
@@ -861,6 +864,16 @@ void test_kfd_topology_8gpu() {
   auto g = kfd_gpus(p);
   CHECK(g && g->size() == 8);
   if (!g || g->size() != 8) return;
+  // unique ids -> the runtime's UUIDs; ROCR_VISIBLE_DEVICES by UUID (any case), mixed with indices
+  CHECK(kfd_uuid((*g)[3]) == "GPU-fedcba9876543213" && (*g)[0].pci_bus_id == bus_id(0));
+  setenv("ROCR_VISIBLE_DEVICES", "GPU-FEDCBA9876543215,2", 1);
+  {
+    const auto u = kfd_gpus(p);
+    CHECK(u && u->size() == 2 && (*u)[0].pci_bus_id == bus_id(5) && (*u)[1].pci_bus_id == bus_id(2));
+  }
+  setenv("ROCR_VISIBLE_DEVICES", "GPU-0000000000000001", 1);  // unknown: the runtime's to interpret
+  CHECK(!kfd_gpus(p));
+  unsetenv("ROCR_VISIBLE_DEVICES");
   // rank -> device -> NUMA node, 8 and 16 ranks per node
   for (int r = 0; r < 16; ++r) {
     const int id = kfd_pick(*g, r, -1);
@@ -901,10 +914,12 @@ void test_kfd_topology_8gpu() {
       for (int r = 0; r < 8; ++r) {
         const int idx = kfd_isolation_index(*all, *vis, r);
         CHECK(idx == 7 - 2 * (r % 4));
-        setenv("ROCR_VISIBLE_DEVICES", std::to_string(idx).c_str(), 1);
-        setenv("HIP_VISIBLE_DEVICES", "0", 1);
-        const auto one = kfd_gpus(p);
-        CHECK(one && one->size() == 1 && kfd_pick(*one, r, -1) == 0 && (*one)[0].pci_bus_id == bus_id(idx));
+        for (const std::string& v : {std::to_string(idx), kfd_uuid((*all)[static_cast<size_t>(idx)])}) {
+          setenv("ROCR_VISIBLE_DEVICES", v.c_str(), 1);  // by index, and by UUID (what final sets)
+          setenv("HIP_VISIBLE_DEVICES", "0", 1);
+          const auto one = kfd_gpus(p);
+          CHECK(one && one->size() == 1 && kfd_pick(*one, r, -1) == 0 && (*one)[0].pci_bus_id == bus_id(idx));
+        }
         setenv("ROCR_VISIBLE_DEVICES", "7,6,5,4,3,2,1,0", 1);
         setenv("HIP_VISIBLE_DEVICES", "0,2,4,6", 1);
       }
