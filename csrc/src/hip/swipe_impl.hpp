@@ -408,6 +408,12 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
         if (RK) bd = (nb == k1 && k1 != 0u) ? bk : bd;
         best = nb;
       }
+#if defined(MOC_SWIPE_AB) && (MOC_SWIPE_AB & 4)  // A/B timing only (wrong results): no selection epilogue
+      best = 0u;
+#pragma unroll
+      for (int q = 0; q < NP; ++q) best ^= E2[q] ^ B2[q];
+      best = (best | 1u) & 0x7fff7fffu;
+#endif
       if (!on) best = 0u;
       int kw = 0;  // RK: the winning mutant's k
       if (RK) {
