@@ -625,7 +625,9 @@ void isolate_gpu(int argc, char** argv) {
     // by the GPU's UUID when the driver gives one: an index counts the GPUs the runtime can open, which
     // a device cgroup can narrow without the topology (or the render nodes' permissions) showing it
     const KfdGpu& g = (*all)[static_cast<size_t>(idx)];
-    const std::string uuid = kfd_uuid(g);
+    std::string uuid = kfd_uuid(g);
+    for (const KfdGpu& o : *all)  // partitions of one device may share its id: an index is exact then
+      if (o.node != g.node && o.unique_id == g.unique_id) uuid.clear();
     const std::string value = uuid.empty() ? std::to_string(idx) : uuid;
     setenv("ROCR_VISIBLE_DEVICES", value.c_str(), 1);
     for (const char* v : {"HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL"})
