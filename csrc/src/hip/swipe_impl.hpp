@@ -52,6 +52,14 @@ constexpr int kMaxTile = 2048;  // records per tile: up to 8 per thread in the t
 constexpr int rpt_of(int lf) { return lf == 0 ? 4 : 8; }
 constexpr int kLdsBudget = 80 * 1024;
 constexpr int kMaxV = 4;  // 16-byte letter vectors per thread per tile (register prefetch)
+// Shifted copies of the profile in LDS: 8 (a step's row segment is read with 16-byte ds_read_b128 at a
+// column multiple of 8) or 4 (8-byte ds_read_b64 at a multiple of 4: twice the reads, half the profile's
+// LDS, so more workgroups per CU).
+#ifndef MOC_SWIPE_COPIES
+#define MOC_SWIPE_COPIES 8
+#endif
+constexpr int kCopies = MOC_SWIPE_COPIES;
+static_assert(kCopies == 8 || kCopies == 4, "swipe profile copies: 8 or 4");
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
@@ -79,7 +87,7 @@ inline SwipeLayout swipe_layout(int L1, int noff, int l2w, int tile_records, int
   // a multiple of 64 int16 (8 chunks of 16 B) so the per-letter XOR swizzle of chunk indices stays in the row
   l.row = (std::max(L1, 4 * l2w) + noff + 8 + 63) & ~63;
   l.copy_elems = kAlphabet * l.row;
-  l.prof_bytes = al16(8 * l.copy_elems * 2);
+  l.prof_bytes = al16(kCopies * l.copy_elems * 2);
   l.s_off = l.prof_bytes;
   l.loff_off = l.s_off + al16(kLutInts + l.row);
   l.codes_off = l.loff_off + al16((tile_records + 1) * 4 + 64);  // + misc: 16 ints
@@ -208,7 +216,7 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
   //      ds_read_b128 group (16 records reading 16 rows) over 8 bank quads — 8-way -> ~2-way conflicts.
   {
     const int row = lay.row, ce = lay.copy_elems;
-    for (int e = tid; e < 8 * ce; e += kBlock) {
+    for (int e = tid; e < kCopies * ce; e += kBlock) {
       const int s = e / ce, rem = e - s * ce, c = rem / row, jj = rem - c * row;
       const int j = ((((jj >> 3) ^ (c & 7)) << 3) | (jj & 7)) + s;  // element stored at jj holds column j
       const int sj = (c >= 1 && j < L1) ? pv.lut[c * kLutStride + pv.seq1[j]] : 0;
@@ -323,7 +331,11 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
           prev = nxt;
         }
       }
+#if defined(MOC_SWIPE_AB) && (MOC_SWIPE_AB & 8)  // A/B timing only (wrong results): one hot-loop step
+      const int steps = min(1, wave_max_small(on ? L2 : 0));
+#else
       const int steps = wave_max_small(on ? L2 : 0);  // L2 <= 4 * L2W <= 64 here
+#endif
 
       uint32_t E2[NP], B2[NP];
       int anchor = 0;  // Tot_NOFF: the diagonal just past this lane's offsets
@@ -343,19 +355,33 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
           if (i >= steps) break;
           const int c = (wd[i >> 2] >> (8 * (i & 3))) & 0xff;
 #if defined(MOC_SWIPE_AB) && (MOC_SWIPE_AB & 2)  // A/B timing only (wrong results): every lane reads row 1
-          const uint4* rowp = reinterpret_cast<const uint4*>(prof + s * lay.copy_elems + 1 * lay.row);
+          const int crow = 1;
 #else
-          const uint4* rowp = reinterpret_cast<const uint4*>(prof + s * lay.copy_elems + c * lay.row);
+          const int crow = c;
 #endif
           const int sw = c & 7;
           uint32_t v[NP];
+          if constexpr (kCopies == 8) {
+            // copy s holds column j + s at j: columns i .. i + NOFF - 1 are 16-byte chunks from i0 on
+            const uint4* rowp = reinterpret_cast<const uint4*>(prof + s * lay.copy_elems + crow * lay.row);
 #pragma unroll
-          for (int q = 0; q < NOFF / 8; ++q) {
-            const uint4 x = rowp[((i0 >> 3) + q) ^ sw];
-            v[4 * q + 0] = x.x;
-            v[4 * q + 1] = x.y;
-            v[4 * q + 2] = x.z;
-            v[4 * q + 3] = x.w;
+            for (int q = 0; q < NOFF / 8; ++q) {
+              const uint4 x = rowp[((i0 >> 3) + q) ^ sw];
+              v[4 * q + 0] = x.x;
+              v[4 * q + 1] = x.y;
+              v[4 * q + 2] = x.z;
+              v[4 * q + 3] = x.w;
+            }
+          } else {
+            // copy s & 3 from column i - (i & 3) = i0 + (s & 4): 8-byte halves of the swizzled 16-byte chunks
+            const uint2* rowp = reinterpret_cast<const uint2*>(prof + (s & 3) * lay.copy_elems + crow * lay.row);
+#pragma unroll
+            for (int q = 0; q < NOFF / 4; ++q) {
+              const int h = (s >> 2) + q;  // 8-byte half index from column i0
+              const uint2 x = rowp[((((i0 >> 3) + (h >> 1)) ^ sw) << 1) | (h & 1)];
+              v[2 * q + 0] = x.x;
+              v[2 * q + 1] = x.y;
+            }
           }
 #if defined(MOC_SWIPE_AB) && (MOC_SWIPE_AB & 1)  // A/B timing only (wrong results): no per-lane LUT read
           anchor += c;
