@@ -210,7 +210,7 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
   Fetch cur, nxt;
   fetch(grab(), cur);  // the first tile's loads are in flight while the block builds its profile
 
-  // ---- 8 shifted int16 difference-profile copies: prof[s][c][j] = Pf[c][j + s], and the plain S rows.
+  // ---- kCopies shifted int16 difference-profile copies: prof[s][c][j] = Pf[c][j + s], and the plain S rows.
   //      Rows are 128-byte multiples, so the 16-byte chunk q of every row would start on the same LDS
   //      bank; chunk q of row c is stored at chunk q ^ (c & 7) instead, spreading the 16 lanes of a
   //      ds_read_b128 group (16 records reading 16 rows) over 8 bank quads — 8-way -> ~2-way conflicts.
