@@ -98,6 +98,13 @@ int moc_engine_auto_format(void* e, int64_t max_l2, int64_t min_l2);
 int moc_engine_r2_params(void* e, int64_t min_l2, int64_t max_l2, int32_t* out3);
 int moc_engine_pin(void* e, const void* p, size_t bytes);
 
+// Device-resident batch in the wire formats (every pointer device memory of the engine's GPU; packed 3 =
+// P33 letters, 0 = bytes; dense offsets; narrow lengths as in moc_engine_solve_ex): the swipe kernel reads
+// them in place (the rccl transport's path, csrc/src/device_batch.cpp). Synchronous; stats give the
+// kernel time.
+int moc_engine_solve_wire_device(void* e, const uint8_t* d_letters, const int64_t* d_offsets, const uint8_t* d_lengths,
+                                 int len_bits, int len_base, int64_t n, void* d_out, int fmt, int64_t min_l2,
+                                 int64_t max_l2, int packed);
 // device time (ms) of the last moc_engine_solve_device's kernels; waits for them
 int moc_engine_device_kernel_ms(void* e, double* ms);
 int moc_engine_solve_device(void* e, const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets,

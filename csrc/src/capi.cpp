@@ -331,6 +331,26 @@ int moc_engine_solve_ex(void* e, const uint8_t* codes, const int64_t* offsets, c
   });
 }
 
+int moc_engine_solve_wire_device(void* e, const uint8_t* d_letters, const int64_t* d_offsets, const uint8_t* d_lengths,
+                                 int len_bits, int len_base, int64_t n, void* d_out, int fmt, int64_t min_l2,
+                                 int64_t max_l2, int packed) {
+  return guard([&] {
+    if (packed != 0 && packed != 3) throw moc::Error("device-resident letters: 0 bytes or 3 P33 fields");
+    moc::WireBatch b;
+    b.letters = d_letters;
+    b.packed33 = packed == 3;
+    b.offsets = d_offsets;
+    b.lengths = d_lengths;
+    b.len_bits = len_bits;
+    b.len_base = len_base;
+    b.n = n;
+    b.min_l2 = min_l2;
+    b.max_l2 = max_l2;
+    b.device = true;
+    static_cast<moc::HipEngine*>(e)->solve_wire(b, d_out, static_cast<moc::ResultFormat>(fmt));
+  });
+}
+
 int moc_engine_auto_format(void* e, int64_t max_l2, int64_t min_l2) {
   return static_cast<int>(static_cast<moc::HipEngine*>(e)->auto_format(max_l2, min_l2));
 }

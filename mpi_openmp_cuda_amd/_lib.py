@@ -85,6 +85,8 @@ def _decl(lib):
         "moc_engine_pin": (c_int, [c_void_p, c_void_p, c_size_t]),
         "moc_expand_results": (c_int, [c_void_p, c_int, c_int64, c_void_p, c_void_p]),
         "moc_engine_solve_device": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+        "moc_engine_solve_wire_device": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int64, c_void_p,
+                                                 c_int, c_int64, c_int64, c_int]),
         "moc_engine_device_kernel_ms": (c_int, [c_void_p, c_void_p]),
         "moc_engine_stats": (c_int, [c_void_p, P(c_double)]),
         "moc_engine_search_keys": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p]),

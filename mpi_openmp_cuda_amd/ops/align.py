@@ -240,6 +240,25 @@ class HipSearchEngine:
             n, ctypes.c_void_p(out_t.data_ptr()), ctypes.c_void_p(stream.cuda_stream)))
         return out_t
 
+    def solve_wire_device(self, letters_t, offsets_t, lengths_t, n: int, out_t, fmt: str, l2_range,
+                          lengths_bits: int = 8, lengths_base: int = 0, packed33: bool = True):
+        """Device-resident batch in the wire formats (torch tensors on this engine's GPU, as the rccl transport
+        holds them): ``letters_t`` P33 fields (``packed33``) or bytes, ``offsets_t`` int64 [n + 1] letter
+        offsets, ``lengths_t`` narrow lengths (as ``solve``'s) or None, results into ``out_t`` (a uint8
+        tensor of n * itemsize bytes of ``fmt``, decoded on the host as ``solve``'s). Synchronous;
+        ``stats()["kernel_ms"]`` is the kernel's time."""
+        import torch
+
+        fid = _format_id(fmt)
+        assert letters_t.dtype == torch.uint8 and offsets_t.dtype == torch.int64 and offsets_t.numel() == n + 1
+        assert out_t.dtype == torch.uint8 and out_t.numel() >= n * _lib.FORMAT_DTYPES[fid].itemsize
+        lp = ctypes.c_void_p(lengths_t.data_ptr()) if lengths_t is not None else None
+        _lib.check(_lib.lib().moc_engine_solve_wire_device(
+            self._h, ctypes.c_void_p(letters_t.data_ptr()), ctypes.c_void_p(offsets_t.data_ptr()), lp,
+            int(lengths_bits), int(lengths_base), int(n), ctypes.c_void_p(out_t.data_ptr()), fid, int(l2_range[0]),
+            int(l2_range[1]), 3 if packed33 else 0))
+        return out_t
+
     def device_kernel_ms(self) -> float:
         """Device time (ms) of the last solve_device's kernels, from events around its launches (after the
         host's per-call planning); waits for them."""

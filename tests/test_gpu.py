@@ -978,3 +978,28 @@ def test_final_cli_gpu_isolate(np_):
                   np_=np_)
     assert r.returncode == 0 and r.stdout.decode() == expected(6)
     assert "runtime isolated" not in r.stderr.decode()
+
+
+@pytest.mark.parametrize("shape,n", [("input6", 200_003), ("input1", 30_001), ("input5", 3_000)])
+def test_wire_device_resident(engine, shape, n):
+    # a batch in the wire formats held in device memory (the rccl transport's form): P33 letters, narrow
+    # lengths, the narrowest results; the swipe kernel reads it in place
+    from mpi_openmp_cuda_amd.parallel.wire import WireSlice
+
+    prob = make_synthetic(shape, n, seed=61)
+    engine.set_problem(prob.weights, prob.seq1)
+    wire = WireSlice.from_csr(prob.codes, prob.offsets)
+    res = wire.alloc_results(engine)
+    dev = torch.device("cuda:0")
+    letters = torch.from_numpy(wire.codes).to(dev)
+    offsets = torch.from_numpy(wire.offsets).to(dev)
+    lengths = torch.from_numpy(wire.lengths).to(dev) if wire.lengths is not None else None
+    out = torch.zeros(res.nbytes, dtype=torch.uint8, device=dev)
+    engine.solve_wire_device(letters, offsets, lengths, wire.n, out, wire.fmt, (wire.l2_min, wire.l2_max),
+                             lengths_bits=wire.len_bits or 8, lengths_base=wire.len_base)
+    st = engine.stats()
+    assert st["direct"] == 1 and st["kernels"] == ["swipe"] and st["h2d_bytes"] == 0
+    res.view(np.uint8)[:] = out.cpu().numpy()
+    got = wire.triples(engine)
+    ref = as_triples(search_cpu(prob))
+    assert np.array_equal(got, ref)

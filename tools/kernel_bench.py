@@ -6,7 +6,8 @@ reference kernel does O(L1*L2^2) work for the same answers.
 
 Every shape is repeated until at least --min-ms (default 60) of kernel time is measured, so launch skew
 and tail effects stay small. --variants tile16,mfma runs the long-record sweep both ways (MOC_MFMA: the
-matrix-core sweep, tile_mfma_kernels.hip) for an A/B on the same data.
+matrix-core sweep, tile_mfma_kernels.hip) for an A/B on the same data; ``wire`` runs short-record shapes in
+the wire formats, device-resident (solve_wire_device: P33 letters, narrow lengths, R2/R4 results).
 
   python tools/kernel_bench.py [--variants tile16,mfma] [--min-ms 60] [shape ...]
 """
@@ -40,6 +41,43 @@ def make(shape, n):
         rng = np.random.default_rng(L1)
         prob = Problem(prob.weights, rng.integers(1, 27, size=L1, dtype=np.uint8), prob.codes, prob.offsets)
     return prob
+
+
+def run_wire(shape, n, min_ms):
+    """The same records in the wire formats, device-resident (P33 letters, narrow lengths, the narrowest
+    results: the rccl transport's batches), through HipSearchEngine.solve_wire_device; kernel time from the
+    engine's events."""
+    from mpi_openmp_cuda_amd.parallel.wire import WireSlice
+
+    prob = make(shape, n)
+    eng = HipSearchEngine(device=0)
+    eng.set_problem(prob.weights, prob.seq1)
+    wire = WireSlice.from_csr(prob.codes, prob.offsets)
+    res = wire.alloc_results(eng)
+    dev = torch.device("cuda:0")
+    letters = torch.from_numpy(wire.codes).to(dev)
+    offsets = torch.from_numpy(wire.offsets).to(dev)
+    lengths = torch.from_numpy(wire.lengths).to(dev) if wire.lengths is not None else None
+    out = torch.zeros(res.nbytes, dtype=torch.uint8, device=dev)
+    args = (letters, offsets, lengths, wire.n, out, wire.fmt, (wire.l2_min, wire.l2_max))
+    kw = dict(lengths_bits=wire.len_bits or 8, lengths_base=wire.len_base)
+    eng.solve_wire_device(*args, **kw)  # warm-up
+    first = max(eng.stats()["kernel_ms"], 1e-3)
+    iters = max(5, math.ceil(min_ms / first))
+    total = 0.0
+    for _ in range(iters):
+        eng.solve_wire_device(*args, **kw)
+        total += eng.stats()["kernel_ms"]
+    ms = total / iters
+    res.view(np.uint8)[:] = out.cpu().numpy()
+    nv = min(prob.n, 4000)
+    ok = bool(np.array_equal(wire.triples(eng, nv), as_triples(search_cpu(prob.slice(0, nv)))))
+    cells = prob.cells()
+    dev_bytes = letters.numel() + (lengths.numel() if lengths is not None else 0) + out.numel()
+    return {"shape": shape, "variant": f"wire-{wire.letter_format}-len{wire.len_bits}-{wire.fmt}", "records": prob.n,
+            "L1": prob.L1, "letters": prob.total_chars, "cells": cells, "iters": iters, "gpu_ms": round(ms, 4),
+            "timing": "kernel_events", "cells_per_s": cells / (ms / 1e3), "records_per_s": prob.n / (ms / 1e3),
+            "hbm_bytes_per_record": round(dev_bytes / prob.n, 2), "kernels": eng.stats()["kernels"], "verified": ok}
 
 
 def run(shape, n, variant, min_ms):
@@ -100,4 +138,7 @@ if __name__ == "__main__":
     shapes = args.shapes or list(CASES)
     for shape in shapes:
         for variant in args.variants.split(","):
-            print(json.dumps(run(shape, CASES[shape][0], variant, args.min_ms)), flush=True)
+            if variant == "wire":
+                print(json.dumps(run_wire(shape, CASES[shape][0], args.min_ms)), flush=True)
+            else:
+                print(json.dumps(run(shape, CASES[shape][0], variant, args.min_ms)), flush=True)
