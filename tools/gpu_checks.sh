@@ -49,7 +49,7 @@ for c in "$@"; do
         steps+=("swipe_ab_$n$sfx:200:echo '# $lib' && MOC_LIB_PATH=$R/$lib python tools/kernel_bench.py input6 input1")
       done ;;
     hello-env)  # the runtime start and the first hardware queue (tools/hip_hello.hip) under runtime settings
-      steps+=("hello_env$sfx:300:(cd build && [ -x hip_hello ] || { make -s -C .. build/mpilib/libmpi.so && hipcc --offload-arch=gfx950 -O2 ../tools/hip_hello.hip -I/opt/conda/include -Lmpilib -lmpi -Wl,-rpath-link,/opt/conda/lib -Wl,-rpath,\$PWD/mpilib -o hip_hello; }) && for e in NONE HSA_ENABLE_INTERRUPT=0 AMD_DIRECT_DISPATCH=0 ROC_AQL_QUEUE_SIZE=1024 HSA_ENABLE_SDMA=0 GPU_MAX_HW_QUEUES=1 HIP_FORCE_DEV_KERNARG=1; do for r in 1 2 3 4 5; do sleep 1; echo \"\$e \$(env \${e/NONE/X=1} timeout -k 10 30 build/hip_hello 2>&1 >/dev/null | tail -1)\" || exit 1; done; done") ;;
+      steps+=("hello_env$sfx:300:(cd build && [ -x hip_hello ] && [ hip_hello -nt ../tools/hip_hello.hip ] || { make -s -C .. build/mpilib/libmpi.so && hipcc --offload-arch=gfx950 -O2 ../tools/hip_hello.hip -I/opt/conda/include -Lmpilib -lmpi -Wl,-rpath-link,/opt/conda/lib -Wl,-rpath,\$PWD/mpilib -o hip_hello; }) && for e in NONE HELLO_NULL_STREAM=1 HSA_ENABLE_INTERRUPT=0 AMD_DIRECT_DISPATCH=0 ROC_AQL_QUEUE_SIZE=1024 HSA_ENABLE_SDMA=0 GPU_MAX_HW_QUEUES=1 HIP_FORCE_DEV_KERNARG=1; do for r in 1 2 3 4 5; do sleep 1; echo \"\$e \$(env \${e/NONE/X=1} timeout -k 10 30 build/hip_hello 2>&1 >/dev/null | tail -1)\" || exit 1; done; done") ;;
     isolate) steps+=("isolate$sfx:200:NPS='1 2' INPUTS='6' REPS=7 SPACING=1 HELLO=0 TIMING=1 EXTRA='--backend=hip --gpu-isolate=1 --log-level=info' bash tools/final_walltime.sh") ;;
     *) echo "unknown check: $c (see the header of $0)"; exit 2 ;;
   esac

@@ -8,6 +8,7 @@
 
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <thread>
 
 __global__ void empty_kernel(int* out) {
@@ -27,14 +28,18 @@ int main(int argc, char** argv) {
     ok = hipGetDeviceCount(&n) == hipSuccess && n > 0;
     t_rt = ms_since(t0);
     if (!ok) return;
-    hipStream_t s;
-    ok = hipSetDevice(0) == hipSuccess && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
+    // HELLO_NULL_STREAM=1: the runtime's null stream instead of a stream of our own (does it come with the
+    // runtime's start, or cost its own hardware queue at first use?)
+    const bool null_stream = std::getenv("HELLO_NULL_STREAM") && std::atoi(std::getenv("HELLO_NULL_STREAM")) != 0;
+    hipStream_t s = nullptr;
+    ok = hipSetDevice(0) == hipSuccess &&
+         (null_stream || hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess);
     t_q = ms_since(t0);
     if (!ok) return;
     hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, s, nullptr);
     ok = hipStreamSynchronize(s) == hipSuccess;
     t_k = ms_since(t0);
-    (void)hipStreamDestroy(s);
+    if (s) (void)hipStreamDestroy(s);
   });
   MPI_Init(&argc, &argv);
   double t_mpi = ms_since(t0);
