@@ -186,7 +186,11 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
     const int r = long_recs ? __builtin_amdgcn_readfirstlane(long_recs[li]) : li;
     const uint8_t* rec = bv.codes + (bv.offsets[r] - bv.offsets[0]);
     const int L2 = __builtin_amdgcn_readfirstlane(static_cast<int>(bv.offsets[r + 1] - bv.offsets[r]));
+#if defined(MOC_T16_AB) && (MOC_T16_AB & 1)  // A/B timing only (wrong results): at most 8 sweep steps
+    const int steps = L2 <= L1 ? min(L2, 8) : 0;
+#else
     const int steps = L2 <= L1 ? L2 : 0;
+#endif
     const int need = L2 <= L1 ? L1 - L2 + 1 : 1;
     const int ntiles = min((need + kSpan - 1) / kSpan, t_win_end);
     const int t_stop = li == end_li ? min(end_t, ntiles) : ntiles;
@@ -306,8 +310,12 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
         const int totA = totB + ca;          // Tot_{oa}
         carry = __shfl(totA, 0, 64);
 #endif
+#if defined(MOC_T16_AB) && (MOC_T16_AB & 2)  // A/B timing only (wrong results): no per-offset candidates
+        acc64 ^= static_cast<unsigned long long>(static_cast<uint32_t>(totA ^ mxA[u] ^ mxB[u]));
+#else
         acc64 = max_u64(acc64, pass1_candidate(oa, L1, L2, pv.semantics, totA, totB, mxA[u]));
         acc64 = max_u64(acc64, pass1_candidate(oa + 1, L1, L2, pv.semantics, totB, totB - cb, mxB[u]));
+#endif
       }
     }
     const unsigned long long k = wave_max_u64(acc64);
