@@ -310,12 +310,8 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
         const int totA = totB + ca;          // Tot_{oa}
         carry = __shfl(totA, 0, 64);
 #endif
-#if defined(MOC_T16_AB) && (MOC_T16_AB & 2)  // A/B timing only (wrong results): no per-offset candidates
-        acc64 ^= static_cast<unsigned long long>(static_cast<uint32_t>(totA ^ mxA[u] ^ mxB[u]));
-#else
         acc64 = max_u64(acc64, pass1_candidate(oa, L1, L2, pv.semantics, totA, totB, mxA[u]));
         acc64 = max_u64(acc64, pass1_candidate(oa + 1, L1, L2, pv.semantics, totB, totB - cb, mxB[u]));
-#endif
       }
     }
     const unsigned long long k = wave_max_u64(acc64);
