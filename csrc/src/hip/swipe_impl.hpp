@@ -144,6 +144,13 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
   // ---- tile fetch: the next tile's lengths and letters are loaded into registers while the current
   //      tile is being scored, so the PCIe / HBM read latency hides behind the compute (the streaming
   //      path is bound by host-link bytes: keep the link busy all the time).
+  // Byte-letter batches without narrow lengths (device-resident: records by dense offsets) load their
+  // tile's offsets in fetch() and take the lengths from them when the tile is staged: subtracting at the load
+  // would make every thread wait there for the loads' return, so the next tile's loads would not stay in
+  // flight behind the current tile's scoring (device-resident input6 0.573 -> 0.547 ms,
+  // profiles/swipe_lds_ab_r4/). Narrow length forms (the host streams') decode at the load: deferring the
+  // base-6 words measured 0.2 % slower on the headline.
+  constexpr bool kDeferLens = LF == 0 && kRpt == 4;
   struct Fetch {
     int64_t t, rb, start, end;
     int m;
@@ -151,6 +158,8 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
     uintptr_t a0;
     int nvec;
     uint4 v[kMaxV];
+    bool lo_set;    // kDeferLens: lens still to be taken from lo
+    int64_t lo[5];  // this thread's 4 records' offsets and the next
   };
   auto fetch = [&](int64_t t, Fetch& f) {
     f.t = t;
@@ -161,6 +170,7 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
     for (int k = 0; k < kMaxV; ++k) f.v[k] = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
     for (int q = 0; q < kRpt; ++q) f.lens[q] = 0;
+    f.lo_set = false;
     if (t >= n_tiles) return;
     f.rb = tile_first(t);
     f.m = static_cast<int>(min(tile_size(t), a.n - f.rb));
@@ -174,7 +184,17 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
     for (int h = 0; h < kRpt / 4; ++h) {  // this thread's kRpt records' lengths, 4 per load
       int l4[4];
       const int r0 = tid * kRpt + 4 * h;
-      record_lengths4(a, f.rb + r0, min(4, max(0, f.m - r0)), l4);
+      const int nv = min(4, max(0, f.m - r0));
+      if constexpr (kDeferLens) {
+        if (!a.lengths3 && !a.lengths4 && !a.lengths6 && !a.lengths8 && !a.off_shift) {
+          const int64_t i0 = f.rb + r0;
+#pragma unroll
+          for (int q = 0; q < 5; ++q) f.lo[q] = nv > 0 && q <= nv ? a.offsets[i0 + q] : 0;  // <= offsets[n]
+          f.lo_set = true;
+          continue;
+        }
+      }
+      record_lengths4(a, f.rb + r0, nv, l4);
 #pragma unroll
       for (int q = 0; q < 4; ++q) f.lens[4 * h + q] = l4[q];
     }
@@ -240,6 +260,13 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
     __syncthreads();  // the previous tile's LDS (loff, letters, results) is free again
 
     // ---- lengths -> block exclusive scan -> loff[0..m]
+    if constexpr (kDeferLens) {
+      if (cur.lo_set) {  // the lengths fetch() left as offsets
+        const int nv = min(4, max(0, m - tid * kRpt));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cur.lens[q] = q < nv ? static_cast<int>(cur.lo[q + 1] - cur.lo[q]) : 0;
+      }
+    }
     int sum = 0;
 #pragma unroll
     for (int q = 0; q < kRpt; ++q) sum += cur.lens[q];
