@@ -187,8 +187,9 @@ class HipEngine {
   R2Params r2_{};                  // R2 parameters of the current solve
   void* d_image_ = nullptr;  // problem image: LUT | Seq1 | profile (views below)
   size_t d_image_cap_ = 0;
-  // page-locked staging of the image: the upload is one DMA on the compute stream (a pageable hipMemcpy
-  // costs the runtime's staging set-up, 8 ms inside a tiny job's first search on the box)
+  // page-locked staging of the image: the upload is one copy kernel on the compute stream (dev::launch_copy;
+  // a pageable hipMemcpy, or any copy the runtime gives its SDMA engine, cost 8-34 ms of engine start-up
+  // inside a tiny job's first search on the box, profiles/copy_path_probe.log)
   void* h_image_ = nullptr;
   size_t h_image_cap_ = 0;
   std::vector<uint8_t> image_;
