@@ -100,6 +100,10 @@ GIT_HASH  := $(shell git rev-parse --short=12 HEAD 2>/dev/null || echo unknown)
 BUILD_ID  := $(BUILD)/build_id
 $(shell mkdir -p $(BUILD); echo 'src=$(SRC_HASH) git=$(GIT_HASH)' | cmp -s - $(BUILD_ID) || echo 'src=$(SRC_HASH) git=$(GIT_HASH)' > $(BUILD_ID))
 
+$(OBJ)/hip/build_info.o: csrc/src/hip/build_info.hip $(BUILD_ID)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -DMOC_SRC_HASH='"$(SRC_HASH)"' -c $< -o $@
+
 $(OBJ)/apps/final.o: csrc/apps/final.cpp csrc/apps/job.hpp $(HEADERS) $(BUILD_ID)
 	@mkdir -p $(dir $@)
 	$(CXX) $(CXXFLAGS) $(MPIFLAGS) -DMOC_BUILD_ID='"src=$(SRC_HASH) git=$(GIT_HASH)"' -c $< -o $@
@@ -154,7 +158,7 @@ tsan: $(MPILIB)/libmpi.so
 debug-kernels:
 	@mkdir -p $(BUILD)/debug
 	for f in $(HIP_SRCS); do \
-	  $(HIPCC) $(HIPFLAGS) -DMOC_DEBUG_KERNELS -c $$f -o $(BUILD)/debug/$$(basename $$f .hip).hip.o || exit 1; \
+	  $(HIPCC) $(HIPFLAGS) -DMOC_DEBUG_KERNELS -DMOC_SRC_HASH='"$(SRC_HASH)"' -c $$f -o $(BUILD)/debug/$$(basename $$f .hip).hip.o || exit 1; \
 	done
 	for lf in 0 2; do for no in $(SWIPE_NOFFS); do \
 	  $(HIPCC) $(HIPFLAGS) -DMOC_DEBUG_KERNELS -DMOC_SWIPE_LF=$$lf -DMOC_SWIPE_NO=$$no -x hip -c $(SWIPE_GROUP) \
@@ -162,12 +166,15 @@ debug-kernels:
 	done; done
 	$(CXX) -shared -fopenmp -o $(BUILD)/debug/libmoc.so $(CORE_OBJS) $(BUILD)/debug/*.hip.o $(LDROCM) -ldl
 
-# Kernel A/B builds: make variant NAME=p4 VDEFS="-DMOC_T16_PREFETCH=4" -> build/variant_p4/libmoc.so
-# (select with MOC_LIB_PATH).
+# Kernel A/B builds: make variant NAME=p4 VDEFS="-DMOC_T16_UNROLL=32" -> build/variant_p4/libmoc.so
+# (select with MOC_LIB_PATH and MOC_ALLOW_VARIANT_LIB=1: the loader refuses a library whose kernels carry
+# defines otherwise; moc_build_info reports them). No switch that gives wrong results lives in the kernel
+# sources: a timing-only experiment is a throwaway patch, not a define.
 variant: lib
 	@mkdir -p $(BUILD)/variant_$(NAME)
 	for f in $(HIP_SRCS); do \
-	  $(HIPCC) $(HIPFLAGS) $(VDEFS) -c $$f -o $(BUILD)/variant_$(NAME)/$$(basename $$f .hip).hip.o || exit 1; \
+	  $(HIPCC) $(HIPFLAGS) $(VDEFS) -DMOC_SRC_HASH='"$(SRC_HASH)"' -DMOC_KERNEL_DEFS='"$(strip $(VDEFS))"' \
+	    -c $$f -o $(BUILD)/variant_$(NAME)/$$(basename $$f .hip).hip.o || exit 1; \
 	done
 	for lf in 0 2; do for no in $(SWIPE_NOFFS); do \
 	  $(HIPCC) $(HIPFLAGS) $(VDEFS) -DMOC_SWIPE_LF=$$lf -DMOC_SWIPE_NO=$$no -x hip -c $(SWIPE_GROUP) \

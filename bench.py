@@ -121,9 +121,14 @@ def visible_gpus(wanted=1):
     n = kfd_gpu_count()
     if n is not None and n >= wanted:
         return n
-    import torch
-
-    return max(n or 0, torch.cuda.device_count())
+    # torch's count in a short-lived child: the launcher itself must not start a HIP runtime
+    r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                       capture_output=True, text=True, timeout=300)
+    try:
+        t = int(r.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        t = 0
+    return max(n or 0, t)
 
 
 SHM_PREFIX = "/dev/shm/moc_bench_"
@@ -517,7 +522,8 @@ def main():
             "lengths": "base6" if wire.len_bits == 6 else (f"{wire.len_bits}bit" if wire.len_bits else "offsets"),
             "letters": wire.letter_format,
             "rank0_numa_node": numa,
-            "rccl_world": dist.get_world_size() if (distributed and nccl) else (1 if nccl else None),
+            # only what ran: an RCCL communicator exists only for N > 1 ranks on the nccl backend
+            "rccl_world": dist.get_world_size() if (distributed and nccl) else None,
             "dist_backend": ("nccl" if nccl else "gloo") if distributed else "none",
             "rank_numa_nodes": [int(x) for x in per_rank[:, 0]],
             "rank_kernel_ms": [round(float(x), 4) for x in per_rank[:, 1]],
@@ -529,6 +535,10 @@ def main():
             "rank0_kernels": st["kernels"],
             "host_stream": "zero_copy" if st["direct"] else "staged",
             "verified": bool(okt.item()),
+            # each timed step broadcasts the header over the process group (N > 1) but the engine's image
+            # comes from the host copy made before the loop (set_problem of an unchanged problem is a
+            # no-op), as the reference broadcasts it once per job (main.c:149-150)
+            "header_per_step": "broadcast_only" if distributed else "none",
             "final_input6_wall": wall6,
             "final_input6_wall_hip": wall6_hip,
         }

@@ -43,6 +43,14 @@ int moc_pack_lengths(const int64_t* offsets, int64_t n, int bits, int64_t base, 
 /* ---- score table ---- */
 int moc_score_table(const int32_t* weights4, int32_t* lut1024, uint8_t* cls1024);
 
+/* ---- exactness bounds of the kernels' narrow-integer forms (moc/kernel_bounds.hpp); no GPU needed ----
+ * out4: [0] swipe key form (moc::bounds::kFormSwipeKBits / kFormSwipeRK, 0 = the swipe kernel's integer
+ * bounds refuse the batch), [1] 1 if the short kernel's packed int16 form is exact, [2] the int32 hot-key
+ * shift of the short / tile kernels (0 = 64-bit keys), [3] 1 if the tile16 profile holds the table. */
+int moc_kernel_bounds(const int32_t* weights4, int64_t L1, int64_t min_l2, int64_t max_l2, int32_t* out4);
+/* "src=<source hash> defs=<-D flags of the kernel objects>" (empty defs: the product build) */
+const char* moc_build_info(void);
+
 /* ---- CPU engine (OpenMP) ---- */
 int moc_cpu_solve(const int32_t* weights4, const uint8_t* seq1, int64_t L1, const uint8_t* codes,
                   const int64_t* offsets, int64_t n, int semantics, int threads, moc_result* out);
@@ -116,7 +124,8 @@ int moc_engine_search_keys_device(void* e, const uint8_t* d_codes, const int64_t
 int moc_engine_finalize_keys_device(void* e, const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets,
                                     int64_t n, const uint64_t* d_keys, void* d_out,
                                     int fmt, void* stream);
-/* stats: kernel_ms, total_ms, h2d_bytes, d2h_bytes, chunks, cells, records, direct, format, kernels */
+/* stats: kernel_ms, total_ms, h2d_bytes, d2h_bytes, chunks, cells, records, direct, format, kernels,
+ * r2 smin, r2 kw, r2 j, forms (moc::bounds::FormBits of the last solve) */
 int moc_engine_stats(void* e, double* out14);
 
 #ifdef __cplusplus

@@ -33,6 +33,7 @@
 #include <cstdint>
 
 #include "moc/common.hpp"
+#include "moc/kernel_bounds.hpp"
 #include "moc/wire.hpp"
 
 namespace moc {
@@ -179,9 +180,17 @@ bool configure_short(int64_t L1, int64_t min_l2, int64_t max_l2, ShortArgs& a);
 bool configure_swipe(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs_weight, ShortArgs& a,
                      bool hbm = false);
 void launch_swipe(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStream_t stream);
+// Key form (moc::bounds::kFormSwipe*) the swipe kernel takes for such a batch, 0 when it cannot take it
+// by its integer bounds (configure_swipe may still refuse it for the LDS budget).
+int32_t swipe_form(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs_weight);
+inline int32_t swipe_launch_form(const ShortArgs& a) {
+  return a.swipe_rk ? bounds::kFormSwipeRK : bounds::kFormSwipeKBits;
+}
 
 // Short-record kernel (all records with lanes_needed <= a.slot are processed; others are skipped).
 void launch_short(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStream_t stream);
+// Arithmetic form (moc::bounds::kFormShort*) launch_short runs for these arguments.
+int32_t short_form(const ProblemView& pv, const ShortArgs& a);
 
 // Tile kernel + finalize for the long records listed in `plan`; results -> out (format fmt).
 // plan.long_recs == nullptr means the identity list (record li of the batch).
@@ -192,6 +201,12 @@ void launch_tiles(const ProblemView& pv, const BatchView& bv, const Plan& plan, 
 // keys (score, ~(2o + mutated)); launch_finalize_keys resolves each record's k on its winning diagonal
 // (one wave per record, O(L2)) and writes the results — no o*L2 + k index, so L1 * L2 >= 2^32 is fine.
 void launch_tile_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream);
+// Arithmetic form (moc::bounds::kFormTile16 / kFormMfma / kFormTilesKey32 / kFormTilesKey64) of the sweep
+// launch_tile_keys runs for this problem view.
+inline int32_t tile_form(const ProblemView& pv) {
+  if (pv.prof16) return pv.mfma_sweep ? bounds::kFormMfma : bounds::kFormTile16;
+  return pv.key_shift > 0 ? bounds::kFormTilesKey32 : bounds::kFormTilesKey64;
+}
 void launch_finalize_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, void* out, int fmt,
                           hipStream_t stream);
 // tile16 variant of launch_tile_keys (pv.prof16 must be set): packed-int16 sweep over the LDS profile.

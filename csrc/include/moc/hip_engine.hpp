@@ -54,6 +54,8 @@ struct EngineStats {
   int32_t direct = 0;    // 1 if the last solve streamed from pinned host memory (zero-copy)
   int32_t format = 0;    // ResultFormat of the last solve
   int32_t kernels = 0;   // bitmask of kernels used: 1 swipe (lane/record), 2 short (lane/offset), 4 tiles
+                         // (LUT tile kernel), 8 tile16
+  int32_t forms = 0;     // bitmask of the arithmetic forms they ran (moc::bounds::FormBits)
   R2Params r2;           // parameters of the R2 results of the last solve (when fmt == R2)
 };
 

@@ -54,6 +54,8 @@ struct Profile16 {
   std::vector<uint16_t> entries;
   int64_t row = 0;  // entries per row (= L1)
 };
+// True when every Dt and T of the table fit the profile bytes (moc/kernel_bounds.hpp profile16_exact).
+bool profile16_fits(const ScoreTable& t);
 bool build_profile16(const ScoreTable& t, const uint8_t* seq1, int64_t L1, int64_t overhang, Profile16& out);
 
 }  // namespace moc

@@ -128,6 +128,18 @@ int moc_score_table(const int32_t* weights4, int32_t* lut1024, uint8_t* cls1024)
   });
 }
 
+int moc_kernel_bounds(const int32_t* weights4, int64_t L1, int64_t min_l2, int64_t max_l2, int32_t* out4) {
+  return guard([&] {
+    const moc::ScoreTable t = moc::ScoreTable::build(weights_of(weights4));
+    const int32_t w = t.max_abs();
+    const int64_t searched = std::max<int64_t>(1, std::min(max_l2, L1 + 1));  // longer records are not searched
+    out4[0] = moc::dev::swipe_form(L1, min_l2, max_l2, w);
+    out4[1] = moc::bounds::short_pk_exact(w, searched) ? 1 : 0;
+    out4[2] = moc::bounds::key_shift(w, searched);
+    out4[3] = moc::profile16_fits(t) ? 1 : 0;
+  });
+}
+
 int moc_cpu_solve(const int32_t* weights4, const uint8_t* seq1, int64_t L1, const uint8_t* codes,
                   const int64_t* offsets, int64_t n, int semantics, int threads, moc_result* out) {
   return guard([&] {
@@ -410,7 +422,7 @@ int moc_engine_stats(void* e, double* out14) {
   return guard([&] {
     double* out13 = out14;
     double* out10 = out14;
-    out14[13] = 0;  // was the retired SDMA mode's flag
+    out14[13] = static_cast<double>(static_cast<moc::HipEngine*>(e)->stats().forms);
     const auto& s = static_cast<moc::HipEngine*>(e)->stats();
     out13[10] = s.r2.smin;
     out13[11] = s.r2.kw;

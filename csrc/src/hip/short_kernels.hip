@@ -19,6 +19,7 @@
 #include <cstdlib>
 
 #include "kernel_common.hpp"
+#include "moc/kernel_bounds.hpp"
 
 namespace moc {
 namespace dev {
@@ -45,6 +46,8 @@ struct ShortLayout {
 };
 
 inline int align16(int x) { return (x + 15) & ~15; }
+// per-block profile S[c][j] (one int per entry) when it is small, else the LUT + Seq1 in LDS
+bool short_profile(int L1) { return kAlphabet * ((L1 + kWave + 3) & ~3) * 4 <= 24 * 1024; }
 
 ShortLayout short_layout(int L1, int tile_records, int codes_cap, int fmt_bytes, bool profile) {
   ShortLayout l;
@@ -263,7 +266,7 @@ bool configure_short(int64_t L1, int64_t min_l2, int64_t max_l2, ShortArgs& a) {
   a.rpw = kWave / a.slot;
   const int64_t l2cap = std::max<int64_t>(1, std::min(max_l2, L1 + 1));
   const int fb = result_bytes(static_cast<ResultFormat>(a.fmt));
-  const bool profile = kAlphabet * ((L1 + kWave + 3) & ~3) * 4 <= 24 * 1024;
+  const bool profile = short_profile(static_cast<int>(L1));
   int max_tile = kMaxTile;  // MOC_SHORT_TILE: cap on records per block tile (A/B runs)
   if (const char* v = std::getenv("MOC_SHORT_TILE")) max_tile = std::max(1, std::min(kMaxTile, std::atoi(v)));
   // Occupancy first: the largest tile whose LDS lets 6 blocks (24 waves) share a CU — the hot loop's
@@ -287,23 +290,30 @@ bool configure_short(int64_t L1, int64_t min_l2, int64_t max_l2, ShortArgs& a) {
   return false;
 }
 
+int32_t short_form(const ProblemView& pv, const ShortArgs& a) {
+  // packed (Dt, S) profile when every partial sum is int16-exact (moc/kernel_bounds.hpp short_pk_exact;
+  // MOC_SHORT_PK=0 forces the int32 DPP form, for A/B runs)
+  static const bool pk_off = [] {
+    const char* v = std::getenv("MOC_SHORT_PK");
+    return v && std::atoi(v) == 0;
+  }();
+  if (short_profile(pv.L1) && !pk_off && bounds::short_pk_exact(pv.max_abs_t, a.max_l2)) return bounds::kFormShortPk;
+  return pv.key_shift > 0 ? bounds::kFormShortKey32 : bounds::kFormShortKey64;
+}
+
 void launch_short(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStream_t stream) {
   if (a.n <= 0) return;
   const int fb = result_bytes(static_cast<ResultFormat>(a.fmt));
-  const bool profile = kAlphabet * ((pv.L1 + kWave + 3) & ~3) * 4 <= 24 * 1024;
+  const bool profile = short_profile(pv.L1);
   const ShortLayout lay = short_layout(pv.L1, a.tile_records, a.codes_cap, fb, profile);
   const int64_t n_tiles = (a.n + a.tile_records - 1) / a.tile_records;
   const int per_cu = std::max(1, std::min(8, 160 * 1024 / std::max(lay.total, 1)));
   const int64_t blocks = std::min<int64_t>(n_tiles, static_cast<int64_t>(num_cus) * per_cu);
   const dim3 grid(static_cast<unsigned>(std::max<int64_t>(blocks, 1))), block(kBlock);
-  // packed (Dt, S) profile when every partial sum is int16-exact: |D| <= 2 max|T| L2, |Tot| <= max|T| L2
-  // (MOC_SHORT_PK=0 forces the int32 DPP form, for A/B runs)
-  const char* pk_env = std::getenv("MOC_SHORT_PK");
-  const bool pk = profile && (!pk_env || std::atoi(pk_env) != 0) &&
-                  2 * static_cast<int64_t>(std::max(pv.max_abs_t, 1)) * std::max(a.max_l2, 1) < 32767;
-  if (pk) {
+  const int32_t form = short_form(pv, a);
+  if (form == bounds::kFormShortPk) {
     hipLaunchKernelGGL((short_search_kernel<false, true, true>), grid, block, lay.total, stream, pv, a, lay);
-  } else if (pv.key_shift > 0) {
+  } else if (form == bounds::kFormShortKey32) {
     if (profile)
       hipLaunchKernelGGL((short_search_kernel<false, true, false>), grid, block, lay.total, stream, pv, a, lay);
     else

@@ -22,7 +22,8 @@
 // A wave runs steps = its longest record's length. Records stream through the same persistent, LDS-tiled
 // block loop as the short kernel (zero-copy from pinned host memory when the batch lives there).
 // Exactness: int16 arithmetic is exact because the host only selects this kernel when
-// 2*max|W|*max|Seq2|*2^KB + 2^KB < 2^15 (no key can wrap) — see configure_swipe. When the weights leave
+// 2*max|W|*max|Seq2|*2^KB + 2^KB < 32767 (no key can wrap) — moc/kernel_bounds.hpp swipe_keys, replayed at
+// and past the bound by csrc/tests/test_core.cpp test_swipe_replay_bounds. When the weights leave
 // no room for k in the keys but the sums still fit int16 (input1: W1 = 100, |Seq2| <= 41), the RK form
 // runs: Pf = Dt, the running sums are D_o(k) themselves, B2 keeps max_k D_o(k), and after the selection
 // each lane whose winner is a mutant re-walks that one diagonal for the first k reaching the best D.
@@ -52,14 +53,9 @@ constexpr int kMaxTile = 2048;  // records per tile: up to 8 per thread in the t
 constexpr int rpt_of(int lf) { return lf == 0 ? 4 : 8; }
 constexpr int kLdsBudget = 80 * 1024;
 constexpr int kMaxV = 4;  // 16-byte letter vectors per thread per tile (register prefetch)
-// Shifted copies of the profile in LDS: 8 (a step's row segment is read with 16-byte ds_read_b128 at a
-// column multiple of 8) or 4 (8-byte ds_read_b64 at a multiple of 4: twice the reads, half the profile's
-// LDS, so more workgroups per CU).
-#ifndef MOC_SWIPE_COPIES
-#define MOC_SWIPE_COPIES 8
-#endif
-constexpr int kCopies = MOC_SWIPE_COPIES;
-static_assert(kCopies == 8 || kCopies == 4, "swipe profile copies: 8 or 4");
+// Shifted copies of the profile in LDS: a step's row segment is read with 16-byte ds_read_b128 at a column
+// multiple of 8. (4 copies with 8-byte reads — half the profile's LDS — measured slower, round 4.)
+constexpr int kCopies = 8;
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
@@ -97,11 +93,6 @@ inline SwipeLayout swipe_layout(int L1, int noff, int l2w, int tile_records, int
   return l;
 }
 
-inline int kbits_for(int l2w) {  // bits for k in the int16 keys: k <= 4*l2w
-  int b = 1;
-  while ((1 << b) <= 4 * l2w) ++b;
-  return b;
-}
 }  // namespace swipe
 
 using namespace swipe;
@@ -125,7 +116,7 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
   uint8_t* raw_l = smem + lay.raw_off;  // P33: the tile's encoded bytes as loaded
   const int L1 = pv.L1;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  constexpr int KB = RK ? 1 : (4 * L2W < 8) ? 3 : (4 * L2W < 16) ? 4 : (4 * L2W < 32) ? 5 : (4 * L2W < 64) ? 6 : 7;
+  constexpr int KB = RK ? 1 : bounds::swipe_kbits(L2W);  // k bits of the int16 keys (moc/kernel_bounds.hpp)
   constexpr int KMASK = (1 << KB) - 1;
   constexpr int NP = NOFF / 2;  // packed accumulators
 
@@ -358,11 +349,7 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
           prev = nxt;
         }
       }
-#if defined(MOC_SWIPE_AB) && (MOC_SWIPE_AB & 8)  // A/B timing only (wrong results): one hot-loop step
-      const int steps = min(1, wave_max_small(on ? L2 : 0));
-#else
       const int steps = wave_max_small(on ? L2 : 0);  // L2 <= 4 * L2W <= 64 here
-#endif
 
       uint32_t E2[NP], B2[NP];
       int anchor = 0;  // Tot_NOFF: the diagonal just past this lane's offsets
@@ -381,40 +368,20 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
           // 8 steps (input6: 11 steps instead of 16); the copy index s stays a compile-time constant
           if (i >= steps) break;
           const int c = (wd[i >> 2] >> (8 * (i & 3))) & 0xff;
-#if defined(MOC_SWIPE_AB) && (MOC_SWIPE_AB & 2)  // A/B timing only (wrong results): every lane reads row 1
-          const int crow = 1;
-#else
           const int crow = c;
-#endif
           const int sw = c & 7;
           uint32_t v[NP];
-          if constexpr (kCopies == 8) {
-            // copy s holds column j + s at j: columns i .. i + NOFF - 1 are 16-byte chunks from i0 on
-            const uint4* rowp = reinterpret_cast<const uint4*>(prof + s * lay.copy_elems + crow * lay.row);
+          // copy s holds column j + s at j: columns i .. i + NOFF - 1 are 16-byte chunks from i0 on
+          const uint4* rowp = reinterpret_cast<const uint4*>(prof + s * lay.copy_elems + crow * lay.row);
 #pragma unroll
-            for (int q = 0; q < NOFF / 8; ++q) {
-              const uint4 x = rowp[((i0 >> 3) + q) ^ sw];
-              v[4 * q + 0] = x.x;
-              v[4 * q + 1] = x.y;
-              v[4 * q + 2] = x.z;
-              v[4 * q + 3] = x.w;
-            }
-          } else {
-            // copy s & 3 from column i - (i & 3) = i0 + (s & 4): 8-byte halves of the swizzled 16-byte chunks
-            const uint2* rowp = reinterpret_cast<const uint2*>(prof + (s & 3) * lay.copy_elems + crow * lay.row);
-#pragma unroll
-            for (int q = 0; q < NOFF / 4; ++q) {
-              const int h = (s >> 2) + q;  // 8-byte half index from column i0
-              const uint2 x = rowp[((((i0 >> 3) + (h >> 1)) ^ sw) << 1) | (h & 1)];
-              v[2 * q + 0] = x.x;
-              v[2 * q + 1] = x.y;
-            }
+          for (int q = 0; q < NOFF / 8; ++q) {
+            const uint4 x = rowp[((i0 >> 3) + q) ^ sw];
+            v[4 * q + 0] = x.x;
+            v[4 * q + 1] = x.y;
+            v[4 * q + 2] = x.z;
+            v[4 * q + 3] = x.w;
           }
-#if defined(MOC_SWIPE_AB) && (MOC_SWIPE_AB & 1)  // A/B timing only (wrong results): no per-lane LUT read
-          anchor += c;
-#else
           anchor += lut8[(s1l[NOFF + i] << 5) | c];
-#endif
 #pragma unroll
           for (int q = 0; q < NP; ++q) {
             E2[q] = as_u32(as_s16x2(E2[q]) + as_s16x2(v[q]));
@@ -461,12 +428,6 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
         if (RK) bd = (nb == k1 && k1 != 0u) ? bk : bd;
         best = nb;
       }
-#if defined(MOC_SWIPE_AB) && (MOC_SWIPE_AB & 4)  // A/B timing only (wrong results): no selection epilogue
-      best = 0u;
-#pragma unroll
-      for (int q = 0; q < NP; ++q) best ^= E2[q] ^ B2[q];
-      best = (best | 1u) & 0x7fff7fffu;
-#endif
       if (!on) best = 0u;
       int kw = 0;  // RK: the winning mutant's k
       if (RK) {

@@ -13,26 +13,26 @@ struct SwipeChoice {
 };
 
 // Offsets per lane (NOFF), record words (L2W) and key form for a batch, or noff 0 when the kernel cannot
-// take it: at most 64 offsets and 64 letters per record, Seq1's profile within the LDS budget, running sums
-// that fit int16 (|D| <= 2 max|T| max L2), an int8 anchor LUT. The keys carry k when 2^KB * |D| leaves
-// room (input6); otherwise (input1: W1 = 100) the RK form re-finds k after the selection. Records of 33-64
-// letters always take the RK form (one set of instances).
+// take it: at most 64 offsets and 64 letters per record, Seq1's profile within the LDS budget, and an
+// int16-exact key form (moc/kernel_bounds.hpp swipe_keys: the keys carry k when 2^KB * |D| leaves room, as
+// on input6; otherwise, input1's W1 = 100, the RK form re-finds k after the selection).
 SwipeChoice swipe_choice(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs_weight) {
   SwipeChoice c;
   const int64_t need = lanes_needed(L1, std::min(min_l2, L1));
   if (need > 64 || max_l2 > 64 || L1 > 200) return c;
-  const int l2w = max_l2 <= 16 ? 4 : max_l2 <= 32 ? 8 : 16;
-  const int noff = static_cast<int>(((std::max<int64_t>(need, 2) + 7) / 8) * 8);
-  const int64_t dmax = 2 * static_cast<int64_t>(std::max(max_abs_weight, 1)) * std::max<int64_t>(max_l2, 1);
-  if (dmax >= 32767) return c;         // sums fit int16
-  if (max_abs_weight > 127) return c;  // the anchor diagonal's LUT is int8
-  const int kb = kbits_for(l2w);
-  c.rk = l2w == 16 || (dmax << kb) + (1 << kb) >= 32767;  // no room for k in the int16 keys
-  c.noff = noff;
-  c.l2w = l2w;
+  const bounds::SwipeKeys keys = bounds::swipe_keys(max_abs_weight, max_l2);
+  if (keys == bounds::SwipeKeys::None) return c;
+  c.rk = keys == bounds::SwipeKeys::RK;
+  c.noff = static_cast<int>(((std::max<int64_t>(need, 2) + 7) / 8) * 8);
+  c.l2w = bounds::swipe_record_words(max_l2);
   return c;
 }
 }  // namespace
+
+int32_t swipe_form(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs_weight) {
+  const SwipeChoice ch = swipe_choice(L1, min_l2, max_l2, max_abs_weight);
+  return !ch.noff ? 0 : ch.rk ? bounds::kFormSwipeRK : bounds::kFormSwipeKBits;
+}
 
 bool configure_swipe(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs_weight, ShortArgs& a, bool hbm) {
   if (a.packed5) return false;  // 5-bit letters go through the staged pipeline (unpacked on the device)

@@ -186,11 +186,7 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
     const int r = long_recs ? __builtin_amdgcn_readfirstlane(long_recs[li]) : li;
     const uint8_t* rec = bv.codes + (bv.offsets[r] - bv.offsets[0]);
     const int L2 = __builtin_amdgcn_readfirstlane(static_cast<int>(bv.offsets[r + 1] - bv.offsets[r]));
-#if defined(MOC_T16_AB) && (MOC_T16_AB & 1)  // A/B timing only (wrong results): at most 8 sweep steps
-    const int steps = L2 <= L1 ? min(L2, 8) : 0;
-#else
     const int steps = L2 <= L1 ? L2 : 0;
-#endif
     const int need = L2 <= L1 ? L1 - L2 + 1 : 1;
     const int ntiles = min((need + kSpan - 1) / kSpan, t_win_end);
     const int t_stop = li == end_li ? min(end_t, ntiles) : ntiles;

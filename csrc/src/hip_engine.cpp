@@ -18,13 +18,7 @@
 
 namespace moc {
 
-int32_t choose_key_shift(int32_t max_abs_weight, int64_t max_l2) {
-  int shift = 1;
-  while ((int64_t{1} << shift) < max_l2 + 1) ++shift;  // mask = 2^shift - 1 >= every k used (<= L2)
-  const int64_t dmax = 2 * static_cast<int64_t>(std::max(max_abs_weight, 1)) * std::max<int64_t>(max_l2, 1);
-  if (shift > 24 || (dmax << shift) >= (int64_t{1} << 31)) return 0;  // 64-bit hot keys
-  return shift;
-}
+int32_t choose_key_shift(int32_t max_abs_weight, int64_t max_l2) { return bounds::key_shift(max_abs_weight, max_l2); }
 
 namespace {
 // Copies between device memory and a caller's host range, one per piece of the range that lies within a
@@ -56,7 +50,13 @@ void copy_d2h(void* dst, const void* src, size_t bytes, hipStream_t s) {
 // host -> device from a hipHostMalloc allocation of the engine's own (h_image_, plan staging)
 void upload_staged(void* dst, const void* h, size_t bytes, hipStream_t s) {
   void* hd = nullptr;
-  if (dev::kernel_copy_fits(dst, h, bytes) && hipHostGetDevicePointer(&hd, const_cast<void*>(h), 0) == hipSuccess && hd)
+  if (dev::kernel_copy_fits(dst, h, bytes)) {
+    if (hipHostGetDevicePointer(&hd, const_cast<void*>(h), 0) != hipSuccess) {
+      (void)hipGetLastError();  // clear the sticky error: the next launch check must not report this lookup
+      hd = nullptr;
+    }
+  }
+  if (hd)
     dev::launch_copy(dst, hd, bytes, s);
   else
     MOC_HIP_CHECK(hipMemcpyAsync(dst, h, bytes, hipMemcpyHostToDevice, s));
@@ -745,6 +745,7 @@ void HipEngine::solve_wire_impl(const WireBatch& batch, void* out, ResultFormat 
     MOC_HIP_CHECK(hipEventRecord(ev_a_, s_compute_));
     launch_direct(pv, a, swipe, graph);
     stats_.kernels = swipe ? 1 : 2;
+    stats_.forms = swipe ? dev::swipe_launch_form(a) : dev::short_form(pv, a);
     MOC_HIP_CHECK(hipEventRecord(ev_b_, s_compute_));
     stats_.direct = 1;
     stats_.chunks = 1;
@@ -941,6 +942,7 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
       else
         dev::launch_short(pv, a, num_cus_, s_compute_);
       stats_.kernels |= swipe ? 1 : 2;
+      stats_.forms |= swipe ? dev::swipe_launch_form(a) : dev::short_form(pv, a);
     }
     if (!starts.empty()) {
       dev::Plan plan = device_plan(s.d_plan, starts.size(), lrecs != nullptr, n_long, tp);
@@ -952,6 +954,7 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
       }
       dev::launch_tiles(tpv, bv, plan, s.d_out, static_cast<int>(fmt), s_compute_);
       stats_.kernels |= tp.tile16 ? 8 : 4;
+      stats_.forms |= dev::tile_form(tpv);
     }
     MOC_HIP_CHECK(hipGetLastError());
     MOC_HIP_CHECK(hipEventRecord(s.ev_k1, s_compute_));
@@ -1036,6 +1039,8 @@ void HipEngine::solve_device(const uint8_t* d_codes, const int64_t* d_offsets, c
   stats_.cells = cp.cells;
   stats_.records = n;
   stats_.kernels = (short_ok ? (swipe ? 1 : 2) : 0) | (starts.empty() ? 0 : (tp.tile16 ? 8 : 4));
+  stats_.forms = (short_ok ? (swipe ? dev::swipe_launch_form(a) : dev::short_form(pv, a)) : 0) |
+                 (starts.empty() ? 0 : dev::tile_form(tile_view(cp.max_l2, tp)));
 }
 
 }  // namespace moc
@@ -1080,6 +1085,7 @@ void HipEngine::search_keys_device(const uint8_t* d_codes, const int64_t* d_offs
   stats_ = EngineStats{};
   stats_.records = n;
   stats_.kernels = plan.n_waves ? (tp.tile16 ? 8 : 4) : 0;
+  stats_.forms = plan.n_waves ? dev::tile_form(tile_view(max_l2, tp)) : 0;
 }
 
 void HipEngine::finalize_keys_device(const uint8_t* d_codes, const int64_t* d_offsets, const int64_t* h_offsets,

@@ -3,6 +3,8 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include "moc/kernel_bounds.hpp"
+
 namespace moc {
 
 const std::vector<std::string>& first_type_groups() {
@@ -66,8 +68,7 @@ int32_t ScoreTable::max_abs() const {
   return m;
 }
 
-bool build_profile16(const ScoreTable& t, const uint8_t* seq1, int64_t L1, int64_t overhang, Profile16& out) {
-  if (L1 <= 0 || overhang < 0) return false;
+bool profile16_fits(const ScoreTable& t) {
   int32_t dmin = INT32_MAX, dmax = INT32_MIN, tabs = 0;
   for (int c = 1; c < kAlphabet; ++c)
     for (int x = 0; x < kAlphabet; ++x) {  // 0: the pad code after Seq1
@@ -80,7 +81,12 @@ bool build_profile16(const ScoreTable& t, const uint8_t* seq1, int64_t L1, int64
     }
   // the kernel's anchor diagonals read T itself as int8 too (negative weights through the API could give
   // a narrow range of large values)
-  if (dmin < -128 || dmax > 127 || tabs > 127) return false;
+  return bounds::profile16_exact(dmin, dmax, tabs);
+}
+
+bool build_profile16(const ScoreTable& t, const uint8_t* seq1, int64_t L1, int64_t overhang, Profile16& out) {
+  if (L1 <= 0 || overhang < 0) return false;
+  if (!profile16_fits(t)) return false;
   out.row = L1;
   out.entries.assign(static_cast<size_t>((kAlphabet - 1) * L1 + overhang), 0);
   std::vector<int32_t> d(static_cast<size_t>(L1) + 1, 0);

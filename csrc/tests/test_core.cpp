@@ -15,6 +15,7 @@
 
 #include "moc/cpu_engine.hpp"
 #include "moc/io.hpp"
+#include "moc/kernel_bounds.hpp"
 #include "moc/partition.hpp"
 #include "moc/problem.hpp"
 #include "moc/runtime/kfd_topology.hpp"
@@ -986,6 +987,376 @@ void test_cutter_count_ahead() {
   }
 }
 
+
+// ---- narrow-integer forms at their exactness bounds (moc/kernel_bounds.hpp) ------------------------------
+// Host replays of the kernels' integer arithmetic, with the same wrap-around (int16 / int32 / int8 casts),
+// driven by the product's own rules: at the bound the rule picks the form and the replay equals brute force;
+// one step past it the rule refuses the form, and the replay of the refused form goes wrong on the same
+// input (so the bound is tight, not just safe). The adversarial input: Seq1 = "AZAZ...", records that are
+// pieces of Seq1 at even offsets (every step Dt = +(W1 + W4)) and odd ones (-(W1 + W4)), constant records,
+// and a periodic Seq1 that makes most offsets tie.
+namespace xv {
+constexpr uint8_t kA = 1, kZ = 26;
+
+struct Fixture {
+  std::vector<uint8_t> s1;
+  RecordBatch batch;
+  int64_t min_l2 = INT64_MAX, max_l2 = 0;
+};
+
+Fixture azaz(int64_t L1, int64_t lo, int64_t hi, uint32_t seed) {
+  Fixture f;
+  f.s1.resize(static_cast<size_t>(L1));
+  for (int64_t j = 0; j < L1; ++j) f.s1[j] = (j & 1) ? kZ : kA;
+  std::mt19937 rng(seed);
+  auto add = [&](std::vector<uint8_t> r) {
+    f.min_l2 = std::min<int64_t>(f.min_l2, static_cast<int64_t>(r.size()));
+    f.max_l2 = std::max<int64_t>(f.max_l2, static_cast<int64_t>(r.size()));
+    f.batch.push_back(r.data(), static_cast<int64_t>(r.size()));
+  };
+  for (int64_t L2 : {lo, hi, (lo + hi) / 2, hi - 1}) {
+    if (L2 < lo || L2 > hi || L2 < 1) continue;
+    for (int64_t at : {int64_t{0}, int64_t{1}, L1 - L2, L1 - L2 - 1}) {  // even / odd pieces of Seq1, both ends
+      if (at < 0 || at + L2 > L1) continue;
+      add(std::vector<uint8_t>(f.s1.begin() + at, f.s1.begin() + at + L2));
+    }
+    add(std::vector<uint8_t>(static_cast<size_t>(L2), kA));
+    add(std::vector<uint8_t>(static_cast<size_t>(L2), kZ));
+    std::vector<uint8_t> r(static_cast<size_t>(L2));
+    for (auto& x : r) x = rng() % 2 ? kA : kZ;  // A/Z noise: large |D| on most diagonals
+    add(r);
+    for (auto& x : r) x = static_cast<uint8_t>(1 + rng() % 26);
+    add(r);
+  }
+  return f;
+}
+
+bool same(const Result& a, const Result& b) { return a.score == b.score && a.n == b.n && a.k == b.k; }
+
+uint64_t final_key(int32_t score, uint32_t idx) {
+  return (static_cast<uint64_t>(static_cast<uint32_t>(score) ^ 0x80000000u) << 32) | (0xffffffffu - idx);
+}
+Result decode_key(uint64_t key, int64_t L2) {
+  if (key == 0) return Result{kNoCandidateScore, 0, 0};
+  const int32_t score = static_cast<int32_t>(static_cast<uint32_t>(key >> 32) ^ 0x80000000u);
+  const uint32_t idx = 0xffffffffu - static_cast<uint32_t>(key);
+  return Result{score, static_cast<int32_t>(idx / static_cast<uint32_t>(L2)),
+                static_cast<int32_t>(idx % static_cast<uint32_t>(L2))};
+}
+int32_t S(const ScoreTable& t, const std::vector<uint8_t>& s1, int c, int64_t j) {
+  return (c >= 1 && j < static_cast<int64_t>(s1.size())) ? t.score(c, s1[j]) : 0;
+}
+
+// swipe_search_kernel (swipe_impl.hpp) for one record: NOFF offsets per lane, KB k bits or the RK form,
+// `steps` = its wave's longest record, `max_l2` = the batch's.
+Result swipe_record(const ScoreTable& t, const std::vector<uint8_t>& s1, const uint8_t* s2, int64_t L2, int noff,
+                    int kb, bool rk, int steps, int64_t max_l2, Semantics sem) {
+  const int64_t L1 = static_cast<int64_t>(s1.size());
+  const int KB = rk ? 1 : kb, KMASK = (1 << KB) - 1;
+  const bool on = L2 <= L1;
+  auto pf = [&](int c, int64_t j) {  // the LDS profile entry (int16)
+    const int d = S(t, s1, c, j) - S(t, s1, c, j + 1);
+    return static_cast<int16_t>(rk ? d : d * (1 << KB) - 1);
+  };
+  std::vector<int16_t> E(static_cast<size_t>(noff), static_cast<int16_t>(rk ? 0 : KMASK)),
+      B(static_cast<size_t>(noff), INT16_MIN);
+  int anchor = 0;
+  for (int i = 0; i < steps; ++i) {
+    const int c = on && i < L2 ? s2[i] : 0;
+    for (int o = 0; o < noff; ++o) {
+      E[o] = static_cast<int16_t>(E[o] + pf(c, i + o));
+      B[o] = std::max(B[o], E[o]);
+    }
+    const int64_t j = noff + i;
+    const int y = j < L1 ? s1[j] : 31;
+    anchor += (y == 31 || c == 0) ? 0 : static_cast<int8_t>(t.score(c, y));  // int8 anchor LUT
+  }
+  const int64_t last = L1 - L2;
+  const int64_t lim0 = on ? last + ((sem == Semantics::Spec || L2 == L1) ? 1 : 0) : 0;
+  const int64_t lim1 = on && L2 >= 2 ? last : 0;
+  const int64_t all_valid = L1 - max_l2;
+  const int16_t eb = static_cast<int16_t>(rk ? 0 : KMASK - steps);
+  uint32_t best = 0, tot = static_cast<uint32_t>(anchor + 32768);
+  int bd = 0;
+  for (int o = noff - 1; o >= 0; --o) {
+    const int16_t dq = rk ? E[o] : static_cast<int16_t>(static_cast<int16_t>(E[o] - eb) >> KB);
+    const uint32_t Pn = tot, Po = Pn + static_cast<uint32_t>(static_cast<int>(dq));
+    tot = Po;
+    const uint32_t kLow0 = 0xffffu - (static_cast<uint32_t>(o) << KB), kLow1 = kLow0 - KMASK;
+    uint32_t k0 = (Po << 16) | kLow0;
+    const int bk = B[o];
+    const uint32_t tt = static_cast<uint32_t>(bk) + (Pn << KB);
+    uint32_t k1 = rk ? ((static_cast<uint32_t>(bk) + Pn) << 16) | (kLow0 - 1u) : ((tt >> KB) << 16) | (tt & KMASK) | kLow1;
+    if (o >= all_valid) {
+      k0 = o < lim0 ? k0 : 0u;
+      k1 = o < lim1 ? k1 : 0u;
+    }
+    const uint32_t nb = std::max(best, std::max(k0, k1));
+    if (rk) bd = (nb == k1 && k1 != 0u) ? bk : bd;
+    best = nb;
+  }
+  if (!on || best == 0u) return Result{kNoCandidateScore, 0, 0};
+  const uint32_t idx = 0xffffu - (best & 0xffffu);
+  if (!rk) return Result{static_cast<int>(best >> 16) - 32768, static_cast<int>(idx >> KB), static_cast<int>(idx & KMASK)};
+  int kw = 0;
+  if (idx & 1u) {  // the k re-walk on the winning diagonal (copy 0 of the profile, int sums)
+    const int ow = static_cast<int>(idx >> 1);
+    int run = 0;
+    for (int i = 0; i < steps; ++i) {
+      run += pf(i < L2 ? s2[i] : 0, ow + i);
+      kw = (kw == 0 && run == bd) ? i + 1 : kw;
+    }
+  }
+  return Result{static_cast<int>(best >> 16) - 32768, static_cast<int>(idx >> 1), (idx & 1u) ? kw : 0};
+}
+
+// short_search_kernel's packed form (Pk): (Dt << 16 | S) entries, one packed int16 add per cell.
+Result short_pk_record(const ScoreTable& t, const std::vector<uint8_t>& s1, const uint8_t* s2, int64_t L2, int steps,
+                       Semantics sem) {
+  const int64_t L1 = static_cast<int64_t>(s1.size());
+  if (L2 > L1) return Result{kNoCandidateScore, 0, 0};
+  uint64_t best_key = 0;
+  for (int64_t o = 0; o <= L1 - L2; ++o) {
+    uint32_t acc = 0;
+    int32_t best16 = INT32_MIN;
+    for (int i = 0; i < steps; ++i) {
+      const int c = i < L2 ? s2[i] : 0;
+      const int sj = S(t, s1, c, o + i), sn = S(t, s1, c, o + i + 1);
+      const uint32_t v = c ? ((static_cast<uint32_t>(sj - sn) << 16) | (static_cast<uint32_t>(sj) & 0xffffu)) : 0u;
+      acc = ((acc + (v & 0xffffu)) & 0xffffu) | (((acc >> 16) + (v >> 16)) << 16);  // v_pk_add_u16
+      best16 = std::max(best16, static_cast<int32_t>((acc & 0xffff0000u) | (0xffffu - static_cast<uint32_t>(i + 1))));
+    }
+    const int tot = static_cast<int16_t>(acc & 0xffffu), dfin = static_cast<int32_t>(acc) >> 16;
+    const int64_t last = L1 - L2;
+    uint64_t key = 0;
+    if (o < last || (sem == Semantics::Spec || L2 == L1)) key = final_key(tot, static_cast<uint32_t>(o * L2));
+    if (o < last && L2 >= 2 && best16 != INT32_MIN) {
+      const int k = 0xffff - (best16 & 0xffff);
+      key = std::max(key, final_key((best16 >> 16) + tot - dfin, static_cast<uint32_t>(o * L2 + k)));
+    }
+    best_key = std::max(best_key, key);
+  }
+  return decode_key(best_key, std::max<int64_t>(L2, 1));
+}
+
+// The int32 hot keys of the short (non-Pk) and LUT tile kernels (HotKey<false>, kernel_common.hpp).
+Result key32_record(const ScoreTable& t, const std::vector<uint8_t>& s1, const uint8_t* s2, int64_t L2, int shift,
+                    Semantics sem) {
+  const int64_t L1 = static_cast<int64_t>(s1.size());
+  if (L2 > L1) return Result{kNoCandidateScore, 0, 0};
+  const int mask = (1 << shift) - 1;
+  uint64_t best_key = 0;
+  for (int64_t o = 0; o <= L1 - L2; ++o) {
+    int P = 0, Pn = 0;
+    int32_t best = INT32_MIN;
+    for (int64_t i = 0; i < L2; ++i) {
+      P += S(t, s1, s2[i], o + i);
+      Pn += S(t, s1, s2[i], o + i + 1);
+      const int32_t key = static_cast<int32_t>((static_cast<uint32_t>(P - Pn) << shift) | static_cast<uint32_t>(mask - (i + 1)));
+      best = std::max(best, key);
+    }
+    const int64_t last = L1 - L2;
+    uint64_t key = 0;
+    if (o < last || (sem == Semantics::Spec || L2 == L1)) key = final_key(P, static_cast<uint32_t>(o * L2));
+    if (o < last && L2 >= 2)
+      key = std::max(key, final_key((best >> shift) + Pn, static_cast<uint32_t>(o * L2 + (mask - (best & mask)))));
+    best_key = std::max(best_key, key);
+  }
+  return decode_key(best_key, L2);
+}
+
+// tile16_search_kernel + resolve_long_kernel (tile16_kernels.hip, align_kernels.hip) over a Profile16 whose
+// bytes are taken as given (so a profile built past the bound wraps as the kernel would see it).
+Result tile16_record(const ScoreTable& t, const std::vector<uint8_t>& s1, const std::vector<uint16_t>& prof,
+                     const uint8_t* s2, int64_t L2, int64_t span, Semantics sem) {
+  const int64_t L1 = static_cast<int64_t>(s1.size());
+  auto entry = [&](int c, int64_t j) { return prof[static_cast<size_t>((c - 1) * L1 + j)]; };
+  const int64_t need = L2 <= L1 ? L1 - L2 + 1 : 0;
+  if (!need) return Result{kNoCandidateScore, 0, 0};
+  std::vector<int32_t> Dc(static_cast<size_t>(need) + 1, 0), maxD(static_cast<size_t>(need) + 1, INT32_MIN);
+  for (int64_t o = 0; o < need; ++o)
+    for (int64_t i0 = 0; i0 < L2; i0 += bounds::kProf16Fold) {
+      const int64_t m = std::min<int64_t>(bounds::kProf16Fold, L2 - i0);
+      uint16_t accD = 0;
+      int16_t bestD = INT16_MIN;
+      bool any = false;
+      for (int64_t j = 0; j < m; ++j) {
+        const uint16_t e = entry(s2[i0 + j], (o & ~int64_t{1}) + i0 + j);
+        const int8_t d = static_cast<int8_t>(o & 1 ? e >> 8 : e & 0xff);
+        accD = static_cast<uint16_t>(accD + static_cast<uint16_t>(static_cast<int16_t>(d)));
+        if (i0 + j + 1 < L2) {
+          bestD = std::max(bestD, static_cast<int16_t>(accD));
+          any = true;
+        }
+      }
+      if (any) maxD[o] = std::max(maxD[o], Dc[o] + bestD);
+      Dc[o] += static_cast<int16_t>(accD);
+    }
+  std::vector<int32_t> tot(static_cast<size_t>(need) + 1, 0);
+  for (int64_t o0 = 0; o0 < need; o0 += span) {
+    const int64_t oA = std::min<int64_t>(o0 + span, need);
+    int32_t acc = 0;
+    for (int64_t i = 0; i < L2; ++i) acc += static_cast<int8_t>(t.score(s2[i], oA + i < L1 ? s1[oA + i] : 0));
+    for (int64_t o = oA - 1; o >= o0; --o) tot[o] = (acc += Dc[o]);
+  }
+  uint64_t best_key = 0;
+  const int64_t last = L1 - L2;
+  for (int64_t o = 0; o < need; ++o) {
+    if (o < last || (o == last && (sem == Semantics::Spec || L2 == L1)))
+      best_key = std::max(best_key, final_key(tot[o], static_cast<uint32_t>(2 * o)));
+    if (o < last && L2 >= 2) best_key = std::max(best_key, final_key(maxD[o] + tot[o] - Dc[o], static_cast<uint32_t>(2 * o + 1)));
+  }
+  if (!best_key) return Result{kNoCandidateScore, 0, 0};
+  const int32_t score = static_cast<int32_t>(static_cast<uint32_t>(best_key >> 32) ^ 0x80000000u);
+  const uint32_t idx = 0xffffffffu - static_cast<uint32_t>(best_key);
+  Result got{score, static_cast<int32_t>(idx >> 1), 0};
+  if (idx & 1) {  // pass 2: smallest k >= 1 on the winning diagonal
+    int32_t tot1 = 0, d = 0;
+    for (int64_t i = 0; i < L2; ++i) tot1 += t.score(s2[i], s1[got.n + 1 + i]);
+    got.k = -1;
+    for (int64_t i = 0; i + 1 < L2 && got.k < 0; ++i) {
+      d += t.score(s2[i], s1[got.n + i]) - t.score(s2[i], s1[got.n + i + 1]);
+      if (d + tot1 == score) got.k = static_cast<int32_t>(i + 1);
+    }
+  }
+  return got;
+}
+
+// Profile16 bytes without the range check (past the bound: the bytes wrap as a kernel would read them).
+std::vector<uint16_t> raw_profile16(const ScoreTable& t, const std::vector<uint8_t>& s1, int64_t overhang) {
+  const int64_t L1 = static_cast<int64_t>(s1.size());
+  std::vector<uint16_t> e(static_cast<size_t>(26 * L1 + overhang), 0);
+  for (int c = 1; c < kAlphabet; ++c)
+    for (int64_t j = 0; j < L1; ++j) {
+      auto d = [&](int64_t x) { return x < L1 ? t.score(c, s1[x]) - t.score(c, x + 1 < L1 ? s1[x + 1] : 0) : 0; };
+      e[static_cast<size_t>((c - 1) * L1 + j)] =
+          static_cast<uint16_t>((static_cast<uint32_t>(d(j + 1) & 0xff) << 8) | static_cast<uint32_t>(d(j) & 0xff));
+    }
+  return e;
+}
+
+// Counts the records whose replay differs from brute force.
+template <typename F>
+int mismatches(const ScoreTable& t, const Fixture& f, Semantics sem, F replay) {
+  int bad = 0;
+  for (int64_t r = 0; r < f.batch.size(); ++r) {
+    const Result bf = brute_force_record(t, f.s1.data(), static_cast<int64_t>(f.s1.size()), f.batch.record(r),
+                                         f.batch.length(r), sem);
+    bad += same(replay(f.batch.record(r), f.batch.length(r)), bf) ? 0 : 1;
+  }
+  return bad;
+}
+}  // namespace xv
+
+void test_swipe_replay_bounds() {
+  using namespace xv;
+  // (L1, record lengths): records <= 16 letters (4 record words, 5 k bits), <= 32 (8 words, 6 k bits),
+  // 33..64 (16 words: RK only). W1 = W4 = w, W2 = W3 = 0: Dt = 2w at every step of an even-offset piece.
+  struct Case {
+    int64_t L1, lo, hi;
+  };
+  for (const Case cs : {Case{40, 6, 16}, Case{60, 20, 32}, Case{70, 40, 64}, Case{100, 40, 64}}) {
+    const Fixture f = azaz(cs.L1, cs.lo, cs.hi, static_cast<uint32_t>(cs.L1));
+    const int l2w = bounds::swipe_record_words(f.max_l2), kb = bounds::swipe_kbits(l2w);
+    const int64_t need = cs.L1 - f.min_l2 + 1;
+    const int noff = static_cast<int>(((std::max<int64_t>(need, 2) + 7) / 8) * 8);
+    const int steps = static_cast<int>(f.max_l2);
+    // the largest w of each form, from the rule itself
+    int w_kbits = 0, w_rk = 0;
+    for (int w = 1; w <= 300; ++w) {
+      const bounds::SwipeKeys k = bounds::swipe_keys(w, f.max_l2);
+      if (k == bounds::SwipeKeys::KBits) w_kbits = w;
+      if (k == bounds::SwipeKeys::RK) w_rk = w;
+    }
+    CHECK(w_rk == bounds::kSwipeMaxWeight);  // the int8 anchor LUT ends the RK form (W <= 127)
+    if (l2w == 16) CHECK(w_kbits == 0);      // 33..64-letter records: RK only
+    if (l2w == 4) CHECK(w_kbits == 31);      // 2*31*16*32 + 32 < 32767 <= 2*32*16*32 + 32
+    if (l2w == 8) CHECK(w_kbits == 7);       // 2*7*32*64 + 64 < 32767 <= 2*8*32*64 + 64
+    for (Semantics sem : {Semantics::Reference, Semantics::Spec}) {
+      if (w_kbits > 0) {
+        const ScoreTable at = ScoreTable::build(Weights{{w_kbits, 0, 0, w_kbits}});
+        CHECK(mismatches(at, f, sem, [&](const uint8_t* s2, int64_t L2) {
+                return swipe_record(at, f.s1, s2, L2, noff, kb, false, steps, f.max_l2, sem);
+              }) == 0);
+        // one past: the rule takes the RK form, which is exact there, and the k-bit keys would wrap
+        const ScoreTable past = ScoreTable::build(Weights{{w_kbits + 1, 0, 0, w_kbits + 1}});
+        CHECK(bounds::swipe_keys(w_kbits + 1, f.max_l2) == bounds::SwipeKeys::RK);
+        CHECK(mismatches(past, f, sem, [&](const uint8_t* s2, int64_t L2) {
+                return swipe_record(past, f.s1, s2, L2, noff, kb, true, steps, f.max_l2, sem);
+              }) == 0);
+        CHECK(mismatches(past, f, sem, [&](const uint8_t* s2, int64_t L2) {
+                return swipe_record(past, f.s1, s2, L2, noff, kb, false, steps, f.max_l2, sem);
+              }) > 0);
+      }
+      const ScoreTable at = ScoreTable::build(Weights{{w_rk, 0, 0, w_rk}});
+      CHECK(mismatches(at, f, sem, [&](const uint8_t* s2, int64_t L2) {
+              return swipe_record(at, f.s1, s2, L2, noff, kb, true, steps, f.max_l2, sem);
+            }) == 0);
+      // W = 128: no swipe form; the int8 anchor LUT would read -128 (where the anchor diagonal NOFF + i
+      // meets Seq1 at all: with NOFF >= L1 it reads only the zero pad)
+      CHECK(bounds::swipe_keys(w_rk + 1, f.max_l2) == bounds::SwipeKeys::None);
+      const ScoreTable past = ScoreTable::build(Weights{{w_rk + 1, 0, 0, w_rk + 1}});
+      const int bad = mismatches(past, f, sem, [&](const uint8_t* s2, int64_t L2) {
+        return swipe_record(past, f.s1, s2, L2, noff, kb, true, steps, f.max_l2, sem);
+      });
+      CHECK(noff >= cs.L1 ? bad == 0 : bad > 0);
+    }
+  }
+}
+
+void test_short_replay_bounds() {
+  using namespace xv;
+  // records of 67..85 letters under a 130-letter Seq1: <= 64 lanes per record, too long for the swipe kernel
+  const Fixture f = azaz(130, 67, 85, 5);
+  const int steps = static_cast<int>(f.max_l2);
+  int w_pk = 0;
+  for (int w = 1; w <= 400; ++w)
+    if (bounds::short_pk_exact(w, f.max_l2)) w_pk = w;
+  CHECK(w_pk == 192);  // 2*192*85 = 32640 < 32767 <= 2*193*85
+  for (Semantics sem : {Semantics::Reference, Semantics::Spec}) {
+    const ScoreTable at = ScoreTable::build(Weights{{w_pk, 0, 0, w_pk}});
+    CHECK(mismatches(at, f, sem, [&](const uint8_t* s2, int64_t L2) { return short_pk_record(at, f.s1, s2, L2, steps, sem); }) == 0);
+    const ScoreTable past = ScoreTable::build(Weights{{w_pk + 1, 0, 0, w_pk + 1}});
+    CHECK(mismatches(past, f, sem, [&](const uint8_t* s2, int64_t L2) { return short_pk_record(past, f.s1, s2, L2, steps, sem); }) > 0);
+    // past the packed form: int32 keys, exact up to their own bound and wrapping one past it
+    const int shift = bounds::key_shift(w_pk + 1, f.max_l2);
+    CHECK(shift == 7);
+    CHECK(mismatches(past, f, sem, [&](const uint8_t* s2, int64_t L2) { return key32_record(past, f.s1, s2, L2, shift, sem); }) == 0);
+    int w32 = 0;
+    for (int w = 98000; w <= 99000; ++w)
+      if (bounds::key_shift(w, f.max_l2) == shift) w32 = w;
+    CHECK(w32 == 98689);  // 2*98689*85 << 7 < 2^31 <= 2*98690*85 << 7
+    CHECK(bounds::key_shift(w32 + 1, f.max_l2) == 0);
+    const ScoreTable at32 = ScoreTable::build(Weights{{w32, 0, 0, w32}});
+    CHECK(mismatches(at32, f, sem, [&](const uint8_t* s2, int64_t L2) { return key32_record(at32, f.s1, s2, L2, shift, sem); }) == 0);
+    const ScoreTable past32 = ScoreTable::build(Weights{{w32 + 1, 0, 0, w32 + 1}});
+    CHECK(mismatches(past32, f, sem, [&](const uint8_t* s2, int64_t L2) { return key32_record(past32, f.s1, s2, L2, shift, sem); }) > 0);
+  }
+}
+
+void test_tile16_replay_bounds() {
+  using namespace xv;
+  // long records (several 64-step folds) under a 600-letter Seq1; W1 + W4 = 127 is the largest Dt a byte holds
+  const Fixture f = azaz(600, 150, 400, 9);
+  for (Semantics sem : {Semantics::Reference, Semantics::Spec}) {
+    for (int64_t span : {512, 1024}) {
+      const ScoreTable at = ScoreTable::build(Weights{{63, 0, 0, 64}});
+      CHECK(profile16_fits(at));
+      Profile16 prof;
+      CHECK(build_profile16(at, f.s1.data(), 600, span, prof));
+      CHECK(mismatches(at, f, sem, [&](const uint8_t* s2, int64_t L2) {
+              return tile16_record(at, f.s1, prof.entries, s2, L2, span, sem);
+            }) == 0);
+      const ScoreTable past = ScoreTable::build(Weights{{64, 0, 0, 64}});
+      CHECK(!profile16_fits(past) && !build_profile16(past, f.s1.data(), 600, span, prof));
+      const std::vector<uint16_t> wrapped = raw_profile16(past, f.s1, span);
+      CHECK(mismatches(past, f, sem, [&](const uint8_t* s2, int64_t L2) {
+              return tile16_record(past, f.s1, wrapped, s2, L2, span, sem);
+            }) > 0);
+    }
+  }
+}
+
 int main() {
   const std::vector<std::pair<const char*, std::function<void()>>> tests = {
       {"score_table", test_score_table}, {"parser", test_parser},     {"stream_reader", test_stream_reader},
@@ -995,7 +1366,8 @@ int main() {
       {"narrow_lengths", test_narrow_lengths}, {"result_formats", test_result_formats},
       {"write_runs", test_write_runs},   {"pack33", test_pack33},
       {"kfd_topology", test_kfd_topology}, {"kfd_topology_8gpu", test_kfd_topology_8gpu},
-      {"cutter_count_ahead", test_cutter_count_ahead}};
+      {"cutter_count_ahead", test_cutter_count_ahead}, {"swipe_replay_bounds", test_swipe_replay_bounds},
+      {"short_replay_bounds", test_short_replay_bounds}, {"tile16_replay_bounds", test_tile16_replay_bounds}};
   for (const auto& t : tests) {
     const int before = g_failed;
     t.second();

@@ -14,7 +14,9 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # MOC_LIB_PATH selects an alternative build of the same library (A/B kernel experiments, the
-# `make debug-kernels` build); the default is the in-tree build.
+# `make debug-kernels` build); the default is the in-tree build. A library whose kernels were built with
+# extra defines (moc_build_info) loads only with MOC_ALLOW_VARIANT_LIB=1: a variant can compute different
+# results and must never stand in for the product silently.
 LIB_PATH = os.environ.get("MOC_LIB_PATH") or os.path.join(_HERE, "lib", "libmoc.so")
 
 RESULT_DTYPE = np.dtype([("score", "<i4"), ("n", "<i4"), ("k", "<i4")])
@@ -48,6 +50,8 @@ def _decl(lib):
         "moc_problem_offsets": (c_void_p, [c_void_p]),
         "moc_format_results": (c_int64, [c_void_p, c_int64, c_int64, c_void_p, c_int64]),
         "moc_score_table": (c_int, [P(c_int32), c_void_p, c_void_p]),
+        "moc_kernel_bounds": (c_int, [P(c_int32), c_int64, c_int64, c_int64, c_void_p]),
+        "moc_build_info": (c_char_p, []),
         "moc_packed5_bytes": (c_int64, [c_int64]),
         "moc_pack5": (c_int, [c_void_p, c_int64, c_void_p]),
         "moc_unpack5": (c_int, [c_void_p, c_int64, c_int64, c_void_p]),
@@ -113,8 +117,23 @@ def lib():
                 "(or `python -c 'import __graft_entry__ as g; g.build()'`) first")
         l = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
         _decl(l)
+        info = build_info(l)
+        if info.get("defs") and os.environ.get("MOC_ALLOW_VARIANT_LIB") != "1":
+            raise NativeError(f"{LIB_PATH} is a variant build (kernel defines: {info['defs']}); "
+                              "set MOC_ALLOW_VARIANT_LIB=1 to load it on purpose")
         _lib = l
     return _lib
+
+
+def build_info(l=None) -> dict:
+    """{"src": source hash, "defs": -D flags of the kernel objects} of the loaded library ({} for builds that
+    predate moc_build_info)."""
+    l = l or lib()
+    if not hasattr(l, "moc_build_info"):
+        return {}
+    s = l.moc_build_info().decode()
+    src, _, defs = s.partition(" defs=")
+    return {"src": src[len("src="):], "defs": defs.strip()}
 
 
 def check(rc):

@@ -252,6 +252,13 @@ class HipSearchEngine:
         fid = _format_id(fmt)
         assert letters_t.dtype == torch.uint8 and offsets_t.dtype == torch.int64 and offsets_t.numel() == n + 1
         assert out_t.dtype == torch.uint8 and out_t.numel() >= n * _lib.FORMAT_DTYPES[fid].itemsize
+        if n > 0:
+            # the kernel sizes its LDS and per-lane record words from l2_range and cannot re-scan device
+            # lengths: a range narrower than the batch would give wrong results, so it is checked here
+            d = offsets_t[1:] - offsets_t[:-1]
+            lo, hi = int(d.min()), int(d.max())
+            if lo < int(l2_range[0]) or hi > int(l2_range[1]):
+                raise ValueError(f"l2_range {tuple(l2_range)} does not hold the batch's lengths [{lo}, {hi}]")
         lp = ctypes.c_void_p(lengths_t.data_ptr()) if lengths_t is not None else None
         _lib.check(_lib.lib().moc_engine_solve_wire_device(
             self._h, ctypes.c_void_p(letters_t.data_ptr()), ctypes.c_void_p(offsets_t.data_ptr()), lp,
@@ -327,7 +334,25 @@ class HipSearchEngine:
         d["r2"] = tuple(int(x) for x in list(v)[10:13])
         d["format"] = _lib.FORMAT_NAMES[int(d["format"])]
         d["kernels"] = [k for b, k in ((1, "swipe"), (2, "short"), (4, "tiles"), (8, "tile16")) if int(d["kernels"]) & b]
+        d["forms"] = [k for b, k in FORM_NAMES if int(v[13]) & b]
         return d
+
+
+# Arithmetic forms of the kernels (csrc/include/moc/kernel_bounds.hpp FormBits), as stats()["forms"] names them.
+FORM_NAMES = ((1, "swipe_kbits"), (2, "swipe_rk"), (4, "short_pk"), (8, "short_key32"), (16, "short_key64"),
+              (32, "tile16"), (64, "tiles_key32"), (128, "tiles_key64"), (256, "mfma"))
+
+
+def kernel_bounds(weights, L1: int, min_l2: int, max_l2: int) -> dict:
+    """The host's exactness rules for a batch (csrc/include/moc/kernel_bounds.hpp), no GPU needed:
+    ``swipe`` = "swipe_kbits" | "swipe_rk" | None (the swipe kernel's integer bounds refuse it), ``short_pk``
+    = the short kernel's packed int16 form is exact, ``key_shift`` = k bits of the int32 hot keys (0: int64
+    keys), ``profile16`` = the tile16 int8 profile holds the table."""
+    out = np.zeros(4, np.int32)
+    _lib.check(_lib.lib().moc_kernel_bounds(_lib.weights_arg(Weights.of(weights).as_list()), int(L1), int(min_l2),
+                                            int(max_l2), _lib.ptr(out)))
+    swipe = {1: "swipe_kbits", 2: "swipe_rk"}.get(int(out[0]))
+    return {"swipe": swipe, "short_pk": bool(out[1]), "key_shift": int(out[2]), "profile16": bool(out[3])}
 
 
 def search_hip(problem: Problem, semantics=Semantics.REFERENCE, device: Optional[int] = None,

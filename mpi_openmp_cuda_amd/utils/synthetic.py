@@ -50,3 +50,32 @@ def fill_codes(out: np.ndarray, seed: int, chunk: int = 1 << 26):
     for b in range(0, out.shape[0], chunk):
         e = min(out.shape[0], b + chunk)
         out[b:e] = rng.integers(1, 27, size=e - b, dtype=np.uint8)
+
+
+A, Z = 1, 26  # letter codes of 'A' and 'Z': in no group together, so a pair is '$' or ' '
+
+
+def make_extreme(L1: int, l2_min: int, l2_max: int, weights, copies: int = 1, seed: int = 0) -> Problem:
+    """Adversarial records for the kernels' integer bounds (csrc/include/moc/kernel_bounds.hpp): Seq1 =
+    "AZAZ...", and records that are pieces of Seq1 at even offsets (with W1 = W4 every step adds the largest
+    difference Dt = W1 + W4, so |D| reaches 2 W L2) and at odd ones (-(W1 + W4)), constant 'A' / 'Z' records,
+    A/Z noise and random letters, at the extreme lengths of [l2_min, l2_max]. The periodic Seq1 makes most
+    offsets tie, so the reference's tie-break (smallest offset, then k = 0) decides. ``copies`` repeats the
+    list (shuffled) so the GPU kernels see every record length mixed in their waves."""
+    rng = np.random.default_rng(seed)
+    s1 = np.where(np.arange(L1) % 2 == 0, A, Z).astype(np.uint8)
+    recs = []
+    for L2 in sorted({l2_min, l2_max, (l2_min + l2_max) // 2, max(l2_min, l2_max - 1)}):
+        for at in (0, 1, L1 - L2, L1 - L2 - 1):
+            if 0 <= at and at + L2 <= L1:
+                recs.append(s1[at:at + L2].copy())
+        recs.append(np.full(L2, A, np.uint8))
+        recs.append(np.full(L2, Z, np.uint8))
+        recs.append(np.where(rng.integers(0, 2, L2) == 0, A, Z).astype(np.uint8))
+        recs.append(rng.integers(1, 27, size=L2, dtype=np.uint8))
+    order = np.concatenate([rng.permutation(len(recs)) for _ in range(copies)])
+    lengths = np.array([len(recs[i]) for i in order], dtype=np.int64)
+    offsets = np.zeros(len(order) + 1, dtype=np.int64)
+    np.cumsum(lengths, out=offsets[1:])
+    codes = np.concatenate([recs[i] for i in order]) if len(order) else np.zeros(0, np.uint8)
+    return Problem(Weights.of(weights), s1, codes, offsets)

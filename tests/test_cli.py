@@ -341,6 +341,40 @@ def test_build_id_matches_sources():
     assert f"src={_source_hash()}" in line, line
 
 
+def test_library_is_the_product_build():
+    # the loaded libmoc.so was built from these sources with no extra kernel defines (a `make variant` or
+    # `make debug-kernels` library reports its defines and is refused by the loader)
+    from mpi_openmp_cuda_amd import _lib
+
+    info = _lib.build_info()
+    assert info == {"src": _source_hash(), "defs": ""}, info
+
+
+def test_variant_library_is_refused(tmp_path):
+    # a library whose kernel objects carry defines must not stand in for the product: the loader refuses it
+    # unless MOC_ALLOW_VARIANT_LIB=1 (built here as a one-file stand-in exporting moc_build_info)
+    import os
+    import sys
+
+    from conftest import ROOT
+
+    src = tmp_path / "v.c"
+    src.write_text('const char* moc_build_info(void) { return "src=x defs=-DMOC_T16_UNROLL=8"; }\n'
+                   'const char* moc_last_error(void) { return ""; }\n')
+    so = tmp_path / "libv.so"
+    subprocess.run(["gcc", "-shared", "-fPIC", "-o", str(so), str(src)], check=True)
+    code = ("import os, sys; sys.path.insert(0, %r)\n"
+            "from mpi_openmp_cuda_amd import _lib\n"
+            "try:\n    _lib.lib()\nexcept _lib.NativeError as e:\n    print('refused', e)\n"
+            "else:\n    print('loaded', _lib.build_info())\n") % ROOT
+    env = dict(os.environ, MOC_LIB_PATH=str(so))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.stdout.startswith("refused") and "MOC_T16_UNROLL" in r.stdout, (r.stdout, r.stderr)
+    env["MOC_ALLOW_VARIANT_LIB"] = "1"
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.stdout.startswith("loaded") and "-DMOC_T16_UNROLL=8" in r.stdout, (r.stdout, r.stderr)
+
+
 @pytest.mark.parametrize("np_", [2, 3, 8])
 @pytest.mark.parametrize("i", [1, 3, 4])
 def test_sliced_bounds_and_timing(np_, i):

@@ -1,0 +1,64 @@
+"""Narrow-integer fast paths at their exactness bounds, CPU tier (csrc/include/moc/kernel_bounds.hpp).
+
+The product's rules pick each kernel form; these tests pin where the rules put the bounds for fixed shapes
+(so a changed rule is visible), and check the CPU engine against brute force on the adversarial inputs the
+GPU tier runs at and one past each bound (tests/test_gpu.py test_extreme_values_*). The host replays of
+the forms' own arithmetic at the bounds are csrc/tests/test_core.cpp *_replay_bounds (test_native_unit.py).
+Reference arithmetic: plain int (/root/reference/cudaFunctions.cu:103,161)."""
+import numpy as np
+import pytest
+
+from mpi_openmp_cuda_amd import Semantics, brute_force_native, search_cpu
+from mpi_openmp_cuda_amd.ops.align import as_triples, kernel_bounds
+from mpi_openmp_cuda_amd.utils.synthetic import make_extreme
+
+# (name, L1, l2_min, l2_max, weights at the bound, weights one past it, bound field, value at, value past)
+BOUNDS = [
+    ("swipe_kbits_w4", 40, 6, 16, (31, 0, 0, 31), (32, 0, 0, 32), "swipe", "swipe_kbits", "swipe_rk"),
+    ("swipe_kbits_w8", 60, 20, 32, (7, 0, 0, 7), (8, 0, 0, 8), "swipe", "swipe_kbits", "swipe_rk"),
+    ("swipe_rk_w8", 60, 20, 32, (127, 0, 0, 127), (128, 0, 0, 128), "swipe", "swipe_rk", None),
+    ("swipe_rk_w16", 70, 40, 64, (127, 0, 0, 127), (128, 0, 0, 128), "swipe", "swipe_rk", None),
+    ("short_pk", 130, 67, 85, (192, 0, 0, 192), (193, 0, 0, 193), "short_pk", True, False),
+    ("short_key32", 130, 67, 85, (98689, 0, 0, 98689), (98690, 0, 0, 98690), "key_shift", 7, 0),
+    ("tile16", 600, 150, 400, (63, 0, 0, 64), (64, 0, 0, 64), "profile16", True, False),
+    ("tiles_key32", 600, 150, 400, (5242, 0, 0, 5242), (5243, 0, 0, 5243), "key_shift", 9, 0),
+]
+
+
+@pytest.mark.parametrize("case", BOUNDS, ids=[c[0] for c in BOUNDS])
+def test_bound_positions(case):
+    _, L1, lo, hi, w_at, w_past, field, at, past = case
+    assert kernel_bounds(w_at, L1, lo, hi)[field] == at
+    assert kernel_bounds(w_past, L1, lo, hi)[field] == past
+
+
+def test_extreme_fixture_reaches_the_bound():
+    # an even-offset piece of "AZAZ..." under W1 = W4 = w: every step adds Dt = 2w, so the diagonal difference
+    # D_o(L2) is exactly the 2 w L2 the rules bound
+    prob = make_extreme(40, 6, 16, (31, 0, 0, 31))
+    s1 = prob.seq1
+    lut = np.where(np.arange(27)[:, None] == np.arange(27)[None, :], 31, -31)
+    for i in range(prob.n):
+        r = prob.codes[prob.offsets[i]:prob.offsets[i + 1]]
+        if len(r) == 16 and np.array_equal(r, s1[:16]):
+            d = sum(int(lut[c, s1[j]]) - int(lut[c, s1[j + 1]]) for j, c in enumerate(r))
+            assert d == 2 * 31 * 16
+            break
+    else:
+        pytest.fail("no even-offset piece of Seq1 in the fixture")
+
+
+@pytest.mark.parametrize("case", [c for c in BOUNDS if c[1] <= 130], ids=[c[0] for c in BOUNDS if c[1] <= 130])
+@pytest.mark.parametrize("sem", [Semantics.REFERENCE, Semantics.SPEC])
+def test_cpu_engine_at_bounds(case, sem):
+    # the oracle the GPU tier compares with: the CPU engine equals brute force on every adversarial input
+    _, L1, lo, hi, w_at, w_past, *_ = case
+    for w in (w_at, w_past):
+        prob = make_extreme(L1, lo, hi, w, seed=L1)
+        assert np.array_equal(as_triples(search_cpu(prob, sem)), as_triples(brute_force_native(prob, sem))), w
+
+
+def test_cpu_engine_long_extremes():
+    # the tile16 shape: records of 150..400 letters under Seq1 = "AZ" * 300, W1 + W4 = 127
+    prob = make_extreme(600, 150, 400, (63, 0, 0, 64), seed=3)
+    assert np.array_equal(as_triples(search_cpu(prob)), as_triples(brute_force_native(prob)))

@@ -1003,3 +1003,129 @@ def test_wire_device_resident(engine, shape, n):
     got = wire.triples(engine)
     ref = as_triples(search_cpu(prob))
     assert np.array_equal(got, ref)
+
+
+# ---- narrow-integer fast paths at their exactness bounds (csrc/include/moc/kernel_bounds.hpp) --------------
+# Every case runs the adversarial input (utils/synthetic.make_extreme: Seq1 = "AZAZ...", pieces of it at even
+# and odd offsets, so |D| reaches 2 W L2 exactly) at the bound — the fast form must be chosen and exact — and
+# one step past it — the rule must fall back to the next form, also exact. The CPU tier pins the same
+# bounds (tests/test_extremes.py) and replays each form's arithmetic (csrc/tests/test_core.cpp).
+EXTREMES = [
+    # name, L1, l2 range, weights, kernels, forms
+    ("swipe_kbits_at", 40, 6, 16, (31, 0, 0, 31), ["swipe"], ["swipe_kbits"]),
+    ("swipe_kbits_past", 40, 6, 16, (32, 0, 0, 32), ["swipe"], ["swipe_rk"]),
+    ("swipe_kbits_w8_at", 60, 20, 32, (7, 0, 0, 7), ["swipe"], ["swipe_kbits"]),
+    ("swipe_kbits_w8_past", 60, 20, 32, (8, 0, 0, 8), ["swipe"], ["swipe_rk"]),
+    ("swipe_rk_at", 70, 40, 64, (127, 0, 0, 127), ["swipe"], ["swipe_rk"]),
+    ("swipe_rk_past", 70, 40, 64, (128, 0, 0, 128), ["short"], ["short_pk"]),
+    ("short_pk_at", 130, 67, 85, (192, 0, 0, 192), ["short"], ["short_pk"]),
+    ("short_pk_past", 130, 67, 85, (193, 0, 0, 193), ["short"], ["short_key32"]),
+    ("short_key32_at", 130, 67, 85, (98689, 0, 0, 98689), ["short"], ["short_key32"]),
+    ("short_key32_past", 130, 67, 85, (98690, 0, 0, 98690), ["short"], ["short_key64"]),
+    ("tile16_at", 600, 150, 400, (63, 0, 0, 64), ["tile16"], ["tile16"]),
+    ("tile16_past", 600, 150, 400, (64, 0, 0, 64), ["tiles"], ["tiles_key32"]),
+    ("tiles_key32_at", 600, 150, 400, (5242, 0, 0, 5242), ["tiles"], ["tiles_key32"]),
+    ("tiles_key32_past", 600, 150, 400, (5243, 0, 0, 5243), ["tiles"], ["tiles_key64"]),
+]
+
+
+def _extreme_ref(prob, sem):
+    # brute force where it is cheap; the CPU engine (itself pinned to brute force on these inputs by
+    # tests/test_extremes.py) for the 600-letter Seq1
+    return as_triples(brute_force_native(prob, sem) if prob.L1 <= 130 else search_cpu(prob, sem))
+
+
+@pytest.mark.parametrize("case", EXTREMES, ids=[c[0] for c in EXTREMES])
+@pytest.mark.parametrize("sem", [Semantics.REFERENCE, Semantics.SPEC])
+def test_extreme_values_staged(engine, case, sem):
+    _, L1, lo, hi, w, kernels, forms = case
+    from mpi_openmp_cuda_amd.utils.synthetic import make_extreme
+
+    prob = make_extreme(L1, lo, hi, w, copies=40 if L1 <= 130 else 3, seed=L1)
+    engine.set_problem(prob.weights, prob.seq1, sem)
+    got = engine.solve(prob.codes, prob.offsets, fmt="auto")
+    st = engine.stats()
+    assert (st["kernels"], st["forms"]) == (kernels, forms), st
+    assert np.array_equal(as_triples(got, r2=st["r2"]), _extreme_ref(prob, sem)), st
+
+
+@pytest.mark.parametrize("case", [c for c in EXTREMES if c[5] == ["swipe"]], ids=[c[0] for c in EXTREMES if c[5] == ["swipe"]])
+def test_extreme_values_wire_p33(case):
+    # the headline's data path: P33 letters + narrow lengths + the narrowest results, zero-copy from pinned memory
+    _, L1, lo, hi, w, kernels, forms = case
+    from mpi_openmp_cuda_amd._lib import Pinned
+    from mpi_openmp_cuda_amd.parallel.wire import WireSlice
+    from mpi_openmp_cuda_amd.utils.synthetic import make_extreme
+
+    prob = make_extreme(L1, lo, hi, w, copies=60, seed=L1 + 1)
+    eng = HipSearchEngine(device=0)
+    eng.set_problem(prob.weights, prob.seq1)
+    ws = WireSlice.from_csr(prob.codes, prob.offsets, letter_format="p33")
+    ws.alloc_results(eng)
+    with Pinned(*ws.arrays()):
+        ws.solve(eng)
+    st = eng.stats()
+    assert (st["kernels"], st["forms"], st["direct"]) == (kernels, forms, 1), st
+    assert np.array_equal(ws.triples(eng), _extreme_ref(prob, Semantics.REFERENCE)), st
+    eng.close()
+
+
+@pytest.mark.parametrize("case", [c for c in EXTREMES if c[5] == ["swipe"]], ids=[c[0] for c in EXTREMES if c[5] == ["swipe"]])
+def test_extreme_values_device_resident(engine, case):
+    # device-resident byte letters with dense offsets only (lengths taken from the offsets in the kernel:
+    # swipe_impl.hpp kDeferLens) and a record count that leaves a partial last tile
+    _, L1, lo, hi, w, kernels, forms = case
+    from mpi_openmp_cuda_amd.utils.synthetic import make_extreme
+
+    prob = make_extreme(L1, lo, hi, w, copies=57, seed=L1 + 2)
+    dev = torch.device("cuda:0")
+    engine.set_problem(prob.weights, prob.seq1)
+    fmt = engine.auto_format(hi, lo)
+    from mpi_openmp_cuda_amd import _lib
+
+    item = _lib.FORMAT_DTYPES[_lib.FORMAT_NAMES.index(fmt)].itemsize
+    out_t = torch.zeros(prob.n * item, dtype=torch.uint8, device=dev)
+    engine.solve_wire_device(torch.from_numpy(prob.codes).to(dev), torch.from_numpy(prob.offsets).to(dev), None,
+                             prob.n, out_t, fmt, (int(np.diff(prob.offsets).min()), int(np.diff(prob.offsets).max())),
+                             packed33=False)
+    st = engine.stats()
+    assert (st["kernels"], st["forms"]) == (kernels, forms), st
+    res = out_t.cpu().numpy().view(_lib.FORMAT_DTYPES[_lib.FORMAT_NAMES.index(fmt)])[:prob.n]
+    r2 = engine.r2_params(lo, hi) if fmt == "r2" else None
+    assert np.array_equal(as_triples(res, r2=r2), _extreme_ref(prob, Semantics.REFERENCE)), st
+
+
+def test_extreme_values_wire_range_checked(engine):
+    # a device batch whose stated length range is narrower than its records is refused (the kernel would
+    # size its LDS from the range)
+    from mpi_openmp_cuda_amd.utils.synthetic import make_extreme
+
+    prob = make_extreme(40, 6, 16, (4, 3, 2, 10), copies=5)
+    dev = torch.device("cuda:0")
+    engine.set_problem(prob.weights, prob.seq1)
+    out_t = torch.zeros(prob.n * 12, dtype=torch.uint8, device=dev)
+    with pytest.raises(ValueError):
+        engine.solve_wire_device(torch.from_numpy(prob.codes).to(dev), torch.from_numpy(prob.offsets).to(dev), None,
+                                 prob.n, out_t, "r12", (6, 12), packed33=False)
+
+
+@pytest.mark.parametrize("w,fmt", [(3, "r2"), (4, "r4"), (2047, "r4"), (2048, "r8")])
+def test_extreme_values_result_formats(engine, w, fmt):
+    # result codes at their bounds: R2 holds (2 w 16 + 1) * 35 * 16 codes <= 65535 up to w = 3; R4's int16
+    # score holds w * 16 < 32767 up to w = 2047
+    from mpi_openmp_cuda_amd.utils.synthetic import make_extreme
+
+    prob = make_extreme(40, 6, 16, (w, 0, 0, w), copies=20, seed=w)
+    engine.set_problem(prob.weights, prob.seq1)
+    assert engine.auto_format(16, 6) == fmt
+    got = engine.solve(prob.codes, prob.offsets, fmt="auto")
+    st = engine.stats()
+    assert st["format"] == fmt, st
+    ref = as_triples(brute_force_native(prob))
+    assert np.array_equal(as_triples(got, r2=st["r2"]), ref), st
+    assert ref[:, 0].max() == 16 * w  # the top of the score range is exercised (a whole even piece of Seq1)
+    if fmt == "r8" and w == 2048:
+        from mpi_openmp_cuda_amd._lib import NativeError
+
+        with pytest.raises(NativeError):
+            engine.solve(prob.codes, prob.offsets, fmt="r4")

@@ -15,7 +15,7 @@
 #   copy-probe    the first host->device copy's cost by size, with and without SDMA (tools/copy_path_probe.hip)
 #   kernels       device-resident kernel throughput (tools/kernel_bench.py)
 #   swipe-ab      kernel_bench on input6 / input1 for the in-tree library and every build/variant_*/libmoc.so
-#                 (make variant NAME=... VDEFS=...: A/B builds, e.g. -DMOC_SWIPE_AB=1)
+#                 (make variant NAME=... VDEFS=...: A/B builds, e.g. -DMOC_T16_UNROLL=32)
 #   isolate       --gpu-isolate=1 at np 1/2 (the rank's runtime shows its GPU only)
 #   hello-env     tools/hip_hello.hip's runtime / first-queue times under runtime environment settings
 # Longer studies have scripts of their own: step_variance.sh, pmc_ab.sh, rehearse_ranks.sh,
