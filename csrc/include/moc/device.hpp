@@ -150,6 +150,8 @@ struct ShortArgs {
   int32_t swipe_rk = 0;               // swipe: 1 = keys without k bits, k re-found on the winning diagonal
   int32_t packed33 = 0;               // 1: `codes` holds P33 fields (moc::pack33: char j in field j / 7 at
                                       // bit 33 * (j / 7)); decoded into LDS per tile; swipe only
+  int32_t lane_direct = 0;            // swipe: 1 = device-resident byte letters with dense offsets, read by
+                                      // each lane straight into registers (swipe_direct_kernel; no counter)
   unsigned* counter = nullptr;        // device work counter {next tile, blocks done}; zero at launch, the
                                       // kernel's last block resets it (no memset between launches)
   int64_t dbg_codes_end = -1;         // debug builds: end of the readable letter bytes (from `codes`)

@@ -97,6 +97,166 @@ inline SwipeLayout swipe_layout(int L1, int noff, int l2w, int tile_records, int
 
 using namespace swipe;
 
+// The block's LDS tables, built once per block (before a barrier): kCopies shifted difference-profile
+// copies, the anchor LUT and Seq1's codes.
+template <bool RK, int KB>
+__device__ __forceinline__ void swipe_build_tables(short* prof, int8_t* lut8, uint8_t* s1l, const SwipeLayout& lay,
+                                                   const ProblemView& pv, int tid, int nthreads) {
+  // ---- kCopies shifted int16 difference-profile copies: prof[s][c][j] = Pf[c][j + s], and the plain S rows.
+  //      Rows are 128-byte multiples, so the 16-byte chunk q of every row would start on the same LDS
+  //      bank; chunk q of row c is stored at chunk q ^ (c & 7) instead, spreading the 16 lanes of a
+  //      ds_read_b128 group (16 records reading 16 rows) over 8 bank quads — 8-way -> ~2-way conflicts.
+  const int L1 = pv.L1;
+  const int row = lay.row, ce = lay.copy_elems;
+  for (int e = tid; e < kCopies * ce; e += nthreads) {
+    const int s = e / ce, rem = e - s * ce, c = rem / row, jj = rem - c * row;
+    const int j = ((((jj >> 3) ^ (c & 7)) << 3) | (jj & 7)) + s;  // element stored at jj holds column j
+    const int sj = (c >= 1 && j < L1) ? pv.lut[c * kLutStride + pv.seq1[j]] : 0;
+    const int sn = (c >= 1 && j + 1 < L1) ? pv.lut[c * kLutStride + pv.seq1[j + 1]] : 0;
+    prof[e] = static_cast<short>(RK ? sj - sn : (sj - sn) * (1 << KB) - 1);  // Pf = Dt * 2^KB - 1 (header)
+  }
+  // the anchor LUT stored by Seq1 letter: entry (y << 5) | c = T[c][y]. A step's Seq1 letter y is the same
+  // for every lane, so the wave's reads fall in one 32-byte row (8 banks, no conflicts); indexed by the
+  // lane's letter c first, 26 rows 32 bytes apart hit the same banks every 8 letters (up to 4-way).
+  // Letter 0 (padding: steps past a lane's record) and Seq1 letter 31 (past Seq1) contribute 0.
+  for (int e = tid; e < kLutInts; e += nthreads) {
+    const int y = e >> 5, c = e & 31;
+    lut8[e] = static_cast<int8_t>(y == 31 || c == 0 ? 0 : pv.lut[c * kLutStride + y]);
+  }
+  for (int j = tid; j < row; j += nthreads) s1l[j] = j < L1 ? pv.seq1[j] : 31;
+}
+
+// A record's letters (rs = byte position of its first letter in `l32`) -> NW aligned words, bits past the
+// record end zeroed (they add row 0 = 0). Lanes that are not `on` get zeros and read nothing.
+template <int NW>
+__device__ __forceinline__ void record_words(const uint32_t* l32, int rs, int L2, bool on, uint32_t (&wd)[NW]) {
+  const int wb = rs >> 2;
+  const int sh = (rs & 3) * 8;
+  const int rbits = 8 * L2;
+  uint32_t prev = on ? l32[wb] : 0u;
+#pragma unroll
+  for (int k = 0; k < NW; ++k) {
+    const uint32_t nxt = on ? l32[wb + k + 1] : 0u;
+    uint32_t w = sh ? ((prev >> sh) | (nxt << (32 - sh))) : prev;
+    const int left = rbits - 32 * k;  // record bits in this word
+    w = left >= 32 ? w : (left <= 0 ? 0u : (w & ((1u << left) - 1u)));
+    wd[k] = on ? w : 0u;
+    prev = nxt;
+  }
+}
+
+// One lane's search of its record (NW = L2W words of letters, `on`: the lane searches; every lane of the
+// wave must call it — the step count is the wave's longest record). max_l2: the batch's longest record.
+template <int NOFF, int L2W, bool RK>
+__device__ __forceinline__ Result swipe_lane(const short* prof, const int8_t* lut8, const uint8_t* s1l,
+                                             const SwipeLayout& lay, const uint32_t (&wd)[L2W], int L2, bool on, int L1,
+                                             int max_l2, int sem) {
+  constexpr int KB = RK ? 1 : bounds::swipe_kbits(L2W);
+  constexpr int KMASK = (1 << KB) - 1;
+  constexpr int NP = NOFF / 2;  // packed accumulators
+  const int steps = wave_max_small(on ? L2 : 0);  // L2 <= 4 * L2W <= 64 here
+
+  uint32_t E2[NP], B2[NP];
+  int anchor = 0;  // Tot_NOFF: the diagonal just past this lane's offsets
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    E2[q] = RK ? 0u : (static_cast<uint32_t>(KMASK) << 16) | KMASK;  // E_o(-1) = KMASK: D 0, k 0
+    B2[q] = 0x80008000u;  // (INT16_MIN, INT16_MIN)
+  }
+#pragma unroll
+  for (int i0 = 0; i0 < 4 * L2W; i0 += 8) {
+    if (i0 >= steps) break;  // wave-uniform
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int i = i0 + s;
+      // wave-uniform (scalar branch): a wave stops at its longest record, not at the next multiple of
+      // 8 steps (input6: 11 steps instead of 16); the copy index s stays a compile-time constant
+      if (i >= steps) break;
+      const int c = (wd[i >> 2] >> (8 * (i & 3))) & 0xff;
+      const int sw = c & 7;
+      uint32_t v[NP];
+      // copy s holds column j + s at j: columns i .. i + NOFF - 1 are 16-byte chunks from i0 on
+      const uint4* rowp = reinterpret_cast<const uint4*>(prof + s * lay.copy_elems + c * lay.row);
+#pragma unroll
+      for (int q = 0; q < NOFF / 8; ++q) {
+        const uint4 x = rowp[((i0 >> 3) + q) ^ sw];
+        v[4 * q + 0] = x.x;
+        v[4 * q + 1] = x.y;
+        v[4 * q + 2] = x.z;
+        v[4 * q + 3] = x.w;
+      }
+      anchor += lut8[(s1l[NOFF + i] << 5) | c];
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        E2[q] = as_u32(as_s16x2(E2[q]) + as_s16x2(v[q]));
+        B2[q] = as_u32(__builtin_elementwise_max(as_s16x2(B2[q]), as_s16x2(E2[q])));
+      }
+    }
+  }
+
+  // ---- per-lane selection over the record's offsets: 32-bit keys (score+2^15 | ~(o<<KB | k)), 0 = none.
+  //      The valid offsets are prefixes: the un-mutated candidate at o < lim0 (o <= last = L1-L2 under
+  //      the spec semantics or when L2 == L1, else o < last), the mutants at o < lim1 = last (L2 >= 2).
+  //      Running sums carry the 2^15 bias, so a key is one shift-or of them (~13 VALU ops per offset).
+  //      RK: the low bits are ~(o << 1 | mutated); bd keeps the winning mutant's D for the k re-walk.
+  //      Offsets below L1 - max_l2 (the batch's longest record) are valid for every lane that searches
+  //      (`on`): their limits are only applied above it (wave-uniform branch).
+  const int last = L1 - L2;
+  const int lim0 = on ? last + ((sem == static_cast<int>(Semantics::Spec) || L2 == L1) ? 1 : 0) : 0;
+  const int lim1 = on && L2 >= 2 ? last : 0;
+  const int all_valid = L1 - max_l2;
+  // D_o(L2) pairs from the final running sums: (E - (KMASK - steps)) >> KB (RK: E itself)
+  const short eb = static_cast<short>(RK ? 0 : KMASK - steps);
+  const s16x2 ebias = {eb, eb};
+  uint32_t best = 0;
+  int bd = 0;  // RK: D_o(k) of the best mutant so far
+  uint32_t tot = static_cast<uint32_t>(anchor + 32768);  // Tot_{o+1} + 2^15 entering offset o
+#pragma unroll
+  for (int o = NOFF - 1; o >= 0; --o) {
+    const s16x2 dq = RK ? as_s16x2(E2[o >> 1]) : (as_s16x2(E2[o >> 1]) - ebias) >> static_cast<short>(KB);
+    const uint32_t Pn = tot;  // Tot_{o+1} + 2^15
+    const uint32_t Po = Pn + static_cast<uint32_t>(static_cast<int>(o & 1 ? dq.y : dq.x));
+    tot = Po;  // suffix pass: Tot_o = Tot_{o+1} + D_o(L2)
+    const uint32_t kLow0 = 0xffffu - (static_cast<uint32_t>(o) << KB);  // ~(o << KB | 0)
+    const uint32_t kLow1 = kLow0 - KMASK;  // its low KB bits are 0: ~(o << KB | k) = kLow1 | (KMASK - k)
+    uint32_t k0 = (Po << 16) | kLow0;
+    // bk = d * 2^KB + (KMASK - k): the best mutant's D_o(k) and its k; t = (d + Tot_{o+1} + 2^15) * 2^KB + (KMASK - k)
+    const int bk = static_cast<short>(o & 1 ? (B2[o >> 1] >> 16) : (B2[o >> 1] & 0xffff));
+    const uint32_t t = static_cast<uint32_t>(bk) + (Pn << KB);
+    uint32_t k1 = RK ? ((static_cast<uint32_t>(bk) + Pn) << 16) | (kLow0 - 1u) : ((t >> KB) << 16) | (t & KMASK) | kLow1;
+    if (o >= all_valid) {  // wave-uniform
+      k0 = o < lim0 ? k0 : 0u;
+      k1 = o < lim1 ? k1 : 0u;
+    }
+    const uint32_t nb = max(best, max(k0, k1));
+    if (RK) bd = (nb == k1 && k1 != 0u) ? bk : bd;
+    best = nb;
+  }
+  if (!on) best = 0u;
+  int kw = 0;  // RK: the winning mutant's k
+  if (RK) {
+    // the first k of the winning offset's diagonal whose D_o(k) is the best D (k < L2: a best D reached
+    // only at k >= L2 equals D_o(L2), and then the un-mutated candidate wins the tie)
+    const bool walk = best != 0u && ((0xffffu - (best & 0xffffu)) & 1u);
+    if (__builtin_amdgcn_ballot_w64(walk) != 0) {  // wave-uniform
+      const int ow = static_cast<int>((0xffffu - (best & 0xffffu)) >> 1);
+      int run = 0;
+#pragma unroll
+      for (int i = 0; i < 4 * L2W; ++i) {
+        if (i >= steps) break;  // wave-uniform
+        const int c = (wd[i >> 2] >> (8 * (i & 3))) & 0xff;
+        const int col = ow + i;  // copy 0 holds column j at ((j >> 3) ^ (c & 7)) << 3 | (j & 7)
+        run += prof[c * lay.row + ((((col >> 3) ^ (c & 7)) << 3) | (col & 7))];
+        kw = (kw == 0 && run == bd) ? i + 1 : kw;
+      }
+    }
+  }
+  if (best == 0u) return Result{INT32_MIN, 0, 0};
+  const uint32_t idx = 0xffffu - (best & 0xffffu);
+  return RK ? Result{static_cast<int>(best >> 16) - 32768, static_cast<int>(idx >> 1), (idx & 1u) ? kw : 0}
+            : Result{static_cast<int>(best >> 16) - 32768, static_cast<int>(idx >> KB), static_cast<int>(idx & KMASK)};
+}
+
 // LF: letter format of `a.codes` — 0 bytes, 2 P33 fields (decoded to bytes in LDS per tile).
 // RK: keys without k bits (the weights leave no room for them in int16): the running sums are plain
 // D_o(k), B2 keeps max_k D_o(k), and the winner's k is re-found afterwards on its diagonal.
@@ -117,8 +277,6 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
   const int L1 = pv.L1;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int KB = RK ? 1 : bounds::swipe_kbits(L2W);  // k bits of the int16 keys (moc/kernel_bounds.hpp)
-  constexpr int KMASK = (1 << KB) - 1;
-  constexpr int NP = NOFF / 2;  // packed accumulators
 
   const int fb = fmt_bytes(a.fmt);
   // tiles [0, tail_from) hold tile_records records, the rest tail_records (the batch's last work, cut finer
@@ -221,29 +379,7 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
   Fetch cur, nxt;
   fetch(grab(), cur);  // the first tile's loads are in flight while the block builds its profile
 
-  // ---- kCopies shifted int16 difference-profile copies: prof[s][c][j] = Pf[c][j + s], and the plain S rows.
-  //      Rows are 128-byte multiples, so the 16-byte chunk q of every row would start on the same LDS
-  //      bank; chunk q of row c is stored at chunk q ^ (c & 7) instead, spreading the 16 lanes of a
-  //      ds_read_b128 group (16 records reading 16 rows) over 8 bank quads — 8-way -> ~2-way conflicts.
-  {
-    const int row = lay.row, ce = lay.copy_elems;
-    for (int e = tid; e < kCopies * ce; e += kBlock) {
-      const int s = e / ce, rem = e - s * ce, c = rem / row, jj = rem - c * row;
-      const int j = ((((jj >> 3) ^ (c & 7)) << 3) | (jj & 7)) + s;  // element stored at jj holds column j
-      const int sj = (c >= 1 && j < L1) ? pv.lut[c * kLutStride + pv.seq1[j]] : 0;
-      const int sn = (c >= 1 && j + 1 < L1) ? pv.lut[c * kLutStride + pv.seq1[j + 1]] : 0;
-      prof[e] = static_cast<short>(RK ? sj - sn : (sj - sn) * (1 << KB) - 1);  // Pf = Dt * 2^KB - 1 (header)
-    }
-    // the anchor LUT stored by Seq1 letter: entry (y << 5) | c = T[c][y]. A step's Seq1 letter y is the same
-    // for every lane, so the wave's reads fall in one 32-byte row (8 banks, no conflicts); indexed by the
-    // lane's letter c first, 26 rows 32 bytes apart hit the same banks every 8 letters (up to 4-way).
-    // Letter 0 (padding: steps past a lane's record) and Seq1 letter 31 (past Seq1) contribute 0.
-    for (int e = tid; e < kLutInts; e += kBlock) {
-      const int y = e >> 5, c = e & 31;
-      lut8[e] = static_cast<int8_t>(y == 31 || c == 0 ? 0 : pv.lut[c * kLutStride + y]);
-    }
-    for (int j = tid; j < row; j += kBlock) s1l[j] = j < L1 ? pv.seq1[j] : 31;
-  }
+  swipe_build_tables<RK, KB>(prof, lut8, s1l, lay, pv, tid, kBlock);
   for (;;) {
     if (cur.t >= n_tiles) break;
     const int64_t rb = cur.rb, start = cur.start, end = cur.end;
@@ -331,133 +467,10 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
       const int need = L2 <= L1 ? L1 - L2 + 1 : 1;
       const bool mine = in && need <= NOFF;  // others belong to the tile kernel (mixed batches)
       const bool on = mine && L2 <= L1;
-      // record letters -> NW aligned words (bits past the record end zeroed: they add row 0 = 0)
       uint32_t wd[NW];
-      {
-        const uint32_t* l32 = reinterpret_cast<const uint32_t*>(codes_l);
-        const int wb = rs >> 2;
-        const int sh = (rs & 3) * 8;
-        const int rbits = 8 * L2;
-        uint32_t prev = on ? l32[wb] : 0u;
-#pragma unroll
-        for (int k = 0; k < NW; ++k) {
-          const uint32_t nxt = on ? l32[wb + k + 1] : 0u;
-          uint32_t w = sh ? ((prev >> sh) | (nxt << (32 - sh))) : prev;
-          const int left = rbits - 32 * k;  // record bits in this word
-          w = left >= 32 ? w : (left <= 0 ? 0u : (w & ((1u << left) - 1u)));
-          wd[k] = on ? w : 0u;
-          prev = nxt;
-        }
-      }
-      const int steps = wave_max_small(on ? L2 : 0);  // L2 <= 4 * L2W <= 64 here
-
-      uint32_t E2[NP], B2[NP];
-      int anchor = 0;  // Tot_NOFF: the diagonal just past this lane's offsets
-#pragma unroll
-      for (int q = 0; q < NP; ++q) {
-        E2[q] = RK ? 0u : (static_cast<uint32_t>(KMASK) << 16) | KMASK;  // E_o(-1) = KMASK: D 0, k 0
-        B2[q] = 0x80008000u;  // (INT16_MIN, INT16_MIN)
-      }
-#pragma unroll
-      for (int i0 = 0; i0 < 4 * L2W; i0 += 8) {
-        if (i0 >= steps) break;  // wave-uniform
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-          const int i = i0 + s;
-          // wave-uniform (scalar branch): a wave stops at its longest record, not at the next multiple of
-          // 8 steps (input6: 11 steps instead of 16); the copy index s stays a compile-time constant
-          if (i >= steps) break;
-          const int c = (wd[i >> 2] >> (8 * (i & 3))) & 0xff;
-          const int crow = c;
-          const int sw = c & 7;
-          uint32_t v[NP];
-          // copy s holds column j + s at j: columns i .. i + NOFF - 1 are 16-byte chunks from i0 on
-          const uint4* rowp = reinterpret_cast<const uint4*>(prof + s * lay.copy_elems + crow * lay.row);
-#pragma unroll
-          for (int q = 0; q < NOFF / 8; ++q) {
-            const uint4 x = rowp[((i0 >> 3) + q) ^ sw];
-            v[4 * q + 0] = x.x;
-            v[4 * q + 1] = x.y;
-            v[4 * q + 2] = x.z;
-            v[4 * q + 3] = x.w;
-          }
-          anchor += lut8[(s1l[NOFF + i] << 5) | c];
-#pragma unroll
-          for (int q = 0; q < NP; ++q) {
-            E2[q] = as_u32(as_s16x2(E2[q]) + as_s16x2(v[q]));
-            B2[q] = as_u32(__builtin_elementwise_max(as_s16x2(B2[q]), as_s16x2(E2[q])));
-          }
-        }
-      }
-
-      // ---- per-lane selection over the record's offsets: 32-bit keys (score+2^15 | ~(o<<KB | k)), 0 = none.
-      //      The valid offsets are prefixes: the un-mutated candidate at o < lim0 (o <= last = L1-L2 under
-      //      the spec semantics or when L2 == L1, else o < last), the mutants at o < lim1 = last (L2 >= 2).
-      //      Running sums carry the 2^15 bias, so a key is one shift-or of them (~13 VALU ops per offset).
-      //      RK: the low bits are ~(o << 1 | mutated); bd keeps the winning mutant's D for the k re-walk.
-      //      Offsets below L1 - max_l2 (the batch's longest record) are valid for every lane that searches
-      //      (`on`): their limits are only applied above it (wave-uniform branch).
-      const int last = L1 - L2;
-      const int lim0 = on ? last + ((sem == static_cast<int>(Semantics::Spec) || L2 == L1) ? 1 : 0) : 0;
-      const int lim1 = on && L2 >= 2 ? last : 0;
-      const int all_valid = L1 - a.max_l2;
-      // D_o(L2) pairs from the final running sums: (E - (KMASK - steps)) >> KB (RK: E itself)
-      const short eb = static_cast<short>(RK ? 0 : KMASK - steps);
-      const s16x2 ebias = {eb, eb};
-      uint32_t best = 0;
-      int bd = 0;  // RK: D_o(k) of the best mutant so far
-      uint32_t tot = static_cast<uint32_t>(anchor + 32768);  // Tot_{o+1} + 2^15 entering offset o
-#pragma unroll
-      for (int o = NOFF - 1; o >= 0; --o) {
-        const s16x2 dq = RK ? as_s16x2(E2[o >> 1]) : (as_s16x2(E2[o >> 1]) - ebias) >> static_cast<short>(KB);
-        const uint32_t Pn = tot;  // Tot_{o+1} + 2^15
-        const uint32_t Po = Pn + static_cast<uint32_t>(static_cast<int>(o & 1 ? dq.y : dq.x));
-        tot = Po;  // suffix pass: Tot_o = Tot_{o+1} + D_o(L2)
-        const uint32_t kLow0 = 0xffffu - (static_cast<uint32_t>(o) << KB);  // ~(o << KB | 0)
-        const uint32_t kLow1 = kLow0 - KMASK;  // its low KB bits are 0: ~(o << KB | k) = kLow1 | (KMASK - k)
-        uint32_t k0 = (Po << 16) | kLow0;
-        // bk = d * 2^KB + (KMASK - k): the best mutant's D_o(k) and its k; t = (d + Tot_{o+1} + 2^15) * 2^KB + (KMASK - k)
-        const int bk = static_cast<short>(o & 1 ? (B2[o >> 1] >> 16) : (B2[o >> 1] & 0xffff));
-        const uint32_t t = static_cast<uint32_t>(bk) + (Pn << KB);
-        uint32_t k1 = RK ? ((static_cast<uint32_t>(bk) + Pn) << 16) | (kLow0 - 1u) : ((t >> KB) << 16) | (t & KMASK) | kLow1;
-        if (o >= all_valid) {  // wave-uniform
-          k0 = o < lim0 ? k0 : 0u;
-          k1 = o < lim1 ? k1 : 0u;
-        }
-        const uint32_t nb = max(best, max(k0, k1));
-        if (RK) bd = (nb == k1 && k1 != 0u) ? bk : bd;
-        best = nb;
-      }
-      if (!on) best = 0u;
-      int kw = 0;  // RK: the winning mutant's k
-      if (RK) {
-        // the first k of the winning offset's diagonal whose D_o(k) is the best D (k < L2: a best D reached
-        // only at k >= L2 equals D_o(L2), and then the un-mutated candidate wins the tie)
-        const bool walk = best != 0u && ((0xffffu - (best & 0xffffu)) & 1u);
-        if (__builtin_amdgcn_ballot_w64(walk) != 0) {  // wave-uniform
-          const int ow = static_cast<int>((0xffffu - (best & 0xffffu)) >> 1);
-          int run = 0;
-#pragma unroll
-          for (int i = 0; i < 4 * L2W; ++i) {
-            if (i >= steps) break;  // wave-uniform
-            const int c = (wd[i >> 2] >> (8 * (i & 3))) & 0xff;
-            const int col = ow + i;  // copy 0 holds column j at ((j >> 3) ^ (c & 7)) << 3 | (j & 7)
-            run += prof[c * lay.row + ((((col >> 3) ^ (c & 7)) << 3) | (col & 7))];
-            kw = (kw == 0 && run == bd) ? i + 1 : kw;
-          }
-        }
-      }
-      if (mine) {
-        Result res;
-        if (best == 0u) {
-          res = Result{INT32_MIN, 0, 0};
-        } else {
-          const uint32_t idx = 0xffffu - (best & 0xffffu);
-          res = RK ? Result{static_cast<int>(best >> 16) - 32768, static_cast<int>(idx >> 1), (idx & 1u) ? kw : 0}
-                   : Result{static_cast<int>(best >> 16) - 32768, static_cast<int>(idx >> KB), static_cast<int>(idx & KMASK)};
-        }
-        store_result(res_l, rl, a.fmt, res, pv.r2);
-      }
+      record_words<NW>(reinterpret_cast<const uint32_t*>(codes_l), rs, L2, on, wd);
+      const Result res = swipe_lane<NOFF, L2W, RK>(prof, lut8, s1l, lay, wd, L2, on, L1, a.max_l2, sem);
+      if (mine) store_result(res_l, rl, a.fmt, res, pv.r2);
     }
     __syncthreads();
     copy_results(static_cast<char*>(a.out) + rb * fb, res_l, m * fb, tid, kBlock);
@@ -467,17 +480,104 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
 }
 
 
+// Device-resident byte batches with dense offsets (solve_device, the staged chunks, the rccl transport's
+// byte batches): each WAVE takes 64 consecutive records at a time, one per lane, loaded straight from
+// device memory into registers — no LDS staging, no block scan, and no barrier after the block's tables are
+// built. (The block-synchronous tile pipeline of swipe_search_kernel — grab, barrier, scan, barrier, copy —
+// held device-resident input6 at ~0.45 of its 0.54 ms even with the hot loop removed, round 4's A/B.)
+// Waves walk the 64-record tiles t = wave, wave + waves, ... and load the next tile's offsets while the
+// current one is scored.
+constexpr int kBlockD = 512;  // 8 waves share one set of LDS tables
+template <int NOFF, int L2W, bool RK>
+__global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, ShortArgs a, SwipeLayout lay) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  short* prof = reinterpret_cast<short*>(smem);
+  int8_t* lut8 = reinterpret_cast<int8_t*>(smem + lay.s_off);
+  uint8_t* s1l = smem + lay.s_off + kLutInts;
+  constexpr int KB = RK ? 1 : bounds::swipe_kbits(L2W);
+  swipe_build_tables<RK, KB>(prof, lut8, s1l, lay, pv, threadIdx.x, kBlockD);
+  __syncthreads();  // the only barrier: tables complete
+  const int lane = threadIdx.x & 63;
+  const int L1 = pv.L1;
+  const int64_t n = a.n, n_tiles = (n + 63) >> 6;
+  const int64_t waves = static_cast<int64_t>(gridDim.x) * (kBlockD / 64);
+  int64_t t = static_cast<int64_t>(blockIdx.x) * (kBlockD / 64) + (threadIdx.x >> 6);
+  auto load_offsets = [&](int64_t tt, int64_t& o0, int64_t& o1) {
+    const int64_t r = (tt << 6) + lane;
+    const bool in = tt < n_tiles && r < n;
+    o0 = in ? a.offsets[r] : 0;
+    o1 = in ? a.offsets[r + 1] : 0;
+  };
+  int64_t o0, o1;
+  load_offsets(t, o0, o1);
+  for (; t < n_tiles; t += waves) {  // wave-uniform
+    const int64_t r = (t << 6) + lane;
+    const int L2 = static_cast<int>(o1 - o0);
+    const bool in = r < n;
+    const bool mine = in && (L2 <= L1 ? L1 - L2 + 1 : 1) <= NOFF;  // others belong to the tile kernel
+    const bool on = mine && L2 <= L1;
+    // the aligned words holding the record's letters, and only those (never past its last letter's word)
+    uint32_t wd[L2W];
+    {
+      const uintptr_t p = reinterpret_cast<uintptr_t>(a.codes + o0);
+      const uint32_t* w32 = reinterpret_cast<const uint32_t*>(p & ~uintptr_t{3});
+      const int sh = static_cast<int>(p & 3) * 8;
+      const int nwords = on ? ((sh >> 3) + L2 + 3) >> 2 : 0;
+      uint32_t raw[L2W + 1];
+#pragma unroll
+      for (int k = 0; k <= L2W; ++k) raw[k] = k < nwords ? __builtin_nontemporal_load(w32 + k) : 0u;
+      const int rbits = 8 * L2;
+#pragma unroll
+      for (int k = 0; k < L2W; ++k) {
+        uint32_t w = sh ? ((raw[k] >> sh) | (raw[k + 1] << (32 - sh))) : raw[k];
+        const int left = rbits - 32 * k;  // record bits in this word
+        wd[k] = left >= 32 ? w : (left <= 0 ? 0u : (w & ((1u << left) - 1u)));
+      }
+    }
+    int64_t n0, n1;
+    load_offsets(t + waves, n0, n1);  // in flight while this tile is scored
+    const Result res = swipe_lane<NOFF, L2W, RK>(prof, lut8, s1l, lay, wd, L2, on, L1, a.max_l2, pv.semantics);
+    if (mine) store_result(a.out, r, a.fmt, res, pv.r2);
+    o0 = n0;
+    o1 = n1;
+  }
+}
+
 // Launches the instance of letter form LF with NO offsets per lane that `b` selects (b.rpw = record words,
 // b.swipe_rk = RK); false when no instance matches.
+// The lane-direct kernel's grid: every block resident at once (the waves stride over the tiles statically,
+// so a block that only starts when another ends would run its share after everyone else), sized by the
+// occupancy the instance reaches.
+inline void launch_direct_instance(void (*kernel)(ProblemView, ShortArgs, SwipeLayout), const ProblemView& pv,
+                                   const ShortArgs& b, const SwipeLayout& lay, int num_cus, hipStream_t stream) {
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(kernel), kBlockD, lay.total) !=
+          hipSuccess ||
+      occ < 1) {
+    (void)hipGetLastError();
+    occ = 1;
+  }
+  const int64_t tiles = (b.n + 63) >> 6;
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((tiles + kBlockD / 64 - 1) / (kBlockD / 64),
+                                                                static_cast<int64_t>(occ) * num_cus));
+  hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(blocks)), dim3(kBlockD), lay.total, stream, pv, b, lay);
+}
+
 template <int NO, int LF>
 bool launch_swipe_noff(const ProblemView& pv, const ShortArgs& b, const SwipeLayout& lay, dim3 grid, dim3 block,
-                       hipStream_t stream) {
+                       int num_cus, hipStream_t stream) {
   const int l2w = b.rpw;
   const bool rk = b.swipe_rk != 0;
-#define MOC_SWIPE_CASE(LW, RKV)                                                                            \
-  if (l2w == LW && rk == RKV) {                                                                          \
+#define MOC_SWIPE_CASE(LW, RKV)                                                                              \
+  if (l2w == LW && rk == RKV) {                                                                            \
+    if constexpr (LF == 0) {                                                                               \
+      if (b.lane_direct) {                                                                                 \
+        launch_direct_instance(&swipe_direct_kernel<NO, LW, RKV>, pv, b, lay, num_cus, stream);           \
+        return true;                                                                                       \
+      }                                                                                                    \
+    }                                                                                                      \
     hipLaunchKernelGGL((swipe_search_kernel<NO, LW, LF, RKV>), grid, block, lay.total, stream, pv, b, lay); \
-    return true;                                                                                         \
+    return true;                                                                                           \
   }
   MOC_SWIPE_CASE(4, false)
   MOC_SWIPE_CASE(8, false)
@@ -499,7 +599,7 @@ bool launch_swipe_noff(const ProblemView& pv, const ShortArgs& b, const SwipeLay
 #define MOC_SWIPE_FOR_NOFF(X, LF) X(LF, 8) X(LF, 16) X(LF, 24) X(LF, 32) X(LF, 40) X(LF, 48) X(LF, 56) X(LF, 64)
 #define MOC_SWIPE_DECLARE(LF, NO)                                                                            \
   bool MOC_SWIPE_FN(LF, NO)(const ProblemView& pv, const ShortArgs& b, const SwipeLayout& lay, dim3 grid,    \
-                            dim3 block, hipStream_t stream);                                                 \
+                            dim3 block, int num_cus, hipStream_t stream);                                    \
   void MOC_SWIPE_PRELOAD_FN(LF, NO)();
 MOC_SWIPE_FOR_NOFF(MOC_SWIPE_DECLARE, 0)
 MOC_SWIPE_FOR_NOFF(MOC_SWIPE_DECLARE, 2)

@@ -71,9 +71,9 @@ void preload_swipe_p33_kernels() { MOC_SWIPE_FOR_NOFF(MOC_SWIPE_PRELOAD_CALL, 2)
 namespace {
 // the instance's code object by letter form (0 bytes, 2 P33) and offsets per lane (a.slot)
 bool launch_swipe_instance(int lf, const ProblemView& pv, const ShortArgs& b, const SwipeLayout& lay, dim3 grid,
-                           dim3 block, hipStream_t stream) {
+                           dim3 block, int num_cus, hipStream_t stream) {
 #define MOC_SWIPE_GROUP_CASE(LF, NO) \
-  if (lf == LF && b.slot == NO) return MOC_SWIPE_FN(LF, NO)(pv, b, lay, grid, block, stream);
+  if (lf == LF && b.slot == NO) return MOC_SWIPE_FN(LF, NO)(pv, b, lay, grid, block, num_cus, stream);
   MOC_SWIPE_FOR_NOFF(MOC_SWIPE_GROUP_CASE, 0)
   MOC_SWIPE_FOR_NOFF(MOC_SWIPE_GROUP_CASE, 2)
 #undef MOC_SWIPE_GROUP_CASE
@@ -96,6 +96,13 @@ static int tail_div() {
 void launch_swipe(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStream_t stream) {
   if (a.n <= 0) return;
   const int fb = result_bytes(static_cast<ResultFormat>(a.fmt));
+  if (a.lane_direct) {  // device-resident byte letters, dense offsets: the wave-autonomous kernel, LDS tables only
+    if (a.packed33 || a.off_shift) throw Error("launch_swipe: lane-direct batches are byte letters with dense offsets");
+    const SwipeLayout lay = swipe_layout(pv.L1, a.slot, a.rpw, 0, 0, 0, 0);
+    if (!launch_swipe_instance(0, pv, a, lay, dim3(1), dim3(kBlockD), num_cus, stream))
+      throw Error("launch_swipe: no instance for this configuration");
+    return;
+  }
   const SwipeLayout lay = swipe_layout(pv.L1, a.slot, a.rpw, a.tile_records, a.codes_cap, fb, letter_form(a));
   const int per_cu = std::max(1, std::min(8, 160 * 1024 / std::max(lay.total, 1)));
   // MOC_SWIPE_SLOTS (test hook): a smaller persistent grid, so modest batches reach the tail-tile region
@@ -118,7 +125,7 @@ void launch_swipe(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStr
       b.tail_records ? b.tail_from + (b.n - big_end + b.tail_records - 1) / b.tail_records : n_big;
   const int64_t blocks = std::min<int64_t>(n_tiles, slots);
   const dim3 grid(static_cast<unsigned>(std::max<int64_t>(blocks, 1))), block(kBlock);
-  const bool ok = launch_swipe_instance(letter_form(a), pv, b, lay, grid, block, stream);
+  const bool ok = launch_swipe_instance(letter_form(a), pv, b, lay, grid, block, num_cus, stream);
   if (!ok) throw Error("launch_swipe: no instance for this configuration");
 }
 

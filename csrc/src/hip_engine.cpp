@@ -62,6 +62,16 @@ void upload_staged(void* dst, const void* h, size_t bytes, hipStream_t s) {
     MOC_HIP_CHECK(hipMemcpyAsync(dst, h, bytes, hipMemcpyHostToDevice, s));
 }
 
+// Device-resident byte batches with dense offsets run the wave-autonomous swipe kernel (swipe_direct_kernel);
+// MOC_SWIPE_DIRECT=0 keeps them on the block-tiled one (A/B runs; both give the same results).
+bool lane_direct_enabled() {
+  static const bool on = [] {
+    const char* v = std::getenv("MOC_SWIPE_DIRECT");
+    return !(v && std::atoi(v) == 0);
+  }();
+  return on;
+}
+
 // True when every byte of [p, p+bytes) is page-locked through the registry (moc/runtime/pinned.hpp);
 // *dev gets the device-side address of p.
 bool pinned_range(const void* p, size_t bytes, const void** dev) {
@@ -740,6 +750,7 @@ void HipEngine::solve_wire_impl(const WireBatch& batch, void* out, ResultFormat 
                                     dev::configure_short(L1_, ls.mn, ls.mx, a))) &&
                          (a.tile_records % (1 << b.off_shift)) == 0;
   if ((opt_.allow_direct || b.device) && kernel_ok && direct_pointers(b, out, fb, a)) {
+    a.lane_direct = swipe && b.device && !b.packed33 && !b.off_shift && lane_direct_enabled() ? 1 : 0;
     const dev::ProblemView pv = problem_view(ls.mx);
     const bool graph = prepare_direct(pv, a, swipe);  // capture / instantiation stays outside the timed span
     MOC_HIP_CHECK(hipEventRecord(ev_a_, s_compute_));
@@ -937,6 +948,7 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
       a.n = cn;
       a.out = s.d_out;
       a.counter = s.d_counter;
+      a.lane_direct = swipe && lane_direct_enabled() ? 1 : 0;
       if (swipe)
         dev::launch_swipe(pv, a, num_cus_, s_compute_);
       else
@@ -1022,6 +1034,7 @@ void HipEngine::solve_device(const uint8_t* d_codes, const int64_t* d_offsets, c
     a.n = n;
     a.out = d_out;
     a.counter = d_counter_;
+    a.lane_direct = swipe && lane_direct_enabled() ? 1 : 0;
     if (swipe)
       dev::launch_swipe(pv, a, num_cus_, stream);
     else
