@@ -62,11 +62,19 @@ typedef short s16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ s16x2 as_s16x2(uint32_t v) { return __builtin_bit_cast(s16x2, v); }
 __device__ __forceinline__ uint32_t as_u32(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
 
+// The profile's geometry is a compile-time function of the instance (NOFF, L2W), so every LDS address in the
+// hot loop is the lane's letter times a constant plus an immediate offset. A step i < 4 L2W reads columns
+// [8 (i >> 3), 8 (i >> 3) + NOFF) of a row (the RK re-walk: < NOFF + steps); rows are a multiple of 16
+// entries, which keeps the rows' bank offsets a bijection of the letter (swipe_build_tables).
+constexpr int swipe_row(int noff, int l2w) { return (4 * l2w + noff + 8 + 15) & ~15; }  // int16 entries
+constexpr int swipe_stride(int noff, int l2w) { return 2 * swipe_row(noff, l2w) + 16; }  // bytes between rows
+constexpr int swipe_copy_bytes(int noff, int l2w) { return kAlphabet * swipe_stride(noff, l2w); }
+constexpr int swipe_prof_bytes(int noff, int l2w) { return kCopies * swipe_copy_bytes(noff, l2w); }
+constexpr int kAnchorBytes = 64 * 32;  // anchor table: int8 [64 steps][32 letters]
+
 struct SwipeLayout {
-  int row = 0;          // profile row length (int16 entries), multiple of 8
-  int copy_elems = 0;   // 27 * row
-  int prof_bytes = 0;   // 8 shifted copies of the Dt profile
-  int s_off = 0;        // int8 LUT (32 x 32, column 31 = 0) + Seq1 codes (31 past Seq1): anchor diagonal
+  int prof_bytes = 0;   // 8 shifted copies of the Dt profile (swipe_prof_bytes)
+  int s_off = 0;        // anchor table: at[i][c] = T[c][Seq1[NOFF + i]] (0 past Seq1), kAnchorBytes
   int loff_off = 0, codes_off = 0, res_off = 0, raw_off = 0, total = 0;  // raw: P33 bytes as loaded
 };
 
@@ -80,12 +88,9 @@ inline int letter_form(const ShortArgs& a) { return a.packed33 ? 2 : 0; }
 
 inline SwipeLayout swipe_layout(int L1, int noff, int l2w, int tile_records, int codes_cap, int fb, int lf) {
   SwipeLayout l;
-  // a multiple of 64 int16 (8 chunks of 16 B) so the per-letter XOR swizzle of chunk indices stays in the row
-  l.row = (std::max(L1, 4 * l2w) + noff + 8 + 63) & ~63;
-  l.copy_elems = kAlphabet * l.row;
-  l.prof_bytes = al16(kCopies * l.copy_elems * 2);
+  l.prof_bytes = swipe_prof_bytes(noff, l2w);
   l.s_off = l.prof_bytes;
-  l.loff_off = l.s_off + al16(kLutInts + l.row);
+  l.loff_off = l.s_off + kAnchorBytes;
   l.codes_off = l.loff_off + al16((tile_records + 1) * 4 + 64);  // + misc: 16 ints
   l.res_off = l.codes_off + al16(codes_cap);
   l.raw_off = l.res_off + al16(tile_records * fb);
@@ -97,33 +102,34 @@ inline SwipeLayout swipe_layout(int L1, int noff, int l2w, int tile_records, int
 
 using namespace swipe;
 
-// The block's LDS tables, built once per block (before a barrier): kCopies shifted difference-profile
-// copies, the anchor LUT and Seq1's codes.
-template <bool RK, int KB>
-__device__ __forceinline__ void swipe_build_tables(short* prof, int8_t* lut8, uint8_t* s1l, const SwipeLayout& lay,
-                                                   const ProblemView& pv, int tid, int nthreads) {
-  // ---- kCopies shifted int16 difference-profile copies: prof[s][c][j] = Pf[c][j + s], and the plain S rows.
-  //      Rows are 128-byte multiples, so the 16-byte chunk q of every row would start on the same LDS
-  //      bank; chunk q of row c is stored at chunk q ^ (c & 7) instead, spreading the 16 lanes of a
-  //      ds_read_b128 group (16 records reading 16 rows) over 8 bank quads — 8-way -> ~2-way conflicts.
+// The block's LDS tables, built once per block (before a barrier):
+//  * kCopies shifted int16 difference-profile copies: copy s, row c, entry j' holds Pf[c][j' + s], at byte
+//    s * copy_bytes + c * stride + 2 j'. A step's read is 16-byte chunks of one row (the lane's letter), so the
+//    16 lanes of a ds_read_b128 group read 16 rows at the same column; the row stride of 2 row + 16 bytes
+//    (row a multiple of 16 entries) puts row c's chunks on bank quad (c (row / 8 + 1) + chunk) mod 16, a
+//    bijection of c mod 16: two lanes conflict only for letters 16 apart (different letters on one quad),
+//    and lanes with the same letter read the same address (a broadcast). The address is one multiply-add
+//    of the letter plus immediate offsets — no per-chunk swizzle arithmetic in the hot loop.
+//  * the anchor table at[i][c] = T[c][Seq1[NOFF + i]] (int8; 0 past Seq1 and for the padding letter 0), read
+//    at the lane's letter plus an immediate offset: the anchor diagonal Tot_NOFF costs one LDS read per step.
+template <bool RK, int KB, int NOFF, int L2W>
+__device__ __forceinline__ void swipe_build_tables(unsigned char* smem, const ProblemView& pv, int tid, int nthreads) {
+  constexpr int row = swipe_row(NOFF, L2W), stride = swipe_stride(NOFF, L2W), cb = swipe_copy_bytes(NOFF, L2W);
   const int L1 = pv.L1;
-  const int row = lay.row, ce = lay.copy_elems;
-  for (int e = tid; e < kCopies * ce; e += nthreads) {
-    const int s = e / ce, rem = e - s * ce, c = rem / row, jj = rem - c * row;
-    const int j = ((((jj >> 3) ^ (c & 7)) << 3) | (jj & 7)) + s;  // element stored at jj holds column j
+  constexpr int n = kCopies * kAlphabet * row;
+  for (int e = tid; e < n; e += nthreads) {
+    const int s = e / (kAlphabet * row), rem = e - s * (kAlphabet * row), c = rem / row, jj = rem - c * row;
+    const int j = jj + s;  // the column entry jj of copy s holds
     const int sj = (c >= 1 && j < L1) ? pv.lut[c * kLutStride + pv.seq1[j]] : 0;
     const int sn = (c >= 1 && j + 1 < L1) ? pv.lut[c * kLutStride + pv.seq1[j + 1]] : 0;
-    prof[e] = static_cast<short>(RK ? sj - sn : (sj - sn) * (1 << KB) - 1);  // Pf = Dt * 2^KB - 1 (header)
+    *reinterpret_cast<short*>(smem + s * cb + c * stride + 2 * jj) =
+        static_cast<short>(RK ? sj - sn : (sj - sn) * (1 << KB) - 1);  // Pf = Dt * 2^KB - 1 (header)
   }
-  // the anchor LUT stored by Seq1 letter: entry (y << 5) | c = T[c][y]. A step's Seq1 letter y is the same
-  // for every lane, so the wave's reads fall in one 32-byte row (8 banks, no conflicts); indexed by the
-  // lane's letter c first, 26 rows 32 bytes apart hit the same banks every 8 letters (up to 4-way).
-  // Letter 0 (padding: steps past a lane's record) and Seq1 letter 31 (past Seq1) contribute 0.
-  for (int e = tid; e < kLutInts; e += nthreads) {
-    const int y = e >> 5, c = e & 31;
-    lut8[e] = static_cast<int8_t>(y == 31 || c == 0 ? 0 : pv.lut[c * kLutStride + y]);
+  int8_t* at = reinterpret_cast<int8_t*>(smem + swipe_prof_bytes(NOFF, L2W));
+  for (int e = tid; e < kAnchorBytes; e += nthreads) {
+    const int i = e >> 5, c = e & 31, j = NOFF + i;
+    at[e] = static_cast<int8_t>(c >= 1 && c < kAlphabet && j < L1 ? pv.lut[c * kLutStride + pv.seq1[j]] : 0);
   }
-  for (int j = tid; j < row; j += nthreads) s1l[j] = j < L1 ? pv.seq1[j] : 31;
 }
 
 // A record's letters (rs = byte position of its first letter in `l32`) -> NW aligned words, bits past the
@@ -145,16 +151,17 @@ __device__ __forceinline__ void record_words(const uint32_t* l32, int rs, int L2
   }
 }
 
-// One lane's search of its record (NW = L2W words of letters, `on`: the lane searches; every lane of the
-// wave must call it — the step count is the wave's longest record). max_l2: the batch's longest record.
+// One lane's search of its record (L2W words of letters, `on`: the lane searches; every lane of the wave
+// must call it — the step count is the wave's longest record). max_l2: the batch's longest record.
 template <int NOFF, int L2W, bool RK>
-__device__ __forceinline__ Result swipe_lane(const short* prof, const int8_t* lut8, const uint8_t* s1l,
-                                             const SwipeLayout& lay, const uint32_t (&wd)[L2W], int L2, bool on, int L1,
-                                             int max_l2, int sem) {
+__device__ __forceinline__ Result swipe_lane(const unsigned char* smem, const uint32_t (&wd)[L2W], int L2, bool on,
+                                             int L1, int max_l2, int sem) {
   constexpr int KB = RK ? 1 : bounds::swipe_kbits(L2W);
   constexpr int KMASK = (1 << KB) - 1;
   constexpr int NP = NOFF / 2;  // packed accumulators
+  constexpr int stride = swipe_stride(NOFF, L2W), cb = swipe_copy_bytes(NOFF, L2W);
   const int steps = wave_max_small(on ? L2 : 0);  // L2 <= 4 * L2W <= 64 here
+  const int8_t* at = reinterpret_cast<const int8_t*>(smem + swipe_prof_bytes(NOFF, L2W));
 
   uint32_t E2[NP], B2[NP];
   int anchor = 0;  // Tot_NOFF: the diagonal just past this lane's offsets
@@ -173,34 +180,33 @@ __device__ __forceinline__ Result swipe_lane(const short* prof, const int8_t* lu
       // 8 steps (input6: 11 steps instead of 16); the copy index s stays a compile-time constant
       if (i >= steps) break;
       const int c = (wd[i >> 2] >> (8 * (i & 3))) & 0xff;
-      const int sw = c & 7;
+      // copy s holds column j' + s at j': columns i .. i + NOFF - 1 are the 16-byte chunks from column i0
+      const unsigned char* rowp = smem + (s * cb + 2 * i0) + __umul24(c, stride);
       uint32_t v[NP];
-      // copy s holds column j + s at j: columns i .. i + NOFF - 1 are 16-byte chunks from i0 on
-      const uint4* rowp = reinterpret_cast<const uint4*>(prof + s * lay.copy_elems + c * lay.row);
 #pragma unroll
       for (int q = 0; q < NOFF / 8; ++q) {
-        const uint4 x = rowp[((i0 >> 3) + q) ^ sw];
+        const uint4 x = *reinterpret_cast<const uint4*>(rowp + 16 * q);
         v[4 * q + 0] = x.x;
         v[4 * q + 1] = x.y;
         v[4 * q + 2] = x.z;
         v[4 * q + 3] = x.w;
       }
-      anchor += lut8[(s1l[NOFF + i] << 5) | c];
+      anchor += at[32 * i + c];
 #pragma unroll
-      for (int q = 0; q < NP; ++q) {
-        E2[q] = as_u32(as_s16x2(E2[q]) + as_s16x2(v[q]));
-        B2[q] = as_u32(__builtin_elementwise_max(as_s16x2(B2[q]), as_s16x2(E2[q])));
-      }
+      for (int q = 0; q < NP; ++q) E2[q] = as_u32(as_s16x2(E2[q]) + as_s16x2(v[q]));
+#pragma unroll
+      for (int q = 0; q < NP; ++q) B2[q] = as_u32(__builtin_elementwise_max(as_s16x2(B2[q]), as_s16x2(E2[q])));
     }
   }
 
   // ---- per-lane selection over the record's offsets: 32-bit keys (score+2^15 | ~(o<<KB | k)), 0 = none.
   //      The valid offsets are prefixes: the un-mutated candidate at o < lim0 (o <= last = L1-L2 under
   //      the spec semantics or when L2 == L1, else o < last), the mutants at o < lim1 = last (L2 >= 2).
-  //      Running sums carry the 2^15 bias, so a key is one shift-or of them (~13 VALU ops per offset).
+  //      Running sums carry the 2^15 bias, so a key is one shift-or of them; the per-pair parts (D_o(L2),
+  //      the best mutant's d and k) come out of the packed sums with one op per two offsets.
   //      RK: the low bits are ~(o << 1 | mutated); bd keeps the winning mutant's D for the k re-walk.
-  //      Offsets below L1 - max_l2 (the batch's longest record) are valid for every lane that searches
-  //      (`on`): their limits are only applied above it (wave-uniform branch).
+  //      Offsets below L1 - max_l2 are valid for every lane that searches (`on`): a group of 8 offsets
+  //      entirely below it skips the limit tests (wave-uniform), the others apply them per lane.
   const int last = L1 - L2;
   const int lim0 = on ? last + ((sem == static_cast<int>(Semantics::Spec) || L2 == L1) ? 1 : 0) : 0;
   const int lim1 = on && L2 >= 2 ? last : 0;
@@ -208,29 +214,47 @@ __device__ __forceinline__ Result swipe_lane(const short* prof, const int8_t* lu
   // D_o(L2) pairs from the final running sums: (E - (KMASK - steps)) >> KB (RK: E itself)
   const short eb = static_cast<short>(RK ? 0 : KMASK - steps);
   const s16x2 ebias = {eb, eb};
+  // packed per offset pair (one op per two offsets): D_o(L2), the best mutant's D_o(k) and its KMASK - k
+  uint32_t dq2[NP], bd2[NP], bl2[NP];
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    dq2[q] = RK ? E2[q] : as_u32((as_s16x2(E2[q]) - ebias) >> static_cast<short>(KB));
+    bd2[q] = RK ? B2[q] : as_u32(as_s16x2(B2[q]) >> static_cast<short>(KB));
+    bl2[q] = B2[q] & (static_cast<uint32_t>(KMASK) * 0x10001u);
+  }
   uint32_t best = 0;
   int bd = 0;  // RK: D_o(k) of the best mutant so far
   uint32_t tot = static_cast<uint32_t>(anchor + 32768);  // Tot_{o+1} + 2^15 entering offset o
-#pragma unroll
-  for (int o = NOFF - 1; o >= 0; --o) {
-    const s16x2 dq = RK ? as_s16x2(E2[o >> 1]) : (as_s16x2(E2[o >> 1]) - ebias) >> static_cast<short>(KB);
+  auto offset = [&](const int o, const bool masked) {
+    const int hi = o & 1;
     const uint32_t Pn = tot;  // Tot_{o+1} + 2^15
-    const uint32_t Po = Pn + static_cast<uint32_t>(static_cast<int>(o & 1 ? dq.y : dq.x));
+    const uint32_t Po = Pn + static_cast<uint32_t>(hi ? static_cast<int>(dq2[o >> 1]) >> 16
+                                                      : static_cast<int>(static_cast<short>(dq2[o >> 1] & 0xffffu)));
     tot = Po;  // suffix pass: Tot_o = Tot_{o+1} + D_o(L2)
     const uint32_t kLow0 = 0xffffu - (static_cast<uint32_t>(o) << KB);  // ~(o << KB | 0)
     const uint32_t kLow1 = kLow0 - KMASK;  // its low KB bits are 0: ~(o << KB | k) = kLow1 | (KMASK - k)
     uint32_t k0 = (Po << 16) | kLow0;
-    // bk = d * 2^KB + (KMASK - k): the best mutant's D_o(k) and its k; t = (d + Tot_{o+1} + 2^15) * 2^KB + (KMASK - k)
-    const int bk = static_cast<short>(o & 1 ? (B2[o >> 1] >> 16) : (B2[o >> 1] & 0xffff));
-    const uint32_t t = static_cast<uint32_t>(bk) + (Pn << KB);
-    uint32_t k1 = RK ? ((static_cast<uint32_t>(bk) + Pn) << 16) | (kLow0 - 1u) : ((t >> KB) << 16) | (t & KMASK) | kLow1;
-    if (o >= all_valid) {  // wave-uniform
+    const int dbest = hi ? static_cast<int>(bd2[o >> 1]) >> 16 : static_cast<int>(static_cast<short>(bd2[o >> 1] & 0xffffu));
+    const uint32_t low = RK ? kLow0 - 1u : kLow1 | (hi ? bl2[o >> 1] >> 16 : bl2[o >> 1] & 0xffffu);
+    uint32_t k1 = ((Pn + static_cast<uint32_t>(dbest)) << 16) | low;
+    if (masked) {
       k0 = o < lim0 ? k0 : 0u;
       k1 = o < lim1 ? k1 : 0u;
     }
     const uint32_t nb = max(best, max(k0, k1));
-    if (RK) bd = (nb == k1 && k1 != 0u) ? bk : bd;
+    if (RK) bd = (nb == k1 && k1 != 0u) ? dbest : bd;
     best = nb;
+  };
+  // groups of 8 offsets, from the top: a group entirely below L1 - max_l2 needs no limits (wave-uniform test)
+#pragma unroll
+  for (int g = (NOFF - 1) / 8; g >= 0; --g) {
+    if (8 * g + 7 < all_valid) {
+#pragma unroll
+      for (int o = 8 * g + 7; o >= 8 * g; --o) offset(o, false);
+    } else {
+#pragma unroll
+      for (int o = 8 * g + 7; o >= 8 * g; --o) offset(o, true);
+    }
   }
   if (!on) best = 0u;
   int kw = 0;  // RK: the winning mutant's k
@@ -245,8 +269,7 @@ __device__ __forceinline__ Result swipe_lane(const short* prof, const int8_t* lu
       for (int i = 0; i < 4 * L2W; ++i) {
         if (i >= steps) break;  // wave-uniform
         const int c = (wd[i >> 2] >> (8 * (i & 3))) & 0xff;
-        const int col = ow + i;  // copy 0 holds column j at ((j >> 3) ^ (c & 7)) << 3 | (j & 7)
-        run += prof[c * lay.row + ((((col >> 3) ^ (c & 7)) << 3) | (col & 7))];
+        run += *reinterpret_cast<const short*>(smem + __umul24(c, stride) + 2 * (ow + i));  // copy 0: column ow + i
         kw = (kw == 0 && run == bd) ? i + 1 : kw;
       }
     }
@@ -266,9 +289,6 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
   constexpr int kRpt = rpt_of(LF);
   constexpr int NW = L2W;  // record words (4 letters each) held per lane
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  short* prof = reinterpret_cast<short*>(smem);
-  int8_t* lut8 = reinterpret_cast<int8_t*>(smem + lay.s_off);
-  uint8_t* s1l = smem + lay.s_off + kLutInts;
   int* loff = reinterpret_cast<int*>(smem + lay.loff_off);
   int* misc = loff + a.tile_records + 1;
   uint8_t* codes_l = smem + lay.codes_off;
@@ -379,7 +399,7 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
   Fetch cur, nxt;
   fetch(grab(), cur);  // the first tile's loads are in flight while the block builds its profile
 
-  swipe_build_tables<RK, KB>(prof, lut8, s1l, lay, pv, tid, kBlock);
+  swipe_build_tables<RK, KB, NOFF, L2W>(smem, pv, tid, kBlock);
   for (;;) {
     if (cur.t >= n_tiles) break;
     const int64_t rb = cur.rb, start = cur.start, end = cur.end;
@@ -469,7 +489,7 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
       const bool on = mine && L2 <= L1;
       uint32_t wd[NW];
       record_words<NW>(reinterpret_cast<const uint32_t*>(codes_l), rs, L2, on, wd);
-      const Result res = swipe_lane<NOFF, L2W, RK>(prof, lut8, s1l, lay, wd, L2, on, L1, a.max_l2, sem);
+      const Result res = swipe_lane<NOFF, L2W, RK>(smem, wd, L2, on, L1, a.max_l2, sem);
       if (mine) store_result(res_l, rl, a.fmt, res, pv.r2);
     }
     __syncthreads();
@@ -491,11 +511,8 @@ constexpr int kBlockD = 512;  // 8 waves share one set of LDS tables
 template <int NOFF, int L2W, bool RK>
 __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, ShortArgs a, SwipeLayout lay) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  short* prof = reinterpret_cast<short*>(smem);
-  int8_t* lut8 = reinterpret_cast<int8_t*>(smem + lay.s_off);
-  uint8_t* s1l = smem + lay.s_off + kLutInts;
   constexpr int KB = RK ? 1 : bounds::swipe_kbits(L2W);
-  swipe_build_tables<RK, KB>(prof, lut8, s1l, lay, pv, threadIdx.x, kBlockD);
+  swipe_build_tables<RK, KB, NOFF, L2W>(smem, pv, threadIdx.x, kBlockD);
   __syncthreads();  // the only barrier: tables complete
   const int lane = threadIdx.x & 63;
   const int L1 = pv.L1;
@@ -536,7 +553,7 @@ __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, S
     }
     int64_t n0, n1;
     load_offsets(t + waves, n0, n1);  // in flight while this tile is scored
-    const Result res = swipe_lane<NOFF, L2W, RK>(prof, lut8, s1l, lay, wd, L2, on, L1, a.max_l2, pv.semantics);
+    const Result res = swipe_lane<NOFF, L2W, RK>(smem, wd, L2, on, L1, a.max_l2, pv.semantics);
     if (mine) store_result(a.out, r, a.fmt, res, pv.r2);
     o0 = n0;
     o1 = n1;
