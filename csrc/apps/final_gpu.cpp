@@ -278,13 +278,22 @@ class GpuRankImpl final : public GpuRank {
     const ncclUniqueId id = RcclComm::exchange_id(ctx_);  // MPI: this (the main) thread
     pending_ = std::async(std::launch::async, [this, id] {
       HipEngine& e = engine();  // resolves the device first
-      return std::make_unique<RcclDeviceComm>(ctx_, device_.load(), e.compute_stream(), id);
+      Stopwatch sw;
+      sw.start();
+      auto dc = std::make_unique<RcclDeviceComm>(ctx_, device_.load(), e.compute_stream(), id);
+      sw.stop();
+      rccl_init_ms_.store(sw.total_ms());
+      return dc;
     });
   }
   void init_rccl() override {
     if (!dc_) {
       init_rccl_begin();
+      Stopwatch sw;
+      sw.start();
       dc_ = pending_.get();
+      sw.stop();
+      rccl_wait_ms_ = sw.total_ms();
     }
     if (!ds_) ds_ = std::make_unique<HipDeviceSearch>(engine());
   }
@@ -299,6 +308,8 @@ class GpuRankImpl final : public GpuRank {
     return *ds_;
   }
   int device() const override { return device_.load(); }
+  double rccl_init_ms() const override { return rccl_init_ms_.load(); }
+  double rccl_wait_ms() const override { return rccl_wait_ms_; }
   void set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, Semantics sem) override {
     std::lock_guard<std::mutex> lock(mu_);
     facts_ = ProblemFacts::of(w, L1);
@@ -470,6 +481,8 @@ class GpuRankImpl final : public GpuRank {
   std::unique_ptr<DeviceSearch> ds_;  // destroyed after dc_ (declared before it)
   std::unique_ptr<DeviceComm> dc_;
   std::future<std::unique_ptr<RcclDeviceComm>> pending_;  // connect in flight (init_rccl_begin)
+  std::atomic<double> rccl_init_ms_{0.0};                 // the connect, on its helper thread
+  double rccl_wait_ms_ = 0;                               // init_rccl's wait for it
 };
 
 }  // namespace

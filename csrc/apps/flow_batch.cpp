@@ -238,6 +238,7 @@ void BatchFlow::batch_rccl(RecordBatch* rb, int64_t n, int64_t total_chars, cons
   }
   j_.compute_ms += out.compute_ms;
   j_.eng.kernel_ms += out.kernel_ms;
+  j_.account_comm(out);
   if (j_.ctx.rank == kRoot) {
     if (!out.rank_records.empty()) j_.rank_records = out.rank_records;
     j_.pt.begin("print");
@@ -325,6 +326,7 @@ void run_text_batch(JobCore& job, std::unique_ptr<BulkParser>& parser, int64_t f
   BatchFlow(job, &parser, text).release_input_now();
   job.compute_ms += out.compute_ms;
   job.eng.kernel_ms += out.kernel_ms;
+  job.account_comm(out);
   if (ctx.rank == kRoot) {
     job.cells += out.cells;
     job.chars += out.letters;

@@ -158,6 +158,7 @@ int run_device_streaming(JobCore& job, const Header& h, StreamSource& src, int64
     }
     job.compute_ms += out.compute_ms;
     job.eng.kernel_ms += out.kernel_ms;
+    job.account_comm(out);
     ++job.batches;
     if (root) {
       job.records += n;

@@ -111,6 +111,11 @@ struct JobCore {
   int64_t cells = 0, chars = 0, records = 0, batches = 0;
   int64_t first_index = 0;  // global index of the current batch's first record
   int64_t pinned_bytes = 0, h2d_bytes = 0, d2h_bytes = 0;  // this rank (--timing)
+  // rccl(-emul) transport (--timing): bytes this rank sent over the comm, the root's bytes to each rank and
+  // its distribution time (per-peer rate = bytes / time)
+  int64_t comm_sent_bytes = 0;
+  std::vector<int64_t> peer_sent;
+  double distribute_ms = 0;
   std::vector<int64_t> rank_pinned, rank_h2d, rank_records, rank_pin_us;  // root: per rank (--timing)
   std::vector<std::pair<std::string, std::string>> extra_timing;          // flow-specific --timing fields
   const char* build_id = "";  // the sources of this binary (--timing)
@@ -129,6 +134,8 @@ struct JobCore {
   // root: rows of the current batch (first = index relative to the batch)
   void print(const Result* r, int64_t n, int64_t first);
   CostModel cost_model() const { return all_gpu ? CostModel{1.0, 200.0, 2400.0} : CostModel{1.0, 4.0, 64.0}; }
+  // adds a device batch's comm traffic to the job's (--timing)
+  void account_comm(const DeviceBatchOut& out);
   // collective: the --timing JSON line on root's stderr
   void report(const Header& h);
 };

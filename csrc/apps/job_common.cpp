@@ -281,14 +281,25 @@ void JobCore::print(const Result* r, int64_t n, int64_t first) {
   pt.end();
 }
 
+void JobCore::account_comm(const DeviceBatchOut& out) {
+  comm_sent_bytes += out.sent_bytes;
+  distribute_ms += out.distribute_ms;
+  if (peer_sent.size() < out.peer_bytes.size()) peer_sent.resize(out.peer_bytes.size(), 0);
+  for (size_t q = 0; q < out.peer_bytes.size(); ++q) peer_sent[q] += out.peer_bytes[q];
+}
+
 void JobCore::report(const Header& h) {
-  double mx[2] = {compute_ms, eng.kernel_ms};
-  MPI_Reduce(ctx.rank == kRoot ? MPI_IN_PLACE : mx, mx, 2, MPI_DOUBLE, MPI_MAX, kRoot, ctx.world);
+  // the RCCL communicator's set-up (connect on its helper thread) and the time the rank then waited for it
+  const bool device_transport = transport == "rccl" || transport == "rccl-emul";
+  const double comm_init = eng.hip && (device_transport || coll_rccl) ? eng.hip->rccl_init_ms() : 0.0;
+  const double comm_wait = eng.hip && (device_transport || coll_rccl) ? eng.hip->rccl_wait_ms() : 0.0;
+  double mx[4] = {compute_ms, eng.kernel_ms, comm_init, comm_wait};
+  MPI_Reduce(ctx.rank == kRoot ? MPI_IN_PLACE : mx, mx, 4, MPI_DOUBLE, MPI_MAX, kRoot, ctx.world);
   // every mode: what each rank page-locked and moved host->device over the job (sliced mode also has
-  // its per-rank records and pin times, gathered with its results)
-  int64_t moved[2] = {pinned_bytes, h2d_bytes};
-  std::vector<int64_t> all_moved(static_cast<size_t>(2 * ctx.size));
-  MPI_Gather(moved, 2, MPI_INT64_T, all_moved.data(), 2, MPI_INT64_T, kRoot, ctx.world);
+  // its per-rank records and pin times, gathered with its results), and what it sent over the comm
+  int64_t moved[3] = {pinned_bytes, h2d_bytes, comm_sent_bytes};
+  std::vector<int64_t> all_moved(static_cast<size_t>(3 * ctx.size));
+  MPI_Gather(moved, 3, MPI_INT64_T, all_moved.data(), 3, MPI_INT64_T, kRoot, ctx.world);
   if (ctx.rank != kRoot || !flags.get_bool("timing", false)) return;
   const double wall_s = total.total_ms() / 1e3;
   auto list = [](const std::vector<int64_t>& v) {
@@ -304,10 +315,28 @@ void JobCore::report(const Header& h) {
   } else {
     std::vector<int64_t> pinned(static_cast<size_t>(ctx.size)), h2d(static_cast<size_t>(ctx.size));
     for (int q = 0; q < ctx.size; ++q) {
-      pinned[q] = all_moved[2 * q];
-      h2d[q] = all_moved[2 * q + 1];
+      pinned[q] = all_moved[3 * q];
+      h2d[q] = all_moved[3 * q + 1];
     }
     per_rank += ", \"rank_pinned_bytes\": " + list(pinned) + ", \"rank_h2d_bytes\": " + list(h2d);
+  }
+  if (device_transport || coll_rccl) {
+    // the numbers a first multi-GPU run reads: communicator set-up, bytes each rank put on the comm, and the
+    // root's rate to each peer over the distribution (bytes to that rank / the root's distribution time)
+    std::vector<int64_t> sent(static_cast<size_t>(ctx.size));
+    for (int q = 0; q < ctx.size; ++q) sent[q] = all_moved[3 * q + 2];
+    char buf[96];
+    std::snprintf(buf, sizeof buf, "%.3f, \"rccl_comm_wait_ms\": %.3f, \"distribute_ms\": %.3f", mx[2], mx[3],
+                  distribute_ms);
+    per_rank += ", \"rccl_comm_init_ms\": " + std::string(buf) + ", \"rank_sent_bytes\": " + list(sent);
+    std::string gbps = "[";
+    for (int q = 0; q < ctx.size; ++q) {
+      const int64_t b = q < static_cast<int>(peer_sent.size()) ? peer_sent[q] : 0;
+      std::snprintf(buf, sizeof buf, "%s%.4g", q ? ", " : "", distribute_ms > 0 ? b / (distribute_ms * 1e6) : 0.0);
+      gbps += buf;
+    }
+    per_rank += ", \"peer_sent_bytes\": " + list(peer_sent.empty() ? std::vector<int64_t>(ctx.size, 0) : peer_sent) +
+                ", \"peer_distribute_gbps\": " + gbps + "]";
   }
   for (const auto& kv : extra_timing) per_rank += ", \"" + kv.first + "\": " + kv.second;
   std::fprintf(stderr,

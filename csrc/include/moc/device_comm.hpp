@@ -113,6 +113,12 @@ struct DeviceBatchOut {
   std::vector<std::vector<char>> storage;  // backing memory of runs (the context-parallel path)
   double compute_ms = 0, kernel_ms = 0;    // this rank
   int64_t scattered_bytes = 0;             // root: device bytes sent to the other ranks
+  // what crossed the comm: bytes this rank sent (root: its slices' pieces; a peer: its results), the root's
+  // bytes to each rank (index = rank, its own 0), and the root's distribution time from its first piece on
+  // the wire to the last one delivered (the per-peer rate of a multi-GPU run: peer_bytes / distribute_ms)
+  int64_t sent_bytes = 0;
+  std::vector<int64_t> peer_bytes;
+  double distribute_ms = 0;
   std::vector<int64_t> rank_records;       // every rank's records (root)
   // device_batch_text: the batch's search cells and letters (root); an input error (every rank; the
   // message on the root), in which case nothing was searched

@@ -77,6 +77,10 @@ class GpuRank {
   // engine over device-resident wire batches (init_rccl first).
   virtual DeviceComm& device_comm() = 0;
   virtual DeviceSearch& device_search() = 0;
+  // The communicator's set-up time on its helper thread, and how long the rank then waited for it (0 before
+  // init_rccl; --timing).
+  virtual double rccl_init_ms() const = 0;
+  virtual double rccl_wait_ms() const = 0;
 };
 
 // Plugin entry points (extern "C", resolved with dlsym).

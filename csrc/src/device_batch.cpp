@@ -260,6 +260,7 @@ void solve_gather(DeviceComm& dc, DeviceSearch& ds, DeviceScratch& sc, const std
       for (int r = 1; r < p; ++r) dc.recv(d_r2 + 24 * r, 24, r);
     } else {
       dc.send(d_mine_r2, 24, 0);
+      out.sent_bytes += 24;
     }
     dc.group_end();
     if (rank == 0) {
@@ -277,6 +278,7 @@ void solve_gather(DeviceComm& dc, DeviceSearch& ds, DeviceScratch& sc, const std
     }
   } else if (fb * mine.n > 0) {
     dc.send(d_out, fb * mine.n, 0);
+    out.sent_bytes += fb * mine.n;
   }
   dc.group_end();
   if (rank == 0) {
@@ -312,6 +314,7 @@ DeviceBatchOut device_batch(DeviceComm& dc, DeviceSearch& ds, const RecordBatch*
   }
   DeviceScratch& sc = *scratch;
   DeviceBatchOut out;
+  Stopwatch dist;  // root: first piece sent -> the last one delivered
   const int rank = dc.rank(), p = dc.size();
 
   // ---- plan (root) -> every rank, through the device layer
@@ -372,6 +375,8 @@ DeviceBatchOut device_batch(DeviceComm& dc, DeviceSearch& ds, const RecordBatch*
     }
     sc.host(kHostResults, results_bytes(plan) + 16);  // the gather's page-locked buffer, ahead of the search
     hooks.begin("pack");  // host packing, and the waits for staging slots (a packing-bound distribution)
+    out.peer_bytes.assign(static_cast<size_t>(p), 0);
+    dist.start();
     int64_t i = 0;
     for (size_t k = 0; k < rounds; ++k)
       for (int step = 1; step <= p; ++step) {
@@ -394,6 +399,7 @@ DeviceBatchOut device_batch(DeviceComm& dc, DeviceSearch& ds, const RecordBatch*
         dc.group_end();
         sent[q] = dc.mark();
         out.scattered_bytes += len;
+        out.peer_bytes[r] += len;
       }
     hooks.begin("distribute");
   } else {
@@ -404,6 +410,11 @@ DeviceBatchOut device_batch(DeviceComm& dc, DeviceSearch& ds, const RecordBatch*
     }
   }
   dc.sync();
+  if (rank == 0) {
+    dist.stop();
+    out.distribute_ms = dist.total_ms();
+    out.sent_bytes += out.scattered_bytes;
+  }
   hooks.end();
 
   solve_gather(dc, ds, sc, plan, mine, d_block, hooks, out);
@@ -425,6 +436,7 @@ DeviceBatchOut device_batch_text(DeviceComm& dc, DeviceSearch& ds, const BulkPar
   }
   DeviceScratch& sc = *scratch;
   DeviceBatchOut out;
+  Stopwatch dist;  // root: first piece sent -> the last one delivered
   const int rank = dc.rank(), p = dc.size();
   constexpr int64_t kPlanBytes = static_cast<int64_t>(sizeof(RankPlan));
   const int64_t chunk = std::max<int64_t>(2640, send_chunk() / 2640 * 2640);
@@ -434,6 +446,8 @@ DeviceBatchOut device_batch_text(DeviceComm& dc, DeviceSearch& ds, const BulkPar
   int64_t status = 0;
   if (rank == 0) {
     hooks.begin("fill");  // encode (host threads), and the waits for a block to be free again
+    out.peer_bytes.assign(static_cast<size_t>(p), 0);
+    dist.start();
     const int64_t L1 = static_cast<int64_t>(parser->seq1().size());
     char* d_plan = sc.dev(kPlanBuf, kPlanBytes * p);
     RankPlan* h_plan = reinterpret_cast<RankPlan*>(sc.host(kHostPlan, kPlanBytes * p));
@@ -518,6 +532,8 @@ DeviceBatchOut device_batch_text(DeviceComm& dc, DeviceSearch& ds, const BulkPar
         dc.group_start();
         dc.send(d_plan + kPlanBytes * r, kPlanBytes, r);
         dc.group_end();
+        out.peer_bytes[r] += kPlanBytes;
+        out.sent_bytes += kPlanBytes;
         for (const Piece& pc : byte_pieces(pl, r, chunk)) {
           const int q = static_cast<int>(qi++ % kSlots);
           const int64_t len = pc.b1 - pc.b0;
@@ -528,6 +544,7 @@ DeviceBatchOut device_batch_text(DeviceComm& dc, DeviceSearch& ds, const BulkPar
           dc.group_end();
           sent[q] = dc.mark();
           out.scattered_bytes += len;
+          out.peer_bytes[r] += len;
         }
       } else {
         d_block = sc.dev(kBlock, pl.block + 16);
@@ -569,6 +586,11 @@ DeviceBatchOut device_batch_text(DeviceComm& dc, DeviceSearch& ds, const BulkPar
   // the input's verdict (the error a sequential reader meets first) on every rank
   dc.bcast(d_status, 8, 0);
   dc.download(&status, d_status, 8);
+  if (rank == 0) {
+    dist.stop();  // the bcast is ordered after every piece on the comm lane: all of them have arrived
+    out.distribute_ms = dist.total_ms();
+    out.sent_bytes += out.scattered_bytes;
+  }
   hooks.end();
   if (status != 0) {
     out.input_error = true;

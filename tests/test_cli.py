@@ -413,6 +413,31 @@ def test_rccl_driver_emulated(np_, partition):
         assert r.stdout.decode() == expected(i), (i, np_, partition)
 
 
+@pytest.mark.parametrize("np_", [1, 3, 8])
+@pytest.mark.parametrize("stream", [False, True])
+def test_rccl_transport_timing_fields(np_, stream):
+    # --timing on the device transport reports what a first multi-GPU run needs: the communicator's set-up,
+    # the bytes each rank put on the comm, the root's bytes to each peer and its per-peer rate
+    import json
+
+    extra = ["--batch-records=8"] if stream else []
+    r = run_final(["--backend=cpu", "--transport=rccl-emul", "--timing"] + extra, stdin_path=input_path(3), np_=np_,
+                  env={"MOC_SEND_CHUNK": "4096"})
+    assert r.returncode == 0, r.stderr.decode()
+    assert r.stdout.decode() == expected(3)
+    d = json.loads([l for l in r.stderr.decode().splitlines() if l.startswith("{")][-1])
+    for k in ("rccl_comm_init_ms", "rccl_comm_wait_ms", "distribute_ms", "rank_sent_bytes", "peer_sent_bytes",
+              "peer_distribute_gbps"):
+        assert k in d, (k, d)
+    assert len(d["rank_sent_bytes"]) == np_ and len(d["peer_sent_bytes"]) == np_ == len(d["peer_distribute_gbps"])
+    assert d["peer_sent_bytes"][0] == 0  # the root's own slice never crosses the comm
+    assert d["rank_sent_bytes"][0] == sum(d["peer_sent_bytes"])  # the root sends exactly what its peers get
+    if np_ > 1:
+        assert all(b > 0 for b in d["peer_sent_bytes"][1:]) and d["distribute_ms"] > 0
+        assert all(b > 0 for b in d["rank_sent_bytes"][1:])  # every peer sends its results back
+        assert all(g > 0 for g in d["peer_distribute_gbps"][1:])
+
+
 @pytest.mark.parametrize("np_", [2, 3])
 def test_rccl_driver_emulated_streaming_and_synthetic(np_, tmp_path):
     # streaming batches through the device driver, and a larger mixed-length synthetic input
