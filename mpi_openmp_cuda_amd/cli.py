@@ -24,7 +24,9 @@ def main(argv=None) -> int:
                                  formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--input", default="-", help="input file (default: stdin)")
     ap.add_argument("--backend", default="auto", choices=["auto", "hip", "cpu"])
-    ap.add_argument("--transport", default="auto", choices=["auto", "shm", "p2p"])
+    ap.add_argument("--transport", default="auto", choices=["auto", "shm", "bcast"],
+                    help="shm: node-shared window (one node); bcast: every record broadcast (--partition=offsets "
+                         "only). Record slices between nodes: ./final --transport=rccl")
     ap.add_argument("--partition", default="records", choices=["records", "offsets"],
                     help="records: cost-balanced record ranges; offsets: context parallel (split every record)")
     ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"])

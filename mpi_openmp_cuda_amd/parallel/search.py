@@ -1,18 +1,20 @@
-"""Distributed search over a torch.distributed process group (Python twin of csrc/apps/final.cpp).
+"""Distributed search over a torch.distributed process group: the torch-facing API of the two distributed
+strategies, on one node.
 
 Reference flow (main.c:110-197): root reads, Bcast x4, Scatter fixed-stride records, per-rank GPU work,
 Gather x3, root prints. Here:
   * header (weights, |Seq1|, N, semantics) + Seq1: exact-count broadcasts through the process group
     (RCCL on GPU ranks, gloo on CPU ranks);
   * cost-balanced contiguous bounds (parallel/partition.py), valid for any world size;
-  * transport "shm": the root writes the CSR batch once into a node-shared /dev/shm window; every rank
-    DMAs its own slice to its GPU and writes its results back in place — no payload collectives at all
-    (single node);
-  * transport "p2p": root sends every rank its slice (lengths + letters) with point-to-point
-    send/recv over the process group (RCCL over xGMI / network on GPUs) and receives the results back.
-  * partition "offsets" (context parallel): every rank sees every record and searches its
-    share of each record's offsets; the packed 64-bit candidate keys are combined with ONE MAX all-reduce
-    (the Reduce the reference never had) and the root decodes them.
+  * partition "records", transport "shm": the root writes the CSR batch once into a node-shared /dev/shm
+    window; every rank streams its own slice to its GPU (zero-copy, the wire formats of parallel/wire.py)
+    and writes its results back in place — no payload collectives at all;
+  * partition "offsets" (context parallel): every rank sees every record (the shm window,
+    or one broadcast with transport "bcast") and searches its share of each record's offsets; the packed
+    64-bit candidate keys are combined with ONE MAX all-reduce (the Reduce the reference never had) and the
+    root decodes them.
+Moving record payloads between ranks (several nodes, or device-resident batches over RCCL/xGMI) is the
+native driver's job, one implementation: ./final --transport=rccl (csrc/src/device_batch.cpp).
 """
 from __future__ import annotations
 
@@ -25,8 +27,8 @@ import numpy as np
 from .. import _lib
 from ..models.problem import Problem
 from ..models.scoring import Semantics
-from ..ops.align import (HipSearchEngine, decode_keys, device_count, empty_results, keys_to_ordered_int64,
-                        ordered_int64_to_keys, search_cpu, search_keys_cpu)
+from ..ops.align import (HipSearchEngine, decode_keys, device_count, keys_to_ordered_int64, ordered_int64_to_keys,
+                        search_cpu, search_keys_cpu)
 from ..utils.timer import PhaseTimer
 from . import dist as D
 from .partition import CPU_COST, GPU_COST, partition
@@ -68,9 +70,14 @@ class DistributedSearch:
             backend = "hip" if device_count() > 0 else "cpu"
         self.backend = backend
         if transport == "auto":
-            transport = "shm" if ctx.single_node else "p2p"
+            transport = "shm" if ctx.single_node else "bcast"
+        if transport not in ("shm", "bcast"):
+            raise ValueError("transport must be shm|bcast")
         if transport == "shm" and not ctx.single_node:
             raise ValueError("transport=shm needs every rank on one node")
+        if partition == "records" and transport != "shm":
+            raise ValueError("record slices move between ranks in ./final (--transport=rccl); the Python driver "
+                             "runs them through a node-shared window (transport=shm, one node)")
         self.transport = transport
         self.threads = threads
         if backend == "hip" and device is None:
@@ -117,9 +124,7 @@ class DistributedSearch:
         b, e = int(bounds[ctx.rank]), int(bounds[ctx.rank + 1])
         if self.partition == "offsets":
             return self._run_offsets(problem, prob, sem, n, total)
-        if self.transport == "shm":
-            return self._run_shm(problem, prob, sem, n, total, b, e)
-        return self._run_p2p(problem, prob, sem, n, bounds, b, e)
+        return self._run_shm(problem, prob, sem, n, total, b, e)
 
     def _run_shm(self, problem, prob, sem, n, total, b, e):
         ctx, T = self.ctx, self.timer
@@ -146,40 +151,6 @@ class DistributedSearch:
             D.barrier(ctx)
             win.close(unlink=ctx.is_root)
         return out
-
-    def _run_p2p(self, problem, prob, sem, n, bounds, b, e):
-        ctx, T = self.ctx, self.timer
-        with T.phase("distribute"):
-            if ctx.is_root:
-                lengths = problem.lengths
-                for r in range(1, ctx.world):
-                    rb, re = int(bounds[r]), int(bounds[r + 1])
-                    if re > rb:
-                        D.send_array(ctx, lengths[rb:re], r)
-                        D.send_array(ctx, problem.codes[problem.offsets[rb]:problem.offsets[re]], r)
-                my_offsets = problem.offsets[b:e + 1] - problem.offsets[b]
-                my_codes = problem.codes[problem.offsets[b]:problem.offsets[e]]
-            else:
-                my_len = D.recv_array(ctx, e - b, np.int64, 0)
-                my_offsets = np.zeros(e - b + 1, np.int64)
-                np.cumsum(my_len, out=my_offsets[1:])
-                my_codes = D.recv_array(ctx, int(my_offsets[-1]), np.uint8, 0)
-        with T.phase("compute"):
-            mine = empty_results(e - b)
-            if e > b:
-                self._compute(prob, sem, my_codes, my_offsets, mine)
-        with T.phase("gather"):
-            if ctx.is_root:
-                out = empty_results(n)
-                out[b:e] = mine
-                for r in range(1, ctx.world):
-                    rb, re = int(bounds[r]), int(bounds[r + 1])
-                    if re > rb:
-                        out[rb:re] = D.recv_array(ctx, 3 * (re - rb), np.int32, r).view(_lib.RESULT_DTYPE)
-                return out
-            if e > b:
-                D.send_array(ctx, mine.view(np.int32), 0)
-            return None
 
     def _keys(self, prob: Problem, sem: Semantics, codes, offsets) -> np.ndarray:
         if self.engine is not None:

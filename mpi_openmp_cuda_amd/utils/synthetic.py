@@ -30,6 +30,9 @@ SHAPES = {
     "input3": Shape((2, 2, 1, 10), 1489, 56, 1152),
     "input4": Shape((10, 2, 3, 4), 2976, 5, 82),
     "limits": Shape((10, 2, 3, 4), 3000, 1, 2000),
+    # between the reference shapes: records too long for the swipe kernel (> 64 letters) whose offset range
+    # still fits a wave (<= 64 lanes): the lane-per-offset short kernel's regime
+    "mid": Shape((10, 2, 3, 4), 130, 67, 85),
 }
 
 

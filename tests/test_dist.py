@@ -1,5 +1,6 @@
-"""Multi-process torch.distributed path on CPU (gloo, world_size 2-3): the Python twin of ./final
-(parallel/search.py) must reproduce the goldens with both transports, for any world size."""
+"""Multi-process torch.distributed path on CPU (gloo, world_size 2-3): the Python driver (parallel/search.py)
+must reproduce the goldens with its record slices (node-shared window) and its context-parallel split
+(window or broadcast), for any world size."""
 import os
 import subprocess
 import sys
@@ -25,7 +26,7 @@ def torchrun(nproc, args, timeout=180):
     return subprocess.run(cmd, capture_output=True, timeout=timeout, env=env, cwd="/tmp")
 
 
-@pytest.mark.parametrize("transport", ["shm", "p2p"])
+@pytest.mark.parametrize("transport", ["shm"])
 @pytest.mark.parametrize("i,nproc", [(3, 2), (6, 3), (2, 2)])
 def test_gloo_goldens(transport, i, nproc):
     r = torchrun(nproc, ["--backend=cpu", "--dist-backend=gloo", f"--transport={transport}",
@@ -34,7 +35,7 @@ def test_gloo_goldens(transport, i, nproc):
     assert r.stdout.decode() == expected(i)
 
 
-@pytest.mark.parametrize("transport", ["shm", "p2p"])
+@pytest.mark.parametrize("transport", ["shm", "bcast"])
 @pytest.mark.parametrize("i,nproc", [(3, 2), (2, 3), (4, 2)])
 def test_gloo_context_parallel(transport, i, nproc):
     # --partition=offsets: every rank searches a share of every record; MAX all-reduce of packed keys
@@ -42,6 +43,13 @@ def test_gloo_context_parallel(transport, i, nproc):
                          f"--input={input_path(i)}"])
     assert r.returncode == 0, r.stderr.decode()[-3000:]
     assert r.stdout.decode() == expected(i)
+
+
+def test_record_slices_between_ranks_belong_to_final():
+    # one distributed implementation per transport: payload sends between ranks are ./final's (rccl)
+    r = torchrun(2, ["--backend=cpu", "--dist-backend=gloo", "--transport=bcast", f"--input={input_path(1)}"],
+                 timeout=120)
+    assert r.returncode != 0 and b"--transport=rccl" in r.stderr
 
 
 def test_single_process_cli_stdin():
