@@ -64,6 +64,9 @@ struct ProblemView {
   // LDS size of a window's rows + overhang. 0 = the whole profile is the LDS image.
   int32_t prof16_window = 0;
   int64_t prof16_entries = 0;
+  // 1: the tile16 sweep stages each byte pair widened to two int16 halves (whole images only; the LDS image
+  // is then tile16_lds_bytes(2 * prof16_bytes, L1))
+  int32_t prof16_wide = 0;
 };
 
 // Entries after the tile16 profile's last row: reads of wave-tile lanes past the valid offsets reach

@@ -53,9 +53,10 @@ constexpr int kMaxTile = 2048;  // records per tile: up to 8 per thread in the t
 constexpr int rpt_of(int lf) { return lf == 0 ? 4 : 8; }
 constexpr int kLdsBudget = 80 * 1024;
 constexpr int kMaxV = 4;  // 16-byte letter vectors per thread per tile (register prefetch)
-// Shifted copies of the profile in LDS: a step's row segment is read with 16-byte ds_read_b128 at a column
-// multiple of 8. (4 copies with 8-byte reads — half the profile's LDS — measured slower, round 4.)
-constexpr int kCopies = 8;
+// Shifted copies of the profile in LDS: a step's row segment is read in 8-byte ds_read_b64 chunks at a column
+// multiple of 4, so copy s = i mod 4 serves step i (see swipe_build_tables for the bank mapping).
+constexpr int kChunk = 8;               // bytes per LDS read (4 int16 entries)
+constexpr int kCopies = kChunk / 2;     // shifted copies
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
@@ -66,15 +67,15 @@ __device__ __forceinline__ uint32_t as_u32(s16x2 v) { return __builtin_bit_cast(
 // hot loop is the lane's letter times a constant plus an immediate offset. A step i < 4 L2W reads columns
 // [8 (i >> 3), 8 (i >> 3) + NOFF) of a row (the RK re-walk: < NOFF + steps); rows are a multiple of 16
 // entries, which keeps the rows' bank offsets a bijection of the letter (swipe_build_tables).
-constexpr int swipe_row(int noff, int l2w) { return (4 * l2w + noff + 8 + 15) & ~15; }  // int16 entries
-constexpr int swipe_stride(int noff, int l2w) { return 2 * swipe_row(noff, l2w) + 16; }  // bytes between rows
+constexpr int swipe_row(int noff, int l2w) { return (4 * l2w + noff + 8 + 7) & ~7; }  // int16 entries
+constexpr int swipe_stride(int noff, int l2w) { return 2 * swipe_row(noff, l2w) + 8; }  // bytes between rows
 constexpr int swipe_copy_bytes(int noff, int l2w) { return kAlphabet * swipe_stride(noff, l2w); }
 constexpr int swipe_prof_bytes(int noff, int l2w) { return kCopies * swipe_copy_bytes(noff, l2w); }
-constexpr int kAnchorBytes = 64 * 32;  // anchor table: int8 [64 steps][32 letters]
+constexpr int kAnchorBytes = 64 * 32 * 4;  // anchor table: int32 [64 steps][32 letters]
 
 struct SwipeLayout {
   int prof_bytes = 0;   // 8 shifted copies of the Dt profile (swipe_prof_bytes)
-  int s_off = 0;        // anchor table: at[i][c] = T[c][Seq1[NOFF + i]] (0 past Seq1), kAnchorBytes
+  int s_off = 0;        // anchor table: at[i][c] = T[c][Seq1[NOFF + i]] (0 past Seq1), int32, kAnchorBytes
   int loff_off = 0, codes_off = 0, res_off = 0, raw_off = 0, total = 0;  // raw: P33 bytes as loaded
 };
 
@@ -104,14 +105,16 @@ using namespace swipe;
 
 // The block's LDS tables, built once per block (before a barrier):
 //  * kCopies shifted int16 difference-profile copies: copy s, row c, entry j' holds Pf[c][j' + s], at byte
-//    s * copy_bytes + c * stride + 2 j'. A step's read is 16-byte chunks of one row (the lane's letter), so the
-//    16 lanes of a ds_read_b128 group read 16 rows at the same column; the row stride of 2 row + 16 bytes
-//    (row a multiple of 16 entries) puts row c's chunks on bank quad (c (row / 8 + 1) + chunk) mod 16, a
-//    bijection of c mod 16: two lanes conflict only for letters 16 apart (different letters on one quad),
-//    and lanes with the same letter read the same address (a broadcast). The address is one multiply-add
-//    of the letter plus immediate offsets — no per-chunk swizzle arithmetic in the hot loop.
-//  * the anchor table at[i][c] = T[c][Seq1[NOFF + i]] (int8; 0 past Seq1 and for the padding letter 0), read
-//    at the lane's letter plus an immediate offset: the anchor diagonal Tot_NOFF costs one LDS read per step.
+//    s * copy_bytes + c * stride + 2 j'. A step's read is 8-byte chunks of one row (the lane's letter), so the
+//    32 lanes of a ds_read_b64 group (2 banks each, 64 banks) read 32 rows at the same column; the row stride
+//    of 2 row + 8 bytes (row a multiple of 8 entries) puts row c's chunk on bank pair
+//    (c (row / 4 + 1) + chunk) mod 32, a bijection of c mod 32 — all 27 letters on distinct bank pairs, and
+//    lanes with the same letter read the same address (a broadcast): conflict-free. (16-byte chunks give a
+//    16-lane group only 16 bank quads for 26 letters: 39 % of the LDS cycles were conflicts, PMC round 5.)
+//    The address is one multiply-add of the letter plus immediate offsets.
+//  * the anchor table at[i][c] = T[c][Seq1[NOFF + i]] (int32: letter c of step i on bank (32 i + c) mod 64,
+//    conflict-free; 0 past Seq1 and for the padding letter 0), read at the lane's letter plus an immediate
+//    offset: the anchor diagonal Tot_NOFF costs one LDS read per step.
 template <bool RK, int KB, int NOFF, int L2W>
 __device__ __forceinline__ void swipe_build_tables(unsigned char* smem, const ProblemView& pv, int tid, int nthreads) {
   constexpr int row = swipe_row(NOFF, L2W), stride = swipe_stride(NOFF, L2W), cb = swipe_copy_bytes(NOFF, L2W);
@@ -125,10 +128,10 @@ __device__ __forceinline__ void swipe_build_tables(unsigned char* smem, const Pr
     *reinterpret_cast<short*>(smem + s * cb + c * stride + 2 * jj) =
         static_cast<short>(RK ? sj - sn : (sj - sn) * (1 << KB) - 1);  // Pf = Dt * 2^KB - 1 (header)
   }
-  int8_t* at = reinterpret_cast<int8_t*>(smem + swipe_prof_bytes(NOFF, L2W));
-  for (int e = tid; e < kAnchorBytes; e += nthreads) {
+  int* at = reinterpret_cast<int*>(smem + swipe_prof_bytes(NOFF, L2W));
+  for (int e = tid; e < kAnchorBytes / 4; e += nthreads) {
     const int i = e >> 5, c = e & 31, j = NOFF + i;
-    at[e] = static_cast<int8_t>(c >= 1 && c < kAlphabet && j < L1 ? pv.lut[c * kLutStride + pv.seq1[j]] : 0);
+    at[e] = c >= 1 && c < kAlphabet && j < L1 ? pv.lut[c * kLutStride + pv.seq1[j]] : 0;
   }
 }
 
@@ -161,7 +164,7 @@ __device__ __forceinline__ Result swipe_lane(const unsigned char* smem, const ui
   constexpr int NP = NOFF / 2;  // packed accumulators
   constexpr int stride = swipe_stride(NOFF, L2W), cb = swipe_copy_bytes(NOFF, L2W);
   const int steps = wave_max_small(on ? L2 : 0);  // L2 <= 4 * L2W <= 64 here
-  const int8_t* at = reinterpret_cast<const int8_t*>(smem + swipe_prof_bytes(NOFF, L2W));
+  const int* at = reinterpret_cast<const int*>(smem + swipe_prof_bytes(NOFF, L2W));
 
   uint32_t E2[NP], B2[NP];
   int anchor = 0;  // Tot_NOFF: the diagonal just past this lane's offsets
@@ -171,25 +174,25 @@ __device__ __forceinline__ Result swipe_lane(const unsigned char* smem, const ui
     B2[q] = 0x80008000u;  // (INT16_MIN, INT16_MIN)
   }
 #pragma unroll
-  for (int i0 = 0; i0 < 4 * L2W; i0 += 8) {
+  for (int i0 = 0; i0 < 4 * L2W; i0 += kCopies) {
     if (i0 >= steps) break;  // wave-uniform
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
+    for (int s = 0; s < kCopies; ++s) {
       const int i = i0 + s;
       // wave-uniform (scalar branch): a wave stops at its longest record, not at the next multiple of
-      // 8 steps (input6: 11 steps instead of 16); the copy index s stays a compile-time constant
+      // kCopies steps; the copy index s stays a compile-time constant
       if (i >= steps) break;
       const int c = (wd[i >> 2] >> (8 * (i & 3))) & 0xff;
-      // copy s holds column j' + s at j': columns i .. i + NOFF - 1 are the 16-byte chunks from column i0
+      // copy s holds column j' + s at j': columns i .. i + NOFF - 1 are the 8-byte chunks from column i0
       const unsigned char* rowp = smem + (s * cb + 2 * i0) + __umul24(c, stride);
       uint32_t v[NP];
 #pragma unroll
-      for (int q = 0; q < NOFF / 8; ++q) {
-        const uint4 x = *reinterpret_cast<const uint4*>(rowp + 16 * q);
-        v[4 * q + 0] = x.x;
-        v[4 * q + 1] = x.y;
-        v[4 * q + 2] = x.z;
-        v[4 * q + 3] = x.w;
+      for (int q = 0; q < NOFF / 4; ++q) {
+        // a relaxed atomic load: one ds_read_b64 per chunk (plain loads get paired into ds_read2_b64, which
+        // reads at half the rate over 32 banks — conflicts again — and needs an address add per pair)
+        const uint64_t x = __atomic_load_n(reinterpret_cast<const uint64_t*>(rowp + 8 * q), __ATOMIC_RELAXED);
+        v[2 * q + 0] = static_cast<uint32_t>(x);
+        v[2 * q + 1] = static_cast<uint32_t>(x >> 32);
       }
       anchor += at[32 * i + c];
 #pragma unroll

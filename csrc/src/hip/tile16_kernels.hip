@@ -71,6 +71,9 @@ __device__ __forceinline__ void add_pair(uint32_t& acc, uint32_t e) {
       : "+v"(acc)
       : "v"(e));
 }
+__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) {  // v_pk_add_u16: both int16 halves
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2, a) + __builtin_bit_cast(s16x2, b));
+}
 __device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b) {
   return __builtin_bit_cast(uint32_t,
                             __builtin_elementwise_max(__builtin_bit_cast(s16x2, a), __builtin_bit_cast(s16x2, b)));
@@ -122,15 +125,21 @@ __device__ __forceinline__ int wave_prefix_sum_dpp(int v) {
 // window m (plan: window-major wave runs, 16-wave aligned, tiles t in [m*T, (m+1)*T) of every record), so it
 // stages only columns [S, S + W) of each profile row (S = m*T*span, W = pv.prof16_window) and the Seq1
 // letters the anchor diagonals read; profile column j lives at LDS column j - S.
-template <int U, bool Win>
+// Wide (whole images only): the LDS entry of a column is the byte pair widened to two int16 halves (4 bytes,
+// expanded while staging), so a step adds both offsets of a lane with one v_pk_add_u16 instead of two SDWA
+// byte adds — 2 VALU per lane and step instead of 3, at twice the profile's LDS (pv.prof16_wide).
+template <int U, bool Win, bool Wide = false>
 __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv, BatchView bv,
                                                                  const WaveStart* __restrict__ starts, int64_t n_waves,
                                                                  const int32_t* __restrict__ long_recs,
                                                                  unsigned long long* __restrict__ keys, int win_tiles) {
+  static_assert(!(Win && Wide), "the windowed sweep stages byte pairs");
+  constexpr int EW = Wide ? 4 : 2;  // LDS bytes per profile column
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // LDS image (tile16_lds_bytes): profile (or its window) | int8 LUT | Seq1 codes (the anchor diagonals)
-  int8_t* lut8 = reinterpret_cast<int8_t*>(smem + pv.prof16_bytes);
-  uint8_t* s1l = smem + pv.prof16_bytes + kProf16Lut8;
+  const int prof_lds = Wide ? 2 * pv.prof16_bytes : pv.prof16_bytes;
+  int8_t* lut8 = reinterpret_cast<int8_t*>(smem + prof_lds);
+  uint8_t* s1l = smem + prof_lds + kProf16Lut8;
   constexpr int kSpan = kSub * U;
   const int64_t w0 = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock16;  // the workgroup's first wave: real
   const int t_base = Win ? (starts[w0].t / win_tiles) * win_tiles : 0;     // first tile of the window
@@ -163,6 +172,25 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
       }
     }
     for (int t = threadIdx.x; t < W + 16; t += blockDim.x) s1l[t] = S + t < pv.L1 ? pv.seq1[S + t] : 0;
+  } else if (Wide) {
+    // 8 byte pairs per 16-byte load -> 8 sign-extended int16 pairs (two 16-byte stores)
+    const uint4* src = reinterpret_cast<const uint4*>(pv.prof16);  // 16-byte padded
+    uint4* dst = reinterpret_cast<uint4*>(smem);
+    const int n16 = pv.prof16_bytes >> 4;
+    auto widen = [](uint32_t pair2) {  // two byte pairs (b0, b1), (b2, b3) -> (sext b0 | sext b1 << 16), ...
+      const uint32_t lo = (static_cast<uint32_t>(static_cast<int8_t>(pair2 & 0xff)) & 0xffffu) |
+                          (static_cast<uint32_t>(static_cast<int8_t>((pair2 >> 8) & 0xff)) << 16);
+      const uint32_t hi = (static_cast<uint32_t>(static_cast<int8_t>((pair2 >> 16) & 0xff)) & 0xffffu) |
+                          (static_cast<uint32_t>(static_cast<int8_t>(pair2 >> 24)) << 16);
+      return make_uint2(lo, hi);
+    };
+    for (int t = threadIdx.x; t < n16; t += blockDim.x) {
+      const uint4 v = src[t];
+      const uint2 a = widen(v.x), b = widen(v.y), c = widen(v.z), d = widen(v.w);
+      dst[2 * t] = make_uint4(a.x, a.y, b.x, b.y);
+      dst[2 * t + 1] = make_uint4(c.x, c.y, d.x, d.y);
+    }
+    stage_bytes(s1l, pv.seq1, pv.L1 + 16);  // Seq1 + zero pad (device copy has kSeq1Pad zeros)
   } else {
     const uint4* src = reinterpret_cast<const uint4*>(pv.prof16);  // 16-byte padded
     uint4* dst = reinterpret_cast<uint4*>(smem);
@@ -175,7 +203,7 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
   const int64_t w = w0 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (w >= n_waves) return;  // wave-uniform; no barrier follows
   const int L1 = pv.L1;
-  const int rowb = 2 * W;  // bytes per LDS profile row
+  const int rowb = EW * W;  // bytes per LDS profile row
   const int lane = threadIdx.x & 63;
   const int t_win_end = Win ? t_base + win_tiles : INT32_MAX;
 
@@ -192,14 +220,14 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
     const int t_stop = li == end_li ? min(end_t, ntiles) : ntiles;
     // lane j of a chunk holds step i0 + j's letter (0 past the record) and its profile row/step offset
     auto letter = [&](int i) { return i < steps ? static_cast<int>(rec[i]) : 0; };
-    auto row_off = [&](int c, int i) { return max(c - 1, 0) * rowb + 2 * i; };
+    auto row_off = [&](int c, int i) { return max(c - 1, 0) * rowb + EW * i; };
     const int c_first = letter(lane);
     unsigned long long acc64 = 0;
     for (; t < t_stop && L2 <= L1; ++t) {
       const int o0 = t * kSpan;
       MOC_DCHECK(o0 >= 0 && o0 <= L1);
       // sub-tile u: lane owns offsets o0 + 128u + 2*lane (low half) and + 1 (high half)
-      const unsigned char* lbase = smem + 2 * (o0 - S) + 4 * lane;
+      const unsigned char* lbase = smem + EW * (o0 - S) + 2 * EW * lane;
       uint32_t acc[U], best[U];
       int DcA[U], DcB[U], mxA[U], mxB[U];
 #pragma unroll
@@ -212,11 +240,15 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
       auto step = [&](int so, int j, bool key) {
         const int soff = __builtin_amdgcn_readlane(so, j);
         const unsigned char* p = lbase + soff;
-        MOC_DCHECK(2 * o0 + 4 * lane + soff + 2 * kSub * (U - 1) + 2 <= pv.prof16_bytes);
+        MOC_DCHECK(EW * o0 + 2 * EW * lane + soff + EW * kSub * (U - 1) + EW <= prof_lds);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          const uint32_t e = *reinterpret_cast<const uint16_t*>(p + 2 * kSub * u);
-          add_pair(acc[u], e);
+          if (Wide) {
+            acc[u] = pk_add(acc[u], *reinterpret_cast<const uint32_t*>(p + EW * kSub * u));
+          } else {
+            const uint32_t e = *reinterpret_cast<const uint16_t*>(p + EW * kSub * u);
+            add_pair(acc[u], e);
+          }
           if (key) best[u] = pk_max(best[u], acc[u]);
         }
       };
@@ -265,13 +297,18 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
           for (int q = 0; q < 8; ++q) {
             const unsigned char* p = lbase + __builtin_amdgcn_readlane(so, j + q);
 #pragma unroll
-            for (int u = 0; u < U; ++u) e[q][u] = *reinterpret_cast<const uint16_t*>(p + 2 * kSub * u);
+            for (int u = 0; u < U; ++u)
+              e[q][u] = Wide ? *reinterpret_cast<const uint32_t*>(p + EW * kSub * u)
+                             : *reinterpret_cast<const uint16_t*>(p + EW * kSub * u);
           }
 #pragma unroll
           for (int q = 0; q < 8; ++q)
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-              add_pair(acc[u], e[q][u]);
+              if (Wide)
+                acc[u] = pk_add(acc[u], e[q][u]);
+              else
+                add_pair(acc[u], e[q][u]);
               best[u] = pk_max(best[u], acc[u]);
             }
         }
@@ -317,13 +354,13 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
   }
 }
 
-int tile16_waves_per_cu(int lds_bytes) {
+int tile16_waves_per_cu(int lds_bytes) {  // lds_bytes: the whole image a workgroup stages
   const int blocks = lds_bytes > 0 ? kProf16MaxLds / lds_bytes : 2;
   return kWavesPerBlock16 * max(1, min(2, blocks));
 }
 
 namespace {
-template <int U, bool Win>
+template <int U, bool Win, bool Wide = false>
 void launch16_t(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream) {
   // dynamic LDS above 64 KiB is declared per kernel and device (engines may live on several devices
   // and threads of one process)
@@ -334,14 +371,14 @@ void launch16_t(const ProblemView& pv, const BatchView& bv, const Plan& plan, hi
   {
     std::lock_guard<std::mutex> lock(mu);
     if (declared.insert(dev).second)
-      MOC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&tile16_search_kernel<U, Win>),
+      MOC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&tile16_search_kernel<U, Win, Wide>),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, kProf16MaxLds));
   }
   const int64_t blocks = (plan.n_waves + kWavesPerBlock16 - 1) / kWavesPerBlock16;
   const int64_t s1_len = Win ? pv.prof16_window : pv.L1;
-  hipLaunchKernelGGL((tile16_search_kernel<U, Win>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock16),
-                     static_cast<size_t>(tile16_lds_bytes(pv.prof16_bytes, s1_len)), stream, pv, bv, plan.starts,
-                     plan.n_waves, plan.long_recs, plan.keys, plan.win_tiles);
+  hipLaunchKernelGGL((tile16_search_kernel<U, Win, Wide>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock16),
+                     static_cast<size_t>(tile16_lds_bytes(Wide ? 2 * pv.prof16_bytes : pv.prof16_bytes, s1_len)),
+                     stream, pv, bv, plan.starts, plan.n_waves, plan.long_recs, plan.keys, plan.win_tiles);
 }
 }  // namespace
 
@@ -353,7 +390,9 @@ void preload_tile16_kernels() {
 void launch_tile16_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream,
                         bool mfma_sweep) {
   const int64_t s1_len = pv.prof16_window > 0 ? pv.prof16_window : pv.L1;
-  if (!pv.prof16 || pv.prof16_bytes <= 0 || tile16_lds_bytes(pv.prof16_bytes, s1_len) > kProf16MaxLds ||
+  const bool wide = pv.prof16_wide && pv.prof16_window == 0 && !mfma_sweep;
+  if (!pv.prof16 || pv.prof16_bytes <= 0 ||
+      tile16_lds_bytes(wide ? 2 * pv.prof16_bytes : pv.prof16_bytes, s1_len) > kProf16MaxLds ||
       (pv.prof16_bytes & 15) || (pv.prof16_window > 0 && (plan.win_tiles <= 0 || mfma_sweep || plan.u > 4)))
     throw Error("launch_tile16_keys: no usable profile");
   if (plan.n_long > 0) MOC_HIP_CHECK(hipMemsetAsync(plan.keys, 0, sizeof(unsigned long long) * plan.n_long, stream));
@@ -366,6 +405,13 @@ void launch_tile16_keys(const ProblemView& pv, const BatchView& bv, const Plan& 
         case 1: launch16_t<1, true>(pv, bv, plan, stream); break;
         case 2: launch16_t<2, true>(pv, bv, plan, stream); break;
         default: launch16_t<4, true>(pv, bv, plan, stream); break;
+      }
+    } else if (wide) {
+      switch (plan.u) {
+        case 1: launch16_t<1, false, true>(pv, bv, plan, stream); break;
+        case 2: launch16_t<2, false, true>(pv, bv, plan, stream); break;
+        case 8: launch16_t<8, false, true>(pv, bv, plan, stream); break;
+        default: launch16_t<4, false, true>(pv, bv, plan, stream); break;
       }
     } else {
       switch (plan.u) {

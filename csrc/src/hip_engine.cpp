@@ -289,8 +289,15 @@ void HipEngine::set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, S
   // the overhang (zero entries past the last row) must cover the widest tile span, 128*U entries: 1024
   // when that still fits the LDS (U = 8 for short records), else 512 (U <= 4, L1 up to 3052)
   auto prof_bytes = [&](int64_t oh) { return ((2 * ((kAlphabet - 1) * L1 + oh)) + 15) & ~int64_t{15}; };
+  // Occupancy first: a CU holds two 16-wave workgroups when the image fits half its LDS, and the sweep is
+  // latency-bound, so the wide overhang (U = 8 tiles, for short records only) is kept only where it costs no
+  // workgroup: input3's 1489-letter Seq1 fits twice with 512 (32 waves per CU), once with 1024 (16).
   int64_t overhang = 2 * dev::kProf16Overhang;
-  if (dev::tile16_lds_bytes(prof_bytes(overhang), L1) > dev::kProf16MaxLds) overhang = dev::kProf16Overhang;
+  const int64_t half = dev::kProf16MaxLds / 2;
+  if (dev::tile16_lds_bytes(prof_bytes(overhang), L1) > dev::kProf16MaxLds ||
+      (dev::tile16_lds_bytes(prof_bytes(overhang), L1) > half &&
+       dev::tile16_lds_bytes(prof_bytes(dev::kProf16Overhang), L1) <= half))
+    overhang = dev::kProf16Overhang;
   int64_t pbytes = prof_bytes(overhang);
   // Seq1 too long for one LDS image: the whole profile lives in device memory and each workgroup stages
   // a window of it (tile16_search_kernel<U, true>); records must then fit a window with two tiles' slack
@@ -305,6 +312,14 @@ void HipEngine::set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, S
                           : 0;
   pbytes = (2 * static_cast<int64_t>(prof.entries.size()) + 15) & ~int64_t{15};
   prof16_overhang_ = t16 ? static_cast<int>(overhang) : 0;
+  // widened entries (two int16 halves per column: one packed add per lane and step) where the doubled image
+  // still fits one CU; MOC_TILE16_WIDE=0 keeps the byte pairs (A/B runs, same results)
+  static const bool wide_env = [] {
+    const char* v = std::getenv("MOC_TILE16_WIDE");
+    return !(v && std::atoi(v) == 0);
+  }();
+  prof16_wide_ = t16 && whole && wide_env &&
+                 dev::tile16_lds_bytes(2 * static_cast<int64_t>(prof16_lds_bytes_), L1) <= dev::kProf16MaxLds;
   const size_t total = t16 ? prof_off + static_cast<size_t>(pbytes) : prof_off;
   std::vector<uint8_t> next(total, 0);
   std::memcpy(next.data(), table_.lut.data(), lut_bytes);
@@ -370,6 +385,7 @@ dev::ProblemView HipEngine::problem_view(int64_t max_l2) const {
   pv.prof16_bytes = prof16_bytes_;
   pv.prof16_window = prof16_window_;
   pv.prof16_entries = prof16_entries_;
+  pv.prof16_wide = prof16_wide_ && !mfma_ ? 1 : 0;
   pv.max_abs_t = table_.max_abs();
   pv.mfma_sweep = mfma_ && d_prof16_ && !prof16_window_ ? 1 : 0;
   return pv;
@@ -513,7 +529,8 @@ std::vector<dev::WaveStart> HipEngine::plan_waves(const int64_t* offsets, const 
     total_tiles += ntiles[li];
   }
   const int s1_len = tp.tile16 && W > 0 ? static_cast<int>(W) : static_cast<int>(L1_);
-  const int waves_per_cu = tp.tile16 ? dev::tile16_waves_per_cu(static_cast<int>(dev::tile16_lds_bytes(prof16_bytes_, s1_len)))
+  const int64_t prof_lds = prof16_wide_ && !mfma_ && W == 0 ? 2 * static_cast<int64_t>(prof16_bytes_) : prof16_bytes_;
+  const int waves_per_cu = tp.tile16 ? dev::tile16_waves_per_cu(static_cast<int>(dev::tile16_lds_bytes(prof_lds, s1_len)))
                                      : tile_waves_per_cu_;
   if (!(tp.tile16 && W > 0)) {
     std::vector<int64_t> pre(static_cast<size_t>(n_long) + 1, 0);
