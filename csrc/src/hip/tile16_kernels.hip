@@ -36,6 +36,7 @@
 
 #include <mutex>
 #include <set>
+#include <type_traits>
 
 #include "kernel_common.hpp"
 #include "moc/runtime/hip_check.hpp"
@@ -48,12 +49,6 @@ using namespace kc;
 namespace {
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
-#ifndef MOC_T16_UNROLL
-#define MOC_T16_UNROLL 64  // hot-loop steps per unrolled group; 64 = the whole chunk (best of 8/16/32/64)
-#endif
-#ifndef MOC_T16_TAIL8
-#define MOC_T16_TAIL8 1  // last chunk in groups of 8 steps (reads first) instead of one step at a time
-#endif
 #ifndef MOC_T16_DPP_SCAN
 #define MOC_T16_DPP_SCAN 1  // tile epilogue scans on DPP instead of ds_bpermute shuffles
 #endif
@@ -93,6 +88,32 @@ __device__ __forceinline__ unsigned long long pass1_candidate(int o, int L1, int
   return key;
 }
 
+// Lane k of each DPP row (16 lanes) broadcast across its row; k a constant once the caller is unrolled
+template <int K>
+__device__ __forceinline__ int newbcast(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, 0x150 + K, 0xf, 0xf, false);
+}
+__device__ __forceinline__ int row_newbcast(int v, int k) {
+  switch (k) {
+    case 0: return newbcast<0>(v);
+    case 1: return newbcast<1>(v);
+    case 2: return newbcast<2>(v);
+    case 3: return newbcast<3>(v);
+    case 4: return newbcast<4>(v);
+    case 5: return newbcast<5>(v);
+    case 6: return newbcast<6>(v);
+    case 7: return newbcast<7>(v);
+    case 8: return newbcast<8>(v);
+    case 9: return newbcast<9>(v);
+    case 10: return newbcast<10>(v);
+    case 11: return newbcast<11>(v);
+    case 12: return newbcast<12>(v);
+    case 13: return newbcast<13>(v);
+    case 14: return newbcast<14>(v);
+    default: return newbcast<15>(v);
+  }
+}
+
 // Inclusive suffix sum over the lanes of a wave (lane l gets sum of v over lanes l..63).
 __device__ __forceinline__ int wave_suffix_sum(int v, int lane) {
 #pragma unroll
@@ -127,7 +148,12 @@ __device__ __forceinline__ int wave_prefix_sum_dpp(int v) {
 // letters the anchor diagonals read; profile column j lives at LDS column j - S.
 // Wide (whole images only): the LDS entry of a column is the byte pair widened to two int16 halves (4 bytes,
 // expanded while staging), so a step adds both offsets of a lane with one v_pk_add_u16 instead of two SDWA
-// byte adds — 2 VALU per lane and step instead of 3, at twice the profile's LDS (pv.prof16_wide).
+// byte adds — 2 VALU per lane and step instead of 3, at twice the profile's LDS (pv.prof16_wide). The widened
+// entries are split by the parity of their flat index e = row * L1 + column: even e at dword e/2 of the first
+// half, odd e at dword e/2 of the second. A step's reads then hit consecutive dwords across the lanes (lane l
+// reads e = o0 + 2l + s), one conflict-free ds_read_b32 per lane and sub-tile; with the entries in column
+// order the lanes' 8-byte stride put two lanes on every bank (SQ_LDS_BANK_CONFLICT = half the LDS cycles,
+// profiles/roofline_r5.md).
 template <int U, bool Win, bool Wide = false>
 __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv, BatchView bv,
                                                                  const WaveStart* __restrict__ starts, int64_t n_waves,
@@ -173,7 +199,8 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
     }
     for (int t = threadIdx.x; t < W + 16; t += blockDim.x) s1l[t] = S + t < pv.L1 ? pv.seq1[S + t] : 0;
   } else if (Wide) {
-    // 8 byte pairs per 16-byte load -> 8 sign-extended int16 pairs (two 16-byte stores)
+    // 8 byte pairs per 16-byte load -> 8 sign-extended int16 pairs: the 4 even entries into the first half,
+    // the 4 odd ones into the second (pv.prof16_bytes each)
     const uint4* src = reinterpret_cast<const uint4*>(pv.prof16);  // 16-byte padded
     uint4* dst = reinterpret_cast<uint4*>(smem);
     const int n16 = pv.prof16_bytes >> 4;
@@ -187,8 +214,8 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
     for (int t = threadIdx.x; t < n16; t += blockDim.x) {
       const uint4 v = src[t];
       const uint2 a = widen(v.x), b = widen(v.y), c = widen(v.z), d = widen(v.w);
-      dst[2 * t] = make_uint4(a.x, a.y, b.x, b.y);
-      dst[2 * t + 1] = make_uint4(c.x, c.y, d.x, d.y);
+      dst[t] = make_uint4(a.x, b.x, c.x, d.x);
+      dst[n16 + t] = make_uint4(a.y, b.y, c.y, d.y);
     }
     stage_bytes(s1l, pv.seq1, pv.L1 + 16);  // Seq1 + zero pad (device copy has kSeq1Pad zeros)
   } else {
@@ -203,7 +230,6 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
   const int64_t w = w0 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (w >= n_waves) return;  // wave-uniform; no barrier follows
   const int L1 = pv.L1;
-  const int rowb = EW * W;  // bytes per LDS profile row
   const int lane = threadIdx.x & 63;
   const int t_win_end = Win ? t_base + win_tiles : INT32_MAX;
 
@@ -220,14 +246,18 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
     const int t_stop = li == end_li ? min(end_t, ntiles) : ntiles;
     // lane j of a chunk holds step i0 + j's letter (0 past the record) and its profile row/step offset
     auto letter = [&](int i) { return i < steps ? static_cast<int>(rec[i]) : 0; };
-    auto row_off = [&](int c, int i) { return max(c - 1, 0) * rowb + EW * i; };
+    auto row_off = [&](int c, int i) {
+      const int e = max(c - 1, 0) * W + i;  // flat entry index past the lane's own
+      return Wide ? ((e & 1) ? pv.prof16_bytes : 0) + 4 * (e >> 1) : 2 * e;
+    };
     const int c_first = letter(lane);
     unsigned long long acc64 = 0;
     for (; t < t_stop && L2 <= L1; ++t) {
       const int o0 = t * kSpan;
       MOC_DCHECK(o0 >= 0 && o0 <= L1);
-      // sub-tile u: lane owns offsets o0 + 128u + 2*lane (low half) and + 1 (high half)
-      const unsigned char* lbase = smem + EW * (o0 - S) + 2 * EW * lane;
+      // sub-tile u: lane owns offsets o0 + 128u + 2*lane (low half) and + 1 (high half); its entries sit at
+      // 4 bytes per lane and 256 bytes per sub-tile in both layouts (Wide: o0 and 2*lane even)
+      const unsigned char* lbase = smem + 2 * (o0 - S) + 4 * lane;
       uint32_t acc[U], best[U];
       int DcA[U], DcB[U], mxA[U], mxB[U];
 #pragma unroll
@@ -240,18 +270,50 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
       auto step = [&](int so, int j, bool key) {
         const int soff = __builtin_amdgcn_readlane(so, j);
         const unsigned char* p = lbase + soff;
-        MOC_DCHECK(EW * o0 + 2 * EW * lane + soff + EW * kSub * (U - 1) + EW <= prof_lds);
+        MOC_DCHECK(2 * o0 + 4 * lane + soff + 2 * kSub * (U - 1) + EW <= prof_lds);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           if (Wide) {
-            acc[u] = pk_add(acc[u], *reinterpret_cast<const uint32_t*>(p + EW * kSub * u));
+            acc[u] = pk_add(acc[u], *reinterpret_cast<const uint32_t*>(p + 2 * kSub * u));
           } else {
-            const uint32_t e = *reinterpret_cast<const uint16_t*>(p + EW * kSub * u);
+            const uint32_t e = *reinterpret_cast<const uint16_t*>(p + 2 * kSub * u);
             add_pair(acc[u], e);
           }
           if (key) best[u] = pk_max(best[u], acc[u]);
         }
       };
+      // The step offsets of 16 steps replicated in every DPP row (lane 16r + k: step 16g + k), so a step's
+      // address is one row_newbcast add: no v_readlane into an SGPR (and its hazard nop) per step.
+      auto replicate = [&](int so, int (&so16)[4]) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) so16[g] = __shfl(so, 16 * g + (lane & 15), 64);
+      };
+      // GG steps from chunk step j (a constant once unrolled), every step a key step: the GG*U profile reads
+      // issue before the first add, so the LDS latency of a group hides under the adds of the group before
+      auto group = [&](const int (&so16)[4], int j, auto gg) {
+        constexpr int GG = decltype(gg)::value;
+        uint32_t e[GG][U];
+#pragma unroll
+        for (int q = 0; q < GG; ++q) {
+          const unsigned char* p = lbase + row_newbcast(so16[(j + q) >> 4], (j + q) & 15);
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            e[q][u] = Wide ? *reinterpret_cast<const uint32_t*>(p + 2 * kSub * u)
+                           : *reinterpret_cast<const uint16_t*>(p + 2 * kSub * u);
+        }
+#pragma unroll
+        for (int q = 0; q < GG; ++q)
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            if (Wide)
+              acc[u] = pk_add(acc[u], e[q][u]);
+            else
+              add_pair(acc[u], e[q][u]);
+            best[u] = pk_max(best[u], acc[u]);
+          }
+      };
+      // full chunks: G steps per group, G * U reads in flight (U = 8 keeps the VGPRs within 4 waves per SIMD)
+      constexpr int G = U >= 8 ? 2 : U >= 4 ? 4 : 8;
       // every 64-step chunk starts from zero halves and folds them into the int32 state at its end
       auto flush = [&](bool any_key) {
 #pragma unroll
@@ -279,8 +341,10 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
         const int c_next = letter(i0 + 64 + lane);
         const int so = row_off(c, i0 + lane);
         anchor_add(c, i0 + lane);
-#pragma unroll MOC_T16_UNROLL
-        for (int j = 0; j < 64; ++j) step(so, j, true);
+        int so16[4];
+        replicate(so, so16);
+#pragma unroll
+        for (int j = 0; j < 64; j += G) group(so16, j, std::integral_constant<int, G>());
         flush(true);
         c = c_next;
       }
@@ -289,30 +353,39 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
         const int so = row_off(c, i0 + lane);
         anchor_add(c, i0 + lane);
         int j = 0;
-#if MOC_T16_TAIL8
-        // groups of 8 steps: all 8*U profile reads issue before the first add (short records live here)
-        for (; j + 8 <= m - 1; j += 8) {
-          uint32_t e[8][U];
+        // groups of 8 steps before the last one (short records live here)
+        if constexpr (U >= 8) {  // 8 sub-tiles: a runtime loop (the unrolled one is too large), v_readlane steps
+          for (; j + 4 <= m - 1; j += 4) {
+            uint32_t e[4][U];
 #pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            const unsigned char* p = lbase + __builtin_amdgcn_readlane(so, j + q);
+            for (int q = 0; q < 4; ++q) {
+              const unsigned char* p = lbase + __builtin_amdgcn_readlane(so, j + q);
 #pragma unroll
-            for (int u = 0; u < U; ++u)
-              e[q][u] = Wide ? *reinterpret_cast<const uint32_t*>(p + EW * kSub * u)
-                             : *reinterpret_cast<const uint16_t*>(p + EW * kSub * u);
-          }
-#pragma unroll
-          for (int q = 0; q < 8; ++q)
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-              if (Wide)
-                acc[u] = pk_add(acc[u], e[q][u]);
-              else
-                add_pair(acc[u], e[q][u]);
-              best[u] = pk_max(best[u], acc[u]);
+              for (int u = 0; u < U; ++u)
+                e[q][u] = Wide ? *reinterpret_cast<const uint32_t*>(p + 2 * kSub * u)
+                               : *reinterpret_cast<const uint16_t*>(p + 2 * kSub * u);
             }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+              for (int u = 0; u < U; ++u) {
+                if (Wide)
+                  acc[u] = pk_add(acc[u], e[q][u]);
+                else
+                  add_pair(acc[u], e[q][u]);
+                best[u] = pk_max(best[u], acc[u]);
+              }
+          }
+        } else {
+          int so16[4];
+          replicate(so, so16);
+#pragma unroll
+          for (int jj = 0; jj + 8 < 64; jj += 8) {
+            if (jj + 8 > m - 1) break;  // wave-uniform
+            group(so16, jj, std::integral_constant<int, 8>());
+            j = jj + 8;
+          }
         }
-#endif
         for (; j < m - 1; ++j) step(so, j, true);
         step(so, m - 1, false);
         flush(m > 1);

@@ -1,6 +1,7 @@
 """CLI behaviour: determinism, semantics flag, error handling, fault injection (no hangs: every run is
 bounded by a timeout), input edge cases through ./final."""
 import json
+import re
 import subprocess
 import numpy as np
 
@@ -700,10 +701,11 @@ def test_device_streaming_large_skip_errors(tr, tmp_path):
 
 
 def _hwloc_components(stderr):
-    for line in stderr.decode(errors="replace").splitlines():
-        if line.startswith("Final list of enabled discovery components:"):
-            return set(line.split(":", 1)[1].strip().split(","))
-    return None
+    # every rank prints its list; with several ranks their stderr lines can interleave mid-line, so match
+    # the lists anywhere and take the components of all of them
+    found = re.findall(r"Final list of enabled discovery components:\s*([A-Za-z0-9_]+(?:,[A-Za-z0-9_]+)*)",
+                       stderr.decode(errors="replace"))
+    return set(",".join(found).split(",")) if found else None
 
 
 @pytest.mark.parametrize("np_", [1, 2])

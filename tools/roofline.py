@@ -26,9 +26,9 @@ SHAPE_KERNEL = {
     "input6": "swipe_direct_kernel<24, 4, false>",
     "input1": "swipe_direct_kernel<24, 16, true>",
     "mid": "short_search_kernel<false, true, true>",
-    "input3": "tile16_search_kernel<2, false>",
-    "input4": "tile16_search_kernel<8, false>",
-    "long20k": "tile16_search_kernel<4, true>",
+    "input3": "tile16_search_kernel<2, false,",  # prefix: <U, windowed, wide> (the wide entries when they fit)
+    "input4": "tile16_search_kernel<8, false,",
+    "long20k": "tile16_search_kernel<4, true,",
 }
 
 
@@ -65,7 +65,7 @@ def main(argv):
         # the counter run's kernel time for the clock (its kernel_bench line), the plain run's for throughput
         clock = span / (pmc_run.get(shape, b)["gpu_ms"] * 1e-3) / 1e9
         cells_per_dispatch = b["cells"]
-        print(f'| {shape} | `{kname}` | {b["cells_per_s"] / 1e12:.2f} | {per["SQ_INSTS_VALU"] * 64 / cells_per_dispatch:.3f} | '
+        print(f'| {shape} | `{row["kernel"].split("(")[0]}` | {b["cells_per_s"] / 1e12:.2f} | {per["SQ_INSTS_VALU"] * 64 / cells_per_dispatch:.3f} | '
               f'{valu:.0%} | {lds:.0%} | {conflict:.0%} | {clock:.2f} | {waits} |')
 
 
