@@ -503,17 +503,142 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
 }
 
 
-// Device-resident byte batches with dense offsets (solve_device, the staged chunks, the rccl transport's
-// byte batches): each WAVE takes 64 consecutive records at a time, one per lane, loaded straight from
-// device memory into registers — no LDS staging, no block scan, and no barrier after the block's tables are
-// built. (The block-synchronous tile pipeline of swipe_search_kernel — grab, barrier, scan, barrier, copy —
-// held device-resident input6 at ~0.45 of its 0.54 ms even with the hot loop removed, round 4's A/B.)
-// Waves walk the 64-record tiles t = wave, wave + waves, ... and load the next tile's offsets while the
-// current one is scored.
+// Device-resident batches (solve_device, the staged chunks, the rccl transport's batches): each WAVE takes 64
+// consecutive records at a time, one per lane, straight from device memory — no block scan and no barrier
+// after the block's tables are built. (The block-synchronous tile pipeline of swipe_search_kernel — grab,
+// barrier, scan, barrier, copy — held device-resident input6 at ~0.45 of its 0.54 ms even with the hot loop
+// removed, round 4's A/B.) Waves walk the 64-record tiles t = wave, wave + waves, ... and load the next
+// tile's offsets (or lengths) while the current one is scored.
+//   LF 0: byte letters, dense offsets — a lane loads its record's aligned words itself.
+//   LF 2: P33 fields (the wire format: 33 bits per 7 letters) with dense or 64-record sparse offsets and
+//         narrow lengths — the wave's tile starts at tile_offset, its lanes' starts come from a wave prefix
+//         sum of the lengths, lanes decode the tile's fields (field = lane, lane + 64, ...) into 8-byte
+//         slots of a wave-private LDS slice (one ds_write_b64 per field: seven byte stores cost +62 % LDS
+//         cycles), and each lane gathers its record's words from there (wave-level ordering
+//         only: the slice is the wave's own).
 constexpr int kBlockD = 512;  // 8 waves share one set of LDS tables
-template <int NOFF, int L2W, bool RK>
+// P33 tiles: one 8-byte slot per field (7 letters + a pad byte) for the fields a tile can span, plus the
+// slots a lane's read may run past the last one
+constexpr int p33_tile_fields(int l2w) { return (64 * 4 * l2w + 6) / 7 + 1; }
+constexpr int p33_lane_slots(int l2w) { return (4 * l2w + 8 + 6) / 7; }  // the letters of words 0..l2w+1
+constexpr int direct_wave_bytes(int l2w) { return 8 * (p33_tile_fields(l2w) + p33_lane_slots(l2w) + 1); }
+inline SwipeLayout direct_layout(int L1, int noff, int l2w, int lf) {
+  SwipeLayout l = swipe_layout(L1, noff, l2w, 0, 0, 0, 0);
+  if (lf == 2) {
+    l.codes_off = al16(l.s_off + kAnchorBytes);
+    l.total = l.codes_off + (kBlockD / 64) * direct_wave_bytes(l2w);
+  }
+  return l;
+}
+
+// Exclusive prefix sum over the lanes of a wave on the DPP network (row shifts, then row broadcasts).
+__device__ __forceinline__ int wave_exclusive_sum_dpp(int v) {
+  int x = v;
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return x - v;
+}
+
+// P33 field f of a tile (33 bits at bit b0 + 33 f of the 32-bit words from base32): its two words are
+// loaded first (p33_field_words, for several fields at once), then decoded to the 7 letter codes 1..26 at
+// d[0..6]. Digits past the first by multiply-high: q = umulhi(v, ceil(2^32 / 26)) is v / 26 exactly for
+// v < 2^30 (the error 4 v / (26 * 2^32) stays under 1 / 26), and v < 26^6 there.
+__device__ __forceinline__ void p33_field_words(const uint32_t* base32, int b0, int f, uint32_t& lo, uint32_t& hi) {
+  const uint32_t* w = base32 + ((b0 + 33 * f) >> 5);
+  lo = __builtin_nontemporal_load(w);
+  hi = __builtin_nontemporal_load(w + 1);
+}
+__device__ __forceinline__ uint2 decode_p33_field(uint32_t lo, uint32_t hi, int b0, int f) {
+  const uint64_t ww = static_cast<uint64_t>(lo) | (static_cast<uint64_t>(hi) << 32);
+  const uint64_t x = (ww >> ((b0 + 33 * f) & 31)) & 0x1FFFFFFFFull;
+  uint32_t v = static_cast<uint32_t>(x >> 1) / 13u;  // x / 26 in 32-bit arithmetic
+  uint32_t d[7];
+  d[0] = static_cast<uint32_t>(x) - 26u * v;
+#pragma unroll
+  for (int j = 1; j < 7; ++j) {
+    const uint32_t q = __umulhi(v, 165191050u);
+    d[j] = v - 26u * q;
+    v = q;
+  }
+  // letter codes are digit + 1; the pad byte stays 0
+  return make_uint2((d[0] | (d[1] << 8) | (d[2] << 16) | (d[3] << 24)) + 0x01010101u,
+                    (d[4] | (d[5] << 8) | (d[6] << 16)) + 0x00010101u);
+}
+
+// The letters of a lane's record from the tile's 8-byte field slots: NS slots from the record's first field
+// (ds_read_b64 each), compacted to contiguous words (one v_perm_b32 each: 4 consecutive letters lie in at most
+// two of the slots' dwords), then shifted by the record's start within its first field (0..6 letters) and
+// masked past its end as record_words does.
+template <int NW>
+__device__ __forceinline__ void record_words_p33(const uint8_t* slots, int q0, int L2, bool on, uint32_t (&wd)[NW]) {
+  constexpr int NS = p33_lane_slots(NW);
+  const int fa = static_cast<int>(__umulhi(static_cast<uint32_t>(q0), 613566757u));  // q0 / 7 (q0 < 2^28)
+  const int sh = q0 - 7 * fa;
+  uint32_t dw[2 * NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    uint2 v = make_uint2(0u, 0u);
+    if (on) v = *reinterpret_cast<const uint2*>(slots + 8 * (fa + k));
+    dw[2 * k] = v.x;
+    dw[2 * k + 1] = v.y;
+  }
+  // compact word c: letters 4c..4c+3 = slot (i / 7) byte (i % 7); byte b of slot k is dw[2k + b / 4] byte b % 4
+  constexpr int NC = NW + 2;
+  uint32_t cw[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int i0 = 4 * c;
+    const int d_first = 2 * (i0 / 7) + (i0 % 7) / 4;  // dword of letter i0
+    uint32_t sel = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int i = i0 + b;
+      const int dwi = 2 * (i / 7) + (i % 7) / 4, byte = (i % 7) % 4;
+      // v_perm_b32(S0 = dw[d_first + 1], S1 = dw[d_first]): selector 0-3 picks S1 bytes, 4-7 S0 bytes
+      sel |= static_cast<uint32_t>((dwi == d_first ? 0 : 4) + byte) << (8 * b);
+    }
+    const uint32_t s1 = d_first < 2 * NS ? dw[d_first] : 0u;
+    const uint32_t s0 = d_first + 1 < 2 * NS ? dw[d_first + 1] : 0u;
+    cw[c] = __builtin_amdgcn_perm(s0, s1, sel);
+  }
+  const bool hs = sh >= 4;
+  const int bs = (sh & 3) * 8;
+  const int rbits = 8 * L2;
+#pragma unroll
+  for (int k = 0; k < NW; ++k) {
+    const uint32_t lo = hs ? cw[k + 1] : cw[k], hi = hs ? cw[k + 2] : cw[k + 1];
+    uint32_t w = bs ? ((lo >> bs) | (hi << (32 - bs))) : lo;
+    const int left = rbits - 32 * k;  // record bits in this word
+    w = left >= 32 ? w : (left <= 0 ? 0u : (w & ((1u << left) - 1u)));
+    wd[k] = on ? w : 0u;
+  }
+}
+
+// Length of record 64 t + lane of a batch with base-6 lengths (three 21-bit octets of 8 digits per 8-byte
+// word): 32-bit index arithmetic and a branch-free digit select (v / 6 = umulhi(v, ceil(2^32 / 6)), exact
+// for v < 2^31).
+__device__ __forceinline__ int lane_length6(const ShortArgs& a, int64_t t, int lane) {
+  const uint32_t octet = static_cast<uint32_t>(t) * 8u + static_cast<uint32_t>(lane >> 3);
+  const uint32_t word = octet / 3u;
+  const uint64_t w = *reinterpret_cast<const uint64_t*>(a.lengths6 + 8 * static_cast<uint64_t>(word));
+  uint32_t v = static_cast<uint32_t>(w >> (21 * (octet - 3u * word))) & 0x1FFFFFu;
+  const int j = lane & 7;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const uint32_t q = __umulhi(v, 715827883u);
+    v = k < j ? q : v;
+  }
+  return a.len_base + static_cast<int>(v - 6u * __umulhi(v, 715827883u));
+}
+
+template <int NOFF, int L2W, int LF, bool RK>
 __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, ShortArgs a, SwipeLayout lay) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr bool P33 = LF == 2;
   constexpr int KB = RK ? 1 : bounds::swipe_kbits(L2W);
   swipe_build_tables<RK, KB, NOFF, L2W>(smem, pv, threadIdx.x, kBlockD);
   __syncthreads();  // the only barrier: tables complete
@@ -522,23 +647,64 @@ __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, S
   const int64_t n = a.n, n_tiles = (n + 63) >> 6;
   const int64_t waves = static_cast<int64_t>(gridDim.x) * (kBlockD / 64);
   int64_t t = static_cast<int64_t>(blockIdx.x) * (kBlockD / 64) + (threadIdx.x >> 6);
-  auto load_offsets = [&](int64_t tt, int64_t& o0, int64_t& o1) {
+  uint8_t* wbuf = smem + lay.codes_off + (threadIdx.x >> 6) * direct_wave_bytes(L2W);  // P33: this wave's
+  // bytes: the record's offsets; P33: the tile's first letter (o0, every lane) and the record's length (o1)
+  auto load_meta = [&](int64_t tt, int64_t& o0, int64_t& o1) {
     const int64_t r = (tt << 6) + lane;
     const bool in = tt < n_tiles && r < n;
-    o0 = in ? a.offsets[r] : 0;
-    o1 = in ? a.offsets[r + 1] : 0;
+    if constexpr (P33) {
+      o0 = tt < n_tiles ? tile_offset(a, tt << 6) : 0;  // 64-record tiles: boundaries of sparse offsets too
+      o1 = !in ? 0 : a.lengths6 && tt < (int64_t{1} << 28) ? lane_length6(a, tt, lane) : record_length(a, r);
+    } else {
+      o0 = in ? a.offsets[r] : 0;
+      o1 = in ? a.offsets[r + 1] : 0;
+    }
   };
   int64_t o0, o1;
-  load_offsets(t, o0, o1);
+  load_meta(t, o0, o1);
   for (; t < n_tiles; t += waves) {  // wave-uniform
     const int64_t r = (t << 6) + lane;
-    const int L2 = static_cast<int>(o1 - o0);
+    const int L2 = static_cast<int>(P33 ? o1 : o1 - o0);
     const bool in = r < n;
     const bool mine = in && (L2 <= L1 ? L1 - L2 + 1 : 1) <= NOFF;  // others belong to the tile kernel
     const bool on = mine && L2 <= L1;
-    // the aligned words holding the record's letters, and only those (never past its last letter's word)
     uint32_t wd[L2W];
-    {
+    if constexpr (P33) {
+      // the tile's first letter and field (wave-uniform: scalar arithmetic), the lane's start within the tile
+      const int64_t st = static_cast<int64_t>(
+          (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(o0 >> 32))))
+           << 32) |
+          static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(o0))));
+      const int64_t f0 = st / 7;
+      const int s0 = static_cast<int>(st - 7 * f0);
+      const int excl = wave_exclusive_sum_dpp(L2);
+      const int nf = (s0 + __builtin_amdgcn_readlane(excl + L2, 63) + 6) / 7;
+      const uint32_t* base32 = reinterpret_cast<const uint32_t*>(a.codes) + ((33 * f0) >> 5);
+      const int b0 = static_cast<int>((33 * f0) & 31);
+      // fields lane, lane + 64, ...: the words of up to kBatch fields per lane are loaded before any is
+      // decoded (one memory latency per batch, not per field)
+      constexpr int kIters = ((64 * 4 * L2W + 6) / 7 + 1 + 63) / 64;  // fields a tile can span / 64
+      constexpr int kBatch = kIters < 4 ? kIters : 4;
+      for (int f0b = 0; f0b < nf; f0b += 64 * kBatch) {  // wave-uniform
+        uint32_t lo[kBatch], hi[kBatch];
+#pragma unroll
+        for (int b = 0; b < kBatch; ++b) {
+          const int f = f0b + 64 * b + lane;
+          lo[b] = hi[b] = 0u;
+          if (f < nf) p33_field_words(base32, b0, f, lo[b], hi[b]);
+        }
+#pragma unroll
+        for (int b = 0; b < kBatch; ++b) {
+          const int f = f0b + 64 * b + lane;
+          if (f < nf) *reinterpret_cast<uint2*>(wbuf + 8 * f) = decode_p33_field(lo[b], hi[b], b0, f);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slice's letters before any lane reads them
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      record_words_p33<L2W>(wbuf, s0 + excl, L2, on, wd);
+    } else {
+      // the aligned words holding the record's letters, and only those (never past its last letter's word)
       const uintptr_t p = reinterpret_cast<uintptr_t>(a.codes + o0);
       const uint32_t* w32 = reinterpret_cast<const uint32_t*>(p & ~uintptr_t{3});
       const int sh = static_cast<int>(p & 3) * 8;
@@ -555,9 +721,10 @@ __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, S
       }
     }
     int64_t n0, n1;
-    load_offsets(t + waves, n0, n1);  // in flight while this tile is scored
+    load_meta(t + waves, n0, n1);  // in flight while this tile is scored
     const Result res = swipe_lane<NOFF, L2W, RK>(smem, wd, L2, on, L1, a.max_l2, pv.semantics);
     if (mine) store_result(a.out, r, a.fmt, res, pv.r2);
+    if constexpr (P33) __builtin_amdgcn_wave_barrier();  // every lane read the slice before the next tile's writes
     o0 = n0;
     o1 = n1;
   }
@@ -590,11 +757,9 @@ bool launch_swipe_noff(const ProblemView& pv, const ShortArgs& b, const SwipeLay
   const bool rk = b.swipe_rk != 0;
 #define MOC_SWIPE_CASE(LW, RKV)                                                                              \
   if (l2w == LW && rk == RKV) {                                                                            \
-    if constexpr (LF == 0) {                                                                               \
-      if (b.lane_direct) {                                                                                 \
-        launch_direct_instance(&swipe_direct_kernel<NO, LW, RKV>, pv, b, lay, num_cus, stream);           \
-        return true;                                                                                       \
-      }                                                                                                    \
+    if (b.lane_direct) {                                                                                   \
+      launch_direct_instance(&swipe_direct_kernel<NO, LW, LF, RKV>, pv, b, lay, num_cus, stream);         \
+      return true;                                                                                         \
     }                                                                                                      \
     hipLaunchKernelGGL((swipe_search_kernel<NO, LW, LF, RKV>), grid, block, lay.total, stream, pv, b, lay); \
     return true;                                                                                           \

@@ -96,10 +96,14 @@ static int tail_div() {
 void launch_swipe(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStream_t stream) {
   if (a.n <= 0) return;
   const int fb = result_bytes(static_cast<ResultFormat>(a.fmt));
-  if (a.lane_direct) {  // device-resident byte letters, dense offsets: the wave-autonomous kernel, LDS tables only
-    if (a.packed33 || a.off_shift) throw Error("launch_swipe: lane-direct batches are byte letters with dense offsets");
-    const SwipeLayout lay = swipe_layout(pv.L1, a.slot, a.rpw, 0, 0, 0, 0);
-    if (!launch_swipe_instance(0, pv, a, lay, dim3(1), dim3(kBlockD), num_cus, stream))
+  if (a.lane_direct) {  // device-resident batches: the wave-autonomous kernel, LDS tables (+ P33 wave slices)
+    if (a.off_shift > 6 || (a.off_shift && !(a.lengths3 || a.lengths4 || a.lengths6 || a.lengths8)) ||
+        (!a.packed33 && a.off_shift))
+      throw Error("launch_swipe: lane-direct batches are byte letters with dense offsets, or P33 letters with "
+                  "64-record sparse offsets and lengths");
+    const int lf = letter_form(a);
+    const SwipeLayout lay = direct_layout(pv.L1, a.slot, a.rpw, lf);
+    if (!launch_swipe_instance(lf, pv, a, lay, dim3(1), dim3(kBlockD), num_cus, stream))
       throw Error("launch_swipe: no instance for this configuration");
     return;
   }

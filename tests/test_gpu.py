@@ -1095,6 +1095,30 @@ def test_extreme_values_device_resident(engine, case):
     assert np.array_equal(as_triples(res, r2=r2), _extreme_ref(prob, Semantics.REFERENCE)), st
 
 
+@pytest.mark.parametrize("case", [c for c in EXTREMES if c[5] == ["swipe"]], ids=[c[0] for c in EXTREMES if c[5] == ["swipe"]])
+def test_extreme_values_wire_p33_device(engine, case):
+    # the rccl transport's batches: P33 letters, 64-record sparse offsets and narrow lengths in device memory,
+    # read in place by the wave-autonomous kernel (each wave decodes its tile's fields into an LDS slice)
+    _, L1, lo, hi, w, kernels, forms = case
+    from mpi_openmp_cuda_amd.parallel.wire import WireSlice
+    from mpi_openmp_cuda_amd.utils.synthetic import make_extreme
+
+    prob = make_extreme(L1, lo, hi, w, copies=61, seed=L1 + 3)
+    engine.set_problem(prob.weights, prob.seq1)
+    wire = WireSlice.from_csr(prob.codes, prob.offsets, letter_format="p33")
+    res = wire.alloc_results(engine)
+    dev = torch.device("cuda:0")
+    lengths = torch.from_numpy(wire.lengths).to(dev) if wire.lengths is not None else None
+    out = torch.zeros(res.nbytes, dtype=torch.uint8, device=dev)
+    engine.solve_wire_device(torch.from_numpy(wire.codes).to(dev), torch.from_numpy(wire.offsets).to(dev), lengths,
+                             wire.n, out, wire.fmt, (wire.l2_min, wire.l2_max), lengths_bits=wire.len_bits or 8,
+                             lengths_base=wire.len_base)
+    st = engine.stats()
+    assert (st["kernels"], st["forms"], st["h2d_bytes"]) == (kernels, forms, 0), st
+    res.view(np.uint8)[:] = out.cpu().numpy()
+    assert np.array_equal(wire.triples(engine), _extreme_ref(prob, Semantics.REFERENCE)), st
+
+
 def test_extreme_values_wire_range_checked(engine):
     # a device batch whose stated length range is narrower than its records is refused (the kernel would
     # size its LDS from the range)

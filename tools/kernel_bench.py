@@ -43,7 +43,7 @@ def make(shape, n):
     return prob
 
 
-def run_wire(shape, n, min_ms):
+def run_wire(shape, n, min_ms, letter_format="p33"):
     """The same records in the wire formats, device-resident (P33 letters, narrow lengths, the narrowest
     results: the rccl transport's batches), through HipSearchEngine.solve_wire_device; kernel time from the
     engine's events."""
@@ -52,7 +52,7 @@ def run_wire(shape, n, min_ms):
     prob = make(shape, n)
     eng = HipSearchEngine(device=0)
     eng.set_problem(prob.weights, prob.seq1)
-    wire = WireSlice.from_csr(prob.codes, prob.offsets)
+    wire = WireSlice.from_csr(prob.codes, prob.offsets, letter_format=letter_format)
     res = wire.alloc_results(eng)
     dev = torch.device("cuda:0")
     letters = torch.from_numpy(wire.codes).to(dev)
@@ -60,7 +60,7 @@ def run_wire(shape, n, min_ms):
     lengths = torch.from_numpy(wire.lengths).to(dev) if wire.lengths is not None else None
     out = torch.zeros(res.nbytes, dtype=torch.uint8, device=dev)
     args = (letters, offsets, lengths, wire.n, out, wire.fmt, (wire.l2_min, wire.l2_max))
-    kw = dict(lengths_bits=wire.len_bits or 8, lengths_base=wire.len_base)
+    kw = dict(lengths_bits=wire.len_bits or 8, lengths_base=wire.len_base, packed33=letter_format == "p33")
     eng.solve_wire_device(*args, **kw)  # warm-up
     first = max(eng.stats()["kernel_ms"], 1e-3)
     iters = max(5, math.ceil(min_ms / first))
@@ -138,7 +138,8 @@ if __name__ == "__main__":
     shapes = args.shapes or list(CASES)
     for shape in shapes:
         for variant in args.variants.split(","):
-            if variant == "wire":
-                print(json.dumps(run_wire(shape, CASES[shape][0], args.min_ms)), flush=True)
+            if variant in ("wire", "wirebytes"):  # wirebytes: the wire lengths and results, byte letters
+                print(json.dumps(run_wire(shape, CASES[shape][0], args.min_ms,
+                                          "bytes" if variant == "wirebytes" else "p33")), flush=True)
             else:
                 print(json.dumps(run(shape, CASES[shape][0], variant, args.min_ms)), flush=True)
