@@ -84,9 +84,13 @@ inline int64_t tile16_lds_bytes(int64_t prof16_bytes, int64_t L1) {
   return prof16_bytes + kProf16Lut8 + ((L1 + 16 + 15) & ~int64_t{15});
 }
 // Widest window (columns) whose rows + 512-entry overhang + LUT + Seq1 window fit one CU's LDS.
-inline int64_t tile16_max_window() {
-  int64_t w = (kProf16MaxLds - kProf16Lut8 - 32 - 2 * kProf16Overhang) / (2 * 26 + 1);
-  while (w > 0 && tile16_lds_bytes(((2 * (26 * w + kProf16Overhang)) + 15) & ~int64_t{15}, w) > kProf16MaxLds) --w;
+// LDS bytes of a window's byte-pair rows + overhang (pv.prof16_bytes of a windowed view)
+inline int64_t tile16_window_bytes(int64_t w) { return ((2 * (26 * w + kProf16Overhang)) + 15) & ~int64_t{15}; }
+// The widest window one LDS image holds (wide: the entries widened to int16 pairs, twice the bytes)
+inline int64_t tile16_max_window(bool wide = false) {
+  const int64_t f = wide ? 2 : 1;
+  int64_t w = (kProf16MaxLds - kProf16Lut8 - 32 - 2 * f * kProf16Overhang) / (2 * f * 26 + 1);
+  while (w > 0 && tile16_lds_bytes(f * tile16_window_bytes(w), w) > kProf16MaxLds) --w;
   return w & ~int64_t{15};
 }
 

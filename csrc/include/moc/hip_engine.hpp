@@ -153,6 +153,8 @@ class HipEngine {
     int u = 2;              // sub-tiles per wave tile
     int win_tiles = 0;      // windowed tile16: tiles per window stride
     bool tile16 = false;    // the plan is for the tile16 sweep (else the LUT tile kernel)
+    int64_t window = 0;     // tile16: columns per LDS window (0: the whole profile is the image)
+    bool wide = false;      // tile16: widened int16-pair entries
   };
   std::vector<dev::WaveStart> plan_waves(const int64_t* offsets, const int32_t* long_recs, int64_t n_long, int part,
                                          int parts, TilePlan& tp) const;
@@ -163,6 +165,11 @@ class HipEngine {
     if (!tp.tile16) {
       pv.prof16 = nullptr;
       pv.mfma_sweep = 0;
+    } else {  // the plan's image: whole or windowed, byte pairs or widened
+      pv.prof16_window = static_cast<int32_t>(tp.window);
+      pv.prof16_bytes = tp.window ? static_cast<int32_t>(dev::tile16_window_bytes(tp.window)) : prof16_bytes_;
+      pv.prof16_wide = tp.wide ? 1 : 0;
+      if (tp.window) pv.mfma_sweep = 0;
     }
     return pv;
   }
@@ -180,6 +187,7 @@ class HipEngine {
   int device_ = 0;
   int num_cus_ = 256;
   int tile_u_ = 0;              // tile-kernel sub-tiles per wave tile (0 = per batch; MOC_TILE_U = 1|2|4)
+  bool tile16_window_wide_ = true;  // widened windows for short records where the widened whole image is too big
   int tile_waves_per_cu_ = 32;  // tile-kernel waves per CU (MOC_TILE_WAVES_PER_CU)
   hipStream_t s_copy_ = nullptr, s_compute_ = nullptr, s_return_ = nullptr;  // copy / return: made on first use
   void ensure_side_streams();

@@ -146,7 +146,7 @@ __device__ __forceinline__ int wave_prefix_sum_dpp(int v) {
 // window m (plan: window-major wave runs, 16-wave aligned, tiles t in [m*T, (m+1)*T) of every record), so it
 // stages only columns [S, S + W) of each profile row (S = m*T*span, W = pv.prof16_window) and the Seq1
 // letters the anchor diagonals read; profile column j lives at LDS column j - S.
-// Wide (whole images only): the LDS entry of a column is the byte pair widened to two int16 halves (4 bytes,
+// Wide: the LDS entry of a column is the byte pair widened to two int16 halves (4 bytes,
 // expanded while staging), so a step adds both offsets of a lane with one v_pk_add_u16 instead of two SDWA
 // byte adds — 2 VALU per lane and step instead of 3, at twice the profile's LDS (pv.prof16_wide). The widened
 // entries are split by the parity of their flat index e = row * L1 + column: even e at dword e/2 of the first
@@ -157,9 +157,8 @@ __device__ __forceinline__ int wave_prefix_sum_dpp(int v) {
 template <int U, bool Win, bool Wide = false>
 __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv, BatchView bv,
                                                                  const WaveStart* __restrict__ starts, int64_t n_waves,
-                                                                 const int32_t* __restrict__ long_recs,
+                                                                 const int32_t* __restrict__ long_recs, int64_t n_long,
                                                                  unsigned long long* __restrict__ keys, int win_tiles) {
-  static_assert(!(Win && Wide), "the windowed sweep stages byte pairs");
   constexpr int EW = Wide ? 4 : 2;  // LDS bytes per profile column
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // LDS image (tile16_lds_bytes): profile (or its window) | int8 LUT | Seq1 codes (the anchor diagonals)
@@ -171,7 +170,44 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
   const int t_base = Win ? (starts[w0].t / win_tiles) * win_tiles : 0;     // first tile of the window
   const int S = t_base * kSpan;                                             // first column of the window
   const int W = Win ? pv.prof16_window : pv.L1;                             // columns per LDS row
-  if (Win) {
+  if (Win && Wide) {
+    // the window's entries e = c * W + x (x < W: global column S + x of row c; then the overhang, zeros),
+    // widened and split by the parity of e as in the whole image (halves of pv.prof16_bytes each)
+    uint32_t* even = reinterpret_cast<uint32_t*>(smem);
+    uint32_t* odd = reinterpret_cast<uint32_t*>(smem + pv.prof16_bytes);
+    const int rows_entries = (kAlphabet - 1) * W;
+    const int n_entries = pv.prof16_bytes >> 1;
+    auto widen1 = [](uint32_t e) {  // byte pair -> two sign-extended int16 halves
+      return (static_cast<uint32_t>(static_cast<int8_t>(e & 0xffu)) & 0xffffu) |
+             (static_cast<uint32_t>(static_cast<int8_t>((e >> 8) & 0xffu)) << 16);
+    };
+    if ((pv.L1 & 7) == 0) {  // rows 16-byte aligned (W and S are multiples of 16): 8 entries per load
+      const int w8 = W >> 3;
+      for (int e = threadIdx.x; e < (kAlphabet - 1) * w8; e += blockDim.x) {
+        const int c = e / w8, x = (e - c * w8) << 3;
+        const int64_t g = static_cast<int64_t>(c) * pv.L1 + S + x;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (g + 8 <= pv.prof16_entries) v = *reinterpret_cast<const uint4*>(pv.prof16 + g);
+        const int d = (c * W + x) >> 1;  // entries c*W + x .. + 7: 4 even, 4 odd, 16-byte aligned
+        *reinterpret_cast<uint4*>(even + d) = make_uint4(widen1(v.x & 0xffffu), widen1(v.y & 0xffffu),
+                                                         widen1(v.z & 0xffffu), widen1(v.w & 0xffffu));
+        *reinterpret_cast<uint4*>(odd + d) = make_uint4(widen1(v.x >> 16), widen1(v.y >> 16), widen1(v.z >> 16),
+                                                        widen1(v.w >> 16));
+      }
+      for (int e = rows_entries + threadIdx.x; e < n_entries; e += blockDim.x) ((e & 1) ? odd : even)[e >> 1] = 0u;
+    } else {
+      for (int e = threadIdx.x; e < n_entries; e += blockDim.x) {
+        uint32_t v = 0;
+        if (e < rows_entries) {
+          const int c = e / W, x = e - c * W;
+          const int64_t g = static_cast<int64_t>(c) * pv.L1 + S + x;
+          if (g < pv.prof16_entries) v = widen1(pv.prof16[g]);
+        }
+        ((e & 1) ? odd : even)[e >> 1] = v;
+      }
+    }
+    for (int t = threadIdx.x; t < W + 16; t += blockDim.x) s1l[t] = S + t < pv.L1 ? pv.seq1[S + t] : 0;
+  } else if (Win) {
     // rows' window columns; entries past the global profile read as 0, then the overhang (zeros)
     uint16_t* dst = reinterpret_cast<uint16_t*>(smem);
     const int rows_entries = (kAlphabet - 1) * W;
@@ -236,10 +272,23 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
   const WaveStart ws = starts[w], we = starts[w + 1];
   int li = __builtin_amdgcn_readfirstlane(ws.li), t = __builtin_amdgcn_readfirstlane(ws.t);
   const int end_li = __builtin_amdgcn_readfirstlane(we.li), end_t = __builtin_amdgcn_readfirstlane(we.t);
+  // The next record's index and letter offsets are loaded one record ahead (scalar loads), and its first 64
+  // letters from the current record's last chunk on (vector loads in flight through that chunk's sweep and
+  // the tile epilogue): a wave moving to its next record does not wait on memory there. (Windowed plans
+  // visit every record once per window, so that wait would come back per window.)
+  const int64_t base_off = bv.offsets[0];
+  auto rec_index = [&](int lj) { return long_recs ? __builtin_amdgcn_readfirstlane(long_recs[lj]) : lj; };
+  int r_cur = li < n_long ? rec_index(li) : 0;
+  int64_t off_a = li < n_long ? bv.offsets[r_cur] : 0, off_b = li < n_long ? bv.offsets[r_cur + 1] : 0;
+  int c_pref = 0;
+  bool pref = false;  // c_pref holds this record's first letters
   while (li < end_li || (li == end_li && t < end_t)) {  // wave-uniform
-    const int r = long_recs ? __builtin_amdgcn_readfirstlane(long_recs[li]) : li;
-    const uint8_t* rec = bv.codes + (bv.offsets[r] - bv.offsets[0]);
-    const int L2 = __builtin_amdgcn_readfirstlane(static_cast<int>(bv.offsets[r + 1] - bv.offsets[r]));
+    const uint8_t* rec = bv.codes + (off_a - base_off);
+    const int L2 = __builtin_amdgcn_readfirstlane(static_cast<int>(off_b - off_a));
+    const bool more = li + 1 < n_long;  // wave-uniform
+    const int r_next = more ? rec_index(li + 1) : 0;
+    const int64_t next_a = more ? bv.offsets[r_next] : 0, next_b = more ? bv.offsets[r_next + 1] : 0;
+    const int next_steps = more && next_b - next_a <= L1 ? static_cast<int>(next_b - next_a) : 0;
     const int steps = L2 <= L1 ? L2 : 0;
     const int need = L2 <= L1 ? L1 - L2 + 1 : 1;
     const int ntiles = min((need + kSpan - 1) / kSpan, t_win_end);
@@ -250,7 +299,8 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
       const int e = max(c - 1, 0) * W + i;  // flat entry index past the lane's own
       return Wide ? ((e & 1) ? pv.prof16_bytes : 0) + 4 * (e >> 1) : 2 * e;
     };
-    const int c_first = letter(lane);
+    const int c_first = pref ? c_pref : letter(lane);
+    pref = false;
     unsigned long long acc64 = 0;
     for (; t < t_stop && L2 <= L1; ++t) {
       const int o0 = t * kSpan;
@@ -349,6 +399,10 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
         c = c_next;
       }
       if (steps > 0) {  // last chunk: 1..64 steps; no hyphen after the final letter
+        if (t + 1 == t_stop && more) {  // the record's last tile here: the next record's first letters
+          c_pref = lane < next_steps ? static_cast<int>(bv.codes[next_a - base_off + lane]) : 0;
+          pref = true;
+        }
         const int m = steps - i0;
         const int so = row_off(c, i0 + lane);
         anchor_add(c, i0 + lane);
@@ -424,6 +478,8 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
     if (lane == 0 && k != 0ull) atomicMax(keys + li, k);
     ++li;
     t = t_base;
+    off_a = next_a;
+    off_b = next_b;
   }
 }
 
@@ -451,7 +507,8 @@ void launch16_t(const ProblemView& pv, const BatchView& bv, const Plan& plan, hi
   const int64_t s1_len = Win ? pv.prof16_window : pv.L1;
   hipLaunchKernelGGL((tile16_search_kernel<U, Win, Wide>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock16),
                      static_cast<size_t>(tile16_lds_bytes(Wide ? 2 * pv.prof16_bytes : pv.prof16_bytes, s1_len)),
-                     stream, pv, bv, plan.starts, plan.n_waves, plan.long_recs, plan.keys, plan.win_tiles);
+                     stream, pv, bv, plan.starts, plan.n_waves, plan.long_recs, plan.n_long, plan.keys,
+                     plan.win_tiles);
 }
 }  // namespace
 
@@ -463,7 +520,7 @@ void preload_tile16_kernels() {
 void launch_tile16_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream,
                         bool mfma_sweep) {
   const int64_t s1_len = pv.prof16_window > 0 ? pv.prof16_window : pv.L1;
-  const bool wide = pv.prof16_wide && pv.prof16_window == 0 && !mfma_sweep;
+  const bool wide = pv.prof16_wide && !mfma_sweep;
   if (!pv.prof16 || pv.prof16_bytes <= 0 ||
       tile16_lds_bytes(wide ? 2 * pv.prof16_bytes : pv.prof16_bytes, s1_len) > kProf16MaxLds ||
       (pv.prof16_bytes & 15) || (pv.prof16_window > 0 && (plan.win_tiles <= 0 || mfma_sweep || plan.u > 4)))
@@ -473,7 +530,13 @@ void launch_tile16_keys(const ProblemView& pv, const BatchView& bv, const Plan& 
   if (mfma_sweep) {
     launch_tile_mfma_sweep(pv, bv, plan, stream);
   } else {
-    if (pv.prof16_window > 0) {
+    if (pv.prof16_window > 0 && wide) {
+      switch (plan.u) {
+        case 1: launch16_t<1, true, true>(pv, bv, plan, stream); break;
+        case 2: launch16_t<2, true, true>(pv, bv, plan, stream); break;
+        default: launch16_t<4, true, true>(pv, bv, plan, stream); break;
+      }
+    } else if (pv.prof16_window > 0) {
       switch (plan.u) {
         case 1: launch16_t<1, true>(pv, bv, plan, stream); break;
         case 2: launch16_t<2, true>(pv, bv, plan, stream); break;

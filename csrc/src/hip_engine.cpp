@@ -159,6 +159,8 @@ HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
     if (v == 1 || v == 2 || v == 4 || v == 8) tile_u_ = v;
   }
   if (const char* t16 = std::getenv("MOC_TILE16")) tile16_ = std::atoi(t16) != 0;
+  // MOC_TILE16_WINWIDE=0: short records on an L1 ~ 1500..3050 problem keep the whole byte-pair image (A/B)
+  if (const char* ww = std::getenv("MOC_TILE16_WINWIDE")) tile16_window_wide_ = std::atoi(ww) != 0;
   if (const char* w = std::getenv("MOC_TILE_WAVES_PER_CU")) {
     const int v = std::atoi(w);
     if (v >= 1 && v <= 32) tile_waves_per_cu_ = v;
@@ -502,7 +504,17 @@ std::vector<dev::WaveStart> HipEngine::plan_waves(const int64_t* offsets, const 
     sum_l2 += L2;
     max_l2 = std::max(max_l2, L2 <= L1_ ? L2 : 0);
   }
-  const int64_t W = prof16_window_;
+  int64_t W = prof16_window_;
+  bool wide = prof16_wide_ && !mfma_ && W == 0;
+  // a whole byte-pair image whose widened form does not fit (L1 ~ 1500..3050): short records take a widened
+  // WINDOW instead (one packed add per lane and step; the window holds U = 4 tiles plus the longest record)
+  if (W == 0 && d_prof16_ && !prof16_wide_ && !mfma_ && tile16_window_wide_ && tile_u_ <= 0 &&
+      max_l2 + 2 * 128 * 4 <= dev::tile16_max_window(true)) {
+    W = dev::tile16_max_window(true);
+    wide = true;
+  }
+  tp.window = W;
+  tp.wide = wide;
   tp.tile16 = d_prof16_ != nullptr && (W == 0 || max_l2 + 2 * 128 <= W);
   // sub-tiles per wave tile: 4 amortises the per-tile setup over short records, 2 keeps more waves busy
   // on long ones (measured, both kernels: profiles/tile_variants.log, profiles/tile16_variants.log)
@@ -529,7 +541,7 @@ std::vector<dev::WaveStart> HipEngine::plan_waves(const int64_t* offsets, const 
     total_tiles += ntiles[li];
   }
   const int s1_len = tp.tile16 && W > 0 ? static_cast<int>(W) : static_cast<int>(L1_);
-  const int64_t prof_lds = prof16_wide_ && !mfma_ && W == 0 ? 2 * static_cast<int64_t>(prof16_bytes_) : prof16_bytes_;
+  const int64_t prof_lds = (wide ? 2 : 1) * (W ? dev::tile16_window_bytes(W) : static_cast<int64_t>(prof16_bytes_));
   const int waves_per_cu = tp.tile16 ? dev::tile16_waves_per_cu(static_cast<int>(dev::tile16_lds_bytes(prof_lds, s1_len)))
                                      : tile_waves_per_cu_;
   if (!(tp.tile16 && W > 0)) {
@@ -552,7 +564,9 @@ std::vector<dev::WaveStart> HipEngine::plan_waves(const int64_t* offsets, const 
     return starts;
   }
   // ---- windowed tile16: window-major runs, whole workgroups per window
-  const int64_t T = std::max<int64_t>(1, (W - span - max_l2) / span);
+  // (a widened window, chosen for short records only, packs one more tile: its columns
+  // [0, T * span + max L2) still lie inside the window)
+  const int64_t T = std::max<int64_t>(1, (W - (wide ? 0 : span) - max_l2) / span);
   tp.win_tiles = static_cast<int32_t>(T);
   int32_t max_nt = 0;
   for (int64_t li = 0; li < n_long; ++li) max_nt = std::max(max_nt, ntiles[li]);
@@ -567,6 +581,31 @@ std::vector<dev::WaveStart> HipEngine::plan_waves(const int64_t* offsets, const 
   const int64_t lo = C * part / parts, hi = C * (part + 1) / parts;
   constexpr int kWg = 16;  // waves per tile16 workgroup
   const int64_t target_wgs = std::max<int64_t>(1, static_cast<int64_t>(num_cus_) * waves_per_cu / kWg);
+  // workgroups per window in proportion to its cost, largest remainders first, so that they add up to
+  // target_wgs: one workgroup over the resident count waits for a second round (ceil per window put input4's
+  // 3 windows at 3 x 86 = 258 on 256 CUs: 2.4 ms instead of 1.3)
+  std::vector<int64_t> wgs_of(static_cast<size_t>(M), 0);
+  {
+    std::vector<std::pair<double, int64_t>> frac;
+    int64_t used = 0;
+    for (int64_t m = 0; m < M; ++m) {
+      const int64_t a = std::max(lo, wstart[m]) - wstart[m], b = std::min(hi, wstart[m + 1]) - wstart[m];
+      if (b <= a) continue;
+      const double ideal = static_cast<double>(target_wgs) * static_cast<double>(b - a) /
+                           static_cast<double>(std::max<int64_t>(hi - lo, 1));
+      const int64_t share_tiles = std::max<int64_t>(1, (b - a) / std::max<int64_t>(1, C / std::max<int64_t>(total_tiles, 1)));
+      const int64_t cap = std::max<int64_t>(1, (share_tiles + kWg - 2) / (kWg - 1));
+      wgs_of[m] = std::clamp<int64_t>(static_cast<int64_t>(ideal), 1, cap);
+      used += wgs_of[m];
+      if (wgs_of[m] < cap) frac.emplace_back(ideal - static_cast<double>(wgs_of[m]), m);
+    }
+    std::sort(frac.begin(), frac.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
+    for (const auto& f : frac) {
+      if (used >= target_wgs) break;
+      ++wgs_of[f.second];
+      ++used;
+    }
+  }
   std::vector<int64_t> pre(static_cast<size_t>(n_long) + 1);
   for (int64_t m = 0; m < M; ++m) {
     const int64_t a = std::max(lo, wstart[m]) - wstart[m], b = std::min(hi, wstart[m + 1]) - wstart[m];
@@ -581,9 +620,7 @@ std::vector<dev::WaveStart> HipEngine::plan_waves(const int64_t* offsets, const 
       if (t >= count(li, m)) return dev::WaveStart{static_cast<int32_t>(li + 1), static_cast<int32_t>(m * T)};
       return dev::WaveStart{static_cast<int32_t>(li), static_cast<int32_t>(m * T + t)};
     };
-    const int64_t share_tiles = std::max<int64_t>(1, (b - a) / std::max<int64_t>(1, C / std::max<int64_t>(total_tiles, 1)));
-    const int64_t wgs = std::clamp<int64_t>((target_wgs * (b - a) + (hi - lo) - 1) / std::max<int64_t>(hi - lo, 1), 1,
-                                            (share_tiles + kWg - 2) / (kWg - 1));
+    const int64_t wgs = wgs_of[m];
     const int64_t real = wgs * kWg - 1;  // + one empty marker wave that ends the window's list
     for (int64_t q = 0; q < real; ++q) starts.push_back(locate(a + (b - a) * q / real));
     starts.push_back(locate(b));  // the last real wave ends at the share's end ...

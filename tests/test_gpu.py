@@ -807,6 +807,33 @@ def test_tile16_windowed(engine, L1, shape, n):
         assert np.array_equal(as_triples(decode_keys(keys, prob)), ref), sem
 
 
+@pytest.mark.parametrize("L1", [1600, 2001, 2976])
+def test_tile16_window_wide(engine, L1):
+    # short records on a Seq1 whose widened image does not fit one CU (L1 ~ 1500..3050): the sweep stages a
+    # widened window (tile16_search_kernel<U, true, true>; L1 = 2001 takes the unaligned staging loop), ==
+    # the CPU engine, both semantics, and against the whole byte-pair image (MOC_TILE16_WINWIDE=0 path)
+    base = make_synthetic("input4", 300, seed=L1)
+    rng = np.random.default_rng(L1)
+    prob = Problem(base.weights, rng.integers(1, 27, size=L1, dtype=np.uint8), base.codes, base.offsets)
+    for sem in (Semantics.REFERENCE, Semantics.SPEC):
+        engine.set_problem(prob.weights, prob.seq1, sem)
+        assert np.array_equal(as_triples(engine.solve(prob.codes, prob.offsets)), as_triples(search_cpu(prob, sem)))
+        assert engine.stats()["kernels"] == ["tile16"], engine.stats()
+
+
+@pytest.mark.parametrize("w,forms", [((63, 0, 0, 64), ["tile16"]), ((64, 0, 0, 64), ["tiles_key32"])])
+def test_extreme_values_tile16_window_wide(engine, w, forms):
+    # the int8 profile bound on the widened-window image: |D| at its extreme, at the bound and one past
+    from mpi_openmp_cuda_amd.utils.synthetic import make_extreme
+
+    prob = make_extreme(2400, 40, 90, w, copies=3, seed=7)
+    engine.set_problem(prob.weights, prob.seq1)
+    got = engine.solve(prob.codes, prob.offsets, fmt="auto")
+    st = engine.stats()
+    assert st["forms"] == forms, st
+    assert np.array_equal(as_triples(got, r2=st["r2"]), _extreme_ref(prob, Semantics.REFERENCE)), st
+
+
 # ---- the Python distributed driver on GPU ranks (parallel/search.py -> parallel/wire.py WireSlice): the same
 # wire-format step bench.py times, pinned here to the goldens and to the CPU engine
 @pytest.mark.parametrize("transport", ["shm"])

@@ -1,23 +1,25 @@
 #!/bin/bash
-# Round-5 roofline counters (profiles/roofline_r5.md): SQ counters of every search kernel, device-resident
-# (tools/kernel_bench.py), one rocprofv3 pass per counter set, each with its own time limit.
+# Round-5 roofline (profiles/roofline_r5.md): the instruction-rate probe, plain throughput of every search
+# kernel (tools/kernel_bench.py, device-resident), then SQ counters in passes of their own, each with its own
+# time limit. Shapes run in separate passes so each kernel instance's counters belong to one shape.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out/r5
-SHAPES=${SHAPES:-"input6 input1 mid input3 input4 long20k"}
-# plain throughput first (no counters), every shape
-timeout -k 10 300 python3 tools/kernel_bench.py $SHAPES > gpurun_out/r5/kb_all.log 2>&1 || { tail -5 gpurun_out/r5/kb_all.log; exit 1; }
-timeout -s KILL 60 rocprofv3 --list-avail > gpurun_out/r5/pmc_avail.txt 2>&1 || true
-grep -o "SQ_[A-Z_0-9]*" gpurun_out/r5/pmc_avail.txt | sort -u | tr '\n' ' ' | head -c 4000 > gpurun_out/r5/pmc_sq_names.txt
+OUT=gpurun_out/r5roof
+mkdir -p $OUT
+timeout -k 10 180 build/isa_peak 20000 > $OUT/isa_peak.log 2>&1 || { tail -5 $OUT/isa_peak.log; exit 1; }
+timeout -k 10 300 python3 tools/kernel_bench.py input6 input1 mid input3 limits input4 long20k > $OUT/kb_all.log 2>&1 || { tail -5 $OUT/kb_all.log; exit 1; }
+timeout -k 10 200 python3 tools/kernel_bench.py input6 input1 --variants wire >> $OUT/kb_all.log 2>&1 || { tail -5 $OUT/kb_all.log; exit 1; }
+SETS=("SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_WAIT_ANY"
+      "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE")
 i=0
-for set in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU" \
-           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE"; do
-  i=$((i+1))
-  timeout -s KILL 300 rocprofv3 --pmc $set --output-format csv -d gpurun_out/r5/pmc_$i -o k \
-    -- python3 tools/kernel_bench.py --min-ms 15 $SHAPES > gpurun_out/r5/pmc_$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/r5/pmc_$i.log; exit 1; }
-  echo "pass $i ok"
+for args in "input6 input1 mid" "input3 limits" "input4 long20k" "input6 input1 --variants wire"; do
+  for j in 0 1; do
+    i=$((i+1))
+    timeout -s KILL 300 rocprofv3 --pmc ${SETS[$j]} --output-format csv -d $OUT/pmc_$i -o k \
+      -- python3 tools/kernel_bench.py --min-ms 15 $args > $OUT/pmc_$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/pmc_$i.log; exit 1; }
+    echo "pass $i ok ($args, set $j)"
+  done
 done
-python3 tools/pmc_summary.py gpurun_out/r5/pmc_1 gpurun_out/r5/pmc_2 > gpurun_out/r5/pmc_summary.jsonl
-python3 tools/roofline.py gpurun_out/r5/pmc_summary.jsonl gpurun_out/r5/pmc_1.log gpurun_out/r5/kb_all.log \
-  > gpurun_out/r5/roofline.md
-cat gpurun_out/r5/roofline.md
+for k in 1 3 5 7; do python3 tools/pmc_summary.py $OUT/pmc_$k $OUT/pmc_$((k+1)); done > $OUT/pmc_summary.jsonl
+python3 tools/roofline.py $OUT/pmc_summary.jsonl $OUT/kb_all.log > $OUT/roofline.md
+cat $OUT/roofline.md
