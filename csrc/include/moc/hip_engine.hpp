@@ -188,6 +188,7 @@ class HipEngine {
   int num_cus_ = 256;
   int tile_u_ = 0;              // tile-kernel sub-tiles per wave tile (0 = per batch; MOC_TILE_U = 1|2|4)
   bool tile16_window_wide_ = true;  // widened windows for short records where the widened whole image is too big
+  bool short_window_u8_ = true;     // ... with 8 sub-tiles per wave tile (MOC_TILE16_WIN_U8=0: 4)
   int tile_waves_per_cu_ = 32;  // tile-kernel waves per CU (MOC_TILE_WAVES_PER_CU)
   hipStream_t s_copy_ = nullptr, s_compute_ = nullptr, s_return_ = nullptr;  // copy / return: made on first use
   void ensure_side_streams();

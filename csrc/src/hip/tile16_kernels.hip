@@ -523,7 +523,8 @@ void launch_tile16_keys(const ProblemView& pv, const BatchView& bv, const Plan& 
   const bool wide = pv.prof16_wide && !mfma_sweep;
   if (!pv.prof16 || pv.prof16_bytes <= 0 ||
       tile16_lds_bytes(wide ? 2 * pv.prof16_bytes : pv.prof16_bytes, s1_len) > kProf16MaxLds ||
-      (pv.prof16_bytes & 15) || (pv.prof16_window > 0 && (plan.win_tiles <= 0 || mfma_sweep || plan.u > 4)))
+      (pv.prof16_bytes & 15) ||
+      (pv.prof16_window > 0 && (plan.win_tiles <= 0 || mfma_sweep || plan.u > (wide ? 8 : 4))))
     throw Error("launch_tile16_keys: no usable profile");
   if (plan.n_long > 0) MOC_HIP_CHECK(hipMemsetAsync(plan.keys, 0, sizeof(unsigned long long) * plan.n_long, stream));
   if (plan.n_waves <= 0) return;
@@ -534,6 +535,7 @@ void launch_tile16_keys(const ProblemView& pv, const BatchView& bv, const Plan& 
       switch (plan.u) {
         case 1: launch16_t<1, true, true>(pv, bv, plan, stream); break;
         case 2: launch16_t<2, true, true>(pv, bv, plan, stream); break;
+        case 8: launch16_t<8, true, true>(pv, bv, plan, stream); break;
         default: launch16_t<4, true, true>(pv, bv, plan, stream); break;
       }
     } else if (pv.prof16_window > 0) {

@@ -161,6 +161,7 @@ HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
   if (const char* t16 = std::getenv("MOC_TILE16")) tile16_ = std::atoi(t16) != 0;
   // MOC_TILE16_WINWIDE=0: short records on an L1 ~ 1500..3050 problem keep the whole byte-pair image (A/B)
   if (const char* ww = std::getenv("MOC_TILE16_WINWIDE")) tile16_window_wide_ = std::atoi(ww) != 0;
+  if (const char* w8 = std::getenv("MOC_TILE16_WIN_U8")) short_window_u8_ = std::atoi(w8) != 0;
   if (const char* w = std::getenv("MOC_TILE_WAVES_PER_CU")) {
     const int v = std::atoi(w);
     if (v >= 1 && v <= 32) tile_waves_per_cu_ = v;
@@ -527,6 +528,8 @@ std::vector<dev::WaveStart> HipEngine::plan_waves(const int64_t* offsets, const 
     // U = 2 -> 8.4, U = 1 -> 7.0; profiles/kernel_bench_long.log)
     if (tile_u_ <= 0) u = 4;
     while (u > 1 && max_l2 + 2 * 128 * u > W) u /= 2;
+    // widened windows (short records): 8 sub-tiles when one tile and the longest record fit the window
+    if (wide && tile_u_ <= 0 && short_window_u8_ && max_l2 + 128 * 8 <= W) u = 8;
   }
   tp.u = u;
   const int span = dev::tile_span(tp.tile16, u);
