@@ -31,13 +31,18 @@ def load(d):
 
 
 def main(dirs):
+    # each pass (directory) is its own run: its dispatch count can differ from another pass's (the bench sizes
+    # its iteration count from a first timing), so every counter is scaled to the dispatch count of the first
+    # pass that saw the kernel — the sums stay "per that many dispatches" across passes
     merged = defaultdict(dict)
     ndisp = {}
     for d in dirs:
         tot, disp = load(d)
         for k, v in tot.items():
-            merged[k].update(v)
-            ndisp[k] = max(ndisp.get(k, 0), len(disp[k]))
+            n = len(disp[k])
+            ndisp.setdefault(k, n)
+            scale = ndisp[k] / n if n else 1.0
+            merged[k].update({c: x * scale for c, x in v.items()})
     for k, v in sorted(merged.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0)):
         out = {"kernel": k[:90], "dispatches": ndisp.get(k, 0)}
         out.update({c: int(x) for c, x in sorted(v.items())})

@@ -31,8 +31,8 @@ ROWS = [
     ("mid", "tile16", "short_search_kernel<", ""),
     ("input3", "tile16", "tile16_search_kernel<2, false, true>", "widened pairs"),
     ("limits", "tile16", "tile16_search_kernel<2, false, false>", "byte pairs"),
-    ("input4", "tile16", "tile16_search_kernel<8, false, false>", "byte pairs"),
-    ("long20k", "tile16", "tile16_search_kernel<4, true, false>", "windowed byte pairs"),
+    ("input4", "tile16", "tile16_search_kernel<8, true, true>", "widened windows"),
+    ("long20k", "tile16", "tile16_search_kernel<4, true, false>", "byte-pair windows"),
 ]
 
 
