@@ -67,6 +67,8 @@ struct ProblemView {
   // 1: the tile16 sweep stages each byte pair widened to two int16 halves (whole images only; the LDS image
   // is then tile16_lds_bytes(2 * prof16_bytes, L1))
   int32_t prof16_wide = 0;
+  // tile16: index bits of the 32-bit selection keys (bounds::tile16_key32_bits; 0 = 64-bit keys)
+  int32_t t16_key_bits = 0;
 };
 
 // Entries after the tile16 profile's last row: reads of wave-tile lanes past the valid offsets reach
@@ -213,7 +215,9 @@ void launch_tile_keys(const ProblemView& pv, const BatchView& bv, const Plan& pl
 // Arithmetic form (moc::bounds::kFormTile16 / kFormMfma / kFormTilesKey32 / kFormTilesKey64) of the sweep
 // launch_tile_keys runs for this problem view.
 inline int32_t tile_form(const ProblemView& pv) {
-  if (pv.prof16) return pv.mfma_sweep ? bounds::kFormMfma : bounds::kFormTile16;
+  if (pv.prof16)
+    return pv.mfma_sweep ? bounds::kFormMfma
+                         : bounds::kFormTile16 | (pv.t16_key_bits ? bounds::kFormTile16Key32 : 0);
   return pv.key_shift > 0 ? bounds::kFormTilesKey32 : bounds::kFormTilesKey64;
 }
 void launch_finalize_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, void* out, int fmt,

@@ -170,6 +170,7 @@ class HipEngine {
       pv.prof16_bytes = tp.window ? static_cast<int32_t>(dev::tile16_window_bytes(tp.window)) : prof16_bytes_;
       pv.prof16_wide = tp.wide ? 1 : 0;
       if (tp.window) pv.mfma_sweep = 0;
+      if (!pv.mfma_sweep) pv.t16_key_bits = bounds::tile16_key32_bits(L1_, table_.max_abs(), max_l2);
     }
     return pv;
   }

@@ -82,6 +82,16 @@ inline bool profile16_exact(int32_t dmin, int32_t dmax, int32_t tabs) {
 }
 static_assert(kProf16Fold * 128 < 32768, "tile16 int16 partial sums");
 
+// tile16's per-lane selection in 32-bit keys: ((score + 2^(31 - IB)) << IB) | (2^IB - 1 - idx), idx = 2o +
+// mutated <= 2 L1 + 1 < 2^IB. Exact when every score fits the 32 - IB score bits: |score| <= max|T| * L2
+// < 2^(31 - IB). Returns IB, or 0 when the 64-bit keys are needed.
+inline int tile16_key32_bits(int64_t L1, int32_t max_abs_t, int64_t max_l2) {
+  int ib = 1;
+  while ((int64_t{1} << ib) <= 2 * L1 + 1) ++ib;
+  if (ib > 24) return 0;
+  return static_cast<int64_t>(max_abs_t) * max_l2 < (int64_t{1} << (31 - ib)) ? ib : 0;
+}
+
 // Form bits reported per solve (EngineStats::forms; Python: stats()["forms"]).
 enum FormBits : int32_t {
   kFormSwipeKBits = 1,    // swipe, int16 keys with k bits
@@ -93,6 +103,7 @@ enum FormBits : int32_t {
   kFormTilesKey32 = 64,   // LUT tile kernel, int32 keys
   kFormTilesKey64 = 128,  // LUT tile kernel, int64 keys
   kFormMfma = 256,        // matrix-core sweep over the tile16 profile
+  kFormTile16Key32 = 512, // tile16's per-lane selection in 32-bit keys (tile16_key32_bits)
 };
 
 }  // namespace bounds

@@ -140,6 +140,22 @@ __device__ __forceinline__ int wave_prefix_sum_dpp(int v) {
   v += dpp_or0<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
   return v;
 }
+// Maximum over the lanes of a wave (unsigned; 0 is the identity) on the DPP network, in every lane's result
+// at lane 63.
+__device__ __forceinline__ uint32_t wave_max_u32_dpp(uint32_t v) {
+  auto dpp = [](uint32_t x, auto ctrl, auto row_mask) {
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), decltype(ctrl)::value,
+                                                             decltype(row_mask)::value, 0xf, false));
+  };
+  using std::integral_constant;
+  v = max(v, dpp(v, integral_constant<int, 0x111>(), integral_constant<int, 0xf>()));  // row_shr:1
+  v = max(v, dpp(v, integral_constant<int, 0x112>(), integral_constant<int, 0xf>()));  // row_shr:2
+  v = max(v, dpp(v, integral_constant<int, 0x114>(), integral_constant<int, 0xf>()));  // row_shr:4
+  v = max(v, dpp(v, integral_constant<int, 0x118>(), integral_constant<int, 0xf>()));  // row_shr:8
+  v = max(v, dpp(v, integral_constant<int, 0x142>(), integral_constant<int, 0xa>()));  // row_bcast:15
+  v = max(v, dpp(v, integral_constant<int, 0x143>(), integral_constant<int, 0xc>()));  // row_bcast:31
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
+}
 }  // namespace
 
 // Win (windowed): Seq1 is longer than one LDS image holds. The workgroup's waves all walk tiles of one
@@ -267,6 +283,8 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
   if (w >= n_waves) return;  // wave-uniform; no barrier follows
   const int L1 = pv.L1;
   const int lane = threadIdx.x & 63;
+  const int kib = pv.t16_key_bits;  // wave-uniform: 32-bit selection keys (0: 64-bit)
+  const uint32_t kmask = kib ? (1u << kib) - 1u : 0u;
   const int t_win_end = Win ? t_base + win_tiles : INT32_MAX;
 
   const WaveStart ws = starts[w], we = starts[w + 1];
@@ -293,6 +311,8 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
     const int need = L2 <= L1 ? L1 - L2 + 1 : 1;
     const int ntiles = min((need + kSpan - 1) / kSpan, t_win_end);
     const int t_stop = li == end_li ? min(end_t, ntiles) : ntiles;
+    const int last = L1 - L2;
+    const bool v0_at_last = pv.semantics == static_cast<int>(Semantics::Spec) || L2 == L1;
     // lane j of a chunk holds step i0 + j's letter (0 past the record) and its profile row/step offset
     auto letter = [&](int i) { return i < steps ? static_cast<int>(rec[i]) : 0; };
     auto row_off = [&](int c, int i) {
@@ -302,6 +322,7 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
     const int c_first = pref ? c_pref : letter(lane);
     pref = false;
     unsigned long long acc64 = 0;
+    uint32_t acc32 = 0;  // pv.t16_key_bits: the same selection in 32-bit keys
     for (; t < t_stop && L2 <= L1; ++t) {
       const int o0 = t * kSpan;
       MOC_DCHECK(o0 >= 0 && o0 <= L1);
@@ -470,12 +491,35 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
         const int totA = totB + ca;          // Tot_{oa}
         carry = __shfl(totA, 0, 64);
 #endif
-        acc64 = max_u64(acc64, pass1_candidate(oa, L1, L2, pv.semantics, totA, totB, mxA[u]));
-        acc64 = max_u64(acc64, pass1_candidate(oa + 1, L1, L2, pv.semantics, totB, totB - cb, mxB[u]));
+        if (kib) {
+          // keys ((score + 2^(31 - kib)) << kib) | (2^kib - 1 - idx): the bias and the index term are one
+          // per-lane constant, so a key is one shift-add of the score (moc/kernel_bounds.hpp tile16_key32_bits)
+          const uint32_t c0 = 0x80000000u + kmask - 2u * static_cast<uint32_t>(oa);  // idx 2 oa
+          const uint32_t kA0 = (static_cast<uint32_t>(totA) << kib) + c0;
+          const uint32_t kA1 = ((static_cast<uint32_t>(mxA[u]) + static_cast<uint32_t>(totB)) << kib) + (c0 - 1u);
+          const uint32_t kB0 = (static_cast<uint32_t>(totB) << kib) + (c0 - 2u);
+          const uint32_t kB1 = ((static_cast<uint32_t>(mxB[u]) + static_cast<uint32_t>(totB - cb)) << kib) + (c0 - 3u);
+          // validity as pass1_candidate: o <= last (o < last, or L2 == L1 / spec semantics, for the
+          // un-mutated one), mutants at o < last with L2 >= 2
+          const uint32_t a0 = oa < last || (oa == last && v0_at_last) ? kA0 : 0u;
+          const uint32_t a1 = oa < last && L2 >= 2 ? kA1 : 0u;
+          const uint32_t b0 = oa + 1 < last || (oa + 1 == last && v0_at_last) ? kB0 : 0u;
+          const uint32_t b1 = oa + 1 < last && L2 >= 2 ? kB1 : 0u;
+          acc32 = max(max(acc32, max(a0, a1)), max(b0, b1));
+        } else {
+          acc64 = max_u64(acc64, pass1_candidate(oa, L1, L2, pv.semantics, totA, totB, mxA[u]));
+          acc64 = max_u64(acc64, pass1_candidate(oa + 1, L1, L2, pv.semantics, totB, totB - cb, mxB[u]));
+        }
       }
     }
-    const unsigned long long k = wave_max_u64(acc64);
-    if (lane == 0 && k != 0ull) atomicMax(keys + li, k);
+    if (kib) {
+      const uint32_t k = wave_max_u32_dpp(acc32);
+      if (lane == 0 && k != 0u)
+        atomicMax(keys + li, final_key(static_cast<int>(k >> kib) - (1 << (31 - kib)), kmask - (k & kmask)));
+    } else {
+      const unsigned long long k = wave_max_u64(acc64);
+      if (lane == 0 && k != 0ull) atomicMax(keys + li, k);
+    }
     ++li;
     t = t_base;
     off_a = next_a;

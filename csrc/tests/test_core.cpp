@@ -1167,8 +1167,10 @@ Result key32_record(const ScoreTable& t, const std::vector<uint8_t>& s1, const u
 
 // tile16_search_kernel + resolve_long_kernel (tile16_kernels.hip, align_kernels.hip) over a Profile16 whose
 // bytes are taken as given (so a profile built past the bound wraps as the kernel would see it).
+// kib > 0: the per-lane selection in 32-bit keys ((score << kib) + 2^31 + 2^kib - 1 - idx, kernel_bounds.hpp
+// tile16_key32_bits), converted back to the 64-bit key at the end as the kernel does.
 Result tile16_record(const ScoreTable& t, const std::vector<uint8_t>& s1, const std::vector<uint16_t>& prof,
-                     const uint8_t* s2, int64_t L2, int64_t span, Semantics sem) {
+                     const uint8_t* s2, int64_t L2, int64_t span, Semantics sem, int kib = 0) {
   const int64_t L1 = static_cast<int64_t>(s1.size());
   auto entry = [&](int c, int64_t j) { return prof[static_cast<size_t>((c - 1) * L1 + j)]; };
   const int64_t need = L2 <= L1 ? L1 - L2 + 1 : 0;
@@ -1200,12 +1202,21 @@ Result tile16_record(const ScoreTable& t, const std::vector<uint8_t>& s1, const 
     for (int64_t o = oA - 1; o >= o0; --o) tot[o] = (acc += Dc[o]);
   }
   uint64_t best_key = 0;
+  uint32_t best32 = 0;
+  const uint32_t kmask = kib ? (1u << kib) - 1u : 0u;
+  auto offer = [&](int32_t score, uint32_t idx) {
+    if (kib)
+      best32 = std::max(best32, (static_cast<uint32_t>(score) << kib) + (0x80000000u + kmask - idx));
+    else
+      best_key = std::max(best_key, final_key(score, idx));
+  };
   const int64_t last = L1 - L2;
   for (int64_t o = 0; o < need; ++o) {
-    if (o < last || (o == last && (sem == Semantics::Spec || L2 == L1)))
-      best_key = std::max(best_key, final_key(tot[o], static_cast<uint32_t>(2 * o)));
-    if (o < last && L2 >= 2) best_key = std::max(best_key, final_key(maxD[o] + tot[o] - Dc[o], static_cast<uint32_t>(2 * o + 1)));
+    if (o < last || (o == last && (sem == Semantics::Spec || L2 == L1))) offer(tot[o], static_cast<uint32_t>(2 * o));
+    if (o < last && L2 >= 2) offer(maxD[o] + tot[o] - Dc[o], static_cast<uint32_t>(2 * o + 1));
   }
+  if (kib && best32)
+    best_key = final_key(static_cast<int32_t>(best32 >> kib) - (1 << (31 - kib)), kmask - (best32 & kmask));
   if (!best_key) return Result{kNoCandidateScore, 0, 0};
   const int32_t score = static_cast<int32_t>(static_cast<uint32_t>(best_key >> 32) ^ 0x80000000u);
   const uint32_t idx = 0xffffffffu - static_cast<uint32_t>(best_key);
@@ -1357,6 +1368,27 @@ void test_tile16_replay_bounds() {
   }
 }
 
+void test_tile16_key32_replay() {
+  using namespace xv;
+  // tile16's 32-bit selection keys against its 64-bit ones (the latter pinned to brute force above): W1 = 127,
+  // L1 = 2600 (13 index bits): even pieces of Seq1 score 127 * L2, inside 2^18 up to L2 = 2064
+  const ScoreTable tt = ScoreTable::build(Weights{{127, 0, 0, 0}});
+  CHECK(profile16_fits(tt));
+  CHECK(bounds::tile16_key32_bits(2600, tt.max_abs(), 2064) == 13 && bounds::tile16_key32_bits(2600, tt.max_abs(), 2065) == 0);
+  for (int64_t hi : {2064, 2065}) {
+    const Fixture f = azaz(2600, hi - 3, hi, 11);
+    Profile16 prof;
+    CHECK(build_profile16(tt, f.s1.data(), 2600, 512, prof));
+    int differ = 0;
+    for (int64_t r = 0; r < f.batch.size(); ++r) {
+      const Result a = tile16_record(tt, f.s1, prof.entries, f.batch.record(r), f.batch.length(r), 512, Semantics::Reference, 13);
+      const Result b = tile16_record(tt, f.s1, prof.entries, f.batch.record(r), f.batch.length(r), 512, Semantics::Reference, 0);
+      differ += same(a, b) ? 0 : 1;
+    }
+    CHECK(hi == 2064 ? differ == 0 : differ > 0);  // one past the bound the 32-bit keys wrap
+  }
+}
+
 int main() {
   const std::vector<std::pair<const char*, std::function<void()>>> tests = {
       {"score_table", test_score_table}, {"parser", test_parser},     {"stream_reader", test_stream_reader},
@@ -1367,7 +1399,8 @@ int main() {
       {"write_runs", test_write_runs},   {"pack33", test_pack33},
       {"kfd_topology", test_kfd_topology}, {"kfd_topology_8gpu", test_kfd_topology_8gpu},
       {"cutter_count_ahead", test_cutter_count_ahead}, {"swipe_replay_bounds", test_swipe_replay_bounds},
-      {"short_replay_bounds", test_short_replay_bounds}, {"tile16_replay_bounds", test_tile16_replay_bounds}};
+      {"short_replay_bounds", test_short_replay_bounds}, {"tile16_replay_bounds", test_tile16_replay_bounds},
+      {"tile16_key32_replay", test_tile16_key32_replay}};
   for (const auto& t : tests) {
     const int before = g_failed;
     t.second();

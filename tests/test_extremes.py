@@ -22,6 +22,9 @@ BOUNDS = [
     ("short_key32", 130, 67, 85, (98689, 0, 0, 98689), (98690, 0, 0, 98690), "key_shift", 7, 0),
     ("tile16", 600, 150, 400, (63, 0, 0, 64), (64, 0, 0, 64), "profile16", True, False),
     ("tiles_key32", 600, 150, 400, (5242, 0, 0, 5242), (5243, 0, 0, 5243), "key_shift", 9, 0),
+    # tile16's 32-bit selection keys: L1 2600 needs 13 index bits, so max|T| * L2 < 2^18 (127 * 2064 = 262128)
+    ("tile16_key32", 2600, 2000, 2064, (127, 0, 0, 0), (127, 0, 0, 0), "tile16_key_bits", 13, 13),
+    ("tile16_key32_l2", 2600, 2000, 2065, (127, 0, 0, 0), (127, 0, 0, 0), "tile16_key_bits", 0, 0),
 ]
 
 
@@ -62,3 +65,11 @@ def test_cpu_engine_long_extremes():
     # the tile16 shape: records of 150..400 letters under Seq1 = "AZ" * 300, W1 + W4 = 127
     prob = make_extreme(600, 150, 400, (63, 0, 0, 64), seed=3)
     assert np.array_equal(as_triples(search_cpu(prob)), as_triples(brute_force_native(prob)))
+
+
+def test_tile16_key32_fixture_reaches_the_bound():
+    # the GPU tier's tile16_key32_at input: an even-offset piece of Seq1 of 2064 letters scores 127 * 2064,
+    # 16 below the 2^18 the 32-bit keys hold at L1 = 2600 (and 2065 letters pass it)
+    prob = make_extreme(2600, 2000, 2064, (127, 0, 0, 0), copies=1, seed=2600)
+    best = max(int(t[0]) for t in as_triples(search_cpu(prob)))
+    assert best == 127 * 2064 and best < 2 ** 18 <= 127 * 2065

@@ -821,7 +821,7 @@ def test_tile16_window_wide(engine, L1):
         assert engine.stats()["kernels"] == ["tile16"], engine.stats()
 
 
-@pytest.mark.parametrize("w,forms", [((63, 0, 0, 64), ["tile16"]), ((64, 0, 0, 64), ["tiles_key32"])])
+@pytest.mark.parametrize("w,forms", [((63, 0, 0, 64), ["tile16", "tile16_key32"]), ((64, 0, 0, 64), ["tiles_key32"])])
 def test_extreme_values_tile16_window_wide(engine, w, forms):
     # the int8 profile bound on the widened-window image: |D| at its extreme, at the bound and one past
     from mpi_openmp_cuda_amd.utils.synthetic import make_extreme
@@ -1049,7 +1049,10 @@ EXTREMES = [
     ("short_pk_past", 130, 67, 85, (193, 0, 0, 193), ["short"], ["short_key32"]),
     ("short_key32_at", 130, 67, 85, (98689, 0, 0, 98689), ["short"], ["short_key32"]),
     ("short_key32_past", 130, 67, 85, (98690, 0, 0, 98690), ["short"], ["short_key64"]),
-    ("tile16_at", 600, 150, 400, (63, 0, 0, 64), ["tile16"], ["tile16"]),
+    ("tile16_at", 600, 150, 400, (63, 0, 0, 64), ["tile16"], ["tile16", "tile16_key32"]),
+    # tile16's 32-bit selection keys: 127 * 2064 < 2^18 (L1 2600: 13 index bits), 127 * 2065 is not
+    ("tile16_key32_at", 2600, 2000, 2064, (127, 0, 0, 0), ["tile16"], ["tile16", "tile16_key32"]),
+    ("tile16_key32_past", 2600, 2000, 2065, (127, 0, 0, 0), ["tile16"], ["tile16"]),
     ("tile16_past", 600, 150, 400, (64, 0, 0, 64), ["tiles"], ["tiles_key32"]),
     ("tiles_key32_at", 600, 150, 400, (5242, 0, 0, 5242), ["tiles"], ["tiles_key32"]),
     ("tiles_key32_past", 600, 150, 400, (5243, 0, 0, 5243), ["tiles"], ["tiles_key64"]),
