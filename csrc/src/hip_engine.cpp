@@ -1018,11 +1018,7 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
     if (!starts.empty()) {
       dev::Plan plan = device_plan(s.d_plan, starts.size(), lrecs != nullptr, n_long, tp);
       dev::BatchView bv{dcodes, doffs, cn};
-      dev::ProblemView tpv = pv;
-      if (!tp.tile16) {
-        tpv.prof16 = nullptr;
-        tpv.mfma_sweep = 0;
-      }
+      const dev::ProblemView tpv = tile_view(cp.max_l2, tp);  // the plan's image: whole / windowed, widened
       dev::launch_tiles(tpv, bv, plan, s.d_out, static_cast<int>(fmt), s_compute_);
       stats_.kernels |= tp.tile16 ? 8 : 4;
       stats_.forms |= dev::tile_form(tpv);
