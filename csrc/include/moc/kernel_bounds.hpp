@@ -37,19 +37,18 @@ constexpr int swipe_kbits(int l2w) {
   while ((1 << b) <= 4 * l2w) ++b;
   return b;
 }
-// The anchor diagonal reads T from an int8 LUT.
-constexpr int32_t kSwipeMaxWeight = 127;
-
 enum class SwipeKeys { None, KBits, RK };
 // Key form of the swipe kernel for a batch:
 //   KBits: E = D * 2^kb + (2^kb - 1 - k) in int16. Its largest value is dmax * 2^kb + 2^kb - 2, so
 //          dmax * 2^kb + 2^kb < 32767 keeps every key (and B2 = max E) exact.
 //   RK:    E = D in int16 (|D| <= dmax < 32767); k is re-found on the winning diagonal afterwards.
 //          Records of 33..64 letters (l2w 16) always take it: no room for 7 k bits.
-//   None:  W > 127 (the int8 anchor LUT) or dmax >= 32767.
+//   None:  dmax >= 32767.
+// The selection keys carry score + 2^15 in 16 bits: |score| <= W L2 = dmax / 2 < 2^14 under either form; the
+// anchor diagonal is summed in int32 from an int32 table (swipe_build_tables), so W itself is not bounded.
 inline SwipeKeys swipe_keys(int32_t max_abs_weight, int64_t max_l2) {
   const int64_t dmax = diff_bound(max_abs_weight, max_l2);
-  if (dmax >= 32767 || max_abs_weight > kSwipeMaxWeight) return SwipeKeys::None;
+  if (dmax >= 32767) return SwipeKeys::None;
   const int l2w = swipe_record_words(max_l2);
   const int kb = swipe_kbits(l2w);
   return (l2w == 16 || (dmax << kb) + (int64_t{1} << kb) >= 32767) ? SwipeKeys::RK : SwipeKeys::KBits;

@@ -1,12 +1,12 @@
-// Inter-record SIMD kernel for tiny problems (input6-shaped: |Seq1| <= ~100, |Seq2| <= 32, small W).
+// Inter-record SIMD kernel for short records (input6-shaped: |Seq1| <= 200, |Seq2| <= 64, <= 64 offsets).
 //
 // One LANE = one whole record (vs. one lane per offset in short_kernels.hip): every lane keeps all its
 // offsets' running diagonal sums in registers as packed int16 pairs, so
 //   * no cross-lane traffic at all in the hot loop (no DPP, no segmented reductions per record),
 //   * two cells per VALU op (v_pk_add_u16 / v_pk_max_i16),
-//   * the profile row segment a lane needs at step i is read with NOFF/8 aligned ds_read_b128: the block
-//     keeps 8 copies of the int16 profile, copy s shifted left by s columns, so step i reads copy (i mod 8)
-//     at column i - (i mod 8) (a multiple of 8 -> 16-byte aligned).
+//   * the profile row segment a lane needs at step i is read with NOFF/4 aligned ds_read_b64: the block
+//     keeps kCopies = 4 copies of the int16 profile, copy s shifted left by s columns, so step i reads copy
+//     (i mod 4) at column i - (i mod 4) (a multiple of 4 -> 8-byte aligned).
 // The profile holds the diagonal DIFFERENCES Dt[c][j] = S[c][j] - S[c][j+1] (S = T[c][Seq1[j]], 0 past
 // Seq1 and in the padding row 0), pre-scaled and pre-biased: Pf[c][j] = Dt[c][j] * 2^KB - 1. A lane's
 // running sum for offset o after step i is then already the selection key of the mutant k = i + 1,
@@ -14,23 +14,24 @@
 // (larger D first, then smaller k), so per step and per pair of offsets (2m, 2m+1):
 //     E2[m] += (Pf[c][i+2m], Pf[c][i+2m+1])            v_pk_add_u16
 //     B2[m]  = max(B2[m], E2[m])                       v_pk_max_i16
-// i.e. 1 VALU op per cell (round 3: 2 more per pair for the shift and the step index). Tot_o is not
-// summed per cell: each lane sums the anchor diagonal Tot_NOFF = sum_i T[c_i][Seq1[NOFF + i]] (an int8
-// LUT + Seq1 staged in LDS; 0 past Seq1, consistent with the profile) and recovers
-// Tot_o = Tot_{o+1} + D_o(L2) by a suffix pass over its offsets in the epilogue, with
-// D_o(L2) = (E_o(steps-1) - (KMASK - steps)) >> KB (steps past a record's end add the padding row, Dt 0).
-// A wave runs steps = its longest record's length. Records stream through the same persistent, LDS-tiled
-// block loop as the short kernel (zero-copy from pinned host memory when the batch lives there).
+// i.e. 1 VALU op per cell. Tot_o is not summed per cell: each lane sums the anchor diagonal
+// Tot_NOFF = sum_i T[c_i][Seq1[NOFF + i]] from an int32 table at[i][c] in LDS (0 past Seq1, consistent with
+// the profile) and recovers Tot_o = Tot_{o+1} + D_o(L2) by a suffix pass over its offsets in the epilogue,
+// with D_o(L2) = (E_o(steps-1) - (KMASK - steps)) >> KB (steps past a record's end add the padding row, Dt 0).
+// A wave runs steps = its longest record's length.
 // Exactness: int16 arithmetic is exact because the host only selects this kernel when
 // 2*max|W|*max|Seq2|*2^KB + 2^KB < 32767 (no key can wrap) — moc/kernel_bounds.hpp swipe_keys, replayed at
 // and past the bound by csrc/tests/test_core.cpp test_swipe_replay_bounds. When the weights leave
 // no room for k in the keys but the sums still fit int16 (input1: W1 = 100, |Seq2| <= 41), the RK form
 // runs: Pf = Dt, the running sums are D_o(k) themselves, B2 keeps max_k D_o(k), and after the selection
 // each lane whose winner is a mutant re-walks that one diagonal for the first k reaching the best D.
+// Two kernels share the lane search (swipe_lane): swipe_search_kernel streams block tiles through LDS
+// (zero-copy from pinned host memory: the host streams), swipe_direct_kernel lets each wave take 64 records
+// straight from HBM (device-resident batches).
 //
-// This header holds the kernel template; swipe_group.inc instantiates it, one code object per letter form
-// (bytes: device-resident batches, P33: host streams) and offsets per lane, and swipe_kernels.hip holds the
-// host-side configuration, dispatch and launch.
+// This header holds the kernel templates; swipe_group.inc instantiates them, one code object per letter
+// form (bytes, P33) and offsets per lane, and swipe_kernels.hip holds the host-side configuration,
+// dispatch and launch.
 #pragma once
 
 #include <hip/hip_runtime.h>

@@ -33,6 +33,8 @@ SHAPES = {
     # between the reference shapes: records too long for the swipe kernel (> 64 letters) whose offset range
     # still fits a wave (<= 64 lanes): the lane-per-offset short kernel's regime
     "mid": Shape((10, 2, 3, 4), 130, 67, 85),
+    # input6's lengths under a heavy weight (W1 = 300): no room for k in the int16 keys, the RK swipe form
+    "heavy6": Shape((300, 3, 2, 10), 26, 6, 11),
 }
 
 

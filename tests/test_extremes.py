@@ -16,8 +16,9 @@ from mpi_openmp_cuda_amd.utils.synthetic import make_extreme
 BOUNDS = [
     ("swipe_kbits_w4", 40, 6, 16, (31, 0, 0, 31), (32, 0, 0, 32), "swipe", "swipe_kbits", "swipe_rk"),
     ("swipe_kbits_w8", 60, 20, 32, (7, 0, 0, 7), (8, 0, 0, 8), "swipe", "swipe_kbits", "swipe_rk"),
-    ("swipe_rk_w8", 60, 20, 32, (127, 0, 0, 127), (128, 0, 0, 128), "swipe", "swipe_rk", None),
-    ("swipe_rk_w16", 70, 40, 64, (127, 0, 0, 127), (128, 0, 0, 128), "swipe", "swipe_rk", None),
+    ("swipe_rk_w4", 40, 6, 16, (1023, 0, 0, 1023), (1024, 0, 0, 1024), "swipe", "swipe_rk", None),
+    ("swipe_rk_w8", 60, 20, 32, (511, 0, 0, 511), (512, 0, 0, 512), "swipe", "swipe_rk", None),
+    ("swipe_rk_w16", 70, 40, 64, (255, 0, 0, 255), (256, 0, 0, 256), "swipe", "swipe_rk", None),
     ("short_pk", 130, 67, 85, (192, 0, 0, 192), (193, 0, 0, 193), "short_pk", True, False),
     ("short_key32", 130, 67, 85, (98689, 0, 0, 98689), (98690, 0, 0, 98690), "key_shift", 7, 0),
     ("tile16", 600, 150, 400, (63, 0, 0, 64), (64, 0, 0, 64), "profile16", True, False),

@@ -301,7 +301,12 @@ def test_kernel_selection(engine):
     engine.set_problem(p1.weights, p1.seq1)
     engine.solve(p1.codes, p1.offsets)
     assert engine.stats()["kernels"] == ["swipe"]
-    engine.set_problem([300, 2, 3, 4], p1.seq1)  # |T| 300 > 127: the int8 anchor LUT -> lane/offset kernel
+    engine.set_problem([300, 2, 3, 4], p1.seq1)  # W1 300, L2 <= 41: 2 W L2 < 2^15 still -> RK swipe
+    got = engine.solve(p1.codes, p1.offsets)
+    assert engine.stats()["kernels"] == ["swipe"]
+    assert np.array_equal(as_triples(got), as_triples(search_cpu(Problem([300, 2, 3, 4], p1.seq1, p1.codes,
+                                                                          p1.offsets))))
+    engine.set_problem([500, 2, 3, 4], p1.seq1)  # 2 * 500 * 41 >= 2^15: the int16 sums would wrap -> lane/offset
     engine.solve(p1.codes, p1.offsets)
     assert engine.stats()["kernels"] == ["short"]
     p4 = make_synthetic("input4", 50, seed=1)  # long records: packed-int16 profile kernel
@@ -1043,8 +1048,10 @@ EXTREMES = [
     ("swipe_kbits_past", 40, 6, 16, (32, 0, 0, 32), ["swipe"], ["swipe_rk"]),
     ("swipe_kbits_w8_at", 60, 20, 32, (7, 0, 0, 7), ["swipe"], ["swipe_kbits"]),
     ("swipe_kbits_w8_past", 60, 20, 32, (8, 0, 0, 8), ["swipe"], ["swipe_rk"]),
-    ("swipe_rk_at", 70, 40, 64, (127, 0, 0, 127), ["swipe"], ["swipe_rk"]),
-    ("swipe_rk_past", 70, 40, 64, (128, 0, 0, 128), ["short"], ["short_pk"]),
+    ("swipe_rk_at", 70, 40, 64, (255, 0, 0, 255), ["swipe"], ["swipe_rk"]),
+    ("swipe_rk_past", 70, 40, 64, (256, 0, 0, 256), ["short"], ["short_key32"]),
+    ("swipe_rk_w4_at", 40, 6, 16, (1023, 0, 0, 1023), ["swipe"], ["swipe_rk"]),
+    ("swipe_rk_w4_past", 40, 6, 16, (1024, 0, 0, 1024), ["short"], ["short_key32"]),
     ("short_pk_at", 130, 67, 85, (192, 0, 0, 192), ["short"], ["short_pk"]),
     ("short_pk_past", 130, 67, 85, (193, 0, 0, 193), ["short"], ["short_key32"]),
     ("short_key32_at", 130, 67, 85, (98689, 0, 0, 98689), ["short"], ["short_key32"]),
