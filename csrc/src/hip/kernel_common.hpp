@@ -111,12 +111,12 @@ __device__ __forceinline__ int wave_max_i32(int v) {
   return v;
 }
 
-// Wave maximum of a value in [0, 128), wave-uniform (an SGPR): seven ballots of a binary search, so branches
+// Wave maximum of a value in [0, 256), wave-uniform (an SGPR): eight ballots of a binary search, so branches
 // on it are scalar and no lane data moves through LDS (wave_max_i32's shuffles are ds_bpermute operations).
 __device__ __forceinline__ int wave_max_small(int v) {
   int m = 0;
 #pragma unroll
-  for (int b = 64; b >= 1; b >>= 1)
+  for (int b = 128; b >= 1; b >>= 1)
     if (__builtin_amdgcn_ballot_w64(v >= m + b) != 0) m += b;
   return __builtin_amdgcn_readfirstlane(m);
 }

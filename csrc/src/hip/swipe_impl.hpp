@@ -72,11 +72,12 @@ constexpr int swipe_row(int noff, int l2w) { return (4 * l2w + noff + 8 + 7) & ~
 constexpr int swipe_stride(int noff, int l2w) { return 2 * swipe_row(noff, l2w) + 8; }  // bytes between rows
 constexpr int swipe_copy_bytes(int noff, int l2w) { return kAlphabet * swipe_stride(noff, l2w); }
 constexpr int swipe_prof_bytes(int noff, int l2w) { return kCopies * swipe_copy_bytes(noff, l2w); }
-constexpr int kAnchorBytes = 64 * 32 * 4;  // anchor table: int32 [64 steps][32 letters]
+// anchor table: int32 [4 * l2w steps][32 letters]
+constexpr int swipe_anchor_bytes(int l2w) { return 4 * l2w * 32 * 4; }
 
 struct SwipeLayout {
   int prof_bytes = 0;   // 8 shifted copies of the Dt profile (swipe_prof_bytes)
-  int s_off = 0;        // anchor table: at[i][c] = T[c][Seq1[NOFF + i]] (0 past Seq1), int32, kAnchorBytes
+  int s_off = 0;        // anchor table: at[i][c] = T[c][Seq1[NOFF + i]] (0 past Seq1), int32, swipe_anchor_bytes
   int loff_off = 0, codes_off = 0, res_off = 0, raw_off = 0, total = 0;  // raw: P33 bytes as loaded
 };
 
@@ -92,7 +93,7 @@ inline SwipeLayout swipe_layout(int L1, int noff, int l2w, int tile_records, int
   SwipeLayout l;
   l.prof_bytes = swipe_prof_bytes(noff, l2w);
   l.s_off = l.prof_bytes;
-  l.loff_off = l.s_off + kAnchorBytes;
+  l.loff_off = l.s_off + swipe_anchor_bytes(l2w);
   l.codes_off = l.loff_off + al16((tile_records + 1) * 4 + 64);  // + misc: 16 ints
   l.res_off = l.codes_off + al16(codes_cap);
   l.raw_off = l.res_off + al16(tile_records * fb);
@@ -130,7 +131,7 @@ __device__ __forceinline__ void swipe_build_tables(unsigned char* smem, const Pr
         static_cast<short>(RK ? sj - sn : (sj - sn) * (1 << KB) - 1);  // Pf = Dt * 2^KB - 1 (header)
   }
   int* at = reinterpret_cast<int*>(smem + swipe_prof_bytes(NOFF, L2W));
-  for (int e = tid; e < kAnchorBytes / 4; e += nthreads) {
+  for (int e = tid; e < swipe_anchor_bytes(L2W) / 4; e += nthreads) {
     const int i = e >> 5, c = e & 31, j = NOFF + i;
     at[e] = c >= 1 && c < kAlphabet && j < L1 ? pv.lut[c * kLutStride + pv.seq1[j]] : 0;
   }
@@ -164,7 +165,7 @@ __device__ __forceinline__ Result swipe_lane(const unsigned char* smem, const ui
   constexpr int KMASK = (1 << KB) - 1;
   constexpr int NP = NOFF / 2;  // packed accumulators
   constexpr int stride = swipe_stride(NOFF, L2W), cb = swipe_copy_bytes(NOFF, L2W);
-  const int steps = wave_max_small(on ? L2 : 0);  // L2 <= 4 * L2W <= 64 here
+  const int steps = wave_max_small(on ? L2 : 0);  // L2 <= 4 * L2W <= 128 here (wave_max_small: < 256)
   const int* at = reinterpret_cast<const int*>(smem + swipe_prof_bytes(NOFF, L2W));
 
   uint32_t E2[NP], B2[NP];
@@ -526,7 +527,7 @@ constexpr int direct_wave_bytes(int l2w) { return 8 * (p33_tile_fields(l2w) + p3
 inline SwipeLayout direct_layout(int L1, int noff, int l2w, int lf) {
   SwipeLayout l = swipe_layout(L1, noff, l2w, 0, 0, 0, 0);
   if (lf == 2) {
-    l.codes_off = al16(l.s_off + kAnchorBytes);
+    l.codes_off = al16(l.s_off + swipe_anchor_bytes(l2w));
     l.total = l.codes_off + (kBlockD / 64) * direct_wave_bytes(l2w);
   }
   return l;
@@ -758,9 +759,11 @@ bool launch_swipe_noff(const ProblemView& pv, const ShortArgs& b, const SwipeLay
   const bool rk = b.swipe_rk != 0;
 #define MOC_SWIPE_CASE(LW, RKV)                                                                              \
   if (l2w == LW && rk == RKV) {                                                                            \
-    if (b.lane_direct) {                                                                                   \
-      launch_direct_instance(&swipe_direct_kernel<NO, LW, LF, RKV>, pv, b, lay, num_cus, stream);         \
-      return true;                                                                                         \
+    if constexpr (LF == 0 || LW <= 16) { /* P33 records over 64 letters: the block-tiled kernel */        \
+      if (b.lane_direct) {                                                                                 \
+        launch_direct_instance(&swipe_direct_kernel<NO, LW, LF, RKV>, pv, b, lay, num_cus, stream);       \
+        return true;                                                                                       \
+      }                                                                                                    \
     }                                                                                                      \
     hipLaunchKernelGGL((swipe_search_kernel<NO, LW, LF, RKV>), grid, block, lay.total, stream, pv, b, lay); \
     return true;                                                                                           \
@@ -769,7 +772,9 @@ bool launch_swipe_noff(const ProblemView& pv, const ShortArgs& b, const SwipeLay
   MOC_SWIPE_CASE(8, false)
   MOC_SWIPE_CASE(4, true)
   MOC_SWIPE_CASE(8, true)
-  MOC_SWIPE_CASE(16, true)  // records of 33..64 letters run the RK form only (configure_swipe)
+  MOC_SWIPE_CASE(16, true)  // records of 33..128 letters run the RK form only (configure_swipe)
+  MOC_SWIPE_CASE(24, true)
+  MOC_SWIPE_CASE(32, true)
 #undef MOC_SWIPE_CASE
   return false;
 }

@@ -13,13 +13,13 @@ struct SwipeChoice {
 };
 
 // Offsets per lane (NOFF), record words (L2W) and key form for a batch, or noff 0 when the kernel cannot
-// take it: at most 64 offsets and 64 letters per record, Seq1's profile within the LDS budget, and an
+// take it: at most 64 offsets and 128 letters per record, the profile within the LDS budget, and an
 // int16-exact key form (moc/kernel_bounds.hpp swipe_keys: the keys carry k when 2^KB * |D| leaves room, as
 // on input6; otherwise, input1's W1 = 100, the RK form re-finds k after the selection).
 SwipeChoice swipe_choice(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs_weight) {
   SwipeChoice c;
   const int64_t need = lanes_needed(L1, std::min(min_l2, L1));
-  if (need > 64 || max_l2 > 64 || L1 > 200) return c;
+  if (need > 64 || max_l2 > bounds::kSwipeMaxL2) return c;
   const bounds::SwipeKeys keys = bounds::swipe_keys(max_abs_weight, max_l2);
   if (keys == bounds::SwipeKeys::None) return c;
   c.rk = keys == bounds::SwipeKeys::RK;
@@ -98,7 +98,7 @@ void launch_swipe(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStr
   const int fb = result_bytes(static_cast<ResultFormat>(a.fmt));
   if (a.lane_direct) {  // device-resident batches: the wave-autonomous kernel, LDS tables (+ P33 wave slices)
     if (a.off_shift > 6 || (a.off_shift && !(a.lengths3 || a.lengths4 || a.lengths6 || a.lengths8)) ||
-        (!a.packed33 && a.off_shift))
+        (!a.packed33 && a.off_shift) || (a.packed33 && a.rpw > 16))
       throw Error("launch_swipe: lane-direct batches are byte letters with dense offsets, or P33 letters with "
                   "64-record sparse offsets and lengths");
     const int lf = letter_form(a);

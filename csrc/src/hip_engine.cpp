@@ -809,7 +809,10 @@ void HipEngine::solve_wire_impl(const WireBatch& batch, void* out, ResultFormat 
   if ((opt_.allow_direct || b.device) && kernel_ok && direct_pointers(b, out, fb, a)) {
     // device-resident: the wave-autonomous swipe kernel (byte letters with dense offsets, or P33 letters with
     // dense or 64-record sparse offsets)
-    a.lane_direct = swipe && b.device && (b.packed33 || !b.off_shift) && lane_direct_enabled() ? 1 : 0;
+    a.lane_direct =
+        swipe && b.device && (b.packed33 || !b.off_shift) && (!b.packed33 || a.rpw <= 16) && lane_direct_enabled()
+            ? 1
+            : 0;
     const dev::ProblemView pv = problem_view(ls.mx);
     const bool graph = prepare_direct(pv, a, swipe);  // capture / instantiation stays outside the timed span
     MOC_HIP_CHECK(hipEventRecord(ev_a_, s_compute_));

@@ -1266,7 +1266,8 @@ void test_swipe_replay_bounds() {
   struct Case {
     int64_t L1, lo, hi;
   };
-  for (const Case cs : {Case{40, 6, 16}, Case{60, 20, 32}, Case{70, 40, 64}, Case{100, 40, 64}}) {
+  for (const Case cs : {Case{40, 6, 16}, Case{60, 20, 32}, Case{70, 40, 64}, Case{100, 40, 64}, Case{130, 67, 96},
+                        Case{190, 127, 128}}) {
     const Fixture f = azaz(cs.L1, cs.lo, cs.hi, static_cast<uint32_t>(cs.L1));
     const int l2w = bounds::swipe_record_words(f.max_l2), kb = bounds::swipe_kbits(l2w);
     const int64_t need = cs.L1 - f.min_l2 + 1;
@@ -1280,7 +1281,7 @@ void test_swipe_replay_bounds() {
       if (k == bounds::SwipeKeys::RK) w_rk = w;
     }
     CHECK(2 * w_rk * f.max_l2 < 32767 && 2 * (w_rk + 1) * f.max_l2 >= 32767);  // int16 sums end the RK form
-    if (l2w == 16) CHECK(w_kbits == 0);      // 33..64-letter records: RK only
+    if (l2w >= 16) CHECK(w_kbits == 0);      // 33..128-letter records: RK only
     if (l2w == 4) CHECK(w_kbits == 31);      // 2*31*16*32 + 32 < 32767 <= 2*32*16*32 + 32
     if (l2w == 8) CHECK(w_kbits == 7);       // 2*7*32*64 + 64 < 32767 <= 2*8*32*64 + 64
     for (Semantics sem : {Semantics::Reference, Semantics::Spec}) {

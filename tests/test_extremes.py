@@ -19,8 +19,10 @@ BOUNDS = [
     ("swipe_rk_w4", 40, 6, 16, (1023, 0, 0, 1023), (1024, 0, 0, 1024), "swipe", "swipe_rk", None),
     ("swipe_rk_w8", 60, 20, 32, (511, 0, 0, 511), (512, 0, 0, 512), "swipe", "swipe_rk", None),
     ("swipe_rk_w16", 70, 40, 64, (255, 0, 0, 255), (256, 0, 0, 256), "swipe", "swipe_rk", None),
-    ("short_pk", 130, 67, 85, (192, 0, 0, 192), (193, 0, 0, 193), "short_pk", True, False),
-    ("short_key32", 130, 67, 85, (98689, 0, 0, 98689), (98690, 0, 0, 98690), "key_shift", 7, 0),
+    ("swipe_rk_w24", 130, 67, 96, (170, 0, 0, 170), (171, 0, 0, 171), "swipe", "swipe_rk", None),
+    ("swipe_rk_w32", 190, 127, 128, (127, 0, 0, 127), (128, 0, 0, 128), "swipe", "swipe_rk", None),
+    ("short_pk", 150, 130, 150, (109, 0, 0, 109), (110, 0, 0, 110), "short_pk", True, False),
+    ("short_key32", 200, 150, 190, (22075, 0, 0, 22075), (22076, 0, 0, 22076), "key_shift", 8, 0),
     ("tile16", 600, 150, 400, (63, 0, 0, 64), (64, 0, 0, 64), "profile16", True, False),
     ("tiles_key32", 600, 150, 400, (5242, 0, 0, 5242), (5243, 0, 0, 5243), "key_shift", 9, 0),
     # tile16's 32-bit selection keys: L1 2600 needs 13 index bits, so max|T| * L2 < 2^18 (127 * 2064 = 262128)
@@ -52,7 +54,7 @@ def test_extreme_fixture_reaches_the_bound():
         pytest.fail("no even-offset piece of Seq1 in the fixture")
 
 
-@pytest.mark.parametrize("case", [c for c in BOUNDS if c[1] <= 130], ids=[c[0] for c in BOUNDS if c[1] <= 130])
+@pytest.mark.parametrize("case", [c for c in BOUNDS if c[1] <= 200], ids=[c[0] for c in BOUNDS if c[1] <= 200])
 @pytest.mark.parametrize("sem", [Semantics.REFERENCE, Semantics.SPEC])
 def test_cpu_engine_at_bounds(case, sem):
     # the oracle the GPU tier compares with: the CPU engine equals brute force on every adversarial input

@@ -203,12 +203,15 @@ def test_group_coded_letters(shape, n, pinned):
 @pytest.mark.parametrize("L1,lo,hi,w", [(26, 6, 11, (4, 3, 2, 10)), (12, 1, 14, (3, 1, 1, 2)),
                                         (40, 20, 32, (5, 2, 3, 4)), (60, 10, 16, (2, 2, 1, 3)),
                                         (9, 9, 9, (7, 1, 2, 3)), (51, 32, 41, (100, 2, 3, 4)),
-                                        (70, 40, 64, (3, 1, 2, 1)), (30, 5, 12, (120, 1, 1, 1))])
+                                        (70, 40, 64, (3, 1, 2, 1)), (30, 5, 12, (120, 1, 1, 1)),
+                                        (130, 67, 85, (10, 2, 3, 4)), (190, 127, 128, (3, 1, 1, 2)),
+                                        (40, 30, 40, (300, 2, 3, 4))])
 @pytest.mark.parametrize("letters", ["p33", "p5"])
 def test_swipe_wire_slices(L1, lo, hi, w, letters):
     # the headline's wire path (parallel/wire.py: narrow lengths, R2/R4 results, zero-copy) across swipe
-    # instantiations (NOFF 8..64, record widths <= 16 / <= 32 / <= 64, keys with k bits and the RK form that
-    # re-walks k) with P33 letters; 5-bit letters take the staged pipeline to the same kernel
+    # instantiations (NOFF 8..64, record widths <= 16 / 32 / 64 / 96 / 128, keys with k bits and the RK form
+    # that re-walks k, weights past 127) with P33 letters; 5-bit letters take the staged pipeline to the same
+    # kernel
     from mpi_openmp_cuda_amd._lib import Pinned
     from mpi_openmp_cuda_amd.parallel.wire import WireSlice
 
@@ -230,9 +233,9 @@ def test_swipe_wire_slices(L1, lo, hi, w, letters):
     eng.close()
 
 
-@pytest.mark.parametrize("L1,lo,hi", [(120, 70, 75), (130, 80, 85)])
+@pytest.mark.parametrize("L1,lo,hi", [(200, 150, 155), (210, 160, 165)])
 def test_short_kernel_base6_lengths(L1, lo, hi):
-    # byte letters + base-6 lengths through the lane-per-offset short kernel (records longer than 64 letters
+    # byte letters + base-6 lengths through the lane-per-offset short kernel (records longer than 128 letters
     # leave the swipe kernel; at most 64 lanes per record keep them on the short one)
     from mpi_openmp_cuda_amd._lib import Pinned
     from mpi_openmp_cuda_amd.parallel.wire import WireSlice
@@ -1012,7 +1015,7 @@ def test_final_cli_gpu_isolate(np_):
     assert "runtime isolated" not in r.stderr.decode()
 
 
-@pytest.mark.parametrize("shape,n", [("input6", 200_003), ("input1", 30_001), ("input6", 777)])
+@pytest.mark.parametrize("shape,n", [("input6", 200_003), ("input1", 30_001), ("input6", 777), ("mid", 20_001)])
 def test_wire_device_resident(engine, shape, n):
     # a batch in the wire formats held in device memory (the rccl transport's form): P33 letters, narrow
     # lengths, the narrowest results; the swipe kernel reads it in place
@@ -1052,10 +1055,15 @@ EXTREMES = [
     ("swipe_rk_past", 70, 40, 64, (256, 0, 0, 256), ["short"], ["short_key32"]),
     ("swipe_rk_w4_at", 40, 6, 16, (1023, 0, 0, 1023), ["swipe"], ["swipe_rk"]),
     ("swipe_rk_w4_past", 40, 6, 16, (1024, 0, 0, 1024), ["short"], ["short_key32"]),
-    ("short_pk_at", 130, 67, 85, (192, 0, 0, 192), ["short"], ["short_pk"]),
-    ("short_pk_past", 130, 67, 85, (193, 0, 0, 193), ["short"], ["short_key32"]),
-    ("short_key32_at", 130, 67, 85, (98689, 0, 0, 98689), ["short"], ["short_key32"]),
-    ("short_key32_past", 130, 67, 85, (98690, 0, 0, 98690), ["short"], ["short_key64"]),
+    ("swipe_rk_w24_at", 130, 67, 96, (170, 0, 0, 170), ["swipe"], ["swipe_rk"]),
+    ("swipe_rk_w24_past", 130, 67, 96, (171, 0, 0, 171), ["short"], ["short_key32"]),
+    ("swipe_rk_w32_at", 190, 127, 128, (127, 0, 0, 127), ["swipe"], ["swipe_rk"]),
+    ("swipe_rk_w32_past", 190, 127, 128, (128, 0, 0, 128), ["short"], ["short_key32"]),
+    # records over 128 letters with <= 64 offsets: the lane-per-offset short kernel
+    ("short_pk_at", 150, 130, 150, (109, 0, 0, 109), ["short"], ["short_pk"]),
+    ("short_pk_past", 150, 130, 150, (110, 0, 0, 110), ["short"], ["short_key32"]),
+    ("short_key32_at", 200, 150, 190, (22075, 0, 0, 22075), ["short"], ["short_key32"]),
+    ("short_key32_past", 200, 150, 190, (22076, 0, 0, 22076), ["short"], ["short_key64"]),
     ("tile16_at", 600, 150, 400, (63, 0, 0, 64), ["tile16"], ["tile16", "tile16_key32"]),
     # tile16's 32-bit selection keys: 127 * 2064 < 2^18 (L1 2600: 13 index bits), 127 * 2065 is not
     ("tile16_key32_at", 2600, 2000, 2064, (127, 0, 0, 0), ["tile16"], ["tile16", "tile16_key32"]),
