@@ -44,11 +44,12 @@ int moc_pack_lengths(const int64_t* offsets, int64_t n, int bits, int64_t base, 
 int moc_score_table(const int32_t* weights4, int32_t* lut1024, uint8_t* cls1024);
 
 /* ---- exactness bounds of the kernels' narrow-integer forms (moc/kernel_bounds.hpp); no GPU needed ----
- * out5: [0] swipe key form (moc::bounds::kFormSwipeKBits / kFormSwipeRK, 0 = the swipe kernel's integer
+ * out6: [0] swipe key form (moc::bounds::kFormSwipeKBits / kFormSwipeRK, 0 = the swipe kernel's integer
  * bounds refuse the batch), [1] 1 if the short kernel's packed int16 form is exact, [2] the int32 hot-key
  * shift of the short / tile kernels (0 = 64-bit keys), [3] 1 if the tile16 profile holds the table, [4] the
- * index bits of tile16's 32-bit selection keys (0 = 64-bit keys). */
-int moc_kernel_bounds(const int32_t* weights4, int64_t L1, int64_t min_l2, int64_t max_l2, int32_t* out5);
+ * index bits of tile16's 32-bit selection keys (0 = 64-bit keys), [5] 1 if the int16 tile16 profile holds the
+ * table. */
+int moc_kernel_bounds(const int32_t* weights4, int64_t L1, int64_t min_l2, int64_t max_l2, int32_t* out6);
 /* "src=<source hash> defs=<-D flags of the kernel objects>" (empty defs: the product build) */
 const char* moc_build_info(void);
 

@@ -69,6 +69,9 @@ struct ProblemView {
   int32_t prof16_wide = 0;
   // tile16: index bits of the 32-bit selection keys (bounds::tile16_key32_bits; 0 = 64-bit keys)
   int32_t t16_key_bits = 0;
+  // 1: prof16 holds one int16 Dt per entry (weights past the byte pairs, bounds::profile16_i16_exact), staged
+  // into widened images only
+  int32_t prof16_i16 = 0;
 };
 
 // Entries after the tile16 profile's last row: reads of wave-tile lanes past the valid offsets reach
@@ -217,7 +220,8 @@ void launch_tile_keys(const ProblemView& pv, const BatchView& bv, const Plan& pl
 inline int32_t tile_form(const ProblemView& pv) {
   if (pv.prof16)
     return pv.mfma_sweep ? bounds::kFormMfma
-                         : bounds::kFormTile16 | (pv.t16_key_bits ? bounds::kFormTile16Key32 : 0);
+                         : bounds::kFormTile16 | (pv.t16_key_bits ? bounds::kFormTile16Key32 : 0) |
+                               (pv.prof16_i16 ? bounds::kFormTile16I16 : 0);
   return pv.key_shift > 0 ? bounds::kFormTilesKey32 : bounds::kFormTilesKey64;
 }
 void launch_finalize_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, void* out, int fmt,

@@ -216,6 +216,7 @@ class HipEngine {
   int64_t prof16_entries_ = 0;   // entries of the device profile (windowed staging bounds)
   int32_t prof16_lds_bytes_ = 0; // LDS bytes of the profile part of a workgroup's image
   bool prof16_wide_ = false;      // the sweep stages widened int16 pairs (dev::ProblemView::prof16_wide)
+  bool prof16_i16_ = false;       // the profile holds one int16 Dt per entry (dev::ProblemView::prof16_i16)
   bool tile16_ = true;            // MOC_TILE16 (A/B switch of the long-record kernel)
   bool mfma_ = false;             // MOC_MFMA: tile16 plans swept on the matrix cores (tile_mfma_kernels.hip)
   int64_t L1_ = 0;

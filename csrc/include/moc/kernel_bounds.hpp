@@ -84,6 +84,10 @@ inline bool profile16_exact(int32_t dmin, int32_t dmax, int32_t tabs) {
   return dmin >= -128 && dmax <= 127 && tabs <= 127;
 }
 static_assert(kProf16Fold * 128 < 32768, "tile16 int16 partial sums");
+// The int16 profile (one Dt per entry, staged into widened images only): |Dt| <= 511 keeps a 64-step partial
+// sum within int16 (64 * 511 = 32704); T is read from the int32 LUT.
+inline bool profile16_i16_exact(int32_t dmin, int32_t dmax) { return dmin >= -511 && dmax <= 511; }
+static_assert(kProf16Fold * 511 < 32768, "tile16 int16 partial sums, int16 profile");
 
 // tile16's per-lane selection in 32-bit keys: ((score + 2^(31 - IB)) << IB) | (2^IB - 1 - idx), idx = 2o +
 // mutated <= 2 L1 + 1 < 2^IB. Exact when every score fits the 32 - IB score bits: |score| <= max|T| * L2
@@ -107,6 +111,7 @@ enum FormBits : int32_t {
   kFormTilesKey64 = 128,  // LUT tile kernel, int64 keys
   kFormMfma = 256,        // matrix-core sweep over the tile16 profile
   kFormTile16Key32 = 512, // tile16's per-lane selection in 32-bit keys (tile16_key32_bits)
+  kFormTile16I16 = 1024,  // tile16 over the int16 profile (profile16_i16_exact)
 };
 
 }  // namespace bounds

@@ -52,10 +52,15 @@ struct ScoreTable {
 // valid offsets). Returns false (out untouched) when some D does not fit a signed byte.
 struct Profile16 {
   std::vector<uint16_t> entries;
-  int64_t row = 0;  // entries per row (= L1)
+  int64_t row = 0;   // entries per row (= L1)
+  bool i16 = false;  // entries are int16 Dt[c][j] (build_profile16 with allow_i16), not byte pairs
 };
 // True when every Dt and T of the table fit the profile bytes (moc/kernel_bounds.hpp profile16_exact).
 bool profile16_fits(const ScoreTable& t);
-bool build_profile16(const ScoreTable& t, const uint8_t* seq1, int64_t L1, int64_t overhang, Profile16& out);
+// True when every Dt fits the int16 profile (moc/kernel_bounds.hpp profile16_i16_exact).
+bool profile16_i16_fits(const ScoreTable& t);
+// Byte pairs when the table fits them; otherwise, with allow_i16, one int16 Dt per entry when it fits that.
+bool build_profile16(const ScoreTable& t, const uint8_t* seq1, int64_t L1, int64_t overhang, Profile16& out,
+                     bool allow_i16 = false);
 
 }  // namespace moc

@@ -128,16 +128,17 @@ int moc_score_table(const int32_t* weights4, int32_t* lut1024, uint8_t* cls1024)
   });
 }
 
-int moc_kernel_bounds(const int32_t* weights4, int64_t L1, int64_t min_l2, int64_t max_l2, int32_t* out5) {
+int moc_kernel_bounds(const int32_t* weights4, int64_t L1, int64_t min_l2, int64_t max_l2, int32_t* out6) {
   return guard([&] {
     const moc::ScoreTable t = moc::ScoreTable::build(weights_of(weights4));
     const int32_t w = t.max_abs();
     const int64_t searched = std::max<int64_t>(1, std::min(max_l2, L1 + 1));  // longer records are not searched
-    out5[0] = moc::dev::swipe_form(L1, min_l2, max_l2, w);
-    out5[1] = moc::bounds::short_pk_exact(w, searched) ? 1 : 0;
-    out5[2] = moc::bounds::key_shift(w, searched);
-    out5[3] = moc::profile16_fits(t) ? 1 : 0;
-    out5[4] = moc::bounds::tile16_key32_bits(L1, w, searched);
+    out6[0] = moc::dev::swipe_form(L1, min_l2, max_l2, w);
+    out6[1] = moc::bounds::short_pk_exact(w, searched) ? 1 : 0;
+    out6[2] = moc::bounds::key_shift(w, searched);
+    out6[3] = moc::profile16_fits(t) ? 1 : 0;
+    out6[4] = moc::bounds::tile16_key32_bits(L1, w, searched);
+    out6[5] = moc::profile16_i16_fits(t) ? 1 : 0;
   });
 }
 

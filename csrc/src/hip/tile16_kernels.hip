@@ -197,7 +197,18 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
       return (static_cast<uint32_t>(static_cast<int8_t>(e & 0xffu)) & 0xffffu) |
              (static_cast<uint32_t>(static_cast<int8_t>((e >> 8) & 0xffu)) << 16);
     };
-    if ((pv.L1 & 7) == 0) {  // rows 16-byte aligned (W and S are multiples of 16): 8 entries per load
+    if (pv.prof16_i16) {  // int16 Dt per entry: the pair of window entry (c, x) is global (g, g + 1)
+      for (int e = threadIdx.x; e < n_entries; e += blockDim.x) {
+        uint32_t v = 0;
+        if (e < rows_entries) {
+          const int c = e / W, x = e - c * W;
+          const int64_t g = static_cast<int64_t>(c) * pv.L1 + S + x;
+          if (g < pv.prof16_entries) v = pv.prof16[g];
+          if (g + 1 < pv.prof16_entries) v |= static_cast<uint32_t>(pv.prof16[g + 1]) << 16;
+        }
+        ((e & 1) ? odd : even)[e >> 1] = v;
+      }
+    } else if ((pv.L1 & 7) == 0) {  // rows 16-byte aligned (W and S are multiples of 16): 8 entries per load
       const int w8 = W >> 3;
       for (int e = threadIdx.x; e < (kAlphabet - 1) * w8; e += blockDim.x) {
         const int c = e / w8, x = (e - c * w8) << 3;
@@ -263,11 +274,23 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
                           (static_cast<uint32_t>(static_cast<int8_t>(pair2 >> 24)) << 16);
       return make_uint2(lo, hi);
     };
-    for (int t = threadIdx.x; t < n16; t += blockDim.x) {
-      const uint4 v = src[t];
-      const uint2 a = widen(v.x), b = widen(v.y), c = widen(v.z), d = widen(v.w);
-      dst[t] = make_uint4(a.x, b.x, c.x, d.x);
-      dst[n16 + t] = make_uint4(a.y, b.y, c.y, d.y);
+    if (pv.prof16_i16) {
+      // int16 Dt per entry: entry e's pair is (Dt[e], Dt[e+1]) — the even pairs are the loaded dwords, the
+      // odd ones straddle them (and the next load's first value)
+      for (int t = threadIdx.x; t < n16; t += blockDim.x) {
+        const uint4 v = src[t];
+        const uint32_t nx = t + 1 < n16 ? reinterpret_cast<const uint32_t*>(src + t + 1)[0] : 0u;
+        dst[t] = v;
+        dst[n16 + t] = make_uint4(__builtin_amdgcn_alignbit(v.y, v.x, 16), __builtin_amdgcn_alignbit(v.z, v.y, 16),
+                                  __builtin_amdgcn_alignbit(v.w, v.z, 16), __builtin_amdgcn_alignbit(nx, v.w, 16));
+      }
+    } else {
+      for (int t = threadIdx.x; t < n16; t += blockDim.x) {
+        const uint4 v = src[t];
+        const uint2 a = widen(v.x), b = widen(v.y), c = widen(v.z), d = widen(v.w);
+        dst[t] = make_uint4(a.x, b.x, c.x, d.x);
+        dst[n16 + t] = make_uint4(a.y, b.y, c.y, d.y);
+      }
     }
     stage_bytes(s1l, pv.seq1, pv.L1 + 16);  // Seq1 + zero pad (device copy has kSeq1Pad zeros)
   } else {
@@ -403,8 +426,8 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
       // lanes add their step's pair score from LDS while the sweep runs
       const int oA = min(o0 + kSpan, need);
       int anchor = 0;
-      auto anchor_add = [&](int c, int i) {
-        if (c != 0) anchor += lut8[c * kLutStride + s1l[oA - S + i]];
+      auto anchor_add = [&](int c, int i) {  // an int16 profile's weights may pass int8: T from the global LUT
+        if (c != 0) anchor += pv.prof16_i16 ? pv.lut[c * kLutStride + s1l[oA - S + i]] : lut8[c * kLutStride + s1l[oA - S + i]];
       };
       int c = c_first;
       int i0 = 0;
@@ -565,6 +588,7 @@ void launch_tile16_keys(const ProblemView& pv, const BatchView& bv, const Plan& 
                         bool mfma_sweep) {
   const int64_t s1_len = pv.prof16_window > 0 ? pv.prof16_window : pv.L1;
   const bool wide = pv.prof16_wide && !mfma_sweep;
+  if (pv.prof16_i16 && !wide) throw Error("launch_tile16_keys: an int16 profile runs the widened image only");
   if (!pv.prof16 || pv.prof16_bytes <= 0 ||
       tile16_lds_bytes(wide ? 2 * pv.prof16_bytes : pv.prof16_bytes, s1_len) > kProf16MaxLds ||
       (pv.prof16_bytes & 15) ||

@@ -306,8 +306,11 @@ void HipEngine::set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, S
   // a window of it (tile16_search_kernel<U, true>); records must then fit a window with two tiles' slack
   const bool whole = dev::tile16_lds_bytes(pbytes, L1) <= dev::kProf16MaxLds;
   const int64_t window = whole ? 0 : dev::tile16_max_window();
-  const bool t16 = tile16_ && L1 > 0 && build_profile16(table_, seq1, L1, overhang, prof);
-  prof16_window_ = t16 ? static_cast<int32_t>(window) : 0;
+  // weights past the byte pairs (|Dt| > 127) up to |Dt| <= 511: one int16 Dt per entry, which only the widened
+  // images take (whole where it fits, windows for short records; otherwise the LUT tile kernel)
+  const bool t16 = tile16_ && L1 > 0 && build_profile16(table_, seq1, L1, overhang, prof, /*allow_i16=*/true);
+  prof16_i16_ = t16 && prof.i16;
+  prof16_window_ = t16 && !prof16_i16_ ? static_cast<int32_t>(window) : 0;
   prof16_entries_ = t16 ? static_cast<int64_t>(prof.entries.size()) : 0;
   prof16_lds_bytes_ = t16 ? static_cast<int32_t>(whole ? pbytes
                                                        : ((2 * ((kAlphabet - 1) * window + dev::kProf16Overhang)) + 15) &
@@ -321,7 +324,8 @@ void HipEngine::set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, S
     const char* v = std::getenv("MOC_TILE16_WIDE");
     return !(v && std::atoi(v) == 0);
   }();
-  prof16_wide_ = t16 && whole && wide_env &&
+  if (prof16_i16_) prof16_lds_bytes_ = static_cast<int32_t>(pbytes);  // the whole image (widened: twice)
+  prof16_wide_ = t16 && (whole || prof16_i16_) && (wide_env || prof16_i16_) &&
                  dev::tile16_lds_bytes(2 * static_cast<int64_t>(prof16_lds_bytes_), L1) <= dev::kProf16MaxLds;
   const size_t total = t16 ? prof_off + static_cast<size_t>(pbytes) : prof_off;
   std::vector<uint8_t> next(total, 0);
@@ -389,8 +393,9 @@ dev::ProblemView HipEngine::problem_view(int64_t max_l2) const {
   pv.prof16_window = prof16_window_;
   pv.prof16_entries = prof16_entries_;
   pv.prof16_wide = prof16_wide_ && !mfma_ ? 1 : 0;
+  pv.prof16_i16 = prof16_i16_ ? 1 : 0;
   pv.max_abs_t = table_.max_abs();
-  pv.mfma_sweep = mfma_ && d_prof16_ && !prof16_window_ ? 1 : 0;
+  pv.mfma_sweep = mfma_ && d_prof16_ && !prof16_window_ && !prof16_i16_ ? 1 : 0;
   return pv;
 }
 
@@ -516,7 +521,7 @@ std::vector<dev::WaveStart> HipEngine::plan_waves(const int64_t* offsets, const 
   }
   tp.window = W;
   tp.wide = wide;
-  tp.tile16 = d_prof16_ != nullptr && (W == 0 || max_l2 + 2 * 128 <= W);
+  tp.tile16 = d_prof16_ != nullptr && (W == 0 || max_l2 + 2 * 128 <= W) && (wide || !prof16_i16_);
   // sub-tiles per wave tile: 4 amortises the per-tile setup over short records, 2 keeps more waves busy
   // on long ones (measured, both kernels: profiles/tile_variants.log, profiles/tile16_variants.log)
   int u = tile_u_ > 0 ? tile_u_ : (sum_l2 < 96 * n_long ? 4 : 2);

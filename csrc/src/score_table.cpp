@@ -84,17 +84,33 @@ bool profile16_fits(const ScoreTable& t) {
   return bounds::profile16_exact(dmin, dmax, tabs);
 }
 
-bool build_profile16(const ScoreTable& t, const uint8_t* seq1, int64_t L1, int64_t overhang, Profile16& out) {
+bool profile16_i16_fits(const ScoreTable& t) {
+  int32_t dmin = INT32_MAX, dmax = INT32_MIN;
+  for (int c = 1; c < kAlphabet; ++c)
+    for (int x = 0; x < kAlphabet; ++x)
+      for (int y = 0; y < kAlphabet; ++y) {
+        const int32_t d = t.score(c, x) - t.score(c, y);
+        dmin = std::min(dmin, d);
+        dmax = std::max(dmax, d);
+      }
+  return bounds::profile16_i16_exact(dmin, dmax);
+}
+
+bool build_profile16(const ScoreTable& t, const uint8_t* seq1, int64_t L1, int64_t overhang, Profile16& out,
+                     bool allow_i16) {
   if (L1 <= 0 || overhang < 0) return false;
-  if (!profile16_fits(t)) return false;
+  const bool pairs = profile16_fits(t);
+  if (!pairs && !(allow_i16 && profile16_i16_fits(t))) return false;
   out.row = L1;
+  out.i16 = !pairs;
   out.entries.assign(static_cast<size_t>((kAlphabet - 1) * L1 + overhang), 0);
   std::vector<int32_t> d(static_cast<size_t>(L1) + 1, 0);
   for (int c = 1; c < kAlphabet; ++c) {
     for (int64_t j = 0; j < L1; ++j) d[j] = t.score(c, seq1[j]) - t.score(c, j + 1 < L1 ? seq1[j + 1] : 0);
     uint16_t* r = out.entries.data() + static_cast<size_t>(c - 1) * static_cast<size_t>(L1);
     for (int64_t j = 0; j < L1; ++j)
-      r[j] = static_cast<uint16_t>((static_cast<uint32_t>(d[j + 1] & 0xff) << 8) | static_cast<uint32_t>(d[j] & 0xff));
+      r[j] = pairs ? static_cast<uint16_t>((static_cast<uint32_t>(d[j + 1] & 0xff) << 8) | static_cast<uint32_t>(d[j] & 0xff))
+                   : static_cast<uint16_t>(static_cast<int16_t>(d[j]));
   }
   return true;
 }

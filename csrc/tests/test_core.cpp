@@ -1169,10 +1169,20 @@ Result key32_record(const ScoreTable& t, const std::vector<uint8_t>& s1, const u
 // bytes are taken as given (so a profile built past the bound wraps as the kernel would see it).
 // kib > 0: the per-lane selection in 32-bit keys ((score << kib) + 2^31 + 2^kib - 1 - idx, kernel_bounds.hpp
 // tile16_key32_bits), converted back to the 64-bit key at the end as the kernel does.
+// i16: prof holds one int16 Dt per entry (the widened images' int16 profile): a lane's pair at column j is
+// entries j and j + 1, read as int16.
 Result tile16_record(const ScoreTable& t, const std::vector<uint8_t>& s1, const std::vector<uint16_t>& prof,
-                     const uint8_t* s2, int64_t L2, int64_t span, Semantics sem, int kib = 0) {
+                     const uint8_t* s2, int64_t L2, int64_t span, Semantics sem, int kib = 0, bool i16 = false) {
   const int64_t L1 = static_cast<int64_t>(s1.size());
   auto entry = [&](int c, int64_t j) { return prof[static_cast<size_t>((c - 1) * L1 + j)]; };
+  auto step_d = [&](int c, int64_t o, int64_t i) -> int16_t {  // Dt of offset o at step i as the kernel adds it
+    if (i16) {
+      const size_t e = static_cast<size_t>((c - 1) * L1 + (o & ~int64_t{1}) + i + (o & 1));
+      return static_cast<int16_t>(prof[e]);
+    }
+    const uint16_t p = entry(c, (o & ~int64_t{1}) + i);
+    return static_cast<int16_t>(static_cast<int8_t>(o & 1 ? p >> 8 : p & 0xff));
+  };
   const int64_t need = L2 <= L1 ? L1 - L2 + 1 : 0;
   if (!need) return Result{kNoCandidateScore, 0, 0};
   std::vector<int32_t> Dc(static_cast<size_t>(need) + 1, 0), maxD(static_cast<size_t>(need) + 1, INT32_MIN);
@@ -1183,9 +1193,8 @@ Result tile16_record(const ScoreTable& t, const std::vector<uint8_t>& s1, const 
       int16_t bestD = INT16_MIN;
       bool any = false;
       for (int64_t j = 0; j < m; ++j) {
-        const uint16_t e = entry(s2[i0 + j], (o & ~int64_t{1}) + i0 + j);
-        const int8_t d = static_cast<int8_t>(o & 1 ? e >> 8 : e & 0xff);
-        accD = static_cast<uint16_t>(accD + static_cast<uint16_t>(static_cast<int16_t>(d)));
+        const int16_t d = step_d(s2[i0 + j], o, i0 + j);
+        accD = static_cast<uint16_t>(accD + static_cast<uint16_t>(d));
         if (i0 + j + 1 < L2) {
           bestD = std::max(bestD, static_cast<int16_t>(accD));
           any = true;
@@ -1198,7 +1207,10 @@ Result tile16_record(const ScoreTable& t, const std::vector<uint8_t>& s1, const 
   for (int64_t o0 = 0; o0 < need; o0 += span) {
     const int64_t oA = std::min<int64_t>(o0 + span, need);
     int32_t acc = 0;
-    for (int64_t i = 0; i < L2; ++i) acc += static_cast<int8_t>(t.score(s2[i], oA + i < L1 ? s1[oA + i] : 0));
+    for (int64_t i = 0; i < L2; ++i) {
+      const int32_t tv = t.score(s2[i], oA + i < L1 ? s1[oA + i] : 0);
+      acc += i16 ? tv : static_cast<int8_t>(tv);  // the int16 profile's anchors read the int32 LUT
+    }
     for (int64_t o = oA - 1; o >= o0; --o) tot[o] = (acc += Dc[o]);
   }
   uint64_t best_key = 0;
@@ -1369,6 +1381,25 @@ void test_tile16_replay_bounds() {
   }
 }
 
+void test_tile16_i16_replay() {
+  using namespace xv;
+  // weights past the byte pairs: |Dt| = W1 + W4 = 511 in the int16 profile (exact: 64-step partial sums stay
+  // within 64 * 511 < 2^15), and 512 refused by the rule; the profile wrapped to int16 past it replays wrong
+  const Fixture f = azaz(600, 150, 400, 13);
+  for (Semantics sem : {Semantics::Reference, Semantics::Spec}) {
+    const ScoreTable at = ScoreTable::build(Weights{{255, 0, 0, 256}});
+    CHECK(!profile16_fits(at) && profile16_i16_fits(at));
+    Profile16 prof;
+    CHECK(!build_profile16(at, f.s1.data(), 600, 512, prof) && build_profile16(at, f.s1.data(), 600, 512, prof, true));
+    CHECK(prof.i16);
+    CHECK(mismatches(at, f, sem, [&](const uint8_t* s2, int64_t L2) {
+            return tile16_record(at, f.s1, prof.entries, s2, L2, 512, sem, 0, true);
+          }) == 0);
+    const ScoreTable past = ScoreTable::build(Weights{{256, 0, 0, 256}});
+    CHECK(!profile16_i16_fits(past) && !build_profile16(past, f.s1.data(), 600, 512, prof, true));
+  }
+}
+
 void test_tile16_key32_replay() {
   using namespace xv;
   // tile16's 32-bit selection keys against its 64-bit ones (the latter pinned to brute force above): W1 = 127,
@@ -1401,7 +1432,7 @@ int main() {
       {"kfd_topology", test_kfd_topology}, {"kfd_topology_8gpu", test_kfd_topology_8gpu},
       {"cutter_count_ahead", test_cutter_count_ahead}, {"swipe_replay_bounds", test_swipe_replay_bounds},
       {"short_replay_bounds", test_short_replay_bounds}, {"tile16_replay_bounds", test_tile16_replay_bounds},
-      {"tile16_key32_replay", test_tile16_key32_replay}};
+      {"tile16_key32_replay", test_tile16_key32_replay}, {"tile16_i16_replay", test_tile16_i16_replay}};
   for (const auto& t : tests) {
     const int before = g_failed;
     t.second();

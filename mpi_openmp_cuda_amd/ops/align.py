@@ -340,7 +340,8 @@ class HipSearchEngine:
 
 # Arithmetic forms of the kernels (csrc/include/moc/kernel_bounds.hpp FormBits), as stats()["forms"] names them.
 FORM_NAMES = ((1, "swipe_kbits"), (2, "swipe_rk"), (4, "short_pk"), (8, "short_key32"), (16, "short_key64"),
-              (32, "tile16"), (64, "tiles_key32"), (128, "tiles_key64"), (256, "mfma"), (512, "tile16_key32"))
+              (32, "tile16"), (64, "tiles_key32"), (128, "tiles_key64"), (256, "mfma"), (512, "tile16_key32"),
+              (1024, "tile16_i16"))
 
 
 def kernel_bounds(weights, L1: int, min_l2: int, max_l2: int) -> dict:
@@ -348,13 +349,13 @@ def kernel_bounds(weights, L1: int, min_l2: int, max_l2: int) -> dict:
     ``swipe`` = "swipe_kbits" | "swipe_rk" | None (the swipe kernel's integer bounds refuse it), ``short_pk``
     = the short kernel's packed int16 form is exact, ``key_shift`` = k bits of the int32 hot keys (0: int64
     keys), ``profile16`` = the tile16 int8 profile holds the table, ``tile16_key_bits`` = index bits of tile16's
-    32-bit selection keys (0: 64-bit keys)."""
-    out = np.zeros(5, np.int32)
+    32-bit selection keys (0: 64-bit keys), ``profile16_i16`` = the int16 tile16 profile holds the table."""
+    out = np.zeros(6, np.int32)
     _lib.check(_lib.lib().moc_kernel_bounds(_lib.weights_arg(Weights.of(weights).as_list()), int(L1), int(min_l2),
                                             int(max_l2), _lib.ptr(out)))
     swipe = {1: "swipe_kbits", 2: "swipe_rk"}.get(int(out[0]))
     return {"swipe": swipe, "short_pk": bool(out[1]), "key_shift": int(out[2]), "profile16": bool(out[3]),
-            "tile16_key_bits": int(out[4])}
+            "tile16_key_bits": int(out[4]), "profile16_i16": bool(out[5])}
 
 
 def search_hip(problem: Problem, semantics=Semantics.REFERENCE, device: Optional[int] = None,

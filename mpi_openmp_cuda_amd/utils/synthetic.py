@@ -35,6 +35,9 @@ SHAPES = {
     "mid": Shape((10, 2, 3, 4), 130, 67, 85),
     # input6's lengths under a heavy weight (W1 = 300): no room for k in the int16 keys, the RK swipe form
     "heavy6": Shape((300, 3, 2, 10), 26, 6, 11),
+    # long records under weights past the int8 difference profile (W1 + max(W2, W3, W4) > 127)
+    "heavy3": Shape((200, 10, 10, 10), 1489, 56, 1152),
+    "heavy4": Shape((120, 20, 1, 1), 2976, 5, 82),
 }
 
 

@@ -24,6 +24,7 @@ BOUNDS = [
     ("short_pk", 150, 130, 150, (109, 0, 0, 109), (110, 0, 0, 110), "short_pk", True, False),
     ("short_key32", 200, 150, 190, (22075, 0, 0, 22075), (22076, 0, 0, 22076), "key_shift", 8, 0),
     ("tile16", 600, 150, 400, (63, 0, 0, 64), (64, 0, 0, 64), "profile16", True, False),
+    ("tile16_i16", 600, 150, 400, (255, 0, 0, 256), (256, 0, 0, 256), "profile16_i16", True, False),
     ("tiles_key32", 600, 150, 400, (5242, 0, 0, 5242), (5243, 0, 0, 5243), "key_shift", 9, 0),
     # tile16's 32-bit selection keys: L1 2600 needs 13 index bits, so max|T| * L2 < 2^18 (127 * 2064 = 262128)
     ("tile16_key32", 2600, 2000, 2064, (127, 0, 0, 0), (127, 0, 0, 0), "tile16_key_bits", 13, 13),

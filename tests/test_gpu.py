@@ -1068,6 +1068,12 @@ EXTREMES = [
     # tile16's 32-bit selection keys: 127 * 2064 < 2^18 (L1 2600: 13 index bits), 127 * 2065 is not
     ("tile16_key32_at", 2600, 2000, 2064, (127, 0, 0, 0), ["tile16"], ["tile16", "tile16_key32"]),
     ("tile16_key32_past", 2600, 2000, 2065, (127, 0, 0, 0), ["tile16"], ["tile16"]),
+    # the int16 profile (widened images only): |Dt| = W1 + W4 = 511 at the bound, 512 past it
+    ("tile16_i16_at", 600, 150, 400, (255, 0, 0, 256), ["tile16"], ["tile16", "tile16_key32", "tile16_i16"]),
+    ("tile16_i16_past", 600, 150, 400, (256, 0, 0, 256), ["tiles"], ["tiles_key32"]),
+    ("tile16_i16_window", 2400, 40, 90, (255, 0, 0, 256), ["tile16"], ["tile16", "tile16_key32", "tile16_i16"]),
+    # no widened image holds it (L1 2400, records to 1200 letters): the LUT tile kernel
+    ("tile16_i16_long", 2400, 1000, 1200, (255, 0, 0, 256), ["tiles"], ["tiles_key32"]),
     ("tile16_past", 600, 150, 400, (64, 0, 0, 64), ["tiles"], ["tiles_key32"]),
     ("tiles_key32_at", 600, 150, 400, (5242, 0, 0, 5242), ["tiles"], ["tiles_key32"]),
     ("tiles_key32_past", 600, 150, 400, (5243, 0, 0, 5243), ["tiles"], ["tiles_key64"]),
