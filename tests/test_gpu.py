@@ -316,7 +316,12 @@ def test_kernel_selection(engine):
     engine.set_problem(p4.weights, p4.seq1)
     engine.solve(p4.codes, p4.offsets)
     assert engine.stats()["kernels"] == ["tile16"]
-    engine.set_problem([120, 20, 1, 1], p4.seq1)  # T range 140 > 127: profile bytes overflow -> DPP tiles
+    engine.set_problem([120, 20, 1, 1], p4.seq1)  # Dt range 140 > 127: the int16 profile, widened windows
+    got = engine.solve(p4.codes, p4.offsets)
+    assert engine.stats()["kernels"] == ["tile16"] and "tile16_i16" in engine.stats()["forms"]
+    assert np.array_equal(as_triples(got), as_triples(search_cpu(Problem([120, 20, 1, 1], p4.seq1, p4.codes,
+                                                                          p4.offsets))))
+    engine.set_problem([300, 300, 1, 1], p4.seq1)  # Dt range 600 > 511: past the int16 profile -> DPP tiles
     engine.solve(p4.codes, p4.offsets)
     assert engine.stats()["kernels"] == ["tiles"]
 
@@ -829,9 +834,12 @@ def test_tile16_window_wide(engine, L1):
         assert engine.stats()["kernels"] == ["tile16"], engine.stats()
 
 
-@pytest.mark.parametrize("w,forms", [((63, 0, 0, 64), ["tile16", "tile16_key32"]), ((64, 0, 0, 64), ["tiles_key32"])])
+@pytest.mark.parametrize("w,forms", [((63, 0, 0, 64), ["tile16", "tile16_key32"]),
+                                     ((64, 0, 0, 64), ["tile16", "tile16_key32", "tile16_i16"]),
+                                     ((256, 0, 0, 256), ["tiles_key32"])])
 def test_extreme_values_tile16_window_wide(engine, w, forms):
-    # the int8 profile bound on the widened-window image: |D| at its extreme, at the bound and one past
+    # the profile bounds on the widened-window image: the byte pairs at |Dt| = 127, the int16 profile one past
+    # it, the LUT tile kernel past |Dt| = 511
     from mpi_openmp_cuda_amd.utils.synthetic import make_extreme
 
     prob = make_extreme(2400, 40, 90, w, copies=3, seed=7)
@@ -1074,7 +1082,7 @@ EXTREMES = [
     ("tile16_i16_window", 2400, 40, 90, (255, 0, 0, 256), ["tile16"], ["tile16", "tile16_key32", "tile16_i16"]),
     # no widened image holds it (L1 2400, records to 1200 letters): the LUT tile kernel
     ("tile16_i16_long", 2400, 1000, 1200, (255, 0, 0, 256), ["tiles"], ["tiles_key32"]),
-    ("tile16_past", 600, 150, 400, (64, 0, 0, 64), ["tiles"], ["tiles_key32"]),
+    ("tile16_past", 600, 150, 400, (64, 0, 0, 64), ["tile16"], ["tile16", "tile16_key32", "tile16_i16"]),
     ("tiles_key32_at", 600, 150, 400, (5242, 0, 0, 5242), ["tiles"], ["tiles_key32"]),
     ("tiles_key32_past", 600, 150, 400, (5243, 0, 0, 5243), ["tiles"], ["tiles_key64"]),
 ]
