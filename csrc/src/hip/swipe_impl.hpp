@@ -546,29 +546,35 @@ __device__ __forceinline__ int wave_exclusive_sum_dpp(int v) {
 }
 
 // P33 field f of a tile (33 bits at bit b0 + 33 f of the 32-bit words from base32): its two words are
-// loaded first (p33_field_words, for several fields at once), then decoded to the 7 letter codes 1..26 at
-// d[0..6]. Digits past the first by multiply-high: q = umulhi(v, ceil(2^32 / 26)) is v / 26 exactly for
-// v < 2^30 (the error 4 v / (26 * 2^32) stays under 1 / 26), and v < 26^6 there.
+// loaded first (p33_field_words, for several fields at once), then decoded to the 7 letter codes 1..26.
+// Digits by 24-bit multiplies (full rate) after one 32-bit multiply-high: x < 26^7 splits into
+// A = x / 26^4 = (x / 16) / 13^4 (umulhi by ceil(2^46 / 28561), >> 14: exact for x / 16 < 2^29) and
+// B = x - 26^4 A < 2^19 (wrapping 32-bit arithmetic); B / 676 and A / 676 by v_mul_hi_u32_u24 with
+// ceil(2^32 / 676) (exact below 2^19), and a pair v < 676 -> (v % 26, v / 26) as the two bytes
+// v + 230 (v / 26), v / 26 = (2521 v) >> 16 (exact below 676). All constants checked exhaustively over
+// their ranges (tools/p33_magic_check.py).
 __device__ __forceinline__ void p33_field_words(const uint32_t* base32, int b0, int f, uint32_t& lo, uint32_t& hi) {
   const uint32_t* w = base32 + ((b0 + 33 * f) >> 5);
   lo = __builtin_nontemporal_load(w);
   hi = __builtin_nontemporal_load(w + 1);
 }
+__device__ __forceinline__ uint32_t mulhi_u24(uint32_t a, uint32_t b) {  // bits 32..47 of the 24 x 24-bit product
+  uint32_t r;
+  asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ uint32_t p33_pair(uint32_t v) {  // v < 676 -> bytes (v % 26, v / 26)
+  return __umul24(__umul24(v, 2521u) >> 16, 230u) + v;
+}
 __device__ __forceinline__ uint2 decode_p33_field(uint32_t lo, uint32_t hi, int b0, int f) {
   const uint64_t ww = static_cast<uint64_t>(lo) | (static_cast<uint64_t>(hi) << 32);
   const uint64_t x = (ww >> ((b0 + 33 * f) & 31)) & 0x1FFFFFFFFull;
-  uint32_t v = static_cast<uint32_t>(x >> 1) / 13u;  // x / 26 in 32-bit arithmetic
-  uint32_t d[7];
-  d[0] = static_cast<uint32_t>(x) - 26u * v;
-#pragma unroll
-  for (int j = 1; j < 7; ++j) {
-    const uint32_t q = __umulhi(v, 165191050u);
-    d[j] = v - 26u * q;
-    v = q;
-  }
+  const uint32_t A = __umulhi(static_cast<uint32_t>(x >> 4), 2463805336u) >> 14;  // digits 4..6
+  const uint32_t B = static_cast<uint32_t>(x) - __umul24(A, 456976u);  // digits 0..3
+  const uint32_t b32 = mulhi_u24(B, 6353502u), a2 = mulhi_u24(A, 6353502u);
+  const uint32_t b10 = B - __umul24(b32, 676u), a10 = A - __umul24(a2, 676u);
   // letter codes are digit + 1; the pad byte stays 0
-  return make_uint2((d[0] | (d[1] << 8) | (d[2] << 16) | (d[3] << 24)) + 0x01010101u,
-                    (d[4] | (d[5] << 8) | (d[6] << 16)) + 0x00010101u);
+  return make_uint2((p33_pair(b10) | (p33_pair(b32) << 16)) + 0x01010101u, (p33_pair(a10) | (a2 << 16)) + 0x00010101u);
 }
 
 // The letters of a lane's record from the tile's 8-byte field slots: NS slots from the record's first field
@@ -621,20 +627,34 @@ __device__ __forceinline__ void record_words_p33(const uint8_t* slots, int q0, i
 }
 
 // Length of record 64 t + lane of a batch with base-6 lengths (three 21-bit octets of 8 digits per 8-byte
-// word): 32-bit index arithmetic and a branch-free digit select (v / 6 = umulhi(v, ceil(2^32 / 6)), exact
-// for v < 2^31).
-__device__ __forceinline__ int lane_length6(const ShortArgs& a, int64_t t, int lane) {
+// word): 32-bit index arithmetic, and digit j = lane % 8 of its octet v < 2^21 as (v / 6^j) % 6 — v / 6^j one
+// multiply-high by the lane's constant (Len6Digit, made once per kernel; exact below 2^21, checked
+// exhaustively by tools/p33_magic_check.py), then one for the % 6.
+struct Len6Digit {
+  uint32_t m = 0;  // ceil(2^(32 + sh) / 6^j); 0: j = 0
+  int sh = 0;
+};
+__device__ __forceinline__ Len6Digit len6_digit(int lane) {
+  constexpr uint32_t kM[8] = {0u, 2863311531u, 3817748708u, 2545165806u,
+                              3393554407u, 2262369605u, 3016492806u, 4021990408u};
+  constexpr int kSh[8] = {0, 2, 5, 7, 10, 12, 15, 18};
+  Len6Digit d;
+  const int j = lane & 7;
+#pragma unroll
+  for (int k = 1; k < 8; ++k)
+    if (j == k) {
+      d.m = kM[k];
+      d.sh = kSh[k];
+    }
+  return d;
+}
+__device__ __forceinline__ int lane_length6(const ShortArgs& a, int64_t t, int lane, Len6Digit dg) {
   const uint32_t octet = static_cast<uint32_t>(t) * 8u + static_cast<uint32_t>(lane >> 3);
   const uint32_t word = octet / 3u;
   const uint64_t w = *reinterpret_cast<const uint64_t*>(a.lengths6 + 8 * static_cast<uint64_t>(word));
   uint32_t v = static_cast<uint32_t>(w >> (21 * (octet - 3u * word))) & 0x1FFFFFu;
-  const int j = lane & 7;
-#pragma unroll
-  for (int k = 0; k < 7; ++k) {
-    const uint32_t q = __umulhi(v, 715827883u);
-    v = k < j ? q : v;
-  }
-  return a.len_base + static_cast<int>(v - 6u * __umulhi(v, 715827883u));
+  v = dg.m ? __umulhi(v, dg.m) >> dg.sh : v;
+  return a.len_base + static_cast<int>(v - __umul24(6u, __umulhi(v, 715827883u)));
 }
 
 template <int NOFF, int L2W, int LF, bool RK>
@@ -649,6 +669,7 @@ __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, S
   const int64_t n = a.n, n_tiles = (n + 63) >> 6;
   const int64_t waves = static_cast<int64_t>(gridDim.x) * (kBlockD / 64);
   int64_t t = static_cast<int64_t>(blockIdx.x) * (kBlockD / 64) + (threadIdx.x >> 6);
+  const Len6Digit dg = len6_digit(lane);
   uint8_t* wbuf = smem + lay.codes_off + (threadIdx.x >> 6) * direct_wave_bytes(L2W);  // P33: this wave's
   // bytes: the record's offsets; P33: the tile's first letter (o0, every lane) and the record's length (o1)
   auto load_meta = [&](int64_t tt, int64_t& o0, int64_t& o1) {
@@ -656,14 +677,44 @@ __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, S
     const bool in = tt < n_tiles && r < n;
     if constexpr (P33) {
       o0 = tt < n_tiles ? tile_offset(a, tt << 6) : 0;  // 64-record tiles: boundaries of sparse offsets too
-      o1 = !in ? 0 : a.lengths6 && tt < (int64_t{1} << 28) ? lane_length6(a, tt, lane) : record_length(a, r);
+      o1 = !in ? 0 : a.lengths6 && tt < (int64_t{1} << 28) ? lane_length6(a, tt, lane, dg) : record_length(a, r);
     } else {
       o0 = in ? a.offsets[r] : 0;
       o1 = in ? a.offsets[r + 1] : 0;
     }
   };
-  int64_t o0, o1;
+  // P33 fields: lanes take fields lane, lane + 64, ... of a tile. Where kBatch per lane cover every field a
+  // tile can span (records of up to 16 letters), the next tile's field words are loaded while this one is
+  // scored — its first letter comes with the metadata loaded one tile further ahead — up to the batch's
+  // last field (fe); beyond that, the words of kBatch fields at a time are loaded after the tile's lengths.
+  constexpr int kIters = ((64 * 4 * L2W + 6) / 7 + 1 + 63) / 64;  // fields a tile can span / 64
+  constexpr int kBatch = kIters < 4 ? kIters : 4;
+  constexpr bool PF = P33 && kIters <= kBatch;
+  auto uniform64 = [](int64_t v) {
+    return static_cast<int64_t>(
+        (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(v >> 32))))
+         << 32) |
+        static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(v))));
+  };
+  const int64_t fe = PF ? (tile_offset(a, n) + 6) / 7 : 0;
+  uint32_t flo[kBatch], fhi[kBatch];
+  auto prefetch_fields = [&](int64_t tt, int64_t oo) {
+    const int64_t f0 = uniform64(oo) / 7;
+    const uint32_t* base32 = reinterpret_cast<const uint32_t*>(a.codes) + ((33 * f0) >> 5);
+    const int b0 = static_cast<int>((33 * f0) & 31);
+#pragma unroll
+    for (int b = 0; b < kBatch; ++b) {
+      const int f = 64 * b + lane;
+      flo[b] = fhi[b] = 0u;
+      if (tt < n_tiles && f0 + f < fe) p33_field_words(base32, b0, f, flo[b], fhi[b]);
+    }
+  };
+  int64_t o0, o1, p0 = 0, p1 = 0;
   load_meta(t, o0, o1);
+  if constexpr (PF) {
+    load_meta(t + waves, p0, p1);
+    prefetch_fields(t, o0);
+  }
   for (; t < n_tiles; t += waves) {  // wave-uniform
     const int64_t r = (t << 6) + lane;
     const int L2 = static_cast<int>(P33 ? o1 : o1 - o0);
@@ -673,21 +724,23 @@ __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, S
     uint32_t wd[L2W];
     if constexpr (P33) {
       // the tile's first letter and field (wave-uniform: scalar arithmetic), the lane's start within the tile
-      const int64_t st = static_cast<int64_t>(
-          (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(o0 >> 32))))
-           << 32) |
-          static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(o0))));
+      const int64_t st = uniform64(o0);
       const int64_t f0 = st / 7;
       const int s0 = static_cast<int>(st - 7 * f0);
       const int excl = wave_exclusive_sum_dpp(L2);
       const int nf = (s0 + __builtin_amdgcn_readlane(excl + L2, 63) + 6) / 7;
       const uint32_t* base32 = reinterpret_cast<const uint32_t*>(a.codes) + ((33 * f0) >> 5);
       const int b0 = static_cast<int>((33 * f0) & 31);
+      if constexpr (PF) {
+#pragma unroll
+        for (int b = 0; b < kBatch; ++b) {
+          const int f = 64 * b + lane;
+          if (f < nf) *reinterpret_cast<uint2*>(wbuf + 8 * f) = decode_p33_field(flo[b], fhi[b], b0, f);
+        }
+      }
       // fields lane, lane + 64, ...: the words of up to kBatch fields per lane are loaded before any is
       // decoded (one memory latency per batch, not per field)
-      constexpr int kIters = ((64 * 4 * L2W + 6) / 7 + 1 + 63) / 64;  // fields a tile can span / 64
-      constexpr int kBatch = kIters < 4 ? kIters : 4;
-      for (int f0b = 0; f0b < nf; f0b += 64 * kBatch) {  // wave-uniform
+      for (int f0b = 0; !PF && f0b < nf; f0b += 64 * kBatch) {  // wave-uniform
         uint32_t lo[kBatch], hi[kBatch];
 #pragma unroll
         for (int b = 0; b < kBatch; ++b) {
@@ -723,12 +776,24 @@ __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, S
       }
     }
     int64_t n0, n1;
-    load_meta(t + waves, n0, n1);  // in flight while this tile is scored
+    if constexpr (PF) {  // in flight while this tile is scored: the next tile's fields, the metadata after it
+      prefetch_fields(t + waves, p0);
+      load_meta(t + 2 * waves, n0, n1);
+    } else {
+      load_meta(t + waves, n0, n1);
+    }
     const Result res = swipe_lane<NOFF, L2W, RK>(smem, wd, L2, on, L1, a.max_l2, pv.semantics);
     if (mine) store_result(a.out, r, a.fmt, res, pv.r2);
     if constexpr (P33) __builtin_amdgcn_wave_barrier();  // every lane read the slice before the next tile's writes
-    o0 = n0;
-    o1 = n1;
+    if constexpr (PF) {
+      o0 = p0;
+      o1 = p1;
+      p0 = n0;
+      p1 = n1;
+    } else {
+      o0 = n0;
+      o1 = n1;
+    }
   }
 }
 

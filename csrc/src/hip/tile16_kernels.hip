@@ -5,33 +5,35 @@
 // atomicMax per record run. The per-cell work is what changes. With the closed form
 //     score(o, 0) = Tot_o,   score(o, k >= 1) = D_o(k) + Tot_{o+1},   D_o(k) = P_o(k) - P_{o+1}(k)
 //     D_o(k) = sum_{i<k} Dt[c_i][o + i],   Dt[c][j] = T[c][Seq1[j]] - T[c][Seq1[j+1]]
-// the hot loop only needs the running sums of Dt along each diagonal and their running maximum. Dt
-// fits a signed byte for every realistic weight set (T range <= 127), so:
-//   * LDS holds Profile16 (moc/score_table.hpp): entry [c][j] = bytes (Dt[c][j], Dt[c][j+1]) — the
-//     step-i terms of the two adjacent diagonals o = j - i and o + 1. A LANE carries such a pair of
-//     offsets, as the two int16 halves of one register, so one conflict-free ds_read_u16 feeds two cells;
-//   * per step and lane:  acc.lo += sext(byte0); acc.hi += sext(byte1)   2 x v_add_u16_sdwa
-//                         best = max(best, acc)                          v_pk_max_i16
-//     i.e. 1.5 VALU + 0.5 LDS read per cell (the LUT-gather + DPP form of tile_search_kernel costs ~7);
-//     the letter's row offset arrives with one v_readlane per step for the whole wave tile, and the U
-//     sub-tiles (128 offsets each) sit at immediate LDS offsets;
-//   * every 64 steps the int16 halves are folded into int32 (|partial sums| <= 64*128 < 2^15: exact);
+// the hot loop only needs the running sums of Dt along each diagonal and their running maximum. A LANE
+// carries a pair of adjacent offsets o, o + 1 as the two int16 halves of one register; LDS holds the
+// difference profile (moc/score_table.hpp Profile16), entry [c][j] = (Dt[c][j], Dt[c][j+1]) — the step-i
+// terms of both diagonals — in one of three forms:
+//   * byte pairs (|Dt| <= 127, 2 bytes per entry): per step and lane one ds_read_u16, then
+//       acc.lo += sext(byte0); acc.hi += sext(byte1)   2 x v_add_u16_sdwa
+//       best = max(best, acc)                          v_pk_max_i16
+//   * widened pairs (Wide: the byte pairs sign-extended to int16 halves while staging, 4 bytes per entry,
+//     split by flat-index parity so the lanes' reads are conflict-free): one ds_read_b32, v_pk_add_u16,
+//     v_pk_max_i16 — where twice the image fits (whole, or as windows for short records);
+//   * an int16 profile (pv.prof16_i16: |Dt| <= 511, weights past the byte pairs): staged straight into the
+//     widened form.
+//   The U sub-tiles (128 offsets each) of a wave tile sit at immediate LDS offsets, a step's row offset
+//   arrives by one DPP row broadcast, and G * U reads issue before a group's adds;
+//   * every 64 steps the int16 halves are folded into int32 (|partial sums| <= 64 * 511 < 2^15: exact);
 //   * Tot_o is not summed per cell: per tile one anchor diagonal Tot_{oA} (oA = first offset past the
 //     tile or past the valid range) is summed alongside the sweep (each chunk's lanes add their step's
-//     pair score from an int8 LUT + Seq1 staged next to the profile), and
+//     pair score from the LUT + Seq1 staged next to the profile), and
 //     Tot_o = Tot_{oA} + sum_{o <= o' < oA} D_{o'}(L2) comes from a wave scan on the DPP network;
-//   * short records (mean |Seq2| < 96) take U = 8 sub-tiles (1024-offset tiles: half the per-tile
-//     epilogues) when the profile's 1024-entry overhang fits the LDS; their last chunk issues the reads
-//     of 8 steps before the adds (profiles/tile16_variants_v2.log).
+//   * short records take U = 8 sub-tiles (1024-offset tiles: fewer per-tile epilogues).
 // Per offset this gives the best score, but not which k: the sweep reduces pass-1 keys (score,
-// ~(2o + mutated)) — the reference order: score, then smallest o, then k = 0 first — and
-// resolve_long_kernel (align_kernels.hip) re-walks only the winning diagonal of each record (one wave,
-// O(L2)) to find the smallest k with that score. Host replay of all of it, ties included:
-// csrc/tests/test_core.cpp test_profile16.
+// ~(2o + mutated)) — the reference order: score, then smallest o, then k = 0 first — 32-bit ones where
+// bounds::tile16_key32_bits says score and index fit — and resolve_long_kernel (align_kernels.hip)
+// re-walks only the winning diagonal of each record (one wave, O(L2)) to find the smallest k with that
+// score. Host replay of all of it, ties included: csrc/tests/test_core.cpp test_profile16,
+// test_tile16_key32_replay, test_tile16_i16_replay.
 //
 // Replaces calc_result (cudaFunctions.cu:63-176) for long records when the weights fit the profile
-// bytes (W1 + max(W2,W3,W4) <= 127) and the LDS image fits one CU (2*(26*L1 + 512) + 1 KiB + L1 bytes
-// <= 160 KiB: L1 <= 3052, covering the reference's 3000-letter Seq1 buffer, myProto.h:3).
+// (byte pairs or int16) and the image fits one CU's LDS (whole, or as windows of Seq1 for longer ones).
 #include <hip/hip_runtime.h>
 
 #include <mutex>
@@ -49,9 +51,6 @@ using namespace kc;
 namespace {
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
-#ifndef MOC_T16_DPP_SCAN
-#define MOC_T16_DPP_SCAN 1  // tile epilogue scans on DPP instead of ds_bpermute shuffles
-#endif
 constexpr int kBlock16 = 1024;  // 16 waves: the profile takes most of the CU's LDS, one workgroup holds it
 constexpr int kWavesPerBlock16 = kBlock16 / 64;
 constexpr int kSub = 128;                    // offsets per sub-tile (2 per lane)
@@ -112,16 +111,6 @@ __device__ __forceinline__ int row_newbcast(int v, int k) {
     case 14: return newbcast<14>(v);
     default: return newbcast<15>(v);
   }
-}
-
-// Inclusive suffix sum over the lanes of a wave (lane l gets sum of v over lanes l..63).
-__device__ __forceinline__ int wave_suffix_sum(int v, int lane) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int t = __shfl_down(v, d, 64);
-    if (lane + d < 64) v += t;
-  }
-  return v;
 }
 
 // Inclusive prefix sum over the lanes of a wave on the DPP network: row shifts 1/2/4/8 (zero-filled),
@@ -489,31 +478,19 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
         flush(m > 1);
       }
       // ---- Tot per offset: anchor diagonal oA, then suffix sums of the D totals (valid offsets only)
-#if MOC_T16_DPP_SCAN
       anchor = __builtin_amdgcn_readlane(wave_prefix_sum_dpp(anchor), 63);
-#else
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) anchor += __shfl_xor(anchor, d, 64);
-#endif
       int carry = anchor;  // Tot at the end of the sub-tile being processed
 #pragma unroll
       for (int u = U - 1; u >= 0; --u) {
         const int oa = o0 + kSub * u + 2 * lane;
         const int ca = oa < oA ? DcA[u] : 0, cb = oa + 1 < oA ? DcB[u] : 0;
         const int pair = ca + cb;
-#if MOC_T16_DPP_SCAN
         const int incl = wave_prefix_sum_dpp(pair);
         const int sub_total = __builtin_amdgcn_readlane(incl, 63);
         const int excl = sub_total - incl;   // lanes above this one
         const int totB = carry + excl + cb;  // Tot_{oa+1}
         const int totA = totB + ca;          // Tot_{oa}
         carry += sub_total;
-#else
-        const int excl = wave_suffix_sum(pair, lane) - pair;
-        const int totB = carry + excl + cb;  // Tot_{oa+1}
-        const int totA = totB + ca;          // Tot_{oa}
-        carry = __shfl(totA, 0, 64);
-#endif
         if (kib) {
           // keys ((score + 2^(31 - kib)) << kib) | (2^kib - 1 - idx): the bias and the index term are one
           // per-lane constant, so a key is one shift-add of the score (moc/kernel_bounds.hpp tile16_key32_bits)

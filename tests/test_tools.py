@@ -52,3 +52,12 @@ def test_step_variance_report(tmp_path):
     assert out["steps"] == 100 and out["slow_steps"] == 10
     assert out["bursts"] == {"count": 10, "longest": 1, "mean_len": 1.0}
     assert out["sclk_mhz"]["normal_median"] == 2400
+
+
+def test_p33_magic_constants():
+    # the device decoders' multiply-by-reciprocal constants (swipe_impl.hpp decode_p33_field, lane_length6),
+    # exhaustively over their input ranges
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "p33_magic_check.py")], capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == "ok"
