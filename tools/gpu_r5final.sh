@@ -9,6 +9,6 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('s
 tail -1 gpurun_out/r5final/smoke.log
 timeout -k 10 600 python -u bench.py --steps 50 --warmup 5 > gpurun_out/r5final/bench.log 2>&1 || { tail -5 gpurun_out/r5final/bench.log; exit 1; }
 tail -1 gpurun_out/r5final/bench.log | cut -c1-400
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/r5final/prof -o bench -- python3 bench.py --steps 20 --warmup 3 > gpurun_out/r5final/bench_prof.log 2>&1 || { tail -5 gpurun_out/r5final/bench_prof.log; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r5final/prof -o bench -- python3 bench.py --steps 20 --warmup 3 > gpurun_out/r5final/bench_prof.log 2>&1 || { tail -5 gpurun_out/r5final/bench_prof.log; exit 1; }
 find gpurun_out/r5final/prof -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} gpurun_out/r5final/bench_kernel_stats.csv
 head -5 gpurun_out/r5final/bench_kernel_stats.csv | cut -c1-200
