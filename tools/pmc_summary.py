@@ -2,7 +2,7 @@
 """Sums rocprofv3 --pmc counter CSVs per kernel name (prefix before '<'), over every dispatch, and prints
 one JSON line per kernel with the counters and derived ratios (VALU instructions per wave cycle, waits).
 
-    python tools/pmc_summary.py gpurun_out/pmc_r4_0/p1 gpurun_out/pmc_r4_0/p2
+    python tools/pmc_summary.py [--tag PASS] gpurun_out/pmc_r4_0/p1 gpurun_out/pmc_r4_0/p2
 """
 import csv
 import glob
@@ -30,7 +30,7 @@ def load(d):
     return tot, disp
 
 
-def main(dirs):
+def main(dirs, tag=None):
     # each pass (directory) is its own run: its dispatch count can differ from another pass's (the bench sizes
     # its iteration count from a first timing), so every counter is scaled to the dispatch count of the first
     # pass that saw the kernel — the sums stay "per that many dispatches" across passes
@@ -45,6 +45,8 @@ def main(dirs):
             merged[k].update({c: x * scale for c, x in v.items()})
     for k, v in sorted(merged.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0)):
         out = {"kernel": k[:90], "dispatches": ndisp.get(k, 0)}
+        if tag is not None:
+            out["pass"] = tag
         out.update({c: int(x) for c, x in sorted(v.items())})
         wc = v.get("SQ_WAVE_CYCLES", 0)
         if wc:
@@ -58,4 +60,8 @@ def main(dirs):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:])
+    args = sys.argv[1:]
+    tag = None
+    if len(args) >= 2 and args[0] == "--tag":  # label every line with its pass (tools/roofline.py ROWS)
+        tag, args = args[1], args[2:]
+    main(args, tag)

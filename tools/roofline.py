@@ -23,16 +23,18 @@ CUS, SES = 256, 32
 PEAK_PACKED, PEAK_VALU32, PEAK_LDS = 0.94, 1.69, 0.48  # wave-instructions per CU-clock (isa_peak)
 
 # kernel-bench row (shape, variant) -> the kernel that does its search (a prefix of its name in the summary)
-ROWS = [
-    ("input6", "tile16", "swipe_direct_kernel<24, 4, 0, false>", "device bytes"),
-    ("input6", "wire", "swipe_direct_kernel<24, 4, 2, false>", "device P33 wire"),
-    ("input1", "tile16", "swipe_direct_kernel<24, 16, 0, true>", "device bytes"),
-    ("input1", "wire", "swipe_direct_kernel<24, 16, 2, true>", "device P33 wire"),
-    ("mid", "tile16", "short_search_kernel<", ""),
-    ("input3", "tile16", "tile16_search_kernel<2, false, true>", "widened pairs"),
-    ("limits", "tile16", "tile16_search_kernel<2, false, false>", "byte pairs"),
-    ("input4", "tile16", "tile16_search_kernel<8, true, true>", "widened windows"),
-    ("long20k", "tile16", "tile16_search_kernel<4, true, false>", "byte-pair windows"),
+ROWS = [  # shape, kernel_bench variant, kernel name prefix, form, PMC pass (tools/pmc_r5.sh)
+    ("input6", "tile16", "swipe_direct_kernel<24, 4, 0, false>", "device bytes", "p1"),
+    ("input6", "wire", "swipe_direct_kernel<24, 4, 2, false>", "device P33 wire", "p4"),
+    ("input1", "tile16", "swipe_direct_kernel<24, 16, 0, true>", "device bytes", "p1"),
+    ("input1", "wire", "swipe_direct_kernel<24, 16, 2, true>", "device P33 wire", "p4"),
+    ("mid", "tile16", "swipe_direct_kernel<64, 24, 0, true>", "device bytes, 24 record words", "p1"),
+    ("input3", "tile16", "tile16_search_kernel<2, false, true>", "widened pairs", "p2"),
+    ("limits", "tile16", "tile16_search_kernel<2, false, false>", "byte pairs", "p2"),
+    ("input4", "tile16", "tile16_search_kernel<8, true, true>", "widened windows", "p3"),
+    ("long20k", "tile16", "tile16_search_kernel<4, true, false>", "byte-pair windows", "p3"),
+    ("heavy3", "tile16", "tile16_search_kernel<2, false, true>", "int16 profile", "p5"),
+    ("heavy4", "tile16", "tile16_search_kernel<8, true, true>", "int16 profile, windows", "p5"),
 ]
 
 
@@ -48,8 +50,8 @@ def main(argv):
     print("| shape | path | kernel | T cells/s | VALU lane-instr / cell | VALU wave-instr / CU-clock | of packed peak | "
           "LDS wave-instr / CU-clock | of LDS peak | LDS conflict share | s_waitcnt share |")
     print("|---|---|---|---:|---:|---:|---:|---:|---:|---:|---:|")
-    for shape, variant, kname, path in ROWS:
-        rows = [r for r in pmc if kname in r["kernel"]]
+    for shape, variant, kname, path, tag in ROWS:
+        rows = [r for r in pmc if kname in r["kernel"] and r.get("pass", tag) == tag]
         b = bench.get((shape, variant))
         if not rows or b is None:
             continue
