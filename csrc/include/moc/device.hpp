@@ -72,6 +72,8 @@ struct ProblemView {
   // 1: prof16 holds one int16 Dt per entry (weights past the byte pairs, bounds::profile16_i16_exact), staged
   // into widened images only
   int32_t prof16_i16 = 0;
+  int32_t t16_slide = 0;               // tile16: sliding widened windows of prof16_window columns
+                                       // (tile16_slide_kernel; the plan's items and groups)
 };
 
 // Entries after the tile16 profile's last row: reads of wave-tile lanes past the valid offsets reach
@@ -119,6 +121,7 @@ struct WaveStart {
 
 // Offsets per wave tile: U sub-tiles of 63 (tile kernel) or 128 (tile16: two offsets per lane).
 inline int tile_span(bool tile16, int u) { return (tile16 ? 128 : kTileOffsets) * u; }
+constexpr int kTile16WavesPerBlock = 16;  // tile16 workgroups: 16 waves
 inline int64_t tiles_of(int64_t need, int span) { return (need + span - 1) / span; }
 
 // Host-built plan for the tile kernel of one batch.
@@ -132,6 +135,8 @@ struct Plan {
   int32_t win_tiles = 0;               // windowed tile16: tiles per window stride (the waves of one
                                        // workgroup all walk tiles t in [m*win_tiles, (m+1)*win_tiles))
   R2Params r2;                         // finalize: parameters of the R2 result format
+  int64_t slide_items = 0;             // tile16 sliding windows: starts = per-workgroup item offsets, then
+  int64_t slide_members = 0;           // items (2 entries each) from slide_items, group members from slide_members
 };
 
 // Arguments of the short-record kernel. All pointers must be device-accessible: device memory, or
@@ -221,7 +226,8 @@ inline int32_t tile_form(const ProblemView& pv) {
   if (pv.prof16)
     return pv.mfma_sweep ? bounds::kFormMfma
                          : bounds::kFormTile16 | (pv.t16_key_bits ? bounds::kFormTile16Key32 : 0) |
-                               (pv.prof16_i16 ? bounds::kFormTile16I16 : 0);
+                               (pv.prof16_i16 ? bounds::kFormTile16I16 : 0) |
+                               (pv.t16_slide ? bounds::kFormTile16Slide : 0);
   return pv.key_shift > 0 ? bounds::kFormTilesKey32 : bounds::kFormTilesKey64;
 }
 void launch_finalize_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, void* out, int fmt,

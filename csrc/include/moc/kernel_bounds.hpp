@@ -112,6 +112,7 @@ enum FormBits : int32_t {
   kFormMfma = 256,        // matrix-core sweep over the tile16 profile
   kFormTile16Key32 = 512, // tile16's per-lane selection in 32-bit keys (tile16_key32_bits)
   kFormTile16I16 = 1024,  // tile16 over the int16 profile (profile16_i16_exact)
+  kFormTile16Slide = 2048,  // tile16 in sliding widened windows (long records, widened image past the LDS)
 };
 
 }  // namespace bounds

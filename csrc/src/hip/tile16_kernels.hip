@@ -147,6 +147,60 @@ __device__ __forceinline__ uint32_t wave_max_u32_dpp(uint32_t v) {
 }
 }  // namespace
 
+// Stages columns [S, S + W) of every profile row as widened entries split by the parity of their window index
+// e = c * W + x (halves of pv.prof16_bytes each; then the overhang, zeros), and Seq1 letters S .. S + W + 16
+// (the anchor diagonals) at s1l. All threads of the workgroup take part.
+__device__ __forceinline__ void stage_window_wide(unsigned char* smem, uint8_t* s1l, const ProblemView& pv, int S,
+                                                  int W) {
+  // the window's entries e = c * W + x (x < W: global column S + x of row c; then the overhang, zeros),
+  // widened and split by the parity of e as in the whole image (halves of pv.prof16_bytes each)
+  uint32_t* even = reinterpret_cast<uint32_t*>(smem);
+  uint32_t* odd = reinterpret_cast<uint32_t*>(smem + pv.prof16_bytes);
+  const int rows_entries = (kAlphabet - 1) * W;
+  const int n_entries = pv.prof16_bytes >> 1;
+  auto widen1 = [](uint32_t e) {  // byte pair -> two sign-extended int16 halves
+    return (static_cast<uint32_t>(static_cast<int8_t>(e & 0xffu)) & 0xffffu) |
+           (static_cast<uint32_t>(static_cast<int8_t>((e >> 8) & 0xffu)) << 16);
+  };
+  if (pv.prof16_i16) {  // int16 Dt per entry: the pair of window entry (c, x) is global (g, g + 1)
+    for (int e = threadIdx.x; e < n_entries; e += blockDim.x) {
+      uint32_t v = 0;
+      if (e < rows_entries) {
+        const int c = e / W, x = e - c * W;
+        const int64_t g = static_cast<int64_t>(c) * pv.L1 + S + x;
+        if (g < pv.prof16_entries) v = pv.prof16[g];
+        if (g + 1 < pv.prof16_entries) v |= static_cast<uint32_t>(pv.prof16[g + 1]) << 16;
+      }
+      ((e & 1) ? odd : even)[e >> 1] = v;
+    }
+  } else if ((pv.L1 & 7) == 0) {  // rows 16-byte aligned (W and S are multiples of 16): 8 entries per load
+    const int w8 = W >> 3;
+    for (int e = threadIdx.x; e < (kAlphabet - 1) * w8; e += blockDim.x) {
+      const int c = e / w8, x = (e - c * w8) << 3;
+      const int64_t g = static_cast<int64_t>(c) * pv.L1 + S + x;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (g + 8 <= pv.prof16_entries) v = *reinterpret_cast<const uint4*>(pv.prof16 + g);
+      const int d = (c * W + x) >> 1;  // entries c*W + x .. + 7: 4 even, 4 odd, 16-byte aligned
+      *reinterpret_cast<uint4*>(even + d) = make_uint4(widen1(v.x & 0xffffu), widen1(v.y & 0xffffu),
+                                                       widen1(v.z & 0xffffu), widen1(v.w & 0xffffu));
+      *reinterpret_cast<uint4*>(odd + d) = make_uint4(widen1(v.x >> 16), widen1(v.y >> 16), widen1(v.z >> 16),
+                                                      widen1(v.w >> 16));
+    }
+    for (int e = rows_entries + threadIdx.x; e < n_entries; e += blockDim.x) ((e & 1) ? odd : even)[e >> 1] = 0u;
+  } else {
+    for (int e = threadIdx.x; e < n_entries; e += blockDim.x) {
+      uint32_t v = 0;
+      if (e < rows_entries) {
+        const int c = e / W, x = e - c * W;
+        const int64_t g = static_cast<int64_t>(c) * pv.L1 + S + x;
+        if (g < pv.prof16_entries) v = widen1(pv.prof16[g]);
+      }
+      ((e & 1) ? odd : even)[e >> 1] = v;
+    }
+  }
+  for (int t = threadIdx.x; t < W + 16; t += blockDim.x) s1l[t] = S + t < pv.L1 ? pv.seq1[S + t] : 0;
+}
+
 // Win (windowed): Seq1 is longer than one LDS image holds. The workgroup's waves all walk tiles of one
 // window m (plan: window-major wave runs, 16-wave aligned, tiles t in [m*T, (m+1)*T) of every record), so it
 // stages only columns [S, S + W) of each profile row (S = m*T*span, W = pv.prof16_window) and the Seq1
@@ -176,53 +230,7 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
   const int S = t_base * kSpan;                                             // first column of the window
   const int W = Win ? pv.prof16_window : pv.L1;                             // columns per LDS row
   if (Win && Wide) {
-    // the window's entries e = c * W + x (x < W: global column S + x of row c; then the overhang, zeros),
-    // widened and split by the parity of e as in the whole image (halves of pv.prof16_bytes each)
-    uint32_t* even = reinterpret_cast<uint32_t*>(smem);
-    uint32_t* odd = reinterpret_cast<uint32_t*>(smem + pv.prof16_bytes);
-    const int rows_entries = (kAlphabet - 1) * W;
-    const int n_entries = pv.prof16_bytes >> 1;
-    auto widen1 = [](uint32_t e) {  // byte pair -> two sign-extended int16 halves
-      return (static_cast<uint32_t>(static_cast<int8_t>(e & 0xffu)) & 0xffffu) |
-             (static_cast<uint32_t>(static_cast<int8_t>((e >> 8) & 0xffu)) << 16);
-    };
-    if (pv.prof16_i16) {  // int16 Dt per entry: the pair of window entry (c, x) is global (g, g + 1)
-      for (int e = threadIdx.x; e < n_entries; e += blockDim.x) {
-        uint32_t v = 0;
-        if (e < rows_entries) {
-          const int c = e / W, x = e - c * W;
-          const int64_t g = static_cast<int64_t>(c) * pv.L1 + S + x;
-          if (g < pv.prof16_entries) v = pv.prof16[g];
-          if (g + 1 < pv.prof16_entries) v |= static_cast<uint32_t>(pv.prof16[g + 1]) << 16;
-        }
-        ((e & 1) ? odd : even)[e >> 1] = v;
-      }
-    } else if ((pv.L1 & 7) == 0) {  // rows 16-byte aligned (W and S are multiples of 16): 8 entries per load
-      const int w8 = W >> 3;
-      for (int e = threadIdx.x; e < (kAlphabet - 1) * w8; e += blockDim.x) {
-        const int c = e / w8, x = (e - c * w8) << 3;
-        const int64_t g = static_cast<int64_t>(c) * pv.L1 + S + x;
-        uint4 v = make_uint4(0u, 0u, 0u, 0u);
-        if (g + 8 <= pv.prof16_entries) v = *reinterpret_cast<const uint4*>(pv.prof16 + g);
-        const int d = (c * W + x) >> 1;  // entries c*W + x .. + 7: 4 even, 4 odd, 16-byte aligned
-        *reinterpret_cast<uint4*>(even + d) = make_uint4(widen1(v.x & 0xffffu), widen1(v.y & 0xffffu),
-                                                         widen1(v.z & 0xffffu), widen1(v.w & 0xffffu));
-        *reinterpret_cast<uint4*>(odd + d) = make_uint4(widen1(v.x >> 16), widen1(v.y >> 16), widen1(v.z >> 16),
-                                                        widen1(v.w >> 16));
-      }
-      for (int e = rows_entries + threadIdx.x; e < n_entries; e += blockDim.x) ((e & 1) ? odd : even)[e >> 1] = 0u;
-    } else {
-      for (int e = threadIdx.x; e < n_entries; e += blockDim.x) {
-        uint32_t v = 0;
-        if (e < rows_entries) {
-          const int c = e / W, x = e - c * W;
-          const int64_t g = static_cast<int64_t>(c) * pv.L1 + S + x;
-          if (g < pv.prof16_entries) v = widen1(pv.prof16[g]);
-        }
-        ((e & 1) ? odd : even)[e >> 1] = v;
-      }
-    }
-    for (int t = threadIdx.x; t < W + 16; t += blockDim.x) s1l[t] = S + t < pv.L1 ? pv.seq1[S + t] : 0;
+    stage_window_wide(smem, s1l, pv, S, W);
   } else if (Win) {
     // rows' window columns; entries past the global profile read as 0, then the overhang (zeros)
     uint16_t* dst = reinterpret_cast<uint16_t*>(smem);
@@ -527,6 +535,190 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
   }
 }
 
+// Sliding windows: long records on a Seq1 whose widened image does not fit one CU (limits: L1 3000,
+// records up to 2000 letters; int16 profiles past L1 ~ 1500). The 16 waves of a workgroup take 16 records of
+// similar length (plan: records sorted by length, groups of 16) and sweep the SAME offset tile t of each, in
+// lockstep over windows of C steps: for steps [iw, iw + C) every wave reads only columns
+// [o0 + iw, o0 + iw + span + C), so the workgroup stages that window (widened, W = span + C columns), runs the
+// window's 64-step chunks, and slides on. The per-offset state stays in registers across windows; waves
+// whose record ends early (or has fewer tiles) only join the barriers. Items (group, tiles [t0, t1)) are
+// LPT-balanced over the workgroups on the host (HipEngine::plan_waves).
+//   plan16[0 .. n_wg]: workgroup b takes items [plan16[b].li, plan16[b + 1].li);
+//   plan16[items + 2k]     = {group g, t0},  plan16[items + 2k + 1] = {group's longest record, t1};
+//   plan16[members + 16g + w] = {li (-1: none), L2} — wave w's record.
+template <int U>
+__global__ __launch_bounds__(kBlock16) void tile16_slide_kernel(ProblemView pv, BatchView bv,
+                                                                const WaveStart* __restrict__ plan16, int64_t items,
+                                                                int64_t members, const int32_t* __restrict__ long_recs,
+                                                                unsigned long long* __restrict__ keys) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int prof_lds = 2 * pv.prof16_bytes;
+  int8_t* lut8 = reinterpret_cast<int8_t*>(smem + prof_lds);
+  uint8_t* s1l = smem + prof_lds + kProf16Lut8;
+  constexpr int kSpan = kSub * U;
+  const int W = pv.prof16_window;  // window columns: span + C
+  const int C = W - kSpan;         // steps per window (a multiple of 64)
+  for (int t = threadIdx.x; t < kProf16Lut8; t += blockDim.x) lut8[t] = static_cast<int8_t>(pv.lut[t]);
+  const int L1 = pv.L1;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int kib = pv.t16_key_bits;
+  const uint32_t kmask = kib ? (1u << kib) - 1u : 0u;
+  const int64_t base_off = bv.offsets[0];
+  const int k_end = __builtin_amdgcn_readfirstlane(plan16[blockIdx.x + 1].li);
+  for (int k = __builtin_amdgcn_readfirstlane(plan16[blockIdx.x].li); k < k_end; ++k) {  // workgroup-uniform
+    const WaveStart ia = plan16[items + 2 * k], ib = plan16[items + 2 * k + 1];
+    const int g = __builtin_amdgcn_readfirstlane(ia.li), t0 = __builtin_amdgcn_readfirstlane(ia.t);
+    const int lmax = __builtin_amdgcn_readfirstlane(ib.li), t1 = __builtin_amdgcn_readfirstlane(ib.t);
+    const WaveStart mem = plan16[members + 16 * static_cast<int64_t>(g) + wave];
+    const int li = __builtin_amdgcn_readfirstlane(mem.li);
+    const int L2 = __builtin_amdgcn_readfirstlane(mem.t);
+    const int r = li < 0 ? 0 : long_recs ? __builtin_amdgcn_readfirstlane(long_recs[li]) : li;
+    const uint8_t* rec = bv.codes + (bv.offsets[r] - base_off);
+    const int steps = li >= 0 && L2 <= L1 ? L2 : 0;
+    const int need = L2 <= L1 ? L1 - L2 + 1 : 1;
+    const int own_tiles = steps > 0 ? (need + kSpan - 1) / kSpan : 0;
+    const int last = L1 - L2;
+    const bool v0_at_last = pv.semantics == static_cast<int>(Semantics::Spec) || L2 == L1;
+    auto letter = [&](int i) { return i < steps ? static_cast<int>(rec[i]) : 0; };
+    unsigned long long acc64 = 0;
+    uint32_t acc32 = 0;
+    for (int t = t0; t < t1; ++t) {  // workgroup-uniform
+      const int o0 = t * kSpan;
+      const bool on = t < own_tiles;  // wave-uniform
+      uint32_t acc[U], best[U];
+      int DcA[U], DcB[U], mxA[U], mxB[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        acc[u] = 0;
+        best[u] = kBestInit;
+        DcA[u] = DcB[u] = 0;
+        mxA[u] = mxB[u] = INT32_MIN;
+      }
+      const int oA = min(o0 + kSpan, need);
+      int anchor = 0;
+      int c = letter(lane);
+      for (int iw = 0; iw < lmax; iw += C) {  // workgroup-uniform
+        const int S = o0 + iw;
+        __syncthreads();  // every wave is done with the previous window
+        stage_window_wide(smem, s1l, pv, S, W);
+        __syncthreads();
+        if (!on || iw >= steps) continue;  // wave-uniform: this wave only joins the barriers
+        // lane l of a chunk holds step i0 + l's letter; its entry sits at (c - 1) * W + (i - iw) + the
+        // lane's own offset within the window (o0 - S = -iw), split by parity (iw is even)
+        const unsigned char* lbase = smem - 2 * iw + 4 * lane;
+        auto row_off = [&](int cc, int i) {
+          const int e = max(cc - 1, 0) * W + i;
+          return ((e & 1) ? pv.prof16_bytes : 0) + 4 * (e >> 1);
+        };
+        auto anchor_add = [&](int cc, int i) {
+          if (cc != 0) anchor += pv.prof16_i16 ? pv.lut[cc * kLutStride + s1l[oA - S + i]] : lut8[cc * kLutStride + s1l[oA - S + i]];
+        };
+        auto step = [&](int so, int j, bool key) {
+          const unsigned char* p = lbase + __builtin_amdgcn_readlane(so, j);
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            acc[u] = pk_add(acc[u], *reinterpret_cast<const uint32_t*>(p + 2 * kSub * u));
+            if (key) best[u] = pk_max(best[u], acc[u]);
+          }
+        };
+        auto group = [&](const int (&so16)[4], int j, auto gg) {
+          constexpr int GG = decltype(gg)::value;
+          uint32_t e[GG][U];
+#pragma unroll
+          for (int q = 0; q < GG; ++q) {
+            const unsigned char* p = lbase + row_newbcast(so16[(j + q) >> 4], (j + q) & 15);
+#pragma unroll
+            for (int u = 0; u < U; ++u) e[q][u] = *reinterpret_cast<const uint32_t*>(p + 2 * kSub * u);
+          }
+#pragma unroll
+          for (int q = 0; q < GG; ++q)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              acc[u] = pk_add(acc[u], e[q][u]);
+              best[u] = pk_max(best[u], acc[u]);
+            }
+        };
+        auto flush = [&](bool any_key) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            if (any_key) {
+              mxA[u] = max(mxA[u], DcA[u] + lo16(best[u]));
+              mxB[u] = max(mxB[u], DcB[u] + hi16(best[u]));
+            }
+            DcA[u] += lo16(acc[u]);
+            DcB[u] += hi16(acc[u]);
+            acc[u] = 0;
+            best[u] = kBestInit;
+          }
+        };
+        constexpr int G = U >= 4 ? 4 : 8;
+        const int i_end = min(iw + C, steps);
+        int i0 = iw;
+        for (; i0 + 64 <= i_end && i0 + 64 < steps; i0 += 64) {  // full chunks (the record goes on past them)
+          const int c_next = letter(i0 + 64 + lane);
+          const int so = row_off(c, i0 + lane);
+          anchor_add(c, i0 + lane);
+          int so16[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) so16[q] = __shfl(so, 16 * q + (lane & 15), 64);
+#pragma unroll
+          for (int j = 0; j < 64; j += G) group(so16, j, std::integral_constant<int, G>());
+          flush(true);
+          c = c_next;
+        }
+        if (i0 < i_end) {  // the record's last chunk (1..64 steps) lies in this window
+          const int m = steps - i0;
+          const int so = row_off(c, i0 + lane);
+          anchor_add(c, i0 + lane);
+          int j = 0;
+          for (; j < m - 1; ++j) step(so, j, true);
+          step(so, m - 1, false);
+          flush(m > 1);
+        }
+      }
+      if (!on) continue;
+      // ---- Tot per offset: anchor diagonal oA, then suffix sums of the D totals (valid offsets only)
+      anchor = __builtin_amdgcn_readlane(wave_prefix_sum_dpp(anchor), 63);
+      int carry = anchor;
+#pragma unroll
+      for (int u = U - 1; u >= 0; --u) {
+        const int oa = o0 + kSub * u + 2 * lane;
+        const int ca = oa < oA ? DcA[u] : 0, cb = oa + 1 < oA ? DcB[u] : 0;
+        const int incl = wave_prefix_sum_dpp(ca + cb);
+        const int sub_total = __builtin_amdgcn_readlane(incl, 63);
+        const int totB = carry + (sub_total - incl) + cb;  // Tot_{oa+1}
+        const int totA = totB + ca;                        // Tot_{oa}
+        carry += sub_total;
+        if (kib) {
+          const uint32_t c0 = 0x80000000u + kmask - 2u * static_cast<uint32_t>(oa);
+          const uint32_t kA0 = (static_cast<uint32_t>(totA) << kib) + c0;
+          const uint32_t kA1 = ((static_cast<uint32_t>(mxA[u]) + static_cast<uint32_t>(totB)) << kib) + (c0 - 1u);
+          const uint32_t kB0 = (static_cast<uint32_t>(totB) << kib) + (c0 - 2u);
+          const uint32_t kB1 = ((static_cast<uint32_t>(mxB[u]) + static_cast<uint32_t>(totB - cb)) << kib) + (c0 - 3u);
+          const uint32_t a0 = oa < last || (oa == last && v0_at_last) ? kA0 : 0u;
+          const uint32_t a1 = oa < last && L2 >= 2 ? kA1 : 0u;
+          const uint32_t b0 = oa + 1 < last || (oa + 1 == last && v0_at_last) ? kB0 : 0u;
+          const uint32_t b1 = oa + 1 < last && L2 >= 2 ? kB1 : 0u;
+          acc32 = max(max(acc32, max(a0, a1)), max(b0, b1));
+        } else {
+          acc64 = max_u64(acc64, pass1_candidate(oa, L1, L2, pv.semantics, totA, totB, mxA[u]));
+          acc64 = max_u64(acc64, pass1_candidate(oa + 1, L1, L2, pv.semantics, totB, totB - cb, mxB[u]));
+        }
+      }
+    }
+    if (li < 0 || L2 > L1) continue;  // wave-uniform; no barrier follows in this item
+    if (kib) {
+      const uint32_t kk = wave_max_u32_dpp(acc32);
+      if (lane == 0 && kk != 0u)
+        atomicMax(keys + li, final_key(static_cast<int>(kk >> kib) - (1 << (31 - kib)), kmask - (kk & kmask)));
+    } else {
+      const unsigned long long kk = wave_max_u64(acc64);
+      if (lane == 0 && kk != 0ull) atomicMax(keys + li, kk);
+    }
+  }
+}
+
 int tile16_waves_per_cu(int lds_bytes) {  // lds_bytes: the whole image a workgroup stages
   const int blocks = lds_bytes > 0 ? kProf16MaxLds / lds_bytes : 2;
   return kWavesPerBlock16 * max(1, min(2, blocks));
@@ -554,6 +746,24 @@ void launch16_t(const ProblemView& pv, const BatchView& bv, const Plan& plan, hi
                      stream, pv, bv, plan.starts, plan.n_waves, plan.long_recs, plan.n_long, plan.keys,
                      plan.win_tiles);
 }
+
+template <int U>
+void launch16_slide(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream) {
+  static std::mutex mu;
+  static std::set<int> declared;
+  int dev = 0;
+  MOC_HIP_CHECK(hipGetDevice(&dev));
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    if (declared.insert(dev).second)
+      MOC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&tile16_slide_kernel<U>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, kProf16MaxLds));
+  }
+  const int64_t blocks = plan.n_waves / kWavesPerBlock16;
+  hipLaunchKernelGGL((tile16_slide_kernel<U>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock16),
+                     static_cast<size_t>(tile16_lds_bytes(2 * pv.prof16_bytes, pv.prof16_window)), stream, pv, bv,
+                     plan.starts, plan.slide_items, plan.slide_members, plan.long_recs, plan.keys);
+}
 }  // namespace
 
 void preload_tile16_kernels() {
@@ -563,6 +773,25 @@ void preload_tile16_kernels() {
 
 void launch_tile16_keys(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream,
                         bool mfma_sweep) {
+  if (pv.t16_slide) {
+    // sliding windows: span + 64k columns, widened, every item's group in lockstep (plan_slide)
+    const int span = kSub * plan.u;
+    if (!pv.prof16 || mfma_sweep || !pv.prof16_wide || (plan.u != 2 && plan.u != 4 && plan.u != 8) ||
+        plan.slide_items <= 0 ||
+        plan.slide_members <= plan.slide_items || plan.n_waves % kWavesPerBlock16 ||
+        pv.prof16_window < span + 64 || (pv.prof16_window - span) % 64 ||
+        pv.prof16_bytes != tile16_window_bytes(pv.prof16_window) ||
+        tile16_lds_bytes(2 * pv.prof16_bytes, pv.prof16_window) > kProf16MaxLds)
+      throw Error("launch_tile16_keys: bad sliding-window plan");
+    if (plan.n_long > 0) MOC_HIP_CHECK(hipMemsetAsync(plan.keys, 0, sizeof(unsigned long long) * plan.n_long, stream));
+    if (plan.n_waves <= 0) return;
+    switch (plan.u) {
+      case 2: launch16_slide<2>(pv, bv, plan, stream); break;
+      case 8: launch16_slide<8>(pv, bv, plan, stream); break;
+      default: launch16_slide<4>(pv, bv, plan, stream); break;
+    }
+    return;
+  }
   const int64_t s1_len = pv.prof16_window > 0 ? pv.prof16_window : pv.L1;
   const bool wide = pv.prof16_wide && !mfma_sweep;
   if (pv.prof16_i16 && !wide) throw Error("launch_tile16_keys: an int16 profile runs the widened image only");

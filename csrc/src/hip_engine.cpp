@@ -7,6 +7,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <future>
+#include <queue>
 #include <string>
 
 #include "moc/problem.hpp"
@@ -162,6 +163,7 @@ HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
   // MOC_TILE16_WINWIDE=0: short records on an L1 ~ 1500..3050 problem keep the whole byte-pair image (A/B)
   if (const char* ww = std::getenv("MOC_TILE16_WINWIDE")) tile16_window_wide_ = std::atoi(ww) != 0;
   if (const char* w8 = std::getenv("MOC_TILE16_WIN_U8")) short_window_u8_ = std::atoi(w8) != 0;
+  if (const char* sl = std::getenv("MOC_TILE16_SLIDE")) tile16_slide_ = std::atoi(sl) != 0;
   if (const char* w = std::getenv("MOC_TILE_WAVES_PER_CU")) {
     const int v = std::atoi(w);
     if (v >= 1 && v <= 32) tile_waves_per_cu_ = v;
@@ -468,6 +470,8 @@ struct PlanLayout {
 
 // Per-tile fixed cost in step units (record/tile setup, the wave reduction), for load balancing.
 constexpr int64_t kTileOverheadSteps = 24;
+// Staging one sliding window (tile16_slide_kernel), per wave, in step units.
+constexpr int64_t kSlideStageSteps = 96;
 }  // namespace
 
 // Device view of an uploaded plan buffer (starts | long_recs | keys). Identity record lists upload no
@@ -479,13 +483,119 @@ dev::Plan HipEngine::device_plan(void* d_plan, size_t n_starts, bool has_long_re
   dev::Plan plan;
   plan.u = tp.u;
   plan.win_tiles = tp.win_tiles;
-  plan.n_waves = static_cast<int64_t>(n_starts) - 1;
+  plan.n_waves = tp.slide ? tp.slide_wgs * dev::kTile16WavesPerBlock : static_cast<int64_t>(n_starts) - 1;
+  plan.slide_items = tp.slide_items;
+  plan.slide_members = tp.slide_members;
   plan.starts = reinterpret_cast<const dev::WaveStart*>(base + lay.starts_off);
   plan.long_recs = has_long_recs ? reinterpret_cast<const int32_t*>(base + lay.long_off) : nullptr;
   plan.n_long = n_long;
   plan.keys = reinterpret_cast<unsigned long long*>(base + lay.keys_off);
   plan.r2 = r2_;
   return plan;
+}
+
+// Sliding-window plan (tile16_slide_kernel): the long records sorted by length (longest first) in groups of 16,
+// one per wave of a workgroup; a group's tiles split into items of at most half a workgroup's share, the
+// items assigned largest first to the least-loaded workgroup (one 16-wave workgroup per CU: the window takes
+// most of the LDS). Encoding in `starts` (dev::Plan::slide_items / slide_members). False: no window fits.
+bool HipEngine::plan_slide(const int64_t* offsets, const int32_t* long_recs, int64_t n_long, TilePlan& tp,
+                           std::vector<dev::WaveStart>& starts) const {
+  // 4 sub-tiles by default: limits 14.9 (U = 2) -> 16.7 T cells/s, the int16 profile on limits' lengths
+  // 10.6 -> 13.8 (profiles/tile16_r5/README.txt)
+  const int u = tile_u_ == 2 || tile_u_ == 8 ? tile_u_ : 4;
+  const int span = dev::tile_span(true, u);
+  const int64_t C = (dev::tile16_max_window(true) - span) / 64 * 64;  // steps per window
+  if (C < 64) return false;
+  constexpr int G = dev::kTile16WavesPerBlock;
+  std::vector<int32_t> order(static_cast<size_t>(n_long));
+  std::vector<int32_t> steps(static_cast<size_t>(n_long));
+  for (int64_t li = 0; li < n_long; ++li) {
+    const int64_t r = long_recs ? long_recs[li] : li;
+    const int64_t L2 = offsets[r + 1] - offsets[r];
+    order[li] = static_cast<int32_t>(li);
+    steps[li] = static_cast<int32_t>(L2 <= L1_ ? L2 : 0);
+  }
+  std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return steps[a] > steps[b]; });
+  const int64_t n_groups = (n_long + G - 1) / G;
+  struct Item {
+    int64_t cost;
+    int32_t g, t0, t1;
+  };
+  std::vector<Item> items;
+  std::vector<int32_t> glmax(static_cast<size_t>(n_groups), 0);
+  int64_t total = 0;
+  std::vector<int64_t> gcost(static_cast<size_t>(n_groups), 0);
+  std::vector<int32_t> gtiles(static_cast<size_t>(n_groups), 0);
+  for (int64_t g = 0; g < n_groups; ++g) {
+    int32_t lmax = 0, nt = 0;
+    for (int64_t k = g * G; k < std::min<int64_t>(n_long, (g + 1) * G); ++k) {
+      const int32_t st = steps[order[k]];
+      if (st <= 0) continue;
+      lmax = std::max(lmax, st);
+      nt = std::max<int32_t>(nt, static_cast<int32_t>(dev::tiles_of(L1_ - st + 1, span)));
+    }
+    glmax[g] = lmax;
+    gtiles[g] = nt;
+    // a tile: every wave in lockstep for the group's longest record, plus the staging of each window
+    gcost[g] = G * (lmax + kTileOverheadSteps + kSlideStageSteps * ((lmax + C - 1) / C));
+    total += gcost[g] * nt;
+  }
+  if (total <= 0) return false;
+  int64_t all_tiles = 0;
+  for (int64_t g = 0; g < n_groups; ++g) all_tiles += gtiles[g];
+  const int64_t n_wg = std::min<int64_t>(num_cus_, all_tiles);
+  const double share = static_cast<double>(total) / static_cast<double>(n_wg);
+  for (int64_t g = 0; g < n_groups; ++g) {
+    if (gtiles[g] <= 0) continue;
+    const int32_t per = static_cast<int32_t>(std::max<int64_t>(1, static_cast<int64_t>(share / 2) / gcost[g]));
+    for (int32_t t0 = 0; t0 < gtiles[g]; t0 += per) {
+      const int32_t t1 = std::min(gtiles[g], t0 + per);
+      items.push_back(Item{gcost[g] * (t1 - t0), static_cast<int32_t>(g), t0, t1});
+    }
+  }
+  std::stable_sort(items.begin(), items.end(), [](const Item& a, const Item& b) { return a.cost > b.cost; });
+  std::vector<std::vector<int32_t>> of(static_cast<size_t>(n_wg));
+  std::priority_queue<std::pair<int64_t, int64_t>, std::vector<std::pair<int64_t, int64_t>>, std::greater<>> load;
+  for (int64_t b = 0; b < n_wg; ++b) load.emplace(0, b);
+  for (size_t k = 0; k < items.size(); ++k) {
+    auto [l, b] = load.top();
+    load.pop();
+    of[static_cast<size_t>(b)].push_back(static_cast<int32_t>(k));
+    load.emplace(l + items[k].cost, b);
+  }
+  starts.clear();
+  starts.reserve(static_cast<size_t>(n_wg + 1 + 2 * static_cast<int64_t>(items.size()) + n_groups * G));
+  int32_t n_it = 0;
+  for (int64_t b = 0; b < n_wg; ++b) {
+    starts.push_back(dev::WaveStart{n_it, 0});
+    n_it += static_cast<int32_t>(of[b].size());
+  }
+  starts.push_back(dev::WaveStart{n_it, 0});
+  tp.slide_items = static_cast<int64_t>(starts.size());
+  for (int64_t b = 0; b < n_wg; ++b)
+    for (const int32_t k : of[b]) {
+      const Item& it = items[k];
+      starts.push_back(dev::WaveStart{it.g, it.t0});
+      starts.push_back(dev::WaveStart{glmax[it.g], it.t1});
+    }
+  tp.slide_members = static_cast<int64_t>(starts.size());
+  for (int64_t k = 0; k < n_groups * G; ++k) {
+    if (k < n_long) {
+      const int32_t li = order[k];
+      const int64_t r = long_recs ? long_recs[li] : li;
+      starts.push_back(dev::WaveStart{li, static_cast<int32_t>(offsets[r + 1] - offsets[r])});
+    } else {
+      starts.push_back(dev::WaveStart{-1, 0});
+    }
+  }
+  tp.slide_wgs = n_wg;
+  tp.tile16 = true;
+  tp.wide = true;
+  tp.slide = true;
+  tp.u = u;
+  tp.window = span + C;
+  tp.win_tiles = 0;
+  return true;
 }
 
 // Cost-balanced contiguous wave runs over the record-major tile list of the long records (record li =
@@ -519,6 +629,11 @@ std::vector<dev::WaveStart> HipEngine::plan_waves(const int64_t* offsets, const 
     W = dev::tile16_max_window(true);
     wide = true;
   }
+  // records too long for a widened window on a Seq1 whose widened image exceeds the LDS (limits: L1 3000,
+  // records up to 2000 letters; int16 profiles past L1 ~ 1500): sliding widened windows
+  if (W == 0 && !wide && d_prof16_ && !mfma_ && tile16_slide_ && parts == 1 &&
+      (tile_u_ <= 0 || tile_u_ == 2 || tile_u_ == 4 || tile_u_ == 8))
+    if (plan_slide(offsets, long_recs, n_long, tp, starts)) return starts;
   tp.window = W;
   tp.wide = wide;
   tp.tile16 = d_prof16_ != nullptr && (W == 0 || max_l2 + 2 * 128 <= W) && (wide || !prof16_i16_);
@@ -1149,7 +1264,11 @@ void HipEngine::search_keys_device(const uint8_t* d_codes, const int64_t* d_offs
   dev::Plan plan;
   plan.u = tp.u;
   plan.win_tiles = tp.win_tiles;
-  plan.n_waves = starts.empty() ? 0 : static_cast<int64_t>(starts.size()) - 1;
+  plan.n_waves = starts.empty() ? 0
+                 : tp.slide   ? tp.slide_wgs * dev::kTile16WavesPerBlock
+                              : static_cast<int64_t>(starts.size()) - 1;
+  plan.slide_items = tp.slide_items;
+  plan.slide_members = tp.slide_members;
   plan.starts = static_cast<const dev::WaveStart*>(d_plan_);
   plan.long_recs = nullptr;
   plan.n_long = n;

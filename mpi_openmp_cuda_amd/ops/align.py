@@ -341,7 +341,7 @@ class HipSearchEngine:
 # Arithmetic forms of the kernels (csrc/include/moc/kernel_bounds.hpp FormBits), as stats()["forms"] names them.
 FORM_NAMES = ((1, "swipe_kbits"), (2, "swipe_rk"), (4, "short_pk"), (8, "short_key32"), (16, "short_key64"),
               (32, "tile16"), (64, "tiles_key32"), (128, "tiles_key64"), (256, "mfma"), (512, "tile16_key32"),
-              (1024, "tile16_i16"))
+              (1024, "tile16_i16"), (2048, "tile16_slide"))
 
 
 def kernel_bounds(weights, L1: int, min_l2: int, max_l2: int) -> dict:

@@ -38,11 +38,17 @@ SHAPES = {
     # long records under weights past the int8 difference profile (W1 + max(W2, W3, W4) > 127)
     "heavy3": Shape((200, 10, 10, 10), 1489, 56, 1152),
     "heavy4": Shape((120, 20, 1, 1), 2976, 5, 82),
+    "heavylim": Shape((200, 10, 10, 10), 3000, 1, 2000),  # limits' lengths, int16 profile (sliding windows)
+    "mid3k": Shape((10, 2, 3, 4), 2000, 400, 900),  # L1 past the widened image, records past a widened window
 }
 
 
 def make_synthetic(shape: str = "input6", n_records: int = 1000, seed: int = 0) -> Problem:
-    s = SHAPES[shape]
+    return make_shape(SHAPES[shape], n_records, seed)
+
+
+def make_shape(s: Shape, n_records: int = 1000, seed: int = 0) -> Problem:
+    """Random Seq1 of s.L1 letters and n_records records of s.l2_min..s.l2_max random letters."""
     rng = np.random.default_rng(seed)
     seq1 = rng.integers(1, 27, size=s.L1, dtype=np.uint8)
     lengths = rng.integers(s.l2_min, s.l2_max + 1, size=n_records, dtype=np.int64)

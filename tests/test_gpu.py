@@ -834,6 +834,39 @@ def test_tile16_window_wide(engine, L1):
         assert engine.stats()["kernels"] == ["tile16"], engine.stats()
 
 
+@pytest.mark.parametrize("L1,lo,hi", [(2000, 400, 900), (2001, 600, 1200), (3000, 1, 2000), (1600, 1100, 1500)])
+def test_tile16_slide(engine, L1, lo, hi):
+    # long records on a Seq1 whose widened image does not fit one CU: sliding widened windows
+    # (tile16_slide_kernel; L1 2001 takes the unaligned staging loop; groups of 16 with empty members when
+    # the count is not a multiple of 16), == the CPU engine, both semantics
+    from mpi_openmp_cuda_amd.utils.synthetic import Shape, make_shape
+
+    prob = make_shape(Shape((10, 2, 3, 4), L1, lo, hi), 301, seed=L1 + lo)
+    for sem in (Semantics.REFERENCE, Semantics.SPEC):
+        engine.set_problem(prob.weights, prob.seq1, sem)
+        got = engine.solve(prob.codes, prob.offsets)
+        st = engine.stats()
+        assert st["kernels"] == ["tile16"] and "tile16_slide" in st["forms"], st
+        assert np.array_equal(as_triples(got), as_triples(search_cpu(prob, sem)))
+
+
+def test_tile16_slide_sub_tiles_and_previous_plan(monkeypatch):
+    # the U = 2 and U = 8 slide kernels (MOC_TILE_U; default 4) and the plan without sliding windows
+    # (MOC_TILE16_SLIDE=0: the whole byte-pair image) give the same results as the CPU engine
+    from mpi_openmp_cuda_amd.utils.synthetic import Shape, make_shape
+
+    prob = make_shape(Shape((10, 2, 3, 4), 2500, 700, 1700), 100, seed=5)
+    ref = as_triples(search_cpu(prob))
+    for env, form in (({"MOC_TILE_U": "2"}, True), ({"MOC_TILE_U": "8"}, True), ({"MOC_TILE16_SLIDE": "0"}, False)):
+        with monkeypatch.context() as m:
+            for k, v in env.items():
+                m.setenv(k, v)
+            eng = HipSearchEngine(device=0)
+            eng.set_problem(prob.weights, prob.seq1)
+            assert np.array_equal(as_triples(eng.solve(prob.codes, prob.offsets)), ref), env
+            assert ("tile16_slide" in eng.stats()["forms"]) == form, (env, eng.stats())
+
+
 @pytest.mark.parametrize("w,forms", [((63, 0, 0, 64), ["tile16", "tile16_key32"]),
                                      ((64, 0, 0, 64), ["tile16", "tile16_key32", "tile16_i16"]),
                                      ((256, 0, 0, 256), ["tiles_key32"])])
@@ -1074,14 +1107,18 @@ EXTREMES = [
     ("short_key32_past", 200, 150, 190, (22076, 0, 0, 22076), ["short"], ["short_key64"]),
     ("tile16_at", 600, 150, 400, (63, 0, 0, 64), ["tile16"], ["tile16", "tile16_key32"]),
     # tile16's 32-bit selection keys: 127 * 2064 < 2^18 (L1 2600: 13 index bits), 127 * 2065 is not
-    ("tile16_key32_at", 2600, 2000, 2064, (127, 0, 0, 0), ["tile16"], ["tile16", "tile16_key32"]),
-    ("tile16_key32_past", 2600, 2000, 2065, (127, 0, 0, 0), ["tile16"], ["tile16"]),
+    # (records past a widened window on a Seq1 past the widened image: sliding windows)
+    ("tile16_key32_at", 2600, 2000, 2064, (127, 0, 0, 0), ["tile16"], ["tile16", "tile16_key32", "tile16_slide"]),
+    ("tile16_key32_past", 2600, 2000, 2065, (127, 0, 0, 0), ["tile16"], ["tile16", "tile16_slide"]),
     # the int16 profile (widened images only): |Dt| = W1 + W4 = 511 at the bound, 512 past it
     ("tile16_i16_at", 600, 150, 400, (255, 0, 0, 256), ["tile16"], ["tile16", "tile16_key32", "tile16_i16"]),
     ("tile16_i16_past", 600, 150, 400, (256, 0, 0, 256), ["tiles"], ["tiles_key32"]),
     ("tile16_i16_window", 2400, 40, 90, (255, 0, 0, 256), ["tile16"], ["tile16", "tile16_key32", "tile16_i16"]),
-    # no widened image holds it (L1 2400, records to 1200 letters): the LUT tile kernel
-    ("tile16_i16_long", 2400, 1000, 1200, (255, 0, 0, 256), ["tiles"], ["tiles_key32"]),
+    # no widened image or window holds it (L1 2400, records to 1200 letters): sliding widened windows
+    ("tile16_i16_long", 2400, 1000, 1200, (255, 0, 0, 256), ["tile16"], ["tile16", "tile16_i16", "tile16_slide"]),
+    ("tile16_slide_at", 2400, 900, 1400, (63, 0, 0, 64), ["tile16"], ["tile16", "tile16_key32", "tile16_slide"]),
+    ("tile16_slide_i16", 2400, 900, 1400, (64, 0, 0, 64), ["tile16"],
+     ["tile16", "tile16_key32", "tile16_i16", "tile16_slide"]),
     ("tile16_past", 600, 150, 400, (64, 0, 0, 64), ["tile16"], ["tile16", "tile16_key32", "tile16_i16"]),
     ("tiles_key32_at", 600, 150, 400, (5242, 0, 0, 5242), ["tiles"], ["tiles_key32"]),
     ("tiles_key32_past", 600, 150, 400, (5243, 0, 0, 5243), ["tiles"], ["tiles_key64"]),

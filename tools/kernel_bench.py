@@ -29,7 +29,7 @@ from mpi_openmp_cuda_amd.ops.align import as_triples  # noqa: E402
 # shape -> (records, Seq1 override length or None)
 CASES = {"input6": (1 << 24, None), "input1": (1 << 21, None), "mid": (1 << 20, None), "heavy6": (1 << 22, None),
          "input4": (1 << 17, None), "heavy3": (1 << 13, None), "heavy4": (1 << 15, None),
-         "input3": (1 << 15, None), "limits": (1 << 12, None),
+         "input3": (1 << 15, None), "limits": (1 << 12, None), "heavylim": (1 << 12, None), "mid3k": (1 << 13, None),
          # long context: Seq1 beyond one LDS image -> the windowed tile16 sweep
          "long20k": (1 << 12, 20_000), "long150k": (1 << 9, 150_000)}
 BASE = {"long20k": "input3", "long150k": "input3"}  # record-length distribution of the long-context shapes
