@@ -160,7 +160,7 @@ class HipEngine {
   };
   std::vector<dev::WaveStart> plan_waves(const int64_t* offsets, const int32_t* long_recs, int64_t n_long, int part,
                                          int parts, TilePlan& tp) const;
-  bool plan_slide(const int64_t* offsets, const int32_t* long_recs, int64_t n_long, TilePlan& tp,
+  bool plan_slide(const int64_t* offsets, const int32_t* long_recs, int64_t n_long, double min_fill, TilePlan& tp,
                   std::vector<dev::WaveStart>& starts) const;
   dev::Plan device_plan(void* d_plan, size_t n_starts, bool has_long_recs, int64_t n_long, const TilePlan& tp) const;
   // problem view for a plan: without the profile when the plan is for the LUT tile kernel

@@ -162,7 +162,33 @@ __device__ __forceinline__ void stage_window_wide(unsigned char* smem, uint8_t* 
     return (static_cast<uint32_t>(static_cast<int8_t>(e & 0xffu)) & 0xffffu) |
            (static_cast<uint32_t>(static_cast<int8_t>((e >> 8) & 0xffu)) << 16);
   };
-  if (pv.prof16_i16) {  // int16 Dt per entry: the pair of window entry (c, x) is global (g, g + 1)
+  if (pv.prof16_i16 && (pv.L1 & 7) == 0) {
+    // int16 Dt per entry, rows 16-byte aligned: 8 entries per load — the even pairs are its dwords, the odd
+    // ones straddle them and the next load's first value
+    const int w8 = W >> 3;
+    for (int e = threadIdx.x; e < (kAlphabet - 1) * w8; e += blockDim.x) {
+      const int c = e / w8, x = (e - c * w8) << 3;
+      const int64_t g = static_cast<int64_t>(c) * pv.L1 + S + x;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      uint32_t nx = 0u;
+      if (g + 9 <= pv.prof16_entries) {
+        v = *reinterpret_cast<const uint4*>(pv.prof16 + g);
+        nx = pv.prof16[g + 8];
+      } else {
+        uint32_t h[9];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) h[q] = g + q < pv.prof16_entries ? pv.prof16[g + q] : 0u;
+        v = make_uint4(h[0] | h[1] << 16, h[2] | h[3] << 16, h[4] | h[5] << 16, h[6] | h[7] << 16);
+        nx = h[8];
+      }
+      const int d = (c * W + x) >> 1;
+      *reinterpret_cast<uint4*>(even + d) = v;
+      *reinterpret_cast<uint4*>(odd + d) =
+          make_uint4(__builtin_amdgcn_alignbit(v.y, v.x, 16), __builtin_amdgcn_alignbit(v.z, v.y, 16),
+                     __builtin_amdgcn_alignbit(v.w, v.z, 16), __builtin_amdgcn_alignbit(nx, v.w, 16));
+    }
+    for (int e = rows_entries + threadIdx.x; e < n_entries; e += blockDim.x) ((e & 1) ? odd : even)[e >> 1] = 0u;
+  } else if (pv.prof16_i16) {  // int16 Dt per entry: the pair of window entry (c, x) is global (g, g + 1)
     for (int e = threadIdx.x; e < n_entries; e += blockDim.x) {
       uint32_t v = 0;
       if (e < rows_entries) {

@@ -497,9 +497,11 @@ dev::Plan HipEngine::device_plan(void* d_plan, size_t n_starts, bool has_long_re
 // Sliding-window plan (tile16_slide_kernel): the long records sorted by length (longest first) in groups of 16,
 // one per wave of a workgroup; a group's tiles split into items of at most half a workgroup's share, the
 // items assigned largest first to the least-loaded workgroup (one 16-wave workgroup per CU: the window takes
-// most of the LDS). Encoding in `starts` (dev::Plan::slide_items / slide_members). False: no window fits.
-bool HipEngine::plan_slide(const int64_t* offsets, const int32_t* long_recs, int64_t n_long, TilePlan& tp,
-                           std::vector<dev::WaveStart>& starts) const {
+// most of the LDS). Encoding in `starts` (dev::Plan::slide_items / slide_members). False: no window fits, or
+// the groups would run less than min_fill of their waves (a few huge records: the other plans give every wave
+// a tile of its own; an int16 profile's other plan is the LUT tile kernel, so it takes emptier groups).
+bool HipEngine::plan_slide(const int64_t* offsets, const int32_t* long_recs, int64_t n_long, double min_fill,
+                           TilePlan& tp, std::vector<dev::WaveStart>& starts) const {
   // 4 sub-tiles by default: limits 14.9 (U = 2) -> 16.7 T cells/s, the int16 profile on limits' lengths
   // 10.6 -> 13.8 (profiles/tile16_r5/README.txt)
   const int u = tile_u_ == 2 || tile_u_ == 8 ? tile_u_ : 4;
@@ -507,6 +509,7 @@ bool HipEngine::plan_slide(const int64_t* offsets, const int32_t* long_recs, int
   const int64_t C = (dev::tile16_max_window(true) - span) / 64 * 64;  // steps per window
   if (C < 64) return false;
   constexpr int G = dev::kTile16WavesPerBlock;
+  if (static_cast<double>(n_long) < min_fill * static_cast<double>(G * ((n_long + G - 1) / G))) return false;
   std::vector<int32_t> order(static_cast<size_t>(n_long));
   std::vector<int32_t> steps(static_cast<size_t>(n_long));
   for (int64_t li = 0; li < n_long; ++li) {
@@ -629,11 +632,14 @@ std::vector<dev::WaveStart> HipEngine::plan_waves(const int64_t* offsets, const 
     W = dev::tile16_max_window(true);
     wide = true;
   }
-  // records too long for a widened window on a Seq1 whose widened image exceeds the LDS (limits: L1 3000,
-  // records up to 2000 letters; int16 profiles past L1 ~ 1500): sliding widened windows
-  if (W == 0 && !wide && d_prof16_ && !mfma_ && tile16_slide_ && parts == 1 &&
+  // records too long for a widened window on a Seq1 whose widened image exceeds the LDS — with the byte pairs
+  // whole (limits: L1 3000, records up to 2000 letters), as windows (L1 past ~3050), or an int16 profile:
+  // sliding widened windows (limits 12.9 -> 16.8 T cells/s, L1 20 000 with input3's records 17.3 -> 20.7,
+  // L1 150 000 9.6 -> 15.9; profiles/tile16_r5/README.txt)
+  if ((W == 0 || max_l2 + 2 * 128 * 4 > dev::tile16_max_window(true)) && !wide && d_prof16_ && !mfma_ &&
+      tile16_slide_ && parts == 1 &&
       (tile_u_ <= 0 || tile_u_ == 2 || tile_u_ == 4 || tile_u_ == 8))
-    if (plan_slide(offsets, long_recs, n_long, tp, starts)) return starts;
+    if (plan_slide(offsets, long_recs, n_long, prof16_i16_ ? 0.25 : 0.8, tp, starts)) return starts;
   tp.window = W;
   tp.wide = wide;
   tp.tile16 = d_prof16_ != nullptr && (W == 0 || max_l2 + 2 * 128 <= W) && (wide || !prof16_i16_);

@@ -850,6 +850,22 @@ def test_tile16_slide(engine, L1, lo, hi):
         assert np.array_equal(as_triples(got), as_triples(search_cpu(prob, sem)))
 
 
+@pytest.mark.parametrize("n,w,slide", [(5, (10, 2, 3, 4), False), (5, (200, 10, 10, 10), True),
+                                        (40, (10, 2, 3, 4), True), (36, (10, 2, 3, 4), False)])
+def test_tile16_slide_group_fill(engine, n, w, slide):
+    # sliding windows need groups of 16 similar records: with fewer than 0.8 of the groups' waves filled the
+    # byte-pair image keeps every wave on a tile of its own; an int16 profile (whose other plan is the LUT
+    # tile kernel) slides from a quarter filled
+    from mpi_openmp_cuda_amd.utils.synthetic import Shape, make_shape
+
+    prob = make_shape(Shape(w, 2400, 1100, 1400), n, seed=n)
+    engine.set_problem(prob.weights, prob.seq1)
+    got = engine.solve(prob.codes, prob.offsets)
+    st = engine.stats()
+    assert st["kernels"] == ["tile16"] and ("tile16_slide" in st["forms"]) == slide, st
+    assert np.array_equal(as_triples(got), as_triples(search_cpu(prob)))
+
+
 def test_tile16_slide_sub_tiles_and_previous_plan(monkeypatch):
     # the U = 2 and U = 8 slide kernels (MOC_TILE_U; default 4) and the plan without sliding windows
     # (MOC_TILE16_SLIDE=0: the whole byte-pair image) give the same results as the CPU engine
