@@ -30,9 +30,12 @@ ROWS = [  # shape, kernel_bench variant, kernel name prefix, form, PMC pass (too
     ("input1", "wire", "swipe_direct_kernel<24, 16, 2, true>", "device P33 wire", "p4"),
     ("mid", "tile16", "swipe_direct_kernel<64, 24, 0, true>", "device bytes, 24 record words", "p1"),
     ("input3", "tile16", "tile16_search_kernel<2, false, true>", "widened pairs", "p2"),
-    ("limits", "tile16", "tile16_search_kernel<2, false, false>", "byte pairs", "p2"),
+    ("limits", "tile16", "tile16_search_kernel<2, false, false>", "byte pairs (before sliding windows)", "p2"),
+    ("limits", "slide", "tile16_slide_kernel<4>", "sliding widened windows", "p6"),
     ("input4", "tile16", "tile16_search_kernel<8, true, true>", "widened windows", "p3"),
-    ("long20k", "tile16", "tile16_search_kernel<4, true, false>", "byte-pair windows", "p3"),
+    ("long20k", "tile16", "tile16_search_kernel<4, true, false>", "byte-pair windows (before sliding windows)", "p3"),
+    ("long20k", "slide", "tile16_slide_kernel<4>", "sliding widened windows", "p7"),
+    ("heavylim", "slide", "tile16_slide_kernel<4>", "int16 profile, sliding widened windows", "p8"),
     ("heavy3", "tile16", "tile16_search_kernel<2, false, true>", "int16 profile", "p5"),
     ("heavy4", "tile16", "tile16_search_kernel<8, true, true>", "int16 profile, windows", "p5"),
 ]
