@@ -72,7 +72,8 @@ struct ProblemView {
   // 1: prof16 holds one int16 Dt per entry (weights past the byte pairs, bounds::profile16_i16_exact), staged
   // into widened images only
   int32_t prof16_i16 = 0;
-  int32_t t16_slide = 0;               // tile16: sliding widened windows of prof16_window columns
+  int32_t t16_slide = 0;               // tile16: sliding widened windows of prof16_window columns (2: the
+                                       // two-workgroups-per-CU instance)
                                        // (tile16_slide_kernel; the plan's items and groups)
 };
 

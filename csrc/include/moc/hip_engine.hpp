@@ -157,6 +157,7 @@ class HipEngine {
     bool wide = false;      // tile16: widened int16-pair entries
     bool slide = false;     // tile16: sliding widened windows (window = their columns; dev::Plan::slide_*)
     int64_t slide_items = 0, slide_members = 0, slide_wgs = 0;
+    int slide_per_cu = 1;  // workgroups per CU the slide plan is for (1, or 2 with half-LDS windows)
   };
   std::vector<dev::WaveStart> plan_waves(const int64_t* offsets, const int32_t* long_recs, int64_t n_long, int part,
                                          int parts, TilePlan& tp) const;
@@ -173,7 +174,7 @@ class HipEngine {
       pv.prof16_window = static_cast<int32_t>(tp.window);
       pv.prof16_bytes = tp.window ? static_cast<int32_t>(dev::tile16_window_bytes(tp.window)) : prof16_bytes_;
       pv.prof16_wide = tp.wide ? 1 : 0;
-      pv.t16_slide = tp.slide ? 1 : 0;
+      pv.t16_slide = tp.slide ? tp.slide_per_cu : 0;
       if (tp.window) pv.mfma_sweep = 0;
       if (!pv.mfma_sweep) pv.t16_key_bits = bounds::tile16_key32_bits(L1_, table_.max_abs(), max_l2);
     }
@@ -196,6 +197,7 @@ class HipEngine {
   bool tile16_window_wide_ = true;  // widened windows for short records where the widened whole image is too big
   bool short_window_u8_ = true;     // ... with 8 sub-tiles per wave tile (MOC_TILE16_WIN_U8=0: 4)
   bool tile16_slide_ = true;        // long records past the widened image: sliding windows (MOC_TILE16_SLIDE=0: not)
+  int slide_wgs_per_cu_ = 2;        // ... two workgroups per CU, half-LDS windows (MOC_TILE16_SLIDE_WG=1: one)
   int tile_waves_per_cu_ = 32;  // tile-kernel waves per CU (MOC_TILE_WAVES_PER_CU)
   hipStream_t s_copy_ = nullptr, s_compute_ = nullptr, s_return_ = nullptr;  // copy / return: made on first use
   void ensure_side_streams();

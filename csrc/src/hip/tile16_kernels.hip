@@ -572,8 +572,9 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
 //   plan16[0 .. n_wg]: workgroup b takes items [plan16[b].li, plan16[b + 1].li);
 //   plan16[items + 2k]     = {group g, t0},  plan16[items + 2k + 1] = {group's longest record, t1};
 //   plan16[members + 16g + w] = {li (-1: none), L2} — wave w's record.
-template <int U>
-__global__ __launch_bounds__(kBlock16) void tile16_slide_kernel(ProblemView pv, BatchView bv,
+template <int U, int WavesPerSimd>
+__global__ __launch_bounds__(kBlock16) __attribute__((amdgpu_waves_per_eu(WavesPerSimd)))
+void tile16_slide_kernel(ProblemView pv, BatchView bv,
                                                                 const WaveStart* __restrict__ plan16, int64_t items,
                                                                 int64_t members, const int32_t* __restrict__ long_recs,
                                                                 unsigned long long* __restrict__ keys) {
@@ -773,7 +774,7 @@ void launch16_t(const ProblemView& pv, const BatchView& bv, const Plan& plan, hi
                      plan.win_tiles);
 }
 
-template <int U>
+template <int U, int WavesPerSimd>
 void launch16_slide(const ProblemView& pv, const BatchView& bv, const Plan& plan, hipStream_t stream) {
   static std::mutex mu;
   static std::set<int> declared;
@@ -782,11 +783,11 @@ void launch16_slide(const ProblemView& pv, const BatchView& bv, const Plan& plan
   {
     std::lock_guard<std::mutex> lock(mu);
     if (declared.insert(dev).second)
-      MOC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&tile16_slide_kernel<U>),
+      MOC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&tile16_slide_kernel<U, WavesPerSimd>),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, kProf16MaxLds));
   }
   const int64_t blocks = plan.n_waves / kWavesPerBlock16;
-  hipLaunchKernelGGL((tile16_slide_kernel<U>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock16),
+  hipLaunchKernelGGL((tile16_slide_kernel<U, WavesPerSimd>), dim3(static_cast<unsigned>(blocks)), dim3(kBlock16),
                      static_cast<size_t>(tile16_lds_bytes(2 * pv.prof16_bytes, pv.prof16_window)), stream, pv, bv,
                      plan.starts, plan.slide_items, plan.slide_members, plan.long_recs, plan.keys);
 }
@@ -802,7 +803,7 @@ void launch_tile16_keys(const ProblemView& pv, const BatchView& bv, const Plan& 
   if (pv.t16_slide) {
     // sliding windows: span + 64k columns, widened, every item's group in lockstep (plan_slide)
     const int span = kSub * plan.u;
-    if (!pv.prof16 || mfma_sweep || !pv.prof16_wide || (plan.u != 2 && plan.u != 4 && plan.u != 8) ||
+    if (!pv.prof16 || mfma_sweep || !pv.prof16_wide || (plan.u != 2 && plan.u != 4 && plan.u != 8) || (pv.t16_slide == 2 && plan.u == 8) ||
         plan.slide_items <= 0 ||
         plan.slide_members <= plan.slide_items || plan.n_waves % kWavesPerBlock16 ||
         pv.prof16_window < span + 64 || (pv.prof16_window - span) % 64 ||
@@ -811,10 +812,17 @@ void launch_tile16_keys(const ProblemView& pv, const BatchView& bv, const Plan& 
       throw Error("launch_tile16_keys: bad sliding-window plan");
     if (plan.n_long > 0) MOC_HIP_CHECK(hipMemsetAsync(plan.keys, 0, sizeof(unsigned long long) * plan.n_long, stream));
     if (plan.n_waves <= 0) return;
-    switch (plan.u) {
-      case 2: launch16_slide<2>(pv, bv, plan, stream); break;
-      case 8: launch16_slide<8>(pv, bv, plan, stream); break;
-      default: launch16_slide<4>(pv, bv, plan, stream); break;
+    if (pv.t16_slide == 2) {  // two workgroups per CU: 8 waves per SIMD, 64 VGPRs
+      if (plan.u == 2)
+        launch16_slide<2, 8>(pv, bv, plan, stream);
+      else
+        launch16_slide<4, 8>(pv, bv, plan, stream);
+    } else {
+      switch (plan.u) {
+        case 2: launch16_slide<2, 4>(pv, bv, plan, stream); break;
+        case 8: launch16_slide<8, 4>(pv, bv, plan, stream); break;
+        default: launch16_slide<4, 4>(pv, bv, plan, stream); break;
+      }
     }
     return;
   }

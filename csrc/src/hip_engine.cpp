@@ -164,6 +164,7 @@ HipEngine::HipEngine(const EngineOptions& opt) : opt_(opt) {
   if (const char* ww = std::getenv("MOC_TILE16_WINWIDE")) tile16_window_wide_ = std::atoi(ww) != 0;
   if (const char* w8 = std::getenv("MOC_TILE16_WIN_U8")) short_window_u8_ = std::atoi(w8) != 0;
   if (const char* sl = std::getenv("MOC_TILE16_SLIDE")) tile16_slide_ = std::atoi(sl) != 0;
+  if (const char* sw = std::getenv("MOC_TILE16_SLIDE_WG")) slide_wgs_per_cu_ = std::atoi(sw) == 1 ? 1 : 2;
   if (const char* w = std::getenv("MOC_TILE_WAVES_PER_CU")) {
     const int v = std::atoi(w);
     if (v >= 1 && v <= 32) tile_waves_per_cu_ = v;
@@ -504,9 +505,14 @@ bool HipEngine::plan_slide(const int64_t* offsets, const int32_t* long_recs, int
                            TilePlan& tp, std::vector<dev::WaveStart>& starts) const {
   // 4 sub-tiles by default: limits 14.9 (U = 2) -> 16.7 T cells/s, the int16 profile on limits' lengths
   // 10.6 -> 13.8 (profiles/tile16_r5/README.txt)
-  const int u = tile_u_ == 2 || tile_u_ == 8 ? tile_u_ : 4;
+  const int u = tile_u_ == 2 || (tile_u_ == 8 && slide_wgs_per_cu_ == 1) ? tile_u_ : 4;
   const int span = dev::tile_span(true, u);
-  const int64_t C = (dev::tile16_max_window(true) - span) / 64 * 64;  // steps per window
+  // two workgroups per CU with half the LDS each (8 waves per SIMD hide the sweep's LDS waits: limits 16.8 ->
+  // 17.6 T cells/s, the int16 profile 16.9 -> 18.0), or one with the widest window (MOC_TILE16_SLIDE_WG=1)
+  int64_t wmax = dev::tile16_max_window(true);
+  if (slide_wgs_per_cu_ == 2)
+    while (wmax > 0 && dev::tile16_lds_bytes(2 * dev::tile16_window_bytes(wmax), wmax) > dev::kProf16MaxLds / 2) --wmax;
+  const int64_t C = (wmax - span) / 64 * 64;  // steps per window
   if (C < 64) return false;
   constexpr int G = dev::kTile16WavesPerBlock;
   if (static_cast<double>(n_long) < min_fill * static_cast<double>(G * ((n_long + G - 1) / G))) return false;
@@ -546,7 +552,7 @@ bool HipEngine::plan_slide(const int64_t* offsets, const int32_t* long_recs, int
   if (total <= 0) return false;
   int64_t all_tiles = 0;
   for (int64_t g = 0; g < n_groups; ++g) all_tiles += gtiles[g];
-  const int64_t n_wg = std::min<int64_t>(num_cus_, all_tiles);
+  const int64_t n_wg = std::min<int64_t>(static_cast<int64_t>(num_cus_) * slide_wgs_per_cu_, all_tiles);
   const double share = static_cast<double>(total) / static_cast<double>(n_wg);
   for (int64_t g = 0; g < n_groups; ++g) {
     if (gtiles[g] <= 0) continue;
@@ -592,6 +598,7 @@ bool HipEngine::plan_slide(const int64_t* offsets, const int32_t* long_recs, int
     }
   }
   tp.slide_wgs = n_wg;
+  tp.slide_per_cu = slide_wgs_per_cu_;
   tp.tile16 = true;
   tp.wide = true;
   tp.slide = true;

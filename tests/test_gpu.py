@@ -867,13 +867,15 @@ def test_tile16_slide_group_fill(engine, n, w, slide):
 
 
 def test_tile16_slide_sub_tiles_and_previous_plan(monkeypatch):
-    # the U = 2 and U = 8 slide kernels (MOC_TILE_U; default 4) and the plan without sliding windows
+    # the U = 2 and U = 8 slide kernels (MOC_TILE_U; default 4), one workgroup per CU (MOC_TILE16_SLIDE_WG=1;
+    # default two, the 64-VGPR instances) and the plan without sliding windows
     # (MOC_TILE16_SLIDE=0: the whole byte-pair image) give the same results as the CPU engine
     from mpi_openmp_cuda_amd.utils.synthetic import Shape, make_shape
 
     prob = make_shape(Shape((10, 2, 3, 4), 2500, 700, 1700), 100, seed=5)
     ref = as_triples(search_cpu(prob))
-    for env, form in (({"MOC_TILE_U": "2"}, True), ({"MOC_TILE_U": "8"}, True), ({"MOC_TILE16_SLIDE": "0"}, False)):
+    for env, form in (({"MOC_TILE_U": "2"}, True), ({"MOC_TILE16_SLIDE_WG": "1"}, True),
+                      ({"MOC_TILE16_SLIDE_WG": "1", "MOC_TILE_U": "8"}, True), ({"MOC_TILE16_SLIDE": "0"}, False)):
         with monkeypatch.context() as m:
             for k, v in env.items():
                 m.setenv(k, v)
