@@ -37,7 +37,7 @@ GPU_PLUGIN := mpi_openmp_cuda_amd/lib/libmoc_final_gpu.so
 # host core without any ROCm dependency (parser, CPU engine, partitioner, runtime utilities)
 CPU_SRCS  := csrc/src/cpu_engine.cpp csrc/src/device_batch.cpp csrc/src/io.cpp csrc/src/partition.cpp csrc/src/problem.cpp csrc/src/wire.cpp \
              csrc/src/score_table.cpp csrc/src/runtime/runtime.cpp csrc/src/runtime/host_region.cpp \
-             csrc/src/runtime/kfd_topology.cpp
+             csrc/src/runtime/kfd_topology.cpp csrc/src/runtime/watchdog.cpp
 # host code of the GPU engine (HIP runtime API) and the C ABI of libmoc.so
 GPU_SRCS  := csrc/src/hip_engine.cpp csrc/src/capi.cpp csrc/src/runtime/device.cpp csrc/src/runtime/pinned.cpp
 CORE_SRCS := $(CPU_SRCS) $(GPU_SRCS)

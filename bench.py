@@ -60,6 +60,8 @@ def parse_args():
     ap.add_argument("--dump-steps", default="", help="rank 0 writes its per-step kernel and host ms to this JSON file")
     ap.add_argument("--dry-launch", action="store_true",
                     help="print the self-launch command (JSON) for --gpus N > 1 and exit; touches no GPU")
+    ap.add_argument("--comm-timeout", type=float, default=300.0,
+                    help="seconds a collective may wait on a peer before the job fails (0: torch's default)")
     ap.add_argument("--allow-shared-gpu", action="store_true",
                     help="rehearsals only (gloo): let several ranks share a GPU instead of failing")
     return ap.parse_args()
@@ -329,10 +331,14 @@ def main():
     # collective runs then, so a device copy of the header would only add a D2H sync per step)
     cdev = dev if (nccl and distributed) else torch.device("cpu")
     if distributed:
+        # a stuck peer fails the step with a timeout instead of hanging the job (the driver's clock)
+        import datetime
+
+        pg_kw = {"timeout": datetime.timedelta(seconds=args.comm_timeout)} if args.comm_timeout > 0 else {}
         if nccl:
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, **pg_kw)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", **pg_kw)
         if dist.get_world_size() != args.gpus:
             print(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}", file=sys.stderr)
             return 2

@@ -39,6 +39,7 @@
 #include "moc/runtime/host_region.hpp"
 #include "moc/runtime/kfd_topology.hpp"
 #include "moc/runtime/log.hpp"
+#include "moc/runtime/watchdog.hpp"
 
 using namespace moc;
 
@@ -133,14 +134,18 @@ const char* kUsage =
     "  --mpi-topology=lean|full    lean (default): MPI_Init skips the host's hardware discovery (CPUs, caches,\n"
     "                              PCI devices: 0.2-0.35 s of a tiny job on a 256-CPU node); full: MPI's own\n"
     "  --log-level=error|warn|info|debug\n"
-    "  --inject-fault=PHASE[:RANK] test hook: fail at parse|bcast|distribute|compute|gather\n"
+    "  --comm-timeout=SECONDS      deadline of every wait on another rank or on the RCCL comm lane (default 300;\n"
+    "                              0 = none): past it the rank aborts the job naming its phase and the peers\n"
+    "                              and bytes still outstanding\n"
+    "  --inject-fault=[stall:|stall-device:]PHASE[:RANK]   test hook: fail (or stall) at\n"
+    "                              parse|bcast|distribute|fill|pack|compute|gather\n"
     "every flag can also be given as environment variable MOC_<FLAG> (e.g. MOC_BACKEND=cpu)\n";
 
 const std::vector<std::string> kKnown = {
     "backend", "collectives", "parallel-print", "gpu-min-cells", "gpu-prewarm-bytes", "transport", "semantics",
     "partition", "batch-records", "batch-chars", "skip-records", "input", "output", "timing", "strict-limits",
     "max-l1", "max-l2", "device", "device-map", "pin-window", "chunk-records", "chunk-bytes", "threads",
-    "log-level", "inject-fault", "mpi-topology", "timing-exit", "quick-exit", "gpu-isolate", "help"};
+    "log-level", "inject-fault", "mpi-topology", "timing-exit", "quick-exit", "gpu-isolate", "comm-timeout", "help"};
 
 struct BatchHeader {
   int64_t n;
@@ -279,12 +284,7 @@ int Job::run() {
   log_set_level(flags.get("log-level", "warn"));
   log_set_rank(ctx.rank);
   if (!g_gpu_isolation.empty()) MOC_LOG_INFO("runtime isolated to %s", g_gpu_isolation.c_str());
-  {
-    std::string f = flags.get("inject-fault", "");
-    auto colon = f.find(':');
-    job_.fault.phase = f.substr(0, colon);
-    if (colon != std::string::npos) job_.fault.rank = std::stoi(f.substr(colon + 1));
-  }
+  job_.fault.parse(flags.get("inject-fault", ""));
   const std::string sem_s = to_lower(flags.get("semantics", "reference"));
   if (sem_s != "reference" && sem_s != "spec") throw Error("--semantics must be reference|spec");
   const Semantics sem = sem_s == "spec" ? Semantics::Spec : Semantics::Reference;
@@ -541,7 +541,7 @@ int Job::run() {
     job_.extra_timing.emplace_back("runtime_up_since_start_ms", buf);
   }
   job_.report(h);
-  MPI_Barrier(ctx.world);
+  barrier(ctx.world, "MPI_Ibarrier (job end)");
   return rc;
 }
 
@@ -741,6 +741,7 @@ int main(int argc, char** argv) {
       return 2;
     }
     if (ctx->rank == kRoot && flags.get_bool("timing-exit", false)) exit_clock.enable();
+    watchdog::set_timeout_s(flags.get_double("comm-timeout", watchdog::kDefaultTimeoutS));
     quick_exit = flags.get_bool("quick-exit", true);
     {
       Job job(*ctx, flags, releaser, std::move(prewarm));
@@ -750,7 +751,10 @@ int main(int argc, char** argv) {
     }
     exit_clock.mark("job_teardown");
   } catch (const std::exception& e) {
-    ctx->abort(3, e.what());
+    // the phase the rank was in (a comm timeout names it already)
+    const std::string ph = watchdog::phase();
+    const std::string msg = e.what();
+    ctx->abort(3, ph.empty() || msg.find("in phase '") != std::string::npos ? msg : msg + " (phase '" + ph + "')");
   }
   ctx.reset();
   exit_clock.mark("mpi_finalize");

@@ -5,6 +5,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <deque>
+#include <exception>
 #include <future>
 #include <memory>
 #include <mutex>
@@ -25,6 +27,7 @@
 #include "moc/runtime/log.hpp"
 #include "moc/runtime/pinned.hpp"
 #include "moc/runtime/timer.hpp"
+#include "moc/runtime/watchdog.hpp"
 #include "moc/score_table.hpp"
 #include "moc/wire.hpp"
 
@@ -33,6 +36,16 @@ namespace {
 
 // RCCL over xGMI as the rccl transport's device layer: comm lane = the engine's compute stream (so the
 // searches and the collectives are ordered without host waits), copy lane = a stream of its own.
+//
+// Every host wait polls (hipEventQuery / hipStreamQuery, ncclCommGetAsyncError every ~1 ms) against the job's
+// comm deadline; past it the communicator is aborted and CommTimeout names the wait and the comm-lane
+// transfers not yet known complete (moc/runtime/watchdog.hpp). The reference's ranks instead exit(1) or block
+// forever (/root/reference/cudaFunctions.cu:15-33, main.c:174,195-197).
+//
+// Completion events are pooled: a ticket is a sequence number; an event goes back to the pool once it has
+// completed (checked in ticket order at the next record), and a ticket whose event was recycled is known
+// complete, so the pool is bounded by what is in flight (the pipelines' depth), not by the job's length
+// (the reference allocated, and leaked, per record: cudaFunctions.cu:206).
 class RcclDeviceComm final : public DeviceComm {
  public:
   RcclDeviceComm(const MpiContext& ctx, int device, hipStream_t comm_lane, const ncclUniqueId& id)
@@ -41,8 +54,9 @@ class RcclDeviceComm final : public DeviceComm {
     MOC_HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
   }
   ~RcclDeviceComm() override {
-    (void)hipStreamSynchronize(copy_);
-    for (hipEvent_t e : events_) (void)hipEventDestroy(e);
+    if (std::uncaught_exceptions() == 0) (void)hipStreamSynchronize(copy_);
+    for (const Live& l : live_) (void)hipEventDestroy(l.e);
+    for (hipEvent_t e : free_) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(copy_);
   }
   int rank() const override { return ctx_.rank; }
@@ -85,46 +99,135 @@ class RcclDeviceComm final : public DeviceComm {
     if (bytes > 0) MOC_HIP_CHECK(hipMemcpyAsync(d, h, static_cast<size_t>(bytes), hipMemcpyHostToDevice, copy_));
     return record(copy_);
   }
-  void wait_upload(int ticket) override { MOC_HIP_CHECK(hipStreamWaitEvent(s_, events_[ticket], 0)); }
+  void wait_upload(int ticket) override {
+    if (hipEvent_t e = pending_event(ticket)) MOC_HIP_CHECK(hipStreamWaitEvent(s_, e, 0));
+  }
   int upload_after(void* d, const void* h, int64_t bytes, int after) override {
-    if (after >= 0) MOC_HIP_CHECK(hipStreamWaitEvent(copy_, events_[after], 0));
+    if (after >= 0)
+      if (hipEvent_t e = pending_event(after)) MOC_HIP_CHECK(hipStreamWaitEvent(copy_, e, 0));
     return upload(d, h, bytes);
   }
-  void wait_upload_host(int ticket) override { MOC_HIP_CHECK(hipEventSynchronize(events_[ticket])); }
+  void wait_upload_host(int ticket) override { host_wait(ticket, "an upload to finish reading its staging buffer"); }
   void download(void* h, const void* d, int64_t bytes) override {
     if (bytes > 0) MOC_HIP_CHECK(hipMemcpyAsync(h, d, static_cast<size_t>(bytes), hipMemcpyDeviceToHost, s_));
     sync();
   }
-  void group_start() override { nccl(ncclGroupStart(), "ncclGroupStart"); }
-  void group_end() override { nccl(ncclGroupEnd(), "ncclGroupEnd"); }
+  void group_start() override { nccl_.settle(ncclGroupStart(), "ncclGroupStart"); }
+  void group_end() override { nccl_.settle(ncclGroupEnd(), "ncclGroupEnd"); }
   void send(const void* d, int64_t bytes, int peer) override {
-    if (bytes > 0) nccl(ncclSend(d, static_cast<size_t>(bytes), ncclUint8, peer, nccl_.comm(), s_), "ncclSend");
+    if (bytes <= 0) return;
+    nccl_.settle(ncclSend(d, static_cast<size_t>(bytes), ncclUint8, peer, nccl_.comm(), s_), "ncclSend");
+    ops_.push_back(Op{++op_seq_, peer, bytes, "send"});
   }
   void recv(void* d, int64_t bytes, int peer) override {
-    if (bytes > 0) nccl(ncclRecv(d, static_cast<size_t>(bytes), ncclUint8, peer, nccl_.comm(), s_), "ncclRecv");
+    if (bytes <= 0) return;
+    nccl_.settle(ncclRecv(d, static_cast<size_t>(bytes), ncclUint8, peer, nccl_.comm(), s_), "ncclRecv");
+    ops_.push_back(Op{++op_seq_, peer, bytes, "recv"});
   }
-  void bcast(void* d, int64_t bytes, int root) override { nccl_.bcast(d, bytes, root, s_); }
+  void bcast(void* d, int64_t bytes, int root) override {
+    nccl_.bcast(d, bytes, root, s_);
+    if (bytes > 0) ops_.push_back(Op{++op_seq_, root, bytes, "bcast"});
+  }
   void allgather(const void* d_send, void* d_recv, int64_t bytes_each) override {
     nccl_.allgather(d_send, d_recv, bytes_each, s_);
+    if (bytes_each > 0) ops_.push_back(Op{++op_seq_, -1, bytes_each * ctx_.size, "allgather"});
   }
-  void allreduce_max_u64(uint64_t* d, int64_t n) override { nccl_.allreduce_max_u64(d, n, s_); }
+  void allreduce_max_u64(uint64_t* d, int64_t n) override {
+    nccl_.allreduce_max_u64(d, n, s_);
+    if (n > 0) ops_.push_back(Op{++op_seq_, -1, 8 * n, "allreduce"});
+  }
   void sync() override {
-    MOC_HIP_CHECK(hipStreamSynchronize(s_));
-    nccl_.check_async();
+    poll([this] { return query(hipStreamQuery(s_)); }, "the comm lane to drain");
+    ops_.clear();  // everything queued on the lane is complete
   }
-  int mark() override { return record(s_); }
-  void wait_mark(int m) override { MOC_HIP_CHECK(hipEventSynchronize(events_[m])); }
+  int mark() override {
+    const int t = record(s_);
+    mark_ops_.emplace_back(t, op_seq_);
+    return t;
+  }
+  void wait_mark(int m) override {
+    host_wait(m, "a comm-lane point (a staging buffer's last send)");
+    // the transfers queued before that point are complete
+    uint64_t upto = 0;
+    while (!mark_ops_.empty() && mark_ops_.front().first <= m) {
+      upto = mark_ops_.front().second;
+      mark_ops_.pop_front();
+    }
+    while (!ops_.empty() && ops_.front().seq <= upto) ops_.pop_front();
+  }
+  void inject_stall(double seconds) override {
+    dev::launch_spin(seconds, s_);
+    MOC_HIP_CHECK(hipGetLastError());
+  }
+  int64_t events_live() const override { return static_cast<int64_t>(live_.size() + free_.size()); }
 
  private:
-  static void nccl(ncclResult_t r, const char* what) {
-    if (r != ncclSuccess) throw Error(std::string(what) + ": " + ncclGetErrorString(r));
+  struct Live {
+    int64_t ticket;
+    hipEvent_t e;
+  };
+  struct Op {
+    uint64_t seq;
+    int peer;
+    int64_t bytes;
+    const char* kind;
+  };
+  static bool query(hipError_t r) {
+    if (r == hipSuccess) return true;
+    if (r != hipErrorNotReady) MOC_HIP_CHECK(r);
+    return false;
+  }
+  // the ticket's event while it may still be pending; nullptr once it is known complete (recycled)
+  hipEvent_t pending_event(int ticket) const {
+    if (live_.empty() || ticket < live_.front().ticket) return nullptr;
+    const size_t i = static_cast<size_t>(ticket - live_.front().ticket);
+    if (i >= live_.size()) throw Error("RcclDeviceComm: unknown ticket " + std::to_string(ticket));
+    return live_[i].e;
+  }
+  void host_wait(int ticket, const char* what) {
+    if (hipEvent_t e = pending_event(ticket)) poll([e] { return query(hipEventQuery(e)); }, what);
+  }
+  template <typename Done>
+  void poll(Done done, const char* what) {
+    watchdog::WaitSpec spec;
+    spec.what = what;
+    spec.poll = watchdog::Poll::Backoff;
+    spec.check = [this] { nccl_.check_async(); };
+    spec.expire = [this] { nccl_.abort(); };
+    spec.outstanding = [this] { return describe_ops(); };
+    watchdog::wait(done, spec);
+    nccl_.check_async();  // an error the communicator hit while the lane drained
+  }
+  std::string describe_ops() const {
+    std::string o;
+    size_t k = 0;
+    for (const Op& op : ops_) {
+      if (++k > 8) break;
+      if (!o.empty()) o += ", ";
+      o += std::string(op.kind) + " " + watchdog::human_bytes(op.bytes);
+      if (op.peer >= 0)
+        o += std::string(op.kind[0] == 's' ? " to" : op.kind[0] == 'r' ? " from" : " root") + " rank " +
+             std::to_string(op.peer);
+    }
+    if (ops_.size() > 8) o += " (+" + std::to_string(ops_.size() - 8) + " more)";
+    return o.empty() ? "no transfer queued (device work on the comm lane)" : "comm-lane transfers " + o;
   }
   int record(hipStream_t st) {
+    // completed events (in ticket order) go back to the pool
+    while (!live_.empty() && hipEventQuery(live_.front().e) == hipSuccess) {
+      free_.push_back(live_.front().e);
+      live_.pop_front();
+    }
     hipEvent_t e = nullptr;
-    MOC_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (free_.empty()) {
+      MOC_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    } else {
+      e = free_.back();
+      free_.pop_back();
+    }
     MOC_HIP_CHECK(hipEventRecord(e, st));
-    events_.push_back(e);
-    return static_cast<int>(events_.size()) - 1;
+    live_.push_back(Live{next_ticket_, e});
+    return static_cast<int>(next_ticket_++);
   }
   static constexpr int64_t kBigHost = int64_t{4} << 20;
   struct Big {
@@ -135,7 +238,12 @@ class RcclDeviceComm final : public DeviceComm {
   int device_;
   hipStream_t s_, copy_ = nullptr;
   RcclComm nccl_;
-  std::vector<hipEvent_t> events_;
+  std::deque<Live> live_;         // recorded, not yet seen complete (ticket order)
+  std::vector<hipEvent_t> free_;  // completed, reusable
+  int64_t next_ticket_ = 0;
+  std::deque<Op> ops_;            // comm-lane transfers not yet known complete (for a timeout's message)
+  uint64_t op_seq_ = 0;
+  std::deque<std::pair<int, uint64_t>> mark_ops_;  // mark ticket -> the last transfer queued before it
   std::unordered_map<void*, Big> big_;
 };
 
@@ -213,6 +321,7 @@ class GpuRankImpl final : public GpuRank {
   GpuRankImpl(const MpiContext& ctx, const GpuRankOptions& opt) : ctx_(ctx) {
     log_set_level(opt.log_level);
     log_set_rank(ctx.rank);
+    watchdog::set_timeout_s(opt.comm_timeout_s);  // this library's copy of the job's deadline
     int requested = opt.device;
     if (requested < 0 && !opt.device_map.empty())
       requested = opt.device_map[static_cast<size_t>(ctx.local_rank) % opt.device_map.size()];

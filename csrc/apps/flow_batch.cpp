@@ -222,13 +222,13 @@ void BatchFlow::batch_mpi(RecordBatch* rb, int64_t n, int64_t total_chars, const
 void BatchFlow::batch_rccl(RecordBatch* rb, int64_t n, int64_t total_chars, const std::vector<int64_t>& bounds,
                            bool cp) {
   PhaseHooks hooks;
-  hooks.begin = [this](const char* phase) {
+  DeviceComm& dc = j_.emul_comm ? static_cast<DeviceComm&>(*j_.emul_comm) : j_.eng.hip->device_comm();
+  hooks.begin = [this, &dc](const char* phase) {
     j_.pt.begin(phase);
-    j_.fault.at(phase, j_.ctx.rank);
+    j_.fault.at(phase, j_.ctx.rank, &dc);
   };
   hooks.end = [this] { j_.pt.end(); };
   DeviceBatchOut out;
-  DeviceComm& dc = j_.emul_comm ? static_cast<DeviceComm&>(*j_.emul_comm) : j_.eng.hip->device_comm();
   if (!j_.scratch) j_.scratch = std::make_unique<DeviceScratch>(dc);
   if (j_.emul_comm) {
     CpuDeviceSearch ds(j_.eng.table, j_.eng.seq1, j_.eng.sem, j_.eng.threads);
@@ -307,12 +307,12 @@ void run_text_batch(JobCore& job, std::unique_ptr<BulkParser>& parser, int64_t f
   job.first_index = first_index;
   job.records += st[1];
   PhaseHooks hooks;
-  hooks.begin = [&job](const char* phase) {
+  DeviceComm& dc = job.emul_comm ? static_cast<DeviceComm&>(*job.emul_comm) : job.eng.hip->device_comm();
+  hooks.begin = [&job, &dc](const char* phase) {
     job.pt.begin(phase);
-    job.fault.at(phase, job.ctx.rank);
+    job.fault.at(phase, job.ctx.rank, &dc);
   };
   hooks.end = [&job] { job.pt.end(); };
-  DeviceComm& dc = job.emul_comm ? static_cast<DeviceComm&>(*job.emul_comm) : job.eng.hip->device_comm();
   if (!job.scratch) job.scratch = std::make_unique<DeviceScratch>(dc);
   DeviceBatchOut out;
   if (job.emul_comm) {

@@ -48,13 +48,13 @@ int run_device_streaming(JobCore& job, const Header& h, StreamSource& src, int64
   }
   job.first_index = next;
 
+  DeviceComm* dc = nullptr;
   PhaseHooks hooks;
-  hooks.begin = [&job](const char* phase) {
+  hooks.begin = [&job, &dc](const char* phase) {
     job.pt.begin(phase);
-    job.fault.at(phase, job.ctx.rank);
+    job.fault.at(phase, job.ctx.rank, dc);
   };
   hooks.end = [&job] { job.pt.end(); };
-  DeviceComm* dc = nullptr;
   std::unique_ptr<CpuDeviceSearch> cpu_search;
   DeviceSearch* ds = nullptr;
   if (device) {

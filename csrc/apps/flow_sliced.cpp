@@ -48,14 +48,25 @@ void run_sliced(JobCore& job, BulkParser& parser, int64_t first_index, SharedWin
       cnt[q] = static_cast<int>(int64_t{nch} * (q + 1) / p) - dsp[q];
     }
     parser.count_chunks(starts, dsp[r], dsp[r] + cnt[r], tk.data() + dsp[r], ch.data() + dsp[r]);
-    MPI_Allgatherv(MPI_IN_PLACE, 0, MPI_DATATYPE_NULL, tk.data(), cnt.data(), dsp.data(), MPI_INT64_T, ctx.world);
-    MPI_Allgatherv(MPI_IN_PLACE, 0, MPI_DATATYPE_NULL, ch.data(), cnt.data(), dsp.data(), MPI_INT64_T, ctx.world);
+    MPI_Request rq[2];
+    mpi_check(MPI_Iallgatherv(MPI_IN_PLACE, 0, MPI_DATATYPE_NULL, tk.data(), cnt.data(), dsp.data(), MPI_INT64_T,
+                              ctx.world, &rq[0]),
+              "MPI_Iallgatherv");
+    mpi_check(MPI_Iallgatherv(MPI_IN_PLACE, 0, MPI_DATATYPE_NULL, ch.data(), cnt.data(), dsp.data(), MPI_INT64_T,
+                              ctx.world, &rq[1]),
+              "MPI_Iallgatherv");
+    std::vector<MPI_Request> reqs(rq, rq + 2);
+    mpi_wait_all(reqs, "MPI_Iallgatherv (pass-1 chunk counts)");
     // inputs up to 256 MiB also get exact chunk costs (a token walk) for the bounds: few, coarse chunks
     // of records of very different lengths are what the mean-length estimate gets wrong
     if (job.partition != "even" && p > 1 && area <= (int64_t{256} << 20)) {
       std::vector<double> costs(static_cast<size_t>(nch));
       parser.chunk_costs(starts, dsp[r], dsp[r] + cnt[r], cost_model, costs.data() + dsp[r]);
-      MPI_Allgatherv(MPI_IN_PLACE, 0, MPI_DATATYPE_NULL, costs.data(), cnt.data(), dsp.data(), MPI_DOUBLE, ctx.world);
+      MPI_Request r;
+      mpi_check(MPI_Iallgatherv(MPI_IN_PLACE, 0, MPI_DATATYPE_NULL, costs.data(), cnt.data(), dsp.data(), MPI_DOUBLE,
+                                ctx.world, &r),
+                "MPI_Iallgatherv");
+      mpi_wait(r, "MPI_Iallgatherv (chunk costs)");
       parser.set_chunk_costs(std::move(costs));
     }
   }
@@ -323,7 +334,7 @@ void run_sliced(JobCore& job, BulkParser& parser, int64_t first_index, SharedWin
     }
     if (n > 0) write_results_at(fd, at, mine, b0);
     if (r != kRoot && fd >= 0) ::close(fd);
-    MPI_Barrier(ctx.world);  // every row is in the file
+    barrier(ctx.world, "MPI_Ibarrier (parallel print)");  // every row is in the file
     if (r == kRoot) std::fseek(job.out, static_cast<long>(dp[1] + total), SEEK_SET);
     pt.end();
     return;

@@ -51,13 +51,20 @@ struct InputError : Error {
   using Error::Error;
 };
 
+// --inject-fault=[stall:|stall-device:]PHASE[:RANK] (test hooks, rank 0 by default). Plain: the rank throws
+// at the start of PHASE (the fail-fast path: message + MPI_Abort). stall: the rank's thread sleeps there
+// for MOC_STALL_S seconds (default 120) — a peer that is alive but stuck, which the other ranks' comm
+// deadline must name. stall-device: the rank's device comm lane is held busy instead (a bounded spin
+// kernel on a GPU rank; MOC_STALL_S default 3), so its own deadline-polled waits expire.
 struct FaultHook {
+  enum class Kind { Fail, Stall, StallDevice };
+  Kind kind = Kind::Fail;
   std::string phase;
   int rank = 0;
-  void at(const char* p, int my_rank) const {
-    if (!phase.empty() && phase == p && my_rank == rank)
-      throw Error(std::string("injected fault at phase '") + p + "'");
-  }
+  double stall_s = 0;  // 0: the kind's default
+  void parse(const std::string& spec);
+  // `dc`: the flow's device comm, the target of stall-device (nullptr: the thread sleeps instead)
+  void at(const char* p, int my_rank, DeviceComm* dc = nullptr) const;
 };
 
 std::string to_lower(std::string s);
@@ -116,6 +123,7 @@ struct JobCore {
   int64_t comm_sent_bytes = 0;
   std::vector<int64_t> peer_sent;
   double distribute_ms = 0;
+  std::vector<int> fill_order;  // root, text batches: the order the slices were encoded (the first batch's)
   std::vector<int64_t> rank_pinned, rank_h2d, rank_records, rank_pin_us;  // root: per rank (--timing)
   std::vector<std::pair<std::string, std::string>> extra_timing;          // flow-specific --timing fields
   const char* build_id = "";  // the sources of this binary (--timing)

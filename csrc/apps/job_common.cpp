@@ -5,14 +5,17 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cctype>
 #include <cstdio>
 #include <cstring>
 #include <sstream>
+#include <thread>
 
 #include "job.hpp"
 #include "moc/runtime/kfd_topology.hpp"
 #include "moc/runtime/log.hpp"
+#include "moc/runtime/watchdog.hpp"
 
 namespace moc {
 
@@ -93,6 +96,36 @@ bool gpu_rccl_warmup(int device) {
 }
 GpuRank* gpu_rank_create(const MpiContext& ctx, const GpuRankOptions& opt) { return gpu_plugin().create(ctx, opt); }
 
+// ---- FaultHook
+
+void FaultHook::parse(const std::string& spec) {
+  std::string f = spec;
+  kind = Kind::Fail;
+  if (f.rfind("stall-device:", 0) == 0) {
+    kind = Kind::StallDevice;
+    f = f.substr(13);
+  } else if (f.rfind("stall:", 0) == 0) {
+    kind = Kind::Stall;
+    f = f.substr(6);
+  }
+  const auto colon = f.find(':');
+  phase = f.substr(0, colon);
+  rank = colon != std::string::npos ? std::stoi(f.substr(colon + 1)) : 0;
+  if (const char* v = std::getenv("MOC_STALL_S")) stall_s = std::atof(v);
+}
+
+void FaultHook::at(const char* p, int my_rank, DeviceComm* dc) const {
+  if (phase.empty() || phase != p || my_rank != rank) return;
+  if (kind == Kind::Fail) throw Error(std::string("injected fault at phase '") + p + "'");
+  const double s = stall_s > 0 ? stall_s : (kind == Kind::Stall ? 120.0 : 3.0);
+  MOC_LOG_WARN("injected %s stall of %.1f s at phase '%s'", kind == Kind::Stall ? "rank" : "device comm lane", s, p);
+  if (kind == Kind::StallDevice && dc) {
+    dc->inject_stall(s);
+    return;
+  }
+  std::this_thread::sleep_for(std::chrono::duration<double>(s));
+}
+
 // ---- RankEngine
 
 namespace {
@@ -168,6 +201,7 @@ void JobCore::setup_engine(int64_t job_cells, int64_t mean_l2) {
     go.chunk_records = flags.get_int("chunk-records", 0);
     go.chunk_bytes = flags.get_int("chunk-bytes", 0);
     go.log_level = flags.get("log-level", "warn");
+    go.comm_timeout_s = watchdog::timeout_s();
     // a job below the GPU crossover (forced with --backend=hip) runs one kernel once: loading every code
     // object up front would cost more than that kernel's own load at its launch
     go.preload_kernels = job_cells < 0 || job_cells >= min_cells * ctx.size;
@@ -178,7 +212,11 @@ void JobCore::setup_engine(int64_t job_cells, int64_t mean_l2) {
   }
   int gpu_minmax[2] = {eng.gpu ? 1 : 0, eng.gpu ? -1 : 0};  // MIN -> {min gpu, -max gpu}
   sw_reduce.start();
-  MPI_Allreduce(MPI_IN_PLACE, gpu_minmax, 2, MPI_INT, MPI_MIN, ctx.world);
+  {
+    MPI_Request r;
+    mpi_check(MPI_Iallreduce(MPI_IN_PLACE, gpu_minmax, 2, MPI_INT, MPI_MIN, ctx.world, &r), "MPI_Iallreduce");
+    mpi_wait(r, "MPI_Iallreduce (engine kinds)");
+  }
   sw_reduce.stop();
   {
     char buf[160];
@@ -216,7 +254,9 @@ void JobCore::setup_engine(int64_t job_cells, int64_t mean_l2) {
   if (all_gpu && coll == "rccl") {
     const int64_t mine = static_cast<int64_t>(std::hash<std::string>{}(ctx.hostname) & 0xffffffffffffull) * 4096 + device;
     std::vector<int64_t> all(static_cast<size_t>(ctx.size));
-    MPI_Allgather(&mine, 1, MPI_INT64_T, all.data(), 1, MPI_INT64_T, ctx.world);
+    MPI_Request r;
+    mpi_check(MPI_Iallgather(&mine, 1, MPI_INT64_T, all.data(), 1, MPI_INT64_T, ctx.world, &r), "MPI_Iallgather");
+    mpi_wait(r, "MPI_Iallgather (rank devices)");
     std::sort(all.begin(), all.end());
     shared_gpu = std::adjacent_find(all.begin(), all.end()) != all.end();
   }
@@ -231,7 +271,9 @@ void JobCore::setup_engine(int64_t job_cells, int64_t mean_l2) {
 
 void JobCore::allgather_i64(const int64_t* mine, int count, int64_t* all) {
   if (!coll_rccl) {
-    MPI_Allgather(mine, count, MPI_INT64_T, all, count, MPI_INT64_T, ctx.world);
+    MPI_Request r;
+    mpi_check(MPI_Iallgather(mine, count, MPI_INT64_T, all, count, MPI_INT64_T, ctx.world, &r), "MPI_Iallgather");
+    mpi_wait(r, "MPI_Iallgather");
     return;
   }
   DeviceComm& dc = eng.hip->device_comm();  // waits for the connect
@@ -286,6 +328,7 @@ void JobCore::account_comm(const DeviceBatchOut& out) {
   distribute_ms += out.distribute_ms;
   if (peer_sent.size() < out.peer_bytes.size()) peer_sent.resize(out.peer_bytes.size(), 0);
   for (size_t q = 0; q < out.peer_bytes.size(); ++q) peer_sent[q] += out.peer_bytes[q];
+  if (fill_order.empty()) fill_order = out.fill_order;
 }
 
 void JobCore::report(const Header& h) {
@@ -294,12 +337,21 @@ void JobCore::report(const Header& h) {
   const double comm_init = eng.hip && (device_transport || coll_rccl) ? eng.hip->rccl_init_ms() : 0.0;
   const double comm_wait = eng.hip && (device_transport || coll_rccl) ? eng.hip->rccl_wait_ms() : 0.0;
   double mx[4] = {compute_ms, eng.kernel_ms, comm_init, comm_wait};
-  MPI_Reduce(ctx.rank == kRoot ? MPI_IN_PLACE : mx, mx, 4, MPI_DOUBLE, MPI_MAX, kRoot, ctx.world);
+  {
+    MPI_Request r;
+    mpi_check(MPI_Ireduce(ctx.rank == kRoot ? MPI_IN_PLACE : mx, mx, 4, MPI_DOUBLE, MPI_MAX, kRoot, ctx.world, &r),
+              "MPI_Ireduce");
+    mpi_wait(r, "MPI_Ireduce (--timing)");
+  }
   // every mode: what each rank page-locked and moved host->device over the job (sliced mode also has
   // its per-rank records and pin times, gathered with its results), and what it sent over the comm
   int64_t moved[3] = {pinned_bytes, h2d_bytes, comm_sent_bytes};
   std::vector<int64_t> all_moved(static_cast<size_t>(3 * ctx.size));
-  MPI_Gather(moved, 3, MPI_INT64_T, all_moved.data(), 3, MPI_INT64_T, kRoot, ctx.world);
+  {
+    MPI_Request r;
+    mpi_check(MPI_Igather(moved, 3, MPI_INT64_T, all_moved.data(), 3, MPI_INT64_T, kRoot, ctx.world, &r), "MPI_Igather");
+    mpi_wait(r, "MPI_Igather (--timing)");
+  }
   if (ctx.rank != kRoot || !flags.get_bool("timing", false)) return;
   const double wall_s = total.total_ms() / 1e3;
   auto list = [](const std::vector<int64_t>& v) {
@@ -337,6 +389,12 @@ void JobCore::report(const Header& h) {
     }
     per_rank += ", \"peer_sent_bytes\": " + list(peer_sent.empty() ? std::vector<int64_t>(ctx.size, 0) : peer_sent) +
                 ", \"peer_distribute_gbps\": " + gbps + "]";
+    if (!fill_order.empty()) per_rank += ", \"fill_order\": " + list(std::vector<int64_t>(fill_order.begin(), fill_order.end()));
+  }
+  if (device_transport) {  // completion events the device comm holds (pooled: bounded by the pipeline depth)
+    const DeviceComm* dc = emul_comm ? static_cast<const DeviceComm*>(emul_comm.get())
+                                     : (eng.hip ? &eng.hip->device_comm() : nullptr);
+    if (dc) per_rank += ", \"comm_events_live\": " + std::to_string(dc->events_live());
   }
   for (const auto& kv : extra_timing) per_rank += ", \"" + kv.first + "\": " + kv.second;
   std::fprintf(stderr,

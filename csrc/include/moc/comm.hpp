@@ -56,6 +56,20 @@ class MpiContext {
 
 void mpi_check(int rc, const char* what);
 
+// A pending point-to-point request's peer and size, named when a wait on it times out.
+struct ReqInfo {
+  int peer = -1;
+  int64_t bytes = 0;
+  bool send = false;
+};
+// MPI_Waitall under the job's comm deadline (moc/runtime/watchdog.hpp: CommTimeout when it passes).
+// `infos` (optional, parallel to reqs) describes the requests still pending then. Leaves reqs empty.
+void mpi_wait_all(std::vector<MPI_Request>& reqs, const char* what, const std::vector<ReqInfo>* infos = nullptr);
+// One request (a non-blocking collective) under the deadline; `detail` describes it in the message.
+void mpi_wait(MPI_Request& req, const char* what, const std::string& detail = {});
+// MPI_Barrier under the deadline.
+void barrier(MPI_Comm comm, const char* what);
+
 // Broadcast of arbitrary byte counts (>2 GiB safe) from root.
 void bcast_bytes(void* buf, int64_t bytes, int root, MPI_Comm comm);
 // Root sends counts[r] bytes at displs[r] of sendbuf to rank r (64-bit safe, any sizes).

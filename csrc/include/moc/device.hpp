@@ -101,6 +101,15 @@ inline int64_t tile16_max_window(bool wide = false) {
   while (w > 0 && tile16_lds_bytes(f * tile16_window_bytes(w), w) > kProf16MaxLds) --w;
   return w & ~int64_t{15};
 }
+// LDS bytes of the profile part of a tile16 workgroup image (pv.prof16_bytes of a whole-image view): the whole
+// profile (26 rows of L1 entries + overhang) when it fits one CU — widened, for int16 entries, which only the
+// widened image takes — else one window's rows. Always an LDS size (it never wraps, whatever L1: a long Seq1's
+// int16 profile lives in device memory and the sliding windows stage it).
+inline int32_t tile16_profile_lds_bytes(int64_t L1, int64_t overhang, bool i16) {
+  const int64_t whole = ((2 * (26 * L1 + overhang)) + 15) & ~int64_t{15};
+  const bool fits = tile16_lds_bytes(i16 ? 2 * whole : whole, L1) <= kProf16MaxLds;
+  return static_cast<int32_t>(fits ? whole : tile16_window_bytes(tile16_max_window()));
+}
 
 // One batch of records on the device. Offsets are absolute (int64) and rebased by offsets[0], so
 // a chunk of a bigger CSR array can be transferred and launched without host-side rebasing.
@@ -181,6 +190,8 @@ struct ShortArgs {
 constexpr size_t kKernelCopyMaxAligned = size_t{8} << 20;
 constexpr size_t kKernelCopyMaxBytes = size_t{1} << 20;
 void launch_copy(void* dst, const void* src, size_t bytes, hipStream_t stream);
+// A single wave idling `seconds` (clamped to 10 s) on `stream`: the comm-timeout test hook's device stall.
+void launch_spin(double seconds, hipStream_t stream);
 bool kernel_copy_fits(const void* dst, const void* src, size_t bytes);
 
 // Unpacks n chars of a 5-bit packed stream (device memory) starting at bit `bit0` into byte codes.

@@ -63,6 +63,13 @@ class DeviceComm {
   // a point of the comm lane, and a host wait for just that point (pipelines reuse staging buffers)
   virtual int mark() = 0;
   virtual void wait_mark(int mark) = 0;
+  // Every host wait above (sync, download, wait_mark, wait_upload_host, group_end) polls against the job's
+  // comm deadline (moc/runtime/watchdog.hpp) and throws CommTimeout naming what is outstanding.
+  // Test hook (--inject-fault=stall-device:PHASE): the comm lane is held busy for `seconds` (a bounded device
+  // spin on GPUs; the calling thread sleeps on the MPI emulation).
+  virtual void inject_stall(double seconds);
+  // Completion events the layer holds right now (pooled: bounded by the pipeline depth, not the job).
+  virtual int64_t events_live() const { return 0; }
 };
 
 class DeviceSearch {
@@ -123,6 +130,7 @@ struct DeviceBatchOut {
   // device_batch_text: the batch's search cells and letters (root); an input error (every rank; the
   // message on the root), in which case nothing was searched
   int64_t cells = 0, letters = 0;
+  std::vector<int> fill_order;  // device_batch_text (root): the ranks in the order their slices were encoded
   bool input_error = false;
   std::string error;
 };
@@ -144,7 +152,8 @@ DeviceBatchOut device_batch(DeviceComm& dc, DeviceSearch& ds, const RecordBatch*
 class BulkParser;
 // The same record-slice batch straight from the input text: the root encodes each rank's slice
 // (BulkParser::fill_slice after pass 1; `parser` and the p+1 record `bounds` are read on the root only)
-// into that rank's wire block in page-locked memory, peers first, and sends a block's pieces while it
+// into that rank's wire block in page-locked memory, its own first (uploaded while the peers' are encoded),
+// then the peers', and sends a block's pieces while it
 // encodes the next rank's slice (no intermediate byte-code batch). Phases: "fill" (root), "distribute",
 // "compute", "gather". An input error found in any slice comes back on every rank (nothing searched).
 // `record_base`: the global index of the parser's record 0 (a streamed batch's area parser), for the

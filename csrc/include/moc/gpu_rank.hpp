@@ -27,6 +27,7 @@ struct GpuRankOptions {
   int64_t chunk_bytes = 0;
   std::string log_level = "warn";
   bool preload_kernels = true;  // false: kernel code objects load at their first launch (tiny jobs)
+  double comm_timeout_s = 300;  // the RCCL comm's wait deadline (--comm-timeout; <= 0: none)
 };
 
 // What the last solve moved and ran (for --timing).

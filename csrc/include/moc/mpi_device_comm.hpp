@@ -46,6 +46,7 @@ class MpiDeviceComm final : public DeviceComm {
   const MpiContext& ctx_;
   int depth_ = 0;
   std::vector<MPI_Request> reqs_;
+  std::vector<ReqInfo> infos_;  // peer and size of each request (named by a comm timeout)
 };
 
 class CpuDeviceSearch final : public DeviceSearch {

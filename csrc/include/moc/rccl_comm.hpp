@@ -38,6 +38,15 @@ class RcclComm {
   void allreduce_max_u64(void* dbuf, int64_t n, hipStream_t s);
   void check_async() const;  // ncclCommGetAsyncError -> throw
   ncclComm_t comm() const { return comm_; }
+  // The communicator is non-blocking (ncclConfig_t::blocking = 0; MOC_RCCL_BLOCKING=1 makes it blocking):
+  // a call that RCCL leaves in progress — the init's exchange with the peers, a group's lazy p2p connect —
+  // returns at once and `settle` polls ncclCommGetAsyncError under the job's comm deadline
+  // (moc/runtime/watchdog.hpp), so a peer that never arrives is named instead of hanging the rank.
+  // Every call of this class goes through it; callers issuing their own ncclSend/ncclRecv/ncclGroupEnd on
+  // comm() pass the result here.
+  void settle(ncclResult_t r, const char* what);
+  // ncclCommAbort (a timed-out or failed rank, before MPI_Abort): the communicator is gone afterwards.
+  void abort();
   // A communicator that lives until the process ends (the `final` CLI's): its destructor leaves it to the
   // process exit instead of ncclCommDestroy, which costs ~0.45 s per communicator on the MI355X box
   // (profiles/rccl_init_variants.log). MOC_RCCL_DESTROY=1 destroys it anyway.

@@ -10,6 +10,7 @@
 #include <thread>
 
 #include "moc/runtime/log.hpp"
+#include "moc/runtime/watchdog.hpp"
 
 namespace moc {
 
@@ -26,6 +27,60 @@ void mpi_check(int rc, const char* what) {
 }
 
 #define MOC_MPI_CHECK(call) ::moc::mpi_check((call), #call)
+
+void mpi_wait_all(std::vector<MPI_Request>& reqs, const char* what, const std::vector<ReqInfo>* infos) {
+  if (reqs.empty()) return;
+  watchdog::WaitSpec spec;
+  spec.what = what;
+  spec.outstanding = [&reqs, infos]() {
+    std::string o;
+    int pending = 0;
+    for (size_t i = 0; i < reqs.size(); ++i) {
+      int f = 1;
+      if (reqs[i] != MPI_REQUEST_NULL) MPI_Test(&reqs[i], &f, MPI_STATUS_IGNORE);
+      if (f) continue;
+      if (++pending > 8) continue;
+      if (!o.empty()) o += ", ";
+      if (infos && i < infos->size()) {
+        const ReqInfo& r = (*infos)[i];
+        o += std::string(r.send ? "send " : "recv ") + watchdog::human_bytes(r.bytes) + (r.send ? " to rank " : " from rank ") +
+             std::to_string(r.peer);
+      } else {
+        o += "request " + std::to_string(i);
+      }
+    }
+    if (pending > 8) o += " (+" + std::to_string(pending - 8) + " more)";
+    return o;
+  };
+  int flag = 0;
+  const int n = static_cast<int>(reqs.size());
+  watchdog::wait(
+      [&] {
+        mpi_check(MPI_Testall(n, reqs.data(), &flag, MPI_STATUSES_IGNORE), what);
+        return flag != 0;
+      },
+      spec);
+  reqs.clear();
+}
+
+void mpi_wait(MPI_Request& req, const char* what, const std::string& detail) {
+  watchdog::WaitSpec spec;
+  spec.what = what;
+  if (!detail.empty()) spec.outstanding = [&detail] { return detail; };
+  int flag = 0;
+  watchdog::wait(
+      [&] {
+        mpi_check(MPI_Test(&req, &flag, MPI_STATUS_IGNORE), what);
+        return flag != 0;
+      },
+      spec);
+}
+
+void barrier(MPI_Comm comm, const char* what) {
+  MPI_Request r;
+  MOC_MPI_CHECK(MPI_Ibarrier(comm, &r));
+  mpi_wait(r, what, "a rank that has not reached the barrier");
+}
 
 void mpi_prepare_env(bool lean_topology) {
   if (lean_topology) setenv("HWLOC_COMPONENTS", "no_os,stop", 0);
@@ -69,7 +124,9 @@ void bcast_bytes(void* buf, int64_t bytes, int root, MPI_Comm comm) {
   char* p = static_cast<char*>(buf);
   for (int64_t off = 0; off < bytes; off += kMpiChunk) {
     const int n = static_cast<int>(std::min(kMpiChunk, bytes - off));
-    MOC_MPI_CHECK(MPI_Bcast(p + off, n, MPI_BYTE, root, comm));
+    MPI_Request r;
+    MOC_MPI_CHECK(MPI_Ibcast(p + off, n, MPI_BYTE, root, comm, &r));
+    mpi_wait(r, "MPI_Ibcast", "broadcast of " + watchdog::human_bytes(n) + " from rank " + std::to_string(root));
   }
 }
 
@@ -77,24 +134,32 @@ void allreduce_max_u64(uint64_t* buf, int64_t n, MPI_Comm comm) {
   const int64_t step = kMpiChunk / 8;
   for (int64_t off = 0; off < n; off += step) {
     const int c = static_cast<int>(std::min(step, n - off));
-    MOC_MPI_CHECK(MPI_Allreduce(MPI_IN_PLACE, buf + off, c, MPI_UINT64_T, MPI_MAX, comm));
+    MPI_Request r;
+    MOC_MPI_CHECK(MPI_Iallreduce(MPI_IN_PLACE, buf + off, c, MPI_UINT64_T, MPI_MAX, comm, &r));
+    mpi_wait(r, "MPI_Iallreduce", "MAX all-reduce of " + std::to_string(c) + " keys");
   }
 }
 
 namespace {
 // Point-to-point transfer of a byte range in < 2^31 pieces (posted as non-blocking requests).
-void post_send(std::vector<MPI_Request>& reqs, const char* p, int64_t bytes, int peer, int tag, MPI_Comm comm) {
+void post_send(std::vector<MPI_Request>& reqs, std::vector<ReqInfo>& infos, const char* p, int64_t bytes, int peer,
+               int tag, MPI_Comm comm) {
   for (int64_t off = 0; off < bytes; off += kMpiChunk) {
     MPI_Request r;
-    MOC_MPI_CHECK(MPI_Isend(p + off, static_cast<int>(std::min(kMpiChunk, bytes - off)), MPI_BYTE, peer, tag, comm, &r));
+    const int64_t n = std::min(kMpiChunk, bytes - off);
+    MOC_MPI_CHECK(MPI_Isend(p + off, static_cast<int>(n), MPI_BYTE, peer, tag, comm, &r));
     reqs.push_back(r);
+    infos.push_back(ReqInfo{peer, n, true});
   }
 }
-void post_recv(std::vector<MPI_Request>& reqs, char* p, int64_t bytes, int peer, int tag, MPI_Comm comm) {
+void post_recv(std::vector<MPI_Request>& reqs, std::vector<ReqInfo>& infos, char* p, int64_t bytes, int peer, int tag,
+               MPI_Comm comm) {
   for (int64_t off = 0; off < bytes; off += kMpiChunk) {
     MPI_Request r;
-    MOC_MPI_CHECK(MPI_Irecv(p + off, static_cast<int>(std::min(kMpiChunk, bytes - off)), MPI_BYTE, peer, tag, comm, &r));
+    const int64_t n = std::min(kMpiChunk, bytes - off);
+    MOC_MPI_CHECK(MPI_Irecv(p + off, static_cast<int>(n), MPI_BYTE, peer, tag, comm, &r));
     reqs.push_back(r);
+    infos.push_back(ReqInfo{peer, n, false});
   }
 }
 }  // namespace
@@ -105,19 +170,20 @@ void scatterv_bytes(const void* sendbuf, const std::vector<int64_t>& counts, con
   MPI_Comm_rank(comm, &rank);
   MPI_Comm_size(comm, &size);
   std::vector<MPI_Request> reqs;
+  std::vector<ReqInfo> infos;
   if (rank == root) {
     const char* s = static_cast<const char*>(sendbuf);
     for (int r = 0; r < size; ++r) {
       if (r == root) {
         if (counts[r] && recvbuf != s + displs[r]) std::memmove(recvbuf, s + displs[r], static_cast<size_t>(counts[r]));
       } else {
-        post_send(reqs, s + displs[r], counts[r], r, 11, comm);
+        post_send(reqs, infos, s + displs[r], counts[r], r, 11, comm);
       }
     }
   } else {
-    post_recv(reqs, static_cast<char*>(recvbuf), counts[rank], root, 11, comm);
+    post_recv(reqs, infos, static_cast<char*>(recvbuf), counts[rank], root, 11, comm);
   }
-  if (!reqs.empty()) MOC_MPI_CHECK(MPI_Waitall(static_cast<int>(reqs.size()), reqs.data(), MPI_STATUSES_IGNORE));
+  mpi_wait_all(reqs, "scatterv", &infos);
 }
 
 void gatherv_bytes(const void* sendbuf, int64_t count, void* recvbuf, const std::vector<int64_t>& counts,
@@ -126,19 +192,20 @@ void gatherv_bytes(const void* sendbuf, int64_t count, void* recvbuf, const std:
   MPI_Comm_rank(comm, &rank);
   MPI_Comm_size(comm, &size);
   std::vector<MPI_Request> reqs;
+  std::vector<ReqInfo> infos;
   if (rank == root) {
     char* d = static_cast<char*>(recvbuf);
     for (int r = 0; r < size; ++r) {
       if (r == root) {
         if (count && d + displs[r] != sendbuf) std::memmove(d + displs[r], sendbuf, static_cast<size_t>(count));
       } else {
-        post_recv(reqs, d + displs[r], counts[r], r, 12, comm);
+        post_recv(reqs, infos, d + displs[r], counts[r], r, 12, comm);
       }
     }
   } else {
-    post_send(reqs, static_cast<const char*>(sendbuf), count, root, 12, comm);
+    post_send(reqs, infos, static_cast<const char*>(sendbuf), count, root, 12, comm);
   }
-  if (!reqs.empty()) MOC_MPI_CHECK(MPI_Waitall(static_cast<int>(reqs.size()), reqs.data(), MPI_STATUSES_IGNORE));
+  mpi_wait_all(reqs, "gatherv", &infos);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -227,7 +294,7 @@ void SharedWindow::release_shares(const MpiContext& ctx) {
 void SharedWindow::fence() const {
   if (map_) return;  // one rank on the node
   MOC_MPI_CHECK(MPI_Win_sync(win_));
-  MOC_MPI_CHECK(MPI_Barrier(comm_));
+  barrier(comm_, "node window fence");
   MOC_MPI_CHECK(MPI_Win_sync(win_));
 }
 
@@ -269,7 +336,7 @@ SegmentWindow::~SegmentWindow() {
 void SegmentWindow::fence() const {
   if (win_ == MPI_WIN_NULL) return;
   MOC_MPI_CHECK(MPI_Win_sync(win_));
-  MOC_MPI_CHECK(MPI_Barrier(comm_));
+  barrier(comm_, "node window fence");
   MOC_MPI_CHECK(MPI_Win_sync(win_));
 }
 

@@ -4,8 +4,10 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 
 #include "moc/cpu_engine.hpp"
+#include "moc/runtime/watchdog.hpp"
 
 namespace moc {
 
@@ -15,7 +17,13 @@ constexpr int kTag = 21;
 }  // namespace
 
 MpiDeviceComm::~MpiDeviceComm() {
-  if (!reqs_.empty()) MPI_Waitall(static_cast<int>(reqs_.size()), reqs_.data(), MPI_STATUSES_IGNORE);
+  // never wait while an error unwinds: a peer may be the stuck party, and the caller is about to abort
+  if (!reqs_.empty() && std::uncaught_exceptions() == 0) {
+    try {
+      mpi_wait_all(reqs_, "MpiDeviceComm teardown", &infos_);
+    } catch (...) {
+    }
+  }
 }
 
 void* MpiDeviceComm::dev_alloc(int64_t bytes) {
@@ -36,17 +44,18 @@ void MpiDeviceComm::download(void* h, const void* d, int64_t bytes) {
 void MpiDeviceComm::group_start() { ++depth_; }
 void MpiDeviceComm::group_end() {
   if (--depth_ > 0 || reqs_.empty()) return;
-  mpi_check(MPI_Waitall(static_cast<int>(reqs_.size()), reqs_.data(), MPI_STATUSES_IGNORE), "MPI_Waitall");
-  reqs_.clear();
+  mpi_wait_all(reqs_, "the device comm's send/recv group", &infos_);
+  infos_.clear();
 }
 
 void MpiDeviceComm::send(const void* d, int64_t bytes, int peer) {
   const char* p = static_cast<const char*>(d);
   for (int64_t off = 0; off < bytes; off += kMpiChunk) {
     MPI_Request r;
-    mpi_check(MPI_Isend(p + off, static_cast<int>(std::min(kMpiChunk, bytes - off)), MPI_BYTE, peer, kTag, ctx_.world, &r),
-              "MPI_Isend");
+    const int64_t n = std::min(kMpiChunk, bytes - off);
+    mpi_check(MPI_Isend(p + off, static_cast<int>(n), MPI_BYTE, peer, kTag, ctx_.world, &r), "MPI_Isend");
     reqs_.push_back(r);
+    infos_.push_back(ReqInfo{peer, n, true});
   }
   if (depth_ == 0) group_end();
 }
@@ -54,9 +63,10 @@ void MpiDeviceComm::recv(void* d, int64_t bytes, int peer) {
   char* p = static_cast<char*>(d);
   for (int64_t off = 0; off < bytes; off += kMpiChunk) {
     MPI_Request r;
-    mpi_check(MPI_Irecv(p + off, static_cast<int>(std::min(kMpiChunk, bytes - off)), MPI_BYTE, peer, kTag, ctx_.world, &r),
-              "MPI_Irecv");
+    const int64_t n = std::min(kMpiChunk, bytes - off);
+    mpi_check(MPI_Irecv(p + off, static_cast<int>(n), MPI_BYTE, peer, kTag, ctx_.world, &r), "MPI_Irecv");
     reqs_.push_back(r);
+    infos_.push_back(ReqInfo{peer, n, false});
   }
   if (depth_ == 0) group_end();
 }
@@ -64,9 +74,11 @@ void MpiDeviceComm::recv(void* d, int64_t bytes, int peer) {
 void MpiDeviceComm::bcast(void* d, int64_t bytes, int root) { bcast_bytes(d, bytes, root, ctx_.world); }
 void MpiDeviceComm::allgather(const void* d_send, void* d_recv, int64_t bytes_each) {
   if (bytes_each >= kMpiChunk) throw Error("MpiDeviceComm::allgather: pieces must stay below 1 GiB");
-  mpi_check(MPI_Allgather(d_send, static_cast<int>(bytes_each), MPI_BYTE, d_recv, static_cast<int>(bytes_each), MPI_BYTE,
-                          ctx_.world),
-            "MPI_Allgather");
+  MPI_Request r;
+  mpi_check(MPI_Iallgather(d_send, static_cast<int>(bytes_each), MPI_BYTE, d_recv, static_cast<int>(bytes_each), MPI_BYTE,
+                           ctx_.world, &r),
+            "MPI_Iallgather");
+  mpi_wait(r, "MPI_Iallgather", "all-gather of " + watchdog::human_bytes(bytes_each) + " per rank");
 }
 void MpiDeviceComm::allreduce_max_u64(uint64_t* d, int64_t n) { moc::allreduce_max_u64(d, n, ctx_.world); }
 

@@ -4,9 +4,11 @@
 #include <omp.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <thread>
 
 #include "moc/device_comm.hpp"
 #include "moc/io.hpp"
@@ -189,6 +191,10 @@ DeviceBatchOut batch_cp(DeviceComm& dc, DeviceSearch& ds, const RecordBatch* rb,
 
 }  // namespace
 
+void DeviceComm::inject_stall(double seconds) {
+  std::this_thread::sleep_for(std::chrono::duration<double>(seconds));
+}
+
 DeviceScratch::~DeviceScratch() {
   for (Buf& b : dev_)
     if (b.p) dc_.dev_free(b.p);
@@ -347,6 +353,11 @@ DeviceBatchOut device_batch(DeviceComm& dc, DeviceSearch& ds, const RecordBatch*
     if (rank == 0) dc.wait_upload(dc.upload(d_plan, plan.data(), bytes));
     dc.bcast(d_plan, bytes, 0);
     dc.download(plan.data(), d_plan, bytes);
+    if (rank == 0) {  // the plan table reaches every peer (counted like device_batch_text's per-peer plans)
+      out.peer_bytes.assign(static_cast<size_t>(p), 0);
+      for (int r = 1; r < p; ++r) out.peer_bytes[r] += bytes;
+      out.sent_bytes += bytes * (p - 1);
+    }
   }
   const RankPlan& mine = plan[rank];
   char* d_block = sc.dev(kBlock, mine.block + 16);
@@ -375,7 +386,6 @@ DeviceBatchOut device_batch(DeviceComm& dc, DeviceSearch& ds, const RecordBatch*
     }
     sc.host(kHostResults, results_bytes(plan) + 16);  // the gather's page-locked buffer, ahead of the search
     hooks.begin("pack");  // host packing, and the waits for staging slots (a packing-bound distribution)
-    out.peer_bytes.assign(static_cast<size_t>(p), 0);
     dist.start();
     int64_t i = 0;
     for (size_t k = 0; k < rounds; ++k)
@@ -422,7 +432,7 @@ DeviceBatchOut device_batch(DeviceComm& dc, DeviceSearch& ds, const RecordBatch*
 }
 
 // ---- text batch: the root encodes every rank's slice straight from the input text into that rank's wire
-// block (page-locked, two blocks in turn), peers first and its own last; a block's pieces upload and leave
+// block (page-locked, two blocks in turn), its own first, then the peers'; a block's pieces upload and leave
 // over the comm lane while the next rank's slice is encoded. Each peer learns its plan from a 96-byte
 // message ahead of its pieces (the plan depends on the slice's length range, known after its encode).
 DeviceBatchOut device_batch_text(DeviceComm& dc, DeviceSearch& ds, const BulkParser* parser,
@@ -447,7 +457,6 @@ DeviceBatchOut device_batch_text(DeviceComm& dc, DeviceSearch& ds, const BulkPar
   if (rank == 0) {
     hooks.begin("fill");  // encode (host threads), and the waits for a block to be free again
     out.peer_bytes.assign(static_cast<size_t>(p), 0);
-    dist.start();
     const int64_t L1 = static_cast<int64_t>(parser->seq1().size());
     char* d_plan = sc.dev(kPlanBuf, kPlanBytes * p);
     RankPlan* h_plan = reinterpret_cast<RankPlan*>(sc.host(kHostPlan, kPlanBytes * p));
@@ -478,7 +487,11 @@ DeviceBatchOut device_batch_text(DeviceComm& dc, DeviceSearch& ds, const BulkPar
     FillReport whole;
     uvector<uint16_t> len16;
     for (int k = 0; k < p; ++k) {
-      const int r = (k + 1) % p;  // peers 1..p-1, then the root
+      // the root's own slice first: its block uploads (copy lane) while the peers' slices are encoded and
+      // sent, so the root's search waits for no encode or upload of its own once the last piece is out
+      // (before: peers first, the root's slice encoded and uploaded after all of them, the critical path)
+      const int r = k;
+      out.fill_order.push_back(r);
       const int hb = k % 2;
       if (block_up[hb] >= 0) dc.wait_upload_host(block_up[hb]);
       const AreaSlice& sl = slices[r];
@@ -527,6 +540,8 @@ DeviceBatchOut device_batch_text(DeviceComm& dc, DeviceSearch& ds, const BulkPar
       int last = -1;
       if (r != 0) {
         h_plan[r] = pl;
+        // the distribution time runs from the first byte on the wire (the first slice's encode is before it)
+        if (r == 1) dist.start();
         const int t = dc.upload(d_plan + kPlanBytes * r, h_plan + r, kPlanBytes);
         dc.wait_upload(t);
         dc.group_start();

@@ -30,6 +30,13 @@ __global__ __launch_bounds__(kCopyBlock) void copy1_kernel(const uint8_t* __rest
     dst[i] = src[i];
 }
 
+// One wave that idles until the device's constant-rate wall clock has advanced `ticks` (the comm-timeout
+// test hook, moc/device_comm.hpp inject_stall): bounded by construction, it stores nothing.
+__global__ __launch_bounds__(64) void spin_kernel(uint64_t ticks) {
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
 dim3 copy_grid(int64_t n) { return dim3(static_cast<unsigned>(std::clamp<int64_t>((n + kCopyBlock - 1) / kCopyBlock, 1, 2048))); }
 }  // namespace
 
@@ -48,6 +55,16 @@ void launch_copy(void* dst, const void* src, size_t bytes, hipStream_t stream) {
     hipLaunchKernelGGL(copy1_kernel, copy_grid(n), dim3(kCopyBlock), 0, stream,
                        static_cast<const uint8_t*>(src) + done, static_cast<uint8_t*>(dst) + done, n);
   }
+}
+
+void launch_spin(double seconds, hipStream_t stream) {
+  seconds = std::clamp(seconds, 0.0, 10.0);  // a test hook never holds the GPU for long
+  int device = 0, khz = 0;
+  if (hipGetDevice(&device) != hipSuccess || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess ||
+      khz <= 0)
+    khz = 100000;  // the MI355X's 100 MHz constant clock
+  const auto ticks = static_cast<uint64_t>(seconds * 1e3 * khz);
+  hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, stream, ticks);
 }
 
 bool kernel_copy_fits(const void* dst, const void* src, size_t bytes) {

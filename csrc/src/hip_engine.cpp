@@ -315,10 +315,7 @@ void HipEngine::set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, S
   prof16_i16_ = t16 && prof.i16;
   prof16_window_ = t16 && !prof16_i16_ ? static_cast<int32_t>(window) : 0;
   prof16_entries_ = t16 ? static_cast<int64_t>(prof.entries.size()) : 0;
-  prof16_lds_bytes_ = t16 ? static_cast<int32_t>(whole ? pbytes
-                                                       : ((2 * ((kAlphabet - 1) * window + dev::kProf16Overhang)) + 15) &
-                                                             ~int64_t{15})
-                          : 0;
+  prof16_lds_bytes_ = t16 ? dev::tile16_profile_lds_bytes(L1, overhang, prof16_i16_) : 0;
   pbytes = (2 * static_cast<int64_t>(prof.entries.size()) + 15) & ~int64_t{15};
   prof16_overhang_ = t16 ? static_cast<int>(overhang) : 0;
   // widened entries (two int16 halves per column: one packed add per lane and step) where the doubled image
@@ -327,7 +324,6 @@ void HipEngine::set_problem(const Weights& w, const uint8_t* seq1, int64_t L1, S
     const char* v = std::getenv("MOC_TILE16_WIDE");
     return !(v && std::atoi(v) == 0);
   }();
-  if (prof16_i16_) prof16_lds_bytes_ = static_cast<int32_t>(pbytes);  // the whole image (widened: twice)
   prof16_wide_ = t16 && (whole || prof16_i16_) && (wide_env || prof16_i16_) &&
                  dev::tile16_lds_bytes(2 * static_cast<int64_t>(prof16_lds_bytes_), L1) <= dev::kProf16MaxLds;
   const size_t total = t16 ? prof_off + static_cast<size_t>(pbytes) : prof_off;

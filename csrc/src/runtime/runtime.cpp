@@ -11,6 +11,7 @@
 #include "moc/runtime/log.hpp"
 #include "moc/runtime/timer.hpp"
 #include "moc/runtime/trace.hpp"
+#include "moc/runtime/watchdog.hpp"
 
 namespace moc {
 
@@ -112,7 +113,10 @@ void log_set_level(const std::string& name) {
   else if (name == "debug") g_level = LogLevel::Debug;
   else throw Error("unknown log level '" + name + "'");
 }
-void log_set_rank(int rank) { g_rank = rank; }
+void log_set_rank(int rank) {
+  g_rank = rank;
+  watchdog::set_rank(rank);
+}
 LogLevel log_level() { return g_level; }
 
 void logf(LogLevel lvl, const char* fmt, ...) {
@@ -181,6 +185,7 @@ void trace_name_thread(const char* name) {
 void PhaseTimer::begin(const std::string& name) {
   if (open_) end();
   cur_ = name;
+  watchdog::set_phase(cur_.c_str());
   sw_.reset();
   sw_.start();
   trace_push(cur_.c_str());

@@ -14,12 +14,14 @@
 #include <vector>
 
 #include "moc/cpu_engine.hpp"
+#include "moc/device.hpp"
 #include "moc/io.hpp"
 #include "moc/kernel_bounds.hpp"
 #include "moc/partition.hpp"
 #include "moc/problem.hpp"
 #include "moc/runtime/kfd_topology.hpp"
 #include "moc/runtime/releaser.hpp"
+#include "moc/runtime/watchdog.hpp"
 #include "moc/score_table.hpp"
 #include "moc/wire.hpp"
 #include "../apps/text_cut.hpp"
@@ -430,6 +432,75 @@ void test_profile16() {
       }
     }
   }
+}
+
+// pv.prof16_bytes of a whole-image view is an LDS size for every Seq1 length the engine accepts (up to 2^30):
+// an int16 profile of a long Seq1 (|Dt| 128..511) used to be sized in int32 from the whole profile, which
+// wrapped past L1 ~ 43 M and could pass the widened-image check with a negative size.
+void test_profile16_lds_bytes() {
+  const int64_t lengths[] = {1, 26, 1489, 2976, 3052, 3100, 20000, 150000, 43'000'000, 60'000'000, 86'000'000,
+                             100'000'000, int64_t{1} << 30};
+  for (int64_t L1 : lengths)
+    for (int64_t oh : {int64_t{dev::kProf16Overhang}, int64_t{2 * dev::kProf16Overhang}})
+      for (bool i16 : {false, true}) {
+        const int32_t b = dev::tile16_profile_lds_bytes(L1, oh, i16);
+        CHECK(b > 0 && b <= dev::kProf16MaxLds && b % 16 == 0);
+        // the widened-image check of HipEngine::set_problem only passes where the doubled image fits
+        const bool wide = dev::tile16_lds_bytes(2 * static_cast<int64_t>(b), L1) <= dev::kProf16MaxLds;
+        if (wide) CHECK(2 * (26 * L1 + oh) <= dev::kProf16MaxLds);
+      }
+  // input3's Seq1: the whole byte-pair profile is the image; an int16 one needs the widened image to fit
+  CHECK(dev::tile16_profile_lds_bytes(1489, 512, false) == ((2 * (26 * 1489 + 512)) + 15) / 16 * 16);
+}
+
+// The comm deadline: a wait that completes returns; one that does not throws CommTimeout naming the
+// operation, what is outstanding, and the phase; expire runs first; 0 disables the deadline.
+void test_watchdog() {
+  watchdog::set_timeout_s(0.05);
+  watchdog::set_rank(3);
+  watchdog::set_phase("gather");
+  int n = 0;
+  watchdog::WaitSpec spec;
+  spec.what = "test op";
+  watchdog::wait([&] { return ++n > 100; }, spec);
+  CHECK(n == 101);
+  bool expired = false;
+  spec.outstanding = [] { return std::string("recv 24 B from rank 2"); };
+  spec.expire = [&] { expired = true; };
+  for (watchdog::Poll poll : {watchdog::Poll::Busy, watchdog::Poll::Backoff}) {
+    spec.poll = poll;
+    expired = false;
+    std::string msg;
+    try {
+      watchdog::wait([] { return false; }, spec);
+    } catch (const CommTimeout& e) {
+      msg = e.what();
+    }
+    CHECK(expired);
+    CHECK(msg.find("rank 3") != std::string::npos && msg.find("phase 'gather'") != std::string::npos &&
+          msg.find("test op") != std::string::npos && msg.find("from rank 2") != std::string::npos);
+  }
+  int checks = 0;
+  spec.check = [&] {
+    if (++checks == 3) throw Error("async error");
+  };
+  spec.poll = watchdog::Poll::Backoff;
+  watchdog::set_timeout_s(10);
+  std::string msg;
+  try {
+    watchdog::wait([] { return false; }, spec);
+  } catch (const Error& e) {
+    msg = e.what();
+  }
+  CHECK(msg == "async error");
+  watchdog::set_timeout_s(0);  // disabled: a slow wait completes
+  int m = 0;
+  watchdog::WaitSpec plain;
+  watchdog::wait([&] { return ++m > 200000; }, plain);
+  CHECK(m == 200001);
+  CHECK(watchdog::human_bytes(24) == "24 B" && watchdog::human_bytes(3 << 20) == "3.0 MiB");
+  watchdog::set_timeout_s(watchdog::kDefaultTimeoutS);
+  watchdog::set_phase("");
 }
 
 void test_formatter() {
@@ -1432,7 +1503,8 @@ int main() {
       {"kfd_topology", test_kfd_topology}, {"kfd_topology_8gpu", test_kfd_topology_8gpu},
       {"cutter_count_ahead", test_cutter_count_ahead}, {"swipe_replay_bounds", test_swipe_replay_bounds},
       {"short_replay_bounds", test_short_replay_bounds}, {"tile16_replay_bounds", test_tile16_replay_bounds},
-      {"tile16_key32_replay", test_tile16_key32_replay}, {"tile16_i16_replay", test_tile16_i16_replay}};
+      {"tile16_key32_replay", test_tile16_key32_replay}, {"tile16_i16_replay", test_tile16_i16_replay},
+      {"profile16_lds_bytes", test_profile16_lds_bytes}, {"watchdog", test_watchdog}};
   for (const auto& t : tests) {
     const int before = g_failed;
     t.second();

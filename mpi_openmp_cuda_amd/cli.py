@@ -26,9 +26,11 @@ def main(argv=None) -> int:
     ap.add_argument("--backend", default="auto", choices=["auto", "hip", "cpu"])
     ap.add_argument("--transport", default="auto", choices=["auto", "shm", "bcast"],
                     help="shm: node-shared window (one node); bcast: every record broadcast (--partition=offsets "
-                         "only). Record slices between nodes: ./final --transport=rccl")
-    ap.add_argument("--partition", default="records", choices=["records", "offsets"],
-                    help="records: cost-balanced record ranges; offsets: context parallel (split every record)")
+                         "only). Record slices between nodes: ./final --transport=rccl (the retired p2p transport "
+                         "of this driver moved into ./final's device batch)")
+    ap.add_argument("--partition", default="auto", choices=["auto", "records", "offsets"],
+                    help="records: cost-balanced record ranges (one node); offsets: context parallel (split every "
+                         "record; the only partition across nodes here). auto: records on one node, else offsets")
     ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"])
     ap.add_argument("--semantics", default="reference", choices=["reference", "spec"])
     ap.add_argument("--threads", type=int, default=0)

@@ -32,6 +32,25 @@ class DistContext:
         return self.rank == 0
 
 
+def comm_timeout_s() -> float:
+    """The job's deadline for any wait on another rank (seconds): MOC_COMM_TIMEOUT, as `./final
+    --comm-timeout` (csrc/include/moc/runtime/watchdog.hpp), default 300; <= 0 leaves torch's own default."""
+    try:
+        return float(os.environ.get("MOC_COMM_TIMEOUT", "300"))
+    except ValueError:
+        return 300.0
+
+
+def pg_timeout_kwargs() -> dict:
+    """init_process_group's `timeout=`: a collective stuck on a peer raises (RCCL: the process group's
+    watchdog aborts the communicator) instead of hanging the job (reference: a failing rank exit(1)s and
+    its peers block forever, /root/reference/cudaFunctions.cu:15-33)."""
+    import datetime
+
+    t = comm_timeout_s()
+    return {"timeout": datetime.timedelta(seconds=t)} if t > 0 else {}
+
+
 def init(backend: str = "auto", use_gpu: Optional[bool] = None) -> DistContext:
     """Initialises the default process group from the environment (no-op for a single process)."""
     import torch
@@ -51,6 +70,7 @@ def init(backend: str = "auto", use_gpu: Optional[bool] = None) -> DistContext:
     ctx = DistContext(rank, world, local_rank, backend if world > 1 else "none", dev)
     if world > 1 and not dist.is_initialized():
         kw = {"device_id": dev} if backend == "nccl" else {}
+        kw.update(pg_timeout_kwargs())
         # gloo prints its connection banner on stdout; stdout must carry results only (main.c:204), so
         # the native banner goes to stderr while the group is set up.
         import sys

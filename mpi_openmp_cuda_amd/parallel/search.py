@@ -61,10 +61,12 @@ class NodeWindow:
 
 class DistributedSearch:
     def __init__(self, ctx: D.DistContext, backend: str = "auto", transport: str = "auto", threads: int = 0,
-                 device: Optional[int] = None, partition: str = "records"):
+                 device: Optional[int] = None, partition: str = "auto"):
         self.ctx = ctx
+        if partition == "auto":  # record slices need the node-shared window; across nodes split offsets
+            partition = "records" if (ctx.single_node and transport in ("auto", "shm")) else "offsets"
         if partition not in ("records", "offsets"):
-            raise ValueError("partition must be records|offsets")
+            raise ValueError("partition must be auto|records|offsets")
         self.partition = partition
         if backend == "auto":
             backend = "hip" if device_count() > 0 else "cpu"

@@ -72,6 +72,48 @@ def test_fault_injection_aborts_cleanly(phase, rank):
     assert b"injected fault" in r.stderr or phase == "parse"
 
 
+# ---- comm deadline: a rank that is alive but stuck ends the job with a diagnosis
+
+@pytest.mark.parametrize("transport,flags,phase,rank", [
+    ("rccl-emul", [], "distribute", 2),          # the device batch driver over MPI point-to-point
+    ("rccl-emul", ["--batch-records=7"], "compute", 1),  # streamed device batches
+    ("rccl-emul", ["--partition=offsets"], "compute", 2),  # context parallel: bcast + MAX all-reduce
+    ("mpi", [], "compute", 1),                    # Scatterv / Gatherv flow
+    ("shm", [], "compute", 2),                    # node-shared slices: host-table collectives
+])
+def test_comm_timeout_names_stuck_rank(transport, flags, phase, rank):
+    import time
+
+    # reference: a failing rank exit(1)s without MPI_Abort and its peers hang in the next collective
+    # (/root/reference/cudaFunctions.cu:15-33, main.c:174,195-197); here a stalled rank (MOC_STALL_S: long
+    # enough that only the deadline can end the job) is caught by its peers' deadline-polled waits
+    t0 = time.time()
+    try:
+        r = run_final(["--backend=cpu", f"--transport={transport}", "--comm-timeout=2",
+                       f"--inject-fault=stall:{phase}:{rank}", *flags], stdin_path=input_path(3), np_=3,
+                      env={"MOC_STALL_S": "60"}, timeout=45)
+    except subprocess.TimeoutExpired:
+        pytest.fail("a stalled rank hung the job past its comm deadline")
+    err = r.stderr.decode()
+    assert r.returncode != 0, err
+    assert time.time() - t0 < 30
+    assert "injected rank stall" in err
+    fatal = [l for l in err.splitlines() if "fatal: comm timeout" in l]
+    assert fatal, err[-2000:]
+    # a peer names the phase it waited in; when the wait was point-to-point, the stalled rank too
+    assert all(re.search(r"in phase '\w+'", l) for l in fatal), fatal
+    if transport in ("rccl-emul", "mpi") and not flags:
+        assert any(f"rank {rank}" in l.split("outstanding:")[-1] for l in fatal), fatal
+
+
+def test_comm_timeout_flag_in_help_and_default_jobs_unaffected():
+    r = run_final(["--help"], stdin_bytes=b"")
+    assert b"--comm-timeout" in r.stdout
+    # a tiny deadline does not fire on a healthy job (waits that complete never see it)
+    r = run_final(["--backend=cpu", "--transport=rccl-emul", "--comm-timeout=5"], stdin_path=input_path(3), np_=3)
+    assert r.returncode == 0 and r.stdout.decode() == expected(3)
+
+
 def test_timing_json():
     import json
 
@@ -437,6 +479,9 @@ def test_rccl_transport_timing_fields(np_, stream):
         assert all(b > 0 for b in d["peer_sent_bytes"][1:]) and d["distribute_ms"] > 0
         assert all(b > 0 for b in d["rank_sent_bytes"][1:])  # every peer sends its results back
         assert all(g > 0 for g in d["peer_distribute_gbps"][1:])
+    # the root encodes (and uploads) its own slice first, then the peers' in rank order: its search waits for
+    # no encode of its own behind the last peer's pieces (device_batch.cpp, device_batch_text)
+    assert d["fill_order"] == list(range(np_))
 
 
 @pytest.mark.parametrize("np_", [2, 3])

@@ -47,9 +47,30 @@ def test_gloo_context_parallel(transport, i, nproc):
 
 def test_record_slices_between_ranks_belong_to_final():
     # one distributed implementation per transport: payload sends between ranks are ./final's (rccl)
-    r = torchrun(2, ["--backend=cpu", "--dist-backend=gloo", "--transport=bcast", f"--input={input_path(1)}"],
-                 timeout=120)
+    r = torchrun(2, ["--backend=cpu", "--dist-backend=gloo", "--transport=bcast", "--partition=records",
+                     f"--input={input_path(1)}"], timeout=120)
     assert r.returncode != 0 and b"--transport=rccl" in r.stderr
+
+
+def test_bcast_transport_defaults_to_offsets_partition():
+    # the default partition (auto) with the transport that crosses nodes splits offsets, so a multi-node
+    # launch on default flags runs instead of failing the records/bcast check
+    r = torchrun(2, ["--backend=cpu", "--dist-backend=gloo", "--transport=bcast", f"--input={input_path(3)}"])
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    assert r.stdout.decode() == expected(3)
+
+
+def test_process_group_timeout_from_env(monkeypatch):
+    import datetime
+
+    from mpi_openmp_cuda_amd.parallel import dist as D
+
+    monkeypatch.setenv("MOC_COMM_TIMEOUT", "7.5")
+    assert D.pg_timeout_kwargs() == {"timeout": datetime.timedelta(seconds=7.5)}
+    monkeypatch.setenv("MOC_COMM_TIMEOUT", "0")
+    assert D.pg_timeout_kwargs() == {}
+    monkeypatch.delenv("MOC_COMM_TIMEOUT")
+    assert D.comm_timeout_s() == 300.0
 
 
 def test_single_process_cli_stdin():

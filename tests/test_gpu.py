@@ -1,5 +1,7 @@
 """GPU (MI355X / gfx950) tests: HIP engine == CPU engine == goldens. Numerics oracle: the CPU engine,
 itself pinned to the brute-force replay of the reference loops (test_oracles.py)."""
+import json
+
 import numpy as np
 import pytest
 
@@ -764,6 +766,39 @@ def test_final_cli_rccl_streaming(tmp_path, extra):
     if "--skip-records=777" in extra:
         want = "".join(want.splitlines(keepends=True)[777:])
     assert r.stdout.decode() == want
+
+
+def test_final_cli_rccl_event_pool_bounded(tmp_path):
+    # the rccl device comm's completion events are pooled: over a streamed job of >= 50 batches (2 uploads
+    # + marks per piece, MOC_SEND_CHUNK: many pieces per batch) the events alive stay at the pipeline's
+    # depth instead of growing per piece (reference: a cudaMalloc leaked per record, cudaFunctions.cu:206)
+    prob = make_synthetic("input6", 60_000, seed=11)
+    path = tmp_path / "in.txt"
+    path.write_text(prob.to_text())
+    r = run_final(["--backend=hip", "--transport=rccl", f"--input={path}", "--batch-records=1000", "--timing"],
+                  stdin_bytes=b"", np_=1, env={"MOC_SEND_CHUNK": "2640"})
+    assert r.returncode == 0, r.stderr.decode()
+    assert r.stdout.decode() == format_results(search_cpu(prob))
+    d = json.loads([l for l in r.stderr.decode().splitlines() if l.startswith("{")][-1])
+    assert d["batches"] >= 50
+    assert 0 < d["comm_events_live"] <= 16, d["comm_events_live"]
+
+
+def test_final_cli_rccl_comm_timeout_fires(tmp_path):
+    # the RCCL comm's poll path driven to its deadline at world size 1: a bounded spin kernel (2 s) holds the
+    # comm lane at the start of the gather; the rank's download waits on it with a 0.3 s deadline, aborts the
+    # communicator and exits non-zero naming the wait and the phase
+    r = run_final(["--backend=hip", "--transport=rccl", "--comm-timeout=0.3", "--inject-fault=stall-device:gather"],
+                  stdin_path=input_path(3), np_=1, env={"MOC_STALL_S": "2"}, timeout=60)
+    err = r.stderr.decode()
+    assert r.returncode != 0, err
+    assert "injected device comm lane stall" in err
+    line = [l for l in err.splitlines() if "fatal: comm timeout" in l]
+    assert line and "comm lane" in line[0] and "phase 'gather'" in line[0], err[-2000:]
+    # and a deadline that the same stall fits inside lets the job finish with the golden output
+    r = run_final(["--backend=hip", "--transport=rccl", "--comm-timeout=20", "--inject-fault=stall-device:gather"],
+                  stdin_path=input_path(3), np_=1, env={"MOC_STALL_S": "0.5"}, timeout=60)
+    assert r.returncode == 0 and r.stdout.decode() == expected(3), r.stderr.decode()[-2000:]
 
 
 def _long_problem(L1, lengths, seed):
