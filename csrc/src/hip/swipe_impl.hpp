@@ -204,78 +204,91 @@ __device__ __forceinline__ Result swipe_lane(const unsigned char* smem, const ui
     }
   }
 
-  // ---- per-lane selection over the record's offsets: 32-bit keys (score+2^15 | ~(o<<KB | k)), 0 = none.
-  //      The valid offsets are prefixes: the un-mutated candidate at o < lim0 (o <= last = L1-L2 under
-  //      the spec semantics or when L2 == L1, else o < last), the mutants at o < lim1 = last (L2 >= 2).
-  //      Running sums carry the 2^15 bias, so a key is one shift-or of them; the per-pair parts (D_o(L2),
-  //      the best mutant's d and k) come out of the packed sums with one op per two offsets.
-  //      RK: the low bits are ~(o << 1 | mutated); bd keeps the winning mutant's D for the k re-walk.
-  //      Offsets below L1 - max_l2 are valid for every lane that searches (`on`): a group of 8 offsets
-  //      entirely below it skips the limit tests (wave-uniform), the others apply them per lane.
+  // ---- per-lane selection over the record's offsets: 32-bit keys (score + 2^15) << 16 | ~(o << KB | k),
+  //      0 = none (RK: the low bits are ~(o << 1 | mutated)). The offsets run from the top down through one
+  //      chain value C_o = (Tot_o + 2^15) << 16 + ~(o << KB | 0): the un-mutated candidate's key IS C_o, and
+  //      the best mutant's key is C_{o+1} + ((d << 16) | (KMASK - k)) + 1 (d = its D_o(k)); so per offset one
+  //      op takes D_o(L2) << 16 (plus the step of the index field) out of the packed sums, one add moves the
+  //      chain, one byte permute builds the mutant's (d, k) word, one add3 its key and one max3 selects —
+  //      five full-rate ops, half the former epilogue (round-5 roofline: a third of the kernel's issue).
+  //      Mod-2^32 arithmetic is exact: every Tot_o + 2^15 and score + 2^15 fits 16 bits (the swipe_keys
+  //      bound), and the index field never carries into the score.
+  //      The valid offsets are prefixes: the un-mutated candidate at o < lim0 (o <= last = L1-L2 under the
+  //      spec semantics or when L2 == L1, else o < last), the mutants at o < lim1 = last (L2 >= 2). Below
+  //      wlo every searching lane's candidates are valid (no limit tests), from whi up none is (the chain
+  //      only): both wave-uniform, applied per group of 4 offsets.
   const int last = L1 - L2;
-  const int lim0 = on ? last + ((sem == static_cast<int>(Semantics::Spec) || L2 == L1) ? 1 : 0) : 0;
+  const bool spec = sem == static_cast<int>(Semantics::Spec);
+  const int lim0 = on ? last + ((spec || L2 == L1) ? 1 : 0) : 0;
   const int lim1 = on && L2 >= 2 ? last : 0;
-  const int all_valid = L1 - max_l2;
-  // D_o(L2) pairs from the final running sums: (E - (KMASK - steps)) >> KB (RK: E itself)
-  const short eb = static_cast<short>(RK ? 0 : KMASK - steps);
-  const s16x2 ebias = {eb, eb};
-  // packed per offset pair (one op per two offsets): D_o(L2), the best mutant's D_o(k) and its KMASK - k
+  const int wlo = __builtin_amdgcn_ballot_w64(on && L2 < 2) != 0 ? 0 : L1 - steps;
+  const int wmin = 255 - wave_max_small(on ? 255 - L2 : 0);  // the wave's shortest searching record
+  const int whi = max(L1 - wmin + (spec ? 1 : 0), 1);
+  (void)max_l2;
+  // packed per offset pair (one op per two offsets): D_o(L2) (E >> KB: E = D * 2^KB + KMASK - steps and
+  // steps <= KMASK), the best mutant's D_o(k) and its KMASK - k
   uint32_t dq2[NP], bd2[NP], bl2[NP];
 #pragma unroll
   for (int q = 0; q < NP; ++q) {
-    dq2[q] = RK ? E2[q] : as_u32((as_s16x2(E2[q]) - ebias) >> static_cast<short>(KB));
+    dq2[q] = RK ? E2[q] : as_u32(as_s16x2(E2[q]) >> static_cast<short>(KB));
     bd2[q] = RK ? B2[q] : as_u32(as_s16x2(B2[q]) >> static_cast<short>(KB));
-    bl2[q] = B2[q] & (static_cast<uint32_t>(KMASK) * 0x10001u);
+    bl2[q] = RK ? 0u : B2[q] & (static_cast<uint32_t>(KMASK) * 0x10001u);
   }
+  constexpr uint32_t kStep = 1u << KB;  // ~(o << KB) - ~((o + 1) << KB)
   uint32_t best = 0;
-  int bd = 0;  // RK: D_o(k) of the best mutant so far
-  uint32_t tot = static_cast<uint32_t>(anchor + 32768);  // Tot_{o+1} + 2^15 entering offset o
-  auto offset = [&](const int o, const bool masked) {
-    const int hi = o & 1;
-    const uint32_t Pn = tot;  // Tot_{o+1} + 2^15
-    const uint32_t Po = Pn + static_cast<uint32_t>(hi ? static_cast<int>(dq2[o >> 1]) >> 16
-                                                      : static_cast<int>(static_cast<short>(dq2[o >> 1] & 0xffffu)));
-    tot = Po;  // suffix pass: Tot_o = Tot_{o+1} + D_o(L2)
-    const uint32_t kLow0 = 0xffffu - (static_cast<uint32_t>(o) << KB);  // ~(o << KB | 0)
-    const uint32_t kLow1 = kLow0 - KMASK;  // its low KB bits are 0: ~(o << KB | k) = kLow1 | (KMASK - k)
-    uint32_t k0 = (Po << 16) | kLow0;
-    const int dbest = hi ? static_cast<int>(bd2[o >> 1]) >> 16 : static_cast<int>(static_cast<short>(bd2[o >> 1] & 0xffffu));
-    const uint32_t low = RK ? kLow0 - 1u : kLow1 | (hi ? bl2[o >> 1] >> 16 : bl2[o >> 1] & 0xffffu);
-    uint32_t k1 = ((Pn + static_cast<uint32_t>(dbest)) << 16) | low;
-    if (masked) {
+  // C_NOFF from the anchor diagonal Tot_NOFF (the index field may borrow: only C_o for o < NOFF is a key)
+  uint32_t C = (static_cast<uint32_t>(anchor + 32768) << 16) + (0xffffu - (static_cast<uint32_t>(NOFF) << KB));
+  auto offset = [&](const int o, const int mode) {  // mode 0: valid everywhere, 1: limit tests, 2: chain only
+    const int q = o >> 1;
+    const bool hi = o & 1;
+    const uint32_t ds = hi ? (dq2[q] & 0xffff0000u) | kStep : (dq2[q] << 16) | kStep;
+    if (mode == 2) {
+      C += ds;
+      return;
+    }
+    // (d << 16) | (KMASK - k): the halves of the pair's packed D and k words (RK: d << 16)
+    const uint32_t m = RK ? (hi ? bd2[q] & 0xffff0000u : bd2[q] << 16)
+                          : __builtin_amdgcn_perm(bd2[q], bl2[q], hi ? 0x07060302u : 0x05040100u);
+    uint32_t k1 = C + m + 1u;  // the best mutant of offset o, from C_{o+1}
+    C += ds;                   // C_o
+    uint32_t k0 = C;           // the un-mutated candidate of offset o
+    if (mode == 1) {
       k0 = o < lim0 ? k0 : 0u;
       k1 = o < lim1 ? k1 : 0u;
     }
-    const uint32_t nb = max(best, max(k0, k1));
-    if (RK) bd = (nb == k1 && k1 != 0u) ? dbest : bd;
-    best = nb;
+    best = max(best, max(k0, k1));
   };
-  // groups of 8 offsets, from the top: a group entirely below L1 - max_l2 needs no limits (wave-uniform test)
+  // groups of 4 offsets, from the top (one wave-uniform branch per group, not per offset)
 #pragma unroll
-  for (int g = (NOFF - 1) / 8; g >= 0; --g) {
-    if (8 * g + 7 < all_valid) {
+  for (int g = NOFF / 4 - 1; g >= 0; --g) {
+    if (4 * g >= whi) {
 #pragma unroll
-      for (int o = 8 * g + 7; o >= 8 * g; --o) offset(o, false);
+      for (int o = 4 * g + 3; o >= 4 * g; --o) offset(o, 2);
+    } else if (4 * g + 3 >= wlo) {
+#pragma unroll
+      for (int o = 4 * g + 3; o >= 4 * g; --o) offset(o, 1);
     } else {
 #pragma unroll
-      for (int o = 8 * g + 7; o >= 8 * g; --o) offset(o, true);
+      for (int o = 4 * g + 3; o >= 4 * g; --o) offset(o, 0);
     }
   }
   if (!on) best = 0u;
   int kw = 0;  // RK: the winning mutant's k
   if (RK) {
-    // the first k of the winning offset's diagonal whose D_o(k) is the best D (k < L2: a best D reached
-    // only at k >= L2 equals D_o(L2), and then the un-mutated candidate wins the tie)
+    // the first k of the winning offset's diagonal with the largest D_o(k): a mutant wins only with a D
+    // above D_o(L2) (at k >= L2 the sums stay D_o(L2), and the un-mutated candidate wins that tie), so
+    // that k is below L2
     const bool walk = best != 0u && ((0xffffu - (best & 0xffffu)) & 1u);
     if (__builtin_amdgcn_ballot_w64(walk) != 0) {  // wave-uniform
       const int ow = static_cast<int>((0xffffu - (best & 0xffffu)) >> 1);
-      int run = 0;
+      int run = 0, top = INT32_MIN;
 #pragma unroll
       for (int i = 0; i < 4 * L2W; ++i) {
         if (i >= steps) break;  // wave-uniform
         const int c = (wd[i >> 2] >> (8 * (i & 3))) & 0xff;
         run += *reinterpret_cast<const short*>(smem + __umul24(c, stride) + 2 * (ow + i));  // copy 0: column ow + i
-        kw = (kw == 0 && run == bd) ? i + 1 : kw;
+        kw = run > top ? i + 1 : kw;
+        top = max(top, run);
       }
     }
   }
