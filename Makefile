@@ -48,7 +48,7 @@ HIP_OBJS  := $(patsubst csrc/src/%.hip,$(OBJ)/%.o,$(HIP_SRCS))
 # swipe kernel instances: one code object per (letter form, offsets per lane), from one source
 # (csrc/src/hip/swipe_group.inc) — HIP loads only the objects whose kernels a job launches
 SWIPE_GROUP := csrc/src/hip/swipe_group.inc
-SWIPE_NOFFS := 8 16 24 32 40 48 56 64
+SWIPE_NOFFS := 4 8 12 16 20 24 28 32 36 40 44 48 52 56 60 64
 SWIPE_OBJS  := $(foreach lf,0 2,$(foreach no,$(SWIPE_NOFFS),$(OBJ)/hip/swipe_lf$(lf)_n$(no).o))
 COMM_OBJS := $(OBJ)/comm/comm.o $(OBJ)/comm/mpi_device_comm.o
 RCCL_OBJS := $(OBJ)/comm/rccl_comm.o

@@ -208,8 +208,13 @@ bool configure_short(int64_t L1, int64_t min_l2, int64_t max_l2, ShortArgs& a);
 // returns false unless every record fits (|Seq1| <= 200, |Seq2| <= 32, int16-exact weights).
 // `hbm`: the records are in device memory (512-record tiles: more blocks per CU, 3.06 vs 2.69 T cells/s on
 // input6); host-resident batches stream in 1024-record tiles (fewer PCIe read requests per record).
+// `spec`: the batch runs under the spec semantics (one more offset per record, bug B8); the offsets per lane
+// follow it (swipe_offsets), the records it accepts do not.
 bool configure_swipe(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs_weight, ShortArgs& a,
-                     bool hbm = false);
+                     bool hbm = false, bool spec = true);
+// Offsets a record's candidates occupy in the swipe kernel: o < L1 - L2 (the reference's exclusive bound,
+// cudaFunctions.cu:116), o <= L1 - L2 under the spec semantics, the single o = 0 when L2 == L1.
+inline int64_t swipe_offsets(int64_t L1, int64_t L2, bool spec) { return L2 < L1 ? L1 - L2 + (spec ? 1 : 0) : 1; }
 void launch_swipe(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStream_t stream);
 // Key form (moc::bounds::kFormSwipe*) the swipe kernel takes for such a batch, 0 when it cannot take it
 // by its integer bounds (configure_swipe may still refuse it for the LDS budget).

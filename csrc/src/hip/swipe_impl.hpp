@@ -327,6 +327,7 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
   };
   auto tile_size = [&](int64_t t) -> int64_t { return t < a.tail_from ? a.tile_records : a.tail_records; };
   const int sem = pv.semantics;
+  const bool spec = sem == static_cast<int>(Semantics::Spec);
 
   // ---- tile fetch: the next tile's lengths and letters are loaded into registers while the current
   //      tile is being scored, so the PCIe / HBM read latency hides behind the compute (the streaming
@@ -502,8 +503,7 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
         rs = shift_b + loff[rl];  // byte position in LDS
         L2 = loff[rl + 1] - loff[rl];
       }
-      const int need = L2 <= L1 ? L1 - L2 + 1 : 1;
-      const bool mine = in && need <= NOFF;  // others belong to the tile kernel (mixed batches)
+      const bool mine = in && (L2 < L1 ? L1 - L2 + (spec ? 1 : 0) : 1) <= NOFF;  // others belong to the tile kernel (mixed batches)
       const bool on = mine && L2 <= L1;
       uint32_t wd[NW];
       record_words<NW>(reinterpret_cast<const uint32_t*>(codes_l), rs, L2, on, wd);
@@ -678,6 +678,7 @@ __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, S
   swipe_build_tables<RK, KB, NOFF, L2W>(smem, pv, threadIdx.x, kBlockD);
   __syncthreads();  // the only barrier: tables complete
   const int lane = threadIdx.x & 63;
+  const bool spec = pv.semantics == static_cast<int>(Semantics::Spec);
   const int L1 = pv.L1;
   const int64_t n = a.n, n_tiles = (n + 63) >> 6;
   const int64_t waves = static_cast<int64_t>(gridDim.x) * (kBlockD / 64);
@@ -732,7 +733,7 @@ __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, S
     const int64_t r = (t << 6) + lane;
     const int L2 = static_cast<int>(P33 ? o1 : o1 - o0);
     const bool in = r < n;
-    const bool mine = in && (L2 <= L1 ? L1 - L2 + 1 : 1) <= NOFF;  // others belong to the tile kernel
+    const bool mine = in && (L2 < L1 ? L1 - L2 + (spec ? 1 : 0) : 1) <= NOFF;  // others belong to the tile kernel
     const bool on = mine && L2 <= L1;
     uint32_t wd[L2W];
     if constexpr (P33) {
@@ -865,7 +866,9 @@ bool launch_swipe_noff(const ProblemView& pv, const ShortArgs& b, const SwipeLay
 #define MOC_SWIPE_FN(LF, NO) MOC_SWIPE_FN_(LF, NO)
 #define MOC_SWIPE_PRELOAD_FN_(LF, NO) preload_swipe_lf##LF##_n##NO
 #define MOC_SWIPE_PRELOAD_FN(LF, NO) MOC_SWIPE_PRELOAD_FN_(LF, NO)
-#define MOC_SWIPE_FOR_NOFF(X, LF) X(LF, 8) X(LF, 16) X(LF, 24) X(LF, 32) X(LF, 40) X(LF, 48) X(LF, 56) X(LF, 64)
+#define MOC_SWIPE_FOR_NOFF(X, LF)                                                                          \
+  X(LF, 4) X(LF, 8) X(LF, 12) X(LF, 16) X(LF, 20) X(LF, 24) X(LF, 28) X(LF, 32) X(LF, 36) X(LF, 40) X(LF, 44) \
+  X(LF, 48) X(LF, 52) X(LF, 56) X(LF, 60) X(LF, 64)
 #define MOC_SWIPE_DECLARE(LF, NO)                                                                            \
   bool MOC_SWIPE_FN(LF, NO)(const ProblemView& pv, const ShortArgs& b, const SwipeLayout& lay, dim3 grid,    \
                             dim3 block, int num_cus, hipStream_t stream);                                    \

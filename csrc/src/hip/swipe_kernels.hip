@@ -16,27 +16,31 @@ struct SwipeChoice {
 // take it: at most 64 offsets and 128 letters per record, the profile within the LDS budget, and an
 // int16-exact key form (moc/kernel_bounds.hpp swipe_keys: the keys carry k when 2^KB * |D| leaves room, as
 // on input6; otherwise, input1's W1 = 100, the RK form re-finds k after the selection).
-SwipeChoice swipe_choice(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs_weight) {
+// Offsets per lane: the batch's widest record offset range under its semantics (swipe_offsets; the
+// reference's needs one offset less than lanes_needed), rounded up to a multiple of 4 (one ds_read_b64 per 4
+// offsets, the epilogue's groups of 4): input6 / input1 run 20 offsets per lane instead of 24.
+SwipeChoice swipe_choice(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs_weight, bool spec) {
   SwipeChoice c;
-  const int64_t need = lanes_needed(L1, std::min(min_l2, L1));
-  if (need > 64 || max_l2 > bounds::kSwipeMaxL2) return c;
+  const int64_t mn = std::min(min_l2, L1);
+  if (lanes_needed(L1, mn) > 64 || max_l2 > bounds::kSwipeMaxL2) return c;
   const bounds::SwipeKeys keys = bounds::swipe_keys(max_abs_weight, max_l2);
   if (keys == bounds::SwipeKeys::None) return c;
   c.rk = keys == bounds::SwipeKeys::RK;
-  c.noff = static_cast<int>(((std::max<int64_t>(need, 2) + 7) / 8) * 8);
+  c.noff = static_cast<int>(((std::max<int64_t>(swipe_offsets(L1, mn, spec), 4) + 3) / 4) * 4);
   c.l2w = bounds::swipe_record_words(max_l2);
   return c;
 }
 }  // namespace
 
 int32_t swipe_form(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs_weight) {
-  const SwipeChoice ch = swipe_choice(L1, min_l2, max_l2, max_abs_weight);
+  const SwipeChoice ch = swipe_choice(L1, min_l2, max_l2, max_abs_weight, true);
   return !ch.noff ? 0 : ch.rk ? bounds::kFormSwipeRK : bounds::kFormSwipeKBits;
 }
 
-bool configure_swipe(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs_weight, ShortArgs& a, bool hbm) {
+bool configure_swipe(int64_t L1, int64_t min_l2, int64_t max_l2, int32_t max_abs_weight, ShortArgs& a, bool hbm,
+                     bool spec) {
   if (a.packed5) return false;  // 5-bit letters go through the staged pipeline (unpacked on the device)
-  const SwipeChoice ch = swipe_choice(L1, min_l2, max_l2, max_abs_weight);
+  const SwipeChoice ch = swipe_choice(L1, min_l2, max_l2, max_abs_weight, spec);
   if (!ch.noff) return false;
   const int fb = result_bytes(static_cast<ResultFormat>(a.fmt));
   // host streams: 2048-record tiles (packed letters fit the register prefetch; 3.59 vs 3.69 ms per headline

@@ -929,7 +929,7 @@ void HipEngine::solve_wire_impl(const WireBatch& batch, void* out, ResultFormat 
   a.counter = d_counter_;
   a.packed5 = b.packed5 ? 1 : 0;
   a.packed33 = b.packed33 ? 1 : 0;
-  const bool swipe = dev::configure_swipe(L1_, ls.mn, ls.mx, table_.max_abs(), a, b.device);
+  const bool swipe = dev::configure_swipe(L1_, ls.mn, ls.mx, table_.max_abs(), a, b.device, sem_ == Semantics::Spec);
   // packed letters stream straight into the swipe kernel only; other kernels read unpacked bytes. Sparse
   // offsets need whole tiles of 2^off_shift records (the swipe tiles are powers of two >= 64).
   const bool kernel_ok = (swipe || (!b.packed5 && !b.packed33 &&
@@ -1082,7 +1082,7 @@ void HipEngine::run_staged(const uint8_t* codes, const int64_t* offsets, int64_t
     dev::ShortArgs a;
     a.fmt = static_cast<int32_t>(fmt);
     const bool swipe = cp.n_short > 0 && cp.long_recs.empty() &&
-                       dev::configure_swipe(L1_, cp.min_short, cp.max_l2, table_.max_abs(), a, true);
+                       dev::configure_swipe(L1_, cp.min_short, cp.max_l2, table_.max_abs(), a, true, sem_ == Semantics::Spec);
     bool short_ok = swipe || (cp.n_short > 0 && dev::configure_short(L1_, cp.min_short, cp.max_l2, a));
     // everything through the tile kernel (identity record list) when the short kernel cannot hold it
     const bool all_tiles = cp.n_short > 0 && !short_ok;
@@ -1191,7 +1191,7 @@ void HipEngine::solve_device(const uint8_t* d_codes, const int64_t* d_offsets, c
   dev::ShortArgs a;
   a.fmt = static_cast<int32_t>(ResultFormat::R12);
   const bool swipe = cp.n_short > 0 && cp.long_recs.empty() &&
-                     dev::configure_swipe(L1_, cp.min_short, cp.max_l2, table_.max_abs(), a, true);
+                     dev::configure_swipe(L1_, cp.min_short, cp.max_l2, table_.max_abs(), a, true, sem_ == Semantics::Spec);
   bool short_ok = swipe || (cp.n_short > 0 && dev::configure_short(L1_, cp.min_short, cp.max_l2, a));
   const bool all_tiles = cp.n_short > 0 && !short_ok;  // everything through the tile kernel
   const int32_t* lrecs = all_tiles ? nullptr : cp.long_recs.data();

@@ -1145,37 +1145,40 @@ Result swipe_record(const ScoreTable& t, const std::vector<uint8_t>& s1, const u
   const int64_t last = L1 - L2;
   const int64_t lim0 = on ? last + ((sem == Semantics::Spec || L2 == L1) ? 1 : 0) : 0;
   const int64_t lim1 = on && L2 >= 2 ? last : 0;
-  const int64_t all_valid = L1 - max_l2;
-  const int16_t eb = static_cast<int16_t>(rk ? 0 : KMASK - steps);
-  uint32_t best = 0, tot = static_cast<uint32_t>(anchor + 32768);
-  int bd = 0;
+  (void)max_l2;
+  // the selection's chain value C_o = (Tot_o + 2^15) << 16 + ~(o << KB), from the anchor diagonal down
+  // (swipe_lane): the un-mutated key is C_o, the best mutant's C_{o+1} + ((d << 16) | (KMASK - k)) + 1. The
+  // kernel skips the limit tests where they hold for its whole wave; applying them everywhere is the same.
+  const uint32_t kStep = 1u << KB;
+  uint32_t C = (static_cast<uint32_t>(anchor + 32768) << 16) + (0xffffu - (static_cast<uint32_t>(noff) << KB));
+  uint32_t best = 0;
   for (int o = noff - 1; o >= 0; --o) {
-    const int16_t dq = rk ? E[o] : static_cast<int16_t>(static_cast<int16_t>(E[o] - eb) >> KB);
-    const uint32_t Pn = tot, Po = Pn + static_cast<uint32_t>(static_cast<int>(dq));
-    tot = Po;
-    const uint32_t kLow0 = 0xffffu - (static_cast<uint32_t>(o) << KB), kLow1 = kLow0 - KMASK;
-    uint32_t k0 = (Po << 16) | kLow0;
-    const int bk = B[o];
-    const uint32_t tt = static_cast<uint32_t>(bk) + (Pn << KB);
-    uint32_t k1 = rk ? ((static_cast<uint32_t>(bk) + Pn) << 16) | (kLow0 - 1u) : ((tt >> KB) << 16) | (tt & KMASK) | kLow1;
-    if (o >= all_valid) {
-      k0 = o < lim0 ? k0 : 0u;
-      k1 = o < lim1 ? k1 : 0u;
-    }
-    const uint32_t nb = std::max(best, std::max(k0, k1));
-    if (rk) bd = (nb == k1 && k1 != 0u) ? bk : bd;
-    best = nb;
+    // D_o(L2) = E >> KB (E = D * 2^KB + KMASK - steps, steps <= KMASK); RK: E itself
+    const int16_t dq = rk ? E[o] : static_cast<int16_t>(E[o] >> KB);
+    const int16_t bd = rk ? B[o] : static_cast<int16_t>(B[o] >> KB);
+    const uint32_t ds = (static_cast<uint32_t>(static_cast<uint16_t>(dq)) << 16) | kStep;
+    const uint32_t m = (static_cast<uint32_t>(static_cast<uint16_t>(bd)) << 16) |
+                       (rk ? 0u : static_cast<uint32_t>(static_cast<uint16_t>(B[o])) & static_cast<uint32_t>(KMASK));
+    uint32_t k1 = C + m + 1u;
+    C += ds;
+    uint32_t k0 = C;
+    k0 = o < lim0 ? k0 : 0u;
+    k1 = o < lim1 ? k1 : 0u;
+    best = std::max(best, std::max(k0, k1));
   }
   if (!on || best == 0u) return Result{kNoCandidateScore, 0, 0};
   const uint32_t idx = 0xffffu - (best & 0xffffu);
   if (!rk) return Result{static_cast<int>(best >> 16) - 32768, static_cast<int>(idx >> KB), static_cast<int>(idx & KMASK)};
   int kw = 0;
-  if (idx & 1u) {  // the k re-walk on the winning diagonal (copy 0 of the profile, int sums)
+  if (idx & 1u) {  // the k re-walk on the winning diagonal (copy 0 of the profile, int sums): the first argmax
     const int ow = static_cast<int>(idx >> 1);
-    int run = 0;
+    int run = 0, top = INT32_MIN;
     for (int i = 0; i < steps; ++i) {
       run += pf(i < L2 ? s2[i] : 0, ow + i);
-      kw = (kw == 0 && run == bd) ? i + 1 : kw;
+      if (run > top) {
+        top = run;
+        kw = i + 1;
+      }
     }
   }
   return Result{static_cast<int>(best >> 16) - 32768, static_cast<int>(idx >> 1), (idx & 1u) ? kw : 0};
@@ -1353,8 +1356,11 @@ void test_swipe_replay_bounds() {
                         Case{190, 127, 128}}) {
     const Fixture f = azaz(cs.L1, cs.lo, cs.hi, static_cast<uint32_t>(cs.L1));
     const int l2w = bounds::swipe_record_words(f.max_l2), kb = bounds::swipe_kbits(l2w);
-    const int64_t need = cs.L1 - f.min_l2 + 1;
-    const int noff = static_cast<int>(((std::max<int64_t>(need, 2) + 7) / 8) * 8);
+    // offsets per lane as swipe_choice sizes them: the semantics' widest range, a multiple of 4
+    auto noff_of = [&](Semantics sem) {
+      const int64_t need = dev::swipe_offsets(cs.L1, std::min(f.min_l2, cs.L1), sem == Semantics::Spec);
+      return static_cast<int>(((std::max<int64_t>(need, 4) + 3) / 4) * 4);
+    };
     const int steps = static_cast<int>(f.max_l2);
     // the largest w of each form, from the rule itself
     int w_kbits = 0, w_rk = 0;
@@ -1368,6 +1374,7 @@ void test_swipe_replay_bounds() {
     if (l2w == 4) CHECK(w_kbits == 31);      // 2*31*16*32 + 32 < 32767 <= 2*32*16*32 + 32
     if (l2w == 8) CHECK(w_kbits == 7);       // 2*7*32*64 + 64 < 32767 <= 2*8*32*64 + 64
     for (Semantics sem : {Semantics::Reference, Semantics::Spec}) {
+      const int noff = noff_of(sem);
       if (w_kbits > 0) {
         const ScoreTable at = ScoreTable::build(Weights{{w_kbits, 0, 0, w_kbits}});
         CHECK(mismatches(at, f, sem, [&](const uint8_t* s2, int64_t L2) {

@@ -297,6 +297,34 @@ def test_swipe_kernel_shapes(engine, L1, lo, hi, w, sem):
         assert kinds == ["swipe"], kinds
 
 
+@pytest.mark.parametrize("noff", list(range(4, 65, 4)))
+@pytest.mark.parametrize("sem", [Semantics.REFERENCE, Semantics.SPEC])
+def test_swipe_every_offset_width(engine, noff, sem):
+    # every swipe code object (offsets per lane: multiples of 4, sized by the semantics' widest record range:
+    # L1 - L2 offsets under the reference, one more under the spec), host-streamed and device-resident,
+    # against the CPU engine; the batch's shortest record needs exactly `noff` offsets (reference; 63 for the
+    # widest instance: a record needing 65 lanes under the spec semantics belongs to the tile kernels)
+    L1 = 70
+    lo = L1 - noff + (1 if noff == 64 else 0)
+    rng = np.random.default_rng(noff * 3 + int(sem == Semantics.SPEC))
+    s1 = "".join(chr(65 + x) for x in rng.integers(0, 26, L1))
+    lens = np.concatenate([[lo], rng.integers(lo, min(lo + 7, L1) + 1, 2999)])
+    recs = ["".join(chr(65 + x) for x in rng.integers(0, 26, n)) for n in lens]
+    prob = Problem.from_strings((4, 3, 2, 10), s1, recs)
+    want = as_triples(search_cpu(prob, sem))
+    engine.set_problem(prob.weights, prob.seq1, sem)
+    got = engine.solve(prob.codes, prob.offsets, fmt="auto")
+    assert engine.stats()["kernels"] == ["swipe"], engine.stats()
+    assert np.array_equal(as_triples(got, r2=engine.stats()["r2"]), want)
+    dev = torch.device("cuda:0")
+    out = torch.empty((len(prob.offsets) - 1, 3), dtype=torch.int32, device=dev)
+    engine.solve_device(torch.from_numpy(prob.codes).to(dev), torch.from_numpy(prob.offsets).to(dev), prob.offsets,
+                        out)
+    torch.cuda.synchronize()
+    assert engine.stats()["kernels"] == ["swipe"], engine.stats()
+    assert np.array_equal(out.cpu().numpy(), want)
+
+
 def test_kernel_selection(engine):
     p6 = make_synthetic("input6", 2000, seed=1)
     engine.set_problem(p6.weights, p6.seq1)
