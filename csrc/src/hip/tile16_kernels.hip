@@ -145,6 +145,21 @@ __device__ __forceinline__ uint32_t wave_max_u32_dpp(uint32_t v) {
   v = max(v, dpp(v, integral_constant<int, 0x143>(), integral_constant<int, 0xc>()));  // row_bcast:31
   return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
 }
+
+// Runs f with the sub-tile count of a tile: the smallest power of two (<= UU) holding its `act` sub-tiles of
+// valid offsets — a record's last, partial tile sweeps only those (a tile of U sub-tiles would spend the
+// others' adds and maxima on offsets past the record's range). `act` is wave-uniform.
+template <int UU, typename F>
+__device__ __forceinline__ void with_subtiles(int act, F&& f) {
+  if constexpr (UU == 1) {
+    f(std::integral_constant<int, 1>());
+  } else {
+    if (act > UU / 2)
+      f(std::integral_constant<int, UU>());
+    else
+      with_subtiles<UU / 2>(act, f);
+  }
+}
 }  // namespace
 
 // Stages columns [S, S + W) of every profile row as widened entries split by the parity of their window index
@@ -372,13 +387,17 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
     for (; t < t_stop && L2 <= L1; ++t) {
       const int o0 = t * kSpan;
       MOC_DCHECK(o0 >= 0 && o0 <= L1);
+      // sub-tiles with valid offsets: all U but in a record's last tile (wave-uniform; no barrier below)
+      const int act = (min(need, o0 + kSpan) - o0 + kSub - 1) / kSub;
+      with_subtiles<U>(act, [&](auto uu) {
+      constexpr int UU = decltype(uu)::value;  // this tile's sub-tiles
       // sub-tile u: lane owns offsets o0 + 128u + 2*lane (low half) and + 1 (high half); its entries sit at
       // 4 bytes per lane and 256 bytes per sub-tile in both layouts (Wide: o0 and 2*lane even)
       const unsigned char* lbase = smem + 2 * (o0 - S) + 4 * lane;
-      uint32_t acc[U], best[U];
-      int DcA[U], DcB[U], mxA[U], mxB[U];
+      uint32_t acc[UU], best[UU];
+      int DcA[UU], DcB[UU], mxA[UU], mxB[UU];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
+      for (int u = 0; u < UU; ++u) {
         acc[u] = 0;
         best[u] = kBestInit;
         DcA[u] = DcB[u] = 0;
@@ -387,9 +406,9 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
       auto step = [&](int so, int j, bool key) {
         const int soff = __builtin_amdgcn_readlane(so, j);
         const unsigned char* p = lbase + soff;
-        MOC_DCHECK(2 * o0 + 4 * lane + soff + 2 * kSub * (U - 1) + EW <= prof_lds);
+        MOC_DCHECK(2 * o0 + 4 * lane + soff + 2 * kSub * (UU - 1) + EW <= prof_lds);
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
+        for (int u = 0; u < UU; ++u) {
           if (Wide) {
             acc[u] = pk_add(acc[u], *reinterpret_cast<const uint32_t*>(p + 2 * kSub * u));
           } else {
@@ -405,23 +424,23 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
 #pragma unroll
         for (int g = 0; g < 4; ++g) so16[g] = __shfl(so, 16 * g + (lane & 15), 64);
       };
-      // GG steps from chunk step j (a constant once unrolled), every step a key step: the GG*U profile reads
+      // GG steps from chunk step j (a constant once unrolled), every step a key step: the GG*UU profile reads
       // issue before the first add, so the LDS latency of a group hides under the adds of the group before
       auto group = [&](const int (&so16)[4], int j, auto gg) {
         constexpr int GG = decltype(gg)::value;
-        uint32_t e[GG][U];
+        uint32_t e[GG][UU];
 #pragma unroll
         for (int q = 0; q < GG; ++q) {
           const unsigned char* p = lbase + row_newbcast(so16[(j + q) >> 4], (j + q) & 15);
 #pragma unroll
-          for (int u = 0; u < U; ++u)
+          for (int u = 0; u < UU; ++u)
             e[q][u] = Wide ? *reinterpret_cast<const uint32_t*>(p + 2 * kSub * u)
                            : *reinterpret_cast<const uint16_t*>(p + 2 * kSub * u);
         }
 #pragma unroll
         for (int q = 0; q < GG; ++q)
 #pragma unroll
-          for (int u = 0; u < U; ++u) {
+          for (int u = 0; u < UU; ++u) {
             if (Wide)
               acc[u] = pk_add(acc[u], e[q][u]);
             else
@@ -429,12 +448,12 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
             best[u] = pk_max(best[u], acc[u]);
           }
       };
-      // full chunks: G steps per group, G * U reads in flight (U = 8 keeps the VGPRs within 4 waves per SIMD)
-      constexpr int G = U >= 8 ? 2 : U >= 4 ? 4 : 8;
+      // full chunks: G steps per group, G * UU reads in flight (UU = 8 keeps the VGPRs within 4 waves per SIMD)
+      constexpr int G = UU >= 8 ? 2 : UU >= 4 ? 4 : 8;
       // every 64-step chunk starts from zero halves and folds them into the int32 state at its end
       auto flush = [&](bool any_key) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
+        for (int u = 0; u < UU; ++u) {
           if (any_key) {
             mxA[u] = max(mxA[u], DcA[u] + lo16(best[u]));
             mxB[u] = max(mxB[u], DcB[u] + hi16(best[u]));
@@ -475,21 +494,21 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
         anchor_add(c, i0 + lane);
         int j = 0;
         // groups of 8 steps before the last one (short records live here)
-        if constexpr (U >= 8) {  // 8 sub-tiles: a runtime loop (the unrolled one is too large), v_readlane steps
+        if constexpr (UU >= 8) {  // 8 sub-tiles: a runtime loop (the unrolled one is too large), v_readlane steps
           for (; j + 4 <= m - 1; j += 4) {
-            uint32_t e[4][U];
+            uint32_t e[4][UU];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const unsigned char* p = lbase + __builtin_amdgcn_readlane(so, j + q);
 #pragma unroll
-              for (int u = 0; u < U; ++u)
+              for (int u = 0; u < UU; ++u)
                 e[q][u] = Wide ? *reinterpret_cast<const uint32_t*>(p + 2 * kSub * u)
                                : *reinterpret_cast<const uint16_t*>(p + 2 * kSub * u);
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q)
 #pragma unroll
-              for (int u = 0; u < U; ++u) {
+              for (int u = 0; u < UU; ++u) {
                 if (Wide)
                   acc[u] = pk_add(acc[u], e[q][u]);
                 else
@@ -515,7 +534,7 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
       anchor = __builtin_amdgcn_readlane(wave_prefix_sum_dpp(anchor), 63);
       int carry = anchor;  // Tot at the end of the sub-tile being processed
 #pragma unroll
-      for (int u = U - 1; u >= 0; --u) {
+      for (int u = UU - 1; u >= 0; --u) {
         const int oa = o0 + kSub * u + 2 * lane;
         const int ca = oa < oA ? DcA[u] : 0, cb = oa + 1 < oA ? DcB[u] : 0;
         const int pair = ca + cb;
@@ -535,16 +554,27 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
           const uint32_t kB1 = ((static_cast<uint32_t>(mxB[u]) + static_cast<uint32_t>(totB - cb)) << kib) + (c0 - 3u);
           // validity as pass1_candidate: o <= last (o < last, or L2 == L1 / spec semantics, for the
           // un-mutated one), mutants at o < last with L2 >= 2
-          const uint32_t a0 = oa < last || (oa == last && v0_at_last) ? kA0 : 0u;
-          const uint32_t a1 = oa < last && L2 >= 2 ? kA1 : 0u;
-          const uint32_t b0 = oa + 1 < last || (oa + 1 == last && v0_at_last) ? kB0 : 0u;
-          const uint32_t b1 = oa + 1 < last && L2 >= 2 ? kB1 : 0u;
-          acc32 = max(max(acc32, max(a0, a1)), max(b0, b1));
+          if (o0 + kSub * (u + 1) < last && L2 >= 2) {  // wave-uniform: every candidate of the sub-tile valid
+            acc32 = max(max(acc32, max(kA0, kA1)), max(kB0, kB1));
+          } else {
+            const uint32_t a0 = oa < last || (oa == last && v0_at_last) ? kA0 : 0u;
+            const uint32_t a1 = oa < last && L2 >= 2 ? kA1 : 0u;
+            const uint32_t b0 = oa + 1 < last || (oa + 1 == last && v0_at_last) ? kB0 : 0u;
+            const uint32_t b1 = oa + 1 < last && L2 >= 2 ? kB1 : 0u;
+            acc32 = max(max(acc32, max(a0, a1)), max(b0, b1));
+          }
         } else {
-          acc64 = max_u64(acc64, pass1_candidate(oa, L1, L2, pv.semantics, totA, totB, mxA[u]));
-          acc64 = max_u64(acc64, pass1_candidate(oa + 1, L1, L2, pv.semantics, totB, totB - cb, mxB[u]));
+          if (o0 + kSub * (u + 1) < last && L2 >= 2) {  // wave-uniform: every candidate of the sub-tile valid
+            const uint32_t i0 = 2u * static_cast<uint32_t>(oa);
+            acc64 = max_u64(acc64, max_u64(max_u64(final_key(totA, i0), final_key(mxA[u] + totB, i0 + 1u)),
+                                           max_u64(final_key(totB, i0 + 2u), final_key(mxB[u] + totB - cb, i0 + 3u))));
+          } else {
+            acc64 = max_u64(acc64, pass1_candidate(oa, L1, L2, pv.semantics, totA, totB, mxA[u]));
+            acc64 = max_u64(acc64, pass1_candidate(oa + 1, L1, L2, pv.semantics, totB, totB - cb, mxB[u]));
+          }
         }
       }
+      });
     }
     if (kib) {
       const uint32_t k = wave_max_u32_dpp(acc32);
@@ -608,8 +638,8 @@ void tile16_slide_kernel(ProblemView pv, BatchView bv,
     const int last = L1 - L2;
     const bool v0_at_last = pv.semantics == static_cast<int>(Semantics::Spec) || L2 == L1;
     auto letter = [&](int i) { return i < steps ? static_cast<int>(rec[i]) : 0; };
+    // the record's best candidate key: 64-bit, or a 32-bit selection key in the low half (pv.t16_key_bits)
     unsigned long long acc64 = 0;
-    uint32_t acc32 = 0;
     for (int t = t0; t < t1; ++t) {  // workgroup-uniform
       const int o0 = t * kSpan;
       const bool on = t < own_tiles;  // wave-uniform
@@ -679,7 +709,8 @@ void tile16_slide_kernel(ProblemView pv, BatchView bv,
             best[u] = kBestInit;
           }
         };
-        constexpr int G = U >= 4 ? 4 : 8;
+        // two workgroups per CU (64 VGPRs): half the reads per group in flight, the other workgroup hides the rest
+        constexpr int G = WavesPerSimd >= 8 ? (U >= 4 ? 2 : 4) : (U >= 4 ? 4 : 8);
         const int i_end = min(iw + C, steps);
         int i0 = iw;
         for (; i0 + 64 <= i_end && i0 + 64 < steps; i0 += 64) {  // full chunks (the record goes on past them)
@@ -723,20 +754,32 @@ void tile16_slide_kernel(ProblemView pv, BatchView bv,
           const uint32_t kA1 = ((static_cast<uint32_t>(mxA[u]) + static_cast<uint32_t>(totB)) << kib) + (c0 - 1u);
           const uint32_t kB0 = (static_cast<uint32_t>(totB) << kib) + (c0 - 2u);
           const uint32_t kB1 = ((static_cast<uint32_t>(mxB[u]) + static_cast<uint32_t>(totB - cb)) << kib) + (c0 - 3u);
-          const uint32_t a0 = oa < last || (oa == last && v0_at_last) ? kA0 : 0u;
-          const uint32_t a1 = oa < last && L2 >= 2 ? kA1 : 0u;
-          const uint32_t b0 = oa + 1 < last || (oa + 1 == last && v0_at_last) ? kB0 : 0u;
-          const uint32_t b1 = oa + 1 < last && L2 >= 2 ? kB1 : 0u;
-          acc32 = max(max(acc32, max(a0, a1)), max(b0, b1));
+          uint32_t k32 = static_cast<uint32_t>(acc64);
+          if (o0 + kSub * (u + 1) < last && L2 >= 2) {  // wave-uniform: every candidate of the sub-tile valid
+            k32 = max(max(k32, max(kA0, kA1)), max(kB0, kB1));
+          } else {
+            const uint32_t a0 = oa < last || (oa == last && v0_at_last) ? kA0 : 0u;
+            const uint32_t a1 = oa < last && L2 >= 2 ? kA1 : 0u;
+            const uint32_t b0 = oa + 1 < last || (oa + 1 == last && v0_at_last) ? kB0 : 0u;
+            const uint32_t b1 = oa + 1 < last && L2 >= 2 ? kB1 : 0u;
+            k32 = max(max(k32, max(a0, a1)), max(b0, b1));
+          }
+          acc64 = k32;
         } else {
-          acc64 = max_u64(acc64, pass1_candidate(oa, L1, L2, pv.semantics, totA, totB, mxA[u]));
-          acc64 = max_u64(acc64, pass1_candidate(oa + 1, L1, L2, pv.semantics, totB, totB - cb, mxB[u]));
+          if (o0 + kSub * (u + 1) < last && L2 >= 2) {  // wave-uniform: every candidate of the sub-tile valid
+            const uint32_t i0 = 2u * static_cast<uint32_t>(oa);
+            acc64 = max_u64(acc64, max_u64(max_u64(final_key(totA, i0), final_key(mxA[u] + totB, i0 + 1u)),
+                                           max_u64(final_key(totB, i0 + 2u), final_key(mxB[u] + totB - cb, i0 + 3u))));
+          } else {
+            acc64 = max_u64(acc64, pass1_candidate(oa, L1, L2, pv.semantics, totA, totB, mxA[u]));
+            acc64 = max_u64(acc64, pass1_candidate(oa + 1, L1, L2, pv.semantics, totB, totB - cb, mxB[u]));
+          }
         }
       }
     }
     if (li < 0 || L2 > L1) continue;  // wave-uniform; no barrier follows in this item
     if (kib) {
-      const uint32_t kk = wave_max_u32_dpp(acc32);
+      const uint32_t kk = wave_max_u32_dpp(static_cast<uint32_t>(acc64));
       if (lane == 0 && kk != 0u)
         atomicMax(keys + li, final_key(static_cast<int>(kk >> kib) - (1 << (31 - kib)), kmask - (kk & kmask)));
     } else {

@@ -647,8 +647,21 @@ std::vector<dev::WaveStart> HipEngine::plan_waves(const int64_t* offsets, const 
   tp.wide = wide;
   tp.tile16 = d_prof16_ != nullptr && (W == 0 || max_l2 + 2 * 128 <= W) && (wide || !prof16_i16_);
   // sub-tiles per wave tile: 4 amortises the per-tile setup over short records, 2 keeps more waves busy
-  // on long ones (measured, both kernels: profiles/tile_variants.log, profiles/tile16_variants.log)
+  // on long ones (measured, both kernels: profiles/tile_variants.log, profiles/tile16_variants.log) — unless
+  // the batch gives every resident wave >= 8 tiles of 4 sub-tiles: with a record's last tile cut to its
+  // valid sub-tiles (tile16_search_kernel) 4 then wins on long records too (input3: 17.2 -> 17.7 T cells/s;
+  // 4 tiles per wave, heavy3's bench batch, stays on 2: 14.8 vs 14.3; profiles/r6/README.txt)
   int u = tile_u_ > 0 ? tile_u_ : (sum_l2 < 96 * n_long ? 4 : 2);
+  if (tile_u_ <= 0 && u == 2 && W == 0 && tp.tile16) {
+    int64_t tiles4 = 0;
+    for (int64_t li = 0; li < n_long; ++li) {
+      const int64_t r = long_recs ? long_recs[li] : li;
+      tiles4 += dev::tiles_of(dev::lanes_needed(L1_, offsets[r + 1] - offsets[r]), dev::tile_span(true, 4));
+    }
+    const int64_t lds = dev::tile16_lds_bytes((wide ? 2 : 1) * static_cast<int64_t>(prof16_bytes_), L1_);
+    const int64_t resident = static_cast<int64_t>(num_cus_) * dev::tile16_waves_per_cu(static_cast<int>(lds));
+    if (tiles4 >= 8 * resident * parts) u = 4;
+  }
   if (tile_u_ <= 0 && u == 4 && tp.tile16 && W == 0 && 128 * 8 <= prof16_overhang_) u = 8;  // tile16: wider tiles
   if (u > 4 && !(tp.tile16 && W == 0 && 128 * u <= prof16_overhang_)) u = 4;  // the overhang bounds the span
   if (u > 2 && mfma_ && tp.tile16 && W == 0) u = 2;  // the matrix-core sweep's register budget (U = 4 spills)

@@ -454,6 +454,28 @@ def test_context_parallel_keys(engine, shape, n, parts):
         assert np.array_equal(keys, full)
 
 
+@pytest.mark.parametrize("shape", ["limits", "heavylim"])
+def test_context_parallel_keys_sliding_windows(engine, shape):
+    # search_keys / search_keys_device with one part take the sliding-window plan (byte pairs and
+    # the int16 profile) and 32-bit selection keys where the bounds allow; their keys equal the CPU's
+    from mpi_openmp_cuda_amd import search_keys_cpu
+
+    prob = make_synthetic(shape, 1024, seed=17)
+    for sem in (Semantics.REFERENCE, Semantics.SPEC):
+        engine.set_problem(prob.weights, prob.seq1, sem)
+        want = search_keys_cpu(prob, 0, 1, sem)
+        keys = engine.search_keys(prob.codes, prob.offsets, 0, 1)
+        assert "tile16_slide" in engine.stats()["forms"], engine.stats()
+        assert np.array_equal(keys, want)
+        dev = torch.device("cuda:0")
+        k = torch.zeros(prob.n, dtype=torch.int64, device=dev)
+        engine.search_keys_device(torch.from_numpy(prob.codes).to(dev), torch.from_numpy(prob.offsets).to(dev),
+                                  prob.offsets, 0, 1, k)
+        torch.cuda.synchronize()
+        assert "tile16_slide" in engine.stats()["forms"], engine.stats()
+        assert np.array_equal(k.cpu().numpy().view(np.uint64), want)
+
+
 def test_context_parallel_device_finalize(engine):
     prob = make_synthetic("input3", 6, seed=3)
     engine.set_problem(prob.weights, prob.seq1)
