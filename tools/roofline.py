@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""One gfx950 roofline for every search kernel, from counters (profiles/roofline_r5.md is its output).
+"""One gfx950 roofline for every search kernel, from counters (profiles/roofline_r6.md is its output; roofline_r5.md the previous round's).
 
 Peak model (MI355X), measured on the box by tools/isa_peak.hip (profiles/roofline_r5/isa_peak.log): 256 CUs of
 4 SIMDs; every SIMD holding 8 waves of independent instructions sustains, per CU-clock,
@@ -23,21 +23,19 @@ CUS, SES = 256, 32
 PEAK_PACKED, PEAK_VALU32, PEAK_LDS = 0.94, 1.69, 0.48  # wave-instructions per CU-clock (isa_peak)
 
 # kernel-bench row (shape, variant) -> the kernel that does its search (a prefix of its name in the summary)
-ROWS = [  # shape, kernel_bench variant, kernel name prefix, form, PMC pass (tools/pmc_r5.sh)
-    ("input6", "tile16", "swipe_direct_kernel<24, 4, 0, false>", "device bytes", "p1"),
-    ("input6", "wire", "swipe_direct_kernel<24, 4, 2, false>", "device P33 wire", "p4"),
-    ("input1", "tile16", "swipe_direct_kernel<24, 16, 0, true>", "device bytes", "p1"),
-    ("input1", "wire", "swipe_direct_kernel<24, 16, 2, true>", "device P33 wire", "p4"),
+ROWS = [  # shape, kernel_bench variant, kernel name prefix, form, PMC pass (tools/pmc_roofline.sh)
+    ("input6", "tile16", "swipe_direct_kernel<20, 4, 0, false>", "device bytes", "p1"),
+    ("input6", "wire", "swipe_direct_kernel<20, 4, 2, false>", "device P33 wire", "p4"),
+    ("input1", "tile16", "swipe_direct_kernel<20, 16, 0, true>", "device bytes", "p1"),
+    ("input1", "wire", "swipe_direct_kernel<20, 16, 2, true>", "device P33 wire", "p4"),
     ("mid", "tile16", "swipe_direct_kernel<64, 24, 0, true>", "device bytes, 24 record words", "p1"),
-    ("input3", "tile16", "tile16_search_kernel<2, false, true>", "widened pairs", "p2"),
-    ("limits", "tile16", "tile16_search_kernel<2, false, false>", "byte pairs (before sliding windows)", "p2"),
-    ("limits", "slide", "tile16_slide_kernel<4>", "sliding widened windows", "p6"),
+    ("input3", "tile16", "tile16_search_kernel<4, false, true>", "widened pairs", "p2"),
+    ("limits", "tile16", "tile16_slide_kernel<4, 8>", "sliding widened windows", "p2"),
     ("input4", "tile16", "tile16_search_kernel<8, true, true>", "widened windows", "p3"),
-    ("long20k", "tile16", "tile16_search_kernel<4, true, false>", "byte-pair windows (before sliding windows)", "p3"),
-    ("long20k", "slide", "tile16_slide_kernel<4>", "sliding widened windows", "p7"),
-    ("heavylim", "slide", "tile16_slide_kernel<4>", "int16 profile, sliding widened windows", "p8"),
+    ("long20k", "tile16", "tile16_slide_kernel<4, 8>", "sliding widened windows", "p3"),
     ("heavy3", "tile16", "tile16_search_kernel<2, false, true>", "int16 profile", "p5"),
     ("heavy4", "tile16", "tile16_search_kernel<8, true, true>", "int16 profile, windows", "p5"),
+    ("heavylim", "tile16", "tile16_slide_kernel<4, 8>", "int16 profile, sliding widened windows", "p6"),
 ]
 
 
