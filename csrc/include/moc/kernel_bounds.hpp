@@ -29,11 +29,12 @@ inline int64_t diff_bound(int32_t max_abs_weight, int64_t max_l2) {
 }
 
 // ---- swipe kernel (swipe_impl.hpp): one lane per record, int16 running sums per offset pair.
-// Record words per lane (4 letters each): 4 for records <= 16 letters, 8 for <= 32, 16 for <= 64, 24 for
-// <= 96, 32 for <= 128 (the longest records the kernel takes).
+// Record words per lane (4 letters each): 4 for records <= 16 letters, 8 for <= 32, 12 for <= 48, 16 for
+// <= 64, 24 for <= 96, 32 for <= 128 (the longest records the kernel takes). The words size the LDS tables
+// (and P33's decode slices), so input1's records of 32..41 letters take 12, not 16.
 constexpr int64_t kSwipeMaxL2 = 128;
 inline int swipe_record_words(int64_t max_l2) {
-  return max_l2 <= 16 ? 4 : max_l2 <= 32 ? 8 : max_l2 <= 64 ? 16 : max_l2 <= 96 ? 24 : 32;
+  return max_l2 <= 16 ? 4 : max_l2 <= 32 ? 8 : max_l2 <= 48 ? 12 : max_l2 <= 64 ? 16 : max_l2 <= 96 ? 24 : 32;
 }
 // Bits for k in the int16 keys: k <= 4 * l2w < 2^kb.
 constexpr int swipe_kbits(int l2w) {
@@ -46,7 +47,7 @@ enum class SwipeKeys { None, KBits, RK };
 //   KBits: E = D * 2^kb + (2^kb - 1 - k) in int16. Its largest value is dmax * 2^kb + 2^kb - 2, so
 //          dmax * 2^kb + 2^kb < 32767 keeps every key (and B2 = max E) exact.
 //   RK:    E = D in int16 (|D| <= dmax < 32767); k is re-found on the winning diagonal afterwards.
-//          Records of more than 32 letters (l2w >= 16) always take it: no room for 7 k bits.
+//          Records of more than 32 letters (l2w >= 12) always take it: no room for 6 k bits.
 //   None:  dmax >= 32767.
 // The selection keys carry score + 2^15 in 16 bits: |score| <= W L2 = dmax / 2 < 2^14 under either form; the
 // anchor diagonal is summed in int32 from an int32 table (swipe_build_tables), so W itself is not bounded.
@@ -55,7 +56,7 @@ inline SwipeKeys swipe_keys(int32_t max_abs_weight, int64_t max_l2) {
   if (dmax >= 32767) return SwipeKeys::None;
   const int l2w = swipe_record_words(max_l2);
   const int kb = swipe_kbits(l2w);
-  return (l2w >= 16 || (dmax << kb) + (int64_t{1} << kb) >= 32767) ? SwipeKeys::RK : SwipeKeys::KBits;
+  return (l2w >= 12 || (dmax << kb) + (int64_t{1} << kb) >= 32767) ? SwipeKeys::RK : SwipeKeys::KBits;
 }
 
 // ---- short kernel (short_kernels.hip): one lane per offset.

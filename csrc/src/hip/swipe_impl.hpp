@@ -38,6 +38,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "kernel_common.hpp"
 
@@ -79,6 +80,7 @@ struct SwipeLayout {
   int prof_bytes = 0;   // 8 shifted copies of the Dt profile (swipe_prof_bytes)
   int s_off = 0;        // anchor table: at[i][c] = T[c][Seq1[NOFF + i]] (0 past Seq1), int32, swipe_anchor_bytes
   int loff_off = 0, codes_off = 0, res_off = 0, raw_off = 0, total = 0;  // raw: P33 bytes as loaded
+  int wave_bytes = 0;  // lane-direct P33: one wave's slice of decoded field slots (direct_layout)
 };
 
 inline int al16(int x) { return (x + 15) & ~15; }
@@ -532,16 +534,18 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
 //         cycles), and each lane gathers its record's words from there (wave-level ordering
 //         only: the slice is the wave's own).
 constexpr int kBlockD = 512;  // 8 waves share one set of LDS tables
-// P33 tiles: one 8-byte slot per field (7 letters + a pad byte) for the fields a tile can span, plus the
-// slots a lane's read may run past the last one
-constexpr int p33_tile_fields(int l2w) { return (64 * 4 * l2w + 6) / 7 + 1; }
+// P33 tiles: one 8-byte slot per field (7 letters + a pad byte) for the fields a tile of records of at most
+// max_l2 letters can span, plus the slots a lane's read may run past the last one. Sized by the batch's
+// longest record, not by the instance's record words: LDS decides how many blocks share a CU.
+constexpr int p33_tile_fields(int max_l2) { return (64 * max_l2 + 6) / 7 + 1; }
 constexpr int p33_lane_slots(int l2w) { return (4 * l2w + 8 + 6) / 7; }  // the letters of words 0..l2w+1
-constexpr int direct_wave_bytes(int l2w) { return 8 * (p33_tile_fields(l2w) + p33_lane_slots(l2w) + 1); }
-inline SwipeLayout direct_layout(int L1, int noff, int l2w, int lf) {
+inline SwipeLayout direct_layout(int L1, int noff, int l2w, int lf, int64_t max_l2) {
   SwipeLayout l = swipe_layout(L1, noff, l2w, 0, 0, 0, 0);
   if (lf == 2) {
+    const int ml = static_cast<int>(std::min<int64_t>(std::max<int64_t>(max_l2, 1), 4 * l2w));
+    l.wave_bytes = 8 * (p33_tile_fields(ml) + p33_lane_slots(l2w) + 1);
     l.codes_off = al16(l.s_off + swipe_anchor_bytes(l2w));
-    l.total = l.codes_off + (kBlockD / 64) * direct_wave_bytes(l2w);
+    l.total = l.codes_off + (kBlockD / 64) * l.wave_bytes;
   }
   return l;
 }
@@ -576,6 +580,12 @@ __device__ __forceinline__ uint32_t mulhi_u24(uint32_t a, uint32_t b) {  // bits
   asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
+__device__ __forceinline__ uint32_t mad_i24(uint32_t a, int b, uint32_t c) {  // a * b + c, a and b signed 24-bit
+  // (written out: the compiler folds c - a * 676 into a quarter-rate v_mul_lo_u32 by -676)
+  uint32_t r;
+  asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c));
+  return r;
+}
 __device__ __forceinline__ uint32_t p33_pair(uint32_t v) {  // v < 676 -> bytes (v % 26, v / 26)
   return __umul24(__umul24(v, 2521u) >> 16, 230u) + v;
 }
@@ -585,7 +595,7 @@ __device__ __forceinline__ uint2 decode_p33_field(uint32_t lo, uint32_t hi, int 
   const uint32_t A = __umulhi(static_cast<uint32_t>(x >> 4), 2463805336u) >> 14;  // digits 4..6
   const uint32_t B = static_cast<uint32_t>(x) - __umul24(A, 456976u);  // digits 0..3
   const uint32_t b32 = mulhi_u24(B, 6353502u), a2 = mulhi_u24(A, 6353502u);
-  const uint32_t b10 = B - __umul24(b32, 676u), a10 = A - __umul24(a2, 676u);
+  const uint32_t b10 = mad_i24(b32, -676, B), a10 = mad_i24(a2, -676, A);
   // letter codes are digit + 1; the pad byte stays 0
   return make_uint2((p33_pair(b10) | (p33_pair(b32) << 16)) + 0x01010101u, (p33_pair(a10) | (a2 << 16)) + 0x00010101u);
 }
@@ -597,8 +607,10 @@ __device__ __forceinline__ uint2 decode_p33_field(uint32_t lo, uint32_t hi, int 
 template <int NW>
 __device__ __forceinline__ void record_words_p33(const uint8_t* slots, int q0, int L2, bool on, uint32_t (&wd)[NW]) {
   constexpr int NS = p33_lane_slots(NW);
-  const int fa = static_cast<int>(__umulhi(static_cast<uint32_t>(q0), 613566757u));  // q0 / 7 (q0 < 2^28)
-  const int sh = q0 - 7 * fa;
+  static_assert(NW <= 16, "the 24-bit q0 / 7 below needs q0 < 13110");
+  // q0 / 7 by a 24-bit multiply (exact below 13110; q0 <= 6 + 63 * 4 * NW <= 4038), q0 % 7 by a 24-bit mad
+  const int fa = static_cast<int>(__umul24(static_cast<uint32_t>(q0), 9363u) >> 16);
+  const int sh = static_cast<int>(mad_i24(static_cast<uint32_t>(fa), -7, static_cast<uint32_t>(q0)));
   uint32_t dw[2 * NS];
 #pragma unroll
   for (int k = 0; k < NS; ++k) {
@@ -640,34 +652,40 @@ __device__ __forceinline__ void record_words_p33(const uint8_t* slots, int q0, i
 }
 
 // Length of record 64 t + lane of a batch with base-6 lengths (three 21-bit octets of 8 digits per 8-byte
-// word): 32-bit index arithmetic, and digit j = lane % 8 of its octet v < 2^21 as (v / 6^j) % 6 — v / 6^j one
-// multiply-high by the lane's constant (Len6Digit, made once per kernel; exact below 2^21, checked
-// exhaustively by tools/p33_magic_check.py), then one for the % 6.
+// word): the tile's first octet 8 t splits into its word and position once per wave (scalar), a lane adds its
+// octet lane / 8 with 24-bit arithmetic, and digit j = lane % 8 of the octet's value v < 2^21 is
+// (v / 6^j) - 6 (v / 6^(j+1)), each quotient trunc((v + 0.5) * fl(1 / 6^i)) in f32 — exact for every
+// v < 2^21 and i <= 8 (v + 0.5 is exact, one rounding in the product; tools/p33_magic_check.py checks all
+// of them). Full-rate ops only: the 32-bit multiply-highs this replaces issue at a quarter of the rate.
 struct Len6Digit {
-  uint32_t m = 0;  // ceil(2^(32 + sh) / 6^j); 0: j = 0
-  int sh = 0;
+  float r = 1.f, r6 = 1.f;  // fl(1 / 6^j), fl(1 / 6^(j+1)) for j = lane % 8
+  uint32_t octet = 0;       // lane / 8
 };
 __device__ __forceinline__ Len6Digit len6_digit(int lane) {
-  constexpr uint32_t kM[8] = {0u, 2863311531u, 3817748708u, 2545165806u,
-                              3393554407u, 2262369605u, 3016492806u, 4021990408u};
-  constexpr int kSh[8] = {0, 2, 5, 7, 10, 12, 15, 18};
+  constexpr float kR[9] = {1.0f, 1.0f / 6, 1.0f / 36, 1.0f / 216, 1.0f / 1296, 1.0f / 7776, 1.0f / 46656,
+                           1.0f / 279936, 1.0f / 1679616};
   Len6Digit d;
   const int j = lane & 7;
 #pragma unroll
-  for (int k = 1; k < 8; ++k)
+  for (int k = 0; k < 8; ++k)
     if (j == k) {
-      d.m = kM[k];
-      d.sh = kSh[k];
+      d.r = kR[k];
+      d.r6 = kR[k + 1];
     }
+  d.octet = static_cast<uint32_t>(lane >> 3);
   return d;
 }
-__device__ __forceinline__ int lane_length6(const ShortArgs& a, int64_t t, int lane, Len6Digit dg) {
-  const uint32_t octet = static_cast<uint32_t>(t) * 8u + static_cast<uint32_t>(lane >> 3);
-  const uint32_t word = octet / 3u;
-  const uint64_t w = *reinterpret_cast<const uint64_t*>(a.lengths6 + 8 * static_cast<uint64_t>(word));
-  uint32_t v = static_cast<uint32_t>(w >> (21 * (octet - 3u * word))) & 0x1FFFFFu;
-  v = dg.m ? __umulhi(v, dg.m) >> dg.sh : v;
-  return a.len_base + static_cast<int>(v - __umul24(6u, __umulhi(v, 715827883u)));
+__device__ __forceinline__ int lane_length6(const ShortArgs& a, int64_t t, Len6Digit dg) {
+  const uint32_t o8 = static_cast<uint32_t>(t) * 8u;  // wave-uniform (t < 2^28)
+  const uint32_t sw = o8 / 3u;
+  const uint32_t sr = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(o8 - 3u * sw)));
+  const uint32_t u = sr + dg.octet;  // <= 9
+  const uint32_t dw = __umul24(u, 11u) >> 5, rem = u - __umul24(dw, 3u);  // u / 3, u % 3
+  const uint64_t w = *reinterpret_cast<const uint64_t*>(a.lengths6 + 8 * static_cast<uint64_t>(sw + dw));
+  const uint32_t v = static_cast<uint32_t>(w >> __umul24(rem, 21u)) & 0x1FFFFFu;
+  const float fv = static_cast<float>(v) + 0.5f;
+  const int q = static_cast<int>(fv * dg.r), q6 = static_cast<int>(fv * dg.r6);
+  return a.len_base + static_cast<int>(mad_i24(static_cast<uint32_t>(q6), -6, static_cast<uint32_t>(q)));
 }
 
 template <int NOFF, int L2W, int LF, bool RK>
@@ -682,16 +700,24 @@ __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, S
   const int L1 = pv.L1;
   const int64_t n = a.n, n_tiles = (n + 63) >> 6;
   const int64_t waves = static_cast<int64_t>(gridDim.x) * (kBlockD / 64);
-  int64_t t = static_cast<int64_t>(blockIdx.x) * (kBlockD / 64) + (threadIdx.x >> 6);
+  // the wave's tile index, its tile start (P33) and the loop bounds live in scalar registers
+  int64_t t = static_cast<int64_t>(blockIdx.x) * (kBlockD / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const Len6Digit dg = len6_digit(lane);
-  uint8_t* wbuf = smem + lay.codes_off + (threadIdx.x >> 6) * direct_wave_bytes(L2W);  // P33: this wave's
+  uint8_t* wbuf = smem + lay.codes_off + (threadIdx.x >> 6) * lay.wave_bytes;  // P33: this wave's
   // bytes: the record's offsets; P33: the tile's first letter (o0, every lane) and the record's length (o1)
-  auto load_meta = [&](int64_t tt, int64_t& o0, int64_t& o1) {
+  using Len = std::conditional_t<P33, int, int64_t>;  // P33: a length; bytes: the record's end offset
+  auto uniform64 = [](int64_t v) {
+    return static_cast<int64_t>(
+        (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(v >> 32))))
+         << 32) |
+        static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(v))));
+  };
+  auto load_meta = [&](int64_t tt, int64_t& o0, Len& o1) {
     const int64_t r = (tt << 6) + lane;
     const bool in = tt < n_tiles && r < n;
     if constexpr (P33) {
-      o0 = tt < n_tiles ? tile_offset(a, tt << 6) : 0;  // 64-record tiles: boundaries of sparse offsets too
-      o1 = !in ? 0 : a.lengths6 && tt < (int64_t{1} << 28) ? lane_length6(a, tt, lane, dg) : record_length(a, r);
+      o0 = uniform64(tt < n_tiles ? tile_offset(a, tt << 6) : 0);  // 64-record tiles: boundaries of sparse offsets too
+      o1 = !in ? 0 : a.lengths6 && tt < (int64_t{1} << 28) ? lane_length6(a, tt, dg) : static_cast<int>(record_length(a, r));
     } else {
       o0 = in ? a.offsets[r] : 0;
       o1 = in ? a.offsets[r + 1] : 0;
@@ -701,15 +727,9 @@ __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, S
   // tile can span (records of up to 16 letters), the next tile's field words are loaded while this one is
   // scored — its first letter comes with the metadata loaded one tile further ahead — up to the batch's
   // last field (fe); beyond that, the words of kBatch fields at a time are loaded after the tile's lengths.
-  constexpr int kIters = ((64 * 4 * L2W + 6) / 7 + 1 + 63) / 64;  // fields a tile can span / 64
+  constexpr int kIters = (p33_tile_fields(4 * L2W) + 63) / 64;  // fields a tile can span / 64
   constexpr int kBatch = kIters < 4 ? kIters : 4;
-  constexpr bool PF = P33 && kIters <= kBatch;
-  auto uniform64 = [](int64_t v) {
-    return static_cast<int64_t>(
-        (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(v >> 32))))
-         << 32) |
-        static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(v))));
-  };
+  constexpr bool PF = false && P33 && kIters <= kBatch;
   const int64_t fe = PF ? (tile_offset(a, n) + 6) / 7 : 0;
   uint32_t flo[kBatch], fhi[kBatch];
   auto prefetch_fields = [&](int64_t tt, int64_t oo) {
@@ -723,7 +743,8 @@ __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, S
       if (tt < n_tiles && f0 + f < fe) p33_field_words(base32, b0, f, flo[b], fhi[b]);
     }
   };
-  int64_t o0, o1, p0 = 0, p1 = 0;
+  int64_t o0, p0 = 0;
+  Len o1, p1 = 0;
   load_meta(t, o0, o1);
   if constexpr (PF) {
     load_meta(t + waves, p0, p1);
@@ -742,7 +763,9 @@ __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, S
       const int64_t f0 = st / 7;
       const int s0 = static_cast<int>(st - 7 * f0);
       const int excl = wave_exclusive_sum_dpp(L2);
-      const int nf = (s0 + __builtin_amdgcn_readlane(excl + L2, 63) + 6) / 7;
+      // (a batch whose records exceed its max_l2 gets wrong results, never another wave's slots)
+      const int nf = min((s0 + __builtin_amdgcn_readlane(excl + L2, 63) + 6) / 7,
+                         (lay.wave_bytes >> 3) - p33_lane_slots(L2W) - 1);
       const uint32_t* base32 = reinterpret_cast<const uint32_t*>(a.codes) + ((33 * f0) >> 5);
       const int b0 = static_cast<int>((33 * f0) & 31);
       if constexpr (PF) {
@@ -757,11 +780,13 @@ __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, S
       for (int f0b = 0; !PF && f0b < nf; f0b += 64 * kBatch) {  // wave-uniform
         uint32_t lo[kBatch], hi[kBatch];
 #pragma unroll
-        for (int b = 0; b < kBatch; ++b) {
+        for (int b = 0; b < kBatch; ++b) {  // unconditional (field 0 for lanes past the tile): one wait per batch
           const int f = f0b + 64 * b + lane;
-          lo[b] = hi[b] = 0u;
-          if (f < nf) p33_field_words(base32, b0, f, lo[b], hi[b]);
+          p33_field_words(base32, b0, f < nf ? f : 0, lo[b], hi[b]);
         }
+#pragma unroll
+        for (int b = 0; b < kBatch; ++b) asm volatile("" ::"v"(lo[b]), "v"(hi[b]));  // the loads stay ahead
+        // of the decode's branches (the compiler would sink each into its branch, one wait per field)
 #pragma unroll
         for (int b = 0; b < kBatch; ++b) {
           const int f = f0b + 64 * b + lane;
@@ -789,7 +814,8 @@ __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, S
         wd[k] = left >= 32 ? w : (left <= 0 ? 0u : (w & ((1u << left) - 1u)));
       }
     }
-    int64_t n0, n1;
+    int64_t n0;
+    Len n1;
     if constexpr (PF) {  // in flight while this tile is scored: the next tile's fields, the metadata after it
       prefetch_fields(t + waves, p0);
       load_meta(t + 2 * waves, n0, n1);
@@ -818,17 +844,18 @@ __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, S
 // occupancy the instance reaches.
 inline void launch_direct_instance(void (*kernel)(ProblemView, ShortArgs, SwipeLayout), const ProblemView& pv,
                                    const ShortArgs& b, const SwipeLayout& lay, int num_cus, hipStream_t stream) {
+  constexpr int block = kBlockD;
   int occ = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(kernel), kBlockD, lay.total) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(kernel), block, lay.total) !=
           hipSuccess ||
       occ < 1) {
     (void)hipGetLastError();
     occ = 1;
   }
   const int64_t tiles = (b.n + 63) >> 6;
-  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((tiles + kBlockD / 64 - 1) / (kBlockD / 64),
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((tiles + block / 64 - 1) / (block / 64),
                                                                 static_cast<int64_t>(occ) * num_cus));
-  hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(blocks)), dim3(kBlockD), lay.total, stream, pv, b, lay);
+  hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(blocks)), dim3(block), lay.total, stream, pv, b, lay);
 }
 
 template <int NO, int LF>
@@ -851,7 +878,8 @@ bool launch_swipe_noff(const ProblemView& pv, const ShortArgs& b, const SwipeLay
   MOC_SWIPE_CASE(8, false)
   MOC_SWIPE_CASE(4, true)
   MOC_SWIPE_CASE(8, true)
-  MOC_SWIPE_CASE(16, true)  // records of 33..128 letters run the RK form only (configure_swipe)
+  MOC_SWIPE_CASE(12, true)  // records of 33..128 letters run the RK form only (configure_swipe)
+  MOC_SWIPE_CASE(16, true)
   MOC_SWIPE_CASE(24, true)
   MOC_SWIPE_CASE(32, true)
 #undef MOC_SWIPE_CASE

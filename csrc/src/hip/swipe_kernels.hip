@@ -106,7 +106,7 @@ void launch_swipe(const ProblemView& pv, const ShortArgs& a, int num_cus, hipStr
       throw Error("launch_swipe: lane-direct batches are byte letters with dense offsets, or P33 letters with "
                   "64-record sparse offsets and lengths");
     const int lf = letter_form(a);
-    const SwipeLayout lay = direct_layout(pv.L1, a.slot, a.rpw, lf);
+    const SwipeLayout lay = direct_layout(pv.L1, a.slot, a.rpw, lf, a.max_l2);
     if (!launch_swipe_instance(lf, pv, a, lay, dim3(1), dim3(kBlockD), num_cus, stream))
       throw Error("launch_swipe: no instance for this configuration");
     return;

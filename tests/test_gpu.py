@@ -1184,6 +1184,31 @@ def test_wire_device_resident(engine, shape, n):
     assert np.array_equal(got, ref)
 
 
+@pytest.mark.parametrize("L1,lo,hi", [(30, 3, 16), (50, 17, 32), (60, 33, 48), (70, 44, 48), (80, 49, 64)])
+def test_wire_device_resident_record_words(engine, L1, lo, hi):
+    # P33 batches at every record-word width of the lane-direct kernel (4, 8, 12 and 16 words): the decode
+    # slices are sized by the batch's longest record, the base-6 lengths (every octet position and digit)
+    # decoded in f32; random lengths and weights, checked against the CPU engine
+    from mpi_openmp_cuda_amd.parallel.wire import WireSlice
+    from mpi_openmp_cuda_amd.utils.synthetic import Shape, make_shape
+
+    prob = make_shape(Shape((7, 3, 2, 5), L1, lo, hi), 40_001, seed=L1 + hi)
+    engine.set_problem(prob.weights, prob.seq1)
+    wire = WireSlice.from_csr(prob.codes, prob.offsets)
+    res = wire.alloc_results(engine)
+    dev = torch.device("cuda:0")
+    letters = torch.from_numpy(wire.codes).to(dev)
+    offsets = torch.from_numpy(wire.offsets).to(dev)
+    lengths = torch.from_numpy(wire.lengths).to(dev) if wire.lengths is not None else None
+    out = torch.zeros(res.nbytes, dtype=torch.uint8, device=dev)
+    engine.solve_wire_device(letters, offsets, lengths, wire.n, out, wire.fmt, (wire.l2_min, wire.l2_max),
+                             lengths_bits=wire.len_bits or 8, lengths_base=wire.len_base)
+    st = engine.stats()
+    assert st["direct"] == 1 and st["kernels"] == ["swipe"], st
+    res.view(np.uint8)[:] = out.cpu().numpy()
+    assert np.array_equal(wire.triples(engine), as_triples(search_cpu(prob)))
+
+
 # ---- narrow-integer fast paths at their exactness bounds (csrc/include/moc/kernel_bounds.hpp) --------------
 # Every case runs the adversarial input (utils/synthetic.make_extreme: Seq1 = "AZAZ...", pieces of it at even
 # and odd offsets, so |D| reaches 2 W L2 exactly) at the bound — the fast form must be chosen and exact — and

@@ -1,5 +1,6 @@
 """Exhaustive checks of the multiply-by-reciprocal constants the device decoders use
-(csrc/src/hip/swipe_impl.hpp: decode_p33_field, len6_digit / lane_length6). numpy, CPU only.
+(csrc/src/hip/swipe_impl.hpp: decode_p33_field, record_words_p33, len6_digit / lane_length6). numpy,
+CPU only.
 
     python tools/p33_magic_check.py
 """
@@ -24,14 +25,18 @@ def main():
     assert m676 == 6353502 and m676 < (1 << 24)  # a v_mul_hi_u32_u24 operand
     check_range(0, 1 << 19, lambda v: (v * U64(m676)) >> U64(32), lambda v: v // U64(676))
     check_range(0, 676, lambda v: (v * U64(2521)) >> U64(16), lambda v: v // U64(26))
-    # base-6 length digits: octet v < 2^21, digit j = (v / 6^j) % 6
-    ms = [0, 2863311531, 3817748708, 2545165806, 3393554407, 2262369605, 3016492806, 4021990408]
-    shs = [0, 2, 5, 7, 10, 12, 15, 18]
-    for j in range(1, 8):
-        assert ms[j] == -(-(1 << (32 + shs[j])) // 6 ** j) and ms[j] < (1 << 32)
-        check_range(0, 1 << 21, lambda v, j=j: ((v * U64(ms[j])) >> U64(32)) >> U64(shs[j]),
-                    lambda v, j=j: v // U64(6 ** j))
-    check_range(0, 1 << 21, lambda v: (v * U64(715827883)) >> U64(32), lambda v: v // U64(6))
+    # record_words_p33: q0 / 7 = (q0 * 9363) >> 16 for every record start q0 <= 6 + 63 * 64 of a tile
+    check_range(0, 13110, lambda v: (v * U64(9363)) >> U64(16), lambda v: v // U64(7))
+    assert (13110 * 9363) >> 16 != 13110 // 7
+    # base-6 length digits (lane_length6): octet v < 2^21, digit j = (v / 6^j) - 6 (v / 6^(j+1)), each
+    # quotient trunc((v + 0.5) * fl(1 / 6^i)) in f32 (round-to-nearest product), i = 0..8
+    v = np.arange(1 << 21, dtype=np.uint32)
+    fv = v.astype(np.float32) + np.float32(0.5)
+    for i in range(9):
+        q = np.trunc(fv * np.float32(1.0 / 6 ** i)).astype(np.int64)
+        assert (q == v // 6 ** i).all(), i
+    # the lane's octet position: u / 3 = (u * 11) >> 5 for u = (8 t) % 3 + lane / 8 <= 9
+    assert all(((u * 11) >> 5) == u // 3 for u in range(10))
     print("ok")
 
 
