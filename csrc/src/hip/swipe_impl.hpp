@@ -544,7 +544,8 @@ inline SwipeLayout direct_layout(int L1, int noff, int l2w, int lf, int64_t max_
   if (lf == 2) {
     const int ml = static_cast<int>(std::min<int64_t>(std::max<int64_t>(max_l2, 1), 4 * l2w));
     l.wave_bytes = 8 * (p33_tile_fields(ml) + p33_lane_slots(l2w) + 1);
-    l.codes_off = al16(l.s_off + swipe_anchor_bytes(l2w));
+    l.res_off = al16(l.s_off + swipe_anchor_bytes(l2w));  // the digit-pair table (p33_pair_table)
+    l.codes_off = l.res_off + al16(2 * 676);
     l.total = l.codes_off + (kBlockD / 64) * l.wave_bytes;
   }
   return l;
@@ -598,6 +599,22 @@ __device__ __forceinline__ uint2 decode_p33_field(uint32_t lo, uint32_t hi, int 
   const uint32_t b10 = mad_i24(b32, -676, B), a10 = mad_i24(a2, -676, A);
   // letter codes are digit + 1; the pad byte stays 0
   return make_uint2((p33_pair(b10) | (p33_pair(b32) << 16)) + 0x01010101u, (p33_pair(a10) | (a2 << 16)) + 0x00010101u);
+}
+
+// The lane-direct kernel's decode: the same digits, each pair of them (v < 676) one LDS read of a table of
+// 16-bit letter-code pairs (built once per block) instead of three multiply-adds.
+__device__ __forceinline__ void build_p33_pair_table(uint16_t* pairs, int tid, int nthreads) {
+  for (int v = tid; v < 676; v += nthreads)
+    pairs[v] = static_cast<uint16_t>((v % 26 + 1) | ((v / 26 + 1) << 8));
+}
+__device__ __forceinline__ uint2 decode_p33_field_lut(uint32_t lo, uint32_t hi, int b0, int f, const uint16_t* pairs) {
+  const uint64_t ww = static_cast<uint64_t>(lo) | (static_cast<uint64_t>(hi) << 32);
+  const uint64_t x = (ww >> ((b0 + 33 * f) & 31)) & 0x1FFFFFFFFull;
+  const uint32_t A = __umulhi(static_cast<uint32_t>(x >> 4), 2463805336u) >> 14;  // digits 4..6
+  const uint32_t B = static_cast<uint32_t>(x) - __umul24(A, 456976u);  // digits 0..3
+  const uint32_t b32 = mulhi_u24(B, 6353502u), a2 = mulhi_u24(A, 6353502u);
+  const uint32_t b10 = mad_i24(b32, -676, B), a10 = mad_i24(a2, -676, A);
+  return make_uint2(pairs[b10] | (static_cast<uint32_t>(pairs[b32]) << 16), pairs[a10] | ((a2 + 1u) << 16));
 }
 
 // The letters of a lane's record from the tile's 8-byte field slots: NS slots from the record's first field
@@ -694,6 +711,8 @@ __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, S
   constexpr bool P33 = LF == 2;
   constexpr int KB = RK ? 1 : bounds::swipe_kbits(L2W);
   swipe_build_tables<RK, KB, NOFF, L2W>(smem, pv, threadIdx.x, kBlockD);
+  uint16_t* pairs = reinterpret_cast<uint16_t*>(smem + lay.res_off);
+  if constexpr (P33) build_p33_pair_table(pairs, threadIdx.x, kBlockD);
   __syncthreads();  // the only barrier: tables complete
   const int lane = threadIdx.x & 63;
   const bool spec = pv.semantics == static_cast<int>(Semantics::Spec);
@@ -723,33 +742,14 @@ __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, S
       o1 = in ? a.offsets[r + 1] : 0;
     }
   };
-  // P33 fields: lanes take fields lane, lane + 64, ... of a tile. Where kBatch per lane cover every field a
-  // tile can span (records of up to 16 letters), the next tile's field words are loaded while this one is
-  // scored — its first letter comes with the metadata loaded one tile further ahead — up to the batch's
-  // last field (fe); beyond that, the words of kBatch fields at a time are loaded after the tile's lengths.
+  // P33 fields: lanes take fields lane, lane + 64, ... of a tile, the words of up to kBatch fields per lane
+  // loaded before any is decoded. (Loading the next tile's words while this one is scored held 18 more
+  // VGPRs across the sweep: 4 waves per SIMD instead of 8, and 7 % slower on input6.)
   constexpr int kIters = (p33_tile_fields(4 * L2W) + 63) / 64;  // fields a tile can span / 64
   constexpr int kBatch = kIters < 4 ? kIters : 4;
-  constexpr bool PF = false && P33 && kIters <= kBatch;
-  const int64_t fe = PF ? (tile_offset(a, n) + 6) / 7 : 0;
-  uint32_t flo[kBatch], fhi[kBatch];
-  auto prefetch_fields = [&](int64_t tt, int64_t oo) {
-    const int64_t f0 = uniform64(oo) / 7;
-    const uint32_t* base32 = reinterpret_cast<const uint32_t*>(a.codes) + ((33 * f0) >> 5);
-    const int b0 = static_cast<int>((33 * f0) & 31);
-#pragma unroll
-    for (int b = 0; b < kBatch; ++b) {
-      const int f = 64 * b + lane;
-      flo[b] = fhi[b] = 0u;
-      if (tt < n_tiles && f0 + f < fe) p33_field_words(base32, b0, f, flo[b], fhi[b]);
-    }
-  };
-  int64_t o0, p0 = 0;
-  Len o1, p1 = 0;
+  int64_t o0;
+  Len o1;
   load_meta(t, o0, o1);
-  if constexpr (PF) {
-    load_meta(t + waves, p0, p1);
-    prefetch_fields(t, o0);
-  }
   for (; t < n_tiles; t += waves) {  // wave-uniform
     const int64_t r = (t << 6) + lane;
     const int L2 = static_cast<int>(P33 ? o1 : o1 - o0);
@@ -768,16 +768,7 @@ __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, S
                          (lay.wave_bytes >> 3) - p33_lane_slots(L2W) - 1);
       const uint32_t* base32 = reinterpret_cast<const uint32_t*>(a.codes) + ((33 * f0) >> 5);
       const int b0 = static_cast<int>((33 * f0) & 31);
-      if constexpr (PF) {
-#pragma unroll
-        for (int b = 0; b < kBatch; ++b) {
-          const int f = 64 * b + lane;
-          if (f < nf) *reinterpret_cast<uint2*>(wbuf + 8 * f) = decode_p33_field(flo[b], fhi[b], b0, f);
-        }
-      }
-      // fields lane, lane + 64, ...: the words of up to kBatch fields per lane are loaded before any is
-      // decoded (one memory latency per batch, not per field)
-      for (int f0b = 0; !PF && f0b < nf; f0b += 64 * kBatch) {  // wave-uniform
+      for (int f0b = 0; f0b < nf; f0b += 64 * kBatch) {  // wave-uniform
         uint32_t lo[kBatch], hi[kBatch];
 #pragma unroll
         for (int b = 0; b < kBatch; ++b) {  // unconditional (field 0 for lanes past the tile): one wait per batch
@@ -790,7 +781,7 @@ __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, S
 #pragma unroll
         for (int b = 0; b < kBatch; ++b) {
           const int f = f0b + 64 * b + lane;
-          if (f < nf) *reinterpret_cast<uint2*>(wbuf + 8 * f) = decode_p33_field(lo[b], hi[b], b0, f);
+          if (f < nf) *reinterpret_cast<uint2*>(wbuf + 8 * f) = decode_p33_field_lut(lo[b], hi[b], b0, f, pairs);
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slice's letters before any lane reads them
@@ -816,24 +807,12 @@ __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, S
     }
     int64_t n0;
     Len n1;
-    if constexpr (PF) {  // in flight while this tile is scored: the next tile's fields, the metadata after it
-      prefetch_fields(t + waves, p0);
-      load_meta(t + 2 * waves, n0, n1);
-    } else {
-      load_meta(t + waves, n0, n1);
-    }
+    load_meta(t + waves, n0, n1);
     const Result res = swipe_lane<NOFF, L2W, RK>(smem, wd, L2, on, L1, a.max_l2, pv.semantics);
     if (mine) store_result(a.out, r, a.fmt, res, pv.r2);
     if constexpr (P33) __builtin_amdgcn_wave_barrier();  // every lane read the slice before the next tile's writes
-    if constexpr (PF) {
-      o0 = p0;
-      o1 = p1;
-      p0 = n0;
-      p1 = n1;
-    } else {
-      o0 = n0;
-      o1 = n1;
-    }
+    o0 = n0;
+    o1 = n1;
   }
 }
 
