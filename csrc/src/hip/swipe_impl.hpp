@@ -537,13 +537,19 @@ constexpr int kBlockD = 512;  // 8 waves share one set of LDS tables
 // P33 tiles: one 8-byte slot per field (7 letters + a pad byte) for the fields a tile of records of at most
 // max_l2 letters can span, plus the slots a lane's read may run past the last one. Sized by the batch's
 // longest record, not by the instance's record words: LDS decides how many blocks share a CU.
-constexpr int p33_tile_fields(int max_l2) { return (64 * max_l2 + 6) / 7 + 1; }
+constexpr int p33_tile_fields(int records, int max_l2) { return (records * max_l2 + 6) / 7 + 1; }
 constexpr int p33_lane_slots(int l2w) { return (4 * l2w + 8 + 6) / 7; }  // the letters of words 0..l2w+1
+// 64-record halves per lane-direct tile: P33 records of at most 16 letters with at most 20 offsets per lane
+// decode the fields of 128 records at once, so the last, partly idle round of 64 fields comes once per 128
+// records (input6: 156 fields in 3 rounds instead of 2 x 78 in 2 + 2). Those instances fit 64 VGPRs (8
+// waves per SIMD, amdgpu_waves_per_eu below) without spills; wider ones would spill, and their sweep
+// outweighs the decode more.
+constexpr int direct_halves(int lf, int l2w, int noff) { return lf == 2 && l2w == 4 && noff <= 20 ? 2 : 1; }
 inline SwipeLayout direct_layout(int L1, int noff, int l2w, int lf, int64_t max_l2) {
   SwipeLayout l = swipe_layout(L1, noff, l2w, 0, 0, 0, 0);
   if (lf == 2) {
     const int ml = static_cast<int>(std::min<int64_t>(std::max<int64_t>(max_l2, 1), 4 * l2w));
-    l.wave_bytes = 8 * (p33_tile_fields(ml) + p33_lane_slots(l2w) + 1);
+    l.wave_bytes = 8 * (p33_tile_fields(64 * direct_halves(lf, l2w, noff), ml) + p33_lane_slots(l2w) + 1);
     l.res_off = al16(l.s_off + swipe_anchor_bytes(l2w));  // the digit-pair table (p33_pair_table)
     l.codes_off = l.res_off + al16(2 * 676);
     l.total = l.codes_off + (kBlockD / 64) * l.wave_bytes;
@@ -625,7 +631,8 @@ template <int NW>
 __device__ __forceinline__ void record_words_p33(const uint8_t* slots, int q0, int L2, bool on, uint32_t (&wd)[NW]) {
   constexpr int NS = p33_lane_slots(NW);
   static_assert(NW <= 16, "the 24-bit q0 / 7 below needs q0 < 13110");
-  // q0 / 7 by a 24-bit multiply (exact below 13110; q0 <= 6 + 63 * 4 * NW <= 4038), q0 % 7 by a 24-bit mad
+  // q0 / 7 by a 24-bit multiply (exact below 13110; q0 <= 6 + 63 * 4 * NW <= 4038 in 64-record tiles,
+  // 6 + 127 * 4 * NW <= 4070 in 128-record ones, NW <= 8), q0 % 7 by a 24-bit mad
   const int fa = static_cast<int>(__umul24(static_cast<uint32_t>(q0), 9363u) >> 16);
   const int sh = static_cast<int>(mad_i24(static_cast<uint32_t>(fa), -7, static_cast<uint32_t>(q0)));
   uint32_t dw[2 * NS];
@@ -706,7 +713,8 @@ __device__ __forceinline__ int lane_length6(const ShortArgs& a, int64_t t, Len6D
 }
 
 template <int NOFF, int L2W, int LF, bool RK>
-__global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, ShortArgs a, SwipeLayout lay) {
+__global__ __launch_bounds__(kBlockD) __attribute__((amdgpu_waves_per_eu(direct_halves(LF, L2W, NOFF) == 2 ? 8 : 1)))
+void swipe_direct_kernel(ProblemView pv, ShortArgs a, SwipeLayout lay) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr bool P33 = LF == 2;
   constexpr int KB = RK ? 1 : bounds::swipe_kbits(L2W);
@@ -717,13 +725,14 @@ __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, S
   const int lane = threadIdx.x & 63;
   const bool spec = pv.semantics == static_cast<int>(Semantics::Spec);
   const int L1 = pv.L1;
-  const int64_t n = a.n, n_tiles = (n + 63) >> 6;
+  constexpr int H = direct_halves(LF, L2W, NOFF);  // 64-record halves per tile
+  const int64_t n = a.n, n_tiles = (n + 64 * H - 1) / (64 * H);
   const int64_t waves = static_cast<int64_t>(gridDim.x) * (kBlockD / 64);
   // the wave's tile index, its tile start (P33) and the loop bounds live in scalar registers
   int64_t t = static_cast<int64_t>(blockIdx.x) * (kBlockD / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const Len6Digit dg = len6_digit(lane);
   uint8_t* wbuf = smem + lay.codes_off + (threadIdx.x >> 6) * lay.wave_bytes;  // P33: this wave's
-  // bytes: the record's offsets; P33: the tile's first letter (o0, every lane) and the record's length (o1)
+  // bytes: the record's offsets; P33: the tile's first letter (o0, every lane) and the records' lengths (o1)
   using Len = std::conditional_t<P33, int, int64_t>;  // P33: a length; bytes: the record's end offset
   auto uniform64 = [](int64_t v) {
     return static_cast<int64_t>(
@@ -731,41 +740,56 @@ __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, S
          << 32) |
         static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(v))));
   };
-  auto load_meta = [&](int64_t tt, int64_t& o0, Len& o1) {
-    const int64_t r = (tt << 6) + lane;
-    const bool in = tt < n_tiles && r < n;
+  auto load_meta = [&](int64_t tt, int64_t& o0, Len (&o1)[H]) {
     if constexpr (P33) {
-      o0 = uniform64(tt < n_tiles ? tile_offset(a, tt << 6) : 0);  // 64-record tiles: boundaries of sparse offsets too
-      o1 = !in ? 0 : a.lengths6 && tt < (int64_t{1} << 28) ? lane_length6(a, tt, dg) : static_cast<int>(record_length(a, r));
+      // tiles of 64 H records: boundaries of sparse (64-record) offsets too
+      o0 = uniform64(tt < n_tiles ? tile_offset(a, tt * 64 * H) : 0);
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        const int64_t t64 = tt * H + h, r = (t64 << 6) + lane;
+        const bool in = tt < n_tiles && r < n;
+        o1[h] = !in ? 0
+                    : a.lengths6 && t64 < (int64_t{1} << 28) ? lane_length6(a, t64, dg)
+                                                              : static_cast<int>(record_length(a, r));
+      }
     } else {
+      const int64_t r = (tt << 6) + lane;
+      const bool in = tt < n_tiles && r < n;
       o0 = in ? a.offsets[r] : 0;
-      o1 = in ? a.offsets[r + 1] : 0;
+      o1[0] = in ? a.offsets[r + 1] : 0;
     }
   };
   // P33 fields: lanes take fields lane, lane + 64, ... of a tile, the words of up to kBatch fields per lane
   // loaded before any is decoded. (Loading the next tile's words while this one is scored held 18 more
   // VGPRs across the sweep: 4 waves per SIMD instead of 8, and 7 % slower on input6.)
-  constexpr int kIters = (p33_tile_fields(4 * L2W) + 63) / 64;  // fields a tile can span / 64
+  constexpr int kIters = (p33_tile_fields(64 * H, 4 * L2W) + 63) / 64;  // fields a tile can span / 64
   constexpr int kBatch = kIters < 4 ? kIters : 4;
   int64_t o0;
-  Len o1;
+  Len o1[H];
   load_meta(t, o0, o1);
   for (; t < n_tiles; t += waves) {  // wave-uniform
-    const int64_t r = (t << 6) + lane;
-    const int L2 = static_cast<int>(P33 ? o1 : o1 - o0);
-    const bool in = r < n;
-    const bool mine = in && (L2 < L1 ? L1 - L2 + (spec ? 1 : 0) : 1) <= NOFF;  // others belong to the tile kernel
-    const bool on = mine && L2 <= L1;
     uint32_t wd[L2W];
+    int L2h[H], excl[H];  // the halves' lengths and (P33) their records' starts within the tile
+#pragma unroll
+    for (int h = 0; h < H; ++h) L2h[h] = static_cast<int>(P33 ? o1[h] : o1[0] - o0);
+    auto searching = [&](int h, int L2) {  // others belong to the tile kernel
+      return ((t * H + h) << 6) + lane < n && (L2 < L1 ? L1 - L2 + (spec ? 1 : 0) : 1) <= NOFF;
+    };
+    int s0 = 0;
     if constexpr (P33) {
-      // the tile's first letter and field (wave-uniform: scalar arithmetic), the lane's start within the tile
+      // the tile's first letter and field (wave-uniform: scalar arithmetic), the lanes' starts within the tile
       const int64_t st = uniform64(o0);
       const int64_t f0 = st / 7;
-      const int s0 = static_cast<int>(st - 7 * f0);
-      const int excl = wave_exclusive_sum_dpp(L2);
+      s0 = static_cast<int>(st - 7 * f0);
+      int tot = 0;
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        const int e = wave_exclusive_sum_dpp(L2h[h]);
+        excl[h] = tot + e;
+        tot += __builtin_amdgcn_readlane(e + L2h[h], 63);
+      }
       // (a batch whose records exceed its max_l2 gets wrong results, never another wave's slots)
-      const int nf = min((s0 + __builtin_amdgcn_readlane(excl + L2, 63) + 6) / 7,
-                         (lay.wave_bytes >> 3) - p33_lane_slots(L2W) - 1);
+      const int nf = min((s0 + tot + 6) / 7, (lay.wave_bytes >> 3) - p33_lane_slots(L2W) - 1);
       const uint32_t* base32 = reinterpret_cast<const uint32_t*>(a.codes) + ((33 * f0) >> 5);
       const int b0 = static_cast<int>((33 * f0) & 31);
       for (int f0b = 0; f0b < nf; f0b += 64 * kBatch) {  // wave-uniform
@@ -787,9 +811,10 @@ __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, S
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the slice's letters before any lane reads them
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      record_words_p33<L2W>(wbuf, s0 + excl, L2, on, wd);
     } else {
       // the aligned words holding the record's letters, and only those (never past its last letter's word)
+      const int L2 = L2h[0];
+      const bool on = searching(0, L2) && L2 <= L1;
       const uintptr_t p = reinterpret_cast<uintptr_t>(a.codes + o0);
       const uint32_t* w32 = reinterpret_cast<const uint32_t*>(p & ~uintptr_t{3});
       const int sh = static_cast<int>(p & 3) * 8;
@@ -806,13 +831,24 @@ __global__ __launch_bounds__(kBlockD) void swipe_direct_kernel(ProblemView pv, S
       }
     }
     int64_t n0;
-    Len n1;
-    load_meta(t + waves, n0, n1);
-    const Result res = swipe_lane<NOFF, L2W, RK>(smem, wd, L2, on, L1, a.max_l2, pv.semantics);
-    if (mine) store_result(a.out, r, a.fmt, res, pv.r2);
+    Len n1[H];
+    load_meta(t + waves, n0, n1);  // in flight while this tile is scored
+    // the second half's length and start in one register across the first half's sweep (VGPRs: 8 waves per
+    // SIMD at 64)
+    const uint32_t later = static_cast<uint32_t>(L2h[H - 1]) | (static_cast<uint32_t>(excl[H - 1]) << 8);
+#pragma unroll 1
+    for (int h = 0; h < H; ++h) {  // wave-uniform; one copy of the sweep
+      const int L2 = h == 0 ? L2h[0] : static_cast<int>(later & 0xffu);
+      const bool mine = searching(h, L2);
+      const bool on = mine && L2 <= L1;
+      if constexpr (P33) record_words_p33<L2W>(wbuf, s0 + (h == 0 ? excl[0] : static_cast<int>(later >> 8)), L2, on, wd);
+      const Result res = swipe_lane<NOFF, L2W, RK>(smem, wd, L2, on, L1, a.max_l2, pv.semantics);
+      if (mine) store_result(a.out, ((t * H + h) << 6) + lane, a.fmt, res, pv.r2);
+    }
     if constexpr (P33) __builtin_amdgcn_wave_barrier();  // every lane read the slice before the next tile's writes
     o0 = n0;
-    o1 = n1;
+#pragma unroll
+    for (int h = 0; h < H; ++h) o1[h] = n1[h];
   }
 }
 

@@ -1184,11 +1184,12 @@ def test_wire_device_resident(engine, shape, n):
     assert np.array_equal(got, ref)
 
 
-@pytest.mark.parametrize("L1,lo,hi", [(30, 3, 16), (50, 17, 32), (60, 33, 48), (70, 44, 48), (80, 49, 64)])
+@pytest.mark.parametrize("L1,lo,hi", [(24, 5, 16), (30, 3, 16), (50, 17, 32), (60, 33, 48), (70, 44, 48), (80, 49, 64)])
 def test_wire_device_resident_record_words(engine, L1, lo, hi):
-    # P33 batches at every record-word width of the lane-direct kernel (4, 8, 12 and 16 words): the decode
-    # slices are sized by the batch's longest record, the base-6 lengths (every octet position and digit)
-    # decoded in f32; random lengths and weights, checked against the CPU engine
+    # P33 batches at every record-word width of the lane-direct kernel (4 — with 20 offsets per lane in
+    # 128-record tiles, with 28 in 64-record ones — 8, 12 and 16 words): the decode slices are sized by the
+    # batch's longest record, the base-6 lengths (every octet position and digit) decoded in f32; random
+    # lengths and weights, checked against the CPU engine
     from mpi_openmp_cuda_amd.parallel.wire import WireSlice
     from mpi_openmp_cuda_amd.utils.synthetic import Shape, make_shape
 
