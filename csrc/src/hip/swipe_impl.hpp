@@ -524,15 +524,15 @@ __global__ __launch_bounds__(kBlock) void swipe_search_kernel(ProblemView pv, Sh
 // consecutive records at a time, one per lane, straight from device memory — no block scan and no barrier
 // after the block's tables are built. (The block-synchronous tile pipeline of swipe_search_kernel — grab,
 // barrier, scan, barrier, copy — held device-resident input6 at ~0.45 of its 0.54 ms even with the hot loop
-// removed, round 4's A/B.) Waves walk the 64-record tiles t = wave, wave + waves, ... and load the next
-// tile's offsets (or lengths) while the current one is scored.
+// removed, round 4's A/B.) Waves walk the tiles t = wave, wave + waves, ... (64 records, or 128 as two
+// halves: direct_halves) and load the next tile's offsets (or lengths) while the current one is scored.
 //   LF 0: byte letters, dense offsets — a lane loads its record's aligned words itself.
 //   LF 2: P33 fields (the wire format: 33 bits per 7 letters) with dense or 64-record sparse offsets and
-//         narrow lengths — the wave's tile starts at tile_offset, its lanes' starts come from a wave prefix
-//         sum of the lengths, lanes decode the tile's fields (field = lane, lane + 64, ...) into 8-byte
-//         slots of a wave-private LDS slice (one ds_write_b64 per field: seven byte stores cost +62 % LDS
-//         cycles), and each lane gathers its record's words from there (wave-level ordering
-//         only: the slice is the wave's own).
+//         narrow lengths — the wave's tile starts at tile_offset, its lanes' starts come from wave prefix
+//         sums of the lengths, lanes decode the tile's fields (field = lane, lane + 64, ...; digit pairs
+//         from an LDS table) into 8-byte slots of a wave-private LDS slice (one ds_write_b64 per field:
+//         seven byte stores cost +62 % LDS cycles), and each lane gathers its record's words from there
+//         (wave-level ordering only: the slice is the wave's own).
 constexpr int kBlockD = 512;  // 8 waves share one set of LDS tables
 // P33 tiles: one 8-byte slot per field (7 letters + a pad byte) for the fields a tile of records of at most
 // max_l2 letters can span, plus the slots a lane's read may run past the last one. Sized by the batch's

@@ -26,8 +26,8 @@ PEAK_PACKED, PEAK_VALU32, PEAK_LDS = 0.94, 1.69, 0.48  # wave-instructions per C
 ROWS = [  # shape, kernel_bench variant, kernel name prefix, form, PMC pass (tools/pmc_roofline.sh)
     ("input6", "tile16", "swipe_direct_kernel<20, 4, 0, false>", "device bytes", "p1"),
     ("input6", "wire", "swipe_direct_kernel<20, 4, 2, false>", "device P33 wire", "p4"),
-    ("input1", "tile16", "swipe_direct_kernel<20, 16, 0, true>", "device bytes", "p1"),
-    ("input1", "wire", "swipe_direct_kernel<20, 16, 2, true>", "device P33 wire", "p4"),
+    ("input1", "tile16", "swipe_direct_kernel<20, 12, 0, true>", "device bytes", "p1"),
+    ("input1", "wire", "swipe_direct_kernel<20, 12, 2, true>", "device P33 wire", "p4"),
     ("mid", "tile16", "swipe_direct_kernel<64, 24, 0, true>", "device bytes, 24 record words", "p1"),
     ("input3", "tile16", "tile16_search_kernel<4, false, true>", "widened pairs", "p2"),
     ("limits", "tile16", "tile16_slide_kernel<4, 8>", "sliding widened windows", "p2"),
