@@ -129,6 +129,23 @@ __device__ __forceinline__ int wave_prefix_sum_dpp(int v) {
   v += dpp_or0<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
   return v;
 }
+// N independent prefix sums step by step: each DPP add waits two cycles on the previous one of its own
+// chain, so the chains interleave instead of stalling on s_nop.
+template <int N>
+__device__ __forceinline__ void wave_prefix_sums_dpp(int (&v)[N]) {
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] += dpp_or0<0x111, 0xf>(v[k]);
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] += dpp_or0<0x112, 0xf>(v[k]);
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] += dpp_or0<0x114, 0xf>(v[k]);
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] += dpp_or0<0x118, 0xf>(v[k]);
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] += dpp_or0<0x142, 0xa>(v[k]);
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] += dpp_or0<0x143, 0xc>(v[k]);
+}
 // Maximum over the lanes of a wave (unsigned; 0 is the identity) on the DPP network, in every lane's result
 // at lane 63.
 __device__ __forceinline__ uint32_t wave_max_u32_dpp(uint32_t v) {
@@ -450,20 +467,25 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
       };
       // full chunks: G steps per group, G * UU reads in flight (UU = 8 keeps the VGPRs within 4 waves per SIMD)
       constexpr int G = UU >= 8 ? 2 : UU >= 4 ? 4 : 8;
-      // every 64-step chunk starts from zero halves and folds them into the int32 state at its end
-      auto flush = [&](bool any_key) {
+      // every 64-step chunk starts from zero halves and folds them into the int32 state at its end; the
+      // record's first chunk sets the state (no adds to zero, no max with INT32_MIN); a chunk of one step
+      // has no key step (compile-time forms: no per-lane selects)
+      auto flush = [&](auto first_c, auto key_c) {
+        constexpr bool First = decltype(first_c)::value, AnyKey = decltype(key_c)::value;
 #pragma unroll
         for (int u = 0; u < UU; ++u) {
-          if (any_key) {
-            mxA[u] = max(mxA[u], DcA[u] + lo16(best[u]));
-            mxB[u] = max(mxB[u], DcB[u] + hi16(best[u]));
+          if (AnyKey) {
+            mxA[u] = First ? lo16(best[u]) : max(mxA[u], DcA[u] + lo16(best[u]));
+            mxB[u] = First ? hi16(best[u]) : max(mxB[u], DcB[u] + hi16(best[u]));
           }
-          DcA[u] += lo16(acc[u]);
-          DcB[u] += hi16(acc[u]);
+          DcA[u] = First ? lo16(acc[u]) : DcA[u] + lo16(acc[u]);
+          DcB[u] = First ? hi16(acc[u]) : DcB[u] + hi16(acc[u]);
           acc[u] = 0;
           best[u] = kBestInit;
         }
       };
+      using True = std::true_type;
+      using False = std::false_type;
       // Tot of the anchor offset oA (first offset past the tile or past the valid range): each chunk's
       // lanes add their step's pair score from LDS while the sweep runs
       const int oA = min(o0 + kSpan, need);
@@ -481,7 +503,7 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
         replicate(so, so16);
 #pragma unroll
         for (int j = 0; j < 64; j += G) group(so16, j, std::integral_constant<int, G>());
-        flush(true);
+        flush(False(), True());  // (a first-chunk form here peels the loop: 128 VGPRs and spills)
         c = c_next;
       }
       if (steps > 0) {  // last chunk: 1..64 steps; no hyphen after the final letter
@@ -528,51 +550,88 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
         }
         for (; j < m - 1; ++j) step(so, j, true);
         step(so, m - 1, false);
-        flush(m > 1);
+        if (i0 == 0 && m > 1)  // wave-uniform: the record's only chunk (short records, input4)
+          flush(True(), True());
+        else if (m > 1)
+          flush(False(), True());
+        else if (i0 == 0)
+          flush(True(), False());
+        else
+          flush(False(), False());
       }
       // ---- Tot per offset: anchor diagonal oA, then suffix sums of the D totals (valid offsets only)
       anchor = __builtin_amdgcn_readlane(wave_prefix_sum_dpp(anchor), 63);
-      int carry = anchor;  // Tot at the end of the sub-tile being processed
+      // Full: every candidate of the tile's sub-tiles is valid (all but a record's last tiles) — no per-lane
+      // limit tests and no masked D totals (compile-time form)
+      auto epilogue = [&](auto full_c, auto key32_c) {
+        constexpr bool Full = decltype(full_c)::value, Key32 = decltype(key32_c)::value;
+        int carry = anchor;  // Tot at the end of the sub-tile being processed
+        int incl[UU];        // the sub-tiles' pair sums, then their inclusive prefix sums over the lanes
 #pragma unroll
-      for (int u = UU - 1; u >= 0; --u) {
-        const int oa = o0 + kSub * u + 2 * lane;
-        const int ca = oa < oA ? DcA[u] : 0, cb = oa + 1 < oA ? DcB[u] : 0;
-        const int pair = ca + cb;
-        const int incl = wave_prefix_sum_dpp(pair);
-        const int sub_total = __builtin_amdgcn_readlane(incl, 63);
-        const int excl = sub_total - incl;   // lanes above this one
-        const int totB = carry + excl + cb;  // Tot_{oa+1}
-        const int totA = totB + ca;          // Tot_{oa}
-        carry += sub_total;
-        if (kib) {
-          // keys ((score + 2^(31 - kib)) << kib) | (2^kib - 1 - idx): the bias and the index term are one
-          // per-lane constant, so a key is one shift-add of the score (moc/kernel_bounds.hpp tile16_key32_bits)
-          const uint32_t c0 = 0x80000000u + kmask - 2u * static_cast<uint32_t>(oa);  // idx 2 oa
-          const uint32_t kA0 = (static_cast<uint32_t>(totA) << kib) + c0;
-          const uint32_t kA1 = ((static_cast<uint32_t>(mxA[u]) + static_cast<uint32_t>(totB)) << kib) + (c0 - 1u);
-          const uint32_t kB0 = (static_cast<uint32_t>(totB) << kib) + (c0 - 2u);
-          const uint32_t kB1 = ((static_cast<uint32_t>(mxB[u]) + static_cast<uint32_t>(totB - cb)) << kib) + (c0 - 3u);
-          // validity as pass1_candidate: o <= last (o < last, or L2 == L1 / spec semantics, for the
-          // un-mutated one), mutants at o < last with L2 >= 2
-          if (o0 + kSub * (u + 1) < last && L2 >= 2) {  // wave-uniform: every candidate of the sub-tile valid
-            acc32 = max(max(acc32, max(kA0, kA1)), max(kB0, kB1));
-          } else {
-            const uint32_t a0 = oa < last || (oa == last && v0_at_last) ? kA0 : 0u;
-            const uint32_t a1 = oa < last && L2 >= 2 ? kA1 : 0u;
-            const uint32_t b0 = oa + 1 < last || (oa + 1 == last && v0_at_last) ? kB0 : 0u;
-            const uint32_t b1 = oa + 1 < last && L2 >= 2 ? kB1 : 0u;
-            acc32 = max(max(acc32, max(a0, a1)), max(b0, b1));
+        for (int u = 0; u < UU; ++u) {
+          const int oa = o0 + kSub * u + 2 * lane;
+          if (!Full) {
+            DcA[u] = oa < oA ? DcA[u] : 0;
+            DcB[u] = oa + 1 < oA ? DcB[u] : 0;
           }
-        } else {
-          if (o0 + kSub * (u + 1) < last && L2 >= 2) {  // wave-uniform: every candidate of the sub-tile valid
-            const uint32_t i0 = 2u * static_cast<uint32_t>(oa);
-            acc64 = max_u64(acc64, max_u64(max_u64(final_key(totA, i0), final_key(mxA[u] + totB, i0 + 1u)),
-                                           max_u64(final_key(totB, i0 + 2u), final_key(mxB[u] + totB - cb, i0 + 3u))));
+          incl[u] = DcA[u] + DcB[u];
+        }
+        wave_prefix_sums_dpp(incl);
+#pragma unroll
+        for (int u = UU - 1; u >= 0; --u) {
+          const int oa = o0 + kSub * u + 2 * lane;
+          const int ca = DcA[u], cb = DcB[u];  // (masked past oA)
+          const int sub_total = __builtin_amdgcn_readlane(incl[u], 63);
+          const int excl = sub_total - incl[u];  // lanes above this one
+          const int totB = carry + excl + cb;    // Tot_{oa+1}
+          const int totA = totB + ca;            // Tot_{oa}
+          carry += sub_total;
+          // every candidate of the sub-tile valid (wave-uniform)
+          const bool all_valid = Full || (o0 + kSub * (u + 1) < last && L2 >= 2);
+          if constexpr (Key32) {
+            // keys ((score + 2^(31 - kib)) << kib) | (2^kib - 1 - idx): the bias and the index term are one
+            // per-lane constant, so a key is one shift-add of the score (moc/kernel_bounds.hpp tile16_key32_bits)
+            const uint32_t c0 = 0x80000000u + kmask - 2u * static_cast<uint32_t>(oa);  // idx 2 oa
+            const uint32_t kA0 = (static_cast<uint32_t>(totA) << kib) + c0;
+            const uint32_t kA1 = ((static_cast<uint32_t>(mxA[u]) + static_cast<uint32_t>(totB)) << kib) + (c0 - 1u);
+            const uint32_t kB0 = (static_cast<uint32_t>(totB) << kib) + (c0 - 2u);
+            const uint32_t kB1 = ((static_cast<uint32_t>(mxB[u]) + static_cast<uint32_t>(totB - cb)) << kib) + (c0 - 3u);
+            // validity as pass1_candidate: o <= last (o < last, or L2 == L1 / spec semantics, for the
+            // un-mutated one), mutants at o < last with L2 >= 2
+            if (all_valid) {
+              acc32 = max(max(acc32, max(kA0, kA1)), max(kB0, kB1));
+            } else {
+              const uint32_t a0 = oa < last || (oa == last && v0_at_last) ? kA0 : 0u;
+              const uint32_t a1 = oa < last && L2 >= 2 ? kA1 : 0u;
+              const uint32_t b0 = oa + 1 < last || (oa + 1 == last && v0_at_last) ? kB0 : 0u;
+              const uint32_t b1 = oa + 1 < last && L2 >= 2 ? kB1 : 0u;
+              acc32 = max(max(acc32, max(a0, a1)), max(b0, b1));
+            }
           } else {
-            acc64 = max_u64(acc64, pass1_candidate(oa, L1, L2, pv.semantics, totA, totB, mxA[u]));
-            acc64 = max_u64(acc64, pass1_candidate(oa + 1, L1, L2, pv.semantics, totB, totB - cb, mxB[u]));
+            if (all_valid) {
+              const uint32_t i0 = 2u * static_cast<uint32_t>(oa);
+              acc64 = max_u64(acc64, max_u64(max_u64(final_key(totA, i0), final_key(mxA[u] + totB, i0 + 1u)),
+                                             max_u64(final_key(totB, i0 + 2u), final_key(mxB[u] + totB - cb, i0 + 3u))));
+            } else {
+              acc64 = max_u64(acc64, pass1_candidate(oa, L1, L2, pv.semantics, totA, totB, mxA[u]));
+              acc64 = max_u64(acc64, pass1_candidate(oa + 1, L1, L2, pv.semantics, totB, totB - cb, mxB[u]));
+            }
           }
         }
+      };
+      // (key width and fullness outside the sub-tile loop: one basic block, the 8 sub-tiles' DPP scans
+      // interleave)
+      const bool full = o0 + kSub * UU < last && L2 >= 2;  // wave-uniform (then oA >= o0 + kSub * UU too)
+      if (kib) {
+        if (full)
+          epilogue(True(), True());
+        else
+          epilogue(False(), True());
+      } else {
+        if (full)
+          epilogue(True(), False());
+        else
+          epilogue(False(), False());
       }
       });
     }
