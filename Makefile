@@ -155,16 +155,20 @@ tsan: $(MPILIB)/libmpi.so
 
 # Device-side bounds checks (MOC_DCHECK: printf, never a fault) in every kernel -> build/debug/libmoc.so;
 # select it with MOC_LIB_PATH=$$PWD/build/debug/libmoc.so.
-debug-kernels:
-	@mkdir -p $(BUILD)/debug
-	for f in $(HIP_SRCS); do \
-	  $(HIPCC) $(HIPFLAGS) -DMOC_DEBUG_KERNELS -DMOC_SRC_HASH='"$(SRC_HASH)"' -c $$f -o $(BUILD)/debug/$$(basename $$f .hip).hip.o || exit 1; \
-	done
-	for lf in 0 2; do for no in $(SWIPE_NOFFS); do \
-	  $(HIPCC) $(HIPFLAGS) -DMOC_DEBUG_KERNELS -DMOC_SWIPE_LF=$$lf -DMOC_SWIPE_NO=$$no -x hip -c $(SWIPE_GROUP) \
-	    -o $(BUILD)/debug/swipe_lf$${lf}_n$${no}.hip.o || exit 1; \
-	done; done
-	$(CXX) -shared -fopenmp -o $(BUILD)/debug/libmoc.so $(CORE_OBJS) $(BUILD)/debug/*.hip.o $(LDROCM) -ldl
+DEBUG_OBJS := $(patsubst csrc/src/hip/%.hip,$(BUILD)/debug/%.hip.o,$(HIP_SRCS)) \
+              $(foreach lf,0 2,$(foreach no,$(SWIPE_NOFFS),$(BUILD)/debug/swipe_lf$(lf)_n$(no).hip.o))
+debug-kernels: $(BUILD)/debug/libmoc.so
+$(BUILD)/debug/libmoc.so: $(CORE_OBJS) $(DEBUG_OBJS)
+	$(CXX) -shared -fopenmp -o $@ $^ $(LDROCM) -ldl
+$(BUILD)/debug/%.hip.o: csrc/src/hip/%.hip $(HEADERS) $(wildcard csrc/src/hip/*.hpp)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -DMOC_DEBUG_KERNELS -DMOC_SRC_HASH='"$(SRC_HASH)"' -c $< -o $@
+$(BUILD)/debug/swipe_lf0_n%.hip.o: $(SWIPE_GROUP) $(HEADERS) $(wildcard csrc/src/hip/*.hpp)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -DMOC_DEBUG_KERNELS -DMOC_SWIPE_LF=0 -DMOC_SWIPE_NO=$* -x hip -c $< -o $@
+$(BUILD)/debug/swipe_lf2_n%.hip.o: $(SWIPE_GROUP) $(HEADERS) $(wildcard csrc/src/hip/*.hpp)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -DMOC_DEBUG_KERNELS -DMOC_SWIPE_LF=2 -DMOC_SWIPE_NO=$* -x hip -c $< -o $@
 
 # Kernel A/B builds: make variant NAME=p4 VDEFS="-DMOC_T16_UNROLL=32" -> build/variant_p4/libmoc.so
 # (select with MOC_LIB_PATH and MOC_ALLOW_VARIANT_LIB=1: the loader refuses a library whose kernels carry

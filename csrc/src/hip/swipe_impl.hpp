@@ -789,7 +789,9 @@ void swipe_direct_kernel(ProblemView pv, ShortArgs a, SwipeLayout lay) {
         tot += __builtin_amdgcn_readlane(e + L2h[h], 63);
       }
       // (a batch whose records exceed its max_l2 gets wrong results, never another wave's slots)
-      const int nf = min((s0 + tot + 6) / 7, (lay.wave_bytes >> 3) - p33_lane_slots(L2W) - 1);
+      const int cap = (lay.wave_bytes >> 3) - p33_lane_slots(L2W) - 1;
+      MOC_DCHECK((s0 + tot + 6) / 7 <= cap);
+      const int nf = min((s0 + tot + 6) / 7, cap);
       const uint32_t* base32 = reinterpret_cast<const uint32_t*>(a.codes) + ((33 * f0) >> 5);
       const int b0 = static_cast<int>((33 * f0) & 31);
       for (int f0b = 0; f0b < nf; f0b += 64 * kBatch) {  // wave-uniform
@@ -841,7 +843,12 @@ void swipe_direct_kernel(ProblemView pv, ShortArgs a, SwipeLayout lay) {
       const int L2 = h == 0 ? L2h[0] : static_cast<int>(later & 0xffu);
       const bool mine = searching(h, L2);
       const bool on = mine && L2 <= L1;
-      if constexpr (P33) record_words_p33<L2W>(wbuf, s0 + (h == 0 ? excl[0] : static_cast<int>(later >> 8)), L2, on, wd);
+      MOC_DCHECK(!on || L2 <= a.max_l2);
+      if constexpr (P33) {
+        const int q0 = s0 + (h == 0 ? excl[0] : static_cast<int>(later >> 8));
+        MOC_DCHECK(!on || 8 * (q0 / 7 + p33_lane_slots(L2W)) <= lay.wave_bytes);
+        record_words_p33<L2W>(wbuf, q0, L2, on, wd);
+      }
       const Result res = swipe_lane<NOFF, L2W, RK>(smem, wd, L2, on, L1, a.max_l2, pv.semantics);
       if (mine) store_result(a.out, ((t * H + h) << 6) + lane, a.fmt, res, pv.r2);
     }

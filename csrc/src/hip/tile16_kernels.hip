@@ -423,7 +423,7 @@ __global__ __launch_bounds__(kBlock16) void tile16_search_kernel(ProblemView pv,
       auto step = [&](int so, int j, bool key) {
         const int soff = __builtin_amdgcn_readlane(so, j);
         const unsigned char* p = lbase + soff;
-        MOC_DCHECK(2 * o0 + 4 * lane + soff + 2 * kSub * (UU - 1) + EW <= prof_lds);
+        MOC_DCHECK(2 * (o0 - S) + 4 * lane + soff + 2 * kSub * (UU - 1) + EW <= prof_lds);
 #pragma unroll
         for (int u = 0; u < UU; ++u) {
           if (Wide) {

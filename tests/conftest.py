@@ -20,6 +20,38 @@ def pytest_configure(config):
 _built = {"done": False}
 
 
+def source_hash():
+    """The hash `make` bakes into libmoc.so and ./final: every file under csrc/ plus the Makefile, sorted."""
+    import glob
+    import hashlib
+
+    pats = ["csrc/*", "csrc/*/*", "csrc/*/*/*", "csrc/*/*/*/*", "csrc/*/*/*/*/*"]
+    files = sorted([f for p in pats for f in glob.glob(p, root_dir=ROOT) if os.path.isfile(os.path.join(ROOT, f))]
+                   + ["Makefile"])
+    h = hashlib.sha1()
+    for f in files:
+        with open(os.path.join(ROOT, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:12]
+
+
+def _products_current():
+    """libmoc.so and ./final carry this tree's source hash and the ./final GPU plugin was linked after the
+    library: the products of these sources, whatever the object files' state (a gpurun box gets the
+    products without build/obj, where `make` would rebuild every object)."""
+    lib = os.path.join(ROOT, "mpi_openmp_cuda_amd", "lib", "libmoc.so")
+    plugin = os.path.join(ROOT, "mpi_openmp_cuda_amd", "lib", "libmoc_final_gpu.so")
+    final = os.path.join(ROOT, "final")
+    if not all(os.path.isfile(p) for p in (lib, plugin, final)) or os.path.getmtime(plugin) < os.path.getmtime(lib):
+        return False
+    tag = ("src=" + source_hash()).encode()
+    for p in (lib, final):
+        with open(p, "rb") as fh:
+            if tag not in fh.read():
+                return False
+    return True
+
+
 def ensure_built():
     """Builds libmoc.so and ./final in-tree once per session if they are missing or stale. pytest-xdist
     workers take turns (file lock): concurrent makes would relink ./final under tests that run it."""
@@ -30,8 +62,9 @@ def ensure_built():
     os.makedirs(os.path.join(ROOT, "build"), exist_ok=True)
     with open(os.path.join(ROOT, "build", ".make.lock"), "w") as lock:
         fcntl.flock(lock, fcntl.LOCK_EX)
-        subprocess.run(["make", "-C", ROOT, f"-j{min(16, os.cpu_count() or 8)}", "build"], check=True,
-                       stdout=subprocess.DEVNULL)
+        if not _products_current():
+            subprocess.run(["make", "-C", ROOT, f"-j{min(16, os.cpu_count() or 8)}", "build"], check=True,
+                           stdout=subprocess.DEVNULL)
     _built["done"] = True
 
 

@@ -360,21 +360,10 @@ def test_fewer_omp_threads_than_requested(tmp_path, omp_env):
 
 
 def _source_hash():
-    """The hash `make` bakes into ./final: every file under csrc/ plus the Makefile, in sorted order."""
-    import glob
-    import hashlib
-    import os
+    """The hash `make` bakes into ./final (conftest.source_hash)."""
+    from conftest import source_hash
 
-    from conftest import ROOT
-
-    pats = ["csrc/*", "csrc/*/*", "csrc/*/*/*", "csrc/*/*/*/*", "csrc/*/*/*/*/*"]
-    files = sorted([f for p in pats for f in glob.glob(p, root_dir=ROOT) if os.path.isfile(os.path.join(ROOT, f))]
-                   + ["Makefile"])
-    h = hashlib.sha1()
-    for f in files:
-        with open(os.path.join(ROOT, f), "rb") as fh:
-            h.update(fh.read())
-    return h.hexdigest()[:12]
+    return source_hash()
 
 
 def test_build_id_matches_sources():
