@@ -713,7 +713,9 @@ __device__ __forceinline__ int lane_length6(const ShortArgs& a, int64_t t, Len6D
 }
 
 template <int NOFF, int L2W, int LF, bool RK>
-__global__ __launch_bounds__(kBlockD) __attribute__((amdgpu_waves_per_eu(direct_halves(LF, L2W, NOFF) == 2 ? 8 : 1)))
+// (instances of >= 56 offsets per lane and <= 24 record words held to 128 VGPRs: 4 waves per SIMD instead of
+// 2, mid 13.6 -> 15.0 T; <64, 24> keeps one 8-byte spill per tile, outside the sweep)
+__global__ __launch_bounds__(kBlockD) __attribute__((amdgpu_waves_per_eu(direct_halves(LF, L2W, NOFF) == 2 ? 8 : NOFF >= 56 && L2W <= 24 ? 4 : 1)))
 void swipe_direct_kernel(ProblemView pv, ShortArgs a, SwipeLayout lay) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr bool P33 = LF == 2;
