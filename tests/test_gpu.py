@@ -1184,7 +1184,8 @@ def test_wire_device_resident(engine, shape, n):
     assert np.array_equal(got, ref)
 
 
-@pytest.mark.parametrize("L1,lo,hi", [(24, 5, 16), (30, 3, 16), (50, 17, 32), (60, 33, 48), (70, 44, 48), (80, 49, 64)])
+@pytest.mark.parametrize("L1,lo,hi", [(24, 5, 16), (30, 3, 16), (50, 17, 32), (60, 33, 48), (70, 44, 48), (80, 49, 64),
+                                      (14, 4, 16), (40, 20, 44)])  # the last two: records longer than Seq1 too
 def test_wire_device_resident_record_words(engine, L1, lo, hi):
     # P33 batches at every record-word width of the lane-direct kernel (4 — with 20 offsets per lane in
     # 128-record tiles, with 28 in 64-record ones — 8, 12 and 16 words): the decode slices are sized by the
