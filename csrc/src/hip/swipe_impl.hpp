@@ -81,6 +81,7 @@ struct SwipeLayout {
   int s_off = 0;        // anchor table: at[i][c] = T[c][Seq1[NOFF + i]] (0 past Seq1), int32, swipe_anchor_bytes
   int loff_off = 0, codes_off = 0, res_off = 0, raw_off = 0, total = 0;  // raw: P33 bytes as loaded
   int wave_bytes = 0;  // lane-direct P33: one wave's slice of decoded field slots (direct_layout)
+  int pairs_off = 0;   // lane-direct P33: the digit-pair table (build_p33_pair_table)
 };
 
 inline int al16(int x) { return (x + 15) & ~15; }
@@ -550,8 +551,8 @@ inline SwipeLayout direct_layout(int L1, int noff, int l2w, int lf, int64_t max_
   if (lf == 2) {
     const int ml = static_cast<int>(std::min<int64_t>(std::max<int64_t>(max_l2, 1), 4 * l2w));
     l.wave_bytes = 8 * (p33_tile_fields(64 * direct_halves(lf, l2w, noff), ml) + p33_lane_slots(l2w) + 1);
-    l.res_off = al16(l.s_off + swipe_anchor_bytes(l2w));  // the digit-pair table (p33_pair_table)
-    l.codes_off = l.res_off + al16(2 * 676);
+    l.pairs_off = al16(l.s_off + swipe_anchor_bytes(l2w));
+    l.codes_off = l.pairs_off + al16(2 * 676);
     l.total = l.codes_off + (kBlockD / 64) * l.wave_bytes;
   }
   return l;
@@ -721,7 +722,7 @@ void swipe_direct_kernel(ProblemView pv, ShortArgs a, SwipeLayout lay) {
   constexpr bool P33 = LF == 2;
   constexpr int KB = RK ? 1 : bounds::swipe_kbits(L2W);
   swipe_build_tables<RK, KB, NOFF, L2W>(smem, pv, threadIdx.x, kBlockD);
-  uint16_t* pairs = reinterpret_cast<uint16_t*>(smem + lay.res_off);
+  uint16_t* pairs = reinterpret_cast<uint16_t*>(smem + lay.pairs_off);
   if constexpr (P33) build_p33_pair_table(pairs, threadIdx.x, kBlockD);
   __syncthreads();  // the only barrier: tables complete
   const int lane = threadIdx.x & 63;
