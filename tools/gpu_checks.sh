@@ -18,9 +18,8 @@
 #                 (make variant NAME=... VDEFS=...: A/B builds, e.g. -DMOC_T16_UNROLL=32)
 #   isolate       --gpu-isolate=1 at np 1/2 (the rank's runtime shows its GPU only)
 #   hello-env     tools/hip_hello.hip's runtime / first-queue times under runtime environment settings
-#   dcheck        the kernel tests on the device-bounds-checked library (make debug-kernels, then copy
-#                 build/debug/libmoc.so to build/dbgk/: build/debug stays out of the upload); counts the
-#                 MOC_DCHECK reports (0 expected) in gpurun_out/dcheck.log
+#   dcheck        tools/dcheck.sh: the kernel tests on the device-bounds-checked library (make debug-kernels,
+#                 then copy build/debug/libmoc.so to build/dbgk/), one COUNT line per distinct MOC_DCHECK report
 # Longer studies have scripts of their own: step_variance.sh, pmc_ab.sh, rehearse_ranks.sh,
 # final_1e10_threads.sh, rccl_init_rootcause.sh.
 set -o pipefail
@@ -54,8 +53,7 @@ for c in "$@"; do
     hello-env)  # the runtime start and the first hardware queue (tools/hip_hello.hip) under runtime settings
       steps+=("hello_env$sfx:300:(cd build && [ -x hip_hello ] && [ hip_hello -nt ../tools/hip_hello.hip ] || { make -s -C .. build/mpilib/libmpi.so && hipcc --offload-arch=gfx950 -O2 ../tools/hip_hello.hip -I/opt/conda/include -Lmpilib -lmpi -Wl,-rpath-link,/opt/conda/lib -Wl,-rpath,\$PWD/mpilib -o hip_hello; }) && for e in NONE HELLO_NULL_STREAM=1 HSA_ENABLE_INTERRUPT=0 AMD_DIRECT_DISPATCH=0 ROC_AQL_QUEUE_SIZE=1024 HSA_ENABLE_SDMA=0 GPU_MAX_HW_QUEUES=1 HIP_FORCE_DEV_KERNARG=1; do for r in 1 2 3 4 5; do sleep 1; echo \"\$e \$(env \${e/NONE/X=1} timeout -k 10 30 build/hip_hello 2>&1 >/dev/null | tail -1)\" || exit 1; done; done") ;;
     isolate) steps+=("isolate$sfx:200:NPS='1 2' INPUTS='6' REPS=7 SPACING=1 HELLO=0 TIMING=1 EXTRA='--backend=hip --gpu-isolate=1 --log-level=info' bash tools/final_walltime.sh") ;;
-    dcheck)
-      steps+=("dcheck$sfx:900:MOC_LIB_PATH=$R/build/dbgk/libmoc.so MOC_ALLOW_VARIANT_LIB=1 python -u -m pytest -s -q --timeout 300 --timeout-method thread tests/test_gpu.py -m gpu -k 'wire or swipe or tile16 or slide or extreme or keys or long'; echo \"MOC_DCHECK reports: \$(grep -c MOC_DCHECK gpurun_out/dcheck$sfx.log)\"") ;;
+    dcheck) steps+=("dcheck$sfx:900:bash tools/dcheck.sh") ;;
     *) echo "unknown check: $c (see the header of $0)"; exit 2 ;;
   esac
 done
