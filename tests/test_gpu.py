@@ -1186,16 +1186,17 @@ def test_wire_device_resident(engine, shape, n):
 
 @pytest.mark.parametrize("L1,lo,hi", [(24, 5, 16), (30, 3, 16), (50, 17, 32), (60, 33, 48), (70, 44, 48), (80, 49, 64),
                                       (14, 4, 16), (40, 20, 44)])  # the last two: records longer than Seq1 too
-def test_wire_device_resident_record_words(engine, L1, lo, hi):
+@pytest.mark.parametrize("sem", [Semantics.REFERENCE, Semantics.SPEC])
+def test_wire_device_resident_record_words(engine, L1, lo, hi, sem):
     # P33 batches at every record-word width of the lane-direct kernel (4 — with 20 offsets per lane in
     # 128-record tiles, with 28 in 64-record ones — 8, 12 and 16 words): the decode slices are sized by the
     # batch's longest record, the base-6 lengths (every octet position and digit) decoded in f32; random
-    # lengths and weights, checked against the CPU engine
+    # lengths and weights, both semantics, checked against the CPU engine
     from mpi_openmp_cuda_amd.parallel.wire import WireSlice
     from mpi_openmp_cuda_amd.utils.synthetic import Shape, make_shape
 
     prob = make_shape(Shape((7, 3, 2, 5), L1, lo, hi), 40_001, seed=L1 + hi)
-    engine.set_problem(prob.weights, prob.seq1)
+    engine.set_problem(prob.weights, prob.seq1, sem)
     wire = WireSlice.from_csr(prob.codes, prob.offsets)
     res = wire.alloc_results(engine)
     dev = torch.device("cuda:0")
@@ -1208,7 +1209,7 @@ def test_wire_device_resident_record_words(engine, L1, lo, hi):
     st = engine.stats()
     assert st["direct"] == 1 and st["kernels"] == ["swipe"], st
     res.view(np.uint8)[:] = out.cpu().numpy()
-    assert np.array_equal(wire.triples(engine), as_triples(search_cpu(prob)))
+    assert np.array_equal(wire.triples(engine), as_triples(search_cpu(prob, sem)))
 
 
 # ---- narrow-integer fast paths at their exactness bounds (csrc/include/moc/kernel_bounds.hpp) --------------
